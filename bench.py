@@ -1,0 +1,204 @@
+#!/usr/bin/env python3
+"""Benchmark: Mpps of FlowSentryX verdicts on MI355X (BASELINE.json metric).
+
+One "step" = one pass of the hot path (parse -> per-source fixed-window rate limit +
+blacklist -> verdicts + map state, src/fsx_kern.c:96-347 semantics) over one batch of
+synthetic packets resident in HBM, starting from empty maps (fsx_reset is inside the
+timed step). N=1 workload: BASELINE config 2 — 64M IPv4/UDP packets from 1M
+Zipf(1.1) sources over 30 s.
+
+Multi-GPU (torch.distributed.run, one rank per GPU): weak scaling — every rank
+generates and processes its own contiguous 64M-packet slice of one stream with
+disjoint source sets (rank-salted addresses), so no data-path collective is needed;
+DESIGN.md §7 describes the hash-sharded all-to-all variant.
+
+Prints ONE JSON line on rank 0 with the driver's contract plus:
+  roofline      the dominant kernel (largest device time per step), its algorithmic
+                bytes per launch over its mean launch time measured with HIP events on
+                the library's stream inside the timed region;
+  pipeline      the whole step against SURVEY §8 d: 77 B/packet + 64 B per source;
+  cpu_baseline  the CPU oracle (sharded over host threads) on a bounded sample.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
+
+# Algorithmic bytes each kernel's function must move, per element it processes
+# (DESIGN.md §3): element = packet (parse) or IP packet (sort / fill).
+KERNEL_BYTES = {
+    "k_parse": ("packet", 64 + 4 + 8 + 8),      # header record + len + ts in, sort word out
+    "k_sort_scatter": ("ip_packet", 16),        # sort word in + out
+    "k_sort_hist": ("ip_packet", 8),
+    "k_fill_scatter": ("ip_packet", 1 + 8 + 1),  # mark + sort word in, verdict out
+}
+
+
+def parse_args():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", type=int, default=2)
+    ap.add_argument("--n", type=int, default=None, help="packets per rank (default: config)")
+    ap.add_argument("--cpu-sample", type=int, default=16 << 20)
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--check", action="store_true", help="verify a prefix against the oracle")
+    return ap.parse_args()
+
+
+def main():
+    args = parse_args()
+    import torch
+
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local = int(os.environ.get("LOCAL_RANK", 0))
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from flowsentryx_amd import lib, synth
+
+    p, zipf_s = synth.config_params(args.config, n=args.n)
+    n = int(p.n)
+    # weak scaling: rank r owns packets [r*n, (r+1)*n) of a world*n-packet stream,
+    # with its own source addresses (salted per rank)
+    p.ip_salt = p.ip_salt + 0x9E3779B1 * rank & 0xFFFFFFFF
+    d_hdr = torch.empty(n * 64, dtype=torch.uint8, device="cuda")
+    d_len = torch.empty(n, dtype=torch.int32, device="cuda")
+    d_ts = torch.empty(n, dtype=torch.int64, device="cuda")
+    d_v = torch.empty(n, dtype=torch.uint8, device="cuda")
+    synth.generate_device(p, zipf_s, 0, n, d_hdr.data_ptr(), d_len.data_ptr(), d_ts.data_ptr())
+    torch.cuda.synchronize()
+
+    max_entries = max(1024, int(p.n_ips) if p.n_ips else n)
+    ctx = lib.FsxContext(max_batch=n, max_entries=max_entries, device=local)
+
+    def step():
+        ctx.reset()
+        ctx.verdict_batch_device(d_hdr.data_ptr(), d_len.data_ptr(), d_ts.data_ptr(), n,
+                                 d_v.data_ptr())
+
+    for _ in range(args.warmup):
+        step()
+    ctx.sync()
+    info = ctx.last_batch_info()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    ctx.enable_timing(True)
+    ctx.last_timings()  # reset accumulators
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    ctx.sync()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    timings = ctx.last_timings()
+    ctx.enable_timing(False)
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    stats = ctx.stats()
+
+    check = None
+    if args.check and rank == 0:
+        from oracle import pyoracle
+        m = min(n, 4 << 20)
+        hdr, ln, ts = pyoracle.synth(p, zipf_s, 0, m)
+        o = pyoracle.Oracle(max_entries=max_entries)
+        vo = o.batch(hdr, ln, ts)
+        with lib.FsxContext(max_batch=m, max_entries=max_entries, device=local) as c2:
+            vg = c2.verdict_batch(hdr, ln, ts)
+        check = {"prefix_packets": m, "verdicts_equal": bool((vo == vg).all())}
+
+    if rank != 0:
+        if dist:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
+
+    total = n * world * args.steps
+    mpps = total / elapsed / 1e6
+    ms_step = elapsed / args.steps * 1e3
+    ip_packets, sources = info["ip_packets"], info["sources"]
+
+    # dominant kernel: largest device time per step
+    dom = max(timings, key=lambda r: r[1]) if timings else None
+    roofline = None
+    if dom:
+        name, ms_per_batch, launches = dom
+        unit, per = KERNEL_BYTES.get(name, ("packet", 0))
+        units = n if unit == "packet" else ip_packets
+        per_launch_ms = ms_per_batch / max(launches, 1e-9)
+        bytes_per_launch = per * units
+        achieved = bytes_per_launch / (per_launch_ms * 1e-3) / 1e9 if per else None
+        traffic = None
+        pmc = ROOT / "profiles" / f"pmc_{name}.json"
+        if pmc.exists():
+            traffic = json.loads(pmc.read_text()).get("hbm_bytes_per_launch")
+        roofline = {
+            "bound": "hbm", "kernel": name, "achieved": round(achieved, 1) if achieved else None,
+            "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
+            "traffic": traffic, "bytes_per_launch": bytes_per_launch,
+            "launch_ms": round(per_launch_ms, 4), "launches_per_step": launches,
+        }
+    algo = 77 * n + 64 * sources
+    pipe_gbs = algo / (ms_step * 1e-3) / 1e9
+    pipeline = {"bound": "hbm", "algorithmic_bytes_per_step": algo,
+                "achieved": round(pipe_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(pipe_gbs / HBM_PEAK_GBS, 4)}
+
+    cpu = None
+    if not args.no_cpu_baseline and world == 1:
+        from oracle import pyoracle
+        m = min(n, args.cpu_sample)
+        hdr, ln, ts = pyoracle.synth(p, zipf_s, 0, m)
+        th = args.cpu_threads
+        c0 = time.perf_counter()
+        _, _ = pyoracle.batch_sharded(hdr, ln, ts, th, max_entries=max_entries)
+        cdt = time.perf_counter() - c0
+        cpu = {"value": round(m / cdt / 1e6, 3), "unit": "Mpps", "cores": th, "kind": "port",
+               "sample": f"first {m} packets of the config-{args.config} stream, fixed window, "
+                         f"oracle/fsx_oracle.c sharded by source over {th} threads "
+                         f"({cdt:.2f} s)"}
+
+    out = {
+        "metric": "Mpps verdicts (parse+rate-limit+MLP) at 1/2/4/8 GPUs; % of HBM BW peak",
+        "value": round(mpps, 2), "unit": "Mpps", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms_step, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u64",
+        "data": "synthetic (counter-based generator, fsx_synth_common.h)",
+        "config": {"workload": f"BASELINE config {args.config}: {n} IPv4/UDP packets per GPU, "
+                               f"{p.n_ips} Zipf(1.1) sources, {p.duration_ns / 1e9:g} s; "
+                               "fixed-window limiter (src/fsx_kern.c), maps reset each step",
+                   "packets_per_gpu": n, "sources": sources, "parallelism": f"dp{world}"},
+        "roofline": roofline, "pipeline": pipeline, "cpu_baseline": cpu,
+        "kernels": [{"name": a, "ms_per_step": round(b, 4), "launches": c} for a, b, c in timings],
+        "stats": {"allowed": stats[0], "dropped": stats[1]}, "check": check,
+    }
+    print(json.dumps(out), flush=True)
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

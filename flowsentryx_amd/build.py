@@ -1,0 +1,79 @@
+"""Build recipe for the in-tree native libraries (gfx950 only).
+
+libfsx_hip.so    the product: C-ABI of include/fsx_hip.h (hot-path kernels + host API)
+libfsx_synth.so  synthetic packet streams on device (bench / tests)
+
+Both are built with `hipcc --offload-arch=gfx950` straight into this package
+directory, so they travel with the repo snapshot to the GPU box. The CPU oracle
+(oracle/Makefile) is test infrastructure and is built by `build_oracle()`.
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+from pathlib import Path
+
+PKG = Path(__file__).resolve().parent
+ROOT = PKG.parent
+CSRC = PKG / "csrc"
+INCLUDE = ROOT / "include"
+
+HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+ARCH = os.environ.get("FSX_OFFLOAD_ARCH", "gfx950")
+COMMON = [
+    f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+    "-ffp-contract=off", "-Wall", "-Wno-unused-function", "-Wno-unused-variable",
+    f"-I{INCLUDE}", f"-I{CSRC}",
+]
+
+LIBS = {
+    "libfsx_hip.so": ["fsx_device.hip", "fsx_score.hip", "fsx_api.hip"],
+    "libfsx_synth.so": ["fsx_synth.hip"],
+}
+HEADERS = ["fsx_internal.h", "fsx_synth_common.h"]
+
+
+def _stale(out: Path, srcs: list[Path]) -> bool:
+    if not out.exists():
+        return True
+    t = out.stat().st_mtime
+    deps = srcs + [CSRC / h for h in HEADERS] + [INCLUDE / "fsx_hip.h", Path(__file__)]
+    return any(d.exists() and d.stat().st_mtime > t for d in deps)
+
+
+def build_lib(name: str, force: bool = False, verbose: bool = False) -> Path:
+    out = PKG / name
+    srcs = [CSRC / s for s in LIBS[name]]
+    if not force and not _stale(out, srcs):
+        return out
+    tmp = out.with_suffix(".so.tmp")
+    cmd = [HIPCC, *COMMON, "-o", str(tmp), *map(str, srcs)]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc failed for {name}:\n{r.stdout}\n{r.stderr}")
+    os.replace(tmp, out)
+    return out
+
+
+def build_all(force: bool = False, verbose: bool = False) -> list[Path]:
+    return [build_lib(n, force, verbose) for n in LIBS]
+
+
+def build_oracle(verbose: bool = False) -> None:
+    """Test infrastructure: CPU oracle (+ oracle/_ref when the reference exists)."""
+    r = subprocess.run(["make", "-C", str(ROOT / "oracle"), "all"], capture_output=True, text=True)
+    if verbose:
+        print(r.stdout, r.stderr, file=sys.stderr)
+    if r.returncode != 0:
+        raise RuntimeError(f"oracle build failed:\n{r.stdout}\n{r.stderr}")
+
+
+if __name__ == "__main__":
+    force = "--force" in sys.argv
+    for p in build_all(force=force, verbose=True):
+        print(p)
+    build_oracle(verbose=True)

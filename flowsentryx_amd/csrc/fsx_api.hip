@@ -1,0 +1,553 @@
+// fsx_api.hip — the C ABI of libfsx_hip.so (include/fsx_hip.h).
+//
+// Host side of the drop-in boundary: context, device memory, map syscalls and the
+// batch entry points that replace the XDP program fsx() (src/fsx_kern.c:96-347)
+// and its five maps (src/fsx_kern.c:56-94). No torch types; plain pointers/sizes;
+// 0 or -errno; nothing throws across the boundary.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cerrno>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <new>
+
+#include "../../include/fsx_hip.h"
+#include "fsx_internal.h"
+
+using namespace fsx;
+
+namespace {
+constexpr int kMaxEv = 32;   // events per batch (one per kernel)
+constexpr int kRing = 64;    // batches of events in flight before a drain
+constexpr int kMaxNames = 48;
+constexpr uint64_t kMaxBatchLimit = 0x7FFFFFFFull;
+}  // namespace
+
+struct fsx_ctx {
+    fsx_config cfg{};
+    int device = 0;
+    hipStream_t own_stream = nullptr;
+    hipStream_t stream = nullptr;
+    Slot *table = nullptr;
+    uint64_t slots = 0;
+    TableState *tstate = nullptr;
+    BatchState *bs = nullptr;
+    Scratch sc{};
+    Limits lim{};
+    // host-pointer staging
+    uint8_t *d_hdr = nullptr;
+    uint32_t *d_len = nullptr;
+    uint64_t *d_ts = nullptr;
+    uint8_t *d_verdict = nullptr;
+    uint64_t stage_cap = 0;
+    // scoring staging
+    float *d_feat = nullptr;
+    float *d_prob = nullptr;
+    uint8_t *d_dec = nullptr;
+    uint64_t score_cap = 0;
+    // small device scratch for map ops
+    int32_t *d_res = nullptr;
+    uint64_t *d_val = nullptr;
+    // model
+    bool model_loaded = false;
+    int8_t w[8]{};
+    float inv_in = 0, bias_over_ats = 0, mult = 0;
+    int32_t zp_in = 0, zp_out = 0;
+    uint8_t lut[256]{};
+    // timing
+    bool timing = false;
+    bool ev_ready = false;
+    hipEvent_t ev[kRing][kMaxEv]{};
+    const char *ev_names[kRing][kMaxEv]{};
+    int ev_used[kRing]{};
+    int ring_n = 0;
+    const char *acc_name[kMaxNames]{};
+    double acc_ms[kMaxNames]{};
+    uint64_t acc_cnt[kMaxNames]{};
+    int acc_n = 0;
+    uint64_t acc_batches = 0;
+    bool pending = false;
+    char err[512]{};
+};
+
+static int set_err(fsx_ctx *c, int code, const char *fmt, ...) {
+    if (c) {
+        va_list ap;
+        va_start(ap, fmt);
+        vsnprintf(c->err, sizeof(c->err), fmt, ap);
+        va_end(ap);
+    }
+    return code;
+}
+
+#define HIPCHK(c, x)                                                                   \
+    do {                                                                               \
+        hipError_t e_ = (x);                                                           \
+        if (e_ != hipSuccess)                                                          \
+            return set_err((c), -EIO, "%s failed: %s", #x, hipGetErrorString(e_));     \
+    } while (0)
+
+static uint64_t next_pow2(uint64_t x) {
+    uint64_t p = 1;
+    while (p < x) p <<= 1;
+    return p;
+}
+
+static void free_scratch(fsx_ctx *c) {
+    Scratch &s = c->sc;
+    hipFree(s.packed[0]); hipFree(s.packed[1]); hipFree(s.marks); hipFree(s.headf);
+    hipFree(s.seg_start); hipFree(s.seg_slot); hipFree(s.hist); hipFree(s.row_total);
+    hipFree(s.tile_aux); hipFree(s.tile_last); hipFree(s.fix_list); hipFree(s.fix_bitmap);
+    s = Scratch{};
+}
+
+static int alloc_scratch(fsx_ctx *c, uint64_t cap) {
+    if (cap <= c->sc.cap) return 0;
+    free_scratch(c);
+    Scratch &s = c->sc;
+    const uint64_t ntiles = cap / kTile + 2;
+    HIPCHK(c, hipMalloc(&s.packed[0], cap * 8));
+    HIPCHK(c, hipMalloc(&s.packed[1], cap * 8));
+    HIPCHK(c, hipMalloc(&s.marks, cap + 16));
+    HIPCHK(c, hipMalloc(&s.headf, cap + 16));
+    HIPCHK(c, hipMalloc(&s.seg_start, (cap + 1) * 4));
+    HIPCHK(c, hipMalloc(&s.seg_slot, cap * 4));
+    HIPCHK(c, hipMalloc(&s.hist, 256ull * kSortMaxBlocks * 4));
+    HIPCHK(c, hipMalloc(&s.row_total, 256 * 4));
+    HIPCHK(c, hipMalloc(&s.tile_aux, ntiles * 4));
+    HIPCHK(c, hipMalloc(&s.tile_last, ntiles));
+    HIPCHK(c, hipMalloc(&s.fix_list, cap * 4));
+    HIPCHK(c, hipMalloc(&s.fix_bitmap, (cap / 64 + 1) * 8));
+    s.cap = cap;
+    return 0;
+}
+
+extern "C" {
+
+int fsx_abi_version(void) { return FSX_ABI_VERSION; }
+
+void fsx_config_default(fsx_config *cfg) {
+    if (!cfg) return;
+    memset(cfg, 0, sizeof(*cfg));
+    cfg->pps_threshold = 1000;          // src/fsx_kern.c:309
+    cfg->bps_threshold = 125000000;     // src/fsx_kern.c:310
+    cfg->window_ns = 1000000000ull;     // src/fsx_kern.c:245
+    cfg->block_ns = 10ull * 1000000000ull;  // src/fsx_kern.c:308,317
+    cfg->max_entries = 100000;          // MAX_TRACK_IPS, src/fsx_struct.h:7
+    cfg->max_batch = 1u << 20;
+    cfg->tb_rate = 1000;
+    cfg->tb_burst = 1000;
+    cfg->hash_seed = 0x5EED0F5A0ull;
+    cfg->limiter = FSX_LIMIT_FIXED_WINDOW;
+    cfg->device = 0;
+}
+
+const char *fsx_last_error(const fsx_ctx *ctx) { return ctx ? ctx->err : "null context"; }
+
+static int sel(fsx_ctx *c) {
+    HIPCHK(c, hipSetDevice(c->device));
+    return 0;
+}
+
+void fsx_close(fsx_ctx *c) {
+    if (!c) return;
+    hipSetDevice(c->device);
+    if (c->stream) hipStreamSynchronize(c->stream);
+    free_scratch(c);
+    hipFree(c->table); hipFree(c->tstate); hipFree(c->bs);
+    hipFree(c->d_hdr); hipFree(c->d_len); hipFree(c->d_ts); hipFree(c->d_verdict);
+    hipFree(c->d_feat); hipFree(c->d_prob); hipFree(c->d_dec);
+    hipFree(c->d_res); hipFree(c->d_val);
+    for (int r = 0; r < kRing; ++r)
+        for (int i = 0; i < kMaxEv; ++i) if (c->ev[r][i]) hipEventDestroy(c->ev[r][i]);
+    if (c->own_stream) hipStreamDestroy(c->own_stream);
+    delete c;
+}
+
+int fsx_open(fsx_ctx **out, const fsx_config *cfg) {
+    if (!out) return -EINVAL;
+    *out = nullptr;
+    fsx_config k;
+    if (cfg) k = *cfg; else fsx_config_default(&k);
+    if (k.max_entries == 0 || k.max_entries > (1ull << 33)) return -EINVAL;
+    if (k.max_batch == 0 || k.max_batch > kMaxBatchLimit) return -EINVAL;
+    if (k.limiter < FSX_LIMIT_FIXED_WINDOW || k.limiter > FSX_LIMIT_TOKEN_BUCKET) return -EINVAL;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return -ENODEV;
+    if (k.device < 0 || k.device >= ndev) return -EINVAL;
+    fsx_ctx *c = new (std::nothrow) fsx_ctx();
+    if (!c) return -ENOMEM;
+    c->cfg = k;
+    c->device = k.device;
+    int rc = sel(c);
+    if (rc) { fsx_close(c); return rc; }
+    c->slots = next_pow2(std::max<uint64_t>(1024, 2 * k.max_entries));
+    auto fail = [&](int r) { fsx_close(c); return r; };
+    if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) return fail(-EIO);
+    c->stream = c->own_stream;
+    if (hipMalloc(&c->table, c->slots * sizeof(Slot)) != hipSuccess) return fail(-ENOMEM);
+    if (hipMalloc(&c->tstate, sizeof(TableState)) != hipSuccess) return fail(-ENOMEM);
+    if (hipMalloc(&c->bs, sizeof(BatchState)) != hipSuccess) return fail(-ENOMEM);
+    if (hipMalloc(&c->d_res, 64) != hipSuccess) return fail(-ENOMEM);
+    if (hipMalloc(&c->d_val, 64) != hipSuccess) return fail(-ENOMEM);
+    if (hipMemset(c->table, 0, c->slots * sizeof(Slot)) != hipSuccess) return fail(-EIO);
+    if (hipMemset(c->tstate, 0, sizeof(TableState)) != hipSuccess) return fail(-EIO);
+    if (hipMemset(c->bs, 0, sizeof(BatchState)) != hipSuccess) return fail(-EIO);
+    if (alloc_scratch(c, k.max_batch)) return fail(-ENOMEM);
+    Limits &L = c->lim;
+    L.pps = k.pps_threshold; L.bps = k.bps_threshold; L.window = k.window_ns; L.block = k.block_ns;
+    L.tb_rate = k.tb_rate;
+    L.tb_cap = k.tb_burst > (~0ull / 1000000000ull) ? ~0ull : k.tb_burst * 1000000000ull;
+    L.max_entries = k.max_entries;
+    L.table_mask = c->slots - 1;
+    L.seed = mix64(k.hash_seed);
+    L.salt32 = (uint32_t)(mix64(k.hash_seed ^ 0xABCDEFull) >> 32);
+    L.limiter = k.limiter;
+    L.test_flags = k.flags;
+    if (hipDeviceSynchronize() != hipSuccess) return fail(-EIO);
+    *out = c;
+    return 0;
+}
+
+int fsx_set_stream(fsx_ctx *c, void *s) {
+    if (!c) return -EINVAL;
+    c->stream = s ? (hipStream_t)s : c->own_stream;
+    return 0;
+}
+
+static int check_batch(fsx_ctx *c) {
+    if (!c->pending) return 0;
+    c->pending = false;
+    BatchState h;
+    HIPCHK(c, hipMemcpy(&h, c->bs, sizeof(h), hipMemcpyDeviceToHost));
+    if (h.err & ERR_TABLE_FULL)
+        return set_err(c, -ENOSPC, "map full: more than max_entries=%llu source IPs",
+                       (unsigned long long)c->cfg.max_entries);
+    if (h.err) return set_err(c, -EIO, "device error flags 0x%x", h.err);
+    return 0;
+}
+
+int fsx_sync(fsx_ctx *c) {
+    if (!c) return -EINVAL;
+    int rc = sel(c);
+    if (rc) return rc;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return check_batch(c);
+}
+
+// Fold the recorded per-kernel event intervals of all pending batches into the
+// per-name accumulators (synchronizes the stream).
+static int drain_timings(fsx_ctx *c) {
+    if (c->ring_n == 0) return 0;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    for (int r = 0; r < c->ring_n; ++r) {
+        for (int i = 1; i < c->ev_used[r]; ++i) {
+            float t = 0;
+            HIPCHK(c, hipEventElapsedTime(&t, c->ev[r][i - 1], c->ev[r][i]));
+            const char *nm = c->ev_names[r][i];
+            int k = 0;
+            while (k < c->acc_n && strcmp(c->acc_name[k], nm) != 0) ++k;
+            if (k == c->acc_n) {
+                if (c->acc_n == kMaxNames) continue;
+                c->acc_name[c->acc_n++] = nm;
+            }
+            c->acc_ms[k] += t;
+            c->acc_cnt[k] += 1;
+        }
+        c->acc_batches += 1;
+    }
+    c->ring_n = 0;
+    return 0;
+}
+
+int fsx_verdict_batch_device(fsx_ctx *c, const uint8_t *d_hdr, const uint32_t *d_len,
+                             const uint64_t *d_ts, size_t n, uint8_t *d_verdict) {
+    if (!c) return -EINVAL;
+    if (n && (!d_hdr || !d_len || !d_ts || !d_verdict)) return set_err(c, -EINVAL, "null buffer");
+    if (n > c->cfg.max_batch) return set_err(c, -E2BIG, "n=%zu exceeds max_batch", n);
+    int rc = sel(c);
+    if (rc) return rc;
+    if (c->pending) { rc = fsx_sync(c); if (rc) return rc; }
+    if (c->cfg.limiter != FSX_LIMIT_FIXED_WINDOW)
+        return set_err(c, -EOPNOTSUPP, "limiter %d not built into this pipeline yet", c->cfg.limiter);
+    hipEvent_t *ev = nullptr;
+    const char **names = nullptr;
+    int *used = nullptr;
+    if (c->timing) {
+        if (c->ring_n == kRing && (rc = drain_timings(c))) return rc;
+        ev = c->ev[c->ring_n];
+        names = c->ev_names[c->ring_n];
+        used = &c->ev_used[c->ring_n];
+        c->ring_n++;
+    }
+    hipError_t e = launch_verdict_pipeline(d_hdr, d_len, d_ts, (uint32_t)n, d_verdict, c->table,
+                                           c->tstate, c->bs, c->sc, c->lim, c->stream, ev, kMaxEv,
+                                           used, names);
+    if (e != hipSuccess) return set_err(c, -EIO, "pipeline launch: %s", hipGetErrorString(e));
+    c->pending = true;
+    return 0;
+}
+
+static int ensure_stage(fsx_ctx *c, uint64_t n) {
+    if (n <= c->stage_cap) return 0;
+    hipFree(c->d_hdr); hipFree(c->d_len); hipFree(c->d_ts); hipFree(c->d_verdict);
+    c->d_hdr = nullptr; c->d_len = nullptr; c->d_ts = nullptr; c->d_verdict = nullptr;
+    c->stage_cap = 0;
+    HIPCHK(c, hipMalloc(&c->d_hdr, n * 64));
+    HIPCHK(c, hipMalloc(&c->d_len, n * 4));
+    HIPCHK(c, hipMalloc(&c->d_ts, n * 8));
+    HIPCHK(c, hipMalloc(&c->d_verdict, n));
+    c->stage_cap = n;
+    return 0;
+}
+
+int fsx_verdict_batch(fsx_ctx *c, const uint8_t *hdr, const uint32_t *len, const uint64_t *ts,
+                      size_t n, uint8_t *verdict) {
+    if (!c) return -EINVAL;
+    if (n && (!hdr || !len || !ts || !verdict)) return set_err(c, -EINVAL, "null buffer");
+    if (n > c->cfg.max_batch) return set_err(c, -E2BIG, "n=%zu exceeds max_batch", n);
+    int rc = sel(c);
+    if (rc) return rc;
+    if (n == 0) return 0;
+    if ((rc = ensure_stage(c, n))) return rc;
+    HIPCHK(c, hipMemcpyAsync(c->d_hdr, hdr, n * 64, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->d_len, len, n * 4, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->d_ts, ts, n * 8, hipMemcpyHostToDevice, c->stream));
+    rc = fsx_verdict_batch_device(c, c->d_hdr, c->d_len, c->d_ts, n, c->d_verdict);
+    if (rc) return rc;
+    HIPCHK(c, hipMemcpyAsync(verdict, c->d_verdict, n, hipMemcpyDeviceToHost, c->stream));
+    return fsx_sync(c);
+}
+
+// ------------------------------------------------------------------ maps
+static int key_words(int map_id, const void *key, uint32_t k[4]) {
+    k[0] = k[1] = k[2] = k[3] = 0;
+    if (map_id == FSX_MAP_IPV4_STATS || map_id == FSX_MAP_IPV4_BLACKLIST) memcpy(k, key, 4);
+    else if (map_id == FSX_MAP_IPV6_STATS || map_id == FSX_MAP_IPV6_BLACKLIST) memcpy(k, key, 16);
+    else return -EINVAL;
+    return 0;
+}
+
+static int map_op(fsx_ctx *c, int op, int map_id, const void *key, const void *value, void *out,
+                  uint64_t flags) {
+    if (!c || !key) return -EINVAL;
+    int rc = sel(c);
+    if (rc) return rc;
+    if ((rc = fsx_sync(c))) return rc;
+    if (map_id == FSX_MAP_STATS) {
+        uint32_t k0;
+        memcpy(&k0, key, 4);
+        if (k0 != 0) return op == 0 ? -ENOENT : -E2BIG;  // ARRAY[1]: index 0 only
+        if (op == 2) return -EINVAL;                     // array elements cannot be deleted
+        if (op == 0) { HIPCHK(c, hipMemcpy(out, c->tstate->stats, 16, hipMemcpyDeviceToHost)); return 0; }
+        if (flags == FSX_BPF_NOEXIST) return -EEXIST;
+        HIPCHK(c, hipMemcpy(c->tstate->stats, value, 16, hipMemcpyHostToDevice));
+        return 0;
+    }
+    uint32_t k[4];
+    if ((rc = key_words(map_id, key, k))) return set_err(c, rc, "bad map id %d", map_id);
+    if (flags > FSX_BPF_EXIST) return -EINVAL;
+    uint64_t v[3] = {0, 0, 0};
+    const bool is_st = map_id == FSX_MAP_IPV4_STATS || map_id == FSX_MAP_IPV6_STATS;
+    if (op == 1) memcpy(v, value, is_st ? 24 : 8);
+    hipError_t e = launch_map_op(c->table, c->tstate, c->lim, op, map_id, k, v, flags, c->d_res,
+                                 c->d_val, c->stream);
+    if (e != hipSuccess) return set_err(c, -EIO, "map op: %s", hipGetErrorString(e));
+    int32_t res = 0;
+    HIPCHK(c, hipMemcpyAsync(&res, c->d_res, 4, hipMemcpyDeviceToHost, c->stream));
+    uint64_t ov[3];
+    HIPCHK(c, hipMemcpyAsync(ov, c->d_val, 24, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (res == 0 && op == 0) memcpy(out, ov, is_st ? 24 : 8);
+    return res;
+}
+
+int fsx_map_lookup(fsx_ctx *c, int map_id, const void *key, void *value) {
+    if (!value) return -EINVAL;
+    return map_op(c, 0, map_id, key, nullptr, value, 0);
+}
+int fsx_map_update(fsx_ctx *c, int map_id, const void *key, const void *value, uint64_t flags) {
+    if (!value) return -EINVAL;
+    return map_op(c, 1, map_id, key, value, nullptr, flags);
+}
+int fsx_map_delete(fsx_ctx *c, int map_id, const void *key) {
+    return map_op(c, 2, map_id, key, nullptr, nullptr, 0);
+}
+
+int fsx_map_dump(fsx_ctx *c, int map_id, void *keys, void *values, size_t cap, size_t *n_out) {
+    if (!c || !n_out) return -EINVAL;
+    int rc = sel(c);
+    if (rc) return rc;
+    if ((rc = fsx_sync(c))) return rc;
+    if (map_id == FSX_MAP_STATS) {
+        if (cap >= 1) {
+            uint32_t z = 0;
+            if (keys) memcpy(keys, &z, 4);
+            if (values) HIPCHK(c, hipMemcpy(values, c->tstate->stats, 16, hipMemcpyDeviceToHost));
+        }
+        *n_out = 1;
+        return 0;
+    }
+    if (map_id < FSX_MAP_IPV4_STATS || map_id > FSX_MAP_IPV6_BLACKLIST) return -EINVAL;
+    const bool v6 = map_id == FSX_MAP_IPV6_STATS || map_id == FSX_MAP_IPV6_BLACKLIST;
+    const bool st = map_id == FSX_MAP_IPV4_STATS || map_id == FSX_MAP_IPV6_STATS;
+    const size_t klen = v6 ? 16 : 4, vlen = st ? 24 : 8;
+    const size_t dcap = std::max<size_t>(cap, 1);
+    uint8_t *dk = nullptr;
+    uint64_t *dv = nullptr;
+    unsigned long long *dc = nullptr;
+    HIPCHK(c, hipMalloc(&dk, dcap * klen));
+    HIPCHK(c, hipMalloc(&dv, dcap * vlen));
+    HIPCHK(c, hipMalloc(&dc, 8));
+    HIPCHK(c, hipMemsetAsync(dc, 0, 8, c->stream));
+    hipError_t e = launch_map_dump(c->table, c->lim, map_id, dk, dv, cap, dc, c->stream);
+    unsigned long long cnt = 0;
+    if (e == hipSuccess) e = hipMemcpyAsync(&cnt, dc, 8, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    const size_t m = std::min<size_t>(cap, cnt);
+    if (e == hipSuccess && m && keys) e = hipMemcpy(keys, dk, m * klen, hipMemcpyDeviceToHost);
+    if (e == hipSuccess && m && values) e = hipMemcpy(values, dv, m * vlen, hipMemcpyDeviceToHost);
+    hipFree(dk); hipFree(dv); hipFree(dc);
+    if (e != hipSuccess) return set_err(c, -EIO, "map dump: %s", hipGetErrorString(e));
+    *n_out = cnt;
+    return 0;
+}
+
+int fsx_get_stats(fsx_ctx *c, fsx_stats *out) {
+    if (!c || !out) return -EINVAL;
+    int rc = sel(c);
+    if (rc) return rc;
+    if ((rc = fsx_sync(c))) return rc;
+    HIPCHK(c, hipMemcpy(out, c->tstate->stats, 16, hipMemcpyDeviceToHost));
+    return 0;
+}
+
+int fsx_reset(fsx_ctx *c) {
+    if (!c) return -EINVAL;
+    int rc = sel(c);
+    if (rc) return rc;
+    HIPCHK(c, hipMemsetAsync(c->table, 0, c->slots * sizeof(Slot), c->stream));
+    HIPCHK(c, hipMemsetAsync(c->tstate, 0, sizeof(TableState), c->stream));
+    return 0;
+}
+
+// ------------------------------------------------------------------ scoring
+int fsx_load_q8_model(fsx_ctx *c, const fsx_q8_model *m) {
+    if (!c || !m) return -EINVAL;
+    if (!(m->in_scale > 0.0f) || !(m->out_scale > 0.0f) || !(m->weight_scale > 0.0f))
+        return set_err(c, -EINVAL, "scales must be positive");
+    if (m->in_zero_point < 0 || m->in_zero_point > 255 || m->out_zero_point < 0 || m->out_zero_point > 255)
+        return set_err(c, -EINVAL, "quint8 zero points must be in [0,255]");
+    memcpy(c->w, m->weight, 8);
+    c->inv_in = 1.0f / m->in_scale;
+    const float ats = m->in_scale * m->weight_scale;      // act_times_w_scale (fp32)
+    c->mult = ats / m->out_scale;                           // requantization multiplier
+    c->bias_over_ats = m->bias / ats;                       // float bias folded into acc units
+    c->zp_in = m->in_zero_point;
+    c->zp_out = m->out_zero_point;
+    // quantized sigmoid: output quint8 (scale 1/256, zero point 0), fp32 arithmetic
+    for (int q = 0; q < 256; ++q) {
+        volatile float x = (float)(q - m->out_zero_point) * m->out_scale;
+        volatile float s = 1.0f / (1.0f + expf(-x));
+        float r = rintf(s * 256.0f);
+        c->lut[q] = (uint8_t)(r > 255.0f ? 255.0f : (r < 0.0f ? 0.0f : r));
+    }
+    c->model_loaded = true;
+    return 0;
+}
+
+int fsx_score_device(fsx_ctx *c, const float *d_feat, size_t n, float *d_prob, uint8_t *d_dec) {
+    if (!c) return -EINVAL;
+    if (!c->model_loaded) return set_err(c, -EINVAL, "no model loaded (fsx_load_q8_model)");
+    if (n && (!d_feat || !d_prob || !d_dec)) return -EINVAL;
+    int rc = sel(c);
+    if (rc) return rc;
+    hipError_t e = launch_score(d_feat, n, d_prob, d_dec, c->w, c->inv_in, c->zp_in,
+                                c->bias_over_ats, c->mult, c->zp_out, c->lut, c->stream);
+    if (e != hipSuccess) return set_err(c, -EIO, "score launch: %s", hipGetErrorString(e));
+    return 0;
+}
+
+int fsx_score(fsx_ctx *c, const float *feat, size_t n, float *prob, uint8_t *mal) {
+    if (!c) return -EINVAL;
+    if (n && (!feat || !prob || !mal)) return -EINVAL;
+    int rc = sel(c);
+    if (rc) return rc;
+    if (n == 0) return 0;
+    if (n > c->score_cap) {
+        hipFree(c->d_feat); hipFree(c->d_prob); hipFree(c->d_dec);
+        c->d_feat = nullptr; c->d_prob = nullptr; c->d_dec = nullptr; c->score_cap = 0;
+        HIPCHK(c, hipMalloc(&c->d_feat, n * 32));
+        HIPCHK(c, hipMalloc(&c->d_prob, n * 4));
+        HIPCHK(c, hipMalloc(&c->d_dec, n));
+        c->score_cap = n;
+    }
+    HIPCHK(c, hipMemcpyAsync(c->d_feat, feat, n * 32, hipMemcpyHostToDevice, c->stream));
+    if ((rc = fsx_score_device(c, c->d_feat, n, c->d_prob, c->d_dec))) return rc;
+    HIPCHK(c, hipMemcpyAsync(prob, c->d_prob, n * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(mal, c->d_dec, n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+int fsx_flow_features(fsx_ctx *c, const uint8_t *, const uint32_t *, const uint64_t *, size_t,
+                      size_t, uint8_t *, uint8_t *, float *, size_t *) {
+    return c ? set_err(c, -EOPNOTSUPP, "flow features not built yet") : -EINVAL;
+}
+
+int fsx_last_batch_info(fsx_ctx *c, uint64_t *info, int cap) {
+    if (!c || (!info && cap > 0)) return -EINVAL;
+    int rc = sel(c);
+    if (rc) return rc;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    BatchState h;
+    HIPCHK(c, hipMemcpy(&h, c->bs, sizeof(h), hipMemcpyDeviceToHost));
+    const uint64_t v[10] = {h.n_valid, h.nseg, h.n_new, h.any_v6, h.nonmono, h.max_len,
+                            h.max_ts, h.allowed, h.dropped, h.n_fix};
+    int k = 0;
+    for (; k < cap && k < 10; ++k) info[k] = v[k];
+    return k;
+}
+
+// ------------------------------------------------------------------ timing
+int fsx_enable_timing(fsx_ctx *c, int on) {
+    if (!c) return -EINVAL;
+    int rc = sel(c);
+    if (rc) return rc;
+    if (on && !c->ev_ready) {
+        for (int r = 0; r < kRing; ++r)
+            for (int i = 0; i < kMaxEv; ++i) HIPCHK(c, hipEventCreate(&c->ev[r][i]));
+        c->ev_ready = true;
+    }
+    if (!on && (rc = drain_timings(c))) return rc;
+    c->timing = on != 0;
+    return 0;
+}
+
+int fsx_last_timings(fsx_ctx *c, float *ms_per_batch, float *launches_per_batch, char *names,
+                     int cap, int name_len, int *count) {
+    if (!c || !count) return -EINVAL;
+    int rc = sel(c);
+    if (rc) return rc;
+    if ((rc = drain_timings(c))) return rc;
+    const double nb = c->acc_batches ? (double)c->acc_batches : 1.0;
+    int k = 0;
+    for (; k < c->acc_n && k < cap; ++k) {
+        if (ms_per_batch) ms_per_batch[k] = (float)(c->acc_ms[k] / nb);
+        if (launches_per_batch) launches_per_batch[k] = (float)(c->acc_cnt[k] / nb);
+        if (names && name_len > 0) {
+            strncpy(names + (size_t)k * name_len, c->acc_name[k], name_len - 1);
+            names[(size_t)k * name_len + name_len - 1] = 0;
+        }
+    }
+    *count = k;
+    c->acc_n = 0;
+    c->acc_batches = 0;
+    return 0;
+}
+
+}  // extern "C"

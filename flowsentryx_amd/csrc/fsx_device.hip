@@ -1,0 +1,1136 @@
+// fsx_device.hip — gfx950 kernels of the packet-verdict hot path.
+//
+// Pipeline for one batch of n packets, all on one HIP stream:
+//   k_parse          header records -> packed sort word per IP packet
+//                    (src/parsing_helper.h:49-136 + src/fsx_kern.c:123-148)
+//   k_sort_* x4      stable LSD radix sort (8-bit digits) of the packed words by
+//                    the 32-bit source key: per-source segments in arrival order
+//   k_v6_mixed/fixup exact separation of IPv6 hash collisions (IPv4 keys are a
+//                    bijection of the address and never collide)
+//   k_heads_*        ordered compaction of segment starts
+//   k_lookup/insert  map state of every source IP (src/fsx_kern.c:56-94)
+//   k_walk_fixed     the fixed-window limiter + blacklist of src/fsx_kern.c:150-346
+//                    evaluated per segment by epoch jumps (binary searches on the
+//                    segment's timestamps), writing verdict change marks
+//   k_fill_*         fill-forward of the marks, scatter of verdicts to arrival
+//                    order, stats_map counters (src/fsx_kern.c:210,332,342)
+#include <hip/hip_runtime.h>
+
+#include "fsx_internal.h"
+
+#define XDP_DROP 1
+#define XDP_PASS 2
+
+namespace fsx {
+
+// ------------------------------------------------------------------ helpers
+__device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
+
+template <typename T>
+__device__ __forceinline__ T wave_incl_sum(T x) {
+    const uint32_t lane = lane_id();
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        T y = __shfl_up(x, o);
+        if (lane >= (uint32_t)o) x += y;
+    }
+    return x;
+}
+
+template <typename T>
+__device__ __forceinline__ T wave_max(T x) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        T y = __shfl_xor(x, o);
+        x = y > x ? y : x;
+    }
+    return x;
+}
+
+// Exclusive prefix sum over the 256 threads of a block. s_tmp: >= 4 entries.
+// Every thread of the block must call it. *total receives the block sum.
+__device__ __forceinline__ uint32_t block256_excl(uint32_t x, uint32_t *s_tmp, uint32_t *total) {
+    const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
+    uint32_t incl = wave_incl_sum(x);
+    if (lane == 63) s_tmp[w] = incl;
+    __syncthreads();
+    uint32_t off = 0, tot = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < 4; ++i) {
+        uint32_t v = s_tmp[i];
+        off += i < w ? v : 0u;
+        tot += v;
+    }
+    __syncthreads();
+    if (total) *total = tot;
+    return off + incl - x;
+}
+
+// "Last non-zero" scan operator over encoded (position << 8 | mark) words: max.
+__device__ __forceinline__ uint32_t wave_incl_max(uint32_t x) {
+    const uint32_t lane = lane_id();
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        uint32_t y = __shfl_up(x, o);
+        if (lane >= (uint32_t)o) x = y > x ? y : x;
+    }
+    return x;
+}
+
+__device__ __forceinline__ uint64_t match_digit(uint32_t d, uint64_t active) {
+    uint64_t peers = active;
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+        const bool bit = (d >> b) & 1u;
+        const uint64_t bal = __ballot(bit);
+        peers &= bit ? bal : ~bal;
+    }
+    return peers;
+}
+
+// IPv6 source address of arrival index i (bytes 22..37 of the record).
+__device__ __forceinline__ void load_key6(const uint8_t *hdr, uint32_t i, uint32_t k[4]) {
+    const uint32_t *d = reinterpret_cast<const uint32_t *>(hdr + (size_t)i * 64);
+    const uint32_t d5 = d[5], d6 = d[6], d7 = d[7], d8 = d[8], d9 = d[9];
+    k[0] = (d5 >> 16) | (d6 << 16);
+    k[1] = (d6 >> 16) | (d7 << 16);
+    k[2] = (d7 >> 16) | (d8 << 16);
+    k[3] = (d8 >> 16) | (d9 << 16);
+}
+
+// Full key (family tag 1/2 + address words) of a packed sort word.
+__device__ __forceinline__ uint32_t key_of(uint64_t v, const uint8_t *hdr, uint32_t salt,
+                                           uint32_t k[4]) {
+    if (pk_fam(v)) {
+        load_key6(hdr, pk_idx(v), k);
+        return 2u;
+    }
+    k[0] = ip_of_skey(pk_skey(v), salt);
+    k[1] = k[2] = k[3] = 0;
+    return 1u;
+}
+
+// Total order on (family, address) used to group colliding IPv6 hash runs.
+__device__ __forceinline__ int key_cmp(uint32_t ta, const uint32_t *a, uint32_t tb,
+                                       const uint32_t *b) {
+    if (ta != tb) return ta < tb ? -1 : 1;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+        if (a[i] != b[i]) return a[i] < b[i] ? -1 : 1;
+    return 0;
+}
+
+// ------------------------------------------------------------------ parse
+// One wave handles 64 consecutive records per step: the 4 KiB tile is loaded with
+// four fully coalesced 1 KiB wave loads and staged through LDS (17-dword record
+// pitch: conflict-free 32-bit reads), then each lane parses its own record.
+__global__ __launch_bounds__(256) void k_parse(const uint8_t *__restrict__ hdr,
+                                               const uint32_t *__restrict__ len,
+                                               const uint64_t *__restrict__ ts, uint32_t n,
+                                               uint64_t *__restrict__ packed,
+                                               uint8_t *__restrict__ verdict, BatchState *bs,
+                                               uint32_t salt, uint64_t seed, uint32_t v6_const) {
+    __shared__ uint32_t s_rec[4][64 * 17];
+    __shared__ uint32_t s_red[4][3];
+    __shared__ unsigned long long s_ts[4];
+    const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
+    uint32_t *rec = s_rec[w];
+    uint32_t any6 = 0, nonmono = 0, maxlen = 0;
+    uint64_t maxts = 0;
+    const uint32_t ntiles = (n + 63u) >> 6;
+    for (uint32_t t = blockIdx.x * 4u + w; t < ntiles; t += gridDim.x * 4u) {
+        const uint32_t base = t << 6;
+        const uint8_t *src = hdr + (size_t)base * 64;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t g = (uint32_t)k * 1024u + lane * 16u;
+            const uint32_t r = g >> 6, off = (g & 63u) >> 2;
+            uint4 v = make_uint4(0, 0, 0, 0);
+            if (base + r < n) v = *reinterpret_cast<const uint4 *>(src + g);
+            uint32_t *d = rec + r * 17u + off;
+            d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        const uint32_t i = base + lane;
+        const bool live = i < n;
+        const uint32_t *my = rec + lane * 17u;
+        const uint32_t d3 = my[3], d5 = my[5], d6 = my[6], d7 = my[7], d8 = my[8], d9 = my[9];
+        const uint32_t L = live ? len[i] : 0u;
+        const uint64_t T = live ? ts[i] : 0ull;
+        uint64_t prev = __shfl_up(T, 1);
+        if (lane == 0) prev = (live && i > 0) ? ts[i - 1] : T;
+        if (live) {
+            // parse_ethhdr (14-byte bound; raw h_proto, no VLAN)
+            const uint32_t proto = ((d3 & 0xFFu) << 8) | ((d3 >> 8) & 0xFFu);
+            uint64_t out = kSentinel;
+            uint8_t v = XDP_PASS;  // non-IP: PASS, not counted (src/fsx_kern.c:128-131)
+            if (L < 14u) {
+                v = XDP_DROP;      // src/fsx_kern.c:124-127
+            } else if (proto == 0x86DDu) {
+                if (L < 54u) v = XDP_DROP;  // parse_ip6hdr bound, src/fsx_kern.c:139-140
+                else {
+                    uint32_t k[4] = {(d5 >> 16) | (d6 << 16), (d6 >> 16) | (d7 << 16),
+                                     (d7 >> 16) | (d8 << 16), (d8 >> 16) | (d9 << 16)};
+                    const uint32_t sk = v6_const ? v6_const : skey_v6(k, seed);
+                    out = ((uint64_t)sk << 32) | (1ull << 31) | i;
+                    any6 = 1;
+                }
+            } else if (proto == 0x0800u) {
+                if (L < 34u) v = XDP_DROP;  // parse_ip4hdr fixed 20-byte bound, :146-147
+                else {
+                    const uint32_t ip = (d6 >> 16) | (d7 << 16);  // bytes 26..29 raw
+                    out = ((uint64_t)skey_v4(ip, salt) << 32) | i;
+                }
+            }
+            packed[i] = out;
+            if (out == kSentinel) verdict[i] = v;
+            nonmono |= T < prev ? 1u : 0u;
+            maxlen = L > maxlen ? L : maxlen;
+            maxts = T > maxts ? T : maxts;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    }
+    any6 = __ballot(any6 != 0) ? 1u : 0u;
+    nonmono = __ballot(nonmono != 0) ? 1u : 0u;
+    maxlen = wave_max(maxlen);
+    maxts = wave_max(maxts);
+    if (lane == 0) { s_red[w][0] = any6; s_red[w][1] = nonmono; s_red[w][2] = maxlen; s_ts[w] = maxts; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t a = 0, m = 0, l = 0;
+        uint64_t mt = 0;
+        for (int k = 0; k < 4; ++k) {
+            a |= s_red[k][0]; m |= s_red[k][1];
+            l = s_red[k][2] > l ? s_red[k][2] : l;
+            mt = s_ts[k] > mt ? s_ts[k] : mt;
+        }
+        if (a) atomicOr(&bs->any_v6, 1u);
+        if (m) atomicOr(&bs->nonmono, 1u);
+        atomicMax(&bs->max_len, l);
+        atomicMax(reinterpret_cast<unsigned long long *>(&bs->max_ts), (unsigned long long)mt);
+    }
+}
+
+// ------------------------------------------------------------------ radix sort
+// Block b of G owns the contiguous range [b*chunk, min(L,(b+1)*chunk)); a pass is
+// hist (per-block digit counts) -> rowscan (per-digit exclusive scan over blocks)
+// -> scatter (stable in-tile ranking by wave ballots, LDS-sorted tile, coalesced
+// runs to the digit buckets). Pass 0 also drops the non-IP sentinels.
+__device__ __forceinline__ void block_range(uint32_t L, uint32_t G, uint32_t b, uint32_t &beg,
+                                            uint32_t &end) {
+    const uint32_t chunk = (L + G - 1) / G;
+    beg = min(L, b * chunk);
+    end = min(L, beg + chunk);
+}
+
+__global__ __launch_bounds__(256) void k_sort_hist(const uint64_t *__restrict__ in, uint32_t L_host,
+                                                   const uint32_t *L_dev, uint32_t shift,
+                                                   uint32_t *__restrict__ hist, uint32_t G,
+                                                   int first, BatchState *bs) {
+    __shared__ uint32_t sh[4][256];
+    __shared__ uint32_t s_tmp[4];
+    const uint32_t tid = threadIdx.x, w = tid >> 6;
+    for (int k = 0; k < 4; ++k) sh[k][tid] = 0;
+    __syncthreads();
+    const uint32_t L = L_dev ? *L_dev : L_host;
+    uint32_t beg, end;
+    block_range(L, G, blockIdx.x, beg, end);
+    for (uint32_t i = beg + tid; i < end; i += 256) {
+        const uint64_t v = in[i];
+        if (first && v == kSentinel) continue;
+        atomicAdd(&sh[w][(uint32_t)(v >> shift) & 255u], 1u);
+    }
+    __syncthreads();
+    const uint32_t c = sh[0][tid] + sh[1][tid] + sh[2][tid] + sh[3][tid];
+    hist[tid * G + blockIdx.x] = c;
+    if (first) {
+        uint32_t tot;
+        block256_excl(c, s_tmp, &tot);
+        if (tid == 0 && tot) atomicAdd(&bs->n_valid, tot);
+    }
+}
+
+// One block per digit: exclusive scan of that digit's row over the G blocks.
+__global__ __launch_bounds__(256) void k_sort_rowscan(uint32_t *__restrict__ hist, uint32_t G,
+                                                      uint32_t *__restrict__ row_total) {
+    __shared__ uint32_t s_tmp[4];
+    uint32_t *row = hist + (size_t)blockIdx.x * G;
+    const uint32_t per = (G + 255) / 256;
+    const uint32_t b0 = threadIdx.x * per;
+    uint32_t loc[8];
+    uint32_t s = 0;
+    for (uint32_t k = 0; k < per && k < 8; ++k) {
+        const uint32_t j = b0 + k;
+        loc[k] = j < G ? row[j] : 0u;
+        s += loc[k];
+    }
+    uint32_t tot;
+    uint32_t off = block256_excl(s, s_tmp, &tot);
+    for (uint32_t k = 0; k < per && k < 8; ++k) {
+        const uint32_t j = b0 + k;
+        if (j < G) row[j] = off;
+        off += loc[k];
+    }
+    if (threadIdx.x == 0) row_total[blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(256) void k_sort_scatter(const uint64_t *__restrict__ in,
+                                                      uint64_t *__restrict__ out,
+                                                      uint32_t L_host, const uint32_t *L_dev,
+                                                      uint32_t shift,
+                                                      const uint32_t *__restrict__ hist,
+                                                      const uint32_t *__restrict__ row_total,
+                                                      uint32_t G, int first) {
+    __shared__ unsigned long long s_el[kSortTile];
+    __shared__ uint32_t s_wc[4][256];
+    __shared__ uint32_t s_base[256], s_tbase[256], s_tcnt[256];
+    __shared__ uint32_t s_tmp[4];
+    const uint32_t tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
+    const uint32_t L = L_dev ? *L_dev : L_host;
+    uint32_t beg, end;
+    block_range(L, G, blockIdx.x, beg, end);
+    {
+        const uint32_t rt = row_total[tid];
+        const uint32_t dbase = block256_excl(rt, s_tmp, nullptr);
+        s_base[tid] = dbase + hist[tid * G + blockIdx.x];
+    }
+    const uint64_t lt_mask = (1ull << lane) - 1ull;
+    for (uint32_t t0 = beg; t0 < end; t0 += kSortTile) {
+        uint64_t v[kSortItems];
+        uint32_t lr[kSortItems];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) s_wc[w][lane * 4 + k] = 0;
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+#pragma unroll
+        for (int r = 0; r < kSortItems; ++r) {
+            const uint32_t i = t0 + w * 1024u + (uint32_t)r * 64u + lane;
+            v[r] = i < end ? in[i] : kSentinel;
+        }
+#pragma unroll
+        for (int r = 0; r < kSortItems; ++r) {
+            const uint32_t i = t0 + w * 1024u + (uint32_t)r * 64u + lane;
+            const bool valid = i < end && !(first && v[r] == kSentinel);
+            const uint64_t act = __ballot(valid);
+            const uint32_t d = (uint32_t)(v[r] >> shift) & 255u;
+            const uint64_t peers = match_digit(d, act);
+            const uint32_t below = (uint32_t)__popcll(peers & lt_mask);
+            uint32_t base = 0;
+            if (valid) base = s_wc[w][d];
+            lr[r] = valid ? base + below : 0xFFFFFFFFu;
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            if (valid && below == 0) s_wc[w][d] = base + (uint32_t)__popcll(peers);
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        }
+        __syncthreads();
+        {
+            const uint32_t d = tid;
+            const uint32_t c0 = s_wc[0][d], c1 = s_wc[1][d], c2 = s_wc[2][d], c3 = s_wc[3][d];
+            const uint32_t tc = c0 + c1 + c2 + c3;
+            __syncthreads();
+            s_wc[0][d] = 0; s_wc[1][d] = c0; s_wc[2][d] = c0 + c1; s_wc[3][d] = c0 + c1 + c2;
+            s_tcnt[d] = tc;
+            s_tbase[d] = block256_excl(tc, s_tmp, nullptr);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < kSortItems; ++r) {
+            if (lr[r] != 0xFFFFFFFFu) {
+                const uint32_t d = (uint32_t)(v[r] >> shift) & 255u;
+                s_el[s_tbase[d] + s_wc[w][d] + lr[r]] = v[r];
+            }
+        }
+        __syncthreads();
+        const uint32_t T = s_tbase[255] + s_tcnt[255];
+        for (uint32_t j = tid; j < T; j += 256) {
+            const uint64_t x = s_el[j];
+            const uint32_t d = (uint32_t)(x >> shift) & 255u;
+            out[s_base[d] + (j - s_tbase[d])] = x;
+        }
+        __syncthreads();
+        s_base[tid] += s_tcnt[tid];
+        __syncthreads();
+    }
+}
+
+// ------------------------------------------------------------------ IPv6 collision fixup
+// Equal 32-bit sort keys with different (family, address) form "mixed runs". Each
+// run is stably re-sorted by (family, address) so every source IP is contiguous.
+__device__ __forceinline__ uint32_t lower_bound_skey(const uint64_t *S, uint32_t lo, uint32_t hi,
+                                                     uint32_t sk) {
+    while (lo < hi) {
+        const uint32_t m = lo + (hi - lo) / 2;
+        if (pk_skey(S[m]) < sk) lo = m + 1; else hi = m;
+    }
+    return lo;
+}
+__device__ __forceinline__ uint32_t upper_bound_skey(const uint64_t *S, uint32_t lo, uint32_t hi,
+                                                     uint32_t sk) {
+    while (lo < hi) {
+        const uint32_t m = lo + (hi - lo) / 2;
+        if (pk_skey(S[m]) <= sk) lo = m + 1; else hi = m;
+    }
+    return lo;
+}
+
+__global__ __launch_bounds__(256) void k_v6_mixed(const uint64_t *__restrict__ S, BatchState *bs,
+                                                  const uint8_t *__restrict__ hdr,
+                                                  uint64_t *bitmap, uint32_t *fix_list) {
+    if (!bs->any_v6) return;
+    const uint32_t M = bs->n_valid;
+    for (uint32_t p = blockIdx.x * 256u + threadIdx.x + 1u; p < M; p += gridDim.x * 256u) {
+        const uint64_t a = S[p - 1], b = S[p];
+        if (pk_skey(a) != pk_skey(b)) continue;
+        const uint32_t fa = pk_fam(a), fb = pk_fam(b);
+        if (!(fa | fb)) continue;  // IPv4 keys are a bijection
+        bool mixed = fa != fb;
+        if (!mixed) {
+            uint32_t ka[4], kb[4];
+            load_key6(hdr, pk_idx(a), ka);
+            load_key6(hdr, pk_idx(b), kb);
+            mixed = key_cmp(2, ka, 2, kb) != 0;
+        }
+        if (!mixed) continue;
+        const uint32_t h = lower_bound_skey(S, 0, p, pk_skey(b));
+        const unsigned long long bit = 1ull << (h & 63u);
+        const unsigned long long old =
+            atomicOr(reinterpret_cast<unsigned long long *>(&bitmap[h >> 6]), bit);
+        if (!(old & bit)) fix_list[atomicAdd(&bs->n_fix, 1u)] = h;
+    }
+}
+
+// Short runs: one thread, stable insertion sort (keys re-gathered per compare).
+constexpr uint32_t kFixShort = 32;
+__global__ __launch_bounds__(256) void k_fixup_short(uint64_t *__restrict__ S, BatchState *bs,
+                                                     const uint8_t *__restrict__ hdr,
+                                                     const uint32_t *fix_list, uint32_t salt) {
+    const uint32_t nf = bs->n_fix, M = bs->n_valid;
+    for (uint32_t f = blockIdx.x * 256u + threadIdx.x; f < nf; f += gridDim.x * 256u) {
+        const uint32_t h = fix_list[f];
+        const uint32_t e = upper_bound_skey(S, h, M, pk_skey(S[h]));
+        if (e - h > kFixShort) continue;
+        for (uint32_t i = h + 1; i < e; ++i) {
+            const uint64_t x = S[i];
+            uint32_t kx[4];
+            const uint32_t tx = key_of(x, hdr, salt, kx);
+            uint32_t j = i;
+            while (j > h) {
+                uint32_t ky[4];
+                const uint32_t ty = key_of(S[j - 1], hdr, salt, ky);
+                if (key_cmp(ty, ky, tx, kx) <= 0) break;
+                S[j] = S[j - 1];
+                --j;
+            }
+            S[j] = x;
+        }
+    }
+}
+
+// Long runs: one block per run, repeated stable partitions (== first key | rest).
+__global__ __launch_bounds__(256) void k_fixup_long(uint64_t *__restrict__ S,
+                                                    uint64_t *__restrict__ tmp, BatchState *bs,
+                                                    const uint8_t *__restrict__ hdr,
+                                                    const uint32_t *fix_list, uint32_t salt) {
+    __shared__ uint32_t s_tmp[4];
+    __shared__ uint32_t s_pk[4];
+    __shared__ uint32_t s_neq;
+    const uint32_t nf = bs->n_fix, M = bs->n_valid;
+    for (uint32_t f = blockIdx.x; f < nf; f += gridDim.x) {
+        const uint32_t h = fix_list[f];
+        const uint32_t e = upper_bound_skey(S, h, M, pk_skey(S[h]));
+        if (e - h <= kFixShort) continue;
+        uint32_t cur = h;
+        while (cur < e) {
+            uint32_t pk[4];
+            const uint32_t pt = key_of(S[cur], hdr, salt, pk);
+            // pass 1: count equal
+            uint32_t neq_local = 0;
+            for (uint32_t i = cur + threadIdx.x; i < e; i += 256) {
+                uint32_t k[4];
+                const uint32_t t = key_of(S[i], hdr, salt, k);
+                neq_local += key_cmp(t, k, pt, pk) == 0 ? 1u : 0u;
+            }
+            uint32_t n_eq;
+            block256_excl(neq_local, s_tmp, &n_eq);
+            // pass 2: stable placement into tmp, chunk by chunk
+            uint32_t eq_off = 0, ne_off = 0;
+            for (uint32_t c0 = cur; c0 < e; c0 += 256) {
+                const uint32_t i = c0 + threadIdx.x;
+                uint32_t is_eq = 0;
+                uint64_t x = 0;
+                if (i < e) {
+                    x = S[i];
+                    uint32_t k[4];
+                    const uint32_t t = key_of(x, hdr, salt, k);
+                    is_eq = key_cmp(t, k, pt, pk) == 0;
+                }
+                uint32_t tot_eq;
+                const uint32_t r_eq = block256_excl(is_eq, s_tmp, &tot_eq);
+                const uint32_t nvalid = min(256u, e - c0);
+                if (i < e) {
+                    const uint32_t r_ne = threadIdx.x - r_eq;
+                    if (is_eq) tmp[cur + eq_off + r_eq] = x;
+                    else tmp[cur + n_eq + ne_off + r_ne] = x;
+                }
+                eq_off += tot_eq;
+                ne_off += nvalid - tot_eq;
+            }
+            __syncthreads();
+            for (uint32_t i = cur + threadIdx.x; i < e; i += 256) S[i] = tmp[i];
+            __syncthreads();
+            cur += n_eq;
+            (void)s_pk; (void)s_neq;
+        }
+    }
+}
+
+// ------------------------------------------------------------------ segment heads
+__device__ __forceinline__ bool is_head(const uint64_t *S, uint32_t p, const uint8_t *hdr,
+                                        bool any6) {
+    if (p == 0) return true;
+    const uint64_t a = S[p - 1], b = S[p];
+    if ((a >> 31) != (b >> 31)) return true;  // sort key or family differs
+    if (!any6 || !pk_fam(b)) return false;
+    uint32_t ka[4], kb[4];
+    load_key6(hdr, pk_idx(a), ka);
+    load_key6(hdr, pk_idx(b), kb);
+    return key_cmp(2, ka, 2, kb) != 0;
+}
+
+// Tile = kTile sorted positions; 256 threads x 16 consecutive positions.
+__global__ __launch_bounds__(256) void k_heads_count(const uint64_t *__restrict__ S,
+                                                     BatchState *bs,
+                                                     const uint8_t *__restrict__ hdr,
+                                                     uint8_t *__restrict__ headf,
+                                                     uint32_t *__restrict__ tile_cnt) {
+    __shared__ uint32_t s_tmp[4];
+    const uint32_t M = bs->n_valid;
+    const bool any6 = bs->any_v6 != 0;
+    const uint32_t ntiles = (M + kTile - 1) / kTile;
+    for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const uint32_t p0 = t * kTile + threadIdx.x * 16u;
+        uint32_t cnt = 0;
+        uint32_t flags[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const uint32_t p = p0 + k;
+            const bool h = p < M && is_head(S, p, hdr, any6);
+            cnt += h;
+            flags[k >> 2] |= (h ? 1u : 0u) << (8 * (k & 3));
+        }
+        if (p0 < M) {
+            if (p0 + 16 <= M) {
+                *reinterpret_cast<uint4 *>(headf + p0) = make_uint4(flags[0], flags[1], flags[2], flags[3]);
+            } else {
+                for (uint32_t k = 0; p0 + k < M; ++k) headf[p0 + k] = (flags[k >> 2] >> (8 * (k & 3))) & 1u;
+            }
+        }
+        uint32_t tot;
+        block256_excl(cnt, s_tmp, &tot);
+        if (threadIdx.x == 0) tile_cnt[t] = tot;
+    }
+}
+
+// Single block: exclusive scan of per-tile counts (in place), nseg, seg_start[nseg]=M.
+__global__ __launch_bounds__(1024) void k_scan_tiles_u32(uint32_t *__restrict__ cnt, BatchState *bs,
+                                                         uint32_t *seg_start) {
+    __shared__ uint32_t s_w[16];
+    __shared__ uint32_t s_carry;
+    const uint32_t M = bs->n_valid;
+    const uint32_t ntiles = (M + kTile - 1) / kTile;
+    const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
+    if (threadIdx.x == 0) s_carry = 0;
+    __syncthreads();
+    for (uint32_t c0 = 0; c0 < ntiles; c0 += 1024) {
+        const uint32_t i = c0 + threadIdx.x;
+        const uint32_t x = i < ntiles ? cnt[i] : 0u;
+        const uint32_t incl = wave_incl_sum(x);
+        if (lane == 63) s_w[w] = incl;
+        __syncthreads();
+        uint32_t off = s_carry, tot = 0;
+        for (uint32_t k = 0; k < 16; ++k) {
+            off += k < w ? s_w[k] : 0u;
+            tot += s_w[k];
+        }
+        if (i < ntiles) cnt[i] = off + incl - x;
+        __syncthreads();
+        if (threadIdx.x == 0) s_carry += tot;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        bs->nseg = s_carry;
+        seg_start[s_carry] = M;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_heads_write(BatchState *bs, const uint8_t *__restrict__ headf,
+                                                     const uint32_t *__restrict__ tile_off,
+                                                     uint32_t *__restrict__ seg_start) {
+    __shared__ uint32_t s_tmp[4];
+    const uint32_t M = bs->n_valid;
+    const uint32_t ntiles = (M + kTile - 1) / kTile;
+    for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const uint32_t p0 = t * kTile + threadIdx.x * 16u;
+        uint32_t f[4] = {0, 0, 0, 0};
+        if (p0 + 16 <= M) {
+            const uint4 v = *reinterpret_cast<const uint4 *>(headf + p0);
+            f[0] = v.x; f[1] = v.y; f[2] = v.z; f[3] = v.w;
+        } else {
+            for (uint32_t k = 0; p0 + k < M && k < 16; ++k) f[k >> 2] |= (uint32_t)headf[p0 + k] << (8 * (k & 3));
+        }
+        uint32_t cnt = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) cnt += __popc(f[k] & 0x01010101u);
+        uint32_t off = tile_off[t] + block256_excl(cnt, s_tmp, nullptr);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            if ((f[k >> 2] >> (8 * (k & 3))) & 1u) seg_start[off++] = p0 + k;
+        }
+    }
+}
+
+// ------------------------------------------------------------------ table lookup / insert
+__device__ __forceinline__ uint32_t seg_key(const uint64_t *S, const uint32_t *seg_start, uint32_t g,
+                                            const uint8_t *hdr, uint32_t salt, uint32_t k[4]) {
+    return key_of(S[seg_start[g]], hdr, salt, k);
+}
+
+__device__ __forceinline__ bool slot_key_eq(const Slot &s, uint32_t tag, const uint32_t k[4]) {
+    return s.tag == tag && s.key[0] == k[0] && s.key[1] == k[1] && s.key[2] == k[2] &&
+           s.key[3] == k[3];
+}
+
+__device__ __forceinline__ uint32_t table_find(const Slot *table, uint64_t mask, uint32_t tag,
+                                               const uint32_t k[4], uint64_t seed) {
+    uint64_t i = slot_hash(tag, k, seed) & mask;
+    for (uint64_t probes = 0; probes <= mask; ++probes) {
+        const uint32_t t = table[i].tag;
+        if (t == 0) return kNoSlot;
+        if (t == tag && slot_key_eq(table[i], tag, k)) return (uint32_t)i;
+        i = (i + 1) & mask;
+    }
+    return kNoSlot;
+}
+
+// Claim an empty slot for a key known to be absent; its key has exactly one inserter.
+__device__ __forceinline__ uint32_t table_claim(Slot *table, uint64_t mask, uint32_t tag,
+                                                const uint32_t k[4], uint64_t seed) {
+    uint64_t i = slot_hash(tag, k, seed) & mask;
+    for (uint64_t probes = 0; probes <= mask; ++probes) {
+        if (table[i].tag == 0 && atomicCAS(&table[i].tag, 0u, tag) == 0u) {
+            Slot &s = table[i];
+            s.flags = 0;
+            s.key[0] = k[0]; s.key[1] = k[1]; s.key[2] = k[2]; s.key[3] = k[3];
+            s.pps = s.bps = s.tt = s.till = s.aux = 0;
+            return (uint32_t)i;
+        }
+        i = (i + 1) & mask;
+    }
+    return kNoSlot;
+}
+
+__global__ __launch_bounds__(256) void k_lookup(const uint64_t *__restrict__ S, BatchState *bs,
+                                                const uint32_t *__restrict__ seg_start,
+                                                uint32_t *__restrict__ seg_slot,
+                                                const uint8_t *__restrict__ hdr, const Slot *table,
+                                                Limits lim) {
+    const uint32_t nseg = bs->nseg;
+    uint32_t nnew = 0;
+    for (uint32_t g = blockIdx.x * 256u + threadIdx.x; g < nseg; g += gridDim.x * 256u) {
+        uint32_t k[4];
+        const uint32_t tag = seg_key(S, seg_start, g, hdr, lim.salt32, k);
+        const uint32_t s = table_find(table, lim.table_mask, tag, k, lim.seed);
+        seg_slot[g] = s;
+        nnew += s == kNoSlot;
+    }
+    nnew = wave_incl_sum(nnew);
+    if (lane_id() == 63 && nnew) atomicAdd(&bs->n_new, nnew);
+}
+
+__global__ __launch_bounds__(256) void k_insert(const uint64_t *__restrict__ S, BatchState *bs,
+                                                const uint32_t *__restrict__ seg_start,
+                                                uint32_t *__restrict__ seg_slot,
+                                                const uint8_t *__restrict__ hdr, Slot *table,
+                                                TableState *tstate, Limits lim) {
+    if (bs->n_new == 0) return;
+    const uint32_t nseg = bs->nseg;
+    for (uint32_t g = blockIdx.x * 256u + threadIdx.x; g < nseg; g += gridDim.x * 256u) {
+        if (seg_slot[g] != kNoSlot) continue;
+        uint32_t k[4];
+        const uint32_t tag = seg_key(S, seg_start, g, hdr, lim.salt32, k);
+        const unsigned long long ticket =
+            atomicAdd(reinterpret_cast<unsigned long long *>(&tstate->count), 1ull);
+        if (ticket >= lim.max_entries) {
+            atomicOr(&bs->err, ERR_TABLE_FULL);
+            atomicAdd(reinterpret_cast<unsigned long long *>(&tstate->count), ~0ull);  // undo
+            continue;
+        }
+        const uint32_t s = table_claim(table, lim.table_mask, tag, k, lim.seed);
+        if (s == kNoSlot) atomicOr(&bs->err, ERR_PROBE);
+        seg_slot[g] = s;
+    }
+}
+
+// ------------------------------------------------------------------ fixed-window walker
+struct SegView {
+    const uint64_t *S;
+    const uint64_t *ts;
+    const uint32_t *len;
+    __device__ __forceinline__ uint64_t t(uint32_t q) const { return ts[pk_idx(S[q])]; }
+    __device__ __forceinline__ uint32_t l(uint32_t q) const { return len[pk_idx(S[q])]; }
+};
+
+// First q in [lo, hi) with t(q) > X, for t non-decreasing on [lo, hi). Galloping
+// from lo: O(log distance), so short epochs of light sources cost O(1).
+__device__ __forceinline__ uint32_t gallop_gt(const SegView &sv, uint32_t lo, uint32_t hi,
+                                              uint64_t X) {
+    if (lo >= hi) return hi;
+    if (sv.t(lo) > X) return lo;
+    uint32_t good = lo, bad = hi;
+    uint32_t step = 1;
+    for (;;) {
+        const uint64_t cand = (uint64_t)good + step;
+        if (cand >= hi) break;
+        if (sv.t((uint32_t)cand) > X) { bad = (uint32_t)cand; break; }
+        good = (uint32_t)cand;
+        step <<= 1;
+    }
+    uint32_t l = good + 1, r = bad;
+    while (l < r) {
+        const uint32_t m = l + (r - l) / 2;
+        if (sv.t(m) > X) r = m; else l = m + 1;
+    }
+    return l;
+}
+
+struct MarkWriter {
+    uint8_t *marks;
+    uint8_t last;
+    __device__ __forceinline__ void emit(uint32_t pos, uint8_t v) {
+        if (v != last) { marks[pos] = v; last = v; }
+    }
+};
+
+constexpr uint64_t kBig = 1ull << 62;
+
+// Exact per-packet replay of src/fsx_kern.c:150-346 for one source (any timestamps).
+__device__ void walk_fixed_exact(const SegView &sv, uint32_t a, uint32_t b, const Limits &lim,
+                                 MarkWriter &mw, bool &has_st, bool &has_bl, uint64_t &pps,
+                                 uint64_t &bps, uint64_t &tt, uint64_t &till) {
+    for (uint32_t q = a; q < b; ++q) {
+        const uint64_t now = sv.t(q);
+        if (has_bl && till > 0) {
+            if (now > till) has_bl = false;                 // :193-204 delete
+            else { mw.emit(q, XDP_DROP); continue; }        // :205-215
+        }
+        uint64_t cp, cb;
+        if (has_st) {
+            if (now - tt > lim.window) { pps = 0; bps = 0; tt = now; cp = 0; cb = 0; }  // :245-250
+            else { pps += 1; bps += sv.l(q); cp = pps; cb = bps; }                        // :258-262
+        } else {
+            has_st = true; pps = 1; bps = sv.l(q); tt = now; cp = pps; cb = bps;          // :265-284
+        }
+        if (cp > lim.pps || cb > lim.bps) {                 // :312
+            till = now + lim.block; has_bl = true;          // :317-326
+            mw.emit(q, XDP_DROP);
+        } else {
+            mw.emit(q, XDP_PASS);
+        }
+    }
+}
+
+// Epoch-jump evaluation (non-decreasing timestamps, no u64 overflow). An epoch
+// starts where ip_stats (re)starts a window: the first-ever packet (count 1), a
+// reset packet (count 0, not counted) or the carried window (continuation). With
+// counts consecutive inside an epoch, the count trigger is at a closed-form
+// position; the window end and the blacklist end are binary searches.
+__device__ void walk_fixed_fast(const SegView &sv, uint32_t a, uint32_t b, const Limits &lim,
+                                uint32_t maxL, MarkWriter &mw, bool &has_st, bool &has_bl,
+                                uint64_t &pps, uint64_t &bps, uint64_t &tt, uint64_t &till) {
+    const uint64_t P = lim.pps, B = lim.bps, W = lim.window, BLK = lim.block;
+    uint32_t p = a;
+    if (has_bl && till > 0) {
+        const uint32_t j = gallop_gt(sv, a, b, till);
+        if (j > a) mw.emit(a, XDP_DROP);
+        if (j < b) has_bl = false;
+        p = j;
+    }
+    bool touched = false;
+    uint32_t ep_lo = 0, ep_hi = 0;
+    uint64_t bps_base = 0;
+    while (p < b) {
+        const uint64_t t = sv.t(p);
+        uint64_t T0, pc, pb;
+        uint32_t cs;
+        if (has_st && !(t - tt > W)) { T0 = tt; pc = pps; pb = bps; cs = 1; }
+        else if (has_st) { T0 = t; pc = 0; pb = 0; cs = 0; }
+        else { T0 = t; pc = 0; pb = 0; cs = 1; }
+        has_st = true;
+        touched = true;
+        const uint32_t e = gallop_gt(sv, p + 1, b, T0 + W);
+        const uint64_t c0 = pc + cs;
+        uint64_t k64 = c0 > P ? (uint64_t)p : (uint64_t)p + (P + 1 - c0);
+        if (k64 > e) k64 = e;
+        // bytes: only scanned when bps could exceed B before the count does
+        bool bytes_possible;
+        {
+            const uint64_t room = P + 1;
+            bytes_possible = pb > B || (maxL && room > (B - pb) / maxL);
+        }
+        if (bytes_possible) {
+            uint64_t acc = pb;
+            for (uint32_t q = cs ? p : p + 1; q < k64; ++q) {
+                acc += sv.l(q);
+                if (acc > B) { k64 = q; break; }
+            }
+        }
+        const uint32_t k = (uint32_t)k64;
+        tt = T0;
+        bps_base = pb;
+        ep_lo = p + 1 - cs;
+        if (k >= e) {   // window closes without a trigger
+            mw.emit(p, XDP_PASS);
+            pps = c0 + (uint64_t)(e - 1 - p);
+            ep_hi = e;
+            p = e;
+            continue;
+        }
+        if (k > p) mw.emit(p, XDP_PASS);
+        mw.emit(k, XDP_DROP);
+        pps = c0 + (uint64_t)(k - p);
+        ep_hi = k + 1;
+        till = sv.t(k) + BLK;
+        has_bl = true;
+        uint32_t q = k + 1;
+        for (;;) {
+            const uint32_t j = gallop_gt(sv, q, b, till);
+            if (j >= b) { p = b; break; }
+            has_bl = false;                     // expired: deleted at packet j
+            const uint64_t tj = sv.t(j);
+            if (tj - tt > W) { p = j; break; }  // j resets the window: next epoch
+            pps += 1;                           // re-trigger inside the window (block < window)
+            bps_base += sv.l(j);
+            till = tj + BLK;
+            has_bl = true;
+            q = j + 1;
+        }
+    }
+    if (touched) {
+        uint64_t s = bps_base;
+        for (uint32_t q = ep_lo; q < ep_hi; ++q) s += sv.l(q);
+        bps = s;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_walk_fixed(const uint64_t *__restrict__ S, BatchState *bs,
+                                                    const uint32_t *__restrict__ seg_start,
+                                                    const uint32_t *__restrict__ seg_slot,
+                                                    const uint64_t *__restrict__ ts,
+                                                    const uint32_t *__restrict__ len,
+                                                    uint8_t *__restrict__ marks, Slot *table,
+                                                    Limits lim) {
+    const uint32_t nseg = bs->nseg;
+    const bool glob_fast = !bs->nonmono && lim.block >= 1 && lim.pps < kBig && lim.bps < kBig &&
+                           lim.window < kBig && lim.block < kBig &&
+                           bs->max_ts <= ~0ull - (lim.window > lim.block ? lim.window : lim.block);
+    const uint32_t maxL = bs->max_len;
+    const SegView sv{S, ts, len};
+    for (uint32_t g = blockIdx.x * 256u + threadIdx.x; g < nseg; g += gridDim.x * 256u) {
+        const uint32_t s = seg_slot[g];
+        if (s == kNoSlot) continue;
+        const uint32_t a = seg_start[g], b = seg_start[g + 1];
+        Slot &sl = table[s];
+        bool has_st = sl.flags & SLOT_HAS_ST, has_bl = sl.flags & SLOT_HAS_BL;
+        uint64_t pps = sl.pps, bps = sl.bps, tt = sl.tt, till = sl.till;
+        MarkWriter mw{marks, 0};
+        const bool fast = glob_fast && (!has_st || (tt <= ~0ull - lim.window && pps < kBig && bps < kBig));
+        if (fast) walk_fixed_fast(sv, a, b, lim, maxL, mw, has_st, has_bl, pps, bps, tt, till);
+        else walk_fixed_exact(sv, a, b, lim, mw, has_st, has_bl, pps, bps, tt, till);
+        sl.flags = (sl.flags & ~(SLOT_HAS_ST | SLOT_HAS_BL)) | (has_st ? SLOT_HAS_ST : 0u) |
+                   (has_bl ? SLOT_HAS_BL : 0u);
+        sl.pps = pps; sl.bps = bps; sl.tt = tt; sl.till = till;
+    }
+}
+
+// ------------------------------------------------------------------ fill + scatter
+// Tile of kTile sorted positions; thread j owns marks [16j, 16j+16).
+__device__ __forceinline__ void load_marks16(const uint8_t *marks, uint32_t p0, uint32_t M, uint32_t f[4]) {
+    if (p0 + 16 <= M) {
+        const uint4 v = *reinterpret_cast<const uint4 *>(marks + p0);
+        f[0] = v.x; f[1] = v.y; f[2] = v.z; f[3] = v.w;
+    } else {
+        f[0] = f[1] = f[2] = f[3] = 0;
+        for (uint32_t k = 0; k < 16 && p0 + k < M; ++k) f[k >> 2] |= (uint32_t)marks[p0 + k] << (8 * (k & 3));
+    }
+}
+
+__global__ __launch_bounds__(256) void k_fill_last(const uint8_t *__restrict__ marks, BatchState *bs,
+                                                   uint8_t *__restrict__ tile_last) {
+    __shared__ uint32_t s_w[4];
+    const uint32_t M = bs->n_valid;
+    const uint32_t ntiles = (M + kTile - 1) / kTile;
+    for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const uint32_t p0 = t * kTile + threadIdx.x * 16u;
+        uint32_t f[4];
+        load_marks16(marks, p0, M, f);
+        uint32_t enc = 0;  // (local index + 1) << 8 | mark of the last non-zero mark
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const uint32_t m = (f[k >> 2] >> (8 * (k & 3))) & 0xFFu;
+            if (m) enc = ((threadIdx.x * 16u + k + 1u) << 8) | m;
+        }
+        enc = wave_max(enc);
+        if (lane_id() == 0) s_w[threadIdx.x >> 6] = enc;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t e = s_w[0];
+            for (int k = 1; k < 4; ++k) e = s_w[k] > e ? s_w[k] : e;
+            tile_last[t] = (uint8_t)(e & 0xFFu);
+        }
+        __syncthreads();
+    }
+}
+
+// Single block: carry[t] = last non-zero of tile_last[0..t-1] (in place, exclusive).
+__global__ __launch_bounds__(1024) void k_fill_carry(uint8_t *__restrict__ tile_last, BatchState *bs) {
+    __shared__ uint32_t s_w[16];
+    __shared__ uint32_t s_carry;
+    const uint32_t M = bs->n_valid;
+    const uint32_t ntiles = (M + kTile - 1) / kTile;
+    const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
+    if (threadIdx.x == 0) s_carry = 0;
+    __syncthreads();
+    for (uint32_t c0 = 0; c0 < ntiles; c0 += 1024) {
+        const uint32_t i = c0 + threadIdx.x;
+        const uint32_t m = i < ntiles ? tile_last[i] : 0u;
+        const uint32_t enc = m ? (((i + 1u) << 8) | m) : 0u;
+        const uint32_t incl = wave_incl_max(enc);
+        if (lane == 63) s_w[w] = incl;
+        __syncthreads();
+        uint32_t pre = s_carry;
+        uint32_t tot = s_carry;
+        for (uint32_t k = 0; k < 16; ++k) {
+            if (k < w) pre = s_w[k] > pre ? s_w[k] : pre;
+            tot = s_w[k] > tot ? s_w[k] : tot;
+        }
+        uint32_t excl = __shfl_up(incl, 1);
+        if (lane == 0) excl = 0;
+        excl = excl > pre ? excl : pre;
+        __syncthreads();
+        if (i < ntiles) tile_last[i] = (uint8_t)(excl & 0xFFu);
+        if (threadIdx.x == 0) s_carry = tot;
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(256) void k_fill_scatter(const uint8_t *__restrict__ marks,
+                                                      const uint64_t *__restrict__ S, BatchState *bs,
+                                                      const uint8_t *__restrict__ carry,
+                                                      uint8_t *__restrict__ verdict,
+                                                      TableState *tstate) {
+    __shared__ uint8_t s_v[kTile];
+    __shared__ uint32_t s_w[4];
+    __shared__ unsigned long long s_cnt[4][2];
+    const uint32_t M = bs->n_valid;
+    const uint32_t ntiles = (M + kTile - 1) / kTile;
+    const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
+    uint64_t n_pass = 0, n_drop = 0;
+    for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const uint32_t p0 = t * kTile + threadIdx.x * 16u;
+        uint32_t f[4];
+        load_marks16(marks, p0, M, f);
+        uint32_t enc = 0;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const uint32_t m = (f[k >> 2] >> (8 * (k & 3))) & 0xFFu;
+            if (m) enc = ((threadIdx.x * 16u + k + 1u) << 8) | m;
+        }
+        // exclusive "last non-zero" over the threads before me, then the tile carry
+        const uint32_t incl = wave_incl_max(enc);
+        if (lane == 63) s_w[w] = incl;
+        __syncthreads();
+        uint32_t pre = 0;
+        for (uint32_t k = 0; k < w; ++k) pre = s_w[k] > pre ? s_w[k] : pre;
+        uint32_t excl = __shfl_up(incl, 1);
+        if (lane == 0) excl = 0;
+        excl = excl > pre ? excl : pre;
+        uint8_t cur = excl ? (uint8_t)(excl & 0xFFu) : carry[t];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const uint32_t m = (f[k >> 2] >> (8 * (k & 3))) & 0xFFu;
+            if (m) cur = (uint8_t)m;
+            s_v[threadIdx.x * 16u + k] = cur;
+        }
+        __syncthreads();
+        const uint32_t tile0 = t * kTile;
+        for (uint32_t j = threadIdx.x; j < kTile && tile0 + j < M; j += 256) {
+            const uint8_t v = s_v[j];
+            verdict[pk_idx(S[tile0 + j])] = v;
+            n_pass += v == XDP_PASS;
+            n_drop += v == XDP_DROP;
+        }
+        __syncthreads();
+    }
+    n_pass = wave_incl_sum(n_pass);
+    n_drop = wave_incl_sum(n_drop);
+    if (lane == 63) { s_cnt[w][0] = n_pass; s_cnt[w][1] = n_drop; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long a = 0, d = 0;
+        for (int k = 0; k < 4; ++k) { a += s_cnt[k][0]; d += s_cnt[k][1]; }
+        if (a) {
+            atomicAdd(reinterpret_cast<unsigned long long *>(&tstate->stats[0]), a);
+            atomicAdd(reinterpret_cast<unsigned long long *>(&bs->allowed), a);
+        }
+        if (d) {
+            atomicAdd(reinterpret_cast<unsigned long long *>(&tstate->stats[1]), d);
+            atomicAdd(reinterpret_cast<unsigned long long *>(&bs->dropped), d);
+        }
+    }
+}
+
+// ------------------------------------------------------------------ pipeline
+static inline uint32_t cdiv(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); }
+
+hipError_t launch_verdict_pipeline(const uint8_t *hdr, const uint32_t *len, const uint64_t *ts,
+                                   uint32_t n, uint8_t *verdict, Slot *table, TableState *tstate,
+                                   BatchState *bs, const Scratch &sc, const Limits &lim,
+                                   hipStream_t st, hipEvent_t *ev, int nev, int *nev_used,
+                                   const char **names) {
+    int ei = 0;
+    auto mark = [&](const char *name) {
+        if (ev && ei < nev) {
+            if (names) names[ei] = name;
+            hipEventRecord(ev[ei], st);
+            ++ei;
+        }
+    };
+    hipError_t e;
+    if ((e = hipMemsetAsync(bs, 0, sizeof(BatchState), st)) != hipSuccess) return e;
+    if (n == 0) { if (nev_used) *nev_used = 0; return hipSuccess; }
+    if ((e = hipMemsetAsync(sc.marks, 0, n, st)) != hipSuccess) return e;
+    const uint32_t G = std::min<uint32_t>(kSortMaxBlocks, std::max<uint32_t>(1, cdiv(n, kSortTile)));
+    const uint32_t gridStream = std::min<uint32_t>(2048, std::max<uint32_t>(1, cdiv(n, 256)));
+    const uint32_t gridTiles = std::min<uint32_t>(4096, std::max<uint32_t>(1, cdiv(n, kTile)));
+
+    // mark(name) closes the interval of the kernel just enqueued (per-kernel timing)
+    mark("start");
+    k_parse<<<std::min<uint32_t>(2048, std::max<uint32_t>(1, cdiv(n, 256))), 256, 0, st>>>(
+        hdr, len, ts, n, sc.packed[0], verdict, bs, lim.salt32, lim.seed,
+        (lim.test_flags & 1u) ? skey_v4(0x0100000Au, lim.salt32) : 0u);
+    mark("k_parse");
+    for (int pass = 0; pass < 4; ++pass) {
+        const uint64_t *in = sc.packed[pass & 1];
+        uint64_t *out = sc.packed[(pass + 1) & 1];
+        const uint32_t shift = 32u + 8u * (uint32_t)pass;
+        const uint32_t *Ld = pass == 0 ? nullptr : &bs->n_valid;
+        k_sort_hist<<<G, 256, 0, st>>>(in, n, Ld, shift, sc.hist, G, pass == 0, bs);
+        mark("k_sort_hist");
+        k_sort_rowscan<<<256, 256, 0, st>>>(sc.hist, G, sc.row_total);
+        mark("k_sort_rowscan");
+        k_sort_scatter<<<G, 256, 0, st>>>(in, out, n, Ld, shift, sc.hist, sc.row_total, G, pass == 0);
+        mark("k_sort_scatter");
+    }
+    uint64_t *S = sc.packed[0];
+    const uint32_t nbm = cdiv(n, 64);
+    if ((e = hipMemsetAsync(sc.fix_bitmap, 0, (size_t)nbm * 8, st)) != hipSuccess) return e;
+    k_v6_mixed<<<gridStream, 256, 0, st>>>(S, bs, hdr, sc.fix_bitmap, sc.fix_list);
+    k_fixup_short<<<256, 256, 0, st>>>(S, bs, hdr, sc.fix_list, lim.salt32);
+    k_fixup_long<<<64, 256, 0, st>>>(S, sc.packed[1], bs, hdr, sc.fix_list, lim.salt32);
+    mark("v6_fixup");
+    k_heads_count<<<gridTiles, 256, 0, st>>>(S, bs, hdr, sc.headf, sc.tile_aux);
+    mark("k_heads_count");
+    k_scan_tiles_u32<<<1, 1024, 0, st>>>(sc.tile_aux, bs, sc.seg_start);
+    k_heads_write<<<gridTiles, 256, 0, st>>>(bs, sc.headf, sc.tile_aux, sc.seg_start);
+    mark("k_heads_write");
+    k_lookup<<<gridStream, 256, 0, st>>>(S, bs, sc.seg_start, sc.seg_slot, hdr, table, lim);
+    mark("k_lookup");
+    k_insert<<<gridStream, 256, 0, st>>>(S, bs, sc.seg_start, sc.seg_slot, hdr, table, tstate, lim);
+    mark("k_insert");
+    k_walk_fixed<<<gridStream, 256, 0, st>>>(S, bs, sc.seg_start, sc.seg_slot, ts, len, sc.marks,
+                                             table, lim);
+    mark("k_walk_fixed");
+    k_fill_last<<<gridTiles, 256, 0, st>>>(sc.marks, bs, sc.tile_last);
+    k_fill_carry<<<1, 1024, 0, st>>>(sc.tile_last, bs);
+    mark("k_fill_last");
+    k_fill_scatter<<<gridTiles, 256, 0, st>>>(sc.marks, S, bs, sc.tile_last, verdict, tstate);
+    mark("k_fill_scatter");
+    if (nev_used) *nev_used = ei;
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------ map syscalls
+// op: 0 lookup, 1 update, 2 delete. Result: 0 / -ENOENT(-2) / -EEXIST(-17) / -ENOSPC(-28).
+__global__ void k_map_op(Slot *table, TableState *tstate, Limits lim, int op, int map_id,
+                         uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3, uint64_t v0,
+                         uint64_t v1, uint64_t v2, uint64_t flags, int32_t *res, uint64_t *outv) {
+    if (threadIdx.x || blockIdx.x) return;
+    const uint32_t k[4] = {k0, k1, k2, k3};
+    const uint32_t tag = (map_id == 2 || map_id == 4) ? 2u : 1u;
+    const uint32_t bit = (map_id == 1 || map_id == 2) ? SLOT_HAS_ST : SLOT_HAS_BL;
+    uint32_t s = table_find(table, lim.table_mask, tag, k, lim.seed);
+    const bool present = s != kNoSlot && (table[s].flags & bit);
+    if (op == 0) {
+        if (!present) { *res = -2; return; }
+        if (bit == SLOT_HAS_ST) { outv[0] = table[s].pps; outv[1] = table[s].bps; outv[2] = table[s].tt; }
+        else outv[0] = table[s].till;
+        *res = 0;
+        return;
+    }
+    if (op == 2) {
+        if (!present) { *res = -2; return; }
+        table[s].flags &= ~bit;
+        *res = 0;
+        return;
+    }
+    if (flags == 1 && present) { *res = -17; return; }
+    if (flags == 2 && !present) { *res = -2; return; }
+    if (s == kNoSlot) {
+        if (tstate->count >= lim.max_entries) { *res = -28; return; }
+        s = table_claim(table, lim.table_mask, tag, k, lim.seed);
+        if (s == kNoSlot) { *res = -28; return; }
+        tstate->count += 1;
+    }
+    if (bit == SLOT_HAS_ST) { table[s].pps = v0; table[s].bps = v1; table[s].tt = v2; }
+    else table[s].till = v0;
+    table[s].flags |= bit;
+    *res = 0;
+}
+
+hipError_t launch_map_op(Slot *table, TableState *tstate, const Limits &lim, int op, int map_id,
+                         const uint32_t key[4], const uint64_t val[3], uint64_t flags,
+                         int32_t *d_result, uint64_t *d_val, hipStream_t st) {
+    k_map_op<<<1, 64, 0, st>>>(table, tstate, lim, op, map_id, key[0], key[1], key[2], key[3],
+                               val[0], val[1], val[2], flags, d_result, d_val);
+    return hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void k_map_dump(const Slot *table, Limits lim, int map_id,
+                                                  uint8_t *keys, uint64_t *vals, uint64_t cap,
+                                                  unsigned long long *count) {
+    const uint32_t tag = (map_id == 2 || map_id == 4) ? 2u : 1u;
+    const uint32_t bit = (map_id == 1 || map_id == 2) ? SLOT_HAS_ST : SLOT_HAS_BL;
+    const uint32_t klen = tag == 2 ? 16u : 4u;
+    const uint32_t vw = bit == SLOT_HAS_ST ? 3u : 1u;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i <= lim.table_mask;
+         i += (uint64_t)gridDim.x * 256u) {
+        const Slot &s = table[i];
+        if (s.tag != tag || !(s.flags & bit)) continue;
+        const unsigned long long o = atomicAdd(count, 1ull);
+        if (o >= cap) continue;
+        const uint8_t *kb = reinterpret_cast<const uint8_t *>(s.key);
+        for (uint32_t b = 0; b < klen; ++b) keys[o * klen + b] = kb[b];
+        if (vw == 3) { vals[o * 3] = s.pps; vals[o * 3 + 1] = s.bps; vals[o * 3 + 2] = s.tt; }
+        else vals[o] = s.till;
+    }
+}
+
+hipError_t launch_map_dump(const Slot *table, const Limits &lim, int map_id, uint8_t *d_keys,
+                           uint64_t *d_vals, uint64_t cap, unsigned long long *d_count,
+                           hipStream_t st) {
+    const uint64_t slots = lim.table_mask + 1;
+    const uint32_t grid = (uint32_t)std::min<uint64_t>(4096, (slots + 255) / 256);
+    k_map_dump<<<grid, 256, 0, st>>>(table, lim, map_id, d_keys, d_vals, cap, d_count);
+    return hipGetLastError();
+}
+
+}  // namespace fsx

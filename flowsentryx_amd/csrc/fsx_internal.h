@@ -1,0 +1,149 @@
+// fsx_internal.h — device data layout and kernel launchers of libfsx_hip.so.
+//
+// HBM layout:
+//   * the five reference maps live in ONE device-resident open-addressing table of
+//     64-byte slots (one cache line per source IP: tag, key, ip_stats, blacklist),
+//     capacity = next_pow2(2 * max_entries) — src/fsx_kern.c:56-94;
+//   * per-batch scratch sized for cfg.max_batch packets: the packed sort words
+//     (two ping-pong arrays of u64), a u8 mark per sorted position, the ordered
+//     segment starts and their table slots.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace fsx {
+
+constexpr uint64_t kSentinel = ~0ull;     // "not an IP packet" in the packed array
+constexpr uint32_t kNoSlot = 0xFFFFFFFFu;
+
+// Radix sort geometry: 8-bit digits, 256-thread blocks, 16 items/thread tiles.
+constexpr int kSortThreads = 256;
+constexpr int kSortItems = 16;
+constexpr int kSortTile = kSortThreads * kSortItems;  // 4096
+constexpr int kSortMaxBlocks = 2048;
+constexpr int kTile = 4096;                            // fill / compaction tile
+
+enum : uint32_t {
+    ERR_TABLE_FULL = 1u,
+    ERR_PROBE = 2u,
+    ERR_FIXUP = 4u,
+};
+
+enum : uint32_t { SLOT_HAS_ST = 1u, SLOT_HAS_BL = 2u, SLOT_HAS_TB = 4u };
+
+// One source IP (either family). tag: 0 empty, 1 IPv4, 2 IPv6.
+struct alignas(64) Slot {
+    uint32_t tag;
+    uint32_t flags;       // SLOT_HAS_*
+    uint32_t key[4];      // raw saddr bytes (IPv4: key[0] only)
+    uint64_t pps;         // struct ip_stats, src/fsx_struct.h:17-22
+    uint64_t bps;
+    uint64_t tt;          // track_time
+    uint64_t till;        // ipv{4,6}_blacklist_map value
+    uint64_t aux;         // token bucket: nano-tokens (tt = last refill time)
+};
+static_assert(sizeof(Slot) == 64, "slot is one cache line");
+
+// Device-side per-batch scalars (zeroed before each batch).
+struct BatchState {
+    uint32_t n_valid;     // IP packets (entries that go through the sort)
+    uint32_t any_v6;
+    uint32_t nonmono;     // a timestamp decreased in arrival order
+    uint32_t nseg;        // distinct source IPs in the batch
+    uint32_t n_new;
+    uint32_t err;
+    uint32_t max_len;
+    uint32_t n_fix;       // mixed hash runs queued for the exact key fixup
+    uint64_t max_ts;
+    uint64_t allowed;     // this batch
+    uint64_t dropped;
+};
+
+// Persistent device scalars.
+struct TableState {
+    uint64_t count;       // occupied slots
+    uint64_t stats[2];    // stats_map {allowed, dropped}, src/fsx_struct.h:11-15
+};
+
+struct Limits {           // the rate-limiter constants, src/fsx_kern.c:245,308-310
+    uint64_t pps, bps, window, block;
+    uint64_t tb_rate, tb_cap;  // token bucket, nano-tokens
+    uint64_t max_entries;
+    uint64_t table_mask;
+    uint64_t seed;
+    uint32_t salt32;
+    int32_t limiter;
+    uint32_t test_flags;  // FSX_FLAG_TEST_*: test hooks (include/fsx_hip.h)
+};
+
+// ------------------------------------------------------------ hashing
+__host__ __device__ inline uint64_t mix64(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+__host__ __device__ inline uint32_t fmix32(uint32_t h) {
+    h ^= h >> 16; h *= 0x85ebca6bu; h ^= h >> 13; h *= 0xc2b2ae35u; h ^= h >> 16;
+    return h;
+}
+__host__ __device__ inline uint32_t fmix32_inv(uint32_t h) {
+    h ^= h >> 16; h *= 0x7ed1b41du; h ^= (h >> 13) ^ (h >> 26); h *= 0xa5cb9243u; h ^= h >> 16;
+    return h;
+}
+// IPv4 sort key: a bijection of the address, so equal sort keys <=> equal address.
+__host__ __device__ inline uint32_t skey_v4(uint32_t ip, uint32_t salt) { return fmix32(ip ^ salt); }
+__host__ __device__ inline uint32_t ip_of_skey(uint32_t sk, uint32_t salt) { return fmix32_inv(sk) ^ salt; }
+// IPv6 sort key: salted 32-bit hash (collisions resolved exactly by the fixup pass).
+__host__ __device__ inline uint32_t skey_v6(const uint32_t k[4], uint64_t seed) {
+    uint64_t a = (uint64_t)k[0] | ((uint64_t)k[1] << 32);
+    uint64_t b = (uint64_t)k[2] | ((uint64_t)k[3] << 32);
+    return (uint32_t)(mix64(mix64(seed ^ a) ^ b) >> 32);
+}
+__host__ __device__ inline uint64_t slot_hash(uint32_t tag, const uint32_t k[4], uint64_t seed) {
+    uint64_t h = mix64(seed ^ ((uint64_t)tag << 56) ^ ((uint64_t)k[0] | ((uint64_t)k[1] << 32)));
+    if (tag == 2) h = mix64(h ^ ((uint64_t)k[2] | ((uint64_t)k[3] << 32)));
+    return h;
+}
+
+// packed sort word: skey << 32 | family << 31 | arrival index (n <= 2^31 - 1)
+__host__ __device__ inline uint32_t pk_skey(uint64_t v) { return (uint32_t)(v >> 32); }
+__host__ __device__ inline uint32_t pk_fam(uint64_t v) { return (uint32_t)(v >> 31) & 1u; }
+__host__ __device__ inline uint32_t pk_idx(uint64_t v) { return (uint32_t)v & 0x7FFFFFFFu; }
+
+// ------------------------------------------------------------ launchers (fsx_device.hip)
+struct Scratch {
+    uint64_t *packed[2];
+    uint8_t *marks;        // per sorted position: 0 none, else verdict starting there
+    uint8_t *headf;        // per sorted position: segment-head flag
+    uint32_t *seg_start;   // nseg + 1
+    uint32_t *seg_slot;
+    uint32_t *hist;        // 256 * kSortMaxBlocks
+    uint32_t *row_total;   // 256
+    uint32_t *tile_aux;    // per kTile tile
+    uint8_t *tile_last;
+    uint32_t *fix_list;
+    uint64_t *fix_bitmap;  // one bit per sorted position
+    uint64_t cap;          // packets the scratch is sized for
+};
+
+hipError_t launch_verdict_pipeline(const uint8_t *hdr, const uint32_t *len, const uint64_t *ts,
+                                   uint32_t n, uint8_t *verdict, Slot *table, TableState *tstate,
+                                   BatchState *bs, const Scratch &sc, const Limits &lim,
+                                   hipStream_t st, hipEvent_t *ev, int nev, int *nev_used,
+                                   const char **names);
+
+hipError_t launch_map_op(Slot *table, TableState *tstate, const Limits &lim, int op, int map_id,
+                         const uint32_t key[4], const uint64_t val[3], uint64_t flags,
+                         int32_t *d_result, uint64_t *d_val, hipStream_t st);
+
+hipError_t launch_map_dump(const Slot *table, const Limits &lim, int map_id, uint8_t *d_keys,
+                           uint64_t *d_vals, uint64_t cap, unsigned long long *d_count,
+                           hipStream_t st);
+
+hipError_t launch_score(const float *feat, size_t n, float *prob, uint8_t *dec,
+                        const int8_t w[8], float inv_in, int32_t zp_in, float bias_over_ats,
+                        float mult, int32_t zp_out, const uint8_t lut[256], hipStream_t st);
+
+}  // namespace fsx

@@ -1,0 +1,349 @@
+"""ctypes binding of libfsx_hip.so (include/fsx_hip.h).
+
+This is the Python side of the drop-in boundary: the role src/fsx_load.py plays for
+the reference (load the data plane, push model weights into it, read its maps),
+calling the C ABI directly. It never falls back to a CPU path: if the native
+library is missing or no GPU is present, opening a context raises FsxError.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import errno
+import os
+from pathlib import Path
+
+import numpy as np
+
+_PKG = Path(__file__).resolve().parent
+
+XDP_DROP = 1
+XDP_PASS = 2
+HDR_BYTES = 64
+
+# enum fsx_map_id — the five maps of src/fsx_kern.c:56-94
+MAP_STATS = 0
+MAP_IPV4_STATS = 1
+MAP_IPV6_STATS = 2
+MAP_IPV4_BLACKLIST = 3
+MAP_IPV6_BLACKLIST = 4
+MAP_NAMES = {
+    MAP_STATS: "stats_map",
+    MAP_IPV4_STATS: "ipv4_stats_map",
+    MAP_IPV6_STATS: "ipv6_stats_map",
+    MAP_IPV4_BLACKLIST: "ipv4_blacklist_map",
+    MAP_IPV6_BLACKLIST: "ipv6_blacklist_map",
+}
+BPF_ANY, BPF_NOEXIST, BPF_EXIST = 0, 1, 2
+
+LIMIT_FIXED_WINDOW = 0
+LIMIT_SLIDING_WINDOW = 1
+LIMIT_TOKEN_BUCKET = 2
+
+
+class FsxError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"[{errno.errorcode.get(-code, code)}] {msg}")
+        self.code = code
+
+
+class FsxConfig(C.Structure):
+    _fields_ = [
+        ("pps_threshold", C.c_uint64),
+        ("bps_threshold", C.c_uint64),
+        ("window_ns", C.c_uint64),
+        ("block_ns", C.c_uint64),
+        ("max_entries", C.c_uint64),
+        ("max_batch", C.c_uint64),
+        ("tb_rate", C.c_uint64),
+        ("tb_burst", C.c_uint64),
+        ("hash_seed", C.c_uint64),
+        ("limiter", C.c_int32),
+        ("device", C.c_int32),
+        ("flags", C.c_uint32),
+        ("reserved", C.c_uint32 * 7),
+    ]
+
+
+class FsxStats(C.Structure):
+    _fields_ = [("allowed", C.c_uint64), ("dropped", C.c_uint64)]
+
+
+class FsxQ8Model(C.Structure):
+    _fields_ = [
+        ("weight", C.c_int8 * 8),
+        ("weight_scale", C.c_float),
+        ("bias", C.c_float),
+        ("in_scale", C.c_float),
+        ("in_zero_point", C.c_int32),
+        ("out_scale", C.c_float),
+        ("out_zero_point", C.c_int32),
+    ]
+
+
+_lib = None
+
+
+def library_path() -> Path:
+    return _PKG / "libfsx_hip.so"
+
+
+def load_library() -> C.CDLL:
+    """Load the in-tree libfsx_hip.so (fails loudly when it is not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    path = library_path()
+    if not path.exists():
+        raise FsxError(-errno.ENOENT,
+                       f"{path} is not built: run `python -m flowsentryx_amd.build`")
+    lib = C.CDLL(str(path))
+    vp, sz, u8p = C.c_void_p, C.c_size_t, C.c_void_p
+    sig = {
+        "fsx_abi_version": (C.c_int, []),
+        "fsx_config_default": (None, [C.POINTER(FsxConfig)]),
+        "fsx_open": (C.c_int, [C.POINTER(vp), C.POINTER(FsxConfig)]),
+        "fsx_close": (None, [vp]),
+        "fsx_last_error": (C.c_char_p, [vp]),
+        "fsx_set_stream": (C.c_int, [vp, vp]),
+        "fsx_sync": (C.c_int, [vp]),
+        "fsx_verdict_batch": (C.c_int, [vp, u8p, u8p, u8p, sz, u8p]),
+        "fsx_verdict_batch_device": (C.c_int, [vp, vp, vp, vp, sz, vp]),
+        "fsx_map_lookup": (C.c_int, [vp, C.c_int, vp, vp]),
+        "fsx_map_update": (C.c_int, [vp, C.c_int, vp, vp, C.c_uint64]),
+        "fsx_map_delete": (C.c_int, [vp, C.c_int, vp]),
+        "fsx_map_dump": (C.c_int, [vp, C.c_int, vp, vp, sz, C.POINTER(sz)]),
+        "fsx_get_stats": (C.c_int, [vp, C.POINTER(FsxStats)]),
+        "fsx_reset": (C.c_int, [vp]),
+        "fsx_load_q8_model": (C.c_int, [vp, C.POINTER(FsxQ8Model)]),
+        "fsx_score": (C.c_int, [vp, vp, sz, vp, vp]),
+        "fsx_score_device": (C.c_int, [vp, vp, sz, vp, vp]),
+        "fsx_flow_features": (C.c_int, [vp, vp, vp, vp, sz, sz, vp, vp, vp, C.POINTER(sz)]),
+        "fsx_last_timings": (C.c_int, [vp, vp, vp, vp, C.c_int, C.c_int, C.POINTER(C.c_int)]),
+        "fsx_enable_timing": (C.c_int, [vp, C.c_int]),
+        "fsx_last_batch_info": (C.c_int, [vp, vp, C.c_int]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = lib
+    return lib
+
+
+# Every symbol include/fsx_hip.h declares (checked by tests/test_abi.py).
+ABI_SYMBOLS = [
+    "fsx_abi_version", "fsx_config_default", "fsx_open", "fsx_close", "fsx_last_error",
+    "fsx_set_stream", "fsx_sync", "fsx_verdict_batch", "fsx_verdict_batch_device",
+    "fsx_map_lookup", "fsx_map_update", "fsx_map_delete", "fsx_map_dump", "fsx_get_stats",
+    "fsx_reset", "fsx_load_q8_model", "fsx_score", "fsx_score_device", "fsx_flow_features",
+    "fsx_last_timings", "fsx_enable_timing", "fsx_last_batch_info",
+]
+
+
+def default_config(**overrides) -> FsxConfig:
+    lib = load_library()
+    cfg = FsxConfig()
+    lib.fsx_config_default(C.byref(cfg))
+    for k, v in overrides.items():
+        if not hasattr(cfg, k):
+            raise TypeError(f"unknown config field {k}")
+        setattr(cfg, k, v)
+    return cfg
+
+
+def _ptr(a: np.ndarray) -> int:
+    return a.ctypes.data
+
+
+def _key_bytes(map_id: int, key) -> bytes:
+    if isinstance(key, int):
+        key = key.to_bytes(4, "little")
+    key = bytes(key)
+    want = 16 if map_id in (MAP_IPV6_STATS, MAP_IPV6_BLACKLIST) else 4
+    if len(key) != want:
+        raise ValueError(f"{MAP_NAMES[map_id]} keys are {want} bytes")
+    return key
+
+
+class FsxContext:
+    """One data-plane instance (the XDP program + its five maps) on one GPU."""
+
+    def __init__(self, config: FsxConfig | None = None, **overrides):
+        self._lib = load_library()
+        self.config = config if config is not None else default_config(**overrides)
+        h = C.c_void_p()
+        rc = self._lib.fsx_open(C.byref(h), C.byref(self.config))
+        if rc != 0:
+            raise FsxError(rc, "fsx_open failed (no GPU or bad config)")
+        self._h = h
+
+    # -- plumbing
+    def _check(self, rc: int, what: str):
+        if rc != 0:
+            msg = self._lib.fsx_last_error(self._h)
+            raise FsxError(rc, f"{what}: {msg.decode() if msg else ''}")
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.fsx_close(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def sync(self):
+        self._check(self._lib.fsx_sync(self._h), "fsx_sync")
+
+    def set_stream(self, stream_handle: int | None):
+        self._check(self._lib.fsx_set_stream(self._h, stream_handle or None), "fsx_set_stream")
+
+    # -- verdict path
+    def verdict_batch(self, hdr: np.ndarray, length: np.ndarray, ts: np.ndarray) -> np.ndarray:
+        hdr = np.ascontiguousarray(hdr, dtype=np.uint8).reshape(-1, HDR_BYTES)
+        n = hdr.shape[0]
+        length = np.ascontiguousarray(length, dtype=np.uint32)
+        ts = np.ascontiguousarray(ts, dtype=np.uint64)
+        if length.shape != (n,) or ts.shape != (n,):
+            raise ValueError("hdr, len and ts must describe the same packets")
+        out = np.empty(n, dtype=np.uint8)
+        if n:
+            self._check(self._lib.fsx_verdict_batch(self._h, _ptr(hdr), _ptr(length), _ptr(ts),
+                                                    n, _ptr(out)), "fsx_verdict_batch")
+        return out
+
+    def verdict_batch_device(self, d_hdr: int, d_len: int, d_ts: int, n: int, d_verdict: int):
+        self._check(self._lib.fsx_verdict_batch_device(self._h, d_hdr, d_len, d_ts, n, d_verdict),
+                    "fsx_verdict_batch_device")
+
+    # -- maps (bpf_map_*_elem)
+    def map_lookup(self, map_id: int, key):
+        if map_id == MAP_STATS:
+            v = (C.c_uint64 * 2)()
+            self._check(self._lib.fsx_map_lookup(self._h, map_id, C.byref(C.c_uint32(0)), v),
+                        "map_lookup")
+            return tuple(v)
+        k = _key_bytes(map_id, key)
+        v = (C.c_uint64 * 3)()
+        rc = self._lib.fsx_map_lookup(self._h, map_id, k, v)
+        if rc == -errno.ENOENT:
+            return None
+        self._check(rc, "map_lookup")
+        return tuple(v) if map_id in (MAP_IPV4_STATS, MAP_IPV6_STATS) else int(v[0])
+
+    def map_update(self, map_id: int, key, value, flags: int = BPF_ANY):
+        if map_id == MAP_STATS:
+            v = (C.c_uint64 * 2)(*value)
+            self._check(self._lib.fsx_map_update(self._h, map_id, C.byref(C.c_uint32(int(key))), v,
+                                                 flags), "map_update")
+            return
+        k = _key_bytes(map_id, key)
+        if map_id in (MAP_IPV4_STATS, MAP_IPV6_STATS):
+            v = (C.c_uint64 * 3)(*value)
+        else:
+            v = (C.c_uint64 * 1)(int(value))
+        self._check(self._lib.fsx_map_update(self._h, map_id, k, v, flags), "map_update")
+
+    def map_delete(self, map_id: int, key) -> bool:
+        rc = self._lib.fsx_map_delete(self._h, map_id, _key_bytes(map_id, key))
+        if rc == -errno.ENOENT:
+            return False
+        self._check(rc, "map_delete")
+        return True
+
+    def map_dump(self, map_id: int) -> dict:
+        n = C.c_size_t()
+        self._check(self._lib.fsx_map_dump(self._h, map_id, None, None, 0, C.byref(n)), "map_dump")
+        cap = n.value
+        if map_id == MAP_STATS:
+            return {0: self.map_lookup(MAP_STATS, 0)}
+        klen = 16 if map_id in (MAP_IPV6_STATS, MAP_IPV6_BLACKLIST) else 4
+        vw = 3 if map_id in (MAP_IPV4_STATS, MAP_IPV6_STATS) else 1
+        keys = np.zeros((max(cap, 1), klen), dtype=np.uint8)
+        vals = np.zeros((max(cap, 1), vw), dtype=np.uint64)
+        self._check(self._lib.fsx_map_dump(self._h, map_id, _ptr(keys), _ptr(vals), cap, C.byref(n)),
+                    "map_dump")
+        m = min(cap, n.value)
+        out = {}
+        for i in range(m):
+            out[keys[i].tobytes()] = tuple(int(x) for x in vals[i]) if vw == 3 else int(vals[i, 0])
+        return out
+
+    def stats(self) -> tuple[int, int]:
+        s = FsxStats()
+        self._check(self._lib.fsx_get_stats(self._h, C.byref(s)), "fsx_get_stats")
+        return int(s.allowed), int(s.dropped)
+
+    def reset(self):
+        self._check(self._lib.fsx_reset(self._h), "fsx_reset")
+
+    # -- scoring
+    def load_q8_model(self, model: FsxQ8Model):
+        self._check(self._lib.fsx_load_q8_model(self._h, C.byref(model)), "fsx_load_q8_model")
+
+    def score(self, features: np.ndarray):
+        f = np.ascontiguousarray(features, dtype=np.float32).reshape(-1, 8)
+        n = f.shape[0]
+        p = np.empty(n, dtype=np.float32)
+        d = np.empty(n, dtype=np.uint8)
+        if n:
+            self._check(self._lib.fsx_score(self._h, _ptr(f), n, _ptr(p), _ptr(d)), "fsx_score")
+        return p, d
+
+    def score_device(self, d_feat: int, n: int, d_prob: int, d_dec: int):
+        self._check(self._lib.fsx_score_device(self._h, d_feat, n, d_prob, d_dec), "fsx_score_device")
+
+    def flow_features(self, hdr: np.ndarray, length: np.ndarray, ts: np.ndarray):
+        hdr = np.ascontiguousarray(hdr, dtype=np.uint8).reshape(-1, HDR_BYTES)
+        n = hdr.shape[0]
+        length = np.ascontiguousarray(length, dtype=np.uint32)
+        ts = np.ascontiguousarray(ts, dtype=np.uint64)
+        keys = np.zeros((max(n, 1), 16), dtype=np.uint8)
+        fam = np.zeros(max(n, 1), dtype=np.uint8)
+        feat = np.zeros((max(n, 1), 8), dtype=np.float32)
+        nf = C.c_size_t()
+        self._check(self._lib.fsx_flow_features(self._h, _ptr(hdr), _ptr(length), _ptr(ts), n,
+                                                max(n, 1), _ptr(keys), _ptr(fam), _ptr(feat),
+                                                C.byref(nf)), "fsx_flow_features")
+        m = nf.value
+        return keys[:m], fam[:m], feat[:m]
+
+    BATCH_INFO = ("ip_packets", "sources", "new_sources", "any_ipv6", "non_monotone",
+                  "max_len", "max_ts", "allowed", "dropped", "v6_fix_runs")
+
+    def last_batch_info(self) -> dict:
+        buf = (C.c_uint64 * 10)()
+        rc = self._lib.fsx_last_batch_info(self._h, buf, 10)
+        if rc < 0:
+            self._check(rc, "fsx_last_batch_info")
+        return {k: int(buf[i]) for i, k in enumerate(self.BATCH_INFO[:rc])}
+
+    # -- timing
+    def enable_timing(self, on: bool = True):
+        self._check(self._lib.fsx_enable_timing(self._h, int(on)), "fsx_enable_timing")
+
+    def last_timings(self) -> list[tuple[str, float, float]]:
+        """[(kernel, ms per batch, launches per batch)] since the previous call."""
+        cap, nl = 48, 32
+        ms = (C.c_float * cap)()
+        nlaunch = (C.c_float * cap)()
+        names = C.create_string_buffer(cap * nl)
+        cnt = C.c_int()
+        self._check(self._lib.fsx_last_timings(self._h, ms, nlaunch, names, cap, nl, C.byref(cnt)),
+                    "fsx_last_timings")
+        raw = names.raw
+        return [(raw[i * nl:(i + 1) * nl].split(b"\0")[0].decode(), float(ms[i]), float(nlaunch[i]))
+                for i in range(cnt.value)]
+
+
+def ipv4_key(addr: str) -> bytes:
+    """Map key of an IPv4 source: the raw saddr bytes (network order)."""
+    return bytes(int(x) for x in addr.split("."))

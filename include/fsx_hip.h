@@ -1,0 +1,193 @@
+/*
+ * fsx_hip.h — C ABI of libfsx_hip.so, the MI355X (gfx950) batch data plane that
+ * replaces FlowSentryX's packet-verdict hot path.
+ *
+ * Reference boundary being replaced (paths relative to the FlowSentryX tree):
+ *   - the XDP program ABI  `SEC("xdp") int fsx(struct xdp_md *ctx)`
+ *       src/fsx_kern.c:96-97  -> fsx_verdict_batch / fsx_verdict_batch_device
+ *     returning XDP_DROP (1) / XDP_PASS (2) per packet, in arrival order;
+ *   - the five BPF maps that are its state/control ABI, src/fsx_kern.c:56-94
+ *       stats_map           ARRAY[1]  key u32 0 -> struct stats {allowed,dropped}
+ *       ipv4_stats_map      LRU_HASH  key 4 B   -> struct ip_stats {pps,bps,track_time}
+ *       ipv6_stats_map      LRU_HASH  key 16 B  -> struct ip_stats
+ *       ipv4_blacklist_map  LRU_HASH  key 4 B   -> u64 blocked_till_ns
+ *       ipv6_blacklist_map  LRU_HASH  key 16 B  -> u64 blocked_till_ns
+ *     -> fsx_map_lookup / fsx_map_update / fsx_map_delete / fsx_map_dump with the
+ *        exact key/value byte layouts of src/fsx_struct.h:11-22;
+ *   - the host weight loader role of src/fsx_load.py:1-18 (push the quantized
+ *     model_weights.pth into the data plane) -> fsx_load_q8_model;
+ *   - the model forward of model/model.py:132-137 and its decision y > 0.5
+ *     (model/model.py:206) -> fsx_score / fsx_score_device.
+ *
+ * Conventions
+ *   - Every entry point returns 0 or a negative errno (-EINVAL, -ENOMEM, -EIO for
+ *     HIP runtime errors, -ENOENT, -EEXIST, -ENOSPC, -E2BIG). Nothing throws or
+ *     longjmps across this boundary. fsx_last_error() returns a message.
+ *   - Host pointers are owned by the caller and are not retained after return.
+ *   - One context per host thread; calls on one context are serialized by the
+ *     caller. Results are deterministic and equal to the reference program's
+ *     single-CPU, arrival-order semantics.
+ *   - A packet is a 64-byte header record (the first min(len,64) frame bytes,
+ *     zero padded), its frame length `len` (data_end - data, FCS excluded) and
+ *     its arrival time `ts_ns` (the value bpf_ktime_get_ns() returns at
+ *     src/fsx_kern.c:150).
+ */
+#ifndef FSX_HIP_H
+#define FSX_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FSX_ABI_VERSION 1
+
+/* Verdict codes: the XDP return values of src/fsx_kern.c (enum xdp_action). */
+#define FSX_XDP_DROP 1
+#define FSX_XDP_PASS 2
+
+#define FSX_HDR_BYTES 64
+
+/* fsx_config.flags — test hooks only. FSX_FLAG_TEST_V6_COLLIDE sends every IPv6
+ * source to one sort key equal to IPv4 10.0.0.1's, forcing the exact collision
+ * fixup path (results must not change). */
+#define FSX_FLAG_TEST_V6_COLLIDE 1u
+
+/* Map ids: the five maps of src/fsx_kern.c:56-94. */
+enum fsx_map_id {
+    FSX_MAP_STATS = 0,          /* stats_map          src/fsx_kern.c:56-62 */
+    FSX_MAP_IPV4_STATS = 1,     /* ipv4_stats_map     src/fsx_kern.c:64-70 */
+    FSX_MAP_IPV6_STATS = 2,     /* ipv6_stats_map     src/fsx_kern.c:72-78 */
+    FSX_MAP_IPV4_BLACKLIST = 3, /* ipv4_blacklist_map src/fsx_kern.c:80-86 */
+    FSX_MAP_IPV6_BLACKLIST = 4, /* ipv6_blacklist_map src/fsx_kern.c:88-94 */
+    FSX_MAP_COUNT = 5
+};
+
+/* bpf_map_update_elem flags (linux/bpf.h). */
+#define FSX_BPF_ANY 0
+#define FSX_BPF_NOEXIST 1
+#define FSX_BPF_EXIST 2
+
+/* Limiter algorithms. FIXED is the reference program (src/fsx_kern.c:225-336).
+ * SLIDING and TOKEN_BUCKET are build-defined (README.md:155-162 only names them);
+ * their semantics are specified in DESIGN.md §4. */
+enum fsx_limiter {
+    FSX_LIMIT_FIXED_WINDOW = 0,
+    FSX_LIMIT_SLIDING_WINDOW = 1,
+    FSX_LIMIT_TOKEN_BUCKET = 2
+};
+
+/* struct stats, src/fsx_struct.h:11-15 */
+typedef struct fsx_stats {
+    uint64_t allowed;
+    uint64_t dropped;
+} fsx_stats;
+
+/* struct ip_stats, src/fsx_struct.h:17-22 */
+typedef struct fsx_ip_stats {
+    uint64_t pps;
+    uint64_t bps;
+    uint64_t track_time;
+} fsx_ip_stats;
+
+typedef struct fsx_config {
+    uint64_t pps_threshold;   /* 1000       src/fsx_kern.c:309 */
+    uint64_t bps_threshold;   /* 125000000  src/fsx_kern.c:310 */
+    uint64_t window_ns;       /* 1000000000 src/fsx_kern.c:245 */
+    uint64_t block_ns;        /* 10 s       src/fsx_kern.c:308,317 */
+    uint64_t max_entries;     /* per map; MAX_TRACK_IPS=100000 src/fsx_struct.h:7.
+                                 No LRU eviction: a full table makes a batch fail
+                                 with -ENOSPC. */
+    uint64_t max_batch;       /* largest n per call (device scratch is sized for it) */
+    uint64_t tb_rate;         /* token bucket: refill in nano-tokens per ns (1000 = 1000 tok/s) */
+    uint64_t tb_burst;        /* token bucket: capacity in tokens */
+    uint64_t hash_seed;       /* salt of the table/IPv6 sort hashes */
+    int32_t limiter;          /* enum fsx_limiter */
+    int32_t device;           /* HIP device ordinal */
+    uint32_t flags;           /* FSX_FLAG_*; 0 in production */
+    uint32_t reserved[7];
+} fsx_config;
+
+/* Quantized scorer: QuantStub -> Linear(8,1) -> sigmoid -> DeQuantStub,
+ * model/model.py:124-137, eager-mode int8 after torch.ao convert(). */
+typedef struct fsx_q8_model {
+    int8_t weight[8];         /* linear._packed_params weight int_repr (per-tensor, zp 0) */
+    float weight_scale;       /* 0.002657087752595544 */
+    float bias;               /* 0.02776797 (fp32) */
+    float in_scale;           /* quant.scale       944881.875 */
+    int32_t in_zero_point;    /* quant.zero_point  0 */
+    float out_scale;          /* linear.scale      398330.96875 */
+    int32_t out_zero_point;   /* linear.zero_point 84 */
+} fsx_q8_model;
+
+typedef struct fsx_ctx fsx_ctx;
+
+/* Fill *cfg with the reference constants. */
+void fsx_config_default(fsx_config *cfg);
+int fsx_abi_version(void);
+
+int fsx_open(fsx_ctx **out, const fsx_config *cfg);
+void fsx_close(fsx_ctx *ctx);
+const char *fsx_last_error(const fsx_ctx *ctx);
+
+/* Attach a caller-owned hipStream_t (NULL restores the context's own stream). */
+int fsx_set_stream(fsx_ctx *ctx, void *hip_stream);
+/* Wait for enqueued device work and report deferred device-side errors. */
+int fsx_sync(fsx_ctx *ctx);
+
+/* Replaces fsx() (src/fsx_kern.c:96-347) over a batch of n packets in arrival
+ * order. Host pointers; hdr is n*64 bytes; verdict receives n bytes (1/2).
+ * Map state and stats carry over between calls exactly as the BPF maps do. */
+int fsx_verdict_batch(fsx_ctx *ctx, const uint8_t *hdr, const uint32_t *len,
+                      const uint64_t *ts_ns, size_t n, uint8_t *verdict);
+/* Same with device (HBM-resident) pointers, enqueued on the context stream.
+ * Returns after enqueue; errors detected on the device surface at fsx_sync. */
+int fsx_verdict_batch_device(fsx_ctx *ctx, const uint8_t *d_hdr, const uint32_t *d_len,
+                             const uint64_t *d_ts, size_t n, uint8_t *d_verdict);
+
+/* BPF map syscalls on the five reference maps (bpf_map_*_elem semantics). */
+int fsx_map_lookup(fsx_ctx *ctx, int map_id, const void *key, void *value);
+int fsx_map_update(fsx_ctx *ctx, int map_id, const void *key, const void *value,
+                   uint64_t flags);
+int fsx_map_delete(fsx_ctx *ctx, int map_id, const void *key);
+/* Copy up to cap entries (unordered) into keys/values; *n_out = entries present. */
+int fsx_map_dump(fsx_ctx *ctx, int map_id, void *keys, void *values, size_t cap,
+                 size_t *n_out);
+int fsx_get_stats(fsx_ctx *ctx, fsx_stats *out);
+/* Empty every map and zero the stats (a fresh program load). */
+int fsx_reset(fsx_ctx *ctx);
+
+/* Scoring (model/model.py:132-137, decision model/model.py:206). */
+int fsx_load_q8_model(fsx_ctx *ctx, const fsx_q8_model *model);
+int fsx_score(fsx_ctx *ctx, const float *features, size_t n, float *prob,
+              uint8_t *malicious);
+int fsx_score_device(fsx_ctx *ctx, const float *d_features, size_t n, float *d_prob,
+                     uint8_t *d_malicious);
+
+/* Per-source-IP flow features (build-defined) for the packets of
+ * one batch, n_flows_out = distinct source IPs; features are n_flows x 8 fp32 in
+ * model/model.py:117 order. Keys: 16 bytes per flow + family byte (4 or 6). */
+int fsx_flow_features(fsx_ctx *ctx, const uint8_t *hdr, const uint32_t *len,
+                      const uint64_t *ts_ns, size_t n, size_t cap, uint8_t *keys16,
+                      uint8_t *family, float *features, size_t *n_flows_out);
+
+/* Facts about the last batch (after fsx_sync): info[0] IP packets, [1] distinct
+ * source IPs, [2] sources new to the maps, [3] any IPv6, [4] non-monotone clock,
+ * [5] max frame length, [6] max timestamp, [7] allowed, [8] dropped, [9] IPv6
+ * hash-collision runs fixed. Returns the number of entries written. */
+int fsx_last_batch_info(fsx_ctx *ctx, uint64_t *info, int cap);
+
+/* Per-kernel device timing for the benchmark: while enabled, every batch records a
+ * HIP event after each kernel on the context stream. fsx_last_timings returns, per
+ * kernel name, the mean device time per batch and the launches per batch over all
+ * batches since the previous call (then resets). */
+int fsx_enable_timing(fsx_ctx *ctx, int on);
+int fsx_last_timings(fsx_ctx *ctx, float *ms_per_batch, float *launches_per_batch,
+                     char *names, int cap, int name_len, int *count);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FSX_HIP_H */

@@ -1,0 +1,239 @@
+"""ctypes binding of the CPU oracle (oracle/build/libfsx_oracle.so).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and the
+cpu_baseline leg of bench.py, as the checker. The product (flowsentryx_amd/) never
+imports this module.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import subprocess
+from pathlib import Path
+
+import numpy as np
+
+HERE = Path(__file__).resolve().parent
+LIB = HERE / "build" / "libfsx_oracle.so"
+REF_LIB = HERE / "_ref" / "libref_parse.so"
+
+
+class OConfig(C.Structure):
+    _fields_ = [
+        ("pps_threshold", C.c_uint64), ("bps_threshold", C.c_uint64),
+        ("window_ns", C.c_uint64), ("block_ns", C.c_uint64), ("max_entries", C.c_uint64),
+        ("tb_rate", C.c_uint64), ("tb_burst", C.c_uint64),
+        ("limiter", C.c_int32), ("pad", C.c_int32),
+    ]
+
+
+class OQ8Model(C.Structure):
+    _fields_ = [
+        ("weight", C.c_int8 * 8), ("weight_scale", C.c_float), ("bias", C.c_float),
+        ("in_scale", C.c_float), ("in_zero_point", C.c_int32), ("out_scale", C.c_float),
+        ("out_zero_point", C.c_int32),
+    ]
+
+
+_lib = None
+
+
+def build():
+    r = subprocess.run(["make", "-C", str(HERE), "build/libfsx_oracle.so"], capture_output=True,
+                       text=True)
+    if r.returncode != 0:
+        raise RuntimeError(r.stdout + r.stderr)
+
+
+def lib() -> C.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not LIB.exists():
+        build()
+    L = C.CDLL(str(LIB))
+    vp, sz = C.c_void_p, C.c_size_t
+    sig = {
+        "fsxo_config_default": (None, [C.POINTER(OConfig)]),
+        "fsxo_open": (vp, [C.POINTER(OConfig)]),
+        "fsxo_close": (None, [vp]),
+        "fsxo_reset": (None, [vp]),
+        "fsxo_error": (C.c_int, [vp]),
+        "fsxo_get_stats": (None, [vp, vp]),
+        "fsxo_batch": (C.c_int, [vp, vp, vp, vp, sz, vp]),
+        "fsxo_parse_batch": (None, [vp, vp, sz, vp, vp]),
+        "fsxo_map_lookup": (C.c_int, [vp, C.c_int, vp, vp]),
+        "fsxo_map_update": (C.c_int, [vp, C.c_int, vp, vp]),
+        "fsxo_map_delete": (C.c_int, [vp, C.c_int, vp]),
+        "fsxo_map_dump": (sz, [vp, C.c_int, vp, vp, sz]),
+        "fsxo_batch_sharded": (C.c_int, [C.POINTER(OConfig), vp, vp, vp, sz, vp, C.c_int, vp]),
+        "fsxo_sigmoid_lut": (None, [C.c_float, C.c_int32, vp]),
+        "fsxo_score": (None, [C.POINTER(OQ8Model), vp, sz, vp, vp, vp]),
+        "fsxo_flow_features": (sz, [vp, vp, vp, sz, sz, vp, vp, vp]),
+        "fsxo_synth": (C.c_int, [vp, C.c_double, C.c_uint64, sz, vp, vp, vp]),
+        "fsxo_zipf_alias": (C.c_int, [C.c_uint32, C.c_double, vp, vp]),
+        "fsxo_dst_port": (C.c_uint32, [vp, C.c_uint32]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = L
+    return L
+
+
+def _p(a: np.ndarray) -> int:
+    return a.ctypes.data
+
+
+def default_config(**kw) -> OConfig:
+    c = OConfig()
+    lib().fsxo_config_default(C.byref(c))
+    for k, v in kw.items():
+        setattr(c, k, v)
+    return c
+
+
+class Oracle:
+    """Sequential restatement of fsx() + its maps (src/fsx_kern.c:56-347)."""
+
+    def __init__(self, **kw):
+        self.cfg = default_config(**kw)
+        self._h = lib().fsxo_open(C.byref(self.cfg))
+        if not self._h:
+            raise MemoryError("fsxo_open")
+
+    def close(self):
+        if self._h:
+            lib().fsxo_close(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+    def batch(self, hdr, length, ts) -> np.ndarray:
+        hdr = np.ascontiguousarray(hdr, dtype=np.uint8).reshape(-1, 64)
+        length = np.ascontiguousarray(length, dtype=np.uint32)
+        ts = np.ascontiguousarray(ts, dtype=np.uint64)
+        out = np.empty(hdr.shape[0], dtype=np.uint8)
+        rc = lib().fsxo_batch(self._h, _p(hdr), _p(length), _p(ts), hdr.shape[0], _p(out))
+        if rc:
+            raise RuntimeError(f"oracle error {rc}")
+        return out
+
+    def stats(self) -> tuple[int, int]:
+        s = np.zeros(2, dtype=np.uint64)
+        lib().fsxo_get_stats(self._h, _p(s))
+        return int(s[0]), int(s[1])
+
+    def map_update(self, map_id: int, key: bytes, value):
+        if map_id in (1, 2):
+            v = np.array(value, dtype=np.uint64)
+        else:
+            v = np.array([value], dtype=np.uint64)
+        k = np.frombuffer(bytes(key), dtype=np.uint8).copy()
+        rc = lib().fsxo_map_update(self._h, map_id, _p(k), _p(v))
+        if rc:
+            raise RuntimeError(f"oracle map update {rc}")
+
+    def map_dump(self, map_id: int) -> dict:
+        klen = 16 if map_id in (2, 4) else 4
+        vw = 3 if map_id in (1, 2) else 1
+        n = lib().fsxo_map_dump(self._h, map_id, None, None, 0)
+        keys = np.zeros((max(n, 1), klen), dtype=np.uint8)
+        vals = np.zeros((max(n, 1), vw), dtype=np.uint64)
+        lib().fsxo_map_dump(self._h, map_id, _p(keys), _p(vals), n)
+        return {keys[i].tobytes(): (tuple(int(x) for x in vals[i]) if vw == 3 else int(vals[i, 0]))
+                for i in range(n)}
+
+
+def parse(hdr, length):
+    hdr = np.ascontiguousarray(hdr, dtype=np.uint8).reshape(-1, 64)
+    length = np.ascontiguousarray(length, dtype=np.uint32)
+    n = hdr.shape[0]
+    cls = np.zeros(n, dtype=np.uint8)
+    keys = np.zeros((n, 16), dtype=np.uint8)
+    lib().fsxo_parse_batch(_p(hdr), _p(length), n, _p(cls), _p(keys))
+    return cls, keys
+
+
+def ref_parse(hdr, length):
+    """The reference's own parsing_helper.h (oracle/_ref), when it was built here."""
+    if not REF_LIB.exists():
+        raise FileNotFoundError(REF_LIB)
+    L = C.CDLL(str(REF_LIB))
+    L.ref_parse_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p]
+    hdr = np.ascontiguousarray(hdr, dtype=np.uint8).reshape(-1, 64)
+    length = np.ascontiguousarray(length, dtype=np.uint32)
+    n = hdr.shape[0]
+    cls = np.zeros(n, dtype=np.uint8)
+    keys = np.zeros((n, 16), dtype=np.uint8)
+    L.ref_parse_batch(_p(hdr), _p(length), n, _p(cls), _p(keys))
+    return cls, keys
+
+
+def batch_sharded(hdr, length, ts, nthreads: int, **kw):
+    cfg = default_config(**kw)
+    hdr = np.ascontiguousarray(hdr, dtype=np.uint8).reshape(-1, 64)
+    length = np.ascontiguousarray(length, dtype=np.uint32)
+    ts = np.ascontiguousarray(ts, dtype=np.uint64)
+    out = np.empty(hdr.shape[0], dtype=np.uint8)
+    st = np.zeros(2, dtype=np.uint64)
+    rc = lib().fsxo_batch_sharded(C.byref(cfg), _p(hdr), _p(length), _p(ts), hdr.shape[0],
+                                  _p(out), nthreads, _p(st))
+    if rc:
+        raise RuntimeError(f"oracle error {rc}")
+    return out, (int(st[0]), int(st[1]))
+
+
+def q8_model(d: dict) -> OQ8Model:
+    m = OQ8Model()
+    for i, w in enumerate(d["weight"]):
+        m.weight[i] = int(w)
+    m.weight_scale = d["weight_scale"]
+    m.bias = d["bias"]
+    m.in_scale = d["in_scale"]
+    m.in_zero_point = d["in_zero_point"]
+    m.out_scale = d["out_scale"]
+    m.out_zero_point = d["out_zero_point"]
+    return m
+
+
+def score(model: dict, feat):
+    f = np.ascontiguousarray(feat, dtype=np.float32).reshape(-1, 8)
+    n = f.shape[0]
+    p = np.zeros(n, dtype=np.float32)
+    d = np.zeros(n, dtype=np.uint8)
+    lq = np.zeros(n, dtype=np.uint8)
+    m = q8_model(model)
+    lib().fsxo_score(C.byref(m), _p(f), n, _p(p), _p(d), _p(lq))
+    return p, d, lq
+
+
+def sigmoid_lut(out_scale: float, out_zp: int) -> np.ndarray:
+    lut = np.zeros(256, dtype=np.uint8)
+    lib().fsxo_sigmoid_lut(out_scale, out_zp, _p(lut))
+    return lut
+
+
+def flow_features(hdr, length, ts):
+    hdr = np.ascontiguousarray(hdr, dtype=np.uint8).reshape(-1, 64)
+    length = np.ascontiguousarray(length, dtype=np.uint32)
+    ts = np.ascontiguousarray(ts, dtype=np.uint64)
+    n = hdr.shape[0]
+    keys = np.zeros((max(n, 1), 16), dtype=np.uint8)
+    fam = np.zeros(max(n, 1), dtype=np.uint8)
+    feat = np.zeros((max(n, 1), 8), dtype=np.float32)
+    nf = lib().fsxo_flow_features(_p(hdr), _p(length), _p(ts), n, max(n, 1), _p(keys), _p(fam),
+                                  _p(feat))
+    return keys[:nf], fam[:nf], feat[:nf]
+
+
+def synth(params, zipf_s: float, j0: int, count: int):
+    """CPU twin of the device generator (flowsentryx_amd.synth.SynthParams)."""
+    hdr = np.zeros((count, 64), dtype=np.uint8)
+    length = np.zeros(count, dtype=np.uint32)
+    ts = np.zeros(count, dtype=np.uint64)
+    rc = lib().fsxo_synth(C.byref(params), zipf_s, j0, count, _p(hdr), _p(length), _p(ts))
+    if rc:
+        raise RuntimeError(f"fsxo_synth {rc}")
+    return hdr, length, ts

@@ -1,0 +1,295 @@
+"""GPU parity: libfsx_hip.so (through the C ABI) against the CPU oracle.
+
+Bit-exact: verdict arrays, stats_map, and every entry of the four per-IP maps.
+Inputs are seeded synthetic streams at sizes the oracle finishes in seconds, the
+golden known-answer tests, and edge cases (short frames, non-IP, IPv6 hash
+collisions, non-monotone clocks, block < window, byte-limit triggers, full maps).
+"""
+import errno
+import zlib
+import json
+
+import numpy as np
+import pytest
+
+from kat import GOLDEN, build_case, expected_maps, load_kats
+
+pytestmark = pytest.mark.gpu
+
+MAPS = (1, 2, 3, 4)
+
+
+def gpu_ctx(native, **kw):
+    kw.setdefault("max_batch", 1 << 20)
+    kw.setdefault("max_entries", 1 << 18)
+    return native.FsxContext(**kw)
+
+
+def assert_same_state(c, o):
+    assert c.stats() == o.stats()
+    for m in MAPS:
+        g, r = c.map_dump(m), o.map_dump(m)
+        assert len(g) == len(r), (m, len(g), len(r))
+        assert g == r, m
+
+
+def run_both(native, oracle, batches, cfg=None, oracle_cfg=None):
+    cfg = cfg or {}
+    okw = {k: v for k, v in cfg.items() if k in ("pps_threshold", "bps_threshold", "window_ns",
+                                                    "block_ns", "max_entries")}
+    okw.setdefault("max_entries", cfg.get("max_entries", 1 << 18))
+    o = oracle.Oracle(**okw)
+    with gpu_ctx(native, **cfg) as c:
+        for hdr, ln, ts in batches:
+            vg = c.verdict_batch(hdr, ln, ts)
+            vo = o.batch(hdr, ln, ts)
+            bad = np.nonzero(vg != vo)[0]
+            assert bad.size == 0, f"{bad.size} verdicts differ, first at {bad[:8]}"
+        assert_same_state(c, o)
+
+
+def rand_stream(rng, n, n_ips, dt_max=2000, v6_frac=0.0, nonip_frac=0.0, short_frac=0.0,
+                len_lo=60, len_hi=1514, t0=10**9):
+    from flowsentryx_amd import synth
+    ips4 = rng.integers(0, 2**32, n_ips, dtype=np.uint64).astype(np.uint32)
+    ips6 = rng.integers(0, 256, (n_ips, 16), dtype=np.uint8)
+    w = 1.0 / np.arange(1, n_ips + 1) ** 1.1
+    pick = rng.choice(n_ips, n, p=w / w.sum())
+    kind = rng.random(n)
+    frames = []
+    ln = rng.integers(len_lo, len_hi + 1, n).astype(np.uint32)
+    for i in range(n):
+        k = kind[i]
+        if k < nonip_frac:
+            frames.append(synth.frame_raw(0x0806, bytes(46), 60))
+        elif k < nonip_frac + v6_frac:
+            frames.append(synth.frame_ipv6_udp(ips6[pick[i]].tobytes(), int(ln[i])))
+        else:
+            frames.append(synth.frame_ipv4_udp(int(ips4[pick[i]]).to_bytes(4, "big"), int(ln[i])))
+        if rng.random() < short_frac:
+            ln[i] = rng.integers(0, 54)
+    ts = t0 + np.cumsum(rng.integers(0, dt_max + 1, n)).astype(np.uint64)
+    return synth.records(frames), ln, ts
+
+
+# ------------------------------------------------------------------ known answers
+@pytest.mark.parametrize("case", load_kats(), ids=lambda c: c["name"])
+def test_known_answers(native, case):
+    hdr, ln, ts, exp = build_case(case)
+    with gpu_ctx(native, max_entries=1000, max_batch=8192) as c:
+        v = c.verdict_batch(hdr, ln, ts)
+        assert np.array_equal(v, exp), np.nonzero(v != exp)[0][:10]
+        assert list(c.stats()) == case["stats"]
+        for mid, entries in expected_maps(case).items():
+            dump = c.map_dump(mid)
+            for k, val in entries.items():
+                assert dump.get(k) == val, (mid, k, dump.get(k), val)
+
+
+def test_known_answers_one_packet_per_batch(native):
+    """Cross-batch state carry: the KAT stream fed one packet per call."""
+    case = load_kats()[1]
+    hdr, ln, ts, exp = build_case(case)
+    with gpu_ctx(native, max_entries=1000, max_batch=16) as c:
+        out = [c.verdict_batch(hdr[i:i + 1], ln[i:i + 1], ts[i:i + 1])[0] for i in range(len(exp))]
+    assert np.array_equal(np.array(out, dtype=np.uint8), exp)
+
+
+# ------------------------------------------------------------------ random streams
+CFGS = {
+    "default": {},
+    "tight": {"pps_threshold": 7, "window_ns": 200_000, "block_ns": 1_000_000},
+    "block_lt_window": {"pps_threshold": 5, "window_ns": 1_000_000, "block_ns": 50_000},
+    "block_zero": {"pps_threshold": 3, "window_ns": 100_000, "block_ns": 0},
+    "bytes_limit": {"pps_threshold": 50, "bps_threshold": 9_000, "window_ns": 500_000,
+                    "block_ns": 2_000_000},
+    "pps_zero": {"pps_threshold": 0, "window_ns": 100_000, "block_ns": 300_000},
+}
+
+
+@pytest.mark.parametrize("name", list(CFGS))
+def test_random_ipv4(native, oracle, name):
+    rng = np.random.default_rng(zlib.crc32(name.encode()))
+    hdr, ln, ts = rand_stream(rng, 40000, 300, dt_max=400)
+    run_both(native, oracle, [(hdr, ln, ts)], CFGS[name])
+
+
+@pytest.mark.parametrize("name", ["default", "tight", "block_lt_window"])
+def test_random_mixed_families(native, oracle, name):
+    rng = np.random.default_rng(11 + len(name))
+    hdr, ln, ts = rand_stream(rng, 30000, 500, dt_max=300, v6_frac=0.4, nonip_frac=0.05,
+                              short_frac=0.03)
+    run_both(native, oracle, [(hdr, ln, ts)], CFGS[name])
+
+
+@pytest.mark.parametrize("name", ["tight", "block_lt_window", "bytes_limit"])
+def test_state_carry_across_batches(native, oracle, name):
+    rng = np.random.default_rng(5)
+    hdr, ln, ts = rand_stream(rng, 30000, 200, dt_max=300, v6_frac=0.2)
+    cuts = [0, 1, 2, 777, 5000, 5001, 17000, 29999, 30000]
+    batches = [(hdr[a:b], ln[a:b], ts[a:b]) for a, b in zip(cuts[:-1], cuts[1:])]
+    run_both(native, oracle, batches, CFGS[name])
+
+
+def test_non_monotone_clock(native, oracle):
+    rng = np.random.default_rng(8)
+    hdr, ln, ts = rand_stream(rng, 20000, 100, dt_max=200)
+    sw = rng.choice(len(ts), 3000, replace=False)
+    ts[sw] = ts[sw] - rng.integers(0, 50000, sw.size).astype(np.uint64)
+    ts[5] = np.uint64(2**64 - 5)   # u64 wraparound in now - track_time
+    run_both(native, oracle, [(hdr, ln, ts)], CFGS["tight"])
+
+
+def test_ipv6_forced_collisions(native, oracle):
+    """FSX_FLAG_TEST_V6_COLLIDE: every IPv6 key shares one sort key (and IPv4 10.0.0.1's),
+    so all IPv6 sources form one huge mixed run resolved by the exact fixup."""
+    rng = np.random.default_rng(21)
+    from flowsentryx_amd import synth
+    hdr, ln, ts = rand_stream(rng, 20000, 50, dt_max=300, v6_frac=0.5)
+    extra = synth.records([synth.frame_ipv4_udp(bytes([10, 0, 0, 1]), 100)] * 500)
+    hdr = np.concatenate([hdr, extra])
+    ln = np.concatenate([ln, np.full(500, 100, np.uint32)])
+    ts = np.concatenate([ts, ts[-1] + np.arange(1, 501, dtype=np.uint64)])
+    run_both(native, oracle, [(hdr, ln, ts)], dict(CFGS["tight"], flags=1))
+
+
+def test_many_ipv6_sources(native, oracle):
+    """2^17 distinct IPv6 + IPv4 sources: natural 32-bit sort-key collisions."""
+    rng = np.random.default_rng(3)
+    n = 1 << 17
+    from flowsentryx_amd import synth
+    hdr = np.zeros((2 * n, 64), np.uint8)
+    for i in range(n):
+        hdr[i] = np.frombuffer(synth.frame_ipv6_udp(rng.bytes(16), 100), np.uint8)
+    k4 = rng.integers(0, 2**32, n, dtype=np.uint64)
+    for i in range(n):
+        hdr[n + i] = np.frombuffer(synth.frame_ipv4_udp(int(k4[i]).to_bytes(4, "big"), 100), np.uint8)
+    perm = rng.permutation(2 * n)
+    hdr = hdr[perm]
+    ln = np.full(2 * n, 100, np.uint32)
+    ts = (10**9 + np.arange(2 * n) * 10).astype(np.uint64)
+    run_both(native, oracle, [(hdr, ln, ts)], {"max_entries": 1 << 19})
+
+
+def test_config1_stream(native, oracle):
+    """BASELINE config 1: 1M-packet IPv4/UDP flood, 1024 Zipf sources over 5 s."""
+    from flowsentryx_amd import synth
+    p, s = synth.config_params(1)
+    hdr, ln, ts = oracle.synth(p, s, 0, p.n)
+    run_both(native, oracle, [(hdr, ln, ts)], {"max_entries": 4096})
+
+
+def test_carpet_stream(native, oracle):
+    """BASELINE config 5 shape (scaled): unique spoofed v4/v6 sources + VLAN + rule table."""
+    from flowsentryx_amd import synth
+    p, s = synth.config_params(5, n=200_000)
+    hdr, ln, ts = oracle.synth(p, s, 0, p.n)
+    rng = np.random.default_rng(4)
+    o = oracle.Oracle(max_entries=1 << 19)
+    with gpu_ctx(native, max_entries=1 << 19) as c:
+        # user rule table: static blocks (till = UINT64_MAX) and ignored entries (till = 0)
+        ip_rows = np.nonzero(hdr[:, 12] == 0x08)[0][:2000]
+        for j, i in enumerate(ip_rows):
+            key = hdr[i, 26:30].tobytes()
+            till = (2**64 - 1) if j % 2 == 0 else 0
+            c.map_update(3, key, till)
+            o.map_update(3, key, till)
+        vg = c.verdict_batch(hdr, ln, ts)
+        vo = o.batch(hdr, ln, ts)
+        assert np.array_equal(vg, vo)
+        assert_same_state(c, o)
+
+
+def test_table_full_reports_enospc(native):
+    from flowsentryx_amd import lib, synth
+    hdr = synth.records([synth.frame_ipv4_udp(bytes([10, 9, i // 256, i % 256]), 80) for i in range(600)])
+    with gpu_ctx(native, max_entries=500, max_batch=1024) as c:
+        with pytest.raises(lib.FsxError) as e:
+            c.verdict_batch(hdr, np.full(600, 80, np.uint32), np.arange(600, dtype=np.uint64) + 5)
+        assert e.value.code == -errno.ENOSPC
+
+
+def test_map_syscalls(native):
+    from flowsentryx_amd import lib
+    with gpu_ctx(native, max_entries=64, max_batch=64) as c:
+        k4, k6 = bytes([1, 2, 3, 4]), bytes(range(16))
+        assert c.map_lookup(lib.MAP_IPV4_STATS, k4) is None
+        c.map_update(lib.MAP_IPV4_STATS, k4, (5, 6, 7))
+        assert c.map_lookup(lib.MAP_IPV4_STATS, k4) == (5, 6, 7)
+        with pytest.raises(lib.FsxError) as e:
+            c.map_update(lib.MAP_IPV4_STATS, k4, (1, 1, 1), lib.BPF_NOEXIST)
+        assert e.value.code == -errno.EEXIST
+        with pytest.raises(lib.FsxError) as e:
+            c.map_update(lib.MAP_IPV6_BLACKLIST, k6, 9, lib.BPF_EXIST)
+        assert e.value.code == -errno.ENOENT
+        c.map_update(lib.MAP_IPV6_BLACKLIST, k6, 9)
+        assert c.map_lookup(lib.MAP_IPV6_BLACKLIST, k6) == 9
+        assert c.map_lookup(lib.MAP_IPV4_BLACKLIST, k4) is None
+        assert c.map_delete(lib.MAP_IPV4_STATS, k4)
+        assert not c.map_delete(lib.MAP_IPV4_STATS, k4)
+        assert c.map_dump(lib.MAP_IPV6_BLACKLIST) == {k6: 9}
+        c.map_update(lib.MAP_STATS, 0, (3, 4))
+        assert c.stats() == (3, 4)
+        c.reset()
+        assert c.stats() == (0, 0) and c.map_dump(lib.MAP_IPV6_BLACKLIST) == {}
+
+
+def test_empty_batch(native):
+    with gpu_ctx(native) as c:
+        v = c.verdict_batch(np.zeros((0, 64), np.uint8), np.zeros(0, np.uint32), np.zeros(0, np.uint64))
+        assert v.size == 0 and c.stats() == (0, 0)
+
+
+# ------------------------------------------------------------------ device entry + synth
+def test_device_synth_and_device_batch(native, oracle):
+    import torch
+    from flowsentryx_amd import synth
+    p, s = synth.config_params(2, n=1 << 20)
+    n = int(p.n)
+    d_hdr = torch.empty(n * 64, dtype=torch.uint8, device="cuda")
+    d_len = torch.empty(n, dtype=torch.int32, device="cuda")
+    d_ts = torch.empty(n, dtype=torch.int64, device="cuda")
+    d_v = torch.empty(n, dtype=torch.uint8, device="cuda")
+    synth.generate_device(p, s, 0, n, d_hdr.data_ptr(), d_len.data_ptr(), d_ts.data_ptr())
+    torch.cuda.synchronize()
+    hdr, ln, ts = oracle.synth(p, s, 0, n)
+    assert np.array_equal(d_hdr.cpu().numpy().reshape(n, 64), hdr)
+    assert np.array_equal(d_len.cpu().numpy().view(np.uint32), ln)
+    assert np.array_equal(d_ts.cpu().numpy().view(np.uint64), ts)
+    with gpu_ctx(native, max_entries=1 << 20, max_batch=n) as c:
+        c.verdict_batch_device(d_hdr.data_ptr(), d_len.data_ptr(), d_ts.data_ptr(), n, d_v.data_ptr())
+        c.sync()
+        vo = oracle.Oracle(max_entries=1 << 20).batch(hdr, ln, ts)
+        assert np.array_equal(d_v.cpu().numpy(), vo)
+
+
+# ------------------------------------------------------------------ scoring
+def _model(native, d):
+    m = native.FsxQ8Model()
+    for i, w in enumerate(d["weight"]):
+        m.weight[i] = int(w)
+    for k in ("weight_scale", "bias", "in_scale", "out_scale"):
+        setattr(m, k, d[k])
+    m.in_zero_point = d["in_zero_point"]
+    m.out_zero_point = d["out_zero_point"]
+    return m
+
+
+def test_score_reference_model(native):
+    g = np.load(GOLDEN / "score_vectors.npz")
+    ref = json.loads((GOLDEN / "model_weights.json").read_text())
+    with gpu_ctx(native) as c:
+        c.load_q8_model(_model(native, ref))
+        p, d = c.score(g["x_ref"])
+    assert np.array_equal(p.view(np.uint32), g["p_ref"].view(np.uint32))
+    assert np.array_equal(d, (g["p_ref"] > 0.5).astype(np.uint8))
+
+
+def test_score_random_models(native):
+    g = np.load(GOLDEN / "score_vectors.npz")
+    models = json.loads((GOLDEN / "score_random_models.json").read_text())
+    with gpu_ctx(native) as c:
+        for i, m in enumerate(models):
+            c.load_q8_model(_model(native, m))
+            p, _ = c.score(g["rand_x"][i])
+            assert np.array_equal(p.view(np.uint32), g["rand_p"][i].view(np.uint32)), i
