@@ -183,7 +183,9 @@ __global__ __launch_bounds__(256) void k_parse(const uint8_t *__restrict__ hdr,
                 }
             }
             packed[i] = out;
-            if (out == kSentinel) verdict[i] = v;
+            // IP packets default to PASS here (coalesced); the fill pass writes only
+            // the DROP verdicts, which cluster in the heavy sources' segments
+            verdict[i] = out == kSentinel ? v : (uint8_t)XDP_PASS;
             nonmono |= T < prev ? 1u : 0u;
             maxlen = L > maxlen ? L : maxlen;
             maxts = T > maxts ? T : maxts;
@@ -235,10 +237,19 @@ __global__ __launch_bounds__(256) void k_sort_hist(const uint64_t *__restrict__ 
     const uint32_t L = L_dev ? *L_dev : L_host;
     uint32_t beg, end;
     block_range(L, G, blockIdx.x, beg, end);
-    for (uint32_t i = beg + tid; i < end; i += 256) {
-        const uint64_t v = in[i];
-        if (first && v == kSentinel) continue;
-        atomicAdd(&sh[w][(uint32_t)(v >> shift) & 255u], 1u);
+    for (uint32_t t0 = beg; t0 < end; t0 += kSortTile) {
+        uint64_t v[kSortItems];  // all loads of the tile in flight before counting
+#pragma unroll
+        for (int r = 0; r < kSortItems; ++r) {
+            const uint32_t i = t0 + (uint32_t)r * 256u + tid;
+            v[r] = i < end ? in[i] : kSentinel;
+        }
+#pragma unroll
+        for (int r = 0; r < kSortItems; ++r) {
+            const uint32_t i = t0 + (uint32_t)r * 256u + tid;
+            if (i < end && !(first && v[r] == kSentinel))
+                atomicAdd(&sh[w][(uint32_t)(v[r] >> shift) & 255u], 1u);
+        }
     }
     __syncthreads();
     const uint32_t c = sh[0][tid] + sh[1][tid] + sh[2][tid] + sh[3][tid];
@@ -506,22 +517,31 @@ __global__ __launch_bounds__(256) void k_heads_count(const uint64_t *__restrict_
     const uint32_t M = bs->n_valid;
     const bool any6 = bs->any_v6 != 0;
     const uint32_t ntiles = (M + kTile - 1) / kTile;
+    const uint32_t lane = lane_id();
     for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
-        const uint32_t p0 = t * kTile + threadIdx.x * 16u;
-        uint32_t cnt = 0;
-        uint32_t flags[4] = {0, 0, 0, 0};
+        // coalesced: round k covers positions [t*kTile + 256k, +256), one per thread
+        uint64_t cur[16];
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
-            const uint32_t p = p0 + k;
-            const bool h = p < M && is_head(S, p, hdr, any6);
-            cnt += h;
-            flags[k >> 2] |= (h ? 1u : 0u) << (8 * (k & 3));
+            const uint32_t p = t * kTile + (uint32_t)k * 256u + threadIdx.x;
+            cur[k] = p < M ? S[p] : kSentinel;
         }
-        if (p0 < M) {
-            if (p0 + 16 <= M) {
-                *reinterpret_cast<uint4 *>(headf + p0) = make_uint4(flags[0], flags[1], flags[2], flags[3]);
-            } else {
-                for (uint32_t k = 0; p0 + k < M; ++k) headf[p0 + k] = (flags[k >> 2] >> (8 * (k & 3))) & 1u;
+        uint32_t cnt = 0;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const uint32_t p = t * kTile + (uint32_t)k * 256u + threadIdx.x;
+            uint64_t prev = __shfl_up(cur[k], 1);
+            if (lane == 0 && p > 0 && p < M) prev = S[p - 1];
+            if (p < M) {
+                bool h = p == 0 || (prev >> 31) != (cur[k] >> 31);
+                if (!h && any6 && pk_fam(cur[k])) {
+                    uint32_t ka[4], kb[4];
+                    load_key6(hdr, pk_idx(prev), ka);
+                    load_key6(hdr, pk_idx(cur[k]), kb);
+                    h = key_cmp(2, ka, 2, kb) != 0;
+                }
+                headf[p] = h ? 1u : 0u;
+                cnt += h;
             }
         }
         uint32_t tot;
@@ -702,6 +722,24 @@ __device__ __forceinline__ uint32_t gallop_gt(const SegView &sv, uint32_t lo, ui
     return l;
 }
 
+// Sum of frame lengths over sorted positions [lo, hi): 16 independent gathers in
+// flight per step instead of one dependent chain per element.
+__device__ __forceinline__ uint64_t sum_len(const SegView &sv, uint32_t lo, uint32_t hi) {
+    uint64_t s = 0;
+    uint32_t q = lo;
+    for (; q + 16 <= hi; q += 16) {
+        uint32_t idx[16], l[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) idx[k] = pk_idx(sv.S[q + k]);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) l[k] = sv.len[idx[k]];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) s += l[k];
+    }
+    for (; q < hi; ++q) s += sv.l(q);
+    return s;
+}
+
 struct MarkWriter {
     uint8_t *marks;
     uint8_t last;
@@ -816,7 +854,7 @@ __device__ void walk_fixed_fast(const SegView &sv, uint32_t a, uint32_t b, const
     }
     if (touched) {
         uint64_t s = bps_base;
-        for (uint32_t q = ep_lo; q < ep_hi; ++q) s += sv.l(q);
+        s += sum_len(sv, ep_lo, ep_hi);
         bps = s;
     }
 }
@@ -964,7 +1002,7 @@ __global__ __launch_bounds__(256) void k_fill_scatter(const uint8_t *__restrict_
         const uint32_t tile0 = t * kTile;
         for (uint32_t j = threadIdx.x; j < kTile && tile0 + j < M; j += 256) {
             const uint8_t v = s_v[j];
-            verdict[pk_idx(S[tile0 + j])] = v;
+            if (v == XDP_DROP) verdict[pk_idx(S[tile0 + j])] = v;
             n_pass += v == XDP_PASS;
             n_drop += v == XDP_DROP;
         }

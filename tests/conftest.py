@@ -13,6 +13,18 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an AMD Instinct GPU (MI355X, gfx950)")
 
 
+def pytest_collection_modifyitems(session, config, items):
+    # torch's wheel bundles its own HIP runtime; when a process uses both torch and
+    # libfsx_hip.so (/opt/rocm runtime), torch must initialise the device first.
+    if any(it.get_closest_marker("gpu") for it in items):
+        try:
+            import torch
+            if torch.cuda.is_available():
+                torch.cuda.init()
+        except Exception:
+            pass
+
+
 @pytest.fixture(scope="session")
 def oracle():
     from oracle import pyoracle
