@@ -1,11 +1,12 @@
 #!/usr/bin/env python3
 """Benchmark: Mpps of FlowSentryX verdicts on MI355X (BASELINE.json metric).
 
-One "step" = one pass of the hot path (parse -> per-source fixed-window rate limit +
-blacklist -> verdicts + map state, src/fsx_kern.c:96-347 semantics) over one batch of
-synthetic packets resident in HBM, starting from empty maps (fsx_reset is inside the
-timed step). N=1 workload: BASELINE config 2 — 64M IPv4/UDP packets from 1M
-Zipf(1.1) sources over 30 s.
+One "step" = one pass of the hot path over one batch of synthetic packets resident
+in HBM, starting from empty maps (fsx_reset is inside the timed step): parse ->
+per-source fixed-window rate limit + blacklist -> verdicts + map state
+(src/fsx_kern.c:96-347 semantics) -> per-source flow features -> q8 MLP score of
+every source with the reference weights (model/model.py:132-137). N=1 workload:
+BASELINE config 2 — 64M IPv4/UDP packets from 1M Zipf(1.1) sources over 30 s.
 
 Multi-GPU (torch.distributed.run, one rank per GPU): weak scaling — every rank
 generates and processes its own contiguous 64M-packet slice of one stream with
@@ -54,6 +55,7 @@ def parse_args():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--check", action="store_true", help="verify a prefix against the oracle")
+    ap.add_argument("--no-mlp", action="store_true", help="verdicts only (no features/scores)")
     return ap.parse_args()
 
 
@@ -86,11 +88,23 @@ def main():
 
     max_entries = max(1024, int(p.n_ips) if p.n_ips else n)
     ctx = lib.FsxContext(max_batch=n, max_entries=max_entries, device=local)
+    from flowsentryx_amd import fsx_load
+    ctx.load_q8_model(fsx_load.load_weights(ROOT / "tests" / "golden" / "model_weights.json"))
+    fcap = max_entries
+    d_keys = torch.empty(fcap * 16, dtype=torch.uint8, device="cuda")
+    d_fam = torch.empty(fcap, dtype=torch.uint8, device="cuda")
+    d_prob = torch.empty(fcap, dtype=torch.float32, device="cuda")
+    d_dec = torch.empty(fcap, dtype=torch.uint8, device="cuda")
 
     def step():
         ctx.reset()
-        ctx.verdict_batch_device(d_hdr.data_ptr(), d_len.data_ptr(), d_ts.data_ptr(), n,
-                                 d_v.data_ptr())
+        if args.no_mlp:
+            ctx.verdict_batch_device(d_hdr.data_ptr(), d_len.data_ptr(), d_ts.data_ptr(), n,
+                                     d_v.data_ptr())
+        else:
+            ctx.process_batch_device(d_hdr.data_ptr(), d_len.data_ptr(), d_ts.data_ptr(), n,
+                                     d_v.data_ptr(), d_keys.data_ptr(), d_fam.data_ptr(), None,
+                                     d_prob.data_ptr(), d_dec.data_ptr(), fcap)
 
     for _ in range(args.warmup):
         step()
@@ -116,6 +130,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     stats = ctx.stats()
+    malicious = None if args.no_mlp else int(d_dec[:info["sources"]].sum().item())
 
     check = None
     if args.check and rank == 0:
@@ -188,11 +203,14 @@ def main():
         "data": "synthetic (counter-based generator, fsx_synth_common.h)",
         "config": {"workload": f"BASELINE config {args.config}: {n} IPv4/UDP packets per GPU, "
                                f"{p.n_ips} Zipf(1.1) sources, {p.duration_ns / 1e9:g} s; "
-                               "fixed-window limiter (src/fsx_kern.c), maps reset each step",
+                               "fixed-window limiter (src/fsx_kern.c), maps reset each step"
+                               + ("" if args.no_mlp else "; per-source features + q8 MLP score "
+                                  "(model_weights.pth)"),
                    "packets_per_gpu": n, "sources": sources, "parallelism": f"dp{world}"},
         "roofline": roofline, "pipeline": pipeline, "cpu_baseline": cpu,
         "kernels": [{"name": a, "ms_per_step": round(b, 4), "launches": c} for a, b, c in timings],
-        "stats": {"allowed": stats[0], "dropped": stats[1]}, "check": check,
+        "stats": {"allowed": stats[0], "dropped": stats[1], "sources": info["sources"],
+                  "malicious_sources": malicious}, "check": check,
     }
     print(json.dumps(out), flush=True)
     if dist:

@@ -102,6 +102,8 @@ static void free_scratch(fsx_ctx *c) {
     hipFree(s.packed[0]); hipFree(s.packed[1]); hipFree(s.marks); hipFree(s.headf);
     hipFree(s.seg_start); hipFree(s.seg_slot); hipFree(s.hist); hipFree(s.row_total);
     hipFree(s.tile_aux); hipFree(s.tile_last); hipFree(s.fix_list); hipFree(s.fix_bitmap);
+    hipFree(s.long_list); hipFree(s.sub_cnt); hipFree(s.flow_first); hipFree(s.flow_last);
+    hipFree(s.span_list);
     s = Scratch{};
 }
 
@@ -122,6 +124,11 @@ static int alloc_scratch(fsx_ctx *c, uint64_t cap) {
     HIPCHK(c, hipMalloc(&s.tile_last, ntiles));
     HIPCHK(c, hipMalloc(&s.fix_list, cap * 4));
     HIPCHK(c, hipMalloc(&s.fix_bitmap, (cap / 64 + 1) * 8));
+    HIPCHK(c, hipMalloc(&s.long_list, (cap / 64 + 1) * 4));
+    HIPCHK(c, hipMalloc(&s.sub_cnt, (cap / 1024 + 8) * 4));
+    HIPCHK(c, hipMalloc(&s.flow_first, (cap / 1024 + 8) * flow_acc_bytes()));
+    HIPCHK(c, hipMalloc(&s.flow_last, (cap / 1024 + 8) * flow_acc_bytes()));
+    HIPCHK(c, hipMalloc(&s.span_list, (cap / 1024 + 8) * 4));
     s.cap = cap;
     return 0;
 }
@@ -264,15 +271,14 @@ static int drain_timings(fsx_ctx *c) {
     return 0;
 }
 
-int fsx_verdict_batch_device(fsx_ctx *c, const uint8_t *d_hdr, const uint32_t *d_len,
-                             const uint64_t *d_ts, size_t n, uint8_t *d_verdict) {
-    if (!c) return -EINVAL;
-    if (n && (!d_hdr || !d_len || !d_ts || !d_verdict)) return set_err(c, -EINVAL, "null buffer");
+// Enqueue one batch: verdicts + maps when d_verdict is set, per-source flows when fr is.
+static int run_batch(fsx_ctx *c, const uint8_t *d_hdr, const uint32_t *d_len, const uint64_t *d_ts,
+                     size_t n, uint8_t *d_verdict, const FlowRequest *fr) {
     if (n > c->cfg.max_batch) return set_err(c, -E2BIG, "n=%zu exceeds max_batch", n);
     int rc = sel(c);
     if (rc) return rc;
     if (c->pending) { rc = fsx_sync(c); if (rc) return rc; }
-    if (c->cfg.limiter != FSX_LIMIT_FIXED_WINDOW)
+    if (d_verdict && c->cfg.limiter != FSX_LIMIT_FIXED_WINDOW)
         return set_err(c, -EOPNOTSUPP, "limiter %d not built into this pipeline yet", c->cfg.limiter);
     hipEvent_t *ev = nullptr;
     const char **names = nullptr;
@@ -285,11 +291,42 @@ int fsx_verdict_batch_device(fsx_ctx *c, const uint8_t *d_hdr, const uint32_t *d
         c->ring_n++;
     }
     hipError_t e = launch_verdict_pipeline(d_hdr, d_len, d_ts, (uint32_t)n, d_verdict, c->table,
-                                           c->tstate, c->bs, c->sc, c->lim, c->stream, ev, kMaxEv,
-                                           used, names);
+                                           c->tstate, c->bs, c->sc, c->lim, d_verdict != nullptr,
+                                           fr, c->stream, ev, kMaxEv, used, names);
     if (e != hipSuccess) return set_err(c, -EIO, "pipeline launch: %s", hipGetErrorString(e));
     c->pending = true;
     return 0;
+}
+
+static FlowRequest flow_request(fsx_ctx *c, uint8_t *keys16, uint8_t *fam, float *feat, float *prob,
+                                uint8_t *dec, size_t cap) {
+    FlowRequest fr{};
+    fr.keys16 = keys16; fr.fam = fam; fr.feat = feat; fr.cap = (uint32_t)std::min<size_t>(cap, 0xFFFFFFFFu);
+    if (c->model_loaded && prob && dec) {
+        fr.prob = prob; fr.dec = dec;
+        fr.score = make_score_params(c->w, c->inv_in, c->zp_in, c->bias_over_ats, c->mult, c->zp_out, c->lut);
+    } else {
+        fr.score.enabled = 0;
+    }
+    return fr;
+}
+
+int fsx_verdict_batch_device(fsx_ctx *c, const uint8_t *d_hdr, const uint32_t *d_len,
+                             const uint64_t *d_ts, size_t n, uint8_t *d_verdict) {
+    if (!c) return -EINVAL;
+    if (n && (!d_hdr || !d_len || !d_ts || !d_verdict)) return set_err(c, -EINVAL, "null buffer");
+    return run_batch(c, d_hdr, d_len, d_ts, n, d_verdict, nullptr);
+}
+
+int fsx_process_batch_device(fsx_ctx *c, const uint8_t *d_hdr, const uint32_t *d_len,
+                             const uint64_t *d_ts, size_t n, uint8_t *d_verdict, uint8_t *d_keys16,
+                             uint8_t *d_family, float *d_features, float *d_prob,
+                             uint8_t *d_malicious, size_t flow_cap) {
+    if (!c) return -EINVAL;
+    if (n && (!d_hdr || !d_len || !d_ts || !d_verdict || !d_keys16 || !d_family))
+        return set_err(c, -EINVAL, "null buffer");
+    const FlowRequest fr = flow_request(c, d_keys16, d_family, d_features, d_prob, d_malicious, flow_cap);
+    return run_batch(c, d_hdr, d_len, d_ts, n, d_verdict, &fr);
 }
 
 static int ensure_stage(fsx_ctx *c, uint64_t n) {
@@ -494,9 +531,37 @@ int fsx_score(fsx_ctx *c, const float *feat, size_t n, float *prob, uint8_t *mal
     return 0;
 }
 
-int fsx_flow_features(fsx_ctx *c, const uint8_t *, const uint32_t *, const uint64_t *, size_t,
-                      size_t, uint8_t *, uint8_t *, float *, size_t *) {
-    return c ? set_err(c, -EOPNOTSUPP, "flow features not built yet") : -EINVAL;
+int fsx_flow_features(fsx_ctx *c, const uint8_t *hdr, const uint32_t *len, const uint64_t *ts,
+                      size_t n, size_t cap, uint8_t *keys16, uint8_t *family, float *features,
+                      size_t *n_flows_out) {
+    if (!c || !n_flows_out) return -EINVAL;
+    if (n && (!hdr || !len || !ts)) return set_err(c, -EINVAL, "null buffer");
+    int rc = sel(c);
+    if (rc) return rc;
+    *n_flows_out = 0;
+    if (n == 0) return 0;
+    if ((rc = ensure_stage(c, n))) return rc;
+    uint8_t *dk = nullptr, *df = nullptr;
+    float *dfeat = nullptr;
+    HIPCHK(c, hipMalloc(&dk, n * 16));
+    HIPCHK(c, hipMalloc(&df, n));
+    HIPCHK(c, hipMalloc(&dfeat, n * 32));
+    HIPCHK(c, hipMemcpyAsync(c->d_hdr, hdr, n * 64, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->d_len, len, n * 4, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->d_ts, ts, n * 8, hipMemcpyHostToDevice, c->stream));
+    FlowRequest fr = flow_request(c, dk, df, dfeat, nullptr, nullptr, n);
+    rc = run_batch(c, c->d_hdr, c->d_len, c->d_ts, n, nullptr, &fr);
+    if (!rc) rc = fsx_sync(c);
+    BatchState h{};
+    if (!rc && hipMemcpy(&h, c->bs, sizeof(h), hipMemcpyDeviceToHost) != hipSuccess) rc = -EIO;
+    const size_t m = std::min<size_t>(h.nseg, cap);
+    if (!rc && m && keys16 && hipMemcpy(keys16, dk, m * 16, hipMemcpyDeviceToHost) != hipSuccess) rc = -EIO;
+    if (!rc && m && family && hipMemcpy(family, df, m, hipMemcpyDeviceToHost) != hipSuccess) rc = -EIO;
+    if (!rc && m && features && hipMemcpy(features, dfeat, m * 32, hipMemcpyDeviceToHost) != hipSuccess) rc = -EIO;
+    hipFree(dk); hipFree(df); hipFree(dfeat);
+    if (rc) return rc == -EIO ? set_err(c, -EIO, "flow features copy failed") : rc;
+    *n_flows_out = h.nseg;
+    return 0;
 }
 
 int fsx_last_batch_info(fsx_ctx *c, uint64_t *info, int cap) {

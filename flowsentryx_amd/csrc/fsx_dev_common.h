@@ -1,0 +1,115 @@
+// fsx_dev_common.h — device helpers shared by the hot-path kernels (wave scans,
+// digit matching, key access on the packed sort words).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "fsx_internal.h"
+
+namespace fsx {
+
+// ------------------------------------------------------------------ helpers
+__device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
+
+template <typename T>
+__device__ __forceinline__ T wave_incl_sum(T x) {
+    const uint32_t lane = lane_id();
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        T y = __shfl_up(x, o);
+        if (lane >= (uint32_t)o) x += y;
+    }
+    return x;
+}
+
+template <typename T>
+__device__ __forceinline__ T wave_max(T x) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        T y = __shfl_xor(x, o);
+        x = y > x ? y : x;
+    }
+    return x;
+}
+
+// Sum over the 64 lanes, result in every lane.
+template <typename T>
+__device__ __forceinline__ T wave_sum(T x) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
+    return x;
+}
+
+// Exclusive prefix sum over the 256 threads of a block. s_tmp: >= 4 entries.
+// Every thread of the block must call it. *total receives the block sum.
+__device__ __forceinline__ uint32_t block256_excl(uint32_t x, uint32_t *s_tmp, uint32_t *total) {
+    const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
+    uint32_t incl = wave_incl_sum(x);
+    if (lane == 63) s_tmp[w] = incl;
+    __syncthreads();
+    uint32_t off = 0, tot = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < 4; ++i) {
+        uint32_t v = s_tmp[i];
+        off += i < w ? v : 0u;
+        tot += v;
+    }
+    __syncthreads();
+    if (total) *total = tot;
+    return off + incl - x;
+}
+
+// "Last non-zero" scan operator over encoded (position << 8 | mark) words: max.
+__device__ __forceinline__ uint32_t wave_incl_max(uint32_t x) {
+    const uint32_t lane = lane_id();
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        uint32_t y = __shfl_up(x, o);
+        if (lane >= (uint32_t)o) x = y > x ? y : x;
+    }
+    return x;
+}
+
+__device__ __forceinline__ uint64_t match_digit(uint32_t d, uint64_t active) {
+    uint64_t peers = active;
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+        const bool bit = (d >> b) & 1u;
+        const uint64_t bal = __ballot(bit);
+        peers &= bit ? bal : ~bal;
+    }
+    return peers;
+}
+
+// IPv6 source address of arrival index i (bytes 22..37 of the record).
+__device__ __forceinline__ void load_key6(const uint8_t *hdr, uint32_t i, uint32_t k[4]) {
+    const uint32_t *d = reinterpret_cast<const uint32_t *>(hdr + (size_t)i * 64);
+    const uint32_t d5 = d[5], d6 = d[6], d7 = d[7], d8 = d[8], d9 = d[9];
+    k[0] = (d5 >> 16) | (d6 << 16);
+    k[1] = (d6 >> 16) | (d7 << 16);
+    k[2] = (d7 >> 16) | (d8 << 16);
+    k[3] = (d8 >> 16) | (d9 << 16);
+}
+
+// Full key (family tag 1/2 + address words) of a packed sort word.
+__device__ __forceinline__ uint32_t key_of(uint64_t v, const uint8_t *hdr, uint32_t salt,
+                                           uint32_t k[4]) {
+    if (pk_fam(v)) {
+        load_key6(hdr, pk_idx(v), k);
+        return 2u;
+    }
+    k[0] = ip_of_skey(pk_skey(v), salt);
+    k[1] = k[2] = k[3] = 0;
+    return 1u;
+}
+
+// Total order on (family, address) used to group colliding IPv6 hash runs.
+__device__ __forceinline__ int key_cmp(uint32_t ta, const uint32_t *a, uint32_t tb,
+                                       const uint32_t *b) {
+    if (ta != tb) return ta < tb ? -1 : 1;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+        if (a[i] != b[i]) return a[i] < b[i] ? -1 : 1;
+    return 0;
+}
+
+}  // namespace fsx

@@ -16,109 +16,13 @@
 //                    order, stats_map counters (src/fsx_kern.c:210,332,342)
 #include <hip/hip_runtime.h>
 
+#include "fsx_dev_common.h"
 #include "fsx_internal.h"
 
 #define XDP_DROP 1
 #define XDP_PASS 2
 
 namespace fsx {
-
-// ------------------------------------------------------------------ helpers
-__device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
-
-template <typename T>
-__device__ __forceinline__ T wave_incl_sum(T x) {
-    const uint32_t lane = lane_id();
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        T y = __shfl_up(x, o);
-        if (lane >= (uint32_t)o) x += y;
-    }
-    return x;
-}
-
-template <typename T>
-__device__ __forceinline__ T wave_max(T x) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        T y = __shfl_xor(x, o);
-        x = y > x ? y : x;
-    }
-    return x;
-}
-
-// Exclusive prefix sum over the 256 threads of a block. s_tmp: >= 4 entries.
-// Every thread of the block must call it. *total receives the block sum.
-__device__ __forceinline__ uint32_t block256_excl(uint32_t x, uint32_t *s_tmp, uint32_t *total) {
-    const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
-    uint32_t incl = wave_incl_sum(x);
-    if (lane == 63) s_tmp[w] = incl;
-    __syncthreads();
-    uint32_t off = 0, tot = 0;
-#pragma unroll
-    for (uint32_t i = 0; i < 4; ++i) {
-        uint32_t v = s_tmp[i];
-        off += i < w ? v : 0u;
-        tot += v;
-    }
-    __syncthreads();
-    if (total) *total = tot;
-    return off + incl - x;
-}
-
-// "Last non-zero" scan operator over encoded (position << 8 | mark) words: max.
-__device__ __forceinline__ uint32_t wave_incl_max(uint32_t x) {
-    const uint32_t lane = lane_id();
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        uint32_t y = __shfl_up(x, o);
-        if (lane >= (uint32_t)o) x = y > x ? y : x;
-    }
-    return x;
-}
-
-__device__ __forceinline__ uint64_t match_digit(uint32_t d, uint64_t active) {
-    uint64_t peers = active;
-#pragma unroll
-    for (int b = 0; b < 8; ++b) {
-        const bool bit = (d >> b) & 1u;
-        const uint64_t bal = __ballot(bit);
-        peers &= bit ? bal : ~bal;
-    }
-    return peers;
-}
-
-// IPv6 source address of arrival index i (bytes 22..37 of the record).
-__device__ __forceinline__ void load_key6(const uint8_t *hdr, uint32_t i, uint32_t k[4]) {
-    const uint32_t *d = reinterpret_cast<const uint32_t *>(hdr + (size_t)i * 64);
-    const uint32_t d5 = d[5], d6 = d[6], d7 = d[7], d8 = d[8], d9 = d[9];
-    k[0] = (d5 >> 16) | (d6 << 16);
-    k[1] = (d6 >> 16) | (d7 << 16);
-    k[2] = (d7 >> 16) | (d8 << 16);
-    k[3] = (d8 >> 16) | (d9 << 16);
-}
-
-// Full key (family tag 1/2 + address words) of a packed sort word.
-__device__ __forceinline__ uint32_t key_of(uint64_t v, const uint8_t *hdr, uint32_t salt,
-                                           uint32_t k[4]) {
-    if (pk_fam(v)) {
-        load_key6(hdr, pk_idx(v), k);
-        return 2u;
-    }
-    k[0] = ip_of_skey(pk_skey(v), salt);
-    k[1] = k[2] = k[3] = 0;
-    return 1u;
-}
-
-// Total order on (family, address) used to group colliding IPv6 hash runs.
-__device__ __forceinline__ int key_cmp(uint32_t ta, const uint32_t *a, uint32_t tb,
-                                       const uint32_t *b) {
-    if (ta != tb) return ta < tb ? -1 : 1;
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-        if (a[i] != b[i]) return a[i] < b[i] ? -1 : 1;
-    return 0;
-}
 
 // ------------------------------------------------------------------ parse
 // One wave handles 64 consecutive records per step: the 4 KiB tile is loaded with
@@ -512,7 +416,8 @@ __global__ __launch_bounds__(256) void k_heads_count(const uint64_t *__restrict_
                                                      BatchState *bs,
                                                      const uint8_t *__restrict__ hdr,
                                                      uint8_t *__restrict__ headf,
-                                                     uint32_t *__restrict__ tile_cnt) {
+                                                     uint32_t *__restrict__ tile_cnt,
+                                                     uint32_t *__restrict__ sub_cnt) {
     __shared__ uint32_t s_tmp[4];
     const uint32_t M = bs->n_valid;
     const bool any6 = bs->any_v6 != 0;
@@ -527,6 +432,7 @@ __global__ __launch_bounds__(256) void k_heads_count(const uint64_t *__restrict_
             cur[k] = p < M ? S[p] : kSentinel;
         }
         uint32_t cnt = 0;
+        uint32_t sub[4] = {0, 0, 0, 0};
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
             const uint32_t p = t * kTile + (uint32_t)k * 256u + threadIdx.x;
@@ -542,7 +448,16 @@ __global__ __launch_bounds__(256) void k_heads_count(const uint64_t *__restrict_
                 }
                 headf[p] = h ? 1u : 0u;
                 cnt += h;
+                sub[k >> 2] += h;
             }
+        }
+        // per-1024-position sub-tile head counts (flow tiles, fsx_flows.hip)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            uint32_t st;
+            block256_excl(sub[j], s_tmp, &st);
+            if (threadIdx.x == 0 && sub_cnt) sub_cnt[t * 4 + j] = st;
+            sub[j] = 0;
         }
         uint32_t tot;
         block256_excl(cnt, s_tmp, &tot);
@@ -671,26 +586,37 @@ __global__ __launch_bounds__(256) void k_insert(const uint64_t *__restrict__ S, 
                                                 uint32_t *__restrict__ seg_slot,
                                                 const uint8_t *__restrict__ hdr, Slot *table,
                                                 TableState *tstate, Limits lim) {
-    if (bs->n_new == 0) return;
+    const uint32_t nnew = bs->n_new;
+    if (nnew == 0) return;
+    // capacity for the whole batch is checked once: a batch that would overflow the
+    // maps is rejected before any state changes (-ENOSPC at the boundary)
+    if (tstate->count + nnew > lim.max_entries) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(&bs->err, ERR_TABLE_FULL);
+        return;
+    }
     const uint32_t nseg = bs->nseg;
     for (uint32_t g = blockIdx.x * 256u + threadIdx.x; g < nseg; g += gridDim.x * 256u) {
         if (seg_slot[g] != kNoSlot) continue;
         uint32_t k[4];
         const uint32_t tag = seg_key(S, seg_start, g, hdr, lim.salt32, k);
-        const unsigned long long ticket =
-            atomicAdd(reinterpret_cast<unsigned long long *>(&tstate->count), 1ull);
-        if (ticket >= lim.max_entries) {
-            atomicOr(&bs->err, ERR_TABLE_FULL);
-            atomicAdd(reinterpret_cast<unsigned long long *>(&tstate->count), ~0ull);  // undo
-            continue;
-        }
         const uint32_t s = table_claim(table, lim.table_mask, tag, k, lim.seed);
         if (s == kNoSlot) atomicOr(&bs->err, ERR_PROBE);
         seg_slot[g] = s;
     }
 }
 
+// Runs after k_insert: account the inserted entries (one thread).
+__global__ void k_count_inserted(BatchState *bs, TableState *tstate) {
+    if (bs->err == 0) tstate->count += bs->n_new;
+}
+
 // ------------------------------------------------------------------ fixed-window walker
+// Segments of at most kShortSeg packets: one thread, exact per-packet replay with 16
+// packets' loads in flight. Longer segments (the heavy sources): one wave each,
+// epoch jumps with 64-wide cooperative searches (few dependent round trips per
+// search instead of one per binary-search step).
+constexpr uint32_t kShortSeg = 512;
+
 struct SegView {
     const uint64_t *S;
     const uint64_t *ts;
@@ -699,8 +625,59 @@ struct SegView {
     __device__ __forceinline__ uint32_t l(uint32_t q) const { return len[pk_idx(S[q])]; }
 };
 
-// First q in [lo, hi) with t(q) > X, for t non-decreasing on [lo, hi). Galloping
-// from lo: O(log distance), so short epochs of light sources cost O(1).
+// First q in [lo, hi) with t(q) > X (t non-decreasing on [lo, hi)); wave-uniform
+// arguments, every lane calls. Round 0 probes 64 consecutive packets, round 1 64
+// exponentially spaced ones, then 64-ary narrowing.
+__device__ uint32_t wave_gallop_gt(const SegView &sv, uint32_t lo, uint32_t hi, uint64_t X) {
+    const uint32_t lane = lane_id();
+    if (lo >= hi) return hi;
+    {
+        const uint32_t q = lo + lane;
+        const bool pr = q < hi && sv.t(q) > X;
+        const uint64_t m = __ballot(pr);
+        if (m) return lo + (uint32_t)__ffsll((unsigned long long)m) - 1u;
+        if (hi - lo <= 64) return hi;
+    }
+    uint32_t good = lo + 63, bad = hi;  // t(good) <= X; answer in (good, bad]
+    {
+        const uint64_t q64 = (uint64_t)lo + (lane < 32 ? (64ull << lane) : (1ull << 40));
+        const bool valid = q64 < hi;
+        const bool pr = valid && sv.t((uint32_t)q64) > X;
+        const uint64_t m = __ballot(pr);
+        const uint64_t vm = __ballot(valid);
+        if (m) {
+            const uint32_t f = (uint32_t)__ffsll((unsigned long long)m) - 1u;
+            bad = lo + (64u << f);
+            if (f) good = lo + (64u << (f - 1));
+        } else if (vm) {
+            const uint32_t lv = 63u - (uint32_t)__clzll((long long)vm);
+            good = lo + (64u << lv);
+        }
+    }
+    while (bad - good > 64) {
+        const uint32_t cnt = bad - good - 1;
+        const uint32_t step = (cnt + 63) / 64;
+        const uint32_t q = good + 1 + lane * step;
+        const bool valid = q < bad;
+        const bool pr = valid && sv.t(q) > X;
+        const uint64_t m = __ballot(pr);
+        if (m) {
+            const uint32_t f = (uint32_t)__ffsll((unsigned long long)m) - 1u;
+            const uint32_t nb = good + 1 + f * step;
+            if (f) good = good + 1 + (f - 1) * step;
+            bad = nb;
+        } else {
+            const uint64_t vm = __ballot(valid);
+            good = good + 1 + (63u - (uint32_t)__clzll((long long)vm)) * step;
+        }
+    }
+    const uint32_t q = good + 1 + lane;
+    const bool pr = q < bad && sv.t(q) > X;
+    const uint64_t m = __ballot(pr);
+    return m ? good + (uint32_t)__ffsll((unsigned long long)m) : bad;
+}
+
+// Thread version: galloping from lo, O(log distance).
 __device__ __forceinline__ uint32_t gallop_gt(const SegView &sv, uint32_t lo, uint32_t hi,
                                               uint64_t X) {
     if (lo >= hi) return hi;
@@ -722,57 +699,142 @@ __device__ __forceinline__ uint32_t gallop_gt(const SegView &sv, uint32_t lo, ui
     return l;
 }
 
-// Sum of frame lengths over sorted positions [lo, hi): 16 independent gathers in
-// flight per step instead of one dependent chain per element.
+// Sum of frame lengths over [lo, hi): wave-strided (4 loads in flight per lane) or,
+// for a thread, 16 independent gathers per step.
+template <bool kWave>
 __device__ __forceinline__ uint64_t sum_len(const SegView &sv, uint32_t lo, uint32_t hi) {
     uint64_t s = 0;
-    uint32_t q = lo;
-    for (; q + 16 <= hi; q += 16) {
-        uint32_t idx[16], l[16];
+    if constexpr (kWave) {
+        const uint32_t lane = lane_id();
+        uint32_t q = lo + lane;
+        for (; q + 192 < hi; q += 256) {
+            const uint32_t i0 = pk_idx(sv.S[q]), i1 = pk_idx(sv.S[q + 64]);
+            const uint32_t i2 = pk_idx(sv.S[q + 128]), i3 = pk_idx(sv.S[q + 192]);
+            s += (uint64_t)sv.len[i0] + sv.len[i1] + sv.len[i2] + sv.len[i3];
+        }
+        for (; q < hi; q += 64) s += sv.l(q);
+        return wave_sum(s);
+    } else {
+        uint32_t q = lo;
+        for (; q + 16 <= hi; q += 16) {
+            uint32_t idx[16], l[16];
 #pragma unroll
-        for (int k = 0; k < 16; ++k) idx[k] = pk_idx(sv.S[q + k]);
+            for (int k = 0; k < 16; ++k) idx[k] = pk_idx(sv.S[q + k]);
 #pragma unroll
-        for (int k = 0; k < 16; ++k) l[k] = sv.len[idx[k]];
+            for (int k = 0; k < 16; ++k) l[k] = sv.len[idx[k]];
 #pragma unroll
-        for (int k = 0; k < 16; ++k) s += l[k];
+            for (int k = 0; k < 16; ++k) s += l[k];
+        }
+        for (; q < hi; ++q) s += sv.l(q);
+        return s;
     }
-    for (; q < hi; ++q) s += sv.l(q);
-    return s;
 }
 
+// First q in [from, lim) with acc0 + sum(L[from..q]) > B, else lim.
+template <bool kWave>
+__device__ uint32_t bytes_trigger(const SegView &sv, uint32_t from, uint32_t lim, uint64_t acc0,
+                                  uint64_t B) {
+    uint64_t acc = acc0;
+    if constexpr (kWave) {
+        const uint32_t lane = lane_id();
+        for (uint32_t q0 = from; q0 < lim; q0 += 64) {
+            const uint32_t q = q0 + lane;
+            const uint64_t L = q < lim ? sv.l(q) : 0;
+            const uint64_t incl = wave_incl_sum(L);
+            const uint64_t m = __ballot(q < lim && acc + incl > B);
+            if (m) return q0 + (uint32_t)__ffsll((unsigned long long)m) - 1u;
+            acc += __shfl(incl, 63);
+        }
+        return lim;
+    } else {
+        for (uint32_t q = from; q < lim; ++q) {
+            acc += sv.l(q);
+            if (acc > B) return q;
+        }
+        return lim;
+    }
+}
+
+template <bool kWave>
+__device__ __forceinline__ uint32_t search_gt(const SegView &sv, uint32_t lo, uint32_t hi, uint64_t X) {
+    if constexpr (kWave) return wave_gallop_gt(sv, lo, hi, X);
+    else return gallop_gt(sv, lo, hi, X);
+}
+
+template <bool kWave>
 struct MarkWriter {
     uint8_t *marks;
     uint8_t last;
     __device__ __forceinline__ void emit(uint32_t pos, uint8_t v) {
-        if (v != last) { marks[pos] = v; last = v; }
+        if (v != last) {
+            if (!kWave || lane_id() == 0) marks[pos] = v;
+            last = v;
+        }
     }
 };
 
 constexpr uint64_t kBig = 1ull << 62;
 
-// Exact per-packet replay of src/fsx_kern.c:150-346 for one source (any timestamps).
-__device__ void walk_fixed_exact(const SegView &sv, uint32_t a, uint32_t b, const Limits &lim,
-                                 MarkWriter &mw, bool &has_st, bool &has_bl, uint64_t &pps,
-                                 uint64_t &bps, uint64_t &tt, uint64_t &till) {
-    for (uint32_t q = a; q < b; ++q) {
-        const uint64_t now = sv.t(q);
-        if (has_bl && till > 0) {
-            if (now > till) has_bl = false;                 // :193-204 delete
-            else { mw.emit(q, XDP_DROP); continue; }        // :205-215
+struct FwState {
+    bool has_st, has_bl;
+    uint64_t pps, bps, tt, till;
+};
+
+// One packet of src/fsx_kern.c:150-346 (exact, any timestamps, u64 wraparound).
+template <bool kWave>
+__device__ __forceinline__ void fw_step(FwState &s, uint64_t now, uint32_t L, uint32_t q,
+                                        const Limits &lim, MarkWriter<kWave> &mw) {
+    if (s.has_bl && s.till > 0) {
+        if (now > s.till) s.has_bl = false;                 // :193-204 delete
+        else { mw.emit(q, XDP_DROP); return; }              // :205-215
+    }
+    uint64_t cp, cb;
+    if (s.has_st) {
+        if (now - s.tt > lim.window) { s.pps = 0; s.bps = 0; s.tt = now; cp = 0; cb = 0; }  // :245-250
+        else { s.pps += 1; s.bps += L; cp = s.pps; cb = s.bps; }                            // :258-262
+    } else {
+        s.has_st = true; s.pps = 1; s.bps = L; s.tt = now; cp = 1; cb = L;                  // :265-284
+    }
+    if (cp > lim.pps || cb > lim.bps) {                     // :312
+        s.till = now + lim.block; s.has_bl = true;          // :317-326
+        mw.emit(q, XDP_DROP);
+    } else {
+        mw.emit(q, XDP_PASS);
+    }
+}
+
+// Exact replay for one thread, 16 packets' loads in flight per step.
+__device__ void walk_fixed_exact_thread(const SegView &sv, uint32_t a, uint32_t b,
+                                        const Limits &lim, MarkWriter<false> &mw, FwState &s) {
+    for (uint32_t q0 = a; q0 < b; q0 += 16) {
+        uint32_t idx[16];
+        uint64_t t[16];
+        uint32_t L[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) idx[k] = q0 + k < b ? pk_idx(sv.S[q0 + k]) : 0u;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            t[k] = q0 + k < b ? sv.ts[idx[k]] : 0ull;
+            L[k] = q0 + k < b ? sv.len[idx[k]] : 0u;
         }
-        uint64_t cp, cb;
-        if (has_st) {
-            if (now - tt > lim.window) { pps = 0; bps = 0; tt = now; cp = 0; cb = 0; }  // :245-250
-            else { pps += 1; bps += sv.l(q); cp = pps; cb = bps; }                        // :258-262
-        } else {
-            has_st = true; pps = 1; bps = sv.l(q); tt = now; cp = pps; cb = bps;          // :265-284
-        }
-        if (cp > lim.pps || cb > lim.bps) {                 // :312
-            till = now + lim.block; has_bl = true;          // :317-326
-            mw.emit(q, XDP_DROP);
-        } else {
-            mw.emit(q, XDP_PASS);
-        }
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+            if (q0 + k < b) fw_step<false>(s, t[k], L[k], q0 + k, lim, mw);
+    }
+}
+
+// Exact replay for one wave: 64 packets loaded in parallel, then stepped uniformly
+// (every lane keeps the same state; values broadcast by shuffles).
+__device__ void walk_fixed_exact_wave(const SegView &sv, uint32_t a, uint32_t b, const Limits &lim,
+                                      MarkWriter<true> &mw, FwState &s) {
+    const uint32_t lane = lane_id();
+    for (uint32_t q0 = a; q0 < b; q0 += 64) {
+        const uint32_t q = q0 + lane;
+        const uint64_t tq = q < b ? sv.t(q) : 0ull;
+        const uint32_t lq = q < b ? sv.l(q) : 0u;
+        const uint32_t cnt = min(64u, b - q0);
+        for (uint32_t k = 0; k < cnt; ++k)
+            fw_step<true>(s, __shfl(tq, (int)k), __shfl(lq, (int)k), q0 + k, lim, mw);
     }
 }
 
@@ -780,16 +842,16 @@ __device__ void walk_fixed_exact(const SegView &sv, uint32_t a, uint32_t b, cons
 // starts where ip_stats (re)starts a window: the first-ever packet (count 1), a
 // reset packet (count 0, not counted) or the carried window (continuation). With
 // counts consecutive inside an epoch, the count trigger is at a closed-form
-// position; the window end and the blacklist end are binary searches.
+// position; the window end and the blacklist end are searches.
+template <bool kWave>
 __device__ void walk_fixed_fast(const SegView &sv, uint32_t a, uint32_t b, const Limits &lim,
-                                uint32_t maxL, MarkWriter &mw, bool &has_st, bool &has_bl,
-                                uint64_t &pps, uint64_t &bps, uint64_t &tt, uint64_t &till) {
+                                uint32_t maxL, MarkWriter<kWave> &mw, FwState &s) {
     const uint64_t P = lim.pps, B = lim.bps, W = lim.window, BLK = lim.block;
     uint32_t p = a;
-    if (has_bl && till > 0) {
-        const uint32_t j = gallop_gt(sv, a, b, till);
+    if (s.has_bl && s.till > 0) {
+        const uint32_t j = search_gt<kWave>(sv, a, b, s.till);
         if (j > a) mw.emit(a, XDP_DROP);
-        if (j < b) has_bl = false;
+        if (j < b) s.has_bl = false;
         p = j;
     }
     bool touched = false;
@@ -799,93 +861,121 @@ __device__ void walk_fixed_fast(const SegView &sv, uint32_t a, uint32_t b, const
         const uint64_t t = sv.t(p);
         uint64_t T0, pc, pb;
         uint32_t cs;
-        if (has_st && !(t - tt > W)) { T0 = tt; pc = pps; pb = bps; cs = 1; }
-        else if (has_st) { T0 = t; pc = 0; pb = 0; cs = 0; }
+        if (s.has_st && !(t - s.tt > W)) { T0 = s.tt; pc = s.pps; pb = s.bps; cs = 1; }
+        else if (s.has_st) { T0 = t; pc = 0; pb = 0; cs = 0; }
         else { T0 = t; pc = 0; pb = 0; cs = 1; }
-        has_st = true;
+        s.has_st = true;
         touched = true;
-        const uint32_t e = gallop_gt(sv, p + 1, b, T0 + W);
+        const uint32_t e = search_gt<kWave>(sv, p + 1, b, T0 + W);
         const uint64_t c0 = pc + cs;
         uint64_t k64 = c0 > P ? (uint64_t)p : (uint64_t)p + (P + 1 - c0);
         if (k64 > e) k64 = e;
         // bytes: only scanned when bps could exceed B before the count does
-        bool bytes_possible;
-        {
-            const uint64_t room = P + 1;
-            bytes_possible = pb > B || (maxL && room > (B - pb) / maxL);
-        }
-        if (bytes_possible) {
-            uint64_t acc = pb;
-            for (uint32_t q = cs ? p : p + 1; q < k64; ++q) {
-                acc += sv.l(q);
-                if (acc > B) { k64 = q; break; }
-            }
-        }
+        const bool bytes_possible = pb > B || (maxL && P + 1 > (B - pb) / maxL);
+        if (bytes_possible) k64 = bytes_trigger<kWave>(sv, cs ? p : p + 1, (uint32_t)k64, pb, B);
         const uint32_t k = (uint32_t)k64;
-        tt = T0;
+        s.tt = T0;
         bps_base = pb;
         ep_lo = p + 1 - cs;
         if (k >= e) {   // window closes without a trigger
             mw.emit(p, XDP_PASS);
-            pps = c0 + (uint64_t)(e - 1 - p);
+            s.pps = c0 + (uint64_t)(e - 1 - p);
             ep_hi = e;
             p = e;
             continue;
         }
         if (k > p) mw.emit(p, XDP_PASS);
         mw.emit(k, XDP_DROP);
-        pps = c0 + (uint64_t)(k - p);
+        s.pps = c0 + (uint64_t)(k - p);
         ep_hi = k + 1;
-        till = sv.t(k) + BLK;
-        has_bl = true;
+        s.till = sv.t(k) + BLK;
+        s.has_bl = true;
         uint32_t q = k + 1;
         for (;;) {
-            const uint32_t j = gallop_gt(sv, q, b, till);
+            const uint32_t j = search_gt<kWave>(sv, q, b, s.till);
             if (j >= b) { p = b; break; }
-            has_bl = false;                     // expired: deleted at packet j
+            s.has_bl = false;                    // expired: deleted at packet j
             const uint64_t tj = sv.t(j);
-            if (tj - tt > W) { p = j; break; }  // j resets the window: next epoch
-            pps += 1;                           // re-trigger inside the window (block < window)
+            if (tj - s.tt > W) { p = j; break; } // j resets the window: next epoch
+            s.pps += 1;                          // re-trigger inside the window (block < window)
             bps_base += sv.l(j);
-            till = tj + BLK;
-            has_bl = true;
+            s.till = tj + BLK;
+            s.has_bl = true;
             q = j + 1;
         }
     }
-    if (touched) {
-        uint64_t s = bps_base;
-        s += sum_len(sv, ep_lo, ep_hi);
-        bps = s;
-    }
+    if (touched) s.bps = bps_base + sum_len<kWave>(sv, ep_lo, ep_hi);
 }
 
+__device__ __forceinline__ FwState load_state(const Slot &sl) {
+    return FwState{(sl.flags & SLOT_HAS_ST) != 0, (sl.flags & SLOT_HAS_BL) != 0, sl.pps, sl.bps,
+                   sl.tt, sl.till};
+}
+__device__ __forceinline__ void store_state(Slot &sl, const FwState &s) {
+    sl.flags = (sl.flags & ~(SLOT_HAS_ST | SLOT_HAS_BL)) | (s.has_st ? SLOT_HAS_ST : 0u) |
+               (s.has_bl ? SLOT_HAS_BL : 0u);
+    sl.pps = s.pps; sl.bps = s.bps; sl.tt = s.tt; sl.till = s.till;
+}
+
+__device__ __forceinline__ bool fast_ok(const BatchState *bs, const Limits &lim) {
+    return !bs->nonmono && lim.block >= 1 && lim.pps < kBig && lim.bps < kBig && lim.window < kBig &&
+           lim.block < kBig && bs->max_ts <= ~0ull - (lim.window > lim.block ? lim.window : lim.block);
+}
+
+// Short segments; long ones are queued for k_walk_fixed_long.
 __global__ __launch_bounds__(256) void k_walk_fixed(const uint64_t *__restrict__ S, BatchState *bs,
                                                     const uint32_t *__restrict__ seg_start,
                                                     const uint32_t *__restrict__ seg_slot,
                                                     const uint64_t *__restrict__ ts,
                                                     const uint32_t *__restrict__ len,
                                                     uint8_t *__restrict__ marks, Slot *table,
-                                                    Limits lim) {
+                                                    uint32_t *__restrict__ long_list, Limits lim) {
+    if (bs->err) return;
     const uint32_t nseg = bs->nseg;
-    const bool glob_fast = !bs->nonmono && lim.block >= 1 && lim.pps < kBig && lim.bps < kBig &&
-                           lim.window < kBig && lim.block < kBig &&
-                           bs->max_ts <= ~0ull - (lim.window > lim.block ? lim.window : lim.block);
+    const SegView sv{S, ts, len};
+    uint32_t nlong = 0;
+    for (uint32_t g = blockIdx.x * 256u + threadIdx.x; g < nseg; g += gridDim.x * 256u) {
+        const uint32_t a = seg_start[g], b = seg_start[g + 1];
+        if (b - a > kShortSeg) {
+            long_list[atomicAdd(&bs->n_long, 1u)] = g;
+            continue;
+        }
+        const uint32_t s = seg_slot[g];
+        Slot &sl = table[s];
+        FwState st = load_state(sl);
+        MarkWriter<false> mw{marks, 0};
+        walk_fixed_exact_thread(sv, a, b, lim, mw, st);
+        store_state(sl, st);
+    }
+    (void)nlong;
+}
+
+__global__ __launch_bounds__(256) void k_walk_fixed_long(const uint64_t *__restrict__ S,
+                                                         BatchState *bs,
+                                                         const uint32_t *__restrict__ seg_start,
+                                                         const uint32_t *__restrict__ seg_slot,
+                                                         const uint64_t *__restrict__ ts,
+                                                         const uint32_t *__restrict__ len,
+                                                         uint8_t *__restrict__ marks, Slot *table,
+                                                         const uint32_t *__restrict__ long_list,
+                                                         Limits lim) {
+    if (bs->err) return;
+    const uint32_t nl = bs->n_long;
+    const bool glob_fast = fast_ok(bs, lim);
     const uint32_t maxL = bs->max_len;
     const SegView sv{S, ts, len};
-    for (uint32_t g = blockIdx.x * 256u + threadIdx.x; g < nseg; g += gridDim.x * 256u) {
-        const uint32_t s = seg_slot[g];
-        if (s == kNoSlot) continue;
+    const uint32_t wave = blockIdx.x * 4u + (threadIdx.x >> 6);
+    for (uint32_t i = wave; i < nl; i += gridDim.x * 4u) {
+        const uint32_t g = long_list[i];
         const uint32_t a = seg_start[g], b = seg_start[g + 1];
-        Slot &sl = table[s];
-        bool has_st = sl.flags & SLOT_HAS_ST, has_bl = sl.flags & SLOT_HAS_BL;
-        uint64_t pps = sl.pps, bps = sl.bps, tt = sl.tt, till = sl.till;
-        MarkWriter mw{marks, 0};
-        const bool fast = glob_fast && (!has_st || (tt <= ~0ull - lim.window && pps < kBig && bps < kBig));
-        if (fast) walk_fixed_fast(sv, a, b, lim, maxL, mw, has_st, has_bl, pps, bps, tt, till);
-        else walk_fixed_exact(sv, a, b, lim, mw, has_st, has_bl, pps, bps, tt, till);
-        sl.flags = (sl.flags & ~(SLOT_HAS_ST | SLOT_HAS_BL)) | (has_st ? SLOT_HAS_ST : 0u) |
-                   (has_bl ? SLOT_HAS_BL : 0u);
-        sl.pps = pps; sl.bps = bps; sl.tt = tt; sl.till = till;
+        Slot &sl = table[seg_slot[g]];
+        FwState st = load_state(sl);
+        MarkWriter<true> mw{marks, 0};
+        const bool fast = glob_fast && (!st.has_st || (st.tt <= ~0ull - lim.window &&
+                                                       st.pps < kBig && st.bps < kBig));
+        if (fast) walk_fixed_fast<true>(sv, a, b, lim, maxL, mw, st);
+        else walk_fixed_exact_wave(sv, a, b, lim, mw, st);
+        if (lane_id() == 0) store_state(sl, st);
     }
 }
 
@@ -968,6 +1058,7 @@ __global__ __launch_bounds__(256) void k_fill_scatter(const uint8_t *__restrict_
     __shared__ uint8_t s_v[kTile];
     __shared__ uint32_t s_w[4];
     __shared__ unsigned long long s_cnt[4][2];
+    if (bs->err) return;
     const uint32_t M = bs->n_valid;
     const uint32_t ntiles = (M + kTile - 1) / kTile;
     const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
@@ -1032,8 +1123,8 @@ static inline uint32_t cdiv(uint64_t a, uint64_t b) { return (uint32_t)((a + b -
 hipError_t launch_verdict_pipeline(const uint8_t *hdr, const uint32_t *len, const uint64_t *ts,
                                    uint32_t n, uint8_t *verdict, Slot *table, TableState *tstate,
                                    BatchState *bs, const Scratch &sc, const Limits &lim,
-                                   hipStream_t st, hipEvent_t *ev, int nev, int *nev_used,
-                                   const char **names) {
+                                   bool do_limit, const FlowRequest *flows, hipStream_t st,
+                                   hipEvent_t *ev, int nev, int *nev_used, const char **names) {
     int ei = 0;
     auto mark = [&](const char *name) {
         if (ev && ei < nev) {
@@ -1075,18 +1166,32 @@ hipError_t launch_verdict_pipeline(const uint8_t *hdr, const uint32_t *len, cons
     k_fixup_short<<<256, 256, 0, st>>>(S, bs, hdr, sc.fix_list, lim.salt32);
     k_fixup_long<<<64, 256, 0, st>>>(S, sc.packed[1], bs, hdr, sc.fix_list, lim.salt32);
     mark("v6_fixup");
-    k_heads_count<<<gridTiles, 256, 0, st>>>(S, bs, hdr, sc.headf, sc.tile_aux);
+    k_heads_count<<<gridTiles, 256, 0, st>>>(S, bs, hdr, sc.headf, sc.tile_aux, sc.sub_cnt);
     mark("k_heads_count");
     k_scan_tiles_u32<<<1, 1024, 0, st>>>(sc.tile_aux, bs, sc.seg_start);
     k_heads_write<<<gridTiles, 256, 0, st>>>(bs, sc.headf, sc.tile_aux, sc.seg_start);
     mark("k_heads_write");
+    if (flows) {
+        launch_flows(S, bs, sc.headf, len, ts, hdr, sc.tile_aux, sc.sub_cnt, sc.seg_start,
+                     sc.flow_first, sc.flow_last, sc.span_list, flows->keys16, flows->fam,
+                     flows->feat, flows->prob, flows->dec, flows->cap, flows->score, lim.salt32, n, st);
+        mark("k_flow_features");
+    }
+    if (!do_limit) {
+        if (nev_used) *nev_used = ei;
+        return hipGetLastError();
+    }
     k_lookup<<<gridStream, 256, 0, st>>>(S, bs, sc.seg_start, sc.seg_slot, hdr, table, lim);
     mark("k_lookup");
     k_insert<<<gridStream, 256, 0, st>>>(S, bs, sc.seg_start, sc.seg_slot, hdr, table, tstate, lim);
+    k_count_inserted<<<1, 1, 0, st>>>(bs, tstate);
     mark("k_insert");
     k_walk_fixed<<<gridStream, 256, 0, st>>>(S, bs, sc.seg_start, sc.seg_slot, ts, len, sc.marks,
-                                             table, lim);
+                                             table, sc.long_list, lim);
     mark("k_walk_fixed");
+    k_walk_fixed_long<<<1024, 256, 0, st>>>(S, bs, sc.seg_start, sc.seg_slot, ts, len, sc.marks,
+                                            table, sc.long_list, lim);
+    mark("k_walk_fixed_long");
     k_fill_last<<<gridTiles, 256, 0, st>>>(sc.marks, bs, sc.tile_last);
     k_fill_carry<<<1, 1024, 0, st>>>(sc.tile_last, bs);
     mark("k_fill_last");

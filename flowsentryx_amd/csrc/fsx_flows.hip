@@ -1,0 +1,320 @@
+// fsx_flows.hip — per-source flow features fused with the quantized scorer.
+//
+// The reference has no feature code (src/fsx_kern_ml.c:1-16 is a comment); the
+// eight model inputs are the CICFlowMeter columns of model/model.py:117. Their
+// build-defined semantics (restated in oracle/fsx_oracle.c
+// fsxo_flow_features) are computed here per source IP over one batch:
+//   n, S1 = sum L, S2 = sum L^2, D1 = sum d, D2 = sum d^2, Dmax = max d
+// (L frame length, d inter-arrival time of consecutive packets of the source) as
+// exact integers (u64 / u128), then the features in fp64, rounded to fp32, then the
+// q8 scorer of model/model.py:132-137 -> probability and decision per source.
+//
+// Work layout: the sources are the segments of the sorted packet array. One wave
+// owns a 1024-position tile (16 consecutive positions per lane): lane-level
+// accumulation, a segmented wave scan to join lanes, and every source that starts
+// and ends inside the tile is finished by the lane holding its last packet. A source
+// crossing tile boundaries leaves one partial per tile (first/last piece) and is
+// finished by k_flow_combine (one wave per such source, lanes striding its tiles).
+// Per packet: 8 B sort word + 12 B gathered (len, ts) in; per source: 8 x fp32
+// features + prob + decision out.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+
+#include "fsx_dev_common.h"
+#include "fsx_internal.h"
+#include "fsx_q8.h"
+
+namespace fsx {
+
+typedef unsigned __int128 u128;
+constexpr uint32_t kFT = 1024;  // flow tile: one wave, 16 positions per lane
+
+struct FlowAcc {
+    uint64_t n, s1, dmax, pad;
+    u128 s2, d1, d2;
+};
+
+__device__ __forceinline__ FlowAcc acc_zero() {
+    FlowAcc a;
+    a.n = a.s1 = a.dmax = a.pad = 0;
+    a.s2 = a.d1 = a.d2 = 0;
+    return a;
+}
+__device__ __forceinline__ void acc_add(FlowAcc &a, const FlowAcc &b) {
+    a.n += b.n; a.s1 += b.s1; a.s2 += b.s2; a.d1 += b.d1; a.d2 += b.d2;
+    a.dmax = b.dmax > a.dmax ? b.dmax : a.dmax;
+}
+__device__ __forceinline__ u128 shfl_up128(u128 v, int d) {
+    const uint64_t lo = __shfl_up((uint64_t)v, d), hi = __shfl_up((uint64_t)(v >> 64), d);
+    return ((u128)hi << 64) | lo;
+}
+__device__ __forceinline__ u128 shfl_xor128(u128 v, int d) {
+    const uint64_t lo = __shfl_xor((uint64_t)v, d), hi = __shfl_xor((uint64_t)(v >> 64), d);
+    return ((u128)hi << 64) | lo;
+}
+__device__ __forceinline__ FlowAcc shfl_up_acc(const FlowAcc &a, int d) {
+    FlowAcc r;
+    r.n = __shfl_up(a.n, d); r.s1 = __shfl_up(a.s1, d); r.dmax = __shfl_up(a.dmax, d); r.pad = 0;
+    r.s2 = shfl_up128(a.s2, d); r.d1 = shfl_up128(a.d1, d); r.d2 = shfl_up128(a.d2, d);
+    return r;
+}
+__device__ __forceinline__ FlowAcc wave_sum_acc(FlowAcc a) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        FlowAcc b;
+        b.n = __shfl_xor(a.n, o); b.s1 = __shfl_xor(a.s1, o); b.dmax = __shfl_xor(a.dmax, o);
+        b.s2 = shfl_xor128(a.s2, o); b.d1 = shfl_xor128(a.d1, o); b.d2 = shfl_xor128(a.d2, o);
+        acc_add(a, b);
+    }
+    return a;
+}
+
+struct FlowOut {
+    uint8_t *keys16;
+    uint8_t *fam;
+    float *feat;   // may be null
+    float *prob;   // may be null
+    uint8_t *dec;  // may be null
+    uint32_t cap;
+};
+
+// L4 destination port of the source's first packet (oracle fsxo_dst_port).
+__device__ __forceinline__ uint32_t dst_port(const uint8_t *f, uint32_t len) {
+    const uint32_t proto = ((uint32_t)f[12] << 8) | f[13];
+    uint32_t off, l4;
+    if (proto == 0x0800u) {
+        if (len < 34) return 0;
+        off = 14u + 4u * (f[14] & 0x0Fu);
+        l4 = f[23];
+    } else if (proto == 0x86DDu) {
+        if (len < 54) return 0;
+        off = 54;
+        l4 = f[20];
+    } else {
+        return 0;
+    }
+    if (l4 != 6 && l4 != 17) return 0;
+    if (off + 4 > len || off + 4 > 64) return 0;
+    return ((uint32_t)f[off + 2] << 8) | f[off + 3];
+}
+
+// Features of source g from its exact sums, then the q8 score.
+__device__ void flow_finish(uint32_t g, const FlowAcc &a, const uint64_t *S,
+                            const uint32_t *seg_start, const uint8_t *hdr, const uint32_t *len,
+                            uint32_t salt, const FlowOut &out, const ScoreParams &P) {
+    if (g >= out.cap) return;
+    const uint64_t v = S[seg_start[g]];
+    uint32_t k[4];
+    const uint32_t tag = key_of(v, hdr, salt, k);
+    const uint32_t idx = pk_idx(v);
+    uint32_t *kw = reinterpret_cast<uint32_t *>(out.keys16 + (size_t)g * 16);
+    kw[0] = k[0]; kw[1] = k[1]; kw[2] = k[2]; kw[3] = k[3];
+    out.fam[g] = tag == 1 ? 4 : 6;
+    const uint64_t n = a.n;
+    const double dn = (double)n;
+    const double mean = (double)a.s1 / dn;
+    double var = 0.0;
+    if (n >= 2) {
+        const u128 num = (u128)n * a.s2 - (u128)a.s1 * (u128)a.s1;
+        var = (double)num / (dn * (dn - 1.0));
+    }
+    double iat_mean = 0.0, iat_var = 0.0;
+    if (n >= 2) iat_mean = (double)a.d1 / (double)(n - 1) / 1000.0;
+    if (n >= 3) {
+        const uint64_t m = n - 1;
+        const u128 num = (u128)m * a.d2 - a.d1 * a.d1;
+        iat_var = (double)num / ((double)m * ((double)m - 1.0)) / 1000000.0;
+    }
+    float x[8];
+    x[0] = (float)dst_port(hdr + (size_t)idx * 64, len[idx]);
+    x[1] = (float)mean;
+    x[2] = (float)sqrt(var);
+    x[3] = (float)var;
+    x[4] = (float)mean;
+    x[5] = (float)iat_mean;
+    x[6] = (float)sqrt(iat_var);
+    x[7] = (float)((double)a.dmax / 1000.0);
+    if (out.feat) {
+        float4 *f4 = reinterpret_cast<float4 *>(out.feat + (size_t)g * 8);
+        f4[0] = make_float4(x[0], x[1], x[2], x[3]);
+        f4[1] = make_float4(x[4], x[5], x[6], x[7]);
+    }
+    if (P.enabled && out.prob) {
+        const float p = (float)lut_get(P, q8_linear(x, P)) * 0.00390625f;
+        out.prob[g] = p;
+        out.dec[g] = p > 0.5f ? 1 : 0;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_flow_tile(const uint64_t *__restrict__ S, BatchState *bs,
+                                                   const uint8_t *__restrict__ headf,
+                                                   const uint32_t *__restrict__ len,
+                                                   const uint64_t *__restrict__ ts,
+                                                   const uint8_t *__restrict__ hdr,
+                                                   const uint32_t *__restrict__ tile_off,
+                                                   const uint32_t *__restrict__ sub_cnt,
+                                                   const uint32_t *__restrict__ seg_start,
+                                                   FlowAcc *__restrict__ firstp,
+                                                   FlowAcc *__restrict__ lastp,
+                                                   uint32_t *__restrict__ span_list, FlowOut out,
+                                                   ScoreParams P, uint32_t salt) {
+    __shared__ unsigned long long s_S[4][64 * 17];
+    const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
+    const uint32_t M = bs->n_valid;
+    const uint32_t nsub = (M + kFT - 1) / kFT;
+    unsigned long long *sS = s_S[w];
+    for (uint32_t sub = blockIdx.x * 4u + w; sub < nsub; sub += gridDim.x * 4u) {
+        const uint32_t base = sub * kFT;
+        const uint32_t p0 = base + lane * 16u;
+        // heads before this tile
+        const uint32_t t4 = sub >> 2, j4 = sub & 3u;
+        uint32_t hb = tile_off[t4];
+        for (uint32_t j = 0; j < j4; ++j) hb += sub_cnt[t4 * 4 + j];
+        // stage the tile's sort words through LDS (coalesced load, 17-word row pitch)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const uint32_t e = (uint32_t)r * 64u + lane;
+            const uint32_t p = base + e;
+            sS[(e >> 4) * 17u + (e & 15u)] = p < M ? S[p] : 0ull;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        uint64_t v[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) v[k] = sS[lane * 17u + k];
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        uint32_t hf[4] = {0, 0, 0, 0};
+        if (p0 + 16 <= M) {
+            const uint4 h4 = *reinterpret_cast<const uint4 *>(headf + p0);
+            hf[0] = h4.x; hf[1] = h4.y; hf[2] = h4.z; hf[3] = h4.w;
+        } else {
+            for (uint32_t k = 0; k < 16 && p0 + k < M; ++k) hf[k >> 2] |= (uint32_t)headf[p0 + k] << (8 * (k & 3));
+        }
+        uint32_t L[16];
+        uint64_t T[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const bool ok = p0 + k < M;
+            const uint32_t idx = pk_idx(v[k]);
+            L[k] = ok ? len[idx] : 0u;
+            T[k] = ok ? ts[idx] : 0ull;
+        }
+        uint64_t tprev = __shfl_up(T[15], 1);
+        if (lane == 0) tprev = (p0 > 0 && p0 < M) ? ts[pk_idx(S[p0 - 1])] : 0ull;
+        // head flag of the position after this lane (end of array counts as a head)
+        const uint32_t h_first = hf[0] & 1u;
+        uint32_t next_head = __shfl_down(h_first, 1);
+        if (lane == 63) next_head = (base + kFT >= M) ? 1u : headf[base + kFT];
+        if (p0 + 16 >= M) next_head = 1;
+        uint32_t nh = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) nh += __popc(hf[k] & 0x01010101u);
+        const uint32_t hoff = wave_incl_sum(nh) - nh;
+        uint32_t g = hb + hoff;  // id of this lane's first head
+        FlowAcc A = acc_zero(), F = acc_zero();
+        uint32_t seen = 0;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            if (p0 + k < M) {
+                const bool h = (hf[k >> 2] >> (8 * (k & 3))) & 1u;
+                if (h) {
+                    if (seen == 0) F = A;
+                    else flow_finish(g + seen - 1, A, S, seg_start, hdr, len, salt, out, P);
+                    ++seen;
+                    A = acc_zero();
+                }
+                FlowAcc c = acc_zero();
+                c.n = 1; c.s1 = L[k]; c.s2 = (u128)L[k] * L[k];
+                if (!h) {
+                    const uint64_t d = T[k] - tprev;
+                    c.d1 = d; c.d2 = (u128)d * d; c.dmax = d;
+                }
+                acc_add(A, c);
+                tprev = T[k];
+            }
+        }
+        if (nh == 0) F = A;
+        // segmented inclusive scan over lanes of (has_head, piece open at lane end)
+        uint32_t fl = nh > 0;
+        FlowAcc val = nh > 0 ? A : F;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t ofl = __shfl_up(fl, o);
+            const FlowAcc ov = shfl_up_acc(val, o);
+            if (lane >= (uint32_t)o) {
+                if (!fl) acc_add(val, ov);
+                fl |= ofl;
+            }
+        }
+        uint32_t in_fl = __shfl_up(fl, 1);
+        FlowAcc in = shfl_up_acc(val, 1);
+        if (lane == 0) { in_fl = 0; in = acc_zero(); }
+        // the source open at this lane's start ends at its first head
+        if (nh > 0 && p0 > 0) {
+            FlowAcc tot = in;
+            acc_add(tot, F);
+            if (in_fl) flow_finish(g - 1, tot, S, seg_start, hdr, len, salt, out, P);
+            else firstp[sub] = tot;   // started in an earlier tile
+        }
+        // ... and the source open at the lane end finishes here if the next packet
+        // starts another source (inside the tile: the next lane handles it)
+        if (lane == 63) {
+            const uint32_t g_last = hb + hoff + nh - 1;
+            if (fl) {
+                if (next_head) flow_finish(g_last, val, S, seg_start, hdr, len, salt, out, P);
+                else {
+                    lastp[sub] = val;
+                    span_list[atomicAdd(&bs->n_span, 1u)] = g_last;
+                }
+            } else {
+                firstp[sub] = val;    // no head in the tile: a middle / final piece
+            }
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_flow_combine(const uint64_t *__restrict__ S, BatchState *bs,
+                                                      const uint32_t *__restrict__ seg_start,
+                                                      const FlowAcc *__restrict__ firstp,
+                                                      const FlowAcc *__restrict__ lastp,
+                                                      const uint32_t *__restrict__ span_list,
+                                                      const uint8_t *__restrict__ hdr,
+                                                      const uint32_t *__restrict__ len, FlowOut out,
+                                                      ScoreParams P, uint32_t salt) {
+    const uint32_t lane = lane_id();
+    const uint32_t ns = bs->n_span;
+    for (uint32_t i = blockIdx.x * 4u + (threadIdx.x >> 6); i < ns; i += gridDim.x * 4u) {
+        const uint32_t g = span_list[i];
+        const uint32_t s = seg_start[g], e = seg_start[g + 1];
+        const uint32_t t0 = s / kFT, t1 = (e - 1) / kFT;
+        FlowAcc a = acc_zero();
+        for (uint32_t t = t0 + 1 + lane; t <= t1; t += 64) acc_add(a, firstp[t]);
+        a = wave_sum_acc(a);
+        if (lane == 0) {
+            FlowAcc tot = lastp[t0];
+            acc_add(tot, a);
+            flow_finish(g, tot, S, seg_start, hdr, len, salt, out, P);
+        }
+    }
+}
+
+hipError_t launch_flows(const uint64_t *S, BatchState *bs, const uint8_t *headf, const uint32_t *len,
+                        const uint64_t *ts, const uint8_t *hdr, const uint32_t *tile_off,
+                        const uint32_t *sub_cnt, const uint32_t *seg_start, void *firstp, void *lastp,
+                        uint32_t *span_list, uint8_t *keys16, uint8_t *fam, float *feat, float *prob,
+                        uint8_t *dec, uint32_t cap, const ScoreParams &P, uint32_t salt, uint32_t n,
+                        hipStream_t st) {
+    const FlowOut out{keys16, fam, feat, prob, dec, cap};
+    const uint32_t nsub = (n + kFT - 1) / kFT;
+    const uint32_t grid = std::max<uint32_t>(1, std::min<uint32_t>(2048, (nsub + 3) / 4));
+    k_flow_tile<<<grid, 256, 0, st>>>(S, bs, headf, len, ts, hdr, tile_off, sub_cnt, seg_start,
+                                      (FlowAcc *)firstp, (FlowAcc *)lastp, span_list, out, P, salt);
+    k_flow_combine<<<256, 256, 0, st>>>(S, bs, seg_start, (const FlowAcc *)firstp,
+                                        (const FlowAcc *)lastp, span_list, hdr, len, out, P, salt);
+    return hipGetLastError();
+}
+
+size_t flow_acc_bytes() { return sizeof(FlowAcc); }
+
+}  // namespace fsx

@@ -12,6 +12,8 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include "fsx_q8.h"
+
 namespace fsx {
 
 constexpr uint64_t kSentinel = ~0ull;     // "not an IP packet" in the packed array
@@ -55,6 +57,8 @@ struct BatchState {
     uint32_t err;
     uint32_t max_len;
     uint32_t n_fix;       // mixed hash runs queued for the exact key fixup
+    uint32_t n_long;      // segments longer than kShortSeg (wave walker)
+    uint32_t n_span;      // sources crossing flow tiles (k_flow_combine)
     uint64_t max_ts;
     uint64_t allowed;     // this batch
     uint64_t dropped;
@@ -125,14 +129,41 @@ struct Scratch {
     uint8_t *tile_last;
     uint32_t *fix_list;
     uint64_t *fix_bitmap;  // one bit per sorted position
+    uint32_t *long_list;   // segments walked by a wave
+    uint32_t *sub_cnt;     // heads per 1024-position flow tile
+    void *flow_first;      // FlowAcc per flow tile (fsx_flows.hip)
+    void *flow_last;
+    uint32_t *span_list;
     uint64_t cap;          // packets the scratch is sized for
 };
 
+// Optional per-source outputs of a batch (flow features + q8 scores), device pointers.
+struct FlowRequest {
+    uint8_t *keys16;
+    uint8_t *fam;
+    float *feat;      // n_sources x 8, may be null
+    float *prob;      // may be null (then no scoring)
+    uint8_t *dec;
+    uint32_t cap;
+    ScoreParams score;
+};
+
+// do_limit: run the rate limiter (verdicts + maps); flows: also per-source features.
 hipError_t launch_verdict_pipeline(const uint8_t *hdr, const uint32_t *len, const uint64_t *ts,
                                    uint32_t n, uint8_t *verdict, Slot *table, TableState *tstate,
                                    BatchState *bs, const Scratch &sc, const Limits &lim,
-                                   hipStream_t st, hipEvent_t *ev, int nev, int *nev_used,
-                                   const char **names);
+                                   bool do_limit, const FlowRequest *flows, hipStream_t st,
+                                   hipEvent_t *ev, int nev, int *nev_used, const char **names);
+
+hipError_t launch_flows(const uint64_t *S, BatchState *bs, const uint8_t *headf, const uint32_t *len,
+                        const uint64_t *ts, const uint8_t *hdr, const uint32_t *tile_off,
+                        const uint32_t *sub_cnt, const uint32_t *seg_start, void *firstp, void *lastp,
+                        uint32_t *span_list, uint8_t *keys16, uint8_t *fam, float *feat, float *prob,
+                        uint8_t *dec, uint32_t cap, const ScoreParams &P, uint32_t salt, uint32_t n,
+                        hipStream_t st);
+size_t flow_acc_bytes();
+ScoreParams make_score_params(const int8_t w[8], float inv_in, int32_t zp_in, float bias_over_ats,
+                              float mult, int32_t zp_out, const uint8_t lut[256]);
 
 hipError_t launch_map_op(Slot *table, TableState *tstate, const Limits &lim, int op, int map_id,
                          const uint32_t key[4], const uint64_t val[3], uint64_t flags,

@@ -147,6 +147,18 @@ int fsx_verdict_batch(fsx_ctx *ctx, const uint8_t *hdr, const uint32_t *len,
 int fsx_verdict_batch_device(fsx_ctx *ctx, const uint8_t *d_hdr, const uint32_t *d_len,
                              const uint64_t *d_ts, size_t n, uint8_t *d_verdict);
 
+/* The full hot path on one device batch: verdicts and map state exactly as
+ * fsx_verdict_batch_device, plus, for every distinct source IP of the batch, its
+ * key (16 bytes, IPv4 in the first 4), family (4 or 6), the eight flow features of
+ * model/model.py:117 (d_features may be NULL) and, when a model is
+ * loaded, its q8 probability and decision (model/model.py:132-137, :206). Source
+ * outputs are indexed 0..sources-1 (sources = fsx_last_batch_info()[1] after
+ * fsx_sync); flow_cap bounds the rows written. */
+int fsx_process_batch_device(fsx_ctx *ctx, const uint8_t *d_hdr, const uint32_t *d_len,
+                             const uint64_t *d_ts, size_t n, uint8_t *d_verdict,
+                             uint8_t *d_keys16, uint8_t *d_family, float *d_features,
+                             float *d_prob, uint8_t *d_malicious, size_t flow_cap);
+
 /* BPF map syscalls on the five reference maps (bpf_map_*_elem semantics). */
 int fsx_map_lookup(fsx_ctx *ctx, int map_id, const void *key, void *value);
 int fsx_map_update(fsx_ctx *ctx, int map_id, const void *key, const void *value,
@@ -167,8 +179,9 @@ int fsx_score_device(fsx_ctx *ctx, const float *d_features, size_t n, float *d_p
                      uint8_t *d_malicious);
 
 /* Per-source-IP flow features (build-defined) for the packets of
- * one batch, n_flows_out = distinct source IPs; features are n_flows x 8 fp32 in
- * model/model.py:117 order. Keys: 16 bytes per flow + family byte (4 or 6). */
+ * one batch (host pointers; the maps are not touched). n_flows_out = distinct
+ * source IPs; up to cap rows of keys (16 B), family (4/6) and features (8 x fp32,
+ * model/model.py:117 order) are written, in no particular order. */
 int fsx_flow_features(fsx_ctx *ctx, const uint8_t *hdr, const uint32_t *len,
                       const uint64_t *ts_ns, size_t n, size_t cap, uint8_t *keys16,
                       uint8_t *family, float *features, size_t *n_flows_out);

@@ -293,3 +293,75 @@ def test_score_random_models(native):
             c.load_q8_model(_model(native, m))
             p, _ = c.score(g["rand_x"][i])
             assert np.array_equal(p.view(np.uint32), g["rand_p"][i].view(np.uint32)), i
+
+
+# ------------------------------------------------------------------ flow features + scoring
+def _sorted_flows(keys, fam, feat):
+    order = sorted(range(len(fam)), key=lambda i: (int(fam[i]), keys[i].tobytes()))
+    return keys[order], fam[order], feat[order]
+
+
+def _check_flows(native, oracle, hdr, ln, ts, cfg=None):
+    ko, fo, xo = oracle.flow_features(hdr, ln, ts)
+    with gpu_ctx(native, **(cfg or {})) as c:
+        kg, fg, xg = c.flow_features(hdr, ln, ts)
+    assert len(fg) == len(fo)
+    ko, fo, xo = _sorted_flows(ko, fo, xo)
+    kg, fg, xg = _sorted_flows(kg, fg, xg)
+    assert np.array_equal(fg, fo) and np.array_equal(kg, ko)
+    bad = np.nonzero((xg.view(np.uint32) != xo.view(np.uint32)).any(axis=1))[0]
+    assert bad.size == 0, (bad[:5], xg[bad[:3]], xo[bad[:3]])
+
+
+def test_flow_features_random(native, oracle):
+    rng = np.random.default_rng(31)
+    hdr, ln, ts = rand_stream(rng, 60000, 700, dt_max=5000, v6_frac=0.3, nonip_frac=0.02,
+                              short_frac=0.01)
+    _check_flows(native, oracle, hdr, ln, ts)
+
+
+def test_flow_features_heavy_sources(native, oracle):
+    """Config-1 stream: 1024 Zipf sources over 1M packets, so the heavy sources span
+    hundreds of flow tiles (exercises the cross-tile combine)."""
+    from flowsentryx_amd import synth
+    p, s = synth.config_params(1)
+    hdr, ln, ts = oracle.synth(p, s, 0, p.n)
+    _check_flows(native, oracle, hdr, ln, ts)
+
+
+def test_process_batch_device(native, oracle):
+    """Full path on device: verdicts + per-source features + q8 scores in one call."""
+    import torch
+    from flowsentryx_amd import fsx_load, synth
+    p, s = synth.config_params(2, n=1 << 19)
+    n = int(p.n)
+    hdr, ln, ts = oracle.synth(p, s, 0, n)
+    ref = json.loads((GOLDEN / "model_weights.json").read_text())
+    dev = lambda a: torch.from_numpy(a.view(np.uint8).reshape(-1)).cuda()
+    d_hdr, d_len, d_ts = dev(hdr), dev(ln), dev(ts)
+    d_v = torch.empty(n, dtype=torch.uint8, device="cuda")
+    d_k = torch.empty(n * 16, dtype=torch.uint8, device="cuda")
+    d_f = torch.empty(n, dtype=torch.uint8, device="cuda")
+    d_x = torch.empty(n * 8, dtype=torch.float32, device="cuda")
+    d_p = torch.empty(n, dtype=torch.float32, device="cuda")
+    d_d = torch.empty(n, dtype=torch.uint8, device="cuda")
+    with gpu_ctx(native, max_entries=1 << 20, max_batch=n) as c:
+        c.load_q8_model(fsx_load.model_from_dict(ref))
+        c.process_batch_device(d_hdr.data_ptr(), d_len.data_ptr(), d_ts.data_ptr(), n,
+                               d_v.data_ptr(), d_k.data_ptr(), d_f.data_ptr(), d_x.data_ptr(),
+                               d_p.data_ptr(), d_d.data_ptr(), n)
+        c.sync()
+        m = c.last_batch_info()["sources"]
+    o = oracle.Oracle(max_entries=1 << 20)
+    assert np.array_equal(d_v.cpu().numpy(), o.batch(hdr, ln, ts))
+    kg = d_k.cpu().numpy().reshape(n, 16)[:m]
+    fg = d_f.cpu().numpy()[:m]
+    xg = d_x.cpu().numpy().reshape(n, 8)[:m]
+    pg = d_p.cpu().numpy()[:m]
+    ko, fo, xo = oracle.flow_features(hdr, ln, ts)
+    assert m == len(fo)
+    order_g = sorted(range(m), key=lambda i: (int(fg[i]), kg[i].tobytes()))
+    order_o = sorted(range(m), key=lambda i: (int(fo[i]), ko[i].tobytes()))
+    assert np.array_equal(xg[order_g].view(np.uint32), xo[order_o].view(np.uint32))
+    po, _, _ = oracle.score(ref, xo[order_o])
+    assert np.array_equal(pg[order_g].view(np.uint32), po.view(np.uint32))
