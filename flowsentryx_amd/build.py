@@ -43,9 +43,12 @@ def _stale(out: Path, srcs: list[Path]) -> bool:
     return any(d.exists() and d.stat().st_mtime > t for d in deps)
 
 
-def build_lib(name: str, force: bool = False, verbose: bool = False) -> Path:
+def build_lib(name: str, force: bool = False, verbose: bool = False,
+              only_missing: bool = False) -> Path:
     out = PKG / name
     srcs = [CSRC / s for s in LIBS[name]]
+    if only_missing and out.exists() and not force:
+        return out
     if not force and not _stale(out, srcs):
         return out
     tmp = out.with_suffix(".so.tmp")
@@ -59,8 +62,8 @@ def build_lib(name: str, force: bool = False, verbose: bool = False) -> Path:
     return out
 
 
-def build_all(force: bool = False, verbose: bool = False) -> list[Path]:
-    return [build_lib(n, force, verbose) for n in LIBS]
+def build_all(force: bool = False, verbose: bool = False, only_missing: bool = False) -> list[Path]:
+    return [build_lib(n, force, verbose, only_missing) for n in LIBS]
 
 
 def build_oracle(verbose: bool = False) -> None:

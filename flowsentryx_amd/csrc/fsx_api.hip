@@ -103,7 +103,7 @@ static void free_scratch(fsx_ctx *c) {
     hipFree(s.seg_start); hipFree(s.seg_slot); hipFree(s.hist); hipFree(s.row_total);
     hipFree(s.tile_aux); hipFree(s.tile_last); hipFree(s.fix_list); hipFree(s.fix_bitmap);
     hipFree(s.long_list); hipFree(s.sub_cnt); hipFree(s.flow_first); hipFree(s.flow_last);
-    hipFree(s.span_list);
+    hipFree(s.span_list); hipFree(s.sort_ctl); hipFree(s.gbase); hipFree(s.status);
     s = Scratch{};
 }
 
@@ -129,6 +129,10 @@ static int alloc_scratch(fsx_ctx *c, uint64_t cap) {
     HIPCHK(c, hipMalloc(&s.flow_first, (cap / 1024 + 8) * flow_acc_bytes()));
     HIPCHK(c, hipMalloc(&s.flow_last, (cap / 1024 + 8) * flow_acc_bytes()));
     HIPCHK(c, hipMalloc(&s.span_list, (cap / 1024 + 8) * 4));
+    HIPCHK(c, hipMalloc(&s.sort_ctl, 1028 * 4));
+    HIPCHK(c, hipMalloc(&s.gbase, 1024 * 4));
+    HIPCHK(c, hipMalloc(&s.status, (cap / kSortTile + 2) * 256 * 8));
+    HIPCHK(c, hipMemset(s.status, 0, (cap / kSortTile + 2) * 256 * 8));
     s.cap = cap;
     return 0;
 }

@@ -16,6 +16,8 @@
 //                    order, stats_map counters (src/fsx_kern.c:210,332,342)
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+
 #include "fsx_dev_common.h"
 #include "fsx_internal.h"
 
@@ -33,11 +35,16 @@ __global__ __launch_bounds__(256) void k_parse(const uint8_t *__restrict__ hdr,
                                                const uint64_t *__restrict__ ts, uint32_t n,
                                                uint64_t *__restrict__ packed,
                                                uint8_t *__restrict__ verdict, BatchState *bs,
-                                               uint32_t salt, uint64_t seed, uint32_t v6_const) {
+                                               uint32_t salt, uint64_t seed, uint32_t v6_const,
+                                               uint32_t *__restrict__ ghist) {
     __shared__ uint32_t s_rec[4][64 * 17];
     __shared__ uint32_t s_red[4][3];
     __shared__ unsigned long long s_ts[4];
+    __shared__ uint32_t s_hist[4][256];  // the 4 radix digits of every sort key
     const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) s_hist[d][threadIdx.x] = 0;
+    __syncthreads();
     uint32_t *rec = s_rec[w];
     uint32_t any6 = 0, nonmono = 0, maxlen = 0;
     uint64_t maxts = 0;
@@ -63,10 +70,10 @@ __global__ __launch_bounds__(256) void k_parse(const uint8_t *__restrict__ hdr,
         const uint64_t T = live ? ts[i] : 0ull;
         uint64_t prev = __shfl_up(T, 1);
         if (lane == 0) prev = (live && i > 0) ? ts[i - 1] : T;
+        uint64_t out = kSentinel;
         if (live) {
             // parse_ethhdr (14-byte bound; raw h_proto, no VLAN)
             const uint32_t proto = ((d3 & 0xFFu) << 8) | ((d3 >> 8) & 0xFFu);
-            uint64_t out = kSentinel;
             uint8_t v = XDP_PASS;  // non-IP: PASS, not counted (src/fsx_kern.c:128-131)
             if (L < 14u) {
                 v = XDP_DROP;      // src/fsx_kern.c:124-127
@@ -94,7 +101,28 @@ __global__ __launch_bounds__(256) void k_parse(const uint8_t *__restrict__ hdr,
             maxlen = L > maxlen ? L : maxlen;
             maxts = T > maxts ? T : maxts;
         }
+        // radix histograms of the 4 key digits: lanes with equal digits are matched by
+        // ballots and one leader adds the count (no same-address LDS atomics, which
+        // serialize on the heavy sources of skewed traffic)
+        if (ghist) {
+            const uint64_t act = __ballot(out != kSentinel);
+#pragma unroll
+            for (int dg = 0; dg < 4; ++dg) {
+                const uint32_t d = (uint32_t)(out >> (32 + 8 * dg)) & 255u;
+                const uint64_t peers = match_digit(d, act);
+                if (out != kSentinel && (peers & ((1ull << lane) - 1ull)) == 0)
+                    atomicAdd(&s_hist[dg][d], (uint32_t)__popcll(peers));
+            }
+        }
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    }
+    if (ghist) {
+        __syncthreads();
+#pragma unroll
+        for (int dg = 0; dg < 4; ++dg) {
+            const uint32_t c = s_hist[dg][threadIdx.x];
+            if (c) atomicAdd(&ghist[dg * 256 + threadIdx.x], c);
+        }
     }
     any6 = __ballot(any6 != 0) ? 1u : 0u;
     nonmono = __ballot(nonmono != 0) ? 1u : 0u;
@@ -264,6 +292,131 @@ __global__ __launch_bounds__(256) void k_sort_scatter(const uint64_t *__restrict
         __syncthreads();
         s_base[tid] += s_tcnt[tid];
         __syncthreads();
+    }
+}
+
+// ------------------------------------------------------------------ onesweep radix sort
+// One kernel per 8-bit digit (Merrill & Garland's single-pass "Onesweep" structure):
+// the digit histograms of all four passes come from k_parse; each tile ranks its
+// 4096 keys stably in LDS (wave-ballot matching, as k_sort_scatter), publishes its
+// per-digit count, and learns its exclusive prefix by decoupled look-back over the
+// preceding tiles. Status words are 8-byte {generation, inclusive?, count} granules
+// written with one agent-scope store and polled with agent-scope loads (no fences:
+// the data is the flag). Tiles take ids from an atomic counter, so a tile only ever
+// waits on tiles whose blocks already started. Traffic per pass: 8 B in + 8 B out
+// per key + 2 KiB of status per 4096-key tile.
+
+// n_valid and the per-pass digit bases (exclusive scans of the k_parse histograms).
+__global__ __launch_bounds__(256) void k_hist_prep(const uint32_t *__restrict__ ghist,
+                                                   uint32_t *__restrict__ gbase, BatchState *bs) {
+    __shared__ uint32_t s_tmp[4];
+#pragma unroll
+    for (int dg = 0; dg < 4; ++dg) {
+        uint32_t tot;
+        const uint32_t b = block256_excl(ghist[dg * 256 + threadIdx.x], s_tmp, &tot);
+        gbase[dg * 256 + threadIdx.x] = b;
+        if (dg == 0 && threadIdx.x == 0) bs->n_valid = tot;
+    }
+}
+
+constexpr uint32_t kSpinLimit = 1u << 22;
+
+__device__ __forceinline__ unsigned long long os_word(uint32_t gen, bool inclusive, uint32_t cnt) {
+    return ((unsigned long long)gen << 33) | ((unsigned long long)(inclusive ? 1u : 0u) << 32) | cnt;
+}
+
+__global__ __launch_bounds__(256) void k_onesweep(const uint64_t *__restrict__ in,
+                                                  uint64_t *__restrict__ out, uint32_t L_host,
+                                                  const uint32_t *L_dev, uint32_t shift,
+                                                  const uint32_t *__restrict__ gbase,
+                                                  unsigned long long *status, uint32_t *tile_ctr,
+                                                  uint32_t gen, int first, BatchState *bs) {
+    __shared__ unsigned long long s_el[kSortTile];
+    __shared__ uint32_t s_wc[4][256];
+    __shared__ uint32_t s_dst[256], s_tbase[256], s_tcnt[256];
+    __shared__ uint32_t s_tmp[4];
+    __shared__ uint32_t s_tile;
+    const uint32_t tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
+    const uint32_t L = L_dev ? *L_dev : L_host;
+    const uint32_t ntiles = (L + kSortTile - 1) / kSortTile;
+    if (tid == 0) s_tile = atomicAdd(tile_ctr, 1u);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) s_wc[w][lane * 4 + k] = 0;
+    __syncthreads();
+    const uint32_t t = s_tile;
+    if (t >= ntiles) return;
+    const uint32_t t0 = t * kSortTile;
+    const uint32_t end = min(L, t0 + kSortTile);
+    const uint64_t lt_mask = (1ull << lane) - 1ull;
+    uint64_t v[kSortItems];
+    uint32_t lr[kSortItems];
+#pragma unroll
+    for (int r = 0; r < kSortItems; ++r) {
+        const uint32_t i = t0 + w * 1024u + (uint32_t)r * 64u + lane;
+        v[r] = i < end ? in[i] : kSentinel;
+    }
+#pragma unroll
+    for (int r = 0; r < kSortItems; ++r) {
+        const uint32_t i = t0 + w * 1024u + (uint32_t)r * 64u + lane;
+        const bool valid = i < end && !(first && v[r] == kSentinel);
+        const uint64_t act = __ballot(valid);
+        const uint32_t d = (uint32_t)(v[r] >> shift) & 255u;
+        const uint64_t peers = match_digit(d, act);
+        const uint32_t below = (uint32_t)__popcll(peers & lt_mask);
+        uint32_t base = 0;
+        if (valid) base = s_wc[w][d];
+        lr[r] = valid ? base + below : 0xFFFFFFFFu;
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        if (valid && below == 0) s_wc[w][d] = base + (uint32_t)__popcll(peers);
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    }
+    __syncthreads();
+    const uint32_t d = tid;
+    const uint32_t c0 = s_wc[0][d], c1 = s_wc[1][d], c2 = s_wc[2][d], c3 = s_wc[3][d];
+    const uint32_t tc = c0 + c1 + c2 + c3;
+    // publish this tile's count, then look back for the exclusive prefix
+    unsigned long long *my = status + (size_t)t * 256u + d;
+    if (t == 0) __hip_atomic_store(my, os_word(gen, true, tc), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else __hip_atomic_store(my, os_word(gen, false, tc), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t excl = 0;
+    if (t > 0) {
+        uint32_t tt = t - 1;
+        uint32_t spins = 0;
+        for (;;) {
+            const unsigned long long wv = __hip_atomic_load(status + (size_t)tt * 256u + d, __ATOMIC_RELAXED,
+                                                            __HIP_MEMORY_SCOPE_AGENT);
+            if ((uint32_t)(wv >> 33) != gen) {
+                if (++spins > kSpinLimit) { atomicOr(&bs->err, ERR_SORT_HANG); break; }
+                __builtin_amdgcn_s_sleep(1);
+                continue;
+            }
+            excl += (uint32_t)wv;
+            if ((wv >> 32) & 1ull) break;
+            if (tt == 0) break;
+            --tt;
+        }
+        __hip_atomic_store(my, os_word(gen, true, excl + tc), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    s_wc[0][d] = 0; s_wc[1][d] = c0; s_wc[2][d] = c0 + c1; s_wc[3][d] = c0 + c1 + c2;
+    s_tcnt[d] = tc;
+    const uint32_t tb = block256_excl(tc, s_tmp, nullptr);
+    s_tbase[d] = tb;
+    s_dst[d] = gbase[d] + excl;
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < kSortItems; ++r) {
+        if (lr[r] != 0xFFFFFFFFu) {
+            const uint32_t dd = (uint32_t)(v[r] >> shift) & 255u;
+            s_el[s_tbase[dd] + s_wc[w][dd] + lr[r]] = v[r];
+        }
+    }
+    __syncthreads();
+    const uint32_t T = s_tbase[255] + s_tcnt[255];
+    for (uint32_t j = tid; j < T; j += 256) {
+        const uint64_t x = s_el[j];
+        const uint32_t dd = (uint32_t)(x >> shift) & 255u;
+        out[s_dst[dd] + (j - s_tbase[dd])] = x;
     }
 }
 
@@ -1120,6 +1273,15 @@ __global__ __launch_bounds__(256) void k_fill_scatter(const uint8_t *__restrict_
 // ------------------------------------------------------------------ pipeline
 static inline uint32_t cdiv(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); }
 
+// Look-back generations: every onesweep pass of every batch gets a fresh value, so
+// stale status words of earlier passes never match (no per-pass memset).
+static std::atomic<uint32_t> g_generation{0};
+static uint32_t next_generation() {
+    uint32_t g = g_generation.fetch_add(4) & 0x3FFFFFFFu;
+    if (g == 0) g = g_generation.fetch_add(4) & 0x3FFFFFFFu;
+    return g;
+}
+
 hipError_t launch_verdict_pipeline(const uint8_t *hdr, const uint32_t *len, const uint64_t *ts,
                                    uint32_t n, uint8_t *verdict, Slot *table, TableState *tstate,
                                    BatchState *bs, const Scratch &sc, const Limits &lim,
@@ -1142,22 +1304,41 @@ hipError_t launch_verdict_pipeline(const uint8_t *hdr, const uint32_t *len, cons
     const uint32_t gridTiles = std::min<uint32_t>(4096, std::max<uint32_t>(1, cdiv(n, kTile)));
 
     // mark(name) closes the interval of the kernel just enqueued (per-kernel timing)
+    const bool classic = (lim.test_flags & 2u) != 0;
+    if (!classic && (e = hipMemsetAsync(sc.sort_ctl, 0, 1028 * 4, st)) != hipSuccess) return e;
     mark("start");
     k_parse<<<std::min<uint32_t>(2048, std::max<uint32_t>(1, cdiv(n, 256))), 256, 0, st>>>(
         hdr, len, ts, n, sc.packed[0], verdict, bs, lim.salt32, lim.seed,
-        (lim.test_flags & 1u) ? skey_v4(0x0100000Au, lim.salt32) : 0u);
+        (lim.test_flags & 1u) ? skey_v4(0x0100000Au, lim.salt32) : 0u,
+        classic ? nullptr : sc.sort_ctl);
     mark("k_parse");
-    for (int pass = 0; pass < 4; ++pass) {
-        const uint64_t *in = sc.packed[pass & 1];
-        uint64_t *out = sc.packed[(pass + 1) & 1];
-        const uint32_t shift = 32u + 8u * (uint32_t)pass;
-        const uint32_t *Ld = pass == 0 ? nullptr : &bs->n_valid;
-        k_sort_hist<<<G, 256, 0, st>>>(in, n, Ld, shift, sc.hist, G, pass == 0, bs);
-        mark("k_sort_hist");
-        k_sort_rowscan<<<256, 256, 0, st>>>(sc.hist, G, sc.row_total);
-        mark("k_sort_rowscan");
-        k_sort_scatter<<<G, 256, 0, st>>>(in, out, n, Ld, shift, sc.hist, sc.row_total, G, pass == 0);
-        mark("k_sort_scatter");
+    if (classic) {
+        for (int pass = 0; pass < 4; ++pass) {
+            const uint64_t *in = sc.packed[pass & 1];
+            uint64_t *out = sc.packed[(pass + 1) & 1];
+            const uint32_t shift = 32u + 8u * (uint32_t)pass;
+            const uint32_t *Ld = pass == 0 ? nullptr : &bs->n_valid;
+            k_sort_hist<<<G, 256, 0, st>>>(in, n, Ld, shift, sc.hist, G, pass == 0, bs);
+            mark("k_sort_hist");
+            k_sort_rowscan<<<256, 256, 0, st>>>(sc.hist, G, sc.row_total);
+            mark("k_sort_rowscan");
+            k_sort_scatter<<<G, 256, 0, st>>>(in, out, n, Ld, shift, sc.hist, sc.row_total, G, pass == 0);
+            mark("k_sort_scatter");
+        }
+    } else {
+        k_hist_prep<<<1, 256, 0, st>>>(sc.sort_ctl, sc.gbase, bs);
+        const uint32_t gen0 = next_generation();
+        const uint32_t ntiles = std::max<uint32_t>(1, cdiv(n, kSortTile));
+        for (int pass = 0; pass < 4; ++pass) {
+            const uint64_t *in = sc.packed[pass & 1];
+            uint64_t *out = sc.packed[(pass + 1) & 1];
+            const uint32_t shift = 32u + 8u * (uint32_t)pass;
+            const uint32_t *Ld = pass == 0 ? nullptr : &bs->n_valid;
+            k_onesweep<<<ntiles, 256, 0, st>>>(in, out, n, Ld, shift, sc.gbase + 256 * pass, sc.status,
+                                               sc.sort_ctl + 1024 + pass, gen0 + (uint32_t)pass,
+                                               pass == 0, bs);
+            mark("k_onesweep");
+        }
     }
     uint64_t *S = sc.packed[0];
     const uint32_t nbm = cdiv(n, 64);

@@ -30,6 +30,7 @@ enum : uint32_t {
     ERR_TABLE_FULL = 1u,
     ERR_PROBE = 2u,
     ERR_FIXUP = 4u,
+    ERR_SORT_HANG = 8u,
 };
 
 enum : uint32_t { SLOT_HAS_ST = 1u, SLOT_HAS_BL = 2u, SLOT_HAS_TB = 4u };
@@ -134,6 +135,9 @@ struct Scratch {
     void *flow_first;      // FlowAcc per flow tile (fsx_flows.hip)
     void *flow_last;
     uint32_t *span_list;
+    uint32_t *sort_ctl;    // [0,1024) digit histograms of the 4 passes, [1024,1028) tile counters
+    uint32_t *gbase;       // 4 x 256 digit bases
+    unsigned long long *status;  // onesweep look-back words, 256 per tile
     uint64_t cap;          // packets the scratch is sized for
 };
 

@@ -54,6 +54,8 @@ extern "C" {
  * source to one sort key equal to IPv4 10.0.0.1's, forcing the exact collision
  * fixup path (results must not change). */
 #define FSX_FLAG_TEST_V6_COLLIDE 1u
+/* Use the classic 3-kernel-per-pass radix sort instead of onesweep (A/B only). */
+#define FSX_FLAG_CLASSIC_SORT 2u
 
 /* Map ids: the five maps of src/fsx_kern.c:56-94. */
 enum fsx_map_id {

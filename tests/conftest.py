@@ -34,7 +34,8 @@ def oracle():
 
 @pytest.fixture(scope="session")
 def native():
-    """The in-tree libfsx_hip.so (built if missing)."""
+    """The in-tree libfsx_hip.so (built only if missing: on the GPU box the libraries
+    built in the source container are used as shipped)."""
     from flowsentryx_amd import build, lib
-    build.build_all()
+    build.build_all(only_missing=True)
     return lib
