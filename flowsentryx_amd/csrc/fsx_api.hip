@@ -277,12 +277,12 @@ static int drain_timings(fsx_ctx *c) {
 
 // Enqueue one batch: verdicts + maps when d_verdict is set, per-source flows when fr is.
 static int run_batch(fsx_ctx *c, const uint8_t *d_hdr, const uint32_t *d_len, const uint64_t *d_ts,
-                     size_t n, uint8_t *d_verdict, const FlowRequest *fr) {
+                     size_t n, uint8_t *d_verdict, bool do_limit, const FlowRequest *fr) {
     if (n > c->cfg.max_batch) return set_err(c, -E2BIG, "n=%zu exceeds max_batch", n);
     int rc = sel(c);
     if (rc) return rc;
     if (c->pending) { rc = fsx_sync(c); if (rc) return rc; }
-    if (d_verdict && c->cfg.limiter != FSX_LIMIT_FIXED_WINDOW)
+    if (do_limit && c->cfg.limiter != FSX_LIMIT_FIXED_WINDOW)
         return set_err(c, -EOPNOTSUPP, "limiter %d not built into this pipeline yet", c->cfg.limiter);
     hipEvent_t *ev = nullptr;
     const char **names = nullptr;
@@ -295,8 +295,8 @@ static int run_batch(fsx_ctx *c, const uint8_t *d_hdr, const uint32_t *d_len, co
         c->ring_n++;
     }
     hipError_t e = launch_verdict_pipeline(d_hdr, d_len, d_ts, (uint32_t)n, d_verdict, c->table,
-                                           c->tstate, c->bs, c->sc, c->lim, d_verdict != nullptr,
-                                           fr, c->stream, ev, kMaxEv, used, names);
+                                           c->tstate, c->bs, c->sc, c->lim, do_limit, fr, c->stream,
+                                           ev, kMaxEv, used, names);
     if (e != hipSuccess) return set_err(c, -EIO, "pipeline launch: %s", hipGetErrorString(e));
     c->pending = true;
     return 0;
@@ -319,7 +319,7 @@ int fsx_verdict_batch_device(fsx_ctx *c, const uint8_t *d_hdr, const uint32_t *d
                              const uint64_t *d_ts, size_t n, uint8_t *d_verdict) {
     if (!c) return -EINVAL;
     if (n && (!d_hdr || !d_len || !d_ts || !d_verdict)) return set_err(c, -EINVAL, "null buffer");
-    return run_batch(c, d_hdr, d_len, d_ts, n, d_verdict, nullptr);
+    return run_batch(c, d_hdr, d_len, d_ts, n, d_verdict, true, nullptr);
 }
 
 int fsx_process_batch_device(fsx_ctx *c, const uint8_t *d_hdr, const uint32_t *d_len,
@@ -330,7 +330,7 @@ int fsx_process_batch_device(fsx_ctx *c, const uint8_t *d_hdr, const uint32_t *d
     if (n && (!d_hdr || !d_len || !d_ts || !d_verdict || !d_keys16 || !d_family))
         return set_err(c, -EINVAL, "null buffer");
     const FlowRequest fr = flow_request(c, d_keys16, d_family, d_features, d_prob, d_malicious, flow_cap);
-    return run_batch(c, d_hdr, d_len, d_ts, n, d_verdict, &fr);
+    return run_batch(c, d_hdr, d_len, d_ts, n, d_verdict, true, &fr);
 }
 
 static int ensure_stage(fsx_ctx *c, uint64_t n) {
@@ -554,7 +554,8 @@ int fsx_flow_features(fsx_ctx *c, const uint8_t *hdr, const uint32_t *len, const
     HIPCHK(c, hipMemcpyAsync(c->d_len, len, n * 4, hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipMemcpyAsync(c->d_ts, ts, n * 8, hipMemcpyHostToDevice, c->stream));
     FlowRequest fr = flow_request(c, dk, df, dfeat, nullptr, nullptr, n);
-    rc = run_batch(c, c->d_hdr, c->d_len, c->d_ts, n, nullptr, &fr);
+    // verdict scratch: parse writes default verdicts; the limiter does not run
+    rc = run_batch(c, c->d_hdr, c->d_len, c->d_ts, n, c->d_verdict, false, &fr);
     if (!rc) rc = fsx_sync(c);
     BatchState h{};
     if (!rc && hipMemcpy(&h, c->bs, sizeof(h), hipMemcpyDeviceToHost) != hipSuccess) rc = -EIO;

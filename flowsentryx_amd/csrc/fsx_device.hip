@@ -96,7 +96,7 @@ __global__ __launch_bounds__(256) void k_parse(const uint8_t *__restrict__ hdr,
             packed[i] = out;
             // IP packets default to PASS here (coalesced); the fill pass writes only
             // the DROP verdicts, which cluster in the heavy sources' segments
-            verdict[i] = out == kSentinel ? v : (uint8_t)XDP_PASS;
+            if (verdict) verdict[i] = out == kSentinel ? v : (uint8_t)XDP_PASS;
             nonmono |= T < prev ? 1u : 0u;
             maxlen = L > maxlen ? L : maxlen;
             maxts = T > maxts ? T : maxts;

@@ -12,7 +12,7 @@ step() {
   tail -5 "gpurun_out/$name.log"
   return $rc
 }
-step pytest_gpu 1200 python -m pytest tests -m gpu -q -p no:cacheprovider --timeout=600
+step pytest_gpu 900 python -m pytest tests -m gpu -q -p no:cacheprovider --timeout=240 --timeout-method=thread
 rc=$?
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $?
