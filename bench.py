@@ -40,6 +40,9 @@ KERNEL_BYTES = {
     "k_parse": ("packet", 64 + 4 + 8 + 8),      # header record + len + ts in, sort word out
     "k_sort_scatter": ("ip_packet", 16),        # sort word in + out
     "k_sort_hist": ("ip_packet", 8),
+    "k_onesweep": ("ip_packet", 16),            # sort word in + out, per digit pass
+    "k_flow_features": ("ip_packet", 8 + 4 + 8),  # sort word + len + ts per packet
+    "k_walk_fixed": ("ip_packet", 8 + 4 + 8 + 1),  # sort word + len + ts in, mark out
     "k_fill_scatter": ("ip_packet", 1 + 8 + 1),  # mark + sort word in, verdict out
 }
 
