@@ -99,7 +99,7 @@ static uint64_t next_pow2(uint64_t x) {
 
 static void free_scratch(fsx_ctx *c) {
     Scratch &s = c->sc;
-    hipFree(s.packed[0]); hipFree(s.packed[1]); hipFree(s.marks); hipFree(s.headf);
+    hipFree(s.packed[0]); hipFree(s.packed[1]); hipFree(s.pay[0]); hipFree(s.pay[1]); hipFree(s.marks); hipFree(s.headf);
     hipFree(s.seg_start); hipFree(s.seg_slot); hipFree(s.hist); hipFree(s.row_total);
     hipFree(s.tile_aux); hipFree(s.tile_last); hipFree(s.fix_list); hipFree(s.fix_bitmap);
     hipFree(s.long_list); hipFree(s.sub_cnt); hipFree(s.flow_first); hipFree(s.flow_last);
@@ -114,6 +114,8 @@ static int alloc_scratch(fsx_ctx *c, uint64_t cap) {
     const uint64_t ntiles = cap / kTile + 2;
     HIPCHK(c, hipMalloc(&s.packed[0], cap * 8));
     HIPCHK(c, hipMalloc(&s.packed[1], cap * 8));
+    HIPCHK(c, hipMalloc(&s.pay[0], cap * 8));
+    HIPCHK(c, hipMalloc(&s.pay[1], cap * 8));
     HIPCHK(c, hipMalloc(&s.marks, cap + 16));
     HIPCHK(c, hipMalloc(&s.headf, cap + 16));
     HIPCHK(c, hipMalloc(&s.seg_start, (cap + 1) * 4));
@@ -576,10 +578,10 @@ int fsx_last_batch_info(fsx_ctx *c, uint64_t *info, int cap) {
     HIPCHK(c, hipStreamSynchronize(c->stream));
     BatchState h;
     HIPCHK(c, hipMemcpy(&h, c->bs, sizeof(h), hipMemcpyDeviceToHost));
-    const uint64_t v[10] = {h.n_valid, h.nseg, h.n_new, h.any_v6, h.nonmono, h.max_len,
-                            h.max_ts, h.allowed, h.dropped, h.n_fix};
+    const uint64_t v[11] = {h.n_valid, h.nseg, h.n_new, h.any_v6, h.nonmono, h.max_len,
+                            h.max_ts, h.allowed, h.dropped, h.n_fix, h.pay_ok};
     int k = 0;
-    for (; k < cap && k < 10; ++k) info[k] = v[k];
+    for (; k < cap && k < 11; ++k) info[k] = v[k];
     return k;
 }
 

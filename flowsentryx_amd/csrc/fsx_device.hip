@@ -39,7 +39,7 @@ __global__ __launch_bounds__(256) void k_parse(const uint8_t *__restrict__ hdr,
                                                uint32_t *__restrict__ ghist) {
     __shared__ uint32_t s_rec[4][64 * 17];
     __shared__ uint32_t s_red[4][3];
-    __shared__ unsigned long long s_ts[4];
+    __shared__ unsigned long long s_ts[4], s_its[4];
     __shared__ uint32_t s_hist[4][256];  // the 4 radix digits of every sort key
     const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
 #pragma unroll
@@ -47,7 +47,7 @@ __global__ __launch_bounds__(256) void k_parse(const uint8_t *__restrict__ hdr,
     __syncthreads();
     uint32_t *rec = s_rec[w];
     uint32_t any6 = 0, nonmono = 0, maxlen = 0;
-    uint64_t maxts = 0;
+    uint64_t maxts = 0, inv_mints = 0;  // ~min ts, max-reduced
     const uint32_t ntiles = (n + 63u) >> 6;
     for (uint32_t t = blockIdx.x * 4u + w; t < ntiles; t += gridDim.x * 4u) {
         const uint32_t base = t << 6;
@@ -100,6 +100,7 @@ __global__ __launch_bounds__(256) void k_parse(const uint8_t *__restrict__ hdr,
             nonmono |= T < prev ? 1u : 0u;
             maxlen = L > maxlen ? L : maxlen;
             maxts = T > maxts ? T : maxts;
+            inv_mints = ~T > inv_mints ? ~T : inv_mints;
         }
         // radix histograms of the 4 key digits: lanes with equal digits are matched by
         // ballots and one leader adds the count (no same-address LDS atomics, which
@@ -128,20 +129,26 @@ __global__ __launch_bounds__(256) void k_parse(const uint8_t *__restrict__ hdr,
     nonmono = __ballot(nonmono != 0) ? 1u : 0u;
     maxlen = wave_max(maxlen);
     maxts = wave_max(maxts);
-    if (lane == 0) { s_red[w][0] = any6; s_red[w][1] = nonmono; s_red[w][2] = maxlen; s_ts[w] = maxts; }
+    inv_mints = wave_max(inv_mints);
+    if (lane == 0) {
+        s_red[w][0] = any6; s_red[w][1] = nonmono; s_red[w][2] = maxlen;
+        s_ts[w] = maxts; s_its[w] = inv_mints;
+    }
     __syncthreads();
     if (threadIdx.x == 0) {
         uint32_t a = 0, m = 0, l = 0;
-        uint64_t mt = 0;
+        uint64_t mt = 0, imt = 0;
         for (int k = 0; k < 4; ++k) {
             a |= s_red[k][0]; m |= s_red[k][1];
             l = s_red[k][2] > l ? s_red[k][2] : l;
             mt = s_ts[k] > mt ? s_ts[k] : mt;
+            imt = s_its[k] > imt ? s_its[k] : imt;
         }
         if (a) atomicOr(&bs->any_v6, 1u);
         if (m) atomicOr(&bs->nonmono, 1u);
         atomicMax(&bs->max_len, l);
         atomicMax(reinterpret_cast<unsigned long long *>(&bs->max_ts), (unsigned long long)mt);
+        atomicMax(reinterpret_cast<unsigned long long *>(&bs->inv_min_ts), (unsigned long long)imt);
     }
 }
 
@@ -317,6 +324,8 @@ __global__ __launch_bounds__(256) void k_hist_prep(const uint32_t *__restrict__ 
         gbase[dg * 256 + threadIdx.x] = b;
         if (dg == 0 && threadIdx.x == 0) bs->n_valid = tot;
     }
+    if (threadIdx.x == 0)
+        bs->pay_ok = bs->max_len < (1u << kPayLenBits) && bs->max_ts - ~bs->inv_min_ts < kPayTsRange;
 }
 
 constexpr uint32_t kSpinLimit = 1u << 22;
@@ -330,7 +339,11 @@ __global__ __launch_bounds__(256) void k_onesweep(const uint64_t *__restrict__ i
                                                   const uint32_t *L_dev, uint32_t shift,
                                                   const uint32_t *__restrict__ gbase,
                                                   unsigned long long *status, uint32_t *tile_ctr,
-                                                  uint32_t gen, int first, BatchState *bs) {
+                                                  uint32_t gen, int first, BatchState *bs,
+                                                  const uint64_t *__restrict__ pin,
+                                                  uint64_t *__restrict__ pout,
+                                                  const uint64_t *__restrict__ ts,
+                                                  const uint32_t *__restrict__ len) {
     __shared__ unsigned long long s_el[kSortTile];
     __shared__ uint32_t s_wc[4][256];
     __shared__ uint32_t s_dst[256], s_tbase[256], s_tcnt[256];
@@ -354,6 +367,19 @@ __global__ __launch_bounds__(256) void k_onesweep(const uint64_t *__restrict__ i
     for (int r = 0; r < kSortItems; ++r) {
         const uint32_t i = t0 + w * 1024u + (uint32_t)r * 64u + lane;
         v[r] = i < end ? in[i] : kSentinel;
+    }
+    // payload words: built from (ts, len) in pass 0 (positions are arrival indices
+    // there), carried afterwards
+    const bool pay = bs->pay_ok != 0;
+    uint64_t pv[kSortItems];
+    if (pay) {
+        const uint64_t tbase = ~bs->inv_min_ts;
+#pragma unroll
+        for (int r = 0; r < kSortItems; ++r) {
+            const uint32_t i = t0 + w * 1024u + (uint32_t)r * 64u + lane;
+            if (first) pv[r] = i < end ? ((ts[i] - tbase) << kPayLenBits) | len[i] : 0ull;
+            else pv[r] = i < end ? pin[i] : 0ull;
+        }
     }
 #pragma unroll
     for (int r = 0; r < kSortItems; ++r) {
@@ -408,15 +434,34 @@ __global__ __launch_bounds__(256) void k_onesweep(const uint64_t *__restrict__ i
     for (int r = 0; r < kSortItems; ++r) {
         if (lr[r] != 0xFFFFFFFFu) {
             const uint32_t dd = (uint32_t)(v[r] >> shift) & 255u;
-            s_el[s_tbase[dd] + s_wc[w][dd] + lr[r]] = v[r];
+            lr[r] += s_tbase[dd] + s_wc[w][dd];  // tile-sorted slot
+            s_el[lr[r]] = v[r];
         }
     }
     __syncthreads();
     const uint32_t T = s_tbase[255] + s_tcnt[255];
-    for (uint32_t j = tid; j < T; j += 256) {
-        const uint64_t x = s_el[j];
-        const uint32_t dd = (uint32_t)(x >> shift) & 255u;
-        out[s_dst[dd] + (j - s_tbase[dd])] = x;
+    uint32_t dst[kSortItems];
+#pragma unroll
+    for (int m = 0; m < kSortItems; ++m) {
+        const uint32_t j = tid + 256u * (uint32_t)m;
+        if (j < T) {
+            const uint64_t x = s_el[j];
+            const uint32_t dd = (uint32_t)(x >> shift) & 255u;
+            dst[m] = s_dst[dd] + (j - s_tbase[dd]);
+            out[dst[m]] = x;
+        }
+    }
+    if (!pay) return;
+    // the payload words follow the same permutation through the same LDS slots
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < kSortItems; ++r)
+        if (lr[r] != 0xFFFFFFFFu) s_el[lr[r]] = pv[r];
+    __syncthreads();
+#pragma unroll
+    for (int m = 0; m < kSortItems; ++m) {
+        const uint32_t j = tid + 256u * (uint32_t)m;
+        if (j < T) pout[dst[m]] = s_el[j];
     }
 }
 
@@ -547,6 +592,25 @@ __global__ __launch_bounds__(256) void k_fixup_long(uint64_t *__restrict__ S,
             __syncthreads();
             cur += n_eq;
             (void)s_pk; (void)s_neq;
+        }
+    }
+}
+
+// The fixup reorders whole runs; rebuild their payload words from (ts, len).
+__global__ __launch_bounds__(256) void k_fixup_pay(const uint64_t *__restrict__ S,
+                                                   uint64_t *__restrict__ pay, BatchState *bs,
+                                                   const uint32_t *__restrict__ fix_list,
+                                                   const uint64_t *__restrict__ ts,
+                                                   const uint32_t *__restrict__ len) {
+    if (!bs->pay_ok) return;
+    const uint32_t nf = bs->n_fix, M = bs->n_valid;
+    const uint64_t tbase = ~bs->inv_min_ts;
+    for (uint32_t f = blockIdx.x; f < nf; f += gridDim.x) {
+        const uint32_t h = fix_list[f];
+        const uint32_t e = upper_bound_skey(S, h, M, pk_skey(S[h]));
+        for (uint32_t p = h + threadIdx.x; p < e; p += 256) {
+            const uint32_t idx = pk_idx(S[p]);
+            pay[p] = ((ts[idx] - tbase) << kPayLenBits) | len[idx];
         }
     }
 }
@@ -770,18 +834,30 @@ __global__ void k_count_inserted(BatchState *bs, TableState *tstate) {
 // search instead of one per binary-search step).
 constexpr uint32_t kShortSeg = 512;
 
+// Timestamp / length of sorted position q: from the payload words carried by the
+// sort (kPay), else gathered through the arrival index.
+template <bool kPay>
 struct SegView {
     const uint64_t *S;
     const uint64_t *ts;
     const uint32_t *len;
-    __device__ __forceinline__ uint64_t t(uint32_t q) const { return ts[pk_idx(S[q])]; }
-    __device__ __forceinline__ uint32_t l(uint32_t q) const { return len[pk_idx(S[q])]; }
+    const uint64_t *pay;
+    uint64_t tbase;
+    __device__ __forceinline__ uint64_t t(uint32_t q) const {
+        if constexpr (kPay) return tbase + (pay[q] >> kPayLenBits);
+        else return ts[pk_idx(S[q])];
+    }
+    __device__ __forceinline__ uint32_t l(uint32_t q) const {
+        if constexpr (kPay) return (uint32_t)pay[q] & ((1u << kPayLenBits) - 1u);
+        else return len[pk_idx(S[q])];
+    }
 };
 
 // First q in [lo, hi) with t(q) > X (t non-decreasing on [lo, hi)); wave-uniform
 // arguments, every lane calls. Round 0 probes 64 consecutive packets, round 1 64
 // exponentially spaced ones, then 64-ary narrowing.
-__device__ uint32_t wave_gallop_gt(const SegView &sv, uint32_t lo, uint32_t hi, uint64_t X) {
+template <class SV>
+__device__ uint32_t wave_gallop_gt(const SV &sv, uint32_t lo, uint32_t hi, uint64_t X) {
     const uint32_t lane = lane_id();
     if (lo >= hi) return hi;
     {
@@ -831,7 +907,8 @@ __device__ uint32_t wave_gallop_gt(const SegView &sv, uint32_t lo, uint32_t hi, 
 }
 
 // Thread version: galloping from lo, O(log distance).
-__device__ __forceinline__ uint32_t gallop_gt(const SegView &sv, uint32_t lo, uint32_t hi,
+template <class SV>
+__device__ __forceinline__ uint32_t gallop_gt(const SV &sv, uint32_t lo, uint32_t hi,
                                               uint64_t X) {
     if (lo >= hi) return hi;
     if (sv.t(lo) > X) return lo;
@@ -854,27 +931,24 @@ __device__ __forceinline__ uint32_t gallop_gt(const SegView &sv, uint32_t lo, ui
 
 // Sum of frame lengths over [lo, hi): wave-strided (4 loads in flight per lane) or,
 // for a thread, 16 independent gathers per step.
-template <bool kWave>
-__device__ __forceinline__ uint64_t sum_len(const SegView &sv, uint32_t lo, uint32_t hi) {
+template <bool kWave, class SV>
+__device__ __forceinline__ uint64_t sum_len(const SV &sv, uint32_t lo, uint32_t hi) {
     uint64_t s = 0;
     if constexpr (kWave) {
         const uint32_t lane = lane_id();
         uint32_t q = lo + lane;
         for (; q + 192 < hi; q += 256) {
-            const uint32_t i0 = pk_idx(sv.S[q]), i1 = pk_idx(sv.S[q + 64]);
-            const uint32_t i2 = pk_idx(sv.S[q + 128]), i3 = pk_idx(sv.S[q + 192]);
-            s += (uint64_t)sv.len[i0] + sv.len[i1] + sv.len[i2] + sv.len[i3];
+            const uint32_t l0 = sv.l(q), l1 = sv.l(q + 64), l2 = sv.l(q + 128), l3 = sv.l(q + 192);
+            s += (uint64_t)l0 + l1 + l2 + l3;
         }
         for (; q < hi; q += 64) s += sv.l(q);
         return wave_sum(s);
     } else {
         uint32_t q = lo;
         for (; q + 16 <= hi; q += 16) {
-            uint32_t idx[16], l[16];
+            uint32_t l[16];
 #pragma unroll
-            for (int k = 0; k < 16; ++k) idx[k] = pk_idx(sv.S[q + k]);
-#pragma unroll
-            for (int k = 0; k < 16; ++k) l[k] = sv.len[idx[k]];
+            for (int k = 0; k < 16; ++k) l[k] = sv.l(q + k);
 #pragma unroll
             for (int k = 0; k < 16; ++k) s += l[k];
         }
@@ -884,8 +958,8 @@ __device__ __forceinline__ uint64_t sum_len(const SegView &sv, uint32_t lo, uint
 }
 
 // First q in [from, lim) with acc0 + sum(L[from..q]) > B, else lim.
-template <bool kWave>
-__device__ uint32_t bytes_trigger(const SegView &sv, uint32_t from, uint32_t lim, uint64_t acc0,
+template <bool kWave, class SV>
+__device__ uint32_t bytes_trigger(const SV &sv, uint32_t from, uint32_t lim, uint64_t acc0,
                                   uint64_t B) {
     uint64_t acc = acc0;
     if constexpr (kWave) {
@@ -908,8 +982,8 @@ __device__ uint32_t bytes_trigger(const SegView &sv, uint32_t from, uint32_t lim
     }
 }
 
-template <bool kWave>
-__device__ __forceinline__ uint32_t search_gt(const SegView &sv, uint32_t lo, uint32_t hi, uint64_t X) {
+template <bool kWave, class SV>
+__device__ __forceinline__ uint32_t search_gt(const SV &sv, uint32_t lo, uint32_t hi, uint64_t X) {
     if constexpr (kWave) return wave_gallop_gt(sv, lo, hi, X);
     else return gallop_gt(sv, lo, hi, X);
 }
@@ -957,18 +1031,16 @@ __device__ __forceinline__ void fw_step(FwState &s, uint64_t now, uint32_t L, ui
 }
 
 // Exact replay for one thread, 16 packets' loads in flight per step.
-__device__ void walk_fixed_exact_thread(const SegView &sv, uint32_t a, uint32_t b,
+template <class SV>
+__device__ void walk_fixed_exact_thread(const SV &sv, uint32_t a, uint32_t b,
                                         const Limits &lim, MarkWriter<false> &mw, FwState &s) {
     for (uint32_t q0 = a; q0 < b; q0 += 16) {
-        uint32_t idx[16];
         uint64_t t[16];
         uint32_t L[16];
 #pragma unroll
-        for (int k = 0; k < 16; ++k) idx[k] = q0 + k < b ? pk_idx(sv.S[q0 + k]) : 0u;
-#pragma unroll
         for (int k = 0; k < 16; ++k) {
-            t[k] = q0 + k < b ? sv.ts[idx[k]] : 0ull;
-            L[k] = q0 + k < b ? sv.len[idx[k]] : 0u;
+            t[k] = q0 + k < b ? sv.t(q0 + k) : 0ull;
+            L[k] = q0 + k < b ? sv.l(q0 + k) : 0u;
         }
 #pragma unroll
         for (int k = 0; k < 16; ++k)
@@ -978,7 +1050,8 @@ __device__ void walk_fixed_exact_thread(const SegView &sv, uint32_t a, uint32_t 
 
 // Exact replay for one wave: 64 packets loaded in parallel, then stepped uniformly
 // (every lane keeps the same state; values broadcast by shuffles).
-__device__ void walk_fixed_exact_wave(const SegView &sv, uint32_t a, uint32_t b, const Limits &lim,
+template <class SV>
+__device__ void walk_fixed_exact_wave(const SV &sv, uint32_t a, uint32_t b, const Limits &lim,
                                       MarkWriter<true> &mw, FwState &s) {
     const uint32_t lane = lane_id();
     for (uint32_t q0 = a; q0 < b; q0 += 64) {
@@ -996,8 +1069,8 @@ __device__ void walk_fixed_exact_wave(const SegView &sv, uint32_t a, uint32_t b,
 // reset packet (count 0, not counted) or the carried window (continuation). With
 // counts consecutive inside an epoch, the count trigger is at a closed-form
 // position; the window end and the blacklist end are searches.
-template <bool kWave>
-__device__ void walk_fixed_fast(const SegView &sv, uint32_t a, uint32_t b, const Limits &lim,
+template <bool kWave, class SV>
+__device__ void walk_fixed_fast(const SV &sv, uint32_t a, uint32_t b, const Limits &lim,
                                 uint32_t maxL, MarkWriter<kWave> &mw, FwState &s) {
     const uint64_t P = lim.pps, B = lim.bps, W = lim.window, BLK = lim.block;
     uint32_t p = a;
@@ -1076,47 +1149,50 @@ __device__ __forceinline__ bool fast_ok(const BatchState *bs, const Limits &lim)
 }
 
 // Short segments; long ones are queued for k_walk_fixed_long.
-__global__ __launch_bounds__(256) void k_walk_fixed(const uint64_t *__restrict__ S, BatchState *bs,
-                                                    const uint32_t *__restrict__ seg_start,
-                                                    const uint32_t *__restrict__ seg_slot,
-                                                    const uint64_t *__restrict__ ts,
-                                                    const uint32_t *__restrict__ len,
-                                                    uint8_t *__restrict__ marks, Slot *table,
-                                                    uint32_t *__restrict__ long_list, Limits lim) {
-    if (bs->err) return;
+template <class SV>
+__device__ __forceinline__ void walk_short(const SV &sv, BatchState *bs, const uint32_t *seg_start,
+                                           const uint32_t *seg_slot, uint8_t *marks, Slot *table,
+                                           uint32_t *long_list, const Limits &lim) {
     const uint32_t nseg = bs->nseg;
-    const SegView sv{S, ts, len};
-    uint32_t nlong = 0;
     for (uint32_t g = blockIdx.x * 256u + threadIdx.x; g < nseg; g += gridDim.x * 256u) {
         const uint32_t a = seg_start[g], b = seg_start[g + 1];
         if (b - a > kShortSeg) {
             long_list[atomicAdd(&bs->n_long, 1u)] = g;
             continue;
         }
-        const uint32_t s = seg_slot[g];
-        Slot &sl = table[s];
+        Slot &sl = table[seg_slot[g]];
         FwState st = load_state(sl);
         MarkWriter<false> mw{marks, 0};
         walk_fixed_exact_thread(sv, a, b, lim, mw, st);
         store_state(sl, st);
     }
-    (void)nlong;
 }
 
-__global__ __launch_bounds__(256) void k_walk_fixed_long(const uint64_t *__restrict__ S,
-                                                         BatchState *bs,
-                                                         const uint32_t *__restrict__ seg_start,
-                                                         const uint32_t *__restrict__ seg_slot,
-                                                         const uint64_t *__restrict__ ts,
-                                                         const uint32_t *__restrict__ len,
-                                                         uint8_t *__restrict__ marks, Slot *table,
-                                                         const uint32_t *__restrict__ long_list,
-                                                         Limits lim) {
+__global__ __launch_bounds__(256) void k_walk_fixed(const uint64_t *__restrict__ S, BatchState *bs,
+                                                    const uint32_t *__restrict__ seg_start,
+                                                    const uint32_t *__restrict__ seg_slot,
+                                                    const uint64_t *__restrict__ ts,
+                                                    const uint32_t *__restrict__ len,
+                                                    const uint64_t *__restrict__ pay,
+                                                    uint8_t *__restrict__ marks, Slot *table,
+                                                    uint32_t *__restrict__ long_list, Limits lim) {
     if (bs->err) return;
+    if (bs->pay_ok) {
+        const SegView<true> sv{S, ts, len, pay, ~bs->inv_min_ts};
+        walk_short(sv, bs, seg_start, seg_slot, marks, table, long_list, lim);
+    } else {
+        const SegView<false> sv{S, ts, len, pay, 0};
+        walk_short(sv, bs, seg_start, seg_slot, marks, table, long_list, lim);
+    }
+}
+
+template <class SV>
+__device__ __forceinline__ void walk_long(const SV &sv, BatchState *bs, const uint32_t *seg_start,
+                                          const uint32_t *seg_slot, uint8_t *marks, Slot *table,
+                                          const uint32_t *long_list, const Limits &lim) {
     const uint32_t nl = bs->n_long;
     const bool glob_fast = fast_ok(bs, lim);
     const uint32_t maxL = bs->max_len;
-    const SegView sv{S, ts, len};
     const uint32_t wave = blockIdx.x * 4u + (threadIdx.x >> 6);
     for (uint32_t i = wave; i < nl; i += gridDim.x * 4u) {
         const uint32_t g = long_list[i];
@@ -1129,6 +1205,26 @@ __global__ __launch_bounds__(256) void k_walk_fixed_long(const uint64_t *__restr
         if (fast) walk_fixed_fast<true>(sv, a, b, lim, maxL, mw, st);
         else walk_fixed_exact_wave(sv, a, b, lim, mw, st);
         if (lane_id() == 0) store_state(sl, st);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_walk_fixed_long(const uint64_t *__restrict__ S,
+                                                         BatchState *bs,
+                                                         const uint32_t *__restrict__ seg_start,
+                                                         const uint32_t *__restrict__ seg_slot,
+                                                         const uint64_t *__restrict__ ts,
+                                                         const uint32_t *__restrict__ len,
+                                                         const uint64_t *__restrict__ pay,
+                                                         uint8_t *__restrict__ marks, Slot *table,
+                                                         const uint32_t *__restrict__ long_list,
+                                                         Limits lim) {
+    if (bs->err) return;
+    if (bs->pay_ok) {
+        const SegView<true> sv{S, ts, len, pay, ~bs->inv_min_ts};
+        walk_long(sv, bs, seg_start, seg_slot, marks, table, long_list, lim);
+    } else {
+        const SegView<false> sv{S, ts, len, pay, 0};
+        walk_long(sv, bs, seg_start, seg_slot, marks, table, long_list, lim);
     }
 }
 
@@ -1336,7 +1432,8 @@ hipError_t launch_verdict_pipeline(const uint8_t *hdr, const uint32_t *len, cons
             const uint32_t *Ld = pass == 0 ? nullptr : &bs->n_valid;
             k_onesweep<<<ntiles, 256, 0, st>>>(in, out, n, Ld, shift, sc.gbase + 256 * pass, sc.status,
                                                sc.sort_ctl + 1024 + pass, gen0 + (uint32_t)pass,
-                                               pass == 0, bs);
+                                               pass == 0, bs, pass == 0 ? nullptr : sc.pay[pass & 1],
+                                               sc.pay[(pass + 1) & 1], ts, len);
             mark("k_onesweep");
         }
     }
@@ -1346,6 +1443,7 @@ hipError_t launch_verdict_pipeline(const uint8_t *hdr, const uint32_t *len, cons
     k_v6_mixed<<<gridStream, 256, 0, st>>>(S, bs, hdr, sc.fix_bitmap, sc.fix_list);
     k_fixup_short<<<256, 256, 0, st>>>(S, bs, hdr, sc.fix_list, lim.salt32);
     k_fixup_long<<<64, 256, 0, st>>>(S, sc.packed[1], bs, hdr, sc.fix_list, lim.salt32);
+    k_fixup_pay<<<64, 256, 0, st>>>(S, sc.pay[0], bs, sc.fix_list, ts, len);
     mark("v6_fixup");
     k_heads_count<<<gridTiles, 256, 0, st>>>(S, bs, hdr, sc.headf, sc.tile_aux, sc.sub_cnt);
     mark("k_heads_count");
@@ -1353,7 +1451,7 @@ hipError_t launch_verdict_pipeline(const uint8_t *hdr, const uint32_t *len, cons
     k_heads_write<<<gridTiles, 256, 0, st>>>(bs, sc.headf, sc.tile_aux, sc.seg_start);
     mark("k_heads_write");
     if (flows) {
-        launch_flows(S, bs, sc.headf, len, ts, hdr, sc.tile_aux, sc.sub_cnt, sc.seg_start,
+        launch_flows(S, sc.pay[0], bs, sc.headf, len, ts, hdr, sc.tile_aux, sc.sub_cnt, sc.seg_start,
                      sc.flow_first, sc.flow_last, sc.span_list, flows->keys16, flows->fam,
                      flows->feat, flows->prob, flows->dec, flows->cap, flows->score, lim.salt32, n, st);
         mark("k_flow_features");
@@ -1367,11 +1465,11 @@ hipError_t launch_verdict_pipeline(const uint8_t *hdr, const uint32_t *len, cons
     k_insert<<<gridStream, 256, 0, st>>>(S, bs, sc.seg_start, sc.seg_slot, hdr, table, tstate, lim);
     k_count_inserted<<<1, 1, 0, st>>>(bs, tstate);
     mark("k_insert");
-    k_walk_fixed<<<gridStream, 256, 0, st>>>(S, bs, sc.seg_start, sc.seg_slot, ts, len, sc.marks,
-                                             table, sc.long_list, lim);
+    k_walk_fixed<<<gridStream, 256, 0, st>>>(S, bs, sc.seg_start, sc.seg_slot, ts, len, sc.pay[0],
+                                             sc.marks, table, sc.long_list, lim);
     mark("k_walk_fixed");
-    k_walk_fixed_long<<<1024, 256, 0, st>>>(S, bs, sc.seg_start, sc.seg_slot, ts, len, sc.marks,
-                                            table, sc.long_list, lim);
+    k_walk_fixed_long<<<1024, 256, 0, st>>>(S, bs, sc.seg_start, sc.seg_slot, ts, len, sc.pay[0],
+                                            sc.marks, table, sc.long_list, lim);
     mark("k_walk_fixed_long");
     k_fill_last<<<gridTiles, 256, 0, st>>>(sc.marks, bs, sc.tile_last);
     k_fill_carry<<<1, 1024, 0, st>>>(sc.tile_last, bs);

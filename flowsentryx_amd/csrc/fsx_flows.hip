@@ -148,19 +148,22 @@ __device__ void flow_finish(uint32_t g, const FlowAcc &a, const uint64_t *S,
     }
 }
 
-__global__ __launch_bounds__(256) void k_flow_tile(const uint64_t *__restrict__ S, BatchState *bs,
-                                                   const uint8_t *__restrict__ headf,
-                                                   const uint32_t *__restrict__ len,
-                                                   const uint64_t *__restrict__ ts,
-                                                   const uint8_t *__restrict__ hdr,
-                                                   const uint32_t *__restrict__ tile_off,
-                                                   const uint32_t *__restrict__ sub_cnt,
-                                                   const uint32_t *__restrict__ seg_start,
-                                                   FlowAcc *__restrict__ firstp,
-                                                   FlowAcc *__restrict__ lastp,
-                                                   uint32_t *__restrict__ span_list, FlowOut out,
-                                                   ScoreParams P, uint32_t salt) {
-    __shared__ unsigned long long s_S[4][64 * 17];
+// kPay: (ts, len) of sorted positions come from the sort's payload words (relative
+// timestamps suffice: only differences are used); else gathered by arrival index.
+template <bool kPay>
+__device__ __forceinline__ void flow_tiles(const uint64_t *__restrict__ S,
+                                           const uint64_t *__restrict__ pay, BatchState *bs,
+                                           const uint8_t *__restrict__ headf,
+                                           const uint32_t *__restrict__ len,
+                                           const uint64_t *__restrict__ ts,
+                                           const uint8_t *__restrict__ hdr,
+                                           const uint32_t *__restrict__ tile_off,
+                                           const uint32_t *__restrict__ sub_cnt,
+                                           const uint32_t *__restrict__ seg_start,
+                                           FlowAcc *__restrict__ firstp, FlowAcc *__restrict__ lastp,
+                                           uint32_t *__restrict__ span_list, const FlowOut &out,
+                                           const ScoreParams &P, uint32_t salt,
+                                           unsigned long long (*s_S)[64 * 17]) {
     const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
     const uint32_t M = bs->n_valid;
     const uint32_t nsub = (M + kFT - 1) / kFT;
@@ -172,12 +175,14 @@ __global__ __launch_bounds__(256) void k_flow_tile(const uint64_t *__restrict__ 
         const uint32_t t4 = sub >> 2, j4 = sub & 3u;
         uint32_t hb = tile_off[t4];
         for (uint32_t j = 0; j < j4; ++j) hb += sub_cnt[t4 * 4 + j];
-        // stage the tile's sort words through LDS (coalesced load, 17-word row pitch)
+        // stage the tile's payload (or sort) words through LDS (coalesced load,
+        // 17-word row pitch)
+        const uint64_t *src = kPay ? pay : S;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const uint32_t e = (uint32_t)r * 64u + lane;
             const uint32_t p = base + e;
-            sS[(e >> 4) * 17u + (e & 15u)] = p < M ? S[p] : 0ull;
+            sS[(e >> 4) * 17u + (e & 15u)] = p < M ? src[p] : 0ull;
         }
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         uint64_t v[16];
@@ -196,12 +201,20 @@ __global__ __launch_bounds__(256) void k_flow_tile(const uint64_t *__restrict__ 
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
             const bool ok = p0 + k < M;
-            const uint32_t idx = pk_idx(v[k]);
-            L[k] = ok ? len[idx] : 0u;
-            T[k] = ok ? ts[idx] : 0ull;
+            if constexpr (kPay) {
+                L[k] = ok ? (uint32_t)v[k] & ((1u << kPayLenBits) - 1u) : 0u;
+                T[k] = ok ? v[k] >> kPayLenBits : 0ull;
+            } else {
+                const uint32_t idx = pk_idx(v[k]);
+                L[k] = ok ? len[idx] : 0u;
+                T[k] = ok ? ts[idx] : 0ull;
+            }
         }
         uint64_t tprev = __shfl_up(T[15], 1);
-        if (lane == 0) tprev = (p0 > 0 && p0 < M) ? ts[pk_idx(S[p0 - 1])] : 0ull;
+        if (lane == 0) {
+            if constexpr (kPay) tprev = (p0 > 0 && p0 < M) ? pay[p0 - 1] >> kPayLenBits : 0ull;
+            else tprev = (p0 > 0 && p0 < M) ? ts[pk_idx(S[p0 - 1])] : 0ull;
+        }
         // head flag of the position after this lane (end of array counts as a head)
         const uint32_t h_first = hf[0] & 1u;
         uint32_t next_head = __shfl_down(h_first, 1);
@@ -274,6 +287,28 @@ __global__ __launch_bounds__(256) void k_flow_tile(const uint64_t *__restrict__ 
     }
 }
 
+__global__ __launch_bounds__(256) void k_flow_tile(const uint64_t *__restrict__ S,
+                                                   const uint64_t *__restrict__ pay, BatchState *bs,
+                                                   const uint8_t *__restrict__ headf,
+                                                   const uint32_t *__restrict__ len,
+                                                   const uint64_t *__restrict__ ts,
+                                                   const uint8_t *__restrict__ hdr,
+                                                   const uint32_t *__restrict__ tile_off,
+                                                   const uint32_t *__restrict__ sub_cnt,
+                                                   const uint32_t *__restrict__ seg_start,
+                                                   FlowAcc *__restrict__ firstp,
+                                                   FlowAcc *__restrict__ lastp,
+                                                   uint32_t *__restrict__ span_list, FlowOut out,
+                                                   ScoreParams P, uint32_t salt) {
+    __shared__ unsigned long long s_S[4][64 * 17];
+    if (bs->pay_ok)
+        flow_tiles<true>(S, pay, bs, headf, len, ts, hdr, tile_off, sub_cnt, seg_start, firstp,
+                         lastp, span_list, out, P, salt, s_S);
+    else
+        flow_tiles<false>(S, pay, bs, headf, len, ts, hdr, tile_off, sub_cnt, seg_start, firstp,
+                          lastp, span_list, out, P, salt, s_S);
+}
+
 __global__ __launch_bounds__(256) void k_flow_combine(const uint64_t *__restrict__ S, BatchState *bs,
                                                       const uint32_t *__restrict__ seg_start,
                                                       const FlowAcc *__restrict__ firstp,
@@ -299,7 +334,7 @@ __global__ __launch_bounds__(256) void k_flow_combine(const uint64_t *__restrict
     }
 }
 
-hipError_t launch_flows(const uint64_t *S, BatchState *bs, const uint8_t *headf, const uint32_t *len,
+hipError_t launch_flows(const uint64_t *S, const uint64_t *pay, BatchState *bs, const uint8_t *headf, const uint32_t *len,
                         const uint64_t *ts, const uint8_t *hdr, const uint32_t *tile_off,
                         const uint32_t *sub_cnt, const uint32_t *seg_start, void *firstp, void *lastp,
                         uint32_t *span_list, uint8_t *keys16, uint8_t *fam, float *feat, float *prob,
@@ -308,7 +343,7 @@ hipError_t launch_flows(const uint64_t *S, BatchState *bs, const uint8_t *headf,
     const FlowOut out{keys16, fam, feat, prob, dec, cap};
     const uint32_t nsub = (n + kFT - 1) / kFT;
     const uint32_t grid = std::max<uint32_t>(1, std::min<uint32_t>(2048, (nsub + 3) / 4));
-    k_flow_tile<<<grid, 256, 0, st>>>(S, bs, headf, len, ts, hdr, tile_off, sub_cnt, seg_start,
+    k_flow_tile<<<grid, 256, 0, st>>>(S, pay, bs, headf, len, ts, hdr, tile_off, sub_cnt, seg_start,
                                       (FlowAcc *)firstp, (FlowAcc *)lastp, span_list, out, P, salt);
     k_flow_combine<<<256, 256, 0, st>>>(S, bs, seg_start, (const FlowAcc *)firstp,
                                         (const FlowAcc *)lastp, span_list, hdr, len, out, P, salt);

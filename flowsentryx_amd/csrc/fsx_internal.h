@@ -63,7 +63,16 @@ struct BatchState {
     uint64_t max_ts;
     uint64_t allowed;     // this batch
     uint64_t dropped;
+    uint64_t inv_min_ts;  // ~(smallest timestamp): max-reduced from 0
+    uint32_t pay_ok;      // sorted payload words valid (see kPayLenBits)
+    uint32_t pad_;
 };
+
+// Sorted payload word carried through the onesweep passes next to each sort word:
+// (ts - min_ts) << 24 | len. Valid when every ts is within 2^40 ns (~18 min) of the
+// batch minimum and every len < 2^24; otherwise consumers gather ts/len by index.
+constexpr uint32_t kPayLenBits = 24;
+constexpr uint64_t kPayTsRange = 1ull << (64 - kPayLenBits);
 
 // Persistent device scalars.
 struct TableState {
@@ -120,6 +129,7 @@ __host__ __device__ inline uint32_t pk_idx(uint64_t v) { return (uint32_t)v & 0x
 // ------------------------------------------------------------ launchers (fsx_device.hip)
 struct Scratch {
     uint64_t *packed[2];
+    uint64_t *pay[2];      // payload words in sort order (kPayLenBits)
     uint8_t *marks;        // per sorted position: 0 none, else verdict starting there
     uint8_t *headf;        // per sorted position: segment-head flag
     uint32_t *seg_start;   // nseg + 1
@@ -159,7 +169,7 @@ hipError_t launch_verdict_pipeline(const uint8_t *hdr, const uint32_t *len, cons
                                    bool do_limit, const FlowRequest *flows, hipStream_t st,
                                    hipEvent_t *ev, int nev, int *nev_used, const char **names);
 
-hipError_t launch_flows(const uint64_t *S, BatchState *bs, const uint8_t *headf, const uint32_t *len,
+hipError_t launch_flows(const uint64_t *S, const uint64_t *pay, BatchState *bs, const uint8_t *headf, const uint32_t *len,
                         const uint64_t *ts, const uint8_t *hdr, const uint32_t *tile_off,
                         const uint32_t *sub_cnt, const uint32_t *seg_start, void *firstp, void *lastp,
                         uint32_t *span_list, uint8_t *keys16, uint8_t *fam, float *feat, float *prob,

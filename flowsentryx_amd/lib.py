@@ -328,11 +328,11 @@ class FsxContext:
         return keys[:m], fam[:m], feat[:m]
 
     BATCH_INFO = ("ip_packets", "sources", "new_sources", "any_ipv6", "non_monotone",
-                  "max_len", "max_ts", "allowed", "dropped", "v6_fix_runs")
+                  "max_len", "max_ts", "allowed", "dropped", "v6_fix_runs", "sorted_payload")
 
     def last_batch_info(self) -> dict:
-        buf = (C.c_uint64 * 10)()
-        rc = self._lib.fsx_last_batch_info(self._h, buf, 10)
+        buf = (C.c_uint64 * len(self.BATCH_INFO))()
+        rc = self._lib.fsx_last_batch_info(self._h, buf, len(self.BATCH_INFO))
         if rc < 0:
             self._check(rc, "fsx_last_batch_info")
         return {k: int(buf[i]) for i, k in enumerate(self.BATCH_INFO[:rc])}

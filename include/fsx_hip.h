@@ -191,7 +191,9 @@ int fsx_flow_features(fsx_ctx *ctx, const uint8_t *hdr, const uint32_t *len,
 /* Facts about the last batch (after fsx_sync): info[0] IP packets, [1] distinct
  * source IPs, [2] sources new to the maps, [3] any IPv6, [4] non-monotone clock,
  * [5] max frame length, [6] max timestamp, [7] allowed, [8] dropped, [9] IPv6
- * hash-collision runs fixed. Returns the number of entries written. */
+ * hash-collision runs fixed, [10] 1 when (ts, len) travelled with the sort as payload
+ * words (timestamps within 2^40 ns of the batch minimum, frame lengths < 2^24), 0 when
+ * they were gathered by index. Returns the number of entries written. */
 int fsx_last_batch_info(fsx_ctx *ctx, uint64_t *info, int cap);
 
 /* Per-kernel device timing for the benchmark: while enabled, every batch records a

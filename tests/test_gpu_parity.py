@@ -365,3 +365,46 @@ def test_process_batch_device(native, oracle):
     assert np.array_equal(xg[order_g].view(np.uint32), xo[order_o].view(np.uint32))
     po, _, _ = oracle.score(ref, xo[order_o])
     assert np.array_equal(pg[order_g].view(np.uint32), po.view(np.uint32))
+
+
+# ------------------------------------------------------------------ payload fallback
+def _with_far_nonip(hdr, ln, ts, dt):
+    """Append one ARP frame dt ns after the last packet: it takes no part in the
+    limiter or the flows, but widens the batch's timestamp range."""
+    from flowsentryx_amd import synth
+    arp = synth.records([synth.frame_raw(0x0806, bytes(46), 60)])
+    return (np.concatenate([hdr, arp]), np.concatenate([ln, np.array([60], np.uint32)]),
+            np.concatenate([ts, np.array([int(ts[-1]) + dt], np.uint64)]))
+
+
+@pytest.mark.parametrize("dt,payload", [(1, 1), ((1 << 40) - 10**9, 1), (1 << 40, 0)])
+def test_sorted_payload_and_gather_paths(native, oracle, dt, payload):
+    """Both ways of reading (ts, len) in sorted order: payload words carried by the
+    sort (timestamps within 2^40 ns of the minimum) and the gather fallback."""
+    rng = np.random.default_rng(77)
+    hdr, ln, ts = rand_stream(rng, 40000, 400, dt_max=400, v6_frac=0.25, t0=10**12)
+    hdr, ln, ts = _with_far_nonip(hdr, ln, ts, dt)
+    for name in ("tight", "bytes_limit"):
+        o = oracle.Oracle(**{k: v for k, v in CFGS[name].items()}, max_entries=1 << 18)
+        with gpu_ctx(native, **CFGS[name]) as c:
+            vg = c.verdict_batch(hdr, ln, ts)
+            info = c.last_batch_info()
+            assert info["sorted_payload"] == payload
+            assert np.array_equal(vg, o.batch(hdr, ln, ts))
+            assert_same_state(c, o)
+    _check_flows(native, oracle, hdr, ln, ts)
+
+
+def test_gather_path_large_frame_len(native, oracle):
+    """A frame length >= 2^24 disables the payload words (len field is 24 bits)."""
+    rng = np.random.default_rng(78)
+    hdr, ln, ts = rand_stream(rng, 20000, 300, dt_max=400)
+    ln[100] = 1 << 24
+    for name in ("tight", "bytes_limit"):
+        o = oracle.Oracle(**CFGS[name], max_entries=1 << 18)
+        with gpu_ctx(native, **CFGS[name]) as c:
+            vg = c.verdict_batch(hdr, ln, ts)
+            assert c.last_batch_info()["sorted_payload"] == 0
+            assert np.array_equal(vg, o.batch(hdr, ln, ts))
+            assert_same_state(c, o)
+    _check_flows(native, oracle, hdr, ln, ts)
