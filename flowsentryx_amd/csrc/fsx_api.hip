@@ -49,6 +49,9 @@ struct fsx_ctx {
     float *d_prob = nullptr;
     uint8_t *d_dec = nullptr;
     uint64_t score_cap = 0;
+    // per-source flow accumulators
+    void *d_flow_acc = nullptr;
+    uint64_t flow_acc_cap = 0;
     // small device scratch for map ops
     int32_t *d_res = nullptr;
     uint64_t *d_val = nullptr;
@@ -102,7 +105,7 @@ static void free_scratch(fsx_ctx *c) {
     hipFree(s.packed[0]); hipFree(s.packed[1]); hipFree(s.pay[0]); hipFree(s.pay[1]); hipFree(s.marks); hipFree(s.headf);
     hipFree(s.seg_start); hipFree(s.seg_slot); hipFree(s.hist); hipFree(s.row_total);
     hipFree(s.tile_aux); hipFree(s.tile_last); hipFree(s.fix_list); hipFree(s.fix_bitmap);
-    hipFree(s.long_list); hipFree(s.sub_cnt); hipFree(s.flow_first); hipFree(s.flow_last);
+    hipFree(s.seg_order); hipFree(s.sub_cnt); hipFree(s.flow_first); hipFree(s.flow_last);
     hipFree(s.span_list); hipFree(s.sort_ctl); hipFree(s.gbase); hipFree(s.status);
     s = Scratch{};
 }
@@ -126,12 +129,12 @@ static int alloc_scratch(fsx_ctx *c, uint64_t cap) {
     HIPCHK(c, hipMalloc(&s.tile_last, ntiles));
     HIPCHK(c, hipMalloc(&s.fix_list, cap * 4));
     HIPCHK(c, hipMalloc(&s.fix_bitmap, (cap / 64 + 1) * 8));
-    HIPCHK(c, hipMalloc(&s.long_list, (cap / 64 + 1) * 4));
+    HIPCHK(c, hipMalloc(&s.seg_order, (cap + 1) * 4));
     HIPCHK(c, hipMalloc(&s.sub_cnt, (cap / 1024 + 8) * 4));
     HIPCHK(c, hipMalloc(&s.flow_first, (cap / 1024 + 8) * flow_acc_bytes()));
     HIPCHK(c, hipMalloc(&s.flow_last, (cap / 1024 + 8) * flow_acc_bytes()));
     HIPCHK(c, hipMalloc(&s.span_list, (cap / 1024 + 8) * 4));
-    HIPCHK(c, hipMalloc(&s.sort_ctl, 1028 * 4));
+    HIPCHK(c, hipMalloc(&s.sort_ctl, kSortCtlWords * 4));
     HIPCHK(c, hipMalloc(&s.gbase, 1024 * 4));
     HIPCHK(c, hipMalloc(&s.status, (cap / kSortTile + 2) * 256 * 8));
     HIPCHK(c, hipMemset(s.status, 0, (cap / kSortTile + 2) * 256 * 8));
@@ -173,7 +176,7 @@ void fsx_close(fsx_ctx *c) {
     free_scratch(c);
     hipFree(c->table); hipFree(c->tstate); hipFree(c->bs);
     hipFree(c->d_hdr); hipFree(c->d_len); hipFree(c->d_ts); hipFree(c->d_verdict);
-    hipFree(c->d_feat); hipFree(c->d_prob); hipFree(c->d_dec);
+    hipFree(c->d_feat); hipFree(c->d_prob); hipFree(c->d_dec); hipFree(c->d_flow_acc);
     hipFree(c->d_res); hipFree(c->d_val);
     for (int r = 0; r < kRing; ++r)
         for (int i = 0; i < kMaxEv; ++i) if (c->ev[r][i]) hipEventDestroy(c->ev[r][i]);
@@ -286,6 +289,21 @@ static int run_batch(fsx_ctx *c, const uint8_t *d_hdr, const uint32_t *d_len, co
     if (c->pending) { rc = fsx_sync(c); if (rc) return rc; }
     if (do_limit && c->cfg.limiter != FSX_LIMIT_FIXED_WINDOW)
         return set_err(c, -EOPNOTSUPP, "limiter %d not built into this pipeline yet", c->cfg.limiter);
+    FlowRequest frq;
+    if (fr) {
+        frq = *fr;
+        const uint64_t need = std::max<uint64_t>(1, std::min<uint64_t>(frq.cap, n));
+        if (need > c->flow_acc_cap) {
+            hipFree(c->d_flow_acc);
+            c->d_flow_acc = nullptr;
+            c->flow_acc_cap = 0;
+            HIPCHK(c, hipMalloc(&c->d_flow_acc, need * flow_acc_bytes()));
+            c->flow_acc_cap = need;
+        }
+        frq.acc = c->d_flow_acc;
+        frq.cap = (uint32_t)std::min<uint64_t>(frq.cap, c->flow_acc_cap);
+        fr = &frq;
+    }
     hipEvent_t *ev = nullptr;
     const char **names = nullptr;
     int *used = nullptr;

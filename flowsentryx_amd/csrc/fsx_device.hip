@@ -40,10 +40,10 @@ __global__ __launch_bounds__(256) void k_parse(const uint8_t *__restrict__ hdr,
     __shared__ uint32_t s_rec[4][64 * 17];
     __shared__ uint32_t s_red[4][3];
     __shared__ unsigned long long s_ts[4], s_its[4];
-    __shared__ uint32_t s_hist[4][256];  // the 4 radix digits of every sort key
+    __shared__ uint32_t s_hist[4][4][256];  // per wave: the 4 radix digits of every sort key
     const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
 #pragma unroll
-    for (int d = 0; d < 4; ++d) s_hist[d][threadIdx.x] = 0;
+    for (int d = 0; d < 16; ++d) (&s_hist[0][0][0])[d * 256 + threadIdx.x] = 0;
     __syncthreads();
     uint32_t *rec = s_rec[w];
     uint32_t any6 = 0, nonmono = 0, maxlen = 0;
@@ -102,18 +102,13 @@ __global__ __launch_bounds__(256) void k_parse(const uint8_t *__restrict__ hdr,
             maxts = T > maxts ? T : maxts;
             inv_mints = ~T > inv_mints ? ~T : inv_mints;
         }
-        // radix histograms of the 4 key digits: lanes with equal digits are matched by
-        // ballots and one leader adds the count (no same-address LDS atomics, which
-        // serialize on the heavy sources of skewed traffic)
-        if (ghist) {
-            const uint64_t act = __ballot(out != kSentinel);
+        // radix histograms of the 4 key digits: per-wave LDS counters (a heavy source
+        // repeats in few lanes of one 64-packet step, so same-address serialization
+        // stays short)
+        if (ghist && out != kSentinel) {
 #pragma unroll
-            for (int dg = 0; dg < 4; ++dg) {
-                const uint32_t d = (uint32_t)(out >> (32 + 8 * dg)) & 255u;
-                const uint64_t peers = match_digit(d, act);
-                if (out != kSentinel && (peers & ((1ull << lane) - 1ull)) == 0)
-                    atomicAdd(&s_hist[dg][d], (uint32_t)__popcll(peers));
-            }
+            for (int dg = 0; dg < 4; ++dg)
+                atomicAdd(&s_hist[w][dg][(uint32_t)(out >> (32 + 8 * dg)) & 255u], 1u);
         }
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     }
@@ -121,7 +116,8 @@ __global__ __launch_bounds__(256) void k_parse(const uint8_t *__restrict__ hdr,
         __syncthreads();
 #pragma unroll
         for (int dg = 0; dg < 4; ++dg) {
-            const uint32_t c = s_hist[dg][threadIdx.x];
+            const uint32_t c = s_hist[0][dg][threadIdx.x] + s_hist[1][dg][threadIdx.x] +
+                               s_hist[2][dg][threadIdx.x] + s_hist[3][dg][threadIdx.x];
             if (c) atomicAdd(&ghist[dg * 256 + threadIdx.x], c);
         }
     }
@@ -1148,18 +1144,104 @@ __device__ __forceinline__ bool fast_ok(const BatchState *bs, const Limits &lim)
            lim.block < kBig && bs->max_ts <= ~0ull - (lim.window > lim.block ? lim.window : lim.block);
 }
 
-// Short segments; long ones are queued for k_walk_fixed_long.
-template <class SV>
-__device__ __forceinline__ void walk_short(const SV &sv, BatchState *bs, const uint32_t *seg_start,
-                                           const uint32_t *seg_slot, uint8_t *marks, Slot *table,
-                                           uint32_t *long_list, const Limits &lim) {
-    const uint32_t nseg = bs->nseg;
-    for (uint32_t g = blockIdx.x * 256u + threadIdx.x; g < nseg; g += gridDim.x * 256u) {
-        const uint32_t a = seg_start[g], b = seg_start[g + 1];
-        if (b - a > kShortSeg) {
-            long_list[atomicAdd(&bs->n_long, 1u)] = g;
-            continue;
+// Segments are walked in order of length class (ceil log2 of the packet count), so
+// the lanes of a wave replay segments of similar length; the last class (longer
+// than kShortSeg) goes to k_walk_fixed_long, one wave per segment.
+__device__ __forceinline__ uint32_t seg_class(uint32_t L) {
+    if (L > kShortSeg) return kSegClasses - 1;
+    return L <= 1 ? 0u : 32u - (uint32_t)__clz((int)(L - 1));
+}
+
+// Counting sort of the segment ids by class: per-block counts over contiguous
+// chunks, one scan, then per-block LDS cursors (no contended global atomics; order
+// inside a class is irrelevant to the result).
+constexpr uint32_t kSegBlocks = 1024;
+
+__device__ __forceinline__ void seg_chunk(uint32_t nseg, uint32_t b, uint32_t &lo, uint32_t &hi) {
+    const uint32_t chunk = (nseg + kSegBlocks - 1) / kSegBlocks;
+    lo = min(nseg, b * chunk);
+    hi = min(nseg, lo + chunk);
+}
+
+template <bool kWrite>
+__device__ __forceinline__ void seg_classes_pass(const uint32_t *seg_start, uint32_t lo, uint32_t hi,
+                                                 uint32_t *sh, uint32_t *order) {
+    const uint32_t lane = lane_id();
+    const uint64_t lt = (1ull << lane) - 1ull;
+    for (uint32_t b = lo; b < hi; b += 256u) {
+        const uint32_t g = b + threadIdx.x;
+        const bool ok = g < hi;
+        const uint32_t c = ok ? seg_class(seg_start[g + 1] - seg_start[g]) : kSegClasses;
+#pragma unroll
+        for (uint32_t k = 0; k < kSegClasses; ++k) {
+            const uint64_t m = __ballot(c == k);
+            if (!m) continue;
+            uint32_t off = 0;
+            if (lane == 0) off = atomicAdd(&sh[k], (uint32_t)__popcll(m));
+            if constexpr (kWrite) {
+                off = __shfl(off, 0);
+                if (c == k) order[off + (uint32_t)__popcll(m & lt)] = g;
+            }
         }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_seg_count(const BatchState *bs,
+                                                   const uint32_t *__restrict__ seg_start,
+                                                   uint32_t *__restrict__ blk) {
+    __shared__ uint32_t sh[kSegClasses];
+    if (threadIdx.x < kSegClasses) sh[threadIdx.x] = 0;
+    __syncthreads();
+    uint32_t lo, hi;
+    seg_chunk(bs->nseg, blockIdx.x, lo, hi);
+    seg_classes_pass<false>(seg_start, lo, hi, sh, nullptr);
+    __syncthreads();
+    if (threadIdx.x < kSegClasses) blk[threadIdx.x * kSegBlocks + blockIdx.x] = sh[threadIdx.x];
+}
+
+// Exclusive scan of the class-major [class][block] counts; class totals to cls.
+__global__ __launch_bounds__(1024) void k_seg_scan(uint32_t *__restrict__ blk, uint32_t *cls) {
+    static_assert(kSegClasses * kSegBlocks == 16 * 1024, "one 16-entry run per thread");
+    __shared__ uint32_t s_w[16];
+    __shared__ uint32_t s_cls[kSegClasses];
+    const uint32_t t = threadIdx.x, lane = lane_id(), w = t >> 6;
+    if (t < kSegClasses) s_cls[t] = 0;
+    uint32_t v[16], sum = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) { v[k] = blk[t * 16 + k]; sum += v[k]; }
+    const uint32_t incl = wave_incl_sum(sum);
+    if (lane == 63) s_w[w] = incl;
+    __syncthreads();
+    uint32_t off = incl - sum;
+    for (uint32_t k = 0; k < w; ++k) off += s_w[k];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) { blk[t * 16 + k] = off; off += v[k]; }
+    if (sum) atomicAdd(&s_cls[(t * 16) / kSegBlocks], sum);
+    __syncthreads();
+    if (t < kSegClasses) cls[t] = s_cls[t];
+}
+
+__global__ __launch_bounds__(256) void k_seg_order(const BatchState *bs,
+                                                   const uint32_t *__restrict__ seg_start,
+                                                   const uint32_t *__restrict__ blk,
+                                                   uint32_t *__restrict__ order) {
+    __shared__ uint32_t cur[kSegClasses];
+    if (threadIdx.x < kSegClasses) cur[threadIdx.x] = blk[threadIdx.x * kSegBlocks + blockIdx.x];
+    __syncthreads();
+    uint32_t lo, hi;
+    seg_chunk(bs->nseg, blockIdx.x, lo, hi);
+    seg_classes_pass<true>(seg_start, lo, hi, cur, order);
+}
+
+template <class SV>
+__device__ __forceinline__ void walk_short(const SV &sv, const BatchState *bs,
+                                           const uint32_t *seg_start, const uint32_t *seg_slot,
+                                           const uint32_t *order, const uint32_t *cls,
+                                           uint8_t *marks, Slot *table, const Limits &lim) {
+    const uint32_t nshort = bs->nseg - cls[kSegClasses - 1];
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < nshort; i += gridDim.x * 256u) {
+        const uint32_t g = order[i];
+        const uint32_t a = seg_start[g], b = seg_start[g + 1];
         Slot &sl = table[seg_slot[g]];
         FwState st = load_state(sl);
         MarkWriter<false> mw{marks, 0};
@@ -1174,28 +1256,31 @@ __global__ __launch_bounds__(256) void k_walk_fixed(const uint64_t *__restrict__
                                                     const uint64_t *__restrict__ ts,
                                                     const uint32_t *__restrict__ len,
                                                     const uint64_t *__restrict__ pay,
+                                                    const uint32_t *__restrict__ order,
+                                                    const uint32_t *__restrict__ cls,
                                                     uint8_t *__restrict__ marks, Slot *table,
-                                                    uint32_t *__restrict__ long_list, Limits lim) {
+                                                    Limits lim) {
     if (bs->err) return;
     if (bs->pay_ok) {
         const SegView<true> sv{S, ts, len, pay, ~bs->inv_min_ts};
-        walk_short(sv, bs, seg_start, seg_slot, marks, table, long_list, lim);
+        walk_short(sv, bs, seg_start, seg_slot, order, cls, marks, table, lim);
     } else {
         const SegView<false> sv{S, ts, len, pay, 0};
-        walk_short(sv, bs, seg_start, seg_slot, marks, table, long_list, lim);
+        walk_short(sv, bs, seg_start, seg_slot, order, cls, marks, table, lim);
     }
 }
 
 template <class SV>
-__device__ __forceinline__ void walk_long(const SV &sv, BatchState *bs, const uint32_t *seg_start,
-                                          const uint32_t *seg_slot, uint8_t *marks, Slot *table,
-                                          const uint32_t *long_list, const Limits &lim) {
-    const uint32_t nl = bs->n_long;
+__device__ __forceinline__ void walk_long(const SV &sv, const BatchState *bs,
+                                          const uint32_t *seg_start, const uint32_t *seg_slot,
+                                          const uint32_t *order, const uint32_t *cls,
+                                          uint8_t *marks, Slot *table, const Limits &lim) {
+    const uint32_t nl = cls[kSegClasses - 1], first = bs->nseg - nl;
     const bool glob_fast = fast_ok(bs, lim);
     const uint32_t maxL = bs->max_len;
     const uint32_t wave = blockIdx.x * 4u + (threadIdx.x >> 6);
     for (uint32_t i = wave; i < nl; i += gridDim.x * 4u) {
-        const uint32_t g = long_list[i];
+        const uint32_t g = order[first + i];
         const uint32_t a = seg_start[g], b = seg_start[g + 1];
         Slot &sl = table[seg_slot[g]];
         FwState st = load_state(sl);
@@ -1215,16 +1300,17 @@ __global__ __launch_bounds__(256) void k_walk_fixed_long(const uint64_t *__restr
                                                          const uint64_t *__restrict__ ts,
                                                          const uint32_t *__restrict__ len,
                                                          const uint64_t *__restrict__ pay,
+                                                         const uint32_t *__restrict__ order,
+                                                         const uint32_t *__restrict__ cls,
                                                          uint8_t *__restrict__ marks, Slot *table,
-                                                         const uint32_t *__restrict__ long_list,
                                                          Limits lim) {
     if (bs->err) return;
     if (bs->pay_ok) {
         const SegView<true> sv{S, ts, len, pay, ~bs->inv_min_ts};
-        walk_long(sv, bs, seg_start, seg_slot, marks, table, long_list, lim);
+        walk_long(sv, bs, seg_start, seg_slot, order, cls, marks, table, lim);
     } else {
         const SegView<false> sv{S, ts, len, pay, 0};
-        walk_long(sv, bs, seg_start, seg_slot, marks, table, long_list, lim);
+        walk_long(sv, bs, seg_start, seg_slot, order, cls, marks, table, lim);
     }
 }
 
@@ -1401,7 +1487,7 @@ hipError_t launch_verdict_pipeline(const uint8_t *hdr, const uint32_t *len, cons
 
     // mark(name) closes the interval of the kernel just enqueued (per-kernel timing)
     const bool classic = (lim.test_flags & 2u) != 0;
-    if (!classic && (e = hipMemsetAsync(sc.sort_ctl, 0, 1028 * 4, st)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(sc.sort_ctl, 0, kSortCtlWords * 4, st)) != hipSuccess) return e;
     mark("start");
     k_parse<<<std::min<uint32_t>(2048, std::max<uint32_t>(1, cdiv(n, 256))), 256, 0, st>>>(
         hdr, len, ts, n, sc.packed[0], verdict, bs, lim.salt32, lim.seed,
@@ -1452,7 +1538,7 @@ hipError_t launch_verdict_pipeline(const uint8_t *hdr, const uint32_t *len, cons
     mark("k_heads_write");
     if (flows) {
         launch_flows(S, sc.pay[0], bs, sc.headf, len, ts, hdr, sc.tile_aux, sc.sub_cnt, sc.seg_start,
-                     sc.flow_first, sc.flow_last, sc.span_list, flows->keys16, flows->fam,
+                     sc.flow_first, sc.flow_last, sc.span_list, flows->acc, flows->keys16, flows->fam,
                      flows->feat, flows->prob, flows->dec, flows->cap, flows->score, lim.salt32, n, st);
         mark("k_flow_features");
     }
@@ -1465,11 +1551,16 @@ hipError_t launch_verdict_pipeline(const uint8_t *hdr, const uint32_t *len, cons
     k_insert<<<gridStream, 256, 0, st>>>(S, bs, sc.seg_start, sc.seg_slot, hdr, table, tstate, lim);
     k_count_inserted<<<1, 1, 0, st>>>(bs, tstate);
     mark("k_insert");
+    uint32_t *cls = sc.sort_ctl + 1028;
+    k_seg_count<<<kSegBlocks, 256, 0, st>>>(bs, sc.seg_start, sc.hist);
+    k_seg_scan<<<1, 1024, 0, st>>>(sc.hist, cls);
+    k_seg_order<<<kSegBlocks, 256, 0, st>>>(bs, sc.seg_start, sc.hist, sc.seg_order);
+    mark("k_seg_order");
     k_walk_fixed<<<gridStream, 256, 0, st>>>(S, bs, sc.seg_start, sc.seg_slot, ts, len, sc.pay[0],
-                                             sc.marks, table, sc.long_list, lim);
+                                             sc.seg_order, cls, sc.marks, table, lim);
     mark("k_walk_fixed");
     k_walk_fixed_long<<<1024, 256, 0, st>>>(S, bs, sc.seg_start, sc.seg_slot, ts, len, sc.pay[0],
-                                            sc.marks, table, sc.long_list, lim);
+                                            sc.seg_order, cls, sc.marks, table, lim);
     mark("k_walk_fixed_long");
     k_fill_last<<<gridTiles, 256, 0, st>>>(sc.marks, bs, sc.tile_last);
     k_fill_carry<<<1, 1024, 0, st>>>(sc.tile_last, bs);

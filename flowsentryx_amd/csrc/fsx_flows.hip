@@ -72,6 +72,7 @@ __device__ __forceinline__ FlowAcc wave_sum_acc(FlowAcc a) {
 }
 
 struct FlowOut {
+    FlowAcc *acc;  // per source: exact sums (finished by k_flow_finish)
     uint8_t *keys16;
     uint8_t *fam;
     float *feat;   // may be null
@@ -98,6 +99,10 @@ __device__ __forceinline__ uint32_t dst_port(const uint8_t *f, uint32_t len) {
     if (l4 != 6 && l4 != 17) return 0;
     if (off + 4 > len || off + 4 > 64) return 0;
     return ((uint32_t)f[off + 2] << 8) | f[off + 3];
+}
+
+__device__ __forceinline__ void acc_store(const FlowOut &out, uint32_t g, const FlowAcc &a) {
+    if (g < out.cap) out.acc[g] = a;
 }
 
 // Features of source g from its exact sums, then the q8 score.
@@ -233,7 +238,7 @@ __device__ __forceinline__ void flow_tiles(const uint64_t *__restrict__ S,
                 const bool h = (hf[k >> 2] >> (8 * (k & 3))) & 1u;
                 if (h) {
                     if (seen == 0) F = A;
-                    else flow_finish(g + seen - 1, A, S, seg_start, hdr, len, salt, out, P);
+                    else acc_store(out, g + seen - 1, A);
                     ++seen;
                     A = acc_zero();
                 }
@@ -267,7 +272,7 @@ __device__ __forceinline__ void flow_tiles(const uint64_t *__restrict__ S,
         if (nh > 0 && p0 > 0) {
             FlowAcc tot = in;
             acc_add(tot, F);
-            if (in_fl) flow_finish(g - 1, tot, S, seg_start, hdr, len, salt, out, P);
+            if (in_fl) acc_store(out, g - 1, tot);
             else firstp[sub] = tot;   // started in an earlier tile
         }
         // ... and the source open at the lane end finishes here if the next packet
@@ -275,7 +280,7 @@ __device__ __forceinline__ void flow_tiles(const uint64_t *__restrict__ S,
         if (lane == 63) {
             const uint32_t g_last = hb + hoff + nh - 1;
             if (fl) {
-                if (next_head) flow_finish(g_last, val, S, seg_start, hdr, len, salt, out, P);
+                if (next_head) acc_store(out, g_last, val);
                 else {
                     lastp[sub] = val;
                     span_list[atomicAdd(&bs->n_span, 1u)] = g_last;
@@ -329,24 +334,38 @@ __global__ __launch_bounds__(256) void k_flow_combine(const uint64_t *__restrict
         if (lane == 0) {
             FlowAcc tot = lastp[t0];
             acc_add(tot, a);
-            flow_finish(g, tot, S, seg_start, hdr, len, salt, out, P);
+            acc_store(out, g, tot);
         }
     }
+}
+
+// One thread per source: features from the exact sums, then the q8 score (kept out
+// of the tile loop, where a source's end lands on arbitrary lanes).
+__global__ __launch_bounds__(256) void k_flow_finish(const uint64_t *__restrict__ S, BatchState *bs,
+                                                     const uint32_t *__restrict__ seg_start,
+                                                     const uint8_t *__restrict__ hdr,
+                                                     const uint32_t *__restrict__ len, FlowOut out,
+                                                     ScoreParams P, uint32_t salt) {
+    const uint32_t ns = min(bs->nseg, out.cap);
+    for (uint32_t g = blockIdx.x * 256u + threadIdx.x; g < ns; g += gridDim.x * 256u)
+        flow_finish(g, out.acc[g], S, seg_start, hdr, len, salt, out, P);
 }
 
 hipError_t launch_flows(const uint64_t *S, const uint64_t *pay, BatchState *bs, const uint8_t *headf, const uint32_t *len,
                         const uint64_t *ts, const uint8_t *hdr, const uint32_t *tile_off,
                         const uint32_t *sub_cnt, const uint32_t *seg_start, void *firstp, void *lastp,
-                        uint32_t *span_list, uint8_t *keys16, uint8_t *fam, float *feat, float *prob,
-                        uint8_t *dec, uint32_t cap, const ScoreParams &P, uint32_t salt, uint32_t n,
-                        hipStream_t st) {
-    const FlowOut out{keys16, fam, feat, prob, dec, cap};
+                        uint32_t *span_list, void *acc, uint8_t *keys16, uint8_t *fam, float *feat,
+                        float *prob, uint8_t *dec, uint32_t cap, const ScoreParams &P, uint32_t salt,
+                        uint32_t n, hipStream_t st) {
+    const FlowOut out{(FlowAcc *)acc, keys16, fam, feat, prob, dec, cap};
     const uint32_t nsub = (n + kFT - 1) / kFT;
     const uint32_t grid = std::max<uint32_t>(1, std::min<uint32_t>(2048, (nsub + 3) / 4));
     k_flow_tile<<<grid, 256, 0, st>>>(S, pay, bs, headf, len, ts, hdr, tile_off, sub_cnt, seg_start,
                                       (FlowAcc *)firstp, (FlowAcc *)lastp, span_list, out, P, salt);
     k_flow_combine<<<256, 256, 0, st>>>(S, bs, seg_start, (const FlowAcc *)firstp,
                                         (const FlowAcc *)lastp, span_list, hdr, len, out, P, salt);
+    const uint32_t gf = std::max<uint32_t>(1, std::min<uint32_t>(4096, (std::min(n, cap) + 255) / 256));
+    k_flow_finish<<<gf, 256, 0, st>>>(S, bs, seg_start, hdr, len, out, P, salt);
     return hipGetLastError();
 }
 

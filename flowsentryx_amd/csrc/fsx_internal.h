@@ -72,6 +72,8 @@ struct BatchState {
 // (ts - min_ts) << 24 | len. Valid when every ts is within 2^40 ns (~18 min) of the
 // batch minimum and every len < 2^24; otherwise consumers gather ts/len by index.
 constexpr uint32_t kPayLenBits = 24;
+constexpr uint32_t kSegClasses = 16;  // walker length classes (last: wave-walked segments)
+constexpr uint32_t kSortCtlWords = 1028 + 2 * kSegClasses;
 constexpr uint64_t kPayTsRange = 1ull << (64 - kPayLenBits);
 
 // Persistent device scalars.
@@ -140,12 +142,13 @@ struct Scratch {
     uint8_t *tile_last;
     uint32_t *fix_list;
     uint64_t *fix_bitmap;  // one bit per sorted position
-    uint32_t *long_list;   // segments walked by a wave
+    uint32_t *seg_order;   // segment ids grouped by length class (walker load balance)
     uint32_t *sub_cnt;     // heads per 1024-position flow tile
     void *flow_first;      // FlowAcc per flow tile (fsx_flows.hip)
     void *flow_last;
     uint32_t *span_list;
-    uint32_t *sort_ctl;    // [0,1024) digit histograms of the 4 passes, [1024,1028) tile counters
+    uint32_t *sort_ctl;    // [0,1024) digit histograms of the 4 passes, [1024,1028) tile
+                           // counters, [1028,1028+2*kSegClasses) segment class counts, cursors
     uint32_t *gbase;       // 4 x 256 digit bases
     unsigned long long *status;  // onesweep look-back words, 256 per tile
     uint64_t cap;          // packets the scratch is sized for
@@ -160,6 +163,7 @@ struct FlowRequest {
     uint8_t *dec;
     uint32_t cap;
     ScoreParams score;
+    void *acc;        // cap x FlowAcc scratch (owned by the context)
 };
 
 // do_limit: run the rate limiter (verdicts + maps); flows: also per-source features.
@@ -172,9 +176,9 @@ hipError_t launch_verdict_pipeline(const uint8_t *hdr, const uint32_t *len, cons
 hipError_t launch_flows(const uint64_t *S, const uint64_t *pay, BatchState *bs, const uint8_t *headf, const uint32_t *len,
                         const uint64_t *ts, const uint8_t *hdr, const uint32_t *tile_off,
                         const uint32_t *sub_cnt, const uint32_t *seg_start, void *firstp, void *lastp,
-                        uint32_t *span_list, uint8_t *keys16, uint8_t *fam, float *feat, float *prob,
-                        uint8_t *dec, uint32_t cap, const ScoreParams &P, uint32_t salt, uint32_t n,
-                        hipStream_t st);
+                        uint32_t *span_list, void *acc, uint8_t *keys16, uint8_t *fam, float *feat,
+                        float *prob, uint8_t *dec, uint32_t cap, const ScoreParams &P, uint32_t salt,
+                        uint32_t n, hipStream_t st);
 size_t flow_acc_bytes();
 ScoreParams make_score_params(const int8_t w[8], float inv_in, int32_t zp_in, float bias_over_ats,
                               float mult, int32_t zp_out, const uint8_t lut[256]);
