@@ -24,6 +24,20 @@
 #define XDP_DROP 1
 #define XDP_PASS 2
 
+// Phase timestamps for the standalone micro-benchmarks (scripts/micro/): compiled in
+// only when the including translation unit defines FSX_MICRO_STAMPS.
+#ifdef FSX_MICRO_STAMPS
+__device__ unsigned long long *g_fsx_stamps;
+#define FSX_STAMP(tile, k)                                                                 \
+    do {                                                                                   \
+        if (threadIdx.x == 0) g_fsx_stamps[(size_t)(tile) * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+#else
+#define FSX_STAMP(tile, k) \
+    do {                   \
+    } while (0)
+#endif
+
 namespace fsx {
 
 // ------------------------------------------------------------------ parse
@@ -49,27 +63,53 @@ __global__ __launch_bounds__(256) void k_parse(const uint8_t *__restrict__ hdr,
     uint32_t any6 = 0, nonmono = 0, maxlen = 0;
     uint64_t maxts = 0, inv_mints = 0;  // ~min ts, max-reduced
     const uint32_t ntiles = (n + 63u) >> 6;
-    for (uint32_t t = blockIdx.x * 4u + w; t < ntiles; t += gridDim.x * 4u) {
-        const uint32_t base = t << 6;
+    const uint32_t stride = gridDim.x * 4u;
+    // software pipeline: the next tile's loads are in flight while this one is parsed
+    auto load = [&](uint32_t tt, uint4 (&h)[4], uint32_t &L_, uint64_t &T_, uint64_t &P_) {
+        const uint32_t base = tt << 6;
         const uint8_t *src = hdr + (size_t)base * 64;
+        const bool tv = tt < ntiles;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t g = (uint32_t)k * 1024u + lane * 16u;
+            h[k] = make_uint4(0, 0, 0, 0);
+            if (tv && base + (g >> 6) < n) h[k] = *reinterpret_cast<const uint4 *>(src + g);
+        }
+        const uint32_t i = base + lane;
+        const bool live = tv && i < n;
+        L_ = live ? len[i] : 0u;
+        T_ = live ? ts[i] : 0ull;
+        P_ = (lane == 0 && live && i > 0) ? ts[i - 1] : 0ull;
+    };
+    uint4 hv[4];
+    uint32_t Lc;
+    uint64_t Tc, Pc;
+    load(blockIdx.x * 4u + w, hv, Lc, Tc, Pc);
+    for (uint32_t t = blockIdx.x * 4u + w; t < ntiles; t += stride) {
+        uint4 hn[4];
+        uint32_t Ln;
+        uint64_t Tn, Pn;
+        load(t + stride, hn, Ln, Tn, Pn);
+        const uint32_t base = t << 6;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const uint32_t g = (uint32_t)k * 1024u + lane * 16u;
             const uint32_t r = g >> 6, off = (g & 63u) >> 2;
-            uint4 v = make_uint4(0, 0, 0, 0);
-            if (base + r < n) v = *reinterpret_cast<const uint4 *>(src + g);
             uint32_t *d = rec + r * 17u + off;
-            d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+            d[0] = hv[k].x; d[1] = hv[k].y; d[2] = hv[k].z; d[3] = hv[k].w;
         }
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         const uint32_t i = base + lane;
         const bool live = i < n;
         const uint32_t *my = rec + lane * 17u;
         const uint32_t d3 = my[3], d5 = my[5], d6 = my[6], d7 = my[7], d8 = my[8], d9 = my[9];
-        const uint32_t L = live ? len[i] : 0u;
-        const uint64_t T = live ? ts[i] : 0ull;
+        const uint32_t L = Lc;
+        const uint64_t T = Tc;
         uint64_t prev = __shfl_up(T, 1);
-        if (lane == 0) prev = (live && i > 0) ? ts[i - 1] : T;
+        if (lane == 0) prev = (live && i > 0) ? Pc : T;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) hv[k] = hn[k];
+        Lc = Ln; Tc = Tn; Pc = Pn;
         uint64_t out = kSentinel;
         if (live) {
             // parse_ethhdr (14-byte bound; raw h_proto, no VLAN)
@@ -149,165 +189,21 @@ __global__ __launch_bounds__(256) void k_parse(const uint8_t *__restrict__ hdr,
 }
 
 // ------------------------------------------------------------------ radix sort
-// Block b of G owns the contiguous range [b*chunk, min(L,(b+1)*chunk)); a pass is
-// hist (per-block digit counts) -> rowscan (per-digit exclusive scan over blocks)
-// -> scatter (stable in-tile ranking by wave ballots, LDS-sorted tile, coalesced
-// runs to the digit buckets). Pass 0 also drops the non-IP sentinels.
-__device__ __forceinline__ void block_range(uint32_t L, uint32_t G, uint32_t b, uint32_t &beg,
-                                            uint32_t &end) {
-    const uint32_t chunk = (L + G - 1) / G;
-    beg = min(L, b * chunk);
-    end = min(L, beg + chunk);
-}
-
-__global__ __launch_bounds__(256) void k_sort_hist(const uint64_t *__restrict__ in, uint32_t L_host,
-                                                   const uint32_t *L_dev, uint32_t shift,
-                                                   uint32_t *__restrict__ hist, uint32_t G,
-                                                   int first, BatchState *bs) {
-    __shared__ uint32_t sh[4][256];
-    __shared__ uint32_t s_tmp[4];
-    const uint32_t tid = threadIdx.x, w = tid >> 6;
-    for (int k = 0; k < 4; ++k) sh[k][tid] = 0;
-    __syncthreads();
-    const uint32_t L = L_dev ? *L_dev : L_host;
-    uint32_t beg, end;
-    block_range(L, G, blockIdx.x, beg, end);
-    for (uint32_t t0 = beg; t0 < end; t0 += kSortTile) {
-        uint64_t v[kSortItems];  // all loads of the tile in flight before counting
-#pragma unroll
-        for (int r = 0; r < kSortItems; ++r) {
-            const uint32_t i = t0 + (uint32_t)r * 256u + tid;
-            v[r] = i < end ? in[i] : kSentinel;
-        }
-#pragma unroll
-        for (int r = 0; r < kSortItems; ++r) {
-            const uint32_t i = t0 + (uint32_t)r * 256u + tid;
-            if (i < end && !(first && v[r] == kSentinel))
-                atomicAdd(&sh[w][(uint32_t)(v[r] >> shift) & 255u], 1u);
-        }
-    }
-    __syncthreads();
-    const uint32_t c = sh[0][tid] + sh[1][tid] + sh[2][tid] + sh[3][tid];
-    hist[tid * G + blockIdx.x] = c;
-    if (first) {
-        uint32_t tot;
-        block256_excl(c, s_tmp, &tot);
-        if (tid == 0 && tot) atomicAdd(&bs->n_valid, tot);
-    }
-}
-
-// One block per digit: exclusive scan of that digit's row over the G blocks.
-__global__ __launch_bounds__(256) void k_sort_rowscan(uint32_t *__restrict__ hist, uint32_t G,
-                                                      uint32_t *__restrict__ row_total) {
-    __shared__ uint32_t s_tmp[4];
-    uint32_t *row = hist + (size_t)blockIdx.x * G;
-    const uint32_t per = (G + 255) / 256;
-    const uint32_t b0 = threadIdx.x * per;
-    uint32_t loc[8];
-    uint32_t s = 0;
-    for (uint32_t k = 0; k < per && k < 8; ++k) {
-        const uint32_t j = b0 + k;
-        loc[k] = j < G ? row[j] : 0u;
-        s += loc[k];
-    }
-    uint32_t tot;
-    uint32_t off = block256_excl(s, s_tmp, &tot);
-    for (uint32_t k = 0; k < per && k < 8; ++k) {
-        const uint32_t j = b0 + k;
-        if (j < G) row[j] = off;
-        off += loc[k];
-    }
-    if (threadIdx.x == 0) row_total[blockIdx.x] = tot;
-}
-
-__global__ __launch_bounds__(256) void k_sort_scatter(const uint64_t *__restrict__ in,
-                                                      uint64_t *__restrict__ out,
-                                                      uint32_t L_host, const uint32_t *L_dev,
-                                                      uint32_t shift,
-                                                      const uint32_t *__restrict__ hist,
-                                                      const uint32_t *__restrict__ row_total,
-                                                      uint32_t G, int first) {
-    __shared__ unsigned long long s_el[kSortTile];
-    __shared__ uint32_t s_wc[4][256];
-    __shared__ uint32_t s_base[256], s_tbase[256], s_tcnt[256];
-    __shared__ uint32_t s_tmp[4];
-    const uint32_t tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
-    const uint32_t L = L_dev ? *L_dev : L_host;
-    uint32_t beg, end;
-    block_range(L, G, blockIdx.x, beg, end);
-    {
-        const uint32_t rt = row_total[tid];
-        const uint32_t dbase = block256_excl(rt, s_tmp, nullptr);
-        s_base[tid] = dbase + hist[tid * G + blockIdx.x];
-    }
-    const uint64_t lt_mask = (1ull << lane) - 1ull;
-    for (uint32_t t0 = beg; t0 < end; t0 += kSortTile) {
-        uint64_t v[kSortItems];
-        uint32_t lr[kSortItems];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) s_wc[w][lane * 4 + k] = 0;
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-#pragma unroll
-        for (int r = 0; r < kSortItems; ++r) {
-            const uint32_t i = t0 + w * 1024u + (uint32_t)r * 64u + lane;
-            v[r] = i < end ? in[i] : kSentinel;
-        }
-#pragma unroll
-        for (int r = 0; r < kSortItems; ++r) {
-            const uint32_t i = t0 + w * 1024u + (uint32_t)r * 64u + lane;
-            const bool valid = i < end && !(first && v[r] == kSentinel);
-            const uint64_t act = __ballot(valid);
-            const uint32_t d = (uint32_t)(v[r] >> shift) & 255u;
-            const uint64_t peers = match_digit(d, act);
-            const uint32_t below = (uint32_t)__popcll(peers & lt_mask);
-            uint32_t base = 0;
-            if (valid) base = s_wc[w][d];
-            lr[r] = valid ? base + below : 0xFFFFFFFFu;
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-            if (valid && below == 0) s_wc[w][d] = base + (uint32_t)__popcll(peers);
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        }
-        __syncthreads();
-        {
-            const uint32_t d = tid;
-            const uint32_t c0 = s_wc[0][d], c1 = s_wc[1][d], c2 = s_wc[2][d], c3 = s_wc[3][d];
-            const uint32_t tc = c0 + c1 + c2 + c3;
-            __syncthreads();
-            s_wc[0][d] = 0; s_wc[1][d] = c0; s_wc[2][d] = c0 + c1; s_wc[3][d] = c0 + c1 + c2;
-            s_tcnt[d] = tc;
-            s_tbase[d] = block256_excl(tc, s_tmp, nullptr);
-        }
-        __syncthreads();
-#pragma unroll
-        for (int r = 0; r < kSortItems; ++r) {
-            if (lr[r] != 0xFFFFFFFFu) {
-                const uint32_t d = (uint32_t)(v[r] >> shift) & 255u;
-                s_el[s_tbase[d] + s_wc[w][d] + lr[r]] = v[r];
-            }
-        }
-        __syncthreads();
-        const uint32_t T = s_tbase[255] + s_tcnt[255];
-        for (uint32_t j = tid; j < T; j += 256) {
-            const uint64_t x = s_el[j];
-            const uint32_t d = (uint32_t)(x >> shift) & 255u;
-            out[s_base[d] + (j - s_tbase[d])] = x;
-        }
-        __syncthreads();
-        s_base[tid] += s_tcnt[tid];
-        __syncthreads();
-    }
-}
-
-// ------------------------------------------------------------------ onesweep radix sort
-// One kernel per 8-bit digit (Merrill & Garland's single-pass "Onesweep" structure):
-// the digit histograms of all four passes come from k_parse; each tile ranks its
-// 4096 keys stably in LDS (wave-ballot matching, as k_sort_scatter), publishes its
-// per-digit count, and learns its exclusive prefix by decoupled look-back over the
-// preceding tiles. Status words are 8-byte {generation, inclusive?, count} granules
-// written with one agent-scope store and polled with agent-scope loads (no fences:
-// the data is the flag). Tiles take ids from an atomic counter, so a tile only ever
-// waits on tiles whose blocks already started. Traffic per pass: 8 B in + 8 B out
-// per key + 2 KiB of status per 4096-key tile.
+// LSD radix sort of the sort words on their 32-bit key: 4 passes of 8 bits, the
+// payload words (kPayLenBits) following the same permutation. Per pass the keys are
+// cut into 4096-key tiles:
+//   k_tile_hist     per-tile digit counts, digit-major [256][tiles]
+//   k_tile_scan     per digit: exclusive scan over the tiles plus the digit's global
+//                   base (exclusive scan of the k_parse histogram of that digit)
+//   k_tile_scatter  stable in-tile ranking (wave-ballot matching), LDS-sorted tile,
+//                   runs written to the digit buckets: keys, then payload words
+// Pass 0 reads the parse output in arrival order: it drops the non-IP sentinels and
+// builds the payload words from (ts, len).
+//
+// The single-pass "onesweep" variant (decoupled look-back instead of k_tile_hist /
+// k_tile_scan) is kept for A/B runs behind FSX_FLAG_ONESWEEP_SORT: on MI355X its
+// look-back polls must bypass the per-XCD L2s, and a tile waited ~11 us in it
+// (scripts/micro/sort_micro.hip), more than the extra key read of k_tile_hist costs.
 
 // n_valid and the per-pass digit bases (exclusive scans of the k_parse histograms).
 __global__ __launch_bounds__(256) void k_hist_prep(const uint32_t *__restrict__ ghist,
@@ -324,36 +220,89 @@ __global__ __launch_bounds__(256) void k_hist_prep(const uint32_t *__restrict__ 
         bs->pay_ok = bs->max_len < (1u << kPayLenBits) && bs->max_ts - ~bs->inv_min_ts < kPayTsRange;
 }
 
-constexpr uint32_t kSpinLimit = 1u << 22;
-
-__device__ __forceinline__ unsigned long long os_word(uint32_t gen, bool inclusive, uint32_t cnt) {
-    return ((unsigned long long)gen << 33) | ((unsigned long long)(inclusive ? 1u : 0u) << 32) | cnt;
+__device__ __forceinline__ bool sort_item(uint32_t i, uint32_t end, int first, uint64_t v) {
+    return i < end && !(first && v == kSentinel);
 }
 
-__global__ __launch_bounds__(256) void k_onesweep(const uint64_t *__restrict__ in,
-                                                  uint64_t *__restrict__ out, uint32_t L_host,
-                                                  const uint32_t *L_dev, uint32_t shift,
-                                                  const uint32_t *__restrict__ gbase,
-                                                  unsigned long long *status, uint32_t *tile_ctr,
-                                                  uint32_t gen, int first, BatchState *bs,
-                                                  const uint64_t *__restrict__ pin,
-                                                  uint64_t *__restrict__ pout,
-                                                  const uint64_t *__restrict__ ts,
-                                                  const uint32_t *__restrict__ len) {
+// Per-tile digit counts (one block per tile; per-wave LDS counters).
+__global__ __launch_bounds__(256) void k_tile_hist(const uint64_t *__restrict__ in, uint32_t L_host,
+                                                   const uint32_t *L_dev, uint32_t shift, int first,
+                                                   uint32_t *__restrict__ thist, uint32_t tcap) {
+    __shared__ uint32_t sh[4][256];
+    const uint32_t tid = threadIdx.x, w = tid >> 6;
+    const uint32_t L = L_dev ? *L_dev : L_host;
+    const uint32_t t = blockIdx.x;
+    if (t * kSortTile >= L) return;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) sh[k][tid] = 0;
+    __syncthreads();
+    const uint32_t t0 = t * kSortTile, end = min(L, t0 + kSortTile);
+    uint64_t v[kSortItems];
+#pragma unroll
+    for (int r = 0; r < kSortItems; ++r) {
+        const uint32_t i = t0 + (uint32_t)r * 256u + tid;
+        v[r] = i < end ? in[i] : kSentinel;
+    }
+    const uint32_t lane = lane_id();
+#pragma unroll
+    for (int r = 0; r < kSortItems; ++r) {
+        const uint32_t i = t0 + (uint32_t)r * 256u + tid;
+        const bool ok = sort_item(i, end, first, v[r]);
+        const uint32_t d = (uint32_t)(v[r] >> shift) & 255u;
+        const uint64_t act = __ballot(ok);
+        if (!act) continue;
+        // runs of one heavy source make whole waves share a digit: one add for them
+        const int lead = __ffsll((unsigned long long)act) - 1;
+        const uint32_t dl = __shfl(d, lead);
+        if (__ballot(ok && d == dl) == act) {
+            if ((int)lane == lead) atomicAdd(&sh[w][dl], (uint32_t)__popcll(act));
+        } else if (ok) {
+            atomicAdd(&sh[w][d], 1u);
+        }
+    }
+    __syncthreads();
+    thist[(size_t)tid * tcap + t] = sh[0][tid] + sh[1][tid] + sh[2][tid] + sh[3][tid];
+}
+
+// Block d: offs[d][t] = base[d] + sum of thist[d][t'] over t' < t (in place); each
+// thread owns one contiguous run of tiles.
+__global__ __launch_bounds__(256) void k_tile_scan(uint32_t *__restrict__ thist, uint32_t tcap,
+                                                   uint32_t L_host, const uint32_t *L_dev,
+                                                   const uint32_t *__restrict__ gbase) {
+    __shared__ uint32_t s_tmp[4];
+    const uint32_t L = L_dev ? *L_dev : L_host;
+    const uint32_t ntiles = (L + kSortTile - 1) / kSortTile;
+    uint32_t *row = thist + (size_t)blockIdx.x * tcap;
+    const uint32_t per = (ntiles + 255) / 256;
+    const uint32_t j0 = min(ntiles, threadIdx.x * per), j1 = min(ntiles, j0 + per);
+    uint32_t sum = 0;
+    for (uint32_t j = j0; j < j1; ++j) sum += row[j];
+    uint32_t off = gbase[blockIdx.x] + block256_excl(sum, s_tmp, nullptr);
+    for (uint32_t j = j0; j < j1; ++j) {
+        const uint32_t x = row[j];
+        row[j] = off;
+        off += x;
+    }
+}
+
+// One tile: stable rank, global bases from offs(d, tile count of d), LDS-sorted
+// tile, runs to the buckets; payload words through the same LDS slots.
+template <bool kLatePay, class Offs>
+__device__ __forceinline__ void sort_tile(uint32_t t, const uint64_t *__restrict__ in,
+                                          uint64_t *__restrict__ out, uint32_t L, uint32_t shift,
+                                          int first, const BatchState *bs,
+                                          const uint64_t *__restrict__ pin, uint64_t *__restrict__ pout,
+                                          const uint64_t *__restrict__ ts,
+                                          const uint32_t *__restrict__ len, Offs offs) {
     __shared__ unsigned long long s_el[kSortTile];
     __shared__ uint32_t s_wc[4][256];
     __shared__ uint32_t s_dst[256], s_tbase[256], s_tcnt[256];
     __shared__ uint32_t s_tmp[4];
-    __shared__ uint32_t s_tile;
     const uint32_t tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
-    const uint32_t L = L_dev ? *L_dev : L_host;
-    const uint32_t ntiles = (L + kSortTile - 1) / kSortTile;
-    if (tid == 0) s_tile = atomicAdd(tile_ctr, 1u);
 #pragma unroll
     for (int k = 0; k < 4; ++k) s_wc[w][lane * 4 + k] = 0;
     __syncthreads();
-    const uint32_t t = s_tile;
-    if (t >= ntiles) return;
+    FSX_STAMP(t, 0);
     const uint32_t t0 = t * kSortTile;
     const uint32_t end = min(L, t0 + kSortTile);
     const uint64_t lt_mask = (1ull << lane) - 1ull;
@@ -368,7 +317,7 @@ __global__ __launch_bounds__(256) void k_onesweep(const uint64_t *__restrict__ i
     // there), carried afterwards
     const bool pay = bs->pay_ok != 0;
     uint64_t pv[kSortItems];
-    if (pay) {
+    auto load_pay = [&]() {
         const uint64_t tbase = ~bs->inv_min_ts;
 #pragma unroll
         for (int r = 0; r < kSortItems; ++r) {
@@ -376,55 +325,41 @@ __global__ __launch_bounds__(256) void k_onesweep(const uint64_t *__restrict__ i
             if (first) pv[r] = i < end ? ((ts[i] - tbase) << kPayLenBits) | len[i] : 0ull;
             else pv[r] = i < end ? pin[i] : 0ull;
         }
-    }
+    };
+    // kLatePay: load the payload words only after the keys are out (fewer live
+    // registers through the ranking, one more memory latency per tile)
+    if (!kLatePay && pay) load_pay();
+    // Stable ranking inside the wave: lanes with equal digits are matched by ballots
+    // (one compare for a wave that shares a digit), the group leader reserves the
+    // group's slots with one returning LDS add, and the group reads the old count from
+    // its leader. A wave's LDS operations execute in order, so consecutive items'
+    // reservations need no round trip in between.
 #pragma unroll
     for (int r = 0; r < kSortItems; ++r) {
         const uint32_t i = t0 + w * 1024u + (uint32_t)r * 64u + lane;
-        const bool valid = i < end && !(first && v[r] == kSentinel);
+        const bool valid = sort_item(i, end, first, v[r]);
         const uint64_t act = __ballot(valid);
         const uint32_t d = (uint32_t)(v[r] >> shift) & 255u;
-        const uint64_t peers = match_digit(d, act);
+        const int lead0 = act ? __ffsll((unsigned long long)act) - 1 : 0;
+        const uint32_t dl = __shfl(d, lead0);
+        const uint64_t peers = __ballot(valid && d == dl) == act ? act : match_digit(d, act);
         const uint32_t below = (uint32_t)__popcll(peers & lt_mask);
         uint32_t base = 0;
-        if (valid) base = s_wc[w][d];
+        if (valid && below == 0) base = atomicAdd(&s_wc[w][d], (uint32_t)__popcll(peers));
+        base = __shfl(base, __ffsll((unsigned long long)peers) - 1);
         lr[r] = valid ? base + below : 0xFFFFFFFFu;
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        if (valid && below == 0) s_wc[w][d] = base + (uint32_t)__popcll(peers);
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     }
     __syncthreads();
+    FSX_STAMP(t, 1);
     const uint32_t d = tid;
     const uint32_t c0 = s_wc[0][d], c1 = s_wc[1][d], c2 = s_wc[2][d], c3 = s_wc[3][d];
     const uint32_t tc = c0 + c1 + c2 + c3;
-    // publish this tile's count, then look back for the exclusive prefix
-    unsigned long long *my = status + (size_t)t * 256u + d;
-    if (t == 0) __hip_atomic_store(my, os_word(gen, true, tc), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    else __hip_atomic_store(my, os_word(gen, false, tc), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    uint32_t excl = 0;
-    if (t > 0) {
-        uint32_t tt = t - 1;
-        uint32_t spins = 0;
-        for (;;) {
-            const unsigned long long wv = __hip_atomic_load(status + (size_t)tt * 256u + d, __ATOMIC_RELAXED,
-                                                            __HIP_MEMORY_SCOPE_AGENT);
-            if ((uint32_t)(wv >> 33) != gen) {
-                if (++spins > kSpinLimit) { atomicOr(&bs->err, ERR_SORT_HANG); break; }
-                __builtin_amdgcn_s_sleep(1);
-                continue;
-            }
-            excl += (uint32_t)wv;
-            if ((wv >> 32) & 1ull) break;
-            if (tt == 0) break;
-            --tt;
-        }
-        __hip_atomic_store(my, os_word(gen, true, excl + tc), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    s_dst[d] = offs(d, tc);
     __syncthreads();
+    FSX_STAMP(t, 2);
     s_wc[0][d] = 0; s_wc[1][d] = c0; s_wc[2][d] = c0 + c1; s_wc[3][d] = c0 + c1 + c2;
     s_tcnt[d] = tc;
-    const uint32_t tb = block256_excl(tc, s_tmp, nullptr);
-    s_tbase[d] = tb;
-    s_dst[d] = gbase[d] + excl;
+    s_tbase[d] = block256_excl(tc, s_tmp, nullptr);
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < kSortItems; ++r) {
@@ -435,6 +370,7 @@ __global__ __launch_bounds__(256) void k_onesweep(const uint64_t *__restrict__ i
         }
     }
     __syncthreads();
+    FSX_STAMP(t, 3);
     const uint32_t T = s_tbase[255] + s_tcnt[255];
     uint32_t dst[kSortItems];
 #pragma unroll
@@ -447,8 +383,9 @@ __global__ __launch_bounds__(256) void k_onesweep(const uint64_t *__restrict__ i
             out[dst[m]] = x;
         }
     }
+    FSX_STAMP(t, 4);
     if (!pay) return;
-    // the payload words follow the same permutation through the same LDS slots
+    if (kLatePay) load_pay();
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < kSortItems; ++r)
@@ -459,6 +396,109 @@ __global__ __launch_bounds__(256) void k_onesweep(const uint64_t *__restrict__ i
         const uint32_t j = tid + 256u * (uint32_t)m;
         if (j < T) pout[dst[m]] = s_el[j];
     }
+    FSX_STAMP(t, 5);
+}
+
+constexpr bool kLatePayDefault = true;
+
+struct TileOffs {
+    const uint32_t *offs;
+    uint32_t tcap, t;
+    __device__ __forceinline__ uint32_t operator()(uint32_t d, uint32_t) const {
+        return offs[(size_t)d * tcap + t];
+    }
+};
+
+template <bool kLatePay>
+__global__ __launch_bounds__(256, kLatePay ? 4 : 1) void k_tile_scatter(const uint64_t *__restrict__ in,
+                                                      uint64_t *__restrict__ out, uint32_t L_host,
+                                                      const uint32_t *L_dev, uint32_t shift, int first,
+                                                      const uint32_t *__restrict__ offs, uint32_t tcap,
+                                                      const BatchState *bs,
+                                                      const uint64_t *__restrict__ pin,
+                                                      uint64_t *__restrict__ pout,
+                                                      const uint64_t *__restrict__ ts,
+                                                      const uint32_t *__restrict__ len) {
+    const uint32_t L = L_dev ? *L_dev : L_host;
+    if (blockIdx.x * kSortTile >= L) return;
+    sort_tile<kLatePay>(blockIdx.x, in, out, L, shift, first, bs, pin, pout, ts, len,
+                        TileOffs{offs, tcap, blockIdx.x});
+}
+
+// ---- onesweep variant (FSX_FLAG_ONESWEEP_SORT): per-digit decoupled look-back.
+// Status words are 8-byte {generation, inclusive?, count} granules written with one
+// agent-scope store and polled with agent-scope loads; tiles take ids from an atomic
+// counter, so a tile only waits on tiles whose blocks already started; every pass of
+// every batch has its own generation, so stale words never match.
+constexpr uint32_t kSpinLimit = 1u << 22;
+constexpr int kLookW = 8;  // predecessor statuses per look-back round trip
+
+__device__ __forceinline__ unsigned long long os_word(uint32_t gen, bool inclusive, uint32_t cnt) {
+    return ((unsigned long long)gen << 33) | ((unsigned long long)(inclusive ? 1u : 0u) << 32) | cnt;
+}
+
+template <int kLW>
+struct LookbackOffs {
+    unsigned long long *status;
+    const uint32_t *gbase;
+    BatchState *bs;
+    uint32_t t, gen;
+    __device__ __forceinline__ uint32_t operator()(uint32_t d, uint32_t tc) const {
+        unsigned long long *my = status + (size_t)t * 256u + d;
+        __hip_atomic_store(my, os_word(gen, t == 0, tc), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        uint32_t excl = 0;
+        if (t == 0) return gbase[d];
+        int32_t tt = (int32_t)t - 1;
+        uint32_t spins = 0;
+        for (;;) {
+            unsigned long long wv[kLW];
+#pragma unroll
+            for (int j = 0; j < kLW; ++j)
+                wv[j] = tt - j >= 0 ? __hip_atomic_load(status + (size_t)(tt - j) * 256u + d,
+                                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                    : os_word(gen, true, 0);
+            int used = 0;
+            bool done = false;
+#pragma unroll
+            for (int j = 0; j < kLW; ++j) {
+                if (done || used < j) break;
+                if ((uint32_t)(wv[j] >> 33) != gen) break;  // not published yet
+                excl += (uint32_t)wv[j];
+                used = j + 1;
+                done = ((wv[j] >> 32) & 1ull) != 0;
+            }
+            if (done) break;
+            tt -= used;
+            if (used == 0) {
+                if (++spins > kSpinLimit) { atomicOr(&bs->err, ERR_SORT_HANG); break; }
+                __builtin_amdgcn_s_sleep(1);
+            }
+        }
+        __hip_atomic_store(my, os_word(gen, true, excl + tc), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return gbase[d] + excl;
+    }
+};
+
+template <int kLW>
+__global__ __launch_bounds__(256) void k_onesweep(const uint64_t *__restrict__ in,
+                                                  uint64_t *__restrict__ out, uint32_t L_host,
+                                                  const uint32_t *L_dev, uint32_t shift,
+                                                  const uint32_t *__restrict__ gbase,
+                                                  unsigned long long *status, uint32_t *tile_ctr,
+                                                  uint32_t gen, int first, BatchState *bs,
+                                                  const uint64_t *__restrict__ pin,
+                                                  uint64_t *__restrict__ pout,
+                                                  const uint64_t *__restrict__ ts,
+                                                  const uint32_t *__restrict__ len) {
+    __shared__ uint32_t s_tile;
+    const uint32_t L = L_dev ? *L_dev : L_host;
+    const uint32_t ntiles = (L + kSortTile - 1) / kSortTile;
+    if (threadIdx.x == 0) s_tile = atomicAdd(tile_ctr, 1u);
+    __syncthreads();
+    const uint32_t t = s_tile;
+    if (t >= ntiles) return;
+    sort_tile<false>(t, in, out, L, shift, first, bs, pin, pout, ts, len,
+                     LookbackOffs<kLW>{status, gbase, bs, t, gen});
 }
 
 // ------------------------------------------------------------------ IPv6 collision fixup
@@ -1481,46 +1521,41 @@ hipError_t launch_verdict_pipeline(const uint8_t *hdr, const uint32_t *len, cons
     if ((e = hipMemsetAsync(bs, 0, sizeof(BatchState), st)) != hipSuccess) return e;
     if (n == 0) { if (nev_used) *nev_used = 0; return hipSuccess; }
     if ((e = hipMemsetAsync(sc.marks, 0, n, st)) != hipSuccess) return e;
-    const uint32_t G = std::min<uint32_t>(kSortMaxBlocks, std::max<uint32_t>(1, cdiv(n, kSortTile)));
     const uint32_t gridStream = std::min<uint32_t>(2048, std::max<uint32_t>(1, cdiv(n, 256)));
     const uint32_t gridTiles = std::min<uint32_t>(4096, std::max<uint32_t>(1, cdiv(n, kTile)));
 
     // mark(name) closes the interval of the kernel just enqueued (per-kernel timing)
-    const bool classic = (lim.test_flags & 2u) != 0;
+    const bool onesweep = (lim.test_flags & 2u) != 0;
     if ((e = hipMemsetAsync(sc.sort_ctl, 0, kSortCtlWords * 4, st)) != hipSuccess) return e;
     mark("start");
     k_parse<<<std::min<uint32_t>(2048, std::max<uint32_t>(1, cdiv(n, 256))), 256, 0, st>>>(
         hdr, len, ts, n, sc.packed[0], verdict, bs, lim.salt32, lim.seed,
-        (lim.test_flags & 1u) ? skey_v4(0x0100000Au, lim.salt32) : 0u,
-        classic ? nullptr : sc.sort_ctl);
+        (lim.test_flags & 1u) ? skey_v4(0x0100000Au, lim.salt32) : 0u, sc.sort_ctl);
     mark("k_parse");
-    if (classic) {
-        for (int pass = 0; pass < 4; ++pass) {
-            const uint64_t *in = sc.packed[pass & 1];
-            uint64_t *out = sc.packed[(pass + 1) & 1];
-            const uint32_t shift = 32u + 8u * (uint32_t)pass;
-            const uint32_t *Ld = pass == 0 ? nullptr : &bs->n_valid;
-            k_sort_hist<<<G, 256, 0, st>>>(in, n, Ld, shift, sc.hist, G, pass == 0, bs);
-            mark("k_sort_hist");
-            k_sort_rowscan<<<256, 256, 0, st>>>(sc.hist, G, sc.row_total);
-            mark("k_sort_rowscan");
-            k_sort_scatter<<<G, 256, 0, st>>>(in, out, n, Ld, shift, sc.hist, sc.row_total, G, pass == 0);
-            mark("k_sort_scatter");
-        }
-    } else {
-        k_hist_prep<<<1, 256, 0, st>>>(sc.sort_ctl, sc.gbase, bs);
-        const uint32_t gen0 = next_generation();
-        const uint32_t ntiles = std::max<uint32_t>(1, cdiv(n, kSortTile));
-        for (int pass = 0; pass < 4; ++pass) {
-            const uint64_t *in = sc.packed[pass & 1];
-            uint64_t *out = sc.packed[(pass + 1) & 1];
-            const uint32_t shift = 32u + 8u * (uint32_t)pass;
-            const uint32_t *Ld = pass == 0 ? nullptr : &bs->n_valid;
-            k_onesweep<<<ntiles, 256, 0, st>>>(in, out, n, Ld, shift, sc.gbase + 256 * pass, sc.status,
-                                               sc.sort_ctl + 1024 + pass, gen0 + (uint32_t)pass,
-                                               pass == 0, bs, pass == 0 ? nullptr : sc.pay[pass & 1],
-                                               sc.pay[(pass + 1) & 1], ts, len);
+    k_hist_prep<<<1, 256, 0, st>>>(sc.sort_ctl, sc.gbase, bs);
+    const uint32_t ntiles = std::max<uint32_t>(1, cdiv(n, kSortTile));
+    const uint32_t tcap = (uint32_t)(sc.cap / kSortTile + 2);
+    const uint32_t gen0 = onesweep ? next_generation() : 0u;
+    for (int pass = 0; pass < 4; ++pass) {
+        const uint64_t *in = sc.packed[pass & 1];
+        uint64_t *out = sc.packed[(pass + 1) & 1];
+        const uint64_t *pin = pass == 0 ? nullptr : sc.pay[pass & 1];
+        uint64_t *pout = sc.pay[(pass + 1) & 1];
+        const uint32_t shift = 32u + 8u * (uint32_t)pass;
+        const uint32_t *Ld = pass == 0 ? nullptr : &bs->n_valid;
+        if (onesweep) {
+            k_onesweep<kLookW><<<ntiles, 256, 0, st>>>(in, out, n, Ld, shift, sc.gbase + 256 * pass,
+                                                       sc.status, sc.sort_ctl + 1024 + pass,
+                                                       gen0 + (uint32_t)pass, pass == 0, bs, pin, pout,
+                                                       ts, len);
             mark("k_onesweep");
+        } else {
+            k_tile_hist<<<ntiles, 256, 0, st>>>(in, n, Ld, shift, pass == 0, sc.hist, tcap);
+            k_tile_scan<<<256, 256, 0, st>>>(sc.hist, tcap, n, Ld, sc.gbase + 256 * pass);
+            mark("k_tile_hist");
+            k_tile_scatter<kLatePayDefault><<<ntiles, 256, 0, st>>>(in, out, n, Ld, shift, pass == 0, sc.hist, tcap, bs,
+                                                   pin, pout, ts, len);
+            mark("k_tile_scatter");
         }
     }
     uint64_t *S = sc.packed[0];

@@ -359,7 +359,7 @@ hipError_t launch_flows(const uint64_t *S, const uint64_t *pay, BatchState *bs, 
                         uint32_t n, hipStream_t st) {
     const FlowOut out{(FlowAcc *)acc, keys16, fam, feat, prob, dec, cap};
     const uint32_t nsub = (n + kFT - 1) / kFT;
-    const uint32_t grid = std::max<uint32_t>(1, std::min<uint32_t>(2048, (nsub + 3) / 4));
+    const uint32_t grid = std::max<uint32_t>(1, std::min<uint32_t>(16384, (nsub + 3) / 4));
     k_flow_tile<<<grid, 256, 0, st>>>(S, pay, bs, headf, len, ts, hdr, tile_off, sub_cnt, seg_start,
                                       (FlowAcc *)firstp, (FlowAcc *)lastp, span_list, out, P, salt);
     k_flow_combine<<<256, 256, 0, st>>>(S, bs, seg_start, (const FlowAcc *)firstp,

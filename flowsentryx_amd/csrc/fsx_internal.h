@@ -136,8 +136,7 @@ struct Scratch {
     uint8_t *headf;        // per sorted position: segment-head flag
     uint32_t *seg_start;   // nseg + 1
     uint32_t *seg_slot;
-    uint32_t *hist;        // 256 * kSortMaxBlocks
-    uint32_t *row_total;   // 256
+    uint32_t *hist;        // sort: per-tile digit counts [256][cap/kSortTile+2]; walker classes
     uint32_t *tile_aux;    // per kTile tile
     uint8_t *tile_last;
     uint32_t *fix_list;
