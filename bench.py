@@ -38,8 +38,10 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.
 # (DESIGN.md §3): element = packet (parse) or IP packet (sort / fill).
 KERNEL_BYTES = {
     "k_parse": ("packet", 64 + 4 + 8 + 8),      # header record + len + ts in, sort word out
-    "k_sort_scatter": ("ip_packet", 16),        # sort word in + out
-    "k_sort_hist": ("ip_packet", 8),
+    # one LSD digit pass: sort word + payload word in and out (pass 0 reads ts + len
+    # instead of a payload word: 36 B; passes 1-3: 32 B) -> 33 B per launch on average
+    "k_tile_scatter": ("ip_packet", 33),
+    "k_tile_hist": ("ip_packet", 8),            # sort word in (+ per-tile counts)
     "k_onesweep": ("ip_packet", 16),            # sort word in + out, per digit pass
     "k_flow_features": ("ip_packet", 8 + 4 + 8),  # sort word + len + ts per packet
     "k_walk_fixed": ("ip_packet", 8 + 4 + 8 + 1),  # sort word + len + ts in, mark out
@@ -168,9 +170,10 @@ def main():
         bytes_per_launch = per * units
         achieved = bytes_per_launch / (per_launch_ms * 1e-3) / 1e9 if per else None
         traffic = None
-        pmc = ROOT / "profiles" / f"pmc_{name}.json"
+        pmc = ROOT / "profiles" / "pmc_traffic.json"
         if pmc.exists():
-            traffic = json.loads(pmc.read_text()).get("hbm_bytes_per_launch")
+            row = json.loads(pmc.read_text()).get("kernels", {}).get(name, {})
+            traffic = row.get("hbm_bytes_per_launch")
         roofline = {
             "bound": "hbm", "kernel": name, "achieved": round(achieved, 1) if achieved else None,
             "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -5,15 +5,23 @@ mean per dispatch over the measured bench steps. FETCH_SIZE and WRITE_SIZE are i
 MI355X_MICROARCH.md (HBM section) — both are reported raw and corrected."""
 import csv
 import json
+import re
 import sys
 from collections import defaultdict
 from pathlib import Path
 
 
+def short_name(k):
+    """'void fsx::k_tile_scatter<true>(unsigned long const*, ...)' -> 'k_tile_scatter'."""
+    k = k.split("(")[0].replace("void ", "").strip()
+    k = re.sub(r"<.*>", "", k)
+    return k.split("::")[-1]
+
+
 def load(path):
     out = defaultdict(lambda: defaultdict(list))
     for r in csv.DictReader(open(path)):
-        name = r["Kernel_Name"].split("(")[0]
+        name = short_name(r["Kernel_Name"])
         out[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
         out[name]["_dur_ns"].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
     return out
@@ -42,7 +50,10 @@ def main():
         if "hbm_read_bytes" in row and "hbm_write_bytes" in row:
             row["hbm_bytes_per_launch"] = row["hbm_read_bytes"] + row["hbm_write_bytes"]
         rows[k] = row
-    print(json.dumps(rows, indent=1))
+    doc = {"source": f"rocprofv3 --kernel-trace --pmc passes under {d.name} (scripts/gpu_pmc.sh)",
+           "correction": "FETCH_SIZE x2 (gfx950, MI355X_MICROARCH.md HBM section); WRITE_SIZE as read",
+           "kernels": rows}
+    print(json.dumps(doc, indent=1))
 
 
 if __name__ == "__main__":
