@@ -107,6 +107,7 @@ static void free_scratch(fsx_ctx *c) {
     hipFree(s.tile_aux); hipFree(s.tile_last); hipFree(s.fix_list); hipFree(s.fix_bitmap);
     hipFree(s.seg_order); hipFree(s.sub_cnt); hipFree(s.flow_first); hipFree(s.flow_last);
     hipFree(s.span_list); hipFree(s.sort_ctl); hipFree(s.gbase); hipFree(s.status);
+    hipFree(s.lim_tiles);
     s = Scratch{};
 }
 
@@ -137,6 +138,8 @@ static int alloc_scratch(fsx_ctx *c, uint64_t cap) {
     HIPCHK(c, hipMalloc(&s.gbase, 1024 * 4));
     HIPCHK(c, hipMalloc(&s.status, (cap / kSortTile + 2) * 256 * 8));
     HIPCHK(c, hipMemset(s.status, 0, (cap / kSortTile + 2) * 256 * 8));
+    s.lim_tiles_n = cap / kTile + 2;
+    HIPCHK(c, hipMalloc(&s.lim_tiles, s.lim_tiles_n * 4 * 8));
     s.cap = cap;
     return 0;
 }
@@ -191,6 +194,8 @@ int fsx_open(fsx_ctx **out, const fsx_config *cfg) {
     if (k.max_entries == 0 || k.max_entries > (1ull << 33)) return -EINVAL;
     if (k.max_batch == 0 || k.max_batch > kMaxBatchLimit) return -EINVAL;
     if (k.limiter < FSX_LIMIT_FIXED_WINDOW || k.limiter > FSX_LIMIT_TOKEN_BUCKET) return -EINVAL;
+    // token bucket: capacity burst * 1e9 nano-tokens must stay <= 2^61
+    if (k.limiter == FSX_LIMIT_TOKEN_BUCKET && k.tb_burst > FSX_TB_MAX_BURST) return -EINVAL;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return -ENODEV;
     if (k.device < 0 || k.device >= ndev) return -EINVAL;
@@ -216,7 +221,7 @@ int fsx_open(fsx_ctx **out, const fsx_config *cfg) {
     Limits &L = c->lim;
     L.pps = k.pps_threshold; L.bps = k.bps_threshold; L.window = k.window_ns; L.block = k.block_ns;
     L.tb_rate = k.tb_rate;
-    L.tb_cap = k.tb_burst > (~0ull / 1000000000ull) ? ~0ull : k.tb_burst * 1000000000ull;
+    L.tb_cap = std::min<uint64_t>(k.tb_burst, FSX_TB_MAX_BURST) * 1000000000ull;
     L.max_entries = k.max_entries;
     L.table_mask = c->slots - 1;
     L.seed = mix64(k.hash_seed);
@@ -286,7 +291,7 @@ static int run_batch(fsx_ctx *c, const uint8_t *d_hdr, const uint32_t *d_len, co
     int rc = sel(c);
     if (rc) return rc;
     if (c->pending) { rc = fsx_sync(c); if (rc) return rc; }
-    if (do_limit && c->cfg.limiter != FSX_LIMIT_FIXED_WINDOW)
+    if (do_limit && c->cfg.limiter == FSX_LIMIT_SLIDING_WINDOW)
         return set_err(c, -EOPNOTSUPP, "limiter %d not built into this pipeline yet", c->cfg.limiter);
     FlowRequest frq;
     if (fr) {
@@ -384,11 +389,20 @@ int fsx_verdict_batch(fsx_ctx *c, const uint8_t *hdr, const uint32_t *len, const
 }
 
 // ------------------------------------------------------------------ maps
+static bool map_v6(int map_id) {
+    return map_id == FSX_MAP_IPV6_STATS || map_id == FSX_MAP_IPV6_BLACKLIST || map_id == FSX_MAP_IPV6_TOKENS;
+}
+// value bytes of a per-IP map: ip_stats 24, token bucket 16, blacklist 8
+static size_t map_vlen(int map_id) {
+    if (map_id == FSX_MAP_IPV4_STATS || map_id == FSX_MAP_IPV6_STATS) return 24;
+    if (map_id == FSX_MAP_IPV4_TOKENS || map_id == FSX_MAP_IPV6_TOKENS) return 16;
+    return 8;
+}
+
 static int key_words(int map_id, const void *key, uint32_t k[4]) {
     k[0] = k[1] = k[2] = k[3] = 0;
-    if (map_id == FSX_MAP_IPV4_STATS || map_id == FSX_MAP_IPV4_BLACKLIST) memcpy(k, key, 4);
-    else if (map_id == FSX_MAP_IPV6_STATS || map_id == FSX_MAP_IPV6_BLACKLIST) memcpy(k, key, 16);
-    else return -EINVAL;
+    if (map_id < FSX_MAP_IPV4_STATS || map_id >= FSX_MAP_COUNT) return -EINVAL;
+    memcpy(k, key, map_v6(map_id) ? 16 : 4);
     return 0;
 }
 
@@ -412,8 +426,8 @@ static int map_op(fsx_ctx *c, int op, int map_id, const void *key, const void *v
     if ((rc = key_words(map_id, key, k))) return set_err(c, rc, "bad map id %d", map_id);
     if (flags > FSX_BPF_EXIST) return -EINVAL;
     uint64_t v[3] = {0, 0, 0};
-    const bool is_st = map_id == FSX_MAP_IPV4_STATS || map_id == FSX_MAP_IPV6_STATS;
-    if (op == 1) memcpy(v, value, is_st ? 24 : 8);
+    const size_t vlen = map_vlen(map_id);
+    if (op == 1) memcpy(v, value, vlen);
     hipError_t e = launch_map_op(c->table, c->tstate, c->lim, op, map_id, k, v, flags, c->d_res,
                                  c->d_val, c->stream);
     if (e != hipSuccess) return set_err(c, -EIO, "map op: %s", hipGetErrorString(e));
@@ -422,7 +436,7 @@ static int map_op(fsx_ctx *c, int op, int map_id, const void *key, const void *v
     uint64_t ov[3];
     HIPCHK(c, hipMemcpyAsync(ov, c->d_val, 24, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    if (res == 0 && op == 0) memcpy(out, ov, is_st ? 24 : 8);
+    if (res == 0 && op == 0) memcpy(out, ov, vlen);
     return res;
 }
 
@@ -452,10 +466,8 @@ int fsx_map_dump(fsx_ctx *c, int map_id, void *keys, void *values, size_t cap, s
         *n_out = 1;
         return 0;
     }
-    if (map_id < FSX_MAP_IPV4_STATS || map_id > FSX_MAP_IPV6_BLACKLIST) return -EINVAL;
-    const bool v6 = map_id == FSX_MAP_IPV6_STATS || map_id == FSX_MAP_IPV6_BLACKLIST;
-    const bool st = map_id == FSX_MAP_IPV4_STATS || map_id == FSX_MAP_IPV6_STATS;
-    const size_t klen = v6 ? 16 : 4, vlen = st ? 24 : 8;
+    if (map_id < FSX_MAP_IPV4_STATS || map_id >= FSX_MAP_COUNT) return -EINVAL;
+    const size_t klen = map_v6(map_id) ? 16 : 4, vlen = map_vlen(map_id);
     const size_t dcap = std::max<size_t>(cap, 1);
     uint8_t *dk = nullptr;
     uint64_t *dv = nullptr;

@@ -20,6 +20,7 @@
 
 #include "fsx_dev_common.h"
 #include "fsx_internal.h"
+#include "fsx_seg.h"
 
 #define XDP_DROP 1
 #define XDP_PASS 2
@@ -870,171 +871,6 @@ __global__ void k_count_inserted(BatchState *bs, TableState *tstate) {
 // search instead of one per binary-search step).
 constexpr uint32_t kShortSeg = 512;
 
-// Timestamp / length of sorted position q: from the payload words carried by the
-// sort (kPay), else gathered through the arrival index.
-template <bool kPay>
-struct SegView {
-    const uint64_t *S;
-    const uint64_t *ts;
-    const uint32_t *len;
-    const uint64_t *pay;
-    uint64_t tbase;
-    __device__ __forceinline__ uint64_t t(uint32_t q) const {
-        if constexpr (kPay) return tbase + (pay[q] >> kPayLenBits);
-        else return ts[pk_idx(S[q])];
-    }
-    __device__ __forceinline__ uint32_t l(uint32_t q) const {
-        if constexpr (kPay) return (uint32_t)pay[q] & ((1u << kPayLenBits) - 1u);
-        else return len[pk_idx(S[q])];
-    }
-};
-
-// First q in [lo, hi) with t(q) > X (t non-decreasing on [lo, hi)); wave-uniform
-// arguments, every lane calls. Round 0 probes 64 consecutive packets, round 1 64
-// exponentially spaced ones, then 64-ary narrowing.
-template <class SV>
-__device__ uint32_t wave_gallop_gt(const SV &sv, uint32_t lo, uint32_t hi, uint64_t X) {
-    const uint32_t lane = lane_id();
-    if (lo >= hi) return hi;
-    {
-        const uint32_t q = lo + lane;
-        const bool pr = q < hi && sv.t(q) > X;
-        const uint64_t m = __ballot(pr);
-        if (m) return lo + (uint32_t)__ffsll((unsigned long long)m) - 1u;
-        if (hi - lo <= 64) return hi;
-    }
-    uint32_t good = lo + 63, bad = hi;  // t(good) <= X; answer in (good, bad]
-    {
-        const uint64_t q64 = (uint64_t)lo + (lane < 32 ? (64ull << lane) : (1ull << 40));
-        const bool valid = q64 < hi;
-        const bool pr = valid && sv.t((uint32_t)q64) > X;
-        const uint64_t m = __ballot(pr);
-        const uint64_t vm = __ballot(valid);
-        if (m) {
-            const uint32_t f = (uint32_t)__ffsll((unsigned long long)m) - 1u;
-            bad = lo + (64u << f);
-            if (f) good = lo + (64u << (f - 1));
-        } else if (vm) {
-            const uint32_t lv = 63u - (uint32_t)__clzll((long long)vm);
-            good = lo + (64u << lv);
-        }
-    }
-    while (bad - good > 64) {
-        const uint32_t cnt = bad - good - 1;
-        const uint32_t step = (cnt + 63) / 64;
-        const uint32_t q = good + 1 + lane * step;
-        const bool valid = q < bad;
-        const bool pr = valid && sv.t(q) > X;
-        const uint64_t m = __ballot(pr);
-        if (m) {
-            const uint32_t f = (uint32_t)__ffsll((unsigned long long)m) - 1u;
-            const uint32_t nb = good + 1 + f * step;
-            if (f) good = good + 1 + (f - 1) * step;
-            bad = nb;
-        } else {
-            const uint64_t vm = __ballot(valid);
-            good = good + 1 + (63u - (uint32_t)__clzll((long long)vm)) * step;
-        }
-    }
-    const uint32_t q = good + 1 + lane;
-    const bool pr = q < bad && sv.t(q) > X;
-    const uint64_t m = __ballot(pr);
-    return m ? good + (uint32_t)__ffsll((unsigned long long)m) : bad;
-}
-
-// Thread version: galloping from lo, O(log distance).
-template <class SV>
-__device__ __forceinline__ uint32_t gallop_gt(const SV &sv, uint32_t lo, uint32_t hi,
-                                              uint64_t X) {
-    if (lo >= hi) return hi;
-    if (sv.t(lo) > X) return lo;
-    uint32_t good = lo, bad = hi;
-    uint32_t step = 1;
-    for (;;) {
-        const uint64_t cand = (uint64_t)good + step;
-        if (cand >= hi) break;
-        if (sv.t((uint32_t)cand) > X) { bad = (uint32_t)cand; break; }
-        good = (uint32_t)cand;
-        step <<= 1;
-    }
-    uint32_t l = good + 1, r = bad;
-    while (l < r) {
-        const uint32_t m = l + (r - l) / 2;
-        if (sv.t(m) > X) r = m; else l = m + 1;
-    }
-    return l;
-}
-
-// Sum of frame lengths over [lo, hi): wave-strided (4 loads in flight per lane) or,
-// for a thread, 16 independent gathers per step.
-template <bool kWave, class SV>
-__device__ __forceinline__ uint64_t sum_len(const SV &sv, uint32_t lo, uint32_t hi) {
-    uint64_t s = 0;
-    if constexpr (kWave) {
-        const uint32_t lane = lane_id();
-        uint32_t q = lo + lane;
-        for (; q + 192 < hi; q += 256) {
-            const uint32_t l0 = sv.l(q), l1 = sv.l(q + 64), l2 = sv.l(q + 128), l3 = sv.l(q + 192);
-            s += (uint64_t)l0 + l1 + l2 + l3;
-        }
-        for (; q < hi; q += 64) s += sv.l(q);
-        return wave_sum(s);
-    } else {
-        uint32_t q = lo;
-        for (; q + 16 <= hi; q += 16) {
-            uint32_t l[16];
-#pragma unroll
-            for (int k = 0; k < 16; ++k) l[k] = sv.l(q + k);
-#pragma unroll
-            for (int k = 0; k < 16; ++k) s += l[k];
-        }
-        for (; q < hi; ++q) s += sv.l(q);
-        return s;
-    }
-}
-
-// First q in [from, lim) with acc0 + sum(L[from..q]) > B, else lim.
-template <bool kWave, class SV>
-__device__ uint32_t bytes_trigger(const SV &sv, uint32_t from, uint32_t lim, uint64_t acc0,
-                                  uint64_t B) {
-    uint64_t acc = acc0;
-    if constexpr (kWave) {
-        const uint32_t lane = lane_id();
-        for (uint32_t q0 = from; q0 < lim; q0 += 64) {
-            const uint32_t q = q0 + lane;
-            const uint64_t L = q < lim ? sv.l(q) : 0;
-            const uint64_t incl = wave_incl_sum(L);
-            const uint64_t m = __ballot(q < lim && acc + incl > B);
-            if (m) return q0 + (uint32_t)__ffsll((unsigned long long)m) - 1u;
-            acc += __shfl(incl, 63);
-        }
-        return lim;
-    } else {
-        for (uint32_t q = from; q < lim; ++q) {
-            acc += sv.l(q);
-            if (acc > B) return q;
-        }
-        return lim;
-    }
-}
-
-template <bool kWave, class SV>
-__device__ __forceinline__ uint32_t search_gt(const SV &sv, uint32_t lo, uint32_t hi, uint64_t X) {
-    if constexpr (kWave) return wave_gallop_gt(sv, lo, hi, X);
-    else return gallop_gt(sv, lo, hi, X);
-}
-
-template <bool kWave>
-struct MarkWriter {
-    uint8_t *marks;
-    uint8_t last;
-    __device__ __forceinline__ void emit(uint32_t pos, uint8_t v) {
-        if (v != last) {
-            if (!kWave || lane_id() == 0) marks[pos] = v;
-            last = v;
-        }
-    }
-};
 
 constexpr uint64_t kBig = 1ull << 62;
 
@@ -1586,17 +1422,22 @@ hipError_t launch_verdict_pipeline(const uint8_t *hdr, const uint32_t *len, cons
     k_insert<<<gridStream, 256, 0, st>>>(S, bs, sc.seg_start, sc.seg_slot, hdr, table, tstate, lim);
     k_count_inserted<<<1, 1, 0, st>>>(bs, tstate);
     mark("k_insert");
-    uint32_t *cls = sc.sort_ctl + 1028;
-    k_seg_count<<<kSegBlocks, 256, 0, st>>>(bs, sc.seg_start, sc.hist);
-    k_seg_scan<<<1, 1024, 0, st>>>(sc.hist, cls);
-    k_seg_order<<<kSegBlocks, 256, 0, st>>>(bs, sc.seg_start, sc.hist, sc.seg_order);
-    mark("k_seg_order");
-    k_walk_fixed<<<gridStream, 256, 0, st>>>(S, bs, sc.seg_start, sc.seg_slot, ts, len, sc.pay[0],
-                                             sc.seg_order, cls, sc.marks, table, lim);
-    mark("k_walk_fixed");
-    k_walk_fixed_long<<<1024, 256, 0, st>>>(S, bs, sc.seg_start, sc.seg_slot, ts, len, sc.pay[0],
-                                            sc.seg_order, cls, sc.marks, table, lim);
-    mark("k_walk_fixed_long");
+    if (lim.limiter == 2) {   // FSX_LIMIT_TOKEN_BUCKET
+        if ((e = launch_token_bucket(S, ts, len, bs, sc, table, lim, n, st)) != hipSuccess) return e;
+        mark("k_token_bucket");
+    } else {
+        uint32_t *cls = sc.sort_ctl + 1028;
+        k_seg_count<<<kSegBlocks, 256, 0, st>>>(bs, sc.seg_start, sc.hist);
+        k_seg_scan<<<1, 1024, 0, st>>>(sc.hist, cls);
+        k_seg_order<<<kSegBlocks, 256, 0, st>>>(bs, sc.seg_start, sc.hist, sc.seg_order);
+        mark("k_seg_order");
+        k_walk_fixed<<<gridStream, 256, 0, st>>>(S, bs, sc.seg_start, sc.seg_slot, ts, len, sc.pay[0],
+                                                 sc.seg_order, cls, sc.marks, table, lim);
+        mark("k_walk_fixed");
+        k_walk_fixed_long<<<1024, 256, 0, st>>>(S, bs, sc.seg_start, sc.seg_slot, ts, len, sc.pay[0],
+                                                sc.seg_order, cls, sc.marks, table, lim);
+        mark("k_walk_fixed_long");
+    }
     k_fill_last<<<gridTiles, 256, 0, st>>>(sc.marks, bs, sc.tile_last);
     k_fill_carry<<<1, 1024, 0, st>>>(sc.tile_last, bs);
     mark("k_fill_last");
@@ -1608,18 +1449,25 @@ hipError_t launch_verdict_pipeline(const uint8_t *hdr, const uint32_t *len, cons
 
 // ------------------------------------------------------------------ map syscalls
 // op: 0 lookup, 1 update, 2 delete. Result: 0 / -ENOENT(-2) / -EEXIST(-17) / -ENOSPC(-28).
+// Map id -> table tag (1 IPv4, 2 IPv6) and slot flag bit (include/fsx_hip.h map ids).
+__host__ __device__ inline uint32_t map_tag(int map_id) { return (map_id == 2 || map_id == 4 || map_id == 6) ? 2u : 1u; }
+__host__ __device__ inline uint32_t map_bit(int map_id) {
+    return (map_id == 1 || map_id == 2) ? SLOT_HAS_ST : (map_id == 5 || map_id == 6) ? SLOT_HAS_TB : SLOT_HAS_BL;
+}
+
 __global__ void k_map_op(Slot *table, TableState *tstate, Limits lim, int op, int map_id,
                          uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3, uint64_t v0,
                          uint64_t v1, uint64_t v2, uint64_t flags, int32_t *res, uint64_t *outv) {
     if (threadIdx.x || blockIdx.x) return;
     const uint32_t k[4] = {k0, k1, k2, k3};
-    const uint32_t tag = (map_id == 2 || map_id == 4) ? 2u : 1u;
-    const uint32_t bit = (map_id == 1 || map_id == 2) ? SLOT_HAS_ST : SLOT_HAS_BL;
+    const uint32_t tag = map_tag(map_id);
+    const uint32_t bit = map_bit(map_id);
     uint32_t s = table_find(table, lim.table_mask, tag, k, lim.seed);
     const bool present = s != kNoSlot && (table[s].flags & bit);
     if (op == 0) {
         if (!present) { *res = -2; return; }
         if (bit == SLOT_HAS_ST) { outv[0] = table[s].pps; outv[1] = table[s].bps; outv[2] = table[s].tt; }
+        else if (bit == SLOT_HAS_TB) { outv[0] = table[s].aux; outv[1] = table[s].tt; }
         else outv[0] = table[s].till;
         *res = 0;
         return;
@@ -1639,6 +1487,7 @@ __global__ void k_map_op(Slot *table, TableState *tstate, Limits lim, int op, in
         tstate->count += 1;
     }
     if (bit == SLOT_HAS_ST) { table[s].pps = v0; table[s].bps = v1; table[s].tt = v2; }
+    else if (bit == SLOT_HAS_TB) { table[s].aux = v0; table[s].tt = v1; }
     else table[s].till = v0;
     table[s].flags |= bit;
     *res = 0;
@@ -1655,10 +1504,10 @@ hipError_t launch_map_op(Slot *table, TableState *tstate, const Limits &lim, int
 __global__ __launch_bounds__(256) void k_map_dump(const Slot *table, Limits lim, int map_id,
                                                   uint8_t *keys, uint64_t *vals, uint64_t cap,
                                                   unsigned long long *count) {
-    const uint32_t tag = (map_id == 2 || map_id == 4) ? 2u : 1u;
-    const uint32_t bit = (map_id == 1 || map_id == 2) ? SLOT_HAS_ST : SLOT_HAS_BL;
+    const uint32_t tag = map_tag(map_id);
+    const uint32_t bit = map_bit(map_id);
     const uint32_t klen = tag == 2 ? 16u : 4u;
-    const uint32_t vw = bit == SLOT_HAS_ST ? 3u : 1u;
+    const uint32_t vw = bit == SLOT_HAS_ST ? 3u : bit == SLOT_HAS_TB ? 2u : 1u;
     for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i <= lim.table_mask;
          i += (uint64_t)gridDim.x * 256u) {
         const Slot &s = table[i];
@@ -1668,6 +1517,7 @@ __global__ __launch_bounds__(256) void k_map_dump(const Slot *table, Limits lim,
         const uint8_t *kb = reinterpret_cast<const uint8_t *>(s.key);
         for (uint32_t b = 0; b < klen; ++b) keys[o * klen + b] = kb[b];
         if (vw == 3) { vals[o * 3] = s.pps; vals[o * 3 + 1] = s.bps; vals[o * 3 + 2] = s.tt; }
+        else if (vw == 2) { vals[o * 2] = s.aux; vals[o * 2 + 1] = s.tt; }
         else vals[o] = s.till;
     }
 }

@@ -44,7 +44,7 @@ struct alignas(64) Slot {
     uint64_t bps;
     uint64_t tt;          // track_time
     uint64_t till;        // ipv{4,6}_blacklist_map value
-    uint64_t aux;         // token bucket: nano-tokens (tt = last refill time)
+    uint64_t aux;         // token bucket: nano-tokens (tt = last refill time, SLOT_HAS_TB)
 };
 static_assert(sizeof(Slot) == 64, "slot is one cache line");
 
@@ -150,6 +150,8 @@ struct Scratch {
                            // counters, [1028,1028+2*kSegClasses) segment class counts, cursors
     uint32_t *gbase;       // 4 x 256 digit bases
     unsigned long long *status;  // onesweep look-back words, 256 per tile
+    uint64_t *lim_tiles;   // limiter scans: 4 u64 per kTile tile (token bucket: map + carry)
+    uint64_t lim_tiles_n;  // tiles lim_tiles is sized for
     uint64_t cap;          // packets the scratch is sized for
 };
 
@@ -171,6 +173,12 @@ hipError_t launch_verdict_pipeline(const uint8_t *hdr, const uint32_t *len, cons
                                    BatchState *bs, const Scratch &sc, const Limits &lim,
                                    bool do_limit, const FlowRequest *flows, hipStream_t st,
                                    hipEvent_t *ev, int nev, int *nev_used, const char **names);
+
+// Build-defined limiters (fsx_limiters.hip), after the table lookup/insert of a batch:
+// one verdict mark per sorted position, final per-source state in the table.
+hipError_t launch_token_bucket(const uint64_t *S, const uint64_t *ts, const uint32_t *len, BatchState *bs,
+                               const Scratch &sc, Slot *table, const Limits &lim, uint32_t n,
+                               hipStream_t st);
 
 hipError_t launch_flows(const uint64_t *S, const uint64_t *pay, BatchState *bs, const uint8_t *headf, const uint32_t *len,
                         const uint64_t *ts, const uint8_t *hdr, const uint32_t *tile_off,

@@ -26,12 +26,16 @@ MAP_IPV4_STATS = 1
 MAP_IPV6_STATS = 2
 MAP_IPV4_BLACKLIST = 3
 MAP_IPV6_BLACKLIST = 4
+MAP_IPV4_TOKENS = 5   # build-defined token-bucket state
+MAP_IPV6_TOKENS = 6
 MAP_NAMES = {
     MAP_STATS: "stats_map",
     MAP_IPV4_STATS: "ipv4_stats_map",
     MAP_IPV6_STATS: "ipv6_stats_map",
     MAP_IPV4_BLACKLIST: "ipv4_blacklist_map",
     MAP_IPV6_BLACKLIST: "ipv6_blacklist_map",
+    MAP_IPV4_TOKENS: "ipv4_tokens_map",
+    MAP_IPV6_TOKENS: "ipv6_tokens_map",
 }
 BPF_ANY, BPF_NOEXIST, BPF_EXIST = 0, 1, 2
 
@@ -157,11 +161,23 @@ def _ptr(a: np.ndarray) -> int:
     return a.ctypes.data
 
 
+_V6_MAPS = (MAP_IPV6_STATS, MAP_IPV6_BLACKLIST, MAP_IPV6_TOKENS)
+
+
+def _value_words(map_id: int) -> int:
+    """u64 words of a per-IP map value: ip_stats 3, token-bucket state 2, blacklist 1."""
+    if map_id in (MAP_IPV4_STATS, MAP_IPV6_STATS):
+        return 3
+    if map_id in (MAP_IPV4_TOKENS, MAP_IPV6_TOKENS):
+        return 2
+    return 1
+
+
 def _key_bytes(map_id: int, key) -> bytes:
     if isinstance(key, int):
         key = key.to_bytes(4, "little")
     key = bytes(key)
-    want = 16 if map_id in (MAP_IPV6_STATS, MAP_IPV6_BLACKLIST) else 4
+    want = 16 if map_id in _V6_MAPS else 4
     if len(key) != want:
         raise ValueError(f"{MAP_NAMES[map_id]} keys are {want} bytes")
     return key
@@ -248,7 +264,8 @@ class FsxContext:
         if rc == -errno.ENOENT:
             return None
         self._check(rc, "map_lookup")
-        return tuple(v) if map_id in (MAP_IPV4_STATS, MAP_IPV6_STATS) else int(v[0])
+        vw = _value_words(map_id)
+        return tuple(v[:vw]) if vw > 1 else int(v[0])
 
     def map_update(self, map_id: int, key, value, flags: int = BPF_ANY):
         if map_id == MAP_STATS:
@@ -257,8 +274,9 @@ class FsxContext:
                                                  flags), "map_update")
             return
         k = _key_bytes(map_id, key)
-        if map_id in (MAP_IPV4_STATS, MAP_IPV6_STATS):
-            v = (C.c_uint64 * 3)(*value)
+        vw = _value_words(map_id)
+        if vw > 1:
+            v = (C.c_uint64 * vw)(*value)
         else:
             v = (C.c_uint64 * 1)(int(value))
         self._check(self._lib.fsx_map_update(self._h, map_id, k, v, flags), "map_update")
@@ -276,8 +294,8 @@ class FsxContext:
         cap = n.value
         if map_id == MAP_STATS:
             return {0: self.map_lookup(MAP_STATS, 0)}
-        klen = 16 if map_id in (MAP_IPV6_STATS, MAP_IPV6_BLACKLIST) else 4
-        vw = 3 if map_id in (MAP_IPV4_STATS, MAP_IPV6_STATS) else 1
+        klen = 16 if map_id in _V6_MAPS else 4
+        vw = _value_words(map_id)
         keys = np.zeros((max(cap, 1), klen), dtype=np.uint8)
         vals = np.zeros((max(cap, 1), vw), dtype=np.uint64)
         self._check(self._lib.fsx_map_dump(self._h, map_id, _ptr(keys), _ptr(vals), cap, C.byref(n)),
@@ -285,7 +303,7 @@ class FsxContext:
         m = min(cap, n.value)
         out = {}
         for i in range(m):
-            out[keys[i].tobytes()] = tuple(int(x) for x in vals[i]) if vw == 3 else int(vals[i, 0])
+            out[keys[i].tobytes()] = tuple(int(x) for x in vals[i]) if vw > 1 else int(vals[i, 0])
         return out
 
     def stats(self) -> tuple[int, int]:

@@ -58,14 +58,17 @@ extern "C" {
  * per-pass tile histograms (A/B measurements only). */
 #define FSX_FLAG_ONESWEEP_SORT 2u
 
-/* Map ids: the five maps of src/fsx_kern.c:56-94. */
+/* Map ids: the five maps of src/fsx_kern.c:56-94, then the token-bucket state maps of
+ * the build-defined token bucket (value fsx_tb_state). */
 enum fsx_map_id {
     FSX_MAP_STATS = 0,          /* stats_map          src/fsx_kern.c:56-62 */
     FSX_MAP_IPV4_STATS = 1,     /* ipv4_stats_map     src/fsx_kern.c:64-70 */
     FSX_MAP_IPV6_STATS = 2,     /* ipv6_stats_map     src/fsx_kern.c:72-78 */
     FSX_MAP_IPV4_BLACKLIST = 3, /* ipv4_blacklist_map src/fsx_kern.c:80-86 */
     FSX_MAP_IPV6_BLACKLIST = 4, /* ipv6_blacklist_map src/fsx_kern.c:88-94 */
-    FSX_MAP_COUNT = 5
+    FSX_MAP_IPV4_TOKENS = 5,    /* build-defined: key 4 B  -> fsx_tb_state */
+    FSX_MAP_IPV6_TOKENS = 6,    /* build-defined: key 16 B -> fsx_tb_state */
+    FSX_MAP_COUNT = 7
 };
 
 /* bpf_map_update_elem flags (linux/bpf.h). */
@@ -95,6 +98,15 @@ typedef struct fsx_ip_stats {
     uint64_t track_time;
 } fsx_ip_stats;
 
+/* Token-bucket state of one source (build-defined). */
+typedef struct fsx_tb_state {
+    uint64_t tokens;          /* nano-tokens (1e9 = one packet) */
+    uint64_t last;            /* ns of the last counted packet */
+} fsx_tb_state;
+
+/* Largest tb_burst (tokens) a token-bucket context accepts: capacity <= 2^61 nano-tokens. */
+#define FSX_TB_MAX_BURST 2305843009ull
+
 typedef struct fsx_config {
     uint64_t pps_threshold;   /* 1000       src/fsx_kern.c:309 */
     uint64_t bps_threshold;   /* 125000000  src/fsx_kern.c:310 */
@@ -105,7 +117,7 @@ typedef struct fsx_config {
                                  with -ENOSPC. */
     uint64_t max_batch;       /* largest n per call (device scratch is sized for it) */
     uint64_t tb_rate;         /* token bucket: refill in nano-tokens per ns (1000 = 1000 tok/s) */
-    uint64_t tb_burst;        /* token bucket: capacity in tokens */
+    uint64_t tb_burst;        /* token bucket: capacity in tokens (<= FSX_TB_MAX_BURST) */
     uint64_t hash_seed;       /* salt of the table/IPv6 sort hashes */
     int32_t limiter;          /* enum fsx_limiter */
     int32_t device;           /* HIP device ordinal */

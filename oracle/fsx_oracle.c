@@ -417,7 +417,10 @@ static int sliding_window_packet(fsxo_ctx *c, int v6, const uint8_t *key, uint32
  *   - new IP: tokens = C, last = now;
  *   - y = min(C, tokens + (now - last) * rate) (u64 wrap of now-last as the
  *     reference's window test; saturating multiply/add), last = now;
- *   - y >= 1e9: tokens = y - 1e9, PASS; else tokens = y, DROP (no blacklist). */
+ *   - y >= 1e9: tokens = y - 1e9, PASS; else tokens = 0, DROP (the partial token is
+ *     discarded: x' = max(0, y - 1e9), a clamp-add map, so the GPU evaluates the
+ *     recurrence as a scan); no blacklist insertions.
+ * Capacity burst * 1e9 must stay <= 2^61 (fsx_open rejects larger bursts). */
 #define TB_COST 1000000000ull
 static int token_bucket_packet(fsxo_ctx *c, int v6, const uint8_t *key, uint32_t len,
                                uint64_t now) {
@@ -447,7 +450,7 @@ static int token_bucket_packet(fsxo_ctx *c, int v6, const uint8_t *key, uint32_t
     }
     int v;
     if (y >= TB_COST) { ns.tokens = y - TB_COST; v = XDP_PASS; c->allowed++; }
-    else { ns.tokens = y; v = XDP_DROP; c->dropped++; }
+    else { ns.tokens = 0; v = XDP_DROP; c->dropped++; }
     ns.last = now;
     if (omap_update(tbm, key, &ns)) c->err = -ENOSPC;
     return v;

@@ -126,7 +126,7 @@ class Oracle:
         return int(s[0]), int(s[1])
 
     def map_update(self, map_id: int, key: bytes, value):
-        if map_id in (1, 2):
+        if map_id in (1, 2, 5, 6):
             v = np.array(value, dtype=np.uint64)
         else:
             v = np.array([value], dtype=np.uint64)
@@ -136,13 +136,13 @@ class Oracle:
             raise RuntimeError(f"oracle map update {rc}")
 
     def map_dump(self, map_id: int) -> dict:
-        klen = 16 if map_id in (2, 4) else 4
-        vw = 3 if map_id in (1, 2) else 1
+        klen = 16 if map_id in (2, 4, 6) else 4
+        vw = 3 if map_id in (1, 2) else 2 if map_id in (5, 6) else 1
         n = lib().fsxo_map_dump(self._h, map_id, None, None, 0)
         keys = np.zeros((max(n, 1), klen), dtype=np.uint8)
         vals = np.zeros((max(n, 1), vw), dtype=np.uint64)
         lib().fsxo_map_dump(self._h, map_id, _p(keys), _p(vals), n)
-        return {keys[i].tobytes(): (tuple(int(x) for x in vals[i]) if vw == 3 else int(vals[i, 0]))
+        return {keys[i].tobytes(): (tuple(int(x) for x in vals[i]) if vw > 1 else int(vals[i, 0]))
                 for i in range(n)}
 
 

@@ -1,0 +1,124 @@
+"""GPU parity of the build-defined limiters against the CPU oracle.
+
+The reference only names a token bucket and a sliding window (README.md:155-162), so
+these are parity-unpinned: the oracle (oracle/fsx_oracle.c) restates the in-repo spec
+sequentially, the GPU evaluates it in parallel (a segmented clamp-add scan for the
+token bucket), and the two must agree bit-exactly: verdicts, stats_map, the blacklist
+maps and the per-source limiter state maps.
+"""
+import zlib
+
+import numpy as np
+import pytest
+
+from test_gpu_parity import rand_stream
+
+pytestmark = pytest.mark.gpu
+
+TB = 2
+ORACLE_KEYS = ("pps_threshold", "bps_threshold", "window_ns", "block_ns", "max_entries",
+               "tb_rate", "tb_burst", "limiter")
+
+
+def run_limiter(native, oracle, batches, cfg, maps, rules=()):
+    cfg = dict(cfg)
+    cfg.setdefault("max_entries", 1 << 16)
+    okw = {k: v for k, v in cfg.items() if k in ORACLE_KEYS}
+    o = oracle.Oracle(**okw)
+    with native.FsxContext(max_batch=1 << 20, **cfg) as c:
+        for mid, key, val in rules:
+            c.map_update(mid, key, val)
+            o.map_update(mid, key, val)
+        for hdr, ln, ts in batches:
+            vg = c.verdict_batch(hdr, ln, ts)
+            vo = o.batch(hdr, ln, ts)
+            bad = np.nonzero(vg != vo)[0]
+            assert bad.size == 0, f"{bad.size} verdicts differ, first at {bad[:8]}"
+        assert c.stats() == o.stats()
+        for m in maps:
+            g, r = c.map_dump(m), o.map_dump(m)
+            assert len(g) == len(r), (m, len(g), len(r))
+            assert g == r, m
+        return c.stats()
+
+
+TB_MAPS = (3, 4, 5, 6)
+TB_CFGS = {
+    "default": {},                                         # 1000 tok/s, burst 1000
+    "mixed": {"tb_rate": 300_000, "tb_burst": 4},          # heavy sources alternate
+    "slow": {"tb_rate": 20_000, "tb_burst": 2},
+    "no_refill": {"tb_rate": 0, "tb_burst": 3},
+    "burst_zero": {"tb_rate": 10**6, "tb_burst": 0},      # capacity < cost: all drop
+    "saturating": {"tb_rate": 1 << 40, "tb_burst": 1},
+    "max_burst": {"tb_rate": 1 << 20, "tb_burst": 2305843009},
+}
+
+
+@pytest.mark.parametrize("name", list(TB_CFGS))
+def test_token_bucket_random(native, oracle, name):
+    rng = np.random.default_rng(zlib.crc32(b"tb" + name.encode()))
+    hdr, ln, ts = rand_stream(rng, 60000, 300, dt_max=400)
+    st = run_limiter(native, oracle, [(hdr, ln, ts)], dict(limiter=TB, **TB_CFGS[name]), TB_MAPS)
+    if name == "burst_zero":
+        assert st[0] == 0
+    if name == "mixed":
+        assert st[0] > 1000 and st[1] > 1000
+
+
+def test_token_bucket_mixed_families(native, oracle):
+    rng = np.random.default_rng(21)
+    hdr, ln, ts = rand_stream(rng, 40000, 600, dt_max=300, v6_frac=0.4, nonip_frac=0.05,
+                              short_frac=0.03)
+    run_limiter(native, oracle, [(hdr, ln, ts)], dict(limiter=TB, **TB_CFGS["mixed"]), TB_MAPS)
+
+
+def test_token_bucket_state_carry(native, oracle):
+    rng = np.random.default_rng(22)
+    hdr, ln, ts = rand_stream(rng, 30000, 200, dt_max=300, v6_frac=0.2)
+    cuts = [0, 1, 2, 777, 4096, 4097, 17000, 29999, 30000]
+    batches = [(hdr[a:b], ln[a:b], ts[a:b]) for a, b in zip(cuts[:-1], cuts[1:])]
+    run_limiter(native, oracle, batches, dict(limiter=TB, **TB_CFGS["mixed"]), TB_MAPS)
+
+
+def test_token_bucket_heavy_source(native, oracle):
+    """One source with most packets of a 300k-packet batch: a segment spanning ~60 scan
+    tiles, alternating verdicts inside one tile."""
+    rng = np.random.default_rng(23)
+    hdr, ln, ts = rand_stream(rng, 300000, 8, dt_max=100)
+    run_limiter(native, oracle, [(hdr, ln, ts)], dict(limiter=TB, tb_rate=4_000_000, tb_burst=7),
+                TB_MAPS)
+
+
+def test_token_bucket_non_monotone_clock(native, oracle):
+    rng = np.random.default_rng(24)
+    hdr, ln, ts = rand_stream(rng, 20000, 100, dt_max=200)
+    sw = rng.choice(len(ts), 3000, replace=False)
+    ts[sw] = ts[sw] - rng.integers(0, 50000, sw.size).astype(np.uint64)
+    ts[7] = np.uint64(2**64 - 3)
+    run_limiter(native, oracle, [(hdr, ln, ts)], dict(limiter=TB, **TB_CFGS["mixed"]), TB_MAPS)
+
+
+def test_token_bucket_with_rules_and_state_updates(native, oracle):
+    """Static and expiring blacklist rules apply before the bucket (src/fsx_kern.c:159-216
+    semantics); user-written bucket states are honoured."""
+    rng = np.random.default_rng(25)
+    hdr, ln, ts = rand_stream(rng, 30000, 60, dt_max=300)
+    srcs = sorted({bytes(hdr[i, 26:30]) for i in range(0, 30000, 97)})
+    t_mid = int(ts[15000])
+    rules = []
+    for i, k in enumerate(srcs[:24]):
+        if i % 4 == 0:
+            rules.append((3, k, 2**64 - 1))          # static block
+        elif i % 4 == 1:
+            rules.append((3, k, t_mid))              # expires mid-batch
+        elif i % 4 == 2:
+            rules.append((3, k, 0))                  # till = 0: ignored (:189)
+        else:
+            rules.append((5, k, (123_456_789, int(ts[0]) - 10)))  # preset bucket state
+    batches = [(hdr[:15000], ln[:15000], ts[:15000]), (hdr[15000:], ln[15000:], ts[15000:])]
+    run_limiter(native, oracle, batches, dict(limiter=TB, **TB_CFGS["mixed"]), TB_MAPS, rules)
+
+
+def test_token_bucket_rejects_oversized_burst(native):
+    with pytest.raises(native.FsxError):
+        native.FsxContext(limiter=TB, tb_burst=2305843010)
