@@ -49,6 +49,8 @@ struct fsx_ctx {
     float *d_prob = nullptr;
     uint8_t *d_dec = nullptr;
     uint64_t score_cap = 0;
+    // sliding-window history (limiter == FSX_LIMIT_SLIDING_WINDOW only)
+    HistBufs hist{};
     // per-source flow accumulators
     void *d_flow_acc = nullptr;
     uint64_t flow_acc_cap = 0;
@@ -107,7 +109,7 @@ static void free_scratch(fsx_ctx *c) {
     hipFree(s.tile_aux); hipFree(s.tile_last); hipFree(s.fix_list); hipFree(s.fix_bitmap);
     hipFree(s.seg_order); hipFree(s.sub_cnt); hipFree(s.flow_first); hipFree(s.flow_last);
     hipFree(s.span_list); hipFree(s.sort_ctl); hipFree(s.gbase); hipFree(s.status);
-    hipFree(s.lim_tiles);
+    hipFree(s.lim_tiles); hipFree(s.sw_seg);
     s = Scratch{};
 }
 
@@ -140,6 +142,7 @@ static int alloc_scratch(fsx_ctx *c, uint64_t cap) {
     HIPCHK(c, hipMemset(s.status, 0, (cap / kSortTile + 2) * 256 * 8));
     s.lim_tiles_n = cap / kTile + 2;
     HIPCHK(c, hipMalloc(&s.lim_tiles, s.lim_tiles_n * 4 * 8));
+    if (c->cfg.limiter == FSX_LIMIT_SLIDING_WINDOW) HIPCHK(c, hipMalloc(&s.sw_seg, cap * sizeof(SwSeg)));
     s.cap = cap;
     return 0;
 }
@@ -180,6 +183,8 @@ void fsx_close(fsx_ctx *c) {
     hipFree(c->d_hdr); hipFree(c->d_len); hipFree(c->d_ts); hipFree(c->d_verdict);
     hipFree(c->d_feat); hipFree(c->d_prob); hipFree(c->d_dec); hipFree(c->d_flow_acc);
     hipFree(c->d_res); hipFree(c->d_val);
+    for (int b = 0; b < 2; ++b) { hipFree(c->hist.t[b]); hipFree(c->hist.l[b]); }
+    hipFree(c->hist.tile_cnt); hipFree(c->hist.tile_off); hipFree(c->hist.total);
     for (int r = 0; r < kRing; ++r)
         for (int i = 0; i < kMaxEv; ++i) if (c->ev[r][i]) hipEventDestroy(c->ev[r][i]);
     if (c->own_stream) hipStreamDestroy(c->own_stream);
@@ -196,6 +201,8 @@ int fsx_open(fsx_ctx **out, const fsx_config *cfg) {
     if (k.limiter < FSX_LIMIT_FIXED_WINDOW || k.limiter > FSX_LIMIT_TOKEN_BUCKET) return -EINVAL;
     // token bucket: capacity burst * 1e9 nano-tokens must stay <= 2^61
     if (k.limiter == FSX_LIMIT_TOKEN_BUCKET && k.tb_burst > FSX_TB_MAX_BURST) return -EINVAL;
+    // sliding window: a carried log holds <= pps_threshold entries (24-bit count)
+    if (k.limiter == FSX_LIMIT_SLIDING_WINDOW && k.pps_threshold > FSX_SW_MAX_PPS) return -EINVAL;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return -ENODEV;
     if (k.device < 0 || k.device >= ndev) return -EINVAL;
@@ -218,11 +225,24 @@ int fsx_open(fsx_ctx **out, const fsx_config *cfg) {
     if (hipMemset(c->tstate, 0, sizeof(TableState)) != hipSuccess) return fail(-EIO);
     if (hipMemset(c->bs, 0, sizeof(BatchState)) != hipSuccess) return fail(-EIO);
     if (alloc_scratch(c, k.max_batch)) return fail(-ENOMEM);
+    if (k.limiter == FSX_LIMIT_SLIDING_WINDOW) {
+        HistBufs &h = c->hist;
+        h.cap = std::max<uint64_t>(2 * k.max_batch, 1u << 16);
+        const uint64_t stiles = c->slots / 4096 + 1;
+        for (int b = 0; b < 2; ++b) {
+            if (hipMalloc(&h.t[b], h.cap * 8) != hipSuccess) return fail(-ENOMEM);
+            if (hipMalloc(&h.l[b], h.cap * 4) != hipSuccess) return fail(-ENOMEM);
+        }
+        if (hipMalloc(&h.tile_cnt, stiles * 4) != hipSuccess) return fail(-ENOMEM);
+        if (hipMalloc(&h.tile_off, stiles * 8) != hipSuccess) return fail(-ENOMEM);
+        if (hipMalloc(&h.total, 8) != hipSuccess) return fail(-ENOMEM);
+    }
     Limits &L = c->lim;
     L.pps = k.pps_threshold; L.bps = k.bps_threshold; L.window = k.window_ns; L.block = k.block_ns;
     L.tb_rate = k.tb_rate;
     L.tb_cap = std::min<uint64_t>(k.tb_burst, FSX_TB_MAX_BURST) * 1000000000ull;
     L.max_entries = k.max_entries;
+    L.hist_cap = c->hist.cap;
     L.table_mask = c->slots - 1;
     L.seed = mix64(k.hash_seed);
     L.salt32 = (uint32_t)(mix64(k.hash_seed ^ 0xABCDEFull) >> 32);
@@ -247,6 +267,9 @@ static int check_batch(fsx_ctx *c) {
     if (h.err & ERR_TABLE_FULL)
         return set_err(c, -ENOSPC, "map full: more than max_entries=%llu source IPs",
                        (unsigned long long)c->cfg.max_entries);
+    if (h.err & ERR_HIST_FULL)
+        return set_err(c, -ENOSPC, "sliding-window history full: carried logs + batch > %llu entries",
+                       (unsigned long long)c->hist.cap);
     if (h.err) return set_err(c, -EIO, "device error flags 0x%x", h.err);
     return 0;
 }
@@ -291,8 +314,6 @@ static int run_batch(fsx_ctx *c, const uint8_t *d_hdr, const uint32_t *d_len, co
     int rc = sel(c);
     if (rc) return rc;
     if (c->pending) { rc = fsx_sync(c); if (rc) return rc; }
-    if (do_limit && c->cfg.limiter == FSX_LIMIT_SLIDING_WINDOW)
-        return set_err(c, -EOPNOTSUPP, "limiter %d not built into this pipeline yet", c->cfg.limiter);
     FlowRequest frq;
     if (fr) {
         frq = *fr;
@@ -319,8 +340,8 @@ static int run_batch(fsx_ctx *c, const uint8_t *d_hdr, const uint32_t *d_len, co
         c->ring_n++;
     }
     hipError_t e = launch_verdict_pipeline(d_hdr, d_len, d_ts, (uint32_t)n, d_verdict, c->table,
-                                           c->tstate, c->bs, c->sc, c->lim, do_limit, fr, c->stream,
-                                           ev, kMaxEv, used, names);
+                                           c->tstate, c->bs, c->sc, c->lim, do_limit, fr, c->hist,
+                                           c->stream, ev, kMaxEv, used, names);
     if (e != hipSuccess) return set_err(c, -EIO, "pipeline launch: %s", hipGetErrorString(e));
     c->pending = true;
     return 0;

@@ -840,6 +840,12 @@ __global__ __launch_bounds__(256) void k_insert(const uint64_t *__restrict__ S, 
                                                 uint32_t *__restrict__ seg_slot,
                                                 const uint8_t *__restrict__ hdr, Slot *table,
                                                 TableState *tstate, Limits lim) {
+    // sliding window: the carried logs plus every packet of this batch must fit the
+    // history buffer (conservative; checked before any state changes)
+    if (lim.limiter == 1 && tstate->hist_total + bs->n_valid > lim.hist_cap) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(&bs->err, ERR_HIST_FULL);
+        return;
+    }
     const uint32_t nnew = bs->n_new;
     if (nnew == 0) return;
     // capacity for the whole batch is checked once: a batch that would overflow the
@@ -1343,8 +1349,9 @@ static uint32_t next_generation() {
 hipError_t launch_verdict_pipeline(const uint8_t *hdr, const uint32_t *len, const uint64_t *ts,
                                    uint32_t n, uint8_t *verdict, Slot *table, TableState *tstate,
                                    BatchState *bs, const Scratch &sc, const Limits &lim,
-                                   bool do_limit, const FlowRequest *flows, hipStream_t st,
-                                   hipEvent_t *ev, int nev, int *nev_used, const char **names) {
+                                   bool do_limit, const FlowRequest *flows, const HistBufs &hist,
+                                   hipStream_t st, hipEvent_t *ev, int nev, int *nev_used,
+                                   const char **names) {
     int ei = 0;
     auto mark = [&](const char *name) {
         if (ev && ei < nev) {
@@ -1431,12 +1438,18 @@ hipError_t launch_verdict_pipeline(const uint8_t *hdr, const uint32_t *len, cons
         k_seg_scan<<<1, 1024, 0, st>>>(sc.hist, cls);
         k_seg_order<<<kSegBlocks, 256, 0, st>>>(bs, sc.seg_start, sc.hist, sc.seg_order);
         mark("k_seg_order");
-        k_walk_fixed<<<gridStream, 256, 0, st>>>(S, bs, sc.seg_start, sc.seg_slot, ts, len, sc.pay[0],
-                                                 sc.seg_order, cls, sc.marks, table, lim);
-        mark("k_walk_fixed");
-        k_walk_fixed_long<<<1024, 256, 0, st>>>(S, bs, sc.seg_start, sc.seg_slot, ts, len, sc.pay[0],
-                                                sc.seg_order, cls, sc.marks, table, lim);
-        mark("k_walk_fixed_long");
+        if (lim.limiter == 1) {   // FSX_LIMIT_SLIDING_WINDOW
+            if ((e = launch_sliding_window(S, ts, len, bs, sc, table, tstate, hist, lim, n, st)) != hipSuccess)
+                return e;
+            mark("k_sliding_window");
+        } else {
+            k_walk_fixed<<<gridStream, 256, 0, st>>>(S, bs, sc.seg_start, sc.seg_slot, ts, len, sc.pay[0],
+                                                     sc.seg_order, cls, sc.marks, table, lim);
+            mark("k_walk_fixed");
+            k_walk_fixed_long<<<1024, 256, 0, st>>>(S, bs, sc.seg_start, sc.seg_slot, ts, len, sc.pay[0],
+                                                    sc.seg_order, cls, sc.marks, table, lim);
+            mark("k_walk_fixed_long");
+        }
     }
     k_fill_last<<<gridTiles, 256, 0, st>>>(sc.marks, bs, sc.tile_last);
     k_fill_carry<<<1, 1024, 0, st>>>(sc.tile_last, bs);

@@ -31,6 +31,7 @@ enum : uint32_t {
     ERR_PROBE = 2u,
     ERR_FIXUP = 4u,
     ERR_SORT_HANG = 8u,
+    ERR_HIST_FULL = 16u,
 };
 
 enum : uint32_t { SLOT_HAS_ST = 1u, SLOT_HAS_BL = 2u, SLOT_HAS_TB = 4u };
@@ -80,12 +81,43 @@ constexpr uint64_t kPayTsRange = 1ull << (64 - kPayLenBits);
 struct TableState {
     uint64_t count;       // occupied slots
     uint64_t stats[2];    // stats_map {allowed, dropped}, src/fsx_struct.h:11-15
+    // sliding window: carried logs and the clock facts pruning needs
+    uint64_t hist_total;  // entries in the current history buffer
+    uint64_t last_max_ts; // largest timestamp of all batches so far
+    uint32_t ever_nonmono;  // some batch (or batch boundary) went back in time
+    uint32_t hist_cur;    // which of the two history buffers is current
+    uint32_t max_len_seen;  // largest frame length of all batches so far
+    uint32_t pad_;
+};
+
+// Sliding-window logs carried between batches: per source, the log of counted packets
+// still inside the window (<= pps_threshold entries, oldest first), packed by source in
+// one of two ping-pong buffers. Slot.aux = offset << kHistCntBits | count.
+constexpr uint32_t kHistCntBits = 24;
+constexpr uint64_t kAuxWalked = 1ull << 63;   // Slot.aux during a batch: walked segment id
+
+struct HistBufs {
+    uint64_t *t[2];
+    uint32_t *l[2];
+    uint64_t cap;
+    uint32_t *tile_cnt;   // per 4096 table slots: surviving log entries
+    uint64_t *tile_off;   // their exclusive scan
+    uint64_t *total;      // entries after the rebuild
+};
+
+// Per walked source: the final log as a virtual range [lo, hi) over its old history
+// (hoff, m) followed by its sorted positions j0, j0+1, ...
+struct SwSeg {
+    uint64_t hoff;
+    uint32_t m, j0, lo, hi;
+    uint32_t pad_[2];
 };
 
 struct Limits {           // the rate-limiter constants, src/fsx_kern.c:245,308-310
     uint64_t pps, bps, window, block;
     uint64_t tb_rate, tb_cap;  // token bucket, nano-tokens
     uint64_t max_entries;
+    uint64_t hist_cap;    // sliding window: history entries per buffer
     uint64_t table_mask;
     uint64_t seed;
     uint32_t salt32;
@@ -152,6 +184,7 @@ struct Scratch {
     unsigned long long *status;  // onesweep look-back words, 256 per tile
     uint64_t *lim_tiles;   // limiter scans: 4 u64 per kTile tile (token bucket: map + carry)
     uint64_t lim_tiles_n;  // tiles lim_tiles is sized for
+    SwSeg *sw_seg;         // sliding window: per source (null for other limiters)
     uint64_t cap;          // packets the scratch is sized for
 };
 
@@ -171,14 +204,19 @@ struct FlowRequest {
 hipError_t launch_verdict_pipeline(const uint8_t *hdr, const uint32_t *len, const uint64_t *ts,
                                    uint32_t n, uint8_t *verdict, Slot *table, TableState *tstate,
                                    BatchState *bs, const Scratch &sc, const Limits &lim,
-                                   bool do_limit, const FlowRequest *flows, hipStream_t st,
-                                   hipEvent_t *ev, int nev, int *nev_used, const char **names);
+                                   bool do_limit, const FlowRequest *flows, const HistBufs &hist,
+                                   hipStream_t st, hipEvent_t *ev, int nev, int *nev_used,
+                                   const char **names);
 
 // Build-defined limiters (fsx_limiters.hip), after the table lookup/insert of a batch:
 // one verdict mark per sorted position, final per-source state in the table.
 hipError_t launch_token_bucket(const uint64_t *S, const uint64_t *ts, const uint32_t *len, BatchState *bs,
                                const Scratch &sc, Slot *table, const Limits &lim, uint32_t n,
                                hipStream_t st);
+
+hipError_t launch_sliding_window(const uint64_t *S, const uint64_t *ts, const uint32_t *len, BatchState *bs,
+                                 const Scratch &sc, Slot *table, TableState *tstate, const HistBufs &hb,
+                                 const Limits &lim, uint32_t n, hipStream_t st);
 
 hipError_t launch_flows(const uint64_t *S, const uint64_t *pay, BatchState *bs, const uint8_t *headf, const uint32_t *len,
                         const uint64_t *ts, const uint8_t *hdr, const uint32_t *tile_off,

@@ -21,6 +21,21 @@
 //   k_tb_carry    one block: state entering every tile
 //   k_tb_tiles<1> per tile: replay the tile from its entering state, verdict marks, the
 //                 final {tokens, last} of every source ending in the tile
+//
+// Sliding window. Per counted packet: expire the source's log from the
+// oldest entry while now - t_oldest >= W, append, count = |log|, bytes = sum of lengths;
+// count > P or bytes > B -> blacklist until now + BLK, clear the log, DROP. The log of
+// a source is a contiguous range of the virtual sequence "carried history, then the
+// source's sorted positions from its first counted one", so a walker only moves two
+// indices. With monotone clocks (and no byte trigger possible before the count one)
+// packet q triggers iff t_q - t_{q-P} < W inside its phase: a wave tests 64 positions
+// per step, then jumps over the blacklisted run with a search.
+//   k_walk_sw / k_walk_sw_long  short segments one thread (exact), long ones one wave
+//   k_sw_hist_count/scan/write  rebuild the carried logs, packed per source, in the
+//                               other history buffer; with monotone clocks entries at
+//                               least W behind the newest timestamp are dropped (they
+//                               would be expired by any later packet)
+//   k_sw_finish                 flip the buffers, clock facts for the next batch
 #include <hip/hip_runtime.h>
 
 #include "fsx_dev_common.h"
@@ -324,6 +339,396 @@ hipError_t launch_token_bucket(const uint64_t *S, const uint64_t *ts, const uint
     k_tb_tiles<true><<<gridTiles, 256, 0, st>>>(S, bs, ts, len, sc.pay[0], sc.headf, sc.tile_aux, seg_j,
                                                 seg_x, sc.seg_slot, table, lim, tile_map, tile_x,
                                                 sc.marks);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------ sliding window
+// The virtual sequence of one source: its carried log (hoff, m) then its sorted
+// positions j0, j0+1, ...
+template <class SV>
+struct VView {
+    SV sv;
+    const uint64_t *ht;
+    const uint32_t *hl;
+    uint64_t hoff;
+    uint32_t m, j0;
+    __device__ __forceinline__ uint64_t t(uint32_t v) const { return v < m ? ht[hoff + v] : sv.t(j0 + (v - m)); }
+    __device__ __forceinline__ uint32_t l(uint32_t v) const { return v < m ? hl[hoff + v] : sv.l(j0 + (v - m)); }
+};
+
+struct SwState {
+    bool has_st, has_bl;
+    uint64_t pps, bps, tt, till;
+};
+
+__device__ __forceinline__ SwState sw_load(const Slot &sl) {
+    return SwState{(sl.flags & SLOT_HAS_ST) != 0, (sl.flags & SLOT_HAS_BL) != 0, sl.pps, sl.bps, sl.tt, sl.till};
+}
+__device__ __forceinline__ void sw_store(Slot &sl, const SwState &s, uint32_t g) {
+    sl.flags = (sl.flags & ~(SLOT_HAS_ST | SLOT_HAS_BL)) | (s.has_st ? SLOT_HAS_ST : 0u) |
+               (s.has_bl ? SLOT_HAS_BL : 0u);
+    sl.pps = s.pps; sl.bps = s.bps; sl.tt = s.tt; sl.till = s.till;
+    sl.aux = kAuxWalked | g;
+}
+__device__ __forceinline__ void sw_hist_of(uint64_t aux, uint64_t &hoff, uint32_t &m) {
+    hoff = aux >> kHistCntBits;
+    m = (uint32_t)(aux & ((1ull << kHistCntBits) - 1));
+}
+
+// Exact sequential replay (any clock, u64 wraparound as the oracle).
+template <class SV>
+__device__ void sw_walk_exact(const SV &sv, uint32_t a, uint32_t b, const Limits &lim,
+                              const uint64_t *ht, const uint32_t *hl, uint64_t hoff, uint32_t m,
+                              MarkWriter<false> &mw, SwState &s, SwSeg &rec) {
+    uint32_t q = a;
+    if (s.has_bl && s.till > 0) {                           // src/fsx_kern.c:189-215 semantics
+        while (q < b && !(sv.t(q) > s.till)) { mw.emit(q, XDP_DROP); ++q; }
+        if (q < b) s.has_bl = false;
+    }
+    const uint32_t j0 = q;
+    const VView<SV> vv{sv, ht, hl, hoff, m, j0};
+    uint32_t lo = 0;
+    uint64_t bytes = 0;
+    for (uint32_t v = 0; v < m; ++v) bytes += hl[hoff + v];
+    bool cleared = false;
+    for (; q < b; ++q) {
+        const uint64_t now = sv.t(q);
+        if (s.has_bl && s.till > 0) {
+            if (now > s.till) s.has_bl = false;
+            else { mw.emit(q, XDP_DROP); continue; }
+        }
+        const uint32_t v = m + (q - j0);
+        if (cleared) { lo = v; bytes = 0; cleared = false; }
+        while (lo < v && now - vv.t(lo) >= lim.window) { bytes -= vv.l(lo); ++lo; }
+        bytes += sv.l(q);
+        const uint64_t cnt = (uint64_t)(v - lo) + 1;
+        s.has_st = true; s.pps = cnt; s.bps = bytes; s.tt = vv.t(lo);
+        if (cnt > lim.pps || bytes > lim.bps) {
+            s.till = now + lim.block; s.has_bl = true;
+            cleared = true;
+            mw.emit(q, XDP_DROP);
+        } else {
+            mw.emit(q, XDP_PASS);
+        }
+    }
+    rec.hoff = hoff; rec.m = m; rec.j0 = j0;
+    if (cleared) { rec.lo = 0; rec.hi = 0; }
+    else { rec.lo = lo; rec.hi = m + (b - j0); }
+}
+
+// Stats of the log [lo, v] (wave): {count, bytes, oldest timestamp}.
+template <class VV>
+__device__ __forceinline__ void sw_stats_wave(const VV &vv, uint32_t lo, uint32_t v, SwState &s) {
+    s.has_st = true;
+    s.pps = (uint64_t)(v - lo) + 1;
+    s.bps = sum_len<true>(vv, lo, v + 1);
+    s.tt = vv.t(lo);
+}
+
+// Oldest log entry at packet time tq: first v in [f, vq] with tq - t(v) < W (monotone).
+template <class VV>
+__device__ __forceinline__ uint32_t sw_log_start(const VV &vv, uint32_t f, uint32_t vq, uint64_t tq, uint64_t W) {
+    if (tq < W) return f;
+    const uint32_t lo = wave_gallop_gt(vv, f, vq + 1, tq - W);
+    return lo < vq ? lo : vq;
+}
+
+// Monotone clocks, no byte trigger possible before the count trigger, no u64 overflow.
+template <class SV>
+__device__ void sw_walk_fast_wave(const SV &sv, uint32_t a, uint32_t b, const Limits &lim,
+                                  const uint64_t *ht, const uint32_t *hl, uint64_t hoff, uint32_t m,
+                                  MarkWriter<true> &mw, SwState &s, SwSeg &rec) {
+    const uint32_t lane = lane_id();
+    const uint64_t P = lim.pps, W = lim.window;
+    uint32_t p = a;
+    if (s.has_bl && s.till > 0) {
+        p = wave_gallop_gt(sv, a, b, s.till);
+        if (p > a) mw.emit(a, XDP_DROP);
+        if (p < b) s.has_bl = false;
+    }
+    const uint32_t j0 = p;
+    const VView<SV> vv{sv, ht, hl, hoff, m, j0};
+    rec.hoff = hoff; rec.m = m; rec.j0 = j0;
+    rec.lo = 0; rec.hi = m;                 // no counted packet: the log is unchanged
+    uint32_t f = 0;                         // first virtual index of the current log
+    while (p < b) {
+        uint32_t k = b;                     // first count trigger at or after p
+        for (uint32_t q0 = p; q0 < b; q0 += 64) {
+            const uint32_t q = q0 + lane;
+            bool pr = false;
+            if (q < b) {
+                const uint32_t v = m + (q - j0);
+                if (P == 0) pr = true;
+                else if ((uint64_t)v >= (uint64_t)f + P) pr = sv.t(q) - vv.t(v - (uint32_t)P) < W;
+            }
+            const uint64_t bal = __ballot(pr);
+            if (bal) { k = q0 + (uint32_t)__ffsll((unsigned long long)bal) - 1u; break; }
+        }
+        if (k >= b) {                       // the phase runs to the end of the batch
+            mw.emit(p, XDP_PASS);
+            const uint32_t vl = m + (b - 1 - j0);
+            const uint32_t lo = sw_log_start(vv, f, vl, sv.t(b - 1), W);
+            sw_stats_wave(vv, lo, vl, s);
+            rec.lo = lo; rec.hi = vl + 1;
+            break;
+        }
+        if (k > p) mw.emit(p, XDP_PASS);
+        mw.emit(k, XDP_DROP);
+        const uint32_t vk = m + (k - j0);
+        const uint64_t tk = sv.t(k);
+        sw_stats_wave(vv, sw_log_start(vv, f, vk, tk, W), vk, s);
+        s.till = tk + lim.block;
+        s.has_bl = true;
+        rec.lo = 0; rec.hi = 0;             // log cleared
+        const uint32_t j = wave_gallop_gt(sv, k + 1, b, s.till);
+        if (j >= b) break;                  // blacklisted to the end of the batch
+        s.has_bl = false;                   // deleted at packet j
+        f = m + (j - j0);
+        p = j;
+    }
+}
+
+__device__ __forceinline__ bool sw_mono(const BatchState *bs, const TableState *ts) {
+    return !bs->nonmono && !ts->ever_nonmono && ~bs->inv_min_ts >= ts->last_max_ts;
+}
+
+template <class SV>
+__device__ __forceinline__ void sw_short_body(const SV &sv, const BatchState *bs, const uint32_t *seg_start,
+                                              const uint32_t *seg_slot, const uint32_t *order,
+                                              const uint32_t *cls, uint8_t *marks, Slot *table,
+                                              const Limits &lim, const uint64_t *ht, const uint32_t *hl,
+                                              SwSeg *segs) {
+    const uint32_t nshort = bs->nseg - cls[kSegClasses - 1];
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < nshort; i += gridDim.x * 256u) {
+        const uint32_t g = order[i];
+        const uint32_t a = seg_start[g], b = seg_start[g + 1];
+        Slot &sl = table[seg_slot[g]];
+        SwState st = sw_load(sl);
+        uint64_t hoff;
+        uint32_t m;
+        sw_hist_of(sl.aux, hoff, m);
+        MarkWriter<false> mw{marks, 0};
+        SwSeg rec{};
+        sw_walk_exact(sv, a, b, lim, ht, hl, hoff, m, mw, st, rec);
+        segs[g] = rec;
+        sw_store(sl, st, g);
+    }
+}
+
+template <class SV>
+__device__ __forceinline__ void sw_long_body(const SV &sv, const BatchState *bs, const TableState *tst,
+                                             const uint32_t *seg_start, const uint32_t *seg_slot,
+                                             const uint32_t *order, const uint32_t *cls, uint8_t *marks,
+                                             Slot *table, const Limits &lim, const uint64_t *ht,
+                                             const uint32_t *hl, SwSeg *segs) {
+    const uint32_t nl = cls[kSegClasses - 1], first = bs->nseg - nl;
+    const uint32_t maxL = bs->max_len > tst->max_len_seen ? bs->max_len : tst->max_len_seen;
+    const uint64_t lim_ts = lim.window > lim.block ? lim.window : lim.block;
+    const bool fast = sw_mono(bs, tst) && lim.pps * (uint64_t)maxL <= lim.bps &&
+                      bs->max_ts <= ~0ull - lim_ts;
+    const uint32_t lane = lane_id();
+    for (uint32_t i = blockIdx.x * 4u + (threadIdx.x >> 6); i < nl; i += gridDim.x * 4u) {
+        const uint32_t g = order[first + i];
+        const uint32_t a = seg_start[g], b = seg_start[g + 1];
+        Slot &sl = table[seg_slot[g]];
+        SwState st = sw_load(sl);
+        uint64_t hoff;
+        uint32_t m;
+        sw_hist_of(sl.aux, hoff, m);
+        SwSeg rec{};
+        if (fast) {
+            MarkWriter<true> mw{marks, 0};
+            sw_walk_fast_wave(sv, a, b, lim, ht, hl, hoff, m, mw, st, rec);
+        } else if (lane == 0) {
+            MarkWriter<false> mw{marks, 0};
+            sw_walk_exact(sv, a, b, lim, ht, hl, hoff, m, mw, st, rec);
+        }
+        if (lane == 0) {
+            segs[g] = rec;
+            sw_store(sl, st, g);
+        }
+    }
+}
+
+template <bool kLong>
+__global__ __launch_bounds__(256) void k_walk_sw(const uint64_t *__restrict__ S, BatchState *bs,
+                                                 const TableState *tst,
+                                                 const uint32_t *__restrict__ seg_start,
+                                                 const uint32_t *__restrict__ seg_slot,
+                                                 const uint64_t *__restrict__ ts,
+                                                 const uint32_t *__restrict__ len,
+                                                 const uint64_t *__restrict__ pay,
+                                                 const uint32_t *__restrict__ order,
+                                                 const uint32_t *__restrict__ cls,
+                                                 uint8_t *__restrict__ marks, Slot *table, Limits lim,
+                                                 HistBufs hb, SwSeg *__restrict__ segs) {
+    if (bs->err) return;
+    const uint32_t cur = tst->hist_cur;
+    const uint64_t *ht = hb.t[cur];
+    const uint32_t *hl = hb.l[cur];
+    if (bs->pay_ok) {
+        const SegView<true> sv{S, ts, len, pay, ~bs->inv_min_ts};
+        if constexpr (kLong) sw_long_body(sv, bs, tst, seg_start, seg_slot, order, cls, marks, table, lim, ht, hl, segs);
+        else sw_short_body(sv, bs, seg_start, seg_slot, order, cls, marks, table, lim, ht, hl, segs);
+    } else {
+        const SegView<false> sv{S, ts, len, pay, 0};
+        if constexpr (kLong) sw_long_body(sv, bs, tst, seg_start, seg_slot, order, cls, marks, table, lim, ht, hl, segs);
+        else sw_short_body(sv, bs, seg_start, seg_slot, order, cls, marks, table, lim, ht, hl, segs);
+    }
+}
+
+// The surviving carried log of table slot i as a virtual range [lo, hi) (pruned), and
+// its view parameters. Returns false for an empty slot / no log.
+template <class SV>
+__device__ __forceinline__ uint32_t sw_slot_log(const SV &sv, const Slot &sl, const SwSeg *segs,
+                                                const uint64_t *ht, const uint32_t *hl, bool prune,
+                                                uint64_t cutoff, SwSeg &r) {
+    if (sl.tag == 0 || sl.aux == 0) return 0;
+    if (sl.aux & kAuxWalked) {
+        r = segs[(uint32_t)(sl.aux & 0xFFFFFFFFull)];
+    } else {
+        sw_hist_of(sl.aux, r.hoff, r.m);
+        r.j0 = 0; r.lo = 0; r.hi = r.m;
+    }
+    if (r.lo >= r.hi) return 0;
+    if (prune) {   // drop entries with t <= cutoff (= newest timestamp - W): a prefix
+        const VView<SV> vv{sv, ht, hl, r.hoff, r.m, r.j0};
+        r.lo = gallop_gt(vv, r.lo, r.hi, cutoff);
+    }
+    return r.hi - r.lo;
+}
+
+constexpr uint32_t kSlotTile = 4096;   // table slots per block in the history rebuild
+
+struct SwClock {
+    bool prune;
+    uint64_t cutoff;
+};
+
+__device__ __forceinline__ SwClock sw_clock(const BatchState *bs, const TableState *tst, const Limits &lim) {
+    const uint64_t T = bs->max_ts > tst->last_max_ts ? bs->max_ts : tst->last_max_ts;
+    return SwClock{sw_mono(bs, tst) && T >= lim.window, T - lim.window};
+}
+
+template <bool kWrite>
+__global__ __launch_bounds__(256) void k_sw_hist(const uint64_t *__restrict__ S, const BatchState *bs,
+                                                 const TableState *tst, const uint64_t *__restrict__ ts,
+                                                 const uint32_t *__restrict__ len,
+                                                 const uint64_t *__restrict__ pay, Slot *table,
+                                                 Limits lim, HistBufs hb, const SwSeg *__restrict__ segs) {
+    __shared__ uint32_t s_tmp[4];
+    if (bs->err) return;
+    const uint64_t nslots = lim.table_mask + 1;
+    const uint64_t ntiles = (nslots + kSlotTile - 1) / kSlotTile;
+    const uint32_t cur = tst->hist_cur;
+    const uint64_t *ht = hb.t[cur];
+    const uint32_t *hl = hb.l[cur];
+    uint64_t *nt = hb.t[cur ^ 1u];
+    uint32_t *nl = hb.l[cur ^ 1u];
+    const SwClock ck = sw_clock(bs, tst, lim);
+    const bool pay_ok = bs->pay_ok != 0;
+    const SegView<true> svp{S, ts, len, pay, ~bs->inv_min_ts};
+    const SegView<false> svg{S, ts, len, pay, 0};
+    uint32_t *tile_cnt = hb.tile_cnt;
+    for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const uint64_t i0 = t * kSlotTile + (uint64_t)threadIdx.x * 16u;
+        auto slot_log = [&](uint64_t i, SwSeg &r) -> uint32_t {
+            if (i >= nslots) return 0;
+            return pay_ok ? sw_slot_log(svp, table[i], segs, ht, hl, ck.prune, ck.cutoff, r)
+                          : sw_slot_log(svg, table[i], segs, ht, hl, ck.prune, ck.cutoff, r);
+        };
+        uint32_t cnt = 0;
+        for (int k = 0; k < 16; ++k) {
+            SwSeg r;
+            cnt += slot_log(i0 + k, r);
+        }
+        if constexpr (!kWrite) {
+            uint32_t tot;
+            block256_excl(cnt, s_tmp, &tot);
+            if (threadIdx.x == 0) tile_cnt[t] = tot;
+        } else {
+            uint64_t off = hb.tile_off[t] + block256_excl(cnt, s_tmp, nullptr);
+            for (int k = 0; k < 16; ++k) {
+                SwSeg r;
+                const uint32_t c = slot_log(i0 + k, r);
+                if (i0 + k >= nslots) break;
+                Slot &sl = table[i0 + k];
+                if (sl.tag == 0) continue;
+                if (c == 0) { sl.aux = 0; continue; }
+                for (uint32_t v = r.lo; v < r.hi; ++v) {
+                    const uint64_t o = off + (v - r.lo);
+                    if (pay_ok) {
+                        const VView<SegView<true>> vv{svp, ht, hl, r.hoff, r.m, r.j0};
+                        nt[o] = vv.t(v); nl[o] = vv.l(v);
+                    } else {
+                        const VView<SegView<false>> vv{svg, ht, hl, r.hoff, r.m, r.j0};
+                        nt[o] = vv.t(v); nl[o] = vv.l(v);
+                    }
+                }
+                sl.aux = (off << kHistCntBits) | c;
+                off += c;
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// One block: exclusive scan of the per-tile log counts into 64-bit offsets, total to *total.
+__global__ __launch_bounds__(1024) void k_sw_hist_scan(const BatchState *bs, const uint32_t *__restrict__ cnt,
+                                                       uint64_t *__restrict__ offs, uint64_t ntiles,
+                                                       uint64_t *total) {
+    __shared__ uint64_t s_w[16];
+    __shared__ uint64_t s_carry;
+    if (bs->err) return;
+    const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
+    if (threadIdx.x == 0) s_carry = 0;
+    __syncthreads();
+    for (uint64_t c0 = 0; c0 < ntiles; c0 += 1024) {
+        const uint64_t i = c0 + threadIdx.x;
+        const uint64_t x = i < ntiles ? cnt[i] : 0u;
+        const uint64_t incl = wave_incl_sum(x);
+        if (lane == 63) s_w[w] = incl;
+        __syncthreads();
+        uint64_t off = s_carry, tot = 0;
+        for (uint32_t k = 0; k < 16; ++k) {
+            off += k < w ? s_w[k] : 0u;
+            tot += s_w[k];
+        }
+        if (i < ntiles) offs[i] = off + incl - x;
+        __syncthreads();
+        if (threadIdx.x == 0) s_carry += tot;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) *total = s_carry;
+}
+
+// Flip the history buffers and record the clock facts of this batch.
+__global__ void k_sw_finish(const BatchState *bs, TableState *tst, const uint64_t *total) {
+    if (bs->err) return;
+    const bool mono = sw_mono(bs, tst);
+    tst->hist_cur ^= 1u;
+    tst->hist_total = *total;
+    if (!mono) tst->ever_nonmono = 1;
+    if (bs->max_ts > tst->last_max_ts) tst->last_max_ts = bs->max_ts;
+    if (bs->max_len > tst->max_len_seen) tst->max_len_seen = bs->max_len;
+}
+
+hipError_t launch_sliding_window(const uint64_t *S, const uint64_t *ts, const uint32_t *len, BatchState *bs,
+                                 const Scratch &sc, Slot *table, TableState *tstate, const HistBufs &hb,
+                                 const Limits &lim, uint32_t n, hipStream_t st) {
+    const uint32_t gridSeg = std::min<uint32_t>(2048, std::max<uint32_t>(1, (n + 255) / 256));
+    const uint32_t *cls = sc.sort_ctl + 1028;
+    k_walk_sw<false><<<gridSeg, 256, 0, st>>>(S, bs, tstate, sc.seg_start, sc.seg_slot, ts, len, sc.pay[0],
+                                              sc.seg_order, cls, sc.marks, table, lim, hb, sc.sw_seg);
+    k_walk_sw<true><<<1024, 256, 0, st>>>(S, bs, tstate, sc.seg_start, sc.seg_slot, ts, len, sc.pay[0],
+                                          sc.seg_order, cls, sc.marks, table, lim, hb, sc.sw_seg);
+    const uint64_t nslots = lim.table_mask + 1;
+    const uint64_t ntiles = (nslots + kSlotTile - 1) / kSlotTile;
+    const uint32_t grid = (uint32_t)std::min<uint64_t>(4096, ntiles);
+    k_sw_hist<false><<<grid, 256, 0, st>>>(S, bs, tstate, ts, len, sc.pay[0], table, lim, hb, sc.sw_seg);
+    k_sw_hist_scan<<<1, 1024, 0, st>>>(bs, hb.tile_cnt, hb.tile_off, ntiles, hb.total);
+    k_sw_hist<true><<<grid, 256, 0, st>>>(S, bs, tstate, ts, len, sc.pay[0], table, lim, hb, sc.sw_seg);
+    k_sw_finish<<<1, 1, 0, st>>>(bs, tstate, hb.total);
     return hipGetLastError();
 }
 

@@ -106,6 +106,9 @@ typedef struct fsx_tb_state {
 
 /* Largest tb_burst (tokens) a token-bucket context accepts: capacity <= 2^61 nano-tokens. */
 #define FSX_TB_MAX_BURST 2305843009ull
+/* Largest pps_threshold a sliding-window context accepts (a carried log holds at most
+ * pps_threshold entries per source). */
+#define FSX_SW_MAX_PPS 16777214ull
 
 typedef struct fsx_config {
     uint64_t pps_threshold;   /* 1000       src/fsx_kern.c:309 */

@@ -122,3 +122,92 @@ def test_token_bucket_with_rules_and_state_updates(native, oracle):
 def test_token_bucket_rejects_oversized_burst(native):
     with pytest.raises(native.FsxError):
         native.FsxContext(limiter=TB, tb_burst=2305843010)
+
+
+# ------------------------------------------------------------------ sliding window
+SW = 1
+SW_MAPS = (1, 2, 3, 4)
+SW_CFGS = {
+    "default": {},
+    "tight": {"pps_threshold": 7, "window_ns": 200_000, "block_ns": 1_000_000},
+    "block_lt_window": {"pps_threshold": 5, "window_ns": 1_000_000, "block_ns": 50_000},
+    "block_zero": {"pps_threshold": 3, "window_ns": 100_000, "block_ns": 0},
+    "bytes_limit": {"pps_threshold": 50, "bps_threshold": 9_000, "window_ns": 500_000,
+                    "block_ns": 2_000_000},
+    "pps_zero": {"pps_threshold": 0, "window_ns": 100_000, "block_ns": 300_000},
+    "window_zero": {"pps_threshold": 3, "window_ns": 0, "block_ns": 100_000},
+}
+
+
+@pytest.mark.parametrize("name", list(SW_CFGS))
+def test_sliding_window_random(native, oracle, name):
+    rng = np.random.default_rng(zlib.crc32(b"sw" + name.encode()))
+    hdr, ln, ts = rand_stream(rng, 60000, 300, dt_max=400)
+    run_limiter(native, oracle, [(hdr, ln, ts)], dict(limiter=SW, **SW_CFGS[name]), SW_MAPS)
+
+
+@pytest.mark.parametrize("name", ["tight", "block_lt_window", "bytes_limit"])
+def test_sliding_window_heavy_sources(native, oracle, name):
+    """Few sources, long segments: the wave walkers (epoch scan on monotone clocks; the
+    exact replay when a byte trigger is possible)."""
+    rng = np.random.default_rng(31)
+    hdr, ln, ts = rand_stream(rng, 200000, 6, dt_max=60)
+    run_limiter(native, oracle, [(hdr, ln, ts)], dict(limiter=SW, **SW_CFGS[name]), SW_MAPS)
+
+
+@pytest.mark.parametrize("name", ["default", "tight", "block_lt_window"])
+def test_sliding_window_mixed_families(native, oracle, name):
+    rng = np.random.default_rng(32 + len(name))
+    hdr, ln, ts = rand_stream(rng, 40000, 500, dt_max=300, v6_frac=0.4, nonip_frac=0.05,
+                              short_frac=0.03)
+    run_limiter(native, oracle, [(hdr, ln, ts)], dict(limiter=SW, **SW_CFGS[name]), SW_MAPS)
+
+
+@pytest.mark.parametrize("name", ["tight", "block_lt_window", "bytes_limit"])
+def test_sliding_window_state_carry(native, oracle, name):
+    """Carried logs across uneven batch cuts (down to one packet), including sources
+    idle for many windows (their logs are pruned by the batch clock)."""
+    rng = np.random.default_rng(33)
+    hdr, ln, ts = rand_stream(rng, 60000, 40, dt_max=200, v6_frac=0.2)
+    cuts = [0, 1, 2, 777, 4096, 4097, 17000, 30000, 45000, 59999, 60000]
+    batches = [(hdr[a:b], ln[a:b], ts[a:b]) for a, b in zip(cuts[:-1], cuts[1:])]
+    run_limiter(native, oracle, batches, dict(limiter=SW, **SW_CFGS[name]), SW_MAPS)
+
+
+def test_sliding_window_long_sources_across_batches(native, oracle):
+    """Heavy sources whose logs (up to P entries) are carried into the next batch and
+    consumed by the wave walker."""
+    rng = np.random.default_rng(34)
+    hdr, ln, ts = rand_stream(rng, 240000, 5, dt_max=40)
+    cfg = dict(limiter=SW, pps_threshold=900, window_ns=1_000_000, block_ns=400_000)
+    cuts = [0, 50000, 50001, 120000, 240000]
+    batches = [(hdr[a:b], ln[a:b], ts[a:b]) for a, b in zip(cuts[:-1], cuts[1:])]
+    run_limiter(native, oracle, batches, cfg, SW_MAPS)
+
+
+def test_sliding_window_non_monotone_clock(native, oracle):
+    rng = np.random.default_rng(35)
+    hdr, ln, ts = rand_stream(rng, 40000, 30, dt_max=200)
+    sw = rng.choice(len(ts), 5000, replace=False)
+    ts[sw] = ts[sw] - rng.integers(0, 50000, sw.size).astype(np.uint64)
+    ts[9] = np.uint64(2**64 - 7)
+    batches = [(ts_[0], ts_[1], ts_[2]) for ts_ in
+               ((hdr[:20000], ln[:20000], ts[:20000]), (hdr[20000:], ln[20000:], ts[20000:]))]
+    run_limiter(native, oracle, batches, dict(limiter=SW, **SW_CFGS["tight"]), SW_MAPS)
+
+
+def test_sliding_window_rules(native, oracle):
+    rng = np.random.default_rng(36)
+    hdr, ln, ts = rand_stream(rng, 30000, 60, dt_max=300)
+    srcs = sorted({bytes(hdr[i, 26:30]) for i in range(0, 30000, 97)})
+    t_mid = int(ts[15000])
+    rules = []
+    for i, k in enumerate(srcs[:24]):
+        rules.append((3, k, [2**64 - 1, t_mid, 0][i % 3]))
+    batches = [(hdr[:15000], ln[:15000], ts[:15000]), (hdr[15000:], ln[15000:], ts[15000:])]
+    run_limiter(native, oracle, batches, dict(limiter=SW, **SW_CFGS["tight"]), SW_MAPS, rules)
+
+
+def test_sliding_window_rejects_large_threshold(native):
+    with pytest.raises(native.FsxError):
+        native.FsxContext(limiter=SW, pps_threshold=1 << 24)

@@ -85,3 +85,63 @@ def test_oracle_token_bucket_matches_spec(oracle, rate, burst):
     assert {(4, k): val for k, val in d4.items()} | {(6, k): val for k, val in d6.items()} == tb
     assert {(4, k): val for k, val in o.map_dump(3).items()} == {k: t for k, t in bl.items()
                                                                   if k[0] == 4}
+
+
+def spec_sliding_window(hdr, ln, ts, P, B, W, BLK, rules=None):
+    """DESIGN.md §4.1, one packet at a time, explicit per-source logs."""
+    bl = dict(rules or {})
+    logs, st = {}, {}
+    out, allowed, dropped = [], 0, 0
+    for i in range(len(ln)):
+        s = _src(hdr[i], int(ln[i]))
+        if s in ("drop", "pass"):
+            out.append(1 if s == "drop" else 2)
+            continue
+        now = int(ts[i])
+        till = bl.get(s)
+        if till is not None and till > 0:
+            if now > till:
+                del bl[s]
+            else:
+                out.append(1)
+                dropped += 1
+                continue
+        log = logs.setdefault(s, [])
+        while log and ((now - log[0][0]) & U64) >= W:
+            log.pop(0)
+        log.append((now, int(ln[i])))
+        cnt, byt = len(log), sum(x[1] for x in log)
+        st[s] = (cnt, byt, log[0][0])
+        if cnt > P or byt > B:
+            bl[s] = (now + BLK) & U64
+            log.clear()
+            out.append(1)
+            dropped += 1
+        else:
+            out.append(2)
+            allowed += 1
+    return np.array(out, dtype=np.uint8), (allowed, dropped), st, bl
+
+
+@pytest.mark.parametrize("P,B,W,BLK", [(1000, 125_000_000, 10**9, 10**10), (7, 10**9, 200_000, 10**6),
+                                       (5, 10**9, 10**6, 50_000), (3, 10**9, 100_000, 0),
+                                       (50, 9000, 500_000, 2 * 10**6), (0, 10**9, 10**5, 3 * 10**5),
+                                       (3, 10**9, 0, 10**5)])
+def test_oracle_sliding_window_matches_spec(oracle, P, B, W, BLK):
+    rng = np.random.default_rng(P + W % 1000)
+    hdr, ln, ts = rand_stream(rng, 4000, 40, dt_max=400, v6_frac=0.3, nonip_frac=0.05,
+                              short_frac=0.02)
+    ts[100] = ts[100] - np.uint64(5000)
+    o = oracle.Oracle(limiter=1, pps_threshold=P, bps_threshold=B, window_ns=W, block_ns=BLK,
+                      max_entries=1 << 12)
+    v = o.batch(hdr[:2500], ln[:2500], ts[:2500])
+    v = np.concatenate([v, o.batch(hdr[2500:], ln[2500:], ts[2500:])])
+    exp, st, stats, bl = spec_sliding_window(hdr, ln, ts, P, B, W, BLK)
+    assert np.array_equal(v, exp)
+    assert o.stats() == st
+    got = {(4, k): val for k, val in o.map_dump(1).items()}
+    got |= {(6, k): val for k, val in o.map_dump(2).items()}
+    assert got == stats
+    gbl = {(4, k): val for k, val in o.map_dump(3).items()}
+    gbl |= {(6, k): val for k, val in o.map_dump(4).items()}
+    assert gbl == bl
