@@ -61,6 +61,8 @@ def parse_args():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--check", action="store_true", help="verify a prefix against the oracle")
     ap.add_argument("--no-mlp", action="store_true", help="verdicts only (no features/scores)")
+    ap.add_argument("--limiter-steps", type=int, default=5,
+                    help="timed steps of the sliding-window and token-bucket legs (0: skip)")
     return ap.parse_args()
 
 
@@ -136,6 +138,41 @@ def main():
         elapsed = float(t.item())
     stats = ctx.stats()
     malicious = None if args.no_mlp else int(d_dec[:info["sources"]].sum().item())
+    ctx.close()
+
+    # BASELINE config 2 also names the sliding-window and token-bucket limiters
+    # (build-defined): the same batch through each, verdicts + maps only
+    limiters = {}
+    if args.limiter_steps > 0:
+        for lname, lid in (("sliding_window", lib.LIMIT_SLIDING_WINDOW),
+                           ("token_bucket", lib.LIMIT_TOKEN_BUCKET)):
+            with lib.FsxContext(max_batch=n, max_entries=max_entries, device=local,
+                                limiter=lid) as lc:
+                def lstep():
+                    lc.reset()
+                    lc.verdict_batch_device(d_hdr.data_ptr(), d_len.data_ptr(), d_ts.data_ptr(), n,
+                                            d_v.data_ptr())
+                lstep()
+                lc.sync()
+                torch.cuda.synchronize()
+                if dist:
+                    dist.barrier()
+                l0 = time.perf_counter()
+                for _ in range(args.limiter_steps):
+                    lstep()
+                lc.sync()
+                torch.cuda.synchronize()
+                if dist:
+                    dist.barrier()
+                lt = time.perf_counter() - l0
+                if dist:
+                    t = torch.tensor([lt], dtype=torch.float64, device="cuda")
+                    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+                    lt = float(t.item())
+                la, ld = lc.stats()
+                limiters[lname] = {"value": round(n * world * args.limiter_steps / lt / 1e6, 2),
+                                   "unit": "Mpps", "ms_per_step": round(lt / args.limiter_steps * 1e3, 4),
+                                   "steps": args.limiter_steps, "allowed": la, "dropped": ld}
 
     check = None
     if args.check and rank == 0:
@@ -210,10 +247,13 @@ def main():
         "config": {"workload": f"BASELINE config {args.config}: {n} IPv4/UDP packets per GPU, "
                                f"{p.n_ips} Zipf(1.1) sources, {p.duration_ns / 1e9:g} s; "
                                "fixed-window limiter (src/fsx_kern.c), maps reset each step"
+                               + ("; sliding-window and token-bucket legs timed separately "
+                                  "(limiters)" if args.limiter_steps > 0 else "")
                                + ("" if args.no_mlp else "; per-source features + q8 MLP score "
                                   "(model_weights.pth)"),
                    "packets_per_gpu": n, "sources": sources, "parallelism": f"dp{world}"},
         "roofline": roofline, "pipeline": pipeline, "cpu_baseline": cpu,
+        "limiters": limiters or None,
         "kernels": [{"name": a, "ms_per_step": round(b, 4), "launches": c} for a, b, c in timings],
         "stats": {"allowed": stats[0], "dropped": stats[1], "sources": info["sources"],
                   "malicious_sources": malicious}, "check": check,
