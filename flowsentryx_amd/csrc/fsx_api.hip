@@ -17,6 +17,7 @@
 
 #include "../../include/fsx_hip.h"
 #include "fsx_internal.h"
+#include "fsx_shard.h"
 
 using namespace fsx;
 
@@ -49,6 +50,9 @@ struct fsx_ctx {
     float *d_prob = nullptr;
     uint8_t *d_dec = nullptr;
     uint64_t score_cap = 0;
+    // sharding: per (owner, tile) counts of fsx_shard_pack_device
+    uint32_t *d_shard_cnt = nullptr;
+    uint64_t shard_cnt_cap = 0;
     // sliding-window history (limiter == FSX_LIMIT_SLIDING_WINDOW only)
     HistBufs hist{};
     // per-source flow accumulators
@@ -185,6 +189,7 @@ void fsx_close(fsx_ctx *c) {
     hipFree(c->d_res); hipFree(c->d_val);
     for (int b = 0; b < 2; ++b) { hipFree(c->hist.t[b]); hipFree(c->hist.l[b]); }
     hipFree(c->hist.tile_cnt); hipFree(c->hist.tile_off); hipFree(c->hist.total);
+    hipFree(c->d_shard_cnt);
     for (int r = 0; r < kRing; ++r)
         for (int i = 0; i < kMaxEv; ++i) if (c->ev[r][i]) hipEventDestroy(c->ev[r][i]);
     if (c->own_stream) hipStreamDestroy(c->own_stream);
@@ -633,6 +638,64 @@ int fsx_last_batch_info(fsx_ctx *c, uint64_t *info, int cap) {
     int k = 0;
     for (; k < cap && k < 11; ++k) info[k] = v[k];
     return k;
+}
+
+// ------------------------------------------------------------------ sharding
+uint32_t fsx_shard_owner(const uint8_t *key16, int family, uint32_t n_shards) {
+    if (!key16 || n_shards == 0) return 0;
+    uint32_t k[4] = {0, 0, 0, 0};
+    memcpy(k, key16, family == 6 ? 16 : 4);
+    return shard_owner_of(family == 6 ? 2u : 1u, k, n_shards);
+}
+
+int fsx_shard_pack_device(fsx_ctx *c, const uint8_t *d_hdr, const uint32_t *d_len, const uint64_t *d_ts,
+                          size_t n, uint32_t G, uint8_t *d_verdict, void *d_records, uint32_t *d_send_idx,
+                          uint64_t *d_counts) {
+    if (!c) return -EINVAL;
+    if (G == 0 || G > FSX_MAX_SHARDS) return set_err(c, -EINVAL, "n_shards must be 1..%d", FSX_MAX_SHARDS);
+    if (n > kMaxBatchLimit) return set_err(c, -E2BIG, "n=%zu too large", n);
+    if (!d_counts || (n && (!d_hdr || !d_len || !d_ts || !d_verdict || !d_records || !d_send_idx)))
+        return set_err(c, -EINVAL, "null buffer");
+    int rc = sel(c);
+    if (rc) return rc;
+    const uint64_t need = (uint64_t)G * (n / 4096 + 1);
+    if (need > c->shard_cnt_cap) {
+        hipFree(c->d_shard_cnt);
+        c->d_shard_cnt = nullptr;
+        c->shard_cnt_cap = 0;
+        HIPCHK(c, hipMalloc(&c->d_shard_cnt, need * 4));
+        c->shard_cnt_cap = need;
+    }
+    hipError_t e = launch_shard_pack(d_hdr, d_len, d_ts, (uint32_t)n, G, d_verdict,
+                                     reinterpret_cast<ShardRecord *>(d_records), d_send_idx, d_counts,
+                                     c->d_shard_cnt, c->stream);
+    if (e != hipSuccess) return set_err(c, -EIO, "shard pack: %s", hipGetErrorString(e));
+    return 0;
+}
+
+int fsx_shard_unpack_device(fsx_ctx *c, const void *d_records, size_t m, uint8_t *d_hdr, uint32_t *d_len,
+                            uint64_t *d_ts) {
+    if (!c) return -EINVAL;
+    if (m > kMaxBatchLimit) return set_err(c, -E2BIG, "m=%zu too large", m);
+    if (m && (!d_records || !d_hdr || !d_len || !d_ts)) return set_err(c, -EINVAL, "null buffer");
+    int rc = sel(c);
+    if (rc) return rc;
+    hipError_t e = launch_shard_unpack(reinterpret_cast<const ShardRecord *>(d_records), (uint32_t)m, d_hdr,
+                                       d_len, d_ts, c->stream);
+    if (e != hipSuccess) return set_err(c, -EIO, "shard unpack: %s", hipGetErrorString(e));
+    return 0;
+}
+
+int fsx_shard_scatter_device(fsx_ctx *c, const uint8_t *d_ret, const uint32_t *d_send_idx, size_t m,
+                             uint8_t *d_verdict) {
+    if (!c) return -EINVAL;
+    if (m > kMaxBatchLimit) return set_err(c, -E2BIG, "m=%zu too large", m);
+    if (m && (!d_ret || !d_send_idx || !d_verdict)) return set_err(c, -EINVAL, "null buffer");
+    int rc = sel(c);
+    if (rc) return rc;
+    hipError_t e = launch_shard_scatter(d_ret, d_send_idx, (uint32_t)m, d_verdict, c->stream);
+    if (e != hipSuccess) return set_err(c, -EIO, "shard scatter: %s", hipGetErrorString(e));
+    return 0;
 }
 
 // ------------------------------------------------------------------ timing

@@ -1,0 +1,38 @@
+// fsx_shard.h — record layout and owner function of the hash(src IP) sharded path
+// (SURVEY.md §8 e; fsx_shard.hip). Shared by host (C ABI) and device code.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "fsx_internal.h"
+
+namespace fsx {
+
+// One IP packet on the wire between ranks (32 bytes).
+struct alignas(16) ShardRecord {
+    uint32_t key[4];      // raw source address words (IPv4: key[0] only)
+    uint64_t ts;          // arrival time (ns)
+    uint32_t len;         // frame length
+    uint16_t dport;       // L4 destination port (host order; 0 when absent)
+    uint8_t family;       // 4 or 6
+    uint8_t pad;
+};
+static_assert(sizeof(ShardRecord) == 32, "32-byte exchange records");
+
+constexpr uint64_t kShardSeed = 0x5A4D0F5EED5ull;   // fixed: every rank must agree
+
+// owner = floor(h * G / 2^32) of a 32-bit mix of (family tag, address).
+__host__ __device__ inline uint32_t shard_owner_of(uint32_t tag, const uint32_t k[4], uint32_t G) {
+    const uint64_t h = slot_hash(tag, k, kShardSeed);
+    return (uint32_t)(((h >> 32) * (uint64_t)G) >> 32);
+}
+
+hipError_t launch_shard_pack(const uint8_t *hdr, const uint32_t *len, const uint64_t *ts, uint32_t n,
+                             uint32_t G, uint8_t *verdict, ShardRecord *rec, uint32_t *send_idx,
+                             uint64_t *owner_total, uint32_t *scratch, hipStream_t st);
+hipError_t launch_shard_unpack(const ShardRecord *rec, uint32_t m, uint8_t *hdr, uint32_t *len,
+                               uint64_t *ts, hipStream_t st);
+hipError_t launch_shard_scatter(const uint8_t *ret, const uint32_t *send_idx, uint32_t m, uint8_t *verdict,
+                                hipStream_t st);
+
+}  // namespace fsx

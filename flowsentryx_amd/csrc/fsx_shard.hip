@@ -1,0 +1,274 @@
+// fsx_shard.hip — hash(src IP) sharding of the verdict path over G GPUs (SURVEY.md §8 e).
+//
+// Every rank holds a contiguous slice of the arrival stream. All limiter state is per
+// source IP, so a source's packets are routed to one owner rank, owner = H(family, key)
+// (fsx_shard_owner), which runs the unchanged batch pipeline on them:
+//   k_shard_count     parse (src/parsing_helper.h:49-136 rules) + owner of every IP
+//                     packet; per-tile per-owner counts
+//   k_shard_scan      exclusive scan over (owner, tile) -> send offsets, per-owner totals
+//   k_shard_pack      stable partition by owner into 32-byte records {src key, ts, len,
+//                     L4 dst port, family}; local verdicts for the packets that never
+//                     reach a limiter (short frames DROP, non-IP PASS: src/fsx_kern.c:
+//                     123-131); for each send slot the local packet index
+//   (RCCL all-to-all of the records, host side: flowsentryx_amd/shard.py)
+//   k_shard_unpack    owner side: records -> 64-byte header records + len + ts whose parse
+//                     and flow features equal the originals'
+//   (owner: fsx_verdict_batch_device / fsx_process_batch_device; all-to-all back)
+//   k_shard_scatter   verdicts back to local arrival positions
+// Slices are contiguous and concatenated by rank on the owner, so every source's
+// packets reach its owner in global arrival order and the result equals the 1-GPU run.
+#include <hip/hip_runtime.h>
+
+#include "fsx_dev_common.h"
+#include "fsx_internal.h"
+#include "fsx_shard.h"
+
+namespace fsx {
+
+constexpr uint32_t kShardTile = 4096;  // 256 threads x 16 packets
+constexpr uint32_t kMaxShards = 64;
+
+// Parse one 64-byte record (same rules as k_parse / the oracle): 0 DROP, 1 PASS
+// (non-IP), 4 / 6 IP family with its key words and L4 destination port.
+__device__ __forceinline__ uint32_t shard_parse(const uint8_t *rec, uint32_t L, uint32_t k[4],
+                                                uint32_t &dport) {
+    const uint32_t *d = reinterpret_cast<const uint32_t *>(rec);
+    const uint32_t d3 = d[3];
+    const uint32_t proto = ((d3 & 0xFFu) << 8) | ((d3 >> 8) & 0xFFu);
+    k[0] = k[1] = k[2] = k[3] = 0;
+    dport = 0;
+    if (L < 14u) return 0;
+    uint32_t off, l4;
+    if (proto == 0x86DDu) {
+        if (L < 54u) return 0;
+        const uint32_t d5 = d[5], d6 = d[6], d7 = d[7], d8 = d[8], d9 = d[9];
+        k[0] = (d5 >> 16) | (d6 << 16);
+        k[1] = (d6 >> 16) | (d7 << 16);
+        k[2] = (d7 >> 16) | (d8 << 16);
+        k[3] = (d8 >> 16) | (d9 << 16);
+        off = 54;
+        l4 = (d5 & 0xFFu);   // byte 20: next header
+    } else if (proto == 0x0800u) {
+        if (L < 34u) return 0;
+        k[0] = (d[6] >> 16) | (d[7] << 16);
+        off = 14u + 4u * (((d3 >> 16) & 0xFFu) & 0x0Fu);   // byte 14: version/IHL
+        l4 = (d[5] >> 24) & 0xFFu;                           // byte 23: protocol
+    } else {
+        return 1;
+    }
+    if ((l4 == 6 || l4 == 17) && off + 4 <= L && off + 4 <= 64)
+        dport = ((uint32_t)rec[off + 2] << 8) | rec[off + 3];
+    return proto == 0x86DDu ? 6u : 4u;
+}
+
+__device__ __forceinline__ uint32_t owner_dev(uint32_t fam, const uint32_t k[4], uint32_t G) {
+    return shard_owner_of(fam == 6 ? 2u : 1u, k, G);
+}
+
+// Per tile: per-owner IP-packet counts, owner-major [G][tiles].
+__global__ __launch_bounds__(256) void k_shard_count(const uint8_t *__restrict__ hdr,
+                                                     const uint32_t *__restrict__ len, uint32_t n,
+                                                     uint32_t G, uint32_t *__restrict__ cnt,
+                                                     uint32_t ntiles) {
+    __shared__ uint32_t sh[kMaxShards];
+    const uint32_t t = blockIdx.x;
+    if (threadIdx.x < kMaxShards) sh[threadIdx.x] = 0;
+    __syncthreads();
+    for (uint32_t r = 0; r < 16; ++r) {
+        const uint32_t i = t * kShardTile + r * 256u + threadIdx.x;
+        if (i >= n) break;
+        uint32_t k[4], dp;
+        const uint32_t f = shard_parse(hdr + (size_t)i * 64, len[i], k, dp);
+        if (f >= 4) atomicAdd(&sh[owner_dev(f, k, G)], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x < G) cnt[(size_t)threadIdx.x * ntiles + t] = sh[threadIdx.x];
+}
+
+// One block: exclusive scan of cnt in owner-major order (in place) and per-owner totals.
+__global__ __launch_bounds__(1024) void k_shard_scan(uint32_t *__restrict__ cnt, uint64_t total_n,
+                                                     uint64_t *__restrict__ owner_total,
+                                                     uint32_t G, uint32_t ntiles) {
+    __shared__ uint32_t s_w[16];
+    __shared__ uint32_t s_carry;
+    const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
+    if (threadIdx.x == 0) s_carry = 0;
+    __syncthreads();
+    const uint64_t N = (uint64_t)G * ntiles;
+    for (uint64_t c0 = 0; c0 < N; c0 += 1024) {
+        const uint64_t i = c0 + threadIdx.x;
+        const uint32_t x = i < N ? cnt[i] : 0u;
+        const uint32_t incl = wave_incl_sum(x);
+        if (lane == 63) s_w[w] = incl;
+        __syncthreads();
+        uint32_t off = s_carry, tot = 0;
+        for (uint32_t k = 0; k < 16; ++k) {
+            off += k < w ? s_w[k] : 0u;
+            tot += s_w[k];
+        }
+        if (i < N) cnt[i] = off + incl - x;
+        __syncthreads();
+        if (threadIdx.x == 0) s_carry += tot;
+        __syncthreads();
+    }
+    // totals: difference of consecutive owner bases
+    if (threadIdx.x < G) {
+        const uint32_t o = threadIdx.x;
+        const uint32_t b0 = cnt[(size_t)o * ntiles];
+        const uint32_t b1 = o + 1 < G ? cnt[(size_t)(o + 1) * ntiles] : s_carry;
+        owner_total[o] = b1 - b0;
+    }
+}
+
+// Per tile: stable (arrival order) placement of every IP packet at its owner's offset.
+__global__ __launch_bounds__(256) void k_shard_pack(const uint8_t *__restrict__ hdr,
+                                                    const uint32_t *__restrict__ len,
+                                                    const uint64_t *__restrict__ ts, uint32_t n,
+                                                    uint32_t G, const uint32_t *__restrict__ offs,
+                                                    uint32_t ntiles, ShardRecord *__restrict__ rec,
+                                                    uint32_t *__restrict__ send_idx,
+                                                    uint8_t *__restrict__ verdict) {
+    __shared__ uint32_t s_base[kMaxShards];
+    __shared__ uint32_t s_wc[4][kMaxShards];
+    const uint32_t t = blockIdx.x, lane = lane_id(), w = threadIdx.x >> 6;
+    if (threadIdx.x < G) s_base[threadIdx.x] = offs[(size_t)threadIdx.x * ntiles + t];
+    // wave w owns packets [t*4096 + w*1024, +1024) in arrival order: count per owner
+    // first (so a wave places after the waves before it), then place in order
+    uint32_t of[16];   // owner << 4 | class (0 DROP, 1 PASS, 4/6 IP, 15 none)
+    for (uint32_t o = threadIdx.x; o < 4 * kMaxShards; o += 256) (&s_wc[0][0])[o] = 0;
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const uint32_t i = t * kShardTile + w * 1024u + (uint32_t)r * 64u + lane;
+        of[r] = 15u;
+        if (i < n) {
+            uint32_t k[4], dp;
+            const uint32_t f = shard_parse(hdr + (size_t)i * 64, len[i], k, dp);
+            if (f >= 4) {
+                const uint32_t o = owner_dev(f, k, G);
+                of[r] = (o << 4) | f;
+                atomicAdd(&s_wc[w][o], 1u);
+            } else {
+                of[r] = f;
+                verdict[i] = f == 0 ? 1u : 2u;   // XDP_DROP / XDP_PASS, never counted
+            }
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < G) {   // exclusive over the waves, from the tile's owner base
+        const uint32_t o = threadIdx.x;
+        uint32_t b = s_base[o];
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t c = s_wc[k][o];
+            s_wc[k][o] = b;
+            b += c;
+        }
+    }
+    __syncthreads();
+    const uint64_t lt = (1ull << lane) - 1ull;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const uint32_t i = t * kShardTile + w * 1024u + (uint32_t)r * 64u + lane;
+        const uint32_t f = of[r] & 15u, own = of[r] >> 4;
+        const bool ip = f == 4u || f == 6u;
+        // rank among this step's lanes with the same owner (ballots over the owner bits)
+        uint64_t peers = __ballot(ip);
+        for (uint32_t b = 0; (1u << b) < G; ++b) {
+            const bool bit = (own >> b) & 1u;
+            const uint64_t bal = __ballot(ip && bit);
+            peers &= bit ? bal : ~bal;
+        }
+        const uint32_t below = (uint32_t)__popcll(peers & lt);
+        uint32_t base = 0;
+        if (ip && below == 0) base = atomicAdd(&s_wc[w][own], (uint32_t)__popcll(peers));
+        base = __shfl(base, ip ? __ffsll((unsigned long long)peers) - 1 : 0);
+        if (ip) {
+            uint32_t k[4], dp;
+            shard_parse(hdr + (size_t)i * 64, len[i], k, dp);
+            const uint32_t slot = base + below;
+            ShardRecord x;
+            x.key[0] = k[0]; x.key[1] = k[1]; x.key[2] = k[2]; x.key[3] = k[3];
+            x.ts = ts[i];
+            x.len = len[i];
+            x.dport = (uint16_t)dp;
+            x.family = (uint8_t)f;
+            x.pad = 0;
+            rec[slot] = x;
+            send_idx[slot] = i;
+            verdict[i] = 2u;   // placeholder until the owner's verdict returns
+        }
+    }
+}
+
+// Owner side: 32-byte records -> header records that parse to the same key, family and
+// dst port, frame length and timestamp.
+__global__ __launch_bounds__(256) void k_shard_unpack(const ShardRecord *__restrict__ rec, uint32_t m,
+                                                      uint8_t *__restrict__ hdr,
+                                                      uint32_t *__restrict__ len,
+                                                      uint64_t *__restrict__ ts) {
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < m; i += gridDim.x * 256u) {
+        const ShardRecord x = rec[i];
+        uint32_t d[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) d[k] = 0;
+        const uint32_t dp = ((x.dport & 0xFFu) << 8) | (x.dport >> 8);   // network order
+        if (x.family == 6) {
+            d[3] = 0xDD86u;                                   // bytes 12-13: 0x86DD
+            d[5] = 17u | (x.key[0] << 16);                    // byte 20 next header = UDP
+            d[6] = (x.key[0] >> 16) | (x.key[1] << 16);
+            d[7] = (x.key[1] >> 16) | (x.key[2] << 16);
+            d[8] = (x.key[2] >> 16) | (x.key[3] << 16);
+            d[9] = x.key[3] >> 16;
+            d[14] = dp;                                       // bytes 56-57 (54 + 2)
+        } else {
+            d[3] = 0x0008u | (0x45u << 16);                   // 0x0800, version 4 / IHL 5
+            d[5] = 17u << 24;                                 // byte 23 protocol = UDP
+            d[6] = x.key[0] << 16;                            // bytes 26-27
+            d[7] = x.key[0] >> 16;                            // bytes 28-29
+            d[9] = dp;                                        // bytes 36-37 (34 + 2)
+        }
+        uint4 *o = reinterpret_cast<uint4 *>(hdr + (size_t)i * 64);
+        o[0] = make_uint4(d[0], d[1], d[2], d[3]);
+        o[1] = make_uint4(d[4], d[5], d[6], d[7]);
+        o[2] = make_uint4(d[8], d[9], d[10], d[11]);
+        o[3] = make_uint4(d[12], d[13], d[14], d[15]);
+        len[i] = x.len;
+        ts[i] = x.ts;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_shard_scatter(const uint8_t *__restrict__ ret,
+                                                       const uint32_t *__restrict__ send_idx, uint32_t m,
+                                                       uint8_t *__restrict__ verdict) {
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < m; i += gridDim.x * 256u)
+        verdict[send_idx[i]] = ret[i];
+}
+
+hipError_t launch_shard_pack(const uint8_t *hdr, const uint32_t *len, const uint64_t *ts, uint32_t n,
+                             uint32_t G, uint8_t *verdict, ShardRecord *rec, uint32_t *send_idx,
+                             uint64_t *owner_total, uint32_t *scratch, hipStream_t st) {
+    if (n == 0) return hipMemsetAsync(owner_total, 0, (size_t)G * 8, st);
+    const uint32_t ntiles = (n + kShardTile - 1) / kShardTile;
+    k_shard_count<<<ntiles, 256, 0, st>>>(hdr, len, n, G, scratch, ntiles);
+    k_shard_scan<<<1, 1024, 0, st>>>(scratch, n, owner_total, G, ntiles);
+    k_shard_pack<<<ntiles, 256, 0, st>>>(hdr, len, ts, n, G, scratch, ntiles, rec, send_idx, verdict);
+    return hipGetLastError();
+}
+
+hipError_t launch_shard_unpack(const ShardRecord *rec, uint32_t m, uint8_t *hdr, uint32_t *len,
+                               uint64_t *ts, hipStream_t st) {
+    if (m == 0) return hipSuccess;
+    const uint32_t grid = std::min<uint32_t>(4096, (m + 255) / 256);
+    k_shard_unpack<<<grid, 256, 0, st>>>(rec, m, hdr, len, ts);
+    return hipGetLastError();
+}
+
+hipError_t launch_shard_scatter(const uint8_t *ret, const uint32_t *send_idx, uint32_t m, uint8_t *verdict,
+                                hipStream_t st) {
+    if (m == 0) return hipSuccess;
+    const uint32_t grid = std::min<uint32_t>(4096, (m + 255) / 256);
+    k_shard_scatter<<<grid, 256, 0, st>>>(ret, send_idx, m, verdict);
+    return hipGetLastError();
+}
+
+}  // namespace fsx

@@ -126,6 +126,10 @@ def load_library() -> C.CDLL:
         "fsx_last_timings": (C.c_int, [vp, vp, vp, vp, C.c_int, C.c_int, C.POINTER(C.c_int)]),
         "fsx_enable_timing": (C.c_int, [vp, C.c_int]),
         "fsx_last_batch_info": (C.c_int, [vp, vp, C.c_int]),
+        "fsx_shard_owner": (C.c_uint32, [vp, C.c_int, C.c_uint32]),
+        "fsx_shard_pack_device": (C.c_int, [vp, vp, vp, vp, sz, C.c_uint32, vp, vp, vp, vp]),
+        "fsx_shard_unpack_device": (C.c_int, [vp, vp, sz, vp, vp, vp]),
+        "fsx_shard_scatter_device": (C.c_int, [vp, vp, vp, sz, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -143,7 +147,18 @@ ABI_SYMBOLS = [
     "fsx_map_lookup", "fsx_map_update", "fsx_map_delete", "fsx_map_dump", "fsx_get_stats",
     "fsx_reset", "fsx_load_q8_model", "fsx_score", "fsx_score_device", "fsx_flow_features",
     "fsx_last_timings", "fsx_enable_timing", "fsx_last_batch_info",
+    "fsx_shard_owner", "fsx_shard_pack_device", "fsx_shard_unpack_device",
+    "fsx_shard_scatter_device",
 ]
+
+SHARD_RECORD_BYTES = 32
+MAX_SHARDS = 64
+
+
+def shard_owner(key16: bytes, family: int, n_shards: int) -> int:
+    """Owner rank of a source (include/fsx_hip.h fsx_shard_owner; host-only)."""
+    k = bytes(key16).ljust(16, b"\0")
+    return int(load_library().fsx_shard_owner(k, int(family), int(n_shards)))
 
 
 def default_config(**overrides) -> FsxConfig:
@@ -354,6 +369,21 @@ class FsxContext:
         if rc < 0:
             self._check(rc, "fsx_last_batch_info")
         return {k: int(buf[i]) for i, k in enumerate(self.BATCH_INFO[:rc])}
+
+    # -- sharding (SURVEY.md §8 e; protocol in flowsentryx_amd/shard.py)
+    def shard_pack_device(self, d_hdr: int, d_len: int, d_ts: int, n: int, n_shards: int,
+                          d_verdict: int, d_records: int, d_send_idx: int, d_counts: int):
+        self._check(self._lib.fsx_shard_pack_device(self._h, d_hdr, d_len, d_ts, n, n_shards,
+                                                    d_verdict, d_records, d_send_idx, d_counts),
+                    "fsx_shard_pack_device")
+
+    def shard_unpack_device(self, d_records: int, m: int, d_hdr: int, d_len: int, d_ts: int):
+        self._check(self._lib.fsx_shard_unpack_device(self._h, d_records, m, d_hdr, d_len, d_ts),
+                    "fsx_shard_unpack_device")
+
+    def shard_scatter_device(self, d_ret: int, d_send_idx: int, m: int, d_verdict: int):
+        self._check(self._lib.fsx_shard_scatter_device(self._h, d_ret, d_send_idx, m, d_verdict),
+                    "fsx_shard_scatter_device")
 
     # -- timing
     def enable_timing(self, on: bool = True):

@@ -204,6 +204,33 @@ int fsx_flow_features(fsx_ctx *ctx, const uint8_t *hdr, const uint32_t *len,
                       const uint64_t *ts_ns, size_t n, size_t cap, uint8_t *keys16,
                       uint8_t *family, float *features, size_t *n_flows_out);
 
+/* ---- hash(src IP) sharding over G GPUs (SURVEY.md §8 e; host protocol in
+ * flowsentryx_amd/shard.py). Every rank holds a contiguous slice of the arrival stream;
+ * every source IP has one owner rank that runs the limiter on all of its packets, so
+ * a sharded run equals the 1-GPU run. No reference counterpart: the reference is one
+ * XDP program per host (src/fsx_kern.c:96-97). */
+#define FSX_MAX_SHARDS 64
+#define FSX_SHARD_RECORD_BYTES 32   /* {u32 key[4]; u64 ts; u32 len; u16 dport; u8 family; u8 pad} */
+
+/* Owner rank of a source: key16 = raw address (IPv4 in the first 4 bytes), family 4/6.
+ * Host-only (no device work). */
+uint32_t fsx_shard_owner(const uint8_t *key16, int family, uint32_t n_shards);
+/* Parse a device batch and partition its IP packets by owner, stable in arrival order:
+ * d_records (n * 32 bytes capacity) receives the records owner by owner, d_send_idx the
+ * local packet index of every record, d_counts[n_shards] the records per owner.
+ * Packets that never reach a limiter get their verdict in d_verdict here (frames too
+ * short for their header: DROP; non-IP: PASS; src/fsx_kern.c:123-148). */
+int fsx_shard_pack_device(fsx_ctx *ctx, const uint8_t *d_hdr, const uint32_t *d_len,
+                          const uint64_t *d_ts, size_t n, uint32_t n_shards, uint8_t *d_verdict,
+                          void *d_records, uint32_t *d_send_idx, uint64_t *d_counts);
+/* Owner side: m received records -> header records + len + ts for the batch entry points
+ * (same source key, family, frame length, timestamp and L4 destination port). */
+int fsx_shard_unpack_device(fsx_ctx *ctx, const void *d_records, size_t m, uint8_t *d_hdr,
+                            uint32_t *d_len, uint64_t *d_ts);
+/* Origin side: d_verdict[d_send_idx[i]] = d_ret[i] for the m returned verdicts. */
+int fsx_shard_scatter_device(fsx_ctx *ctx, const uint8_t *d_ret, const uint32_t *d_send_idx,
+                             size_t m, uint8_t *d_verdict);
+
 /* Facts about the last batch (after fsx_sync): info[0] IP packets, [1] distinct
  * source IPs, [2] sources new to the maps, [3] any IPv6, [4] non-monotone clock,
  * [5] max frame length, [6] max timestamp, [7] allowed, [8] dropped, [9] IPv6

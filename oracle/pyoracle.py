@@ -237,3 +237,11 @@ def synth(params, zipf_s: float, j0: int, count: int):
     if rc:
         raise RuntimeError(f"fsxo_synth {rc}")
     return hdr, length, ts
+
+
+def dst_port(hdr, length) -> np.ndarray:
+    """L4 destination port per record (DESIGN.md §5 rule; 0 when absent)."""
+    hdr = np.ascontiguousarray(hdr, dtype=np.uint8).reshape(-1, 64)
+    length = np.ascontiguousarray(length, dtype=np.uint32)
+    f = lib().fsxo_dst_port
+    return np.array([f(_p(hdr[i]), int(length[i])) for i in range(hdr.shape[0])], dtype=np.uint32)

@@ -1,0 +1,93 @@
+"""CPU engine of the sharded protocol (flowsentryx_amd/shard.py) for gloo tests.
+
+TEST INFRASTRUCTURE: the per-owner limiter is the CPU oracle, the exchange records are
+built with numpy in the 32-byte layout of include/fsx_hip.h, owners come from the
+library's host function fsx_shard_owner. The protocol code under test is the product's.
+"""
+import contextlib
+
+import numpy as np
+import torch
+
+from flowsentryx_amd import lib
+
+REC_DTYPE = np.dtype([("key", "<u4", 4), ("ts", "<u8"), ("len", "<u4"), ("dport", "<u2"),
+                      ("family", "u1"), ("pad", "u1")])
+assert REC_DTYPE.itemsize == lib.SHARD_RECORD_BYTES
+
+
+def records_to_headers(rec: np.ndarray):
+    """Header records that parse to the records' source, family, length and dst port."""
+    m = rec.shape[0]
+    hdr = np.zeros((m, 64), dtype=np.uint8)
+    key = rec["key"].copy().view(np.uint8).reshape(m, 16)
+    v6 = rec["family"] == 6
+    dp = rec["dport"].astype(np.uint32)
+    hdr[:, 12] = np.where(v6, 0x86, 0x08)
+    hdr[:, 13] = np.where(v6, 0xDD, 0x00)
+    hdr[~v6, 14] = 0x45
+    hdr[~v6, 23] = 17
+    hdr[~v6, 26:30] = key[~v6, :4]
+    hdr[~v6, 36] = (dp[~v6] >> 8) & 0xFF
+    hdr[~v6, 37] = dp[~v6] & 0xFF
+    hdr[v6, 20] = 17
+    hdr[v6, 22:38] = key[v6]
+    hdr[v6, 56] = (dp[v6] >> 8) & 0xFF
+    hdr[v6, 57] = dp[v6] & 0xFF
+    return hdr, rec["len"].copy(), rec["ts"].copy()
+
+
+class CpuShardEngine:
+    def __init__(self, oracle, **cfg):
+        self.oracle = oracle
+        self.o = oracle.Oracle(**cfg)
+        self.send_idx = np.zeros(0, dtype=np.int64)
+
+    def stream_ctx(self):
+        return contextlib.nullcontext()
+
+    @staticmethod
+    def _np(hdr, length, ts, n):
+        return (hdr.numpy().reshape(-1, 64)[:n], length.numpy().view(np.uint32)[:n],
+                ts.numpy().view(np.uint64)[:n])
+
+    def direct(self, hdr, length, ts, n, verdict):
+        h, l, t = self._np(hdr, length, ts, n)
+        verdict[:n] = torch.from_numpy(self.o.batch(h, l, t))
+
+    def pack(self, hdr, length, ts, n, G, verdict):
+        h, l, t = self._np(hdr, length, ts, n)
+        cls, keys = self.oracle.parse(h, l)
+        v = verdict.numpy()
+        v[:n][cls == 0] = 1
+        v[:n][cls == 1] = 2
+        ip = np.nonzero(cls >= 2)[0]
+        fam = np.where(cls[ip] == 3, 6, 4).astype(np.uint8)
+        own = np.array([lib.shard_owner(keys[i].tobytes(), int(f), G) for i, f in zip(ip, fam)],
+                       dtype=np.int64)
+        order = np.argsort(own, kind="stable")
+        ip, fam = ip[order], fam[order]
+        rec = np.zeros(ip.size, dtype=REC_DTYPE)
+        rec["key"] = keys[ip].view("<u4").reshape(-1, 4)
+        rec["ts"] = t[ip]
+        rec["len"] = l[ip]
+        rec["dport"] = self.oracle.dst_port(h[ip], l[ip]).astype(np.uint16)
+        rec["family"] = fam
+        self.send_idx = ip
+        counts = np.bincount(own, minlength=G).astype(np.int64)
+        return torch.from_numpy(rec.view(np.uint8).copy()), torch.from_numpy(counts)
+
+    def recv_buffer(self, m):
+        return torch.empty(max(1, m) * lib.SHARD_RECORD_BYTES, dtype=torch.uint8)
+
+    def owner_batch(self, recv, m):
+        rec = recv.numpy()[:m * lib.SHARD_RECORD_BYTES].view(REC_DTYPE)
+        h, l, t = records_to_headers(rec)
+        v = self.o.batch(h, l, t) if m else np.zeros(1, dtype=np.uint8)
+        return torch.from_numpy(v)
+
+    def scatter(self, ret, m, verdict):
+        verdict.numpy()[self.send_idx] = ret.numpy()[:m]
+
+    def stats(self):
+        return torch.tensor(self.o.stats(), dtype=torch.int64)

@@ -1,0 +1,91 @@
+"""One rank of a multi-process sharded run (spawned by tests/test_shard_*.py).
+
+Every rank builds the same seeded global stream, takes its contiguous slice of every
+global batch, runs flowsentryx_amd.shard.ShardedDataPlane, and rank 0 compares the
+gathered verdicts, stats_map and map dumps with ONE sequential oracle over the whole
+stream (the 1-GPU semantics)."""
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+
+def _stream(spec):
+    from test_gpu_parity import rand_stream
+    rng = np.random.default_rng(spec["seed"])
+    return rand_stream(rng, spec["n"], spec["n_ips"], dt_max=spec.get("dt_max", 300),
+                       v6_frac=spec.get("v6_frac", 0.0), nonip_frac=spec.get("nonip_frac", 0.0),
+                       short_frac=spec.get("short_frac", 0.0))
+
+
+def worker(rank, world, port, spec, out_path, engine_kind):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from oracle import pyoracle
+        from flowsentryx_amd.shard import ShardedDataPlane
+        cfg = spec["cfg"]
+        hdr, ln, ts = _stream(spec)
+        cuts = spec["cuts"]
+        if engine_kind == "cpu":
+            from shard_cpu import CpuShardEngine
+            eng = CpuShardEngine(pyoracle, **cfg)
+            dev = torch.device("cpu")
+        else:
+            torch.cuda.init()                 # torch's runtime first (tests/conftest.py)
+            torch.cuda.set_device(0)
+            from flowsentryx_amd import lib
+            from flowsentryx_amd.shard import HipShardEngine
+            dev = torch.device("cuda", 0)
+            ctx = lib.FsxContext(max_batch=spec.get("owner_batch", 1 << 16), **cfg)
+            eng = HipShardEngine(ctx, max(b - a for a, b in zip(cuts[:-1], cuts[1:])), dev)
+        plane = ShardedDataPlane(eng)
+        mine = []
+        for a, b in zip(cuts[:-1], cuts[1:]):
+            bounds = np.linspace(a, b, world + 1).astype(np.int64)
+            s0, s1 = int(bounds[rank]), int(bounds[rank + 1])
+            n = s1 - s0
+            th = torch.from_numpy(hdr[s0:s1].reshape(-1).copy()).to(dev)
+            tl = torch.from_numpy(ln[s0:s1].view(np.int32).copy()).to(dev)
+            tt = torch.from_numpy(ts[s0:s1].view(np.int64).copy()).to(dev)
+            tv = torch.zeros(max(n, 1), dtype=torch.uint8, device=dev)
+            plane.verdict_batch(th, tl, tt, n, tv)
+            mine.append(tv[:n].cpu().numpy().copy())
+        stats = plane.stats()
+        if engine_kind == "cpu":
+            dumps = {m: eng.o.map_dump(m) for m in spec["maps"]}
+        else:
+            dumps = {m: ctx.map_dump(m) for m in spec["maps"]}
+        got = [None] * world
+        dist.all_gather_object(got, (mine, dumps))
+        if rank == 0:
+            o = pyoracle.Oracle(**cfg)
+            ok, msg = True, []
+            for bi, (a, b) in enumerate(zip(cuts[:-1], cuts[1:])):
+                exp = o.batch(hdr[a:b], ln[a:b], ts[a:b])
+                v = np.concatenate([got[r][0][bi] for r in range(world)])
+                if not np.array_equal(v, exp):
+                    ok = False
+                    msg.append(f"batch {bi}: {int((v != exp).sum())} verdicts differ")
+            if tuple(stats) != o.stats():
+                ok = False
+                msg.append(f"stats {stats} != {o.stats()}")
+            for m in spec["maps"]:
+                union = {}
+                for r in range(world):
+                    d = got[r][1][m]
+                    if set(d) & set(union):
+                        ok = False
+                        msg.append(f"map {m}: a source on two owners")
+                    union.update(d)
+                if union != o.map_dump(m):
+                    ok = False
+                    msg.append(f"map {m}: {len(union)} vs {len(o.map_dump(m))} entries differ")
+            with open(out_path, "w") as f:
+                json.dump({"ok": ok, "msg": msg, "stats": list(stats)}, f)
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()

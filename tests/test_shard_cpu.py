@@ -1,0 +1,52 @@
+"""CPU (gloo, world_size 2 and 3): the sharded protocol of flowsentryx_amd/shard.py with
+the CPU engine (oracle owners) equals one sequential oracle over the whole stream —
+verdicts, stats_map and every map entry (SURVEY.md §8 e: the result must be exactly the
+1-GPU result)."""
+import json
+import socket
+
+import pytest
+import torch.multiprocessing as mp
+
+import shard_worker
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def run_sharded(tmp_path, world, spec, engine="cpu"):
+    out = tmp_path / "result.json"
+    mp.start_processes(shard_worker.worker, args=(world, _port(), spec, str(out), engine),
+                       nprocs=world, start_method="spawn")
+    res = json.loads(out.read_text())
+    assert res["ok"], res["msg"]
+    return res
+
+
+BASE = dict(n=24000, n_ips=300, seed=7, maps=[1, 2, 3, 4],
+            cuts=[0, 5000, 5001, 16000, 24000])
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_fixed_window(tmp_path, world):
+    spec = dict(BASE, cfg=dict(pps_threshold=7, window_ns=200_000, block_ns=1_000_000,
+                               max_entries=4096))
+    run_sharded(tmp_path, world, spec)
+
+
+def test_sharded_mixed_families_sliding_window(tmp_path):
+    spec = dict(BASE, v6_frac=0.3, nonip_frac=0.05, short_frac=0.03, seed=9,
+                cfg=dict(limiter=1, pps_threshold=5, window_ns=1_000_000, block_ns=50_000,
+                         max_entries=4096))
+    run_sharded(tmp_path, 2, spec)
+
+
+def test_sharded_token_bucket(tmp_path):
+    spec = dict(BASE, seed=11, maps=[3, 4, 5, 6],
+                cfg=dict(limiter=2, tb_rate=300_000, tb_burst=4, max_entries=4096))
+    run_sharded(tmp_path, 2, spec)
