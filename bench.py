@@ -8,10 +8,12 @@ per-source fixed-window rate limit + blacklist -> verdicts + map state
 every source with the reference weights (model/model.py:132-137). N=1 workload:
 BASELINE config 2 — 64M IPv4/UDP packets from 1M Zipf(1.1) sources over 30 s.
 
-Multi-GPU (torch.distributed.run, one rank per GPU): weak scaling — every rank
-generates and processes its own contiguous 64M-packet slice of one stream with
-disjoint source sets (rank-salted addresses), so no data-path collective is needed;
-DESIGN.md §7 describes the hash-sharded all-to-all variant.
+Multi-GPU (torch.distributed.run, one rank per GPU): weak scaling — one stream of
+N x 64M packets from one source population at the config's packet rate; rank r holds
+the contiguous slice [r*64M, (r+1)*64M) and every source is owned by one rank
+(hash of the address): RCCL all-to-all of 32-byte records to the owners, the full
+pipeline there, verdicts back by a second all-to-all (flowsentryx_amd/shard.py,
+DESIGN.md §7). The result equals the 1-GPU run over the whole stream.
 
 Prints ONE JSON line on rank 0 with the driver's contract plus:
   roofline      the dominant kernel (largest device time per step), its algorithmic
@@ -55,12 +57,17 @@ def parse_args():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", type=int, default=2)
-    ap.add_argument("--n", type=int, default=None, help="packets per rank (default: config)")
+    ap.add_argument("--packets", type=int, default=None, help="packets per rank (default: config)")
     ap.add_argument("--cpu-sample", type=int, default=16 << 20)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--check", action="store_true", help="verify a prefix against the oracle")
     ap.add_argument("--no-mlp", action="store_true", help="verdicts only (no features/scores)")
+    ap.add_argument("--chunks", type=int, default=4,
+                    help="N>1: sub-batches per step (the replicated blocklist of one filters "
+                         "the next)")
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="N>1 collectives: nccl (RCCL over xGMI) or gloo (rehearsal on one GPU)")
     ap.add_argument("--limiter-steps", type=int, default=5,
                     help="timed steps of the sliding-window and token-bucket legs (0: skip)")
     return ap.parse_args()
@@ -72,26 +79,43 @@ def main():
 
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
-    local = int(os.environ.get("LOCAL_RANK", 0))
+    # one rank per GPU; more ranks than GPUs only in a gloo rehearsal on one device
+    local = int(os.environ.get("LOCAL_RANK", 0)) % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(args.dist_backend)
 
     from flowsentryx_amd import lib, synth
 
-    p, zipf_s = synth.config_params(args.config, n=args.n)
+    p, zipf_s = synth.config_params(args.config, n=args.packets)
     n = int(p.n)
-    # weak scaling: rank r owns packets [r*n, (r+1)*n) of a world*n-packet stream,
-    # with its own source addresses (salted per rank)
-    p.ip_salt = p.ip_salt + 0x9E3779B1 * rank & 0xFFFFFFFF
+    # weak scaling: ONE stream of world*n packets at the config's packet rate (so
+    # world times as long) from one source population; rank r holds the contiguous
+    # slice [r*n, (r+1)*n) and the sources are hash-sharded over the ranks (RCCL
+    # all-to-all to their owners, flowsentryx_amd/shard.py)
+    p.n = n * world
+    p.duration_ns = p.duration_ns * world
     d_hdr = torch.empty(n * 64, dtype=torch.uint8, device="cuda")
     d_len = torch.empty(n, dtype=torch.int32, device="cuda")
     d_ts = torch.empty(n, dtype=torch.int64, device="cuda")
     d_v = torch.empty(n, dtype=torch.uint8, device="cuda")
-    synth.generate_device(p, zipf_s, 0, n, d_hdr.data_ptr(), d_len.data_ptr(), d_ts.data_ptr())
+    # N>1: the stream in world*chunks pieces of n/chunks packets, piece j on rank j % world
+    # (sub-batch j // world): rank r's slice is its pieces r, r+world, ... in order
+    chunks = max(1, args.chunks) if world > 1 else 1
+    bounds = [n * i // chunks for i in range(chunks + 1)]
+    for i in range(chunks):
+        a, b = bounds[i], bounds[i + 1]
+        j0 = world * a + rank * (b - a)
+        synth.generate_device(p, zipf_s, j0, b - a, d_hdr.data_ptr() + a * 64,
+                              d_len.data_ptr() + a * 4, d_ts.data_ptr() + a * 8)
     torch.cuda.synchronize()
+    p.n = n
+    p.duration_ns = p.duration_ns // world
 
     max_entries = max(1024, int(p.n_ips) if p.n_ips else n)
     ctx = lib.FsxContext(max_batch=n, max_entries=max_entries, device=local)
@@ -103,9 +127,20 @@ def main():
     d_prob = torch.empty(fcap, dtype=torch.float32, device="cuda")
     d_dec = torch.empty(fcap, dtype=torch.uint8, device="cuda")
 
+    plane = None
+    if world > 1:
+        from flowsentryx_amd.shard import HipShardEngine, ShardedDataPlane
+        eng = HipShardEngine(ctx, n, torch.device("cuda", local))
+        if not args.no_mlp:
+            eng.enable_flows(fcap)
+        plane = ShardedDataPlane(eng)
+
     def step():
         ctx.reset()
-        if args.no_mlp:
+        if plane is not None:
+            plane.reset()
+            plane.verdict_batch(d_hdr, d_len, d_ts, n, d_v, bounds=bounds, chunks=chunks)
+        elif args.no_mlp:
             ctx.verdict_batch_device(d_hdr.data_ptr(), d_len.data_ptr(), d_ts.data_ptr(), n,
                                      d_v.data_ptr())
         else:
@@ -133,17 +168,34 @@ def main():
     timings = ctx.last_timings()
     ctx.enable_timing(False)
     if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed], dtype=torch.float64,
+                         device="cuda" if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    stats = ctx.stats()
-    malicious = None if args.no_mlp else int(d_dec[:info["sources"]].sum().item())
+    exchange = None
+    if plane is not None:
+        stats = plane.stats()
+        ex = plane.last_exchange or {"sent": [], "received": []}
+        exchange = {"records_sent": ex["sent"], "records_received": ex["received"],
+                    "dropped_by_replica": ex.get("filtered", 0), "sub_batches": chunks,
+                    "record_bytes": lib.SHARD_RECORD_BYTES, "backend": args.dist_backend}
+        malicious = None
+        if not args.no_mlp:
+            fl = eng.flows
+            mal = torch.tensor([int(fl["dec"][:info["sources"]].sum().item())], device="cuda")
+            if args.dist_backend == "gloo":
+                mal = mal.cpu()
+            dist.all_reduce(mal)
+            malicious = int(mal.item())
+    else:
+        stats = ctx.stats()
+        malicious = None if args.no_mlp else int(d_dec[:info["sources"]].sum().item())
     ctx.close()
 
     # BASELINE config 2 also names the sliding-window and token-bucket limiters
     # (build-defined): the same batch through each, verdicts + maps only
     limiters = {}
-    if args.limiter_steps > 0:
+    if args.limiter_steps > 0 and world == 1:
         for lname, lid in (("sliding_window", lib.LIMIT_SLIDING_WINDOW),
                            ("token_bucket", lib.LIMIT_TOKEN_BUCKET)):
             with lib.FsxContext(max_batch=n, max_entries=max_entries, device=local,
@@ -166,7 +218,8 @@ def main():
                     dist.barrier()
                 lt = time.perf_counter() - l0
                 if dist:
-                    t = torch.tensor([lt], dtype=torch.float64, device="cuda")
+                    t = torch.tensor([lt], dtype=torch.float64,
+                                     device="cuda" if args.dist_backend == "nccl" else "cpu")
                     dist.all_reduce(t, op=dist.ReduceOp.MAX)
                     lt = float(t.item())
                 la, ld = lc.stats()
@@ -209,8 +262,10 @@ def main():
         traffic = None
         pmc = ROOT / "profiles" / "pmc_traffic.json"
         if pmc.exists():
-            row = json.loads(pmc.read_text()).get("kernels", {}).get(name, {})
-            traffic = row.get("hbm_bytes_per_launch")
+            doc = json.loads(pmc.read_text())
+            wl = doc.get("workload", {})
+            if wl.get("packets_per_gpu") == n and wl.get("config") == args.config and world == 1:
+                traffic = doc.get("kernels", {}).get(name, {}).get("hbm_bytes_per_launch")
         roofline = {
             "bound": "hbm", "kernel": name, "achieved": round(achieved, 1) if achieved else None,
             "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -251,9 +306,11 @@ def main():
                                   "(limiters)" if args.limiter_steps > 0 else "")
                                + ("" if args.no_mlp else "; per-source features + q8 MLP score "
                                   "(model_weights.pth)"),
-                   "packets_per_gpu": n, "sources": sources, "parallelism": f"dp{world}"},
+                   "packets_per_gpu": n, "sources": sources,
+                   "parallelism": f"dp{world}" + ("" if world == 1 else
+                                                  " (sources hash-sharded, all-to-all)")},
         "roofline": roofline, "pipeline": pipeline, "cpu_baseline": cpu,
-        "limiters": limiters or None,
+        "limiters": limiters or None, "exchange": exchange,
         "kernels": [{"name": a, "ms_per_step": round(b, 4), "launches": c} for a, b, c in timings],
         "stats": {"allowed": stats[0], "dropped": stats[1], "sources": info["sources"],
                   "malicious_sources": malicious}, "check": check,

@@ -50,9 +50,12 @@ struct fsx_ctx {
     float *d_prob = nullptr;
     uint8_t *d_dec = nullptr;
     uint64_t score_cap = 0;
-    // sharding: per (owner, tile) counts of fsx_shard_pack_device
+    // sharding: per (owner, tile) counts of fsx_shard_pack_device, blocklist replica
     uint32_t *d_shard_cnt = nullptr;
     uint64_t shard_cnt_cap = 0;
+    ShardBlock *d_rep = nullptr;
+    uint64_t rep_slots = 0;
+    bool rep_valid = false;
     // sliding-window history (limiter == FSX_LIMIT_SLIDING_WINDOW only)
     HistBufs hist{};
     // per-source flow accumulators
@@ -189,7 +192,7 @@ void fsx_close(fsx_ctx *c) {
     hipFree(c->d_res); hipFree(c->d_val);
     for (int b = 0; b < 2; ++b) { hipFree(c->hist.t[b]); hipFree(c->hist.l[b]); }
     hipFree(c->hist.tile_cnt); hipFree(c->hist.tile_off); hipFree(c->hist.total);
-    hipFree(c->d_shard_cnt);
+    hipFree(c->d_shard_cnt); hipFree(c->d_rep);
     for (int r = 0; r < kRing; ++r)
         for (int i = 0; i < kMaxEv; ++i) if (c->ev[r][i]) hipEventDestroy(c->ev[r][i]);
     if (c->own_stream) hipStreamDestroy(c->own_stream);
@@ -649,8 +652,8 @@ uint32_t fsx_shard_owner(const uint8_t *key16, int family, uint32_t n_shards) {
 }
 
 int fsx_shard_pack_device(fsx_ctx *c, const uint8_t *d_hdr, const uint32_t *d_len, const uint64_t *d_ts,
-                          size_t n, uint32_t G, uint8_t *d_verdict, void *d_records, uint32_t *d_send_idx,
-                          uint64_t *d_counts) {
+                          size_t n, uint32_t G, uint32_t flags, uint8_t *d_verdict, void *d_records,
+                          uint32_t *d_send_idx, uint64_t *d_counts) {
     if (!c) return -EINVAL;
     if (G == 0 || G > FSX_MAX_SHARDS) return set_err(c, -EINVAL, "n_shards must be 1..%d", FSX_MAX_SHARDS);
     if (n > kMaxBatchLimit) return set_err(c, -E2BIG, "n=%zu too large", n);
@@ -660,16 +663,63 @@ int fsx_shard_pack_device(fsx_ctx *c, const uint8_t *d_hdr, const uint32_t *d_le
     if (rc) return rc;
     const uint64_t need = (uint64_t)G * (n / 4096 + 1);
     if (need > c->shard_cnt_cap) {
-        hipFree(c->d_shard_cnt);
+        hipFree(c->d_shard_cnt); hipFree(c->d_rep);
         c->d_shard_cnt = nullptr;
         c->shard_cnt_cap = 0;
         HIPCHK(c, hipMalloc(&c->d_shard_cnt, need * 4));
         c->shard_cnt_cap = need;
     }
+    const Replica rep{c->d_rep, c->rep_slots ? c->rep_slots - 1 : 0};
+    const bool filt = (flags & FSX_SHARD_FILTER_BLOCKLIST) && c->rep_valid;
     hipError_t e = launch_shard_pack(d_hdr, d_len, d_ts, (uint32_t)n, G, d_verdict,
                                      reinterpret_cast<ShardRecord *>(d_records), d_send_idx, d_counts,
-                                     c->d_shard_cnt, c->stream);
+                                     c->d_shard_cnt, filt ? &rep : nullptr, c->stream);
     if (e != hipSuccess) return set_err(c, -EIO, "shard pack: %s", hipGetErrorString(e));
+    return 0;
+}
+
+int fsx_shard_clock_device(fsx_ctx *c, const uint64_t *d_ts, size_t n, uint64_t *d_out3) {
+    if (!c || !d_out3 || (n && !d_ts)) return -EINVAL;
+    if (n > kMaxBatchLimit) return set_err(c, -E2BIG, "n=%zu too large", n);
+    int rc = sel(c);
+    if (rc) return rc;
+    hipError_t e = launch_shard_clock(d_ts, (uint32_t)n, d_out3, c->stream);
+    if (e != hipSuccess) return set_err(c, -EIO, "shard clock: %s", hipGetErrorString(e));
+    return 0;
+}
+
+int fsx_blocklist_export_device(fsx_ctx *c, void *d_entries, size_t cap, uint64_t *d_count) {
+    if (!c || !d_count || (cap && !d_entries)) return -EINVAL;
+    int rc = sel(c);
+    if (rc) return rc;
+    if (c->pending && (rc = fsx_sync(c))) return rc;
+    hipError_t e = launch_blocklist_export(c->table, c->lim.table_mask, reinterpret_cast<ShardBlock *>(d_entries),
+                                           cap, reinterpret_cast<unsigned long long *>(d_count), c->stream);
+    if (e != hipSuccess) return set_err(c, -EIO, "blocklist export: %s", hipGetErrorString(e));
+    return 0;
+}
+
+int fsx_blocklist_replica_device(fsx_ctx *c, const void *d_entries, size_t m) {
+    if (!c || (m && !d_entries)) return -EINVAL;
+    int rc = sel(c);
+    if (rc) return rc;
+    const uint64_t need = next_pow2(std::max<uint64_t>(64, 2 * (uint64_t)m));
+    if (need > c->rep_slots) {
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        hipFree(c->d_rep);
+        c->d_rep = nullptr;
+        c->rep_slots = 0;
+        c->rep_valid = false;
+        HIPCHK(c, hipMalloc(&c->d_rep, need * sizeof(ShardBlock)));
+        c->rep_slots = need;
+    }
+    hipError_t e = launch_replica_build(reinterpret_cast<const ShardBlock *>(d_entries), m, c->d_rep,
+                                        c->rep_slots - 1, c->stream);
+    if (e != hipSuccess)
+        return set_err(c, -EIO, "replica build (m=%zu slots=%llu rep=%p in=%p stream=%p): %s", m,
+                       (unsigned long long)c->rep_slots, (void *)c->d_rep, d_entries, (void *)c->stream,
+                       hipGetErrorString(e));
+    c->rep_valid = true;
     return 0;
 }
 

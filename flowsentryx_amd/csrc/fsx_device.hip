@@ -1352,6 +1352,7 @@ hipError_t launch_verdict_pipeline(const uint8_t *hdr, const uint32_t *len, cons
                                    bool do_limit, const FlowRequest *flows, const HistBufs &hist,
                                    hipStream_t st, hipEvent_t *ev, int nev, int *nev_used,
                                    const char **names) {
+    (void)hipGetLastError();   // a stale error of another caller is not ours
     int ei = 0;
     auto mark = [&](const char *name) {
         if (ev && ei < nev) {
@@ -1509,6 +1510,7 @@ __global__ void k_map_op(Slot *table, TableState *tstate, Limits lim, int op, in
 hipError_t launch_map_op(Slot *table, TableState *tstate, const Limits &lim, int op, int map_id,
                          const uint32_t key[4], const uint64_t val[3], uint64_t flags,
                          int32_t *d_result, uint64_t *d_val, hipStream_t st) {
+    (void)hipGetLastError();   // a stale error of another caller is not ours
     k_map_op<<<1, 64, 0, st>>>(table, tstate, lim, op, map_id, key[0], key[1], key[2], key[3],
                                val[0], val[1], val[2], flags, d_result, d_val);
     return hipGetLastError();
@@ -1538,6 +1540,7 @@ __global__ __launch_bounds__(256) void k_map_dump(const Slot *table, Limits lim,
 hipError_t launch_map_dump(const Slot *table, const Limits &lim, int map_id, uint8_t *d_keys,
                            uint64_t *d_vals, uint64_t cap, unsigned long long *d_count,
                            hipStream_t st) {
+    (void)hipGetLastError();   // a stale error of another caller is not ours
     const uint64_t slots = lim.table_mask + 1;
     const uint32_t grid = (uint32_t)std::min<uint64_t>(4096, (slots + 255) / 256);
     k_map_dump<<<grid, 256, 0, st>>>(table, lim, map_id, d_keys, d_vals, cap, d_count);

@@ -357,6 +357,7 @@ hipError_t launch_flows(const uint64_t *S, const uint64_t *pay, BatchState *bs, 
                         uint32_t *span_list, void *acc, uint8_t *keys16, uint8_t *fam, float *feat,
                         float *prob, uint8_t *dec, uint32_t cap, const ScoreParams &P, uint32_t salt,
                         uint32_t n, hipStream_t st) {
+    (void)hipGetLastError();   // a stale error of another caller is not ours
     const FlowOut out{(FlowAcc *)acc, keys16, fam, feat, prob, dec, cap};
     const uint32_t nsub = (n + kFT - 1) / kFT;
     const uint32_t grid = std::max<uint32_t>(1, std::min<uint32_t>(16384, (nsub + 3) / 4));

@@ -324,6 +324,7 @@ __global__ __launch_bounds__(1024) void k_tb_carry(BatchState *bs, const CMap *_
 hipError_t launch_token_bucket(const uint64_t *S, const uint64_t *ts, const uint32_t *len, BatchState *bs,
                                const Scratch &sc, Slot *table, const Limits &lim, uint32_t n,
                                hipStream_t st) {
+    (void)hipGetLastError();   // a stale error of another caller is not ours
     const uint32_t gridSeg = std::min<uint32_t>(2048, std::max<uint32_t>(1, (n + 255) / 256));
     const uint32_t gridTiles = std::min<uint32_t>(4096, std::max<uint32_t>(1, (n + kTile - 1) / kTile));
     uint32_t *seg_j = sc.seg_order;
@@ -716,6 +717,7 @@ __global__ void k_sw_finish(const BatchState *bs, TableState *tst, const uint64_
 hipError_t launch_sliding_window(const uint64_t *S, const uint64_t *ts, const uint32_t *len, BatchState *bs,
                                  const Scratch &sc, Slot *table, TableState *tstate, const HistBufs &hb,
                                  const Limits &lim, uint32_t n, hipStream_t st) {
+    (void)hipGetLastError();   // a stale error of another caller is not ours
     const uint32_t gridSeg = std::min<uint32_t>(2048, std::max<uint32_t>(1, (n + 255) / 256));
     const uint32_t *cls = sc.sort_ctl + 1028;
     k_walk_sw<false><<<gridSeg, 256, 0, st>>>(S, bs, tstate, sc.seg_start, sc.seg_slot, ts, len, sc.pay[0],

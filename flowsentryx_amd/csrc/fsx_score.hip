@@ -48,6 +48,7 @@ ScoreParams make_score_params(const int8_t w[8], float inv_in, int32_t zp_in, fl
 hipError_t launch_score(const float *feat, size_t n, float *prob, uint8_t *dec, const int8_t w[8],
                         float inv_in, int32_t zp_in, float bias_over_ats, float mult, int32_t zp_out,
                         const uint8_t lut[256], hipStream_t st) {
+    (void)hipGetLastError();   // a stale error of another caller is not ours
     if (n == 0) return hipSuccess;
     const ScoreParams P = make_score_params(w, inv_in, zp_in, bias_over_ats, mult, zp_out, lut);
     const uint32_t grid = (uint32_t)std::min<uint64_t>(8192, (n + 255) / 256);

@@ -21,6 +21,23 @@ static_assert(sizeof(ShardRecord) == 32, "32-byte exchange records");
 
 constexpr uint64_t kShardSeed = 0x5A4D0F5EED5ull;   // fixed: every rank must agree
 
+// One blacklist entry of the replicated blocklist (all-gathered between ranks).
+struct alignas(16) ShardBlock {
+    uint32_t key[4];
+    uint64_t till;        // ipv{4,6}_blacklist_map value
+    uint32_t tag;         // 1 IPv4, 2 IPv6
+    uint32_t pad;
+};
+static_assert(sizeof(ShardBlock) == 32, "32-byte blocklist entries");
+
+// The replica: open addressing over next_pow2(2 m) ShardBlock slots (tag 0 = empty).
+struct Replica {
+    const ShardBlock *slots;
+    uint64_t mask;
+};
+
+constexpr uint32_t kShardFilter = 1u;   // fsx_shard_pack_device flag (FSX_SHARD_FILTER_BLOCKLIST)
+
 // owner = floor(h * G / 2^32) of a 32-bit mix of (family tag, address).
 __host__ __device__ inline uint32_t shard_owner_of(uint32_t tag, const uint32_t k[4], uint32_t G) {
     const uint64_t h = slot_hash(tag, k, kShardSeed);
@@ -29,7 +46,13 @@ __host__ __device__ inline uint32_t shard_owner_of(uint32_t tag, const uint32_t 
 
 hipError_t launch_shard_pack(const uint8_t *hdr, const uint32_t *len, const uint64_t *ts, uint32_t n,
                              uint32_t G, uint8_t *verdict, ShardRecord *rec, uint32_t *send_idx,
-                             uint64_t *owner_total, uint32_t *scratch, hipStream_t st);
+                             uint64_t *owner_total, uint32_t *scratch, const Replica *rep,
+                             hipStream_t st);
+hipError_t launch_shard_clock(const uint64_t *ts, uint32_t n, uint64_t *out3, hipStream_t st);
+hipError_t launch_blocklist_export(const Slot *table, uint64_t table_mask, ShardBlock *out, uint64_t cap,
+                                   unsigned long long *count, hipStream_t st);
+hipError_t launch_replica_build(const ShardBlock *in, uint64_t m, ShardBlock *slots, uint64_t mask,
+                                hipStream_t st);
 hipError_t launch_shard_unpack(const ShardRecord *rec, uint32_t m, uint8_t *hdr, uint32_t *len,
                                uint64_t *ts, hipStream_t st);
 hipError_t launch_shard_scatter(const uint8_t *ret, const uint32_t *send_idx, uint32_t m, uint8_t *verdict,

@@ -65,11 +65,41 @@ __device__ __forceinline__ uint32_t owner_dev(uint32_t fam, const uint32_t k[4],
     return shard_owner_of(fam == 6 ? 2u : 1u, k, G);
 }
 
+constexpr uint64_t kReplicaSeed = kShardSeed ^ 0xB10C;
+
+// Blacklist entry of (tag, key) in the replica, or null.
+__device__ __forceinline__ const ShardBlock *replica_find(const Replica &r, uint32_t tag, const uint32_t k[4]) {
+    uint64_t i = slot_hash(tag, k, kReplicaSeed) & r.mask;
+    for (uint64_t probes = 0; probes <= r.mask; ++probes) {
+        const ShardBlock &b = r.slots[i];
+        if (b.tag == 0) return nullptr;
+        if (b.tag == tag && b.key[0] == k[0] && b.key[1] == k[1] && b.key[2] == k[2] && b.key[3] == k[3])
+            return &b;
+        i = (i + 1) & r.mask;
+    }
+    return nullptr;
+}
+
+// Parse + replica check: 0 DROP (parse), 1 PASS (non-IP), 2 DROP (blacklisted in the
+// replica: till > 0 and now <= till, src/fsx_kern.c:189-215 — exact when the clock is
+// monotone over the batches so far, which the host checks before asking for it),
+// 4 / 6 an IP packet for its owner.
+__device__ __forceinline__ uint32_t shard_classify(const uint8_t *rec, uint32_t L, uint64_t now,
+                                                   const Replica *rep, uint32_t k[4], uint32_t &dport) {
+    const uint32_t f = shard_parse(rec, L, k, dport);
+    if (f >= 4 && rep) {
+        const ShardBlock *b = replica_find(*rep, f == 6 ? 2u : 1u, k);
+        if (b && b->till > 0 && !(now > b->till)) return 2;
+    }
+    return f;
+}
+
 // Per tile: per-owner IP-packet counts, owner-major [G][tiles].
 __global__ __launch_bounds__(256) void k_shard_count(const uint8_t *__restrict__ hdr,
-                                                     const uint32_t *__restrict__ len, uint32_t n,
+                                                     const uint32_t *__restrict__ len,
+                                                     const uint64_t *__restrict__ ts, uint32_t n,
                                                      uint32_t G, uint32_t *__restrict__ cnt,
-                                                     uint32_t ntiles) {
+                                                     uint32_t ntiles, Replica rep, int use_rep) {
     __shared__ uint32_t sh[kMaxShards];
     const uint32_t t = blockIdx.x;
     if (threadIdx.x < kMaxShards) sh[threadIdx.x] = 0;
@@ -78,7 +108,7 @@ __global__ __launch_bounds__(256) void k_shard_count(const uint8_t *__restrict__
         const uint32_t i = t * kShardTile + r * 256u + threadIdx.x;
         if (i >= n) break;
         uint32_t k[4], dp;
-        const uint32_t f = shard_parse(hdr + (size_t)i * 64, len[i], k, dp);
+        const uint32_t f = shard_classify(hdr + (size_t)i * 64, len[i], ts[i], use_rep ? &rep : nullptr, k, dp);
         if (f >= 4) atomicAdd(&sh[owner_dev(f, k, G)], 1u);
     }
     __syncthreads();
@@ -118,6 +148,7 @@ __global__ __launch_bounds__(1024) void k_shard_scan(uint32_t *__restrict__ cnt,
         const uint32_t b1 = o + 1 < G ? cnt[(size_t)(o + 1) * ntiles] : s_carry;
         owner_total[o] = b1 - b0;
     }
+    if (threadIdx.x == 0) owner_total[G] = 0;   // packets dropped by the replica (k_shard_pack)
 }
 
 // Per tile: stable (arrival order) placement of every IP packet at its owner's offset.
@@ -127,34 +158,45 @@ __global__ __launch_bounds__(256) void k_shard_pack(const uint8_t *__restrict__ 
                                                     uint32_t G, const uint32_t *__restrict__ offs,
                                                     uint32_t ntiles, ShardRecord *__restrict__ rec,
                                                     uint32_t *__restrict__ send_idx,
-                                                    uint8_t *__restrict__ verdict) {
+                                                    uint8_t *__restrict__ verdict, Replica rep,
+                                                    int use_rep, uint64_t *__restrict__ owner_total) {
     __shared__ uint32_t s_base[kMaxShards];
     __shared__ uint32_t s_wc[4][kMaxShards];
+    __shared__ uint32_t s_filtered;
     const uint32_t t = blockIdx.x, lane = lane_id(), w = threadIdx.x >> 6;
     if (threadIdx.x < G) s_base[threadIdx.x] = offs[(size_t)threadIdx.x * ntiles + t];
     // wave w owns packets [t*4096 + w*1024, +1024) in arrival order: count per owner
     // first (so a wave places after the waves before it), then place in order
     uint32_t of[16];   // owner << 4 | class (0 DROP, 1 PASS, 4/6 IP, 15 none)
     for (uint32_t o = threadIdx.x; o < 4 * kMaxShards; o += 256) (&s_wc[0][0])[o] = 0;
+    if (threadIdx.x == 0) s_filtered = 0;
     __syncthreads();
+    uint32_t filtered = 0;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
         const uint32_t i = t * kShardTile + w * 1024u + (uint32_t)r * 64u + lane;
         of[r] = 15u;
         if (i < n) {
             uint32_t k[4], dp;
-            const uint32_t f = shard_parse(hdr + (size_t)i * 64, len[i], k, dp);
+            const uint32_t f = shard_classify(hdr + (size_t)i * 64, len[i], ts[i], use_rep ? &rep : nullptr, k, dp);
             if (f >= 4) {
                 const uint32_t o = owner_dev(f, k, G);
                 of[r] = (o << 4) | f;
                 atomicAdd(&s_wc[w][o], 1u);
             } else {
                 of[r] = f;
-                verdict[i] = f == 0 ? 1u : 2u;   // XDP_DROP / XDP_PASS, never counted
+                // parse DROP / non-IP PASS are never counted; a replica DROP is counted
+                // in stats_map.dropped (src/fsx_kern.c:208-214) by the host
+                verdict[i] = f == 1 ? 2u : 1u;
+                filtered += f == 2;
             }
         }
     }
+    filtered = wave_sum(filtered);
+    if (lane == 0 && filtered) atomicAdd(&s_filtered, filtered);
     __syncthreads();
+    if (threadIdx.x == 0 && s_filtered)
+        atomicAdd(reinterpret_cast<unsigned long long *>(&owner_total[G]), (unsigned long long)s_filtered);
     if (threadIdx.x < G) {   // exclusive over the waves, from the tile's owner base
         const uint32_t o = threadIdx.x;
         uint32_t b = s_base[o];
@@ -246,17 +288,115 @@ __global__ __launch_bounds__(256) void k_shard_scatter(const uint8_t *__restrict
 
 hipError_t launch_shard_pack(const uint8_t *hdr, const uint32_t *len, const uint64_t *ts, uint32_t n,
                              uint32_t G, uint8_t *verdict, ShardRecord *rec, uint32_t *send_idx,
-                             uint64_t *owner_total, uint32_t *scratch, hipStream_t st) {
-    if (n == 0) return hipMemsetAsync(owner_total, 0, (size_t)G * 8, st);
+                             uint64_t *owner_total, uint32_t *scratch, const Replica *rep,
+                             hipStream_t st) {
+    (void)hipGetLastError();   // a stale error of another caller is not ours
+    if (n == 0) return hipMemsetAsync(owner_total, 0, (size_t)(G + 1) * 8, st);
     const uint32_t ntiles = (n + kShardTile - 1) / kShardTile;
-    k_shard_count<<<ntiles, 256, 0, st>>>(hdr, len, n, G, scratch, ntiles);
+    const Replica r = rep ? *rep : Replica{nullptr, 0};
+    const int use = rep != nullptr && rep->slots != nullptr;
+    k_shard_count<<<ntiles, 256, 0, st>>>(hdr, len, ts, n, G, scratch, ntiles, r, use);
     k_shard_scan<<<1, 1024, 0, st>>>(scratch, n, owner_total, G, ntiles);
-    k_shard_pack<<<ntiles, 256, 0, st>>>(hdr, len, ts, n, G, scratch, ntiles, rec, send_idx, verdict);
+    k_shard_pack<<<ntiles, 256, 0, st>>>(hdr, len, ts, n, G, scratch, ntiles, rec, send_idx, verdict, r,
+                                         use, owner_total);
+    return hipGetLastError();
+}
+
+// Clock facts of a local batch: {min ts, max ts, any decrease in arrival order}.
+__global__ __launch_bounds__(256) void k_shard_clock(const uint64_t *__restrict__ ts, uint32_t n,
+                                                     unsigned long long *out3) {
+    uint64_t mn = ~0ull, mx = 0;
+    uint32_t dec = 0;
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) {
+        const uint64_t t = ts[i];
+        mn = t < mn ? t : mn;
+        mx = t > mx ? t : mx;
+        if (i > 0 && ts[i - 1] > t) dec = 1;
+    }
+    mx = wave_max(mx);
+    mn = ~wave_max(~mn);
+    dec = __ballot(dec != 0) ? 1u : 0u;
+    if (lane_id() == 0) {
+        atomicMin(&out3[0], (unsigned long long)mn);
+        atomicMax(&out3[1], (unsigned long long)mx);
+        if (dec) atomicOr(&out3[2], 1ull);
+    }
+}
+
+hipError_t launch_shard_clock(const uint64_t *ts, uint32_t n, uint64_t *out3, hipStream_t st) {
+    (void)hipGetLastError();   // a stale error of another caller is not ours
+    const uint64_t init[3] = {~0ull, 0ull, 0ull};
+    hipError_t e = hipMemcpyAsync(out3, init, sizeof(init), hipMemcpyHostToDevice, st);
+    if (e != hipSuccess || n == 0) return e;
+    const uint32_t grid = std::min<uint32_t>(2048, (n + 255) / 256);
+    k_shard_clock<<<grid, 256, 0, st>>>(ts, n, reinterpret_cast<unsigned long long *>(out3));
+    return hipGetLastError();
+}
+
+// Every live blacklist entry (till > 0) of this rank's table.
+__global__ __launch_bounds__(256) void k_blocklist_export(const Slot *table, uint64_t mask, ShardBlock *out,
+                                                          uint64_t cap, unsigned long long *count) {
+    for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i <= mask; i += (uint64_t)gridDim.x * 256u) {
+        const Slot &s = table[i];
+        if (s.tag == 0 || !(s.flags & SLOT_HAS_BL) || s.till == 0) continue;
+        const unsigned long long o = atomicAdd(count, 1ull);
+        if (o >= cap) continue;
+        ShardBlock b;
+        b.key[0] = s.key[0]; b.key[1] = s.key[1]; b.key[2] = s.key[2]; b.key[3] = s.key[3];
+        b.till = s.till;
+        b.tag = s.tag;
+        b.pad = 0;
+        out[o] = b;
+    }
+}
+
+hipError_t launch_blocklist_export(const Slot *table, uint64_t table_mask, ShardBlock *out, uint64_t cap,
+                                   unsigned long long *count, hipStream_t st) {
+    (void)hipGetLastError();   // a stale error of another caller is not ours
+    hipError_t e = hipMemsetAsync(count, 0, 8, st);
+    if (e != hipSuccess) return e;
+    const uint32_t grid = (uint32_t)std::min<uint64_t>(4096, (table_mask + 256) / 256);
+    k_blocklist_export<<<grid, 256, 0, st>>>(table, table_mask, out, cap, count);
+    return hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void k_replica_clear(ShardBlock *slots, uint64_t mask) {
+    for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i <= mask; i += (uint64_t)gridDim.x * 256u)
+        slots[i].tag = 0;
+}
+
+// Insert m distinct entries (every source has one owner) into cleared replica slots.
+__global__ __launch_bounds__(256) void k_replica_build(const ShardBlock *__restrict__ in, uint64_t m,
+                                                       ShardBlock *slots, uint64_t mask) {
+    for (uint64_t j = (uint64_t)blockIdx.x * 256u + threadIdx.x; j < m; j += (uint64_t)gridDim.x * 256u) {
+        const ShardBlock b = in[j];
+        uint64_t i = slot_hash(b.tag, b.key, kReplicaSeed) & mask;
+        for (uint64_t probes = 0; probes <= mask; ++probes) {
+            if (atomicCAS(&slots[i].tag, 0u, b.tag) == 0u) {
+                slots[i].key[0] = b.key[0]; slots[i].key[1] = b.key[1];
+                slots[i].key[2] = b.key[2]; slots[i].key[3] = b.key[3];
+                slots[i].till = b.till;
+                break;
+            }
+            i = (i + 1) & mask;
+        }
+    }
+}
+
+hipError_t launch_replica_build(const ShardBlock *in, uint64_t m, ShardBlock *slots, uint64_t mask,
+                                hipStream_t st) {
+    (void)hipGetLastError();   // a stale error of another caller is not ours
+    const uint32_t cgrid = (uint32_t)std::min<uint64_t>(1024, (mask + 256) / 256);
+    k_replica_clear<<<cgrid, 256, 0, st>>>(slots, mask);
+    if (m == 0) return hipGetLastError();
+    const uint32_t grid = (uint32_t)std::min<uint64_t>(1024, (m + 255) / 256);
+    k_replica_build<<<grid, 256, 0, st>>>(in, m, slots, mask);
     return hipGetLastError();
 }
 
 hipError_t launch_shard_unpack(const ShardRecord *rec, uint32_t m, uint8_t *hdr, uint32_t *len,
                                uint64_t *ts, hipStream_t st) {
+    (void)hipGetLastError();   // a stale error of another caller is not ours
     if (m == 0) return hipSuccess;
     const uint32_t grid = std::min<uint32_t>(4096, (m + 255) / 256);
     k_shard_unpack<<<grid, 256, 0, st>>>(rec, m, hdr, len, ts);
@@ -265,6 +405,7 @@ hipError_t launch_shard_unpack(const ShardRecord *rec, uint32_t m, uint8_t *hdr,
 
 hipError_t launch_shard_scatter(const uint8_t *ret, const uint32_t *send_idx, uint32_t m, uint8_t *verdict,
                                 hipStream_t st) {
+    (void)hipGetLastError();   // a stale error of another caller is not ours
     if (m == 0) return hipSuccess;
     const uint32_t grid = std::min<uint32_t>(4096, (m + 255) / 256);
     k_shard_scatter<<<grid, 256, 0, st>>>(ret, send_idx, m, verdict);

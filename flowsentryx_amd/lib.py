@@ -127,7 +127,11 @@ def load_library() -> C.CDLL:
         "fsx_enable_timing": (C.c_int, [vp, C.c_int]),
         "fsx_last_batch_info": (C.c_int, [vp, vp, C.c_int]),
         "fsx_shard_owner": (C.c_uint32, [vp, C.c_int, C.c_uint32]),
-        "fsx_shard_pack_device": (C.c_int, [vp, vp, vp, vp, sz, C.c_uint32, vp, vp, vp, vp]),
+        "fsx_shard_pack_device": (C.c_int, [vp, vp, vp, vp, sz, C.c_uint32, C.c_uint32, vp, vp,
+                                            vp, vp]),
+        "fsx_shard_clock_device": (C.c_int, [vp, vp, sz, vp]),
+        "fsx_blocklist_export_device": (C.c_int, [vp, vp, sz, vp]),
+        "fsx_blocklist_replica_device": (C.c_int, [vp, vp, sz]),
         "fsx_shard_unpack_device": (C.c_int, [vp, vp, sz, vp, vp, vp]),
         "fsx_shard_scatter_device": (C.c_int, [vp, vp, vp, sz, vp]),
     }
@@ -148,10 +152,13 @@ ABI_SYMBOLS = [
     "fsx_reset", "fsx_load_q8_model", "fsx_score", "fsx_score_device", "fsx_flow_features",
     "fsx_last_timings", "fsx_enable_timing", "fsx_last_batch_info",
     "fsx_shard_owner", "fsx_shard_pack_device", "fsx_shard_unpack_device",
-    "fsx_shard_scatter_device",
+    "fsx_shard_scatter_device", "fsx_shard_clock_device", "fsx_blocklist_export_device",
+    "fsx_blocklist_replica_device",
 ]
 
 SHARD_RECORD_BYTES = 32
+SHARD_BLOCK_BYTES = 32
+SHARD_FILTER_BLOCKLIST = 1
 MAX_SHARDS = 64
 
 
@@ -372,10 +379,23 @@ class FsxContext:
 
     # -- sharding (SURVEY.md §8 e; protocol in flowsentryx_amd/shard.py)
     def shard_pack_device(self, d_hdr: int, d_len: int, d_ts: int, n: int, n_shards: int,
-                          d_verdict: int, d_records: int, d_send_idx: int, d_counts: int):
+                          d_verdict: int, d_records: int, d_send_idx: int, d_counts: int,
+                          flags: int = 0):
         self._check(self._lib.fsx_shard_pack_device(self._h, d_hdr, d_len, d_ts, n, n_shards,
-                                                    d_verdict, d_records, d_send_idx, d_counts),
-                    "fsx_shard_pack_device")
+                                                    flags, d_verdict, d_records, d_send_idx,
+                                                    d_counts), "fsx_shard_pack_device")
+
+    def shard_clock_device(self, d_ts: int, n: int, d_out3: int):
+        self._check(self._lib.fsx_shard_clock_device(self._h, d_ts, n, d_out3),
+                    "fsx_shard_clock_device")
+
+    def blocklist_export_device(self, d_entries: int, cap: int, d_count: int):
+        self._check(self._lib.fsx_blocklist_export_device(self._h, d_entries, cap, d_count),
+                    "fsx_blocklist_export_device")
+
+    def blocklist_replica_device(self, d_entries: int, m: int):
+        self._check(self._lib.fsx_blocklist_replica_device(self._h, d_entries, m),
+                    "fsx_blocklist_replica_device")
 
     def shard_unpack_device(self, d_records: int, m: int, d_hdr: int, d_len: int, d_ts: int):
         self._check(self._lib.fsx_shard_unpack_device(self._h, d_records, m, d_hdr, d_len, d_ts),

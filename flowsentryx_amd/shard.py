@@ -13,11 +13,20 @@ unchanged batch pipeline on all of that source's packets:
   3. owner     records -> header records, the batch pipeline on them (maps, verdicts,
                optionally flow features + MLP scores of the owned sources)
   4. all-to-all of the verdicts back (1 byte per packet), scatter to arrival positions
-  5. stats_map = all-reduce(sum) of the owners' counters
+  5. all-gather of every owner's live blacklist entries (the replicated blocklist);
+     the next sub-batch's pack drops packets of replica-blacklisted sources locally
+     (now <= till: the owner would drop them without touching any state,
+     src/fsx_kern.c:189-215) — taken only when that sub-batch's clock is non-decreasing
+     in global order (one all-gather of {min, max, decreases} per rank), which is exactly
+     the condition under which no earlier packet can have deleted the entry
+  6. stats_map = all-reduce(sum) of the owners' counters + the locally dropped packets
 
-Rank slices are concatenated in rank order on the owner, so every source's packets
-arrive there in global arrival order and the sharded result equals the 1-GPU run
-(tests/test_shard_*.py check this bit-exactly).
+A global batch is cut into `chunks` sub-batches; in sub-batch i every rank contributes
+the i-th piece of its slice, and the global order of a sub-batch is rank 0's piece,
+then rank 1's, ... (the arrival shard "chunk j on rank j mod G" of SURVEY.md §8 d
+config 4). Pieces are concatenated in rank order on the owner, so every source's
+packets arrive there in global arrival order and the sharded result equals the 1-GPU
+run over the same order (tests/test_shard_*.py check this bit-exactly).
 
 The protocol is written against an engine (pack / owner_batch / scatter / stats): the
 HIP engine below drives libfsx_hip.so on device tensors; tests drive the same protocol
@@ -69,7 +78,10 @@ class HipShardEngine:
         self.owner_cap = int(ctx.config.max_batch)
         self.rec = torch.empty(max(1, max_local) * REC, dtype=torch.uint8, device=device)
         self.send_idx = torch.empty(max(1, max_local), dtype=torch.int32, device=device)
-        self.counts = torch.empty(lib.MAX_SHARDS, dtype=torch.int64, device=device)
+        self.counts = torch.empty(lib.MAX_SHARDS + 1, dtype=torch.int64, device=device)
+        self.clock3 = torch.empty(3, dtype=torch.int64, device=device)
+        self.blk = torch.empty(1024 * lib.SHARD_BLOCK_BYTES, dtype=torch.uint8, device=device)
+        self.blk_count = torch.empty(1, dtype=torch.int64, device=device)
         self._oh = None  # owner-side header/len/ts/verdict buffers, grown on demand
         self.flows = None
 
@@ -112,13 +124,33 @@ class HipShardEngine:
             self.ctx.process_batch_device(h, l, t, n, v, f["keys"].data_ptr(), f["fam"].data_ptr(),
                                           None, f["prob"].data_ptr(), f["dec"].data_ptr(), f["cap"])
 
-    def pack(self, hdr, length, ts, n, G, verdict):
+    def clock(self, ts, n) -> torch.Tensor:
+        self.ctx.shard_clock_device(ts.data_ptr(), n, self.clock3.data_ptr())
+        return self.clock3
+
+    def pack(self, hdr, length, ts, n, G, verdict, filt=False):
+        """-> records, counts[G + 1] (counts[G]: packets dropped by the replica)."""
         if n > self.max_local:
             raise ValueError(f"local slice of {n} packets exceeds {self.max_local}")
         self.ctx.shard_pack_device(hdr.data_ptr(), length.data_ptr(), ts.data_ptr(), n, G,
                                    verdict.data_ptr(), self.rec.data_ptr(),
-                                   self.send_idx.data_ptr(), self.counts.data_ptr())
-        return self.rec, self.counts[:G]
+                                   self.send_idx.data_ptr(), self.counts.data_ptr(),
+                                   lib.SHARD_FILTER_BLOCKLIST if filt else 0)
+        return self.rec, self.counts[:G + 1]
+
+    def export_blocklist(self) -> tuple[torch.Tensor, int]:
+        """This rank's live blacklist entries (32-byte records) and their count."""
+        while True:
+            cap = self.blk.numel() // lib.SHARD_BLOCK_BYTES
+            self.ctx.blocklist_export_device(self.blk.data_ptr(), cap, self.blk_count.data_ptr())
+            m = int(self.blk_count.item())
+            if m <= cap:
+                return self.blk, m
+            self.blk = torch.empty(2 * m * lib.SHARD_BLOCK_BYTES, dtype=torch.uint8,
+                                   device=self.device)
+
+    def load_replica(self, entries: torch.Tensor, m: int):
+        self.ctx.blocklist_replica_device(entries.data_ptr(), m)
 
     def recv_buffer(self, m: int) -> torch.Tensor:
         return torch.empty(max(1, m) * REC, dtype=torch.uint8, device=self.device)
@@ -146,31 +178,73 @@ class HipShardEngine:
         return torch.tensor([a, d], dtype=torch.int64, device=self.device)
 
 
+def _all_gather(t: torch.Tensor, G: int, group=None) -> torch.Tensor:
+    """[G * numel] concatenation of every rank's equally sized t."""
+    if t.is_cuda and dist.get_backend(group) == "gloo":
+        out = torch.empty(G * t.numel(), dtype=t.dtype)
+        dist.all_gather_into_tensor(out, t.cpu().contiguous(), group=group)
+        return out.to(t.device)
+    out = torch.empty(G * t.numel(), dtype=t.dtype, device=t.device)
+    dist.all_gather_into_tensor(out, t.contiguous(), group=group)
+    return out
+
+
 class ShardedDataPlane:
     """The sharded verdict path of one rank (one process per GPU)."""
 
-    def __init__(self, engine, group=None):
+    def __init__(self, engine, group=None, blocklist_filter: bool = True):
         self.engine = engine
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.filter = blocklist_filter and self.world > 1
+        self.filtered = 0          # packets dropped at their arrival rank by the replica
         self.last_exchange = None
 
-    def verdict_batch(self, hdr, length, ts, n: int, verdict):
+    def verdict_batch(self, hdr, length, ts, n: int, verdict, chunks: int = 1, bounds=None):
         """Verdicts for this rank's slice (arrival order) of one global batch; every rank
-        calls it once per batch with its own slice."""
+        calls it once per batch with its own slice, cut into `chunks` equal sub-batch
+        pieces (or at the explicit local cut points `bounds`, chunks + 1 of them)."""
         with self.engine.stream_ctx():
-            self._step(hdr, length, ts, n, verdict)
+            if self.world == 1:
+                self.engine.direct(hdr, length, ts, n, verdict)
+                return
+            if self.filter:
+                self._sync_blocklist()   # maps may have changed since the last batch
+            if bounds is None:
+                bounds = [n * i // chunks for i in range(chunks + 1)]
+            sent = recv = 0
+            for a, b in zip(bounds[:-1], bounds[1:]):
+                ms, mr = self._sub_batch(hdr[a * 64:], length[a:], ts[a:], b - a, verdict[a:])
+                sent, recv = sent + ms, recv + mr
+            self.last_exchange = {"sent": sent, "received": recv, "filtered": self.filtered}
 
-    def _step(self, hdr, length, ts, n: int, verdict):
+    def _clock_monotone(self, ts, n: int) -> bool:
+        """Is this sub-batch's clock non-decreasing in global order (rank 0's piece, then
+        rank 1's, ...)? One all-gather of {min, max, decreases} per rank."""
+        c = _all_gather(self.engine.clock(ts, n), self.world, self.group).tolist()
+        last = None
+        for r in range(self.world):
+            mn, mx, dec = c[3 * r: 3 * r + 3]
+            if dec:
+                return False
+            if mx == 0 and mn == -1:      # empty piece ({~0, 0} as int64)
+                continue
+            if last is not None and (mn & (2**64 - 1)) < last:
+                return False
+            last = mx & (2**64 - 1)
+        return True
+
+    def _sub_batch(self, hdr, length, ts, n: int, verdict):
         G, e = self.world, self.engine
-        if G == 1:
-            e.direct(hdr, length, ts, n, verdict)
-            return
-        recs, counts = e.pack(hdr, length, ts, n, G, verdict)
-        recv_counts = torch.empty_like(counts)
+        filt = self.filter and self._clock_monotone(ts, n)
+        recs, counts = e.pack(hdr, length, ts, n, G, verdict, filt)
+        cnt = counts.tolist()
+        self.filtered += int(cnt[G])
+        send = counts[:G].contiguous()
+        recv_counts = torch.empty_like(send)
         ones = [1] * G
-        _a2a(recv_counts, counts, ones, ones, self.group)
-        sc = [int(x) for x in counts.tolist()]
+        _a2a(recv_counts, send, ones, ones, self.group)
+        sc = [int(x) for x in cnt[:G]]
         rc = [int(x) for x in recv_counts.tolist()]
         ms, mr = sum(sc), sum(rc)
         recv = e.recv_buffer(mr)
@@ -180,12 +254,37 @@ class ShardedDataPlane:
         ret = torch.empty(max(ms, 1), dtype=torch.uint8, device=v.device)
         _a2a(ret[:ms], v[:mr], sc, rc, self.group)
         e.scatter(ret, ms, verdict)
-        self.last_exchange = {"sent": sc, "received": rc}
+        if self.filter:
+            self._sync_blocklist()
+        return ms, mr
+
+    def _sync_blocklist(self):
+        """All-gather every owner's live blacklist entries into every rank's replica."""
+        G, e = self.world, self.engine
+        ent, m = e.export_blocklist()
+        sizes = _all_gather(torch.tensor([m], dtype=torch.int64, device=ent.device), G,
+                            self.group).tolist()
+        mx = max(sizes)
+        B = lib.SHARD_BLOCK_BYTES
+        if mx == 0:
+            e.load_replica(ent, 0)
+            return
+        pad = torch.zeros(mx * B, dtype=torch.uint8, device=ent.device)
+        pad[:m * B] = ent[:m * B]
+        allb = _all_gather(pad, G, self.group)
+        parts = [allb[r * mx * B: r * mx * B + sizes[r] * B] for r in range(G) if sizes[r]]
+        e.load_replica(torch.cat(parts), sum(sizes))
 
     def stats(self) -> tuple[int, int]:
-        """stats_map of the whole sharded data plane: sum over the owners."""
+        """stats_map of the whole sharded data plane: sum over the owners, plus the
+        packets the replicas dropped at their arrival ranks."""
         with self.engine.stream_ctx():
             s = self.engine.stats()
+            s[1] += self.filtered
             if self.world > 1:
                 _all_reduce_sum(s, self.group)
             return int(s[0]), int(s[1])
+
+    def reset(self):
+        """Forget the replica-drop count (the owners' maps are reset by the caller)."""
+        self.filtered = 0

@@ -215,14 +215,29 @@ int fsx_flow_features(fsx_ctx *ctx, const uint8_t *hdr, const uint32_t *len,
 /* Owner rank of a source: key16 = raw address (IPv4 in the first 4 bytes), family 4/6.
  * Host-only (no device work). */
 uint32_t fsx_shard_owner(const uint8_t *key16, int family, uint32_t n_shards);
+#define FSX_SHARD_BLOCK_BYTES 32    /* {u32 key[4]; u64 till; u32 tag (1 v4, 2 v6); u32 pad} */
+#define FSX_SHARD_FILTER_BLOCKLIST 1u
+
 /* Parse a device batch and partition its IP packets by owner, stable in arrival order:
  * d_records (n * 32 bytes capacity) receives the records owner by owner, d_send_idx the
  * local packet index of every record, d_counts[n_shards] the records per owner.
  * Packets that never reach a limiter get their verdict in d_verdict here (frames too
- * short for their header: DROP; non-IP: PASS; src/fsx_kern.c:123-148). */
+ * short for their header: DROP; non-IP: PASS; src/fsx_kern.c:123-148). With
+ * FSX_SHARD_FILTER_BLOCKLIST, IP packets whose source is in the context's blocklist
+ * replica with till > 0 and now <= till are dropped here (src/fsx_kern.c:189-215) and
+ * counted in d_counts[n_shards] (the caller adds them to stats_map.dropped); exact only
+ * when timestamps are non-decreasing over all batches so far (fsx_shard_clock_device). */
 int fsx_shard_pack_device(fsx_ctx *ctx, const uint8_t *d_hdr, const uint32_t *d_len,
-                          const uint64_t *d_ts, size_t n, uint32_t n_shards, uint8_t *d_verdict,
-                          void *d_records, uint32_t *d_send_idx, uint64_t *d_counts);
+                          const uint64_t *d_ts, size_t n, uint32_t n_shards, uint32_t flags,
+                          uint8_t *d_verdict, void *d_records, uint32_t *d_send_idx,
+                          uint64_t *d_counts);
+/* d_out3 = {min ts, max ts, 1 if some ts decreases in arrival order}. */
+int fsx_shard_clock_device(fsx_ctx *ctx, const uint64_t *d_ts, size_t n, uint64_t *d_out3);
+/* Every live blacklist entry (till > 0) of this context's maps as FSX_SHARD_BLOCK_BYTES
+ * records; *d_count = entries present (records beyond cap are not written). */
+int fsx_blocklist_export_device(fsx_ctx *ctx, void *d_entries, size_t cap, uint64_t *d_count);
+/* Replace the context's blocklist replica with m all-gathered entries (distinct keys). */
+int fsx_blocklist_replica_device(fsx_ctx *ctx, const void *d_entries, size_t m);
 /* Owner side: m received records -> header records + len + ts for the batch entry points
  * (same source key, family, frame length, timestamp and L4 destination port). */
 int fsx_shard_unpack_device(fsx_ctx *ctx, const void *d_records, size_t m, uint8_t *d_hdr,

@@ -42,6 +42,7 @@ class CpuShardEngine:
         self.oracle = oracle
         self.o = oracle.Oracle(**cfg)
         self.send_idx = np.zeros(0, dtype=np.int64)
+        self.replica = {}
 
     def stream_ctx(self):
         return contextlib.nullcontext()
@@ -55,13 +56,29 @@ class CpuShardEngine:
         h, l, t = self._np(hdr, length, ts, n)
         verdict[:n] = torch.from_numpy(self.o.batch(h, l, t))
 
-    def pack(self, hdr, length, ts, n, G, verdict):
+    def clock(self, ts, n):
+        t = ts.numpy().view(np.uint64)[:n]
+        if n == 0:
+            return torch.tensor([-1, 0, 0], dtype=torch.int64)
+        dec = int(np.any(t[1:] < t[:-1]))
+        return torch.tensor(np.array([t.min(), t.max(), dec], dtype=np.uint64).view(np.int64))
+
+    def pack(self, hdr, length, ts, n, G, verdict, filt=False):
         h, l, t = self._np(hdr, length, ts, n)
         cls, keys = self.oracle.parse(h, l)
         v = verdict.numpy()
         v[:n][cls == 0] = 1
         v[:n][cls == 1] = 2
-        ip = np.nonzero(cls >= 2)[0]
+        filtered = 0
+        if filt:
+            for i in np.nonzero(cls >= 2)[0]:
+                k = (6 if cls[i] == 3 else 4, keys[i].tobytes()[:16 if cls[i] == 3 else 4])
+                till = self.replica.get(k)
+                if till is not None and till > 0 and not int(t[i]) > till:
+                    cls[i] = 9          # dropped here, counted by the protocol
+                    v[i] = 1
+                    filtered += 1
+        ip = np.nonzero((cls >= 2) & (cls <= 3))[0]
         fam = np.where(cls[ip] == 3, 6, 4).astype(np.uint8)
         own = np.array([lib.shard_owner(keys[i].tobytes(), int(f), G) for i, f in zip(ip, fam)],
                        dtype=np.int64)
@@ -75,7 +92,29 @@ class CpuShardEngine:
         rec["family"] = fam
         self.send_idx = ip
         counts = np.bincount(own, minlength=G).astype(np.int64)
+        counts = np.concatenate([counts, [filtered]]).astype(np.int64)
         return torch.from_numpy(rec.view(np.uint8).copy()), torch.from_numpy(counts)
+
+    BLK_DTYPE = np.dtype([("key", "<u4", 4), ("till", "<u8"), ("tag", "<u4"), ("pad", "<u4")])
+
+    def export_blocklist(self):
+        rows = []
+        for mid, tag, klen in ((3, 1, 4), (4, 2, 16)):
+            for k, till in self.o.map_dump(mid).items():
+                if till > 0:
+                    rows.append((np.frombuffer(k.ljust(16, b"\0"), dtype="<u4"), till, tag, 0))
+        a = np.zeros(len(rows), dtype=self.BLK_DTYPE)
+        for i, r in enumerate(rows):
+            a[i] = r
+        return torch.from_numpy(a.view(np.uint8).copy()), len(rows)
+
+    def load_replica(self, entries, m):
+        a = entries.numpy()[:m * 32].view(self.BLK_DTYPE)
+        self.replica = {}
+        for e in a:
+            fam = 6 if e["tag"] == 2 else 4
+            k = e["key"].tobytes()[:16 if fam == 6 else 4]
+            self.replica[(fam, k)] = int(e["till"])
 
     def recv_buffer(self, m):
         return torch.empty(max(1, m) * lib.SHARD_RECORD_BYTES, dtype=torch.uint8)

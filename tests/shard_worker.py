@@ -16,9 +16,14 @@ import torch.distributed as dist
 def _stream(spec):
     from test_gpu_parity import rand_stream
     rng = np.random.default_rng(spec["seed"])
-    return rand_stream(rng, spec["n"], spec["n_ips"], dt_max=spec.get("dt_max", 300),
-                       v6_frac=spec.get("v6_frac", 0.0), nonip_frac=spec.get("nonip_frac", 0.0),
-                       short_frac=spec.get("short_frac", 0.0))
+    hdr, ln, ts = rand_stream(rng, spec["n"], spec["n_ips"], dt_max=spec.get("dt_max", 300),
+                              v6_frac=spec.get("v6_frac", 0.0),
+                              nonip_frac=spec.get("nonip_frac", 0.0),
+                              short_frac=spec.get("short_frac", 0.0))
+    if spec.get("jitter"):   # timestamps going back by up to `jitter` ns
+        sw = rng.choice(len(ts), len(ts) // 10, replace=False)
+        ts[sw] = ts[sw] - rng.integers(0, spec["jitter"], sw.size).astype(np.uint64)
+    return hdr, ln, ts
 
 
 def worker(rank, world, port, spec, out_path, engine_kind):
@@ -42,18 +47,24 @@ def worker(rank, world, port, spec, out_path, engine_kind):
             dev = torch.device("cuda", 0)
             ctx = lib.FsxContext(max_batch=spec.get("owner_batch", 1 << 16), **cfg)
             eng = HipShardEngine(ctx, max(b - a for a, b in zip(cuts[:-1], cuts[1:])), dev)
-        plane = ShardedDataPlane(eng)
+        plane = ShardedDataPlane(eng, blocklist_filter=spec.get("filter", True))
+        k = spec.get("chunks", 1)
         mine = []
         for a, b in zip(cuts[:-1], cuts[1:]):
-            bounds = np.linspace(a, b, world + 1).astype(np.int64)
-            s0, s1 = int(bounds[rank]), int(bounds[rank + 1])
-            n = s1 - s0
-            th = torch.from_numpy(hdr[s0:s1].reshape(-1).copy()).to(dev)
-            tl = torch.from_numpy(ln[s0:s1].view(np.int32).copy()).to(dev)
-            tt = torch.from_numpy(ts[s0:s1].view(np.int64).copy()).to(dev)
+            # the batch in k*world pieces; piece j is on rank j % world, in sub-batch j // world
+            pb = np.linspace(a, b, k * world + 1).astype(np.int64)
+            idx = np.concatenate([np.arange(pb[i * world + rank], pb[i * world + rank + 1])
+                                  for i in range(k)]).astype(np.int64)
+            local_bounds = [0]
+            for i in range(k):
+                local_bounds.append(local_bounds[-1] + int(pb[i * world + rank + 1] - pb[i * world + rank]))
+            n = idx.size
+            th = torch.from_numpy(hdr[idx].reshape(-1).copy()).to(dev)
+            tl = torch.from_numpy(ln[idx].view(np.int32).copy()).to(dev)
+            tt = torch.from_numpy(ts[idx].view(np.int64).copy()).to(dev)
             tv = torch.zeros(max(n, 1), dtype=torch.uint8, device=dev)
-            plane.verdict_batch(th, tl, tt, n, tv)
-            mine.append(tv[:n].cpu().numpy().copy())
+            plane.verdict_batch(th, tl, tt, n, tv, chunks=k, bounds=local_bounds)
+            mine.append((idx, tv[:n].cpu().numpy().copy()))
         stats = plane.stats()
         if engine_kind == "cpu":
             dumps = {m: eng.o.map_dump(m) for m in spec["maps"]}
@@ -66,7 +77,10 @@ def worker(rank, world, port, spec, out_path, engine_kind):
             ok, msg = True, []
             for bi, (a, b) in enumerate(zip(cuts[:-1], cuts[1:])):
                 exp = o.batch(hdr[a:b], ln[a:b], ts[a:b])
-                v = np.concatenate([got[r][0][bi] for r in range(world)])
+                v = np.zeros(b - a, dtype=np.uint8)
+                for r in range(world):
+                    ridx, rv = got[r][0][bi]
+                    v[ridx - a] = rv
                 if not np.array_equal(v, exp):
                     ok = False
                     msg.append(f"batch {bi}: {int((v != exp).sum())} verdicts differ")
@@ -85,7 +99,8 @@ def worker(rank, world, port, spec, out_path, engine_kind):
                     ok = False
                     msg.append(f"map {m}: {len(union)} vs {len(o.map_dump(m))} entries differ")
             with open(out_path, "w") as f:
-                json.dump({"ok": ok, "msg": msg, "stats": list(stats)}, f)
+                json.dump({"ok": ok, "msg": msg, "stats": list(stats),
+                           "filtered": plane.filtered}, f)
         dist.barrier()
     finally:
         dist.destroy_process_group()

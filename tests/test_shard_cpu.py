@@ -29,14 +29,30 @@ def run_sharded(tmp_path, world, spec, engine="cpu"):
 
 
 BASE = dict(n=24000, n_ips=300, seed=7, maps=[1, 2, 3, 4],
-            cuts=[0, 5000, 5001, 16000, 24000])
+            cuts=[0, 5000, 5001, 16000, 24000], chunks=3)
 
 
 @pytest.mark.parametrize("world", [2, 3])
 def test_sharded_fixed_window(tmp_path, world):
     spec = dict(BASE, cfg=dict(pps_threshold=7, window_ns=200_000, block_ns=1_000_000,
                                max_entries=4096))
-    run_sharded(tmp_path, world, spec)
+    res = run_sharded(tmp_path, world, spec)
+    assert res["filtered"] > 0      # the replicated blocklist dropped packets at arrival
+
+
+def test_sharded_without_blocklist_filter_one_chunk(tmp_path):
+    spec = dict(BASE, chunks=1, filter=False,
+                cfg=dict(pps_threshold=7, window_ns=200_000, block_ns=1_000_000, max_entries=4096))
+    res = run_sharded(tmp_path, 2, spec)
+    assert res["filtered"] == 0
+
+
+def test_sharded_non_monotone_clock_disables_filter(tmp_path):
+    """Sub-batches whose clock goes back skip the replica (exactness first)."""
+    spec = dict(BASE, seed=23, dt_max=40, cfg=dict(pps_threshold=5, window_ns=100_000,
+                                                   block_ns=400_000, max_entries=4096),
+                jitter=3000)
+    run_sharded(tmp_path, 2, spec)
 
 
 def test_sharded_mixed_families_sliding_window(tmp_path):
