@@ -29,7 +29,8 @@ COMMON = [
 ]
 
 LIBS = {
-    "libfsx_hip.so": ["fsx_device.hip", "fsx_limiters.hip", "fsx_shard.hip", "fsx_flows.hip", "fsx_score.hip",
+    "libfsx_hip.so": ["fsx_device.hip", "fsx_limiters.hip", "fsx_shard.hip", "fsx_pcap.hip",
+                      "fsx_flows.hip", "fsx_score.hip",
                       "fsx_api.hip"],
     "libfsx_synth.so": ["fsx_synth.hip"],
 }

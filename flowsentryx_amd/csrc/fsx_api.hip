@@ -748,6 +748,19 @@ int fsx_shard_scatter_device(fsx_ctx *c, const uint8_t *d_ret, const uint32_t *d
     return 0;
 }
 
+// ------------------------------------------------------------------ pcap
+int fsx_pcap_records_device(fsx_ctx *c, const uint8_t *d_buf, const uint64_t *d_off, const uint32_t *d_caplen,
+                            size_t n, uint8_t *d_hdr) {
+    if (!c) return -EINVAL;
+    if (n > kMaxBatchLimit) return set_err(c, -E2BIG, "n=%zu too large", n);
+    if (n && (!d_buf || !d_off || !d_caplen || !d_hdr)) return set_err(c, -EINVAL, "null buffer");
+    int rc = sel(c);
+    if (rc) return rc;
+    hipError_t e = launch_pcap_records(d_buf, d_off, d_caplen, (uint32_t)n, d_hdr, c->stream);
+    if (e != hipSuccess) return set_err(c, -EIO, "pcap records: %s", hipGetErrorString(e));
+    return 0;
+}
+
 // ------------------------------------------------------------------ timing
 int fsx_enable_timing(fsx_ctx *c, int on) {
     if (!c) return -EINVAL;

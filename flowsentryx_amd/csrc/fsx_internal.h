@@ -218,6 +218,9 @@ hipError_t launch_sliding_window(const uint64_t *S, const uint64_t *ts, const ui
                                  const Scratch &sc, Slot *table, TableState *tstate, const HistBufs &hb,
                                  const Limits &lim, uint32_t n, hipStream_t st);
 
+hipError_t launch_pcap_records(const uint8_t *buf, const uint64_t *off, const uint32_t *caplen, uint32_t n,
+                               uint8_t *hdr, hipStream_t st);
+
 hipError_t launch_flows(const uint64_t *S, const uint64_t *pay, BatchState *bs, const uint8_t *headf, const uint32_t *len,
                         const uint64_t *ts, const uint8_t *hdr, const uint32_t *tile_off,
                         const uint32_t *sub_cnt, const uint32_t *seg_start, void *firstp, void *lastp,

@@ -153,7 +153,7 @@ ABI_SYMBOLS = [
     "fsx_last_timings", "fsx_enable_timing", "fsx_last_batch_info",
     "fsx_shard_owner", "fsx_shard_pack_device", "fsx_shard_unpack_device",
     "fsx_shard_scatter_device", "fsx_shard_clock_device", "fsx_blocklist_export_device",
-    "fsx_blocklist_replica_device",
+    "fsx_blocklist_replica_device", "fsx_pcap_index", "fsx_pcap_records_device",
 ]
 
 SHARD_RECORD_BYTES = 32

@@ -246,6 +246,22 @@ int fsx_shard_unpack_device(fsx_ctx *ctx, const void *d_records, size_t m, uint8
 int fsx_shard_scatter_device(fsx_ctx *ctx, const uint8_t *d_ret, const uint32_t *d_send_idx,
                              size_t m, uint8_t *d_verdict);
 
+/* ---- pcap ingest (SURVEY.md §8 f). Classic pcap records (the 24-byte file header is
+ * the caller's): FSX_PCAP_NANOSECONDS for magic 0xA1B23C4D, FSX_PCAP_SWAPPED when the
+ * magic reads byte-swapped. The frame length is the record's original length (what
+ * data_end - data is in XDP, src/fsx_kern.c:123). */
+#define FSX_PCAP_NANOSECONDS 1u
+#define FSX_PCAP_SWAPPED 2u
+/* Host only: index up to cap complete records of buf[0, size): data offset, captured
+ * and original length, timestamp in ns; *consumed = bytes of the indexed records. */
+int fsx_pcap_index(const uint8_t *buf, size_t size, uint32_t flags, uint64_t *data_off,
+                   uint32_t *caplen, uint32_t *origlen, uint64_t *ts_ns, size_t cap,
+                   size_t *n_out, size_t *consumed);
+/* Device: 64-byte header records (first min(caplen, 64) bytes, zero padded) of n indexed
+ * records from an HBM copy of the pcap bytes. */
+int fsx_pcap_records_device(fsx_ctx *ctx, const uint8_t *d_buf, const uint64_t *d_data_off,
+                            const uint32_t *d_caplen, size_t n, uint8_t *d_hdr);
+
 /* Facts about the last batch (after fsx_sync): info[0] IP packets, [1] distinct
  * source IPs, [2] sources new to the maps, [3] any IPv6, [4] non-monotone clock,
  * [5] max frame length, [6] max timestamp, [7] allowed, [8] dropped, [9] IPv6
