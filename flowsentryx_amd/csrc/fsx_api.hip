@@ -50,6 +50,7 @@ struct fsx_ctx {
     float *d_prob = nullptr;
     uint8_t *d_dec = nullptr;
     uint64_t score_cap = 0;
+    uint32_t id_gen = 0;       // generation of the per-batch source-id table
     // sharding: per (owner, tile) counts of fsx_shard_pack_device, blocklist replica
     uint32_t *d_shard_cnt = nullptr;
     uint64_t shard_cnt_cap = 0;
@@ -113,7 +114,7 @@ static void free_scratch(fsx_ctx *c) {
     Scratch &s = c->sc;
     hipFree(s.packed[0]); hipFree(s.packed[1]); hipFree(s.pay[0]); hipFree(s.pay[1]); hipFree(s.marks); hipFree(s.headf);
     hipFree(s.seg_start); hipFree(s.seg_slot); hipFree(s.hist);
-    hipFree(s.tile_aux); hipFree(s.tile_last); hipFree(s.fix_list); hipFree(s.fix_bitmap);
+    hipFree(s.tile_aux); hipFree(s.tile_last); hipFree(s.id_tab);
     hipFree(s.seg_order); hipFree(s.sub_cnt); hipFree(s.flow_first); hipFree(s.flow_last);
     hipFree(s.span_list); hipFree(s.sort_ctl); hipFree(s.gbase); hipFree(s.status);
     hipFree(s.lim_tiles); hipFree(s.sw_seg);
@@ -136,8 +137,9 @@ static int alloc_scratch(fsx_ctx *c, uint64_t cap) {
     HIPCHK(c, hipMalloc(&s.hist, 256ull * std::max<uint64_t>(kSortMaxBlocks, cap / kSortTile + 2) * 4));
     HIPCHK(c, hipMalloc(&s.tile_aux, ntiles * 4));
     HIPCHK(c, hipMalloc(&s.tile_last, ntiles));
-    HIPCHK(c, hipMalloc(&s.fix_list, cap * 4));
-    HIPCHK(c, hipMalloc(&s.fix_bitmap, (cap / 64 + 1) * 8));
+    HIPCHK(c, hipMalloc(&s.id_tab, c->slots * 32));
+    HIPCHK(c, hipMemset(s.id_tab, 0, c->slots * 32));   // generation 0: every slot empty
+    c->id_gen = 0;
     HIPCHK(c, hipMalloc(&s.seg_order, (cap + 1) * 4));
     HIPCHK(c, hipMalloc(&s.sub_cnt, (cap / 1024 + 8) * 4));
     HIPCHK(c, hipMalloc(&s.flow_first, (cap / 1024 + 8) * flow_acc_bytes()));
@@ -347,9 +349,13 @@ static int run_batch(fsx_ctx *c, const uint8_t *d_hdr, const uint32_t *d_len, co
         used = &c->ev_used[c->ring_n];
         c->ring_n++;
     }
+    if (++c->id_gen == 0x10000u) {   // 16-bit generations: clear the id table on wrap
+        HIPCHK(c, hipMemsetAsync(c->sc.id_tab, 0, c->slots * 32, c->stream));
+        c->id_gen = 1;
+    }
     hipError_t e = launch_verdict_pipeline(d_hdr, d_len, d_ts, (uint32_t)n, d_verdict, c->table,
-                                           c->tstate, c->bs, c->sc, c->lim, do_limit, fr, c->hist,
-                                           c->stream, ev, kMaxEv, used, names);
+                                           c->tstate, c->bs, c->sc, c->id_gen, c->lim, do_limit, fr,
+                                           c->hist, c->stream, ev, kMaxEv, used, names);
     if (e != hipSuccess) return set_err(c, -EIO, "pipeline launch: %s", hipGetErrorString(e));
     c->pending = true;
     return 0;

@@ -41,6 +41,81 @@ __device__ unsigned long long *g_fsx_stamps;
 
 namespace fsx {
 
+// ------------------------------------------------------------------ per-batch source ids
+// Every IP source of a batch gets a dense id: its slot in an open-addressing table of
+// table_mask + 1 slots: a 64-bit head {generation 16 | state 8 | tag 8 | key word 0}
+// (8 bytes: IPv4 probes stay dense in L2) and, in a parallel array, IPv6 key words
+// 1..3. Slots of older generations are empty, so the table is never cleared. IPv4 keys are published by one 64-bit CAS; IPv6 slots are claimed
+// BUSY, their key words stored at agent scope, then published READY (release). Other
+// XCDs' L2s are not coherent with each other, so every head and IPv6 key word is read
+// with an agent-scope (coherent) load; a stale line would otherwise force a CAS on
+// every packet of a hot source until it is evicted.
+constexpr uint64_t kIdSeed = 0x1D5EED0F5A11ull;
+constexpr uint64_t kIdBusy = 1, kIdReady = 2;
+constexpr uint32_t kIdSpin = 1u << 22;
+
+__device__ __forceinline__ uint64_t id_head(uint32_t gen, uint64_t state, uint32_t tag, uint32_t k0) {
+    return ((uint64_t)gen << 48) | (state << 40) | ((uint64_t)tag << 32) | k0;
+}
+
+struct IdTable {
+    unsigned long long *head;   // [slots]
+    uint32_t *k6;               // [slots][4]: IPv6 key words 1..3
+    uint64_t mask;
+    uint32_t gen;
+    uint32_t v6_start;   // FSX_FLAG_TEST_V6_COLLIDE: every IPv6 key probes from here
+};
+
+__device__ __forceinline__ uint64_t id_start(const IdTable &T, uint32_t tag, const uint32_t k[4]) {
+    return (tag == 2 && T.v6_start != 0xFFFFFFFFu) ? T.v6_start : (slot_hash(tag, k, kIdSeed) & T.mask);
+}
+
+// Slot of (tag, key), inserted if absent; kNoSlot when the table is full or a
+// publication never completes (reported as a full table). h = id_start(...), hint0 =
+// a plain load of T.head[h] issued earlier (the parse loop issues it one tile ahead).
+__device__ __forceinline__ uint32_t id_resolve(const IdTable &T, uint32_t tag, const uint32_t k[4],
+                                               uint64_t h, uint64_t hint0) {
+    const uint64_t ready = id_head(T.gen, kIdReady, tag, k[0]);
+    for (uint64_t probes = 0; probes <= T.mask; ++probes, h = (h + 1) & T.mask) {
+        unsigned long long *hp = T.head + h;
+        uint64_t cur = probes == 0 ? hint0 : *hp;   // hint
+        for (;;) {
+            if ((uint32_t)(cur >> 48) != T.gen) {   // empty in this generation: claim it
+                const uint64_t want = tag == 2 ? id_head(T.gen, kIdBusy, tag, k[0]) : ready;
+                const uint64_t prev = atomicCAS(hp, (unsigned long long)cur, (unsigned long long)want);
+                if (prev == cur) {
+                    if (tag == 2) {
+                        uint32_t *kw = T.k6 + h * 4;
+                        __hip_atomic_store(kw + 0, k[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        __hip_atomic_store(kw + 1, k[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        __hip_atomic_store(kw + 2, k[3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        __hip_atomic_store(hp, (unsigned long long)ready, __ATOMIC_RELEASE,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+                    }
+                    return (uint32_t)h;
+                }
+                cur = prev;       // lost a race, or the hint was stale: decide on the truth
+                continue;
+            }
+            uint32_t spins = 0;
+            while (((cur >> 40) & 0xFFu) == kIdBusy) {
+                if (++spins > kIdSpin) return kNoSlot;
+                cur = __hip_atomic_load(hp, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            break;
+        }
+        if (((cur >> 32) & 0xFFu) != tag || (uint32_t)cur != k[0]) continue;
+        if (tag == 1) return (uint32_t)h;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        const uint32_t *kw = T.k6 + h * 4;
+        if (__hip_atomic_load(kw + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == k[1] &&
+            __hip_atomic_load(kw + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == k[2] &&
+            __hip_atomic_load(kw + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == k[3])
+            return (uint32_t)h;
+    }
+    return kNoSlot;
+}
+
 // ------------------------------------------------------------------ parse
 // One wave handles 64 consecutive records per step: the 4 KiB tile is loaded with
 // four fully coalesced 1 KiB wave loads and staged through LDS (17-dword record
@@ -50,8 +125,7 @@ __global__ __launch_bounds__(256) void k_parse(const uint8_t *__restrict__ hdr,
                                                const uint64_t *__restrict__ ts, uint32_t n,
                                                uint64_t *__restrict__ packed,
                                                uint8_t *__restrict__ verdict, BatchState *bs,
-                                               uint32_t salt, uint64_t seed, uint32_t v6_const,
-                                               uint32_t *__restrict__ ghist) {
+                                               IdTable idt, uint32_t *__restrict__ ghist) {
     __shared__ uint32_t s_rec[4][64 * 17];
     __shared__ uint32_t s_red[4][3];
     __shared__ unsigned long long s_ts[4], s_its[4];
@@ -86,6 +160,8 @@ __global__ __launch_bounds__(256) void k_parse(const uint8_t *__restrict__ hdr,
     uint32_t Lc;
     uint64_t Tc, Pc;
     load(blockIdx.x * 4u + w, hv, Lc, Tc, Pc);
+    // software pipeline: the next tile's loads are in flight while this one is parsed
+    // (measured faster than issuing the id probes ahead of the prefetch)
     for (uint32_t t = blockIdx.x * 4u + w; t < ntiles; t += stride) {
         uint4 hn[4];
         uint32_t Ln;
@@ -108,36 +184,51 @@ __global__ __launch_bounds__(256) void k_parse(const uint8_t *__restrict__ hdr,
         const uint64_t T = Tc;
         uint64_t prev = __shfl_up(T, 1);
         if (lane == 0) prev = (live && i > 0) ? Pc : T;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) hv[k] = hn[k];
-        Lc = Ln; Tc = Tn; Pc = Pn;
-        uint64_t out = kSentinel;
+        bool ip = false;
+        uint8_t v = XDP_PASS;  // non-IP: PASS, not counted (src/fsx_kern.c:128-131)
+        uint32_t tag = 0, k[4] = {0, 0, 0, 0};
         if (live) {
             // parse_ethhdr (14-byte bound; raw h_proto, no VLAN)
             const uint32_t proto = ((d3 & 0xFFu) << 8) | ((d3 >> 8) & 0xFFu);
-            uint8_t v = XDP_PASS;  // non-IP: PASS, not counted (src/fsx_kern.c:128-131)
             if (L < 14u) {
                 v = XDP_DROP;      // src/fsx_kern.c:124-127
             } else if (proto == 0x86DDu) {
                 if (L < 54u) v = XDP_DROP;  // parse_ip6hdr bound, src/fsx_kern.c:139-140
                 else {
-                    uint32_t k[4] = {(d5 >> 16) | (d6 << 16), (d6 >> 16) | (d7 << 16),
-                                     (d7 >> 16) | (d8 << 16), (d8 >> 16) | (d9 << 16)};
-                    const uint32_t sk = v6_const ? v6_const : skey_v6(k, seed);
-                    out = ((uint64_t)sk << 32) | (1ull << 31) | i;
+                    k[0] = (d5 >> 16) | (d6 << 16); k[1] = (d6 >> 16) | (d7 << 16);
+                    k[2] = (d7 >> 16) | (d8 << 16); k[3] = (d8 >> 16) | (d9 << 16);
+                    tag = 2;
+                    ip = true;
                     any6 = 1;
                 }
             } else if (proto == 0x0800u) {
                 if (L < 34u) v = XDP_DROP;  // parse_ip4hdr fixed 20-byte bound, :146-147
                 else {
-                    const uint32_t ip = (d6 >> 16) | (d7 << 16);  // bytes 26..29 raw
-                    out = ((uint64_t)skey_v4(ip, salt) << 32) | i;
+                    k[0] = (d6 >> 16) | (d7 << 16);  // bytes 26..29 raw
+                    tag = 1;
+                    ip = true;
                 }
             }
+        }
+        uint64_t h = 0, hint = 0;
+        if (ip) {
+            h = id_start(idt, tag, k);
+            hint = idt.head[h];   // a hint: the CAS decides when it shows an older generation
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) hv[q] = hn[q];
+        Lc = Ln; Tc = Tn; Pc = Pn;
+        uint64_t out = kSentinel;
+        if (ip) {
+            const uint32_t id = id_resolve(idt, tag, k, h, hint);
+            if (id == kNoSlot) atomicOr(&bs->err, ERR_TABLE_FULL);
+            out = ((uint64_t)(id & idt.mask) << 32) | ((uint64_t)(tag - 1u) << 31) | i;
+        }
+        if (live) {
             packed[i] = out;
             // IP packets default to PASS here (coalesced); the fill pass writes only
             // the DROP verdicts, which cluster in the heavy sources' segments
-            if (verdict) verdict[i] = out == kSentinel ? v : (uint8_t)XDP_PASS;
+            if (verdict) verdict[i] = ip ? (uint8_t)XDP_PASS : v;
             nonmono |= T < prev ? 1u : 0u;
             maxlen = L > maxlen ? L : maxlen;
             maxts = T > maxts ? T : maxts;
@@ -146,7 +237,7 @@ __global__ __launch_bounds__(256) void k_parse(const uint8_t *__restrict__ hdr,
         // radix histograms of the 4 key digits: per-wave LDS counters (a heavy source
         // repeats in few lanes of one 64-packet step, so same-address serialization
         // stays short)
-        if (ghist && out != kSentinel) {
+        if (ghist && ip) {
 #pragma unroll
             for (int dg = 0; dg < 4; ++dg)
                 atomicAdd(&s_hist[w][dg][(uint32_t)(out >> (32 + 8 * dg)) & 255u], 1u);
@@ -502,169 +593,8 @@ __global__ __launch_bounds__(256) void k_onesweep(const uint64_t *__restrict__ i
                      LookbackOffs<kLW>{status, gbase, bs, t, gen});
 }
 
-// ------------------------------------------------------------------ IPv6 collision fixup
-// Equal 32-bit sort keys with different (family, address) form "mixed runs". Each
-// run is stably re-sorted by (family, address) so every source IP is contiguous.
-__device__ __forceinline__ uint32_t lower_bound_skey(const uint64_t *S, uint32_t lo, uint32_t hi,
-                                                     uint32_t sk) {
-    while (lo < hi) {
-        const uint32_t m = lo + (hi - lo) / 2;
-        if (pk_skey(S[m]) < sk) lo = m + 1; else hi = m;
-    }
-    return lo;
-}
-__device__ __forceinline__ uint32_t upper_bound_skey(const uint64_t *S, uint32_t lo, uint32_t hi,
-                                                     uint32_t sk) {
-    while (lo < hi) {
-        const uint32_t m = lo + (hi - lo) / 2;
-        if (pk_skey(S[m]) <= sk) lo = m + 1; else hi = m;
-    }
-    return lo;
-}
-
-__global__ __launch_bounds__(256) void k_v6_mixed(const uint64_t *__restrict__ S, BatchState *bs,
-                                                  const uint8_t *__restrict__ hdr,
-                                                  uint64_t *bitmap, uint32_t *fix_list) {
-    if (!bs->any_v6) return;
-    const uint32_t M = bs->n_valid;
-    for (uint32_t p = blockIdx.x * 256u + threadIdx.x + 1u; p < M; p += gridDim.x * 256u) {
-        const uint64_t a = S[p - 1], b = S[p];
-        if (pk_skey(a) != pk_skey(b)) continue;
-        const uint32_t fa = pk_fam(a), fb = pk_fam(b);
-        if (!(fa | fb)) continue;  // IPv4 keys are a bijection
-        bool mixed = fa != fb;
-        if (!mixed) {
-            uint32_t ka[4], kb[4];
-            load_key6(hdr, pk_idx(a), ka);
-            load_key6(hdr, pk_idx(b), kb);
-            mixed = key_cmp(2, ka, 2, kb) != 0;
-        }
-        if (!mixed) continue;
-        const uint32_t h = lower_bound_skey(S, 0, p, pk_skey(b));
-        const unsigned long long bit = 1ull << (h & 63u);
-        const unsigned long long old =
-            atomicOr(reinterpret_cast<unsigned long long *>(&bitmap[h >> 6]), bit);
-        if (!(old & bit)) fix_list[atomicAdd(&bs->n_fix, 1u)] = h;
-    }
-}
-
-// Short runs: one thread, stable insertion sort (keys re-gathered per compare).
-constexpr uint32_t kFixShort = 32;
-__global__ __launch_bounds__(256) void k_fixup_short(uint64_t *__restrict__ S, BatchState *bs,
-                                                     const uint8_t *__restrict__ hdr,
-                                                     const uint32_t *fix_list, uint32_t salt) {
-    const uint32_t nf = bs->n_fix, M = bs->n_valid;
-    for (uint32_t f = blockIdx.x * 256u + threadIdx.x; f < nf; f += gridDim.x * 256u) {
-        const uint32_t h = fix_list[f];
-        const uint32_t e = upper_bound_skey(S, h, M, pk_skey(S[h]));
-        if (e - h > kFixShort) continue;
-        for (uint32_t i = h + 1; i < e; ++i) {
-            const uint64_t x = S[i];
-            uint32_t kx[4];
-            const uint32_t tx = key_of(x, hdr, salt, kx);
-            uint32_t j = i;
-            while (j > h) {
-                uint32_t ky[4];
-                const uint32_t ty = key_of(S[j - 1], hdr, salt, ky);
-                if (key_cmp(ty, ky, tx, kx) <= 0) break;
-                S[j] = S[j - 1];
-                --j;
-            }
-            S[j] = x;
-        }
-    }
-}
-
-// Long runs: one block per run, repeated stable partitions (== first key | rest).
-__global__ __launch_bounds__(256) void k_fixup_long(uint64_t *__restrict__ S,
-                                                    uint64_t *__restrict__ tmp, BatchState *bs,
-                                                    const uint8_t *__restrict__ hdr,
-                                                    const uint32_t *fix_list, uint32_t salt) {
-    __shared__ uint32_t s_tmp[4];
-    __shared__ uint32_t s_pk[4];
-    __shared__ uint32_t s_neq;
-    const uint32_t nf = bs->n_fix, M = bs->n_valid;
-    for (uint32_t f = blockIdx.x; f < nf; f += gridDim.x) {
-        const uint32_t h = fix_list[f];
-        const uint32_t e = upper_bound_skey(S, h, M, pk_skey(S[h]));
-        if (e - h <= kFixShort) continue;
-        uint32_t cur = h;
-        while (cur < e) {
-            uint32_t pk[4];
-            const uint32_t pt = key_of(S[cur], hdr, salt, pk);
-            // pass 1: count equal
-            uint32_t neq_local = 0;
-            for (uint32_t i = cur + threadIdx.x; i < e; i += 256) {
-                uint32_t k[4];
-                const uint32_t t = key_of(S[i], hdr, salt, k);
-                neq_local += key_cmp(t, k, pt, pk) == 0 ? 1u : 0u;
-            }
-            uint32_t n_eq;
-            block256_excl(neq_local, s_tmp, &n_eq);
-            // pass 2: stable placement into tmp, chunk by chunk
-            uint32_t eq_off = 0, ne_off = 0;
-            for (uint32_t c0 = cur; c0 < e; c0 += 256) {
-                const uint32_t i = c0 + threadIdx.x;
-                uint32_t is_eq = 0;
-                uint64_t x = 0;
-                if (i < e) {
-                    x = S[i];
-                    uint32_t k[4];
-                    const uint32_t t = key_of(x, hdr, salt, k);
-                    is_eq = key_cmp(t, k, pt, pk) == 0;
-                }
-                uint32_t tot_eq;
-                const uint32_t r_eq = block256_excl(is_eq, s_tmp, &tot_eq);
-                const uint32_t nvalid = min(256u, e - c0);
-                if (i < e) {
-                    const uint32_t r_ne = threadIdx.x - r_eq;
-                    if (is_eq) tmp[cur + eq_off + r_eq] = x;
-                    else tmp[cur + n_eq + ne_off + r_ne] = x;
-                }
-                eq_off += tot_eq;
-                ne_off += nvalid - tot_eq;
-            }
-            __syncthreads();
-            for (uint32_t i = cur + threadIdx.x; i < e; i += 256) S[i] = tmp[i];
-            __syncthreads();
-            cur += n_eq;
-            (void)s_pk; (void)s_neq;
-        }
-    }
-}
-
-// The fixup reorders whole runs; rebuild their payload words from (ts, len).
-__global__ __launch_bounds__(256) void k_fixup_pay(const uint64_t *__restrict__ S,
-                                                   uint64_t *__restrict__ pay, BatchState *bs,
-                                                   const uint32_t *__restrict__ fix_list,
-                                                   const uint64_t *__restrict__ ts,
-                                                   const uint32_t *__restrict__ len) {
-    if (!bs->pay_ok) return;
-    const uint32_t nf = bs->n_fix, M = bs->n_valid;
-    const uint64_t tbase = ~bs->inv_min_ts;
-    for (uint32_t f = blockIdx.x; f < nf; f += gridDim.x) {
-        const uint32_t h = fix_list[f];
-        const uint32_t e = upper_bound_skey(S, h, M, pk_skey(S[h]));
-        for (uint32_t p = h + threadIdx.x; p < e; p += 256) {
-            const uint32_t idx = pk_idx(S[p]);
-            pay[p] = ((ts[idx] - tbase) << kPayLenBits) | len[idx];
-        }
-    }
-}
-
 // ------------------------------------------------------------------ segment heads
-__device__ __forceinline__ bool is_head(const uint64_t *S, uint32_t p, const uint8_t *hdr,
-                                        bool any6) {
-    if (p == 0) return true;
-    const uint64_t a = S[p - 1], b = S[p];
-    if ((a >> 31) != (b >> 31)) return true;  // sort key or family differs
-    if (!any6 || !pk_fam(b)) return false;
-    uint32_t ka[4], kb[4];
-    load_key6(hdr, pk_idx(a), ka);
-    load_key6(hdr, pk_idx(b), kb);
-    return key_cmp(2, ka, 2, kb) != 0;
-}
-
+// A source starts wherever the id changes (ids are exact: one per (family, address)).
 // Tile = kTile sorted positions; 256 threads x 16 consecutive positions.
 __global__ __launch_bounds__(256) void k_heads_count(const uint64_t *__restrict__ S,
                                                      BatchState *bs,
@@ -674,7 +604,6 @@ __global__ __launch_bounds__(256) void k_heads_count(const uint64_t *__restrict_
                                                      uint32_t *__restrict__ sub_cnt) {
     __shared__ uint32_t s_tmp[4];
     const uint32_t M = bs->n_valid;
-    const bool any6 = bs->any_v6 != 0;
     const uint32_t ntiles = (M + kTile - 1) / kTile;
     const uint32_t lane = lane_id();
     for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
@@ -693,13 +622,7 @@ __global__ __launch_bounds__(256) void k_heads_count(const uint64_t *__restrict_
             uint64_t prev = __shfl_up(cur[k], 1);
             if (lane == 0 && p > 0 && p < M) prev = S[p - 1];
             if (p < M) {
-                bool h = p == 0 || (prev >> 31) != (cur[k] >> 31);
-                if (!h && any6 && pk_fam(cur[k])) {
-                    uint32_t ka[4], kb[4];
-                    load_key6(hdr, pk_idx(prev), ka);
-                    load_key6(hdr, pk_idx(cur[k]), kb);
-                    h = key_cmp(2, ka, 2, kb) != 0;
-                }
+                const bool h = p == 0 || (prev >> 32) != (cur[k] >> 32);
                 headf[p] = h ? 1u : 0u;
                 cnt += h;
                 sub[k >> 2] += h;
@@ -840,6 +763,7 @@ __global__ __launch_bounds__(256) void k_insert(const uint64_t *__restrict__ S, 
                                                 uint32_t *__restrict__ seg_slot,
                                                 const uint8_t *__restrict__ hdr, Slot *table,
                                                 TableState *tstate, Limits lim) {
+    if (bs->err) return;    // e.g. the id table overflowed: no state changes
     // sliding window: the carried logs plus every packet of this batch must fit the
     // history buffer (conservative; checked before any state changes)
     if (lim.limiter == 1 && tstate->hist_total + bs->n_valid > lim.hist_cap) {
@@ -1348,11 +1272,12 @@ static uint32_t next_generation() {
 
 hipError_t launch_verdict_pipeline(const uint8_t *hdr, const uint32_t *len, const uint64_t *ts,
                                    uint32_t n, uint8_t *verdict, Slot *table, TableState *tstate,
-                                   BatchState *bs, const Scratch &sc, const Limits &lim,
-                                   bool do_limit, const FlowRequest *flows, const HistBufs &hist,
-                                   hipStream_t st, hipEvent_t *ev, int nev, int *nev_used,
-                                   const char **names) {
+                                   BatchState *bs, const Scratch &sc_in, uint32_t id_gen,
+                                   const Limits &lim, bool do_limit, const FlowRequest *flows,
+                                   const HistBufs &hist, hipStream_t st, hipEvent_t *ev, int nev,
+                                   int *nev_used, const char **names) {
     (void)hipGetLastError();   // a stale error of another caller is not ours
+    Scratch sc = sc_in;        // packed[0] / pay[0] become the sorted output below
     int ei = 0;
     auto mark = [&](const char *name) {
         if (ev && ei < nev) {
@@ -1372,15 +1297,24 @@ hipError_t launch_verdict_pipeline(const uint8_t *hdr, const uint32_t *len, cons
     const bool onesweep = (lim.test_flags & 2u) != 0;
     if ((e = hipMemsetAsync(sc.sort_ctl, 0, kSortCtlWords * 4, st)) != hipSuccess) return e;
     mark("start");
+    // test hook: every IPv6 source probes the id table from IPv4 10.0.0.1's slot
+    const uint32_t k10[4] = {0x0100000Au, 0, 0, 0};
+    const IdTable idt{reinterpret_cast<unsigned long long *>(sc.id_tab),
+                      sc.id_tab + 2 * (lim.table_mask + 1), lim.table_mask, id_gen,
+                      (lim.test_flags & 1u) ? (uint32_t)(slot_hash(1u, k10, kIdSeed) & lim.table_mask)
+                                            : 0xFFFFFFFFu};
     k_parse<<<std::min<uint32_t>(2048, std::max<uint32_t>(1, cdiv(n, 256))), 256, 0, st>>>(
-        hdr, len, ts, n, sc.packed[0], verdict, bs, lim.salt32, lim.seed,
-        (lim.test_flags & 1u) ? skey_v4(0x0100000Au, lim.salt32) : 0u, sc.sort_ctl);
+        hdr, len, ts, n, sc.packed[0], verdict, bs, idt, sc.sort_ctl);
     mark("k_parse");
     k_hist_prep<<<1, 256, 0, st>>>(sc.sort_ctl, sc.gbase, bs);
     const uint32_t ntiles = std::max<uint32_t>(1, cdiv(n, kSortTile));
     const uint32_t tcap = (uint32_t)(sc.cap / kSortTile + 2);
     const uint32_t gen0 = onesweep ? next_generation() : 0u;
-    for (int pass = 0; pass < 4; ++pass) {
+    // source ids have log2(slots) bits: one 8-bit digit pass per byte of them
+    uint32_t idbits = 0;
+    while ((1ull << idbits) <= lim.table_mask) ++idbits;
+    const int npass = std::max(1, (int)((idbits + 7) / 8));
+    for (int pass = 0; pass < npass; ++pass) {
         const uint64_t *in = sc.packed[pass & 1];
         uint64_t *out = sc.packed[(pass + 1) & 1];
         const uint64_t *pin = pass == 0 ? nullptr : sc.pay[pass & 1];
@@ -1402,14 +1336,11 @@ hipError_t launch_verdict_pipeline(const uint8_t *hdr, const uint32_t *len, cons
             mark("k_tile_scatter");
         }
     }
+    if (npass & 1) {
+        std::swap(sc.packed[0], sc.packed[1]);
+        std::swap(sc.pay[0], sc.pay[1]);
+    }
     uint64_t *S = sc.packed[0];
-    const uint32_t nbm = cdiv(n, 64);
-    if ((e = hipMemsetAsync(sc.fix_bitmap, 0, (size_t)nbm * 8, st)) != hipSuccess) return e;
-    k_v6_mixed<<<gridStream, 256, 0, st>>>(S, bs, hdr, sc.fix_bitmap, sc.fix_list);
-    k_fixup_short<<<256, 256, 0, st>>>(S, bs, hdr, sc.fix_list, lim.salt32);
-    k_fixup_long<<<64, 256, 0, st>>>(S, sc.packed[1], bs, hdr, sc.fix_list, lim.salt32);
-    k_fixup_pay<<<64, 256, 0, st>>>(S, sc.pay[0], bs, sc.fix_list, ts, len);
-    mark("v6_fixup");
     k_heads_count<<<gridTiles, 256, 0, st>>>(S, bs, hdr, sc.headf, sc.tile_aux, sc.sub_cnt);
     mark("k_heads_count");
     k_scan_tiles_u32<<<1, 1024, 0, st>>>(sc.tile_aux, bs, sc.seg_start);

@@ -58,7 +58,7 @@ struct BatchState {
     uint32_t n_new;
     uint32_t err;
     uint32_t max_len;
-    uint32_t n_fix;       // mixed hash runs queued for the exact key fixup
+    uint32_t n_fix;       // unused (0): source ids are exact, no collision fixups
     uint32_t n_long;      // segments longer than kShortSeg (wave walker)
     uint32_t n_span;      // sources crossing flow tiles (k_flow_combine)
     uint64_t max_ts;
@@ -155,7 +155,9 @@ __host__ __device__ inline uint64_t slot_hash(uint32_t tag, const uint32_t k[4],
     return h;
 }
 
-// packed sort word: skey << 32 | family << 31 | arrival index (n <= 2^31 - 1)
+// packed sort word: source id << 32 | family << 31 | arrival index (n <= 2^31 - 1); the
+// source id is the source's slot in the per-batch id table (k_parse), so equal ids <=>
+// equal (family, address) and the sort needs only log2(slots) key bits
 __host__ __device__ inline uint32_t pk_skey(uint64_t v) { return (uint32_t)(v >> 32); }
 __host__ __device__ inline uint32_t pk_fam(uint64_t v) { return (uint32_t)(v >> 31) & 1u; }
 __host__ __device__ inline uint32_t pk_idx(uint64_t v) { return (uint32_t)v & 0x7FFFFFFFu; }
@@ -171,8 +173,6 @@ struct Scratch {
     uint32_t *hist;        // sort: per-tile digit counts [256][cap/kSortTile+2]; walker classes
     uint32_t *tile_aux;    // per kTile tile
     uint8_t *tile_last;
-    uint32_t *fix_list;
-    uint64_t *fix_bitmap;  // one bit per sorted position
     uint32_t *seg_order;   // segment ids grouped by length class (walker load balance)
     uint32_t *sub_cnt;     // heads per 1024-position flow tile
     void *flow_first;      // FlowAcc per flow tile (fsx_flows.hip)
@@ -185,6 +185,8 @@ struct Scratch {
     uint64_t *lim_tiles;   // limiter scans: 4 u64 per kTile tile (token bucket: map + carry)
     uint64_t lim_tiles_n;  // tiles lim_tiles is sized for
     SwSeg *sw_seg;         // sliding window: per source (null for other limiters)
+    uint32_t *id_tab;      // per-batch source ids: u64 heads [slots] then u32 IPv6 key
+                           // words [slots][4] (generation-tagged, never cleared)
     uint64_t cap;          // packets the scratch is sized for
 };
 
@@ -203,7 +205,7 @@ struct FlowRequest {
 // do_limit: run the rate limiter (verdicts + maps); flows: also per-source features.
 hipError_t launch_verdict_pipeline(const uint8_t *hdr, const uint32_t *len, const uint64_t *ts,
                                    uint32_t n, uint8_t *verdict, Slot *table, TableState *tstate,
-                                   BatchState *bs, const Scratch &sc, const Limits &lim,
+                                   BatchState *bs, const Scratch &sc, uint32_t id_gen, const Limits &lim,
                                    bool do_limit, const FlowRequest *flows, const HistBufs &hist,
                                    hipStream_t st, hipEvent_t *ev, int nev, int *nev_used,
                                    const char **names);
