@@ -50,9 +50,9 @@ extern "C" {
 
 #define FSX_HDR_BYTES 64
 
-/* fsx_config.flags — test hooks only. FSX_FLAG_TEST_V6_COLLIDE sends every IPv6
- * source to one sort key equal to IPv4 10.0.0.1's, forcing the exact collision
- * fixup path (results must not change). */
+/* fsx_config.flags — test hooks only. FSX_FLAG_TEST_V6_COLLIDE makes every IPv6
+ * source start its probe of the per-batch source-id table at IPv4 10.0.0.1's slot
+ * (one long probe chain shared by all of them; results must not change). */
 #define FSX_FLAG_TEST_V6_COLLIDE 1u
 /* Sort with the single-pass onesweep variant (decoupled look-back) instead of the
  * per-pass tile histograms (A/B measurements only). */

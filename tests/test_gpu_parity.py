@@ -141,8 +141,8 @@ def test_non_monotone_clock(native, oracle):
 
 
 def test_ipv6_forced_collisions(native, oracle):
-    """FSX_FLAG_TEST_V6_COLLIDE: every IPv6 key shares one sort key (and IPv4 10.0.0.1's),
-    so all IPv6 sources form one huge mixed run resolved by the exact fixup."""
+    """FSX_FLAG_TEST_V6_COLLIDE: every IPv6 source starts probing the per-batch id table
+    at IPv4 10.0.0.1's slot, so all of them (and 10.0.0.1) share one long probe chain."""
     rng = np.random.default_rng(21)
     from flowsentryx_amd import synth
     hdr, ln, ts = rand_stream(rng, 20000, 50, dt_max=300, v6_frac=0.5)
@@ -154,7 +154,7 @@ def test_ipv6_forced_collisions(native, oracle):
 
 
 def test_many_ipv6_sources(native, oracle):
-    """2^17 distinct IPv6 + IPv4 sources: natural 32-bit sort-key collisions."""
+    """2^17 distinct IPv6 + 2^17 IPv4 sources in one batch (a half-full id table)."""
     rng = np.random.default_rng(3)
     n = 1 << 17
     from flowsentryx_amd import synth
