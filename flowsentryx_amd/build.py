@@ -24,7 +24,7 @@ HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
 ARCH = os.environ.get("FSX_OFFLOAD_ARCH", "gfx950")
 COMMON = [
     f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-    "-ffp-contract=off", "-Wall", "-Wno-unused-function", "-Wno-unused-variable",
+    "-ffp-contract=off", "-Wall", "-Wshadow", "-Wno-unused-function", "-Wno-unused-variable",
     f"-I{INCLUDE}", f"-I{CSRC}",
 ]
 

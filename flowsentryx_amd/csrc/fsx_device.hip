@@ -125,20 +125,31 @@ __global__ __launch_bounds__(256) void k_parse(const uint8_t *__restrict__ hdr,
                                                const uint64_t *__restrict__ ts, uint32_t n,
                                                uint64_t *__restrict__ packed,
                                                uint8_t *__restrict__ verdict, BatchState *bs,
-                                               IdTable idt, uint32_t *__restrict__ ghist) {
+                                               IdTable idt, uint32_t *__restrict__ ghist,
+                                               uint32_t *__restrict__ thist, uint32_t tcap) {
     __shared__ uint32_t s_rec[4][64 * 17];
     __shared__ uint32_t s_red[4][3];
     __shared__ unsigned long long s_ts[4], s_its[4];
     __shared__ uint32_t s_hist[4][4][256];  // per wave: the 4 radix digits of every sort key
+    __shared__ uint32_t s_t0[4][256];       // per wave: digit 0 of the current sort tile
     const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
 #pragma unroll
     for (int d = 0; d < 16; ++d) (&s_hist[0][0][0])[d * 256 + threadIdx.x] = 0;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) s_t0[d][threadIdx.x] = 0;
     __syncthreads();
     uint32_t *rec = s_rec[w];
     uint32_t any6 = 0, nonmono = 0, maxlen = 0;
     uint64_t maxts = 0, inv_mints = 0;  // ~min ts, max-reduced
+    // a block owns whole 4096-record sort tiles (so it can emit pass 0's per-tile digit
+    // counts: no k_tile_hist for pass 0); wave w parses records [w*1024, +1024) of the
+    // tile in 64-record steps
     const uint32_t ntiles = (n + 63u) >> 6;
-    const uint32_t stride = gridDim.x * 4u;
+    const uint32_t nsort = (n + kSortTile - 1) / kSortTile;
+    auto step_of = [&](uint32_t st, uint32_t j) { return st * (kSortTile / 64) + w * 16u + j; };
+    auto next_step = [&](uint32_t st, uint32_t j, uint32_t &st2, uint32_t &j2) {
+        if (j + 1 < 16) { st2 = st; j2 = j + 1; } else { st2 = st + gridDim.x; j2 = 0; }
+    };
     // software pipeline: the next tile's loads are in flight while this one is parsed
     auto load = [&](uint32_t tt, uint4 (&h)[4], uint32_t &L_, uint64_t &T_, uint64_t &P_) {
         const uint32_t base = tt << 6;
@@ -159,14 +170,18 @@ __global__ __launch_bounds__(256) void k_parse(const uint8_t *__restrict__ hdr,
     uint4 hv[4];
     uint32_t Lc;
     uint64_t Tc, Pc;
-    load(blockIdx.x * 4u + w, hv, Lc, Tc, Pc);
-    // software pipeline: the next tile's loads are in flight while this one is parsed
+    load(step_of(blockIdx.x, 0), hv, Lc, Tc, Pc);
+    // software pipeline: the next step's loads are in flight while this one is parsed
     // (measured faster than issuing the id probes ahead of the prefetch)
-    for (uint32_t t = blockIdx.x * 4u + w; t < ntiles; t += stride) {
+    for (uint32_t tile = blockIdx.x; tile < nsort; tile += gridDim.x)
+    for (uint32_t j = 0; j < 16; ++j) {
+        const uint32_t t = step_of(tile, j);
+        uint32_t T2, j2;
+        next_step(tile, j, T2, j2);
         uint4 hn[4];
         uint32_t Ln;
         uint64_t Tn, Pn;
-        load(t + stride, hn, Ln, Tn, Pn);
+        load(T2 < nsort ? step_of(T2, j2) : ntiles, hn, Ln, Tn, Pn);
         const uint32_t base = t << 6;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -241,8 +256,18 @@ __global__ __launch_bounds__(256) void k_parse(const uint8_t *__restrict__ hdr,
 #pragma unroll
             for (int dg = 0; dg < 4; ++dg)
                 atomicAdd(&s_hist[w][dg][(uint32_t)(out >> (32 + 8 * dg)) & 255u], 1u);
+            atomicAdd(&s_t0[w][(uint32_t)(out >> 32) & 255u], 1u);
         }
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        if (j == 15 && thist) {   // sort tile done: its digit-0 counts, digit-major
+            __syncthreads();
+            const uint32_t c = s_t0[0][threadIdx.x] + s_t0[1][threadIdx.x] + s_t0[2][threadIdx.x] +
+                               s_t0[3][threadIdx.x];
+            thist[(size_t)threadIdx.x * tcap + tile] = c;
+#pragma unroll
+            for (int d = 0; d < 4; ++d) s_t0[d][threadIdx.x] = 0;
+            __syncthreads();
+        }
     }
     if (ghist) {
         __syncthreads();
@@ -1303,12 +1328,12 @@ hipError_t launch_verdict_pipeline(const uint8_t *hdr, const uint32_t *len, cons
                       sc.id_tab + 2 * (lim.table_mask + 1), lim.table_mask, id_gen,
                       (lim.test_flags & 1u) ? (uint32_t)(slot_hash(1u, k10, kIdSeed) & lim.table_mask)
                                             : 0xFFFFFFFFu};
-    k_parse<<<std::min<uint32_t>(2048, std::max<uint32_t>(1, cdiv(n, 256))), 256, 0, st>>>(
-        hdr, len, ts, n, sc.packed[0], verdict, bs, idt, sc.sort_ctl);
-    mark("k_parse");
-    k_hist_prep<<<1, 256, 0, st>>>(sc.sort_ctl, sc.gbase, bs);
     const uint32_t ntiles = std::max<uint32_t>(1, cdiv(n, kSortTile));
     const uint32_t tcap = (uint32_t)(sc.cap / kSortTile + 2);
+    k_parse<<<std::min<uint32_t>(1024, ntiles), 256, 0, st>>>(
+        hdr, len, ts, n, sc.packed[0], verdict, bs, idt, sc.sort_ctl, onesweep ? nullptr : sc.hist, tcap);
+    mark("k_parse");
+    k_hist_prep<<<1, 256, 0, st>>>(sc.sort_ctl, sc.gbase, bs);
     const uint32_t gen0 = onesweep ? next_generation() : 0u;
     // source ids have log2(slots) bits: one 8-bit digit pass per byte of them
     uint32_t idbits = 0;
@@ -1328,7 +1353,8 @@ hipError_t launch_verdict_pipeline(const uint8_t *hdr, const uint32_t *len, cons
                                                        ts, len);
             mark("k_onesweep");
         } else {
-            k_tile_hist<<<ntiles, 256, 0, st>>>(in, n, Ld, shift, pass == 0, sc.hist, tcap);
+            if (pass > 0)   // pass 0's per-tile counts come from k_parse
+                k_tile_hist<<<ntiles, 256, 0, st>>>(in, n, Ld, shift, pass == 0, sc.hist, tcap);
             k_tile_scan<<<256, 256, 0, st>>>(sc.hist, tcap, n, Ld, sc.gbase + 256 * pass);
             mark("k_tile_hist");
             k_tile_scatter<kLatePayDefault><<<ntiles, 256, 0, st>>>(in, out, n, Ld, shift, pass == 0, sc.hist, tcap, bs,
