@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 
 #include <atomic>
+#include <cstdlib>
 
 #include "fsx_dev_common.h"
 #include "fsx_internal.h"
@@ -126,13 +127,15 @@ __global__ __launch_bounds__(256) void k_parse(const uint8_t *__restrict__ hdr,
                                                uint64_t *__restrict__ packed,
                                                uint8_t *__restrict__ verdict, BatchState *bs,
                                                IdTable idt, uint32_t *__restrict__ ghist,
-                                               uint32_t *__restrict__ thist, uint32_t tcap) {
+                                               uint32_t *__restrict__ thist, uint32_t tcap,
+                                               uint32_t dbits) {
     __shared__ uint32_t s_rec[4][64 * 17];
     __shared__ uint32_t s_red[4][3];
     __shared__ unsigned long long s_ts[4], s_its[4];
     __shared__ uint32_t s_hist[4][4][256];  // per wave: the 4 radix digits of every sort key
     __shared__ uint32_t s_t0[4][256];       // per wave: digit 0 of the current sort tile
     const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
+    const uint32_t dmask = (1u << dbits) - 1u;   // radix digits of dbits <= 8 bits
 #pragma unroll
     for (int d = 0; d < 16; ++d) (&s_hist[0][0][0])[d * 256 + threadIdx.x] = 0;
 #pragma unroll
@@ -255,8 +258,8 @@ __global__ __launch_bounds__(256) void k_parse(const uint8_t *__restrict__ hdr,
         if (ghist && ip) {
 #pragma unroll
             for (int dg = 0; dg < 4; ++dg)
-                atomicAdd(&s_hist[w][dg][(uint32_t)(out >> (32 + 8 * dg)) & 255u], 1u);
-            atomicAdd(&s_t0[w][(uint32_t)(out >> 32) & 255u], 1u);
+                atomicAdd(&s_hist[w][dg][(uint32_t)(out >> (32 + dbits * dg)) & dmask], 1u);
+            atomicAdd(&s_t0[w][(uint32_t)(out >> 32) & dmask], 1u);
         }
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         if (j == 15 && thist) {   // sort tile done: its digit-0 counts, digit-major
@@ -343,8 +346,8 @@ __device__ __forceinline__ bool sort_item(uint32_t i, uint32_t end, int first, u
 
 // Per-tile digit counts (one block per tile; per-wave LDS counters).
 __global__ __launch_bounds__(256) void k_tile_hist(const uint64_t *__restrict__ in, uint32_t L_host,
-                                                   const uint32_t *L_dev, uint32_t shift, int first,
-                                                   uint32_t *__restrict__ thist, uint32_t tcap) {
+                                                   const uint32_t *L_dev, uint32_t shift, uint32_t dmask,
+                                                   int first, uint32_t *__restrict__ thist, uint32_t tcap) {
     __shared__ uint32_t sh[4][256];
     const uint32_t tid = threadIdx.x, w = tid >> 6;
     const uint32_t L = L_dev ? *L_dev : L_host;
@@ -365,7 +368,7 @@ __global__ __launch_bounds__(256) void k_tile_hist(const uint64_t *__restrict__ 
     for (int r = 0; r < kSortItems; ++r) {
         const uint32_t i = t0 + (uint32_t)r * 256u + tid;
         const bool ok = sort_item(i, end, first, v[r]);
-        const uint32_t d = (uint32_t)(v[r] >> shift) & 255u;
+        const uint32_t d = (uint32_t)(v[r] >> shift) & dmask;
         const uint64_t act = __ballot(ok);
         if (!act) continue;
         // runs of one heavy source make whole waves share a digit: one add for them
@@ -407,7 +410,7 @@ __global__ __launch_bounds__(256) void k_tile_scan(uint32_t *__restrict__ thist,
 template <bool kLatePay, class Offs>
 __device__ __forceinline__ void sort_tile(uint32_t t, const uint64_t *__restrict__ in,
                                           uint64_t *__restrict__ out, uint32_t L, uint32_t shift,
-                                          int first, const BatchState *bs,
+                                          uint32_t dmask, int first, const BatchState *bs,
                                           const uint64_t *__restrict__ pin, uint64_t *__restrict__ pout,
                                           const uint64_t *__restrict__ ts,
                                           const uint32_t *__restrict__ len, Offs offs) {
@@ -456,7 +459,7 @@ __device__ __forceinline__ void sort_tile(uint32_t t, const uint64_t *__restrict
         const uint32_t i = t0 + w * 1024u + (uint32_t)r * 64u + lane;
         const bool valid = sort_item(i, end, first, v[r]);
         const uint64_t act = __ballot(valid);
-        const uint32_t d = (uint32_t)(v[r] >> shift) & 255u;
+        const uint32_t d = (uint32_t)(v[r] >> shift) & dmask;
         const int lead0 = act ? __ffsll((unsigned long long)act) - 1 : 0;
         const uint32_t dl = __shfl(d, lead0);
         const uint64_t peers = __ballot(valid && d == dl) == act ? act : match_digit(d, act);
@@ -481,7 +484,7 @@ __device__ __forceinline__ void sort_tile(uint32_t t, const uint64_t *__restrict
 #pragma unroll
     for (int r = 0; r < kSortItems; ++r) {
         if (lr[r] != 0xFFFFFFFFu) {
-            const uint32_t dd = (uint32_t)(v[r] >> shift) & 255u;
+            const uint32_t dd = (uint32_t)(v[r] >> shift) & dmask;
             lr[r] += s_tbase[dd] + s_wc[w][dd];  // tile-sorted slot
             s_el[lr[r]] = v[r];
         }
@@ -495,7 +498,7 @@ __device__ __forceinline__ void sort_tile(uint32_t t, const uint64_t *__restrict
         const uint32_t j = tid + 256u * (uint32_t)m;
         if (j < T) {
             const uint64_t x = s_el[j];
-            const uint32_t dd = (uint32_t)(x >> shift) & 255u;
+            const uint32_t dd = (uint32_t)(x >> shift) & dmask;
             dst[m] = s_dst[dd] + (j - s_tbase[dd]);
             out[dst[m]] = x;
         }
@@ -529,8 +532,9 @@ struct TileOffs {
 template <bool kLatePay>
 __global__ __launch_bounds__(256, kLatePay ? 4 : 1) void k_tile_scatter(const uint64_t *__restrict__ in,
                                                       uint64_t *__restrict__ out, uint32_t L_host,
-                                                      const uint32_t *L_dev, uint32_t shift, int first,
-                                                      const uint32_t *__restrict__ offs, uint32_t tcap,
+                                                      const uint32_t *L_dev, uint32_t shift, uint32_t dmask,
+                                                      int first, const uint32_t *__restrict__ offs,
+                                                      uint32_t tcap,
                                                       const BatchState *bs,
                                                       const uint64_t *__restrict__ pin,
                                                       uint64_t *__restrict__ pout,
@@ -538,7 +542,7 @@ __global__ __launch_bounds__(256, kLatePay ? 4 : 1) void k_tile_scatter(const ui
                                                       const uint32_t *__restrict__ len) {
     const uint32_t L = L_dev ? *L_dev : L_host;
     if (blockIdx.x * kSortTile >= L) return;
-    sort_tile<kLatePay>(blockIdx.x, in, out, L, shift, first, bs, pin, pout, ts, len,
+    sort_tile<kLatePay>(blockIdx.x, in, out, L, shift, dmask, first, bs, pin, pout, ts, len,
                         TileOffs{offs, tcap, blockIdx.x});
 }
 
@@ -599,7 +603,7 @@ struct LookbackOffs {
 template <int kLW>
 __global__ __launch_bounds__(256) void k_onesweep(const uint64_t *__restrict__ in,
                                                   uint64_t *__restrict__ out, uint32_t L_host,
-                                                  const uint32_t *L_dev, uint32_t shift,
+                                                  const uint32_t *L_dev, uint32_t shift, uint32_t dmask,
                                                   const uint32_t *__restrict__ gbase,
                                                   unsigned long long *status, uint32_t *tile_ctr,
                                                   uint32_t gen, int first, BatchState *bs,
@@ -614,7 +618,7 @@ __global__ __launch_bounds__(256) void k_onesweep(const uint64_t *__restrict__ i
     __syncthreads();
     const uint32_t t = s_tile;
     if (t >= ntiles) return;
-    sort_tile<false>(t, in, out, L, shift, first, bs, pin, pout, ts, len,
+    sort_tile<false>(t, in, out, L, shift, dmask, first, bs, pin, pout, ts, len,
                      LookbackOffs<kLW>{status, gbase, bs, t, gen});
 }
 
@@ -1330,34 +1334,39 @@ hipError_t launch_verdict_pipeline(const uint8_t *hdr, const uint32_t *len, cons
                                             : 0xFFFFFFFFu};
     const uint32_t ntiles = std::max<uint32_t>(1, cdiv(n, kSortTile));
     const uint32_t tcap = (uint32_t)(sc.cap / kSortTile + 2);
-    k_parse<<<std::min<uint32_t>(1024, ntiles), 256, 0, st>>>(
-        hdr, len, ts, n, sc.packed[0], verdict, bs, idt, sc.sort_ctl, onesweep ? nullptr : sc.hist, tcap);
-    mark("k_parse");
-    k_hist_prep<<<1, 256, 0, st>>>(sc.sort_ctl, sc.gbase, bs);
-    const uint32_t gen0 = onesweep ? next_generation() : 0u;
-    // source ids have log2(slots) bits: one 8-bit digit pass per byte of them
+    // source ids have log2(slots) bits: ceil(bits / 8) LSD passes of equal digits of at
+    // most 8 bits (21 bits: 3 x 7 — fewer buckets, longer runs per tile than 8 + 8 + 5)
     uint32_t idbits = 0;
     while ((1ull << idbits) <= lim.table_mask) ++idbits;
     const int npass = std::max(1, (int)((idbits + 7) / 8));
+    static const bool full_digits = getenv("FSX_SORT_FULL_DIGITS") != nullptr;   // A/B: 8,8,..,rest
+    const uint32_t dbits = full_digits ? 8u : std::max<uint32_t>(1, (idbits + npass - 1) / npass);
+    const uint32_t dmask = (1u << dbits) - 1u;
+    k_parse<<<std::min<uint32_t>(1024, ntiles), 256, 0, st>>>(
+        hdr, len, ts, n, sc.packed[0], verdict, bs, idt, sc.sort_ctl, onesweep ? nullptr : sc.hist, tcap,
+        dbits);
+    mark("k_parse");
+    k_hist_prep<<<1, 256, 0, st>>>(sc.sort_ctl, sc.gbase, bs);
+    const uint32_t gen0 = onesweep ? next_generation() : 0u;
     for (int pass = 0; pass < npass; ++pass) {
         const uint64_t *in = sc.packed[pass & 1];
         uint64_t *out = sc.packed[(pass + 1) & 1];
         const uint64_t *pin = pass == 0 ? nullptr : sc.pay[pass & 1];
         uint64_t *pout = sc.pay[(pass + 1) & 1];
-        const uint32_t shift = 32u + 8u * (uint32_t)pass;
+        const uint32_t shift = 32u + dbits * (uint32_t)pass;
         const uint32_t *Ld = pass == 0 ? nullptr : &bs->n_valid;
         if (onesweep) {
-            k_onesweep<kLookW><<<ntiles, 256, 0, st>>>(in, out, n, Ld, shift, sc.gbase + 256 * pass,
+            k_onesweep<kLookW><<<ntiles, 256, 0, st>>>(in, out, n, Ld, shift, dmask, sc.gbase + 256 * pass,
                                                        sc.status, sc.sort_ctl + 1024 + pass,
                                                        gen0 + (uint32_t)pass, pass == 0, bs, pin, pout,
                                                        ts, len);
             mark("k_onesweep");
         } else {
             if (pass > 0)   // pass 0's per-tile counts come from k_parse
-                k_tile_hist<<<ntiles, 256, 0, st>>>(in, n, Ld, shift, pass == 0, sc.hist, tcap);
+                k_tile_hist<<<ntiles, 256, 0, st>>>(in, n, Ld, shift, dmask, pass == 0, sc.hist, tcap);
             k_tile_scan<<<256, 256, 0, st>>>(sc.hist, tcap, n, Ld, sc.gbase + 256 * pass);
             mark("k_tile_hist");
-            k_tile_scatter<kLatePayDefault><<<ntiles, 256, 0, st>>>(in, out, n, Ld, shift, pass == 0, sc.hist, tcap, bs,
+            k_tile_scatter<kLatePayDefault><<<ntiles, 256, 0, st>>>(in, out, n, Ld, shift, dmask, pass == 0, sc.hist, tcap, bs,
                                                    pin, pout, ts, len);
             mark("k_tile_scatter");
         }
