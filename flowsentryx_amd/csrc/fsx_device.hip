@@ -149,9 +149,10 @@ __global__ __launch_bounds__(256) void k_parse(const uint8_t *__restrict__ hdr,
     // tile in 64-record steps
     const uint32_t ntiles = (n + 63u) >> 6;
     const uint32_t nsort = (n + kSortTile - 1) / kSortTile;
-    auto step_of = [&](uint32_t st, uint32_t j) { return st * (kSortTile / 64) + w * 16u + j; };
+    constexpr uint32_t kSteps = kSortTile / 256;   // 64-record steps per wave and sort tile
+    auto step_of = [&](uint32_t st, uint32_t j) { return st * (kSortTile / 64) + w * kSteps + j; };
     auto next_step = [&](uint32_t st, uint32_t j, uint32_t &st2, uint32_t &j2) {
-        if (j + 1 < 16) { st2 = st; j2 = j + 1; } else { st2 = st + gridDim.x; j2 = 0; }
+        if (j + 1 < kSteps) { st2 = st; j2 = j + 1; } else { st2 = st + gridDim.x; j2 = 0; }
     };
     // software pipeline: the next tile's loads are in flight while this one is parsed
     auto load = [&](uint32_t tt, uint4 (&h)[4], uint32_t &L_, uint64_t &T_, uint64_t &P_) {
@@ -177,7 +178,7 @@ __global__ __launch_bounds__(256) void k_parse(const uint8_t *__restrict__ hdr,
     // software pipeline: the next step's loads are in flight while this one is parsed
     // (measured faster than issuing the id probes ahead of the prefetch)
     for (uint32_t tile = blockIdx.x; tile < nsort; tile += gridDim.x)
-    for (uint32_t j = 0; j < 16; ++j) {
+    for (uint32_t j = 0; j < kSteps; ++j) {
         const uint32_t t = step_of(tile, j);
         uint32_t T2, j2;
         next_step(tile, j, T2, j2);
@@ -262,7 +263,7 @@ __global__ __launch_bounds__(256) void k_parse(const uint8_t *__restrict__ hdr,
             atomicAdd(&s_t0[w][(uint32_t)(out >> 32) & dmask], 1u);
         }
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        if (j == 15 && thist) {   // sort tile done: its digit-0 counts, digit-major
+        if (j == kSteps - 1 && thist) {   // sort tile done: its digit-0 counts, digit-major
             __syncthreads();
             const uint32_t c = s_t0[0][threadIdx.x] + s_t0[1][threadIdx.x] + s_t0[2][threadIdx.x] +
                                s_t0[3][threadIdx.x];
@@ -430,7 +431,7 @@ __device__ __forceinline__ void sort_tile(uint32_t t, const uint64_t *__restrict
     uint32_t lr[kSortItems];
 #pragma unroll
     for (int r = 0; r < kSortItems; ++r) {
-        const uint32_t i = t0 + w * 1024u + (uint32_t)r * 64u + lane;
+        const uint32_t i = t0 + w * (kSortItems * 64u) + (uint32_t)r * 64u + lane;
         v[r] = i < end ? in[i] : kSentinel;
     }
     // payload words: built from (ts, len) in pass 0 (positions are arrival indices
@@ -441,7 +442,7 @@ __device__ __forceinline__ void sort_tile(uint32_t t, const uint64_t *__restrict
         const uint64_t tbase = ~bs->inv_min_ts;
 #pragma unroll
         for (int r = 0; r < kSortItems; ++r) {
-            const uint32_t i = t0 + w * 1024u + (uint32_t)r * 64u + lane;
+            const uint32_t i = t0 + w * (kSortItems * 64u) + (uint32_t)r * 64u + lane;
             if (first) pv[r] = i < end ? ((ts[i] - tbase) << kPayLenBits) | len[i] : 0ull;
             else pv[r] = i < end ? pin[i] : 0ull;
         }
@@ -456,7 +457,7 @@ __device__ __forceinline__ void sort_tile(uint32_t t, const uint64_t *__restrict
     // reservations need no round trip in between.
 #pragma unroll
     for (int r = 0; r < kSortItems; ++r) {
-        const uint32_t i = t0 + w * 1024u + (uint32_t)r * 64u + lane;
+        const uint32_t i = t0 + w * (kSortItems * 64u) + (uint32_t)r * 64u + lane;
         const bool valid = sort_item(i, end, first, v[r]);
         const uint64_t act = __ballot(valid);
         const uint32_t d = (uint32_t)(v[r] >> shift) & dmask;
