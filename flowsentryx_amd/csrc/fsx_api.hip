@@ -76,7 +76,11 @@ struct fsx_ctx {
     bool ev_ready = false;
     hipEvent_t ev[kRing][kMaxEv]{};
     const char *ev_names[kRing][kMaxEv]{};
+    int ev_prev[kRing][kMaxEv]{};
     int ev_used[kRing]{};
+    // second stream: flow features beside the limiter (fork / join events)
+    hipStream_t aux_stream = nullptr;
+    hipEvent_t fork_ev = nullptr, join_ev = nullptr;
     int ring_n = 0;
     const char *acc_name[kMaxNames]{};
     double acc_ms[kMaxNames]{};
@@ -198,6 +202,9 @@ void fsx_close(fsx_ctx *c) {
     for (int r = 0; r < kRing; ++r)
         for (int i = 0; i < kMaxEv; ++i) if (c->ev[r][i]) hipEventDestroy(c->ev[r][i]);
     if (c->own_stream) hipStreamDestroy(c->own_stream);
+    if (c->aux_stream) hipStreamDestroy(c->aux_stream);
+    if (c->fork_ev) hipEventDestroy(c->fork_ev);
+    if (c->join_ev) hipEventDestroy(c->join_ev);
     delete c;
 }
 
@@ -225,6 +232,9 @@ int fsx_open(fsx_ctx **out, const fsx_config *cfg) {
     c->slots = next_pow2(std::max<uint64_t>(1024, 2 * k.max_entries));
     auto fail = [&](int r) { fsx_close(c); return r; };
     if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) return fail(-EIO);
+    if (hipStreamCreateWithFlags(&c->aux_stream, hipStreamNonBlocking) != hipSuccess) return fail(-EIO);
+    if (hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming) != hipSuccess) return fail(-EIO);
+    if (hipEventCreateWithFlags(&c->join_ev, hipEventDisableTiming) != hipSuccess) return fail(-EIO);
     c->stream = c->own_stream;
     if (hipMalloc(&c->table, c->slots * sizeof(Slot)) != hipSuccess) return fail(-ENOMEM);
     if (hipMalloc(&c->tstate, sizeof(TableState)) != hipSuccess) return fail(-ENOMEM);
@@ -298,9 +308,11 @@ static int drain_timings(fsx_ctx *c) {
     if (c->ring_n == 0) return 0;
     HIPCHK(c, hipStreamSynchronize(c->stream));
     for (int r = 0; r < c->ring_n; ++r) {
-        for (int i = 1; i < c->ev_used[r]; ++i) {
+        for (int i = 0; i < c->ev_used[r]; ++i) {
+            const int p = c->ev_prev[r][i];
+            if (p < 0 || !c->ev_names[r][i]) continue;   // start markers
             float t = 0;
-            HIPCHK(c, hipEventElapsedTime(&t, c->ev[r][i - 1], c->ev[r][i]));
+            HIPCHK(c, hipEventElapsedTime(&t, c->ev[r][p], c->ev[r][i]));
             const char *nm = c->ev_names[r][i];
             int k = 0;
             while (k < c->acc_n && strcmp(c->acc_name[k], nm) != 0) ++k;
@@ -315,6 +327,12 @@ static int drain_timings(fsx_ctx *c) {
     }
     c->ring_n = 0;
     return 0;
+}
+
+// A/B switch: FSX_SERIAL_FLOWS=1 keeps the flow features on the batch stream.
+static bool fork_flows() {
+    static const bool serial = getenv("FSX_SERIAL_FLOWS") != nullptr;
+    return !serial;
 }
 
 // Enqueue one batch: verdicts + maps when d_verdict is set, per-source flows when fr is.
@@ -339,15 +357,12 @@ static int run_batch(fsx_ctx *c, const uint8_t *d_hdr, const uint32_t *d_len, co
         frq.cap = (uint32_t)std::min<uint64_t>(frq.cap, c->flow_acc_cap);
         fr = &frq;
     }
-    hipEvent_t *ev = nullptr;
-    const char **names = nullptr;
-    int *used = nullptr;
+    PipeTiming tmv{};
+    PipeTiming *tm = nullptr;
     if (c->timing) {
         if (c->ring_n == kRing && (rc = drain_timings(c))) return rc;
-        ev = c->ev[c->ring_n];
-        names = c->ev_names[c->ring_n];
-        used = &c->ev_used[c->ring_n];
-        c->ring_n++;
+        tmv = PipeTiming{c->ev[c->ring_n], c->ev_names[c->ring_n], c->ev_prev[c->ring_n], kMaxEv, 0};
+        tm = &tmv;
     }
     if (++c->id_gen == 0x10000u) {   // 16-bit generations: clear the id table on wrap
         HIPCHK(c, hipMemsetAsync(c->sc.id_tab, 0, c->slots * 32, c->stream));
@@ -355,7 +370,9 @@ static int run_batch(fsx_ctx *c, const uint8_t *d_hdr, const uint32_t *d_len, co
     }
     hipError_t e = launch_verdict_pipeline(d_hdr, d_len, d_ts, (uint32_t)n, d_verdict, c->table,
                                            c->tstate, c->bs, c->sc, c->id_gen, c->lim, do_limit, fr,
-                                           c->hist, c->stream, ev, kMaxEv, used, names);
+                                           c->hist, c->stream, fork_flows() ? c->aux_stream : nullptr,
+                                           c->fork_ev, c->join_ev, tm);
+    if (tm) c->ev_used[c->ring_n++] = tm->used;
     if (e != hipSuccess) return set_err(c, -EIO, "pipeline launch: %s", hipGetErrorString(e));
     c->pending = true;
     return 0;

@@ -1304,21 +1304,25 @@ hipError_t launch_verdict_pipeline(const uint8_t *hdr, const uint32_t *len, cons
                                    uint32_t n, uint8_t *verdict, Slot *table, TableState *tstate,
                                    BatchState *bs, const Scratch &sc_in, uint32_t id_gen,
                                    const Limits &lim, bool do_limit, const FlowRequest *flows,
-                                   const HistBufs &hist, hipStream_t st, hipEvent_t *ev, int nev,
-                                   int *nev_used, const char **names) {
+                                   const HistBufs &hist, hipStream_t st, hipStream_t st2,
+                                   hipEvent_t fork_ev, hipEvent_t join_ev, PipeTiming *tm) {
     (void)hipGetLastError();   // a stale error of another caller is not ours
     Scratch sc = sc_in;        // packed[0] / pay[0] become the sorted output below
-    int ei = 0;
-    auto mark = [&](const char *name) {
-        if (ev && ei < nev) {
-            if (names) names[ei] = name;
-            hipEventRecord(ev[ei], st);
-            ++ei;
-        }
+    int last[2] = {-1, -1};    // last event index per stream (timing)
+    // mark(name) closes the interval of the kernel just enqueued on stream s (0: st, 1: st2)
+    auto mark_on = [&](const char *name, int s_id) {
+        if (!tm || tm->used >= tm->cap) return;
+        const int i = tm->used++;
+        tm->names[i] = name;
+        tm->prev[i] = last[s_id];
+        hipEventRecord(tm->ev[i], s_id ? st2 : st);
+        last[s_id] = i;
     };
+    auto mark = [&](const char *name) { mark_on(name, 0); };
+    if (tm) tm->used = 0;
     hipError_t e;
     if ((e = hipMemsetAsync(bs, 0, sizeof(BatchState), st)) != hipSuccess) return e;
-    if (n == 0) { if (nev_used) *nev_used = 0; return hipSuccess; }
+    if (n == 0) return hipSuccess;
     if ((e = hipMemsetAsync(sc.marks, 0, n, st)) != hipSuccess) return e;
     const uint32_t gridStream = std::min<uint32_t>(2048, std::max<uint32_t>(1, cdiv(n, 256)));
     const uint32_t gridTiles = std::min<uint32_t>(4096, std::max<uint32_t>(1, cdiv(n, kTile)));
@@ -1382,16 +1386,24 @@ hipError_t launch_verdict_pipeline(const uint8_t *hdr, const uint32_t *len, cons
     k_scan_tiles_u32<<<1, 1024, 0, st>>>(sc.tile_aux, bs, sc.seg_start);
     k_heads_write<<<gridTiles, 256, 0, st>>>(bs, sc.headf, sc.tile_aux, sc.seg_start);
     mark("k_heads_write");
+    const bool fork = flows && do_limit && st2 && fork_ev && join_ev;
     if (flows) {
-        launch_flows(S, sc.pay[0], bs, sc.headf, len, ts, hdr, sc.tile_aux, sc.sub_cnt, sc.seg_start,
-                     sc.flow_first, sc.flow_last, sc.span_list, flows->acc, flows->keys16, flows->fam,
-                     flows->feat, flows->prob, flows->dec, flows->cap, flows->score, lim.salt32, n, st);
-        mark("k_flow_features");
+        hipStream_t fs = st;
+        if (fork) {   // the features run beside the limiter
+            if ((e = hipEventRecord(fork_ev, st)) != hipSuccess) return e;
+            if ((e = hipStreamWaitEvent(st2, fork_ev, 0)) != hipSuccess) return e;
+            fs = st2;
+            mark_on(nullptr, 1);
+        }
+        if ((e = launch_flows(S, sc.pay[0], bs, sc.headf, len, ts, hdr, sc.tile_aux, sc.sub_cnt, sc.seg_start,
+                              sc.flow_first, sc.flow_last, sc.span_list, flows->acc, flows->keys16,
+                              flows->fam, flows->feat, flows->prob, flows->dec, flows->cap, flows->score,
+                              lim.salt32, n, fs)) != hipSuccess)
+            return e;
+        mark_on("k_flow_features", fork ? 1 : 0);
+        if (fork && (e = hipEventRecord(join_ev, st2)) != hipSuccess) return e;
     }
-    if (!do_limit) {
-        if (nev_used) *nev_used = ei;
-        return hipGetLastError();
-    }
+    if (!do_limit) return hipGetLastError();
     k_lookup<<<gridStream, 256, 0, st>>>(S, bs, sc.seg_start, sc.seg_slot, hdr, table, lim);
     mark("k_lookup");
     k_insert<<<gridStream, 256, 0, st>>>(S, bs, sc.seg_start, sc.seg_slot, hdr, table, tstate, lim);
@@ -1424,7 +1436,7 @@ hipError_t launch_verdict_pipeline(const uint8_t *hdr, const uint32_t *len, cons
     mark("k_fill_last");
     k_fill_scatter<<<gridTiles, 256, 0, st>>>(sc.marks, S, bs, sc.tile_last, verdict, tstate);
     mark("k_fill_scatter");
-    if (nev_used) *nev_used = ei;
+    if (fork && (e = hipStreamWaitEvent(st, join_ev, 0)) != hipSuccess) return e;
     return hipGetLastError();
 }
 

@@ -203,12 +203,24 @@ struct FlowRequest {
 };
 
 // do_limit: run the rate limiter (verdicts + maps); flows: also per-source features.
+// Per-kernel timing of one batch: events recorded after each kernel; interval i runs
+// from event prev[i] to event i (on the same stream; prev < 0: a start marker).
+struct PipeTiming {
+    hipEvent_t *ev;
+    const char **names;
+    int *prev;
+    int cap;
+    int used;
+};
+
+// st: the batch stream. st2 (optional, with fork/join events): the flow features run
+// on it concurrently with the rate limiter (they share only read-only inputs).
 hipError_t launch_verdict_pipeline(const uint8_t *hdr, const uint32_t *len, const uint64_t *ts,
                                    uint32_t n, uint8_t *verdict, Slot *table, TableState *tstate,
                                    BatchState *bs, const Scratch &sc, uint32_t id_gen, const Limits &lim,
                                    bool do_limit, const FlowRequest *flows, const HistBufs &hist,
-                                   hipStream_t st, hipEvent_t *ev, int nev, int *nev_used,
-                                   const char **names);
+                                   hipStream_t st, hipStream_t st2, hipEvent_t fork_ev,
+                                   hipEvent_t join_ev, PipeTiming *tm);
 
 // Build-defined limiters (fsx_limiters.hip), after the table lookup/insert of a batch:
 // one verdict mark per sorted position, final per-source state in the table.
