@@ -81,6 +81,8 @@ struct fsx_ctx {
     // second stream: flow features beside the limiter (fork / join events)
     hipStream_t aux_stream = nullptr;
     hipEvent_t fork_ev = nullptr, join_ev = nullptr;
+    hipStream_t walk_stream = nullptr;   // third stream: long-segment walker
+    hipEvent_t walk_fork_ev = nullptr, walk_join_ev = nullptr;
     int ring_n = 0;
     const char *acc_name[kMaxNames]{};
     double acc_ms[kMaxNames]{};
@@ -203,6 +205,9 @@ void fsx_close(fsx_ctx *c) {
         for (int i = 0; i < kMaxEv; ++i) if (c->ev[r][i]) hipEventDestroy(c->ev[r][i]);
     if (c->own_stream) hipStreamDestroy(c->own_stream);
     if (c->aux_stream) hipStreamDestroy(c->aux_stream);
+    if (c->walk_stream) hipStreamDestroy(c->walk_stream);
+    if (c->walk_fork_ev) hipEventDestroy(c->walk_fork_ev);
+    if (c->walk_join_ev) hipEventDestroy(c->walk_join_ev);
     if (c->fork_ev) hipEventDestroy(c->fork_ev);
     if (c->join_ev) hipEventDestroy(c->join_ev);
     delete c;
@@ -235,6 +240,9 @@ int fsx_open(fsx_ctx **out, const fsx_config *cfg) {
     if (hipStreamCreateWithFlags(&c->aux_stream, hipStreamNonBlocking) != hipSuccess) return fail(-EIO);
     if (hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming) != hipSuccess) return fail(-EIO);
     if (hipEventCreateWithFlags(&c->join_ev, hipEventDisableTiming) != hipSuccess) return fail(-EIO);
+    if (hipStreamCreateWithFlags(&c->walk_stream, hipStreamNonBlocking) != hipSuccess) return fail(-EIO);
+    if (hipEventCreateWithFlags(&c->walk_fork_ev, hipEventDisableTiming) != hipSuccess) return fail(-EIO);
+    if (hipEventCreateWithFlags(&c->walk_join_ev, hipEventDisableTiming) != hipSuccess) return fail(-EIO);
     c->stream = c->own_stream;
     if (hipMalloc(&c->table, c->slots * sizeof(Slot)) != hipSuccess) return fail(-ENOMEM);
     if (hipMalloc(&c->tstate, sizeof(TableState)) != hipSuccess) return fail(-ENOMEM);
@@ -371,7 +379,8 @@ static int run_batch(fsx_ctx *c, const uint8_t *d_hdr, const uint32_t *d_len, co
     hipError_t e = launch_verdict_pipeline(d_hdr, d_len, d_ts, (uint32_t)n, d_verdict, c->table,
                                            c->tstate, c->bs, c->sc, c->id_gen, c->lim, do_limit, fr,
                                            c->hist, c->stream, fork_flows() ? c->aux_stream : nullptr,
-                                           c->fork_ev, c->join_ev, tm);
+                                           c->fork_ev, c->join_ev, fork_flows() ? c->walk_stream : nullptr,
+                                           c->walk_fork_ev, c->walk_join_ev, tm);
     if (tm) c->ev_used[c->ring_n++] = tm->used;
     if (e != hipSuccess) return set_err(c, -EIO, "pipeline launch: %s", hipGetErrorString(e));
     c->pending = true;

@@ -1305,17 +1305,19 @@ hipError_t launch_verdict_pipeline(const uint8_t *hdr, const uint32_t *len, cons
                                    BatchState *bs, const Scratch &sc_in, uint32_t id_gen,
                                    const Limits &lim, bool do_limit, const FlowRequest *flows,
                                    const HistBufs &hist, hipStream_t st, hipStream_t st2,
-                                   hipEvent_t fork_ev, hipEvent_t join_ev, PipeTiming *tm) {
+                                   hipEvent_t fork_ev, hipEvent_t join_ev, hipStream_t st3,
+                                   hipEvent_t walk_fork_ev, hipEvent_t walk_join_ev, PipeTiming *tm) {
     (void)hipGetLastError();   // a stale error of another caller is not ours
     Scratch sc = sc_in;        // packed[0] / pay[0] become the sorted output below
-    int last[2] = {-1, -1};    // last event index per stream (timing)
-    // mark(name) closes the interval of the kernel just enqueued on stream s (0: st, 1: st2)
+    int last[3] = {-1, -1, -1};   // last event index per stream (timing)
+    // mark(name) closes the interval of the kernel just enqueued on stream s (0: st, 1: st2,
+    // 2: st3)
     auto mark_on = [&](const char *name, int s_id) {
         if (!tm || tm->used >= tm->cap) return;
         const int i = tm->used++;
         tm->names[i] = name;
         tm->prev[i] = last[s_id];
-        hipEventRecord(tm->ev[i], s_id ? st2 : st);
+        (void)hipEventRecord(tm->ev[i], s_id == 2 ? st3 : s_id == 1 ? st2 : st);
         last[s_id] = i;
     };
     auto mark = [&](const char *name) { mark_on(name, 0); };
@@ -1423,12 +1425,23 @@ hipError_t launch_verdict_pipeline(const uint8_t *hdr, const uint32_t *len, cons
                 return e;
             mark("k_sliding_window");
         } else {
+            // short and long segments are disjoint: the wave walker runs on its own
+            // stream beside the thread walker when a third stream is available
+            const bool fork3 = st3 && walk_fork_ev && walk_join_ev;
+            if (fork3) {
+                if ((e = hipEventRecord(walk_fork_ev, st)) != hipSuccess) return e;
+                if ((e = hipStreamWaitEvent(st3, walk_fork_ev, 0)) != hipSuccess) return e;
+                mark_on(nullptr, 2);
+            }
+            k_walk_fixed_long<<<1024, 256, 0, fork3 ? st3 : st>>>(S, bs, sc.seg_start, sc.seg_slot, ts, len,
+                                                                  sc.pay[0], sc.seg_order, cls, sc.marks,
+                                                                  table, lim);
+            mark_on("k_walk_fixed_long", fork3 ? 2 : 0);
+            if (fork3 && (e = hipEventRecord(walk_join_ev, st3)) != hipSuccess) return e;
             k_walk_fixed<<<gridStream, 256, 0, st>>>(S, bs, sc.seg_start, sc.seg_slot, ts, len, sc.pay[0],
                                                      sc.seg_order, cls, sc.marks, table, lim);
             mark("k_walk_fixed");
-            k_walk_fixed_long<<<1024, 256, 0, st>>>(S, bs, sc.seg_start, sc.seg_slot, ts, len, sc.pay[0],
-                                                    sc.seg_order, cls, sc.marks, table, lim);
-            mark("k_walk_fixed_long");
+            if (fork3 && (e = hipStreamWaitEvent(st, walk_join_ev, 0)) != hipSuccess) return e;
         }
     }
     k_fill_last<<<gridTiles, 256, 0, st>>>(sc.marks, bs, sc.tile_last);

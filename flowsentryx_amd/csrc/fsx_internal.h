@@ -214,13 +214,15 @@ struct PipeTiming {
 };
 
 // st: the batch stream. st2 (optional, with fork/join events): the flow features run
-// on it concurrently with the rate limiter (they share only read-only inputs).
+// on it concurrently with the rate limiter (they share only read-only inputs). st3
+// (optional): the fixed-window wave walker beside the thread walker.
 hipError_t launch_verdict_pipeline(const uint8_t *hdr, const uint32_t *len, const uint64_t *ts,
                                    uint32_t n, uint8_t *verdict, Slot *table, TableState *tstate,
                                    BatchState *bs, const Scratch &sc, uint32_t id_gen, const Limits &lim,
                                    bool do_limit, const FlowRequest *flows, const HistBufs &hist,
                                    hipStream_t st, hipStream_t st2, hipEvent_t fork_ev,
-                                   hipEvent_t join_ev, PipeTiming *tm);
+                                   hipEvent_t join_ev, hipStream_t st3, hipEvent_t walk_fork_ev,
+                                   hipEvent_t walk_join_ev, PipeTiming *tm);
 
 // Build-defined limiters (fsx_limiters.hip), after the table lookup/insert of a batch:
 // one verdict mark per sorted position, final per-source state in the table.
