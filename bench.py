@@ -63,6 +63,8 @@ def parse_args():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--check", action="store_true", help="verify a prefix against the oracle")
     ap.add_argument("--no-mlp", action="store_true", help="verdicts only (no features/scores)")
+    ap.add_argument("--no-reset", action="store_true",
+                    help="diagnostics: keep the maps between steps (state carries over)")
     ap.add_argument("--chunks", type=int, default=4,
                     help="N>1: sub-batches per step (the replicated blocklist of one filters "
                          "the next)")
@@ -136,7 +138,8 @@ def main():
         plane = ShardedDataPlane(eng)
 
     def step():
-        ctx.reset()
+        if not args.no_reset:
+            ctx.reset()
         if plane is not None:
             plane.reset()
             plane.verdict_batch(d_hdr, d_len, d_ts, n, d_v, bounds=bounds, chunks=chunks)

@@ -50,7 +50,12 @@ struct fsx_ctx {
     float *d_prob = nullptr;
     uint8_t *d_dec = nullptr;
     uint64_t score_cap = 0;
-    uint32_t id_gen = 0;       // generation of the per-batch source-id table
+    uint32_t id_gen = 0;       // batch generation: per-batch id table, born stamps
+    // persistent source index (TableIndex): heads + IPv6 key words, epoch
+    unsigned long long *idx_heads = nullptr;
+    uint32_t *idx_k6 = nullptr;
+    uint32_t idx_epoch = 1;
+    uint32_t pending_born = 0;  // generation of the in-flight limiter batch (rollback)
     // sharding: per (owner, tile) counts of fsx_shard_pack_device, blocklist replica
     uint32_t *d_shard_cnt = nullptr;
     uint64_t shard_cnt_cap = 0;
@@ -201,6 +206,7 @@ void fsx_close(fsx_ctx *c) {
     for (int b = 0; b < 2; ++b) { hipFree(c->hist.t[b]); hipFree(c->hist.l[b]); }
     hipFree(c->hist.tile_cnt); hipFree(c->hist.tile_off); hipFree(c->hist.total);
     hipFree(c->d_shard_cnt); hipFree(c->d_rep);
+    hipFree(c->idx_heads); hipFree(c->idx_k6);
     for (int r = 0; r < kRing; ++r)
         for (int i = 0; i < kMaxEv; ++i) if (c->ev[r][i]) hipEventDestroy(c->ev[r][i]);
     if (c->own_stream) hipStreamDestroy(c->own_stream);
@@ -250,6 +256,10 @@ int fsx_open(fsx_ctx **out, const fsx_config *cfg) {
     if (hipMalloc(&c->d_res, 64) != hipSuccess) return fail(-ENOMEM);
     if (hipMalloc(&c->d_val, 64) != hipSuccess) return fail(-ENOMEM);
     if (hipMemset(c->table, 0, c->slots * sizeof(Slot)) != hipSuccess) return fail(-EIO);
+    if (hipMalloc(&c->idx_heads, c->slots * 8) != hipSuccess) return fail(-ENOMEM);
+    if (hipMalloc(&c->idx_k6, c->slots * 16) != hipSuccess) return fail(-ENOMEM);
+    if (hipMemset(c->idx_heads, 0, c->slots * 8) != hipSuccess) return fail(-EIO);
+    c->idx_epoch = 1;
     if (hipMemset(c->tstate, 0, sizeof(TableState)) != hipSuccess) return fail(-EIO);
     if (hipMemset(c->bs, 0, sizeof(BatchState)) != hipSuccess) return fail(-EIO);
     if (alloc_scratch(c, k.max_batch)) return fail(-ENOMEM);
@@ -287,11 +297,43 @@ int fsx_set_stream(fsx_ctx *c, void *s) {
     return 0;
 }
 
+static TableIndex table_index(const fsx_ctx *c) {
+    return TableIndex{c->idx_heads, c->idx_k6, c->idx_epoch};
+}
+
+// New epoch of the persistent index (every head reads empty); heads are cleared once
+// per 2^16 epochs so a stale cached line can never carry a current epoch.
+static int next_epoch(fsx_ctx *c) {
+    if (++c->idx_epoch == 0x10000u) {
+        HIPCHK(c, hipMemsetAsync(c->idx_heads, 0, c->slots * 8, c->stream));
+        c->idx_epoch = 1;
+    }
+    return 0;
+}
+
+// A limiter batch failed after k_parse inserted its new sources: drop them and
+// re-publish the survivors under a new epoch (no map state changed: every limiter
+// kernel skips a batch whose error flag is set).
+static int rollback_batch(fsx_ctx *c, uint32_t born) {
+    int rc = next_epoch(c);
+    if (rc) return rc;
+    hipError_t e = launch_index_rebuild(c->table, c->lim, table_index(c), born, c->stream);
+    if (e != hipSuccess) return set_err(c, -EIO, "index rebuild: %s", hipGetErrorString(e));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return 0;
+}
+
 static int check_batch(fsx_ctx *c) {
     if (!c->pending) return 0;
     c->pending = false;
+    const uint32_t born = c->pending_born;
+    c->pending_born = 0;
     BatchState h;
     HIPCHK(c, hipMemcpy(&h, c->bs, sizeof(h), hipMemcpyDeviceToHost));
+    if (h.err && born) {
+        const int rc = rollback_batch(c, born);
+        if (rc) return rc;
+    }
     if (h.err & ERR_TABLE_FULL)
         return set_err(c, -ENOSPC, "map full: more than max_entries=%llu source IPs",
                        (unsigned long long)c->cfg.max_entries);
@@ -377,13 +419,15 @@ static int run_batch(fsx_ctx *c, const uint8_t *d_hdr, const uint32_t *d_len, co
         c->id_gen = 1;
     }
     hipError_t e = launch_verdict_pipeline(d_hdr, d_len, d_ts, (uint32_t)n, d_verdict, c->table,
-                                           c->tstate, c->bs, c->sc, c->id_gen, c->lim, do_limit, fr,
+                                           c->tstate, c->bs, c->sc, c->id_gen, table_index(c), c->lim,
+                                           do_limit, fr,
                                            c->hist, c->stream, fork_flows() ? c->aux_stream : nullptr,
                                            c->fork_ev, c->join_ev, fork_flows() ? c->walk_stream : nullptr,
                                            c->walk_fork_ev, c->walk_join_ev, tm);
     if (tm) c->ev_used[c->ring_n++] = tm->used;
-    if (e != hipSuccess) return set_err(c, -EIO, "pipeline launch: %s", hipGetErrorString(e));
     c->pending = true;
+    c->pending_born = do_limit && n ? c->id_gen : 0;
+    if (e != hipSuccess) return set_err(c, -EIO, "pipeline launch: %s", hipGetErrorString(e));
     return 0;
 }
 
@@ -489,7 +533,7 @@ static int map_op(fsx_ctx *c, int op, int map_id, const void *key, const void *v
     uint64_t v[3] = {0, 0, 0};
     const size_t vlen = map_vlen(map_id);
     if (op == 1) memcpy(v, value, vlen);
-    hipError_t e = launch_map_op(c->table, c->tstate, c->lim, op, map_id, k, v, flags, c->d_res,
+    hipError_t e = launch_map_op(c->table, c->tstate, c->lim, table_index(c), op, map_id, k, v, flags, c->d_res,
                                  c->d_val, c->stream);
     if (e != hipSuccess) return set_err(c, -EIO, "map op: %s", hipGetErrorString(e));
     int32_t res = 0;
@@ -563,9 +607,10 @@ int fsx_reset(fsx_ctx *c) {
     if (!c) return -EINVAL;
     int rc = sel(c);
     if (rc) return rc;
+    c->pending_born = 0;   // the whole table is wiped: no rollback of a pending batch
     HIPCHK(c, hipMemsetAsync(c->table, 0, c->slots * sizeof(Slot), c->stream));
     HIPCHK(c, hipMemsetAsync(c->tstate, 0, sizeof(TableState), c->stream));
-    return 0;
+    return next_epoch(c);   // every index head reads empty
 }
 
 // ------------------------------------------------------------------ scoring
@@ -696,6 +741,7 @@ int fsx_shard_pack_device(fsx_ctx *c, const uint8_t *d_hdr, const uint32_t *d_le
     const uint64_t need = (uint64_t)G * (n / 4096 + 1);
     if (need > c->shard_cnt_cap) {
         hipFree(c->d_shard_cnt); hipFree(c->d_rep);
+    hipFree(c->idx_heads); hipFree(c->idx_k6);
         c->d_shard_cnt = nullptr;
         c->shard_cnt_cap = 0;
         HIPCHK(c, hipMalloc(&c->d_shard_cnt, need * 4));

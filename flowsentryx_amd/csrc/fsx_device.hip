@@ -8,7 +8,7 @@
 //   k_v6_mixed/fixup exact separation of IPv6 hash collisions (IPv4 keys are a
 //                    bijection of the address and never collide)
 //   k_heads_*        ordered compaction of segment starts
-//   k_lookup/insert  map state of every source IP (src/fsx_kern.c:56-94)
+//   k_batch_check    new sources must fit max_entries (else the batch is rolled back)
 //   k_walk_fixed     the fixed-window limiter + blacklist of src/fsx_kern.c:150-346
 //                    evaluated per segment by epoch jumps (binary searches on the
 //                    segment's timestamps), writing verdict change marks
@@ -51,7 +51,6 @@ namespace fsx {
 // XCDs' L2s are not coherent with each other, so every head and IPv6 key word is read
 // with an agent-scope (coherent) load; a stale line would otherwise force a CAS on
 // every packet of a hot source until it is evicted.
-constexpr uint64_t kIdSeed = 0x1D5EED0F5A11ull;
 constexpr uint64_t kIdBusy = 1, kIdReady = 2;
 constexpr uint32_t kIdSpin = 1u << 22;
 
@@ -63,19 +62,23 @@ struct IdTable {
     unsigned long long *head;   // [slots]
     uint32_t *k6;               // [slots][4]: IPv6 key words 1..3
     uint64_t mask;
-    uint32_t gen;
-    uint32_t v6_start;   // FSX_FLAG_TEST_V6_COLLIDE: every IPv6 key probes from here
+    uint64_t seed;              // probe_start() seed (the table's, for the persistent index)
+    uint32_t gen;               // generation (per batch) or epoch (persistent index)
+    uint32_t test_flags;
+    Slot *slots;                // persistent index: a new source also gets its Slot here
+    uint32_t born;              // ... stamped with this batch generation (rollback)
+    uint32_t coherent;          // first probe with an agent-scope load (A/B: FSX_ID_COHERENT)
 };
 
 __device__ __forceinline__ uint64_t id_start(const IdTable &T, uint32_t tag, const uint32_t k[4]) {
-    return (tag == 2 && T.v6_start != 0xFFFFFFFFu) ? T.v6_start : (slot_hash(tag, k, kIdSeed) & T.mask);
+    return probe_start(tag, k, T.seed, T.mask, T.test_flags);
 }
 
-// Slot of (tag, key), inserted if absent; kNoSlot when the table is full or a
-// publication never completes (reported as a full table). h = id_start(...), hint0 =
-// a plain load of T.head[h] issued earlier (the parse loop issues it one tile ahead).
+// Slot of (tag, key), inserted if absent (*fresh = true); kNoSlot when the table is full
+// or a publication never completes (reported as a full table). h = id_start(...),
+// hint0 = a plain load of T.head[h] issued earlier.
 __device__ __forceinline__ uint32_t id_resolve(const IdTable &T, uint32_t tag, const uint32_t k[4],
-                                               uint64_t h, uint64_t hint0) {
+                                               uint64_t h, uint64_t hint0, bool *fresh) {
     const uint64_t ready = id_head(T.gen, kIdReady, tag, k[0]);
     for (uint64_t probes = 0; probes <= T.mask; ++probes, h = (h + 1) & T.mask) {
         unsigned long long *hp = T.head + h;
@@ -85,6 +88,14 @@ __device__ __forceinline__ uint32_t id_resolve(const IdTable &T, uint32_t tag, c
                 const uint64_t want = tag == 2 ? id_head(T.gen, kIdBusy, tag, k[0]) : ready;
                 const uint64_t prev = atomicCAS(hp, (unsigned long long)cur, (unsigned long long)want);
                 if (prev == cur) {
+                    *fresh = true;
+                    if (T.slots) {   // a new source of the persistent index: its map state
+                        Slot &sl = T.slots[h];
+                        sl.flags = T.born << kBornShift;
+                        sl.key[0] = k[0]; sl.key[1] = k[1]; sl.key[2] = k[2]; sl.key[3] = k[3];
+                        sl.pps = sl.bps = sl.tt = sl.till = sl.aux = 0;
+                        sl.tag = tag;
+                    }
                     if (tag == 2) {
                         uint32_t *kw = T.k6 + h * 4;
                         __hip_atomic_store(kw + 0, k[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -142,7 +153,7 @@ __global__ __launch_bounds__(256) void k_parse(const uint8_t *__restrict__ hdr,
     for (int d = 0; d < 4; ++d) s_t0[d][threadIdx.x] = 0;
     __syncthreads();
     uint32_t *rec = s_rec[w];
-    uint32_t any6 = 0, nonmono = 0, maxlen = 0;
+    uint32_t any6 = 0, nonmono = 0, maxlen = 0, nfresh = 0;
     uint64_t maxts = 0, inv_mints = 0;  // ~min ts, max-reduced
     // a block owns whole 4096-record sort tiles (so it can emit pass 0's per-tile digit
     // counts: no k_tile_hist for pass 0); wave w parses records [w*1024, +1024) of the
@@ -232,17 +243,22 @@ __global__ __launch_bounds__(256) void k_parse(const uint8_t *__restrict__ hdr,
         uint64_t h = 0, hint = 0;
         if (ip) {
             h = id_start(idt, tag, k);
-            hint = idt.head[h];   // a hint: the CAS decides when it shows an older generation
+            // a hint: the CAS decides when it shows an older generation (coherent=1 reads
+            // past the XCD's L2, which may still hold the head of an older epoch)
+            hint = idt.coherent ? __hip_atomic_load(idt.head + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                : idt.head[h];
         }
 #pragma unroll
         for (int q = 0; q < 4; ++q) hv[q] = hn[q];
         Lc = Ln; Tc = Tn; Pc = Pn;
         uint64_t out = kSentinel;
+        bool fresh = false;
         if (ip) {
-            const uint32_t id = id_resolve(idt, tag, k, h, hint);
+            const uint32_t id = id_resolve(idt, tag, k, h, hint, &fresh);
             if (id == kNoSlot) atomicOr(&bs->err, ERR_TABLE_FULL);
             out = ((uint64_t)(id & idt.mask) << 32) | ((uint64_t)(tag - 1u) << 31) | i;
         }
+        nfresh += (uint32_t)__popcll(__ballot(fresh));   // new sources (persistent index)
         if (live) {
             packed[i] = out;
             // IP packets default to PASS here (coalesced); the fill pass writes only
@@ -282,6 +298,8 @@ __global__ __launch_bounds__(256) void k_parse(const uint8_t *__restrict__ hdr,
             if (c) atomicAdd(&ghist[dg * 256 + threadIdx.x], c);
         }
     }
+    // one add per wave: a per-step add to one counter serializes at the memory side
+    if (lane == 0 && nfresh && idt.slots) atomicAdd(&bs->n_new, nfresh);
     any6 = __ballot(any6 != 0) ? 1u : 0u;
     nonmono = __ballot(nonmono != 0) ? 1u : 0u;
     maxlen = wave_max(maxlen);
@@ -706,7 +724,9 @@ __global__ __launch_bounds__(1024) void k_scan_tiles_u32(uint32_t *__restrict__ 
 
 __global__ __launch_bounds__(256) void k_heads_write(BatchState *bs, const uint8_t *__restrict__ headf,
                                                      const uint32_t *__restrict__ tile_off,
-                                                     uint32_t *__restrict__ seg_start) {
+                                                     uint32_t *__restrict__ seg_start,
+                                                     const uint64_t *__restrict__ S,
+                                                     uint32_t *__restrict__ seg_slot) {
     __shared__ uint32_t s_tmp[4];
     const uint32_t M = bs->n_valid;
     const uint32_t ntiles = (M + kTile - 1) / kTile;
@@ -725,103 +745,102 @@ __global__ __launch_bounds__(256) void k_heads_write(BatchState *bs, const uint8
         uint32_t off = tile_off[t] + block256_excl(cnt, s_tmp, nullptr);
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
-            if ((f[k >> 2] >> (8 * (k & 3))) & 1u) seg_start[off++] = p0 + k;
+            if ((f[k >> 2] >> (8 * (k & 3))) & 1u) {
+                seg_start[off] = p0 + k;
+                if (seg_slot) seg_slot[off] = (uint32_t)(S[p0 + k] >> 32);   // id = table slot
+                ++off;
+            }
         }
     }
 }
 
 // ------------------------------------------------------------------ table lookup / insert
-__device__ __forceinline__ uint32_t seg_key(const uint64_t *S, const uint32_t *seg_start, uint32_t g,
-                                            const uint8_t *hdr, uint32_t salt, uint32_t k[4]) {
-    return key_of(S[seg_start[g]], hdr, salt, k);
-}
 
 __device__ __forceinline__ bool slot_key_eq(const Slot &s, uint32_t tag, const uint32_t k[4]) {
     return s.tag == tag && s.key[0] == k[0] && s.key[1] == k[1] && s.key[2] == k[2] &&
            s.key[3] == k[3];
 }
 
-__device__ __forceinline__ uint32_t table_find(const Slot *table, uint64_t mask, uint32_t tag,
-                                               const uint32_t k[4], uint64_t seed) {
-    uint64_t i = slot_hash(tag, k, seed) & mask;
-    for (uint64_t probes = 0; probes <= mask; ++probes) {
+__device__ __forceinline__ uint32_t table_find(const Slot *table, const Limits &lim, uint32_t tag,
+                                               const uint32_t k[4]) {
+    uint64_t i = probe_start(tag, k, lim.seed, lim.table_mask, lim.test_flags);
+    for (uint64_t probes = 0; probes <= lim.table_mask; ++probes) {
         const uint32_t t = table[i].tag;
         if (t == 0) return kNoSlot;
         if (t == tag && slot_key_eq(table[i], tag, k)) return (uint32_t)i;
-        i = (i + 1) & mask;
+        i = (i + 1) & lim.table_mask;
     }
     return kNoSlot;
 }
 
-// Claim an empty slot for a key known to be absent; its key has exactly one inserter.
-__device__ __forceinline__ uint32_t table_claim(Slot *table, uint64_t mask, uint32_t tag,
-                                                const uint32_t k[4], uint64_t seed) {
-    uint64_t i = slot_hash(tag, k, seed) & mask;
-    for (uint64_t probes = 0; probes <= mask; ++probes) {
-        if (table[i].tag == 0 && atomicCAS(&table[i].tag, 0u, tag) == 0u) {
+// Publish slot i of (tag, key) in the persistent index (single writer, between batches).
+__device__ __forceinline__ void index_publish(const TableIndex &X, uint64_t i, uint32_t tag,
+                                              const uint32_t k[4]) {
+    if (tag == 2) {
+        X.k6[i * 4 + 0] = k[1]; X.k6[i * 4 + 1] = k[2]; X.k6[i * 4 + 2] = k[3];
+    }
+    __threadfence();
+    X.heads[i] = id_head(X.epoch, kIdReady, tag, k[0]);
+}
+
+// Claim an empty slot for a key known to be absent (map ops: one thread, no batch in
+// flight) and publish it in the index.
+__device__ __forceinline__ uint32_t table_claim(Slot *table, const Limits &lim, const TableIndex &X,
+                                                uint32_t tag, const uint32_t k[4]) {
+    uint64_t i = probe_start(tag, k, lim.seed, lim.table_mask, lim.test_flags);
+    for (uint64_t probes = 0; probes <= lim.table_mask; ++probes) {
+        if (table[i].tag == 0) {
             Slot &s = table[i];
+            s.tag = tag;
             s.flags = 0;
             s.key[0] = k[0]; s.key[1] = k[1]; s.key[2] = k[2]; s.key[3] = k[3];
             s.pps = s.bps = s.tt = s.till = s.aux = 0;
+            index_publish(X, i, tag, k);
             return (uint32_t)i;
         }
-        i = (i + 1) & mask;
+        i = (i + 1) & lim.table_mask;
     }
     return kNoSlot;
 }
 
-__global__ __launch_bounds__(256) void k_lookup(const uint64_t *__restrict__ S, BatchState *bs,
-                                                const uint32_t *__restrict__ seg_start,
-                                                uint32_t *__restrict__ seg_slot,
-                                                const uint8_t *__restrict__ hdr, const Slot *table,
-                                                Limits lim) {
-    const uint32_t nseg = bs->nseg;
-    uint32_t nnew = 0;
-    for (uint32_t g = blockIdx.x * 256u + threadIdx.x; g < nseg; g += gridDim.x * 256u) {
-        uint32_t k[4];
-        const uint32_t tag = seg_key(S, seg_start, g, hdr, lim.salt32, k);
-        const uint32_t s = table_find(table, lim.table_mask, tag, k, lim.seed);
-        seg_slot[g] = s;
-        nnew += s == kNoSlot;
-    }
-    nnew = wave_incl_sum(nnew);
-    if (lane_id() == 63 && nnew) atomicAdd(&bs->n_new, nnew);
-}
-
-__global__ __launch_bounds__(256) void k_insert(const uint64_t *__restrict__ S, BatchState *bs,
-                                                const uint32_t *__restrict__ seg_start,
-                                                uint32_t *__restrict__ seg_slot,
-                                                const uint8_t *__restrict__ hdr, Slot *table,
-                                                TableState *tstate, Limits lim) {
-    if (bs->err) return;    // e.g. the id table overflowed: no state changes
-    // sliding window: the carried logs plus every packet of this batch must fit the
-    // history buffer (conservative; checked before any state changes)
+// After k_parse (one thread): the batch's new sources must fit max_entries, and with the
+// sliding window its carried logs plus packets the history buffer — checked before any
+// limiter state changes; a failing batch is rolled back by the host (fsx_api.hip).
+__global__ void k_batch_check(BatchState *bs, TableState *tstate, Limits lim) {
+    if (bs->err) return;
+    if (tstate->count + bs->n_new > lim.max_entries) { bs->err |= ERR_TABLE_FULL; return; }
     if (lim.limiter == 1 && tstate->hist_total + bs->n_valid > lim.hist_cap) {
-        if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(&bs->err, ERR_HIST_FULL);
+        bs->err |= ERR_HIST_FULL;
         return;
     }
-    const uint32_t nnew = bs->n_new;
-    if (nnew == 0) return;
-    // capacity for the whole batch is checked once: a batch that would overflow the
-    // maps is rejected before any state changes (-ENOSPC at the boundary)
-    if (tstate->count + nnew > lim.max_entries) {
-        if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(&bs->err, ERR_TABLE_FULL);
-        return;
-    }
-    const uint32_t nseg = bs->nseg;
-    for (uint32_t g = blockIdx.x * 256u + threadIdx.x; g < nseg; g += gridDim.x * 256u) {
-        if (seg_slot[g] != kNoSlot) continue;
-        uint32_t k[4];
-        const uint32_t tag = seg_key(S, seg_start, g, hdr, lim.salt32, k);
-        const uint32_t s = table_claim(table, lim.table_mask, tag, k, lim.seed);
-        if (s == kNoSlot) atomicOr(&bs->err, ERR_PROBE);
-        seg_slot[g] = s;
+    tstate->count += bs->n_new;
+}
+
+// Rollback / epoch change: re-publish every live slot under the new epoch; slots born in
+// the failed batch `born` (nonzero) are emptied instead.
+__global__ __launch_bounds__(256) void k_index_rebuild(Slot *table, Limits lim, TableIndex X, uint32_t born) {
+    for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i <= lim.table_mask;
+         i += (uint64_t)gridDim.x * 256u) {
+        Slot &s = table[i];
+        if (s.tag == 0) continue;
+        if (born && (s.flags >> kBornShift) == born) {
+            s.tag = 0;
+            s.flags = 0;
+            continue;
+        }
+        if (s.tag == 2) {
+            X.k6[i * 4 + 0] = s.key[1]; X.k6[i * 4 + 1] = s.key[2]; X.k6[i * 4 + 2] = s.key[3];
+        }
+        X.heads[i] = id_head(X.epoch, kIdReady, s.tag, s.key[0]);
     }
 }
 
-// Runs after k_insert: account the inserted entries (one thread).
-__global__ void k_count_inserted(BatchState *bs, TableState *tstate) {
-    if (bs->err == 0) tstate->count += bs->n_new;
+hipError_t launch_index_rebuild(Slot *table, const Limits &lim, const TableIndex &X, uint32_t born,
+                                hipStream_t st) {
+    (void)hipGetLastError();   // a stale error of another caller is not ours
+    const uint32_t grid = (uint32_t)std::min<uint64_t>(4096, (lim.table_mask + 256) / 256);
+    k_index_rebuild<<<grid, 256, 0, st>>>(table, lim, X, born);
+    return hipGetLastError();
 }
 
 // ------------------------------------------------------------------ fixed-window walker
@@ -970,7 +989,8 @@ __device__ __forceinline__ FwState load_state(const Slot &sl) {
                    sl.tt, sl.till};
 }
 __device__ __forceinline__ void store_state(Slot &sl, const FwState &s) {
-    sl.flags = (sl.flags & ~(SLOT_HAS_ST | SLOT_HAS_BL)) | (s.has_st ? SLOT_HAS_ST : 0u) |
+    // (also clears the born stamp: the batch that inserted the slot got this far)
+    sl.flags = (sl.flags & kFlagBits & ~(SLOT_HAS_ST | SLOT_HAS_BL)) | (s.has_st ? SLOT_HAS_ST : 0u) |
                (s.has_bl ? SLOT_HAS_BL : 0u);
     sl.pps = s.pps; sl.bps = s.bps; sl.tt = s.tt; sl.till = s.till;
 }
@@ -1303,7 +1323,8 @@ static uint32_t next_generation() {
 hipError_t launch_verdict_pipeline(const uint8_t *hdr, const uint32_t *len, const uint64_t *ts,
                                    uint32_t n, uint8_t *verdict, Slot *table, TableState *tstate,
                                    BatchState *bs, const Scratch &sc_in, uint32_t id_gen,
-                                   const Limits &lim, bool do_limit, const FlowRequest *flows,
+                                   const TableIndex &X, const Limits &lim, bool do_limit,
+                                   const FlowRequest *flows,
                                    const HistBufs &hist, hipStream_t st, hipStream_t st2,
                                    hipEvent_t fork_ev, hipEvent_t join_ev, hipStream_t st3,
                                    hipEvent_t walk_fork_ev, hipEvent_t walk_join_ev, PipeTiming *tm) {
@@ -1333,12 +1354,13 @@ hipError_t launch_verdict_pipeline(const uint8_t *hdr, const uint32_t *len, cons
     const bool onesweep = (lim.test_flags & 2u) != 0;
     if ((e = hipMemsetAsync(sc.sort_ctl, 0, kSortCtlWords * 4, st)) != hipSuccess) return e;
     mark("start");
-    // test hook: every IPv6 source probes the id table from IPv4 10.0.0.1's slot
-    const uint32_t k10[4] = {0x0100000Au, 0, 0, 0};
-    const IdTable idt{reinterpret_cast<unsigned long long *>(sc.id_tab),
-                      sc.id_tab + 2 * (lim.table_mask + 1), lim.table_mask, id_gen,
-                      (lim.test_flags & 1u) ? (uint32_t)(slot_hash(1u, k10, kIdSeed) & lim.table_mask)
-                                            : 0xFFFFFFFFu};
+    // with the limiter, sources are found / inserted in the persistent index (sort id =
+    // table slot); flow features alone use a per-batch id table and touch no map state
+    static const uint32_t coherent = getenv("FSX_ID_COHERENT") ? 1u : 0u;
+    const IdTable idt = do_limit
+        ? IdTable{X.heads, X.k6, lim.table_mask, lim.seed, X.epoch, lim.test_flags, table, id_gen, coherent}
+        : IdTable{reinterpret_cast<unsigned long long *>(sc.id_tab), sc.id_tab + 2 * (lim.table_mask + 1),
+                  lim.table_mask, lim.seed, id_gen, lim.test_flags, nullptr, 0, coherent};
     const uint32_t ntiles = std::max<uint32_t>(1, cdiv(n, kSortTile));
     const uint32_t tcap = (uint32_t)(sc.cap / kSortTile + 2);
     // source ids have log2(slots) bits: ceil(bits / 8) LSD passes of equal digits of at
@@ -1354,6 +1376,7 @@ hipError_t launch_verdict_pipeline(const uint8_t *hdr, const uint32_t *len, cons
         dbits);
     mark("k_parse");
     k_hist_prep<<<1, 256, 0, st>>>(sc.sort_ctl, sc.gbase, bs);
+    if (do_limit) k_batch_check<<<1, 1, 0, st>>>(bs, tstate, lim);
     const uint32_t gen0 = onesweep ? next_generation() : 0u;
     for (int pass = 0; pass < npass; ++pass) {
         const uint64_t *in = sc.packed[pass & 1];
@@ -1386,7 +1409,8 @@ hipError_t launch_verdict_pipeline(const uint8_t *hdr, const uint32_t *len, cons
     k_heads_count<<<gridTiles, 256, 0, st>>>(S, bs, hdr, sc.headf, sc.tile_aux, sc.sub_cnt);
     mark("k_heads_count");
     k_scan_tiles_u32<<<1, 1024, 0, st>>>(sc.tile_aux, bs, sc.seg_start);
-    k_heads_write<<<gridTiles, 256, 0, st>>>(bs, sc.headf, sc.tile_aux, sc.seg_start);
+    k_heads_write<<<gridTiles, 256, 0, st>>>(bs, sc.headf, sc.tile_aux, sc.seg_start, S,
+                                             do_limit ? sc.seg_slot : nullptr);
     mark("k_heads_write");
     const bool fork = flows && do_limit && st2 && fork_ev && join_ev;
     if (flows) {
@@ -1406,11 +1430,6 @@ hipError_t launch_verdict_pipeline(const uint8_t *hdr, const uint32_t *len, cons
         if (fork && (e = hipEventRecord(join_ev, st2)) != hipSuccess) return e;
     }
     if (!do_limit) return hipGetLastError();
-    k_lookup<<<gridStream, 256, 0, st>>>(S, bs, sc.seg_start, sc.seg_slot, hdr, table, lim);
-    mark("k_lookup");
-    k_insert<<<gridStream, 256, 0, st>>>(S, bs, sc.seg_start, sc.seg_slot, hdr, table, tstate, lim);
-    k_count_inserted<<<1, 1, 0, st>>>(bs, tstate);
-    mark("k_insert");
     if (lim.limiter == 2) {   // FSX_LIMIT_TOKEN_BUCKET
         if ((e = launch_token_bucket(S, ts, len, bs, sc, table, lim, n, st)) != hipSuccess) return e;
         mark("k_token_bucket");
@@ -1461,14 +1480,14 @@ __host__ __device__ inline uint32_t map_bit(int map_id) {
     return (map_id == 1 || map_id == 2) ? SLOT_HAS_ST : (map_id == 5 || map_id == 6) ? SLOT_HAS_TB : SLOT_HAS_BL;
 }
 
-__global__ void k_map_op(Slot *table, TableState *tstate, Limits lim, int op, int map_id,
+__global__ void k_map_op(Slot *table, TableState *tstate, Limits lim, TableIndex X, int op, int map_id,
                          uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3, uint64_t v0,
                          uint64_t v1, uint64_t v2, uint64_t flags, int32_t *res, uint64_t *outv) {
     if (threadIdx.x || blockIdx.x) return;
     const uint32_t k[4] = {k0, k1, k2, k3};
     const uint32_t tag = map_tag(map_id);
     const uint32_t bit = map_bit(map_id);
-    uint32_t s = table_find(table, lim.table_mask, tag, k, lim.seed);
+    uint32_t s = table_find(table, lim, tag, k);
     const bool present = s != kNoSlot && (table[s].flags & bit);
     if (op == 0) {
         if (!present) { *res = -2; return; }
@@ -1488,7 +1507,7 @@ __global__ void k_map_op(Slot *table, TableState *tstate, Limits lim, int op, in
     if (flags == 2 && !present) { *res = -2; return; }
     if (s == kNoSlot) {
         if (tstate->count >= lim.max_entries) { *res = -28; return; }
-        s = table_claim(table, lim.table_mask, tag, k, lim.seed);
+        s = table_claim(table, lim, X, tag, k);
         if (s == kNoSlot) { *res = -28; return; }
         tstate->count += 1;
     }
@@ -1499,11 +1518,11 @@ __global__ void k_map_op(Slot *table, TableState *tstate, Limits lim, int op, in
     *res = 0;
 }
 
-hipError_t launch_map_op(Slot *table, TableState *tstate, const Limits &lim, int op, int map_id,
-                         const uint32_t key[4], const uint64_t val[3], uint64_t flags,
+hipError_t launch_map_op(Slot *table, TableState *tstate, const Limits &lim, const TableIndex &X, int op,
+                         int map_id, const uint32_t key[4], const uint64_t val[3], uint64_t flags,
                          int32_t *d_result, uint64_t *d_val, hipStream_t st) {
     (void)hipGetLastError();   // a stale error of another caller is not ours
-    k_map_op<<<1, 64, 0, st>>>(table, tstate, lim, op, map_id, key[0], key[1], key[2], key[3],
+    k_map_op<<<1, 64, 0, st>>>(table, tstate, lim, X, op, map_id, key[0], key[1], key[2], key[3],
                                val[0], val[1], val[2], flags, d_result, d_val);
     return hipGetLastError();
 }

@@ -35,6 +35,21 @@ enum : uint32_t {
 };
 
 enum : uint32_t { SLOT_HAS_ST = 1u, SLOT_HAS_BL = 2u, SLOT_HAS_TB = 4u };
+// Slot.flags bits 16..31: the batch generation that inserted the slot (0 once a batch
+// has walked it, or for map-op inserts); a failed batch's inserts are rolled back.
+constexpr uint32_t kBornShift = 16;
+constexpr uint32_t kFlagBits = (1u << kBornShift) - 1u;
+
+// Persistent source index: one 8-byte head per table slot {epoch 16 | state 8 | tag 8 |
+// key word 0} plus IPv6 key words 1..3, mirroring Slot.tag/key. k_parse probes the
+// dense heads (not the 64-byte slots) and inserts new sources, so a source's sort id IS
+// its table slot. The epoch changes on fsx_reset and after a rolled-back batch, which
+// empties every head at once (no clearing; stale cached lines read as empty).
+struct TableIndex {
+    unsigned long long *heads;
+    uint32_t *k6;          // [slots][4]: IPv6 key words 1..3
+    uint32_t epoch;
+};
 
 // One source IP (either family). tag: 0 empty, 1 IPv4, 2 IPv6.
 struct alignas(64) Slot {
@@ -155,6 +170,18 @@ __host__ __device__ inline uint64_t slot_hash(uint32_t tag, const uint32_t k[4],
     return h;
 }
 
+// First probe slot of a source in the table (shared by k_parse, the map ops and the
+// index rebuild). Test hook FSX_FLAG_TEST_V6_COLLIDE: every IPv6 source starts at IPv4
+// 10.0.0.1's slot.
+__host__ __device__ inline uint64_t probe_start(uint32_t tag, const uint32_t k[4], uint64_t seed,
+                                                uint64_t mask, uint32_t test_flags) {
+    if (tag == 2 && (test_flags & 1u)) {
+        const uint32_t k10[4] = {0x0100000Au, 0, 0, 0};
+        return slot_hash(1u, k10, seed) & mask;
+    }
+    return slot_hash(tag, k, seed) & mask;
+}
+
 // packed sort word: source id << 32 | family << 31 | arrival index (n <= 2^31 - 1); the
 // source id is the source's slot in the per-batch id table (k_parse), so equal ids <=>
 // equal (family, address) and the sort needs only log2(slots) key bits
@@ -218,8 +245,9 @@ struct PipeTiming {
 // (optional): the fixed-window wave walker beside the thread walker.
 hipError_t launch_verdict_pipeline(const uint8_t *hdr, const uint32_t *len, const uint64_t *ts,
                                    uint32_t n, uint8_t *verdict, Slot *table, TableState *tstate,
-                                   BatchState *bs, const Scratch &sc, uint32_t id_gen, const Limits &lim,
-                                   bool do_limit, const FlowRequest *flows, const HistBufs &hist,
+                                   BatchState *bs, const Scratch &sc, uint32_t id_gen,
+                                   const TableIndex &X, const Limits &lim, bool do_limit,
+                                   const FlowRequest *flows, const HistBufs &hist,
                                    hipStream_t st, hipStream_t st2, hipEvent_t fork_ev,
                                    hipEvent_t join_ev, hipStream_t st3, hipEvent_t walk_fork_ev,
                                    hipEvent_t walk_join_ev, PipeTiming *tm);
@@ -247,9 +275,13 @@ size_t flow_acc_bytes();
 ScoreParams make_score_params(const int8_t w[8], float inv_in, int32_t zp_in, float bias_over_ats,
                               float mult, int32_t zp_out, const uint8_t lut[256]);
 
-hipError_t launch_map_op(Slot *table, TableState *tstate, const Limits &lim, int op, int map_id,
-                         const uint32_t key[4], const uint64_t val[3], uint64_t flags,
+hipError_t launch_map_op(Slot *table, TableState *tstate, const Limits &lim, const TableIndex &X, int op,
+                         int map_id, const uint32_t key[4], const uint64_t val[3], uint64_t flags,
                          int32_t *d_result, uint64_t *d_val, hipStream_t st);
+// Re-publish the live slots under X.epoch; slots born in batch `born` (nonzero) are
+// emptied (rollback of a failed batch).
+hipError_t launch_index_rebuild(Slot *table, const Limits &lim, const TableIndex &X, uint32_t born,
+                                hipStream_t st);
 
 hipError_t launch_map_dump(const Slot *table, const Limits &lim, int map_id, uint8_t *d_keys,
                            uint64_t *d_vals, uint64_t cap, unsigned long long *d_count,

@@ -89,14 +89,15 @@ __device__ __forceinline__ void tb_seg_body(const SV &sv, BatchState *bs, const 
     for (uint32_t g = blockIdx.x * 256u + threadIdx.x; g < nseg; g += gridDim.x * 256u) {
         const uint32_t a = seg_start[g], b = seg_start[g + 1];
         Slot &sl = table[seg_slot[g]];
-        uint32_t flags = sl.flags;
+        const uint32_t flags = sl.flags & kFlagBits;   // (drops the born stamp)
         uint32_t j = a;
         if ((flags & SLOT_HAS_BL) && sl.till > 0) {   // src/fsx_kern.c:189
             const uint64_t till = sl.till;
             if (mono) j = gallop_gt(sv, a, b, till);
             else while (j < b && !(sv.t(j) > till)) ++j;
-            if (j < b) sl.flags = flags & ~SLOT_HAS_BL;  // deleted at packet j (:193-204)
         }
+        sl.flags = j < b && (flags & SLOT_HAS_BL) && sl.till > 0 ? flags & ~SLOT_HAS_BL  // deleted at j
+                                                                  : flags;            // (:193-204)
         seg_j[g] = j;
         if (j >= b) continue;
         const uint64_t C = lim.tb_cap;
@@ -366,7 +367,7 @@ __device__ __forceinline__ SwState sw_load(const Slot &sl) {
     return SwState{(sl.flags & SLOT_HAS_ST) != 0, (sl.flags & SLOT_HAS_BL) != 0, sl.pps, sl.bps, sl.tt, sl.till};
 }
 __device__ __forceinline__ void sw_store(Slot &sl, const SwState &s, uint32_t g) {
-    sl.flags = (sl.flags & ~(SLOT_HAS_ST | SLOT_HAS_BL)) | (s.has_st ? SLOT_HAS_ST : 0u) |
+    sl.flags = (sl.flags & kFlagBits & ~(SLOT_HAS_ST | SLOT_HAS_BL)) | (s.has_st ? SLOT_HAS_ST : 0u) |
                (s.has_bl ? SLOT_HAS_BL : 0u);
     sl.pps = s.pps; sl.bps = s.bps; sl.tt = s.tt; sl.till = s.till;
     sl.aux = kAuxWalked | g;
