@@ -209,6 +209,35 @@ def test_table_full_reports_enospc(native):
         assert e.value.code == -errno.ENOSPC
 
 
+@pytest.mark.parametrize("limiter", [0, 1, 2])
+def test_failed_batch_rolls_back(native, oracle, limiter):
+    """A batch that would exceed max_entries changes nothing (its new sources are rolled
+    back out of the source index): the next batches equal an oracle that never saw it."""
+    from flowsentryx_amd import lib, synth
+    rng = np.random.default_rng(60 + limiter)
+    cfg = dict(pps_threshold=5, window_ns=100_000, block_ns=300_000, max_entries=300, limiter=limiter,
+               tb_rate=300_000, tb_burst=4)
+    h1, l1, t1 = rand_stream(rng, 3000, 120, dt_max=200)
+    t1 = t1 + np.uint64(10**6)
+    big = synth.records([synth.frame_ipv4_udp(bytes([10, 77, i // 256, i % 256]), 90) for i in range(400)])
+    tb = t1[-1] + np.arange(1, 401, dtype=np.uint64)
+    h3, l3, t3 = rand_stream(rng, 3000, 120, dt_max=200)
+    t3 = t3 + tb[-1]
+    okw = {k: v for k, v in cfg.items() if k != "max_entries"}
+    o = oracle.Oracle(max_entries=1 << 12, **okw)
+    with gpu_ctx(native, max_batch=4096, **cfg) as c:
+        assert np.array_equal(c.verdict_batch(h1, l1, t1), o.batch(h1, l1, t1))
+        before = {m: c.map_dump(m) for m in (1, 2, 3, 4, 5, 6)}
+        with pytest.raises(lib.FsxError) as e:
+            c.verdict_batch(big, np.full(400, 90, np.uint32), tb)
+        assert e.value.code == -errno.ENOSPC
+        assert {m: c.map_dump(m) for m in (1, 2, 3, 4, 5, 6)} == before
+        assert np.array_equal(c.verdict_batch(h3, l3, t3), o.batch(h3, l3, t3))
+        assert c.stats() == o.stats()
+        for m in ((1, 2, 3, 4) if limiter < 2 else (3, 4, 5, 6)):
+            assert c.map_dump(m) == o.map_dump(m), m
+
+
 def test_map_syscalls(native):
     from flowsentryx_amd import lib
     with gpu_ctx(native, max_entries=64, max_batch=64) as c:
