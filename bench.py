@@ -70,6 +70,8 @@ def parse_args():
                          "the next)")
     ap.add_argument("--dist-backend", default="nccl",
                     help="N>1 collectives: nccl (RCCL over xGMI) or gloo (rehearsal on one GPU)")
+    ap.add_argument("--limiter", choices=["fixed", "sliding", "token"], default="fixed",
+                    help="limiter of the timed main loop (diagnostics; the headline is fixed)")
     ap.add_argument("--limiter-steps", type=int, default=5,
                     help="timed steps of the sliding-window and token-bucket legs (0: skip)")
     return ap.parse_args()
@@ -120,7 +122,9 @@ def main():
     p.duration_ns = p.duration_ns // world
 
     max_entries = max(1024, int(p.n_ips) if p.n_ips else n)
-    ctx = lib.FsxContext(max_batch=n, max_entries=max_entries, device=local)
+    lim_id = {"fixed": lib.LIMIT_FIXED_WINDOW, "sliding": lib.LIMIT_SLIDING_WINDOW,
+              "token": lib.LIMIT_TOKEN_BUCKET}[args.limiter]
+    ctx = lib.FsxContext(max_batch=n, max_entries=max_entries, device=local, limiter=lim_id)
     from flowsentryx_amd import fsx_load
     ctx.load_q8_model(fsx_load.load_weights(ROOT / "tests" / "golden" / "model_weights.json"))
     fcap = max_entries

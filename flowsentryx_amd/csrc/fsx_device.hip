@@ -1342,6 +1342,7 @@ hipError_t launch_verdict_pipeline(const uint8_t *hdr, const uint32_t *len, cons
         last[s_id] = i;
     };
     auto mark = [&](const char *name) { mark_on(name, 0); };
+    const Marker mk{[](void *p, const char *name) { (*static_cast<decltype(mark) *>(p))(name); }, &mark};
     if (tm) tm->used = 0;
     hipError_t e;
     if ((e = hipMemsetAsync(bs, 0, sizeof(BatchState), st)) != hipSuccess) return e;
@@ -1431,8 +1432,7 @@ hipError_t launch_verdict_pipeline(const uint8_t *hdr, const uint32_t *len, cons
     }
     if (!do_limit) return hipGetLastError();
     if (lim.limiter == 2) {   // FSX_LIMIT_TOKEN_BUCKET
-        if ((e = launch_token_bucket(S, ts, len, bs, sc, table, lim, n, st)) != hipSuccess) return e;
-        mark("k_token_bucket");
+        if ((e = launch_token_bucket(S, ts, len, bs, sc, table, lim, n, st, mk)) != hipSuccess) return e;
     } else {
         uint32_t *cls = sc.sort_ctl + 1028;
         k_seg_count<<<kSegBlocks, 256, 0, st>>>(bs, sc.seg_start, sc.hist);
@@ -1440,9 +1440,9 @@ hipError_t launch_verdict_pipeline(const uint8_t *hdr, const uint32_t *len, cons
         k_seg_order<<<kSegBlocks, 256, 0, st>>>(bs, sc.seg_start, sc.hist, sc.seg_order);
         mark("k_seg_order");
         if (lim.limiter == 1) {   // FSX_LIMIT_SLIDING_WINDOW
-            if ((e = launch_sliding_window(S, ts, len, bs, sc, table, tstate, hist, lim, n, st)) != hipSuccess)
+            if ((e = launch_sliding_window(S, ts, len, bs, sc, table, tstate, hist, lim, n, st, mk)) !=
+                hipSuccess)
                 return e;
-            mark("k_sliding_window");
         } else {
             // short and long segments are disjoint: the wave walker runs on its own
             // stream beside the thread walker when a third stream is available

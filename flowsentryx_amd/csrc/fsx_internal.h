@@ -254,13 +254,21 @@ hipError_t launch_verdict_pipeline(const uint8_t *hdr, const uint32_t *len, cons
 
 // Build-defined limiters (fsx_limiters.hip), after the table lookup/insert of a batch:
 // one verdict mark per sorted position, final per-source state in the table.
+// mark(name) closes the timing interval of the kernels just enqueued (may be empty).
+typedef void (*MarkFn)(void *ctx, const char *name);
+struct Marker {
+    MarkFn fn;
+    void *ctx;
+    void operator()(const char *name) const { if (fn) fn(ctx, name); }
+};
+
 hipError_t launch_token_bucket(const uint64_t *S, const uint64_t *ts, const uint32_t *len, BatchState *bs,
                                const Scratch &sc, Slot *table, const Limits &lim, uint32_t n,
-                               hipStream_t st);
+                               hipStream_t st, const Marker &mark);
 
 hipError_t launch_sliding_window(const uint64_t *S, const uint64_t *ts, const uint32_t *len, BatchState *bs,
                                  const Scratch &sc, Slot *table, TableState *tstate, const HistBufs &hb,
-                                 const Limits &lim, uint32_t n, hipStream_t st);
+                                 const Limits &lim, uint32_t n, hipStream_t st, const Marker &mark);
 
 hipError_t launch_pcap_records(const uint8_t *buf, const uint64_t *off, const uint32_t *caplen, uint32_t n,
                                uint8_t *hdr, hipStream_t st);

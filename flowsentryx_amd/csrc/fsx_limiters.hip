@@ -72,9 +72,11 @@ __device__ __forceinline__ CMap cm_shfl_up(const CMap &m, int o) {
 }
 
 // Refill of a gap dt (u64 wraparound of now - last, as the oracle), saturated at 2^61.
-__device__ __forceinline__ int64_t tb_refill(uint64_t dt, uint64_t rate) {
+// dt_sat = 2^61 / rate, hoisted (a 64-bit division is ~100 instructions on CDNA).
+__device__ __forceinline__ uint64_t tb_dt_sat(uint64_t rate) { return rate ? (uint64_t)kTbSat / rate : 0; }
+__device__ __forceinline__ int64_t tb_refill(uint64_t dt, uint64_t rate, uint64_t dt_sat) {
     if (rate == 0) return 0;
-    if (dt > (uint64_t)kTbSat / rate) return kTbSat;
+    if (dt > dt_sat) return kTbSat;
     return (int64_t)(dt * rate);
 }
 
@@ -148,6 +150,7 @@ __device__ __forceinline__ void tb_tile(const SV &sv, uint32_t t, uint32_t M,
     const uint32_t p0 = t * kTile + tid * 16u;
     const int64_t hi = lim.tb_cap >= kTbCost ? (int64_t)(lim.tb_cap - kTbCost) : 0;
     const bool degen = lim.tb_cap < kTbCost;    // C < cost: every counted packet drops
+    const uint64_t dt_sat = tb_dt_sat(lim.tb_rate);
     // head bits of positions p0 .. p0+16 (a position >= M ends the last segment)
     uint32_t hf = 0;
     if (p0 + 17 <= M) {
@@ -164,41 +167,50 @@ __device__ __forceinline__ void tb_tile(const SV &sv, uint32_t t, uint32_t M,
     }
     const uint32_t nh = p0 < M ? (uint32_t)__popc(hf & 0xFFFFu) : 0u;
     const uint32_t hb = tile_off[t] + block256_excl(nh, s_tmp, nullptr);
-    // per-position maps
-    int64_t D[16];
+    // per-position kinds, and the thread's composed map folded on the fly (the apply
+    // pass recomputes the per-position deltas from the 16 timestamps). Blocked / absent
+    // positions are identity maps and skipped; a source's first counted packet is a
+    // constant map.
     uint32_t kind = 0;  // 2 bits per position
-    uint64_t tprev = (p0 > 0 && p0 < M) ? sv.t(p0 - 1) : 0ull;
-    int32_t cg = (int32_t)hb - 1;
-    uint32_t cj = 0;
-    uint64_t cx = 0;
-    if (p0 < M && !(hf & 1u)) { cj = seg_j[cg]; cx = seg_x[cg]; }
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        const uint32_t p = p0 + (uint32_t)k;
-        uint32_t kd = TB_NONE;
-        D[k] = 0;
-        if (p < M) {
-            if ((hf >> k) & 1u) { ++cg; cj = seg_j[cg]; cx = seg_x[cg]; }
-            const uint64_t tp = sv.t(p);
-            if (p < cj) kd = TB_BLOCKED;
-            else if (p == cj) { kd = TB_FIRST; D[k] = (int64_t)cx; }
-            else { kd = TB_NEXT; D[k] = tb_refill(tp - tprev, lim.tb_rate) - (int64_t)kTbCost; }
-            tprev = tp;
-        }
-        kind |= kd << (2 * k);
-    }
-    auto map_of = [&](int k) -> CMap {
-        const uint32_t kd = (kind >> (2 * k)) & 3u;
-        if (kd == TB_FIRST) {
-            const int64_t x = D[k] & (int64_t)~(1ull << 63);
-            return CMap{x, x, 0};
-        }
-        if (kd == TB_NEXT) return degen ? CMap{0, 0, 0} : CMap{0, hi, D[k]};
-        return CMap{0, hi, 0};
+    const uint64_t tprev0 = (p0 > 0 && p0 < M) ? sv.t(p0 - 1) : 0ull;
+    auto delta = [&](uint64_t tp, uint64_t tprev) -> int64_t {
+        return tb_refill(tp - tprev, lim.tb_rate, dt_sat) - (int64_t)kTbCost;
     };
-    CMap T{0, hi, 0};
+    uint64_t tt[16];
+    if (p0 + 16 <= M) sv.t16(p0, tt);
+    else {
 #pragma unroll
-    for (int k = 0; k < 16; ++k) T = cm_compose(map_of(k), T);
+        for (int k = 0; k < 16; ++k) tt[k] = p0 + k < M ? sv.t(p0 + k) : 0ull;
+    }
+    CMap T{0, hi, 0};
+    {
+        uint64_t tprev = tprev0;
+        int32_t cg = (int32_t)hb - 1;
+        uint32_t cj = 0;
+        uint64_t cx = 0;
+        if (p0 < M && !(hf & 1u)) { cj = seg_j[cg]; cx = seg_x[cg]; }
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const uint32_t p = p0 + (uint32_t)k;
+            uint32_t kd = TB_NONE;
+            if (p < M) {
+                if ((hf >> k) & 1u) { ++cg; cj = seg_j[cg]; cx = seg_x[cg]; }
+                const uint64_t tp = tt[k];
+                if (p < cj) {
+                    kd = TB_BLOCKED;
+                } else if (p == cj) {
+                    kd = TB_FIRST;
+                    const int64_t x = (int64_t)(cx & ~(1ull << 63));
+                    T = CMap{x, x, 0};
+                } else {
+                    kd = TB_NEXT;
+                    T = cm_compose(degen ? CMap{0, 0, 0} : CMap{0, hi, delta(tp, tprev)}, T);
+                }
+                tprev = tp;
+            }
+            kind |= kd << (2 * k);
+        }
+    }
     // block scan of the thread maps (in position order)
     CMap incl = T;
 #pragma unroll
@@ -223,32 +235,36 @@ __device__ __forceinline__ void tb_tile(const SV &sv, uint32_t t, uint32_t M,
         int64_t x = cm_apply(excl, tile_x[t]);
         uint32_t out[4] = {0, 0, 0, 0};
         int32_t g = (int32_t)hb - 1;
-        uint64_t tp = 0;
+        uint64_t tprev = tprev0;
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
             const uint32_t p = p0 + (uint32_t)k;
             const uint32_t kd = (kind >> (2 * k)) & 3u;
             if (kd == TB_NONE) continue;
             if ((hf >> k) & 1u) ++g;
+            const uint64_t tp = tt[k];
             uint8_t v;
             if (kd == TB_BLOCKED) {
                 v = XDP_DROP;
             } else if (kd == TB_FIRST) {
-                v = ((uint64_t)D[k] >> 63) ? XDP_PASS : XDP_DROP;
-                x = D[k] & (int64_t)~(1ull << 63);
+                const uint64_t cx = seg_x[g];
+                v = (cx >> 63) ? XDP_PASS : XDP_DROP;
+                x = (int64_t)(cx & ~(1ull << 63));
             } else if (degen) {
                 v = XDP_DROP;
                 x = 0;
             } else {
-                v = x + D[k] >= 0 ? XDP_PASS : XDP_DROP;
-                x = clamp64(x + D[k], 0, hi);
+                const int64_t d = delta(tp, tprev);
+                v = x + d >= 0 ? XDP_PASS : XDP_DROP;
+                x = clamp64(x + d, 0, hi);
             }
+            tprev = tp;
             out[k >> 2] |= (uint32_t)v << (8 * (k & 3));
             // last position of its source: the final {tokens, last} (counted packets only)
             if (kd != TB_BLOCKED && ((hf >> (k + 1)) & 1u)) {
                 Slot &sl = table[seg_slot[g]];
                 sl.aux = (uint64_t)x;
-                sl.tt = sv.t(p);
+                sl.tt = tp;
                 sl.flags |= SLOT_HAS_TB;
             }
         }
@@ -324,7 +340,7 @@ __global__ __launch_bounds__(1024) void k_tb_carry(BatchState *bs, const CMap *_
 
 hipError_t launch_token_bucket(const uint64_t *S, const uint64_t *ts, const uint32_t *len, BatchState *bs,
                                const Scratch &sc, Slot *table, const Limits &lim, uint32_t n,
-                               hipStream_t st) {
+                               hipStream_t st, const Marker &mark) {
     (void)hipGetLastError();   // a stale error of another caller is not ours
     const uint32_t gridSeg = std::min<uint32_t>(2048, std::max<uint32_t>(1, (n + 255) / 256));
     const uint32_t gridTiles = std::min<uint32_t>(4096, std::max<uint32_t>(1, (n + kTile - 1) / kTile));
@@ -334,13 +350,16 @@ hipError_t launch_token_bucket(const uint64_t *S, const uint64_t *ts, const uint
     int64_t *tile_x = reinterpret_cast<int64_t *>(sc.lim_tiles + 3 * sc.lim_tiles_n);
     k_tb_seg<<<gridSeg, 256, 0, st>>>(S, bs, sc.seg_start, sc.seg_slot, ts, len, sc.pay[0], table, lim,
                                       seg_j, seg_x);
+    mark("k_tb_seg");
     k_tb_tiles<false><<<gridTiles, 256, 0, st>>>(S, bs, ts, len, sc.pay[0], sc.headf, sc.tile_aux, seg_j,
                                                  seg_x, sc.seg_slot, table, lim, tile_map, tile_x,
                                                  sc.marks);
+    mark("k_tb_tiles_reduce");
     k_tb_carry<<<1, 1024, 0, st>>>(bs, tile_map, tile_x, lim);
     k_tb_tiles<true><<<gridTiles, 256, 0, st>>>(S, bs, ts, len, sc.pay[0], sc.headf, sc.tile_aux, seg_j,
                                                 seg_x, sc.seg_slot, table, lim, tile_map, tile_x,
                                                 sc.marks);
+    mark("k_tb_tiles_apply");
     return hipGetLastError();
 }
 
@@ -490,17 +509,94 @@ __device__ void sw_walk_fast_wave(const SV &sv, uint32_t a, uint32_t b, const Li
     }
 }
 
+// Thread version of sw_walk_fast_wave for short segments: the count trigger of a phase
+// starting at virtual index f cannot fire before v = f + P, so the scan starts there
+// (a segment shorter than P - m has no trigger to look for: O(log) per segment).
+template <class SV>
+__device__ void sw_walk_fast_thread(const SV &sv, uint32_t a, uint32_t b, const Limits &lim,
+                                    const uint64_t *ht, const uint32_t *hl, uint64_t hoff, uint32_t m,
+                                    MarkWriter<false> &mw, SwState &s, SwSeg &rec) {
+    const uint64_t P = lim.pps, W = lim.window;
+    uint32_t p = a;
+    if (s.has_bl && s.till > 0) {
+        p = gallop_gt(sv, a, b, s.till);
+        if (p > a) mw.emit(a, XDP_DROP);
+        if (p < b) s.has_bl = false;
+    }
+    const uint32_t j0 = p;
+    const VView<SV> vv{sv, ht, hl, hoff, m, j0};
+    rec.hoff = hoff; rec.m = m; rec.j0 = j0;
+    rec.lo = 0; rec.hi = m;
+    uint32_t f = 0;
+    auto log_start = [&](uint32_t vq, uint64_t tq) -> uint32_t {
+        if (tq < W) return f;
+        const uint32_t lo = gallop_gt(vv, f, vq + 1, tq - W);
+        return lo < vq ? lo : vq;
+    };
+    auto stats = [&](uint32_t lo, uint32_t v) {
+        s.has_st = true;
+        s.pps = (uint64_t)(v - lo) + 1;
+        s.bps = sum_len<false>(vv, lo, v + 1);
+        s.tt = vv.t(lo);
+    };
+    while (p < b) {
+        uint32_t k = b;
+        if (P == 0) {
+            k = p;
+        } else {
+            const uint64_t need = (uint64_t)f + P;                 // first v that can trigger
+            const uint64_t vp = (uint64_t)m + (p - j0);
+            const uint64_t q0 = need <= vp ? p : (uint64_t)j0 + (need - m);
+            for (uint64_t q = q0; q < b; ++q) {
+                const uint32_t v = m + ((uint32_t)q - j0);
+                if (sv.t((uint32_t)q) - vv.t(v - (uint32_t)P) < W) { k = (uint32_t)q; break; }
+            }
+        }
+        if (k >= b) {
+            mw.emit(p, XDP_PASS);
+            const uint32_t vl = m + (b - 1 - j0);
+            const uint32_t lo = log_start(vl, sv.t(b - 1));
+            stats(lo, vl);
+            rec.lo = lo; rec.hi = vl + 1;
+            break;
+        }
+        if (k > p) mw.emit(p, XDP_PASS);
+        mw.emit(k, XDP_DROP);
+        const uint32_t vk = m + (k - j0);
+        const uint64_t tk = sv.t(k);
+        stats(log_start(vk, tk), vk);
+        s.till = tk + lim.block;
+        s.has_bl = true;
+        rec.lo = 0; rec.hi = 0;
+        const uint32_t j = gallop_gt(sv, k + 1, b, s.till);
+        if (j >= b) break;
+        s.has_bl = false;
+        f = m + (j - j0);
+        p = j;
+    }
+}
+
 __device__ __forceinline__ bool sw_mono(const BatchState *bs, const TableState *ts) {
     return !bs->nonmono && !ts->ever_nonmono && ~bs->inv_min_ts >= ts->last_max_ts;
 }
 
+// The epoch-style walkers hold when clocks are monotone, no byte trigger can come before
+// the count trigger and till / window ends do not overflow u64.
+__device__ __forceinline__ bool sw_fast(const BatchState *bs, const TableState *tst, const Limits &lim) {
+    const uint32_t maxL = bs->max_len > tst->max_len_seen ? bs->max_len : tst->max_len_seen;
+    const uint64_t lim_ts = lim.window > lim.block ? lim.window : lim.block;
+    return sw_mono(bs, tst) && lim.pps * (uint64_t)maxL <= lim.bps && bs->max_ts <= ~0ull - lim_ts;
+}
+
 template <class SV>
-__device__ __forceinline__ void sw_short_body(const SV &sv, const BatchState *bs, const uint32_t *seg_start,
+__device__ __forceinline__ void sw_short_body(const SV &sv, const BatchState *bs, const TableState *tst,
+                                              const uint32_t *seg_start,
                                               const uint32_t *seg_slot, const uint32_t *order,
                                               const uint32_t *cls, uint8_t *marks, Slot *table,
                                               const Limits &lim, const uint64_t *ht, const uint32_t *hl,
                                               SwSeg *segs) {
     const uint32_t nshort = bs->nseg - cls[kSegClasses - 1];
+    const bool fast = sw_fast(bs, tst, lim);
     for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < nshort; i += gridDim.x * 256u) {
         const uint32_t g = order[i];
         const uint32_t a = seg_start[g], b = seg_start[g + 1];
@@ -511,7 +607,8 @@ __device__ __forceinline__ void sw_short_body(const SV &sv, const BatchState *bs
         sw_hist_of(sl.aux, hoff, m);
         MarkWriter<false> mw{marks, 0};
         SwSeg rec{};
-        sw_walk_exact(sv, a, b, lim, ht, hl, hoff, m, mw, st, rec);
+        if (fast) sw_walk_fast_thread(sv, a, b, lim, ht, hl, hoff, m, mw, st, rec);
+        else sw_walk_exact(sv, a, b, lim, ht, hl, hoff, m, mw, st, rec);
         segs[g] = rec;
         sw_store(sl, st, g);
     }
@@ -524,10 +621,7 @@ __device__ __forceinline__ void sw_long_body(const SV &sv, const BatchState *bs,
                                              Slot *table, const Limits &lim, const uint64_t *ht,
                                              const uint32_t *hl, SwSeg *segs) {
     const uint32_t nl = cls[kSegClasses - 1], first = bs->nseg - nl;
-    const uint32_t maxL = bs->max_len > tst->max_len_seen ? bs->max_len : tst->max_len_seen;
-    const uint64_t lim_ts = lim.window > lim.block ? lim.window : lim.block;
-    const bool fast = sw_mono(bs, tst) && lim.pps * (uint64_t)maxL <= lim.bps &&
-                      bs->max_ts <= ~0ull - lim_ts;
+    const bool fast = sw_fast(bs, tst, lim);
     const uint32_t lane = lane_id();
     for (uint32_t i = blockIdx.x * 4u + (threadIdx.x >> 6); i < nl; i += gridDim.x * 4u) {
         const uint32_t g = order[first + i];
@@ -571,11 +665,11 @@ __global__ __launch_bounds__(256) void k_walk_sw(const uint64_t *__restrict__ S,
     if (bs->pay_ok) {
         const SegView<true> sv{S, ts, len, pay, ~bs->inv_min_ts};
         if constexpr (kLong) sw_long_body(sv, bs, tst, seg_start, seg_slot, order, cls, marks, table, lim, ht, hl, segs);
-        else sw_short_body(sv, bs, seg_start, seg_slot, order, cls, marks, table, lim, ht, hl, segs);
+        else sw_short_body(sv, bs, tst, seg_start, seg_slot, order, cls, marks, table, lim, ht, hl, segs);
     } else {
         const SegView<false> sv{S, ts, len, pay, 0};
         if constexpr (kLong) sw_long_body(sv, bs, tst, seg_start, seg_slot, order, cls, marks, table, lim, ht, hl, segs);
-        else sw_short_body(sv, bs, seg_start, seg_slot, order, cls, marks, table, lim, ht, hl, segs);
+        else sw_short_body(sv, bs, tst, seg_start, seg_slot, order, cls, marks, table, lim, ht, hl, segs);
     }
 }
 
@@ -601,6 +695,7 @@ __device__ __forceinline__ uint32_t sw_slot_log(const SV &sv, const Slot &sl, co
 }
 
 constexpr uint32_t kSlotTile = 4096;   // table slots per block in the history rebuild
+constexpr uint32_t kCoopLog = 32;      // longer carried logs are copied by the whole wave
 
 struct SwClock {
     bool prune;
@@ -633,7 +728,9 @@ __global__ __launch_bounds__(256) void k_sw_hist(const uint64_t *__restrict__ S,
     const SegView<false> svg{S, ts, len, pay, 0};
     uint32_t *tile_cnt = hb.tile_cnt;
     for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
-        const uint64_t i0 = t * kSlotTile + (uint64_t)threadIdx.x * 16u;
+        // thread x owns slots i0 + 256 k (coalesced slot reads); its logs are stored
+        // contiguously in k order (any order works: the slot's aux holds the offset)
+        const uint64_t i0 = t * kSlotTile + threadIdx.x;
         auto slot_log = [&](uint64_t i, SwSeg &r) -> uint32_t {
             if (i >= nslots) return 0;
             return pay_ok ? sw_slot_log(svp, table[i], segs, ht, hl, ck.prune, ck.cutoff, r)
@@ -642,7 +739,7 @@ __global__ __launch_bounds__(256) void k_sw_hist(const uint64_t *__restrict__ S,
         uint32_t cnt = 0;
         for (int k = 0; k < 16; ++k) {
             SwSeg r;
-            cnt += slot_log(i0 + k, r);
+            cnt += slot_log(i0 + 256u * k, r);
         }
         if constexpr (!kWrite) {
             uint32_t tot;
@@ -650,24 +747,48 @@ __global__ __launch_bounds__(256) void k_sw_hist(const uint64_t *__restrict__ S,
             if (threadIdx.x == 0) tile_cnt[t] = tot;
         } else {
             uint64_t off = hb.tile_off[t] + block256_excl(cnt, s_tmp, nullptr);
-            for (int k = 0; k < 16; ++k) {
-                SwSeg r;
-                const uint32_t c = slot_log(i0 + k, r);
-                if (i0 + k >= nslots) break;
-                Slot &sl = table[i0 + k];
-                if (sl.tag == 0) continue;
-                if (c == 0) { sl.aux = 0; continue; }
-                for (uint32_t v = r.lo; v < r.hi; ++v) {
-                    const uint64_t o = off + (v - r.lo);
-                    if (pay_ok) {
-                        const VView<SegView<true>> vv{svp, ht, hl, r.hoff, r.m, r.j0};
-                        nt[o] = vv.t(v); nl[o] = vv.l(v);
-                    } else {
-                        const VView<SegView<false>> vv{svg, ht, hl, r.hoff, r.m, r.j0};
-                        nt[o] = vv.t(v); nl[o] = vv.l(v);
+            // copy log entries [lo + first, hi) step `step` of r to off + (v - lo)
+            auto copy = [&](const SwSeg &r, uint64_t o0, uint32_t first, uint32_t step) {
+                if (pay_ok) {
+                    const VView<SegView<true>> vv{svp, ht, hl, r.hoff, r.m, r.j0};
+                    for (uint32_t v = r.lo + first; v < r.hi; v += step) {
+                        nt[o0 + (v - r.lo)] = vv.t(v); nl[o0 + (v - r.lo)] = vv.l(v);
+                    }
+                } else {
+                    const VView<SegView<false>> vv{svg, ht, hl, r.hoff, r.m, r.j0};
+                    for (uint32_t v = r.lo + first; v < r.hi; v += step) {
+                        nt[o0 + (v - r.lo)] = vv.t(v); nl[o0 + (v - r.lo)] = vv.l(v);
                     }
                 }
-                sl.aux = (off << kHistCntBits) | c;
+            };
+            const uint32_t lane = lane_id();
+            for (int k = 0; k < 16; ++k) {   // wave-uniform trip count (no early exit)
+                SwSeg r{};
+                const uint64_t i = i0 + 256u * k;
+                const uint32_t c = slot_log(i, r);
+                if (i < nslots) {
+                    Slot &sl = table[i];
+                    if (sl.tag != 0) {
+                        if (c == 0) sl.aux = 0;
+                        else {
+                            if (c <= kCoopLog) copy(r, off, 0, 1);
+                            sl.aux = (off << kHistCntBits) | c;
+                        }
+                    }
+                }
+                // long logs (a heavy source keeps up to P entries): the whole wave copies
+                uint64_t big = __ballot(c > kCoopLog);
+                while (big) {
+                    const int src = __ffsll((unsigned long long)big) - 1;
+                    big &= big - 1;
+                    SwSeg rb;
+                    rb.hoff = __shfl(r.hoff, src);
+                    rb.m = __shfl(r.m, src);
+                    rb.j0 = __shfl(r.j0, src);
+                    rb.lo = __shfl(r.lo, src);
+                    rb.hi = __shfl(r.hi, src);
+                    copy(rb, __shfl(off, src), lane, 64);
+                }
                 off += c;
             }
         }
@@ -717,21 +838,25 @@ __global__ void k_sw_finish(const BatchState *bs, TableState *tst, const uint64_
 
 hipError_t launch_sliding_window(const uint64_t *S, const uint64_t *ts, const uint32_t *len, BatchState *bs,
                                  const Scratch &sc, Slot *table, TableState *tstate, const HistBufs &hb,
-                                 const Limits &lim, uint32_t n, hipStream_t st) {
+                                 const Limits &lim, uint32_t n, hipStream_t st, const Marker &mark) {
     (void)hipGetLastError();   // a stale error of another caller is not ours
     const uint32_t gridSeg = std::min<uint32_t>(2048, std::max<uint32_t>(1, (n + 255) / 256));
     const uint32_t *cls = sc.sort_ctl + 1028;
     k_walk_sw<false><<<gridSeg, 256, 0, st>>>(S, bs, tstate, sc.seg_start, sc.seg_slot, ts, len, sc.pay[0],
                                               sc.seg_order, cls, sc.marks, table, lim, hb, sc.sw_seg);
+    mark("k_walk_sw_short");
     k_walk_sw<true><<<1024, 256, 0, st>>>(S, bs, tstate, sc.seg_start, sc.seg_slot, ts, len, sc.pay[0],
                                           sc.seg_order, cls, sc.marks, table, lim, hb, sc.sw_seg);
+    mark("k_walk_sw_long");
     const uint64_t nslots = lim.table_mask + 1;
     const uint64_t ntiles = (nslots + kSlotTile - 1) / kSlotTile;
     const uint32_t grid = (uint32_t)std::min<uint64_t>(4096, ntiles);
     k_sw_hist<false><<<grid, 256, 0, st>>>(S, bs, tstate, ts, len, sc.pay[0], table, lim, hb, sc.sw_seg);
     k_sw_hist_scan<<<1, 1024, 0, st>>>(bs, hb.tile_cnt, hb.tile_off, ntiles, hb.total);
+    mark("k_sw_hist_count");
     k_sw_hist<true><<<grid, 256, 0, st>>>(S, bs, tstate, ts, len, sc.pay[0], table, lim, hb, sc.sw_seg);
     k_sw_finish<<<1, 1, 0, st>>>(bs, tstate, hb.total);
+    mark("k_sw_hist_write");
     return hipGetLastError();
 }
 

@@ -29,6 +29,22 @@ struct SegView {
         if constexpr (kPay) return (uint32_t)pay[q] & ((1u << kPayLenBits) - 1u);
         else return len[pk_idx(S[q])];
     }
+    // Timestamps of positions q0 .. q0+15, q0 % 2 == 0, all < the valid count: 16-byte
+    // vector loads of the payload words (one thread reads a whole 128-byte line).
+    __device__ __forceinline__ void t16(uint32_t q0, uint64_t (&out)[16]) const {
+        if constexpr (kPay) {
+            const ulonglong2 *p = reinterpret_cast<const ulonglong2 *>(pay + q0);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const ulonglong2 v = p[k];
+                out[2 * k] = tbase + (v.x >> kPayLenBits);
+                out[2 * k + 1] = tbase + (v.y >> kPayLenBits);
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < 16; ++k) out[k] = t(q0 + k);
+        }
+    }
 };
 
 // First q in [lo, hi) with t(q) > X (t non-decreasing on [lo, hi)); wave-uniform
