@@ -844,11 +844,14 @@ hipError_t launch_index_rebuild(Slot *table, const Limits &lim, const TableIndex
 }
 
 // ------------------------------------------------------------------ fixed-window walker
-// Segments of at most kShortSeg packets: one thread, exact per-packet replay with 16
+// Segments of at most short_seg packets: one thread, exact per-packet replay with 16
 // packets' loads in flight. Longer segments (the heavy sources): one wave each,
 // epoch jumps with 64-wide cooperative searches (few dependent round trips per
-// search instead of one per binary-search step).
-constexpr uint32_t kShortSeg = 512;
+// search instead of one per binary-search step). The boundary is per limiter: the
+// fixed-window wave walker runs beside the thread walker on its own stream, so a
+// lower boundary balances the two (measured on config 2: 256 fixed, 512 sliding).
+constexpr uint32_t kShortSegFixed = 256;
+constexpr uint32_t kShortSegSliding = 512;
 
 
 constexpr uint64_t kBig = 1ull << 62;
@@ -1002,9 +1005,9 @@ __device__ __forceinline__ bool fast_ok(const BatchState *bs, const Limits &lim)
 
 // Segments are walked in order of length class (ceil log2 of the packet count), so
 // the lanes of a wave replay segments of similar length; the last class (longer
-// than kShortSeg) goes to k_walk_fixed_long, one wave per segment.
-__device__ __forceinline__ uint32_t seg_class(uint32_t L) {
-    if (L > kShortSeg) return kSegClasses - 1;
+// than short_seg) goes to the wave walkers, one wave per segment.
+__device__ __forceinline__ uint32_t seg_class(uint32_t L, uint32_t short_seg) {
+    if (L > short_seg) return kSegClasses - 1;
     return L <= 1 ? 0u : 32u - (uint32_t)__clz((int)(L - 1));
 }
 
@@ -1021,13 +1024,13 @@ __device__ __forceinline__ void seg_chunk(uint32_t nseg, uint32_t b, uint32_t &l
 
 template <bool kWrite>
 __device__ __forceinline__ void seg_classes_pass(const uint32_t *seg_start, uint32_t lo, uint32_t hi,
-                                                 uint32_t *sh, uint32_t *order) {
+                                                 uint32_t short_seg, uint32_t *sh, uint32_t *order) {
     const uint32_t lane = lane_id();
     const uint64_t lt = (1ull << lane) - 1ull;
     for (uint32_t b = lo; b < hi; b += 256u) {
         const uint32_t g = b + threadIdx.x;
         const bool ok = g < hi;
-        const uint32_t c = ok ? seg_class(seg_start[g + 1] - seg_start[g]) : kSegClasses;
+        const uint32_t c = ok ? seg_class(seg_start[g + 1] - seg_start[g], short_seg) : kSegClasses;
 #pragma unroll
         for (uint32_t k = 0; k < kSegClasses; ++k) {
             const uint64_t m = __ballot(c == k);
@@ -1044,13 +1047,13 @@ __device__ __forceinline__ void seg_classes_pass(const uint32_t *seg_start, uint
 
 __global__ __launch_bounds__(256) void k_seg_count(const BatchState *bs,
                                                    const uint32_t *__restrict__ seg_start,
-                                                   uint32_t *__restrict__ blk) {
+                                                   uint32_t *__restrict__ blk, uint32_t short_seg) {
     __shared__ uint32_t sh[kSegClasses];
     if (threadIdx.x < kSegClasses) sh[threadIdx.x] = 0;
     __syncthreads();
     uint32_t lo, hi;
     seg_chunk(bs->nseg, blockIdx.x, lo, hi);
-    seg_classes_pass<false>(seg_start, lo, hi, sh, nullptr);
+    seg_classes_pass<false>(seg_start, lo, hi, short_seg, sh, nullptr);
     __syncthreads();
     if (threadIdx.x < kSegClasses) blk[threadIdx.x * kSegBlocks + blockIdx.x] = sh[threadIdx.x];
 }
@@ -1080,13 +1083,13 @@ __global__ __launch_bounds__(1024) void k_seg_scan(uint32_t *__restrict__ blk, u
 __global__ __launch_bounds__(256) void k_seg_order(const BatchState *bs,
                                                    const uint32_t *__restrict__ seg_start,
                                                    const uint32_t *__restrict__ blk,
-                                                   uint32_t *__restrict__ order) {
+                                                   uint32_t *__restrict__ order, uint32_t short_seg) {
     __shared__ uint32_t cur[kSegClasses];
     if (threadIdx.x < kSegClasses) cur[threadIdx.x] = blk[threadIdx.x * kSegBlocks + blockIdx.x];
     __syncthreads();
     uint32_t lo, hi;
     seg_chunk(bs->nseg, blockIdx.x, lo, hi);
-    seg_classes_pass<true>(seg_start, lo, hi, cur, order);
+    seg_classes_pass<true>(seg_start, lo, hi, short_seg, cur, order);
 }
 
 template <class SV>
@@ -1435,9 +1438,10 @@ hipError_t launch_verdict_pipeline(const uint8_t *hdr, const uint32_t *len, cons
         if ((e = launch_token_bucket(S, ts, len, bs, sc, table, lim, n, st, mk)) != hipSuccess) return e;
     } else {
         uint32_t *cls = sc.sort_ctl + 1028;
-        k_seg_count<<<kSegBlocks, 256, 0, st>>>(bs, sc.seg_start, sc.hist);
+        const uint32_t short_seg = lim.limiter == 1 ? kShortSegSliding : kShortSegFixed;
+        k_seg_count<<<kSegBlocks, 256, 0, st>>>(bs, sc.seg_start, sc.hist, short_seg);
         k_seg_scan<<<1, 1024, 0, st>>>(sc.hist, cls);
-        k_seg_order<<<kSegBlocks, 256, 0, st>>>(bs, sc.seg_start, sc.hist, sc.seg_order);
+        k_seg_order<<<kSegBlocks, 256, 0, st>>>(bs, sc.seg_start, sc.hist, sc.seg_order, short_seg);
         mark("k_seg_order");
         if (lim.limiter == 1) {   // FSX_LIMIT_SLIDING_WINDOW
             if ((e = launch_sliding_window(S, ts, len, bs, sc, table, tstate, hist, lim, n, st, mk)) !=

@@ -74,7 +74,7 @@ struct BatchState {
     uint32_t err;
     uint32_t max_len;
     uint32_t n_fix;       // unused (0): source ids are exact, no collision fixups
-    uint32_t n_long;      // segments longer than kShortSeg (wave walker)
+    uint32_t n_long;      // segments longer than the short-segment bound (wave walker)
     uint32_t n_span;      // sources crossing flow tiles (k_flow_combine)
     uint64_t max_ts;
     uint64_t allowed;     // this batch
