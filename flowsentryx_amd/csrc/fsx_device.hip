@@ -132,7 +132,7 @@ __device__ __forceinline__ uint32_t id_resolve(const IdTable &T, uint32_t tag, c
 // One wave handles 64 consecutive records per step: the 4 KiB tile is loaded with
 // four fully coalesced 1 KiB wave loads and staged through LDS (17-dword record
 // pitch: conflict-free 32-bit reads), then each lane parses its own record.
-__global__ __launch_bounds__(256) void k_parse(const uint8_t *__restrict__ hdr,
+__global__ __launch_bounds__(256, 4) void k_parse(const uint8_t *__restrict__ hdr,
                                                const uint32_t *__restrict__ len,
                                                const uint64_t *__restrict__ ts, uint32_t n,
                                                uint64_t *__restrict__ packed,
@@ -182,21 +182,27 @@ __global__ __launch_bounds__(256) void k_parse(const uint8_t *__restrict__ hdr,
         T_ = live ? ts[i] : 0ull;
         P_ = (lane == 0 && live && i > 0) ? ts[i - 1] : 0ull;
     };
-    uint4 hv[4];
-    uint32_t Lc;
-    uint64_t Tc, Pc;
+    uint4 hv[4], hn[4];
+    uint32_t Lc, Ln;
+    uint64_t Tc, Pc, Tn, Pn;
     load(step_of(blockIdx.x, 0), hv, Lc, Tc, Pc);
-    // software pipeline: the next step's loads are in flight while this one is parsed
-    // (measured faster than issuing the id probes ahead of the prefetch)
+    {
+        uint32_t T1, j1;
+        next_step(blockIdx.x, 0, T1, j1);
+        load(T1 < nsort ? step_of(T1, j1) : ntiles, hn, Ln, Tn, Pn);
+    }
+    // software pipeline: the loads of the next two steps are in flight while this one
+    // is parsed (measured faster than issuing the id probes ahead of the prefetch)
     for (uint32_t tile = blockIdx.x; tile < nsort; tile += gridDim.x)
     for (uint32_t j = 0; j < kSteps; ++j) {
         const uint32_t t = step_of(tile, j);
-        uint32_t T2, j2;
-        next_step(tile, j, T2, j2);
-        uint4 hn[4];
-        uint32_t Ln;
-        uint64_t Tn, Pn;
-        load(T2 < nsort ? step_of(T2, j2) : ntiles, hn, Ln, Tn, Pn);
+        uint32_t T1, j1, T2, j2;
+        next_step(tile, j, T1, j1);
+        next_step(T1, j1, T2, j2);
+        uint4 h2[4];
+        uint32_t L2;
+        uint64_t Tn2, Pn2;
+        load(T2 < nsort ? step_of(T2, j2) : ntiles, h2, L2, Tn2, Pn2);
         const uint32_t base = t << 6;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -249,8 +255,9 @@ __global__ __launch_bounds__(256) void k_parse(const uint8_t *__restrict__ hdr,
                                 : idt.head[h];
         }
 #pragma unroll
-        for (int q = 0; q < 4; ++q) hv[q] = hn[q];
+        for (int q = 0; q < 4; ++q) { hv[q] = hn[q]; hn[q] = h2[q]; }
         Lc = Ln; Tc = Tn; Pc = Pn;
+        Ln = L2; Tn = Tn2; Pn = Pn2;
         uint64_t out = kSentinel;
         bool fresh = false;
         if (ip) {
