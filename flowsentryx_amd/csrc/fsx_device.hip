@@ -290,7 +290,7 @@ __global__ __launch_bounds__(256, 4) void k_parse(const uint8_t *__restrict__ hd
             __syncthreads();
             const uint32_t c = s_t0[0][threadIdx.x] + s_t0[1][threadIdx.x] + s_t0[2][threadIdx.x] +
                                s_t0[3][threadIdx.x];
-            thist[(size_t)threadIdx.x * tcap + tile] = c;
+            if (threadIdx.x <= dmask) thist[(size_t)threadIdx.x * tcap + tile] = c;
 #pragma unroll
             for (int d = 0; d < 4; ++d) s_t0[d][threadIdx.x] = 0;
             __syncthreads();
@@ -383,16 +383,24 @@ __global__ __launch_bounds__(256) void k_tile_hist(const uint64_t *__restrict__ 
     for (int k = 0; k < 4; ++k) sh[k][tid] = 0;
     __syncthreads();
     const uint32_t t0 = t * kSortTile, end = min(L, t0 + kSortTile);
+    // 16-byte loads: thread x holds keys 2(256 r + x) and 2(256 r + x) + 1 (the order of
+    // a histogram's inputs is irrelevant)
     uint64_t v[kSortItems];
+    auto item = [&](int r) { return t0 + 2u * ((uint32_t)(r >> 1) * 256u + tid) + (uint32_t)(r & 1); };
+    if (t0 + kSortTile <= end) {
 #pragma unroll
-    for (int r = 0; r < kSortItems; ++r) {
-        const uint32_t i = t0 + (uint32_t)r * 256u + tid;
-        v[r] = i < end ? in[i] : kSentinel;
+        for (int r = 0; r < kSortItems; r += 2) {
+            const ulonglong2 x = *reinterpret_cast<const ulonglong2 *>(in + item(r));
+            v[r] = x.x; v[r + 1] = x.y;
+        }
+    } else {
+#pragma unroll
+        for (int r = 0; r < kSortItems; ++r) v[r] = item(r) < end ? in[item(r)] : kSentinel;
     }
     const uint32_t lane = lane_id();
 #pragma unroll
     for (int r = 0; r < kSortItems; ++r) {
-        const uint32_t i = t0 + (uint32_t)r * 256u + tid;
+        const uint32_t i = item(r);
         const bool ok = sort_item(i, end, first, v[r]);
         const uint32_t d = (uint32_t)(v[r] >> shift) & dmask;
         const uint64_t act = __ballot(ok);
@@ -407,11 +415,12 @@ __global__ __launch_bounds__(256) void k_tile_hist(const uint64_t *__restrict__ 
         }
     }
     __syncthreads();
-    thist[(size_t)tid * tcap + t] = sh[0][tid] + sh[1][tid] + sh[2][tid] + sh[3][tid];
+    // digit-major rows (one partial line per count: only the dmask + 1 live digits)
+    if (tid <= dmask) thist[(size_t)tid * tcap + t] = sh[0][tid] + sh[1][tid] + sh[2][tid] + sh[3][tid];
 }
 
-// Block d: offs[d][t] = base[d] + sum of thist[d][t'] over t' < t (in place); each
-// thread owns one contiguous run of tiles.
+// Block d: offs[d][t] = base[d] + sum of thist[d][t'] over t' < t (in place), in
+// coalesced chunks of 1024 tiles (4 per thread) with a running carry.
 __global__ __launch_bounds__(256) void k_tile_scan(uint32_t *__restrict__ thist, uint32_t tcap,
                                                    uint32_t L_host, const uint32_t *L_dev,
                                                    const uint32_t *__restrict__ gbase) {
@@ -419,15 +428,18 @@ __global__ __launch_bounds__(256) void k_tile_scan(uint32_t *__restrict__ thist,
     const uint32_t L = L_dev ? *L_dev : L_host;
     const uint32_t ntiles = (L + kSortTile - 1) / kSortTile;
     uint32_t *row = thist + (size_t)blockIdx.x * tcap;
-    const uint32_t per = (ntiles + 255) / 256;
-    const uint32_t j0 = min(ntiles, threadIdx.x * per), j1 = min(ntiles, j0 + per);
-    uint32_t sum = 0;
-    for (uint32_t j = j0; j < j1; ++j) sum += row[j];
-    uint32_t off = gbase[blockIdx.x] + block256_excl(sum, s_tmp, nullptr);
-    for (uint32_t j = j0; j < j1; ++j) {
-        const uint32_t x = row[j];
-        row[j] = off;
-        off += x;
+    uint32_t carry = gbase[blockIdx.x];
+    for (uint32_t c0 = 0; c0 < ntiles; c0 += 1024) {
+        const uint32_t i = c0 + threadIdx.x * 4u;
+        uint32_t x[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) x[k] = i + k < ntiles ? row[i + k] : 0u;
+        uint32_t tot;
+        uint32_t off = carry + block256_excl(x[0] + x[1] + x[2] + x[3], s_tmp, &tot);
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (i + k < ntiles) { row[i + k] = off; off += x[k]; }
+        carry += tot;
     }
 }
 
@@ -500,7 +512,7 @@ __device__ __forceinline__ void sort_tile(uint32_t t, const uint64_t *__restrict
     const uint32_t d = tid;
     const uint32_t c0 = s_wc[0][d], c1 = s_wc[1][d], c2 = s_wc[2][d], c3 = s_wc[3][d];
     const uint32_t tc = c0 + c1 + c2 + c3;
-    s_dst[d] = offs(d, tc);
+    s_dst[d] = d <= dmask ? offs(d, tc) : 0u;   // rows of dead digits are never written
     __syncthreads();
     FSX_STAMP(t, 2);
     s_wc[0][d] = 0; s_wc[1][d] = c0; s_wc[2][d] = c0 + c1; s_wc[3][d] = c0 + c1 + c2;
@@ -546,6 +558,9 @@ __device__ __forceinline__ void sort_tile(uint32_t t, const uint64_t *__restrict
 }
 
 constexpr bool kLatePayDefault = true;
+#ifndef FSX_SCATTER_MINB
+#define FSX_SCATTER_MINB 4   // waves/SIMD bound of k_tile_scatter (A/B: scripts/build_variant.sh)
+#endif
 
 struct TileOffs {
     const uint32_t *offs;
@@ -556,7 +571,7 @@ struct TileOffs {
 };
 
 template <bool kLatePay>
-__global__ __launch_bounds__(256, kLatePay ? 4 : 1) void k_tile_scatter(const uint64_t *__restrict__ in,
+__global__ __launch_bounds__(256, kLatePay ? FSX_SCATTER_MINB : 1) void k_tile_scatter(const uint64_t *__restrict__ in,
                                                       uint64_t *__restrict__ out, uint32_t L_host,
                                                       const uint32_t *L_dev, uint32_t shift, uint32_t dmask,
                                                       int first, const uint32_t *__restrict__ offs,
@@ -1403,10 +1418,12 @@ hipError_t launch_verdict_pipeline(const uint8_t *hdr, const uint32_t *len, cons
                                                        ts, len);
             mark("k_onesweep");
         } else {
-            if (pass > 0)   // pass 0's per-tile counts come from k_parse
+            if (pass > 0) {   // pass 0's per-tile counts come from k_parse
                 k_tile_hist<<<ntiles, 256, 0, st>>>(in, n, Ld, shift, dmask, pass == 0, sc.hist, tcap);
-            k_tile_scan<<<256, 256, 0, st>>>(sc.hist, tcap, n, Ld, sc.gbase + 256 * pass);
-            mark("k_tile_hist");
+                mark("k_tile_hist");
+            }
+            k_tile_scan<<<dmask + 1, 256, 0, st>>>(sc.hist, tcap, n, Ld, sc.gbase + 256 * pass);
+            mark("k_tile_scan");
             k_tile_scatter<kLatePayDefault><<<ntiles, 256, 0, st>>>(in, out, n, Ld, shift, dmask, pass == 0, sc.hist, tcap, bs,
                                                    pin, pout, ts, len);
             mark("k_tile_scatter");

@@ -88,7 +88,10 @@ _lib = None
 
 
 def library_path() -> Path:
-    return _PKG / "libfsx_hip.so"
+    # FSX_LIB_VARIANT=x loads libfsx_hip.x.so: in-tree A/B builds of the same sources
+    # with different tuning macros (scripts/build_variant.sh); unset in production
+    v = os.environ.get("FSX_LIB_VARIANT")
+    return _PKG / (f"libfsx_hip.{v}.so" if v else "libfsx_hip.so")
 
 
 def load_library() -> C.CDLL:
