@@ -129,6 +129,157 @@ __device__ __forceinline__ uint32_t id_resolve(const IdTable &T, uint32_t tag, c
 }
 
 // ------------------------------------------------------------------ parse
+// Radix digits of the sort: pass p uses (word >> shift[p]) & mask[p]. Plain: equal
+// digits of the source id. Heavy-source sort: pass 0 uses the 8-bit bucket (bits
+// 56..63: light digit 0, or the heavy index above it), passes 1.. the remaining id
+// digits of the light entries only.
+struct DigitPlan {
+    uint32_t shift[4], mask[4];
+    uint32_t npass;
+    uint32_t light_b;   // heavy sort: buckets below light_b are light (id digit 0); 0 = plain
+};
+
+// parse_ethhdr / parse_ip6hdr / parse_ip4hdr (src/parsing_helper.h:49-136, dispatch
+// src/fsx_kern.c:123-148) on a record's dwords 3 and 5..9: family tag 1 (IPv4) / 2
+// (IPv6) with the raw source address in k, or 0 with the verdict of a packet that
+// never reaches the limiter (short frame: DROP; not IPv4/IPv6: PASS, uncounted).
+__device__ __forceinline__ uint32_t parse_src(uint32_t L, uint32_t d3, uint32_t d5, uint32_t d6,
+                                              uint32_t d7, uint32_t d8, uint32_t d9, uint32_t k[4],
+                                              uint8_t &v) {
+    v = XDP_PASS;
+    k[0] = k[1] = k[2] = k[3] = 0;
+    // parse_ethhdr (14-byte bound; raw h_proto, no VLAN)
+    const uint32_t proto = ((d3 & 0xFFu) << 8) | ((d3 >> 8) & 0xFFu);
+    if (L < 14u) {
+        v = XDP_DROP;                // src/fsx_kern.c:124-127
+        return 0;
+    }
+    if (proto == 0x86DDu) {
+        if (L < 54u) { v = XDP_DROP; return 0; }   // parse_ip6hdr bound, src/fsx_kern.c:139-140
+        k[0] = (d5 >> 16) | (d6 << 16); k[1] = (d6 >> 16) | (d7 << 16);
+        k[2] = (d7 >> 16) | (d8 << 16); k[3] = (d8 >> 16) | (d9 << 16);
+        return 2;
+    }
+    if (proto == 0x0800u) {
+        if (L < 34u) { v = XDP_DROP; return 0; }   // parse_ip4hdr fixed 20-byte bound, :146-147
+        k[0] = (d6 >> 16) | (d7 << 16);            // bytes 26..29 raw
+        return 1;
+    }
+    return 0;
+}
+
+// Count sketch of a strided sample of the batch (kHeavySample packets spread over all
+// of it): per-block LDS counts, then one add per bucket; the candidate of a bucket is
+// one sampled packet that hashed there (the heavy source when one dominates it).
+// Sketch and map hash of a source: its probe start in the id table (already computed by
+// k_parse for every packet; tables of heavy-sort size have >= 2^17 slots).
+__global__ __launch_bounds__(256) void k_heavy_sample(const uint8_t *__restrict__ hdr,
+                                                      const uint32_t *__restrict__ len, uint32_t n,
+                                                      uint32_t *__restrict__ sketch, uint64_t seed,
+                                                      uint64_t mask, uint32_t test_flags) {
+    __shared__ uint32_t s_cnt[kSketch], s_cand[kSketch];
+    for (uint32_t c = threadIdx.x; c < kSketch; c += 256) s_cnt[c] = 0;
+    __syncthreads();
+    const uint32_t S = n < kHeavySample ? n : kHeavySample;
+    const uint32_t per = (S + gridDim.x - 1) / gridDim.x;
+    const uint32_t s0 = blockIdx.x * per, s1 = min(S, s0 + per);
+    for (uint32_t q = s0 + threadIdx.x; q < s1; q += 256) {
+        const uint32_t i = (uint32_t)((uint64_t)q * n / S);
+        const uint32_t *d = reinterpret_cast<const uint32_t *>(hdr + (size_t)i * 64);
+        uint32_t k[4];
+        uint8_t v;
+        const uint32_t tag = parse_src(len[i], d[3], d[5], d[6], d[7], d[8], d[9], k, v);
+        if (!tag) continue;
+        const uint32_t h = (uint32_t)probe_start(tag, k, seed, mask, test_flags) & (kSketch - 1);
+        atomicAdd(&s_cnt[h], 1u);
+        s_cand[h] = i;
+    }
+    __syncthreads();
+    for (uint32_t c = threadIdx.x; c < kSketch; c += 256) {
+        const uint32_t x = s_cnt[c];
+        if (x >= 2) {
+            atomicAdd(&sketch[c], x);
+            sketch[kSketch + c] = s_cand[c];
+        }
+    }
+}
+
+// One block: the (at most nmax) sketch buckets of highest count >= floor become the heavy
+// set: their candidates' keys and an open-addressing map of them. Zeroes the counts.
+__global__ __launch_bounds__(1024) void k_heavy_pick(const uint8_t *__restrict__ hdr,
+                                                     const uint32_t *__restrict__ len,
+                                                     uint32_t *__restrict__ sketch, HeavySet *hs,
+                                                     uint32_t nmax, uint32_t floor_cnt, uint64_t seed,
+                                                     uint64_t mask, uint32_t test_flags) {
+    constexpr uint32_t kMap = 1u << kHeavyMapBits;
+    __shared__ uint32_t s_n;
+    __shared__ uint32_t s_sel[kHeavyMax];
+    __shared__ uint32_t s_tag[kHeavyMax], s_key[kHeavyMax][4];
+    __shared__ uint8_t s_map[kMap];
+    const uint32_t tid = threadIdx.x;
+    static_assert(kSketch == 4 * 1024, "4 buckets per thread");
+    uint32_t c[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) c[k] = sketch[tid * 4 + k];
+    // the nmax highest counts >= floor, by log2 bins: every bucket of the bins above the
+    // cut bin B, then buckets of bin B - 1 while room is left
+    __shared__ uint32_t s_bin[32], s_cut, s_room, s_extra;
+    if (tid < 32) s_bin[tid] = 0;
+    if (tid == 0) { s_n = 0; s_extra = 0; }
+    s_map[tid] = 0;
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        if (c[k] >= floor_cnt) atomicAdd(&s_bin[31 - __clz((int)c[k])], 1u);
+    __syncthreads();
+    if (tid == 0) {
+        uint32_t acc = 0, B = 32;
+        for (int b = 31; b >= 0; --b) {
+            if (acc + s_bin[b] > nmax) break;
+            acc += s_bin[b];
+            B = (uint32_t)b;
+        }
+        s_cut = B;
+        s_room = nmax - acc;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t x = c[k];
+        if (x >= floor_cnt) {
+            const uint32_t b = 31u - (uint32_t)__clz((int)x);
+            if (b >= s_cut || (b + 1 == s_cut && atomicAdd(&s_extra, 1u) < s_room))
+                s_sel[atomicAdd(&s_n, 1u)] = tid * 4 + k;
+        }
+        sketch[tid * 4 + k] = 0;
+    }
+    __syncthreads();
+    const uint32_t n = s_n;
+    if (tid < n) {
+        const uint32_t i = sketch[kSketch + s_sel[tid]];
+        const uint32_t *d = reinterpret_cast<const uint32_t *>(hdr + (size_t)i * 64);
+        uint32_t k[4];
+        uint8_t v;
+        s_tag[tid] = parse_src(len[i], d[3], d[5], d[6], d[7], d[8], d[9], k, v);
+        for (int j = 0; j < 4; ++j) s_key[tid][j] = k[j];
+    }
+    __syncthreads();
+    if (tid == 0) {
+        for (uint32_t e = 0; e < n; ++e) {
+            uint32_t h = (uint32_t)probe_start(s_tag[e], s_key[e], seed, mask, test_flags) & (kMap - 1);
+            while (s_map[h]) h = (h + 1) & (kMap - 1);
+            s_map[h] = (uint8_t)(e + 1);
+        }
+        hs->n = n;
+    }
+    __syncthreads();
+    if (tid < n) {
+        hs->tag[tid] = s_tag[tid];
+        for (int j = 0; j < 4; ++j) hs->key[tid][j] = s_key[tid][j];
+    }
+    hs->map[tid] = s_map[tid];
+}
+
 // One wave handles 64 consecutive records per step: the 4 KiB tile is loaded with
 // four fully coalesced 1 KiB wave loads and staged through LDS (17-dword record
 // pitch: conflict-free 32-bit reads), then each lane parses its own record.
@@ -139,18 +290,28 @@ __global__ __launch_bounds__(256, 4) void k_parse(const uint8_t *__restrict__ hd
                                                uint8_t *__restrict__ verdict, BatchState *bs,
                                                IdTable idt, uint32_t *__restrict__ ghist,
                                                uint32_t *__restrict__ thist, uint32_t tcap,
-                                               uint32_t dbits) {
+                                               DigitPlan dp, const HeavySet *__restrict__ heavy) {
     __shared__ uint32_t s_rec[4][64 * 17];
     __shared__ uint32_t s_red[4][3];
     __shared__ unsigned long long s_ts[4], s_its[4];
-    __shared__ uint32_t s_hist[4][4][256];  // per wave: the 4 radix digits of every sort key
-    __shared__ uint32_t s_t0[4][256];       // per wave: digit 0 of the current sort tile
+    __shared__ uint32_t s_hist[4][256];     // the radix digits of every sort key (per pass)
+    __shared__ uint32_t s_t0[256];          // pass-0 digit of the current sort tile
+    __shared__ uint32_t s_hkey[kHeavyMax][4];
+    __shared__ uint32_t s_htag[kHeavyMax];
+    __shared__ uint32_t s_hmap4[(1u << kHeavyMapBits) / 4];   // HeavySet::map
+    const uint8_t *s_hmap = reinterpret_cast<const uint8_t *>(s_hmap4);
     const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
-    const uint32_t dmask = (1u << dbits) - 1u;   // radix digits of dbits <= 8 bits
 #pragma unroll
-    for (int d = 0; d < 16; ++d) (&s_hist[0][0][0])[d * 256 + threadIdx.x] = 0;
-#pragma unroll
-    for (int d = 0; d < 4; ++d) s_t0[d][threadIdx.x] = 0;
+    for (int d = 0; d < 4; ++d) s_hist[d][threadIdx.x] = 0;
+    s_t0[threadIdx.x] = 0;
+    const uint32_t nh = heavy ? heavy->n : 0u;
+    if (heavy) {
+        s_hmap4[threadIdx.x] = reinterpret_cast<const uint32_t *>(heavy->map)[threadIdx.x];
+        if (threadIdx.x < nh) {
+            s_htag[threadIdx.x] = heavy->tag[threadIdx.x];
+            for (int j = 0; j < 4; ++j) s_hkey[threadIdx.x][j] = heavy->key[threadIdx.x][j];
+        }
+    }
     __syncthreads();
     uint32_t *rec = s_rec[w];
     uint32_t any6 = 0, nonmono = 0, maxlen = 0, nfresh = 0;
@@ -220,32 +381,11 @@ __global__ __launch_bounds__(256, 4) void k_parse(const uint8_t *__restrict__ hd
         const uint64_t T = Tc;
         uint64_t prev = __shfl_up(T, 1);
         if (lane == 0) prev = (live && i > 0) ? Pc : T;
-        bool ip = false;
         uint8_t v = XDP_PASS;  // non-IP: PASS, not counted (src/fsx_kern.c:128-131)
-        uint32_t tag = 0, k[4] = {0, 0, 0, 0};
-        if (live) {
-            // parse_ethhdr (14-byte bound; raw h_proto, no VLAN)
-            const uint32_t proto = ((d3 & 0xFFu) << 8) | ((d3 >> 8) & 0xFFu);
-            if (L < 14u) {
-                v = XDP_DROP;      // src/fsx_kern.c:124-127
-            } else if (proto == 0x86DDu) {
-                if (L < 54u) v = XDP_DROP;  // parse_ip6hdr bound, src/fsx_kern.c:139-140
-                else {
-                    k[0] = (d5 >> 16) | (d6 << 16); k[1] = (d6 >> 16) | (d7 << 16);
-                    k[2] = (d7 >> 16) | (d8 << 16); k[3] = (d8 >> 16) | (d9 << 16);
-                    tag = 2;
-                    ip = true;
-                    any6 = 1;
-                }
-            } else if (proto == 0x0800u) {
-                if (L < 34u) v = XDP_DROP;  // parse_ip4hdr fixed 20-byte bound, :146-147
-                else {
-                    k[0] = (d6 >> 16) | (d7 << 16);  // bytes 26..29 raw
-                    tag = 1;
-                    ip = true;
-                }
-            }
-        }
+        uint32_t k[4] = {0, 0, 0, 0};
+        const uint32_t tag = live ? parse_src(L, d3, d5, d6, d7, d8, d9, k, v) : 0u;
+        const bool ip = tag != 0;
+        if (tag == 2) any6 = 1;
         uint64_t h = 0, hint = 0;
         if (ip) {
             h = id_start(idt, tag, k);
@@ -253,6 +393,20 @@ __global__ __launch_bounds__(256, 4) void k_parse(const uint8_t *__restrict__ hd
             // past the XCD's L2, which may still hold the head of an older epoch)
             hint = idt.coherent ? __hip_atomic_load(idt.head + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                                 : idt.head[h];
+        }
+        // heavy source? (LDS map of the batch's heavy set, while the hint is in flight)
+        int hidx = -1;
+        if (ip && nh) {
+            constexpr uint32_t kMapMask = (1u << kHeavyMapBits) - 1u;
+            uint32_t hh = (uint32_t)h & kMapMask;
+            for (uint32_t e; (e = s_hmap[hh]) != 0; hh = (hh + 1) & kMapMask) {
+                --e;
+                if (s_htag[e] == tag && s_hkey[e][0] == k[0] &&
+                    (tag == 1 || (s_hkey[e][1] == k[1] && s_hkey[e][2] == k[2] && s_hkey[e][3] == k[3]))) {
+                    hidx = (int)e;
+                    break;
+                }
+            }
         }
 #pragma unroll
         for (int q = 0; q < 4; ++q) { hv[q] = hn[q]; hn[q] = h2[q]; }
@@ -264,6 +418,9 @@ __global__ __launch_bounds__(256, 4) void k_parse(const uint8_t *__restrict__ hd
             const uint32_t id = id_resolve(idt, tag, k, h, hint, &fresh);
             if (id == kNoSlot) atomicOr(&bs->err, ERR_TABLE_FULL);
             out = ((uint64_t)(id & idt.mask) << 32) | ((uint64_t)(tag - 1u) << 31) | i;
+            if (dp.light_b)   // heavy-source sort: the first pass's bucket in bits 56..63
+                out |= (uint64_t)(hidx >= 0 ? dp.light_b + (uint32_t)hidx
+                                            : (uint32_t)(out >> 32) & (dp.light_b - 1u)) << 56;
         }
         nfresh += (uint32_t)__popcll(__ballot(fresh));   // new sources (persistent index)
         if (live) {
@@ -276,23 +433,21 @@ __global__ __launch_bounds__(256, 4) void k_parse(const uint8_t *__restrict__ hd
             maxts = T > maxts ? T : maxts;
             inv_mints = ~T > inv_mints ? ~T : inv_mints;
         }
-        // radix histograms of the 4 key digits: per-wave LDS counters (a heavy source
-        // repeats in few lanes of one 64-packet step, so same-address serialization
-        // stays short)
+        // radix histograms of the key digits: block LDS counters (a heavy source repeats
+        // in few lanes of one 64-packet step, so same-address serialization stays short)
         if (ghist && ip) {
-#pragma unroll
-            for (int dg = 0; dg < 4; ++dg)
-                atomicAdd(&s_hist[w][dg][(uint32_t)(out >> (32 + dbits * dg)) & dmask], 1u);
-            atomicAdd(&s_t0[w][(uint32_t)(out >> 32) & dmask], 1u);
+            const uint32_t d0 = (uint32_t)(out >> dp.shift[0]) & dp.mask[0];
+            atomicAdd(&s_hist[0][d0], 1u);
+            atomicAdd(&s_t0[d0], 1u);
+            if (hidx < 0)   // heavy entries are final after pass 0
+                for (uint32_t dg = 1; dg < dp.npass; ++dg)
+                    atomicAdd(&s_hist[dg][(uint32_t)(out >> dp.shift[dg]) & dp.mask[dg]], 1u);
         }
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         if (j == kSteps - 1 && thist) {   // sort tile done: its digit-0 counts, digit-major
             __syncthreads();
-            const uint32_t c = s_t0[0][threadIdx.x] + s_t0[1][threadIdx.x] + s_t0[2][threadIdx.x] +
-                               s_t0[3][threadIdx.x];
-            if (threadIdx.x <= dmask) thist[(size_t)threadIdx.x * tcap + tile] = c;
-#pragma unroll
-            for (int d = 0; d < 4; ++d) s_t0[d][threadIdx.x] = 0;
+            if (threadIdx.x <= dp.mask[0]) thist[(size_t)threadIdx.x * tcap + tile] = s_t0[threadIdx.x];
+            s_t0[threadIdx.x] = 0;
             __syncthreads();
         }
     }
@@ -300,8 +455,7 @@ __global__ __launch_bounds__(256, 4) void k_parse(const uint8_t *__restrict__ hd
         __syncthreads();
 #pragma unroll
         for (int dg = 0; dg < 4; ++dg) {
-            const uint32_t c = s_hist[0][dg][threadIdx.x] + s_hist[1][dg][threadIdx.x] +
-                               s_hist[2][dg][threadIdx.x] + s_hist[3][dg][threadIdx.x];
+            const uint32_t c = s_hist[dg][threadIdx.x];
             if (c) atomicAdd(&ghist[dg * 256 + threadIdx.x], c);
         }
     }
@@ -352,8 +506,10 @@ __global__ __launch_bounds__(256, 4) void k_parse(const uint8_t *__restrict__ hd
 // (scripts/micro/sort_micro.hip), more than the extra key read of k_tile_hist costs.
 
 // n_valid and the per-pass digit bases (exclusive scans of the k_parse histograms).
+// light_b: pass-0 buckets below it hold the light entries (256: all entries).
 __global__ __launch_bounds__(256) void k_hist_prep(const uint32_t *__restrict__ ghist,
-                                                   uint32_t *__restrict__ gbase, BatchState *bs) {
+                                                   uint32_t *__restrict__ gbase, BatchState *bs,
+                                                   uint32_t light_b) {
     __shared__ uint32_t s_tmp[4];
 #pragma unroll
     for (int dg = 0; dg < 4; ++dg) {
@@ -361,6 +517,8 @@ __global__ __launch_bounds__(256) void k_hist_prep(const uint32_t *__restrict__ 
         const uint32_t b = block256_excl(ghist[dg * 256 + threadIdx.x], s_tmp, &tot);
         gbase[dg * 256 + threadIdx.x] = b;
         if (dg == 0 && threadIdx.x == 0) bs->n_valid = tot;
+        if (dg == 0 && light_b == 256 && threadIdx.x == 0) bs->n_light = tot;
+        if (dg == 0 && light_b < 256 && threadIdx.x == light_b) bs->n_light = b;
     }
     if (threadIdx.x == 0)
         bs->pay_ok = bs->max_len < (1u << kPayLenBits) && bs->max_ts - ~bs->inv_min_ts < kPayTsRange;
@@ -769,7 +927,7 @@ __global__ __launch_bounds__(256) void k_heads_write(BatchState *bs, const uint8
         for (int k = 0; k < 16; ++k) {
             if ((f[k >> 2] >> (8 * (k & 3))) & 1u) {
                 seg_start[off] = p0 + k;
-                if (seg_slot) seg_slot[off] = (uint32_t)(S[p0 + k] >> 32);   // id = table slot
+                if (seg_slot) seg_slot[off] = pk_id(S[p0 + k]);   // id = table slot
                 ++off;
             }
         }
@@ -1395,13 +1553,33 @@ hipError_t launch_verdict_pipeline(const uint8_t *hdr, const uint32_t *len, cons
     while ((1ull << idbits) <= lim.table_mask) ++idbits;
     const int npass = std::max(1, (int)((idbits + 7) / 8));
     static const bool full_digits = getenv("FSX_SORT_FULL_DIGITS") != nullptr;   // A/B: 8,8,..,rest
+    static const bool no_heavy = getenv("FSX_NO_HEAVY_SORT") != nullptr;          // A/B: plain LSD
     const uint32_t dbits = full_digits ? 8u : std::max<uint32_t>(1, (idbits + npass - 1) / npass);
     const uint32_t dmask = (1u << dbits) - 1u;
+    // Heavy-source sort (3-pass tables of <= 2^23 slots): pass 0 buckets the light
+    // entries by a 7-bit id digit and every heavy source into a bucket of its own; passes
+    // 1-2 sort the light entries only, by the remaining id bits in two equal digits.
+    const bool heavy_sort = !onesweep && !full_digits && !no_heavy && npass == 3 && idbits <= 23;
+    DigitPlan dp{};
+    dp.npass = (uint32_t)npass;
+    if (heavy_sort) {
+        const uint32_t rest = idbits - 7, w1 = (rest + 1) / 2;
+        dp.light_b = 128;
+        dp.shift[0] = 56; dp.mask[0] = 255;
+        dp.shift[1] = 39; dp.mask[1] = (1u << w1) - 1u;
+        dp.shift[2] = 39 + w1; dp.mask[2] = (1u << (rest - w1)) - 1u;
+        k_heavy_sample<<<64, 256, 0, st>>>(hdr, len, n, sc.sketch, lim.seed, lim.table_mask, lim.test_flags);
+        k_heavy_pick<<<1, 1024, 0, st>>>(hdr, len, sc.sketch, sc.heavy, kHeavyMax, 16, lim.seed,
+                                         lim.table_mask, lim.test_flags);
+        mark("k_heavy_pick");
+    } else {
+        for (int p = 0; p < 4; ++p) { dp.shift[p] = 32u + dbits * (uint32_t)p; dp.mask[p] = dmask; }
+    }
     k_parse<<<std::min<uint32_t>(1024, ntiles), 256, 0, st>>>(
         hdr, len, ts, n, sc.packed[0], verdict, bs, idt, sc.sort_ctl, onesweep ? nullptr : sc.hist, tcap,
-        dbits);
+        dp, heavy_sort ? sc.heavy : nullptr);
     mark("k_parse");
-    k_hist_prep<<<1, 256, 0, st>>>(sc.sort_ctl, sc.gbase, bs);
+    k_hist_prep<<<1, 256, 0, st>>>(sc.sort_ctl, sc.gbase, bs, heavy_sort ? dp.light_b : 256u);
     if (do_limit) k_batch_check<<<1, 1, 0, st>>>(bs, tstate, lim);
     const uint32_t gen0 = onesweep ? next_generation() : 0u;
     for (int pass = 0; pass < npass; ++pass) {
@@ -1409,22 +1587,25 @@ hipError_t launch_verdict_pipeline(const uint8_t *hdr, const uint32_t *len, cons
         uint64_t *out = sc.packed[(pass + 1) & 1];
         const uint64_t *pin = pass == 0 ? nullptr : sc.pay[pass & 1];
         uint64_t *pout = sc.pay[(pass + 1) & 1];
-        const uint32_t shift = 32u + dbits * (uint32_t)pass;
-        const uint32_t *Ld = pass == 0 ? nullptr : &bs->n_valid;
+        const uint32_t shift = dp.shift[pass], pmask = dp.mask[pass];
         if (onesweep) {
-            k_onesweep<kLookW><<<ntiles, 256, 0, st>>>(in, out, n, Ld, shift, dmask, sc.gbase + 256 * pass,
+            const uint32_t *Ld = pass == 0 ? nullptr : &bs->n_valid;
+            k_onesweep<kLookW><<<ntiles, 256, 0, st>>>(in, out, n, Ld, shift, pmask, sc.gbase + 256 * pass,
                                                        sc.status, sc.sort_ctl + 1024 + pass,
                                                        gen0 + (uint32_t)pass, pass == 0, bs, pin, pout,
                                                        ts, len);
             mark("k_onesweep");
         } else {
+            // passes >= 1 cover [0, n_light): the heavy entries (pass 0's top buckets) are
+            // final in pass 0's output, which is also the last pass's (npass odd)
+            const uint32_t *Ld = pass == 0 ? nullptr : &bs->n_light;
             if (pass > 0) {   // pass 0's per-tile counts come from k_parse
-                k_tile_hist<<<ntiles, 256, 0, st>>>(in, n, Ld, shift, dmask, pass == 0, sc.hist, tcap);
+                k_tile_hist<<<ntiles, 256, 0, st>>>(in, n, Ld, shift, pmask, pass == 0, sc.hist, tcap);
                 mark("k_tile_hist");
             }
-            k_tile_scan<<<dmask + 1, 256, 0, st>>>(sc.hist, tcap, n, Ld, sc.gbase + 256 * pass);
+            k_tile_scan<<<pmask + 1, 256, 0, st>>>(sc.hist, tcap, n, Ld, sc.gbase + 256 * pass);
             mark("k_tile_scan");
-            k_tile_scatter<kLatePayDefault><<<ntiles, 256, 0, st>>>(in, out, n, Ld, shift, dmask, pass == 0, sc.hist, tcap, bs,
+            k_tile_scatter<kLatePayDefault><<<ntiles, 256, 0, st>>>(in, out, n, Ld, shift, pmask, pass == 0, sc.hist, tcap, bs,
                                                    pin, pout, ts, len);
             mark("k_tile_scatter");
         }

@@ -81,7 +81,7 @@ struct BatchState {
     uint64_t dropped;
     uint64_t inv_min_ts;  // ~(smallest timestamp): max-reduced from 0
     uint32_t pay_ok;      // sorted payload words valid (see kPayLenBits)
-    uint32_t pad_;
+    uint32_t n_light;     // entries of non-heavy sources: sort passes >= 1 cover [0, n_light)
 };
 
 // Sorted payload word carried through the onesweep passes next to each sort word:
@@ -182,14 +182,36 @@ __host__ __device__ inline uint64_t probe_start(uint32_t tag, const uint32_t k[4
     return slot_hash(tag, k, seed) & mask;
 }
 
-// packed sort word: source id << 32 | family << 31 | arrival index (n <= 2^31 - 1); the
-// source id is the source's slot in the per-batch id table (k_parse), so equal ids <=>
-// equal (family, address) and the sort needs only log2(slots) key bits
+// packed sort word: bucket << 56 | source id << 32 | family << 31 | arrival index
+// (n <= 2^31 - 1); the source id is the source's slot in the id table (k_parse), so equal
+// ids <=> equal (family, address) and the sort needs only log2(slots) key bits. The
+// bucket (heavy-source sort only, ids of <= 24 bits) is the first sort pass's digit: the
+// source's heavy index above the light digits, or digit 0 of its id (HeavySet).
 __host__ __device__ inline uint32_t pk_skey(uint64_t v) { return (uint32_t)(v >> 32); }
+__host__ __device__ inline uint32_t pk_id(uint64_t v) { return (uint32_t)(v >> 32) & 0x00FFFFFFu; }
 __host__ __device__ inline uint32_t pk_fam(uint64_t v) { return (uint32_t)(v >> 31) & 1u; }
 __host__ __device__ inline uint32_t pk_idx(uint64_t v) { return (uint32_t)v & 0x7FFFFFFFu; }
 
 // ------------------------------------------------------------ launchers (fsx_device.hip)
+// Heavy sources of a batch: up to kHeavyMax source keys picked from a
+// strided sample of the batch by k_heavy_sample / k_heavy_pick. Their packets get a
+// first-pass sort bucket of their own, so after that pass each of them is one run in
+// arrival order and the later passes sort only the other sources' entries. A wrong pick
+// costs time only: the grouping is exact for any set of keys.
+constexpr uint32_t kHeavyMax = 128;
+constexpr uint32_t kSketchBits = 12;
+constexpr uint32_t kSketch = 1u << kSketchBits;   // count sketch buckets
+constexpr uint32_t kHeavySample = 65536;           // sampled packets per batch
+constexpr uint32_t kHeavyMapBits = 10;
+struct HeavySet {
+    uint32_t n;
+    uint32_t tag[kHeavyMax];
+    uint32_t key[kHeavyMax][4];
+    // open addressing on the source's probe start (its table hash) modulo the map size:
+    // heavy index + 1, 0 empty
+    alignas(16) uint8_t map[1u << kHeavyMapBits];
+};
+
 struct Scratch {
     uint64_t *packed[2];
     uint64_t *pay[2];      // payload words in sort order (kPayLenBits)
@@ -214,6 +236,9 @@ struct Scratch {
     SwSeg *sw_seg;         // sliding window: per source (null for other limiters)
     uint32_t *id_tab;      // per-batch source ids: u64 heads [slots] then u32 IPv6 key
                            // words [slots][4] (generation-tagged, never cleared)
+    uint32_t *sketch;      // heavy-source sample: counts [kSketch], candidate packets [kSketch]
+                           // (counts zeroed by k_heavy_pick after use)
+    HeavySet *heavy;
     uint64_t cap;          // packets the scratch is sized for
 };
 
