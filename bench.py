@@ -320,7 +320,8 @@ def main():
         "limiters": limiters or None, "exchange": exchange,
         "kernels": [{"name": a, "ms_per_step": round(b, 4), "launches": c} for a, b, c in timings],
         "stats": {"allowed": stats[0], "dropped": stats[1], "sources": info["sources"],
-                  "malicious_sources": malicious}, "check": check,
+                  "light_packets": info["light_packets"], "malicious_sources": malicious},
+        "check": check,
     }
     print(json.dumps(out), flush=True)
     if dist:

@@ -717,10 +717,10 @@ int fsx_last_batch_info(fsx_ctx *c, uint64_t *info, int cap) {
     HIPCHK(c, hipStreamSynchronize(c->stream));
     BatchState h;
     HIPCHK(c, hipMemcpy(&h, c->bs, sizeof(h), hipMemcpyDeviceToHost));
-    const uint64_t v[11] = {h.n_valid, h.nseg, h.n_new, h.any_v6, h.nonmono, h.max_len,
-                            h.max_ts, h.allowed, h.dropped, h.n_fix, h.pay_ok};
+    const uint64_t v[12] = {h.n_valid, h.nseg, h.n_new, h.any_v6, h.nonmono, h.max_len,
+                            h.max_ts, h.allowed, h.dropped, h.n_fix, h.pay_ok, h.n_light};
     int k = 0;
-    for (; k < cap && k < 11; ++k) info[k] = v[k];
+    for (; k < cap && k < 12; ++k) info[k] = v[k];
     return k;
 }
 

@@ -371,7 +371,8 @@ class FsxContext:
         return keys[:m], fam[:m], feat[:m]
 
     BATCH_INFO = ("ip_packets", "sources", "new_sources", "any_ipv6", "non_monotone",
-                  "max_len", "max_ts", "allowed", "dropped", "v6_fix_runs", "sorted_payload")
+                  "max_len", "max_ts", "allowed", "dropped", "v6_fix_runs", "sorted_payload",
+                  "light_packets")
 
     def last_batch_info(self) -> dict:
         buf = (C.c_uint64 * len(self.BATCH_INFO))()

@@ -267,7 +267,8 @@ int fsx_pcap_records_device(fsx_ctx *ctx, const uint8_t *d_buf, const uint64_t *
  * [5] max frame length, [6] max timestamp, [7] allowed, [8] dropped, [9] IPv6
  * hash-collision runs fixed, [10] 1 when (ts, len) travelled with the sort as payload
  * words (timestamps within 2^40 ns of the batch minimum, frame lengths < 2^24), 0 when
- * they were gathered by index. Returns the number of entries written. */
+ * they were gathered by index, [11] IP packets of non-heavy sources (the entries the
+ * later sort passes covered). Returns the number of entries written. */
 int fsx_last_batch_info(fsx_ctx *ctx, uint64_t *info, int cap);
 
 /* Per-kernel device timing for the benchmark: while enabled, every batch records a

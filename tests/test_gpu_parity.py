@@ -290,6 +290,45 @@ def test_device_synth_and_device_batch(native, oracle):
         c.sync()
         vo = oracle.Oracle(max_entries=1 << 20).batch(hdr, ln, ts)
         assert np.array_equal(d_v.cpu().numpy(), vo)
+        info = c.last_batch_info()   # the heavy-source sort took the Zipf head out early
+        assert 0 < info["light_packets"] < info["ip_packets"] * 0.6
+
+
+# ------------------------------------------------------------------ heavy-source sort
+def _uniform_stream(rng, n, n_ips, dt_max=50):
+    from flowsentryx_amd import synth
+    ips = rng.integers(0, 2**32, n_ips, dtype=np.uint64).astype(np.uint32)
+    pick = rng.integers(0, n_ips, n)
+    ln = rng.integers(60, 1515, n).astype(np.uint32)
+    frames = [synth.frame_ipv4_udp(int(ips[j]).to_bytes(4, "big"), int(ln[i]))
+              for i, j in enumerate(pick)]
+    ts = 10**9 + np.cumsum(rng.integers(0, dt_max + 1, n)).astype(np.uint64)
+    return synth.records(frames), ln, ts
+
+
+@pytest.mark.parametrize("name", ["default", "tight"])
+def test_heavy_sort_mixed_families(native, oracle, name):
+    """Heavy IPv4 and IPv6 sources (DESIGN.md §3 heavy-source sort) across uneven batches."""
+    rng = np.random.default_rng(41)
+    hdr, ln, ts = rand_stream(rng, 200000, 3000, dt_max=40, v6_frac=0.5, nonip_frac=0.02,
+                              short_frac=0.01)
+    cuts = [0, 3, 70000, 70001, 200000]
+    batches = [(hdr[a:b], ln[a:b], ts[a:b]) for a, b in zip(cuts[:-1], cuts[1:])]
+    run_both(native, oracle, batches, CFGS[name])
+
+
+def test_heavy_sort_more_candidates_than_buckets(native, oracle):
+    """400 equally heavy sources: 128 of them get their own first-pass bucket, the rest
+    go through the light passes; same results either way."""
+    rng = np.random.default_rng(42)
+    hdr, ln, ts = _uniform_stream(rng, 120000, 400)
+    with gpu_ctx(native) as c:
+        vg = c.verdict_batch(hdr, ln, ts)
+        info = c.last_batch_info()
+        assert 0 < info["light_packets"] < info["ip_packets"]
+    o = oracle.Oracle(max_entries=1 << 18)
+    assert np.array_equal(vg, o.batch(hdr, ln, ts))
+    run_both(native, oracle, [(hdr, ln, ts)], CFGS["tight"])
 
 
 # ------------------------------------------------------------------ scoring
