@@ -190,10 +190,6 @@ __device__ __forceinline__ void flow_tiles(const uint64_t *__restrict__ S,
             sS[(e >> 4) * 17u + (e & 15u)] = p < M ? src[p] : 0ull;
         }
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        uint64_t v[16];
-#pragma unroll
-        for (int k = 0; k < 16; ++k) v[k] = sS[lane * 17u + k];
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         uint32_t hf[4] = {0, 0, 0, 0};
         if (p0 + 16 <= M) {
             const uint4 h4 = *reinterpret_cast<const uint4 *>(headf + p0);
@@ -201,21 +197,24 @@ __device__ __forceinline__ void flow_tiles(const uint64_t *__restrict__ S,
         } else {
             for (uint32_t k = 0; k < 16 && p0 + k < M; ++k) hf[k >> 2] |= (uint32_t)headf[p0 + k] << (8 * (k & 3));
         }
-        uint32_t L[16];
-        uint64_t T[16];
-#pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            const bool ok = p0 + k < M;
+        // (len, ts) of the lane's position k, read from the LDS row when needed (holding
+        // all 16 in registers halved the occupancy)
+        auto LT = [&](int k, uint32_t &Lk, uint64_t &Tk) {
+            const uint64_t v = sS[lane * 17u + (uint32_t)k];
+            const bool ok = p0 + (uint32_t)k < M;
             if constexpr (kPay) {
-                L[k] = ok ? (uint32_t)v[k] & ((1u << kPayLenBits) - 1u) : 0u;
-                T[k] = ok ? v[k] >> kPayLenBits : 0ull;
+                Lk = ok ? (uint32_t)v & ((1u << kPayLenBits) - 1u) : 0u;
+                Tk = ok ? v >> kPayLenBits : 0ull;
             } else {
-                const uint32_t idx = pk_idx(v[k]);
-                L[k] = ok ? len[idx] : 0u;
-                T[k] = ok ? ts[idx] : 0ull;
+                const uint32_t idx = pk_idx(v);
+                Lk = ok ? len[idx] : 0u;
+                Tk = ok ? ts[idx] : 0ull;
             }
-        }
-        uint64_t tprev = __shfl_up(T[15], 1);
+        };
+        uint32_t L15;
+        uint64_t T15;
+        LT(15, L15, T15);
+        uint64_t tprev = __shfl_up(T15, 1);
         if (lane == 0) {
             if constexpr (kPay) tprev = (p0 > 0 && p0 < M) ? pay[p0 - 1] >> kPayLenBits : 0ull;
             else tprev = (p0 > 0 && p0 < M) ? ts[pk_idx(S[p0 - 1])] : 0ull;
@@ -235,6 +234,9 @@ __device__ __forceinline__ void flow_tiles(const uint64_t *__restrict__ S,
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
             if (p0 + k < M) {
+                uint32_t Lk;
+                uint64_t Tk;
+                LT(k, Lk, Tk);
                 const bool h = (hf[k >> 2] >> (8 * (k & 3))) & 1u;
                 if (h) {
                     if (seen == 0) F = A;
@@ -243,13 +245,13 @@ __device__ __forceinline__ void flow_tiles(const uint64_t *__restrict__ S,
                     A = acc_zero();
                 }
                 FlowAcc c = acc_zero();
-                c.n = 1; c.s1 = L[k]; c.s2 = (u128)L[k] * L[k];
+                c.n = 1; c.s1 = Lk; c.s2 = (u128)Lk * Lk;
                 if (!h) {
-                    const uint64_t d = T[k] - tprev;
+                    const uint64_t d = Tk - tprev;
                     c.d1 = d; c.d2 = (u128)d * d; c.dmax = d;
                 }
                 acc_add(A, c);
-                tprev = T[k];
+                tprev = Tk;
             }
         }
         if (nh == 0) F = A;
@@ -292,7 +294,10 @@ __device__ __forceinline__ void flow_tiles(const uint64_t *__restrict__ S,
     }
 }
 
-__global__ __launch_bounds__(256) void k_flow_tile(const uint64_t *__restrict__ S,
+#ifndef FSX_FLOW_MINB
+#define FSX_FLOW_MINB 4   // waves/SIMD bound of k_flow_tile (A/B: scripts/build_variant.sh)
+#endif
+__global__ __launch_bounds__(256, FSX_FLOW_MINB) void k_flow_tile(const uint64_t *__restrict__ S,
                                                    const uint64_t *__restrict__ pay, BatchState *bs,
                                                    const uint8_t *__restrict__ headf,
                                                    const uint32_t *__restrict__ len,
