@@ -129,6 +129,7 @@ static void free_scratch(fsx_ctx *c) {
     hipFree(s.seg_order); hipFree(s.sub_cnt); hipFree(s.flow_first); hipFree(s.flow_last);
     hipFree(s.span_list); hipFree(s.sort_ctl); hipFree(s.gbase); hipFree(s.status);
     hipFree(s.lim_tiles); hipFree(s.sw_seg); hipFree(s.sketch); hipFree(s.heavy);
+    hipFree(s.drop_list); hipFree(s.drop_cur);
     s = Scratch{};
 }
 
@@ -163,6 +164,10 @@ static int alloc_scratch(fsx_ctx *c, uint64_t cap) {
     s.lim_tiles_n = cap / kTile + 2;
     HIPCHK(c, hipMalloc(&s.lim_tiles, s.lim_tiles_n * 4 * 8));
     if (c->cfg.limiter == FSX_LIMIT_SLIDING_WINDOW) HIPCHK(c, hipMalloc(&s.sw_seg, cap * sizeof(SwSeg)));
+    const uint64_t nchunks = (cap + kVChunk - 1) / kVChunk;
+    HIPCHK(c, hipMalloc(&s.drop_list, nchunks * kVChunk * 4));
+    HIPCHK(c, hipMalloc(&s.drop_cur, nchunks * 4));
+    HIPCHK(c, hipMemset(s.drop_cur, 0, nchunks * 4));
     HIPCHK(c, hipMalloc(&s.sketch, 2 * kSketch * 4));
     HIPCHK(c, hipMemset(s.sketch, 0, 2 * kSketch * 4));
     HIPCHK(c, hipMalloc(&s.heavy, sizeof(HeavySet)));

@@ -1424,10 +1424,16 @@ __global__ __launch_bounds__(1024) void k_fill_carry(uint8_t *__restrict__ tile_
     }
 }
 
+// Fill + DROP collection: the verdict of every sorted position (last mark at or before
+// it), counted into stats_map; DROP positions append their arrival index to the list of
+// their arrival chunk (one cursor add per chunk and wave: a heavy source's run of drops
+// lands in few chunks), so k_verdict_apply writes the verdict bytes chunk by chunk
+// instead of one scattered byte store per drop.
 __global__ __launch_bounds__(256) void k_fill_scatter(const uint8_t *__restrict__ marks,
                                                       const uint64_t *__restrict__ S, BatchState *bs,
                                                       const uint8_t *__restrict__ carry,
-                                                      uint8_t *__restrict__ verdict,
+                                                      uint32_t *__restrict__ drop_list,
+                                                      uint32_t *__restrict__ drop_cur,
                                                       TableState *tstate) {
     __shared__ uint8_t s_v[kTile];
     __shared__ uint32_t s_w[4];
@@ -1465,11 +1471,28 @@ __global__ __launch_bounds__(256) void k_fill_scatter(const uint8_t *__restrict_
         }
         __syncthreads();
         const uint32_t tile0 = t * kTile;
-        for (uint32_t j = threadIdx.x; j < kTile && tile0 + j < M; j += 256) {
-            const uint8_t v = s_v[j];
-            if (v == XDP_DROP) verdict[pk_idx(S[tile0 + j])] = v;
+        const uint64_t lt = (1ull << lane) - 1ull;
+        for (uint32_t j0 = 0; j0 < kTile && tile0 + j0 < M; j0 += 256) {   // block-uniform trips
+            const uint32_t j = j0 + threadIdx.x;
+            const bool ok = tile0 + j < M;
+            const uint8_t v = ok ? s_v[j] : 0;
             n_pass += v == XDP_PASS;
             n_drop += v == XDP_DROP;
+            const bool drop = v == XDP_DROP;
+            const uint32_t idx = drop ? pk_idx(S[tile0 + j]) : 0u;
+            const uint32_t ch = idx >> kVChunkBits;
+            uint64_t pending = __ballot(drop);
+            while (pending) {
+                const int lead = __ffsll((unsigned long long)pending) - 1;
+                const uint32_t lc = __shfl(ch, lead);
+                const uint64_t same = __ballot(drop && ch == lc) & pending;
+                uint32_t base = 0;
+                if ((int)lane == lead) base = atomicAdd(&drop_cur[lc], (uint32_t)__popcll(same));
+                base = __shfl(base, lead);
+                if ((same >> lane) & 1ull)
+                    drop_list[(size_t)lc * kVChunk + base + (uint32_t)__popcll(same & lt)] = idx;
+                pending &= ~same;
+            }
         }
         __syncthreads();
     }
@@ -1488,6 +1511,40 @@ __global__ __launch_bounds__(256) void k_fill_scatter(const uint8_t *__restrict_
             atomicAdd(reinterpret_cast<unsigned long long *>(&tstate->stats[1]), d);
             atomicAdd(reinterpret_cast<unsigned long long *>(&bs->dropped), d);
         }
+    }
+}
+
+// One block per arrival chunk of kVChunk verdict bytes: the chunk through LDS, its DROP
+// list applied, written back with 16-byte stores (IP packets were written PASS by
+// k_parse). Resets the chunk's cursor for the next batch.
+__global__ __launch_bounds__(256) void k_verdict_apply(uint8_t *__restrict__ verdict, uint32_t n,
+                                                       const uint32_t *__restrict__ drop_list,
+                                                       uint32_t *__restrict__ drop_cur,
+                                                       const BatchState *bs) {
+    __shared__ uint4 s_v4[kVChunk / 16];
+    uint8_t *s_v = reinterpret_cast<uint8_t *>(s_v4);
+    const uint32_t c = blockIdx.x;
+    const uint32_t cnt = drop_cur[c];
+    __syncthreads();
+    if (threadIdx.x == 0) drop_cur[c] = 0;
+    if (cnt == 0 || bs->err) return;
+    const uint32_t b0 = c * kVChunk, nb = min(kVChunk, n - b0);
+    const bool vec = ((reinterpret_cast<uintptr_t>(verdict) & 15u) == 0) && nb == kVChunk;
+    if (vec) {
+        const uint4 *src = reinterpret_cast<const uint4 *>(verdict + b0);
+        for (uint32_t q = threadIdx.x; q < kVChunk / 16; q += 256) s_v4[q] = src[q];
+    } else {
+        for (uint32_t q = threadIdx.x; q < nb; q += 256) s_v[q] = verdict[b0 + q];
+    }
+    __syncthreads();
+    const uint32_t *lst = drop_list + (size_t)c * kVChunk;
+    for (uint32_t q = threadIdx.x; q < cnt; q += 256) s_v[lst[q] - b0] = XDP_DROP;
+    __syncthreads();
+    if (vec) {
+        uint4 *dst = reinterpret_cast<uint4 *>(verdict + b0);
+        for (uint32_t q = threadIdx.x; q < kVChunk / 16; q += 256) dst[q] = s_v4[q];
+    } else {
+        for (uint32_t q = threadIdx.x; q < nb; q += 256) verdict[b0 + q] = s_v[q];
     }
 }
 
@@ -1675,8 +1732,11 @@ hipError_t launch_verdict_pipeline(const uint8_t *hdr, const uint32_t *len, cons
     k_fill_last<<<gridTiles, 256, 0, st>>>(sc.marks, bs, sc.tile_last);
     k_fill_carry<<<1, 1024, 0, st>>>(sc.tile_last, bs);
     mark("k_fill_last");
-    k_fill_scatter<<<gridTiles, 256, 0, st>>>(sc.marks, S, bs, sc.tile_last, verdict, tstate);
+    k_fill_scatter<<<gridTiles, 256, 0, st>>>(sc.marks, S, bs, sc.tile_last, sc.drop_list, sc.drop_cur,
+                                              tstate);
     mark("k_fill_scatter");
+    k_verdict_apply<<<cdiv(n, kVChunk), 256, 0, st>>>(verdict, n, sc.drop_list, sc.drop_cur, bs);
+    mark("k_verdict_apply");
     if (fork && (e = hipStreamWaitEvent(st, join_ev, 0)) != hipSuccess) return e;
     return hipGetLastError();
 }

@@ -25,6 +25,8 @@ constexpr int kSortItems = 16;
 constexpr int kSortTile = kSortThreads * kSortItems;  // 4096
 constexpr int kSortMaxBlocks = 2048;
 constexpr int kTile = 4096;                            // fill / compaction tile
+constexpr uint32_t kVChunkBits = 14;
+constexpr uint32_t kVChunk = 1u << kVChunkBits;         // verdict bytes per k_verdict_apply block
 
 enum : uint32_t {
     ERR_TABLE_FULL = 1u,
@@ -236,6 +238,8 @@ struct Scratch {
     SwSeg *sw_seg;         // sliding window: per source (null for other limiters)
     uint32_t *id_tab;      // per-batch source ids: u64 heads [slots] then u32 IPv6 key
                            // words [slots][4] (generation-tagged, never cleared)
+    uint32_t *drop_list;   // DROP verdicts by arrival chunk: chunk c owns [c, c + 1) * kVChunk
+    uint32_t *drop_cur;    // entries per chunk (zeroed by k_verdict_apply after use)
     uint32_t *sketch;      // heavy-source sample: counts [kSketch], candidate packets [kSketch]
                            // (counts zeroed by k_heavy_pick after use)
     HeavySet *heavy;
