@@ -162,8 +162,6 @@ def main():
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
-    ctx.enable_timing(True)
-    ctx.last_timings()  # reset accumulators
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
@@ -172,6 +170,14 @@ def main():
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    # per-kernel device times (a HIP event after every kernel) from separate steps, so the
+    # timed steps above carry no event records
+    ctx.enable_timing(True)
+    ctx.last_timings()  # reset accumulators
+    for _ in range(max(1, min(args.steps, 5))):
+        step()
+    ctx.sync()
+    torch.cuda.synchronize()
     timings = ctx.last_timings()
     ctx.enable_timing(False)
     if dist:
