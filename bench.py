@@ -58,7 +58,8 @@ def parse_args():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", type=int, default=2)
     ap.add_argument("--packets", type=int, default=None, help="packets per rank (default: config)")
-    ap.add_argument("--cpu-sample", type=int, default=16 << 20)
+    ap.add_argument("--cpu-sample", type=int, default=64 << 20,
+                    help="packets of the CPU baseline sample (default: the whole config-2 stream)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--check", action="store_true", help="verify a prefix against the oracle")
