@@ -749,8 +749,7 @@ int fsx_shard_pack_device(fsx_ctx *c, const uint8_t *d_hdr, const uint32_t *d_le
     if (rc) return rc;
     const uint64_t need = (uint64_t)G * (n / 4096 + 1);
     if (need > c->shard_cnt_cap) {
-        hipFree(c->d_shard_cnt); hipFree(c->d_rep);
-    hipFree(c->idx_heads); hipFree(c->idx_k6);
+        hipFree(c->d_shard_cnt);
         c->d_shard_cnt = nullptr;
         c->shard_cnt_cap = 0;
         HIPCHK(c, hipMalloc(&c->d_shard_cnt, need * 4));
