@@ -757,9 +757,9 @@ int fsx_shard_pack_device(fsx_ctx *c, const uint8_t *d_hdr, const uint32_t *d_le
     }
     const Replica rep{c->d_rep, c->rep_slots ? c->rep_slots - 1 : 0};
     const bool filt = (flags & FSX_SHARD_FILTER_BLOCKLIST) && c->rep_valid;
-    hipError_t e = launch_shard_pack(d_hdr, d_len, d_ts, (uint32_t)n, G, d_verdict,
-                                     reinterpret_cast<ShardRecord *>(d_records), d_send_idx, d_counts,
-                                     c->d_shard_cnt, filt ? &rep : nullptr, c->stream);
+    const bool compact = (flags & FSX_SHARD_COMPACT) != 0;
+    hipError_t e = launch_shard_pack(d_hdr, d_len, d_ts, (uint32_t)n, G, d_verdict, d_records, d_send_idx,
+                                     d_counts, c->d_shard_cnt, filt ? &rep : nullptr, compact, c->stream);
     if (e != hipSuccess) return set_err(c, -EIO, "shard pack: %s", hipGetErrorString(e));
     return 0;
 }
@@ -809,17 +809,26 @@ int fsx_blocklist_replica_device(fsx_ctx *c, const void *d_entries, size_t m) {
     return 0;
 }
 
-int fsx_shard_unpack_device(fsx_ctx *c, const void *d_records, size_t m, uint8_t *d_hdr, uint32_t *d_len,
-                            uint64_t *d_ts) {
+static int shard_unpack(fsx_ctx *c, const void *d_records, uint32_t rec_bytes, size_t m, uint8_t *d_hdr,
+                        uint32_t *d_len, uint64_t *d_ts) {
     if (!c) return -EINVAL;
     if (m > kMaxBatchLimit) return set_err(c, -E2BIG, "m=%zu too large", m);
     if (m && (!d_records || !d_hdr || !d_len || !d_ts)) return set_err(c, -EINVAL, "null buffer");
     int rc = sel(c);
     if (rc) return rc;
-    hipError_t e = launch_shard_unpack(reinterpret_cast<const ShardRecord *>(d_records), (uint32_t)m, d_hdr,
-                                       d_len, d_ts, c->stream);
+    hipError_t e = launch_shard_unpack(d_records, rec_bytes, (uint32_t)m, d_hdr, d_len, d_ts, c->stream);
     if (e != hipSuccess) return set_err(c, -EIO, "shard unpack: %s", hipGetErrorString(e));
     return 0;
+}
+
+int fsx_shard_unpack_device(fsx_ctx *c, const void *d_records, size_t m, uint8_t *d_hdr, uint32_t *d_len,
+                            uint64_t *d_ts) {
+    return shard_unpack(c, d_records, FSX_SHARD_RECORD_BYTES, m, d_hdr, d_len, d_ts);
+}
+
+int fsx_shard_unpack16_device(fsx_ctx *c, const void *d_records, size_t m, uint8_t *d_hdr, uint32_t *d_len,
+                              uint64_t *d_ts) {
+    return shard_unpack(c, d_records, FSX_SHARD_RECORD16_BYTES, m, d_hdr, d_len, d_ts);
 }
 
 int fsx_shard_scatter_device(fsx_ctx *c, const uint8_t *d_ret, const uint32_t *d_send_idx, size_t m,

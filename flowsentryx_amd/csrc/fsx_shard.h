@@ -19,6 +19,16 @@ struct alignas(16) ShardRecord {
 };
 static_assert(sizeof(ShardRecord) == 32, "32-byte exchange records");
 
+// Compact record of an IPv4 packet: a sender whose slice has no IPv6 source and no frame
+// of 64 KiB or more ships these instead (half the all-to-all volume of the common case).
+struct alignas(16) ShardRecord16 {
+    uint32_t key;         // raw IPv4 source address
+    uint16_t len;         // frame length
+    uint16_t dport;       // L4 destination port (host order; 0 when absent)
+    uint64_t ts;          // arrival time (ns)
+};
+static_assert(sizeof(ShardRecord16) == 16, "16-byte compact records");
+
 constexpr uint64_t kShardSeed = 0x5A4D0F5EED5ull;   // fixed: every rank must agree
 
 // One blacklist entry of the replicated blocklist (all-gathered between ranks).
@@ -37,6 +47,7 @@ struct Replica {
 };
 
 constexpr uint32_t kShardFilter = 1u;   // fsx_shard_pack_device flag (FSX_SHARD_FILTER_BLOCKLIST)
+constexpr uint32_t kShardCompact = 2u;  // fsx_shard_pack_device flag (FSX_SHARD_COMPACT)
 
 // owner = floor(h * G / 2^32) of a 32-bit mix of (family tag, address).
 __host__ __device__ inline uint32_t shard_owner_of(uint32_t tag, const uint32_t k[4], uint32_t G) {
@@ -44,16 +55,17 @@ __host__ __device__ inline uint32_t shard_owner_of(uint32_t tag, const uint32_t 
     return (uint32_t)(((h >> 32) * (uint64_t)G) >> 32);
 }
 
+// owner_total: [G] per-owner records, [G] replica drops, [G + 1] (compact only) record bytes.
 hipError_t launch_shard_pack(const uint8_t *hdr, const uint32_t *len, const uint64_t *ts, uint32_t n,
-                             uint32_t G, uint8_t *verdict, ShardRecord *rec, uint32_t *send_idx,
+                             uint32_t G, uint8_t *verdict, void *rec, uint32_t *send_idx,
                              uint64_t *owner_total, uint32_t *scratch, const Replica *rep,
-                             hipStream_t st);
+                             bool compact, hipStream_t st);
 hipError_t launch_shard_clock(const uint64_t *ts, uint32_t n, uint64_t *out3, hipStream_t st);
 hipError_t launch_blocklist_export(const Slot *table, uint64_t table_mask, ShardBlock *out, uint64_t cap,
                                    unsigned long long *count, hipStream_t st);
 hipError_t launch_replica_build(const ShardBlock *in, uint64_t m, ShardBlock *slots, uint64_t mask,
                                 hipStream_t st);
-hipError_t launch_shard_unpack(const ShardRecord *rec, uint32_t m, uint8_t *hdr, uint32_t *len,
+hipError_t launch_shard_unpack(const void *rec, uint32_t rec_bytes, uint32_t m, uint8_t *hdr, uint32_t *len,
                                uint64_t *ts, hipStream_t st);
 hipError_t launch_shard_scatter(const uint8_t *ret, const uint32_t *send_idx, uint32_t m, uint8_t *verdict,
                                 hipStream_t st);

@@ -7,7 +7,9 @@
 //                     packet; per-tile per-owner counts
 //   k_shard_scan      exclusive scan over (owner, tile) -> send offsets, per-owner totals
 //   k_shard_pack      stable partition by owner into 32-byte records {src key, ts, len,
-//                     L4 dst port, family}; local verdicts for the packets that never
+//                     L4 dst port, family} (16-byte {IPv4 key, len, dport, ts} when the
+//                     caller allows it and the slice has no IPv6 source and no frame of
+//                     64 KiB or more); local verdicts for the packets that never
 //                     reach a limiter (short frames DROP, non-IP PASS: src/fsx_kern.c:
 //                     123-131); for each send slot the local packet index
 //   (RCCL all-to-all of the records, host side: flowsentryx_amd/shard.py)
@@ -95,30 +97,40 @@ __device__ __forceinline__ uint32_t shard_classify(const uint8_t *rec, uint32_t 
 }
 
 // Per tile: per-owner IP-packet counts, owner-major [G][tiles].
+// wide: (compact requests only) set when an IP packet needs the 32-byte record.
 __global__ __launch_bounds__(256) void k_shard_count(const uint8_t *__restrict__ hdr,
                                                      const uint32_t *__restrict__ len,
                                                      const uint64_t *__restrict__ ts, uint32_t n,
                                                      uint32_t G, uint32_t *__restrict__ cnt,
-                                                     uint32_t ntiles, Replica rep, int use_rep) {
+                                                     uint32_t ntiles, Replica rep, int use_rep,
+                                                     unsigned long long *wide) {
     __shared__ uint32_t sh[kMaxShards];
     const uint32_t t = blockIdx.x;
     if (threadIdx.x < kMaxShards) sh[threadIdx.x] = 0;
     __syncthreads();
+    bool need_wide = false;
     for (uint32_t r = 0; r < 16; ++r) {
         const uint32_t i = t * kShardTile + r * 256u + threadIdx.x;
         if (i >= n) break;
         uint32_t k[4], dp;
-        const uint32_t f = shard_classify(hdr + (size_t)i * 64, len[i], ts[i], use_rep ? &rep : nullptr, k, dp);
-        if (f >= 4) atomicAdd(&sh[owner_dev(f, k, G)], 1u);
+        const uint32_t L = len[i];
+        const uint32_t f = shard_classify(hdr + (size_t)i * 64, L, ts[i], use_rep ? &rep : nullptr, k, dp);
+        if (f >= 4) {
+            atomicAdd(&sh[owner_dev(f, k, G)], 1u);
+            need_wide |= f == 6 || L > 0xFFFFu;
+        }
     }
+    if (wide && __ballot(need_wide) && lane_id() == 0) atomicOr(wide, 1ull);
     __syncthreads();
     if (threadIdx.x < G) cnt[(size_t)threadIdx.x * ntiles + t] = sh[threadIdx.x];
 }
 
+__global__ void k_shard_fmt_init(unsigned long long *wide) { *wide = 0; }
+
 // One block: exclusive scan of cnt in owner-major order (in place) and per-owner totals.
 __global__ __launch_bounds__(1024) void k_shard_scan(uint32_t *__restrict__ cnt, uint64_t total_n,
                                                      uint64_t *__restrict__ owner_total,
-                                                     uint32_t G, uint32_t ntiles) {
+                                                     uint32_t G, uint32_t ntiles, int compact) {
     __shared__ uint32_t s_w[16];
     __shared__ uint32_t s_carry;
     const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
@@ -148,7 +160,11 @@ __global__ __launch_bounds__(1024) void k_shard_scan(uint32_t *__restrict__ cnt,
         const uint32_t b1 = o + 1 < G ? cnt[(size_t)(o + 1) * ntiles] : s_carry;
         owner_total[o] = b1 - b0;
     }
-    if (threadIdx.x == 0) owner_total[G] = 0;   // packets dropped by the replica (k_shard_pack)
+    if (threadIdx.x == 0) {
+        owner_total[G] = 0;   // packets dropped by the replica (k_shard_pack)
+        // compact requests: the wide flag of k_shard_count becomes the record size
+        if (compact) owner_total[G + 1] = owner_total[G + 1] ? 32u : 16u;
+    }
 }
 
 // Per tile: stable (arrival order) placement of every IP packet at its owner's offset.
@@ -156,10 +172,12 @@ __global__ __launch_bounds__(256) void k_shard_pack(const uint8_t *__restrict__ 
                                                     const uint32_t *__restrict__ len,
                                                     const uint64_t *__restrict__ ts, uint32_t n,
                                                     uint32_t G, const uint32_t *__restrict__ offs,
-                                                    uint32_t ntiles, ShardRecord *__restrict__ rec,
+                                                    uint32_t ntiles, void *__restrict__ rec,
                                                     uint32_t *__restrict__ send_idx,
                                                     uint8_t *__restrict__ verdict, Replica rep,
-                                                    int use_rep, uint64_t *__restrict__ owner_total) {
+                                                    int use_rep, uint64_t *__restrict__ owner_total,
+                                                    int compact) {
+    const bool rec16 = compact && owner_total[G + 1] == 16u;
     __shared__ uint32_t s_base[kMaxShards];
     __shared__ uint32_t s_wc[4][kMaxShards];
     __shared__ uint32_t s_filtered;
@@ -228,14 +246,23 @@ __global__ __launch_bounds__(256) void k_shard_pack(const uint8_t *__restrict__ 
             uint32_t k[4], dp;
             shard_parse(hdr + (size_t)i * 64, len[i], k, dp);
             const uint32_t slot = base + below;
-            ShardRecord x;
-            x.key[0] = k[0]; x.key[1] = k[1]; x.key[2] = k[2]; x.key[3] = k[3];
-            x.ts = ts[i];
-            x.len = len[i];
-            x.dport = (uint16_t)dp;
-            x.family = (uint8_t)f;
-            x.pad = 0;
-            rec[slot] = x;
+            if (rec16) {
+                ShardRecord16 x;
+                x.key = k[0];
+                x.len = (uint16_t)len[i];
+                x.dport = (uint16_t)dp;
+                x.ts = ts[i];
+                reinterpret_cast<ShardRecord16 *>(rec)[slot] = x;
+            } else {
+                ShardRecord x;
+                x.key[0] = k[0]; x.key[1] = k[1]; x.key[2] = k[2]; x.key[3] = k[3];
+                x.ts = ts[i];
+                x.len = len[i];
+                x.dport = (uint16_t)dp;
+                x.family = (uint8_t)f;
+                x.pad = 0;
+                reinterpret_cast<ShardRecord *>(rec)[slot] = x;
+            }
             send_idx[slot] = i;
             verdict[i] = 2u;   // placeholder until the owner's verdict returns
         }
@@ -244,12 +271,25 @@ __global__ __launch_bounds__(256) void k_shard_pack(const uint8_t *__restrict__ 
 
 // Owner side: 32-byte records -> header records that parse to the same key, family and
 // dst port, frame length and timestamp.
-__global__ __launch_bounds__(256) void k_shard_unpack(const ShardRecord *__restrict__ rec, uint32_t m,
+__device__ __forceinline__ ShardRecord widen(const ShardRecord &x) { return x; }
+__device__ __forceinline__ ShardRecord widen(const ShardRecord16 &c) {
+    ShardRecord x;
+    x.key[0] = c.key; x.key[1] = x.key[2] = x.key[3] = 0;
+    x.ts = c.ts;
+    x.len = c.len;
+    x.dport = c.dport;
+    x.family = 4;
+    x.pad = 0;
+    return x;
+}
+
+template <class R>
+__global__ __launch_bounds__(256) void k_shard_unpack(const R *__restrict__ rec, uint32_t m,
                                                       uint8_t *__restrict__ hdr,
                                                       uint32_t *__restrict__ len,
                                                       uint64_t *__restrict__ ts) {
     for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < m; i += gridDim.x * 256u) {
-        const ShardRecord x = rec[i];
+        const ShardRecord x = widen(rec[i]);
         uint32_t d[16];
 #pragma unroll
         for (int k = 0; k < 16; ++k) d[k] = 0;
@@ -286,19 +326,29 @@ __global__ __launch_bounds__(256) void k_shard_scatter(const uint8_t *__restrict
         verdict[send_idx[i]] = ret[i];
 }
 
+__global__ void k_shard_empty(uint64_t *owner_total, uint32_t G, int compact) {
+    for (uint32_t o = 0; o <= G; ++o) owner_total[o] = 0;
+    if (compact) owner_total[G + 1] = 16u;
+}
+
 hipError_t launch_shard_pack(const uint8_t *hdr, const uint32_t *len, const uint64_t *ts, uint32_t n,
-                             uint32_t G, uint8_t *verdict, ShardRecord *rec, uint32_t *send_idx,
+                             uint32_t G, uint8_t *verdict, void *rec, uint32_t *send_idx,
                              uint64_t *owner_total, uint32_t *scratch, const Replica *rep,
-                             hipStream_t st) {
+                             bool compact, hipStream_t st) {
     (void)hipGetLastError();   // a stale error of another caller is not ours
-    if (n == 0) return hipMemsetAsync(owner_total, 0, (size_t)(G + 1) * 8, st);
+    if (n == 0) {
+        k_shard_empty<<<1, 1, 0, st>>>(owner_total, G, compact);
+        return hipGetLastError();
+    }
     const uint32_t ntiles = (n + kShardTile - 1) / kShardTile;
     const Replica r = rep ? *rep : Replica{nullptr, 0};
     const int use = rep != nullptr && rep->slots != nullptr;
-    k_shard_count<<<ntiles, 256, 0, st>>>(hdr, len, ts, n, G, scratch, ntiles, r, use);
-    k_shard_scan<<<1, 1024, 0, st>>>(scratch, n, owner_total, G, ntiles);
+    unsigned long long *wide = compact ? reinterpret_cast<unsigned long long *>(owner_total + G + 1) : nullptr;
+    if (wide) k_shard_fmt_init<<<1, 1, 0, st>>>(wide);
+    k_shard_count<<<ntiles, 256, 0, st>>>(hdr, len, ts, n, G, scratch, ntiles, r, use, wide);
+    k_shard_scan<<<1, 1024, 0, st>>>(scratch, n, owner_total, G, ntiles, compact);
     k_shard_pack<<<ntiles, 256, 0, st>>>(hdr, len, ts, n, G, scratch, ntiles, rec, send_idx, verdict, r,
-                                         use, owner_total);
+                                         use, owner_total, compact);
     return hipGetLastError();
 }
 
@@ -394,12 +444,15 @@ hipError_t launch_replica_build(const ShardBlock *in, uint64_t m, ShardBlock *sl
     return hipGetLastError();
 }
 
-hipError_t launch_shard_unpack(const ShardRecord *rec, uint32_t m, uint8_t *hdr, uint32_t *len,
+hipError_t launch_shard_unpack(const void *rec, uint32_t rec_bytes, uint32_t m, uint8_t *hdr, uint32_t *len,
                                uint64_t *ts, hipStream_t st) {
     (void)hipGetLastError();   // a stale error of another caller is not ours
     if (m == 0) return hipSuccess;
     const uint32_t grid = std::min<uint32_t>(4096, (m + 255) / 256);
-    k_shard_unpack<<<grid, 256, 0, st>>>(rec, m, hdr, len, ts);
+    if (rec_bytes == 16)
+        k_shard_unpack<<<grid, 256, 0, st>>>(reinterpret_cast<const ShardRecord16 *>(rec), m, hdr, len, ts);
+    else
+        k_shard_unpack<<<grid, 256, 0, st>>>(reinterpret_cast<const ShardRecord *>(rec), m, hdr, len, ts);
     return hipGetLastError();
 }
 

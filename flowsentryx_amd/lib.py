@@ -136,6 +136,7 @@ def load_library() -> C.CDLL:
         "fsx_blocklist_export_device": (C.c_int, [vp, vp, sz, vp]),
         "fsx_blocklist_replica_device": (C.c_int, [vp, vp, sz]),
         "fsx_shard_unpack_device": (C.c_int, [vp, vp, sz, vp, vp, vp]),
+        "fsx_shard_unpack16_device": (C.c_int, [vp, vp, sz, vp, vp, vp]),
         "fsx_shard_scatter_device": (C.c_int, [vp, vp, vp, sz, vp]),
     }
     for name, (res, args) in sig.items():
@@ -154,14 +155,16 @@ ABI_SYMBOLS = [
     "fsx_map_lookup", "fsx_map_update", "fsx_map_delete", "fsx_map_dump", "fsx_get_stats",
     "fsx_reset", "fsx_load_q8_model", "fsx_score", "fsx_score_device", "fsx_flow_features",
     "fsx_last_timings", "fsx_enable_timing", "fsx_last_batch_info",
-    "fsx_shard_owner", "fsx_shard_pack_device", "fsx_shard_unpack_device",
+    "fsx_shard_owner", "fsx_shard_pack_device", "fsx_shard_unpack_device", "fsx_shard_unpack16_device",
     "fsx_shard_scatter_device", "fsx_shard_clock_device", "fsx_blocklist_export_device",
     "fsx_blocklist_replica_device", "fsx_pcap_index", "fsx_pcap_records_device",
 ]
 
 SHARD_RECORD_BYTES = 32
+SHARD_RECORD16_BYTES = 16
 SHARD_BLOCK_BYTES = 32
 SHARD_FILTER_BLOCKLIST = 1
+SHARD_COMPACT = 2
 MAX_SHARDS = 64
 
 
@@ -401,9 +404,10 @@ class FsxContext:
         self._check(self._lib.fsx_blocklist_replica_device(self._h, d_entries, m),
                     "fsx_blocklist_replica_device")
 
-    def shard_unpack_device(self, d_records: int, m: int, d_hdr: int, d_len: int, d_ts: int):
-        self._check(self._lib.fsx_shard_unpack_device(self._h, d_records, m, d_hdr, d_len, d_ts),
-                    "fsx_shard_unpack_device")
+    def shard_unpack_device(self, d_records: int, m: int, d_hdr: int, d_len: int, d_ts: int,
+                            rec_bytes: int = SHARD_RECORD_BYTES):
+        fn = "fsx_shard_unpack16_device" if rec_bytes == SHARD_RECORD16_BYTES else "fsx_shard_unpack_device"
+        self._check(getattr(self._lib, fn)(self._h, d_records, m, d_hdr, d_len, d_ts), fn)
 
     def shard_scatter_device(self, d_ret: int, d_send_idx: int, m: int, d_verdict: int):
         self._check(self._lib.fsx_shard_scatter_device(self._h, d_ret, d_send_idx, m, d_verdict),

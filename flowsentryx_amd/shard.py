@@ -6,10 +6,12 @@ no shared state: every rank holds a contiguous slice of each arrival batch, ever
 source has ONE owner rank (include/fsx_hip.h fsx_shard_owner), and the owner runs the
 unchanged batch pipeline on all of that source's packets:
 
-  1. pack      parse the local slice, partition its IP packets by owner into 32-byte
-               records (stable: arrival order), verdicts for packets that never reach a
+  1. pack      parse the local slice, partition its IP packets by owner into 16-byte
+               IPv4 records (32-byte when the slice has an IPv6 source or a frame of 64 KiB
+               or more; stable: arrival order), verdicts for packets that never reach a
                limiter (short frames DROP, non-IP PASS)
-  2. all-to-all of the per-owner counts, then of the records (RCCL over xGMI)
+  2. all-to-all of the per-owner counts (record format in the low bit), then of the
+     records (RCCL over xGMI)
   3. owner     records -> header records, the batch pipeline on them (maps, verdicts,
                optionally flow features + MLP scores of the owned sources)
   4. all-to-all of the verdicts back (1 byte per packet), scatter to arrival positions
@@ -78,7 +80,7 @@ class HipShardEngine:
         self.owner_cap = int(ctx.config.max_batch)
         self.rec = torch.empty(max(1, max_local) * REC, dtype=torch.uint8, device=device)
         self.send_idx = torch.empty(max(1, max_local), dtype=torch.int32, device=device)
-        self.counts = torch.empty(lib.MAX_SHARDS + 1, dtype=torch.int64, device=device)
+        self.counts = torch.empty(lib.MAX_SHARDS + 2, dtype=torch.int64, device=device)
         self.clock3 = torch.empty(3, dtype=torch.int64, device=device)
         self.blk = torch.empty(1024 * lib.SHARD_BLOCK_BYTES, dtype=torch.uint8, device=device)
         self.blk_count = torch.empty(1, dtype=torch.int64, device=device)
@@ -129,14 +131,15 @@ class HipShardEngine:
         return self.clock3
 
     def pack(self, hdr, length, ts, n, G, verdict, filt=False):
-        """-> records, counts[G + 1] (counts[G]: packets dropped by the replica)."""
+        """-> records, counts[G + 2] (counts[G]: packets dropped by the replica,
+        counts[G + 1]: record bytes, 16 or 32)."""
         if n > self.max_local:
             raise ValueError(f"local slice of {n} packets exceeds {self.max_local}")
+        flags = lib.SHARD_COMPACT | (lib.SHARD_FILTER_BLOCKLIST if filt else 0)
         self.ctx.shard_pack_device(hdr.data_ptr(), length.data_ptr(), ts.data_ptr(), n, G,
                                    verdict.data_ptr(), self.rec.data_ptr(),
-                                   self.send_idx.data_ptr(), self.counts.data_ptr(),
-                                   lib.SHARD_FILTER_BLOCKLIST if filt else 0)
-        return self.rec, self.counts[:G + 1]
+                                   self.send_idx.data_ptr(), self.counts.data_ptr(), flags)
+        return self.rec, self.counts[:G + 2]
 
     def export_blocklist(self) -> tuple[torch.Tensor, int]:
         """This rank's live blacklist entries (32-byte records) and their count."""
@@ -152,16 +155,21 @@ class HipShardEngine:
     def load_replica(self, entries: torch.Tensor, m: int):
         self.ctx.blocklist_replica_device(entries.data_ptr(), m)
 
-    def recv_buffer(self, m: int) -> torch.Tensor:
-        return torch.empty(max(1, m) * REC, dtype=torch.uint8, device=self.device)
+    def recv_buffer(self, nbytes: int) -> torch.Tensor:
+        return torch.empty(max(1, nbytes), dtype=torch.uint8, device=self.device)
 
-    def owner_batch(self, recv: torch.Tensor, m: int) -> torch.Tensor:
-        """The limiter over the m received records, in received order (chunked by the
-        context's max_batch: state carries across chunks exactly as across batches)."""
+    def owner_batch(self, recv: torch.Tensor, segs) -> torch.Tensor:
+        """The limiter over the received records, in received order: segs = [(byte
+        offset, records, record bytes)] per sender (chunked by the context's max_batch:
+        state carries across chunks exactly as across batches)."""
+        m = sum(c for _, c, _ in segs)
         hdr, ln, ts, v = self._owner_buffers(m)
-        if m:
-            self.ctx.shard_unpack_device(recv.data_ptr(), m, hdr.data_ptr(), ln.data_ptr(),
-                                         ts.data_ptr())
+        r = 0
+        for off, cnt, rb in segs:
+            if cnt:
+                self.ctx.shard_unpack_device(recv.data_ptr() + off, cnt, hdr.data_ptr() + r * 64,
+                                             ln.data_ptr() + r * 4, ts.data_ptr() + r * 8, rb)
+            r += cnt
         for a in range(0, m, self.owner_cap):
             b = min(m, a + self.owner_cap)
             self._run(hdr.data_ptr() + a * 64, ln.data_ptr() + a * 4, ts.data_ptr() + a * 8,
@@ -199,6 +207,7 @@ class ShardedDataPlane:
         self.filter = blocklist_filter and self.world > 1
         self.filtered = 0          # packets dropped at their arrival rank by the replica
         self.last_exchange = None
+        self.formats = set()       # record sizes received (16 / 32)
 
     def verdict_batch(self, hdr, length, ts, n: int, verdict, chunks: int = 1, bounds=None):
         """Verdicts for this rank's slice (arrival order) of one global batch; every rank
@@ -240,17 +249,28 @@ class ShardedDataPlane:
         recs, counts = e.pack(hdr, length, ts, n, G, verdict, filt)
         cnt = counts.tolist()
         self.filtered += int(cnt[G])
-        send = counts[:G].contiguous()
+        rb = int(cnt[G + 1])   # this sender's record size (16: compact IPv4 records)
+        # per-owner counts with the record format in the low bit
+        send = (counts[:G] * 2 + (1 if rb == lib.SHARD_RECORD16_BYTES else 0)).contiguous()
         recv_counts = torch.empty_like(send)
         ones = [1] * G
         _a2a(recv_counts, send, ones, ones, self.group)
         sc = [int(x) for x in cnt[:G]]
-        rc = [int(x) for x in recv_counts.tolist()]
+        rw = [int(x) for x in recv_counts.tolist()]
+        rc = [x >> 1 for x in rw]
+        rf = [lib.SHARD_RECORD16_BYTES if x & 1 else lib.SHARD_RECORD_BYTES for x in rw]
         ms, mr = sum(sc), sum(rc)
-        recv = e.recv_buffer(mr)
-        _a2a(recv[:mr * REC], recs[:ms * REC], [x * REC for x in rc], [x * REC for x in sc],
-             self.group)
-        v = e.owner_batch(recv, mr)
+        in_b = [x * rb for x in sc]
+        out_b = [c * f for c, f in zip(rc, rf)]
+        recv = e.recv_buffer(sum(out_b))
+        _a2a(recv[:sum(out_b)], recs[:sum(in_b)], out_b, in_b, self.group)
+        segs, off = [], 0
+        for c, f, b in zip(rc, rf, out_b):
+            segs.append((off, c, f))
+            off += b
+            if c:
+                self.formats.add(f)
+        v = e.owner_batch(recv, segs)
         ret = torch.empty(max(ms, 1), dtype=torch.uint8, device=v.device)
         _a2a(ret[:ms], v[:mr], sc, rc, self.group)
         e.scatter(ret, ms, verdict)

@@ -215,8 +215,10 @@ int fsx_flow_features(fsx_ctx *ctx, const uint8_t *hdr, const uint32_t *len,
 /* Owner rank of a source: key16 = raw address (IPv4 in the first 4 bytes), family 4/6.
  * Host-only (no device work). */
 uint32_t fsx_shard_owner(const uint8_t *key16, int family, uint32_t n_shards);
+#define FSX_SHARD_RECORD16_BYTES 16 /* {u32 ipv4 key; u16 len; u16 dport; u64 ts} */
 #define FSX_SHARD_BLOCK_BYTES 32    /* {u32 key[4]; u64 till; u32 tag (1 v4, 2 v6); u32 pad} */
 #define FSX_SHARD_FILTER_BLOCKLIST 1u
+#define FSX_SHARD_COMPACT 2u
 
 /* Parse a device batch and partition its IP packets by owner, stable in arrival order:
  * d_records (n * 32 bytes capacity) receives the records owner by owner, d_send_idx the
@@ -226,7 +228,10 @@ uint32_t fsx_shard_owner(const uint8_t *key16, int family, uint32_t n_shards);
  * FSX_SHARD_FILTER_BLOCKLIST, IP packets whose source is in the context's blocklist
  * replica with till > 0 and now <= till are dropped here (src/fsx_kern.c:189-215) and
  * counted in d_counts[n_shards] (the caller adds them to stats_map.dropped); exact only
- * when timestamps are non-decreasing over all batches so far (fsx_shard_clock_device). */
+ * when timestamps are non-decreasing over all batches so far (fsx_shard_clock_device).
+ * With FSX_SHARD_COMPACT, d_counts has n_shards + 2 entries and d_counts[n_shards + 1]
+ * receives the record size written: FSX_SHARD_RECORD16_BYTES when no IP packet of the
+ * slice is IPv6 or 64 KiB or longer, else FSX_SHARD_RECORD_BYTES. */
 int fsx_shard_pack_device(fsx_ctx *ctx, const uint8_t *d_hdr, const uint32_t *d_len,
                           const uint64_t *d_ts, size_t n, uint32_t n_shards, uint32_t flags,
                           uint8_t *d_verdict, void *d_records, uint32_t *d_send_idx,
@@ -242,6 +247,9 @@ int fsx_blocklist_replica_device(fsx_ctx *ctx, const void *d_entries, size_t m);
  * (same source key, family, frame length, timestamp and L4 destination port). */
 int fsx_shard_unpack_device(fsx_ctx *ctx, const void *d_records, size_t m, uint8_t *d_hdr,
                             uint32_t *d_len, uint64_t *d_ts);
+/* Same for m compact 16-byte IPv4 records. */
+int fsx_shard_unpack16_device(fsx_ctx *ctx, const void *d_records, size_t m, uint8_t *d_hdr,
+                              uint32_t *d_len, uint64_t *d_ts);
 /* Origin side: d_verdict[d_send_idx[i]] = d_ret[i] for the m returned verdicts. */
 int fsx_shard_scatter_device(fsx_ctx *ctx, const uint8_t *d_ret, const uint32_t *d_send_idx,
                              size_t m, uint8_t *d_verdict);

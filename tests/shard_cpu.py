@@ -1,7 +1,7 @@
 """CPU engine of the sharded protocol (flowsentryx_amd/shard.py) for gloo tests.
 
 TEST INFRASTRUCTURE: the per-owner limiter is the CPU oracle, the exchange records are
-built with numpy in the 32-byte layout of include/fsx_hip.h, owners come from the
+built with numpy in the 16- and 32-byte layouts of include/fsx_hip.h, owners come from the
 library's host function fsx_shard_owner. The protocol code under test is the product's.
 """
 import contextlib
@@ -14,6 +14,18 @@ from flowsentryx_amd import lib
 REC_DTYPE = np.dtype([("key", "<u4", 4), ("ts", "<u8"), ("len", "<u4"), ("dport", "<u2"),
                       ("family", "u1"), ("pad", "u1")])
 assert REC_DTYPE.itemsize == lib.SHARD_RECORD_BYTES
+REC16_DTYPE = np.dtype([("key", "<u4"), ("len", "<u2"), ("dport", "<u2"), ("ts", "<u8")])
+assert REC16_DTYPE.itemsize == lib.SHARD_RECORD16_BYTES
+
+
+def widen(rec16: np.ndarray) -> np.ndarray:
+    r = np.zeros(rec16.shape[0], dtype=REC_DTYPE)
+    r["key"][:, 0] = rec16["key"]
+    r["ts"] = rec16["ts"]
+    r["len"] = rec16["len"]
+    r["dport"] = rec16["dport"]
+    r["family"] = 4
+    return r
 
 
 def records_to_headers(rec: np.ndarray):
@@ -92,7 +104,14 @@ class CpuShardEngine:
         rec["family"] = fam
         self.send_idx = ip
         counts = np.bincount(own, minlength=G).astype(np.int64)
-        counts = np.concatenate([counts, [filtered]]).astype(np.int64)
+        compact = not np.any(fam == 6) and not np.any(rec["len"] > 0xFFFF)
+        if compact:
+            r16 = np.zeros(ip.size, dtype=REC16_DTYPE)
+            for f in ("key", "len", "dport", "ts"):
+                r16[f] = rec[f][:, 0] if f == "key" else rec[f]
+            rec = r16
+        rb = lib.SHARD_RECORD16_BYTES if compact else lib.SHARD_RECORD_BYTES
+        counts = np.concatenate([counts, [filtered, rb]]).astype(np.int64)
         return torch.from_numpy(rec.view(np.uint8).copy()), torch.from_numpy(counts)
 
     BLK_DTYPE = np.dtype([("key", "<u4", 4), ("till", "<u8"), ("tag", "<u4"), ("pad", "<u4")])
@@ -116,11 +135,18 @@ class CpuShardEngine:
             k = e["key"].tobytes()[:16 if fam == 6 else 4]
             self.replica[(fam, k)] = int(e["till"])
 
-    def recv_buffer(self, m):
-        return torch.empty(max(1, m) * lib.SHARD_RECORD_BYTES, dtype=torch.uint8)
+    def recv_buffer(self, nbytes):
+        return torch.empty(max(1, nbytes), dtype=torch.uint8)
 
-    def owner_batch(self, recv, m):
-        rec = recv.numpy()[:m * lib.SHARD_RECORD_BYTES].view(REC_DTYPE)
+    def owner_batch(self, recv, segs):
+        b = recv.numpy()
+        parts = []
+        for off, cnt, rb in segs:
+            seg = b[off:off + cnt * rb]
+            parts.append(widen(seg.view(REC16_DTYPE)) if rb == lib.SHARD_RECORD16_BYTES
+                         else seg.view(REC_DTYPE))
+        rec = np.concatenate(parts) if parts else np.zeros(0, dtype=REC_DTYPE)
+        m = rec.shape[0]
         h, l, t = records_to_headers(rec)
         v = self.o.batch(h, l, t) if m else np.zeros(1, dtype=np.uint8)
         return torch.from_numpy(v)

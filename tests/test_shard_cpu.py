@@ -66,3 +66,12 @@ def test_sharded_token_bucket(tmp_path):
     spec = dict(BASE, seed=11, maps=[3, 4, 5, 6],
                 cfg=dict(limiter=2, tb_rate=300_000, tb_burst=4, max_entries=4096))
     run_sharded(tmp_path, 2, spec)
+
+
+def test_sharded_mixed_record_formats(tmp_path):
+    """A few IPv6 sources: pieces without one ship 16-byte records, the others 32-byte
+    records, in the same sub-batch (the format travels in the counts' low bit)."""
+    spec = dict(BASE, v6_frac=0.0007, seed=29, n_ips=60,
+                cfg=dict(pps_threshold=7, window_ns=200_000, block_ns=1_000_000, max_entries=4096))
+    res = run_sharded(tmp_path, 2, spec)
+    assert set(res["formats"]) == {16, 32}, res["formats"]

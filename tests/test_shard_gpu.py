@@ -1,7 +1,8 @@
 """GPU: the sharded path's HIP kernels (fsx_shard.hip) and the protocol end to end.
 
 * pack / unpack / scatter against the CPU engine's numpy restatement of the 32-byte
-  record layout (records, per-owner counts and send order byte-identical);
+  and compact 16-byte record layouts (records, per-owner counts and send order
+  byte-identical);
 * 2 and 3 ranks on the one GPU of the box (gloo carries the exchange through host
   memory; RCCL refuses two ranks on one device) with libfsx_hip.so owners: verdicts,
   stats_map and map dumps equal one sequential oracle over the whole stream.
@@ -10,16 +11,17 @@ import numpy as np
 import pytest
 import torch
 
-from shard_cpu import CpuShardEngine, REC_DTYPE, records_to_headers
+from shard_cpu import CpuShardEngine, REC_DTYPE, REC16_DTYPE, records_to_headers, widen
 from test_gpu_parity import rand_stream
 from test_shard_cpu import BASE, run_sharded
 
 pytestmark = pytest.mark.gpu
 
 
-def test_pack_unpack_scatter_match_restatement(native, oracle):
+@pytest.mark.parametrize("v6_frac,rec_bytes", [(0.4, 32), (0.0, 16)])
+def test_pack_unpack_scatter_match_restatement(native, oracle, v6_frac, rec_bytes):
     rng = np.random.default_rng(41)
-    hdr, ln, ts = rand_stream(rng, 20000, 500, dt_max=300, v6_frac=0.4, nonip_frac=0.05,
+    hdr, ln, ts = rand_stream(rng, 20000, 500, dt_max=300, v6_frac=v6_frac, nonip_frac=0.05,
                               short_frac=0.05)
     n, G = hdr.shape[0], 5
     dev = torch.device("cuda", 0)
@@ -37,19 +39,22 @@ def test_pack_unpack_scatter_match_restatement(native, oracle):
         crec, ccounts = cpu.pack(torch.from_numpy(hdr.reshape(-1).copy()),
                                  torch.from_numpy(ln.view(np.int32).copy()),
                                  torch.from_numpy(ts.view(np.int64).copy()), n, G, cv)
-        m = int(ccounts.sum())
+        m = int(ccounts[:G].sum())
         assert counts.cpu().tolist() == ccounts.tolist()
-        assert np.array_equal(rec[:m * 32].cpu().numpy(), crec.numpy())
+        assert int(ccounts[G + 1]) == rec_bytes
+        assert np.array_equal(rec[:m * rec_bytes].cpu().numpy(), crec.numpy())
         assert np.array_equal(e.send_idx[:m].cpu().numpy().astype(np.int64), cpu.send_idx)
         ipmask = np.zeros(n, dtype=bool)
         ipmask[cpu.send_idx] = True
         assert np.array_equal(tv.cpu().numpy()[~ipmask], cv.numpy()[~ipmask])
         # unpack: same parse, keys, lengths, timestamps, dst ports as the restatement
         hdr_o, ln_o, ts_o, _ = e._owner_buffers(m)
-        c.shard_unpack_device(rec.data_ptr(), m, hdr_o.data_ptr(), ln_o.data_ptr(), ts_o.data_ptr())
+        c.shard_unpack_device(rec.data_ptr(), m, hdr_o.data_ptr(), ln_o.data_ptr(), ts_o.data_ptr(),
+                              rec_bytes)
         c.sync()
         gh = hdr_o[:m * 64].cpu().numpy().reshape(m, 64)
-        eh, el, et = records_to_headers(crec.numpy().view(REC_DTYPE))
+        crec32 = widen(crec.numpy().view(REC16_DTYPE)) if rec_bytes == 16 else crec.numpy().view(REC_DTYPE)
+        eh, el, et = records_to_headers(crec32)
         assert np.array_equal(gh, eh)
         assert np.array_equal(ln_o[:m].cpu().numpy().view(np.uint32), el)
         assert np.array_equal(ts_o[:m].cpu().numpy().view(np.uint64), et)
