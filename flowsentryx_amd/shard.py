@@ -130,6 +130,23 @@ class HipShardEngine:
         self.ctx.shard_clock_device(ts.data_ptr(), n, self.clock3.data_ptr())
         return self.clock3
 
+    def clocks(self, ts, bounds) -> torch.Tensor:
+        """{min, max, decreases} of every piece [bounds[j], bounds[j+1]) (int64 [3 * pieces])."""
+        k = len(bounds) - 1
+        out = torch.empty(3 * k, dtype=torch.int64, device=self.device)
+        for j in range(k):
+            a, b = bounds[j], bounds[j + 1]
+            self.ctx.shard_clock_device(ts.data_ptr() + 8 * a, b - a, out.data_ptr() + 24 * j)
+        return out
+
+    def blocklist_buffer(self, cap: int) -> torch.Tensor:
+        """This rank's live blacklist entries for one all-gather: 32 header bytes (int64
+        entry count first) then up to cap 32-byte entries; no host synchronization."""
+        B = lib.SHARD_BLOCK_BYTES
+        buf = torch.empty(B + cap * B, dtype=torch.uint8, device=self.device)
+        self.ctx.blocklist_export_device(buf.data_ptr() + B, cap, buf.data_ptr())
+        return buf
+
     def pack(self, hdr, length, ts, n, G, verdict, filt=False):
         """-> records, counts[G + 2] (counts[G]: packets dropped by the replica,
         counts[G + 1]: record bytes, 16 or 32)."""
@@ -208,6 +225,7 @@ class ShardedDataPlane:
         self.filtered = 0          # packets dropped at their arrival rank by the replica
         self.last_exchange = None
         self.formats = set()       # record sizes received (16 / 32)
+        self.blk_cap = 1024        # blocklist entries per rank of one all-gather (grows)
 
     def verdict_batch(self, hdr, length, ts, n: int, verdict, chunks: int = 1, bounds=None):
         """Verdicts for this rank's slice (arrival order) of one global batch; every rank
@@ -221,42 +239,52 @@ class ShardedDataPlane:
                 self._sync_blocklist()   # maps may have changed since the last batch
             if bounds is None:
                 bounds = [n * i // chunks for i in range(chunks + 1)]
+            k = len(bounds) - 1
+            mono = self._clocks_monotone(ts, bounds) if self.filter else [False] * k
             sent = recv = 0
-            for a, b in zip(bounds[:-1], bounds[1:]):
-                ms, mr = self._sub_batch(hdr[a * 64:], length[a:], ts[a:], b - a, verdict[a:])
+            for j, (a, b) in enumerate(zip(bounds[:-1], bounds[1:])):
+                # the replica refresh after the last piece is the next batch's first step
+                ms, mr = self._sub_batch(hdr[a * 64:], length[a:], ts[a:], b - a, verdict[a:],
+                                         mono[j], refresh=self.filter and j + 1 < k)
                 sent, recv = sent + ms, recv + mr
             self.last_exchange = {"sent": sent, "received": recv, "filtered": self.filtered}
 
-    def _clock_monotone(self, ts, n: int) -> bool:
-        """Is this sub-batch's clock non-decreasing in global order (rank 0's piece, then
-        rank 1's, ...)? One all-gather of {min, max, decreases} per rank."""
-        c = _all_gather(self.engine.clock(ts, n), self.world, self.group).tolist()
-        last = None
-        for r in range(self.world):
-            mn, mx, dec = c[3 * r: 3 * r + 3]
-            if dec:
-                return False
-            if mx == 0 and mn == -1:      # empty piece ({~0, 0} as int64)
-                continue
-            if last is not None and (mn & (2**64 - 1)) < last:
-                return False
-            last = mx & (2**64 - 1)
-        return True
+    def _clocks_monotone(self, ts, bounds) -> list:
+        """Per sub-batch: is its clock non-decreasing in global order (rank 0's piece,
+        then rank 1's, ...)? One all-gather of {min, max, decreases} of every piece."""
+        k = len(bounds) - 1
+        c = _all_gather(self.engine.clocks(ts, bounds), self.world, self.group).tolist()
+        out = []
+        for j in range(k):
+            ok, last = True, None
+            for r in range(self.world):
+                mn, mx, dec = c[3 * (r * k + j): 3 * (r * k + j) + 3]
+                if dec:
+                    ok = False
+                    break
+                if mx == 0 and mn == -1:      # empty piece ({~0, 0} as int64)
+                    continue
+                if last is not None and (mn & (2**64 - 1)) < last:
+                    ok = False
+                    break
+                last = mx & (2**64 - 1)
+            out.append(ok)
+        return out
 
-    def _sub_batch(self, hdr, length, ts, n: int, verdict):
+    def _sub_batch(self, hdr, length, ts, n: int, verdict, filt: bool, refresh: bool):
         G, e = self.world, self.engine
-        filt = self.filter and self._clock_monotone(ts, n)
         recs, counts = e.pack(hdr, length, ts, n, G, verdict, filt)
-        cnt = counts.tolist()
-        self.filtered += int(cnt[G])
-        rb = int(cnt[G + 1])   # this sender's record size (16: compact IPv4 records)
-        # per-owner counts with the record format in the low bit
-        send = (counts[:G] * 2 + (1 if rb == lib.SHARD_RECORD16_BYTES else 0)).contiguous()
+        # per-owner counts with the record format in the low bit (device-side: the host
+        # reads its own and the received counts together, one synchronization)
+        send = (counts[:G] * 2 + (counts[G + 1] == lib.SHARD_RECORD16_BYTES).to(counts.dtype)).contiguous()
         recv_counts = torch.empty_like(send)
         ones = [1] * G
         _a2a(recv_counts, send, ones, ones, self.group)
+        both = torch.cat([counts.to(recv_counts.device), recv_counts]).tolist()
+        cnt, rw = both[:G + 2], [int(x) for x in both[G + 2:]]
+        self.filtered += int(cnt[G])
+        rb = int(cnt[G + 1])   # this sender's record size (16: compact IPv4 records)
         sc = [int(x) for x in cnt[:G]]
-        rw = [int(x) for x in recv_counts.tolist()]
         rc = [x >> 1 for x in rw]
         rf = [lib.SHARD_RECORD16_BYTES if x & 1 else lib.SHARD_RECORD_BYTES for x in rw]
         ms, mr = sum(sc), sum(rc)
@@ -274,26 +302,29 @@ class ShardedDataPlane:
         ret = torch.empty(max(ms, 1), dtype=torch.uint8, device=v.device)
         _a2a(ret[:ms], v[:mr], sc, rc, self.group)
         e.scatter(ret, ms, verdict)
-        if self.filter:
+        if refresh:
             self._sync_blocklist()
         return ms, mr
 
     def _sync_blocklist(self):
-        """All-gather every owner's live blacklist entries into every rank's replica."""
+        """All-gather every owner's live blacklist entries into every rank's replica: one
+        all-gather of fixed-capacity buffers (entry count in the header), repeated with a
+        larger capacity only when some rank overflowed it."""
         G, e = self.world, self.engine
-        ent, m = e.export_blocklist()
-        sizes = _all_gather(torch.tensor([m], dtype=torch.int64, device=ent.device), G,
-                            self.group).tolist()
-        mx = max(sizes)
         B = lib.SHARD_BLOCK_BYTES
-        if mx == 0:
-            e.load_replica(ent, 0)
-            return
-        pad = torch.zeros(mx * B, dtype=torch.uint8, device=ent.device)
-        pad[:m * B] = ent[:m * B]
-        allb = _all_gather(pad, G, self.group)
-        parts = [allb[r * mx * B: r * mx * B + sizes[r] * B] for r in range(G) if sizes[r]]
-        e.load_replica(torch.cat(parts), sum(sizes))
+        while True:
+            cap = self.blk_cap
+            allb = _all_gather(e.blocklist_buffer(cap), G, self.group)
+            per = B + cap * B
+            sizes = allb.view(-1)[:G * per].view(G, per)[:, :8].contiguous().view(torch.int64).view(-1).tolist()
+            if max(sizes) <= cap:
+                break
+            self.blk_cap = 2 * max(sizes)
+        parts = [allb[r * per + B: r * per + B + sizes[r] * B] for r in range(G) if sizes[r]]
+        if parts:
+            e.load_replica(torch.cat(parts), sum(sizes))
+        else:
+            e.load_replica(allb, 0)
 
     def stats(self) -> tuple[int, int]:
         """stats_map of the whole sharded data plane: sum over the owners, plus the

@@ -75,6 +75,17 @@ class CpuShardEngine:
         dec = int(np.any(t[1:] < t[:-1]))
         return torch.tensor(np.array([t.min(), t.max(), dec], dtype=np.uint64).view(np.int64))
 
+    def clocks(self, ts, bounds):
+        return torch.cat([self.clock(ts[a:], b - a) for a, b in zip(bounds[:-1], bounds[1:])])
+
+    def blocklist_buffer(self, cap):
+        ent, m = self.export_blocklist()
+        buf = torch.zeros(32 + cap * 32, dtype=torch.uint8)
+        buf[:8] = torch.from_numpy(np.array([m], dtype=np.int64).view(np.uint8))
+        k = min(m, cap)
+        buf[32:32 + k * 32] = ent[:k * 32]
+        return buf
+
     def pack(self, hdr, length, ts, n, G, verdict, filt=False):
         h, l, t = self._np(hdr, length, ts, n)
         cls, keys = self.oracle.parse(h, l)
