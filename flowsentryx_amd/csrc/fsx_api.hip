@@ -59,6 +59,12 @@ struct fsx_ctx {
     // sharding: per (owner, tile) counts of fsx_shard_pack_device, blocklist replica
     uint32_t *d_shard_cnt = nullptr;
     uint64_t shard_cnt_cap = 0;
+    uint32_t *d_rec_len = nullptr;       // record mode: len / ts written by k_parse
+    uint64_t *d_rec_ts = nullptr;
+    uint64_t rec_cap = 0;
+    uint8_t *d_shard_own = nullptr;      // per packet owner (k_shard_parse)
+    void *d_shard_crec = nullptr;        // per packet 16-byte record in arrival order
+    uint64_t shard_scr_cap = 0;
     ShardBlock *d_rep = nullptr;
     uint64_t rep_slots = 0;
     bool rep_valid = false;
@@ -214,7 +220,8 @@ void fsx_close(fsx_ctx *c) {
     hipFree(c->d_res); hipFree(c->d_val);
     for (int b = 0; b < 2; ++b) { hipFree(c->hist.t[b]); hipFree(c->hist.l[b]); }
     hipFree(c->hist.tile_cnt); hipFree(c->hist.tile_off); hipFree(c->hist.total);
-    hipFree(c->d_shard_cnt); hipFree(c->d_rep);
+    hipFree(c->d_shard_cnt); hipFree(c->d_rep); hipFree(c->d_shard_own); hipFree(c->d_shard_crec);
+    hipFree(c->d_rec_len); hipFree(c->d_rec_ts);
     hipFree(c->idx_heads); hipFree(c->idx_k6);
     for (int r = 0; r < kRing; ++r)
         for (int i = 0; i < kMaxEv; ++i) if (c->ev[r][i]) hipEventDestroy(c->ev[r][i]);
@@ -395,7 +402,7 @@ static bool fork_flows() {
 }
 
 // Enqueue one batch: verdicts + maps when d_verdict is set, per-source flows when fr is.
-static int run_batch(fsx_ctx *c, const uint8_t *d_hdr, const uint32_t *d_len, const uint64_t *d_ts,
+static int run_batch(fsx_ctx *c, const PacketIn &in, const uint32_t *d_len, const uint64_t *d_ts,
                      size_t n, uint8_t *d_verdict, bool do_limit, const FlowRequest *fr) {
     if (n > c->cfg.max_batch) return set_err(c, -E2BIG, "n=%zu exceeds max_batch", n);
     int rc = sel(c);
@@ -427,7 +434,7 @@ static int run_batch(fsx_ctx *c, const uint8_t *d_hdr, const uint32_t *d_len, co
         HIPCHK(c, hipMemsetAsync(c->sc.id_tab, 0, c->slots * 32, c->stream));
         c->id_gen = 1;
     }
-    hipError_t e = launch_verdict_pipeline(d_hdr, d_len, d_ts, (uint32_t)n, d_verdict, c->table,
+    hipError_t e = launch_verdict_pipeline(in, d_len, d_ts, (uint32_t)n, d_verdict, c->table,
                                            c->tstate, c->bs, c->sc, c->id_gen, table_index(c), c->lim,
                                            do_limit, fr,
                                            c->hist, c->stream, fork_flows() ? c->aux_stream : nullptr,
@@ -457,7 +464,7 @@ int fsx_verdict_batch_device(fsx_ctx *c, const uint8_t *d_hdr, const uint32_t *d
                              const uint64_t *d_ts, size_t n, uint8_t *d_verdict) {
     if (!c) return -EINVAL;
     if (n && (!d_hdr || !d_len || !d_ts || !d_verdict)) return set_err(c, -EINVAL, "null buffer");
-    return run_batch(c, d_hdr, d_len, d_ts, n, d_verdict, true, nullptr);
+    return run_batch(c, PacketIn{d_hdr, nullptr, 0, nullptr, nullptr}, d_len, d_ts, n, d_verdict, true, nullptr);
 }
 
 int fsx_process_batch_device(fsx_ctx *c, const uint8_t *d_hdr, const uint32_t *d_len,
@@ -468,7 +475,45 @@ int fsx_process_batch_device(fsx_ctx *c, const uint8_t *d_hdr, const uint32_t *d
     if (n && (!d_hdr || !d_len || !d_ts || !d_verdict || !d_keys16 || !d_family))
         return set_err(c, -EINVAL, "null buffer");
     const FlowRequest fr = flow_request(c, d_keys16, d_family, d_features, d_prob, d_malicious, flow_cap);
-    return run_batch(c, d_hdr, d_len, d_ts, n, d_verdict, true, &fr);
+    return run_batch(c, PacketIn{d_hdr, nullptr, 0, nullptr, nullptr}, d_len, d_ts, n, d_verdict, true, &fr);
+}
+
+// Record mode (the owner side of the sharded path): the pipeline reads the exchange
+// records directly; their len / ts land in context scratch for the later kernels.
+static int run_records(fsx_ctx *c, const void *d_records, size_t n, uint32_t rec_bytes, uint8_t *d_verdict,
+                       const FlowRequest *fr) {
+    if (rec_bytes != FSX_SHARD_RECORD_BYTES && rec_bytes != FSX_SHARD_RECORD16_BYTES)
+        return set_err(c, -EINVAL, "record size must be %d or %d", FSX_SHARD_RECORD16_BYTES,
+                       FSX_SHARD_RECORD_BYTES);
+    if (n > c->cfg.max_batch) return set_err(c, -E2BIG, "n=%zu exceeds max_batch", n);
+    if (n && (!d_records || !d_verdict)) return set_err(c, -EINVAL, "null buffer");
+    int rc = sel(c);
+    if (rc) return rc;
+    if (n > c->rec_cap) {
+        if (c->pending && (rc = fsx_sync(c))) return rc;   // the old buffers may be in use
+        hipFree(c->d_rec_len); hipFree(c->d_rec_ts);
+        c->d_rec_len = nullptr; c->d_rec_ts = nullptr; c->rec_cap = 0;
+        HIPCHK(c, hipMalloc(&c->d_rec_len, n * 4));
+        HIPCHK(c, hipMalloc(&c->d_rec_ts, n * 8));
+        c->rec_cap = n;
+    }
+    const PacketIn in{nullptr, d_records, rec_bytes, c->d_rec_len, c->d_rec_ts};
+    return run_batch(c, in, c->d_rec_len, c->d_rec_ts, n, d_verdict, true, fr);
+}
+
+int fsx_verdict_records_device(fsx_ctx *c, const void *d_records, size_t n, uint32_t rec_bytes,
+                               uint8_t *d_verdict) {
+    if (!c) return -EINVAL;
+    return run_records(c, d_records, n, rec_bytes, d_verdict, nullptr);
+}
+
+int fsx_process_records_device(fsx_ctx *c, const void *d_records, size_t n, uint32_t rec_bytes,
+                               uint8_t *d_verdict, uint8_t *d_keys16, uint8_t *d_family, float *d_features,
+                               float *d_prob, uint8_t *d_malicious, size_t flow_cap) {
+    if (!c) return -EINVAL;
+    if (n && (!d_keys16 || !d_family)) return set_err(c, -EINVAL, "null buffer");
+    const FlowRequest fr = flow_request(c, d_keys16, d_family, d_features, d_prob, d_malicious, flow_cap);
+    return run_records(c, d_records, n, rec_bytes, d_verdict, &fr);
 }
 
 static int ensure_stage(fsx_ctx *c, uint64_t n) {
@@ -701,7 +746,8 @@ int fsx_flow_features(fsx_ctx *c, const uint8_t *hdr, const uint32_t *len, const
     HIPCHK(c, hipMemcpyAsync(c->d_ts, ts, n * 8, hipMemcpyHostToDevice, c->stream));
     FlowRequest fr = flow_request(c, dk, df, dfeat, nullptr, nullptr, n);
     // verdict scratch: parse writes default verdicts; the limiter does not run
-    rc = run_batch(c, c->d_hdr, c->d_len, c->d_ts, n, c->d_verdict, false, &fr);
+    rc = run_batch(c, PacketIn{c->d_hdr, nullptr, 0, nullptr, nullptr}, c->d_len, c->d_ts, n, c->d_verdict,
+                   false, &fr);
     if (!rc) rc = fsx_sync(c);
     BatchState h{};
     if (!rc && hipMemcpy(&h, c->bs, sizeof(h), hipMemcpyDeviceToHost) != hipSuccess) rc = -EIO;
@@ -755,11 +801,22 @@ int fsx_shard_pack_device(fsx_ctx *c, const uint8_t *d_hdr, const uint32_t *d_le
         HIPCHK(c, hipMalloc(&c->d_shard_cnt, need * 4));
         c->shard_cnt_cap = need;
     }
+    if (n > c->shard_scr_cap) {
+        hipFree(c->d_shard_own);
+        hipFree(c->d_shard_crec);
+        c->d_shard_own = nullptr;
+        c->d_shard_crec = nullptr;
+        c->shard_scr_cap = 0;
+        HIPCHK(c, hipMalloc(&c->d_shard_own, n));
+        HIPCHK(c, hipMalloc(&c->d_shard_crec, n * FSX_SHARD_RECORD16_BYTES));
+        c->shard_scr_cap = n;
+    }
     const Replica rep{c->d_rep, c->rep_slots ? c->rep_slots - 1 : 0};
     const bool filt = (flags & FSX_SHARD_FILTER_BLOCKLIST) && c->rep_valid;
     const bool compact = (flags & FSX_SHARD_COMPACT) != 0;
     hipError_t e = launch_shard_pack(d_hdr, d_len, d_ts, (uint32_t)n, G, d_verdict, d_records, d_send_idx,
-                                     d_counts, c->d_shard_cnt, filt ? &rep : nullptr, compact, c->stream);
+                                     d_counts, c->d_shard_cnt, c->d_shard_own, c->d_shard_crec,
+                                     filt ? &rep : nullptr, compact, c->stream);
     if (e != hipSuccess) return set_err(c, -EIO, "shard pack: %s", hipGetErrorString(e));
     return 0;
 }

@@ -22,6 +22,7 @@
 #include "fsx_dev_common.h"
 #include "fsx_internal.h"
 #include "fsx_seg.h"
+#include "fsx_shard.h"
 
 #define XDP_DROP 1
 #define XDP_PASS 2
@@ -173,10 +174,22 @@ __device__ __forceinline__ uint32_t parse_src(uint32_t L, uint32_t d3, uint32_t 
 // one sampled packet that hashed there (the heavy source when one dominates it).
 // Sketch and map hash of a source: its probe start in the id table (already computed by
 // k_parse for every packet; tables of heavy-sort size have >= 2^17 slots).
-__global__ __launch_bounds__(256) void k_heavy_sample(const uint8_t *__restrict__ hdr,
-                                                      const uint32_t *__restrict__ len, uint32_t n,
-                                                      uint32_t *__restrict__ sketch, uint64_t seed,
-                                                      uint64_t mask, uint32_t test_flags) {
+// Source of packet i (tag 0: not an IP packet) in either input mode.
+__device__ __forceinline__ uint32_t packet_src(const PacketIn &in, const uint32_t *len, uint32_t i,
+                                               uint32_t k[4]) {
+    if (in.rec) {
+        uint32_t L, dp;
+        uint64_t T;
+        return rec_read(in.rec, in.rec_bytes, i, k, L, T, dp);
+    }
+    const uint32_t *d = reinterpret_cast<const uint32_t *>(in.hdr + (size_t)i * 64);
+    uint8_t v;
+    return parse_src(len[i], d[3], d[5], d[6], d[7], d[8], d[9], k, v);
+}
+
+__global__ __launch_bounds__(256) void k_heavy_sample(PacketIn in, const uint32_t *__restrict__ len,
+                                                      uint32_t n, uint32_t *__restrict__ sketch,
+                                                      uint64_t seed, uint64_t mask, uint32_t test_flags) {
     __shared__ uint32_t s_cnt[kSketch], s_cand[kSketch];
     for (uint32_t c = threadIdx.x; c < kSketch; c += 256) s_cnt[c] = 0;
     __syncthreads();
@@ -185,10 +198,8 @@ __global__ __launch_bounds__(256) void k_heavy_sample(const uint8_t *__restrict_
     const uint32_t s0 = blockIdx.x * per, s1 = min(S, s0 + per);
     for (uint32_t q = s0 + threadIdx.x; q < s1; q += 256) {
         const uint32_t i = (uint32_t)((uint64_t)q * n / S);
-        const uint32_t *d = reinterpret_cast<const uint32_t *>(hdr + (size_t)i * 64);
         uint32_t k[4];
-        uint8_t v;
-        const uint32_t tag = parse_src(len[i], d[3], d[5], d[6], d[7], d[8], d[9], k, v);
+        const uint32_t tag = packet_src(in, len, i, k);
         if (!tag) continue;
         const uint32_t h = (uint32_t)probe_start(tag, k, seed, mask, test_flags) & (kSketch - 1);
         atomicAdd(&s_cnt[h], 1u);
@@ -206,8 +217,7 @@ __global__ __launch_bounds__(256) void k_heavy_sample(const uint8_t *__restrict_
 
 // One block: the (at most nmax) sketch buckets of highest count >= floor become the heavy
 // set: their candidates' keys and an open-addressing map of them. Zeroes the counts.
-__global__ __launch_bounds__(1024) void k_heavy_pick(const uint8_t *__restrict__ hdr,
-                                                     const uint32_t *__restrict__ len,
+__global__ __launch_bounds__(1024) void k_heavy_pick(PacketIn in, const uint32_t *__restrict__ len,
                                                      uint32_t *__restrict__ sketch, HeavySet *hs,
                                                      uint32_t nmax, uint32_t floor_cnt, uint64_t seed,
                                                      uint64_t mask, uint32_t test_flags) {
@@ -257,10 +267,8 @@ __global__ __launch_bounds__(1024) void k_heavy_pick(const uint8_t *__restrict__
     const uint32_t n = s_n;
     if (tid < n) {
         const uint32_t i = sketch[kSketch + s_sel[tid]];
-        const uint32_t *d = reinterpret_cast<const uint32_t *>(hdr + (size_t)i * 64);
         uint32_t k[4];
-        uint8_t v;
-        s_tag[tid] = parse_src(len[i], d[3], d[5], d[6], d[7], d[8], d[9], k, v);
+        s_tag[tid] = packet_src(in, len, i, k);
         for (int j = 0; j < 4; ++j) s_key[tid][j] = k[j];
     }
     __syncthreads();
@@ -283,7 +291,10 @@ __global__ __launch_bounds__(1024) void k_heavy_pick(const uint8_t *__restrict__
 // One wave handles 64 consecutive records per step: the 4 KiB tile is loaded with
 // four fully coalesced 1 KiB wave loads and staged through LDS (17-dword record
 // pitch: conflict-free 32-bit reads), then each lane parses its own record.
-__global__ __launch_bounds__(256, 4) void k_parse(const uint8_t *__restrict__ hdr,
+// Record mode (kRec = 16 / 32): every lane loads its own exchange record (coalesced, no
+// LDS staging), all of them IP packets; their len / ts go out to in.rec_len / rec_ts.
+template <uint32_t kRec>
+__global__ __launch_bounds__(256, 4) void k_parse(PacketIn in,
                                                const uint32_t *__restrict__ len,
                                                const uint64_t *__restrict__ ts, uint32_t n,
                                                uint64_t *__restrict__ packed,
@@ -329,19 +340,37 @@ __global__ __launch_bounds__(256, 4) void k_parse(const uint8_t *__restrict__ hd
     // software pipeline: the next tile's loads are in flight while this one is parsed
     auto load = [&](uint32_t tt, uint4 (&h)[4], uint32_t &L_, uint64_t &T_, uint64_t &P_) {
         const uint32_t base = tt << 6;
-        const uint8_t *src = hdr + (size_t)base * 64;
         const bool tv = tt < ntiles;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const uint32_t g = (uint32_t)k * 1024u + lane * 16u;
-            h[k] = make_uint4(0, 0, 0, 0);
-            if (tv && base + (g >> 6) < n) h[k] = *reinterpret_cast<const uint4 *>(src + g);
-        }
         const uint32_t i = base + lane;
         const bool live = tv && i < n;
-        L_ = live ? len[i] : 0u;
-        T_ = live ? ts[i] : 0ull;
-        P_ = (lane == 0 && live && i > 0) ? ts[i - 1] : 0ull;
+        if constexpr (kRec == 0) {
+            const uint8_t *src = in.hdr + (size_t)base * 64;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t g = (uint32_t)k * 1024u + lane * 16u;
+                h[k] = make_uint4(0, 0, 0, 0);
+                if (tv && base + (g >> 6) < n) h[k] = *reinterpret_cast<const uint4 *>(src + g);
+            }
+            L_ = live ? len[i] : 0u;
+            T_ = live ? ts[i] : 0ull;
+            P_ = (lane == 0 && live && i > 0) ? ts[i - 1] : 0ull;
+        } else {
+            const uint4 *r = reinterpret_cast<const uint4 *>(in.rec);
+            constexpr uint32_t kW = kRec / 16;   // uint4 words per record
+#pragma unroll
+            for (int k = 0; k < 4; ++k) h[k] = make_uint4(0, 0, 0, 0);
+            if (live) {
+                h[0] = r[(size_t)i * kW];
+                if constexpr (kW == 2) h[1] = r[(size_t)i * kW + 1];
+            }
+            L_ = 0u;
+            T_ = 0ull;
+            P_ = 0ull;
+            if (lane == 0 && live && i > 0) {   // timestamp of the record before the step
+                const uint4 pr = r[(size_t)(i - 1) * kW + (kW - 1)];
+                P_ = kW == 1 ? ((uint64_t)pr.z | ((uint64_t)pr.w << 32)) : ((uint64_t)pr.x | ((uint64_t)pr.y << 32));
+            }
+        }
     };
     uint4 hv[4], hn[4];
     uint32_t Lc, Ln;
@@ -365,25 +394,42 @@ __global__ __launch_bounds__(256, 4) void k_parse(const uint8_t *__restrict__ hd
         uint64_t Tn2, Pn2;
         load(T2 < nsort ? step_of(T2, j2) : ntiles, h2, L2, Tn2, Pn2);
         const uint32_t base = t << 6;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const uint32_t g = (uint32_t)k * 1024u + lane * 16u;
-            const uint32_t r = g >> 6, off = (g & 63u) >> 2;
-            uint32_t *d = rec + r * 17u + off;
-            d[0] = hv[k].x; d[1] = hv[k].y; d[2] = hv[k].z; d[3] = hv[k].w;
-        }
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         const uint32_t i = base + lane;
         const bool live = i < n;
-        const uint32_t *my = rec + lane * 17u;
-        const uint32_t d3 = my[3], d5 = my[5], d6 = my[6], d7 = my[7], d8 = my[8], d9 = my[9];
-        const uint32_t L = Lc;
-        const uint64_t T = Tc;
-        uint64_t prev = __shfl_up(T, 1);
-        if (lane == 0) prev = (live && i > 0) ? Pc : T;
+        uint32_t L = Lc;
+        uint64_t T = Tc;
         uint8_t v = XDP_PASS;  // non-IP: PASS, not counted (src/fsx_kern.c:128-131)
         uint32_t k[4] = {0, 0, 0, 0};
-        const uint32_t tag = live ? parse_src(L, d3, d5, d6, d7, d8, d9, k, v) : 0u;
+        uint32_t tag = 0;
+        if constexpr (kRec == 0) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t g = (uint32_t)q * 1024u + lane * 16u;
+                const uint32_t r = g >> 6, off = (g & 63u) >> 2;
+                uint32_t *d = rec + r * 17u + off;
+                d[0] = hv[q].x; d[1] = hv[q].y; d[2] = hv[q].z; d[3] = hv[q].w;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            const uint32_t *my = rec + lane * 17u;
+            const uint32_t d3 = my[3], d5 = my[5], d6 = my[6], d7 = my[7], d8 = my[8], d9 = my[9];
+            tag = live ? parse_src(L, d3, d5, d6, d7, d8, d9, k, v) : 0u;
+        } else if (live) {   // ShardRecord16 {key, len | dport << 16, ts} / ShardRecord
+            if constexpr (kRec == 16) {
+                k[0] = hv[0].x;
+                L = hv[0].y & 0xFFFFu;
+                T = (uint64_t)hv[0].z | ((uint64_t)hv[0].w << 32);
+                tag = 1;
+            } else {
+                k[0] = hv[0].x; k[1] = hv[0].y; k[2] = hv[0].z; k[3] = hv[0].w;
+                T = (uint64_t)hv[1].x | ((uint64_t)hv[1].y << 32);
+                L = hv[1].z;
+                tag = ((hv[1].w >> 16) & 0xFFu) == 6 ? 2u : 1u;
+            }
+            in.rec_len[i] = L;
+            in.rec_ts[i] = T;
+        }
+        uint64_t prev = __shfl_up(T, 1);
+        if (lane == 0) prev = (live && i > 0) ? Pc : T;
         const bool ip = tag != 0;
         if (tag == 2) any6 = 1;
         uint64_t h = 0, hint = 0;
@@ -1560,7 +1606,7 @@ static uint32_t next_generation() {
     return g;
 }
 
-hipError_t launch_verdict_pipeline(const uint8_t *hdr, const uint32_t *len, const uint64_t *ts,
+hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, const uint64_t *ts,
                                    uint32_t n, uint8_t *verdict, Slot *table, TableState *tstate,
                                    BatchState *bs, const Scratch &sc_in, uint32_t id_gen,
                                    const TableIndex &X, const Limits &lim, bool do_limit,
@@ -1625,16 +1671,24 @@ hipError_t launch_verdict_pipeline(const uint8_t *hdr, const uint32_t *len, cons
         dp.shift[0] = 56; dp.mask[0] = 255;
         dp.shift[1] = 39; dp.mask[1] = (1u << w1) - 1u;
         dp.shift[2] = 39 + w1; dp.mask[2] = (1u << (rest - w1)) - 1u;
-        k_heavy_sample<<<64, 256, 0, st>>>(hdr, len, n, sc.sketch, lim.seed, lim.table_mask, lim.test_flags);
-        k_heavy_pick<<<1, 1024, 0, st>>>(hdr, len, sc.sketch, sc.heavy, kHeavyMax, 16, lim.seed,
+        k_heavy_sample<<<64, 256, 0, st>>>(in, len, n, sc.sketch, lim.seed, lim.table_mask, lim.test_flags);
+        k_heavy_pick<<<1, 1024, 0, st>>>(in, len, sc.sketch, sc.heavy, kHeavyMax, 16, lim.seed,
                                          lim.table_mask, lim.test_flags);
         mark("k_heavy_pick");
     } else {
         for (int p = 0; p < 4; ++p) { dp.shift[p] = 32u + dbits * (uint32_t)p; dp.mask[p] = dmask; }
     }
-    k_parse<<<std::min<uint32_t>(1024, ntiles), 256, 0, st>>>(
-        hdr, len, ts, n, sc.packed[0], verdict, bs, idt, sc.sort_ctl, onesweep ? nullptr : sc.hist, tcap,
-        dp, heavy_sort ? sc.heavy : nullptr);
+    {
+        const uint32_t g = std::min<uint32_t>(1024, ntiles);
+        const HeavySet *hs = heavy_sort ? sc.heavy : nullptr;
+        uint32_t *th = onesweep ? nullptr : sc.hist;
+        if (!in.rec)
+            k_parse<0><<<g, 256, 0, st>>>(in, len, ts, n, sc.packed[0], verdict, bs, idt, sc.sort_ctl, th, tcap, dp, hs);
+        else if (in.rec_bytes == 16)
+            k_parse<16><<<g, 256, 0, st>>>(in, len, ts, n, sc.packed[0], verdict, bs, idt, sc.sort_ctl, th, tcap, dp, hs);
+        else
+            k_parse<32><<<g, 256, 0, st>>>(in, len, ts, n, sc.packed[0], verdict, bs, idt, sc.sort_ctl, th, tcap, dp, hs);
+    }
     mark("k_parse");
     k_hist_prep<<<1, 256, 0, st>>>(sc.sort_ctl, sc.gbase, bs, heavy_sort ? dp.light_b : 256u);
     if (do_limit) k_batch_check<<<1, 1, 0, st>>>(bs, tstate, lim);
@@ -1672,7 +1726,7 @@ hipError_t launch_verdict_pipeline(const uint8_t *hdr, const uint32_t *len, cons
         std::swap(sc.pay[0], sc.pay[1]);
     }
     uint64_t *S = sc.packed[0];
-    k_heads_count<<<gridTiles, 256, 0, st>>>(S, bs, hdr, sc.headf, sc.tile_aux, sc.sub_cnt);
+    k_heads_count<<<gridTiles, 256, 0, st>>>(S, bs, in.hdr, sc.headf, sc.tile_aux, sc.sub_cnt);
     mark("k_heads_count");
     k_scan_tiles_u32<<<1, 1024, 0, st>>>(sc.tile_aux, bs, sc.seg_start);
     k_heads_write<<<gridTiles, 256, 0, st>>>(bs, sc.headf, sc.tile_aux, sc.seg_start, S,
@@ -1687,7 +1741,7 @@ hipError_t launch_verdict_pipeline(const uint8_t *hdr, const uint32_t *len, cons
             fs = st2;
             mark_on(nullptr, 1);
         }
-        if ((e = launch_flows(S, sc.pay[0], bs, sc.headf, len, ts, hdr, sc.tile_aux, sc.sub_cnt, sc.seg_start,
+        if ((e = launch_flows(S, sc.pay[0], bs, sc.headf, len, ts, in, sc.tile_aux, sc.sub_cnt, sc.seg_start,
                               sc.flow_first, sc.flow_last, sc.span_list, flows->acc, flows->keys16,
                               flows->fam, flows->feat, flows->prob, flows->dec, flows->cap, flows->score,
                               lim.salt32, n, fs)) != hipSuccess)

@@ -25,6 +25,7 @@
 #include "fsx_dev_common.h"
 #include "fsx_internal.h"
 #include "fsx_q8.h"
+#include "fsx_shard.h"
 
 namespace fsx {
 
@@ -107,13 +108,21 @@ __device__ __forceinline__ void acc_store(const FlowOut &out, uint32_t g, const 
 
 // Features of source g from its exact sums, then the q8 score.
 __device__ void flow_finish(uint32_t g, const FlowAcc &a, const uint64_t *S,
-                            const uint32_t *seg_start, const uint8_t *hdr, const uint32_t *len,
+                            const uint32_t *seg_start, const PacketIn &in, const uint32_t *len,
                             uint32_t salt, const FlowOut &out, const ScoreParams &P) {
     if (g >= out.cap) return;
     const uint64_t v = S[seg_start[g]];
     uint32_t k[4];
-    const uint32_t tag = key_of(v, hdr, salt, k);
     const uint32_t idx = pk_idx(v);
+    uint32_t tag, dport;
+    if (in.rec) {   // record mode: key and port travel in the exchange record
+        uint32_t L;
+        uint64_t T;
+        tag = rec_read(in.rec, in.rec_bytes, idx, k, L, T, dport);
+    } else {
+        tag = key_of(v, in.hdr, salt, k);
+        dport = dst_port(in.hdr + (size_t)idx * 64, len[idx]);
+    }
     uint32_t *kw = reinterpret_cast<uint32_t *>(out.keys16 + (size_t)g * 16);
     kw[0] = k[0]; kw[1] = k[1]; kw[2] = k[2]; kw[3] = k[3];
     out.fam[g] = tag == 1 ? 4 : 6;
@@ -133,7 +142,7 @@ __device__ void flow_finish(uint32_t g, const FlowAcc &a, const uint64_t *S,
         iat_var = (double)num / ((double)m * ((double)m - 1.0)) / 1000000.0;
     }
     float x[8];
-    x[0] = (float)dst_port(hdr + (size_t)idx * 64, len[idx]);
+    x[0] = (float)dport;
     x[1] = (float)mean;
     x[2] = (float)sqrt(var);
     x[3] = (float)var;
@@ -161,7 +170,7 @@ __device__ __forceinline__ void flow_tiles(const uint64_t *__restrict__ S,
                                            const uint8_t *__restrict__ headf,
                                            const uint32_t *__restrict__ len,
                                            const uint64_t *__restrict__ ts,
-                                           const uint8_t *__restrict__ hdr,
+                                           const PacketIn &in,
                                            const uint32_t *__restrict__ tile_off,
                                            const uint32_t *__restrict__ sub_cnt,
                                            const uint32_t *__restrict__ seg_start,
@@ -302,7 +311,7 @@ __global__ __launch_bounds__(256, FSX_FLOW_MINB) void k_flow_tile(const uint64_t
                                                    const uint8_t *__restrict__ headf,
                                                    const uint32_t *__restrict__ len,
                                                    const uint64_t *__restrict__ ts,
-                                                   const uint8_t *__restrict__ hdr,
+                                                   PacketIn in,
                                                    const uint32_t *__restrict__ tile_off,
                                                    const uint32_t *__restrict__ sub_cnt,
                                                    const uint32_t *__restrict__ seg_start,
@@ -312,10 +321,10 @@ __global__ __launch_bounds__(256, FSX_FLOW_MINB) void k_flow_tile(const uint64_t
                                                    ScoreParams P, uint32_t salt) {
     __shared__ unsigned long long s_S[4][64 * 17];
     if (bs->pay_ok)
-        flow_tiles<true>(S, pay, bs, headf, len, ts, hdr, tile_off, sub_cnt, seg_start, firstp,
+        flow_tiles<true>(S, pay, bs, headf, len, ts, in, tile_off, sub_cnt, seg_start, firstp,
                          lastp, span_list, out, P, salt, s_S);
     else
-        flow_tiles<false>(S, pay, bs, headf, len, ts, hdr, tile_off, sub_cnt, seg_start, firstp,
+        flow_tiles<false>(S, pay, bs, headf, len, ts, in, tile_off, sub_cnt, seg_start, firstp,
                           lastp, span_list, out, P, salt, s_S);
 }
 
@@ -324,7 +333,7 @@ __global__ __launch_bounds__(256) void k_flow_combine(const uint64_t *__restrict
                                                       const FlowAcc *__restrict__ firstp,
                                                       const FlowAcc *__restrict__ lastp,
                                                       const uint32_t *__restrict__ span_list,
-                                                      const uint8_t *__restrict__ hdr,
+                                                      PacketIn in,
                                                       const uint32_t *__restrict__ len, FlowOut out,
                                                       ScoreParams P, uint32_t salt) {
     const uint32_t lane = lane_id();
@@ -348,16 +357,16 @@ __global__ __launch_bounds__(256) void k_flow_combine(const uint64_t *__restrict
 // of the tile loop, where a source's end lands on arbitrary lanes).
 __global__ __launch_bounds__(256) void k_flow_finish(const uint64_t *__restrict__ S, BatchState *bs,
                                                      const uint32_t *__restrict__ seg_start,
-                                                     const uint8_t *__restrict__ hdr,
+                                                     PacketIn in,
                                                      const uint32_t *__restrict__ len, FlowOut out,
                                                      ScoreParams P, uint32_t salt) {
     const uint32_t ns = min(bs->nseg, out.cap);
     for (uint32_t g = blockIdx.x * 256u + threadIdx.x; g < ns; g += gridDim.x * 256u)
-        flow_finish(g, out.acc[g], S, seg_start, hdr, len, salt, out, P);
+        flow_finish(g, out.acc[g], S, seg_start, in, len, salt, out, P);
 }
 
 hipError_t launch_flows(const uint64_t *S, const uint64_t *pay, BatchState *bs, const uint8_t *headf, const uint32_t *len,
-                        const uint64_t *ts, const uint8_t *hdr, const uint32_t *tile_off,
+                        const uint64_t *ts, const PacketIn &in, const uint32_t *tile_off,
                         const uint32_t *sub_cnt, const uint32_t *seg_start, void *firstp, void *lastp,
                         uint32_t *span_list, void *acc, uint8_t *keys16, uint8_t *fam, float *feat,
                         float *prob, uint8_t *dec, uint32_t cap, const ScoreParams &P, uint32_t salt,
@@ -366,12 +375,12 @@ hipError_t launch_flows(const uint64_t *S, const uint64_t *pay, BatchState *bs, 
     const FlowOut out{(FlowAcc *)acc, keys16, fam, feat, prob, dec, cap};
     const uint32_t nsub = (n + kFT - 1) / kFT;
     const uint32_t grid = std::max<uint32_t>(1, std::min<uint32_t>(16384, (nsub + 3) / 4));
-    k_flow_tile<<<grid, 256, 0, st>>>(S, pay, bs, headf, len, ts, hdr, tile_off, sub_cnt, seg_start,
+    k_flow_tile<<<grid, 256, 0, st>>>(S, pay, bs, headf, len, ts, in, tile_off, sub_cnt, seg_start,
                                       (FlowAcc *)firstp, (FlowAcc *)lastp, span_list, out, P, salt);
     k_flow_combine<<<256, 256, 0, st>>>(S, bs, seg_start, (const FlowAcc *)firstp,
-                                        (const FlowAcc *)lastp, span_list, hdr, len, out, P, salt);
+                                        (const FlowAcc *)lastp, span_list, in, len, out, P, salt);
     const uint32_t gf = std::max<uint32_t>(1, std::min<uint32_t>(4096, (std::min(n, cap) + 255) / 256));
-    k_flow_finish<<<gf, 256, 0, st>>>(S, bs, seg_start, hdr, len, out, P, salt);
+    k_flow_finish<<<gf, 256, 0, st>>>(S, bs, seg_start, in, len, out, P, salt);
     return hipGetLastError();
 }
 

@@ -269,10 +269,22 @@ struct PipeTiming {
     int used;
 };
 
+// The packets of a batch: 64-byte header records (hdr, with the caller's len / ts), or
+// the exchange records of the sharded path (record mode: rec, rec_bytes 16 / 32, every
+// record an IP packet; k_parse writes their len / ts into rec_len / rec_ts for the rest
+// of the pipeline).
+struct PacketIn {
+    const uint8_t *hdr;
+    const void *rec;
+    uint32_t rec_bytes;
+    uint32_t *rec_len;
+    uint64_t *rec_ts;
+};
+
 // st: the batch stream. st2 (optional, with fork/join events): the flow features run
 // on it concurrently with the rate limiter (they share only read-only inputs). st3
 // (optional): the fixed-window wave walker beside the thread walker.
-hipError_t launch_verdict_pipeline(const uint8_t *hdr, const uint32_t *len, const uint64_t *ts,
+hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, const uint64_t *ts,
                                    uint32_t n, uint8_t *verdict, Slot *table, TableState *tstate,
                                    BatchState *bs, const Scratch &sc, uint32_t id_gen,
                                    const TableIndex &X, const Limits &lim, bool do_limit,
@@ -303,7 +315,7 @@ hipError_t launch_pcap_records(const uint8_t *buf, const uint64_t *off, const ui
                                uint8_t *hdr, hipStream_t st);
 
 hipError_t launch_flows(const uint64_t *S, const uint64_t *pay, BatchState *bs, const uint8_t *headf, const uint32_t *len,
-                        const uint64_t *ts, const uint8_t *hdr, const uint32_t *tile_off,
+                        const uint64_t *ts, const PacketIn &in, const uint32_t *tile_off,
                         const uint32_t *sub_cnt, const uint32_t *seg_start, void *firstp, void *lastp,
                         uint32_t *span_list, void *acc, uint8_t *keys16, uint8_t *fam, float *feat,
                         float *prob, uint8_t *dec, uint32_t cap, const ScoreParams &P, uint32_t salt,

@@ -29,6 +29,27 @@ struct alignas(16) ShardRecord16 {
 };
 static_assert(sizeof(ShardRecord16) == 16, "16-byte compact records");
 
+// Exchange record i of a record-mode batch (every record an IP packet): family tag 1 / 2,
+// source key, frame length, timestamp and L4 destination port.
+__device__ __forceinline__ uint32_t rec_read(const void *rec, uint32_t rec_bytes, uint32_t i, uint32_t k[4],
+                                             uint32_t &L, uint64_t &T, uint32_t &dport) {
+    if (rec_bytes == sizeof(ShardRecord16)) {
+        const uint4 a = reinterpret_cast<const uint4 *>(rec)[i];
+        k[0] = a.x; k[1] = k[2] = k[3] = 0;
+        L = a.y & 0xFFFFu;
+        dport = a.y >> 16;
+        T = (uint64_t)a.z | ((uint64_t)a.w << 32);
+        return 1;
+    }
+    const uint4 *p = reinterpret_cast<const uint4 *>(rec) + 2 * (size_t)i;
+    const uint4 a = p[0], b = p[1];
+    k[0] = a.x; k[1] = a.y; k[2] = a.z; k[3] = a.w;
+    T = (uint64_t)b.x | ((uint64_t)b.y << 32);
+    L = b.z;
+    dport = b.w & 0xFFFFu;
+    return ((b.w >> 16) & 0xFFu) == 6 ? 2u : 1u;
+}
+
 constexpr uint64_t kShardSeed = 0x5A4D0F5EED5ull;   // fixed: every rank must agree
 
 // One blacklist entry of the replicated blocklist (all-gathered between ranks).
@@ -56,10 +77,11 @@ __host__ __device__ inline uint32_t shard_owner_of(uint32_t tag, const uint32_t 
 }
 
 // owner_total: [G] per-owner records, [G] replica drops, [G + 1] (compact only) record bytes.
+// own8 [n] and crec [n] (16-byte records in arrival order) are scratch.
 hipError_t launch_shard_pack(const uint8_t *hdr, const uint32_t *len, const uint64_t *ts, uint32_t n,
                              uint32_t G, uint8_t *verdict, void *rec, uint32_t *send_idx,
-                             uint64_t *owner_total, uint32_t *scratch, const Replica *rep,
-                             bool compact, hipStream_t st);
+                             uint64_t *owner_total, uint32_t *scratch, uint8_t *own8, void *crec,
+                             const Replica *rep, bool compact, hipStream_t st);
 hipError_t launch_shard_clock(const uint64_t *ts, uint32_t n, uint64_t *out3, hipStream_t st);
 hipError_t launch_blocklist_export(const Slot *table, uint64_t table_mask, ShardBlock *out, uint64_t cap,
                                    unsigned long long *count, hipStream_t st);

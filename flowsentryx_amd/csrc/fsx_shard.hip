@@ -3,10 +3,12 @@
 // Every rank holds a contiguous slice of the arrival stream. All limiter state is per
 // source IP, so a source's packets are routed to one owner rank, owner = H(family, key)
 // (fsx_shard_owner), which runs the unchanged batch pipeline on them:
-//   k_shard_count     parse (src/parsing_helper.h:49-136 rules) + owner of every IP
-//                     packet; per-tile per-owner counts
+//   k_shard_parse     parse (src/parsing_helper.h:49-136 rules) + owner of every IP
+//                     packet from coalesced, LDS-staged header loads; per-tile per-owner
+//                     counts, local verdicts, and the 16-byte records in arrival order
 //   k_shard_scan      exclusive scan over (owner, tile) -> send offsets, per-owner totals
-//   k_shard_pack      stable partition by owner into 32-byte records {src key, ts, len,
+//   k_shard_pack16 /  stable partition by owner (16-byte records from k_shard_parse's
+//   k_shard_pack      arrival-order copy / re-parsed into 32-byte records {src key, ts, len,
 //                     L4 dst port, family} (16-byte {IPv4 key, len, dport, ts} when the
 //                     caller allows it and the slice has no IPv6 source and no frame of
 //                     64 KiB or more); local verdicts for the packets that never
@@ -97,35 +99,138 @@ __device__ __forceinline__ uint32_t shard_classify(const uint8_t *rec, uint32_t 
 }
 
 // Per tile: per-owner IP-packet counts, owner-major [G][tiles].
-// wide: (compact requests only) set when an IP packet needs the 32-byte record.
-__global__ __launch_bounds__(256) void k_shard_count(const uint8_t *__restrict__ hdr,
+__global__ void k_shard_fmt_init(unsigned long long *wide) { *wide = 0; }
+
+// One pass over the headers (the k_count counts of k_shard_count, plus everything the
+// compact pack needs): a tile of 4096 packets per block, wave w owns [w*1024, +1024) in
+// 64-packet steps whose records are loaded with four coalesced 1 KiB wave loads and
+// staged through LDS (17-dword pitch, as k_parse). Per packet: its verdict when it never
+// reaches a limiter (and a PASS placeholder otherwise), its owner (0xFF: not sent) and,
+// for an IPv4 packet, its 16-byte record in arrival order (compact requests).
+__global__ __launch_bounds__(256) void k_shard_parse(const uint8_t *__restrict__ hdr,
                                                      const uint32_t *__restrict__ len,
                                                      const uint64_t *__restrict__ ts, uint32_t n,
                                                      uint32_t G, uint32_t *__restrict__ cnt,
                                                      uint32_t ntiles, Replica rep, int use_rep,
-                                                     unsigned long long *wide) {
+                                                     unsigned long long *wide,
+                                                     uint8_t *__restrict__ verdict,
+                                                     uint8_t *__restrict__ own8,
+                                                     ShardRecord16 *__restrict__ crec,
+                                                     uint64_t *__restrict__ owner_total) {
+    __shared__ uint32_t s_rec[4][64 * 17];
     __shared__ uint32_t sh[kMaxShards];
-    const uint32_t t = blockIdx.x;
+    const uint32_t t = blockIdx.x, lane = lane_id(), w = threadIdx.x >> 6;
     if (threadIdx.x < kMaxShards) sh[threadIdx.x] = 0;
     __syncthreads();
+    uint32_t *rec = s_rec[w];
     bool need_wide = false;
-    for (uint32_t r = 0; r < 16; ++r) {
-        const uint32_t i = t * kShardTile + r * 256u + threadIdx.x;
-        if (i >= n) break;
-        uint32_t k[4], dp;
-        const uint32_t L = len[i];
-        const uint32_t f = shard_classify(hdr + (size_t)i * 64, L, ts[i], use_rep ? &rep : nullptr, k, dp);
-        if (f >= 4) {
-            atomicAdd(&sh[owner_dev(f, k, G)], 1u);
-            need_wide |= f == 6 || L > 0xFFFFu;
+    uint32_t filtered = 0;
+    for (uint32_t j = 0; j < kShardTile / 256u; ++j) {
+        const uint32_t base = t * kShardTile + w * 1024u + j * 64u;
+        const uint8_t *src = hdr + (size_t)base * 64;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t g = (uint32_t)k * 1024u + lane * 16u;
+            uint4 x = make_uint4(0, 0, 0, 0);
+            if (base + (g >> 6) < n) x = *reinterpret_cast<const uint4 *>(src + g);
+            uint32_t *d = rec + (g >> 6) * 17u + ((g & 63u) >> 2);
+            d[0] = x.x; d[1] = x.y; d[2] = x.z; d[3] = x.w;
         }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        const uint32_t i = base + lane;
+        if (i < n) {
+            // the staged record: 64 contiguous LDS bytes (shard_parse reads dwords and the
+            // L4 port bytes)
+            const uint32_t L = len[i];
+            const uint64_t now = ts[i];
+            uint32_t k[4], dp;
+            const uint32_t f = shard_classify(reinterpret_cast<const uint8_t *>(rec + lane * 17u), L, now,
+                                              use_rep ? &rep : nullptr, k, dp);
+            uint8_t o = 0xFFu;
+            if (f >= 4) {
+                o = (uint8_t)owner_dev(f, k, G);
+                atomicAdd(&sh[o], 1u);
+                need_wide |= f == 6 || L > 0xFFFFu;
+                if (crec && f == 4) {
+                    ShardRecord16 x;
+                    x.key = k[0];
+                    x.len = (uint16_t)L;
+                    x.dport = (uint16_t)dp;
+                    x.ts = now;
+                    crec[i] = x;
+                }
+            }
+            // parse DROP / non-IP PASS are never counted; a replica DROP is counted in
+            // stats_map.dropped (src/fsx_kern.c:208-214) by the host
+            verdict[i] = f == 1 || f >= 4 ? 2u : 1u;
+            filtered += f == 2;
+            own8[i] = o;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     }
-    if (wide && __ballot(need_wide) && lane_id() == 0) atomicOr(wide, 1ull);
+    if (wide && __ballot(need_wide) && lane == 0) atomicOr(wide, 1ull);
+    filtered = wave_sum(filtered);
+    if (lane == 0 && filtered)
+        atomicAdd(reinterpret_cast<unsigned long long *>(&owner_total[G]), (unsigned long long)filtered);
     __syncthreads();
     if (threadIdx.x < G) cnt[(size_t)threadIdx.x * ntiles + t] = sh[threadIdx.x];
 }
 
-__global__ void k_shard_fmt_init(unsigned long long *wide) { *wide = 0; }
+// Compact pack (16-byte records, no header re-read): per tile, the owners and records
+// k_shard_parse left in arrival order are placed stably at their owners' offsets.
+__global__ __launch_bounds__(256) void k_shard_pack16(const uint8_t *__restrict__ own8,
+                                                      const ShardRecord16 *__restrict__ crec,
+                                                      uint32_t n, uint32_t G,
+                                                      const uint32_t *__restrict__ offs, uint32_t ntiles,
+                                                      ShardRecord16 *__restrict__ rec,
+                                                      uint32_t *__restrict__ send_idx,
+                                                      const uint64_t *__restrict__ owner_total) {
+    __shared__ uint32_t s_wc[4][kMaxShards];
+    if (owner_total[G + 1] != 16u) return;   // wide slice: k_shard_pack places 32-byte records
+    const uint32_t t = blockIdx.x, lane = lane_id(), w = threadIdx.x >> 6;
+    for (uint32_t o = threadIdx.x; o < 4 * kMaxShards; o += 256) (&s_wc[0][0])[o] = 0;
+    __syncthreads();
+    uint8_t ob[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const uint32_t i = t * kShardTile + w * 1024u + (uint32_t)r * 64u + lane;
+        ob[r] = i < n ? own8[i] : 0xFFu;
+        if (ob[r] != 0xFFu) atomicAdd(&s_wc[w][ob[r]], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x < G) {   // exclusive over the waves, from the tile's owner base
+        const uint32_t o = threadIdx.x;
+        uint32_t b = offs[(size_t)o * ntiles + t];
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t c = s_wc[k][o];
+            s_wc[k][o] = b;
+            b += c;
+        }
+    }
+    __syncthreads();
+    const uint64_t lt = (1ull << lane) - 1ull;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const uint32_t i = t * kShardTile + w * 1024u + (uint32_t)r * 64u + lane;
+        const uint32_t own = ob[r];
+        const bool ip = own != 0xFFu;
+        uint64_t peers = __ballot(ip);
+        for (uint32_t b = 0; (1u << b) < G; ++b) {
+            const bool bit = (own >> b) & 1u;
+            const uint64_t bal = __ballot(ip && bit);
+            peers &= bit ? bal : ~bal;
+        }
+        const uint32_t below = (uint32_t)__popcll(peers & lt);
+        uint32_t base = 0;
+        if (ip && below == 0) base = atomicAdd(&s_wc[w][own], (uint32_t)__popcll(peers));
+        base = __shfl(base, ip ? __ffsll((unsigned long long)peers) - 1 : 0);
+        if (ip) {
+            const uint32_t slot = base + below;
+            rec[slot] = crec[i];
+            send_idx[slot] = i;
+        }
+    }
+}
 
 // One block: exclusive scan of cnt in owner-major order (in place) and per-owner totals.
 __global__ __launch_bounds__(1024) void k_shard_scan(uint32_t *__restrict__ cnt, uint64_t total_n,
@@ -161,8 +266,7 @@ __global__ __launch_bounds__(1024) void k_shard_scan(uint32_t *__restrict__ cnt,
         owner_total[o] = b1 - b0;
     }
     if (threadIdx.x == 0) {
-        owner_total[G] = 0;   // packets dropped by the replica (k_shard_pack)
-        // compact requests: the wide flag of k_shard_count becomes the record size
+        // compact requests: the wide flag of k_shard_parse becomes the record size
         if (compact) owner_total[G + 1] = owner_total[G + 1] ? 32u : 16u;
     }
 }
@@ -177,19 +281,16 @@ __global__ __launch_bounds__(256) void k_shard_pack(const uint8_t *__restrict__ 
                                                     uint8_t *__restrict__ verdict, Replica rep,
                                                     int use_rep, uint64_t *__restrict__ owner_total,
                                                     int compact) {
-    const bool rec16 = compact && owner_total[G + 1] == 16u;
+    if (compact && owner_total[G + 1] == 16u) return;   // k_shard_pack16 places the records
     __shared__ uint32_t s_base[kMaxShards];
     __shared__ uint32_t s_wc[4][kMaxShards];
-    __shared__ uint32_t s_filtered;
     const uint32_t t = blockIdx.x, lane = lane_id(), w = threadIdx.x >> 6;
     if (threadIdx.x < G) s_base[threadIdx.x] = offs[(size_t)threadIdx.x * ntiles + t];
     // wave w owns packets [t*4096 + w*1024, +1024) in arrival order: count per owner
     // first (so a wave places after the waves before it), then place in order
     uint32_t of[16];   // owner << 4 | class (0 DROP, 1 PASS, 4/6 IP, 15 none)
     for (uint32_t o = threadIdx.x; o < 4 * kMaxShards; o += 256) (&s_wc[0][0])[o] = 0;
-    if (threadIdx.x == 0) s_filtered = 0;
     __syncthreads();
-    uint32_t filtered = 0;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
         const uint32_t i = t * kShardTile + w * 1024u + (uint32_t)r * 64u + lane;
@@ -206,15 +307,10 @@ __global__ __launch_bounds__(256) void k_shard_pack(const uint8_t *__restrict__ 
                 // parse DROP / non-IP PASS are never counted; a replica DROP is counted
                 // in stats_map.dropped (src/fsx_kern.c:208-214) by the host
                 verdict[i] = f == 1 ? 2u : 1u;
-                filtered += f == 2;
             }
         }
     }
-    filtered = wave_sum(filtered);
-    if (lane == 0 && filtered) atomicAdd(&s_filtered, filtered);
     __syncthreads();
-    if (threadIdx.x == 0 && s_filtered)
-        atomicAdd(reinterpret_cast<unsigned long long *>(&owner_total[G]), (unsigned long long)s_filtered);
     if (threadIdx.x < G) {   // exclusive over the waves, from the tile's owner base
         const uint32_t o = threadIdx.x;
         uint32_t b = s_base[o];
@@ -246,23 +342,14 @@ __global__ __launch_bounds__(256) void k_shard_pack(const uint8_t *__restrict__ 
             uint32_t k[4], dp;
             shard_parse(hdr + (size_t)i * 64, len[i], k, dp);
             const uint32_t slot = base + below;
-            if (rec16) {
-                ShardRecord16 x;
-                x.key = k[0];
-                x.len = (uint16_t)len[i];
-                x.dport = (uint16_t)dp;
-                x.ts = ts[i];
-                reinterpret_cast<ShardRecord16 *>(rec)[slot] = x;
-            } else {
-                ShardRecord x;
-                x.key[0] = k[0]; x.key[1] = k[1]; x.key[2] = k[2]; x.key[3] = k[3];
-                x.ts = ts[i];
-                x.len = len[i];
-                x.dport = (uint16_t)dp;
-                x.family = (uint8_t)f;
-                x.pad = 0;
-                reinterpret_cast<ShardRecord *>(rec)[slot] = x;
-            }
+            ShardRecord x;
+            x.key[0] = k[0]; x.key[1] = k[1]; x.key[2] = k[2]; x.key[3] = k[3];
+            x.ts = ts[i];
+            x.len = len[i];
+            x.dport = (uint16_t)dp;
+            x.family = (uint8_t)f;
+            x.pad = 0;
+            reinterpret_cast<ShardRecord *>(rec)[slot] = x;
             send_idx[slot] = i;
             verdict[i] = 2u;   // placeholder until the owner's verdict returns
         }
@@ -333,20 +420,23 @@ __global__ void k_shard_empty(uint64_t *owner_total, uint32_t G, int compact) {
 
 hipError_t launch_shard_pack(const uint8_t *hdr, const uint32_t *len, const uint64_t *ts, uint32_t n,
                              uint32_t G, uint8_t *verdict, void *rec, uint32_t *send_idx,
-                             uint64_t *owner_total, uint32_t *scratch, const Replica *rep,
-                             bool compact, hipStream_t st) {
+                             uint64_t *owner_total, uint32_t *scratch, uint8_t *own8, void *crec,
+                             const Replica *rep, bool compact, hipStream_t st) {
     (void)hipGetLastError();   // a stale error of another caller is not ours
-    if (n == 0) {
-        k_shard_empty<<<1, 1, 0, st>>>(owner_total, G, compact);
-        return hipGetLastError();
-    }
+    k_shard_empty<<<1, 1, 0, st>>>(owner_total, G, compact);   // also the wide flag / filtered
+    if (n == 0) return hipGetLastError();
     const uint32_t ntiles = (n + kShardTile - 1) / kShardTile;
     const Replica r = rep ? *rep : Replica{nullptr, 0};
     const int use = rep != nullptr && rep->slots != nullptr;
     unsigned long long *wide = compact ? reinterpret_cast<unsigned long long *>(owner_total + G + 1) : nullptr;
     if (wide) k_shard_fmt_init<<<1, 1, 0, st>>>(wide);
-    k_shard_count<<<ntiles, 256, 0, st>>>(hdr, len, ts, n, G, scratch, ntiles, r, use, wide);
+    ShardRecord16 *cr = compact ? reinterpret_cast<ShardRecord16 *>(crec) : nullptr;
+    k_shard_parse<<<ntiles, 256, 0, st>>>(hdr, len, ts, n, G, scratch, ntiles, r, use, wide, verdict, own8, cr,
+                                          owner_total);
     k_shard_scan<<<1, 1024, 0, st>>>(scratch, n, owner_total, G, ntiles, compact);
+    if (compact)
+        k_shard_pack16<<<ntiles, 256, 0, st>>>(own8, cr, n, G, scratch, ntiles,
+                                               reinterpret_cast<ShardRecord16 *>(rec), send_idx, owner_total);
     k_shard_pack<<<ntiles, 256, 0, st>>>(hdr, len, ts, n, G, scratch, ntiles, rec, send_idx, verdict, r,
                                          use, owner_total, compact);
     return hipGetLastError();

@@ -116,6 +116,8 @@ def load_library() -> C.CDLL:
         "fsx_verdict_batch": (C.c_int, [vp, u8p, u8p, u8p, sz, u8p]),
         "fsx_verdict_batch_device": (C.c_int, [vp, vp, vp, vp, sz, vp]),
         "fsx_process_batch_device": (C.c_int, [vp, vp, vp, vp, sz, vp, vp, vp, vp, vp, vp, sz]),
+        "fsx_verdict_records_device": (C.c_int, [vp, vp, sz, C.c_uint32, vp]),
+        "fsx_process_records_device": (C.c_int, [vp, vp, sz, C.c_uint32, vp, vp, vp, vp, vp, vp, sz]),
         "fsx_map_lookup": (C.c_int, [vp, C.c_int, vp, vp]),
         "fsx_map_update": (C.c_int, [vp, C.c_int, vp, vp, C.c_uint64]),
         "fsx_map_delete": (C.c_int, [vp, C.c_int, vp]),
@@ -151,7 +153,7 @@ def load_library() -> C.CDLL:
 ABI_SYMBOLS = [
     "fsx_abi_version", "fsx_config_default", "fsx_open", "fsx_close", "fsx_last_error",
     "fsx_set_stream", "fsx_sync", "fsx_verdict_batch", "fsx_verdict_batch_device",
-    "fsx_process_batch_device",
+    "fsx_process_batch_device", "fsx_verdict_records_device", "fsx_process_records_device",
     "fsx_map_lookup", "fsx_map_update", "fsx_map_delete", "fsx_map_dump", "fsx_get_stats",
     "fsx_reset", "fsx_load_q8_model", "fsx_score", "fsx_score_device", "fsx_flow_features",
     "fsx_last_timings", "fsx_enable_timing", "fsx_last_batch_info",
@@ -278,6 +280,19 @@ class FsxContext:
                                                        d_keys16, d_family, d_features, d_prob,
                                                        d_malicious, flow_cap),
                     "fsx_process_batch_device")
+
+    def verdict_records_device(self, d_records: int, n: int, rec_bytes: int, d_verdict: int):
+        """Owner side of the sharded path: the pipeline on n exchange records (asynchronous)."""
+        self._check(self._lib.fsx_verdict_records_device(self._h, d_records, n, rec_bytes, d_verdict),
+                    "fsx_verdict_records_device")
+
+    def process_records_device(self, d_records: int, n: int, rec_bytes: int, d_verdict: int,
+                               d_keys16: int, d_family: int, d_features: int | None,
+                               d_prob: int | None, d_malicious: int | None, flow_cap: int):
+        self._check(self._lib.fsx_process_records_device(self._h, d_records, n, rec_bytes, d_verdict,
+                                                         d_keys16, d_family, d_features, d_prob,
+                                                         d_malicious, flow_cap),
+                    "fsx_process_records_device")
 
     # -- maps (bpf_map_*_elem)
     def map_lookup(self, map_id: int, key):

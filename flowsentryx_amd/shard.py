@@ -12,8 +12,9 @@ unchanged batch pipeline on all of that source's packets:
                limiter (short frames DROP, non-IP PASS)
   2. all-to-all of the per-owner counts (record format in the low bit), then of the
      records (RCCL over xGMI)
-  3. owner     records -> header records, the batch pipeline on them (maps, verdicts,
-               optionally flow features + MLP scores of the owned sources)
+  3. owner     the batch pipeline straight on the received records (record mode; when
+               senders used both record sizes: records -> header records first) — maps,
+               verdicts, optionally flow features + MLP scores of the owned sources
   4. all-to-all of the verdicts back (1 byte per packet), scatter to arrival positions
   5. all-gather of every owner's live blacklist entries (the replicated blocklist);
      the next sub-batch's pack drops packets of replica-blacklisted sources locally
@@ -85,6 +86,7 @@ class HipShardEngine:
         self.blk = torch.empty(1024 * lib.SHARD_BLOCK_BYTES, dtype=torch.uint8, device=device)
         self.blk_count = torch.empty(1, dtype=torch.int64, device=device)
         self._oh = None  # owner-side header/len/ts/verdict buffers, grown on demand
+        self._ov = None  # owner-side verdicts of record-mode batches
         self.flows = None
 
     @contextlib.contextmanager
@@ -117,6 +119,19 @@ class HipShardEngine:
     def direct(self, hdr, length, ts, n, verdict):
         """G == 1: the batch pipeline straight on the local slice."""
         self._run(hdr.data_ptr(), length.data_ptr(), ts.data_ptr(), n, verdict.data_ptr())
+
+    def _owner_verdicts(self, m: int) -> torch.Tensor:
+        if self._ov is None or self._ov.numel() < m:
+            self._ov = torch.empty(max(m, 1), dtype=torch.uint8, device=self.device)
+        return self._ov
+
+    def _run_records(self, rec, n, rb, v):
+        if self.flows is None:
+            self.ctx.verdict_records_device(rec, n, rb, v)
+        else:
+            f = self.flows
+            self.ctx.process_records_device(rec, n, rb, v, f["keys"].data_ptr(), f["fam"].data_ptr(),
+                                            None, f["prob"].data_ptr(), f["dec"].data_ptr(), f["cap"])
 
     def _run(self, h, l, t, n, v):
         if self.flows is None:
@@ -180,6 +195,15 @@ class HipShardEngine:
         offset, records, record bytes)] per sender (chunked by the context's max_batch:
         state carries across chunks exactly as across batches)."""
         m = sum(c for _, c, _ in segs)
+        fmts = {rb for _, c, rb in segs if c}
+        if len(fmts) == 1:
+            # one record format: the pipeline reads the received records directly
+            rb = fmts.pop()
+            v = self._owner_verdicts(m)
+            for a in range(0, m, self.owner_cap):
+                b = min(m, a + self.owner_cap)
+                self._run_records(recv.data_ptr() + a * rb, b - a, rb, v.data_ptr() + a)
+            return v[:max(m, 1)]
         hdr, ln, ts, v = self._owner_buffers(m)
         r = 0
         for off, cnt, rb in segs:

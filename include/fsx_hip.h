@@ -250,6 +250,17 @@ int fsx_shard_unpack_device(fsx_ctx *ctx, const void *d_records, size_t m, uint8
 /* Same for m compact 16-byte IPv4 records. */
 int fsx_shard_unpack16_device(fsx_ctx *ctx, const void *d_records, size_t m, uint8_t *d_hdr,
                               uint32_t *d_len, uint64_t *d_ts);
+/* Owner side, record mode: the batch pipeline straight on n received exchange records
+ * of rec_bytes each (FSX_SHARD_RECORD_BYTES or FSX_SHARD_RECORD16_BYTES; one format per
+ * call), in their order — verdicts and map state exactly as fsx_verdict_batch_device /
+ * fsx_process_batch_device on the header records fsx_shard_unpack_device would build,
+ * without building them. */
+int fsx_verdict_records_device(fsx_ctx *ctx, const void *d_records, size_t n, uint32_t rec_bytes,
+                               uint8_t *d_verdict);
+int fsx_process_records_device(fsx_ctx *ctx, const void *d_records, size_t n, uint32_t rec_bytes,
+                               uint8_t *d_verdict, uint8_t *d_keys16, uint8_t *d_family,
+                               float *d_features, float *d_prob, uint8_t *d_malicious,
+                               size_t flow_cap);
 /* Origin side: d_verdict[d_send_idx[i]] = d_ret[i] for the m returned verdicts. */
 int fsx_shard_scatter_device(fsx_ctx *ctx, const uint8_t *d_ret, const uint32_t *d_send_idx,
                              size_t m, uint8_t *d_verdict);

@@ -1,0 +1,78 @@
+"""Single-GPU timing of the sharded path's local kernels on a config-2 batch: pack (parse
++ owner partition into exchange records) for G owners, and the owner-side unpack of the
+records a rank would receive. The collectives themselves need a multi-GPU node.
+"""
+import json
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, ".")
+from flowsentryx_amd import lib, synth  # noqa: E402
+from flowsentryx_amd.shard import HipShardEngine  # noqa: E402
+
+
+def main():
+    G = int(sys.argv[1]) if len(sys.argv) > 1 else 8
+    p, s = synth.config_params(2)
+    n = int(p.n)
+    dev = torch.device("cuda", 0)
+    hdr = torch.empty(n * 64, dtype=torch.uint8, device=dev)
+    ln = torch.empty(n, dtype=torch.int32, device=dev)
+    ts = torch.empty(n, dtype=torch.int64, device=dev)
+    v = torch.empty(n, dtype=torch.uint8, device=dev)
+    synth.generate_device(p, s, 0, n, hdr.data_ptr(), ln.data_ptr(), ts.data_ptr())
+    torch.cuda.synchronize()
+    out = {"G": G, "n": n}
+    with lib.FsxContext(max_batch=n, max_entries=int(p.n_ips), device=0) as ctx:
+        e = HipShardEngine(ctx, n, dev)
+        with e.stream_ctx():
+            for _ in range(2):
+                rec, counts = e.pack(hdr, ln, ts, n, G, v)
+            ctx.sync()
+            t0 = time.perf_counter()
+            for _ in range(5):
+                rec, counts = e.pack(hdr, ln, ts, n, G, v)
+            ctx.sync()
+            out["pack_ms"] = (time.perf_counter() - t0) / 5 * 1e3
+            c = counts.tolist()
+            rb = int(c[G + 1])
+            m = int(sum(c[:G]))
+            out["record_bytes"] = rb
+            hb, lb, tb, _ = e._owner_buffers(m)
+            segs = [(0, m, rb)]
+            ctx.shard_unpack_device(rec.data_ptr(), m, hb.data_ptr(), lb.data_ptr(), tb.data_ptr(), rb)
+            ctx.sync()
+            t0 = time.perf_counter()
+            for _ in range(5):
+                ctx.shard_unpack_device(rec.data_ptr(), m, hb.data_ptr(), lb.data_ptr(), tb.data_ptr(), rb)
+            ctx.sync()
+            out["unpack_ms"] = (time.perf_counter() - t0) / 5 * 1e3
+            out["records"] = m
+            out["exchange_bytes_per_rank"] = m * rb * (G - 1) // G
+            # owner pipeline on all records in arrival order (a G = 1 pack: monotone clock,
+            # as every owner's received stream is)
+            rec, counts = e.pack(hdr, ln, ts, n, 1, v)
+            m = int(counts[0].item())
+            ov = torch.empty(m, dtype=torch.uint8, device=dev)
+            for mode in ("records", "headers"):
+                for it in range(4):
+                    if it == 1:
+                        ctx.sync()
+                        t0 = time.perf_counter()
+                    ctx.reset()
+                    if mode == "records":
+                        ctx.verdict_records_device(rec.data_ptr(), m, rb, ov.data_ptr())
+                    else:
+                        ctx.shard_unpack_device(rec.data_ptr(), m, hb.data_ptr(), lb.data_ptr(),
+                                                tb.data_ptr(), rb)
+                        ctx.verdict_batch_device(hb.data_ptr(), lb.data_ptr(), tb.data_ptr(), m,
+                                                 ov.data_ptr())
+                ctx.sync()
+                out[f"owner_{mode}_ms"] = (time.perf_counter() - t0) / 3 * 1e3
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
