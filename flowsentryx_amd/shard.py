@@ -77,17 +77,49 @@ class HipShardEngine:
         # stream: a NULL handle would give the context its own stream back)
         self.stream = torch.cuda.Stream(device)
         ctx.set_stream(self.stream.cuda_stream)
+        # collectives run from a second stream, so the exchange of sub-batch j + 1 overlaps
+        # the owner pipeline of sub-batch j (ShardedDataPlane)
+        self.comm = torch.cuda.Stream(device)
         self.max_local = max_local
         self.owner_cap = int(ctx.config.max_batch)
-        self.rec = torch.empty(max(1, max_local) * REC, dtype=torch.uint8, device=device)
-        self.send_idx = torch.empty(max(1, max_local), dtype=torch.int32, device=device)
-        self.counts = torch.empty(lib.MAX_SHARDS + 2, dtype=torch.int64, device=device)
+        # two pipeline slots: sub-batch j uses slot j % 2 of every per-sub-batch buffer
+        self.recs = [torch.empty(max(1, max_local) * REC, dtype=torch.uint8, device=device)
+                     for _ in range(2)]
+        self.send_idxs = [torch.empty(max(1, max_local), dtype=torch.int32, device=device)
+                          for _ in range(2)]
+        self.countss = [torch.empty(lib.MAX_SHARDS + 2, dtype=torch.int64, device=device)
+                        for _ in range(2)]
+        self.rec, self.send_idx, self.counts = self.recs[0], self.send_idxs[0], self.countss[0]
         self.clock3 = torch.empty(3, dtype=torch.int64, device=device)
         self.blk = torch.empty(1024 * lib.SHARD_BLOCK_BYTES, dtype=torch.uint8, device=device)
         self.blk_count = torch.empty(1, dtype=torch.int64, device=device)
-        self._oh = None  # owner-side header/len/ts/verdict buffers, grown on demand
-        self._ov = None  # owner-side verdicts of record-mode batches
+        self._oh = None  # owner-side header/len/ts buffers, grown on demand
+        self._ov = [None, None]   # owner-side verdicts per slot
         self.flows = None
+
+    # -- streams of the pipelined plane (the CPU engine has none)
+    @contextlib.contextmanager
+    def comm_ctx(self):
+        """Collectives on the comm stream, after all work enqueued on the engine stream."""
+        self.comm.wait_stream(self.stream)
+        with torch.cuda.stream(self.comm):
+            yield
+
+    def comm_event(self):
+        """An event after the work enqueued on the comm stream so far."""
+        ev = torch.cuda.Event()
+        ev.record(self.comm)
+        return ev
+
+    def engine_wait(self, ev):
+        """The engine stream continues after `ev` (a comm_event)."""
+        self.stream.wait_event(ev)
+
+    def keep(self, t: torch.Tensor):
+        """t (allocated on the comm stream) is also used by the engine stream: its memory
+        is not reused before the engine stream's work so far has finished."""
+        if t.is_cuda:
+            t.record_stream(self.stream)
 
     @contextlib.contextmanager
     def stream_ctx(self):
@@ -120,10 +152,10 @@ class HipShardEngine:
         """G == 1: the batch pipeline straight on the local slice."""
         self._run(hdr.data_ptr(), length.data_ptr(), ts.data_ptr(), n, verdict.data_ptr())
 
-    def _owner_verdicts(self, m: int) -> torch.Tensor:
-        if self._ov is None or self._ov.numel() < m:
-            self._ov = torch.empty(max(m, 1), dtype=torch.uint8, device=self.device)
-        return self._ov
+    def _owner_verdicts(self, m: int, slot: int) -> torch.Tensor:
+        if self._ov[slot] is None or self._ov[slot].numel() < m:
+            self._ov[slot] = torch.empty(max(m, 1), dtype=torch.uint8, device=self.device)
+        return self._ov[slot]
 
     def _run_records(self, rec, n, rb, v):
         if self.flows is None:
@@ -162,16 +194,18 @@ class HipShardEngine:
         self.ctx.blocklist_export_device(buf.data_ptr() + B, cap, buf.data_ptr())
         return buf
 
-    def pack(self, hdr, length, ts, n, G, verdict, filt=False):
+    def pack(self, hdr, length, ts, n, G, verdict, filt=False, slot=0):
         """-> records, counts[G + 2] (counts[G]: packets dropped by the replica,
-        counts[G + 1]: record bytes, 16 or 32)."""
+        counts[G + 1]: record bytes, 16 or 32), in pipeline slot `slot`."""
         if n > self.max_local:
             raise ValueError(f"local slice of {n} packets exceeds {self.max_local}")
         flags = lib.SHARD_COMPACT | (lib.SHARD_FILTER_BLOCKLIST if filt else 0)
+        rec, idx, cnt = self.recs[slot], self.send_idxs[slot], self.countss[slot]
+        self.rec, self.send_idx, self.counts = rec, idx, cnt   # (tests read the last pack)
         self.ctx.shard_pack_device(hdr.data_ptr(), length.data_ptr(), ts.data_ptr(), n, G,
-                                   verdict.data_ptr(), self.rec.data_ptr(),
-                                   self.send_idx.data_ptr(), self.counts.data_ptr(), flags)
-        return self.rec, self.counts[:G + 2]
+                                   verdict.data_ptr(), rec.data_ptr(), idx.data_ptr(), cnt.data_ptr(),
+                                   flags)
+        return rec, cnt[:G + 2]
 
     def export_blocklist(self) -> tuple[torch.Tensor, int]:
         """This rank's live blacklist entries (32-byte records) and their count."""
@@ -190,7 +224,7 @@ class HipShardEngine:
     def recv_buffer(self, nbytes: int) -> torch.Tensor:
         return torch.empty(max(1, nbytes), dtype=torch.uint8, device=self.device)
 
-    def owner_batch(self, recv: torch.Tensor, segs) -> torch.Tensor:
+    def owner_batch(self, recv: torch.Tensor, segs, slot: int = 0) -> torch.Tensor:
         """The limiter over the received records, in received order: segs = [(byte
         offset, records, record bytes)] per sender (chunked by the context's max_batch:
         state carries across chunks exactly as across batches)."""
@@ -199,12 +233,13 @@ class HipShardEngine:
         if len(fmts) == 1:
             # one record format: the pipeline reads the received records directly
             rb = fmts.pop()
-            v = self._owner_verdicts(m)
+            v = self._owner_verdicts(m, slot)
             for a in range(0, m, self.owner_cap):
                 b = min(m, a + self.owner_cap)
                 self._run_records(recv.data_ptr() + a * rb, b - a, rb, v.data_ptr() + a)
             return v[:max(m, 1)]
-        hdr, ln, ts, v = self._owner_buffers(m)
+        hdr, ln, ts, _ = self._owner_buffers(m)
+        v = self._owner_verdicts(m, slot)
         r = 0
         for off, cnt, rb in segs:
             if cnt:
@@ -217,9 +252,9 @@ class HipShardEngine:
                       b - a, v.data_ptr() + a)
         return v[:max(m, 1)]
 
-    def scatter(self, ret: torch.Tensor, m: int, verdict):
+    def scatter(self, ret: torch.Tensor, m: int, verdict, slot: int = 0):
         if m:
-            self.ctx.shard_scatter_device(ret.data_ptr(), self.send_idx.data_ptr(), m,
+            self.ctx.shard_scatter_device(ret.data_ptr(), self.send_idxs[slot].data_ptr(), m,
                                           verdict.data_ptr())
 
     def stats(self) -> torch.Tensor:
@@ -254,7 +289,11 @@ class ShardedDataPlane:
     def verdict_batch(self, hdr, length, ts, n: int, verdict, chunks: int = 1, bounds=None):
         """Verdicts for this rank's slice (arrival order) of one global batch; every rank
         calls it once per batch with its own slice, cut into `chunks` equal sub-batch
-        pieces (or at the explicit local cut points `bounds`, chunks + 1 of them)."""
+        pieces (or at the explicit local cut points `bounds`, chunks + 1 of them).
+
+        Sub-batches run as a two-stage software pipeline: the pack and record exchange of
+        sub-batch j + 1 (collectives on the engine's comm stream) overlap the owner
+        pipeline of sub-batch j; buffers alternate between two slots."""
         with self.engine.stream_ctx():
             if self.world == 1:
                 self.engine.direct(hdr, length, ts, n, verdict)
@@ -264,70 +303,112 @@ class ShardedDataPlane:
             if bounds is None:
                 bounds = [n * i // chunks for i in range(chunks + 1)]
             k = len(bounds) - 1
-            mono = self._clocks_monotone(ts, bounds) if self.filter else [False] * k
+            filt = self._filter_plan(ts, bounds) if self.filter else [False] * k
+            pend = [None] * k
+            pend[0] = self._stage_exchange(hdr, length, ts, verdict, bounds, 0, filt[0])
             sent = recv = 0
-            for j, (a, b) in enumerate(zip(bounds[:-1], bounds[1:])):
-                # the replica refresh after the last piece is the next batch's first step
-                ms, mr = self._sub_batch(hdr[a * 64:], length[a:], ts[a:], b - a, verdict[a:],
-                                         mono[j], refresh=self.filter and j + 1 < k)
+            for j in range(k):
+                if j + 1 < k:   # enqueued before the owner work of j: its exchange overlaps it
+                    pend[j + 1] = self._stage_exchange(hdr, length, ts, verdict, bounds, j + 1,
+                                                       filt[j + 1])
+                ms, mr = self._stage_owner(verdict, bounds, j, pend[j])
+                pend[j] = None
                 sent, recv = sent + ms, recv + mr
+                # the replica packs j + 2 onward filter with (one sub-batch stale: exact for
+                # clocks that do not go back between consecutive sub-batches, _filter_plan)
+                if self.filter and j + 2 < k:
+                    self._sync_blocklist()
             self.last_exchange = {"sent": sent, "received": recv, "filtered": self.filtered}
 
-    def _clocks_monotone(self, ts, bounds) -> list:
-        """Per sub-batch: is its clock non-decreasing in global order (rank 0's piece,
-        then rank 1's, ...)? One all-gather of {min, max, decreases} of every piece."""
+    def _filter_plan(self, ts, bounds) -> list:
+        """Per sub-batch: may its pack drop replica-blacklisted packets? Pack j filters
+        with the replica refreshed at the batch start (j = 0, 1) or after the owners of
+        sub-batch j - 2 (j >= 2), so it can miss what the owners did in sub-batch j - 1.
+        A stale entry only drops packets the owner drops too unless some earlier packet
+        deleted it at a later time, so the filter is exact when the clock is
+        non-decreasing in global order (rank 0's piece, then rank 1's, ...) inside the
+        sub-batch and no packet of an earlier sub-batch of the batch is later than its
+        first. One all-gather of {min, max, decreases} of every piece."""
         k = len(bounds) - 1
         c = _all_gather(self.engine.clocks(ts, bounds), self.world, self.group).tolist()
-        out = []
+        within, lo, hi = [], [], []
         for j in range(k):
-            ok, last = True, None
+            ok, last, mn_j, mx_j = True, None, None, None
             for r in range(self.world):
                 mn, mx, dec = c[3 * (r * k + j): 3 * (r * k + j) + 3]
                 if dec:
                     ok = False
-                    break
                 if mx == 0 and mn == -1:      # empty piece ({~0, 0} as int64)
                     continue
-                if last is not None and (mn & (2**64 - 1)) < last:
+                mn, mx = mn & (2**64 - 1), mx & (2**64 - 1)
+                if last is not None and mn < last:
                     ok = False
-                    break
-                last = mx & (2**64 - 1)
+                last = mx
+                mn_j = mn if mn_j is None else min(mn_j, mn)
+                mx_j = mx if mx_j is None else max(mx_j, mx)
+            within.append(ok)
+            lo.append(mn_j)
+            hi.append(mx_j)
+        out = []
+        for j in range(k):
+            ok = within[j]
+            if ok and j >= 1:
+                prev = max((h for h in hi[:j] if h is not None), default=None)
+                if prev is not None and lo[j] is not None and lo[j] < prev:
+                    ok = False
             out.append(ok)
         return out
 
-    def _sub_batch(self, hdr, length, ts, n: int, verdict, filt: bool, refresh: bool):
+    def _stage_exchange(self, hdr, length, ts, verdict, bounds, j: int, filt: bool):
+        """Pack sub-batch j (engine stream) and exchange its counts and records (comm stream)."""
         G, e = self.world, self.engine
-        recs, counts = e.pack(hdr, length, ts, n, G, verdict, filt)
-        # per-owner counts with the record format in the low bit (device-side: the host
-        # reads its own and the received counts together, one synchronization)
-        send = (counts[:G] * 2 + (counts[G + 1] == lib.SHARD_RECORD16_BYTES).to(counts.dtype)).contiguous()
-        recv_counts = torch.empty_like(send)
-        ones = [1] * G
-        _a2a(recv_counts, send, ones, ones, self.group)
-        both = torch.cat([counts.to(recv_counts.device), recv_counts]).tolist()
-        cnt, rw = both[:G + 2], [int(x) for x in both[G + 2:]]
-        self.filtered += int(cnt[G])
-        rb = int(cnt[G + 1])   # this sender's record size (16: compact IPv4 records)
-        sc = [int(x) for x in cnt[:G]]
-        rc = [x >> 1 for x in rw]
-        rf = [lib.SHARD_RECORD16_BYTES if x & 1 else lib.SHARD_RECORD_BYTES for x in rw]
-        ms, mr = sum(sc), sum(rc)
-        in_b = [x * rb for x in sc]
-        out_b = [c * f for c, f in zip(rc, rf)]
-        recv = e.recv_buffer(sum(out_b))
-        _a2a(recv[:sum(out_b)], recs[:sum(in_b)], out_b, in_b, self.group)
-        segs, off = [], 0
-        for c, f, b in zip(rc, rf, out_b):
+        a, b = bounds[j], bounds[j + 1]
+        slot = j % 2
+        recs, counts = e.pack(hdr[a * 64:], length[a:], ts[a:], b - a, G, verdict[a:], filt, slot)
+        with e.comm_ctx():
+            # per-owner counts with the record format in the low bit; the host reads its
+            # own and the received counts together (one synchronization, comm stream)
+            send = (counts[:G] * 2 + (counts[G + 1] == lib.SHARD_RECORD16_BYTES).to(counts.dtype)).contiguous()
+            recv_counts = torch.empty_like(send)
+            ones = [1] * G
+            _a2a(recv_counts, send, ones, ones, self.group)
+            both = torch.cat([counts.to(recv_counts.device), recv_counts]).tolist()
+            cnt, rw = both[:G + 2], [int(x) for x in both[G + 2:]]
+            self.filtered += int(cnt[G])
+            rb = int(cnt[G + 1])   # this sender's record size (16: compact IPv4 records)
+            sc = [int(x) for x in cnt[:G]]
+            rc = [x >> 1 for x in rw]
+            rf = [lib.SHARD_RECORD16_BYTES if x & 1 else lib.SHARD_RECORD_BYTES for x in rw]
+            in_b = [x * rb for x in sc]
+            out_b = [c * f for c, f in zip(rc, rf)]
+            recv = e.recv_buffer(sum(out_b))
+            _a2a(recv[:sum(out_b)], recs[:sum(in_b)], out_b, in_b, self.group)
+        arrived = e.comm_event()      # only these records: the owner work of the previous
+        segs, off = [], 0             # sub-batch must not wait for later exchanges
+        for c, f, nb in zip(rc, rf, out_b):
             segs.append((off, c, f))
-            off += b
+            off += nb
             if c:
                 self.formats.add(f)
-        v = e.owner_batch(recv, segs)
-        ret = torch.empty(max(ms, 1), dtype=torch.uint8, device=v.device)
-        _a2a(ret[:ms], v[:mr], sc, rc, self.group)
-        e.scatter(ret, ms, verdict)
-        if refresh:
-            self._sync_blocklist()
+        return recv, segs, sc, rc, arrived
+
+    def _stage_owner(self, verdict, bounds, j: int, pend):
+        """Owner pipeline of sub-batch j (engine stream), verdicts back (comm stream) and
+        into arrival positions (engine stream)."""
+        G, e = self.world, self.engine
+        recv, segs, sc, rc, arrived = pend
+        a = bounds[j]
+        slot = j % 2
+        ms, mr = sum(sc), sum(rc)
+        e.engine_wait(arrived)        # the records of sub-batch j have arrived
+        e.keep(recv)                  # allocated on the comm stream, read on the engine's
+        v = e.owner_batch(recv, segs, slot)
+        with e.comm_ctx():
+            ret = torch.empty(max(ms, 1), dtype=torch.uint8, device=v.device)
+            _a2a(ret[:ms], v[:mr], sc, rc, self.group)
+        e.engine_wait(e.comm_event())
+        e.keep(ret)
+        e.scatter(ret, ms, verdict[a:], slot)
         return ms, mr
 
     def _sync_blocklist(self):

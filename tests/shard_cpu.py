@@ -54,10 +54,23 @@ class CpuShardEngine:
         self.oracle = oracle
         self.o = oracle.Oracle(**cfg)
         self.send_idx = np.zeros(0, dtype=np.int64)
+        self.send_idxs = [self.send_idx, self.send_idx]
         self.replica = {}
 
     def stream_ctx(self):
         return contextlib.nullcontext()
+
+    def comm_ctx(self):
+        return contextlib.nullcontext()
+
+    def comm_event(self):
+        return None
+
+    def engine_wait(self, ev):
+        pass
+
+    def keep(self, t):
+        pass
 
     @staticmethod
     def _np(hdr, length, ts, n):
@@ -86,7 +99,7 @@ class CpuShardEngine:
         buf[32:32 + k * 32] = ent[:k * 32]
         return buf
 
-    def pack(self, hdr, length, ts, n, G, verdict, filt=False):
+    def pack(self, hdr, length, ts, n, G, verdict, filt=False, slot=0):
         h, l, t = self._np(hdr, length, ts, n)
         cls, keys = self.oracle.parse(h, l)
         v = verdict.numpy()
@@ -114,6 +127,7 @@ class CpuShardEngine:
         rec["dport"] = self.oracle.dst_port(h[ip], l[ip]).astype(np.uint16)
         rec["family"] = fam
         self.send_idx = ip
+        self.send_idxs[slot] = ip
         counts = np.bincount(own, minlength=G).astype(np.int64)
         compact = not np.any(fam == 6) and not np.any(rec["len"] > 0xFFFF)
         if compact:
@@ -149,7 +163,7 @@ class CpuShardEngine:
     def recv_buffer(self, nbytes):
         return torch.empty(max(1, nbytes), dtype=torch.uint8)
 
-    def owner_batch(self, recv, segs):
+    def owner_batch(self, recv, segs, slot=0):
         b = recv.numpy()
         parts = []
         for off, cnt, rb in segs:
@@ -162,8 +176,8 @@ class CpuShardEngine:
         v = self.o.batch(h, l, t) if m else np.zeros(1, dtype=np.uint8)
         return torch.from_numpy(v)
 
-    def scatter(self, ret, m, verdict):
-        verdict.numpy()[self.send_idx] = ret.numpy()[:m]
+    def scatter(self, ret, m, verdict, slot=0):
+        verdict.numpy()[self.send_idxs[slot]] = ret.numpy()[:m]
 
     def stats(self):
         return torch.tensor(self.o.stats(), dtype=torch.int64)
