@@ -1760,8 +1760,8 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
         k_seg_order<<<kSegBlocks, 256, 0, st>>>(bs, sc.seg_start, sc.hist, sc.seg_order, short_seg);
         mark("k_seg_order");
         if (lim.limiter == 1) {   // FSX_LIMIT_SLIDING_WINDOW
-            if ((e = launch_sliding_window(S, ts, len, bs, sc, table, tstate, hist, lim, n, st, mk)) !=
-                hipSuccess)
+            if ((e = launch_sliding_window(S, ts, len, bs, sc, table, tstate, hist, lim, n, st, mk, st3,
+                                           walk_fork_ev, walk_join_ev)) != hipSuccess)
                 return e;
         } else {
             // short and long segments are disjoint: the wave walker runs on its own

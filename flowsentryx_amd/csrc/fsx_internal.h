@@ -307,9 +307,11 @@ hipError_t launch_token_bucket(const uint64_t *S, const uint64_t *ts, const uint
                                const Scratch &sc, Slot *table, const Limits &lim, uint32_t n,
                                hipStream_t st, const Marker &mark);
 
+// st3 (optional, with fork/join events): the long-segment walker beside the short one.
 hipError_t launch_sliding_window(const uint64_t *S, const uint64_t *ts, const uint32_t *len, BatchState *bs,
                                  const Scratch &sc, Slot *table, TableState *tstate, const HistBufs &hb,
-                                 const Limits &lim, uint32_t n, hipStream_t st, const Marker &mark);
+                                 const Limits &lim, uint32_t n, hipStream_t st, const Marker &mark,
+                                 hipStream_t st3, hipEvent_t fork_ev, hipEvent_t join_ev);
 
 hipError_t launch_pcap_records(const uint8_t *buf, const uint64_t *off, const uint32_t *caplen, uint32_t n,
                                uint8_t *hdr, hipStream_t st);

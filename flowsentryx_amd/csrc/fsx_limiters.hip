@@ -474,7 +474,13 @@ __device__ void sw_walk_fast_wave(const SV &sv, uint32_t a, uint32_t b, const Li
     uint32_t f = 0;                         // first virtual index of the current log
     while (p < b) {
         uint32_t k = b;                     // first count trigger at or after p
-        for (uint32_t q0 = p; q0 < b; q0 += 64) {
+        // no trigger before v = f + P (the count cannot exceed P earlier in the phase)
+        uint32_t qs = p;
+        if (P > 0) {
+            const uint64_t need = (uint64_t)f + P, vp = (uint64_t)m + (p - j0);
+            if (need > vp) qs = (uint32_t)min((uint64_t)b, (uint64_t)j0 + (need - m));
+        }
+        for (uint32_t q0 = qs; q0 < b; q0 += 64) {
             const uint32_t q = q0 + lane;
             bool pr = false;
             if (q < b) {
@@ -838,16 +844,28 @@ __global__ void k_sw_finish(const BatchState *bs, TableState *tst, const uint64_
 
 hipError_t launch_sliding_window(const uint64_t *S, const uint64_t *ts, const uint32_t *len, BatchState *bs,
                                  const Scratch &sc, Slot *table, TableState *tstate, const HistBufs &hb,
-                                 const Limits &lim, uint32_t n, hipStream_t st, const Marker &mark) {
+                                 const Limits &lim, uint32_t n, hipStream_t st, const Marker &mark,
+                                 hipStream_t st3, hipEvent_t fork_ev, hipEvent_t join_ev) {
     (void)hipGetLastError();   // a stale error of another caller is not ours
     const uint32_t gridSeg = std::min<uint32_t>(2048, std::max<uint32_t>(1, (n + 255) / 256));
     const uint32_t *cls = sc.sort_ctl + 1028;
+    // short and long segments are disjoint (marks, slots, log records): the wave walker
+    // runs on its own stream beside the thread walker when one is given
+    const bool fork = st3 && fork_ev && join_ev;
+    hipError_t e;
+    if (fork) {
+        if ((e = hipEventRecord(fork_ev, st)) != hipSuccess) return e;
+        if ((e = hipStreamWaitEvent(st3, fork_ev, 0)) != hipSuccess) return e;
+    }
+    k_walk_sw<true><<<1024, 256, 0, fork ? st3 : st>>>(S, bs, tstate, sc.seg_start, sc.seg_slot, ts, len,
+                                                       sc.pay[0], sc.seg_order, cls, sc.marks, table, lim, hb,
+                                                       sc.sw_seg);
+    if (fork && (e = hipEventRecord(join_ev, st3)) != hipSuccess) return e;
     k_walk_sw<false><<<gridSeg, 256, 0, st>>>(S, bs, tstate, sc.seg_start, sc.seg_slot, ts, len, sc.pay[0],
                                               sc.seg_order, cls, sc.marks, table, lim, hb, sc.sw_seg);
     mark("k_walk_sw_short");
-    k_walk_sw<true><<<1024, 256, 0, st>>>(S, bs, tstate, sc.seg_start, sc.seg_slot, ts, len, sc.pay[0],
-                                          sc.seg_order, cls, sc.marks, table, lim, hb, sc.sw_seg);
-    mark("k_walk_sw_long");
+    if (fork && (e = hipStreamWaitEvent(st, join_ev, 0)) != hipSuccess) return e;
+    mark("k_walk_sw_long_join");
     const uint64_t nslots = lim.table_mask + 1;
     const uint64_t ntiles = (nslots + kSlotTile - 1) / kSlotTile;
     const uint32_t grid = (uint32_t)std::min<uint64_t>(4096, ntiles);
