@@ -1480,14 +1480,21 @@ __global__ __launch_bounds__(256) void k_fill_scatter(const uint8_t *__restrict_
                                                       const uint8_t *__restrict__ carry,
                                                       uint32_t *__restrict__ drop_list,
                                                       uint32_t *__restrict__ drop_cur,
-                                                      TableState *tstate) {
+                                                      TableState *tstate, uint32_t nchunks) {
     __shared__ uint8_t s_v[kTile];
     __shared__ uint32_t s_w[4];
     __shared__ unsigned long long s_cnt[4][2];
+    __shared__ uint32_t s_cc[kMaxTileChunks];   // per arrival chunk: tile count, then base
+    __shared__ uint16_t s_rk[kTile];            // per DROP position: rank in its chunk
     if (bs->err) return;
     const uint32_t M = bs->n_valid;
     const uint32_t ntiles = (M + kTile - 1) / kTile;
     const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
+    // batches of <= kMaxTileChunks chunks: a tile reserves its DROPs' list slots with one
+    // cursor add per chunk it touches, all in parallel (otherwise one per chunk and wave)
+    const bool agg = nchunks <= kMaxTileChunks;
+    if (agg)
+        for (uint32_t c = threadIdx.x; c < nchunks; c += 256) s_cc[c] = 0;
     uint64_t n_pass = 0, n_drop = 0;
     for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
         const uint32_t p0 = t * kTile + threadIdx.x * 16u;
@@ -1518,6 +1525,44 @@ __global__ __launch_bounds__(256) void k_fill_scatter(const uint8_t *__restrict_
         __syncthreads();
         const uint32_t tile0 = t * kTile;
         const uint64_t lt = (1ull << lane) - 1ull;
+        if (agg) {
+            for (uint32_t j0 = 0; j0 < kTile; j0 += 256) {
+                const uint32_t j = j0 + threadIdx.x;
+                const bool ok = tile0 + j < M;
+                const uint8_t v = ok ? s_v[j] : 0;
+                n_pass += v == XDP_PASS;
+                n_drop += v == XDP_DROP;
+                const bool drop = v == XDP_DROP;
+                const uint32_t ch = drop ? pk_idx(S[tile0 + j]) >> kVChunkBits : 0u;
+                uint64_t pending = __ballot(drop);
+                while (pending) {   // rank among the tile's drops of the same chunk
+                    const int lead = __ffsll((unsigned long long)pending) - 1;
+                    const uint32_t lc = __shfl(ch, lead);
+                    const uint64_t same = __ballot(drop && ch == lc) & pending;
+                    uint32_t base = 0;
+                    if ((int)lane == lead) base = atomicAdd(&s_cc[lc], (uint32_t)__popcll(same));
+                    base = __shfl(base, lead);
+                    if ((same >> lane) & 1ull) s_rk[j] = (uint16_t)(base + (uint32_t)__popcll(same & lt));
+                    pending &= ~same;
+                }
+            }
+            __syncthreads();
+            for (uint32_t c = threadIdx.x; c < nchunks; c += 256) {
+                const uint32_t cnt = s_cc[c];
+                if (cnt) s_cc[c] = atomicAdd(&drop_cur[c], cnt);
+            }
+            __syncthreads();
+            for (uint32_t j = threadIdx.x; j < kTile && tile0 + j < M; j += 256) {
+                if (s_v[j] != XDP_DROP) continue;
+                const uint32_t idx = pk_idx(S[tile0 + j]);   // (an L2 hit: read above)
+                const uint32_t ch = idx >> kVChunkBits;
+                drop_list[(size_t)ch * kVChunk + s_cc[ch] + s_rk[j]] = idx;
+            }
+            __syncthreads();
+            for (uint32_t c = threadIdx.x; c < nchunks; c += 256) s_cc[c] = 0;
+            __syncthreads();
+            continue;
+        }
         for (uint32_t j0 = 0; j0 < kTile && tile0 + j0 < M; j0 += 256) {   // block-uniform trips
             const uint32_t j = j0 + threadIdx.x;
             const bool ok = tile0 + j < M;
@@ -1787,7 +1832,7 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
     k_fill_carry<<<1, 1024, 0, st>>>(sc.tile_last, bs);
     mark("k_fill_last");
     k_fill_scatter<<<gridTiles, 256, 0, st>>>(sc.marks, S, bs, sc.tile_last, sc.drop_list, sc.drop_cur,
-                                              tstate);
+                                              tstate, cdiv(n, kVChunk));
     mark("k_fill_scatter");
     k_verdict_apply<<<cdiv(n, kVChunk), 256, 0, st>>>(verdict, n, sc.drop_list, sc.drop_cur, bs);
     mark("k_verdict_apply");

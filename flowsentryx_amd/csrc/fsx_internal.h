@@ -27,6 +27,7 @@ constexpr int kSortMaxBlocks = 2048;
 constexpr int kTile = 4096;                            // fill / compaction tile
 constexpr uint32_t kVChunkBits = 14;
 constexpr uint32_t kVChunk = 1u << kVChunkBits;         // verdict bytes per k_verdict_apply block
+constexpr uint32_t kMaxTileChunks = 4096;               // k_fill_scatter's per-tile chunk counters
 
 enum : uint32_t {
     ERR_TABLE_FULL = 1u,
