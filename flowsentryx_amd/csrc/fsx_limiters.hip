@@ -98,8 +98,11 @@ __device__ __forceinline__ void tb_seg_body(const SV &sv, BatchState *bs, const 
             if (mono) j = gallop_gt(sv, a, b, till);
             else while (j < b && !(sv.t(j) > till)) ++j;
         }
-        sl.flags = j < b && (flags & SLOT_HAS_BL) && sl.till > 0 ? flags & ~SLOT_HAS_BL  // deleted at j
-                                                                  : flags;            // (:193-204)
+        // blacklist entry deleted at j (src/fsx_kern.c:193-204); a source with a counted
+        // packet gets its bucket state here (k_tb_tiles<1> then only stores, no read)
+        uint32_t nf = j < b && (flags & SLOT_HAS_BL) && sl.till > 0 ? flags & ~SLOT_HAS_BL : flags;
+        if (j < b) nf |= SLOT_HAS_TB;
+        sl.flags = nf;
         seg_j[g] = j;
         if (j >= b) continue;
         const uint64_t C = lim.tb_cap;
@@ -262,10 +265,9 @@ __device__ __forceinline__ void tb_tile(const SV &sv, uint32_t t, uint32_t M,
             out[k >> 2] |= (uint32_t)v << (8 * (k & 3));
             // last position of its source: the final {tokens, last} (counted packets only)
             if (kd != TB_BLOCKED && ((hf >> (k + 1)) & 1u)) {
-                Slot &sl = table[seg_slot[g]];
+                Slot &sl = table[seg_slot[g]];   // (SLOT_HAS_TB: set by k_tb_seg)
                 sl.aux = (uint64_t)x;
                 sl.tt = tp;
-                sl.flags |= SLOT_HAS_TB;
             }
         }
         if (p0 + 16 <= M) {
