@@ -294,7 +294,10 @@ __global__ __launch_bounds__(1024) void k_heavy_pick(PacketIn in, const uint32_t
 // Record mode (kRec = 16 / 32): every lane loads its own exchange record (coalesced, no
 // LDS staging), all of them IP packets; their len / ts go out to in.rec_len / rec_ts.
 template <uint32_t kRec>
-__global__ __launch_bounds__(256, 4) void k_parse(PacketIn in,
+#ifndef FSX_PARSE_MINB
+#define FSX_PARSE_MINB 4   // waves/SIMD bound of k_parse (A/B: scripts/build_variant.sh)
+#endif
+__global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
                                                const uint32_t *__restrict__ len,
                                                const uint64_t *__restrict__ ts, uint32_t n,
                                                uint64_t *__restrict__ packed,
@@ -1724,7 +1727,7 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
         for (int p = 0; p < 4; ++p) { dp.shift[p] = 32u + dbits * (uint32_t)p; dp.mask[p] = dmask; }
     }
     {
-        const uint32_t g = std::min<uint32_t>(1024, ntiles);
+        const uint32_t g = std::min<uint32_t>(256u * FSX_PARSE_MINB, ntiles);   // one resident block per slot
         const HeavySet *hs = heavy_sort ? sc.heavy : nullptr;
         uint32_t *th = onesweep ? nullptr : sc.hist;
         if (!in.rec)
