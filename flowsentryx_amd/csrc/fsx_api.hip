@@ -611,6 +611,43 @@ int fsx_map_delete(fsx_ctx *c, int map_id, const void *key) {
     return map_op(c, 2, map_id, key, nullptr, nullptr, 0);
 }
 
+int fsx_map_update_batch(fsx_ctx *c, int map_id, const void *keys, const void *values, size_t n,
+                         uint64_t flags) {
+    if (!c || (n && (!keys || !values))) return -EINVAL;
+    if (flags != FSX_BPF_ANY) return set_err(c, -EINVAL, "batched updates take BPF_ANY only");
+    if (map_id <= FSX_MAP_STATS || map_id >= FSX_MAP_COUNT)
+        return set_err(c, -EINVAL, "map id %d has no batched update", map_id);
+    if (n > kMaxBatchLimit) return set_err(c, -E2BIG, "n=%zu too large", n);
+    int rc = sel(c);
+    if (rc) return rc;
+    if ((rc = fsx_sync(c))) return rc;
+    if (n == 0) return 0;
+    const size_t klen = map_v6(map_id) ? 16 : 4, vlen = map_vlen(map_id);
+    uint32_t *dk = nullptr;
+    uint64_t *dv = nullptr;
+    HIPCHK(c, hipMalloc(&dk, n * klen));
+    if (hipMalloc(&dv, n * vlen) != hipSuccess) { hipFree(dk); return set_err(c, -ENOMEM, "map import"); }
+    hipError_t e = hipMemcpyAsync(dk, keys, n * klen, hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(dv, values, n * vlen, hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess && ++c->id_gen == 0x10000u) {   // 16-bit generations (as run_batch)
+        e = hipMemsetAsync(c->sc.id_tab, 0, c->slots * 32, c->stream);
+        c->id_gen = 1;
+    }
+    const uint32_t born = c->id_gen;
+    if (e == hipSuccess)
+        e = launch_map_import(c->table, c->tstate, c->bs, c->lim, table_index(c), born, map_id, dk, dv,
+                              (uint32_t)n, c->stream);
+    if (e == hipSuccess) {
+        c->pending = true;          // checked (and rolled back when the map is full) like a batch
+        c->pending_born = born;
+        rc = fsx_sync(c);
+    }
+    hipFree(dk);
+    hipFree(dv);
+    if (e != hipSuccess) return set_err(c, -EIO, "map import: %s", hipGetErrorString(e));
+    return rc;
+}
+
 int fsx_map_dump(fsx_ctx *c, int map_id, void *keys, void *values, size_t cap, size_t *n_out) {
     if (!c || !n_out) return -EINVAL;
     int rc = sel(c);

@@ -1889,6 +1889,50 @@ __global__ void k_map_op(Slot *table, TableState *tstate, Limits lim, TableIndex
     *res = 0;
 }
 
+// Batched update (BPF_MAP_UPDATE_BATCH with BPF_ANY; distinct keys): one thread per
+// entry finds or inserts its source in the index exactly as k_parse does (CAS claims,
+// slots stamped with generation `born` so a failing import rolls back like a batch),
+// then writes the value; new sources are counted in bs->n_new and checked against
+// max_entries by k_batch_check.
+__global__ __launch_bounds__(256) void k_map_import(Slot *table, Limits lim, TableIndex X, uint32_t born,
+                                                    int map_id, const uint32_t *__restrict__ keys,
+                                                    const uint64_t *__restrict__ vals, uint32_t n,
+                                                    BatchState *bs) {
+    const uint32_t tag = map_tag(map_id), bit = map_bit(map_id);
+    const uint32_t kw = tag == 2 ? 4u : 1u;
+    const uint32_t vw = bit == SLOT_HAS_ST ? 3u : bit == SLOT_HAS_TB ? 2u : 1u;
+    const IdTable idt{X.heads, X.k6, lim.table_mask, lim.seed, X.epoch, lim.test_flags, table, born, 0u};
+    uint32_t fresh_n = 0;
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) {
+        uint32_t k[4] = {0, 0, 0, 0};
+        for (uint32_t q = 0; q < kw; ++q) k[q] = keys[(size_t)i * kw + q];
+        const uint64_t h = probe_start(tag, k, lim.seed, lim.table_mask, lim.test_flags);
+        bool fresh = false;
+        const uint32_t s = id_resolve(idt, tag, k, h, X.heads[h], &fresh);
+        if (s == kNoSlot) { atomicOr(&bs->err, ERR_TABLE_FULL); continue; }
+        fresh_n += fresh;
+        Slot &sl = table[s];
+        const uint64_t *v = vals + (size_t)i * vw;
+        if (bit == SLOT_HAS_ST) { sl.pps = v[0]; sl.bps = v[1]; sl.tt = v[2]; }
+        else if (bit == SLOT_HAS_TB) { sl.aux = v[0]; sl.tt = v[1]; }
+        else sl.till = v[0];
+        atomicOr(&sl.flags, bit);
+    }
+    if (fresh_n) atomicAdd(&bs->n_new, fresh_n);
+}
+
+hipError_t launch_map_import(Slot *table, TableState *tstate, BatchState *bs, const Limits &lim,
+                             const TableIndex &X, uint32_t born, int map_id, const uint32_t *d_keys,
+                             const uint64_t *d_vals, uint32_t n, hipStream_t st) {
+    (void)hipGetLastError();   // a stale error of another caller is not ours
+    hipError_t e = hipMemsetAsync(bs, 0, sizeof(BatchState), st);
+    if (e != hipSuccess || n == 0) return e;
+    const uint32_t grid = std::min<uint32_t>(4096, (n + 255) / 256);
+    k_map_import<<<grid, 256, 0, st>>>(table, lim, X, born, map_id, d_keys, d_vals, n, bs);
+    k_batch_check<<<1, 1, 0, st>>>(bs, tstate, lim);
+    return hipGetLastError();
+}
+
 hipError_t launch_map_op(Slot *table, TableState *tstate, const Limits &lim, const TableIndex &X, int op,
                          int map_id, const uint32_t key[4], const uint64_t val[3], uint64_t flags,
                          int32_t *d_result, uint64_t *d_val, hipStream_t st) {

@@ -330,6 +330,12 @@ ScoreParams make_score_params(const int8_t w[8], float inv_in, int32_t zp_in, fl
 hipError_t launch_map_op(Slot *table, TableState *tstate, const Limits &lim, const TableIndex &X, int op,
                          int map_id, const uint32_t key[4], const uint64_t val[3], uint64_t flags,
                          int32_t *d_result, uint64_t *d_val, hipStream_t st);
+// Batched BPF_ANY update of distinct keys (key words: 1 per IPv4 / 4 per IPv6 key; value
+// words: 3 stats / 2 token state / 1 blacklist); new sources counted and checked like a
+// batch's (bs->err, rollback by generation `born`).
+hipError_t launch_map_import(Slot *table, TableState *tstate, BatchState *bs, const Limits &lim,
+                             const TableIndex &X, uint32_t born, int map_id, const uint32_t *d_keys,
+                             const uint64_t *d_vals, uint32_t n, hipStream_t st);
 // Re-publish the live slots under X.epoch; slots born in batch `born` (nonzero) are
 // emptied (rollback of a failed batch).
 hipError_t launch_index_rebuild(Slot *table, const Limits &lim, const TableIndex &X, uint32_t born,

@@ -117,6 +117,7 @@ def load_library() -> C.CDLL:
         "fsx_verdict_batch_device": (C.c_int, [vp, vp, vp, vp, sz, vp]),
         "fsx_process_batch_device": (C.c_int, [vp, vp, vp, vp, sz, vp, vp, vp, vp, vp, vp, sz]),
         "fsx_verdict_records_device": (C.c_int, [vp, vp, sz, C.c_uint32, vp]),
+        "fsx_map_update_batch": (C.c_int, [vp, C.c_int, vp, vp, sz, C.c_uint64]),
         "fsx_process_records_device": (C.c_int, [vp, vp, sz, C.c_uint32, vp, vp, vp, vp, vp, vp, sz]),
         "fsx_map_lookup": (C.c_int, [vp, C.c_int, vp, vp]),
         "fsx_map_update": (C.c_int, [vp, C.c_int, vp, vp, C.c_uint64]),
@@ -154,7 +155,8 @@ ABI_SYMBOLS = [
     "fsx_abi_version", "fsx_config_default", "fsx_open", "fsx_close", "fsx_last_error",
     "fsx_set_stream", "fsx_sync", "fsx_verdict_batch", "fsx_verdict_batch_device",
     "fsx_process_batch_device", "fsx_verdict_records_device", "fsx_process_records_device",
-    "fsx_map_lookup", "fsx_map_update", "fsx_map_delete", "fsx_map_dump", "fsx_get_stats",
+    "fsx_map_lookup", "fsx_map_update", "fsx_map_update_batch", "fsx_map_delete", "fsx_map_dump",
+    "fsx_get_stats",
     "fsx_reset", "fsx_load_q8_model", "fsx_score", "fsx_score_device", "fsx_flow_features",
     "fsx_last_timings", "fsx_enable_timing", "fsx_last_batch_info",
     "fsx_shard_owner", "fsx_shard_pack_device", "fsx_shard_unpack_device", "fsx_shard_unpack16_device",
@@ -323,6 +325,22 @@ class FsxContext:
         else:
             v = (C.c_uint64 * 1)(int(value))
         self._check(self._lib.fsx_map_update(self._h, map_id, k, v, flags), "map_update")
+
+    def map_update_batch(self, map_id: int, entries: dict):
+        """BPF_MAP_UPDATE_BATCH (BPF_ANY) of {key: value} in the map's layouts (the dict
+        map_dump returns): one device pass; all or nothing (-ENOSPC when full)."""
+        if map_id == MAP_STATS:
+            raise ValueError("stats_map has no batched update")
+        klen = 16 if map_id in _V6_MAPS else 4
+        vw = _value_words(map_id)
+        n = len(entries)
+        keys = np.zeros((max(n, 1), klen), dtype=np.uint8)
+        vals = np.zeros((max(n, 1), vw), dtype=np.uint64)
+        for i, (k, v) in enumerate(entries.items()):
+            keys[i] = np.frombuffer(_key_bytes(map_id, k), dtype=np.uint8)
+            vals[i] = v if vw > 1 else [int(v)]
+        self._check(self._lib.fsx_map_update_batch(self._h, map_id, _ptr(keys), _ptr(vals), n, BPF_ANY),
+                    "map_update_batch")
 
     def map_delete(self, map_id: int, key) -> bool:
         rc = self._lib.fsx_map_delete(self._h, map_id, _key_bytes(map_id, key))

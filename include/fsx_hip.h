@@ -182,6 +182,12 @@ int fsx_map_lookup(fsx_ctx *ctx, int map_id, const void *key, void *value);
 int fsx_map_update(fsx_ctx *ctx, int map_id, const void *key, const void *value,
                    uint64_t flags);
 int fsx_map_delete(fsx_ctx *ctx, int map_id, const void *key);
+/* BPF_MAP_UPDATE_BATCH analogue (flags = FSX_BPF_ANY): n entries of map 1..6, keys and
+ * values in the map's byte layouts, keys distinct. All or nothing: when the new sources
+ * would exceed max_entries the call fails with -ENOSPC and no map changes (restore of a
+ * map_dump after a restart, bulk rule-table loads). */
+int fsx_map_update_batch(fsx_ctx *ctx, int map_id, const void *keys, const void *values, size_t n,
+                         uint64_t flags);
 /* Copy up to cap entries (unordered) into keys/values; *n_out = entries present. */
 int fsx_map_dump(fsx_ctx *ctx, int map_id, void *keys, void *values, size_t cap,
                  size_t *n_out);

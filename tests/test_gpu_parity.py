@@ -476,3 +476,47 @@ def test_gather_path_large_frame_len(native, oracle):
             assert np.array_equal(vg, o.batch(hdr, ln, ts))
             assert_same_state(c, o)
     _check_flows(native, oracle, hdr, ln, ts)
+
+
+# ------------------------------------------------------------------ batched map updates
+@pytest.mark.parametrize("limiter,maps", [(0, (1, 2, 3, 4)), (1, (1, 2, 3, 4)), (2, (3, 4, 5, 6))])
+def test_map_update_batch_restores_state(native, oracle, limiter, maps):
+    """A restart: every map of one context dumped and batch-imported into a fresh one
+    (stats_map with map_update); the next batch then gives identical verdicts, maps and
+    stats on both (state carry through export/import, SURVEY §8 f row 1)."""
+    rng = np.random.default_rng(51 + limiter)
+    hdr, ln, ts = rand_stream(rng, 40000, 400, dt_max=300, v6_frac=0.3)
+    cfg = dict(CFGS["tight"], limiter=limiter, max_entries=1 << 14)
+    if limiter == 2:
+        cfg = dict(limiter=2, tb_rate=300_000, tb_burst=4, max_entries=1 << 14)
+    with gpu_ctx(native, **cfg) as a, gpu_ctx(native, **cfg) as b:
+        a.verdict_batch(hdr[:20000], ln[:20000], ts[:20000])
+        for m in maps:
+            b.map_update_batch(m, a.map_dump(m))
+        b.map_update(0, 0, a.stats())
+        for m in maps:
+            assert b.map_dump(m) == a.map_dump(m), m
+        if limiter != 1:   # (the sliding window's carried logs are not map state)
+            va = a.verdict_batch(hdr[20000:], ln[20000:], ts[20000:])
+            vb = b.verdict_batch(hdr[20000:], ln[20000:], ts[20000:])
+            assert np.array_equal(va, vb)
+            assert a.stats() == b.stats()
+            for m in maps:
+                assert b.map_dump(m) == a.map_dump(m), m
+
+
+def test_map_update_batch_all_or_nothing(native):
+    from flowsentryx_amd import lib
+    with gpu_ctx(native, max_entries=100, max_batch=1024) as c:
+        c.map_update(3, bytes([1, 2, 3, 4]), 77)
+        rules = {bytes([10, 0, i // 256, i % 256]): 2**64 - 1 for i in range(150)}
+        with pytest.raises(lib.FsxError) as e:
+            c.map_update_batch(3, rules)
+        assert e.value.code == -errno.ENOSPC
+        assert c.map_dump(3) == {bytes([1, 2, 3, 4]): 77}
+        few = dict(list(rules.items())[:60])
+        c.map_update_batch(3, few)
+        assert c.map_dump(3) == {**few, bytes([1, 2, 3, 4]): 77}
+        v6 = {bytes(range(i, i + 16)): (5, 6 + i, 7) for i in range(30)}
+        c.map_update_batch(2, v6)
+        assert c.map_dump(2) == v6
