@@ -73,6 +73,8 @@ def parse_args():
                     help="N>1 collectives: nccl (RCCL over xGMI) or gloo (rehearsal on one GPU)")
     ap.add_argument("--limiter", choices=["fixed", "sliding", "token"], default="fixed",
                     help="limiter of the timed main loop (diagnostics; the headline is fixed)")
+    ap.add_argument("--rule-steps", type=int, default=5,
+                    help="steps of the prefix-blocklist leg (64K rules; 0 skips it)")
     ap.add_argument("--limiter-steps", type=int, default=5,
                     help="timed steps of the sliding-window and token-bucket legs (0: skip)")
     return ap.parse_args()
@@ -241,6 +243,42 @@ def main():
                                    "unit": "Mpps", "ms_per_step": round(lt / args.limiter_steps * 1e3, 4),
                                    "steps": args.limiter_steps, "allowed": la, "dropped": ld}
 
+    # prefix blocklists (SURVEY §8 f row 4): the same batch with a 64K-rule
+    # table — 61440 random /24 prefixes (mostly missing the stream) and 4096 rules on the
+    # stream's own sources (/32 and /28, permanent) — fixed window, verdicts + maps
+    rules_leg = None
+    if args.rule_steps > 0 and world == 1:
+        import numpy as np
+        rng = np.random.default_rng(5)
+        seen = d_hdr[: min(n, 1 << 16) * 64].view(-1, 64)[:, 26:30].cpu().numpy()
+        srcs = np.unique(seen.view(np.uint32).reshape(-1))[:4096]
+        r4 = {}
+        for a in rng.integers(0, 2**32, 61440, dtype=np.uint64).astype(np.uint32):
+            r4[lib.prefix_key((int(a) & 0xFFFFFF).to_bytes(4, "little"), 24)] = 2**64 - 1
+        for i, a in enumerate(srcs):
+            r4[lib.prefix_key(int(a).to_bytes(4, "little"), 32 if i & 1 else 28)] = 2**64 - 1
+        with lib.FsxContext(max_batch=n, max_entries=max_entries, device=local) as rc_:
+            rc_.map_update_batch(lib.MAP_IPV4_PREFIX, r4)
+            def rstep():
+                rc_.reset()
+                rc_.verdict_batch_device(d_hdr.data_ptr(), d_len.data_ptr(), d_ts.data_ptr(), n,
+                                         d_v.data_ptr())
+            rstep()
+            rc_.sync()
+            torch.cuda.synchronize()
+            r0 = time.perf_counter()
+            for _ in range(args.rule_steps):
+                rstep()
+            rc_.sync()
+            torch.cuda.synchronize()
+            rt = time.perf_counter() - r0
+            ri = rc_.last_batch_info()
+            ra, rd = rc_.stats()
+        rules_leg = {"value": round(n * args.rule_steps / rt / 1e6, 2), "unit": "Mpps",
+                     "ms_per_step": round(rt / args.rule_steps * 1e3, 4), "steps": args.rule_steps,
+                     "rules": len(r4), "prefix_lengths": [24, 28, 32],
+                     "rule_drops": ri["prefix_rule_drops"], "allowed": ra, "dropped": rd}
+
     check = None
     if args.check and rank == 0:
         from oracle import pyoracle
@@ -324,7 +362,7 @@ def main():
                    "parallelism": f"dp{world}" + ("" if world == 1 else
                                                   " (sources hash-sharded, all-to-all)")},
         "roofline": roofline, "pipeline": pipeline, "cpu_baseline": cpu,
-        "limiters": limiters or None, "exchange": exchange,
+        "limiters": limiters or None, "prefix_rules": rules_leg, "exchange": exchange,
         "kernels": [{"name": a, "ms_per_step": round(b, 4), "launches": c} for a, b, c in timings],
         "stats": {"allowed": stats[0], "dropped": stats[1], "sources": info["sources"],
                   "light_packets": info["light_packets"], "malicious_sources": malicious},

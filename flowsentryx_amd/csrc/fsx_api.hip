@@ -7,13 +7,16 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <cerrno>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <new>
+#include <vector>
 
 #include "../../include/fsx_hip.h"
 #include "fsx_internal.h"
@@ -73,6 +76,17 @@ struct fsx_ctx {
     // per-source flow accumulators
     void *d_flow_acc = nullptr;
     uint64_t flow_acc_cap = 0;
+    // prefix blocklists (FSX_MAP_IPV4_PREFIX / _IPV6_PREFIX): the host copy is the map;
+    // the device probe table is rebuilt from it before the next batch after a change
+    std::map<std::array<uint32_t, 5>, uint64_t> rules;   // {family << 8 | len, addr words}
+    uint32_t rule_cnt[2]{};
+    uint32_t rule_len_cnt[2][129]{};
+    bool rules_dirty = false;
+    RuleSlot *d_rule_slot = nullptr;
+    uint8_t *d_rule_lens = nullptr;
+    uint32_t *d_rule_filter = nullptr;
+    uint64_t rule_cap = 0;
+    RuleSet rs{};
     // small device scratch for map ops
     int32_t *d_res = nullptr;
     uint64_t *d_val = nullptr;
@@ -223,6 +237,7 @@ void fsx_close(fsx_ctx *c) {
     hipFree(c->d_shard_cnt); hipFree(c->d_rep); hipFree(c->d_shard_own); hipFree(c->d_shard_crec);
     hipFree(c->d_rec_len); hipFree(c->d_rec_ts);
     hipFree(c->idx_heads); hipFree(c->idx_k6);
+    hipFree(c->d_rule_slot); hipFree(c->d_rule_lens); hipFree(c->d_rule_filter);
     for (int r = 0; r < kRing; ++r)
         for (int i = 0; i < kMaxEv; ++i) if (c->ev[r][i]) hipEventDestroy(c->ev[r][i]);
     if (c->own_stream) hipStreamDestroy(c->own_stream);
@@ -401,6 +416,124 @@ static bool fork_flows() {
     return !serial;
 }
 
+// ------------------------------------------------------------------ prefix rules
+// The device tables of the prefix blocklists (RuleSet, fsx_internal.h): the probe table
+// (four times as many slots as rules, linear probing by rule_hash), the distinct lengths
+// per family longest first, and the per-family /24 filter bits. Rebuilt whole from the
+// host map (rules change rarely; 64K rules: 8 MiB of slots + 4 MiB of filter). Called
+// with the stream idle.
+static int upload_rules(fsx_ctx *c) {
+    c->rules_dirty = false;
+    if (c->rules.empty()) { c->rs = RuleSet{}; return 0; }
+    const uint64_t cap = next_pow2(std::max<uint64_t>(64, 4 * c->rules.size()));
+    constexpr size_t kFw = size_t(1) << (kRuleFilterBits - 5);   // filter words per family
+    std::vector<uint32_t> filt(2 * kFw, 0u);
+    std::vector<RuleSlot> tab(cap);
+    memset(tab.data(), 0, cap * sizeof(RuleSlot));
+    for (const auto &r : c->rules) {
+        const uint32_t a[4] = {r.first[1], r.first[2], r.first[3], r.first[4]};
+        uint64_t h = rule_hash(r.first[0], a) & (cap - 1);
+        while (tab[h].tag) h = (h + 1) & (cap - 1);
+        tab[h].tag = r.first[0];
+        tab[h].fp = rule_fp(a);
+        tab[h].till = r.second;
+        memcpy(tab[h].a, a, 16);
+        // the /24s the rule touches: [p, p + 2^(24 - len)) of the first 24 address bits
+        const uint32_t L = r.first[0] & 0xFFu, f = (r.first[0] >> 8) - 1u;
+        const uint32_t p = (a[0] & 0xFFu) << 16 | (a[0] & 0xFF00u) | ((a[0] >> 16) & 0xFFu);
+        const uint32_t span = L >= kRuleFilterBits ? 1u : 1u << (kRuleFilterBits - L);
+        uint32_t *fw = filt.data() + f * kFw;
+        for (uint32_t q = p; q < p + span;) {
+            if ((q & 31u) == 0 && q + 32 <= p + span) { fw[q >> 5] = ~0u; q += 32; continue; }
+            fw[q >> 5] |= 1u << (q & 31u);
+            ++q;
+        }
+    }
+    uint8_t lens[256] = {};
+    uint32_t nl[2] = {0, 0};
+    for (int f = 0; f < 2; ++f)
+        for (int L = f ? 128 : 32; L >= 0; --L)
+            if (c->rule_len_cnt[f][L]) lens[(f ? kRuleLens6 : 0) + nl[f]++] = (uint8_t)L;
+    if (cap > c->rule_cap) {
+        hipFree(c->d_rule_slot);
+        c->d_rule_slot = nullptr;
+        c->rule_cap = 0;
+        HIPCHK(c, hipMalloc(&c->d_rule_slot, cap * sizeof(RuleSlot)));
+        c->rule_cap = cap;
+    }
+    if (!c->d_rule_lens) HIPCHK(c, hipMalloc(&c->d_rule_lens, sizeof(lens)));
+    if (!c->d_rule_filter) HIPCHK(c, hipMalloc(&c->d_rule_filter, filt.size() * 4));
+    HIPCHK(c, hipMemcpy(c->d_rule_filter, filt.data(), filt.size() * 4, hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy(c->d_rule_slot, tab.data(), cap * sizeof(RuleSlot), hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy(c->d_rule_lens, lens, sizeof(lens), hipMemcpyHostToDevice));
+    c->rs = RuleSet{c->d_rule_slot, c->d_rule_lens, c->d_rule_filter, (uint32_t)(cap - 1), nl[0], nl[1]};
+    return 0;
+}
+
+static bool prefix_map(int map_id) { return map_id == FSX_MAP_IPV4_PREFIX || map_id == FSX_MAP_IPV6_PREFIX; }
+static size_t prefix_klen(int map_id) { return map_id == FSX_MAP_IPV6_PREFIX ? 20 : 8; }
+
+// Canonical rule key of a bpf_lpm_trie_key-style map key; -EINVAL on a too-long prefix.
+static int prefix_rule_key(int map_id, const void *key, std::array<uint32_t, 5> &rk) {
+    const bool v6 = map_id == FSX_MAP_IPV6_PREFIX;
+    uint32_t plen, k[4] = {0, 0, 0, 0};
+    memcpy(&plen, key, 4);
+    if (plen > (v6 ? 128u : 32u)) return -EINVAL;
+    memcpy(k, static_cast<const uint8_t *>(key) + 4, v6 ? 16 : 4);
+    uint32_t a[4];
+    rule_mask(k, plen, a);
+    rk = {(v6 ? 2u : 1u) << 8 | plen, a[0], a[1], a[2], a[3]};
+    return 0;
+}
+
+static void rule_count(fsx_ctx *c, const std::array<uint32_t, 5> &rk, int d) {
+    const int f = (int)(rk[0] >> 8) - 1;
+    c->rule_cnt[f] += (uint32_t)d;
+    c->rule_len_cnt[f][rk[0] & 0xFFu] += (uint32_t)d;
+}
+
+// op 0 lookup (longest match of the key's first prefixlen bits), 1 update, 2 delete
+static int prefix_op(fsx_ctx *c, int op, int map_id, const void *key, const void *value, void *out,
+                     uint64_t flags) {
+    std::array<uint32_t, 5> rk;
+    int rc = prefix_rule_key(map_id, key, rk);
+    if (rc) return rc;
+    const int f = map_id == FSX_MAP_IPV6_PREFIX ? 1 : 0;
+    if (op == 0) {
+        uint32_t k[4] = {rk[1], rk[2], rk[3], rk[4]};
+        for (int L = (int)(rk[0] & 0xFFu); L >= 0; --L) {
+            if (!c->rule_len_cnt[f][L]) continue;
+            uint32_t a[4];
+            rule_mask(k, (uint32_t)L, a);
+            auto it = c->rules.find({(uint32_t)(f + 1) << 8 | (uint32_t)L, a[0], a[1], a[2], a[3]});
+            if (it != c->rules.end()) { memcpy(out, &it->second, 8); return 0; }
+        }
+        return -ENOENT;
+    }
+    auto it = c->rules.find(rk);
+    if (op == 2) {
+        if (it == c->rules.end()) return -ENOENT;
+        c->rules.erase(it);
+        rule_count(c, rk, -1);
+        c->rules_dirty = true;
+        return 0;
+    }
+    if (flags > FSX_BPF_EXIST) return -EINVAL;
+    if (flags == FSX_BPF_NOEXIST && it != c->rules.end()) return -EEXIST;
+    if (flags == FSX_BPF_EXIST && it == c->rules.end()) return -ENOENT;
+    uint64_t till;
+    memcpy(&till, value, 8);
+    if (it != c->rules.end()) {
+        it->second = till;
+    } else {
+        if (c->rule_cnt[f] >= FSX_PREFIX_MAX_ENTRIES) return -ENOSPC;
+        c->rules.emplace(rk, till);
+        rule_count(c, rk, +1);
+    }
+    c->rules_dirty = true;
+    return 0;
+}
+
 // Enqueue one batch: verdicts + maps when d_verdict is set, per-source flows when fr is.
 static int run_batch(fsx_ctx *c, const PacketIn &in, const uint32_t *d_len, const uint64_t *d_ts,
                      size_t n, uint8_t *d_verdict, bool do_limit, const FlowRequest *fr) {
@@ -408,6 +541,7 @@ static int run_batch(fsx_ctx *c, const PacketIn &in, const uint32_t *d_len, cons
     int rc = sel(c);
     if (rc) return rc;
     if (c->pending) { rc = fsx_sync(c); if (rc) return rc; }
+    if (do_limit && c->rules_dirty && (rc = upload_rules(c))) return rc;
     FlowRequest frq;
     if (fr) {
         frq = *fr;
@@ -436,7 +570,7 @@ static int run_batch(fsx_ctx *c, const PacketIn &in, const uint32_t *d_len, cons
     }
     hipError_t e = launch_verdict_pipeline(in, d_len, d_ts, (uint32_t)n, d_verdict, c->table,
                                            c->tstate, c->bs, c->sc, c->id_gen, table_index(c), c->lim,
-                                           do_limit, fr,
+                                           c->rs, do_limit, fr,
                                            c->hist, c->stream, fork_flows() ? c->aux_stream : nullptr,
                                            c->fork_ev, c->join_ev, fork_flows() ? c->walk_stream : nullptr,
                                            c->walk_fork_ev, c->walk_join_ev, tm);
@@ -560,7 +694,7 @@ static size_t map_vlen(int map_id) {
 
 static int key_words(int map_id, const void *key, uint32_t k[4]) {
     k[0] = k[1] = k[2] = k[3] = 0;
-    if (map_id < FSX_MAP_IPV4_STATS || map_id >= FSX_MAP_COUNT) return -EINVAL;
+    if (map_id < FSX_MAP_IPV4_STATS || map_id > FSX_MAP_IPV6_TOKENS) return -EINVAL;
     memcpy(k, key, map_v6(map_id) ? 16 : 4);
     return 0;
 }
@@ -581,6 +715,7 @@ static int map_op(fsx_ctx *c, int op, int map_id, const void *key, const void *v
         HIPCHK(c, hipMemcpy(c->tstate->stats, value, 16, hipMemcpyHostToDevice));
         return 0;
     }
+    if (prefix_map(map_id)) return prefix_op(c, op, map_id, key, value, out, flags);
     uint32_t k[4];
     if ((rc = key_words(map_id, key, k))) return set_err(c, rc, "bad map id %d", map_id);
     if (flags > FSX_BPF_EXIST) return -EINVAL;
@@ -622,6 +757,27 @@ int fsx_map_update_batch(fsx_ctx *c, int map_id, const void *keys, const void *v
     if (rc) return rc;
     if ((rc = fsx_sync(c))) return rc;
     if (n == 0) return 0;
+    if (prefix_map(map_id)) {   // host map: validated and sized first, all or nothing
+        const size_t klen = prefix_klen(map_id);
+        const int f = map_id == FSX_MAP_IPV6_PREFIX ? 1 : 0;
+        std::vector<std::array<uint32_t, 5>> rks(n);
+        std::map<std::array<uint32_t, 5>, int> fresh;
+        for (size_t i = 0; i < n; ++i) {
+            if ((rc = prefix_rule_key(map_id, static_cast<const uint8_t *>(keys) + i * klen, rks[i])))
+                return set_err(c, rc, "prefix key %zu: prefixlen too long", i);
+            if (!c->rules.count(rks[i])) fresh[rks[i]] = 1;
+        }
+        if (c->rule_cnt[f] + fresh.size() > FSX_PREFIX_MAX_ENTRIES)
+            return set_err(c, -ENOSPC, "prefix map full");
+        for (size_t i = 0; i < n; ++i) {
+            uint64_t till;
+            memcpy(&till, static_cast<const uint8_t *>(values) + i * 8, 8);
+            auto ins = c->rules.insert_or_assign(rks[i], till);
+            if (ins.second) rule_count(c, rks[i], +1);
+        }
+        c->rules_dirty = true;
+        return 0;
+    }
     const size_t klen = map_v6(map_id) ? 16 : 4, vlen = map_vlen(map_id);
     uint32_t *dk = nullptr;
     uint64_t *dv = nullptr;
@@ -660,6 +816,26 @@ int fsx_map_dump(fsx_ctx *c, int map_id, void *keys, void *values, size_t cap, s
             if (values) HIPCHK(c, hipMemcpy(values, c->tstate->stats, 16, hipMemcpyDeviceToHost));
         }
         *n_out = 1;
+        return 0;
+    }
+    if (prefix_map(map_id)) {
+        const size_t klen = prefix_klen(map_id);
+        const uint32_t fam = map_id == FSX_MAP_IPV6_PREFIX ? 2u : 1u;
+        size_t m = 0;
+        for (const auto &r : c->rules) {
+            if ((r.first[0] >> 8) != fam) continue;
+            if (m < cap) {
+                if (keys) {
+                    uint8_t *kp = static_cast<uint8_t *>(keys) + m * klen;
+                    const uint32_t plen = r.first[0] & 0xFFu;
+                    memcpy(kp, &plen, 4);
+                    memcpy(kp + 4, &r.first[1], klen - 4);
+                }
+                if (values) memcpy(static_cast<uint8_t *>(values) + m * 8, &r.second, 8);
+            }
+            ++m;
+        }
+        *n_out = m;
         return 0;
     }
     if (map_id < FSX_MAP_IPV4_STATS || map_id >= FSX_MAP_COUNT) return -EINVAL;
@@ -701,7 +877,7 @@ int fsx_reset(fsx_ctx *c) {
     c->pending_born = 0;   // the whole table is wiped: no rollback of a pending batch
     HIPCHK(c, hipMemsetAsync(c->table, 0, c->slots * sizeof(Slot), c->stream));
     HIPCHK(c, hipMemsetAsync(c->tstate, 0, sizeof(TableState), c->stream));
-    return next_epoch(c);   // every index head reads empty
+    return next_epoch(c);   // (the prefix blocklists stay: configuration)   // every index head reads empty
 }
 
 // ------------------------------------------------------------------ scoring
@@ -806,7 +982,7 @@ int fsx_last_batch_info(fsx_ctx *c, uint64_t *info, int cap) {
     BatchState h;
     HIPCHK(c, hipMemcpy(&h, c->bs, sizeof(h), hipMemcpyDeviceToHost));
     const uint64_t v[12] = {h.n_valid, h.nseg, h.n_new, h.any_v6, h.nonmono, h.max_len,
-                            h.max_ts, h.allowed, h.dropped, h.n_fix, h.pay_ok, h.n_light};
+                            h.max_ts, h.allowed, h.dropped, h.n_rule, h.pay_ok, h.n_light};
     int k = 0;
     for (; k < cap && k < 12; ++k) info[k] = v[k];
     return k;

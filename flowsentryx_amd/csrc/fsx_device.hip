@@ -288,12 +288,66 @@ __global__ __launch_bounds__(1024) void k_heavy_pick(PacketIn in, const uint32_t
     hs->map[tid] = s_map[tid];
 }
 
+// Prefix blocklist: a packet whose /24 filter bit is clear matches no
+// rule (one load); otherwise the family's distinct rule lengths are probed longest first
+// (the first slots of four lengths at a time loaded together); the first rule found is
+// the longest match and drops the packet when 0 < now <= till (till 0 or expired: the
+// packet goes on, an exception inside a shorter blocked prefix).
+__device__ __forceinline__ bool rule_drop(const RuleSet &R, uint32_t tag, const uint32_t k[4], uint64_t now) {
+    const uint32_t p24 = (k[0] & 0xFFu) << 16 | (k[0] & 0xFF00u) | ((k[0] >> 16) & 0xFFu);
+    const uint32_t fw = R.filter[(tag - 1u) << (kRuleFilterBits - 5) | p24 >> 5];
+    if (!((fw >> (p24 & 31u)) & 1u)) return false;
+    const uint32_t nl = tag == 1 ? R.nlen4 : R.nlen6;
+    const uint8_t *lens = R.lens + (tag == 1 ? 0u : kRuleLens6);
+    const uint4 *slot = reinterpret_cast<const uint4 *>(R.slot);   // 2 uint4 per slot
+    // first probe slot of length index q (q >= nl: an empty dummy)
+    auto first = [&](uint32_t q, uint32_t &sq) -> uint4 {
+        sq = 0;
+        if (q >= nl) return make_uint4(0, 0, 0, 0);
+        const uint32_t L = lens[q];
+        uint32_t a[4];
+        rule_mask(k, L, a);
+        sq = rule_hash(tag << 8 | L, a) & R.mask;
+        return slot[2 * sq];
+    };
+    // the chain of length index q from its loaded first slot (a load factor <= 1/4 keeps
+    // it short): -1 no rule of this length, else the rule's verdict (1 drop). An IPv4
+    // fingerprint is the address itself; an IPv6 one is confirmed on the words.
+    auto walk = [&](uint32_t q, uint4 e, uint32_t sq) -> int {
+        if (q >= nl) return -1;
+        const uint32_t L = lens[q], rt = tag << 8 | L;
+        uint32_t a[4];
+        rule_mask(k, L, a);
+        const uint32_t fp = rule_fp(a);
+        for (; e.x != 0; sq = (sq + 1) & R.mask, e = slot[2 * sq]) {
+            if (e.x != rt || e.y != fp) continue;
+            if (tag == 2) {
+                const uint4 w = slot[2 * sq + 1];
+                if (w.x != a[0] || w.y != a[1] || w.z != a[2] || w.w != a[3]) continue;
+            }
+            const uint64_t till = (uint64_t)e.z | ((uint64_t)e.w << 32);
+            return till > 0 && now <= till ? 1 : 0;
+        }
+        return -1;
+    };
+    for (uint32_t q = 0; q < nl; q += 4) {   // four lengths' first slots loaded together
+        uint32_t s0, s1, s2, s3;
+        const uint4 e0 = first(q, s0), e1 = first(q + 1, s1), e2 = first(q + 2, s2), e3 = first(q + 3, s3);
+        int r;
+        if ((r = walk(q, e0, s0)) >= 0) return r == 1;
+        if ((r = walk(q + 1, e1, s1)) >= 0) return r == 1;
+        if ((r = walk(q + 2, e2, s2)) >= 0) return r == 1;
+        if ((r = walk(q + 3, e3, s3)) >= 0) return r == 1;
+    }
+    return false;
+}
+
 // One wave handles 64 consecutive records per step: the 4 KiB tile is loaded with
 // four fully coalesced 1 KiB wave loads and staged through LDS (17-dword record
 // pitch: conflict-free 32-bit reads), then each lane parses its own record.
 // Record mode (kRec = 16 / 32): every lane loads its own exchange record (coalesced, no
 // LDS staging), all of them IP packets; their len / ts go out to in.rec_len / rec_ts.
-template <uint32_t kRec>
+template <uint32_t kRec, bool kRules>
 #ifndef FSX_PARSE_MINB
 #define FSX_PARSE_MINB 4   // waves/SIMD bound of k_parse (A/B: scripts/build_variant.sh)
 #endif
@@ -304,7 +358,8 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
                                                uint8_t *__restrict__ verdict, BatchState *bs,
                                                IdTable idt, uint32_t *__restrict__ ghist,
                                                uint32_t *__restrict__ thist, uint32_t tcap,
-                                               DigitPlan dp, const HeavySet *__restrict__ heavy) {
+                                               DigitPlan dp, const HeavySet *__restrict__ heavy,
+                                               RuleSet rules) {
     __shared__ uint32_t s_rec[4][64 * 17];
     __shared__ uint32_t s_red[4][3];
     __shared__ unsigned long long s_ts[4], s_its[4];
@@ -328,7 +383,7 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
     }
     __syncthreads();
     uint32_t *rec = s_rec[w];
-    uint32_t any6 = 0, nonmono = 0, maxlen = 0, nfresh = 0;
+    uint32_t any6 = 0, nonmono = 0, maxlen = 0, nfresh = 0, nrule = 0;
     uint64_t maxts = 0, inv_mints = 0;  // ~min ts, max-reduced
     // a block owns whole 4096-record sort tiles (so it can emit pass 0's per-tile digit
     // counts: no k_tile_hist for pass 0); wave w parses records [w*1024, +1024) of the
@@ -431,6 +486,13 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
             in.rec_len[i] = L;
             in.rec_ts[i] = T;
         }
+        if constexpr (kRules) {   // prefix blocklist: the longest matching rule decides
+            if (tag && rule_drop(rules, tag, k, T)) {
+                tag = 0;              // never reaches the per-source path
+                v = XDP_DROP;
+                ++nrule;
+            }
+        }
         uint64_t prev = __shfl_up(T, 1);
         if (lane == 0) prev = (live && i > 0) ? Pc : T;
         const bool ip = tag != 0;
@@ -510,6 +572,10 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
     }
     // one add per wave: a per-step add to one counter serializes at the memory side
     if (lane == 0 && nfresh && idt.slots) atomicAdd(&bs->n_new, nfresh);
+    if constexpr (kRules) {
+        nrule = wave_incl_sum(nrule);
+        if (lane == 63 && nrule) atomicAdd(&bs->n_rule, nrule);
+    }
     any6 = __ballot(any6 != 0) ? 1u : 0u;
     nonmono = __ballot(nonmono != 0) ? 1u : 0u;
     maxlen = wave_max(maxlen);
@@ -1043,6 +1109,10 @@ __global__ void k_batch_check(BatchState *bs, TableState *tstate, Limits lim) {
         return;
     }
     tstate->count += bs->n_new;
+    if (bs->n_rule) {   // prefix-rule drops count in stats_map like blacklist drops
+        tstate->stats[1] += bs->n_rule;
+        bs->dropped += bs->n_rule;
+    }
 }
 
 // Rollback / epoch change: re-publish every live slot under the new epoch; slots born in
@@ -1657,8 +1727,8 @@ static uint32_t next_generation() {
 hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, const uint64_t *ts,
                                    uint32_t n, uint8_t *verdict, Slot *table, TableState *tstate,
                                    BatchState *bs, const Scratch &sc_in, uint32_t id_gen,
-                                   const TableIndex &X, const Limits &lim, bool do_limit,
-                                   const FlowRequest *flows,
+                                   const TableIndex &X, const Limits &lim, const RuleSet &rules,
+                                   bool do_limit, const FlowRequest *flows,
                                    const HistBufs &hist, hipStream_t st, hipStream_t st2,
                                    hipEvent_t fork_ev, hipEvent_t join_ev, hipStream_t st3,
                                    hipEvent_t walk_fork_ev, hipEvent_t walk_join_ev, PipeTiming *tm) {
@@ -1730,12 +1800,18 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
         const uint32_t g = std::min<uint32_t>(256u * FSX_PARSE_MINB, ntiles);   // one resident block per slot
         const HeavySet *hs = heavy_sort ? sc.heavy : nullptr;
         uint32_t *th = onesweep ? nullptr : sc.hist;
+        // the prefix rules apply to limiter batches (an instantiation of its own, so the
+        // rule-free parse keeps its registers)
+        const bool rl = do_limit && rules.slot;
+#define FSX_PARSE(R, Q) k_parse<R, Q><<<g, 256, 0, st>>>(in, len, ts, n, sc.packed[0], verdict, bs, idt, \
+                                                        sc.sort_ctl, th, tcap, dp, hs, rules)
         if (!in.rec)
-            k_parse<0><<<g, 256, 0, st>>>(in, len, ts, n, sc.packed[0], verdict, bs, idt, sc.sort_ctl, th, tcap, dp, hs);
+            rl ? FSX_PARSE(0, true) : FSX_PARSE(0, false);
         else if (in.rec_bytes == 16)
-            k_parse<16><<<g, 256, 0, st>>>(in, len, ts, n, sc.packed[0], verdict, bs, idt, sc.sort_ctl, th, tcap, dp, hs);
+            rl ? FSX_PARSE(16, true) : FSX_PARSE(16, false);
         else
-            k_parse<32><<<g, 256, 0, st>>>(in, len, ts, n, sc.packed[0], verdict, bs, idt, sc.sort_ctl, th, tcap, dp, hs);
+            rl ? FSX_PARSE(32, true) : FSX_PARSE(32, false);
+#undef FSX_PARSE
     }
     mark("k_parse");
     k_hist_prep<<<1, 256, 0, st>>>(sc.sort_ctl, sc.gbase, bs, heavy_sort ? dp.light_b : 256u);

@@ -76,7 +76,7 @@ struct BatchState {
     uint32_t n_new;
     uint32_t err;
     uint32_t max_len;
-    uint32_t n_fix;       // unused (0): source ids are exact, no collision fixups
+    uint32_t n_rule;      // IP packets dropped by a prefix rule (not in n_valid)
     uint32_t n_long;      // segments longer than the short-segment bound (wave walker)
     uint32_t n_span;      // sources crossing flow tiles (k_flow_combine)
     uint64_t max_ts;
@@ -171,6 +171,50 @@ __host__ __device__ inline uint64_t slot_hash(uint32_t tag, const uint32_t k[4],
     uint64_t h = mix64(seed ^ ((uint64_t)tag << 56) ^ ((uint64_t)k[0] | ((uint64_t)k[1] << 32)));
     if (tag == 2) h = mix64(h ^ ((uint64_t)k[2] | ((uint64_t)k[3] << 32)));
     return h;
+}
+
+// ------------------------------------------------------------ prefix rules
+// Prefix blocklist (FSX_MAP_IPV4_PREFIX / _IPV6_PREFIX): one open-addressing
+// table of both families' rules keyed by (family, prefix length, masked address), built by
+// the host when the rules change; the lookup probes the family's distinct lengths longest
+// first, so the first hit is the longest match.
+struct RuleSlot {
+    uint32_t tag;        // family << 8 | prefix length (family 1 / 2: never 0); 0 = empty
+    uint32_t fp;         // rule_fp(a): the IPv4 address itself, an IPv6 fingerprint
+    uint64_t till;       // blocked while 0 < now <= till
+    uint32_t a[4];       // the address words (key byte order), bits past the length zero
+};
+static_assert(sizeof(RuleSlot) == 32, "one 32-byte probe per slot");
+constexpr uint32_t kRuleLens6 = 64;  // RuleSet::lens: [0, 33) IPv4, [64, 193) IPv6
+constexpr uint32_t kRuleFilterBits = 24;   // filter: one bit per /24 (per family)
+struct RuleSet {
+    const RuleSlot *slot = nullptr;   // nullptr: no rules
+    const uint8_t *lens = nullptr;    // distinct prefix lengths per family, descending
+    // per family 2^24 bits: bit p set when some rule covers part of the /24 p (the
+    // first 24 address bits), so most packets are cleared by one load (2 MiB per family)
+    const uint32_t *filter = nullptr;
+    uint32_t mask = 0;                // slots - 1
+    uint32_t nlen4 = 0, nlen6 = 0;
+};
+// The first len bits (network order) of the key words k (raw address bytes, little-endian
+// words) kept, the rest zeroed.
+__host__ __device__ inline void rule_mask(const uint32_t k[4], uint32_t len, uint32_t a[4]) {
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        const int bits = (int)len - 32 * w;
+        const uint32_t be = bits <= 0 ? 0u : bits >= 32 ? 0xFFFFFFFFu : ~0u << (32 - bits);
+        // byte-swap the big-endian mask into the key word's byte order
+        const uint32_t le = (be >> 24) | ((be >> 8) & 0xFF00u) | ((be << 8) & 0xFF0000u) | (be << 24);
+        a[w] = k[w] & le;
+    }
+}
+__host__ __device__ inline uint32_t rule_fp(const uint32_t a[4]) {
+    return a[0] ^ (a[1] * 0x9E3779B1u) ^ (a[2] * 0x85EBCA77u) ^ (a[3] * 0xC2B2AE3Du);
+}
+__host__ __device__ inline uint32_t rule_hash(uint32_t tag, const uint32_t a[4]) {
+    uint64_t h = mix64(((uint64_t)tag << 32) ^ a[0]);
+    if ((tag >> 8) == 2) h = mix64(h ^ ((uint64_t)a[1] | ((uint64_t)a[2] << 32)) ^ ((uint64_t)a[3] << 17));
+    return (uint32_t)(h >> 32);
 }
 
 // First probe slot of a source in the table (shared by k_parse, the map ops and the
@@ -288,8 +332,8 @@ struct PacketIn {
 hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, const uint64_t *ts,
                                    uint32_t n, uint8_t *verdict, Slot *table, TableState *tstate,
                                    BatchState *bs, const Scratch &sc, uint32_t id_gen,
-                                   const TableIndex &X, const Limits &lim, bool do_limit,
-                                   const FlowRequest *flows, const HistBufs &hist,
+                                   const TableIndex &X, const Limits &lim, const RuleSet &rules,
+                                   bool do_limit, const FlowRequest *flows, const HistBufs &hist,
                                    hipStream_t st, hipStream_t st2, hipEvent_t fork_ev,
                                    hipEvent_t join_ev, hipStream_t st3, hipEvent_t walk_fork_ev,
                                    hipEvent_t walk_join_ev, PipeTiming *tm);

@@ -28,6 +28,9 @@ MAP_IPV4_BLACKLIST = 3
 MAP_IPV6_BLACKLIST = 4
 MAP_IPV4_TOKENS = 5   # build-defined token-bucket state
 MAP_IPV6_TOKENS = 6
+MAP_IPV4_PREFIX = 7   # build-defined prefix blocklists: LPM-trie keys
+MAP_IPV6_PREFIX = 8
+PREFIX_MAX_ENTRIES = 65536
 MAP_NAMES = {
     MAP_STATS: "stats_map",
     MAP_IPV4_STATS: "ipv4_stats_map",
@@ -36,6 +39,8 @@ MAP_NAMES = {
     MAP_IPV6_BLACKLIST: "ipv6_blacklist_map",
     MAP_IPV4_TOKENS: "ipv4_tokens_map",
     MAP_IPV6_TOKENS: "ipv6_tokens_map",
+    MAP_IPV4_PREFIX: "ipv4_prefix_blocklist",
+    MAP_IPV6_PREFIX: "ipv6_prefix_blocklist",
 }
 BPF_ANY, BPF_NOEXIST, BPF_EXIST = 0, 1, 2
 
@@ -196,6 +201,22 @@ def _ptr(a: np.ndarray) -> int:
 _V6_MAPS = (MAP_IPV6_STATS, MAP_IPV6_BLACKLIST, MAP_IPV6_TOKENS)
 
 
+def _key_len(map_id: int) -> int:
+    if map_id == MAP_IPV4_PREFIX:
+        return 8
+    if map_id == MAP_IPV6_PREFIX:
+        return 20
+    return 16 if map_id in _V6_MAPS else 4
+
+
+def prefix_key(addr: bytes, prefixlen: int) -> bytes:
+    """struct bpf_lpm_trie_key {u32 prefixlen; u8 addr[4 | 16]} of a prefix-map key."""
+    addr = bytes(addr)
+    if len(addr) not in (4, 16):
+        raise ValueError("prefix addresses are 4 or 16 bytes")
+    return int(prefixlen).to_bytes(4, "little") + addr
+
+
 def _value_words(map_id: int) -> int:
     """u64 words of a per-IP map value: ip_stats 3, token-bucket state 2, blacklist 1."""
     if map_id in (MAP_IPV4_STATS, MAP_IPV6_STATS):
@@ -209,7 +230,7 @@ def _key_bytes(map_id: int, key) -> bytes:
     if isinstance(key, int):
         key = key.to_bytes(4, "little")
     key = bytes(key)
-    want = 16 if map_id in _V6_MAPS else 4
+    want = _key_len(map_id)
     if len(key) != want:
         raise ValueError(f"{MAP_NAMES[map_id]} keys are {want} bytes")
     return key
@@ -331,7 +352,7 @@ class FsxContext:
         map_dump returns): one device pass; all or nothing (-ENOSPC when full)."""
         if map_id == MAP_STATS:
             raise ValueError("stats_map has no batched update")
-        klen = 16 if map_id in _V6_MAPS else 4
+        klen = _key_len(map_id)
         vw = _value_words(map_id)
         n = len(entries)
         keys = np.zeros((max(n, 1), klen), dtype=np.uint8)
@@ -355,7 +376,7 @@ class FsxContext:
         cap = n.value
         if map_id == MAP_STATS:
             return {0: self.map_lookup(MAP_STATS, 0)}
-        klen = 16 if map_id in _V6_MAPS else 4
+        klen = _key_len(map_id)
         vw = _value_words(map_id)
         keys = np.zeros((max(cap, 1), klen), dtype=np.uint8)
         vals = np.zeros((max(cap, 1), vw), dtype=np.uint64)
@@ -407,7 +428,7 @@ class FsxContext:
         return keys[:m], fam[:m], feat[:m]
 
     BATCH_INFO = ("ip_packets", "sources", "new_sources", "any_ipv6", "non_monotone",
-                  "max_len", "max_ts", "allowed", "dropped", "v6_fix_runs", "sorted_payload",
+                  "max_len", "max_ts", "allowed", "dropped", "prefix_rule_drops", "sorted_payload",
                   "light_packets")
 
     def last_batch_info(self) -> dict:

@@ -59,7 +59,10 @@ extern "C" {
 #define FSX_FLAG_ONESWEEP_SORT 2u
 
 /* Map ids: the five maps of src/fsx_kern.c:56-94, then the token-bucket state maps of
- * the build-defined token bucket (value fsx_tb_state). */
+ * the build-defined token bucket (value fsx_tb_state), then the
+ * build-defined prefix blocklists: BPF_MAP_TYPE_LPM_TRIE-style maps
+ * whose key is struct bpf_lpm_trie_key {u32 prefixlen; u8 addr[4 | 16]} (8 / 20 bytes)
+ * and whose value is a u64 "blocked till" in ns like the blacklists'. */
 enum fsx_map_id {
     FSX_MAP_STATS = 0,          /* stats_map          src/fsx_kern.c:56-62 */
     FSX_MAP_IPV4_STATS = 1,     /* ipv4_stats_map     src/fsx_kern.c:64-70 */
@@ -68,8 +71,22 @@ enum fsx_map_id {
     FSX_MAP_IPV6_BLACKLIST = 4, /* ipv6_blacklist_map src/fsx_kern.c:88-94 */
     FSX_MAP_IPV4_TOKENS = 5,    /* build-defined: key 4 B  -> fsx_tb_state */
     FSX_MAP_IPV6_TOKENS = 6,    /* build-defined: key 16 B -> fsx_tb_state */
-    FSX_MAP_COUNT = 7
+    FSX_MAP_IPV4_PREFIX = 7,    /* build-defined: fsx_prefix_key4 -> u64 till */
+    FSX_MAP_IPV6_PREFIX = 8,    /* build-defined: fsx_prefix_key6 -> u64 till */
+    FSX_MAP_COUNT = 9
 };
+
+/* Prefix-blocklist keys (struct bpf_lpm_trie_key layout; prefixlen in host order).
+ * Update and delete are exact on (prefixlen, the first prefixlen bits of addr); the
+ * address bits past prefixlen are ignored. Lookup is a longest-prefix match of addr
+ * over the rules of length <= prefixlen (BPF LPM-trie lookup semantics). Every IP packet
+ * of a limiter batch is first matched against its family's rules: when the longest
+ * matching rule has 0 < now <= till the packet is dropped (stats_map dropped + 1) and
+ * never reaches the per-source maps; a longest match with till == 0 or expired lets it
+ * through (an exception inside a shorter blocked prefix). */
+typedef struct fsx_prefix_key4 { uint32_t prefixlen; uint8_t addr[4]; } fsx_prefix_key4;
+typedef struct fsx_prefix_key6 { uint32_t prefixlen; uint8_t addr[16]; } fsx_prefix_key6;
+#define FSX_PREFIX_MAX_ENTRIES 65536   /* rules per prefix map */
 
 /* bpf_map_update_elem flags (linux/bpf.h). */
 #define FSX_BPF_ANY 0
@@ -192,7 +209,8 @@ int fsx_map_update_batch(fsx_ctx *ctx, int map_id, const void *keys, const void 
 int fsx_map_dump(fsx_ctx *ctx, int map_id, void *keys, void *values, size_t cap,
                  size_t *n_out);
 int fsx_get_stats(fsx_ctx *ctx, fsx_stats *out);
-/* Empty every map and zero the stats (a fresh program load). */
+/* Empty every per-source map and zero the stats (a fresh program load). The prefix
+ * blocklists are operator configuration, like the loaded model, and stay. */
 int fsx_reset(fsx_ctx *ctx);
 
 /* Scoring (model/model.py:132-137, decision model/model.py:206). */
@@ -289,8 +307,8 @@ int fsx_pcap_records_device(fsx_ctx *ctx, const uint8_t *d_buf, const uint64_t *
 
 /* Facts about the last batch (after fsx_sync): info[0] IP packets, [1] distinct
  * source IPs, [2] sources new to the maps, [3] any IPv6, [4] non-monotone clock,
- * [5] max frame length, [6] max timestamp, [7] allowed, [8] dropped, [9] IPv6
- * hash-collision runs fixed, [10] 1 when (ts, len) travelled with the sort as payload
+ * [5] max frame length, [6] max timestamp, [7] allowed, [8] dropped, [9] packets
+ * dropped by a prefix rule (counted in [8], not in [0]), [10] 1 when (ts, len) travelled with the sort as payload
  * words (timestamps within 2^40 ns of the batch minimum, frame lengths < 2^24), 0 when
  * they were gathered by index, [11] IP packets of non-heavy sources (the entries the
  * later sort passes covered). Returns the number of entries written. */

@@ -18,14 +18,16 @@
  *                    with cvtps_epi32 overflow -> INT32_MIN; quantized sigmoid with
  *                    output qparams (1/256, 0)).
  *   build-defined    sliding window, token bucket, flow features: DESIGN.md §4-§5
- *                    (no reference code exists: README.md:155-162, src/fsx_kern_ml.c:1-16).
+ *                    (no reference code exists: README.md:155-162, src/fsx_kern_ml.c:1-16);
+ *                    prefix blocklists DESIGN.md §4.4 (the reference's TODO.md:1-3 defers
+ *                    LPM; BPF_MAP_TYPE_LPM_TRIE key/lookup semantics).
  *
  * Pinning: parse is checked against the reference's own
  * parsing_helper.h compiled by oracle/Makefile into oracle/_ref/; the fixed window
  * against the known-answer behaviours recorded from the reference program
  * (tests/golden/kat_fixed_window.json); scoring against vectors
  * produced by torch with the reference weights (tests/golden/make_score_vectors.py).
- * Sliding window, token bucket and features: parity unpinned (no reference).
+ * Sliding window, token bucket, features, prefix rules: parity unpinned (no reference).
  *
  * Semantics are sequential, single-CPU, arrival order. Maps never evict: an insert
  * into a full map sets the context error (the reference LRU would evict an
@@ -181,13 +183,17 @@ typedef struct ip_stats { uint64_t pps, bps, track_time; } ip_stats;  /* fsx_str
 typedef struct tb_state { uint64_t tokens, last; } tb_state;
 
 enum { MAP_STATS = 0, MAP_V4_STATS = 1, MAP_V6_STATS = 2, MAP_V4_BL = 3, MAP_V6_BL = 4,
-       MAP_V4_TB = 5, MAP_V6_TB = 6 };
+       MAP_V4_TB = 5, MAP_V6_TB = 6, MAP_V4_PREFIX = 7, MAP_V6_PREFIX = 8 };
+#define PREFIX_MAX_ENTRIES 65536
 
 typedef struct sw_log { uint64_t *t; uint32_t *l; size_t n, cap; } sw_log;
 
 typedef struct fsxo_ctx {
     fsxo_config cfg;
     omap m[7];
+    /* prefix blocklists: {u32 prefixlen; addr bytes, bits past prefixlen zero} -> till */
+    omap pfx[2];
+    uint32_t pfx_len_cnt[2][129];
     uint64_t allowed, dropped;      /* stats_map, fsx_struct.h:11-15 */
     int err;
     /* sliding window logs, indexed by a side map key -> slot */
@@ -223,6 +229,8 @@ fsxo_ctx *fsxo_open(const fsxo_config *cfg) {
     r |= omap_init(&c->m[MAP_V6_TB], me, 16, 16);
     r |= omap_init(&c->swidx[0], me, 4, 8);
     r |= omap_init(&c->swidx[1], me, 16, 8);
+    r |= omap_init(&c->pfx[0], PREFIX_MAX_ENTRIES, 8, 8);
+    r |= omap_init(&c->pfx[1], PREFIX_MAX_ENTRIES, 20, 8);
     if (r) return NULL;
     return c;
 }
@@ -237,6 +245,7 @@ void fsxo_close(fsxo_ctx *c) {
     if (!c) return;
     for (int i = 0; i < 7; ++i) omap_free(&c->m[i]);
     omap_free(&c->swidx[0]); omap_free(&c->swidx[1]);
+    omap_free(&c->pfx[0]); omap_free(&c->pfx[1]);
     sw_free_logs(c);
     free(c);
 }
@@ -244,7 +253,7 @@ void fsxo_close(fsxo_ctx *c) {
 void fsxo_reset(fsxo_ctx *c) {
     for (int i = 0; i < 7; ++i) omap_clear(&c->m[i]);
     omap_clear(&c->swidx[0]); omap_clear(&c->swidx[1]);
-    sw_free_logs(c);
+    sw_free_logs(c);   /* (the prefix blocklists stay: configuration, fsx_hip.h) */
     c->allowed = c->dropped = 0;
     c->err = 0;
 }
@@ -258,12 +267,64 @@ static omap *map_of(fsxo_ctx *c, int map_id) {
     return &c->m[map_id];
 }
 
+/* ------------------------------------------------------------------ prefix rules */
+/* Canonical rule key: prefixlen, then the address with every bit past prefixlen
+ * cleared (network bit order: byte b holds bits 8b..8b+7, most significant first). */
+static void prefix_canon(uint32_t plen, const uint8_t *addr, int alen, uint8_t *out) {
+    memcpy(out, &plen, 4);
+    for (int b = 0; b < alen; ++b) {
+        int bits = (int)plen - 8 * b;
+        uint8_t m = bits >= 8 ? 0xFF : bits <= 0 ? 0 : (uint8_t)(0xFF << (8 - bits));
+        out[4 + b] = addr[b] & m;
+    }
+}
+
+/* Longest-prefix match of addr over the rules of length <= maxlen; NULL if none. */
+static uint64_t *prefix_match(fsxo_ctx *c, int v6, const uint8_t *addr, uint32_t maxlen) {
+    const int alen = v6 ? 16 : 4;
+    uint8_t k[20];
+    for (int L = (int)maxlen; L >= 0; --L) {
+        if (!c->pfx_len_cnt[v6][L]) continue;
+        prefix_canon((uint32_t)L, addr, alen, k);
+        uint64_t *v = (uint64_t *)omap_lookup(&c->pfx[v6], k);
+        if (v) return v;
+    }
+    return NULL;
+}
+
+static int prefix_op(fsxo_ctx *c, int op, int map_id, const void *key, const void *val, void *out) {
+    const int v6 = map_id == MAP_V6_PREFIX, alen = v6 ? 16 : 4;
+    uint32_t plen;
+    memcpy(&plen, key, 4);
+    if (plen > (uint32_t)(8 * alen)) return -EINVAL;
+    const uint8_t *addr = (const uint8_t *)key + 4;
+    if (op == 0) {
+        uint64_t *v = prefix_match(c, v6, addr, plen);
+        if (!v) return -ENOENT;
+        memcpy(out, v, 8);
+        return 0;
+    }
+    uint8_t k[20];
+    prefix_canon(plen, addr, alen, k);
+    omap *m = &c->pfx[v6];
+    if (op == 2) {
+        int r = omap_delete(m, k);
+        if (!r) c->pfx_len_cnt[v6][plen]--;
+        return r;
+    }
+    int existed = omap_lookup(m, k) != NULL;
+    int r = omap_update(m, k, val);
+    if (!r && !existed) c->pfx_len_cnt[v6][plen]++;
+    return r;
+}
+
 int fsxo_map_lookup(fsxo_ctx *c, int map_id, const void *key, void *val) {
     if (map_id == MAP_STATS) {
         uint64_t s[2] = {c->allowed, c->dropped};
         memcpy(val, s, 16);
         return 0;
     }
+    if (map_id == MAP_V4_PREFIX || map_id == MAP_V6_PREFIX) return prefix_op(c, 0, map_id, key, NULL, val);
     omap *m = map_of(c, map_id);
     if (!m) return -EINVAL;
     void *v = omap_lookup(m, (const uint8_t *)key);
@@ -279,19 +340,21 @@ int fsxo_map_update(fsxo_ctx *c, int map_id, const void *key, const void *val) {
         c->allowed = s[0]; c->dropped = s[1];
         return 0;
     }
+    if (map_id == MAP_V4_PREFIX || map_id == MAP_V6_PREFIX) return prefix_op(c, 1, map_id, key, val, NULL);
     omap *m = map_of(c, map_id);
     if (!m) return -EINVAL;
     return omap_update(m, (const uint8_t *)key, val);
 }
 
 int fsxo_map_delete(fsxo_ctx *c, int map_id, const void *key) {
+    if (map_id == MAP_V4_PREFIX || map_id == MAP_V6_PREFIX) return prefix_op(c, 2, map_id, key, NULL, NULL);
     omap *m = map_of(c, map_id);
     if (!m) return -EINVAL;
     return omap_delete(m, (const uint8_t *)key);
 }
 
 size_t fsxo_map_dump(fsxo_ctx *c, int map_id, void *keys, void *vals, size_t cap) {
-    omap *m = map_of(c, map_id);
+    omap *m = map_id == MAP_V4_PREFIX ? &c->pfx[0] : map_id == MAP_V6_PREFIX ? &c->pfx[1] : map_of(c, map_id);
     if (!m) return 0;
     return omap_dump(m, (uint8_t *)keys, (uint8_t *)vals, cap);
 }
@@ -463,6 +526,12 @@ static int one_packet(fsxo_ctx *c, const uint8_t *hdr, uint32_t len, uint64_t ts
     if (cls == CLS_DROP_PARSE) return XDP_DROP;        /* src/fsx_kern.c:124-127,139-140,146-147 */
     if (cls == CLS_PASS_NONIP) return XDP_PASS;        /* src/fsx_kern.c:128-131 */
     int v6 = cls == CLS_V6;
+    /* prefix blocklist first: the longest matching rule decides */
+    const uint64_t *till = prefix_match(c, v6, key, v6 ? 128 : 32);
+    if (till && *till > 0 && ts <= *till) {
+        c->dropped++;
+        return XDP_DROP;
+    }
     switch (c->cfg.limiter) {
     case 1: return sliding_window_packet(c, v6, key, len, ts);
     case 2: return token_bucket_packet(c, v6, key, len, ts);

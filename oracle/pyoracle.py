@@ -135,8 +135,22 @@ class Oracle:
         if rc:
             raise RuntimeError(f"oracle map update {rc}")
 
+    def map_lookup(self, map_id: int, key: bytes):
+        """Scalar value (blacklists, prefix maps: longest match) or None."""
+        vw = 3 if map_id in (1, 2) else 2 if map_id in (5, 6) else 1
+        v = np.zeros(vw, dtype=np.uint64)
+        k = np.frombuffer(bytes(key), dtype=np.uint8).copy()
+        rc = lib().fsxo_map_lookup(self._h, map_id, _p(k), _p(v))
+        if rc:
+            return None
+        return tuple(int(x) for x in v) if vw > 1 else int(v[0])
+
+    def map_delete(self, map_id: int, key: bytes) -> int:
+        k = np.frombuffer(bytes(key), dtype=np.uint8).copy()
+        return lib().fsxo_map_delete(self._h, map_id, _p(k))
+
     def map_dump(self, map_id: int) -> dict:
-        klen = 16 if map_id in (2, 4, 6) else 4
+        klen = 16 if map_id in (2, 4, 6) else 8 if map_id == 7 else 20 if map_id == 8 else 4
         vw = 3 if map_id in (1, 2) else 2 if map_id in (5, 6) else 1
         n = lib().fsxo_map_dump(self._h, map_id, None, None, 0)
         keys = np.zeros((max(n, 1), klen), dtype=np.uint8)
