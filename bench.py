@@ -243,7 +243,7 @@ def main():
                                    "unit": "Mpps", "ms_per_step": round(lt / args.limiter_steps * 1e3, 4),
                                    "steps": args.limiter_steps, "allowed": la, "dropped": ld}
 
-    # prefix blocklists (DESIGN.md §4.4; SURVEY §8 f row 4): the same batch with a 64K-rule
+    # prefix blocklists (DESIGN.md §4.3; SURVEY §8 f row 4): the same batch with a 64K-rule
     # table — 61440 random /24 prefixes (mostly missing the stream) and 4096 rules on the
     # stream's own sources (/32 and /28, permanent) — fixed window, verdicts + maps
     rules_leg = None

@@ -288,7 +288,7 @@ __global__ __launch_bounds__(1024) void k_heavy_pick(PacketIn in, const uint32_t
     hs->map[tid] = s_map[tid];
 }
 
-// Prefix blocklist (DESIGN.md §4.4): a packet whose /24 filter bit is clear matches no
+// Prefix blocklist (DESIGN.md §4.3): a packet whose /24 filter bit is clear matches no
 // rule (one load); otherwise the family's distinct rule lengths are probed longest first
 // (the first slots of four lengths at a time loaded together); the first rule found is
 // the longest match and drops the packet when 0 < now <= till (till 0 or expired: the

@@ -174,7 +174,7 @@ __host__ __device__ inline uint64_t slot_hash(uint32_t tag, const uint32_t k[4],
 }
 
 // ------------------------------------------------------------ prefix rules
-// Prefix blocklist (FSX_MAP_IPV4_PREFIX / _IPV6_PREFIX, DESIGN.md §4.4): one open-addressing
+// Prefix blocklist (FSX_MAP_IPV4_PREFIX / _IPV6_PREFIX, DESIGN.md §4.3): one open-addressing
 // table of both families' rules keyed by (family, prefix length, masked address), built by
 // the host when the rules change; the lookup probes the family's distinct lengths longest
 // first, so the first hit is the longest match.

@@ -28,7 +28,7 @@ MAP_IPV4_BLACKLIST = 3
 MAP_IPV6_BLACKLIST = 4
 MAP_IPV4_TOKENS = 5   # build-defined token-bucket state
 MAP_IPV6_TOKENS = 6
-MAP_IPV4_PREFIX = 7   # build-defined prefix blocklists (DESIGN.md §4.4): LPM-trie keys
+MAP_IPV4_PREFIX = 7   # build-defined prefix blocklists (DESIGN.md §4.3): LPM-trie keys
 MAP_IPV6_PREFIX = 8
 PREFIX_MAX_ENTRIES = 65536
 MAP_NAMES = {

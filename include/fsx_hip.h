@@ -60,7 +60,7 @@ extern "C" {
 
 /* Map ids: the five maps of src/fsx_kern.c:56-94, then the token-bucket state maps of
  * the build-defined token bucket (value fsx_tb_state), then the
- * build-defined prefix blocklists (DESIGN.md §4.4): BPF_MAP_TYPE_LPM_TRIE-style maps
+ * build-defined prefix blocklists (DESIGN.md §4.3): BPF_MAP_TYPE_LPM_TRIE-style maps
  * whose key is struct bpf_lpm_trie_key {u32 prefixlen; u8 addr[4 | 16]} (8 / 20 bytes)
  * and whose value is a u64 "blocked till" in ns like the blacklists'. */
 enum fsx_map_id {

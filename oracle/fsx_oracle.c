@@ -19,7 +19,7 @@
  *                    output qparams (1/256, 0)).
  *   build-defined    sliding window, token bucket, flow features: DESIGN.md §4-§5
  *                    (no reference code exists: README.md:155-162, src/fsx_kern_ml.c:1-16);
- *                    prefix blocklists DESIGN.md §4.4 (the reference's TODO.md:1-3 defers
+ *                    prefix blocklists DESIGN.md §4.3 (the reference's TODO.md:251 defers
  *                    LPM; BPF_MAP_TYPE_LPM_TRIE key/lookup semantics).
  *
  * Pinning: parse is checked against the reference's own
@@ -526,7 +526,7 @@ static int one_packet(fsxo_ctx *c, const uint8_t *hdr, uint32_t len, uint64_t ts
     if (cls == CLS_DROP_PARSE) return XDP_DROP;        /* src/fsx_kern.c:124-127,139-140,146-147 */
     if (cls == CLS_PASS_NONIP) return XDP_PASS;        /* src/fsx_kern.c:128-131 */
     int v6 = cls == CLS_V6;
-    /* prefix blocklist first (DESIGN.md §4.4): the longest matching rule decides */
+    /* prefix blocklist first (DESIGN.md §4.3): the longest matching rule decides */
     const uint64_t *till = prefix_match(c, v6, key, v6 ? 128 : 32);
     if (till && *till > 0 && ts <= *till) {
         c->dropped++;

@@ -1,8 +1,8 @@
-"""GPU parity of the prefix blocklists (FSX_MAP_IPV4_PREFIX / _IPV6_PREFIX, DESIGN.md §4.4)
+"""GPU parity of the prefix blocklists (FSX_MAP_IPV4_PREFIX / _IPV6_PREFIX, DESIGN.md §4.3)
 against the CPU oracle: verdicts, stats_map and every map (the prefix maps included) under
 all three limiters, rule changes between batches, the map syscalls' LPM semantics, the
 owner's record mode, and the flow features of the packets that reach the per-source path.
-Build-defined semantics (the reference defers LPM, TODO.md:1-3): parity unpinned against
+Build-defined semantics (the reference defers LPM, TODO.md:251): parity unpinned against
 the reference itself; hand-worked cases pin the oracle (tests/test_oracle_prefix.py).
 """
 import errno

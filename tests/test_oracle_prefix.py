@@ -1,6 +1,6 @@
-"""Prefix blocklists in the CPU oracle (DESIGN.md §4.4): known answers worked by hand.
+"""Prefix blocklists in the CPU oracle (DESIGN.md §4.3): known answers worked by hand.
 
-Build-defined feature (the reference defers LPM, TODO.md:1-3): the semantics are those
+Build-defined feature (the reference defers LPM, TODO.md:251): the semantics are those
 of a BPF_MAP_TYPE_LPM_TRIE consulted before the per-source maps — parity unpinned
 against the reference, pinned here by hand-computed cases.
 """
