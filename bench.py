@@ -194,7 +194,7 @@ def main():
         ex = plane.last_exchange or {"sent": [], "received": []}
         exchange = {"records_sent": ex["sent"], "records_received": ex["received"],
                     "dropped_by_replica": ex.get("filtered", 0), "sub_batches": chunks,
-                    "record_bytes": lib.SHARD_RECORD_BYTES, "backend": args.dist_backend}
+                    "record_bytes": sorted(plane.formats) or None, "backend": args.dist_backend}
         malicious = None
         if not args.no_mlp:
             fl = eng.flows

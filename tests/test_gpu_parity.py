@@ -489,7 +489,12 @@ def test_map_update_batch_restores_state(native, oracle, limiter, maps):
     cfg = dict(CFGS["tight"], limiter=limiter, max_entries=1 << 14)
     if limiter == 2:
         cfg = dict(limiter=2, tb_rate=300_000, tb_burst=4, max_entries=1 << 14)
+    from flowsentryx_amd.lib import prefix_key
+    maps = maps + (7, 8)   # with prefix rules: configuration travels too
     with gpu_ctx(native, **cfg) as a, gpu_ctx(native, **cfg) as b:
+        for i in range(0, 2000, 97):
+            a.map_update(7, prefix_key(bytes(hdr[i, 26:30]), 24 + i % 9), 2**64 - 1 if i % 3 else 0)
+        a.map_update(8, prefix_key(bytes(16), 1), 2**64 - 1)
         a.verdict_batch(hdr[:20000], ln[:20000], ts[:20000])
         for m in maps:
             b.map_update_batch(m, a.map_dump(m))
