@@ -342,8 +342,19 @@ __global__ __launch_bounds__(256) void k_flow_combine(const uint64_t *__restrict
         const uint32_t g = span_list[i];
         const uint32_t s = seg_start[g], e = seg_start[g + 1];
         const uint32_t t0 = s / kFT, t1 = (e - 1) / kFT;
+        // a heavy source spans thousands of tiles: four partials in flight per lane
+        // (integer sums and max: any grouping gives the same result)
         FlowAcc a = acc_zero();
-        for (uint32_t t = t0 + 1 + lane; t <= t1; t += 64) acc_add(a, firstp[t]);
+        uint32_t t = t0 + 1 + lane;
+        for (; t + 192u <= t1; t += 256u) {
+            FlowAcc b0 = firstp[t], b1 = firstp[t + 64u];
+            const FlowAcc b2 = firstp[t + 128u], b3 = firstp[t + 192u];
+            acc_add(b0, b2);
+            acc_add(b1, b3);
+            acc_add(a, b0);
+            acc_add(a, b1);
+        }
+        for (; t <= t1; t += 64u) acc_add(a, firstp[t]);
         a = wave_sum_acc(a);
         if (lane == 0) {
             FlowAcc tot = lastp[t0];
