@@ -169,8 +169,8 @@ static int alloc_scratch(fsx_ctx *c, uint64_t cap) {
     HIPCHK(c, hipMalloc(&s.hist, 256ull * std::max<uint64_t>(kSortMaxBlocks, cap / kSortTile + 2) * 4));
     HIPCHK(c, hipMalloc(&s.tile_aux, ntiles * 4));
     HIPCHK(c, hipMalloc(&s.tile_last, ntiles));
-    HIPCHK(c, hipMalloc(&s.id_tab, c->slots * 32));
-    HIPCHK(c, hipMemset(s.id_tab, 0, c->slots * 32));   // generation 0: every slot empty
+    // (s.id_tab, the per-batch id table of flow-only batches, is allocated on first use:
+    // slots * 32 bytes, 16 GiB for a 2^28-source context that never needs it)
     c->id_gen = 0;
     HIPCHK(c, hipMalloc(&s.seg_order, (cap + 1) * 4));
     HIPCHK(c, hipMalloc(&s.sub_cnt, (cap / 1024 + 8) * 4));
@@ -255,7 +255,9 @@ int fsx_open(fsx_ctx **out, const fsx_config *cfg) {
     *out = nullptr;
     fsx_config k;
     if (cfg) k = *cfg; else fsx_config_default(&k);
-    if (k.max_entries == 0 || k.max_entries > (1ull << 33)) return -EINVAL;
+    // slots = next_pow2(2 * max_entries) <= 2^32: a source id (its slot) fills at most the
+    // sort word's 32 id bits (fsx_internal.h pk_id)
+    if (k.max_entries == 0 || k.max_entries > (1ull << 31)) return -EINVAL;
     if (k.max_batch == 0 || k.max_batch > kMaxBatchLimit) return -EINVAL;
     if (k.limiter < FSX_LIMIT_FIXED_WINDOW || k.limiter > FSX_LIMIT_TOKEN_BUCKET) return -EINVAL;
     // token bucket: capacity burst * 1e9 nano-tokens must stay <= 2^61
@@ -564,8 +566,12 @@ static int run_batch(fsx_ctx *c, const PacketIn &in, const uint32_t *d_len, cons
         tmv = PipeTiming{c->ev[c->ring_n], c->ev_names[c->ring_n], c->ev_prev[c->ring_n], kMaxEv, 0};
         tm = &tmv;
     }
+    if (!do_limit && !c->sc.id_tab) {   // flow-only batch: its per-batch id table
+        HIPCHK(c, hipMalloc(&c->sc.id_tab, c->slots * 32));
+        HIPCHK(c, hipMemsetAsync(c->sc.id_tab, 0, c->slots * 32, c->stream));   // every slot empty
+    }
     if (++c->id_gen == 0x10000u) {   // 16-bit generations: clear the id table on wrap
-        HIPCHK(c, hipMemsetAsync(c->sc.id_tab, 0, c->slots * 32, c->stream));
+        if (c->sc.id_tab) HIPCHK(c, hipMemsetAsync(c->sc.id_tab, 0, c->slots * 32, c->stream));
         c->id_gen = 1;
     }
     hipError_t e = launch_verdict_pipeline(in, d_len, d_ts, (uint32_t)n, d_verdict, c->table,
@@ -786,7 +792,7 @@ int fsx_map_update_batch(fsx_ctx *c, int map_id, const void *keys, const void *v
     hipError_t e = hipMemcpyAsync(dk, keys, n * klen, hipMemcpyHostToDevice, c->stream);
     if (e == hipSuccess) e = hipMemcpyAsync(dv, values, n * vlen, hipMemcpyHostToDevice, c->stream);
     if (e == hipSuccess && ++c->id_gen == 0x10000u) {   // 16-bit generations (as run_batch)
-        e = hipMemsetAsync(c->sc.id_tab, 0, c->slots * 32, c->stream);
+        if (c->sc.id_tab) e = hipMemsetAsync(c->sc.id_tab, 0, c->slots * 32, c->stream);
         c->id_gen = 1;
     }
     const uint32_t born = c->id_gen;

@@ -1021,7 +1021,7 @@ __global__ __launch_bounds__(256) void k_heads_write(BatchState *bs, const uint8
                                                      const uint32_t *__restrict__ tile_off,
                                                      uint32_t *__restrict__ seg_start,
                                                      const uint64_t *__restrict__ S,
-                                                     uint32_t *__restrict__ seg_slot) {
+                                                     uint32_t *__restrict__ seg_slot, uint64_t id_mask) {
     __shared__ uint32_t s_tmp[4];
     const uint32_t M = bs->n_valid;
     const uint32_t ntiles = (M + kTile - 1) / kTile;
@@ -1042,7 +1042,7 @@ __global__ __launch_bounds__(256) void k_heads_write(BatchState *bs, const uint8
         for (int k = 0; k < 16; ++k) {
             if ((f[k >> 2] >> (8 * (k & 3))) & 1u) {
                 seg_start[off] = p0 + k;
-                if (seg_slot) seg_slot[off] = pk_id(S[p0 + k]);   // id = table slot
+                if (seg_slot) seg_slot[off] = pk_id(S[p0 + k], id_mask);   // id = table slot
                 ++off;
             }
         }
@@ -1854,7 +1854,7 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
     mark("k_heads_count");
     k_scan_tiles_u32<<<1, 1024, 0, st>>>(sc.tile_aux, bs, sc.seg_start);
     k_heads_write<<<gridTiles, 256, 0, st>>>(bs, sc.headf, sc.tile_aux, sc.seg_start, S,
-                                             do_limit ? sc.seg_slot : nullptr);
+                                             do_limit ? sc.seg_slot : nullptr, lim.table_mask);
     mark("k_heads_write");
     const bool fork = flows && do_limit && st2 && fork_ev && join_ev;
     if (flows) {

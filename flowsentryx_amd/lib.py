@@ -388,6 +388,19 @@ class FsxContext:
             out[keys[i].tobytes()] = tuple(int(x) for x in vals[i]) if vw > 1 else int(vals[i, 0])
         return out
 
+    def map_arrays(self, map_id: int):
+        """(keys [n, klen] u8, values [n, words] u64) of one per-IP map, unordered: the
+        array form of map_dump for maps of millions of entries."""
+        n = C.c_size_t()
+        self._check(self._lib.fsx_map_dump(self._h, map_id, None, None, 0, C.byref(n)), "map_dump")
+        cap = n.value
+        keys = np.zeros((max(cap, 1), _key_len(map_id)), dtype=np.uint8)
+        vals = np.zeros((max(cap, 1), _value_words(map_id)), dtype=np.uint64)
+        self._check(self._lib.fsx_map_dump(self._h, map_id, _ptr(keys), _ptr(vals), cap, C.byref(n)),
+                    "map_dump")
+        m = min(cap, n.value)
+        return keys[:m], vals[:m]
+
     def stats(self) -> tuple[int, int]:
         s = FsxStats()
         self._check(self._lib.fsx_get_stats(self._h, C.byref(s)), "fsx_get_stats")

@@ -134,7 +134,7 @@ typedef struct fsx_config {
     uint64_t block_ns;        /* 10 s       src/fsx_kern.c:308,317 */
     uint64_t max_entries;     /* per map; MAX_TRACK_IPS=100000 src/fsx_struct.h:7.
                                  No LRU eviction: a full table makes a batch fail
-                                 with -ENOSPC. */
+                                 with -ENOSPC. 1 .. 2^31. */
     uint64_t max_batch;       /* largest n per call (device scratch is sized for it) */
     uint64_t tb_rate;         /* token bucket: refill in nano-tokens per ns (1000 = 1000 tok/s) */
     uint64_t tb_burst;        /* token bucket: capacity in tokens (<= FSX_TB_MAX_BURST) */

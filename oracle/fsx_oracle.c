@@ -607,6 +607,111 @@ int fsxo_batch_sharded(const fsxo_config *cfg, const uint8_t *hdr, const uint32_
     return err;
 }
 
+/* Persistent sharded runner (full-size parity checks in bench.py and the large GPU
+ * tests): T contexts on IP-disjoint shards (the owner rule of shard_main) that keep
+ * their maps across batches, so map dumps, stats and state carry equal one sequential
+ * context's. Each shard's maps hold ceil(1.25 * max_entries / T) + 4096 sources (the hash
+ * spreads sources evenly): -ENOSPC is not reproduced at max_entries exactly. Prefix
+ * rules go to every shard; per-source map updates to the source's owner. */
+typedef struct fsxo_shards { int T; fsxo_ctx *c[256]; } fsxo_shards;
+
+static int shard_of(int v6, const uint8_t *key, int T) {
+    const uint64_t hk = omap_hash(key, v6 ? 16 : 4) ^ (uint64_t)(v6 ? CLS_V6 : CLS_V4);
+    return (int)(fsx_splitmix64(hk) % (uint64_t)T);
+}
+
+void fsxo_shards_close(fsxo_shards *h) {
+    if (!h) return;
+    for (int t = 0; t < h->T; ++t) fsxo_close(h->c[t]);
+    free(h);
+}
+
+fsxo_shards *fsxo_shards_open(const fsxo_config *cfg, int nthreads) {
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 256) nthreads = 256;
+    fsxo_shards *h = (fsxo_shards *)calloc(1, sizeof(*h));
+    if (!h) return NULL;
+    fsxo_config k = *cfg;
+    if (nthreads > 1) k.max_entries = (5 * cfg->max_entries / 4 + nthreads - 1) / nthreads + 4096;
+    h->T = nthreads;
+    for (int t = 0; t < nthreads; ++t)
+        if (!(h->c[t] = fsxo_open(&k))) { fsxo_shards_close(h); return NULL; }
+    return h;
+}
+
+void fsxo_shards_reset(fsxo_shards *h) { for (int t = 0; t < h->T; ++t) fsxo_reset(h->c[t]); }
+
+int fsxo_shards_map_update(fsxo_shards *h, int map_id, const void *key, const void *val) {
+    if (map_id == MAP_V4_PREFIX || map_id == MAP_V6_PREFIX) {
+        for (int t = 0; t < h->T; ++t) {
+            int r = fsxo_map_update(h->c[t], map_id, key, val);
+            if (r) return r;
+        }
+        return 0;
+    }
+    if (map_id < 1 || map_id > 6) return -EINVAL;
+    const int v6 = map_id == MAP_V6_STATS || map_id == MAP_V6_BL || map_id == MAP_V6_TB;
+    return fsxo_map_update(h->c[shard_of(v6, (const uint8_t *)key, h->T)], map_id, key, val);
+}
+
+typedef struct shards_arg {
+    fsxo_ctx *c; const uint8_t *hdr; const uint32_t *len; const uint64_t *ts;
+    size_t n; uint8_t *verdict; int tid, T;
+} shards_arg;
+
+static void *shards_main(void *p) {
+    shards_arg *a = (shards_arg *)p;
+    for (size_t i = 0; i < a->n; ++i) {
+        uint8_t key[16];
+        const uint8_t *f = a->hdr + i * 64;
+        const int cls = fsxo_parse(f, a->len[i], key);
+        if (cls <= CLS_PASS_NONIP) {
+            if (a->tid == 0) a->verdict[i] = cls == CLS_DROP_PARSE ? XDP_DROP : XDP_PASS;
+            continue;
+        }
+        if (shard_of(cls == CLS_V6, key, a->T) != a->tid) continue;
+        a->verdict[i] = (uint8_t)one_packet(a->c, f, a->len[i], a->ts[i]);
+    }
+    return NULL;
+}
+
+int fsxo_shards_batch(fsxo_shards *h, const uint8_t *hdr, const uint32_t *len, const uint64_t *ts,
+                      size_t n, uint8_t *verdict) {
+    pthread_t th[256];
+    shards_arg args[256];
+    for (int t = 0; t < h->T; ++t) {
+        shards_arg a = {h->c[t], hdr, len, ts, n, verdict, t, h->T};
+        args[t] = a;
+        pthread_create(&th[t], NULL, shards_main, &args[t]);
+    }
+    int err = 0;
+    for (int t = 0; t < h->T; ++t) {
+        pthread_join(th[t], NULL);
+        if (h->c[t]->err) err = h->c[t]->err;
+    }
+    return err;
+}
+
+void fsxo_shards_stats(const fsxo_shards *h, uint64_t out[2]) {
+    out[0] = out[1] = 0;
+    for (int t = 0; t < h->T; ++t) { out[0] += h->c[t]->allowed; out[1] += h->c[t]->dropped; }
+}
+
+/* The shards' entries of map_id, concatenated (keys / vals may be NULL: count only). */
+size_t fsxo_shards_dump(fsxo_shards *h, int map_id, void *keys, void *vals, size_t cap) {
+    size_t n = 0;
+    if (map_id == MAP_V4_PREFIX || map_id == MAP_V6_PREFIX)   /* identical on every shard */
+        return fsxo_map_dump(h->c[0], map_id, keys, vals, cap);
+    omap *m0 = map_of(h->c[0], map_id);
+    if (!m0) return 0;
+    for (int t = 0; t < h->T; ++t) {
+        const size_t left = cap > n ? cap - n : 0;
+        n += fsxo_map_dump(h->c[t], map_id, keys ? (uint8_t *)keys + n * m0->klen : NULL,
+                           vals ? (uint8_t *)vals + n * m0->vlen : NULL, left);
+    }
+    return n;
+}
+
 /* ------------------------------------------------------------------ scoring */
 typedef struct fsxo_q8_model {
     int8_t weight[8];

@@ -66,6 +66,13 @@ def lib() -> C.CDLL:
         "fsxo_map_delete": (C.c_int, [vp, C.c_int, vp]),
         "fsxo_map_dump": (sz, [vp, C.c_int, vp, vp, sz]),
         "fsxo_batch_sharded": (C.c_int, [C.POINTER(OConfig), vp, vp, vp, sz, vp, C.c_int, vp]),
+        "fsxo_shards_open": (vp, [C.POINTER(OConfig), C.c_int]),
+        "fsxo_shards_close": (None, [vp]),
+        "fsxo_shards_reset": (None, [vp]),
+        "fsxo_shards_map_update": (C.c_int, [vp, C.c_int, vp, vp]),
+        "fsxo_shards_batch": (C.c_int, [vp, vp, vp, vp, sz, vp]),
+        "fsxo_shards_stats": (None, [vp, vp]),
+        "fsxo_shards_dump": (sz, [vp, C.c_int, vp, vp, sz]),
         "fsxo_sigmoid_lut": (None, [C.c_float, C.c_int32, vp]),
         "fsxo_score": (None, [C.POINTER(OQ8Model), vp, sz, vp, vp, vp]),
         "fsxo_flow_features": (sz, [vp, vp, vp, sz, sz, vp, vp, vp]),
@@ -158,6 +165,99 @@ class Oracle:
         lib().fsxo_map_dump(self._h, map_id, _p(keys), _p(vals), n)
         return {keys[i].tobytes(): (tuple(int(x) for x in vals[i]) if vw > 1 else int(vals[i, 0]))
                 for i in range(n)}
+
+
+def _klen(map_id: int) -> int:
+    return 16 if map_id in (2, 4, 6) else 8 if map_id == 7 else 20 if map_id == 8 else 4
+
+
+def _vw(map_id: int) -> int:
+    return 3 if map_id in (1, 2) else 2 if map_id in (5, 6) else 1
+
+
+def _map_value(map_id: int, value) -> np.ndarray:
+    return np.array(value if map_id in (1, 2, 5, 6) else [value], dtype=np.uint64)
+
+
+class ShardedOracle:
+    """The sequential oracle on T host threads over IP-disjoint shards, with persistent
+    maps (fsxo_shards_*): verdicts, stats_map and map dumps equal one Oracle's for the
+    same stream (per-source arrival order is kept), in 1/T of the time. Used for the
+    full-size checks (bench.py, large GPU tests); -ENOSPC is not reproduced."""
+
+    def __init__(self, nthreads: int, **kw):
+        self.cfg = default_config(**kw)
+        self._h = lib().fsxo_shards_open(C.byref(self.cfg), int(nthreads))
+        if not self._h:
+            raise MemoryError("fsxo_shards_open")
+
+    def close(self):
+        if self._h:
+            lib().fsxo_shards_close(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def reset(self):
+        lib().fsxo_shards_reset(self._h)
+
+    def batch(self, hdr, length, ts) -> np.ndarray:
+        hdr = np.ascontiguousarray(hdr, dtype=np.uint8).reshape(-1, 64)
+        length = np.ascontiguousarray(length, dtype=np.uint32)
+        ts = np.ascontiguousarray(ts, dtype=np.uint64)
+        out = np.empty(hdr.shape[0], dtype=np.uint8)
+        rc = lib().fsxo_shards_batch(self._h, _p(hdr), _p(length), _p(ts), hdr.shape[0], _p(out))
+        if rc:
+            raise RuntimeError(f"oracle error {rc}")
+        return out
+
+    def stats(self) -> tuple[int, int]:
+        s = np.zeros(2, dtype=np.uint64)
+        lib().fsxo_shards_stats(self._h, _p(s))
+        return int(s[0]), int(s[1])
+
+    def map_update(self, map_id: int, key: bytes, value):
+        k = np.frombuffer(bytes(key), dtype=np.uint8).copy()
+        v = _map_value(map_id, value)
+        rc = lib().fsxo_shards_map_update(self._h, map_id, _p(k), _p(v))
+        if rc:
+            raise RuntimeError(f"oracle map update {rc}")
+
+    def map_arrays(self, map_id: int):
+        """(keys [n, klen] u8, values [n, words] u64) of one map, unordered."""
+        n = lib().fsxo_shards_dump(self._h, map_id, None, None, 0)
+        keys = np.zeros((n, _klen(map_id)), dtype=np.uint8)
+        vals = np.zeros((n, _vw(map_id)), dtype=np.uint64)
+        if n:
+            lib().fsxo_shards_dump(self._h, map_id, _p(keys), _p(vals), n)
+        return keys, vals
+
+
+def sort_map_arrays(keys: np.ndarray, vals: np.ndarray):
+    """Rows of a map dump in key order (any key width), for array comparisons."""
+    k = np.ascontiguousarray(keys, dtype=np.uint8)
+    if k.shape[0] == 0:
+        return k, vals
+    w = (k.shape[1] + 7) // 8 * 8
+    kp = np.zeros((k.shape[0], w), dtype=np.uint8)
+    kp[:, :k.shape[1]] = k
+    cols = kp.view(">u8")   # big-endian words: byte-lexicographic order
+    order = np.lexsort(cols.T[::-1])
+    return k[order], np.ascontiguousarray(vals)[order]
+
+
+def same_map(a, b) -> bool:
+    """Two (keys, values) dumps hold the same entries."""
+    ka, va = sort_map_arrays(*a)
+    kb, vb = sort_map_arrays(*b)
+    return ka.shape == kb.shape and np.array_equal(ka, kb) and np.array_equal(va, vb)
 
 
 def parse(hdr, length):
