@@ -1,31 +1,38 @@
 #!/usr/bin/env python3
 """Benchmark: Mpps of FlowSentryX verdicts on MI355X (BASELINE.json metric).
 
-One "step" = one pass of the hot path over one batch of synthetic packets resident
-in HBM, starting from empty maps (fsx_reset is inside the timed step): parse ->
-per-source fixed-window rate limit + blacklist -> verdicts + map state
-(src/fsx_kern.c:96-347 semantics) -> per-source flow features -> q8 MLP score of
-every source with the reference weights (model/model.py:132-137). N=1 workload:
-BASELINE config 2 — 64M IPv4/UDP packets from 1M Zipf(1.1) sources over 30 s.
+One "step" = one pass of the hot path over one batch of synthetic packets resident in
+HBM, starting from empty maps (fsx_reset is inside the timed step): parse -> per-source
+fixed-window rate limit + blacklist -> verdicts + map state (src/fsx_kern.c:96-347
+semantics) -> per-source flow features -> q8 MLP score of every source with the
+reference weights (model/model.py:132-137). N=1 headline workload: BASELINE config 2 —
+64M IPv4/UDP packets from 1M Zipf(1.1) sources over 30 s.
 
 Multi-GPU (torch.distributed.run, one rank per GPU): weak scaling — one stream of
 N x 64M packets from one source population at the config's packet rate; rank r holds
-the contiguous slice [r*64M, (r+1)*64M) and every source is owned by one rank
-(hash of the address): RCCL all-to-all of 32-byte records to the owners, the full
-pipeline there, verdicts back by a second all-to-all (flowsentryx_amd/shard.py,
-DESIGN.md §7). The result equals the 1-GPU run over the whole stream.
+its slice and every source is owned by one rank (hash of the address): RCCL all-to-all
+of 16/32-byte records to the owners, the pipeline there, verdicts back
+(flowsentryx_amd/shard.py).
 
 Prints ONE JSON line on rank 0 with the driver's contract plus:
-  roofline      the dominant kernel (largest device time per step), its algorithmic
-                bytes per launch over its mean launch time measured with HIP events on
-                the library's stream inside the timed region;
+  roofline      the dominant kernel (largest device time per step): SURVEY §8 d
+                algorithmic bytes per launch (77 B per packet for k_parse) over its mean
+                launch time, HIP events on the library's stream (separate steps);
   pipeline      the whole step against SURVEY §8 d: 77 B/packet + 64 B per source;
-  cpu_baseline  the CPU oracle (sharded over host threads) on a bounded sample.
+  check         full-size parity of the benchmarked step (outside the timed region):
+                verdicts, stats_map and every map entry against the sharded CPU oracle,
+                for all three limiters; per-source features + scores too;
+  cpu_baseline  the oracle (the reference CPU path restated in C, sharded over the host
+                cores) on the whole config-2 stream, plus CPU PyTorch scoring of config 3;
+  legs          limiters, prefix_rules, warm (maps carried across steps), config3
+                (scoring), config4 (one rank's share of the 1B-packet / 16M-source flood;
+                at N=8 the whole of config 4), config5 (2^28-packet carpet + 64K rules).
 """
 from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -36,19 +43,18 @@ sys.path.insert(0, str(ROOT))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
 
-# Algorithmic bytes each kernel's function must move, per element it processes
-# (DESIGN.md §3): element = packet (parse) or IP packet (sort / fill).
+# SURVEY.md §8 d algorithmic bytes (what the function must move) per unit, per kernel;
+# impl = what this implementation's kernel moves by design, for reference
 KERNEL_BYTES = {
-    "k_parse": ("packet", 64 + 4 + 8 + 8),      # header record + len + ts in, sort word out
-    # one LSD digit pass: sort word + payload word in and out (pass 0 reads ts + len
-    # instead of a payload word: 36 B; passes 1-3: 32 B) -> 33 B per launch on average
-    "k_tile_scatter": ("ip_packet", 33),
-    "k_tile_hist": ("ip_packet", 8),            # sort word in (+ per-tile counts)
-    "k_onesweep": ("ip_packet", 16),            # sort word in + out, per digit pass
-    "k_flow_features": ("ip_packet", 8 + 4 + 8),  # sort word + len + ts per packet
-    "k_walk_fixed": ("ip_packet", 8 + 4 + 8 + 1),  # sort word + len + ts in, mark out
-    "k_fill_scatter": ("ip_packet", 1 + 8 + 1),  # mark + sort word in, verdict out
+    # 64-B header record + len + ts in, verdict byte out (the sort word is implementation)
+    "k_parse": {"unit": "packet", "algo": 77, "impl": 64 + 4 + 8 + 8 + 1},
+    "k_tile_scatter": {"unit": "ip_packet", "algo": 0, "impl": 33},
+    "k_flow_features": {"unit": "ip_packet", "algo": 0, "impl": 8 + 4 + 8},
+    "k_score": {"unit": "flow", "algo": 37, "impl": 37},
 }
+PKT_ALGO_BYTES = 77        # SURVEY §8 d: 76 B in + 1 B verdict
+SRC_ALGO_BYTES = 64        # per distinct source per batch: 32 B state read + 32 B written
+FLOW_ALGO_BYTES = 32 + 4 + 1   # 8 fp32 features in, fp32 p + u8 decision out
 
 
 def parse_args():
@@ -58,11 +64,11 @@ def parse_args():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", type=int, default=2)
     ap.add_argument("--packets", type=int, default=None, help="packets per rank (default: config)")
-    ap.add_argument("--cpu-sample", type=int, default=64 << 20,
-                    help="packets of the CPU baseline sample (default: the whole config-2 stream)")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=None,
+                    help="oracle / torch threads of the CPU baseline (default: the cores this "
+                         "process may use: affinity, cgroup quota, OMP_NUM_THREADS)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--check", action="store_true", help="verify a prefix against the oracle")
+    ap.add_argument("--no-check", action="store_true", help="skip the full-size parity checks")
     ap.add_argument("--no-mlp", action="store_true", help="verdicts only (no features/scores)")
     ap.add_argument("--no-reset", action="store_true",
                     help="diagnostics: keep the maps between steps (state carries over)")
@@ -73,15 +79,116 @@ def parse_args():
                     help="N>1 collectives: nccl (RCCL over xGMI) or gloo (rehearsal on one GPU)")
     ap.add_argument("--limiter", choices=["fixed", "sliding", "token"], default="fixed",
                     help="limiter of the timed main loop (diagnostics; the headline is fixed)")
-    ap.add_argument("--rule-steps", type=int, default=5,
-                    help="steps of the prefix-blocklist leg (64K rules; 0 skips it)")
-    ap.add_argument("--limiter-steps", type=int, default=5,
-                    help="timed steps of the sliding-window and token-bucket legs (0: skip)")
+    ap.add_argument("--legs", default="limiters,rules,warm,config3,config4,config5",
+                    help="comma-separated extra legs ('' for none)")
+    ap.add_argument("--leg-steps", type=int, default=5, help="timed steps per leg")
+    ap.add_argument("--config5-packets", type=int, default=1 << 28)
+    ap.add_argument("--leg-timing", action="store_true",
+                    help="per-kernel device times of the config-4 / config-5 legs (extra steps)")
+    ap.add_argument("--config5-oracle", action="store_true",
+                    help="also check the full config-5 leg against the sharded oracle (slow)")
     return ap.parse_args()
+
+
+def cpu_cores() -> tuple[int, dict]:
+    """Threads the CPU baseline may use on this host: the affinity mask, bounded by the
+    cgroup CPU quota and by OMP_NUM_THREADS (the GPU box's CPU share) when set."""
+    vis = len(os.sched_getaffinity(0))
+    n, why = vis, {"affinity": vis}
+    try:
+        q, per = Path("/sys/fs/cgroup/cpu.max").read_text().split()[:2]
+        if q != "max":
+            why["cgroup_quota"] = int(q) / int(per)
+            n = min(n, max(1, math.ceil(int(q) / int(per))))
+    except (OSError, ValueError):
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        why["OMP_NUM_THREADS"] = int(omp)
+        n = min(n, int(omp))
+    return n, why
+
+
+class Timer:
+    """Device time of work enqueued on one torch stream (HIP events on that stream)."""
+
+    def __init__(self, torch, stream):
+        self.torch, self.stream, self.ms = torch, stream, []
+
+    def __enter__(self):
+        self.e0 = self.torch.cuda.Event(enable_timing=True)
+        self.e1 = self.torch.cuda.Event(enable_timing=True)
+        self.e0.record(self.stream)
+        return self
+
+    def __exit__(self, *exc):
+        self.e1.record(self.stream)
+
+    def done(self):
+        self.stream.synchronize()
+        return self.e0.elapsed_time(self.e1)
+
+
+def gen_stream(torch, synth, p, zipf_s, j0s, n, bounds=None):
+    """Device buffers of n packets: pieces [bounds[i], bounds[i+1]) from stream index j0s[i]."""
+    d = dict(hdr=torch.empty(n * 64, dtype=torch.uint8, device="cuda"),
+             len=torch.empty(n, dtype=torch.int32, device="cuda"),
+             ts=torch.empty(n, dtype=torch.int64, device="cuda"),
+             v=torch.empty(n, dtype=torch.uint8, device="cuda"))
+    bounds = bounds or [0, n]
+    for i, j0 in enumerate(j0s):
+        a, b = bounds[i], bounds[i + 1]
+        synth.generate_device(p, zipf_s, j0, b - a, d["hdr"].data_ptr() + a * 64,
+                              d["len"].data_ptr() + a * 4, d["ts"].data_ptr() + a * 8)
+    torch.cuda.synchronize()
+    return d
+
+
+def host_inputs(d, n):
+    import numpy as np
+    return (d["hdr"][: n * 64].cpu().numpy().reshape(n, 64), d["len"][:n].cpu().numpy().view(np.uint32),
+            d["ts"][:n].cpu().numpy().view(np.uint64))
+
+
+def compare_state(ctx, orc, maps) -> dict:
+    """stats_map + every map entry of the GPU context against the sharded oracle."""
+    from oracle import pyoracle
+    out = {"stats_equal": ctx.stats() == orc.stats()}
+    ok = True
+    for m in maps:
+        g, r = ctx.map_arrays(m), orc.map_arrays(m)
+        same = g[0].shape[0] == r[0].shape[0] and pyoracle.same_map(g, r)
+        out[f"map{m}_entries"] = int(g[0].shape[0])
+        ok = ok and same
+    out["maps_equal"] = ok
+    return out
+
+
+def check_flows(d_keys, d_fam, d_feat, d_prob, m, hdr, ln, ts, model) -> dict:
+    """Per-source features (bit-exact) and q8 scores of the step against the oracle."""
+    import numpy as np
+    from oracle import pyoracle
+    kg = d_keys[: m * 16].cpu().numpy().reshape(m, 16)
+    fg = d_fam[:m].cpu().numpy()
+    xg = d_feat[: m * 8].cpu().numpy().reshape(m, 8)
+    pg = d_prob[:m].cpu().numpy()
+    ko, fo, xo = pyoracle.flow_features(hdr, ln, ts, max_sources=max(m, 1))
+    if len(fo) != m:
+        return {"sources_equal": False}
+
+    def order(k, f):
+        kk = np.concatenate([f.reshape(-1, 1), k], axis=1)
+        return np.lexsort(kk.T[::-1])
+    og, oo = order(kg, fg), order(ko, fo)
+    po, _, _ = pyoracle.score(model, xo[oo])
+    return {"sources_equal": bool(np.array_equal(kg[og], ko[oo]) and np.array_equal(fg[og], fo[oo])),
+            "features_equal": bool(np.array_equal(xg[og].view(np.uint32), xo[oo].view(np.uint32))),
+            "prob_equal": bool(np.array_equal(pg[og].view(np.uint32), po.view(np.uint32)))}
 
 
 def main():
     args = parse_args()
+    import numpy as np
     import torch
 
     rank = int(os.environ.get("RANK", 0))
@@ -96,221 +203,381 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(args.dist_backend)
+    cores, cores_why = cpu_cores()
+    if args.cpu_threads:
+        cores = args.cpu_threads
+    legs = {x for x in args.legs.split(",") if x}
 
-    from flowsentryx_amd import lib, synth
+    from flowsentryx_amd import fsx_load, lib, synth
+    model_json = ROOT / "tests" / "golden" / "model_weights.json"
+    model = fsx_load.load_weights(model_json)
+    model_fields = json.loads(model_json.read_text())
 
-    p, zipf_s = synth.config_params(args.config, n=args.packets)
-    n = int(p.n)
-    # weak scaling: ONE stream of world*n packets at the config's packet rate (so
-    # world times as long) from one source population; rank r holds the contiguous
-    # slice [r*n, (r+1)*n) and the sources are hash-sharded over the ranks (RCCL
-    # all-to-all to their owners, flowsentryx_amd/shard.py)
-    p.n = n * world
-    p.duration_ns = p.duration_ns * world
-    d_hdr = torch.empty(n * 64, dtype=torch.uint8, device="cuda")
-    d_len = torch.empty(n, dtype=torch.int32, device="cuda")
-    d_ts = torch.empty(n, dtype=torch.int64, device="cuda")
-    d_v = torch.empty(n, dtype=torch.uint8, device="cuda")
-    # N>1: the stream in world*chunks pieces of n/chunks packets, piece j on rank j % world
-    # (sub-batch j // world): rank r's slice is its pieces r, r+world, ... in order
-    chunks = max(1, args.chunks) if world > 1 else 1
-    bounds = [n * i // chunks for i in range(chunks + 1)]
-    for i in range(chunks):
-        a, b = bounds[i], bounds[i + 1]
-        j0 = world * a + rank * (b - a)
-        synth.generate_device(p, zipf_s, j0, b - a, d_hdr.data_ptr() + a * 64,
-                              d_len.data_ptr() + a * 4, d_ts.data_ptr() + a * 8)
-    torch.cuda.synchronize()
-    p.n = n
-    p.duration_ns = p.duration_ns // world
+    def barrier():
+        if dist:
+            dist.barrier()
 
-    max_entries = max(1024, int(p.n_ips) if p.n_ips else n)
-    lim_id = {"fixed": lib.LIMIT_FIXED_WINDOW, "sliding": lib.LIMIT_SLIDING_WINDOW,
-              "token": lib.LIMIT_TOKEN_BUCKET}[args.limiter]
-    ctx = lib.FsxContext(max_batch=n, max_entries=max_entries, device=local, limiter=lim_id)
-    from flowsentryx_amd import fsx_load
-    ctx.load_q8_model(fsx_load.load_weights(ROOT / "tests" / "golden" / "model_weights.json"))
-    fcap = max_entries
-    d_keys = torch.empty(fcap * 16, dtype=torch.uint8, device="cuda")
-    d_fam = torch.empty(fcap, dtype=torch.uint8, device="cuda")
-    d_prob = torch.empty(fcap, dtype=torch.float32, device="cuda")
-    d_dec = torch.empty(fcap, dtype=torch.uint8, device="cuda")
-
-    plane = None
-    if world > 1:
-        from flowsentryx_amd.shard import HipShardEngine, ShardedDataPlane
-        eng = HipShardEngine(ctx, n, torch.device("cuda", local))
-        if not args.no_mlp:
-            eng.enable_flows(fcap)
-        plane = ShardedDataPlane(eng)
-
-    def step():
-        if not args.no_reset:
-            ctx.reset()
-        if plane is not None:
-            plane.reset()
-            plane.verdict_batch(d_hdr, d_len, d_ts, n, d_v, bounds=bounds, chunks=chunks)
-        elif args.no_mlp:
-            ctx.verdict_batch_device(d_hdr.data_ptr(), d_len.data_ptr(), d_ts.data_ptr(), n,
-                                     d_v.data_ptr())
-        else:
-            ctx.process_batch_device(d_hdr.data_ptr(), d_len.data_ptr(), d_ts.data_ptr(), n,
-                                     d_v.data_ptr(), d_keys.data_ptr(), d_fam.data_ptr(), None,
-                                     d_prob.data_ptr(), d_dec.data_ptr(), fcap)
-
-    for _ in range(args.warmup):
-        step()
-    ctx.sync()
-    info = ctx.last_batch_info()
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    ctx.sync()
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    # per-kernel device times (a HIP event after every kernel) from separate steps, so the
-    # timed steps above carry no event records
-    ctx.enable_timing(True)
-    ctx.last_timings()  # reset accumulators
-    for _ in range(max(1, min(args.steps, 5))):
-        step()
-    ctx.sync()
-    torch.cuda.synchronize()
-    timings = ctx.last_timings()
-    ctx.enable_timing(False)
-    if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64,
-                         device="cuda" if args.dist_backend == "nccl" else "cpu")
+    def max_over_ranks(x: float) -> float:
+        if not dist:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device="cuda" if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    exchange = None
-    if plane is not None:
-        stats = plane.stats()
-        ex = plane.last_exchange or {"sent": [], "received": []}
-        exchange = {"records_sent": ex["sent"], "records_received": ex["received"],
-                    "dropped_by_replica": ex.get("filtered", 0), "sub_batches": chunks,
-                    "record_bytes": sorted(plane.formats) or None, "backend": args.dist_backend}
-        malicious = None
-        if not args.no_mlp:
-            fl = eng.flows
-            mal = torch.tensor([int(fl["dec"][:info["sources"]].sum().item())], device="cuda")
-            if args.dist_backend == "gloo":
-                mal = mal.cpu()
-            dist.all_reduce(mal)
-            malicious = int(mal.item())
-    else:
-        stats = ctx.stats()
-        malicious = None if args.no_mlp else int(d_dec[:info["sources"]].sum().item())
-    ctx.close()
+        return float(t.item())
 
-    # BASELINE config 2 also names the sliding-window and token-bucket limiters
-    # (build-defined): the same batch through each, verdicts + maps only
-    limiters = {}
-    if args.limiter_steps > 0 and world == 1:
-        for lname, lid in (("sliding_window", lib.LIMIT_SLIDING_WINDOW),
-                           ("token_bucket", lib.LIMIT_TOKEN_BUCKET)):
-            with lib.FsxContext(max_batch=n, max_entries=max_entries, device=local,
-                                limiter=lid) as lc:
+    def sum_over_ranks(x: int) -> int:
+        if not dist:
+            return x
+        t = torch.tensor([x], dtype=torch.int64, device="cuda" if args.dist_backend == "nccl" else "cpu")
+        dist.all_reduce(t)
+        return int(t.item())
+
+    # ------------------------------------------------------------------ workload runner
+    def run_workload(cfg_no, n, steps, warmup, with_flows, kernel_timing=False, check=False,
+                     cpu=False):
+        """Weak-scaled config cfg_no (n packets per rank), full pipeline; returns a dict."""
+        p, zipf_s = synth.config_params(cfg_no, n=None if cfg_no == 4 else n)
+        # ONE stream of world*n packets at the config's packet rate from one population
+        # (config 4: the 1B-packet stream itself, rank r's share of n packets); in
+        # world*chunks pieces of n/chunks packets, piece j on rank j % world
+        chunks = max(1, args.chunks) if world > 1 else 1
+        bounds = [n * i // chunks for i in range(chunks + 1)]
+        if cfg_no != 4:
+            p.n = n * world
+            p.duration_ns = p.duration_ns * world
+        j0s = [world * bounds[i] + rank * (bounds[i + 1] - bounds[i]) for i in range(chunks)]
+        d = gen_stream(torch, synth, p, zipf_s, j0s, n, bounds)
+        max_entries = max(1024, int(p.n_ips) if p.n_ips else n * world)
+        lim_id = {"fixed": lib.LIMIT_FIXED_WINDOW, "sliding": lib.LIMIT_SLIDING_WINDOW,
+                  "token": lib.LIMIT_TOKEN_BUCKET}[args.limiter]
+        ctx = lib.FsxContext(max_batch=n, max_entries=max_entries, device=local, limiter=lim_id)
+        ctx.load_q8_model(model)
+        fcap = max_entries
+        fl = dict(keys=torch.empty(fcap * 16, dtype=torch.uint8, device="cuda"),
+                  fam=torch.empty(fcap, dtype=torch.uint8, device="cuda"),
+                  feat=torch.empty(fcap * 8, dtype=torch.float32, device="cuda"),
+                  prob=torch.empty(fcap, dtype=torch.float32, device="cuda"),
+                  dec=torch.empty(fcap, dtype=torch.uint8, device="cuda"))
+        plane = eng = None
+        if world > 1:
+            from flowsentryx_amd.shard import HipShardEngine, ShardedDataPlane
+            eng = HipShardEngine(ctx, n, torch.device("cuda", local))
+            if with_flows:
+                eng.enable_flows(fcap)
+            plane = ShardedDataPlane(eng)
+        ptr = {k: v.data_ptr() for k, v in d.items()}
+
+        def step(feat=False):
+            if not args.no_reset:
+                ctx.reset()
+            if plane is not None:
+                plane.reset()
+                plane.verdict_batch(d["hdr"], d["len"], d["ts"], n, d["v"], bounds=bounds, chunks=chunks)
+            elif not with_flows:
+                ctx.verdict_batch_device(ptr["hdr"], ptr["len"], ptr["ts"], n, ptr["v"])
+            else:
+                ctx.process_batch_device(ptr["hdr"], ptr["len"], ptr["ts"], n, ptr["v"],
+                                         fl["keys"].data_ptr(), fl["fam"].data_ptr(),
+                                         fl["feat"].data_ptr() if feat else None,
+                                         fl["prob"].data_ptr(), fl["dec"].data_ptr(), fcap)
+
+        for _ in range(warmup):
+            step()
+        ctx.sync()
+        torch.cuda.synchronize()
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        ctx.sync()
+        torch.cuda.synchronize()
+        barrier()
+        elapsed = max_over_ranks(time.perf_counter() - t0)
+        out = {"n": n, "p": p, "steps": steps, "elapsed": elapsed, "max_entries": max_entries,
+               "mpps": n * world * steps / elapsed / 1e6, "ms_step": elapsed / steps * 1e3}
+        info = ctx.last_batch_info()
+        if kernel_timing:
+            # per-kernel device times (a HIP event after every kernel) from separate
+            # steps, so the timed steps above carry no event records
+            ctx.enable_timing(True)
+            ctx.last_timings()
+            for _ in range(max(1, min(steps, 5))):
+                step()
+            ctx.sync()
+            torch.cuda.synchronize()
+            out["timings"] = ctx.last_timings()
+            ctx.enable_timing(False)
+        if plane is not None:
+            ex = plane.last_exchange or {"sent": [], "received": []}
+            out["exchange"] = {"records_sent": ex["sent"], "records_received": ex["received"],
+                               "dropped_by_replica": ex.get("filtered", 0), "sub_batches": chunks,
+                               "record_bytes": sorted(plane.formats) or None,
+                               "backend": args.dist_backend}
+            out["stats"] = plane.stats()
+            out["sources"] = None   # per-owner chunks; see the exchange counts
+        else:
+            out["stats"] = ctx.stats()
+            out["sources"] = info["sources"]
+            out["info"] = info
+            if with_flows:
+                out["malicious_sources"] = int(fl["dec"][:info["sources"]].sum().item())
+        if (check or cpu) and world == 1:
+            # one more step, with the features written, then the CPU oracle on the same
+            # input bytes (the device generator is checked equal to the CPU twin by
+            # tests/test_gpu_parity.py::test_device_synth_and_device_batch)
+            ctx.reset()
+            step(feat=True)
+            ctx.sync()
+            hdr, ln, ts = host_inputs(d, n)
+            vg = d["v"].cpu().numpy()
+            from oracle import pyoracle
+            orc = pyoracle.ShardedOracle(cores, max_entries=max_entries)
+            c0 = time.perf_counter()
+            vo = orc.batch(hdr, ln, ts)
+            cdt = time.perf_counter() - c0
+            out["cpu"] = {"value": round(n / cdt / 1e6, 3), "unit": "Mpps", "seconds": round(cdt, 3)}
+            if check:
+                chk = {"packets": n, "verdicts_equal": bool(np.array_equal(vg, vo))}
+                chk.update(compare_state(ctx, orc, (1, 2, 3, 4)))
+                if with_flows:
+                    chk["flows"] = check_flows(fl["keys"], fl["fam"], fl["feat"], fl["prob"],
+                                               ctx.last_batch_info()["sources"], hdr, ln, ts, model_fields)
+                out["check"] = chk
+            orc.close()
+            del hdr, ln, ts
+        ctx.close()
+        out["d"] = d
+        return out
+
+    # ------------------------------------------------------------------ headline
+    n_head = args.packets or int(synth.config_params(args.config)[0].n)
+    head = run_workload(args.config, n_head, args.steps, args.warmup, not args.no_mlp,
+                        kernel_timing=True, check=not args.no_check and world == 1,
+                        cpu=not args.no_cpu_baseline and world == 1)
+    n = head["n"]
+    p = head["p"]
+    timings = head.get("timings", [])
+
+    results = {}
+    # ------------------------------------------------------------------ legs (N=1)
+    d = head.pop("d")
+    if world == 1 and "limiters" in legs:
+        res = {}
+        for lname, lid, extra in (("sliding_window", lib.LIMIT_SLIDING_WINDOW, {}),
+                                  ("token_bucket", lib.LIMIT_TOKEN_BUCKET, {})):
+            with lib.FsxContext(max_batch=n, max_entries=head["max_entries"], device=local,
+                                limiter=lid, **extra) as lc:
                 def lstep():
                     lc.reset()
-                    lc.verdict_batch_device(d_hdr.data_ptr(), d_len.data_ptr(), d_ts.data_ptr(), n,
-                                            d_v.data_ptr())
+                    lc.verdict_batch_device(d["hdr"].data_ptr(), d["len"].data_ptr(), d["ts"].data_ptr(),
+                                            n, d["v"].data_ptr())
                 lstep()
                 lc.sync()
                 torch.cuda.synchronize()
-                if dist:
-                    dist.barrier()
                 l0 = time.perf_counter()
-                for _ in range(args.limiter_steps):
+                for _ in range(args.leg_steps):
                     lstep()
                 lc.sync()
                 torch.cuda.synchronize()
-                if dist:
-                    dist.barrier()
                 lt = time.perf_counter() - l0
-                if dist:
-                    t = torch.tensor([lt], dtype=torch.float64,
-                                     device="cuda" if args.dist_backend == "nccl" else "cpu")
-                    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-                    lt = float(t.item())
                 la, ld = lc.stats()
-                limiters[lname] = {"value": round(n * world * args.limiter_steps / lt / 1e6, 2),
-                                   "unit": "Mpps", "ms_per_step": round(lt / args.limiter_steps * 1e3, 4),
-                                   "steps": args.limiter_steps, "allowed": la, "dropped": ld}
+                r = {"value": round(n * args.leg_steps / lt / 1e6, 2), "unit": "Mpps",
+                     "ms_per_step": round(lt / args.leg_steps * 1e3, 4), "steps": args.leg_steps,
+                     "allowed": la, "dropped": ld}
+                if not args.no_check:
+                    from oracle import pyoracle
+                    hdr, ln, ts = host_inputs(d, n)
+                    orc = pyoracle.ShardedOracle(cores, max_entries=head["max_entries"], limiter=lid)
+                    vo = orc.batch(hdr, ln, ts)
+                    r["check"] = {"packets": n, "verdicts_equal": bool(np.array_equal(d["v"].cpu().numpy(), vo))}
+                    r["check"].update(compare_state(lc, orc, (3, 4, 5, 6) if lid == 2 else (1, 2, 3, 4)))
+                    orc.close()
+                    del hdr, ln, ts
+                res[lname] = r
+        results["limiters"] = res
 
-    # prefix blocklists (SURVEY §8 f row 4): the same batch with a 64K-rule
-    # table — 61440 random /24 prefixes (mostly missing the stream) and 4096 rules on the
-    # stream's own sources (/32 and /28, permanent) — fixed window, verdicts + maps
-    rules_leg = None
-    if args.rule_steps > 0 and world == 1:
-        import numpy as np
+    if world == 1 and "rules" in legs:
+        # prefix blocklists (DESIGN.md §4.3; SURVEY §8 f row 4): the same batch with a 64K-rule
+        # table — 61440 random /24 prefixes (mostly missing the stream) and 4096 rules on
+        # the stream's own sources (/32 and /28, permanent) — fixed window, verdicts + maps
         rng = np.random.default_rng(5)
-        seen = d_hdr[: min(n, 1 << 16) * 64].view(-1, 64)[:, 26:30].cpu().numpy()
-        srcs = np.unique(seen.view(np.uint32).reshape(-1))[:4096]
+        seen = d["hdr"][: min(n, 1 << 16) * 64].view(-1, 64)[:, 26:30].cpu().numpy()
+        srcs = np.unique(seen.copy().view(np.uint32).reshape(-1))[:4096]
         r4 = {}
         for a in rng.integers(0, 2**32, 61440, dtype=np.uint64).astype(np.uint32):
             r4[lib.prefix_key((int(a) & 0xFFFFFF).to_bytes(4, "little"), 24)] = 2**64 - 1
         for i, a in enumerate(srcs):
             r4[lib.prefix_key(int(a).to_bytes(4, "little"), 32 if i & 1 else 28)] = 2**64 - 1
-        with lib.FsxContext(max_batch=n, max_entries=max_entries, device=local) as rc_:
+        with lib.FsxContext(max_batch=n, max_entries=head["max_entries"], device=local) as rc_:
             rc_.map_update_batch(lib.MAP_IPV4_PREFIX, r4)
+
             def rstep():
                 rc_.reset()
-                rc_.verdict_batch_device(d_hdr.data_ptr(), d_len.data_ptr(), d_ts.data_ptr(), n,
-                                         d_v.data_ptr())
+                rc_.verdict_batch_device(d["hdr"].data_ptr(), d["len"].data_ptr(), d["ts"].data_ptr(), n,
+                                         d["v"].data_ptr())
             rstep()
             rc_.sync()
             torch.cuda.synchronize()
             r0 = time.perf_counter()
-            for _ in range(args.rule_steps):
+            for _ in range(args.leg_steps):
                 rstep()
             rc_.sync()
             torch.cuda.synchronize()
             rt = time.perf_counter() - r0
             ri = rc_.last_batch_info()
             ra, rd = rc_.stats()
-        rules_leg = {"value": round(n * args.rule_steps / rt / 1e6, 2), "unit": "Mpps",
-                     "ms_per_step": round(rt / args.rule_steps * 1e3, 4), "steps": args.rule_steps,
-                     "rules": len(r4), "prefix_lengths": [24, 28, 32],
-                     "rule_drops": ri["prefix_rule_drops"], "allowed": ra, "dropped": rd}
+            leg = {"value": round(n * args.leg_steps / rt / 1e6, 2), "unit": "Mpps",
+                   "ms_per_step": round(rt / args.leg_steps * 1e3, 4), "steps": args.leg_steps,
+                   "rules": len(r4), "prefix_lengths": [24, 28, 32],
+                   "rule_drops": ri["prefix_rule_drops"], "allowed": ra, "dropped": rd}
+            if not args.no_check:
+                from oracle import pyoracle
+                hdr, ln, ts = host_inputs(d, n)
+                orc = pyoracle.ShardedOracle(cores, max_entries=head["max_entries"])
+                for k, v in r4.items():
+                    orc.map_update(lib.MAP_IPV4_PREFIX, k, v)
+                vo = orc.batch(hdr, ln, ts)
+                leg["check"] = {"packets": n, "verdicts_equal": bool(np.array_equal(d["v"].cpu().numpy(), vo))}
+                leg["check"].update(compare_state(rc_, orc, (1, 3)))
+                orc.close()
+                del hdr, ln, ts
+        results["prefix_rules"] = leg
 
-    check = None
-    if args.check and rank == 0:
-        from oracle import pyoracle
-        m = min(n, 4 << 20)
-        hdr, ln, ts = pyoracle.synth(p, zipf_s, 0, m)
-        o = pyoracle.Oracle(max_entries=max_entries)
-        vo = o.batch(hdr, ln, ts)
-        with lib.FsxContext(max_batch=m, max_entries=max_entries, device=local) as c2:
-            vg = c2.verdict_batch(hdr, ln, ts)
-        check = {"prefix_packets": m, "verdicts_equal": bool((vo == vg).all())}
+    if world == 1 and "warm" in legs:
+        # streaming with the maps carried: step k replays the batch shifted by k stream
+        # durations (heavy sources stay blacklisted across the boundary, windows carry);
+        # device time of each pipeline call between HIP events on its stream, the time
+        # shift of the input (one elementwise kernel) outside the events
+        st = torch.cuda.Stream()   # a real stream (a NULL handle = the context's own stream)
+        with torch.cuda.stream(st), \
+                lib.FsxContext(max_batch=n, max_entries=head["max_entries"], device=local) as wc:
+            wc.load_q8_model(model)
+            wc.set_stream(st.cuda_stream)
+            fcap = head["max_entries"]
+            keys = torch.empty(fcap * 16, dtype=torch.uint8, device="cuda")
+            fam = torch.empty(fcap, dtype=torch.uint8, device="cuda")
+            prob = torch.empty(fcap, dtype=torch.float32, device="cuda")
+            dec = torch.empty(fcap, dtype=torch.uint8, device="cuda")
+            ts0 = d["ts"].clone()
+            ms = []
+            for k in range(args.leg_steps + 1):
+                if k:
+                    d["ts"].add_(int(p.duration_ns))
+                with Timer(torch, st) as tmr:
+                    wc.process_batch_device(d["hdr"].data_ptr(), d["len"].data_ptr(), d["ts"].data_ptr(), n,
+                                            d["v"].data_ptr(), keys.data_ptr(), fam.data_ptr(), None,
+                                            prob.data_ptr(), dec.data_ptr(), fcap)
+                wc.sync()
+                if k:   # step 0 fills the maps from empty
+                    ms.append(tmr.done())
+            wi = wc.last_batch_info()
+            wa, wd = wc.stats()
+            d["ts"].copy_(ts0)
+            del ts0
+            wc.set_stream(None)
+        wms = sum(ms) / len(ms)
+        results["warm"] = {"value": round(n / wms / 1e3, 2), "unit": "Mpps", "ms_per_step": round(wms, 4),
+                           "steps": len(ms), "new_sources_last_step": wi["new_sources"],
+                           "sources": wi["sources"], "allowed": wa, "dropped": wd,
+                           "note": "maps carried: step k = the batch shifted by k x 30 s"}
+
+    del d
+    torch.cuda.empty_cache()
+
+    if world == 1 and "config3" in legs:
+        # BASELINE config 3: q8 scoring of 4M per-IP flows (fsx_score_device), inputs in HBM
+        from oracle import torch_model
+        nf = 4 << 20
+        x = torch_model.config3_features(nf)
+        dx = torch.from_numpy(x).cuda()
+        dp = torch.empty(nf, dtype=torch.float32, device="cuda")
+        dd = torch.empty(nf, dtype=torch.uint8, device="cuda")
+        st = torch.cuda.Stream()
+        with torch.cuda.stream(st), lib.FsxContext(max_batch=1024, max_entries=1024, device=local) as sc_:
+            sc_.load_q8_model(model)
+            sc_.set_stream(st.cuda_stream)
+            sc_.score_device(dx.data_ptr(), nf, dp.data_ptr(), dd.data_ptr())
+            reps = 50
+            with Timer(torch, st) as tmr:
+                for _ in range(reps):
+                    sc_.score_device(dx.data_ptr(), nf, dp.data_ptr(), dd.data_ptr())
+            sms = tmr.done() / reps
+            sc_.set_stream(None)
+        leg = {"flows": nf, "value": round(nf / sms / 1e3, 1), "unit": "Mflows/s",
+               "ms_per_launch": round(sms, 5),
+               "roofline": {"bound": "hbm", "kernel": "k_score", "bytes_per_flow": FLOW_ALGO_BYTES,
+                            "achieved": round(nf * FLOW_ALGO_BYTES / (sms * 1e-3) / 1e9, 1),
+                            "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                            "frac": round(nf * FLOW_ALGO_BYTES / (sms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
+               "features": "synthetic, uniform over the CICIDS ranges + boundary grid "
+                           "(oracle/torch_model.py config3_features)"}
+        if not args.no_cpu_baseline or not args.no_check:
+            mq = torch_model.build(model_fields)
+            nth = torch.get_num_threads()
+            torch.set_num_threads(cores)
+            pt = torch_model.score(mq, x)   # (warm-up + the checker's output)
+            best = None
+            for _ in range(3):
+                c0 = time.perf_counter()
+                torch_model.score(mq, x)
+                dt = time.perf_counter() - c0
+                best = dt if best is None else min(best, dt)
+            torch.set_num_threads(nth)
+            leg["cpu_torch"] = {"value": round(nf / best / 1e6, 2), "unit": "Mflows/s", "cores": cores,
+                                "seconds": round(best, 4)}
+            pg = dp.cpu().numpy()
+            leg["check"] = {"flows": nf, "prob_equal_torch": bool(np.array_equal(pg.view(np.uint32), pt.view(np.uint32))),
+                            "decision_equal_torch": bool(np.array_equal(dd.cpu().numpy(), (pt > 0.5).astype(np.uint8)))}
+        results["config3"] = leg
+        del dx, dp, dd, x
+
+    if "config4" in legs:
+        # BASELINE config 4: the 1B-packet / 16M-source flood over 120 s; rank r holds the
+        # r-th 1/8 share of the stream (weak scaling: at N = 8 the whole of config 4)
+        p4, _ = synth.config_params(4)
+        n4 = int(p4.n) // 8
+        r4 = run_workload(4, n4, max(1, args.leg_steps // 2), 1, not args.no_mlp,
+                          kernel_timing=args.leg_timing, check=not args.no_check and world == 1)
+        r4.pop("d")
+        torch.cuda.empty_cache()
+        leg = {"value": round(r4["mpps"], 2), "unit": "Mpps", "ms_per_step": round(r4["ms_step"], 4),
+               "steps": r4["steps"], "packets_per_gpu": n4, "n_gpus": world,
+               "packets_total": n4 * world, "source_population": int(p4.n_ips),
+               "sources": r4["sources"], "allowed": r4["stats"][0], "dropped": r4["stats"][1],
+               "stream": f"packets [r*{n4}, (r+1)*{n4}) of the config-4 stream per rank r"
+                         if world == 1 else f"{world} x {n4} packets of the config-4 stream"}
+        if r4["sources"]:
+            algo = PKT_ALGO_BYTES * n4 + SRC_ALGO_BYTES * r4["sources"]
+            leg["pipeline_frac"] = round(algo / (r4["ms_step"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+        if "check" in r4:
+            leg["check"] = r4["check"]
+        if "cpu" in r4:
+            leg["cpu_oracle"] = dict(r4["cpu"], cores=cores)
+        if r4.get("timings"):
+            leg["kernels"] = [{"name": a, "ms_per_step": round(b, 4), "launches": c} for a, b, c in r4["timings"]]
+        results["config4"] = leg
+
+    if world == 1 and "config5" in legs:
+        results["config5"] = config5_leg(args, torch, np, lib, synth, local, cores)
 
     if rank != 0:
+        barrier()
         if dist:
-            dist.barrier()
             dist.destroy_process_group()
         return
 
-    total = n * world * args.steps
-    mpps = total / elapsed / 1e6
-    ms_step = elapsed / args.steps * 1e3
-    ip_packets, sources = info["ip_packets"], info["sources"]
-
-    # dominant kernel: largest device time per step
+    # ------------------------------------------------------------------ report
+    ms_step = head["ms_step"]
+    sources = head["sources"]
+    info = head.get("info", {})
     dom = max(timings, key=lambda r: r[1]) if timings else None
     roofline = None
     if dom:
         name, ms_per_batch, launches = dom
-        unit, per = KERNEL_BYTES.get(name, ("packet", 0))
-        units = n if unit == "packet" else ip_packets
+        kb = KERNEL_BYTES.get(name, {"unit": "packet", "algo": 0, "impl": 0})
+        units = n if kb["unit"] == "packet" else info.get("ip_packets", n)
         per_launch_ms = ms_per_batch / max(launches, 1e-9)
-        bytes_per_launch = per * units
-        achieved = bytes_per_launch / (per_launch_ms * 1e-3) / 1e9 if per else None
+        bytes_per_launch = kb["algo"] * units
+        achieved = bytes_per_launch / (per_launch_ms * 1e-3) / 1e9 if kb["algo"] else None
         traffic = None
         pmc = ROOT / "profiles" / "pmc_traffic.json"
         if pmc.exists():
@@ -322,56 +589,192 @@ def main():
             "bound": "hbm", "kernel": name, "achieved": round(achieved, 1) if achieved else None,
             "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
-            "traffic": traffic, "bytes_per_launch": bytes_per_launch,
+            "traffic": traffic, "bytes_per_unit": kb["algo"], "unit_of_work": kb["unit"],
+            "impl_bytes_per_unit": kb["impl"], "bytes_per_launch": bytes_per_launch,
             "launch_ms": round(per_launch_ms, 4), "launches_per_step": launches,
+            "traffic_source": "profiles/pmc_traffic.json (rocprofv3 PMC passes, FETCH_SIZE x2 + WRITE_SIZE)"
+            if traffic else None,
         }
-    algo = 77 * n + 64 * sources
-    pipe_gbs = algo / (ms_step * 1e-3) / 1e9
-    pipeline = {"bound": "hbm", "algorithmic_bytes_per_step": algo,
-                "achieved": round(pipe_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(pipe_gbs / HBM_PEAK_GBS, 4)}
+    pipeline = None
+    if sources:
+        algo = PKT_ALGO_BYTES * n + SRC_ALGO_BYTES * sources
+        pipe_gbs = algo / (ms_step * 1e-3) / 1e9
+        pipeline = {"bound": "hbm", "algorithmic_bytes_per_step": algo, "achieved": round(pipe_gbs, 1),
+                    "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(pipe_gbs / HBM_PEAK_GBS, 4)}
 
     cpu = None
-    if not args.no_cpu_baseline and world == 1:
-        from oracle import pyoracle
-        m = min(n, args.cpu_sample)
-        hdr, ln, ts = pyoracle.synth(p, zipf_s, 0, m)
-        th = args.cpu_threads
-        c0 = time.perf_counter()
-        _, _ = pyoracle.batch_sharded(hdr, ln, ts, th, max_entries=max_entries)
-        cdt = time.perf_counter() - c0
-        cpu = {"value": round(m / cdt / 1e6, 3), "unit": "Mpps", "cores": th, "kind": "port",
-               "sample": f"first {m} packets of the config-{args.config} stream, fixed window, "
-                         f"oracle/fsx_oracle.c sharded by source over {th} threads "
-                         f"({cdt:.2f} s)"}
+    if "cpu" in head:
+        cpu = {"value": head["cpu"]["value"], "unit": "Mpps", "cores": cores, "cores_detail": cores_why,
+               "kind": "port",
+               "sample": f"the whole config-{args.config} stream ({n} packets), fixed window: "
+                         f"oracle/fsx_oracle.c (the reference's fsx() restated) sharded by source over "
+                         f"{cores} threads ({head['cpu']['seconds']} s)"}
+        if "config3" in results and "cpu_torch" in results["config3"]:
+            cpu["scoring"] = dict(results["config3"]["cpu_torch"], kind="reference",
+                                  sample="config 3: 4M flows x 8 fp32 through the converted "
+                                         "model/model.py:124-137 module (torch x86 engine)")
 
     out = {
         "metric": "Mpps verdicts (parse+rate-limit+MLP) at 1/2/4/8 GPUs; % of HBM BW peak",
-        "value": round(mpps, 2), "unit": "Mpps", "n_gpus": world, "steps": args.steps,
+        "value": round(head["mpps"], 2), "unit": "Mpps", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms_step, 4), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "u64",
         "data": "synthetic (counter-based generator, fsx_synth_common.h)",
         "config": {"workload": f"BASELINE config {args.config}: {n} IPv4/UDP packets per GPU, "
                                f"{p.n_ips} Zipf(1.1) sources, {p.duration_ns / 1e9:g} s; "
                                "fixed-window limiter (src/fsx_kern.c), maps reset each step"
-                               + ("; sliding-window and token-bucket legs timed separately "
-                                  "(limiters)" if args.limiter_steps > 0 else "")
                                + ("" if args.no_mlp else "; per-source features + q8 MLP score "
                                   "(model_weights.pth)"),
                    "packets_per_gpu": n, "sources": sources,
-                   "parallelism": f"dp{world}" + ("" if world == 1 else
-                                                  " (sources hash-sharded, all-to-all)")},
+                   "parallelism": f"dp{world}" + ("" if world == 1 else " (sources hash-sharded, all-to-all)")},
         "roofline": roofline, "pipeline": pipeline, "cpu_baseline": cpu,
-        "limiters": limiters or None, "prefix_rules": rules_leg, "exchange": exchange,
+        "check": head.get("check"),
+        "limiters": results.get("limiters"), "prefix_rules": results.get("prefix_rules"),
+        "warm": results.get("warm"), "config3": results.get("config3"),
+        "config4": results.get("config4"), "config5": results.get("config5"),
+        "exchange": head.get("exchange"),
         "kernels": [{"name": a, "ms_per_step": round(b, 4), "launches": c} for a, b, c in timings],
-        "stats": {"allowed": stats[0], "dropped": stats[1], "sources": info["sources"],
-                  "light_packets": info["light_packets"], "malicious_sources": malicious},
-        "check": check,
+        "stats": {"allowed": head["stats"][0], "dropped": head["stats"][1], "sources": sources,
+                  "light_packets": info.get("light_packets"),
+                  "malicious_sources": head.get("malicious_sources")},
     }
     print(json.dumps(out), flush=True)
+    barrier()
     if dist:
-        dist.barrier()
         dist.destroy_process_group()
+
+
+def config5_leg(args, torch, np, lib, synth, local, cores):
+    """BASELINE config 5: 2^28 packets, every one a fresh spoofed source (60% IPv4 / 30%
+    IPv6 / 10% 802.1Q-tagged, PASS per parse), plus a 64K-entry rule table: 24K IPv4 and
+    8K IPv6 exact blacklist entries on stream sources (maps 3 / 4, till UINT64_MAX; every
+    8th till 0 = ignored), 30K random IPv4 /24 and 2K IPv6 /48 prefix rules (maps 7 / 8).
+    Step = fsx_reset + batched import of the 32K exact rules + the verdict batch; the
+    prefix rules are configuration (they survive fsx_reset). max_entries = 2^28.
+
+    Check at full size (size-independent properties, recomputed with torch on device):
+    every source occurs once, so the limiter never triggers and a packet is DROP exactly
+    when an exact rule (till > 0) or a prefix rule covers its source: the verdict array,
+    stats_map and the map sizes must equal that. The 2^24 slice is checked bit-exactly
+    against the oracle in tests/test_gpu_scale.py."""
+    n = args.config5_packets
+    p, s = synth.config_params(5, n=n)
+    d = gen_stream(torch, synth, p, s, [0], n)
+    H = d["hdr"].view(n, 64)
+    et = H[:, 12].to(torch.int32) * 256 + H[:, 13].to(torch.int32)
+    is4, is6 = et == 0x0800, et == 0x86DD
+    rng = np.random.default_rng(55)
+    # rules from the stream's sources (first 4M packets)
+    m = min(n, 1 << 22)
+    h0 = H[:m].cpu().numpy()
+    v4 = np.nonzero((h0[:, 12] == 0x08) & (h0[:, 13] == 0))[0]
+    v6 = np.nonzero((h0[:, 12] == 0x86) & (h0[:, 13] == 0xDD))[0]
+    e4 = rng.choice(v4, 24576, replace=False)
+    e6 = rng.choice(v6, 8192, replace=False)
+    k4 = np.ascontiguousarray(h0[e4, 26:30])
+    k6 = np.ascontiguousarray(h0[e6, 22:38])
+    t4 = np.where(np.arange(len(e4)) % 8 == 0, 0, 2**64 - 1).astype(np.uint64)
+    t6 = np.where(np.arange(len(e6)) % 8 == 0, 0, 2**64 - 1).astype(np.uint64)
+    p4 = rng.integers(0, 2**24, 30720, dtype=np.int64)          # /24: first 3 address bytes
+    p6 = np.ascontiguousarray(h0[rng.choice(v6, 2048, replace=False), 22:28])   # /48
+    rules7 = {lib.prefix_key(int(a << 8).to_bytes(4, "big"), 24): 2**64 - 1 for a in p4}
+    rules8 = {lib.prefix_key(bytes(r) + bytes(10), 48): 2**64 - 1 for r in p6}
+    max_entries = 1 << 28
+    with lib.FsxContext(max_batch=n, max_entries=max_entries, device=local) as c:
+        c.map_update_batch(lib.MAP_IPV4_PREFIX, rules7)
+        c.map_update_batch(lib.MAP_IPV6_PREFIX, rules8)
+
+        def step():
+            c.reset()
+            c.map_update_arrays(lib.MAP_IPV4_BLACKLIST, k4, t4)
+            c.map_update_arrays(lib.MAP_IPV6_BLACKLIST, k6, t6)
+            c.verdict_batch_device(d["hdr"].data_ptr(), d["len"].data_ptr(), d["ts"].data_ptr(), n,
+                                   d["v"].data_ptr())
+        step()
+        c.sync()
+        torch.cuda.synchronize()
+        steps = max(1, args.leg_steps // 2)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        c.sync()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        kern = None
+        if args.leg_timing:
+            c.enable_timing(True)
+            c.last_timings()
+            t1 = time.perf_counter()
+            step()
+            c.sync()
+            kern = {"host_ms": round((time.perf_counter() - t1) * 1e3, 3),
+                    "kernels": [{"name": a, "ms_per_step": round(b, 4), "launches": l_}
+                                for a, b, l_ in c.last_timings()]}
+            c.enable_timing(False)
+        info = c.last_batch_info()
+        stats = c.stats()
+        cnt = {m_: c.map_count(m_) for m_ in (1, 2, 3, 4)}
+    # expected verdicts, recomputed on device with torch
+    def be(cols):   # big-endian integer of byte columns
+        v = torch.zeros(n, dtype=torch.int64, device="cuda")
+        for cidx in cols:
+            v = v * 256 + H[:, cidx].to(torch.int64)
+        return v
+    key4 = be(range(26, 30))
+    blk4 = torch.from_numpy(k4[t4 != 0].astype(np.int64) @ np.array([1 << 24, 1 << 16, 1 << 8, 1], np.int64)).cuda()
+    pfx4 = torch.from_numpy(p4).cuda()
+    drop4 = is4 & (torch.isin(key4, blk4) | torch.isin(key4 >> 8, pfx4))
+    del key4
+    id6 = be(range(30, 38))      # the unique 64-bit id part of a carpet IPv6 source
+    hi6 = be(range(22, 30))
+    ids_blk = torch.from_numpy(np.ascontiguousarray(k6[t6 != 0, 8:16]).view(">i8").astype(np.int64).reshape(-1)).cuda()
+    his_blk = torch.from_numpy(np.ascontiguousarray(k6[t6 != 0, 0:8]).view(">i8").astype(np.int64).reshape(-1)).cuda()
+    p48 = torch.from_numpy(np.concatenate([p6, np.zeros((len(p6), 2), np.uint8)], 1).view(">i8").astype(np.int64).reshape(-1)).cuda()
+    ex6 = torch.isin(id6, ids_blk)
+    if ex6.any():   # the id identifies the source; confirm the high half too
+        idx = torch.nonzero(ex6).reshape(-1)
+        pos = torch.searchsorted(torch.sort(ids_blk).values, id6[idx])
+        order = torch.argsort(ids_blk)
+        ex6[idx] = his_blk[order][pos.clamp(max=len(order) - 1)] == hi6[idx]
+    drop6 = is6 & (ex6 | torch.isin(hi6 >> 16, p48 >> 16))
+    del id6, hi6
+    exp = torch.where(drop4 | drop6, 1, 2).to(torch.uint8)
+    ip = int((is4 | is6).sum().item())
+    ndrop = int((drop4 | drop6).sum().item())
+    n4, n6 = int(is4.sum().item()), int(is6.sum().item())
+    check = {"packets": n, "kind": "properties (every source once: DROP iff an exact or prefix rule covers it)",
+             "verdicts_equal": bool(torch.equal(exp, d["v"])),
+             "stats_equal": tuple(stats) == (ip - ndrop, ndrop),
+             "ipv4_stats_entries_equal": cnt[1] == n4 - int(drop4.sum().item()),
+             "ipv6_stats_entries_equal": cnt[2] == n6 - int(drop6.sum().item()),
+             "blacklist_entries_equal": cnt[3] == len(k4) and cnt[4] == len(k6)}
+    leg = {"value": round(n * steps / el / 1e6, 2), "unit": "Mpps", "ms_per_step": round(el / steps * 1e3, 3),
+           "steps": steps, "packets": n, "ipv4": n4, "ipv6": n6, "vlan": n - n4 - n6,
+           "sources": info["sources"], "max_entries": max_entries,
+           "rules": {"exact_v4": len(k4), "exact_v6": len(k6), "prefix_v4_24": len(rules7),
+                     "prefix_v6_48": len(rules8)},
+           "rule_drops": info["prefix_rule_drops"], "allowed": stats[0], "dropped": stats[1],
+           "step": "fsx_reset + import of the 32K exact rules + verdict batch",
+           "check": check}
+    if kern:
+        leg["timing"] = kern
+    if args.config5_oracle:
+        from oracle import pyoracle
+        hdr, ln, ts = host_inputs(d, n)
+        orc = pyoracle.ShardedOracle(cores, max_entries=max_entries)
+        for (mid, ks, ts_) in ((3, k4, t4), (4, k6, t6)):
+            for k, t in zip(ks, ts_):
+                orc.map_update(mid, k.tobytes(), int(t))
+        for mid, rr in ((7, rules7), (8, rules8)):
+            for k, v in rr.items():
+                orc.map_update(mid, k, v)
+        vo = orc.batch(hdr, ln, ts)
+        leg["oracle_check"] = {"verdicts_equal": bool(np.array_equal(d["v"].cpu().numpy(), vo)),
+                               "stats_equal": tuple(stats) == orc.stats()}
+        orc.close()
+    del d, H, et, is4, is6, exp, drop4, drop6
+    torch.cuda.empty_cache()
+    return leg
 
 
 if __name__ == "__main__":

@@ -98,11 +98,20 @@ __device__ __forceinline__ uint32_t id_resolve(const IdTable &T, uint32_t tag, c
                         sl.tag = tag;
                     }
                     if (tag == 2) {
+                        // Publication without release / acquire fences: on gfx950 an
+                        // agent-scope release is a whole-L2 writeback (buffer_wbl2) and an
+                        // acquire a whole-L2 invalidate (buffer_inv), per new IPv6 source.
+                        // The key words go out as returning agent-scope exchanges (performed
+                        // at the coherence point before they return); READY is stored only
+                        // after all three returned (the asm consumes their results), and
+                        // readers load the words with agent-scope (L2-bypassing) loads issued
+                        // after they saw READY.
                         uint32_t *kw = T.k6 + h * 4;
-                        __hip_atomic_store(kw + 0, k[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        __hip_atomic_store(kw + 1, k[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        __hip_atomic_store(kw + 2, k[3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        __hip_atomic_store(hp, (unsigned long long)ready, __ATOMIC_RELEASE,
+                        const uint32_t r1 = __hip_atomic_exchange(kw + 0, k[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        const uint32_t r2 = __hip_atomic_exchange(kw + 1, k[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        const uint32_t r3 = __hip_atomic_exchange(kw + 2, k[3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        asm volatile("" ::"v"(r1), "v"(r2), "v"(r3) : "memory");
+                        __hip_atomic_store(hp, (unsigned long long)ready, __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_AGENT);
                     }
                     return (uint32_t)h;
@@ -113,13 +122,14 @@ __device__ __forceinline__ uint32_t id_resolve(const IdTable &T, uint32_t tag, c
             uint32_t spins = 0;
             while (((cur >> 40) & 0xFFu) == kIdBusy) {
                 if (++spins > kIdSpin) return kNoSlot;
-                cur = __hip_atomic_load(hp, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+                __builtin_amdgcn_s_sleep(1);
+                cur = __hip_atomic_load(hp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
             break;
         }
         if (((cur >> 32) & 0xFFu) != tag || (uint32_t)cur != k[0]) continue;
         if (tag == 1) return (uint32_t)h;
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("" ::"v"((uint32_t)(cur >> 40)) : "memory");   // the words after READY
         const uint32_t *kw = T.k6 + h * 4;
         if (__hip_atomic_load(kw + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == k[1] &&
             __hip_atomic_load(kw + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == k[2] &&

@@ -363,6 +363,22 @@ class FsxContext:
         self._check(self._lib.fsx_map_update_batch(self._h, map_id, _ptr(keys), _ptr(vals), n, BPF_ANY),
                     "map_update_batch")
 
+    def map_update_arrays(self, map_id: int, keys: np.ndarray, values: np.ndarray):
+        """map_update_batch from arrays: keys [n, klen] u8, values [n] or [n, words] u64."""
+        klen, vw = _key_len(map_id), _value_words(map_id)
+        k = np.ascontiguousarray(keys, dtype=np.uint8).reshape(-1, klen)
+        v = np.ascontiguousarray(values, dtype=np.uint64).reshape(-1, vw)
+        if k.shape[0] != v.shape[0]:
+            raise ValueError("keys and values differ in length")
+        self._check(self._lib.fsx_map_update_batch(self._h, map_id, _ptr(k), _ptr(v), k.shape[0], BPF_ANY),
+                    "map_update_batch")
+
+    def map_count(self, map_id: int) -> int:
+        """Entries of one map (fsx_map_dump with no buffers)."""
+        n = C.c_size_t()
+        self._check(self._lib.fsx_map_dump(self._h, map_id, None, None, 0, C.byref(n)), "map_dump")
+        return int(n.value)
+
     def map_delete(self, map_id: int, key) -> bool:
         rc = self._lib.fsx_map_delete(self._h, map_id, _key_bytes(map_id, key))
         if rc == -errno.ENOENT:

@@ -849,14 +849,16 @@ typedef struct feat_acc {
 } feat_acc;
 
 /* Returns number of flows (distinct source IPs, order of first appearance). */
+/* max_sources bounds the distinct sources (0: n); more sources than that stop the scan
+ * and return (size_t)-1. */
 size_t fsxo_flow_features(const uint8_t *hdr, const uint32_t *len, const uint64_t *ts,
                           size_t n, size_t cap, uint8_t *keys16, uint8_t *family,
-                          float *features) {
+                          float *features, size_t max_sources) {
     omap idx[2];
-    size_t me = n + 1;
+    size_t me = max_sources ? max_sources : n + 1;
     omap_init(&idx[0], me, 4, 8);
     omap_init(&idx[1], me, 16, 8);
-    feat_acc *acc = (feat_acc *)calloc(n + 1, sizeof(feat_acc));
+    feat_acc *acc = (feat_acc *)calloc(me + 1, sizeof(feat_acc));
     size_t nf = 0;
     for (size_t i = 0; i < n; ++i) {
         uint8_t key[16];
@@ -867,6 +869,7 @@ size_t fsxo_flow_features(const uint8_t *hdr, const uint32_t *len, const uint64_
         uint64_t *slot = (uint64_t *)omap_lookup(&idx[v6], key);
         feat_acc *a;
         if (!slot) {
+            if (nf == me) { nf = (size_t)-1; break; }
             uint64_t s = nf++;
             omap_update(&idx[v6], key, &s);
             a = &acc[s];
@@ -884,7 +887,7 @@ size_t fsxo_flow_features(const uint8_t *hdr, const uint32_t *len, const uint64_
         a->s2 += (u128)len[i] * len[i];
         a->last_t = ts[i];
     }
-    for (size_t f = 0; f < nf && f < cap; ++f) {
+    for (size_t f = 0; nf != (size_t)-1 && f < nf && f < cap; ++f) {
         feat_acc *a = &acc[f];
         if (keys16) memcpy(keys16 + f * 16, a->key, 16);
         if (family) family[f] = a->fam;

@@ -75,7 +75,7 @@ def lib() -> C.CDLL:
         "fsxo_shards_dump": (sz, [vp, C.c_int, vp, vp, sz]),
         "fsxo_sigmoid_lut": (None, [C.c_float, C.c_int32, vp]),
         "fsxo_score": (None, [C.POINTER(OQ8Model), vp, sz, vp, vp, vp]),
-        "fsxo_flow_features": (sz, [vp, vp, vp, sz, sz, vp, vp, vp]),
+        "fsxo_flow_features": (sz, [vp, vp, vp, sz, sz, vp, vp, vp, sz]),
         "fsxo_synth": (C.c_int, [vp, C.c_double, C.c_uint64, sz, vp, vp, vp]),
         "fsxo_zipf_alias": (C.c_int, [C.c_uint32, C.c_double, vp, vp]),
         "fsxo_dst_port": (C.c_uint32, [vp, C.c_uint32]),
@@ -329,16 +329,21 @@ def sigmoid_lut(out_scale: float, out_zp: int) -> np.ndarray:
     return lut
 
 
-def flow_features(hdr, length, ts):
+def flow_features(hdr, length, ts, max_sources: int | None = None):
+    """Per-source features (DESIGN.md §5), sources in order of first appearance;
+    max_sources (default n) sizes the tables (more sources raise)."""
     hdr = np.ascontiguousarray(hdr, dtype=np.uint8).reshape(-1, 64)
     length = np.ascontiguousarray(length, dtype=np.uint32)
     ts = np.ascontiguousarray(ts, dtype=np.uint64)
     n = hdr.shape[0]
-    keys = np.zeros((max(n, 1), 16), dtype=np.uint8)
-    fam = np.zeros(max(n, 1), dtype=np.uint8)
-    feat = np.zeros((max(n, 1), 8), dtype=np.float32)
-    nf = lib().fsxo_flow_features(_p(hdr), _p(length), _p(ts), n, max(n, 1), _p(keys), _p(fam),
-                                  _p(feat))
+    cap = max(1, min(n, max_sources or n))
+    keys = np.zeros((cap, 16), dtype=np.uint8)
+    fam = np.zeros(cap, dtype=np.uint8)
+    feat = np.zeros((cap, 8), dtype=np.float32)
+    nf = lib().fsxo_flow_features(_p(hdr), _p(length), _p(ts), n, cap, _p(keys), _p(fam),
+                                  _p(feat), max_sources or 0)
+    if nf == 2**64 - 1:
+        raise ValueError(f"more than {max_sources} sources")
     return keys[:nf], fam[:nf], feat[:nf]
 
 
