@@ -227,10 +227,15 @@ __global__ __launch_bounds__(256) void k_heavy_sample(PacketIn in, const uint32_
 
 // One block: the (at most nmax) sketch buckets of highest count >= floor become the heavy
 // set: their candidates' keys and an open-addressing map of them. Zeroes the counts.
+// With `resolve`, every heavy source is also found in (or inserted into) the id table
+// here, once, so k_parse takes its slot from LDS instead of probing per packet (not with
+// prefix rules: a rule may drop every packet of the source, which must then never be
+// inserted).
 __global__ __launch_bounds__(1024) void k_heavy_pick(PacketIn in, const uint32_t *__restrict__ len,
                                                      uint32_t *__restrict__ sketch, HeavySet *hs,
                                                      uint32_t nmax, uint32_t floor_cnt, uint64_t seed,
-                                                     uint64_t mask, uint32_t test_flags) {
+                                                     uint64_t mask, uint32_t test_flags, IdTable idt,
+                                                     uint32_t resolve, BatchState *bs) {
     constexpr uint32_t kMap = 1u << kHeavyMapBits;
     __shared__ uint32_t s_n;
     __shared__ uint32_t s_sel[kHeavyMax];
@@ -294,7 +299,18 @@ __global__ __launch_bounds__(1024) void k_heavy_pick(PacketIn in, const uint32_t
     if (tid < n) {
         hs->tag[tid] = s_tag[tid];
         for (int j = 0; j < 4; ++j) hs->key[tid][j] = s_key[tid][j];
+        uint32_t slot = kNoSlot;
+        if (resolve) {
+            const uint64_t h = id_start(idt, s_tag[tid], s_key[tid]);
+            const uint64_t hint = __hip_atomic_load(idt.head + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            bool fresh = false;
+            slot = id_resolve(idt, s_tag[tid], s_key[tid], h, hint, &fresh);
+            if (slot == kNoSlot) atomicOr(&bs->err, ERR_TABLE_FULL);
+            if (fresh && idt.slots) atomicAdd(&bs->n_new, 1u);
+        }
+        hs->slot[tid] = slot;
     }
+    if (tid == 0) hs->resolved = resolve;
     hs->map[tid] = s_map[tid];
 }
 
@@ -378,17 +394,20 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
     __shared__ uint32_t s_hkey[kHeavyMax][4];
     __shared__ uint32_t s_htag[kHeavyMax];
     __shared__ uint32_t s_hmap4[(1u << kHeavyMapBits) / 4];   // HeavySet::map
+    __shared__ uint32_t s_hslot[kHeavyMax];
     const uint8_t *s_hmap = reinterpret_cast<const uint8_t *>(s_hmap4);
     const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
 #pragma unroll
     for (int d = 0; d < 4; ++d) s_hist[d][threadIdx.x] = 0;
     s_t0[threadIdx.x] = 0;
     const uint32_t nh = heavy ? heavy->n : 0u;
+    const bool hres = heavy && heavy->resolved;   // heavy slots known: no probe for them
     if (heavy) {
         s_hmap4[threadIdx.x] = reinterpret_cast<const uint32_t *>(heavy->map)[threadIdx.x];
         if (threadIdx.x < nh) {
             s_htag[threadIdx.x] = heavy->tag[threadIdx.x];
             for (int j = 0; j < 4; ++j) s_hkey[threadIdx.x][j] = heavy->key[threadIdx.x][j];
+            s_hslot[threadIdx.x] = heavy->slot[threadIdx.x];
         }
     }
     __syncthreads();
@@ -508,14 +527,8 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
         const bool ip = tag != 0;
         if (tag == 2) any6 = 1;
         uint64_t h = 0, hint = 0;
-        if (ip) {
-            h = id_start(idt, tag, k);
-            // a hint: the CAS decides when it shows an older generation (coherent=1 reads
-            // past the XCD's L2, which may still hold the head of an older epoch)
-            hint = idt.coherent ? __hip_atomic_load(idt.head + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                : idt.head[h];
-        }
-        // heavy source? (LDS map of the batch's heavy set, while the hint is in flight)
+        if (ip) h = id_start(idt, tag, k);
+        // heavy source? (LDS map of the batch's heavy set)
         int hidx = -1;
         if (ip && nh) {
             constexpr uint32_t kMapMask = (1u << kHeavyMapBits) - 1u;
@@ -529,6 +542,13 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
                 }
             }
         }
+        const bool probe = ip && !(hres && hidx >= 0);
+        if (probe) {
+            // a hint: the CAS decides when it shows an older generation (coherent=1 reads
+            // past the XCD's L2, which may still hold the head of an older epoch)
+            hint = idt.coherent ? __hip_atomic_load(idt.head + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                : idt.head[h];
+        }
 #pragma unroll
         for (int q = 0; q < 4; ++q) { hv[q] = hn[q]; hn[q] = h2[q]; }
         Lc = Ln; Tc = Tn; Pc = Pn;
@@ -536,7 +556,7 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
         uint64_t out = kSentinel;
         bool fresh = false;
         if (ip) {
-            const uint32_t id = id_resolve(idt, tag, k, h, hint, &fresh);
+            const uint32_t id = probe ? id_resolve(idt, tag, k, h, hint, &fresh) : s_hslot[hidx];
             if (id == kNoSlot) atomicOr(&bs->err, ERR_TABLE_FULL);
             out = ((uint64_t)(id & idt.mask) << 32) | ((uint64_t)(tag - 1u) << 31) | i;
             if (dp.light_b)   // heavy-source sort: the first pass's bucket in bits 56..63
@@ -1767,8 +1787,6 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
 
     // mark(name) closes the interval of the kernel just enqueued (per-kernel timing)
     const bool onesweep = (lim.test_flags & 2u) != 0;
-    if ((e = hipMemsetAsync(sc.sort_ctl, 0, kSortCtlWords * 4, st)) != hipSuccess) return e;
-    mark("start");
     // with the limiter, sources are found / inserted in the persistent index (sort id =
     // table slot); flow features alone use a per-batch id table and touch no map state
     static const uint32_t coherent = getenv("FSX_ID_COHERENT") ? 1u : 0u;
@@ -1776,6 +1794,8 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
         ? IdTable{X.heads, X.k6, lim.table_mask, lim.seed, X.epoch, lim.test_flags, table, id_gen, coherent}
         : IdTable{reinterpret_cast<unsigned long long *>(sc.id_tab), sc.id_tab + 2 * (lim.table_mask + 1),
                   lim.table_mask, lim.seed, id_gen, lim.test_flags, nullptr, 0, coherent};
+    if ((e = hipMemsetAsync(sc.sort_ctl, 0, kSortCtlWords * 4, st)) != hipSuccess) return e;
+    mark("start");
     const uint32_t ntiles = std::max<uint32_t>(1, cdiv(n, kSortTile));
     const uint32_t tcap = (uint32_t)(sc.cap / kSortTile + 2);
     // source ids have log2(slots) bits: ceil(bits / 8) LSD passes of equal digits of at
@@ -1800,8 +1820,11 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
         dp.shift[1] = 39; dp.mask[1] = (1u << w1) - 1u;
         dp.shift[2] = 39 + w1; dp.mask[2] = (1u << (rest - w1)) - 1u;
         k_heavy_sample<<<64, 256, 0, st>>>(in, len, n, sc.sketch, lim.seed, lim.table_mask, lim.test_flags);
+        // heavy slots resolved once (not under prefix rules; FSX_NO_HEAVY_SLOTS=1: A/B)
+        static const bool no_hslots = getenv("FSX_NO_HEAVY_SLOTS") != nullptr;
+        const uint32_t resolve = !no_hslots && !(do_limit && rules.slot) ? 1u : 0u;
         k_heavy_pick<<<1, 1024, 0, st>>>(in, len, sc.sketch, sc.heavy, kHeavyMax, 16, lim.seed,
-                                         lim.table_mask, lim.test_flags);
+                                         lim.table_mask, lim.test_flags, idt, resolve, bs);
         mark("k_heavy_pick");
     } else {
         for (int p = 0; p < 4; ++p) { dp.shift[p] = 32u + dbits * (uint32_t)p; dp.mask[p] = dmask; }

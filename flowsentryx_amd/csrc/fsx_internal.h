@@ -254,8 +254,11 @@ constexpr uint32_t kHeavySample = 65536;           // sampled packets per batch
 constexpr uint32_t kHeavyMapBits = 10;
 struct HeavySet {
     uint32_t n;
+    uint32_t resolved;   // slot[] holds each heavy source's table slot (k_heavy_pick inserted
+                         // new ones), so k_parse takes it from LDS instead of probing
     uint32_t tag[kHeavyMax];
     uint32_t key[kHeavyMax][4];
+    uint32_t slot[kHeavyMax];
     // open addressing on the source's probe start (its table hash) modulo the map size:
     // heavy index + 1, 0 empty
     alignas(16) uint8_t map[1u << kHeavyMapBits];
