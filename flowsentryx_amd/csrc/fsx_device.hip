@@ -385,7 +385,7 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
                                                IdTable idt, uint32_t *__restrict__ ghist,
                                                uint32_t *__restrict__ thist, uint32_t tcap,
                                                DigitPlan dp, const HeavySet *__restrict__ heavy,
-                                               RuleSet rules) {
+                                               RuleSet rules, uint32_t tagh) {
     __shared__ uint32_t s_rec[4][64 * 17];
     __shared__ uint32_t s_red[4][3];
     __shared__ unsigned long long s_ts[4], s_its[4];
@@ -395,6 +395,7 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
     __shared__ uint32_t s_htag[kHeavyMax];
     __shared__ uint32_t s_hmap4[(1u << kHeavyMapBits) / 4];   // HeavySet::map
     __shared__ uint32_t s_hslot[kHeavyMax];
+    __shared__ uint32_t s_def[4][256 * 3];  // per wave: deferred probes {i, tag | hidx, key word 0}
     const uint8_t *s_hmap = reinterpret_cast<const uint8_t *>(s_hmap4);
     const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
 #pragma unroll
@@ -424,8 +425,11 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
     auto next_step = [&](uint32_t st, uint32_t j, uint32_t &st2, uint32_t &j2) {
         if (j + 1 < kSteps) { st2 = st; j2 = j + 1; } else { st2 = st + gridDim.x; j2 = 0; }
     };
-    // software pipeline: the next tile's loads are in flight while this one is parsed
-    auto load = [&](uint32_t tt, uint4 (&h)[4], uint32_t &L_, uint64_t &T_, uint64_t &P_) {
+    // software pipeline: the next tile's loads are in flight while this one is parsed.
+    // Header records: only their first 48 bytes (the parse reads bytes 12..39), as 3 x 16 B
+    // per lane: flat chunk f = k * 64 + lane is chunk f % 3 of record f / 3
+    constexpr int kHv = kRec == 0 ? 3 : (int)(kRec / 16);   // uint4 registers per lane and step
+    auto load = [&](uint32_t tt, uint4 (&h)[kHv], uint32_t &L_, uint64_t &T_, uint64_t &P_) {
         const uint32_t base = tt << 6;
         const bool tv = tt < ntiles;
         const uint32_t i = base + lane;
@@ -433,10 +437,10 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
         if constexpr (kRec == 0) {
             const uint8_t *src = in.hdr + (size_t)base * 64;
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const uint32_t g = (uint32_t)k * 1024u + lane * 16u;
+            for (int k = 0; k < 3; ++k) {
+                const uint32_t f = (uint32_t)k * 64u + lane, r = f / 3u, c = f - 3u * r;
                 h[k] = make_uint4(0, 0, 0, 0);
-                if (tv && base + (g >> 6) < n) h[k] = *reinterpret_cast<const uint4 *>(src + g);
+                if (tv && base + r < n) h[k] = *reinterpret_cast<const uint4 *>(src + r * 64u + c * 16u);
             }
             L_ = live ? len[i] : 0u;
             T_ = live ? ts[i] : 0ull;
@@ -445,7 +449,7 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
             const uint4 *r = reinterpret_cast<const uint4 *>(in.rec);
             constexpr uint32_t kW = kRec / 16;   // uint4 words per record
 #pragma unroll
-            for (int k = 0; k < 4; ++k) h[k] = make_uint4(0, 0, 0, 0);
+            for (int k = 0; k < kHv; ++k) h[k] = make_uint4(0, 0, 0, 0);
             if (live) {
                 h[0] = r[(size_t)i * kW];
                 if constexpr (kW == 2) h[1] = r[(size_t)i * kW + 1];
@@ -459,30 +463,75 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
             }
         }
     };
-    uint4 hv[4], hn[4];
+    // Software pipeline, per wave: iteration j parses step j + 1 (its
+    // records were loaded two iterations earlier) and issues that step's source-index
+    // probes, then issues the record loads of step j + 3, then resolves step j from the
+    // probes issued one iteration earlier. vmcnt drains in issue order, so a probe read
+    // issued after a prefetch would wait for the prefetch; issued one iteration ahead,
+    // before it, the probes never stall the stream. A probe that does not find its
+    // source READY in the first two slots (new source, longer probe chain, IPv6) is
+    // deferred: the wave resolves its deferred packets together (CAS inserts) at the end
+    // of the sort tile, or earlier when the LDS list fills.
+    uint4 hv[kHv], hn[kHv];
     uint32_t Lc, Ln;
     uint64_t Tc, Pc, Tn, Pn;
-    load(step_of(blockIdx.x, 0), hv, Lc, Tc, Pc);
-    {
-        uint32_t T1, j1;
-        next_step(blockIdx.x, 0, T1, j1);
-        load(T1 < nsort ? step_of(T1, j1) : ntiles, hn, Ln, Tn, Pn);
-    }
-    // software pipeline: the loads of the next two steps are in flight while this one
-    // is parsed (measured faster than issuing the id probes ahead of the prefetch)
-    for (uint32_t tile = blockIdx.x; tile < nsort; tile += gridDim.x)
-    for (uint32_t j = 0; j < kSteps; ++j) {
-        const uint32_t t = step_of(tile, j);
-        uint32_t T1, j1, T2, j2;
-        next_step(tile, j, T1, j1);
-        next_step(T1, j1, T2, j2);
-        uint4 h2[4];
-        uint32_t L2;
-        uint64_t Tn2, Pn2;
-        load(T2 < nsort ? step_of(T2, j2) : ntiles, h2, L2, Tn2, Pn2);
+    // the parsed step awaiting resolution: tag, key word 0, probe start, heavy index, the
+    // two probe reads
+    uint32_t c_tag = 0, c_k0 = 0, c_h = 0;
+    int c_hidx = -1;
+    uint64_t c_hint0 = 0, c_hint1 = 0;
+    constexpr uint32_t kDefCap = 256;   // deferred packets per wave (LDS)
+    uint32_t *dq = s_def[w];
+    uint32_t ndef = 0;
+    const uint64_t lt_mask = (1ull << lane) - 1ull;
+    // radix histograms of the key digits: block LDS counters (a heavy source repeats in
+    // few lanes of one 64-packet step, so same-address serialization stays short)
+    auto count_digits = [&](uint64_t out, int hidx) {
+        if (!ghist) return;
+        const uint32_t d0 = (uint32_t)(out >> dp.shift[0]) & dp.mask[0];
+        atomicAdd(&s_hist[0][d0], 1u);
+        atomicAdd(&s_t0[d0], 1u);
+        if (hidx < 0)   // heavy entries are final after pass 0
+            for (uint32_t dg = 1; dg < dp.npass; ++dg)
+                atomicAdd(&s_hist[dg][(uint32_t)(out >> dp.shift[dg]) & dp.mask[dg]], 1u);
+    };
+    auto word_of = [&](uint32_t id, uint32_t tag, uint32_t i, int hidx) -> uint64_t {
+        uint64_t out = ((uint64_t)(id & idt.mask) << 32) | ((uint64_t)(tag - 1u) << 31) | i;
+        if (dp.light_b)   // heavy-source sort: the first pass's bucket in bits 56..63
+            out |= (uint64_t)(hidx >= 0 ? dp.light_b + (uint32_t)hidx
+                                        : (uint32_t)(out >> 32) & (dp.light_b - 1u)) << 56;
+        return out;
+    };
+    // the deferred packets of this wave: full probes (CAS inserts), 64 at a time
+    auto flush = [&]() {
+        for (uint32_t e0 = 0; e0 < ndef; e0 += 64) {
+            const uint32_t e = e0 + lane;
+            bool fresh = false;
+            if (e < ndef) {
+                const uint32_t *q = dq + e * 3;
+                const uint32_t i = q[0], tag = q[1] & 0xFFu;
+                const int hidx = (int)(q[1] >> 8) - 1;
+                uint32_t k[4] = {q[2], 0, 0, 0};
+                if (tag == 2) packet_src(in, len, i, k);   // IPv6: the key again from the record
+                const uint64_t h = id_start(idt, tag, k);
+                const uint64_t hint = __hip_atomic_load(idt.head + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const uint32_t id = id_resolve(idt, tag, k, h, hint, &fresh);
+                if (id == kNoSlot) atomicOr(&bs->err, ERR_TABLE_FULL);
+                const uint64_t out = word_of(id, tag, i, hidx);
+                packed[i] = out;
+                count_digits(out, hidx);
+            }
+            nfresh += (uint32_t)__popcll(__ballot(fresh));   // new sources (persistent index)
+        }
+        ndef = 0;
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    };
+    // parse one step (its records in hv / Lc / Tc / Pc): verdict bytes, clock facts, and
+    // the probes of its IP packets into the c_* registers
+    auto parse_step = [&](uint32_t t) {
         const uint32_t base = t << 6;
         const uint32_t i = base + lane;
-        const bool live = i < n;
+        const bool live = t < ntiles && i < n;
         uint32_t L = Lc;
         uint64_t T = Tc;
         uint8_t v = XDP_PASS;  // non-IP: PASS, not counted (src/fsx_kern.c:128-131)
@@ -490,10 +539,9 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
         uint32_t tag = 0;
         if constexpr (kRec == 0) {
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const uint32_t g = (uint32_t)q * 1024u + lane * 16u;
-                const uint32_t r = g >> 6, off = (g & 63u) >> 2;
-                uint32_t *d = rec + r * 17u + off;
+            for (int q = 0; q < 3; ++q) {
+                const uint32_t f = (uint32_t)q * 64u + lane, r = f / 3u, c = f - 3u * r;
+                uint32_t *d = rec + r * 17u + c * 4u;
                 d[0] = hv[q].x; d[1] = hv[q].y; d[2] = hv[q].z; d[3] = hv[q].w;
             }
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -526,7 +574,7 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
         if (lane == 0) prev = (live && i > 0) ? Pc : T;
         const bool ip = tag != 0;
         if (tag == 2) any6 = 1;
-        uint64_t h = 0, hint = 0;
+        uint64_t h = 0;
         if (ip) h = id_start(idt, tag, k);
         // heavy source? (LDS map of the batch's heavy set)
         int hidx = -1;
@@ -542,54 +590,117 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
                 }
             }
         }
-        const bool probe = ip && !(hres && hidx >= 0);
-        if (probe) {
-            // a hint: the CAS decides when it shows an older generation (coherent=1 reads
-            // past the XCD's L2, which may still hold the head of an older epoch)
-            hint = idt.coherent ? __hip_atomic_load(idt.head + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                : idt.head[h];
+        // the fast path reads the first two slots of an IPv4 source's probe chain (IPv6
+        // sources are always resolved by the full protocol, which reads their key words
+        // only after the head shows READY)
+        c_hint0 = c_hint1 = 0;
+        if (tag == 1 && !(hres && hidx >= 0)) {
+            // (coherent=1 reads past the XCD's L2, which may hold the head of an older
+            // epoch: a stale head can only fail the match, never fake one)
+            const uint64_t h1 = (h + 1) & idt.mask;
+            if (idt.coherent) {
+                c_hint0 = __hip_atomic_load(idt.head + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                c_hint1 = __hip_atomic_load(idt.head + h1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else {
+                c_hint0 = idt.head[h];
+                c_hint1 = idt.head[h1];
+            }
         }
-#pragma unroll
-        for (int q = 0; q < 4; ++q) { hv[q] = hn[q]; hn[q] = h2[q]; }
-        Lc = Ln; Tc = Tn; Pc = Pn;
-        Ln = L2; Tn = Tn2; Pn = Pn2;
-        uint64_t out = kSentinel;
-        bool fresh = false;
-        if (ip) {
-            const uint32_t id = probe ? id_resolve(idt, tag, k, h, hint, &fresh) : s_hslot[hidx];
-            if (id == kNoSlot) atomicOr(&bs->err, ERR_TABLE_FULL);
-            out = ((uint64_t)(id & idt.mask) << 32) | ((uint64_t)(tag - 1u) << 31) | i;
-            if (dp.light_b)   // heavy-source sort: the first pass's bucket in bits 56..63
-                out |= (uint64_t)(hidx >= 0 ? dp.light_b + (uint32_t)hidx
-                                            : (uint32_t)(out >> 32) & (dp.light_b - 1u)) << 56;
-        }
-        nfresh += (uint32_t)__popcll(__ballot(fresh));   // new sources (persistent index)
+        c_tag = live ? tag : 0u;
+        c_k0 = k[0];
+        c_h = (uint32_t)h;
+        c_hidx = hidx;
         if (live) {
-            packed[i] = out;
             // IP packets default to PASS here (coalesced); the fill pass writes only
             // the DROP verdicts, which cluster in the heavy sources' segments
-            if (verdict) verdict[i] = ip ? (uint8_t)XDP_PASS : v;
+            // (tagh: a heavy source's packet carries 0x80 | its index until k_verdict_apply)
+            if (verdict) verdict[i] = !ip ? v : (tagh && hidx >= 0) ? (uint8_t)(0x80u | (uint32_t)hidx)
+                                                                  : (uint8_t)XDP_PASS;
+            if (!ip) packed[i] = kSentinel;
             nonmono |= T < prev ? 1u : 0u;
             maxlen = L > maxlen ? L : maxlen;
             maxts = T > maxts ? T : maxts;
             inv_mints = ~T > inv_mints ? ~T : inv_mints;
         }
-        // radix histograms of the key digits: block LDS counters (a heavy source repeats
-        // in few lanes of one 64-packet step, so same-address serialization stays short)
-        if (ghist && ip) {
-            const uint32_t d0 = (uint32_t)(out >> dp.shift[0]) & dp.mask[0];
-            atomicAdd(&s_hist[0][d0], 1u);
-            atomicAdd(&s_t0[d0], 1u);
-            if (hidx < 0)   // heavy entries are final after pass 0
-                for (uint32_t dg = 1; dg < dp.npass; ++dg)
-                    atomicAdd(&s_hist[dg][(uint32_t)(out >> dp.shift[dg]) & dp.mask[dg]], 1u);
+    };
+    // resolve step t ("cur"): heavy slot from LDS, the fast-path probe match, or defer
+    auto resolve_step = [&](uint32_t t) {
+        const uint32_t i = (t << 6) + lane;
+        uint32_t id = kNoSlot;
+        bool defer = false;
+        if (c_tag) {
+            if (hres && c_hidx >= 0) {
+                id = s_hslot[c_hidx];
+            } else if (c_tag == 1) {
+                const uint64_t ready = id_head(idt.gen, kIdReady, 1u, c_k0);
+                if (c_hint0 == ready) id = c_h;
+                else if (c_hint1 == ready) id = (uint32_t)((c_h + 1) & idt.mask);
+                else defer = true;
+            } else {
+                defer = true;
+            }
         }
+        const uint64_t dm = __ballot(defer);
+        if (dm) {
+            if (ndef + 64 > kDefCap) flush();
+            if (defer) {
+                uint32_t *q = dq + (ndef + (uint32_t)__popcll(dm & lt_mask)) * 3;
+                q[0] = i; q[1] = c_tag | (uint32_t)(c_hidx + 1) << 8; q[2] = c_k0;
+            }
+            ndef += (uint32_t)__popcll(dm);
+        }
+        if (c_tag && !defer) {
+            const uint64_t out = word_of(id, c_tag, i, c_hidx);
+            packed[i] = out;
+            count_digits(out, c_hidx);
+        }
+    };
+    // prologue: steps 0 and 1 loading, step 0 parsed (its probes in flight), step 2 loading
+    load(step_of(blockIdx.x, 0), hv, Lc, Tc, Pc);
+    {
+        uint32_t T1, j1;
+        next_step(blockIdx.x, 0, T1, j1);
+        load(T1 < nsort ? step_of(T1, j1) : ntiles, hn, Ln, Tn, Pn);
+        if (blockIdx.x < nsort) parse_step(step_of(blockIdx.x, 0));
+        uint32_t T2, j2;
+        next_step(T1, j1, T2, j2);
+#pragma unroll
+        for (int q = 0; q < kHv; ++q) hv[q] = hn[q];
+        Lc = Ln; Tc = Tn; Pc = Pn;
+        load(T2 < nsort ? step_of(T2, j2) : ntiles, hn, Ln, Tn, Pn);
+    }
+    for (uint32_t tile = blockIdx.x; tile < nsort; tile += gridDim.x)
+    for (uint32_t j = 0; j < kSteps; ++j) {
+        const uint32_t t = step_of(tile, j);
+        uint32_t T1, j1, T2, j2, T3, j3;
+        next_step(tile, j, T1, j1);
+        next_step(T1, j1, T2, j2);
+        next_step(T2, j2, T3, j3);
+        // C: resolve this step with the probes issued one iteration ago
+        resolve_step(t);
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        if (j == kSteps - 1 && thist) {   // sort tile done: its digit-0 counts, digit-major
-            __syncthreads();
-            if (threadIdx.x <= dp.mask[0]) thist[(size_t)threadIdx.x * tcap + tile] = s_t0[threadIdx.x];
-            s_t0[threadIdx.x] = 0;
-            __syncthreads();
+        if (j == kSteps - 1) {   // sort tile done: its deferred packets, then its digit-0 counts
+            flush();
+            if (thist) {
+                __syncthreads();
+                if (threadIdx.x <= dp.mask[0]) thist[(size_t)threadIdx.x * tcap + tile] = s_t0[threadIdx.x];
+                s_t0[threadIdx.x] = 0;
+                __syncthreads();
+            }
+        }
+        // A: parse the next step (records loaded two iterations ago), its probes issued
+        c_tag = 0; c_hidx = -1; c_hint0 = c_hint1 = 0;
+        if (T1 < nsort) parse_step(step_of(T1, j1));
+        // B: the record loads of step + 3
+        {
+            uint4 h2[kHv];
+            uint32_t L2;
+            uint64_t Tn2, Pn2;
+            load(T3 < nsort ? step_of(T3, j3) : ntiles, h2, L2, Tn2, Pn2);
+#pragma unroll
+            for (int q = 0; q < kHv; ++q) { hv[q] = hn[q]; hn[q] = h2[q]; }
+            Lc = Ln; Tc = Tn; Pc = Pn;
+            Ln = L2; Tn = Tn2; Pn = Pn2;
         }
     }
     if (ghist) {
@@ -1191,9 +1302,9 @@ struct FwState {
 };
 
 // One packet of src/fsx_kern.c:150-346 (exact, any timestamps, u64 wraparound).
-template <bool kWave>
+template <class MW>
 __device__ __forceinline__ void fw_step(FwState &s, uint64_t now, uint32_t L, uint32_t q,
-                                        const Limits &lim, MarkWriter<kWave> &mw) {
+                                        const Limits &lim, MW &mw) {
     if (s.has_bl && s.till > 0) {
         if (now > s.till) s.has_bl = false;                 // :193-204 delete
         else { mw.emit(q, XDP_DROP); return; }              // :205-215
@@ -1214,9 +1325,9 @@ __device__ __forceinline__ void fw_step(FwState &s, uint64_t now, uint32_t L, ui
 }
 
 // Exact replay for one thread, 16 packets' loads in flight per step.
-template <class SV>
+template <class SV, class MW>
 __device__ void walk_fixed_exact_thread(const SV &sv, uint32_t a, uint32_t b,
-                                        const Limits &lim, MarkWriter<false> &mw, FwState &s) {
+                                        const Limits &lim, MW &mw, FwState &s) {
     for (uint32_t q0 = a; q0 < b; q0 += 16) {
         uint64_t t[16];
         uint32_t L[16];
@@ -1227,15 +1338,15 @@ __device__ void walk_fixed_exact_thread(const SV &sv, uint32_t a, uint32_t b,
         }
 #pragma unroll
         for (int k = 0; k < 16; ++k)
-            if (q0 + k < b) fw_step<false>(s, t[k], L[k], q0 + k, lim, mw);
+            if (q0 + k < b) fw_step(s, t[k], L[k], q0 + k, lim, mw);
     }
 }
 
 // Exact replay for one wave: 64 packets loaded in parallel, then stepped uniformly
 // (every lane keeps the same state; values broadcast by shuffles).
-template <class SV>
+template <class SV, class MW>
 __device__ void walk_fixed_exact_wave(const SV &sv, uint32_t a, uint32_t b, const Limits &lim,
-                                      MarkWriter<true> &mw, FwState &s) {
+                                      MW &mw, FwState &s) {
     const uint32_t lane = lane_id();
     for (uint32_t q0 = a; q0 < b; q0 += 64) {
         const uint32_t q = q0 + lane;
@@ -1243,7 +1354,7 @@ __device__ void walk_fixed_exact_wave(const SV &sv, uint32_t a, uint32_t b, cons
         const uint32_t lq = q < b ? sv.l(q) : 0u;
         const uint32_t cnt = min(64u, b - q0);
         for (uint32_t k = 0; k < cnt; ++k)
-            fw_step<true>(s, __shfl(tq, (int)k), __shfl(lq, (int)k), q0 + k, lim, mw);
+            fw_step(s, __shfl(tq, (int)k), __shfl(lq, (int)k), q0 + k, lim, mw);
     }
 }
 
@@ -1252,9 +1363,9 @@ __device__ void walk_fixed_exact_wave(const SV &sv, uint32_t a, uint32_t b, cons
 // reset packet (count 0, not counted) or the carried window (continuation). With
 // counts consecutive inside an epoch, the count trigger is at a closed-form
 // position; the window end and the blacklist end are searches.
-template <bool kWave, class SV>
+template <bool kWave, class SV, class MW>
 __device__ void walk_fixed_fast(const SV &sv, uint32_t a, uint32_t b, const Limits &lim,
-                                uint32_t maxL, MarkWriter<kWave> &mw, FwState &s) {
+                                uint32_t maxL, MW &mw, FwState &s) {
     const uint64_t P = lim.pps, B = lim.bps, W = lim.window, BLK = lim.block;
     uint32_t p = a;
     if (s.has_bl && s.till > 0) {
@@ -1421,15 +1532,54 @@ __global__ __launch_bounds__(256) void k_seg_order(const BatchState *bs,
     seg_classes_pass<true>(seg_start, lo, hi, short_seg, cur, order);
 }
 
+// Heavy verdict lists: a heavy source's segment (the sorted positions from
+// n_light on, one run per heavy source) writes its verdict changes as an arrival-index list
+// over its own positions in hl instead of marks, and counts its PASS / DROP packets into
+// stats_map here (k_fill_* cover the light positions only).
+struct HeavyLists {
+    uint32_t *list;   // nullptr: every segment writes marks
+    HeavySet *hs;
+    TableState *tstate;
+    BatchState *bs;
+};
+
+template <bool kWave>
+__device__ __forceinline__ int heavy_list_open(const HeavyLists &H, const uint64_t *S, uint32_t a,
+                                               MarkWriter<kWave, true> &mw) {
+    mw.list = H.list + a;
+    mw.S = S;
+    return (int)(S[a] >> 56) - (int)kHeavyMax;   // bucket = 128 + heavy index
+}
+
+template <bool kWave>
+__device__ __forceinline__ void heavy_list_close(const HeavyLists &H, int h, uint32_t a, uint32_t b,
+                                                 MarkWriter<kWave, true> &mw) {
+    mw.finish(b);
+    if (kWave && lane_id() != 0) return;
+    H.hs->lbase[h] = a;
+    H.hs->lcnt[h] = mw.nl;
+    unsigned long long *st = reinterpret_cast<unsigned long long *>(H.tstate->stats);
+    if (mw.npass) {
+        atomicAdd(st, (unsigned long long)mw.npass);
+        atomicAdd(reinterpret_cast<unsigned long long *>(&H.bs->allowed), (unsigned long long)mw.npass);
+    }
+    if (mw.ndrop) {
+        atomicAdd(st + 1, (unsigned long long)mw.ndrop);
+        atomicAdd(reinterpret_cast<unsigned long long *>(&H.bs->dropped), (unsigned long long)mw.ndrop);
+    }
+}
+
 template <class SV>
 __device__ __forceinline__ void walk_short(const SV &sv, const BatchState *bs,
                                            const uint32_t *seg_start, const uint32_t *seg_slot,
                                            const uint32_t *order, const uint32_t *cls,
-                                           uint8_t *marks, Slot *table, const Limits &lim) {
+                                           uint8_t *marks, Slot *table, const Limits &lim,
+                                           const HeavyLists &H) {
     const uint32_t nshort = bs->nseg - cls[kSegClasses - 1];
     for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < nshort; i += gridDim.x * 256u) {
         const uint32_t g = order[i];
         const uint32_t a = seg_start[g], b = seg_start[g + 1];
+        if (H.list && a >= bs->n_light) continue;   // a heavy source: k_walk_heavy
         Slot &sl = table[seg_slot[g]];
         FwState st = load_state(sl);
         MarkWriter<false> mw{marks, 0};
@@ -1447,14 +1597,14 @@ __global__ __launch_bounds__(256) void k_walk_fixed(const uint64_t *__restrict__
                                                     const uint32_t *__restrict__ order,
                                                     const uint32_t *__restrict__ cls,
                                                     uint8_t *__restrict__ marks, Slot *table,
-                                                    Limits lim) {
+                                                    Limits lim, HeavyLists H) {
     if (bs->err) return;
     if (bs->pay_ok) {
         const SegView<true> sv{S, ts, len, pay, ~bs->inv_min_ts};
-        walk_short(sv, bs, seg_start, seg_slot, order, cls, marks, table, lim);
+        walk_short(sv, bs, seg_start, seg_slot, order, cls, marks, table, lim, H);
     } else {
         const SegView<false> sv{S, ts, len, pay, 0};
-        walk_short(sv, bs, seg_start, seg_slot, order, cls, marks, table, lim);
+        walk_short(sv, bs, seg_start, seg_slot, order, cls, marks, table, lim, H);
     }
 }
 
@@ -1462,7 +1612,8 @@ template <class SV>
 __device__ __forceinline__ void walk_long(const SV &sv, const BatchState *bs,
                                           const uint32_t *seg_start, const uint32_t *seg_slot,
                                           const uint32_t *order, const uint32_t *cls,
-                                          uint8_t *marks, Slot *table, const Limits &lim) {
+                                          uint8_t *marks, Slot *table, const Limits &lim,
+                                          const HeavyLists &H) {
     const uint32_t nl = cls[kSegClasses - 1], first = bs->nseg - nl;
     const bool glob_fast = fast_ok(bs, lim);
     const uint32_t maxL = bs->max_len;
@@ -1470,11 +1621,12 @@ __device__ __forceinline__ void walk_long(const SV &sv, const BatchState *bs,
     for (uint32_t i = wave; i < nl; i += gridDim.x * 4u) {
         const uint32_t g = order[first + i];
         const uint32_t a = seg_start[g], b = seg_start[g + 1];
+        if (H.list && a >= bs->n_light) continue;   // a heavy source: k_walk_heavy
         Slot &sl = table[seg_slot[g]];
         FwState st = load_state(sl);
-        MarkWriter<true> mw{marks, 0};
         const bool fast = glob_fast && (!st.has_st || (st.tt <= ~0ull - lim.window &&
                                                        st.pps < kBig && st.bps < kBig));
+        MarkWriter<true> mw{marks, 0};
         if (fast) walk_fixed_fast<true>(sv, a, b, lim, maxL, mw, st);
         else walk_fixed_exact_wave(sv, a, b, lim, mw, st);
         if (lane_id() == 0) store_state(sl, st);
@@ -1491,14 +1643,56 @@ __global__ __launch_bounds__(256) void k_walk_fixed_long(const uint64_t *__restr
                                                          const uint32_t *__restrict__ order,
                                                          const uint32_t *__restrict__ cls,
                                                          uint8_t *__restrict__ marks, Slot *table,
-                                                         Limits lim) {
+                                                         Limits lim, HeavyLists H) {
     if (bs->err) return;
     if (bs->pay_ok) {
         const SegView<true> sv{S, ts, len, pay, ~bs->inv_min_ts};
-        walk_long(sv, bs, seg_start, seg_slot, order, cls, marks, table, lim);
+        walk_long(sv, bs, seg_start, seg_slot, order, cls, marks, table, lim, H);
     } else {
         const SegView<false> sv{S, ts, len, pay, 0};
-        walk_long(sv, bs, seg_start, seg_slot, order, cls, marks, table, lim);
+        walk_long(sv, bs, seg_start, seg_slot, order, cls, marks, table, lim, H);
+    }
+}
+
+// The heavy sources' segments (heavy verdict lists): one wave per heavy bucket of pass 0,
+// whose run [gbase, gbase + count) of sorted positions is the source's segment.
+template <class SV>
+__device__ __forceinline__ void walk_heavy(const SV &sv, const BatchState *bs, const uint32_t *cnt0,
+                                           const uint32_t *base0, Slot *table, const Limits &lim,
+                                           const HeavyLists &H) {
+    const bool glob_fast = fast_ok(bs, lim);
+    const uint32_t maxL = bs->max_len;
+    const uint32_t h = blockIdx.x * 4u + (threadIdx.x >> 6);
+    if (h >= H.hs->n) return;
+    const uint32_t c = cnt0[kHeavyMax + h];
+    if (c == 0) return;
+    const uint32_t a = base0[kHeavyMax + h], b = a + c;
+    Slot &sl = table[pk_id(sv.S[a], lim.table_mask)];
+    FwState st = load_state(sl);
+    const bool fast = glob_fast && (!st.has_st || (st.tt <= ~0ull - lim.window &&
+                                                   st.pps < kBig && st.bps < kBig));
+    MarkWriter<true, true> mw{nullptr, 0};
+    heavy_list_open(H, sv.S, a, mw);
+    if (fast) walk_fixed_fast<true>(sv, a, b, lim, maxL, mw, st);
+    else walk_fixed_exact_wave(sv, a, b, lim, mw, st);
+    heavy_list_close(H, (int)h, a, b, mw);
+    if (lane_id() == 0) store_state(sl, st);
+}
+
+__global__ __launch_bounds__(256) void k_walk_heavy(const uint64_t *__restrict__ S, BatchState *bs,
+                                                    const uint32_t *__restrict__ cnt0,
+                                                    const uint32_t *__restrict__ base0,
+                                                    const uint64_t *__restrict__ ts,
+                                                    const uint32_t *__restrict__ len,
+                                                    const uint64_t *__restrict__ pay, Slot *table,
+                                                    Limits lim, HeavyLists H) {
+    if (bs->err) return;
+    if (bs->pay_ok) {
+        const SegView<true> sv{S, ts, len, pay, ~bs->inv_min_ts};
+        walk_heavy(sv, bs, cnt0, base0, table, lim, H);
+    } else {
+        const SegView<false> sv{S, ts, len, pay, 0};
+        walk_heavy(sv, bs, cnt0, base0, table, lim, H);
     }
 }
 
@@ -1514,10 +1708,11 @@ __device__ __forceinline__ void load_marks16(const uint8_t *marks, uint32_t p0, 
     }
 }
 
+// (light_only: the heavy sources' positions [n_light, n_valid) have verdict lists instead)
 __global__ __launch_bounds__(256) void k_fill_last(const uint8_t *__restrict__ marks, BatchState *bs,
-                                                   uint8_t *__restrict__ tile_last) {
+                                                   uint8_t *__restrict__ tile_last, uint32_t light_only) {
     __shared__ uint32_t s_w[4];
-    const uint32_t M = bs->n_valid;
+    const uint32_t M = light_only ? bs->n_light : bs->n_valid;
     const uint32_t ntiles = (M + kTile - 1) / kTile;
     for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
         const uint32_t p0 = t * kTile + threadIdx.x * 16u;
@@ -1542,10 +1737,11 @@ __global__ __launch_bounds__(256) void k_fill_last(const uint8_t *__restrict__ m
 }
 
 // Single block: carry[t] = last non-zero of tile_last[0..t-1] (in place, exclusive).
-__global__ __launch_bounds__(1024) void k_fill_carry(uint8_t *__restrict__ tile_last, BatchState *bs) {
+__global__ __launch_bounds__(1024) void k_fill_carry(uint8_t *__restrict__ tile_last, BatchState *bs,
+                                                     uint32_t light_only) {
     __shared__ uint32_t s_w[16];
     __shared__ uint32_t s_carry;
-    const uint32_t M = bs->n_valid;
+    const uint32_t M = light_only ? bs->n_light : bs->n_valid;
     const uint32_t ntiles = (M + kTile - 1) / kTile;
     const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
     if (threadIdx.x == 0) s_carry = 0;
@@ -1583,14 +1779,15 @@ __global__ __launch_bounds__(256) void k_fill_scatter(const uint8_t *__restrict_
                                                       const uint8_t *__restrict__ carry,
                                                       uint32_t *__restrict__ drop_list,
                                                       uint32_t *__restrict__ drop_cur,
-                                                      TableState *tstate, uint32_t nchunks) {
+                                                      TableState *tstate, uint32_t nchunks,
+                                                      uint32_t light_only) {
     __shared__ uint8_t s_v[kTile];
     __shared__ uint32_t s_w[4];
     __shared__ unsigned long long s_cnt[4][2];
     __shared__ uint32_t s_cc[kMaxTileChunks];   // per arrival chunk: tile count, then base
     __shared__ uint16_t s_rk[kTile];            // per DROP position: rank in its chunk
     if (bs->err) return;
-    const uint32_t M = bs->n_valid;
+    const uint32_t M = light_only ? bs->n_light : bs->n_valid;
     const uint32_t ntiles = (M + kTile - 1) / kTile;
     const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
     // batches of <= kMaxTileChunks chunks: a tile reserves its DROPs' list slots with one
@@ -1711,17 +1908,22 @@ __global__ __launch_bounds__(256) void k_fill_scatter(const uint8_t *__restrict_
 // One block per arrival chunk of kVChunk verdict bytes: the chunk through LDS, its DROP
 // list applied, written back with 16-byte stores (IP packets were written PASS by
 // k_parse). Resets the chunk's cursor for the next batch.
+// With heavy verdict lists (hl != nullptr) every chunk is rewritten: the bytes k_parse
+// tagged 0x80 | h take heavy source h's verdict at their arrival index (the last list entry
+// at or before it; each block first narrows every list to the entries around its chunk).
 __global__ __launch_bounds__(256) void k_verdict_apply(uint8_t *__restrict__ verdict, uint32_t n,
                                                        const uint32_t *__restrict__ drop_list,
                                                        uint32_t *__restrict__ drop_cur,
-                                                       const BatchState *bs) {
+                                                       const BatchState *bs, const HeavySet *hs,
+                                                       const uint32_t *__restrict__ hl) {
     __shared__ uint4 s_v4[kVChunk / 16];
+    __shared__ uint32_t s_lo[kHeavyMax], s_hi[kHeavyMax], s_tmp4[4];
     uint8_t *s_v = reinterpret_cast<uint8_t *>(s_v4);
     const uint32_t c = blockIdx.x;
     const uint32_t cnt = drop_cur[c];
     __syncthreads();
     if (threadIdx.x == 0) drop_cur[c] = 0;
-    if (cnt == 0 || bs->err) return;
+    if ((cnt == 0 && !hl) || bs->err) return;
     const uint32_t b0 = c * kVChunk, nb = min(kVChunk, n - b0);
     const bool vec = ((reinterpret_cast<uintptr_t>(verdict) & 15u) == 0) && nb == kVChunk;
     if (vec) {
@@ -1733,6 +1935,46 @@ __global__ __launch_bounds__(256) void k_verdict_apply(uint8_t *__restrict__ ver
     __syncthreads();
     const uint32_t *lst = drop_list + (size_t)c * kVChunk;
     for (uint32_t q = threadIdx.x; q < cnt; q += 256) s_v[lst[q] - b0] = XDP_DROP;
+    if (hl) {
+        // entries [lo, hi) of list h decide this chunk's packets of h; they are copied to
+        // LDS (s_ent from s_off[h]) when all lists' chunk entries fit, else read in place
+        constexpr uint32_t kEnt = 2048;
+        __shared__ uint32_t s_off[kHeavyMax + 1], s_ent[kEnt];
+        const uint32_t nh = hs->n;
+        uint32_t lo = 0, hi = 0;
+        if (threadIdx.x < nh) {
+            const uint32_t *L = hl + hs->lbase[threadIdx.x];
+            const uint32_t m = hs->lcnt[threadIdx.x];
+            uint32_t l = 0, r = m;   // first entry with index > b0
+            while (l < r) { const uint32_t md = (l + r) >> 1; if ((L[md] >> 1) <= b0) l = md + 1; else r = md; }
+            lo = l ? l - 1 : 0;
+            r = m;                   // first entry with index >= b0 + nb
+            while (l < r) { const uint32_t md = (l + r) >> 1; if ((L[md] >> 1) < b0 + nb) l = md + 1; else r = md; }
+            hi = m == 0 ? 0 : l > lo ? l : lo + 1;   // (a source without packets: no entries)
+            s_lo[threadIdx.x] = lo;
+            s_hi[threadIdx.x] = hi;
+        }
+        uint32_t tot;
+        const uint32_t off = block256_excl(threadIdx.x < nh ? hi - lo : 0u, s_tmp4, &tot);
+        const bool staged = tot <= kEnt;
+        if (threadIdx.x < nh) {
+            s_off[threadIdx.x] = off;
+            if (staged) {
+                const uint32_t *L = hl + hs->lbase[threadIdx.x];
+                for (uint32_t e = lo; e < hi; ++e) s_ent[off + e - lo] = L[e];
+            }
+        }
+        __syncthreads();
+        for (uint32_t q = threadIdx.x; q < nb; q += 256) {
+            const uint32_t v = s_v[q];
+            if (v < 0x80u) continue;
+            const uint32_t h = v & 0x7Fu, i = b0 + q;
+            uint32_t l = 0, r = s_hi[h] - s_lo[h];   // last entry with index <= i
+            const uint32_t *L = staged ? s_ent + s_off[h] : hl + hs->lbase[h] + s_lo[h];
+            while (r - l > 1) { const uint32_t md = (l + r) >> 1; if ((L[md] >> 1) <= i) l = md; else r = md; }
+            s_v[q] = (L[l] & 1u) ? XDP_DROP : XDP_PASS;
+        }
+    }
     __syncthreads();
     if (vec) {
         uint4 *dst = reinterpret_cast<uint4 *>(verdict + b0);
@@ -1829,6 +2071,9 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
     } else {
         for (int p = 0; p < 4; ++p) { dp.shift[p] = 32u + dbits * (uint32_t)p; dp.mask[p] = dmask; }
     }
+    // heavy verdict lists (fixed window with the heavy-source sort; FSX_NO_HEAVY_LISTS=1: A/B)
+    static const bool no_hlists = getenv("FSX_NO_HEAVY_LISTS") != nullptr;
+    const bool tagh = heavy_sort && do_limit && lim.limiter == 0 && verdict && !no_hlists;
     {
         const uint32_t g = std::min<uint32_t>(256u * FSX_PARSE_MINB, ntiles);   // one resident block per slot
         const HeavySet *hs = heavy_sort ? sc.heavy : nullptr;
@@ -1837,7 +2082,7 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
         // rule-free parse keeps its registers)
         const bool rl = do_limit && rules.slot;
 #define FSX_PARSE(R, Q) k_parse<R, Q><<<g, 256, 0, st>>>(in, len, ts, n, sc.packed[0], verdict, bs, idt, \
-                                                        sc.sort_ctl, th, tcap, dp, hs, rules)
+                                                        sc.sort_ctl, th, tcap, dp, hs, rules, tagh ? 1u : 0u)
         if (!in.rec)
             rl ? FSX_PARSE(0, true) : FSX_PARSE(0, false);
         else if (in.rec_bytes == 16)
@@ -1883,6 +2128,8 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
         std::swap(sc.pay[0], sc.pay[1]);
     }
     uint64_t *S = sc.packed[0];
+    // heavy verdict lists live in the sort's other buffer (free from here on)
+    const HeavyLists hlists{tagh ? reinterpret_cast<uint32_t *>(sc.packed[1]) : nullptr, sc.heavy, tstate, bs};
     k_heads_count<<<gridTiles, 256, 0, st>>>(S, bs, in.hdr, sc.headf, sc.tile_aux, sc.sub_cnt);
     mark("k_heads_count");
     k_scan_tiles_u32<<<1, 1024, 0, st>>>(sc.tile_aux, bs, sc.seg_start);
@@ -1931,22 +2178,28 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
             }
             k_walk_fixed_long<<<1024, 256, 0, fork3 ? st3 : st>>>(S, bs, sc.seg_start, sc.seg_slot, ts, len,
                                                                   sc.pay[0], sc.seg_order, cls, sc.marks,
-                                                                  table, lim);
+                                                                  table, lim, hlists);
             mark_on("k_walk_fixed_long", fork3 ? 2 : 0);
+            if (tagh) {   // pass 0's digit counts / bases of the heavy buckets: their runs
+                k_walk_heavy<<<kHeavyMax / 4, 256, 0, fork3 ? st3 : st>>>(S, bs, sc.sort_ctl, sc.gbase, ts, len,
+                                                                          sc.pay[0], table, lim, hlists);
+                mark_on("k_walk_heavy", fork3 ? 2 : 0);
+            }
             if (fork3 && (e = hipEventRecord(walk_join_ev, st3)) != hipSuccess) return e;
             k_walk_fixed<<<gridStream, 256, 0, st>>>(S, bs, sc.seg_start, sc.seg_slot, ts, len, sc.pay[0],
-                                                     sc.seg_order, cls, sc.marks, table, lim);
+                                                     sc.seg_order, cls, sc.marks, table, lim, hlists);
             mark("k_walk_fixed");
             if (fork3 && (e = hipStreamWaitEvent(st, walk_join_ev, 0)) != hipSuccess) return e;
         }
     }
-    k_fill_last<<<gridTiles, 256, 0, st>>>(sc.marks, bs, sc.tile_last);
-    k_fill_carry<<<1, 1024, 0, st>>>(sc.tile_last, bs);
+    k_fill_last<<<gridTiles, 256, 0, st>>>(sc.marks, bs, sc.tile_last, tagh ? 1u : 0u);
+    k_fill_carry<<<1, 1024, 0, st>>>(sc.tile_last, bs, tagh ? 1u : 0u);
     mark("k_fill_last");
     k_fill_scatter<<<gridTiles, 256, 0, st>>>(sc.marks, S, bs, sc.tile_last, sc.drop_list, sc.drop_cur,
-                                              tstate, cdiv(n, kVChunk));
+                                              tstate, cdiv(n, kVChunk), tagh ? 1u : 0u);
     mark("k_fill_scatter");
-    k_verdict_apply<<<cdiv(n, kVChunk), 256, 0, st>>>(verdict, n, sc.drop_list, sc.drop_cur, bs);
+    k_verdict_apply<<<cdiv(n, kVChunk), 256, 0, st>>>(verdict, n, sc.drop_list, sc.drop_cur, bs, sc.heavy,
+                                                      hlists.list);
     mark("k_verdict_apply");
     if (fork && (e = hipStreamWaitEvent(st, join_ev, 0)) != hipSuccess) return e;
     return hipGetLastError();

@@ -259,6 +259,11 @@ struct HeavySet {
     uint32_t tag[kHeavyMax];
     uint32_t key[kHeavyMax][4];
     uint32_t slot[kHeavyMax];
+    // heavy verdict lists (fixed window): heavy source h's verdict changes
+    // are lcnt[h] entries {arrival index << 1 | DROP} at list + lbase[h] (written by the
+    // walker of its segment; read by k_verdict_apply for the packets k_parse tagged 0x80 | h)
+    uint32_t lbase[kHeavyMax];
+    uint32_t lcnt[kHeavyMax];
     // open addressing on the source's probe start (its table hash) modulo the map size:
     // heavy index + 1, 0 empty
     alignas(16) uint8_t map[1u << kHeavyMapBits];

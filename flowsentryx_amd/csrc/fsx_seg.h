@@ -182,15 +182,38 @@ __device__ __forceinline__ uint32_t search_gt(const SV &sv, uint32_t lo, uint32_
     else return gallop_gt(sv, lo, hi, X);
 }
 
-template <bool kWave>
+// Verdict-change marks of a segment: marks[pos] = the verdict from sorted position pos on
+// (fill-forward by k_fill_*), or, in list mode (a heavy source's segment),
+// an ordered list of {arrival index << 1 | DROP} of the packets where the verdict
+// changes, stored over the segment's own positions, plus the PASS / DROP packet counts.
+template <bool kWave, bool kList = false>
 struct MarkWriter {
     uint8_t *marks;
     uint8_t last;
+    uint32_t *list = nullptr;     // kList: entry e at list[e]
+    const uint64_t *S = nullptr;  // sort words (arrival index of a position)
+    uint32_t nl = 0, last_pos = 0;
+    uint64_t npass = 0, ndrop = 0;
     __device__ __forceinline__ void emit(uint32_t pos, uint8_t v) {
         if (v != last) {
-            if (!kWave || lane_id() == 0) marks[pos] = v;
+            if constexpr (kList) {
+                if (last == XDP_DROP) ndrop += pos - last_pos;
+                else if (last) npass += pos - last_pos;
+                const uint32_t e = pk_idx(S[pos]) << 1 | (v == XDP_DROP ? 1u : 0u);
+                if (!kWave || lane_id() == 0) list[nl] = e;
+                ++nl;
+                last_pos = pos;
+            } else if (!kWave || lane_id() == 0) {
+                marks[pos] = v;
+            }
             last = v;
         }
+    }
+    // list mode: close the counts at the segment end b
+    __device__ __forceinline__ void finish(uint32_t b) {
+        if (last == XDP_DROP) ndrop += b - last_pos;
+        else if (last) npass += b - last_pos;
+        last_pos = b;
     }
 };
 
