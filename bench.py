@@ -313,7 +313,11 @@ def main():
                                "record_bytes": sorted(plane.formats) or None,
                                "backend": args.dist_backend}
             out["stats"] = plane.stats()
-            out["sources"] = None   # per-owner chunks; see the exchange counts
+            out["sources"] = None
+            if with_flows:   # one row per source on its owner: the global distinct sources
+                rows = int(eng.flows["rows"].item())
+                out["sources"] = sum_over_ranks(rows)
+                out["malicious_sources"] = sum_over_ranks(int(eng.flows["dec"][:rows].sum().item()))
         else:
             out["stats"] = ctx.stats()
             out["sources"] = info["sources"]

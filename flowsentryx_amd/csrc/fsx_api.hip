@@ -76,6 +76,11 @@ struct fsx_ctx {
     // per-source flow accumulators
     void *d_flow_acc = nullptr;
     uint64_t flow_acc_cap = 0;
+    // fsx_flows_begin .. fsx_flows_end: per table slot sums carried across calls
+    void *d_slot_acc = nullptr;
+    unsigned long long *d_flow_rows = nullptr;
+    uint32_t flow_epoch = 0;
+    bool flow_accum = false;
     // prefix blocklists (FSX_MAP_IPV4_PREFIX / _IPV6_PREFIX): the host copy is the map;
     // the device probe table is rebuilt from it before the next batch after a change
     std::map<std::array<uint32_t, 5>, uint64_t> rules;   // {family << 8 | len, addr words}
@@ -231,6 +236,7 @@ void fsx_close(fsx_ctx *c) {
     hipFree(c->table); hipFree(c->tstate); hipFree(c->bs);
     hipFree(c->d_hdr); hipFree(c->d_len); hipFree(c->d_ts); hipFree(c->d_verdict);
     hipFree(c->d_feat); hipFree(c->d_prob); hipFree(c->d_dec); hipFree(c->d_flow_acc);
+    hipFree(c->d_slot_acc); hipFree(c->d_flow_rows);
     hipFree(c->d_res); hipFree(c->d_val);
     for (int b = 0; b < 2; ++b) { hipFree(c->hist.t[b]); hipFree(c->hist.l[b]); }
     hipFree(c->hist.tile_cnt); hipFree(c->hist.tile_off); hipFree(c->hist.total);
@@ -591,6 +597,10 @@ static FlowRequest flow_request(fsx_ctx *c, uint8_t *keys16, uint8_t *fam, float
                                 uint8_t *dec, size_t cap) {
     FlowRequest fr{};
     fr.keys16 = keys16; fr.fam = fam; fr.feat = feat; fr.cap = (uint32_t)std::min<size_t>(cap, 0xFFFFFFFFu);
+    if (c->flow_accum) {   // rows come from fsx_flows_end
+        fr.sacc = c->d_slot_acc;
+        fr.epoch = c->flow_epoch;
+    }
     if (c->model_loaded && prob && dec) {
         fr.prob = prob; fr.dec = dec;
         fr.score = make_score_params(c->w, c->inv_in, c->zp_in, c->bias_over_ats, c->mult, c->zp_out, c->lut);
@@ -612,7 +622,7 @@ int fsx_process_batch_device(fsx_ctx *c, const uint8_t *d_hdr, const uint32_t *d
                              uint8_t *d_family, float *d_features, float *d_prob,
                              uint8_t *d_malicious, size_t flow_cap) {
     if (!c) return -EINVAL;
-    if (n && (!d_hdr || !d_len || !d_ts || !d_verdict || !d_keys16 || !d_family))
+    if (n && (!d_hdr || !d_len || !d_ts || !d_verdict || (!c->flow_accum && (!d_keys16 || !d_family))))
         return set_err(c, -EINVAL, "null buffer");
     const FlowRequest fr = flow_request(c, d_keys16, d_family, d_features, d_prob, d_malicious, flow_cap);
     return run_batch(c, PacketIn{d_hdr, nullptr, 0, nullptr, nullptr}, d_len, d_ts, n, d_verdict, true, &fr);
@@ -651,7 +661,7 @@ int fsx_process_records_device(fsx_ctx *c, const void *d_records, size_t n, uint
                                uint8_t *d_verdict, uint8_t *d_keys16, uint8_t *d_family, float *d_features,
                                float *d_prob, uint8_t *d_malicious, size_t flow_cap) {
     if (!c) return -EINVAL;
-    if (n && (!d_keys16 || !d_family)) return set_err(c, -EINVAL, "null buffer");
+    if (n && !c->flow_accum && (!d_keys16 || !d_family)) return set_err(c, -EINVAL, "null buffer");
     const FlowRequest fr = flow_request(c, d_keys16, d_family, d_features, d_prob, d_malicious, flow_cap);
     return run_records(c, d_records, n, rec_bytes, d_verdict, &fr);
 }
@@ -980,6 +990,40 @@ int fsx_flow_features(fsx_ctx *c, const uint8_t *hdr, const uint32_t *len, const
     return 0;
 }
 
+int fsx_flows_begin(fsx_ctx *c) {
+    if (!c) return -EINVAL;
+    int rc = sel(c);
+    if (rc) return rc;
+    if (!c->d_slot_acc) {
+        if (c->pending && (rc = fsx_sync(c))) return rc;
+        HIPCHK(c, hipMalloc(&c->d_slot_acc, c->slots * slot_acc_bytes()));
+        HIPCHK(c, hipMemsetAsync(c->d_slot_acc, 0, c->slots * slot_acc_bytes(), c->stream));   // epoch 0
+        HIPCHK(c, hipMalloc(&c->d_flow_rows, 8));
+        c->flow_epoch = 0;
+    }
+    if (++c->flow_epoch == 0) {   // (after 2^32 epochs: clear, so no stale epoch can match)
+        HIPCHK(c, hipMemsetAsync(c->d_slot_acc, 0, c->slots * slot_acc_bytes(), c->stream));
+        c->flow_epoch = 1;
+    }
+    c->flow_accum = true;
+    return 0;
+}
+
+int fsx_flows_end(fsx_ctx *c, uint8_t *d_keys16, uint8_t *d_family, float *d_features, float *d_prob,
+                  uint8_t *d_malicious, size_t cap, uint64_t *d_rows) {
+    if (!c || !c->flow_accum) return -EINVAL;
+    if (cap && (!d_keys16 || !d_family)) return set_err(c, -EINVAL, "null buffer");
+    int rc = sel(c);
+    if (rc) return rc;
+    c->flow_accum = false;
+    const FlowRequest fr = flow_request(c, d_keys16, d_family, d_features, d_prob, d_malicious, cap);
+    unsigned long long *cnt = d_rows ? reinterpret_cast<unsigned long long *>(d_rows) : c->d_flow_rows;
+    hipError_t e = launch_flows_end(c->d_slot_acc, c->flow_epoch, c->table, c->slots, fr.keys16, fr.fam, fr.feat,
+                                    fr.prob, fr.dec, fr.cap, fr.score, cnt, c->stream);
+    if (e != hipSuccess) return set_err(c, -EIO, "flows end: %s", hipGetErrorString(e));
+    return 0;
+}
+
 int fsx_last_batch_info(fsx_ctx *c, uint64_t *info, int cap) {
     if (!c || (!info && cap > 0)) return -EINVAL;
     int rc = sel(c);
@@ -1054,7 +1098,7 @@ int fsx_blocklist_export_device(fsx_ctx *c, void *d_entries, size_t cap, uint64_
     if (!c || !d_count || (cap && !d_entries)) return -EINVAL;
     int rc = sel(c);
     if (rc) return rc;
-    if (c->pending && (rc = fsx_sync(c))) return rc;
+    // (stream-ordered after a pending batch; its errors surface at the next fsx_sync)
     hipError_t e = launch_blocklist_export(c->table, c->lim.table_mask, reinterpret_cast<ShardBlock *>(d_entries),
                                            cap, reinterpret_cast<unsigned long long *>(d_count), c->stream);
     if (e != hipSuccess) return set_err(c, -EIO, "blocklist export: %s", hipGetErrorString(e));

@@ -2148,7 +2148,8 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
         if ((e = launch_flows(S, sc.pay[0], bs, sc.headf, len, ts, in, sc.tile_aux, sc.sub_cnt, sc.seg_start,
                               sc.flow_first, sc.flow_last, sc.span_list, flows->acc, flows->keys16,
                               flows->fam, flows->feat, flows->prob, flows->dec, flows->cap, flows->score,
-                              lim.salt32, n, fs)) != hipSuccess)
+                              lim.salt32, n, do_limit ? flows->sacc : nullptr, flows->epoch, sc.seg_slot,
+                              fs)) != hipSuccess)
             return e;
         mark_on("k_flow_features", fork ? 1 : 0);
         if (fork && (e = hipEventRecord(join_ev, st2)) != hipSuccess) return e;

@@ -72,6 +72,18 @@ __device__ __forceinline__ FlowAcc wave_sum_acc(FlowAcc a) {
     return a;
 }
 
+// A source's sums carried across the calls of one fsx_flows_begin .. fsx_flows_end
+// epoch (the sharded owner receives a source's packets over several sub-batches, in
+// global arrival order): merging call B after call A adds B's sums plus the gap
+// d = first_t(B) - last_t(A) to the inter-arrival sums; dport is the first call's.
+struct SlotAcc {
+    uint64_t n, s1, dmax, last_t;
+    u128 s2, d1, d2;
+    uint32_t dport, epoch;
+    uint32_t pad_[2];
+};
+static_assert(sizeof(SlotAcc) == 96, "SlotAcc layout");
+
 struct FlowOut {
     FlowAcc *acc;  // per source: exact sums (finished by k_flow_finish)
     uint8_t *keys16;
@@ -80,6 +92,10 @@ struct FlowOut {
     float *prob;   // may be null
     uint8_t *dec;  // may be null
     uint32_t cap;
+    SlotAcc *sacc;             // accumulate mode (else null)
+    uint32_t epoch;
+    const uint32_t *seg_slot;  // table slot of each source (accumulate mode)
+    const uint64_t *ts;        // arrival timestamps (first / last packet of a source)
 };
 
 // L4 destination port of the source's first packet (oracle fsxo_dst_port).
@@ -106,12 +122,17 @@ __device__ __forceinline__ void acc_store(const FlowOut &out, uint32_t g, const 
     if (g < out.cap) out.acc[g] = a;
 }
 
-// Features of source g from its exact sums, then the q8 score.
+__device__ void write_row(uint32_t g, const FlowAcc &a, uint32_t tag, const uint32_t k[4],
+                          uint32_t dport, const FlowOut &out, const ScoreParams &P);
+
+// Features of source g from its exact sums, then the q8 score (accumulate mode: the sums
+// merge into the source's SlotAcc instead).
 __device__ void flow_finish(uint32_t g, const FlowAcc &a, const uint64_t *S,
                             const uint32_t *seg_start, const PacketIn &in, const uint32_t *len,
                             uint32_t salt, const FlowOut &out, const ScoreParams &P) {
     if (g >= out.cap) return;
-    const uint64_t v = S[seg_start[g]];
+    const uint32_t p0 = seg_start[g];
+    const uint64_t v = S[p0];
     uint32_t k[4];
     const uint32_t idx = pk_idx(v);
     uint32_t tag, dport;
@@ -123,6 +144,30 @@ __device__ void flow_finish(uint32_t g, const FlowAcc &a, const uint64_t *S,
         tag = key_of(v, in.hdr, salt, k);
         dport = dst_port(in.hdr + (size_t)idx * 64, len[idx]);
     }
+    if (out.sacc) {
+        SlotAcc &m = out.sacc[out.seg_slot[g]];
+        const uint64_t t0 = out.ts[idx], t1 = out.ts[pk_idx(S[seg_start[g + 1] - 1])];
+        if (m.epoch != out.epoch) {   // the source's first call of this epoch
+            m.n = a.n; m.s1 = a.s1; m.s2 = a.s2; m.d1 = a.d1; m.d2 = a.d2; m.dmax = a.dmax;
+            m.dport = dport;
+            m.epoch = out.epoch;
+        } else {
+            const uint64_t d = t0 - m.last_t;
+            m.n += a.n; m.s1 += a.s1; m.s2 += a.s2;
+            m.d1 += a.d1 + (u128)d;
+            m.d2 += a.d2 + (u128)d * d;
+            const uint64_t mx = a.dmax > d ? a.dmax : d;
+            m.dmax = mx > m.dmax ? mx : m.dmax;
+        }
+        m.last_t = t1;
+        return;
+    }
+    write_row(g, a, tag, k, dport, out, P);
+}
+
+// Output row g: key, family, the eight features, q8 probability / decision.
+__device__ void write_row(uint32_t g, const FlowAcc &a, uint32_t tag, const uint32_t k[4],
+                          uint32_t dport, const FlowOut &out, const ScoreParams &P) {
     uint32_t *kw = reinterpret_cast<uint32_t *>(out.keys16 + (size_t)g * 16);
     kw[0] = k[0]; kw[1] = k[1]; kw[2] = k[2]; kw[3] = k[3];
     out.fam[g] = tag == 1 ? 4 : 6;
@@ -381,9 +426,9 @@ hipError_t launch_flows(const uint64_t *S, const uint64_t *pay, BatchState *bs, 
                         const uint32_t *sub_cnt, const uint32_t *seg_start, void *firstp, void *lastp,
                         uint32_t *span_list, void *acc, uint8_t *keys16, uint8_t *fam, float *feat,
                         float *prob, uint8_t *dec, uint32_t cap, const ScoreParams &P, uint32_t salt,
-                        uint32_t n, hipStream_t st) {
+                        uint32_t n, void *sacc, uint32_t epoch, const uint32_t *seg_slot, hipStream_t st) {
     (void)hipGetLastError();   // a stale error of another caller is not ours
-    const FlowOut out{(FlowAcc *)acc, keys16, fam, feat, prob, dec, cap};
+    const FlowOut out{(FlowAcc *)acc, keys16, fam, feat, prob, dec, cap, (SlotAcc *)sacc, epoch, seg_slot, ts};
     const uint32_t nsub = (n + kFT - 1) / kFT;
     const uint32_t grid = std::max<uint32_t>(1, std::min<uint32_t>(16384, (nsub + 3) / 4));
     k_flow_tile<<<grid, 256, 0, st>>>(S, pay, bs, headf, len, ts, in, tile_off, sub_cnt, seg_start,
@@ -396,5 +441,37 @@ hipError_t launch_flows(const uint64_t *S, const uint64_t *pay, BatchState *bs, 
 }
 
 size_t flow_acc_bytes() { return sizeof(FlowAcc); }
+size_t slot_acc_bytes() { return sizeof(SlotAcc); }
+
+// The rows of an accumulation epoch: every slot merged in it, in slot order of arrival at
+// the row counter (rows unordered), features + score from the carried sums.
+__global__ __launch_bounds__(256) void k_flows_end(const SlotAcc *__restrict__ sacc, uint32_t epoch,
+                                                   const Slot *__restrict__ table, uint64_t slots,
+                                                   FlowOut out, ScoreParams P,
+                                                   unsigned long long *count) {
+    for (uint64_t s = (uint64_t)blockIdx.x * 256u + threadIdx.x; s < slots; s += (uint64_t)gridDim.x * 256u) {
+        const SlotAcc &m = sacc[s];
+        if (m.epoch != epoch) continue;
+        const unsigned long long g = atomicAdd(count, 1ull);
+        if (g >= out.cap) continue;
+        FlowAcc a = acc_zero();
+        a.n = m.n; a.s1 = m.s1; a.s2 = m.s2; a.d1 = m.d1; a.d2 = m.d2; a.dmax = m.dmax;
+        const Slot &sl = table[s];
+        write_row((uint32_t)g, a, sl.tag, sl.key, m.dport, out, P);
+    }
+}
+
+hipError_t launch_flows_end(const void *sacc, uint32_t epoch, const Slot *table, uint64_t slots,
+                            uint8_t *keys16, uint8_t *fam, float *feat, float *prob, uint8_t *dec,
+                            uint32_t cap, const ScoreParams &P, unsigned long long *d_count,
+                            hipStream_t st) {
+    (void)hipGetLastError();
+    const FlowOut out{nullptr, keys16, fam, feat, prob, dec, cap, nullptr, epoch, nullptr, nullptr};
+    hipError_t e = hipMemsetAsync(d_count, 0, 8, st);
+    if (e != hipSuccess) return e;
+    const uint32_t grid = (uint32_t)std::min<uint64_t>(4096, (slots + 255) / 256);
+    k_flows_end<<<grid, 256, 0, st>>>((const SlotAcc *)sacc, epoch, table, slots, out, P, d_count);
+    return hipGetLastError();
+}
 
 }  // namespace fsx

@@ -311,6 +311,10 @@ struct FlowRequest {
     uint32_t cap;
     ScoreParams score;
     void *acc;        // cap x FlowAcc scratch (owned by the context)
+    // accumulate mode (fsx_flows_begin .. fsx_flows_end): every source's sums merge into
+    // its table slot's SlotAcc of this epoch instead of becoming an output row
+    void *sacc;
+    uint32_t epoch;
 };
 
 // do_limit: run the rate limiter (verdicts + maps); flows: also per-source features.
@@ -376,8 +380,14 @@ hipError_t launch_flows(const uint64_t *S, const uint64_t *pay, BatchState *bs, 
                         const uint32_t *sub_cnt, const uint32_t *seg_start, void *firstp, void *lastp,
                         uint32_t *span_list, void *acc, uint8_t *keys16, uint8_t *fam, float *feat,
                         float *prob, uint8_t *dec, uint32_t cap, const ScoreParams &P, uint32_t salt,
-                        uint32_t n, hipStream_t st);
+                        uint32_t n, void *sacc, uint32_t epoch, const uint32_t *seg_slot, hipStream_t st);
 size_t flow_acc_bytes();
+size_t slot_acc_bytes();
+// Rows of every source accumulated in epoch `epoch` (slots of the table), *d_count = rows.
+hipError_t launch_flows_end(const void *sacc, uint32_t epoch, const Slot *table, uint64_t slots,
+                            uint8_t *keys16, uint8_t *fam, float *feat, float *prob, uint8_t *dec,
+                            uint32_t cap, const ScoreParams &P, unsigned long long *d_count,
+                            hipStream_t st);
 ScoreParams make_score_params(const int8_t w[8], float inv_in, int32_t zp_in, float bias_over_ats,
                               float mult, int32_t zp_out, const uint8_t lut[256]);
 

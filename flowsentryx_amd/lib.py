@@ -134,6 +134,8 @@ def load_library() -> C.CDLL:
         "fsx_score": (C.c_int, [vp, vp, sz, vp, vp]),
         "fsx_score_device": (C.c_int, [vp, vp, sz, vp, vp]),
         "fsx_flow_features": (C.c_int, [vp, vp, vp, vp, sz, sz, vp, vp, vp, C.POINTER(sz)]),
+        "fsx_flows_begin": (C.c_int, [vp]),
+        "fsx_flows_end": (C.c_int, [vp, vp, vp, vp, vp, vp, sz, vp]),
         "fsx_last_timings": (C.c_int, [vp, vp, vp, vp, C.c_int, C.c_int, C.POINTER(C.c_int)]),
         "fsx_enable_timing": (C.c_int, [vp, C.c_int]),
         "fsx_last_batch_info": (C.c_int, [vp, vp, C.c_int]),
@@ -163,6 +165,7 @@ ABI_SYMBOLS = [
     "fsx_map_lookup", "fsx_map_update", "fsx_map_update_batch", "fsx_map_delete", "fsx_map_dump",
     "fsx_get_stats",
     "fsx_reset", "fsx_load_q8_model", "fsx_score", "fsx_score_device", "fsx_flow_features",
+    "fsx_flows_begin", "fsx_flows_end",
     "fsx_last_timings", "fsx_enable_timing", "fsx_last_batch_info",
     "fsx_shard_owner", "fsx_shard_pack_device", "fsx_shard_unpack_device", "fsx_shard_unpack16_device",
     "fsx_shard_scatter_device", "fsx_shard_clock_device", "fsx_blocklist_export_device",
@@ -455,6 +458,16 @@ class FsxContext:
                                                 C.byref(nf)), "fsx_flow_features")
         m = nf.value
         return keys[:m], fam[:m], feat[:m]
+
+    def flows_begin(self):
+        """Start accumulating one global batch's per-source sums over several calls."""
+        self._check(self._lib.fsx_flows_begin(self._h), "fsx_flows_begin")
+
+    def flows_end(self, d_keys16: int, d_family: int, d_features: int | None, d_prob: int | None,
+                  d_malicious: int | None, cap: int, d_rows: int | None):
+        """Rows of every source accumulated since flows_begin (device pointers, async)."""
+        self._check(self._lib.fsx_flows_end(self._h, d_keys16, d_family, d_features, d_prob,
+                                            d_malicious, cap, d_rows), "fsx_flows_end")
 
     BATCH_INFO = ("ip_packets", "sources", "new_sources", "any_ipv6", "non_monotone",
                   "max_len", "max_ts", "allowed", "dropped", "prefix_rule_drops", "sorted_payload",

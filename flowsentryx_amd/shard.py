@@ -23,6 +23,10 @@ unchanged batch pipeline on all of that source's packets:
      in global order (one all-gather of {min, max, decreases} per rank), which is exactly
      the condition under which no earlier packet can have deleted the entry
   6. stats_map = all-reduce(sum) of the owners' counters + the locally dropped packets
+  7. with flow features (HipShardEngine.enable_flows): every owner accumulates its sources'
+     sums over the batch's sub-batches (fsx_flows_begin / fsx_flows_end) and writes one row
+     per owned source at the end of the batch — the row the 1-GPU run over the whole batch
+     gives; the replica filter (5) is off then, so every packet reaches its owner
 
 A global batch is cut into `chunks` sub-batches; in sub-batch i every rank contributes
 the i-th piece of its slice, and the global order of a sub-batch is rank 0's piece,
@@ -141,12 +145,28 @@ class HipShardEngine:
         return self._oh
 
     def enable_flows(self, cap: int):
-        """Per owned source: key, family, q8 probability and decision of every batch."""
+        """Per owned source of every global batch: key, family, the eight features, q8
+        probability and decision, over ALL of the source's packets of the batch (its
+        sub-batches accumulate, fsx_flows_begin / fsx_flows_end); rows[0] = row count."""
         d = self.device
         self.flows = dict(keys=torch.empty(cap * 16, dtype=torch.uint8, device=d),
                           fam=torch.empty(cap, dtype=torch.uint8, device=d),
+                          feat=torch.empty(cap * 8, dtype=torch.float32, device=d),
                           prob=torch.empty(cap, dtype=torch.float32, device=d),
-                          dec=torch.empty(cap, dtype=torch.uint8, device=d), cap=cap)
+                          dec=torch.empty(cap, dtype=torch.uint8, device=d),
+                          rows=torch.zeros(1, dtype=torch.int64, device=d), cap=cap)
+
+    def flows_begin(self):
+        if self.flows is not None:
+            self.ctx.flows_begin()
+
+    def flows_end(self):
+        """The batch's rows into self.flows (asynchronous; rows[0] = their count)."""
+        if self.flows is None:
+            return
+        f = self.flows
+        self.ctx.flows_end(f["keys"].data_ptr(), f["fam"].data_ptr(), f["feat"].data_ptr(),
+                           f["prob"].data_ptr(), f["dec"].data_ptr(), f["cap"], f["rows"].data_ptr())
 
     def direct(self, hdr, length, ts, n, verdict):
         """G == 1: the batch pipeline straight on the local slice."""
@@ -163,7 +183,8 @@ class HipShardEngine:
         else:
             f = self.flows
             self.ctx.process_records_device(rec, n, rb, v, f["keys"].data_ptr(), f["fam"].data_ptr(),
-                                            None, f["prob"].data_ptr(), f["dec"].data_ptr(), f["cap"])
+                                            f["feat"].data_ptr(), f["prob"].data_ptr(), f["dec"].data_ptr(),
+                                            f["cap"])
 
     def _run(self, h, l, t, n, v):
         if self.flows is None:
@@ -171,7 +192,8 @@ class HipShardEngine:
         else:
             f = self.flows
             self.ctx.process_batch_device(h, l, t, n, v, f["keys"].data_ptr(), f["fam"].data_ptr(),
-                                          None, f["prob"].data_ptr(), f["dec"].data_ptr(), f["cap"])
+                                          f["feat"].data_ptr(), f["prob"].data_ptr(), f["dec"].data_ptr(),
+                                          f["cap"])
 
     def clock(self, ts, n) -> torch.Tensor:
         self.ctx.shard_clock_device(ts.data_ptr(), n, self.clock3.data_ptr())
@@ -295,15 +317,24 @@ class ShardedDataPlane:
         sub-batch j + 1 (collectives on the engine's comm stream) overlap the owner
         pipeline of sub-batch j; buffers alternate between two slots."""
         with self.engine.stream_ctx():
+            flows = getattr(self.engine, "flows", None) is not None
             if self.world == 1:
                 self.engine.direct(hdr, length, ts, n, verdict)
+                if flows:   # one call: its rows are the batch's rows
+                    f = self.engine.flows
+                    f["rows"].fill_(-1)   # (count: ctx.last_batch_info()["sources"])
                 return
-            if self.filter:
+            # with flow features every packet must reach its source's owner (the features
+            # are over all of the source's packets), so the replica filter is off
+            filt_on = self.filter and not flows
+            if flows:
+                self.engine.flows_begin()
+            if filt_on:
                 self._sync_blocklist()   # maps may have changed since the last batch
             if bounds is None:
                 bounds = [n * i // chunks for i in range(chunks + 1)]
             k = len(bounds) - 1
-            filt = self._filter_plan(ts, bounds) if self.filter else [False] * k
+            filt = self._filter_plan(ts, bounds) if filt_on else [False] * k
             pend = [None] * k
             pend[0] = self._stage_exchange(hdr, length, ts, verdict, bounds, 0, filt[0])
             sent = recv = 0
@@ -316,8 +347,10 @@ class ShardedDataPlane:
                 sent, recv = sent + ms, recv + mr
                 # the replica packs j + 2 onward filter with (one sub-batch stale: exact for
                 # clocks that do not go back between consecutive sub-batches, _filter_plan)
-                if self.filter and j + 2 < k:
+                if filt_on and j + 2 < k:
                     self._sync_blocklist()
+            if flows:
+                self.engine.flows_end()
             self.last_exchange = {"sent": sent, "received": recv, "filtered": self.filtered}
 
     def _filter_plan(self, ts, bounds) -> list:

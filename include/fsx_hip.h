@@ -220,6 +220,17 @@ int fsx_score(fsx_ctx *ctx, const float *features, size_t n, float *prob,
 int fsx_score_device(fsx_ctx *ctx, const float *d_features, size_t n, float *d_prob,
                      uint8_t *d_malicious);
 
+/* One global batch's flow features delivered over several calls (the owner side of the
+ * sharded path, where a source's packets arrive in sub-batches, in global arrival order):
+ * after fsx_flows_begin, every fsx_process_batch_device / fsx_process_records_device call
+ * merges its per-source sums into the source's running sums (table slot) instead of writing
+ * rows (its keys/family/feature/score pointers may be NULL); fsx_flows_end writes one row
+ * per source merged since fsx_flows_begin — exactly the row one call over the whole batch
+ * would give — and the row count to *d_rows (device pointer; NULL: none). Asynchronous. */
+int fsx_flows_begin(fsx_ctx *ctx);
+int fsx_flows_end(fsx_ctx *ctx, uint8_t *d_keys16, uint8_t *d_family, float *d_features,
+                  float *d_prob, uint8_t *d_malicious, size_t cap, uint64_t *d_rows);
+
 /* Per-source-IP flow features (build-defined) for the packets of
  * one batch (host pointers; the maps are not touched). n_flows_out = distinct
  * source IPs; up to cap rows of keys (16 B), family (4/6) and features (8 x fp32,

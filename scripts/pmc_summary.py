@@ -30,7 +30,7 @@ def load(path):
 def main():
     d = Path(sys.argv[1])
     res = defaultdict(dict)
-    for tag in ("fetch", "write", "sq"):
+    for tag in ("fetch", "write", "sq", "sq2", "tcc"):
         f = d / tag / "run_counter_collection.csv"
         if not f.exists():
             continue
@@ -49,10 +49,17 @@ def main():
             row["hbm_write_bytes"] = cs["WRITE_SIZE"] * 1024
         if "hbm_read_bytes" in row and "hbm_write_bytes" in row:
             row["hbm_bytes_per_launch"] = row["hbm_read_bytes"] + row["hbm_write_bytes"]
+        if cs.get("SQ_WAVE_CYCLES"):
+            row["wait_any_frac"] = cs.get("SQ_WAIT_ANY", 0) / cs["SQ_WAVE_CYCLES"]
+            row["valu_frac"] = cs.get("SQ_ACTIVE_INST_VALU", 0) / cs["SQ_WAVE_CYCLES"]
+            row["lds_frac"] = cs.get("SQ_ACTIVE_INST_LDS", 0) / cs["SQ_WAVE_CYCLES"]
+        if cs.get("TCC_HIT_sum") is not None and cs.get("TCC_MISS_sum") is not None:
+            tot = cs["TCC_HIT_sum"] + cs["TCC_MISS_sum"]
+            row["l2_hit_rate"] = cs["TCC_HIT_sum"] / tot if tot else None
         rows[k] = row
     doc = {"source": f"rocprofv3 --kernel-trace --pmc passes under {d.name} (scripts/gpu_pmc.sh)",
            "workload": {"config": 2, "packets_per_gpu": 67108864, "n_gpus": 1,
-                        "command": "python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline"},
+                        "command": "python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-check --legs ''"},
            "correction": "FETCH_SIZE x2 (gfx950, MI355X_MICROARCH.md HBM section); WRITE_SIZE as read",
            "kernels": rows}
     print(json.dumps(doc, indent=1))

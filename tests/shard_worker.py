@@ -47,6 +47,11 @@ def worker(rank, world, port, spec, out_path, engine_kind):
             dev = torch.device("cuda", 0)
             ctx = lib.FsxContext(max_batch=spec.get("owner_batch", 1 << 16), **cfg)
             eng = HipShardEngine(ctx, max(b - a for a, b in zip(cuts[:-1], cuts[1:])), dev)
+            if spec.get("flows"):   # per-source features + q8 scores of every global batch
+                from pathlib import Path
+                from flowsentryx_amd import fsx_load
+                ctx.load_q8_model(fsx_load.load_weights(Path(__file__).parent / "golden" / "model_weights.json"))
+                eng.enable_flows(cfg["max_entries"])
         plane = ShardedDataPlane(eng, blocklist_filter=spec.get("filter", True))
         k = spec.get("chunks", 1)
         mine = []
@@ -64,7 +69,13 @@ def worker(rank, world, port, spec, out_path, engine_kind):
             tt = torch.from_numpy(ts[idx].view(np.int64).copy()).to(dev)
             tv = torch.zeros(max(n, 1), dtype=torch.uint8, device=dev)
             plane.verdict_batch(th, tl, tt, n, tv, chunks=k, bounds=local_bounds)
-            mine.append((idx, tv[:n].cpu().numpy().copy()))
+            rows = None
+            if spec.get("flows"):
+                f = eng.flows
+                m = int(f["rows"].item())
+                rows = (f["keys"][:m * 16].cpu().numpy().reshape(m, 16).copy(), f["fam"][:m].cpu().numpy().copy(),
+                        f["feat"][:m * 8].cpu().numpy().reshape(m, 8).copy(), f["prob"][:m].cpu().numpy().copy())
+            mine.append((idx, tv[:n].cpu().numpy().copy(), rows))
         stats = plane.stats()
         if engine_kind == "cpu":
             dumps = {m: eng.o.map_dump(m) for m in spec["maps"]}
@@ -79,11 +90,32 @@ def worker(rank, world, port, spec, out_path, engine_kind):
                 exp = o.batch(hdr[a:b], ln[a:b], ts[a:b])
                 v = np.zeros(b - a, dtype=np.uint8)
                 for r in range(world):
-                    ridx, rv = got[r][0][bi]
+                    ridx, rv, _ = got[r][0][bi]
                     v[ridx - a] = rv
                 if not np.array_equal(v, exp):
                     ok = False
                     msg.append(f"batch {bi}: {int((v != exp).sum())} verdicts differ")
+                if spec.get("flows"):
+                    # the union of the owners' rows = the 1-GPU rows over the whole batch
+                    # (features bit-exact, q8 probabilities bit-exact)
+                    from pathlib import Path
+                    model = json.loads((Path(__file__).parent / "golden" / "model_weights.json").read_text())
+                    ko, fo, xo = pyoracle.flow_features(hdr[a:b], ln[a:b], ts[a:b])
+                    po, _, _ = pyoracle.score(model, xo)
+                    want = {(int(fo[i]), ko[i].tobytes()): (xo[i].tobytes(), po[i].tobytes()) for i in range(len(fo))}
+                    have = {}
+                    for r in range(world):
+                        kk, ff, xx, pp = got[r][0][bi][2]
+                        for i in range(len(ff)):
+                            key = (int(ff[i]), kk[i].tobytes())
+                            if key in have:
+                                ok = False
+                                msg.append(f"batch {bi}: source {key} has rows on two owners")
+                            have[key] = (xx[i].tobytes(), pp[i].tobytes())
+                    if have != want:
+                        ok = False
+                        bad = sum(1 for k_ in want if have.get(k_) != want[k_])
+                        msg.append(f"batch {bi}: {len(have)} rows vs {len(want)}, {bad} differ")
             if tuple(stats) != o.stats():
                 ok = False
                 msg.append(f"stats {stats} != {o.stats()}")

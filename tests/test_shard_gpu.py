@@ -77,6 +77,18 @@ def test_sharded_hip_owners(tmp_path, world):
     run_sharded(tmp_path, world, spec, engine="hip")
 
 
+@pytest.mark.parametrize("world,v6", [(2, 0.0), (3, 0.3)])
+def test_sharded_flow_features_equal_one_gpu(tmp_path, world, v6):
+    """Per-source features + q8 scores under sharding: every owner accumulates its sources
+    over the batch's sub-batches (fsx_flows_begin / fsx_flows_end); the union of the rows
+    equals the 1-GPU rows over each whole global batch, bit for bit."""
+    spec = dict(BASE, v6_frac=v6, nonip_frac=0.03, short_frac=0.02, seed=29 + world, flows=True,
+                cfg=dict(pps_threshold=7, window_ns=200_000, block_ns=1_000_000, max_entries=4096),
+                owner_batch=4096)
+    res = run_sharded(tmp_path, world, spec, engine="hip")
+    assert res["filtered"] == 0   # (flows: every packet reaches its owner)
+
+
 def test_sharded_hip_owners_limiters(tmp_path):
     for lim, maps, extra in ((1, [1, 2, 3, 4], dict(pps_threshold=5, window_ns=1_000_000,
                                                      block_ns=50_000)),
