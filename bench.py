@@ -83,6 +83,8 @@ def parse_args():
                     help="comma-separated extra legs ('' for none)")
     ap.add_argument("--leg-steps", type=int, default=5, help="timed steps per leg")
     ap.add_argument("--config5-packets", type=int, default=1 << 28)
+    ap.add_argument("--config4-packets", type=int, default=None,
+                    help="config-4 packets per rank (default: 1/8 of the 1B-packet stream)")
     ap.add_argument("--leg-timing", action="store_true",
                     help="per-kernel device times of the config-4 / config-5 legs (extra steps)")
     ap.add_argument("--config5-oracle", action="store_true",
@@ -538,7 +540,7 @@ def main():
         # BASELINE config 4: the 1B-packet / 16M-source flood over 120 s; rank r holds the
         # r-th 1/8 share of the stream (weak scaling: at N = 8 the whole of config 4)
         p4, _ = synth.config_params(4)
-        n4 = int(p4.n) // 8
+        n4 = args.config4_packets or int(p4.n) // 8
         r4 = run_workload(4, n4, max(1, args.leg_steps // 2), 1, not args.no_mlp,
                           kernel_timing=args.leg_timing, check=not args.no_check and world == 1)
         r4.pop("d")

@@ -10,6 +10,14 @@ namespace fsx {
 // ------------------------------------------------------------------ helpers
 __device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
 
+// Orders this wave's LDS accesses for the compiler (the hardware executes one wave's LDS
+// operations in order). A wavefront-scope fence would also wait for every outstanding
+// global load (s_waitcnt vmcnt(0)), draining software-pipelined prefetches each step.
+__device__ __forceinline__ void wave_lds_order() {
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+}
+
 template <typename T>
 __device__ __forceinline__ T wave_incl_sum(T x) {
     const uint32_t lane = lane_id();

@@ -422,45 +422,39 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
     const uint32_t nsort = (n + kSortTile - 1) / kSortTile;
     constexpr uint32_t kSteps = kSortTile / 256;   // 64-record steps per wave and sort tile
     auto step_of = [&](uint32_t st, uint32_t j) { return st * (kSortTile / 64) + w * kSteps + j; };
-    auto next_step = [&](uint32_t st, uint32_t j, uint32_t &st2, uint32_t &j2) {
-        if (j + 1 < kSteps) { st2 = st; j2 = j + 1; } else { st2 = st + gridDim.x; j2 = 0; }
-    };
     // software pipeline: the next tile's loads are in flight while this one is parsed.
     // Header records: only their first 48 bytes (the parse reads bytes 12..39), as 3 x 16 B
     // per lane: flat chunk f = k * 64 + lane is chunk f % 3 of record f / 3
     constexpr int kHv = kRec == 0 ? 3 : (int)(kRec / 16);   // uint4 registers per lane and step
+    // Unconditional loads (out-of-range lanes read record / packet 0 and are discarded by
+    // the parse's `live`), so every step issues the same loads and s_waitcnt counts stay
+    // exact: a conditional load would make the compiler wait for everything in flight.
     auto load = [&](uint32_t tt, uint4 (&h)[kHv], uint32_t &L_, uint64_t &T_, uint64_t &P_) {
         const uint32_t base = tt << 6;
         const bool tv = tt < ntiles;
         const uint32_t i = base + lane;
         const bool live = tv && i < n;
+        const uint32_t ic = live ? i : 0u;
         if constexpr (kRec == 0) {
-            const uint8_t *src = in.hdr + (size_t)base * 64;
 #pragma unroll
             for (int k = 0; k < 3; ++k) {
                 const uint32_t f = (uint32_t)k * 64u + lane, r = f / 3u, c = f - 3u * r;
-                h[k] = make_uint4(0, 0, 0, 0);
-                if (tv && base + r < n) h[k] = *reinterpret_cast<const uint4 *>(src + r * 64u + c * 16u);
+                const uint32_t rr = tv && base + r < n ? base + r : 0u;
+                h[k] = *reinterpret_cast<const uint4 *>(in.hdr + (size_t)rr * 64u + c * 16u);
             }
-            L_ = live ? len[i] : 0u;
-            T_ = live ? ts[i] : 0ull;
-            P_ = (lane == 0 && live && i > 0) ? ts[i - 1] : 0ull;
+            L_ = len[ic];
+            T_ = ts[ic];
+            P_ = ts[ic > 0 ? ic - 1 : 0];   // (used by lane 0 only: the record before the step)
         } else {
             const uint4 *r = reinterpret_cast<const uint4 *>(in.rec);
             constexpr uint32_t kW = kRec / 16;   // uint4 words per record
-#pragma unroll
-            for (int k = 0; k < kHv; ++k) h[k] = make_uint4(0, 0, 0, 0);
-            if (live) {
-                h[0] = r[(size_t)i * kW];
-                if constexpr (kW == 2) h[1] = r[(size_t)i * kW + 1];
-            }
+            h[0] = r[(size_t)ic * kW];
+            if constexpr (kW == 2) h[1] = r[(size_t)ic * kW + 1];
             L_ = 0u;
             T_ = 0ull;
-            P_ = 0ull;
-            if (lane == 0 && live && i > 0) {   // timestamp of the record before the step
-                const uint4 pr = r[(size_t)(i - 1) * kW + (kW - 1)];
-                P_ = kW == 1 ? ((uint64_t)pr.z | ((uint64_t)pr.w << 32)) : ((uint64_t)pr.x | ((uint64_t)pr.y << 32));
-            }
+            // timestamp of the record before the step (lane 0)
+            const uint4 pr = r[(size_t)(ic > 0 ? ic - 1 : 0) * kW + (kW - 1)];
+            P_ = kW == 1 ? ((uint64_t)pr.z | ((uint64_t)pr.w << 32)) : ((uint64_t)pr.x | ((uint64_t)pr.y << 32));
         }
     };
     // Software pipeline, per wave: iteration j parses step j + 1 (its
@@ -472,9 +466,6 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
     // source READY in the first two slots (new source, longer probe chain, IPv6) is
     // deferred: the wave resolves its deferred packets together (CAS inserts) at the end
     // of the sort tile, or earlier when the LDS list fills.
-    uint4 hv[kHv], hn[kHv];
-    uint32_t Lc, Ln;
-    uint64_t Tc, Pc, Tn, Pn;
     // the parsed step awaiting resolution: tag, key word 0, probe start, heavy index, the
     // two probe reads
     uint32_t c_tag = 0, c_k0 = 0, c_h = 0;
@@ -486,6 +477,8 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
     const uint64_t lt_mask = (1ull << lane) - 1ull;
     // radix histograms of the key digits: block LDS counters (a heavy source repeats in
     // few lanes of one 64-packet step, so same-address serialization stays short)
+    // (FSX_MEASURE_NO_PROBE: a cost-attribution build for scripts/ab.sh only — every
+    // IPv4 source takes its first probe slot, wrong ids but in range; never the product)
     auto count_digits = [&](uint64_t out, int hidx) {
         if (!ghist) return;
         const uint32_t d0 = (uint32_t)(out >> dp.shift[0]) & dp.mask[0];
@@ -524,11 +517,11 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
             nfresh += (uint32_t)__popcll(__ballot(fresh));   // new sources (persistent index)
         }
         ndef = 0;
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        wave_lds_order();
     };
     // parse one step (its records in hv / Lc / Tc / Pc): verdict bytes, clock facts, and
     // the probes of its IP packets into the c_* registers
-    auto parse_step = [&](uint32_t t) {
+    auto parse_step = [&](uint32_t t, const uint4 (&hv)[kHv], uint32_t Lc, uint64_t Tc, uint64_t Pc) {
         const uint32_t base = t << 6;
         const uint32_t i = base + lane;
         const bool live = t < ntiles && i < n;
@@ -544,7 +537,7 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
                 uint32_t *d = rec + r * 17u + c * 4u;
                 d[0] = hv[q].x; d[1] = hv[q].y; d[2] = hv[q].z; d[3] = hv[q].w;
             }
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            wave_lds_order();
             const uint32_t *my = rec + lane * 17u;
             const uint32_t d3 = my[3], d5 = my[5], d6 = my[6], d7 = my[7], d8 = my[8], d9 = my[9];
             tag = live ? parse_src(L, d3, d5, d6, d7, d8, d9, k, v) : 0u;
@@ -594,7 +587,11 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
         // sources are always resolved by the full protocol, which reads their key words
         // only after the head shows READY)
         c_hint0 = c_hint1 = 0;
+#ifdef FSX_MEASURE_NO_PROBE
+        if (false) {
+#else
         if (tag == 1 && !(hres && hidx >= 0)) {
+#endif
             // (coherent=1 reads past the XCD's L2, which may hold the head of an older
             // epoch: a stale head can only fail the match, never fake one)
             const uint64_t h1 = (h + 1) & idt.mask;
@@ -632,6 +629,10 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
             if (hres && c_hidx >= 0) {
                 id = s_hslot[c_hidx];
             } else if (c_tag == 1) {
+#ifdef FSX_MEASURE_NO_PROBE
+                id = c_h;
+                c_hint0 = id_head(idt.gen, kIdReady, 1u, c_k0);
+#endif
                 const uint64_t ready = id_head(idt.gen, kIdReady, 1u, c_k0);
                 if (c_hint0 == ready) id = c_h;
                 else if (c_hint1 == ready) id = (uint32_t)((c_h + 1) & idt.mask);
@@ -655,53 +656,47 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
             count_digits(out, c_hidx);
         }
     };
-    // prologue: steps 0 and 1 loading, step 0 parsed (its probes in flight), step 2 loading
-    load(step_of(blockIdx.x, 0), hv, Lc, Tc, Pc);
-    {
-        uint32_t T1, j1;
-        next_step(blockIdx.x, 0, T1, j1);
-        load(T1 < nsort ? step_of(T1, j1) : ntiles, hn, Ln, Tn, Pn);
-        if (blockIdx.x < nsort) parse_step(step_of(blockIdx.x, 0));
-        uint32_t T2, j2;
-        next_step(T1, j1, T2, j2);
-#pragma unroll
-        for (int q = 0; q < kHv; ++q) hv[q] = hn[q];
-        Lc = Ln; Tc = Tn; Pc = Pn;
-        load(T2 < nsort ? step_of(T2, j2) : ntiles, hn, Ln, Tn, Pn);
-    }
-    for (uint32_t tile = blockIdx.x; tile < nsort; tile += gridDim.x)
-    for (uint32_t j = 0; j < kSteps; ++j) {
-        const uint32_t t = step_of(tile, j);
-        uint32_t T1, j1, T2, j2, T3, j3;
-        next_step(tile, j, T1, j1);
-        next_step(T1, j1, T2, j2);
-        next_step(T2, j2, T3, j3);
-        // C: resolve this step with the probes issued one iteration ago
-        resolve_step(t);
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        if (j == kSteps - 1) {   // sort tile done: its deferred packets, then its digit-0 counts
+    // The wave's steps in order: s -> (tile blockIdx.x + (s / kSteps) * gridDim.x, step
+    // s % kSteps). Three register sets, the loop unrolled by three, so no register holding
+    // an in-flight load is ever moved (a move would wait for the load): iteration s
+    // resolves step s, parses step s + 1 from set (s + 1) % 3 and loads step s + 3 into
+    // set s % 3.
+    const uint32_t my_tiles = nsort > blockIdx.x ? (nsort - blockIdx.x + gridDim.x - 1) / gridDim.x : 0u;
+    const uint32_t S = my_tiles * kSteps;
+    auto tile_of = [&](uint32_t q) { return blockIdx.x + (q / kSteps) * gridDim.x; };
+    auto step_at = [&](uint32_t q) { return q < S ? step_of(tile_of(q), q % kSteps) : ntiles; };
+    uint4 h0[kHv], h1[kHv], h2[kHv];
+    uint32_t L0, L1, L2;
+    uint64_t T0, T1, T2, P0, P1, P2;
+    load(step_at(0), h0, L0, T0, P0);
+    load(step_at(1), h1, L1, T1, P1);
+    load(step_at(2), h2, L2, T2, P2);
+    c_tag = 0; c_hidx = -1; c_hint0 = c_hint1 = 0;
+    if (S) parse_step(step_at(0), h0, L0, T0, P0);
+    auto iter = [&](uint32_t q, const uint4 (&hp)[kHv], uint32_t Lp, uint64_t Tp, uint64_t Pp,
+                    uint4 (&hl)[kHv], uint32_t &Ll, uint64_t &Tl, uint64_t &Pl) {
+        // C: resolve step q with the probes issued one iteration ago
+        resolve_step(step_at(q));
+        wave_lds_order();
+        if (q % kSteps == kSteps - 1) {   // sort tile done: its deferred packets, then its digit-0 counts
             flush();
             if (thist) {
                 __syncthreads();
-                if (threadIdx.x <= dp.mask[0]) thist[(size_t)threadIdx.x * tcap + tile] = s_t0[threadIdx.x];
+                if (threadIdx.x <= dp.mask[0]) thist[(size_t)threadIdx.x * tcap + tile_of(q)] = s_t0[threadIdx.x];
                 s_t0[threadIdx.x] = 0;
                 __syncthreads();
             }
         }
-        // A: parse the next step (records loaded two iterations ago), its probes issued
+        // A: parse step q + 1 (its records were loaded two iterations ago), probes issued
         c_tag = 0; c_hidx = -1; c_hint0 = c_hint1 = 0;
-        if (T1 < nsort) parse_step(step_of(T1, j1));
-        // B: the record loads of step + 3
-        {
-            uint4 h2[kHv];
-            uint32_t L2;
-            uint64_t Tn2, Pn2;
-            load(T3 < nsort ? step_of(T3, j3) : ntiles, h2, L2, Tn2, Pn2);
-#pragma unroll
-            for (int q = 0; q < kHv; ++q) { hv[q] = hn[q]; hn[q] = h2[q]; }
-            Lc = Ln; Tc = Tn; Pc = Pn;
-            Ln = L2; Tn = Tn2; Pn = Pn2;
-        }
+        if (q + 1 < S) parse_step(step_at(q + 1), hp, Lp, Tp, Pp);
+        // B: the record loads of step q + 3 into the set step q used
+        load(step_at(q + 3), hl, Ll, Tl, Pl);
+    };
+    for (uint32_t q = 0; q < S; q += 3) {
+        iter(q, h1, L1, T1, P1, h0, L0, T0, P0);
+        if (q + 1 < S) iter(q + 1, h2, L2, T2, P2, h1, L1, T1, P1);
+        if (q + 2 < S) iter(q + 2, h0, L0, T0, P0, h2, L2, T2, P2);
     }
     if (ghist) {
         __syncthreads();

@@ -243,7 +243,7 @@ __device__ __forceinline__ void flow_tiles(const uint64_t *__restrict__ S,
             const uint32_t p = base + e;
             sS[(e >> 4) * 17u + (e & 15u)] = p < M ? src[p] : 0ull;
         }
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        wave_lds_order();
         uint32_t hf[4] = {0, 0, 0, 0};
         if (p0 + 16 <= M) {
             const uint4 h4 = *reinterpret_cast<const uint4 *>(headf + p0);

@@ -136,7 +136,7 @@ __global__ __launch_bounds__(256) void k_shard_parse(const uint8_t *__restrict__
             uint32_t *d = rec + (g >> 6) * 17u + ((g & 63u) >> 2);
             d[0] = x.x; d[1] = x.y; d[2] = x.z; d[3] = x.w;
         }
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        wave_lds_order();
         const uint32_t i = base + lane;
         if (i < n) {
             // the staged record: 64 contiguous LDS bytes (shard_parse reads dwords and the
@@ -166,7 +166,7 @@ __global__ __launch_bounds__(256) void k_shard_parse(const uint8_t *__restrict__
             filtered += f == 2;
             own8[i] = o;
         }
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        wave_lds_order();
     }
     if (wide && __ballot(need_wide) && lane == 0) atomicOr(wide, 1ull);
     filtered = wave_sum(filtered);

@@ -1,12 +1,12 @@
 #!/bin/bash
 # A/B timing of library variants on the GPU box: scripts/ab.sh "" s3 s2 ...
 # ("" = the product build). Prints ms/step and the per-kernel split of each.
-# AB_MLP=1 keeps features + scores in the step (default: verdicts only).
+# AB_MLP=0 drops features + scores from the step (default: the headline step).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 for v in "$@"; do
-  FSX_LIB_VARIANT=$v timeout -k 10 240 python bench.py --steps 10 --warmup 2 --no-cpu-baseline \
-      --limiter-steps 0 $([ "${AB_MLP:-0}" = 1 ] || echo --no-mlp) ${AB_ARGS:-} > gpurun_out/ab_$v.json 2> gpurun_out/ab_$v.err || exit $?
+  FSX_LIB_VARIANT=$v timeout -k 10 240 python bench.py --steps ${AB_STEPS:-20} --warmup 3 --no-cpu-baseline \
+      --no-check --legs "" $([ "${AB_MLP:-1}" = 1 ] || echo --no-mlp) ${AB_ARGS:-} > gpurun_out/ab_$v.json 2> gpurun_out/ab_$v.err || exit $?
   python - "$v" <<'PY'
 import json, sys
 v = sys.argv[1]
