@@ -122,4 +122,25 @@ __device__ __forceinline__ int key_cmp(uint32_t ta, const uint32_t *a, uint32_t 
     return 0;
 }
 
+// Loads of data read exactly once per batch (packet records, lengths, timestamps):
+// non-temporal, so the stream does not evict what is re-read from L2 (the source
+// index). FSX_STREAM_NT=0 builds plain loads (A/B: scripts/build_variant.sh).
+#ifndef FSX_STREAM_NT
+#define FSX_STREAM_NT 1
+#endif
+template <class T>
+__device__ __forceinline__ T stream_load(const T *p) {
+    if constexpr (FSX_STREAM_NT) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+__device__ __forceinline__ uint4 stream_load16(const uint8_t *p) {
+    if constexpr (FSX_STREAM_NT) {
+        typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+        const v4u q = __builtin_nontemporal_load(reinterpret_cast<const v4u *>(p));
+        return make_uint4(q.x, q.y, q.z, q.w);
+    } else {
+        return *reinterpret_cast<const uint4 *>(p);
+    }
+}
+
 }  // namespace fsx

@@ -440,10 +440,10 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
             for (int k = 0; k < 3; ++k) {
                 const uint32_t f = (uint32_t)k * 64u + lane, r = f / 3u, c = f - 3u * r;
                 const uint32_t rr = tv && base + r < n ? base + r : 0u;
-                h[k] = *reinterpret_cast<const uint4 *>(in.hdr + (size_t)rr * 64u + c * 16u);
+                h[k] = stream_load16(in.hdr + (size_t)rr * 64u + c * 16u);
             }
-            L_ = len[ic];
-            T_ = ts[ic];
+            L_ = stream_load(len + ic);
+            T_ = stream_load(ts + ic);
             P_ = ts[ic > 0 ? ic - 1 : 0];   // (used by lane 0 only: the record before the step)
         } else {
             const uint4 *r = reinterpret_cast<const uint4 *>(in.rec);
@@ -1328,8 +1328,8 @@ __device__ void walk_fixed_exact_thread(const SV &sv, uint32_t a, uint32_t b,
         uint32_t L[16];
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
-            t[k] = q0 + k < b ? sv.t(q0 + k) : 0ull;
-            L[k] = q0 + k < b ? sv.l(q0 + k) : 0u;
+            if (q0 + k < b) sv.tl(q0 + k, t[k], L[k]);
+            else { t[k] = 0; L[k] = 0; }
         }
 #pragma unroll
         for (int k = 0; k < 16; ++k)
@@ -2131,7 +2131,8 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
     k_heads_write<<<gridTiles, 256, 0, st>>>(bs, sc.headf, sc.tile_aux, sc.seg_start, S,
                                              do_limit ? sc.seg_slot : nullptr, lim.table_mask);
     mark("k_heads_write");
-    const bool fork = flows && do_limit && st2 && fork_ev && join_ev;
+    static const bool no_fork = getenv("FSX_NO_FLOW_FORK") != nullptr;   // A/B: flows serialized
+    const bool fork = flows && do_limit && st2 && fork_ev && join_ev && !no_fork;
     if (flows) {
         hipStream_t fs = st;
         if (fork) {   // the features run beside the limiter

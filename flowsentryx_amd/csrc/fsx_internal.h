@@ -381,6 +381,7 @@ hipError_t launch_flows(const uint64_t *S, const uint64_t *pay, BatchState *bs, 
                         uint32_t *span_list, void *acc, uint8_t *keys16, uint8_t *fam, float *feat,
                         float *prob, uint8_t *dec, uint32_t cap, const ScoreParams &P, uint32_t salt,
                         uint32_t n, void *sacc, uint32_t epoch, const uint32_t *seg_slot, hipStream_t st);
+
 size_t flow_acc_bytes();
 size_t slot_acc_bytes();
 // Rows of every source accumulated in epoch `epoch` (slots of the table), *d_count = rows.

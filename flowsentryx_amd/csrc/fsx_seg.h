@@ -29,6 +29,18 @@ struct SegView {
         if constexpr (kPay) return (uint32_t)pay[q] & ((1u << kPayLenBits) - 1u);
         else return len[pk_idx(S[q])];
     }
+    // both from one payload word (or one arrival index)
+    __device__ __forceinline__ void tl(uint32_t q, uint64_t &T, uint32_t &L) const {
+        if constexpr (kPay) {
+            const uint64_t w = pay[q];
+            T = tbase + (w >> kPayLenBits);
+            L = (uint32_t)w & ((1u << kPayLenBits) - 1u);
+        } else {
+            const uint32_t i = pk_idx(S[q]);
+            T = ts[i];
+            L = len[i];
+        }
+    }
     // Timestamps of positions q0 .. q0+15, q0 % 2 == 0, all < the valid count: 16-byte
     // vector loads of the payload words (one thread reads a whole 128-byte line).
     __device__ __forceinline__ void t16(uint32_t q0, uint64_t (&out)[16]) const {

@@ -397,42 +397,77 @@ def test_flow_features_heavy_sources(native, oracle):
     _check_flows(native, oracle, hdr, ln, ts)
 
 
-def test_process_batch_device(native, oracle):
-    """Full path on device: verdicts + per-source features + q8 scores in one call."""
+def _process_batch_device(native, oracle, batches, max_entries=1 << 20):
+    """Verdicts + per-source features + q8 scores of each batch in one device call on one
+    context (maps carried), against the oracle's verdicts and its per-batch flow rows."""
     import torch
-    from flowsentryx_amd import fsx_load, synth
-    p, s = synth.config_params(2, n=1 << 19)
-    n = int(p.n)
-    hdr, ln, ts = oracle.synth(p, s, 0, n)
+    from flowsentryx_amd import fsx_load
     ref = json.loads((GOLDEN / "model_weights.json").read_text())
+    o = oracle.Oracle(max_entries=max_entries)
+    cap = max(len(b[0]) for b in batches)
     dev = lambda a: torch.from_numpy(a.view(np.uint8).reshape(-1)).cuda()
-    d_hdr, d_len, d_ts = dev(hdr), dev(ln), dev(ts)
-    d_v = torch.empty(n, dtype=torch.uint8, device="cuda")
-    d_k = torch.empty(n * 16, dtype=torch.uint8, device="cuda")
-    d_f = torch.empty(n, dtype=torch.uint8, device="cuda")
-    d_x = torch.empty(n * 8, dtype=torch.float32, device="cuda")
-    d_p = torch.empty(n, dtype=torch.float32, device="cuda")
-    d_d = torch.empty(n, dtype=torch.uint8, device="cuda")
-    with gpu_ctx(native, max_entries=1 << 20, max_batch=n) as c:
+    d_v = torch.empty(cap, dtype=torch.uint8, device="cuda")
+    d_k = torch.empty(cap * 16, dtype=torch.uint8, device="cuda")
+    d_f = torch.empty(cap, dtype=torch.uint8, device="cuda")
+    d_x = torch.empty(cap * 8, dtype=torch.float32, device="cuda")
+    d_p = torch.empty(cap, dtype=torch.float32, device="cuda")
+    d_d = torch.empty(cap, dtype=torch.uint8, device="cuda")
+    with gpu_ctx(native, max_entries=max_entries, max_batch=cap) as c:
         c.load_q8_model(fsx_load.model_from_dict(ref))
-        c.process_batch_device(d_hdr.data_ptr(), d_len.data_ptr(), d_ts.data_ptr(), n,
-                               d_v.data_ptr(), d_k.data_ptr(), d_f.data_ptr(), d_x.data_ptr(),
-                               d_p.data_ptr(), d_d.data_ptr(), n)
-        c.sync()
-        m = c.last_batch_info()["sources"]
-    o = oracle.Oracle(max_entries=1 << 20)
-    assert np.array_equal(d_v.cpu().numpy(), o.batch(hdr, ln, ts))
-    kg = d_k.cpu().numpy().reshape(n, 16)[:m]
-    fg = d_f.cpu().numpy()[:m]
-    xg = d_x.cpu().numpy().reshape(n, 8)[:m]
-    pg = d_p.cpu().numpy()[:m]
-    ko, fo, xo = oracle.flow_features(hdr, ln, ts)
-    assert m == len(fo)
-    order_g = sorted(range(m), key=lambda i: (int(fg[i]), kg[i].tobytes()))
-    order_o = sorted(range(m), key=lambda i: (int(fo[i]), ko[i].tobytes()))
-    assert np.array_equal(xg[order_g].view(np.uint32), xo[order_o].view(np.uint32))
-    po, _, _ = oracle.score(ref, xo[order_o])
-    assert np.array_equal(pg[order_g].view(np.uint32), po.view(np.uint32))
+        for hdr, ln, ts in batches:
+            n = len(ln)
+            d_hdr, d_len, d_ts = dev(hdr), dev(ln), dev(ts)
+            c.process_batch_device(d_hdr.data_ptr(), d_len.data_ptr(), d_ts.data_ptr(), n,
+                                   d_v.data_ptr(), d_k.data_ptr(), d_f.data_ptr(), d_x.data_ptr(),
+                                   d_p.data_ptr(), d_d.data_ptr(), cap)
+            c.sync()
+            m = c.last_batch_info()["sources"]
+            assert np.array_equal(d_v[:n].cpu().numpy(), o.batch(hdr, ln, ts))
+            kg = d_k.cpu().numpy().reshape(cap, 16)[:m]
+            fg = d_f.cpu().numpy()[:m]
+            xg = d_x.cpu().numpy().reshape(cap, 8)[:m]
+            pg = d_p.cpu().numpy()[:m]
+            ko, fo, xo = oracle.flow_features(hdr, ln, ts)
+            assert m == len(fo)
+            order_g = sorted(range(m), key=lambda i: (int(fg[i]), kg[i].tobytes()))
+            order_o = sorted(range(m), key=lambda i: (int(fo[i]), ko[i].tobytes()))
+            assert np.array_equal(kg[order_g], ko[order_o])
+            assert np.array_equal(xg[order_g].view(np.uint32), xo[order_o].view(np.uint32))
+            po, _, _ = oracle.score(ref, xo[order_o])
+            assert np.array_equal(pg[order_g].view(np.uint32), po.view(np.uint32))
+
+
+def test_process_batch_device(native, oracle):
+    """Full path on device: verdicts + per-source features + q8 scores in one call (the
+    fixed-window walkers finish the light sources' rows, the flow tiles the heavy ones)."""
+    from flowsentryx_amd import synth
+    p, s = synth.config_params(2, n=1 << 19)
+    _process_batch_device(native, oracle, [oracle.synth(p, s, 0, int(p.n))])
+
+
+@pytest.mark.parametrize("case", ["mixed", "gather", "jitter", "carry"])
+def test_fused_flows(native, oracle, case):
+    """The walker-fused flow rows beside the heavy-source flow tiles: mixed families with
+    short / long / heavy sources, the gather path (no payload words), non-monotone clocks
+    (exact wave replay, wrapped inter-arrival times) and maps carried across batches."""
+    from flowsentryx_amd import synth
+    rng = np.random.default_rng(0xF10 + len(case))
+    if case == "mixed":
+        batches = [rand_stream(rng, 300_000, 3000, dt_max=400, v6_frac=0.3, nonip_frac=0.03, short_frac=0.01)]
+    elif case == "gather":
+        p, s = synth.config_params(2, n=1 << 18)
+        batches = [_with_far_nonip(*oracle.synth(p, s, 0, int(p.n)), 1 << 40)]
+    elif case == "jitter":
+        hdr, ln, ts = rand_stream(rng, 200_000, 1500, dt_max=300)
+        sw = rng.choice(len(ts), len(ts) // 10, replace=False)
+        ts[sw] = ts[sw] - rng.integers(0, 5000, sw.size).astype(np.uint64)
+        batches = [(hdr, ln, ts)]
+    else:
+        p, s = synth.config_params(2, n=3 << 17)
+        hdr, ln, ts = oracle.synth(p, s, 0, int(p.n))
+        cut = [0, 100_000, 250_000, len(ln)]
+        batches = [(hdr[a:b], ln[a:b], ts[a:b]) for a, b in zip(cut[:-1], cut[1:])]
+    _process_batch_device(native, oracle, batches)
 
 
 # ------------------------------------------------------------------ payload fallback
