@@ -113,6 +113,7 @@ struct fsx_ctx {
     hipEvent_t fork_ev = nullptr, join_ev = nullptr;
     hipStream_t walk_stream = nullptr;   // third stream: long-segment walker
     hipEvent_t walk_fork_ev = nullptr, walk_join_ev = nullptr;
+    hipEvent_t heavy_fork_ev = nullptr, heavy_flow_ev = nullptr;   // heavy work after sort pass 0
     int ring_n = 0;
     const char *acc_name[kMaxNames]{};
     double acc_ms[kMaxNames]{};
@@ -154,7 +155,7 @@ static void free_scratch(fsx_ctx *c) {
     hipFree(s.seg_order); hipFree(s.sub_cnt); hipFree(s.flow_first); hipFree(s.flow_last);
     hipFree(s.span_list); hipFree(s.sort_ctl); hipFree(s.gbase); hipFree(s.status);
     hipFree(s.lim_tiles); hipFree(s.sw_seg); hipFree(s.sketch); hipFree(s.heavy);
-    hipFree(s.drop_list); hipFree(s.drop_cur);
+    hipFree(s.drop_list); hipFree(s.drop_cur); hipFree(s.heavy_flow);
     s = Scratch{};
 }
 
@@ -197,6 +198,7 @@ static int alloc_scratch(fsx_ctx *c, uint64_t cap) {
     HIPCHK(c, hipMemset(s.sketch, 0, 2 * kSketch * 4));
     HIPCHK(c, hipMalloc(&s.heavy, sizeof(HeavySet)));
     HIPCHK(c, hipMemset(s.heavy, 0, sizeof(HeavySet)));
+    HIPCHK(c, hipMalloc(&s.heavy_flow, heavy_flow_bytes(cap)));
     s.cap = cap;
     return 0;
 }
@@ -251,6 +253,8 @@ void fsx_close(fsx_ctx *c) {
     if (c->walk_stream) hipStreamDestroy(c->walk_stream);
     if (c->walk_fork_ev) hipEventDestroy(c->walk_fork_ev);
     if (c->walk_join_ev) hipEventDestroy(c->walk_join_ev);
+    if (c->heavy_fork_ev) hipEventDestroy(c->heavy_fork_ev);
+    if (c->heavy_flow_ev) hipEventDestroy(c->heavy_flow_ev);
     if (c->fork_ev) hipEventDestroy(c->fork_ev);
     if (c->join_ev) hipEventDestroy(c->join_ev);
     delete c;
@@ -288,6 +292,8 @@ int fsx_open(fsx_ctx **out, const fsx_config *cfg) {
     if (hipStreamCreateWithFlags(&c->walk_stream, hipStreamNonBlocking) != hipSuccess) return fail(-EIO);
     if (hipEventCreateWithFlags(&c->walk_fork_ev, hipEventDisableTiming) != hipSuccess) return fail(-EIO);
     if (hipEventCreateWithFlags(&c->walk_join_ev, hipEventDisableTiming) != hipSuccess) return fail(-EIO);
+    if (hipEventCreateWithFlags(&c->heavy_fork_ev, hipEventDisableTiming) != hipSuccess) return fail(-EIO);
+    if (hipEventCreateWithFlags(&c->heavy_flow_ev, hipEventDisableTiming) != hipSuccess) return fail(-EIO);
     c->stream = c->own_stream;
     if (hipMalloc(&c->table, c->slots * sizeof(Slot)) != hipSuccess) return fail(-ENOMEM);
     if (hipMalloc(&c->tstate, sizeof(TableState)) != hipSuccess) return fail(-ENOMEM);
@@ -585,7 +591,8 @@ static int run_batch(fsx_ctx *c, const PacketIn &in, const uint32_t *d_len, cons
                                            c->rs, do_limit, fr,
                                            c->hist, c->stream, fork_flows() ? c->aux_stream : nullptr,
                                            c->fork_ev, c->join_ev, fork_flows() ? c->walk_stream : nullptr,
-                                           c->walk_fork_ev, c->walk_join_ev, tm);
+                                           c->walk_fork_ev, c->walk_join_ev, c->heavy_fork_ev,
+                                           c->heavy_flow_ev, tm);
     if (tm) c->ev_used[c->ring_n++] = tm->used;
     c->pending = true;
     c->pending_born = do_limit && n ? c->id_gen : 0;

@@ -1074,15 +1074,17 @@ __global__ __launch_bounds__(256) void k_onesweep(const uint64_t *__restrict__ i
 
 // ------------------------------------------------------------------ segment heads
 // A source starts wherever the id changes (ids are exact: one per (family, address)).
-// Tile = kTile sorted positions; 256 threads x 16 consecutive positions.
+// Tile = kTile sorted positions; 256 threads x 16 consecutive positions. light_only
+// (heavy verdict lists): the heads of [0, n_light) only; each heavy source is one run of
+// pass 0 and k_heads_heavy appends those segments from pass 0's bucket counts.
 __global__ __launch_bounds__(256) void k_heads_count(const uint64_t *__restrict__ S,
                                                      BatchState *bs,
                                                      const uint8_t *__restrict__ hdr,
                                                      uint8_t *__restrict__ headf,
                                                      uint32_t *__restrict__ tile_cnt,
-                                                     uint32_t *__restrict__ sub_cnt) {
+                                                     uint32_t *__restrict__ sub_cnt, uint32_t light_only) {
     __shared__ uint32_t s_tmp[4];
-    const uint32_t M = bs->n_valid;
+    const uint32_t M = light_only ? bs->n_light : bs->n_valid;
     const uint32_t ntiles = (M + kTile - 1) / kTile;
     const uint32_t lane = lane_id();
     for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
@@ -1123,10 +1125,10 @@ __global__ __launch_bounds__(256) void k_heads_count(const uint64_t *__restrict_
 
 // Single block: exclusive scan of per-tile counts (in place), nseg, seg_start[nseg]=M.
 __global__ __launch_bounds__(1024) void k_scan_tiles_u32(uint32_t *__restrict__ cnt, BatchState *bs,
-                                                         uint32_t *seg_start) {
+                                                         uint32_t *seg_start, uint32_t light_only) {
     __shared__ uint32_t s_w[16];
     __shared__ uint32_t s_carry;
-    const uint32_t M = bs->n_valid;
+    const uint32_t M = light_only ? bs->n_light : bs->n_valid;
     const uint32_t ntiles = (M + kTile - 1) / kTile;
     const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
     if (threadIdx.x == 0) s_carry = 0;
@@ -1157,9 +1159,10 @@ __global__ __launch_bounds__(256) void k_heads_write(BatchState *bs, const uint8
                                                      const uint32_t *__restrict__ tile_off,
                                                      uint32_t *__restrict__ seg_start,
                                                      const uint64_t *__restrict__ S,
-                                                     uint32_t *__restrict__ seg_slot, uint64_t id_mask) {
+                                                     uint32_t *__restrict__ seg_slot, uint64_t id_mask,
+                                                     uint32_t light_only) {
     __shared__ uint32_t s_tmp[4];
-    const uint32_t M = bs->n_valid;
+    const uint32_t M = light_only ? bs->n_light : bs->n_valid;
     const uint32_t ntiles = (M + kTile - 1) / kTile;
     for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
         const uint32_t p0 = t * kTile + threadIdx.x * 16u;
@@ -1182,6 +1185,32 @@ __global__ __launch_bounds__(256) void k_heads_write(BatchState *bs, const uint8
                 ++off;
             }
         }
+    }
+}
+
+// The heavy sources' segments after the light ones (light_only heads): non-empty heavy
+// bucket h of pass 0 is segment nseg_light + (its rank among the non-empty buckets), its
+// run [gbase, gbase + count) as positions; nseg and the end sentinel follow.
+__global__ __launch_bounds__(256) void k_heads_heavy(BatchState *bs, const uint32_t *__restrict__ cnt0,
+                                                     const uint32_t *__restrict__ base0,
+                                                     uint32_t *__restrict__ seg_start,
+                                                     uint32_t *__restrict__ seg_slot,
+                                                     const uint64_t *__restrict__ S, uint64_t id_mask) {
+    __shared__ uint32_t s_tmp[4];
+    const uint32_t h = threadIdx.x;
+    const uint32_t L = bs->nseg;   // light segments (k_scan_tiles_u32); read before the barrier
+    const bool live = h < kHeavyMax && cnt0[kHeavyMax + h] > 0;
+    uint32_t H;
+    const uint32_t r = block256_excl(live ? 1u : 0u, s_tmp, &H);
+    if (live) {
+        const uint32_t a = base0[kHeavyMax + h];
+        seg_start[L + r] = a;
+        if (seg_slot) seg_slot[L + r] = pk_id(S[a], id_mask);
+    }
+    if (h == 0) {
+        bs->nseg_light = L;
+        bs->nseg = L + H;
+        seg_start[L + H] = bs->n_valid;
     }
 }
 
@@ -1541,7 +1570,7 @@ struct HeavyLists {
 template <bool kWave>
 __device__ __forceinline__ int heavy_list_open(const HeavyLists &H, const uint64_t *S, uint32_t a,
                                                MarkWriter<kWave, true> &mw) {
-    mw.list = H.list + a;
+    mw.list = H.list + 2u * a;   // bytes [8a, 8a + 4 * entries): inside the run's own 8-byte positions
     mw.S = S;
     return (int)(S[a] >> 56) - (int)kHeavyMax;   // bucket = 128 + heavy index
 }
@@ -1551,7 +1580,7 @@ __device__ __forceinline__ void heavy_list_close(const HeavyLists &H, int h, uin
                                                  MarkWriter<kWave, true> &mw) {
     mw.finish(b);
     if (kWave && lane_id() != 0) return;
-    H.hs->lbase[h] = a;
+    H.hs->lbase[h] = 2u * a;
     H.hs->lcnt[h] = mw.nl;
     unsigned long long *st = reinterpret_cast<unsigned long long *>(H.tstate->stats);
     if (mw.npass) {
@@ -1998,7 +2027,8 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
                                    bool do_limit, const FlowRequest *flows,
                                    const HistBufs &hist, hipStream_t st, hipStream_t st2,
                                    hipEvent_t fork_ev, hipEvent_t join_ev, hipStream_t st3,
-                                   hipEvent_t walk_fork_ev, hipEvent_t walk_join_ev, PipeTiming *tm) {
+                                   hipEvent_t walk_fork_ev, hipEvent_t walk_join_ev, hipEvent_t heavy_fork_ev,
+                                   hipEvent_t heavy_flow_ev, PipeTiming *tm) {
     (void)hipGetLastError();   // a stale error of another caller is not ours
     Scratch sc = sc_in;        // packed[0] / pay[0] become the sorted output below
     int last[3] = {-1, -1, -1};   // last event index per stream (timing)
@@ -2087,6 +2117,18 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
 #undef FSX_PARSE
     }
     mark("k_parse");
+    // Heavy verdict lists: every heavy source is one run of pass 0's output (the later passes
+    // write [0, n_light) only) whose segment needs no head search, so its walker and its flow
+    // sums run on the third stream beside the heads, the classes and the light walkers, which
+    // like the light flow tiles cover [0, n_light) only (k_heads_heavy appends the heavy
+    // segments).
+    hipStream_t hs = (st3 && heavy_fork_ev && heavy_flow_ev) ? st3 : st;
+    const int hs_id = hs == st ? 0 : 2;
+    uint64_t *S_fin = sc.packed[npass & 1], *pay_fin = sc.pay[npass & 1];
+    // heavy verdict lists live in the sort's other buffer, over the heavy positions (which the
+    // passes >= 1 never write)
+    const HeavyLists hlists{tagh ? reinterpret_cast<uint32_t *>(sc.packed[(npass + 1) & 1]) : nullptr, sc.heavy,
+                            tstate, bs};
     k_hist_prep<<<1, 256, 0, st>>>(sc.sort_ctl, sc.gbase, bs, heavy_sort ? dp.light_b : 256u);
     if (do_limit) k_batch_check<<<1, 1, 0, st>>>(bs, tstate, lim);
     const uint32_t gen0 = onesweep ? next_generation() : 0u;
@@ -2116,6 +2158,25 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
             k_tile_scatter<kLatePayDefault><<<ntiles, 256, 0, st>>>(in, out, n, Ld, shift, pmask, pass == 0, sc.hist, tcap, bs,
                                                    pin, pout, ts, len);
             mark("k_tile_scatter");
+            // after the last pass (right after pass 0 the heavy work slowed passes 1-2 by more
+            // than it gained: 4.18 vs 4.12 ms/step, scripts/ab_env.sh)
+            if (pass == npass - 1 && tagh) {   // the heavy runs: their walker and flow sums
+                if (hs != st) {
+                    if ((e = hipEventRecord(heavy_fork_ev, st)) != hipSuccess) return e;
+                    if ((e = hipStreamWaitEvent(hs, heavy_fork_ev, 0)) != hipSuccess) return e;
+                    mark_on(nullptr, hs_id);
+                }
+                k_walk_heavy<<<kHeavyMax / 4, 256, 0, hs>>>(S_fin, bs, sc.sort_ctl, sc.gbase, ts, len, pay_fin,
+                                                              table, lim, hlists);
+                mark_on("k_walk_heavy", hs_id);
+                if (flows) {
+                    if ((e = launch_flows_heavy(S_fin, pay_fin, ts, len, bs, sc.sort_ctl, sc.gbase, sc.heavy_flow,
+                                                sc.cap, hs)) != hipSuccess)
+                        return e;
+                    mark_on("k_flow_heavy", hs_id);
+                    if (hs != st && (e = hipEventRecord(heavy_flow_ev, hs)) != hipSuccess) return e;
+                }
+            }
         }
     }
     if (npass & 1) {
@@ -2123,13 +2184,15 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
         std::swap(sc.pay[0], sc.pay[1]);
     }
     uint64_t *S = sc.packed[0];
-    // heavy verdict lists live in the sort's other buffer (free from here on)
-    const HeavyLists hlists{tagh ? reinterpret_cast<uint32_t *>(sc.packed[1]) : nullptr, sc.heavy, tstate, bs};
-    k_heads_count<<<gridTiles, 256, 0, st>>>(S, bs, in.hdr, sc.headf, sc.tile_aux, sc.sub_cnt);
+    const uint32_t lo = tagh ? 1u : 0u;   // light-only heads
+    k_heads_count<<<gridTiles, 256, 0, st>>>(S, bs, in.hdr, sc.headf, sc.tile_aux, sc.sub_cnt, lo);
     mark("k_heads_count");
-    k_scan_tiles_u32<<<1, 1024, 0, st>>>(sc.tile_aux, bs, sc.seg_start);
+    k_scan_tiles_u32<<<1, 1024, 0, st>>>(sc.tile_aux, bs, sc.seg_start, lo);
     k_heads_write<<<gridTiles, 256, 0, st>>>(bs, sc.headf, sc.tile_aux, sc.seg_start, S,
-                                             do_limit ? sc.seg_slot : nullptr, lim.table_mask);
+                                             do_limit ? sc.seg_slot : nullptr, lim.table_mask, lo);
+    if (tagh)
+        k_heads_heavy<<<1, 256, 0, st>>>(bs, sc.sort_ctl, sc.gbase, sc.seg_start, do_limit ? sc.seg_slot : nullptr,
+                                         S, lim.table_mask);
     mark("k_heads_write");
     static const bool no_fork = getenv("FSX_NO_FLOW_FORK") != nullptr;   // A/B: flows serialized
     const bool fork = flows && do_limit && st2 && fork_ev && join_ev && !no_fork;
@@ -2145,8 +2208,17 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
                               sc.flow_first, sc.flow_last, sc.span_list, flows->acc, flows->keys16,
                               flows->fam, flows->feat, flows->prob, flows->dec, flows->cap, flows->score,
                               lim.salt32, n, do_limit ? flows->sacc : nullptr, flows->epoch, sc.seg_slot,
-                              fs)) != hipSuccess)
+                              tagh, fs)) != hipSuccess)
             return e;
+        if (tagh) {   // the heavy sources' rows, from their sums (k_flow_heavy)
+            if (hs != fs && (e = hipStreamWaitEvent(fs, heavy_flow_ev, 0)) != hipSuccess) return e;
+            if ((e = launch_flows_heavy_finish(S, bs, sc.sort_ctl, sc.seg_start, in, len, ts, sc.heavy_flow, sc.cap,
+                                               flows->keys16, flows->fam, flows->feat, flows->prob, flows->dec,
+                                               flows->cap, flows->score, lim.salt32,
+                                               do_limit ? flows->sacc : nullptr, flows->epoch, sc.seg_slot, fs)) !=
+                hipSuccess)
+                return e;
+        }
         mark_on("k_flow_features", fork ? 1 : 0);
         if (fork && (e = hipEventRecord(join_ev, st2)) != hipSuccess) return e;
     }
@@ -2177,11 +2249,6 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
                                                                   sc.pay[0], sc.seg_order, cls, sc.marks,
                                                                   table, lim, hlists);
             mark_on("k_walk_fixed_long", fork3 ? 2 : 0);
-            if (tagh) {   // pass 0's digit counts / bases of the heavy buckets: their runs
-                k_walk_heavy<<<kHeavyMax / 4, 256, 0, fork3 ? st3 : st>>>(S, bs, sc.sort_ctl, sc.gbase, ts, len,
-                                                                          sc.pay[0], table, lim, hlists);
-                mark_on("k_walk_heavy", fork3 ? 2 : 0);
-            }
             if (fork3 && (e = hipEventRecord(walk_join_ev, st3)) != hipSuccess) return e;
             k_walk_fixed<<<gridStream, 256, 0, st>>>(S, bs, sc.seg_start, sc.seg_slot, ts, len, sc.pay[0],
                                                      sc.seg_order, cls, sc.marks, table, lim, hlists);

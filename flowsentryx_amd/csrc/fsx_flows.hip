@@ -17,6 +17,11 @@
 // finished by k_flow_combine (one wave per such source, lanes striding its tiles).
 // Per packet: 8 B sort word + 12 B gathered (len, ts) in; per source: 8 x fp32
 // features + prob + decision out.
+//
+// light_only (the fixed window with heavy verdict lists): these kernels cover the light
+// positions [0, n_light) and segments [0, nseg_light); each heavy source is one run of
+// sort pass 0, summed right after that pass in kHeavyChunk-position chunks (k_flow_heavy,
+// beside sort passes 1-2) and finished after the heads (k_flow_heavy_finish).
 
 #include <hip/hip_runtime.h>
 
@@ -24,6 +29,7 @@
 #include <cmath>
 
 #include "fsx_flow_common.h"
+#include "fsx_seg.h"
 
 namespace fsx {
 
@@ -44,9 +50,9 @@ __device__ __forceinline__ void flow_tiles(const uint64_t *__restrict__ S,
                                            FlowAcc *__restrict__ firstp, FlowAcc *__restrict__ lastp,
                                            uint32_t *__restrict__ span_list, const FlowOut &out,
                                            const ScoreParams &P, uint32_t salt,
-                                           unsigned long long (*s_S)[64 * 17]) {
+                                           unsigned long long (*s_S)[64 * 17], uint32_t light_only) {
     const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
-    const uint32_t M = bs->n_valid;
+    const uint32_t M = light_only ? bs->n_light : bs->n_valid;
     const uint32_t nsub = (M + kFT - 1) / kFT;
     unsigned long long *sS = s_S[w];
     for (uint32_t sub = blockIdx.x * 4u + w; sub < nsub; sub += gridDim.x * 4u) {
@@ -185,14 +191,14 @@ __global__ __launch_bounds__(256, FSX_FLOW_MINB) void k_flow_tile(const uint64_t
                                                    FlowAcc *__restrict__ firstp,
                                                    FlowAcc *__restrict__ lastp,
                                                    uint32_t *__restrict__ span_list, FlowOut out,
-                                                   ScoreParams P, uint32_t salt) {
+                                                   ScoreParams P, uint32_t salt, uint32_t light_only) {
     __shared__ unsigned long long s_S[4][64 * 17];
     if (bs->pay_ok)
         flow_tiles<true>(S, pay, bs, headf, len, ts, in, tile_off, sub_cnt, seg_start, firstp,
-                         lastp, span_list, out, P, salt, s_S);
+                         lastp, span_list, out, P, salt, s_S, light_only);
     else
         flow_tiles<false>(S, pay, bs, headf, len, ts, in, tile_off, sub_cnt, seg_start, firstp,
-                          lastp, span_list, out, P, salt, s_S);
+                          lastp, span_list, out, P, salt, s_S, light_only);
 }
 
 __global__ __launch_bounds__(256) void k_flow_combine(const uint64_t *__restrict__ S, BatchState *bs,
@@ -237,8 +243,8 @@ __global__ __launch_bounds__(256) void k_flow_finish(const uint64_t *__restrict_
                                                      const uint32_t *__restrict__ seg_start,
                                                      PacketIn in,
                                                      const uint32_t *__restrict__ len, FlowOut out,
-                                                     ScoreParams P, uint32_t salt) {
-    const uint32_t ns = min(bs->nseg, out.cap);
+                                                     ScoreParams P, uint32_t salt, uint32_t light_only) {
+    const uint32_t ns = min(light_only ? bs->nseg_light : bs->nseg, out.cap);
     for (uint32_t g = blockIdx.x * 256u + threadIdx.x; g < ns; g += gridDim.x * 256u)
         flow_finish(g, out.acc[g], S, seg_start, in, len, salt, out, P);
 }
@@ -248,17 +254,170 @@ hipError_t launch_flows(const uint64_t *S, const uint64_t *pay, BatchState *bs, 
                         const uint32_t *sub_cnt, const uint32_t *seg_start, void *firstp, void *lastp,
                         uint32_t *span_list, void *acc, uint8_t *keys16, uint8_t *fam, float *feat,
                         float *prob, uint8_t *dec, uint32_t cap, const ScoreParams &P, uint32_t salt,
-                        uint32_t n, void *sacc, uint32_t epoch, const uint32_t *seg_slot, hipStream_t st) {
+                        uint32_t n, void *sacc, uint32_t epoch, const uint32_t *seg_slot, bool light_only,
+                        hipStream_t st) {
     (void)hipGetLastError();   // a stale error of another caller is not ours
     const FlowOut out{(FlowAcc *)acc, keys16, fam, feat, prob, dec, cap, (SlotAcc *)sacc, epoch, seg_slot, ts};
     const uint32_t nsub = (n + kFT - 1) / kFT;
     const uint32_t grid = std::max<uint32_t>(1, std::min<uint32_t>(16384, (nsub + 3) / 4));
     k_flow_tile<<<grid, 256, 0, st>>>(S, pay, bs, headf, len, ts, in, tile_off, sub_cnt, seg_start,
-                                      (FlowAcc *)firstp, (FlowAcc *)lastp, span_list, out, P, salt);
+                                      (FlowAcc *)firstp, (FlowAcc *)lastp, span_list, out, P, salt,
+                                      light_only ? 1u : 0u);
     k_flow_combine<<<256, 256, 0, st>>>(S, bs, seg_start, (const FlowAcc *)firstp,
                                         (const FlowAcc *)lastp, span_list, in, len, out, P, salt);
     const uint32_t gf = std::max<uint32_t>(1, std::min<uint32_t>(4096, (std::min(n, cap) + 255) / 256));
-    k_flow_finish<<<gf, 256, 0, st>>>(S, bs, seg_start, in, len, out, P, salt);
+    k_flow_finish<<<gf, 256, 0, st>>>(S, bs, seg_start, in, len, out, P, salt, light_only ? 1u : 0u);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------ heavy sources
+// Heavy bucket h of pass 0 holds heavy source h's packets as one run [base0, +cnt0) of the
+// final sorted arrays (passes >= 1 write only [0, n_light)). Chunk j of run h is item
+// pre[h] + j; pre (computed by every block, written by block 0) and the per-chunk
+// partials live in the context's heavy-flow scratch.
+constexpr uint32_t kHeavyChunk = 8192;
+
+__device__ __forceinline__ void heavy_chunk_prefix(const uint32_t *cnt0, uint32_t *s_pre, uint32_t *s_tmp) {
+    const uint32_t h = threadIdx.x;
+    const uint32_t c = h < kHeavyMax ? (cnt0[kHeavyMax + h] + kHeavyChunk - 1) / kHeavyChunk : 0u;
+    uint32_t tot;
+    const uint32_t e = block256_excl(c, s_tmp, &tot);
+    if (h < kHeavyMax) s_pre[h] = e;
+    if (h == 0) s_pre[kHeavyMax] = tot;
+    __syncthreads();
+}
+
+// Flow sums of positions [a, b) of the run that starts at rs <= a, one wave: 1024
+// consecutive positions per round (16 loads in flight per lane), inter-arrival times
+// across lanes by shuffles; the total in every lane.
+template <class SV>
+__device__ FlowAcc flow_wave_acc(const SV &sv, uint32_t rs, uint32_t a, uint32_t b) {
+    const uint32_t lane = lane_id();
+    FlowAcc A = acc_zero();
+    uint64_t carry = a > rs ? sv.t(a - 1) : 0ull;   // timestamp of the position before the round
+    for (uint32_t q0 = a; q0 < b; q0 += 1024) {
+        uint64_t t[16];
+        uint32_t L[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const uint32_t q = q0 + 64u * (uint32_t)r + lane;
+            if (q < b) sv.tl(q, t[r], L[r]);
+            else { t[r] = 0; L[r] = 0; }
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const uint32_t q = q0 + 64u * (uint32_t)r + lane;
+            uint64_t tp = __shfl_up(t[r], 1);
+            if (lane == 0) tp = carry;
+            if (q < b) {
+                FlowAcc c = acc_zero();
+                c.n = 1; c.s1 = L[r]; c.s2 = (u128)L[r] * L[r];
+                if (q != rs) {
+                    const uint64_t d = t[r] - tp;
+                    c.d1 = d; c.d2 = (u128)d * d; c.dmax = d;
+                }
+                acc_add(A, c);
+            }
+            carry = __shfl(t[r], 63);
+        }
+    }
+    return wave_sum_acc(A);
+}
+
+template <class SV>
+__device__ __forceinline__ void flow_heavy_body(const SV &sv, const uint32_t *cnt0, const uint32_t *base0,
+                                                const uint32_t *s_pre, FlowAcc *part) {
+    const uint32_t items = s_pre[kHeavyMax];
+    for (uint32_t it = blockIdx.x * 4u + (threadIdx.x >> 6); it < items; it += gridDim.x * 4u) {
+        uint32_t lo = 0, hi = kHeavyMax;   // the bucket h with pre[h] <= it < pre[h + 1]
+        while (hi - lo > 1) {
+            const uint32_t m = (lo + hi) >> 1;
+            if (s_pre[m] <= it) lo = m; else hi = m;
+        }
+        const uint32_t rs = base0[kHeavyMax + lo], e = rs + cnt0[kHeavyMax + lo];
+        const uint32_t a = rs + (it - s_pre[lo]) * kHeavyChunk, b = min(e, a + kHeavyChunk);
+        const FlowAcc A = flow_wave_acc(sv, rs, a, b);
+        if (lane_id() == 0) part[it] = A;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_flow_heavy(const uint64_t *__restrict__ S, const uint64_t *__restrict__ pay,
+                                                    const uint64_t *__restrict__ ts, const uint32_t *__restrict__ len,
+                                                    const BatchState *bs, const uint32_t *__restrict__ cnt0,
+                                                    const uint32_t *__restrict__ base0, uint32_t *__restrict__ pre,
+                                                    FlowAcc *__restrict__ part) {
+    __shared__ uint32_t s_pre[kHeavyMax + 1];
+    __shared__ uint32_t s_tmp[4];
+    if (bs->err) return;
+    heavy_chunk_prefix(cnt0, s_pre, s_tmp);
+    if (blockIdx.x == 0 && threadIdx.x <= kHeavyMax) pre[threadIdx.x] = s_pre[threadIdx.x];
+    if (bs->pay_ok) {
+        const SegView<true> sv{S, ts, len, pay, ~bs->inv_min_ts};
+        flow_heavy_body(sv, cnt0, base0, s_pre, part);
+    } else {
+        const SegView<false> sv{S, ts, len, pay, 0};
+        flow_heavy_body(sv, cnt0, base0, s_pre, part);
+    }
+}
+
+// One wave per heavy bucket: the sum of its chunks.
+__global__ __launch_bounds__(256) void k_flow_heavy_sum(const BatchState *bs, const uint32_t *__restrict__ pre,
+                                                        const FlowAcc *__restrict__ part, FlowAcc *__restrict__ hacc) {
+    if (bs->err) return;
+    const uint32_t h = blockIdx.x * 4u + (threadIdx.x >> 6), lane = lane_id();
+    if (h >= kHeavyMax) return;
+    FlowAcc A = acc_zero();
+    for (uint32_t it = pre[h] + lane; it < pre[h + 1]; it += 64) acc_add(A, part[it]);
+    A = wave_sum_acc(A);
+    if (lane == 0) hacc[h] = A;
+}
+
+// After the heads: heavy bucket h's row is segment nseg_light + (rank among the non-empty
+// buckets), as k_heads_heavy numbered them.
+__global__ __launch_bounds__(256) void k_flow_heavy_finish(const uint64_t *__restrict__ S, const BatchState *bs,
+                                                           const uint32_t *__restrict__ cnt0,
+                                                           const uint32_t *__restrict__ seg_start,
+                                                           const FlowAcc *__restrict__ hacc, PacketIn in,
+                                                           const uint32_t *__restrict__ len, FlowOut out,
+                                                           ScoreParams P, uint32_t salt) {
+    __shared__ uint32_t s_tmp[4];
+    if (bs->err) return;
+    const uint32_t h = threadIdx.x;
+    const bool live = h < kHeavyMax && cnt0[kHeavyMax + h] > 0;
+    const uint32_t r = block256_excl(live ? 1u : 0u, s_tmp, nullptr);
+    if (live) flow_finish(bs->nseg_light + r, hacc[h], S, seg_start, in, len, salt, out, P);
+}
+
+size_t heavy_flow_bytes(uint64_t cap) {
+    return (cap / kHeavyChunk + kHeavyMax + 1) * sizeof(FlowAcc) + kHeavyMax * sizeof(FlowAcc) +
+           (kHeavyMax + 1) * 4;
+}
+
+// The heavy runs' sums (right after sort pass 0): part = scratch of heavy_flow_bytes(cap).
+hipError_t launch_flows_heavy(const uint64_t *S, const uint64_t *pay, const uint64_t *ts, const uint32_t *len,
+                              const BatchState *bs, const uint32_t *cnt0, const uint32_t *base0, void *scratch,
+                              uint64_t cap, hipStream_t st) {
+    (void)hipGetLastError();
+    FlowAcc *part = reinterpret_cast<FlowAcc *>(scratch);
+    FlowAcc *hacc = part + (cap / kHeavyChunk + kHeavyMax + 1);
+    uint32_t *pre = reinterpret_cast<uint32_t *>(hacc + kHeavyMax);
+    const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(1024, (cap / kHeavyChunk + kHeavyMax + 3) / 4));
+    k_flow_heavy<<<grid, 256, 0, st>>>(S, pay, ts, len, bs, cnt0, base0, pre, part);
+    k_flow_heavy_sum<<<kHeavyMax / 4, 256, 0, st>>>(bs, pre, part, hacc);
+    return hipGetLastError();
+}
+
+// The heavy sources' rows (after k_heads_heavy).
+hipError_t launch_flows_heavy_finish(const uint64_t *S, const BatchState *bs, const uint32_t *cnt0,
+                                     const uint32_t *seg_start, const PacketIn &in, const uint32_t *len,
+                                     const uint64_t *ts, void *scratch, uint64_t cap, uint8_t *keys16, uint8_t *fam,
+                                     float *feat, float *prob, uint8_t *dec, uint32_t rows_cap,
+                                     const ScoreParams &P, uint32_t salt, void *sacc, uint32_t epoch,
+                                     const uint32_t *seg_slot, hipStream_t st) {
+    (void)hipGetLastError();
+    const FlowAcc *hacc = reinterpret_cast<const FlowAcc *>(scratch) + (cap / kHeavyChunk + kHeavyMax + 1);
+    const FlowOut out{nullptr, keys16, fam, feat, prob, dec, rows_cap, (SlotAcc *)sacc, epoch, seg_slot, ts};
+    k_flow_heavy_finish<<<1, 256, 0, st>>>(S, bs, cnt0, seg_start, hacc, in, len, out, P, salt);
     return hipGetLastError();
 }
 

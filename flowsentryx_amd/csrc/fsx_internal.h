@@ -85,6 +85,8 @@ struct BatchState {
     uint64_t inv_min_ts;  // ~(smallest timestamp): max-reduced from 0
     uint32_t pay_ok;      // sorted payload words valid (see kPayLenBits)
     uint32_t n_light;     // entries of non-heavy sources: sort passes >= 1 cover [0, n_light)
+    uint32_t nseg_light;  // heavy verdict lists: segments ids [0, nseg_light) are light, the
+                          // heavy sources' segments follow (k_heads_heavy)
 };
 
 // Sorted payload word carried through the onesweep passes next to each sort word:
@@ -298,6 +300,7 @@ struct Scratch {
     uint32_t *sketch;      // heavy-source sample: counts [kSketch], candidate packets [kSketch]
                            // (counts zeroed by k_heavy_pick after use)
     HeavySet *heavy;
+    void *heavy_flow;      // heavy sources' flow chunk sums (heavy_flow_bytes)
     uint64_t cap;          // packets the scratch is sized for
 };
 
@@ -350,7 +353,8 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
                                    bool do_limit, const FlowRequest *flows, const HistBufs &hist,
                                    hipStream_t st, hipStream_t st2, hipEvent_t fork_ev,
                                    hipEvent_t join_ev, hipStream_t st3, hipEvent_t walk_fork_ev,
-                                   hipEvent_t walk_join_ev, PipeTiming *tm);
+                                   hipEvent_t walk_join_ev, hipEvent_t heavy_fork_ev,
+                                   hipEvent_t heavy_flow_ev, PipeTiming *tm);
 
 // Build-defined limiters (fsx_limiters.hip), after the table lookup/insert of a batch:
 // one verdict mark per sorted position, final per-source state in the table.
@@ -380,7 +384,20 @@ hipError_t launch_flows(const uint64_t *S, const uint64_t *pay, BatchState *bs, 
                         const uint32_t *sub_cnt, const uint32_t *seg_start, void *firstp, void *lastp,
                         uint32_t *span_list, void *acc, uint8_t *keys16, uint8_t *fam, float *feat,
                         float *prob, uint8_t *dec, uint32_t cap, const ScoreParams &P, uint32_t salt,
-                        uint32_t n, void *sacc, uint32_t epoch, const uint32_t *seg_slot, hipStream_t st);
+                        uint32_t n, void *sacc, uint32_t epoch, const uint32_t *seg_slot, bool light_only,
+                        hipStream_t st);
+// Heavy verdict lists: the heavy sources' flow sums right after sort pass 0, their rows
+// after the heads (fsx_flows.hip "heavy sources"); scratch of heavy_flow_bytes(cap).
+size_t heavy_flow_bytes(uint64_t cap);
+hipError_t launch_flows_heavy(const uint64_t *S, const uint64_t *pay, const uint64_t *ts, const uint32_t *len,
+                              const BatchState *bs, const uint32_t *cnt0, const uint32_t *base0, void *scratch,
+                              uint64_t cap, hipStream_t st);
+hipError_t launch_flows_heavy_finish(const uint64_t *S, const BatchState *bs, const uint32_t *cnt0,
+                                     const uint32_t *seg_start, const PacketIn &in, const uint32_t *len,
+                                     const uint64_t *ts, void *scratch, uint64_t cap, uint8_t *keys16, uint8_t *fam,
+                                     float *feat, float *prob, uint8_t *dec, uint32_t rows_cap,
+                                     const ScoreParams &P, uint32_t salt, void *sacc, uint32_t epoch,
+                                     const uint32_t *seg_slot, hipStream_t st);
 
 size_t flow_acc_bytes();
 size_t slot_acc_bytes();
