@@ -113,7 +113,7 @@ struct fsx_ctx {
     hipEvent_t fork_ev = nullptr, join_ev = nullptr;
     hipStream_t walk_stream = nullptr;   // third stream: long-segment walker
     hipEvent_t walk_fork_ev = nullptr, walk_join_ev = nullptr;
-    hipEvent_t heavy_fork_ev = nullptr, heavy_flow_ev = nullptr;   // heavy work after sort pass 0
+    hipEvent_t heavy_fork_ev = nullptr, heavy_flow_ev = nullptr;   // heavy work after the sort
     int ring_n = 0;
     const char *acc_name[kMaxNames]{};
     double acc_ms[kMaxNames]{};

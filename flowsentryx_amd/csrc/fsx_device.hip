@@ -2124,11 +2124,42 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
     // segments).
     hipStream_t hs = (st3 && heavy_fork_ev && heavy_flow_ev) ? st3 : st;
     const int hs_id = hs == st ? 0 : 2;
+    // the heavy flow sums: on the flow stream ahead of the light flow tiles (a fourth stream
+    // would share a hardware queue with the limiter chain: GPU_MAX_HW_QUEUES is 4)
+    const bool fork_f = flows && do_limit && st2 && fork_ev && join_ev && !getenv("FSX_NO_FLOW_FORK");
+    hipStream_t hf = (hs != st && fork_f) ? st2 : hs;
+    const int hf_id = hf == st2 && hf != st ? 1 : hs_id;
     uint64_t *S_fin = sc.packed[npass & 1], *pay_fin = sc.pay[npass & 1];
     // heavy verdict lists live in the sort's other buffer, over the heavy positions (which the
     // passes >= 1 never write)
     const HeavyLists hlists{tagh ? reinterpret_cast<uint32_t *>(sc.packed[(npass + 1) & 1]) : nullptr, sc.heavy,
                             tstate, bs};
+    // the heavy runs' walker and flow sums, forked right after the sort (A/B, config 2: right
+    // after pass 0 they slowed passes 1-2, after the heads they delayed the walkers; a fourth
+    // stream shared a hardware queue with the limiter chain)
+    auto launch_heavy = [&]() -> hipError_t {
+        hipError_t e;
+        if (hs != st) {
+            if ((e = hipEventRecord(heavy_fork_ev, st)) != hipSuccess) return e;
+            if ((e = hipStreamWaitEvent(hs, heavy_fork_ev, 0)) != hipSuccess) return e;
+            mark_on(nullptr, hs_id);
+            if (flows && hf != hs) {
+                if ((e = hipStreamWaitEvent(hf, heavy_fork_ev, 0)) != hipSuccess) return e;
+                mark_on(nullptr, hf_id);
+            }
+        }
+        k_walk_heavy<<<kHeavyMax / 4, 256, 0, hs>>>(S_fin, bs, sc.sort_ctl, sc.gbase, ts, len, pay_fin,
+                                                      table, lim, hlists);
+        mark_on("k_walk_heavy", hs_id);
+        if (flows) {
+            if ((e = launch_flows_heavy(S_fin, pay_fin, ts, len, bs, sc.sort_ctl, sc.gbase, sc.heavy_flow,
+                                        sc.cap, hf)) != hipSuccess)
+                return e;
+            mark_on("k_flow_heavy", hf_id);
+            if (hf != st && (e = hipEventRecord(heavy_flow_ev, hf)) != hipSuccess) return e;
+        }
+        return hipSuccess;
+    };
     k_hist_prep<<<1, 256, 0, st>>>(sc.sort_ctl, sc.gbase, bs, heavy_sort ? dp.light_b : 256u);
     if (do_limit) k_batch_check<<<1, 1, 0, st>>>(bs, tstate, lim);
     const uint32_t gen0 = onesweep ? next_generation() : 0u;
@@ -2158,27 +2189,9 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
             k_tile_scatter<kLatePayDefault><<<ntiles, 256, 0, st>>>(in, out, n, Ld, shift, pmask, pass == 0, sc.hist, tcap, bs,
                                                    pin, pout, ts, len);
             mark("k_tile_scatter");
-            // after the last pass (right after pass 0 the heavy work slowed passes 1-2 by more
-            // than it gained: 4.18 vs 4.12 ms/step, scripts/ab_env.sh)
-            if (pass == npass - 1 && tagh) {   // the heavy runs: their walker and flow sums
-                if (hs != st) {
-                    if ((e = hipEventRecord(heavy_fork_ev, st)) != hipSuccess) return e;
-                    if ((e = hipStreamWaitEvent(hs, heavy_fork_ev, 0)) != hipSuccess) return e;
-                    mark_on(nullptr, hs_id);
-                }
-                k_walk_heavy<<<kHeavyMax / 4, 256, 0, hs>>>(S_fin, bs, sc.sort_ctl, sc.gbase, ts, len, pay_fin,
-                                                              table, lim, hlists);
-                mark_on("k_walk_heavy", hs_id);
-                if (flows) {
-                    if ((e = launch_flows_heavy(S_fin, pay_fin, ts, len, bs, sc.sort_ctl, sc.gbase, sc.heavy_flow,
-                                                sc.cap, hs)) != hipSuccess)
-                        return e;
-                    mark_on("k_flow_heavy", hs_id);
-                    if (hs != st && (e = hipEventRecord(heavy_flow_ev, hs)) != hipSuccess) return e;
-                }
-            }
         }
     }
+    if (tagh && (e = launch_heavy()) != hipSuccess) return e;
     if (npass & 1) {
         std::swap(sc.packed[0], sc.packed[1]);
         std::swap(sc.pay[0], sc.pay[1]);
@@ -2211,7 +2224,7 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
                               tagh, fs)) != hipSuccess)
             return e;
         if (tagh) {   // the heavy sources' rows, from their sums (k_flow_heavy)
-            if (hs != fs && (e = hipStreamWaitEvent(fs, heavy_flow_ev, 0)) != hipSuccess) return e;
+            if (hf != fs && (e = hipStreamWaitEvent(fs, heavy_flow_ev, 0)) != hipSuccess) return e;
             if ((e = launch_flows_heavy_finish(S, bs, sc.sort_ctl, sc.seg_start, in, len, ts, sc.heavy_flow, sc.cap,
                                                flows->keys16, flows->fam, flows->feat, flows->prob, flows->dec,
                                                flows->cap, flows->score, lim.salt32,
