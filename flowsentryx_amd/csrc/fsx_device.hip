@@ -1124,34 +1124,29 @@ __global__ __launch_bounds__(256) void k_heads_count(const uint64_t *__restrict_
 }
 
 // Single block: exclusive scan of per-tile counts (in place), nseg, seg_start[nseg]=M.
-__global__ __launch_bounds__(1024) void k_scan_tiles_u32(uint32_t *__restrict__ cnt, BatchState *bs,
-                                                         uint32_t *seg_start, uint32_t light_only) {
-    __shared__ uint32_t s_w[16];
-    __shared__ uint32_t s_carry;
+// (256 threads, four tiles each per round: a single block of this size still finds a CU
+// while the side streams' grids occupy the chip)
+__global__ __launch_bounds__(256) void k_scan_tiles_u32(uint32_t *__restrict__ cnt, BatchState *bs,
+                                                        uint32_t *seg_start, uint32_t light_only) {
+    __shared__ uint32_t s_tmp[4];
     const uint32_t M = light_only ? bs->n_light : bs->n_valid;
     const uint32_t ntiles = (M + kTile - 1) / kTile;
-    const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
-    if (threadIdx.x == 0) s_carry = 0;
-    __syncthreads();
+    uint32_t carry = 0;
     for (uint32_t c0 = 0; c0 < ntiles; c0 += 1024) {
-        const uint32_t i = c0 + threadIdx.x;
-        const uint32_t x = i < ntiles ? cnt[i] : 0u;
-        const uint32_t incl = wave_incl_sum(x);
-        if (lane == 63) s_w[w] = incl;
-        __syncthreads();
-        uint32_t off = s_carry, tot = 0;
-        for (uint32_t k = 0; k < 16; ++k) {
-            off += k < w ? s_w[k] : 0u;
-            tot += s_w[k];
-        }
-        if (i < ntiles) cnt[i] = off + incl - x;
-        __syncthreads();
-        if (threadIdx.x == 0) s_carry += tot;
-        __syncthreads();
+        const uint32_t i = c0 + threadIdx.x * 4u;
+        uint32_t x[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) x[k] = i + k < ntiles ? cnt[i + k] : 0u;
+        uint32_t tot;
+        uint32_t off = carry + block256_excl(x[0] + x[1] + x[2] + x[3], s_tmp, &tot);
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (i + k < ntiles) { cnt[i + k] = off; off += x[k]; }
+        carry += tot;
     }
     if (threadIdx.x == 0) {
-        bs->nseg = s_carry;
-        seg_start[s_carry] = M;
+        bs->nseg = carry;
+        seg_start[carry] = M;
     }
 }
 
@@ -1522,24 +1517,21 @@ __global__ __launch_bounds__(256) void k_seg_count(const BatchState *bs,
     if (threadIdx.x < kSegClasses) blk[threadIdx.x * kSegBlocks + blockIdx.x] = sh[threadIdx.x];
 }
 
-// Exclusive scan of the class-major [class][block] counts; class totals to cls.
-__global__ __launch_bounds__(1024) void k_seg_scan(uint32_t *__restrict__ blk, uint32_t *cls) {
-    static_assert(kSegClasses * kSegBlocks == 16 * 1024, "one 16-entry run per thread");
-    __shared__ uint32_t s_w[16];
+// Exclusive scan of the class-major [class][block] counts; class totals to cls (256
+// threads, 64 consecutive counts each: a run never crosses a class).
+__global__ __launch_bounds__(256) void k_seg_scan(uint32_t *__restrict__ blk, uint32_t *cls) {
+    static_assert(kSegClasses * kSegBlocks == 64 * 256 && kSegBlocks % 64 == 0, "one 64-count run per thread");
+    __shared__ uint32_t s_tmp[4];
     __shared__ uint32_t s_cls[kSegClasses];
-    const uint32_t t = threadIdx.x, lane = lane_id(), w = t >> 6;
+    const uint32_t t = threadIdx.x;
     if (t < kSegClasses) s_cls[t] = 0;
-    uint32_t v[16], sum = 0;
+    uint32_t v[64], sum = 0;
 #pragma unroll
-    for (int k = 0; k < 16; ++k) { v[k] = blk[t * 16 + k]; sum += v[k]; }
-    const uint32_t incl = wave_incl_sum(sum);
-    if (lane == 63) s_w[w] = incl;
-    __syncthreads();
-    uint32_t off = incl - sum;
-    for (uint32_t k = 0; k < w; ++k) off += s_w[k];
+    for (int k = 0; k < 64; ++k) { v[k] = blk[t * 64 + k]; sum += v[k]; }
+    uint32_t off = block256_excl(sum, s_tmp, nullptr);   // (its barriers order the s_cls reset)
 #pragma unroll
-    for (int k = 0; k < 16; ++k) { blk[t * 16 + k] = off; off += v[k]; }
-    if (sum) atomicAdd(&s_cls[(t * 16) / kSegBlocks], sum);
+    for (int k = 0; k < 64; ++k) { blk[t * 64 + k] = off; off += v[k]; }
+    if (sum) atomicAdd(&s_cls[(t * 64) / kSegBlocks], sum);
     __syncthreads();
     if (t < kSegClasses) cls[t] = s_cls[t];
 }
@@ -2200,7 +2192,7 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
     const uint32_t lo = tagh ? 1u : 0u;   // light-only heads
     k_heads_count<<<gridTiles, 256, 0, st>>>(S, bs, in.hdr, sc.headf, sc.tile_aux, sc.sub_cnt, lo);
     mark("k_heads_count");
-    k_scan_tiles_u32<<<1, 1024, 0, st>>>(sc.tile_aux, bs, sc.seg_start, lo);
+    k_scan_tiles_u32<<<1, 256, 0, st>>>(sc.tile_aux, bs, sc.seg_start, lo);
     k_heads_write<<<gridTiles, 256, 0, st>>>(bs, sc.headf, sc.tile_aux, sc.seg_start, S,
                                              do_limit ? sc.seg_slot : nullptr, lim.table_mask, lo);
     if (tagh)
@@ -2242,7 +2234,7 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
         uint32_t *cls = sc.sort_ctl + 1028;
         const uint32_t short_seg = lim.limiter == 1 ? kShortSegSliding : kShortSegFixed;
         k_seg_count<<<kSegBlocks, 256, 0, st>>>(bs, sc.seg_start, sc.hist, short_seg);
-        k_seg_scan<<<1, 1024, 0, st>>>(sc.hist, cls);
+        k_seg_scan<<<1, 256, 0, st>>>(sc.hist, cls);
         k_seg_order<<<kSegBlocks, 256, 0, st>>>(bs, sc.seg_start, sc.hist, sc.seg_order, short_seg);
         mark("k_seg_order");
         if (lim.limiter == 1) {   // FSX_LIMIT_SLIDING_WINDOW
