@@ -482,8 +482,7 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
     auto count_digits = [&](uint64_t out, int hidx) {
         if (!ghist) return;
         const uint32_t d0 = (uint32_t)(out >> dp.shift[0]) & dp.mask[0];
-        atomicAdd(&s_hist[0][d0], 1u);
-        atomicAdd(&s_t0[d0], 1u);
+        atomicAdd(&s_t0[d0], 1u);   // (the block's digit-0 totals from s_t0 per sort tile)
         if (hidx < 0)   // heavy entries are final after pass 0
             for (uint32_t dg = 1; dg < dp.npass; ++dg)
                 atomicAdd(&s_hist[dg][(uint32_t)(out >> dp.shift[dg]) & dp.mask[dg]], 1u);
@@ -680,9 +679,11 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
         wave_lds_order();
         if (q % kSteps == kSteps - 1) {   // sort tile done: its deferred packets, then its digit-0 counts
             flush();
-            if (thist) {
+            if (ghist) {
                 __syncthreads();
-                if (threadIdx.x <= dp.mask[0]) thist[(size_t)threadIdx.x * tcap + tile_of(q)] = s_t0[threadIdx.x];
+                const uint32_t c0 = s_t0[threadIdx.x];
+                s_hist[0][threadIdx.x] += c0;
+                if (thist && threadIdx.x <= dp.mask[0]) thist[(size_t)threadIdx.x * tcap + tile_of(q)] = c0;
                 s_t0[threadIdx.x] = 0;
                 __syncthreads();
             }
