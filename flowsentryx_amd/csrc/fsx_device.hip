@@ -1833,13 +1833,24 @@ __global__ __launch_bounds__(256) void k_fill_scatter(const uint8_t *__restrict_
         if (lane == 0) excl = 0;
         excl = excl > pre ? excl : pre;
         uint8_t cur = excl ? (uint8_t)(excl & 0xFFu) : carry[t];
+        bool mine = false;   // a DROP among this thread's valid positions
+        uint32_t nvalid = 0;
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
             const uint32_t m = (f[k >> 2] >> (8 * (k & 3))) & 0xFFu;
             if (m) cur = (uint8_t)m;
             s_v[threadIdx.x * 16u + k] = cur;
+            if (p0 + (uint32_t)k < M) {
+                ++nvalid;
+                mine |= cur == XDP_DROP;
+            }
         }
-        __syncthreads();
+        // most light tiles hold no DROP at all (the floods are the heavy sources, whose
+        // verdicts travel as lists): count them PASS and move on
+        if (!__syncthreads_or(mine ? 1 : 0)) {
+            n_pass += nvalid;
+            continue;
+        }
         const uint32_t tile0 = t * kTile;
         const uint64_t lt = (1ull << lane) - 1ull;
         if (agg) {
