@@ -1310,7 +1310,16 @@ hipError_t launch_index_rebuild(Slot *table, const Limits &lim, const TableIndex
 // search instead of one per binary-search step). The boundary is per limiter: the
 // fixed-window wave walker runs beside the thread walker on its own stream, so a
 // lower boundary balances the two (measured on config 2: 256 fixed, 512 sliding).
-constexpr uint32_t kShortSegFixed = 256;
+#ifndef FSX_SHORT_SEG_FIXED
+#define FSX_SHORT_SEG_FIXED 256   // (A/B: scripts/build_variant.sh)
+#endif
+constexpr uint32_t kShortSegFixed = FSX_SHORT_SEG_FIXED;
+#ifndef FSX_WALK_LONG_BLOCKS
+#define FSX_WALK_LONG_BLOCKS 2048   // blocks of the wave walker (one source per wave)
+#endif
+#ifndef FSX_WALK_SHORT_BLOCKS
+#define FSX_WALK_SHORT_BLOCKS 2048  // blocks of the thread walker
+#endif
 constexpr uint32_t kShortSegSliding = 512;
 
 
@@ -2262,12 +2271,12 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
                 if ((e = hipStreamWaitEvent(st3, walk_fork_ev, 0)) != hipSuccess) return e;
                 mark_on(nullptr, 2);
             }
-            k_walk_fixed_long<<<1024, 256, 0, fork3 ? st3 : st>>>(S, bs, sc.seg_start, sc.seg_slot, ts, len,
+            k_walk_fixed_long<<<FSX_WALK_LONG_BLOCKS, 256, 0, fork3 ? st3 : st>>>(S, bs, sc.seg_start, sc.seg_slot, ts, len,
                                                                   sc.pay[0], sc.seg_order, cls, sc.marks,
                                                                   table, lim, hlists);
             mark_on("k_walk_fixed_long", fork3 ? 2 : 0);
             if (fork3 && (e = hipEventRecord(walk_join_ev, st3)) != hipSuccess) return e;
-            k_walk_fixed<<<gridStream, 256, 0, st>>>(S, bs, sc.seg_start, sc.seg_slot, ts, len, sc.pay[0],
+            k_walk_fixed<<<std::min<uint32_t>(FSX_WALK_SHORT_BLOCKS, cdiv(n, 256)), 256, 0, st>>>(S, bs, sc.seg_start, sc.seg_slot, ts, len, sc.pay[0],
                                                      sc.seg_order, cls, sc.marks, table, lim, hlists);
             mark("k_walk_fixed");
             if (fork3 && (e = hipStreamWaitEvent(st, walk_join_ev, 0)) != hipSuccess) return e;
