@@ -577,6 +577,11 @@ def main():
     info = head.get("info", {})
     dom = max(timings, key=lambda r: r[1]) if timings else None
     roofline = None
+    if world > 1:   # the per-kernel split is of one owner sub-batch: the roofline is the N = 1 line's
+        roofline = {"bound": "hbm", "kernel": "k_parse", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": None, "traffic": None,
+                    "note": "N > 1: kernels run on owner sub-batches of received records; see the N = 1 line"}
+        dom = None
     if dom:
         name, ms_per_batch, launches = dom
         kb = KERNEL_BYTES.get(name, {"unit": "packet", "algo": 0, "impl": 0})

@@ -89,6 +89,16 @@ def test_sharded_flow_features_equal_one_gpu(tmp_path, world, v6):
     assert res["filtered"] == 0   # (flows: every packet reaches its owner)
 
 
+def test_sharded_flow_features_heavy_path(tmp_path):
+    """The same with a table of 2^17 slots, so every owner runs the heavy-source sort, the
+    heavy verdict lists and the heavy runs' flow sums (k_flow_heavy) in accumulate mode."""
+    spec = dict(BASE, n_ips=600, v6_frac=0.2, nonip_frac=0.02, seed=41, flows=True,
+                cfg=dict(pps_threshold=40, window_ns=2_000_000, block_ns=5_000_000, max_entries=1 << 16),
+                owner_batch=1 << 15)
+    res = run_sharded(tmp_path, 2, spec, engine="hip")
+    assert res["filtered"] == 0
+
+
 def test_sharded_hip_owners_limiters(tmp_path):
     for lim, maps, extra in ((1, [1, 2, 3, 4], dict(pps_threshold=5, window_ns=1_000_000,
                                                      block_ns=50_000)),
