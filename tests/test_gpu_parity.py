@@ -445,14 +445,20 @@ def test_process_batch_device(native, oracle):
     _process_batch_device(native, oracle, [oracle.synth(p, s, 0, int(p.n))])
 
 
-@pytest.mark.parametrize("case", ["mixed", "gather", "jitter", "carry"])
+@pytest.mark.parametrize("case", ["mixed", "gather", "jitter", "carry", "all_heavy", "nonip_only"])
 def test_fused_flows(native, oracle, case):
-    """The walker-fused flow rows beside the heavy-source flow tiles: mixed families with
-    short / long / heavy sources, the gather path (no payload words), non-monotone clocks
-    (exact wave replay, wrapped inter-arrival times) and maps carried across batches."""
+    """The full path with the heavy-source machinery (light-only heads, heavy runs appended,
+    heavy verdict lists, chunked heavy flow sums): mixed families with short / long / heavy
+    sources, the gather path (no payload words), non-monotone clocks (exact wave replay,
+    wrapped inter-arrival times), maps carried across batches, a stream whose sources are all
+    heavy (no light entries) and one without IP packets."""
     from flowsentryx_amd import synth
     rng = np.random.default_rng(0xF10 + len(case))
-    if case == "mixed":
+    if case == "all_heavy":
+        batches = [rand_stream(rng, 60_000, 40, dt_max=300, v6_frac=0.2)]
+    elif case == "nonip_only":
+        batches = [rand_stream(rng, 5_000, 10, dt_max=300, nonip_frac=1.0)]
+    elif case == "mixed":
         batches = [rand_stream(rng, 300_000, 3000, dt_max=400, v6_frac=0.3, nonip_frac=0.03, short_frac=0.01)]
     elif case == "gather":
         p, s = synth.config_params(2, n=1 << 18)
