@@ -1869,19 +1869,9 @@ __global__ __launch_bounds__(256) void k_fill_scatter(const uint8_t *__restrict_
                 const uint8_t v = ok ? s_v[j] : 0;
                 n_pass += v == XDP_PASS;
                 n_drop += v == XDP_DROP;
-                const bool drop = v == XDP_DROP;
-                const uint32_t ch = drop ? pk_idx(S[tile0 + j]) >> kVChunkBits : 0u;
-                uint64_t pending = __ballot(drop);
-                while (pending) {   // rank among the tile's drops of the same chunk
-                    const int lead = __ffsll((unsigned long long)pending) - 1;
-                    const uint32_t lc = __shfl(ch, lead);
-                    const uint64_t same = __ballot(drop && ch == lc) & pending;
-                    uint32_t base = 0;
-                    if ((int)lane == lead) base = atomicAdd(&s_cc[lc], (uint32_t)__popcll(same));
-                    base = __shfl(base, lead);
-                    if ((same >> lane) & 1ull) s_rk[j] = (uint16_t)(base + (uint32_t)__popcll(same & lt));
-                    pending &= ~same;
-                }
+                // its slot among the tile's drops of its arrival chunk (a list's order is
+                // irrelevant to k_verdict_apply): one returning LDS add per DROP
+                if (v == XDP_DROP) s_rk[j] = (uint16_t)atomicAdd(&s_cc[pk_idx(S[tile0 + j]) >> kVChunkBits], 1u);
             }
             __syncthreads();
             for (uint32_t c = threadIdx.x; c < nchunks; c += 256) {
