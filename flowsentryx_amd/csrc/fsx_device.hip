@@ -2129,8 +2129,9 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
     const int hs_id = hs == st ? 0 : 2;
     // the heavy flow sums: on the flow stream ahead of the light flow tiles (a fourth stream
     // would share a hardware queue with the limiter chain: GPU_MAX_HW_QUEUES is 4)
-    const bool fork_f = flows && do_limit && st2 && fork_ev && join_ev && !getenv("FSX_NO_FLOW_FORK");
-    hipStream_t hf = (hs != st && fork_f) ? st2 : hs;
+    static const bool no_fork = getenv("FSX_NO_FLOW_FORK") != nullptr;   // A/B: flows serialized
+    const bool fork = flows && do_limit && st2 && fork_ev && join_ev && !no_fork;   // flows beside the limiter
+    hipStream_t hf = (hs != st && fork) ? st2 : hs;
     const int hf_id = hf == st2 && hf != st ? 1 : hs_id;
     uint64_t *S_fin = sc.packed[npass & 1], *pay_fin = sc.pay[npass & 1];
     // heavy verdict lists live in the sort's other buffer, over the heavy positions (which the
@@ -2210,8 +2211,6 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
         k_heads_heavy<<<1, 256, 0, st>>>(bs, sc.sort_ctl, sc.gbase, sc.seg_start, do_limit ? sc.seg_slot : nullptr,
                                          S, lim.table_mask);
     mark("k_heads_write");
-    static const bool no_fork = getenv("FSX_NO_FLOW_FORK") != nullptr;   // A/B: flows serialized
-    const bool fork = flows && do_limit && st2 && fork_ev && join_ev && !no_fork;
     if (flows) {
         hipStream_t fs = st;
         if (fork) {   // the features run beside the limiter

@@ -275,7 +275,13 @@ hipError_t launch_flows(const uint64_t *S, const uint64_t *pay, BatchState *bs, 
 // final sorted arrays (passes >= 1 write only [0, n_light)). Chunk j of run h is item
 // pre[h] + j; pre (computed by every block, written by block 0) and the per-chunk
 // partials live in the context's heavy-flow scratch.
-constexpr uint32_t kHeavyChunk = 8192;
+#ifndef FSX_HEAVY_CHUNK
+#define FSX_HEAVY_CHUNK 8192   // positions per k_flow_heavy wave (A/B: scripts/build_variant.sh)
+#endif
+#ifndef FSX_HEAVY_FLOW_BLOCKS
+#define FSX_HEAVY_FLOW_BLOCKS 1024
+#endif
+constexpr uint32_t kHeavyChunk = FSX_HEAVY_CHUNK;
 
 __device__ __forceinline__ void heavy_chunk_prefix(const uint32_t *cnt0, uint32_t *s_pre, uint32_t *s_tmp) {
     const uint32_t h = threadIdx.x;
@@ -401,7 +407,7 @@ hipError_t launch_flows_heavy(const uint64_t *S, const uint64_t *pay, const uint
     FlowAcc *part = reinterpret_cast<FlowAcc *>(scratch);
     FlowAcc *hacc = part + (cap / kHeavyChunk + kHeavyMax + 1);
     uint32_t *pre = reinterpret_cast<uint32_t *>(hacc + kHeavyMax);
-    const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(1024, (cap / kHeavyChunk + kHeavyMax + 3) / 4));
+    const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(FSX_HEAVY_FLOW_BLOCKS, (cap / kHeavyChunk + kHeavyMax + 3) / 4));
     k_flow_heavy<<<grid, 256, 0, st>>>(S, pay, ts, len, bs, cnt0, base0, pre, part);
     k_flow_heavy_sum<<<kHeavyMax / 4, 256, 0, st>>>(bs, pre, part, hacc);
     return hipGetLastError();
