@@ -2,11 +2,14 @@
 """Benchmark: Mpps of FlowSentryX verdicts on MI355X (BASELINE.json metric).
 
 One "step" = one pass of the hot path over one batch of synthetic packets resident in
-HBM, starting from empty maps (fsx_reset is inside the timed step): parse -> per-source
-fixed-window rate limit + blacklist -> verdicts + map state (src/fsx_kern.c:96-347
-semantics) -> per-source flow features -> q8 MLP score of every source with the
-reference weights (model/model.py:132-137). N=1 headline workload: BASELINE config 2 —
-64M IPv4/UDP packets from 1M Zipf(1.1) sources over 30 s.
+HBM: parse -> per-source fixed-window rate limit + blacklist -> verdicts + map state
+(src/fsx_kern.c:96-347 semantics) -> per-source flow features -> q8 MLP score of every
+source with the reference weights (model/model.py:132-137). N=1 headline workload: BASELINE
+config 2 — 64M IPv4/UDP packets from 1M Zipf(1.1) sources over 30 s — as a stream: step k
+is the batch shifted by k x 30 s and the maps carry from batch to batch, as the reference's
+BPF maps persist across packets; consecutive batches are pipelined on the device
+(fsx_set_pipeline). Legs: `cold` (every step the same batch from empty maps, fsx_reset in
+the step) and `unpipelined` (the stream without pipelining).
 
 Multi-GPU (torch.distributed.run, one rank per GPU): weak scaling — one stream of
 N x 64M packets from one source population at the config's packet rate; rank r holds
@@ -79,9 +82,14 @@ def parse_args():
                     help="N>1 collectives: nccl (RCCL over xGMI) or gloo (rehearsal on one GPU)")
     ap.add_argument("--limiter", choices=["fixed", "sliding", "token"], default="fixed",
                     help="limiter of the timed main loop (diagnostics; the headline is fixed)")
-    ap.add_argument("--legs", default="limiters,rules,warm,config3,config4,config5",
+    ap.add_argument("--cold", action="store_true",
+                    help="headline: every step the same batch from empty maps (fsx_reset inside "
+                         "the step) instead of consecutive batches with the maps carried")
+    ap.add_argument("--legs", default="cold,unpipelined,limiters,rules,config3,config4,config5",
                     help="comma-separated extra legs ('' for none)")
     ap.add_argument("--leg-steps", type=int, default=5, help="timed steps per leg")
+    ap.add_argument("--kernel-timing-steps", type=int, default=5,
+                    help="extra steps with per-kernel HIP events (0: none)")
     ap.add_argument("--config5-packets", type=int, default=1 << 28)
     ap.add_argument("--config4-packets", type=int, default=None,
                     help="config-4 packets per rank (default: 1/8 of the 1B-packet stream)")
@@ -235,8 +243,15 @@ def main():
 
     # ------------------------------------------------------------------ workload runner
     def run_workload(cfg_no, n, steps, warmup, with_flows, kernel_timing=False, check=False,
-                     cpu=False):
-        """Weak-scaled config cfg_no (n packets per rank), full pipeline; returns a dict."""
+                     cpu=False, stream=False, pipelined=True):
+        """Weak-scaled config cfg_no (n packets per rank), full pipeline; returns a dict.
+
+        stream=False (cold): every step is the same batch from empty maps (fsx_reset inside
+        the step). stream=True: consecutive batches of one stream with the maps carried
+        (the reference's maps persist; no reset) — batch k is the config batch shifted by k
+        stream durations (one pre-generated ts array per batch in HBM, two verdict buffers
+        alternating); on one GPU the batches are pipelined (fsx_set_pipeline: the parse and
+        sort of batch k + 1 overlap the tail of batch k)."""
         p, zipf_s = synth.config_params(cfg_no, n=None if cfg_no == 4 else n)
         # ONE stream of world*n packets at the config's packet rate from one population
         # (config 4: the 1B-packet stream itself, rank r's share of n packets); in
@@ -266,30 +281,42 @@ def main():
             if with_flows:
                 eng.enable_flows(fcap)
             plane = ShardedDataPlane(eng)
-        ptr = {k: v.data_ptr() for k, v in d.items()}
+        ntime = max(1, min(steps, args.kernel_timing_steps)) if kernel_timing and args.kernel_timing_steps else 0
+        if stream:
+            dur = int(p.duration_ns)
+            tss = [d["ts"] + k * dur for k in range(warmup + steps + ntime)]
+            vb = [d["v"], torch.empty_like(d["v"])]
+            torch.cuda.synchronize()   # (torch's kernels are not ordered with the library's streams)
+            if world == 1 and pipelined:
+                ctx.set_pipeline(True)
+        else:
+            tss, vb = [d["ts"]], [d["v"]]
 
-        def step(feat=False):
-            if not args.no_reset:
+        def step(k, feat=False, v=None):
+            ts_k = tss[k if stream else 0]
+            v = vb[k % 2] if v is None else v
+            if not stream and not args.no_reset:
                 ctx.reset()
             if plane is not None:
-                plane.reset()
-                plane.verdict_batch(d["hdr"], d["len"], d["ts"], n, d["v"], bounds=bounds, chunks=chunks)
+                if not stream:
+                    plane.reset()
+                plane.verdict_batch(d["hdr"], d["len"], ts_k, n, v, bounds=bounds, chunks=chunks)
             elif not with_flows:
-                ctx.verdict_batch_device(ptr["hdr"], ptr["len"], ptr["ts"], n, ptr["v"])
+                ctx.verdict_batch_device(d["hdr"].data_ptr(), d["len"].data_ptr(), ts_k.data_ptr(), n, v.data_ptr())
             else:
-                ctx.process_batch_device(ptr["hdr"], ptr["len"], ptr["ts"], n, ptr["v"],
+                ctx.process_batch_device(d["hdr"].data_ptr(), d["len"].data_ptr(), ts_k.data_ptr(), n, v.data_ptr(),
                                          fl["keys"].data_ptr(), fl["fam"].data_ptr(),
                                          fl["feat"].data_ptr() if feat else None,
                                          fl["prob"].data_ptr(), fl["dec"].data_ptr(), fcap)
 
-        for _ in range(warmup):
-            step()
+        for k in range(warmup):
+            step(k)
         ctx.sync()
         torch.cuda.synchronize()
         barrier()
         t0 = time.perf_counter()
-        for _ in range(steps):
-            step()
+        for k in range(warmup, warmup + steps):
+            step(k)
         ctx.sync()
         torch.cuda.synchronize()
         barrier()
@@ -297,13 +324,14 @@ def main():
         out = {"n": n, "p": p, "steps": steps, "elapsed": elapsed, "max_entries": max_entries,
                "mpps": n * world * steps / elapsed / 1e6, "ms_step": elapsed / steps * 1e3}
         info = ctx.last_batch_info()
-        if kernel_timing:
-            # per-kernel device times (a HIP event after every kernel) from separate
-            # steps, so the timed steps above carry no event records
+        if ntime:
+            # per-kernel device times (a HIP event after every kernel) from separate steps
+            # (the stream continued; timed batches run unpipelined), so the timed steps
+            # above carry no event records
             ctx.enable_timing(True)
             ctx.last_timings()
-            for _ in range(max(1, min(steps, 5))):
-                step()
+            for k in range(warmup + steps, warmup + steps + ntime):
+                step(k)
             ctx.sync()
             torch.cuda.synchronize()
             out["timings"] = ctx.last_timings()
@@ -327,30 +355,41 @@ def main():
             if with_flows:
                 out["malicious_sources"] = int(fl["dec"][:info["sources"]].sum().item())
         if (check or cpu) and world == 1:
-            # one more step, with the features written, then the CPU oracle on the same
-            # input bytes (the device generator is checked equal to the CPU twin by
+            # from empty maps: one batch (cold) or three consecutive pipelined batches
+            # (stream), the features written, then the CPU oracle on the same input bytes
+            # carrying its maps (the device generator is checked equal to the CPU twin by
             # tests/test_gpu_parity.py::test_device_synth_and_device_batch)
+            nb = 3 if stream else 1
             ctx.reset()
-            step(feat=True)
+            vs = [vb[0], vb[1], torch.empty_like(d["v"])][:nb]
+            for k in range(nb):
+                step(k, feat=k == nb - 1, v=vs[k])
             ctx.sync()
-            hdr, ln, ts = host_inputs(d, n)
-            vg = d["v"].cpu().numpy()
+            hdr, ln, _ = host_inputs(d, n)
             from oracle import pyoracle
             orc = pyoracle.ShardedOracle(cores, max_entries=max_entries)
-            c0 = time.perf_counter()
-            vo = orc.batch(hdr, ln, ts)
-            cdt = time.perf_counter() - c0
+            ok = True
+            for k in range(nb):
+                ts_k = tss[k].cpu().numpy().view(np.uint64)
+                c0 = time.perf_counter()
+                vo = orc.batch(hdr, ln, ts_k)
+                if k == 0:   # the CPU baseline: one batch from empty maps
+                    cdt = time.perf_counter() - c0
+                ok = ok and bool(np.array_equal(vs[k].cpu().numpy(), vo))
             out["cpu"] = {"value": round(n / cdt / 1e6, 3), "unit": "Mpps", "seconds": round(cdt, 3)}
             if check:
-                chk = {"packets": n, "verdicts_equal": bool(np.array_equal(vg, vo))}
+                chk = {"batches": nb, "packets": nb * n, "verdicts_equal": ok}
                 chk.update(compare_state(ctx, orc, (1, 2, 3, 4)))
                 if with_flows:
-                    chk["flows"] = check_flows(fl["keys"], fl["fam"], fl["feat"], fl["prob"],
-                                               ctx.last_batch_info()["sources"], hdr, ln, ts, model_fields)
+                    chk["flows" if nb == 1 else "flows_last_batch"] = check_flows(
+                        fl["keys"], fl["fam"], fl["feat"], fl["prob"], ctx.last_batch_info()["sources"],
+                        hdr, ln, ts_k, model_fields)
                 out["check"] = chk
             orc.close()
-            del hdr, ln, ts
+            del hdr, ln, ts_k
+            del vs
         ctx.close()
+        del tss, vb
         out["d"] = d
         return out
 
@@ -358,7 +397,7 @@ def main():
     n_head = args.packets or int(synth.config_params(args.config)[0].n)
     head = run_workload(args.config, n_head, args.steps, args.warmup, not args.no_mlp,
                         kernel_timing=True, check=not args.no_check and world == 1,
-                        cpu=not args.no_cpu_baseline and world == 1)
+                        cpu=not args.no_cpu_baseline and world == 1, stream=not args.cold)
     n = head["n"]
     p = head["p"]
     timings = head.get("timings", [])
@@ -485,6 +524,23 @@ def main():
                            "steps": len(ms), "new_sources_last_step": wi["new_sources"],
                            "sources": wi["sources"], "allowed": wa, "dropped": wd,
                            "note": "maps carried: step k = the batch shifted by k x 30 s"}
+
+    del d
+    torch.cuda.empty_cache()
+    for leg_name in ("cold", "unpipelined"):
+        if world == 1 and leg_name in legs and not (args.cold and leg_name == "cold"):
+            r_ = run_workload(args.config, n_head, args.leg_steps, 1, not args.no_mlp,
+                              check=leg_name == "cold" and not args.no_check,
+                              stream=leg_name != "cold", pipelined=False)
+            results[leg_name] = {"value": round(r_["mpps"], 2), "unit": "Mpps",
+                                 "ms_per_step": round(r_["ms_step"], 4), "steps": r_["steps"],
+                                 "check": r_.get("check"),
+                                 "note": "every step the same batch from empty maps (fsx_reset in the step)"
+                                 if leg_name == "cold" else
+                                 "the headline's stream (maps carried), batches not pipelined"}
+            del r_["d"], r_
+            torch.cuda.empty_cache()
+    d = None
 
     del d
     torch.cuda.empty_cache()
@@ -633,7 +689,11 @@ def main():
         "data": "synthetic (counter-based generator, fsx_synth_common.h)",
         "config": {"workload": f"BASELINE config {args.config}: {n} IPv4/UDP packets per GPU, "
                                f"{p.n_ips} Zipf(1.1) sources, {p.duration_ns / 1e9:g} s; "
-                               "fixed-window limiter (src/fsx_kern.c), maps reset each step"
+                               "fixed-window limiter (src/fsx_kern.c), "
+                               + ("maps reset each step" if args.cold else
+                                  "consecutive batches of the stream with the maps carried (batch k = the "
+                                  "config batch shifted by k x duration)"
+                                  + (", batches pipelined" if world == 1 else ""))
                                + ("" if args.no_mlp else "; per-source features + q8 MLP score "
                                   "(model_weights.pth)"),
                    "packets_per_gpu": n, "sources": sources,
@@ -641,6 +701,7 @@ def main():
         "roofline": roofline, "pipeline": pipeline, "cpu_baseline": cpu,
         "check": head.get("check"),
         "limiters": results.get("limiters"), "prefix_rules": results.get("prefix_rules"),
+        "cold": results.get("cold"), "unpipelined": results.get("unpipelined"),
         "warm": results.get("warm"), "config3": results.get("config3"),
         "config4": results.get("config4"), "config5": results.get("config5"),
         "exchange": head.get("exchange"),

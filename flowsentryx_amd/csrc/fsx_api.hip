@@ -121,6 +121,26 @@ struct fsx_ctx {
     int acc_n = 0;
     uint64_t acc_batches = 0;
     bool pending = false;
+    // batch pipelining (fsx_set_pipeline): two sets of the front buffers (sort arrays,
+    // BatchState), the batch of each set still in flight, the tail-done event per set
+    struct FrontBufs {
+        uint64_t *packed[2], *pay[2];
+        uint32_t *hist, *sort_ctl, *gbase;
+        HeavySet *heavy;
+        BatchState *bs;
+    };
+    bool pipe = false;
+    FrontBufs fb[2]{};
+    int par = 0;                      // set of the last pipelined batch
+    bool fl_on[2]{};                  // a pipelined batch of set p is in flight
+    uint32_t fl_born[2]{};
+    hipEvent_t tail_done[2]{};
+    hipEvent_t front_done = nullptr;  // after the last pipelined batch's sort
+    hipEvent_t parse_done = nullptr;  // after the current pipelined batch's parse
+    TailArgs tail_args{};             // the last pipelined batch's tail, not yet enqueued
+    bool tail_pending = false;
+    int tail_par = 0;
+    bool tail_join = false;           // the last pipelined batch's tail is not joined into stream
     char err[512]{};
 };
 
@@ -225,15 +245,74 @@ void fsx_config_default(fsx_config *cfg) {
 
 const char *fsx_last_error(const fsx_ctx *ctx) { return ctx ? ctx->err : "null context"; }
 
+// The deferred tail of the last pipelined batch onto the walker stream (and the flows on the
+// aux stream), after event `after` on the context stream.
+static hipError_t flush_tail(fsx_ctx *c, hipEvent_t after) {
+    if (!c->tail_pending) return hipSuccess;
+    c->tail_pending = false;
+    hipError_t e;
+    if ((e = hipStreamWaitEvent(c->walk_stream, after, 0)) != hipSuccess) return e;
+    if ((e = hipStreamWaitEvent(c->aux_stream, after, 0)) != hipSuccess) return e;
+    if ((e = launch_tail(c->tail_args)) != hipSuccess) return e;
+    return hipEventRecord(c->tail_done[c->tail_par], c->walk_stream);
+}
+
+// PipeSplit::on_parse: the previous batch's tail goes in right after this batch's parse.
+static hipError_t pipe_on_parse(void *p) {
+    fsx_ctx *c = static_cast<fsx_ctx *>(p);
+    if (!c->tail_pending) return hipSuccess;
+    hipError_t e = hipEventRecord(c->parse_done, c->stream);
+    return e != hipSuccess ? e : flush_tail(c, c->parse_done);
+}
+
+// Every entry point except the batch calls: the last pipelined batch's tail is enqueued and
+// the context stream continues after it (the tail runs on its own streams).
 static int sel(fsx_ctx *c) {
     HIPCHK(c, hipSetDevice(c->device));
+    if (c->tail_pending) {
+        hipError_t e = flush_tail(c, c->front_done);
+        if (e != hipSuccess) return set_err(c, -EIO, "pipelined tail: %s", hipGetErrorString(e));
+    }
+    if (c->tail_join) {
+        c->tail_join = false;
+        HIPCHK(c, hipStreamWaitEvent(c->stream, c->tail_done[c->par], 0));
+    }
     return 0;
+}
+
+static bool busy(const fsx_ctx *c) { return c->pending || c->fl_on[0] || c->fl_on[1]; }
+
+// The front buffers of set p become the context's current sort arrays and BatchState.
+static void use_front(fsx_ctx *c, int p) {
+    const fsx_ctx::FrontBufs &f = c->fb[p];
+    for (int b = 0; b < 2; ++b) { c->sc.packed[b] = f.packed[b]; c->sc.pay[b] = f.pay[b]; }
+    c->sc.hist = f.hist;
+    c->sc.sort_ctl = f.sort_ctl;
+    c->sc.gbase = f.gbase;
+    c->sc.heavy = f.heavy;
+    c->bs = f.bs;
+}
+
+static void free_front(fsx_ctx::FrontBufs &f) {
+    for (int b = 0; b < 2; ++b) { hipFree(f.packed[b]); hipFree(f.pay[b]); }
+    hipFree(f.hist); hipFree(f.sort_ctl); hipFree(f.gbase); hipFree(f.heavy); hipFree(f.bs);
+    f = fsx_ctx::FrontBufs{};
 }
 
 void fsx_close(fsx_ctx *c) {
     if (!c) return;
     hipSetDevice(c->device);
+    sel(c);   // (a pipelined batch's deferred tail)
     if (c->stream) hipStreamSynchronize(c->stream);
+    if (c->walk_stream) hipStreamSynchronize(c->walk_stream);
+    if (c->aux_stream) hipStreamSynchronize(c->aux_stream);
+    if (c->fb[1].bs) {
+        use_front(c, 0);
+        free_front(c->fb[1]);
+    }
+    for (int p = 0; p < 2; ++p) if (c->tail_done[p]) hipEventDestroy(c->tail_done[p]);
+    if (c->front_done) hipEventDestroy(c->front_done);
+    if (c->parse_done) hipEventDestroy(c->parse_done);
     free_scratch(c);
     hipFree(c->table); hipFree(c->tstate); hipFree(c->bs);
     hipFree(c->d_hdr); hipFree(c->d_len); hipFree(c->d_ts); hipFree(c->d_verdict);
@@ -285,11 +364,14 @@ int fsx_open(fsx_ctx **out, const fsx_config *cfg) {
     if (rc) { fsx_close(c); return rc; }
     c->slots = next_pow2(std::max<uint64_t>(1024, 2 * k.max_entries));
     auto fail = [&](int r) { fsx_close(c); return r; };
-    if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) return fail(-EIO);
-    if (hipStreamCreateWithFlags(&c->aux_stream, hipStreamNonBlocking) != hipSuccess) return fail(-EIO);
+    // stream priorities (A/B: FSX_STREAM_PRIO="own,aux,walk", lower = more urgent)
+    int prio[3] = {0, 0, 0};
+    if (const char *ps = getenv("FSX_STREAM_PRIO")) sscanf(ps, "%d,%d,%d", &prio[0], &prio[1], &prio[2]);
+    if (hipStreamCreateWithPriority(&c->own_stream, hipStreamNonBlocking, prio[0]) != hipSuccess) return fail(-EIO);
+    if (hipStreamCreateWithPriority(&c->aux_stream, hipStreamNonBlocking, prio[1]) != hipSuccess) return fail(-EIO);
     if (hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming) != hipSuccess) return fail(-EIO);
     if (hipEventCreateWithFlags(&c->join_ev, hipEventDisableTiming) != hipSuccess) return fail(-EIO);
-    if (hipStreamCreateWithFlags(&c->walk_stream, hipStreamNonBlocking) != hipSuccess) return fail(-EIO);
+    if (hipStreamCreateWithPriority(&c->walk_stream, hipStreamNonBlocking, prio[2]) != hipSuccess) return fail(-EIO);
     if (hipEventCreateWithFlags(&c->walk_fork_ev, hipEventDisableTiming) != hipSuccess) return fail(-EIO);
     if (hipEventCreateWithFlags(&c->walk_join_ev, hipEventDisableTiming) != hipSuccess) return fail(-EIO);
     if (hipEventCreateWithFlags(&c->heavy_fork_ev, hipEventDisableTiming) != hipSuccess) return fail(-EIO);
@@ -308,6 +390,12 @@ int fsx_open(fsx_ctx **out, const fsx_config *cfg) {
     if (hipMemset(c->tstate, 0, sizeof(TableState)) != hipSuccess) return fail(-EIO);
     if (hipMemset(c->bs, 0, sizeof(BatchState)) != hipSuccess) return fail(-EIO);
     if (alloc_scratch(c, k.max_batch)) return fail(-ENOMEM);
+    {
+        fsx_ctx::FrontBufs &f = c->fb[0];
+        for (int b = 0; b < 2; ++b) { f.packed[b] = c->sc.packed[b]; f.pay[b] = c->sc.pay[b]; }
+        f.hist = c->sc.hist; f.sort_ctl = c->sc.sort_ctl; f.gbase = c->sc.gbase; f.heavy = c->sc.heavy;
+        f.bs = c->bs;
+    }
     if (k.limiter == FSX_LIMIT_SLIDING_WINDOW) {
         HistBufs &h = c->hist;
         h.cap = std::max<uint64_t>(2 * k.max_batch, 1u << 16);
@@ -338,6 +426,8 @@ int fsx_open(fsx_ctx **out, const fsx_config *cfg) {
 
 int fsx_set_stream(fsx_ctx *c, void *s) {
     if (!c) return -EINVAL;
+    int rc = sel(c);   // (the old stream joins the last pipelined tail)
+    if (rc) return rc;
     c->stream = s ? (hipStream_t)s : c->own_stream;
     return 0;
 }
@@ -368,6 +458,8 @@ static int rollback_batch(fsx_ctx *c, uint32_t born) {
     return 0;
 }
 
+static int batch_error(fsx_ctx *c, uint32_t err);
+
 static int check_batch(fsx_ctx *c) {
     if (!c->pending) return 0;
     c->pending = false;
@@ -379,13 +471,38 @@ static int check_batch(fsx_ctx *c) {
         const int rc = rollback_batch(c, born);
         if (rc) return rc;
     }
-    if (h.err & ERR_TABLE_FULL)
+    return batch_error(c, h.err);
+}
+
+// Pipelined batches still in flight, oldest first, with the device idle: the first failed
+// one and every later one (cancelled on the device) are rolled back; its error is returned.
+static int check_pipelined(fsx_ctx *c) {
+    int rc = 0;
+    bool failed = false;
+    for (int p : {c->par ^ 1, c->par}) {
+        if (!c->fl_on[p]) continue;
+        c->fl_on[p] = false;
+        BatchState h;
+        HIPCHK(c, hipMemcpy(&h, c->fb[p].bs, sizeof(h), hipMemcpyDeviceToHost));
+        if (!h.err && !failed) continue;
+        if (c->fl_born[p]) {
+            const int r = rollback_batch(c, c->fl_born[p]);
+            if (r) return r;
+        }
+        if (!failed) rc = batch_error(c, h.err);
+        failed = true;
+    }
+    return rc;
+}
+
+static int batch_error(fsx_ctx *c, uint32_t err) {
+    if (err & ERR_TABLE_FULL)
         return set_err(c, -ENOSPC, "map full: more than max_entries=%llu source IPs",
                        (unsigned long long)c->cfg.max_entries);
-    if (h.err & ERR_HIST_FULL)
+    if (err & ERR_HIST_FULL)
         return set_err(c, -ENOSPC, "sliding-window history full: carried logs + batch > %llu entries",
                        (unsigned long long)c->hist.cap);
-    if (h.err) return set_err(c, -EIO, "device error flags 0x%x", h.err);
+    if (err) return set_err(c, -EIO, "device error flags 0x%x", err);
     return 0;
 }
 
@@ -394,7 +511,40 @@ int fsx_sync(fsx_ctx *c) {
     int rc = sel(c);
     if (rc) return rc;
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    if ((rc = check_pipelined(c))) return rc;
     return check_batch(c);
+}
+
+int fsx_set_pipeline(fsx_ctx *c, int on) {
+    if (!c) return -EINVAL;
+    int rc = fsx_sync(c);
+    if (rc) return rc;
+    if (on && !c->fb[1].bs) {
+        fsx_ctx::FrontBufs &f = c->fb[1];
+        const uint64_t cap = c->sc.cap;
+        for (int b = 0; b < 2; ++b) {
+            HIPCHK(c, hipMalloc(&f.packed[b], cap * 8));
+            HIPCHK(c, hipMalloc(&f.pay[b], cap * 8));
+        }
+        HIPCHK(c, hipMalloc(&f.hist, 256ull * std::max<uint64_t>(kSortMaxBlocks, cap / kSortTile + 2) * 4));
+        HIPCHK(c, hipMalloc(&f.sort_ctl, kSortCtlWords * 4));
+        HIPCHK(c, hipMalloc(&f.gbase, 1024 * 4));
+        HIPCHK(c, hipMalloc(&f.heavy, sizeof(HeavySet)));
+        HIPCHK(c, hipMemset(f.heavy, 0, sizeof(HeavySet)));
+        HIPCHK(c, hipMalloc(&f.bs, sizeof(BatchState)));
+        HIPCHK(c, hipMemset(f.bs, 0, sizeof(BatchState)));
+        for (int p = 0; p < 2; ++p)
+            if (!c->tail_done[p]) HIPCHK(c, hipEventCreateWithFlags(&c->tail_done[p], hipEventDisableTiming));
+        if (!c->front_done) HIPCHK(c, hipEventCreateWithFlags(&c->front_done, hipEventDisableTiming));
+        if (!c->parse_done) HIPCHK(c, hipEventCreateWithFlags(&c->parse_done, hipEventDisableTiming));
+    }
+    if (!on && c->par == 1) {   // back to set 0, keeping the last batch's facts
+        HIPCHK(c, hipMemcpy(c->fb[0].bs, c->fb[1].bs, sizeof(BatchState), hipMemcpyDeviceToDevice));
+        use_front(c, 0);
+        c->par = 0;
+    }
+    c->pipe = on != 0;
+    return 0;
 }
 
 // Fold the recorded per-kernel event intervals of all pending batches into the
@@ -548,27 +698,69 @@ static int prefix_op(fsx_ctx *c, int op, int map_id, const void *key, const void
     return 0;
 }
 
+static FlowRequest flow_slots(fsx_ctx *c, const FlowRequest *fr, size_t n, int *rc);
+
+// A pipelined batch (fsx_set_pipeline): its front (parse, sort) on the context stream, its
+// tail on the walker stream (flows on the aux stream), so the next batch's front overlaps
+// this tail. The batch two back used this batch's front buffers: the host waits for its
+// tail (the device still has the previous batch to run) and checks it.
+static int run_pipelined(fsx_ctx *c, const PacketIn &in, const uint32_t *d_len, const uint64_t *d_ts, size_t n,
+                         uint8_t *d_verdict, const FlowRequest *fr) {
+    HIPCHK(c, hipSetDevice(c->device));
+    int rc;
+    if (c->pending && (rc = fsx_sync(c))) return rc;
+    const int q = c->par ^ 1;
+    if (c->fl_on[q]) {
+        HIPCHK(c, hipEventSynchronize(c->tail_done[q]));
+        BatchState h;
+        HIPCHK(c, hipMemcpy(&h, c->fb[q].bs, sizeof(h), hipMemcpyDeviceToHost));
+        if (h.err) return fsx_sync(c);   // rolls it back, and the batch after it
+        c->fl_on[q] = false;
+    }
+    FlowRequest frq;
+    if (fr) {
+        frq = flow_slots(c, fr, n, &rc);
+        if (rc) return rc;
+        fr = &frq;
+    }
+    use_front(c, q);
+    c->par = q;
+    if (++c->id_gen == 0x10000u) {
+        if (c->sc.id_tab) HIPCHK(c, hipMemsetAsync(c->sc.id_tab, 0, c->slots * 32, c->stream));
+        c->id_gen = 1;
+    }
+    const PipeSplit sp{c->walk_stream, c->front_done, c->fl_on[q ^ 1] ? c->fb[q ^ 1].bs : nullptr,
+                       pipe_on_parse, c, &c->tail_args};
+    hipError_t e = launch_verdict_pipeline(in, d_len, d_ts, (uint32_t)n, d_verdict, c->table, c->tstate, c->bs,
+                                           c->sc, c->id_gen, table_index(c), c->lim, c->rs, true, fr, c->hist,
+                                           c->stream, fork_flows() ? c->aux_stream : nullptr, c->fork_ev,
+                                           c->join_ev, nullptr, c->walk_fork_ev, c->walk_join_ev,
+                                           c->heavy_fork_ev, c->heavy_flow_ev, nullptr, &sp);
+    if (e != hipSuccess) return set_err(c, -EIO, "pipeline launch: %s", hipGetErrorString(e));
+    c->tail_pending = true;   // enqueued after the next batch's parse, or by the next sel()
+    c->tail_par = q;
+    c->fl_on[q] = true;
+    c->fl_born[q] = c->id_gen;
+    c->tail_join = true;
+    return 0;
+}
+
 // Enqueue one batch: verdicts + maps when d_verdict is set, per-source flows when fr is.
 static int run_batch(fsx_ctx *c, const PacketIn &in, const uint32_t *d_len, const uint64_t *d_ts,
                      size_t n, uint8_t *d_verdict, bool do_limit, const FlowRequest *fr) {
     if (n > c->cfg.max_batch) return set_err(c, -E2BIG, "n=%zu exceeds max_batch", n);
+    // pipelined: the fixed window on header records, no per-kernel timing, rules uploaded
+    const bool pipe = c->pipe && do_limit && n && !in.rec && c->cfg.limiter == FSX_LIMIT_FIXED_WINDOW &&
+                      !c->timing && !c->rules_dirty;
+    if (pipe) return run_pipelined(c, in, d_len, d_ts, n, d_verdict, fr);
     int rc = sel(c);
     if (rc) return rc;
-    if (c->pending) { rc = fsx_sync(c); if (rc) return rc; }
+    if (busy(c)) { rc = fsx_sync(c); if (rc) return rc; }
     if (do_limit && c->rules_dirty && (rc = upload_rules(c))) return rc;
     FlowRequest frq;
     if (fr) {
-        frq = *fr;
-        const uint64_t need = std::max<uint64_t>(1, std::min<uint64_t>(frq.cap, n));
-        if (need > c->flow_acc_cap) {
-            hipFree(c->d_flow_acc);
-            c->d_flow_acc = nullptr;
-            c->flow_acc_cap = 0;
-            HIPCHK(c, hipMalloc(&c->d_flow_acc, need * flow_acc_bytes()));
-            c->flow_acc_cap = need;
-        }
-        frq.acc = c->d_flow_acc;
-        frq.cap = (uint32_t)std::min<uint64_t>(frq.cap, c->flow_acc_cap);
+        frq = flow_slots(c, fr, n, &rc);
+        if (rc) return rc;
         fr = &frq;
     }
     PipeTiming tmv{};
@@ -598,6 +790,28 @@ static int run_batch(fsx_ctx *c, const PacketIn &in, const uint32_t *d_len, cons
     c->pending_born = do_limit && n ? c->id_gen : 0;
     if (e != hipSuccess) return set_err(c, -EIO, "pipeline launch: %s", hipGetErrorString(e));
     return 0;
+}
+
+// The per-source flow accumulators of a batch (context scratch, grown on demand; only the
+// flow stream uses them, in batch order).
+static FlowRequest flow_slots(fsx_ctx *c, const FlowRequest *fr, size_t n, int *rc) {
+    FlowRequest frq = *fr;
+    *rc = 0;
+    const uint64_t need = std::max<uint64_t>(1, std::min<uint64_t>(frq.cap, n));
+    if (need > c->flow_acc_cap) {
+        if (busy(c) && (*rc = fsx_sync(c))) return frq;   // the old accumulators may be in use
+        hipFree(c->d_flow_acc);
+        c->d_flow_acc = nullptr;
+        c->flow_acc_cap = 0;
+        if (hipMalloc(&c->d_flow_acc, need * flow_acc_bytes()) != hipSuccess) {
+            *rc = set_err(c, -ENOMEM, "flow accumulators");
+            return frq;
+        }
+        c->flow_acc_cap = need;
+    }
+    frq.acc = c->d_flow_acc;
+    frq.cap = (uint32_t)std::min<uint64_t>(frq.cap, c->flow_acc_cap);
+    return frq;
 }
 
 static FlowRequest flow_request(fsx_ctx *c, uint8_t *keys16, uint8_t *fam, float *feat, float *prob,
@@ -647,7 +861,7 @@ static int run_records(fsx_ctx *c, const void *d_records, size_t n, uint32_t rec
     int rc = sel(c);
     if (rc) return rc;
     if (n > c->rec_cap) {
-        if (c->pending && (rc = fsx_sync(c))) return rc;   // the old buffers may be in use
+        if (busy(c) && (rc = fsx_sync(c))) return rc;   // the old buffers may be in use
         hipFree(c->d_rec_len); hipFree(c->d_rec_ts);
         c->d_rec_len = nullptr; c->d_rec_ts = nullptr; c->rec_cap = 0;
         HIPCHK(c, hipMalloc(&c->d_rec_len, n * 4));
@@ -897,6 +1111,7 @@ int fsx_reset(fsx_ctx *c) {
     if (!c) return -EINVAL;
     int rc = sel(c);
     if (rc) return rc;
+    if ((c->fl_on[0] || c->fl_on[1]) && (rc = fsx_sync(c))) return rc;   // (pipelined batches)
     c->pending_born = 0;   // the whole table is wiped: no rollback of a pending batch
     HIPCHK(c, hipMemsetAsync(c->table, 0, c->slots * sizeof(Slot), c->stream));
     HIPCHK(c, hipMemsetAsync(c->tstate, 0, sizeof(TableState), c->stream));
@@ -1002,7 +1217,7 @@ int fsx_flows_begin(fsx_ctx *c) {
     int rc = sel(c);
     if (rc) return rc;
     if (!c->d_slot_acc) {
-        if (c->pending && (rc = fsx_sync(c))) return rc;
+        if (busy(c) && (rc = fsx_sync(c))) return rc;
         HIPCHK(c, hipMalloc(&c->d_slot_acc, c->slots * slot_acc_bytes()));
         HIPCHK(c, hipMemsetAsync(c->d_slot_acc, 0, c->slots * slot_acc_bytes(), c->stream));   // epoch 0
         HIPCHK(c, hipMalloc(&c->d_flow_rows, 8));

@@ -1262,8 +1262,10 @@ __device__ __forceinline__ uint32_t table_claim(Slot *table, const Limits &lim, 
 // After k_parse (one thread): the batch's new sources must fit max_entries, and with the
 // sliding window its carried logs plus packets the history buffer — checked before any
 // limiter state changes; a failing batch is rolled back by the host (fsx_api.hip).
-__global__ void k_batch_check(BatchState *bs, TableState *tstate, Limits lim) {
+// Pipelined batches: a batch whose predecessor failed is cancelled (the host rolls both back).
+__global__ void k_batch_check(BatchState *bs, TableState *tstate, Limits lim, const BatchState *prev) {
     if (bs->err) return;
+    if (prev && prev->err) { bs->err |= ERR_CANCELED; return; }
     if (tstate->count + bs->n_new > lim.max_entries) { bs->err |= ERR_TABLE_FULL; return; }
     if (lim.limiter == 1 && tstate->hist_total + bs->n_valid > lim.hist_cap) {
         bs->err |= ERR_HIST_FULL;
@@ -1271,7 +1273,8 @@ __global__ void k_batch_check(BatchState *bs, TableState *tstate, Limits lim) {
     }
     tstate->count += bs->n_new;
     if (bs->n_rule) {   // prefix-rule drops count in stats_map like blacklist drops
-        tstate->stats[1] += bs->n_rule;
+        // (atomic: a pipelined batch's tail may be adding its counters meanwhile)
+        atomicAdd(reinterpret_cast<unsigned long long *>(&tstate->stats[1]), (unsigned long long)bs->n_rule);
         bs->dropped += bs->n_rule;
     }
 }
@@ -2023,20 +2026,32 @@ static uint32_t next_generation() {
     return g;
 }
 
-hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, const uint64_t *ts,
-                                   uint32_t n, uint8_t *verdict, Slot *table, TableState *tstate,
-                                   BatchState *bs, const Scratch &sc_in, uint32_t id_gen,
-                                   const TableIndex &X, const Limits &lim, const RuleSet &rules,
-                                   bool do_limit, const FlowRequest *flows,
-                                   const HistBufs &hist, hipStream_t st, hipStream_t st2,
-                                   hipEvent_t fork_ev, hipEvent_t join_ev, hipStream_t st3,
-                                   hipEvent_t walk_fork_ev, hipEvent_t walk_join_ev, hipEvent_t heavy_fork_ev,
-                                   hipEvent_t heavy_flow_ev, PipeTiming *tm) {
-    (void)hipGetLastError();   // a stale error of another caller is not ours
-    Scratch sc = sc_in;        // packed[0] / pay[0] become the sorted output below
-    int last[3] = {-1, -1, -1};   // last event index per stream (timing)
-    // mark(name) closes the interval of the kernel just enqueued on stream s (0: st, 1: st2,
-    // 2: st3)
+// The tail of a batch (after its sort): heavy walker and flow sums, segment heads, flows,
+// the limiter's walkers, verdict fill and apply. Enqueued right after the front, or — for
+// pipelined batches — later, after the next batch's parse (fsx_api.hip run_pipelined).
+hipError_t launch_tail(const TailArgs &a) {
+    const PacketIn &in = a.in;
+    const uint32_t *len = a.len;
+    const uint64_t *ts = a.ts;
+    const uint32_t n = a.n;
+    uint8_t *verdict = a.verdict;
+    Slot *table = a.table;
+    TableState *tstate = a.tstate;
+    BatchState *bs = a.bs;
+    Scratch sc = a.sc;
+    const Limits &lim = a.lim;
+    const bool do_limit = a.do_limit;
+    const FlowRequest *flows = a.has_flows ? &a.fq : nullptr;
+    const HistBufs &hist = a.hist;
+    hipStream_t st = a.st, st2 = a.st2, st3 = a.st3;
+    hipEvent_t fork_ev = a.fork_ev, join_ev = a.join_ev, walk_fork_ev = a.walk_fork_ev,
+               walk_join_ev = a.walk_join_ev, heavy_fork_ev = a.heavy_fork_ev, heavy_flow_ev = a.heavy_flow_ev;
+    PipeTiming *tm = a.tm;
+    const PipeSplit *split = a.split ? &a.sp : nullptr;
+    const int npass = a.npass;
+    const bool tagh = a.tagh;
+    const uint32_t gridTiles = a.gridTiles;
+    int last[3] = {a.last[0], a.last[1], a.last[2]};
     auto mark_on = [&](const char *name, int s_id) {
         if (!tm || tm->used >= tm->cap) return;
         const int i = tm->used++;
@@ -2047,92 +2062,14 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
     };
     auto mark = [&](const char *name) { mark_on(name, 0); };
     const Marker mk{[](void *p, const char *name) { (*static_cast<decltype(mark) *>(p))(name); }, &mark};
-    if (tm) tm->used = 0;
     hipError_t e;
-    if ((e = hipMemsetAsync(bs, 0, sizeof(BatchState), st)) != hipSuccess) return e;
-    if (n == 0) return hipSuccess;
-    if ((e = hipMemsetAsync(sc.marks, 0, n, st)) != hipSuccess) return e;
-    const uint32_t gridStream = std::min<uint32_t>(2048, std::max<uint32_t>(1, cdiv(n, 256)));
-    const uint32_t gridTiles = std::min<uint32_t>(4096, std::max<uint32_t>(1, cdiv(n, kTile)));
-
-    // mark(name) closes the interval of the kernel just enqueued (per-kernel timing)
-    const bool onesweep = (lim.test_flags & 2u) != 0;
-    // with the limiter, sources are found / inserted in the persistent index (sort id =
-    // table slot); flow features alone use a per-batch id table and touch no map state
-    static const uint32_t coherent = getenv("FSX_ID_COHERENT") ? 1u : 0u;
-    const IdTable idt = do_limit
-        ? IdTable{X.heads, X.k6, lim.table_mask, lim.seed, X.epoch, lim.test_flags, table, id_gen, coherent}
-        : IdTable{reinterpret_cast<unsigned long long *>(sc.id_tab), sc.id_tab + 2 * (lim.table_mask + 1),
-                  lim.table_mask, lim.seed, id_gen, lim.test_flags, nullptr, 0, coherent};
-    if ((e = hipMemsetAsync(sc.sort_ctl, 0, kSortCtlWords * 4, st)) != hipSuccess) return e;
-    mark("start");
-    const uint32_t ntiles = std::max<uint32_t>(1, cdiv(n, kSortTile));
-    const uint32_t tcap = (uint32_t)(sc.cap / kSortTile + 2);
-    // source ids have log2(slots) bits: ceil(bits / 8) LSD passes of equal digits of at
-    // most 8 bits (21 bits: 3 x 7 — fewer buckets, longer runs per tile than 8 + 8 + 5)
-    uint32_t idbits = 0;
-    while ((1ull << idbits) <= lim.table_mask) ++idbits;
-    const int npass = std::max(1, (int)((idbits + 7) / 8));
-    static const bool full_digits = getenv("FSX_SORT_FULL_DIGITS") != nullptr;   // A/B: 8,8,..,rest
-    static const bool no_heavy = getenv("FSX_NO_HEAVY_SORT") != nullptr;          // A/B: plain LSD
-    const uint32_t dbits = full_digits ? 8u : std::max<uint32_t>(1, (idbits + npass - 1) / npass);
-    const uint32_t dmask = (1u << dbits) - 1u;
-    // Heavy-source sort (3-pass tables of <= 2^23 slots): pass 0 buckets the light
-    // entries by a 7-bit id digit and every heavy source into a bucket of its own; passes
-    // 1-2 sort the light entries only, by the remaining id bits in two equal digits.
-    const bool heavy_sort = !onesweep && !full_digits && !no_heavy && npass == 3 && idbits <= 23;
-    DigitPlan dp{};
-    dp.npass = (uint32_t)npass;
-    if (heavy_sort) {
-        const uint32_t rest = idbits - 7, w1 = (rest + 1) / 2;
-        dp.light_b = 128;
-        dp.shift[0] = 56; dp.mask[0] = 255;
-        dp.shift[1] = 39; dp.mask[1] = (1u << w1) - 1u;
-        dp.shift[2] = 39 + w1; dp.mask[2] = (1u << (rest - w1)) - 1u;
-        k_heavy_sample<<<64, 256, 0, st>>>(in, len, n, sc.sketch, lim.seed, lim.table_mask, lim.test_flags);
-        // heavy slots resolved once (not under prefix rules; FSX_NO_HEAVY_SLOTS=1: A/B)
-        static const bool no_hslots = getenv("FSX_NO_HEAVY_SLOTS") != nullptr;
-        const uint32_t resolve = !no_hslots && !(do_limit && rules.slot) ? 1u : 0u;
-        k_heavy_pick<<<1, 1024, 0, st>>>(in, len, sc.sketch, sc.heavy, kHeavyMax, 16, lim.seed,
-                                         lim.table_mask, lim.test_flags, idt, resolve, bs);
-        mark("k_heavy_pick");
-    } else {
-        for (int p = 0; p < 4; ++p) { dp.shift[p] = 32u + dbits * (uint32_t)p; dp.mask[p] = dmask; }
-    }
-    // heavy verdict lists (fixed window with the heavy-source sort; FSX_NO_HEAVY_LISTS=1: A/B)
-    static const bool no_hlists = getenv("FSX_NO_HEAVY_LISTS") != nullptr;
-    const bool tagh = heavy_sort && do_limit && lim.limiter == 0 && verdict && !no_hlists;
-    {
-        const uint32_t g = std::min<uint32_t>(256u * FSX_PARSE_MINB, ntiles);   // one resident block per slot
-        const HeavySet *hs = heavy_sort ? sc.heavy : nullptr;
-        uint32_t *th = onesweep ? nullptr : sc.hist;
-        // the prefix rules apply to limiter batches (an instantiation of its own, so the
-        // rule-free parse keeps its registers)
-        const bool rl = do_limit && rules.slot;
-#define FSX_PARSE(R, Q) k_parse<R, Q><<<g, 256, 0, st>>>(in, len, ts, n, sc.packed[0], verdict, bs, idt, \
-                                                        sc.sort_ctl, th, tcap, dp, hs, rules, tagh ? 1u : 0u)
-        if (!in.rec)
-            rl ? FSX_PARSE(0, true) : FSX_PARSE(0, false);
-        else if (in.rec_bytes == 16)
-            rl ? FSX_PARSE(16, true) : FSX_PARSE(16, false);
-        else
-            rl ? FSX_PARSE(32, true) : FSX_PARSE(32, false);
-#undef FSX_PARSE
-    }
-    mark("k_parse");
-    // Heavy verdict lists: every heavy source is one run of pass 0's output (the later passes
-    // write [0, n_light) only) whose segment needs no head search, so its walker and its flow
-    // sums run on the third stream beside the heads, the classes and the light walkers, which
-    // like the light flow tiles cover [0, n_light) only (k_heads_heavy appends the heavy
-    // segments).
     hipStream_t hs = (st3 && heavy_fork_ev && heavy_flow_ev) ? st3 : st;
-    const int hs_id = hs == st ? 0 : 2;
+    int hs_id = hs == st ? 0 : 2;
     // the heavy flow sums: on the flow stream ahead of the light flow tiles (a fourth stream
     // would share a hardware queue with the limiter chain: GPU_MAX_HW_QUEUES is 4)
-    static const bool no_fork = getenv("FSX_NO_FLOW_FORK") != nullptr;   // A/B: flows serialized
-    const bool fork = flows && do_limit && st2 && fork_ev && join_ev && !no_fork;   // flows beside the limiter
+    const bool fork = a.fork;   // flows beside the limiter
     hipStream_t hf = (hs != st && fork) ? st2 : hs;
-    const int hf_id = hf == st2 && hf != st ? 1 : hs_id;
+    int hf_id = hf == st2 && hf != st ? 1 : hs_id;
     uint64_t *S_fin = sc.packed[npass & 1], *pay_fin = sc.pay[npass & 1];
     // heavy verdict lists live in the sort's other buffer, over the heavy positions (which the
     // passes >= 1 never write)
@@ -2164,36 +2101,16 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
         }
         return hipSuccess;
     };
-    k_hist_prep<<<1, 256, 0, st>>>(sc.sort_ctl, sc.gbase, bs, heavy_sort ? dp.light_b : 256u);
-    if (do_limit) k_batch_check<<<1, 1, 0, st>>>(bs, tstate, lim);
-    const uint32_t gen0 = onesweep ? next_generation() : 0u;
-    for (int pass = 0; pass < npass; ++pass) {
-        const uint64_t *in = sc.packed[pass & 1];
-        uint64_t *out = sc.packed[(pass + 1) & 1];
-        const uint64_t *pin = pass == 0 ? nullptr : sc.pay[pass & 1];
-        uint64_t *pout = sc.pay[(pass + 1) & 1];
-        const uint32_t shift = dp.shift[pass], pmask = dp.mask[pass];
-        if (onesweep) {
-            const uint32_t *Ld = pass == 0 ? nullptr : &bs->n_valid;
-            k_onesweep<kLookW><<<ntiles, 256, 0, st>>>(in, out, n, Ld, shift, pmask, sc.gbase + 256 * pass,
-                                                       sc.status, sc.sort_ctl + 1024 + pass,
-                                                       gen0 + (uint32_t)pass, pass == 0, bs, pin, pout,
-                                                       ts, len);
-            mark("k_onesweep");
-        } else {
-            // passes >= 1 cover [0, n_light): the heavy entries (pass 0's top buckets) are
-            // final in pass 0's output, which is also the last pass's (npass odd)
-            const uint32_t *Ld = pass == 0 ? nullptr : &bs->n_light;
-            if (pass > 0) {   // pass 0's per-tile counts come from k_parse
-                k_tile_hist<<<ntiles, 256, 0, st>>>(in, n, Ld, shift, pmask, pass == 0, sc.hist, tcap);
-                mark("k_tile_hist");
-            }
-            k_tile_scan<<<pmask + 1, 256, 0, st>>>(sc.hist, tcap, n, Ld, sc.gbase + 256 * pass);
-            mark("k_tile_scan");
-            k_tile_scatter<kLatePayDefault><<<ntiles, 256, 0, st>>>(in, out, n, Ld, shift, pmask, pass == 0, sc.hist, tcap, bs,
-                                                   pin, pout, ts, len);
-            mark("k_tile_scatter");
-        }
+    if (split) {
+        // pipelined: the tail on its own stream (the caller made it and st2 wait for the
+        // front); walkers serial on it, the heavy flow sums and the flows on st2
+        st = split->tail;
+        if ((e = hipMemsetAsync(sc.marks, 0, n, st)) != hipSuccess) return e;
+        st3 = nullptr;
+        hs = st;
+        hs_id = 0;
+        hf = fork ? st2 : st;
+        hf_id = fork ? 1 : 0;
     }
     if (tagh && (e = launch_heavy()) != hipSuccess) return e;
     if (npass & 1) {
@@ -2284,6 +2201,168 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
     return hipGetLastError();
 }
 
+hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, const uint64_t *ts,
+                                   uint32_t n, uint8_t *verdict, Slot *table, TableState *tstate,
+                                   BatchState *bs, const Scratch &sc_in, uint32_t id_gen,
+                                   const TableIndex &X, const Limits &lim, const RuleSet &rules,
+                                   bool do_limit, const FlowRequest *flows,
+                                   const HistBufs &hist, hipStream_t st, hipStream_t st2,
+                                   hipEvent_t fork_ev, hipEvent_t join_ev, hipStream_t st3,
+                                   hipEvent_t walk_fork_ev, hipEvent_t walk_join_ev, hipEvent_t heavy_fork_ev,
+                                   hipEvent_t heavy_flow_ev, PipeTiming *tm, const PipeSplit *split) {
+    (void)hipGetLastError();   // a stale error of another caller is not ours
+    Scratch sc = sc_in;        // packed[0] / pay[0] become the sorted output below
+    int last[3] = {-1, -1, -1};   // last event index per stream (timing)
+    // mark(name) closes the interval of the kernel just enqueued on stream s (0: st, 1: st2,
+    // 2: st3)
+    auto mark_on = [&](const char *name, int s_id) {
+        if (!tm || tm->used >= tm->cap) return;
+        const int i = tm->used++;
+        tm->names[i] = name;
+        tm->prev[i] = last[s_id];
+        (void)hipEventRecord(tm->ev[i], s_id == 2 ? st3 : s_id == 1 ? st2 : st);
+        last[s_id] = i;
+    };
+    auto mark = [&](const char *name) { mark_on(name, 0); };
+    const Marker mk{[](void *p, const char *name) { (*static_cast<decltype(mark) *>(p))(name); }, &mark};
+    if (tm) tm->used = 0;
+    hipError_t e;
+    if ((e = hipMemsetAsync(bs, 0, sizeof(BatchState), st)) != hipSuccess) return e;
+    if (n == 0) return hipSuccess;
+    if (!split && (e = hipMemsetAsync(sc.marks, 0, n, st)) != hipSuccess) return e;
+    const uint32_t gridStream = std::min<uint32_t>(2048, std::max<uint32_t>(1, cdiv(n, 256)));
+    const uint32_t gridTiles = std::min<uint32_t>(4096, std::max<uint32_t>(1, cdiv(n, kTile)));
+
+    // mark(name) closes the interval of the kernel just enqueued (per-kernel timing)
+    const bool onesweep = (lim.test_flags & 2u) != 0;
+    // with the limiter, sources are found / inserted in the persistent index (sort id =
+    // table slot); flow features alone use a per-batch id table and touch no map state
+    static const uint32_t coherent = getenv("FSX_ID_COHERENT") ? 1u : 0u;
+    const IdTable idt = do_limit
+        ? IdTable{X.heads, X.k6, lim.table_mask, lim.seed, X.epoch, lim.test_flags, table, id_gen, coherent}
+        : IdTable{reinterpret_cast<unsigned long long *>(sc.id_tab), sc.id_tab + 2 * (lim.table_mask + 1),
+                  lim.table_mask, lim.seed, id_gen, lim.test_flags, nullptr, 0, coherent};
+    if ((e = hipMemsetAsync(sc.sort_ctl, 0, kSortCtlWords * 4, st)) != hipSuccess) return e;
+    mark("start");
+    const uint32_t ntiles = std::max<uint32_t>(1, cdiv(n, kSortTile));
+    const uint32_t tcap = (uint32_t)(sc.cap / kSortTile + 2);
+    // source ids have log2(slots) bits: ceil(bits / 8) LSD passes of equal digits of at
+    // most 8 bits (21 bits: 3 x 7 — fewer buckets, longer runs per tile than 8 + 8 + 5)
+    uint32_t idbits = 0;
+    while ((1ull << idbits) <= lim.table_mask) ++idbits;
+    const int npass = std::max(1, (int)((idbits + 7) / 8));
+    static const bool full_digits = getenv("FSX_SORT_FULL_DIGITS") != nullptr;   // A/B: 8,8,..,rest
+    static const bool no_heavy = getenv("FSX_NO_HEAVY_SORT") != nullptr;          // A/B: plain LSD
+    const uint32_t dbits = full_digits ? 8u : std::max<uint32_t>(1, (idbits + npass - 1) / npass);
+    const uint32_t dmask = (1u << dbits) - 1u;
+    // Heavy-source sort (3-pass tables of <= 2^23 slots): pass 0 buckets the light
+    // entries by a 7-bit id digit and every heavy source into a bucket of its own; passes
+    // 1-2 sort the light entries only, by the remaining id bits in two equal digits.
+    const bool heavy_sort = !onesweep && !full_digits && !no_heavy && npass == 3 && idbits <= 23;
+    DigitPlan dp{};
+    dp.npass = (uint32_t)npass;
+    if (heavy_sort) {
+        const uint32_t rest = idbits - 7, w1 = (rest + 1) / 2;
+        dp.light_b = 128;
+        dp.shift[0] = 56; dp.mask[0] = 255;
+        dp.shift[1] = 39; dp.mask[1] = (1u << w1) - 1u;
+        dp.shift[2] = 39 + w1; dp.mask[2] = (1u << (rest - w1)) - 1u;
+        k_heavy_sample<<<64, 256, 0, st>>>(in, len, n, sc.sketch, lim.seed, lim.table_mask, lim.test_flags);
+        // heavy slots resolved once (not under prefix rules; FSX_NO_HEAVY_SLOTS=1: A/B)
+        static const bool no_hslots = getenv("FSX_NO_HEAVY_SLOTS") != nullptr;
+        const uint32_t resolve = !no_hslots && !(do_limit && rules.slot) ? 1u : 0u;
+        k_heavy_pick<<<1, 1024, 0, st>>>(in, len, sc.sketch, sc.heavy, kHeavyMax, 16, lim.seed,
+                                         lim.table_mask, lim.test_flags, idt, resolve, bs);
+        mark("k_heavy_pick");
+    } else {
+        for (int p = 0; p < 4; ++p) { dp.shift[p] = 32u + dbits * (uint32_t)p; dp.mask[p] = dmask; }
+    }
+    // heavy verdict lists (fixed window with the heavy-source sort; FSX_NO_HEAVY_LISTS=1: A/B)
+    static const bool no_hlists = getenv("FSX_NO_HEAVY_LISTS") != nullptr;
+    const bool tagh = heavy_sort && do_limit && lim.limiter == 0 && verdict && !no_hlists;
+    {
+        const uint32_t g = std::min<uint32_t>(256u * FSX_PARSE_MINB, ntiles);   // one resident block per slot
+        const HeavySet *hs = heavy_sort ? sc.heavy : nullptr;
+        uint32_t *th = onesweep ? nullptr : sc.hist;
+        // the prefix rules apply to limiter batches (an instantiation of its own, so the
+        // rule-free parse keeps its registers)
+        const bool rl = do_limit && rules.slot;
+#define FSX_PARSE(R, Q) k_parse<R, Q><<<g, 256, 0, st>>>(in, len, ts, n, sc.packed[0], verdict, bs, idt, \
+                                                        sc.sort_ctl, th, tcap, dp, hs, rules, tagh ? 1u : 0u)
+        if (!in.rec)
+            rl ? FSX_PARSE(0, true) : FSX_PARSE(0, false);
+        else if (in.rec_bytes == 16)
+            rl ? FSX_PARSE(16, true) : FSX_PARSE(16, false);
+        else
+            rl ? FSX_PARSE(32, true) : FSX_PARSE(32, false);
+#undef FSX_PARSE
+    }
+    mark("k_parse");
+    // Heavy verdict lists: every heavy source is one run of pass 0's output (the later passes
+    // write [0, n_light) only) whose segment needs no head search, so its walker and its flow
+    // sums run on the third stream beside the heads, the classes and the light walkers, which
+    // like the light flow tiles cover [0, n_light) only (k_heads_heavy appends the heavy
+    // segments).
+    static const bool no_fork = getenv("FSX_NO_FLOW_FORK") != nullptr;   // A/B: flows serialized
+    // pipelined: the previous batch's tail goes in right after this parse (it overlaps the sort;
+    // A/B: FSX_TAIL_AFTER_PASS0=1 after the first sort pass)
+    static const bool tail_p0 = getenv("FSX_TAIL_AFTER_PASS0") != nullptr;
+    if (split && split->on_parse && !tail_p0 && (e = split->on_parse(split->cb)) != hipSuccess) return e;
+    k_hist_prep<<<1, 256, 0, st>>>(sc.sort_ctl, sc.gbase, bs, heavy_sort ? dp.light_b : 256u);
+    if (do_limit) k_batch_check<<<1, 1, 0, st>>>(bs, tstate, lim, split ? split->prev : nullptr);
+    const uint32_t gen0 = onesweep ? next_generation() : 0u;
+    for (int pass = 0; pass < npass; ++pass) {
+        const uint64_t *in = sc.packed[pass & 1];
+        uint64_t *out = sc.packed[(pass + 1) & 1];
+        const uint64_t *pin = pass == 0 ? nullptr : sc.pay[pass & 1];
+        uint64_t *pout = sc.pay[(pass + 1) & 1];
+        const uint32_t shift = dp.shift[pass], pmask = dp.mask[pass];
+        if (onesweep) {
+            const uint32_t *Ld = pass == 0 ? nullptr : &bs->n_valid;
+            k_onesweep<kLookW><<<ntiles, 256, 0, st>>>(in, out, n, Ld, shift, pmask, sc.gbase + 256 * pass,
+                                                       sc.status, sc.sort_ctl + 1024 + pass,
+                                                       gen0 + (uint32_t)pass, pass == 0, bs, pin, pout,
+                                                       ts, len);
+            mark("k_onesweep");
+        } else {
+            // passes >= 1 cover [0, n_light): the heavy entries (pass 0's top buckets) are
+            // final in pass 0's output, which is also the last pass's (npass odd)
+            const uint32_t *Ld = pass == 0 ? nullptr : &bs->n_light;
+            if (pass > 0) {   // pass 0's per-tile counts come from k_parse
+                k_tile_hist<<<ntiles, 256, 0, st>>>(in, n, Ld, shift, pmask, pass == 0, sc.hist, tcap);
+                mark("k_tile_hist");
+            }
+            k_tile_scan<<<pmask + 1, 256, 0, st>>>(sc.hist, tcap, n, Ld, sc.gbase + 256 * pass);
+            mark("k_tile_scan");
+            k_tile_scatter<kLatePayDefault><<<ntiles, 256, 0, st>>>(in, out, n, Ld, shift, pmask, pass == 0, sc.hist, tcap, bs,
+                                                   pin, pout, ts, len);
+            mark("k_tile_scatter");
+            if (pass == 0 && tail_p0 && split && split->on_parse && (e = split->on_parse(split->cb)) != hipSuccess)
+                return e;
+        }
+    }
+    if (split) {   // pipelined: the front is done; the tail is handed back (run later)
+        if ((e = hipEventRecord(split->front_done, st)) != hipSuccess) return e;
+    }
+    TailArgs ta{};
+    ta.in = in; ta.len = len; ta.ts = ts; ta.n = n; ta.verdict = verdict; ta.table = table; ta.tstate = tstate;
+    ta.bs = bs; ta.sc = sc; ta.lim = lim; ta.do_limit = do_limit;
+    ta.has_flows = flows != nullptr;
+    if (flows) ta.fq = *flows;
+    ta.hist = hist; ta.st = st; ta.st2 = st2; ta.st3 = st3; ta.fork_ev = fork_ev; ta.join_ev = join_ev;
+    ta.walk_fork_ev = walk_fork_ev; ta.walk_join_ev = walk_join_ev; ta.heavy_fork_ev = heavy_fork_ev;
+    ta.heavy_flow_ev = heavy_flow_ev; ta.tm = tm; ta.split = split != nullptr;
+    if (split) ta.sp = *split;
+    ta.npass = npass; ta.tagh = tagh; ta.gridTiles = gridTiles;
+    ta.fork = flows && do_limit && st2 && fork_ev && join_ev && !no_fork;
+    for (int k = 0; k < 3; ++k) ta.last[k] = last[k];
+    if (split && split->tail_out) {
+        *split->tail_out = ta;
+        return hipGetLastError();
+    }
+    return launch_tail(ta);
+}
+
 // ------------------------------------------------------------------ map syscalls
 // op: 0 lookup, 1 update, 2 delete. Result: 0 / -ENOENT(-2) / -EEXIST(-17) / -ENOSPC(-28).
 // Map id -> table tag (1 IPv4, 2 IPv6) and slot flag bit (include/fsx_hip.h map ids).
@@ -2370,7 +2449,7 @@ hipError_t launch_map_import(Slot *table, TableState *tstate, BatchState *bs, co
     if (e != hipSuccess || n == 0) return e;
     const uint32_t grid = std::min<uint32_t>(4096, (n + 255) / 256);
     k_map_import<<<grid, 256, 0, st>>>(table, lim, X, born, map_id, d_keys, d_vals, n, bs);
-    k_batch_check<<<1, 1, 0, st>>>(bs, tstate, lim);
+    k_batch_check<<<1, 1, 0, st>>>(bs, tstate, lim, nullptr);
     return hipGetLastError();
 }
 

@@ -35,6 +35,7 @@ enum : uint32_t {
     ERR_FIXUP = 4u,
     ERR_SORT_HANG = 8u,
     ERR_HIST_FULL = 16u,
+    ERR_CANCELED = 32u,   // pipelined batches: the batch before this one failed
 };
 
 enum : uint32_t { SLOT_HAS_ST = 1u, SLOT_HAS_BL = 2u, SLOT_HAS_TB = 4u };
@@ -343,6 +344,49 @@ struct PacketIn {
     uint64_t *rec_ts;
 };
 
+// Batch pipelining (fsx_set_pipeline, DESIGN.md §3 "Pipelined batches"): the front of a
+// batch (heavy pick, parse, sort) stays on st; the rest (heads, walkers, fill, verdicts;
+// flows on st2) runs on tail, after `front_done`, so the next batch's front overlaps this
+// batch's tail. Its front buffers (Scratch sort arrays, BatchState) alternate between two
+// sets; prev (the batch before, or null) cancels this one when it failed.
+struct TailArgs;
+struct PipeSplit {
+    hipStream_t tail;
+    hipEvent_t front_done;     // recorded on st after the sort
+    const BatchState *prev;
+    // called right after this batch's parse (enqueues the previous batch's deferred tail, so
+    // it overlaps this batch's sort rather than its parse)
+    hipError_t (*on_parse)(void *cb);
+    void *cb;
+    TailArgs *tail_out;        // this batch's tail is returned here, not enqueued
+};
+
+// Everything the tail of a batch needs (launch_tail): by value, so a pipelined batch's tail can
+// be enqueued after the call that built it has returned.
+struct TailArgs {
+    PacketIn in;
+    const uint32_t *len;
+    const uint64_t *ts;
+    uint32_t n;
+    uint8_t *verdict;
+    Slot *table;
+    TableState *tstate;
+    BatchState *bs;
+    Scratch sc;
+    Limits lim;
+    bool do_limit, has_flows, split, tagh, fork;
+    FlowRequest fq;
+    HistBufs hist;
+    hipStream_t st, st2, st3;
+    hipEvent_t fork_ev, join_ev, walk_fork_ev, walk_join_ev, heavy_fork_ev, heavy_flow_ev;
+    PipeTiming *tm;
+    PipeSplit sp;
+    int npass;
+    uint32_t gridTiles;
+    int last[3];
+};
+hipError_t launch_tail(const TailArgs &a);
+
 // st: the batch stream. st2 (optional, with fork/join events): the flow features run
 // on it concurrently with the rate limiter (they share only read-only inputs). st3
 // (optional): the fixed-window wave walker beside the thread walker.
@@ -354,7 +398,8 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
                                    hipStream_t st, hipStream_t st2, hipEvent_t fork_ev,
                                    hipEvent_t join_ev, hipStream_t st3, hipEvent_t walk_fork_ev,
                                    hipEvent_t walk_join_ev, hipEvent_t heavy_fork_ev,
-                                   hipEvent_t heavy_flow_ev, PipeTiming *tm);
+                                   hipEvent_t heavy_flow_ev, PipeTiming *tm,
+                                   const PipeSplit *split = nullptr);
 
 // Build-defined limiters (fsx_limiters.hip), after the table lookup/insert of a batch:
 // one verdict mark per sorted position, final per-source state in the table.

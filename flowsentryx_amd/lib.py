@@ -118,6 +118,7 @@ def load_library() -> C.CDLL:
         "fsx_last_error": (C.c_char_p, [vp]),
         "fsx_set_stream": (C.c_int, [vp, vp]),
         "fsx_sync": (C.c_int, [vp]),
+        "fsx_set_pipeline": (C.c_int, [vp, C.c_int]),
         "fsx_verdict_batch": (C.c_int, [vp, u8p, u8p, u8p, sz, u8p]),
         "fsx_verdict_batch_device": (C.c_int, [vp, vp, vp, vp, sz, vp]),
         "fsx_process_batch_device": (C.c_int, [vp, vp, vp, vp, sz, vp, vp, vp, vp, vp, vp, sz]),
@@ -160,7 +161,7 @@ def load_library() -> C.CDLL:
 # Every symbol include/fsx_hip.h declares (checked by tests/test_abi.py).
 ABI_SYMBOLS = [
     "fsx_abi_version", "fsx_config_default", "fsx_open", "fsx_close", "fsx_last_error",
-    "fsx_set_stream", "fsx_sync", "fsx_verdict_batch", "fsx_verdict_batch_device",
+    "fsx_set_stream", "fsx_sync", "fsx_set_pipeline", "fsx_verdict_batch", "fsx_verdict_batch_device",
     "fsx_process_batch_device", "fsx_verdict_records_device", "fsx_process_records_device",
     "fsx_map_lookup", "fsx_map_update", "fsx_map_update_batch", "fsx_map_delete", "fsx_map_dump",
     "fsx_get_stats",
@@ -276,6 +277,11 @@ class FsxContext:
 
     def sync(self):
         self._check(self._lib.fsx_sync(self._h), "fsx_sync")
+
+    def set_pipeline(self, on: bool = True):
+        """Batch pipelining (include/fsx_hip.h fsx_set_pipeline): the next batch's parse and
+        sort overlap this batch's walkers and verdicts; read outputs after sync()."""
+        self._check(self._lib.fsx_set_pipeline(self._h, 1 if on else 0), "fsx_set_pipeline")
 
     def set_stream(self, stream_handle: int | None):
         self._check(self._lib.fsx_set_stream(self._h, stream_handle or None), "fsx_set_stream")

@@ -171,6 +171,19 @@ const char *fsx_last_error(const fsx_ctx *ctx);
 int fsx_set_stream(fsx_ctx *ctx, void *hip_stream);
 /* Wait for enqueued device work and report deferred device-side errors. */
 int fsx_sync(fsx_ctx *ctx);
+/* Batch pipelining (default off; DESIGN.md §3 "Pipelined batches"). When on, a fixed-window
+ * fsx_verdict_batch_device / fsx_process_batch_device call enqueues the batch's front
+ * (parse, sort) on the context stream and its tail (walkers, verdicts, flows) on the
+ * context's own side streams, so the next batch's front overlaps this batch's tail; results
+ * and map state are exactly those of the same calls without pipelining. Up to two batches
+ * are in flight: a call first waits (on the host) for the batch two calls back. The caller
+ * keeps a batch's input and output buffers untouched until that batch completes: read the
+ * outputs after fsx_sync (or any other entry point, which orders the context stream after
+ * the last tail). A failed batch cancels the batch after it; the error (e.g. -ENOSPC) is
+ * returned by fsx_sync or by the call that found it, which enqueues nothing, and neither
+ * failed batch changes any map. Other limiters, record mode and timed batches run
+ * unpipelined. */
+int fsx_set_pipeline(fsx_ctx *ctx, int on);
 
 /* Replaces fsx() (src/fsx_kern.c:96-347) over a batch of n packets in arrival
  * order. Host pointers; hdr is n*64 bytes; verdict receives n bytes (1/2).

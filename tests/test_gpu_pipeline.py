@@ -1,0 +1,204 @@
+"""Pipelined batches (include/fsx_hip.h fsx_set_pipeline, DESIGN.md §3 "Pipelined batches").
+
+The front of batch k + 1 (heavy pick, parse, sort) runs while the tail of batch k (walkers,
+verdicts, flows) is still on the device, with alternating front buffers. Checked bit-exactly
+against the oracle fed the same batches in order: every batch's verdicts (each batch keeps
+its own output buffer; nothing is read before fsx_sync), its flow rows, stats_map and every
+map entry at the end; map syscalls between pipelined batches; a failed batch cancelling
+the one after it.
+"""
+import errno
+import json
+
+import numpy as np
+import pytest
+
+from kat import GOLDEN
+from test_gpu_parity import MAPS, assert_same_state, rand_stream
+
+pytestmark = pytest.mark.gpu
+
+
+def _dev(torch, a):
+    return torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).reshape(-1)).cuda()
+
+
+def _flows_of(d, m):
+    k = d["k"].cpu().numpy().reshape(-1, 16)[:m]
+    f = d["f"].cpu().numpy()[:m]
+    x = d["x"].cpu().numpy().reshape(-1, 8)[:m]
+    p = d["p"].cpu().numpy()[:m]
+    o = sorted(range(m), key=lambda i: (int(f[i]), k[i].tobytes()))
+    return k[o], f[o], x[o], p[o]
+
+
+def _run(native, oracle, batches, flows=True, between=None, max_entries=1 << 20):
+    """All batches launched back to back on a pipelined context (one sync at the end),
+    then each batch's verdicts / flow rows and the final maps against the oracle."""
+    import torch
+    from flowsentryx_amd import fsx_load
+    ref = json.loads((GOLDEN / "model_weights.json").read_text())
+    o = oracle.Oracle(max_entries=max_entries)
+    cap = max(len(b[1]) for b in batches)
+    bufs = []
+    with native.FsxContext(max_batch=cap, max_entries=max_entries) as c:
+        c.load_q8_model(fsx_load.model_from_dict(ref))
+        c.set_pipeline(True)
+        for j, (hdr, ln, ts) in enumerate(batches):
+            n = len(ln)
+            d = dict(h=_dev(torch, hdr), l=_dev(torch, ln), t=_dev(torch, ts),
+                     v=torch.empty(n, dtype=torch.uint8, device="cuda"))
+            if flows:
+                d.update(k=torch.empty(n * 16, dtype=torch.uint8, device="cuda"),
+                         f=torch.empty(n, dtype=torch.uint8, device="cuda"),
+                         x=torch.empty(n * 8, dtype=torch.float32, device="cuda"),
+                         p=torch.empty(n, dtype=torch.float32, device="cuda"),
+                         d=torch.empty(n, dtype=torch.uint8, device="cuda"))
+                c.process_batch_device(d["h"].data_ptr(), d["l"].data_ptr(), d["t"].data_ptr(), n,
+                                       d["v"].data_ptr(), d["k"].data_ptr(), d["f"].data_ptr(),
+                                       d["x"].data_ptr(), d["p"].data_ptr(), d["d"].data_ptr(), n)
+            else:
+                c.verdict_batch_device(d["h"].data_ptr(), d["l"].data_ptr(), d["t"].data_ptr(), n,
+                                       d["v"].data_ptr())
+            bufs.append(d)
+            d["vo"] = o.batch(hdr, ln, ts)
+            if between:
+                between(j, c, o)
+            if flows:
+                d["fo"] = oracle.flow_features(hdr, ln, ts)
+        c.sync()
+        for j, d in enumerate(bufs):
+            vg = d["v"].cpu().numpy()
+            bad = np.nonzero(vg != d["vo"])[0]
+            assert bad.size == 0, f"batch {j}: {bad.size} verdicts differ, first at {bad[:8]}"
+        if flows:
+            # rows of the last batch (every batch writes its own buffers; rows counted by
+            # the last batch's facts), and of every batch by their own count
+            for j, d in enumerate(bufs):
+                ko, fo, xo = d["fo"]
+                m = len(fo)
+                kg, fg, xg, pg = _flows_of(d, m)
+                oo = sorted(range(m), key=lambda i: (int(fo[i]), ko[i].tobytes()))
+                assert np.array_equal(kg, ko[oo]), j
+                assert np.array_equal(xg.view(np.uint32), xo[oo].view(np.uint32)), j
+                po, _, _ = oracle.score(ref, xo[oo])
+                assert np.array_equal(pg.view(np.uint32), po.view(np.uint32)), j
+            assert c.last_batch_info()["sources"] == len(bufs[-1]["fo"][1])
+        assert_same_state(c, o)
+
+
+def _config2_batches(oracle, n, cuts):
+    from flowsentryx_amd import synth
+    p, s = synth.config_params(2, n=n)
+    hdr, ln, ts = oracle.synth(p, s, 0, int(p.n))
+    return [(hdr[a:b], ln[a:b], ts[a:b]) for a, b in zip(cuts[:-1], cuts[1:])]
+
+
+def test_pipelined_config2_flows(native, oracle):
+    """Four uneven batches of a config-2 stream (the heavy-source path active), features +
+    scores, maps carried, launched back to back."""
+    n = 1 << 20
+    _run(native, oracle, _config2_batches(oracle, n, [0, 300_000, 300_001, 700_000, n]))
+
+
+def test_pipelined_replayed_stream(native, oracle):
+    """The warm streaming case of bench.py: the same batch shifted by its duration, 5 times."""
+    from flowsentryx_amd import synth
+    p, s = synth.config_params(2, n=1 << 19)
+    hdr, ln, ts = oracle.synth(p, s, 0, int(p.n))
+    batches = [(hdr, ln, ts + np.uint64(k * int(p.duration_ns))) for k in range(5)]
+    _run(native, oracle, batches)
+
+
+def test_pipelined_mixed_families_verdicts(native, oracle):
+    """Mixed IPv4 / IPv6 / non-IP / short frames, a jittered (non-monotone) batch between
+    monotone ones, verdicts only, many small batches."""
+    rng = np.random.default_rng(0x919E)
+    hdr, ln, ts = rand_stream(rng, 240_000, 2500, dt_max=60, v6_frac=0.3, nonip_frac=0.02,
+                              short_frac=0.01)
+    sw = rng.choice(np.arange(100_000, 140_000), 3000, replace=False)
+    ts[sw] -= rng.integers(0, 4000, sw.size).astype(np.uint64)
+    cuts = [0, 1, 5000, 60_000, 100_000, 140_000, 141_000, 240_000]
+    batches = [(hdr[a:b], ln[a:b], ts[a:b]) for a, b in zip(cuts[:-1], cuts[1:])]
+    _run(native, oracle, batches, flows=False, max_entries=1 << 18)
+
+
+def test_pipelined_map_ops_between_batches(native, oracle):
+    """A map update and a lookup between pipelined batches see (and order after) the batches
+    enqueued before them."""
+    from flowsentryx_amd import lib
+    batches = _config2_batches(oracle, 1 << 19, [0, 200_000, 400_000, 1 << 19])
+    key = batches[1][0][5, 26:30].tobytes()   # a source of the stream, blacklisted by hand
+
+    def between(j, c, o):
+        if j == 0:
+            till = int(batches[1][2][0]) + 10**12
+            c.map_update(lib.MAP_IPV4_BLACKLIST, key, till)
+            o.map_update(lib.MAP_IPV4_BLACKLIST, key, till)
+            assert c.map_lookup(lib.MAP_IPV4_BLACKLIST, key) == till
+    _run(native, oracle, batches, between=between)
+
+
+def test_pipelined_failed_batch_cancels_next(native, oracle):
+    """A batch that overflows max_entries fails; the batch launched after it is cancelled; the
+    error surfaces at sync and neither changes any map; the context then carries on."""
+    from flowsentryx_amd import lib, synth
+    import torch
+    rng = np.random.default_rng(77)
+    cfg = dict(pps_threshold=5, window_ns=100_000, block_ns=300_000)
+    h1, l1, t1 = rand_stream(rng, 3000, 120, dt_max=200)
+    big = synth.records([synth.frame_ipv4_udp(bytes([10, 77, i // 256, i % 256]), 90) for i in range(400)])
+    lb = np.full(400, 90, np.uint32)
+    tb = t1[-1] + np.arange(1, 401, dtype=np.uint64)
+    h3, l3, t3 = rand_stream(rng, 3000, 120, dt_max=200)
+    t3 = t3 + tb[-1]
+    h4, l4, t4 = rand_stream(rng, 3000, 120, dt_max=200)
+    t4 = t4 + t3[-1]
+    o = oracle.Oracle(max_entries=1 << 12, **cfg)
+    keep = []
+
+    def launch(c, h, l, t):
+        d = [_dev(torch, h), _dev(torch, l), _dev(torch, t), torch.empty(len(l), dtype=torch.uint8, device="cuda")]
+        keep.append(d)
+        c.verdict_batch_device(d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr(), len(l), d[3].data_ptr())
+        return d[3]
+
+    with native.FsxContext(max_batch=4096, max_entries=300, **cfg) as c:
+        c.set_pipeline(True)
+        v1 = launch(c, h1, l1, t1)
+        c.sync()
+        assert np.array_equal(v1.cpu().numpy(), o.batch(h1, l1, t1))
+        before = {m: c.map_dump(m) for m in MAPS}
+        s_before = c.stats()
+        launch(c, big, lb, tb)          # fails: 400 new sources > 300 - 120
+        launch(c, h3, l3, t3)           # cancelled by the device
+        with pytest.raises(lib.FsxError) as e:
+            c.sync()
+        assert e.value.code == -errno.ENOSPC
+        assert {m: c.map_dump(m) for m in MAPS} == before
+        assert c.stats() == s_before
+        v4 = launch(c, h4, l4, t4)
+        c.sync()
+        assert np.array_equal(v4.cpu().numpy(), o.batch(h4, l4, t4))
+        assert_same_state(c, o)
+
+
+def test_pipelined_failure_found_by_the_next_call(native, oracle):
+    """Three calls in a row: the third finds the first one's failure (waiting for the batch
+    two back before reusing its buffers), returns its error and enqueues nothing."""
+    from flowsentryx_amd import lib, synth
+    import torch
+    big = synth.records([synth.frame_ipv4_udp(bytes([10, 78, i // 256, i % 256]), 90) for i in range(400)])
+    ln = np.full(400, 90, np.uint32)
+    ts = np.arange(1, 401, dtype=np.uint64) + 10**9
+    d = [_dev(torch, big), _dev(torch, ln), _dev(torch, ts), torch.empty(400, dtype=torch.uint8, device="cuda")]
+    with native.FsxContext(max_batch=4096, max_entries=300) as c:
+        c.set_pipeline(True)
+        args = (d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr(), 400, d[3].data_ptr())
+        c.verdict_batch_device(*args)
+        c.verdict_batch_device(*args)
+        with pytest.raises(lib.FsxError) as e:
+            c.verdict_batch_device(*args)
+        assert e.value.code == -errno.ENOSPC
+        c.sync()   # nothing left in flight
+        assert len(c.map_dump(lib.MAP_IPV4_STATS)) == 0
