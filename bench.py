@@ -82,6 +82,8 @@ def parse_args():
                     help="N>1 collectives: nccl (RCCL over xGMI) or gloo (rehearsal on one GPU)")
     ap.add_argument("--limiter", choices=["fixed", "sliding", "token"], default="fixed",
                     help="limiter of the timed main loop (diagnostics; the headline is fixed)")
+    ap.add_argument("--no-pipeline", action="store_true",
+                    help="headline stream without batch pipelining (diagnostics)")
     ap.add_argument("--cold", action="store_true",
                     help="headline: every step the same batch from empty maps (fsx_reset inside "
                          "the step) instead of consecutive batches with the maps carried")
@@ -294,7 +296,7 @@ def main():
 
         def step(k, feat=False, v=None):
             ts_k = tss[k if stream else 0]
-            v = vb[k % 2] if v is None else v
+            v = vb[k % len(vb)] if v is None else v
             if not stream and not args.no_reset:
                 ctx.reset()
             if plane is not None:
@@ -361,7 +363,7 @@ def main():
             # tests/test_gpu_parity.py::test_device_synth_and_device_batch)
             nb = 3 if stream else 1
             ctx.reset()
-            vs = [vb[0], vb[1], torch.empty_like(d["v"])][:nb]
+            vs = [vb[0], vb[1], torch.empty_like(d["v"])][:nb] if stream else [vb[0]]
             for k in range(nb):
                 step(k, feat=k == nb - 1, v=vs[k])
             ctx.sync()
@@ -397,7 +399,8 @@ def main():
     n_head = args.packets or int(synth.config_params(args.config)[0].n)
     head = run_workload(args.config, n_head, args.steps, args.warmup, not args.no_mlp,
                         kernel_timing=True, check=not args.no_check and world == 1,
-                        cpu=not args.no_cpu_baseline and world == 1, stream=not args.cold)
+                        cpu=not args.no_cpu_baseline and world == 1, stream=not args.cold,
+                        pipelined=not args.no_pipeline)
     n = head["n"]
     p = head["p"]
     timings = head.get("timings", [])
@@ -631,7 +634,9 @@ def main():
     ms_step = head["ms_step"]
     sources = head["sources"]
     info = head.get("info", {})
-    dom = max(timings, key=lambda r: r[1]) if timings else None
+    # the dominant kernel: the longest launch (k_parse; the sort's three passes are shorter
+    # launches of pure implementation traffic)
+    dom = max(timings, key=lambda r: r[1] / max(r[2], 1e-9)) if timings else None
     roofline = None
     if world > 1:   # the per-kernel split is of one owner sub-batch: the roofline is the N = 1 line's
         roofline = {"bound": "hbm", "kernel": "k_parse", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -129,7 +129,7 @@ struct fsx_ctx {
         HeavySet *heavy;
         BatchState *bs;
     };
-    bool pipe = false;
+    int pipe = 0;                     // fsx_set_pipeline mode (2: never split front / tail)
     FrontBufs fb[2]{};
     int par = 0;                      // set of the last pipelined batch
     bool fl_on[2]{};                  // a pipelined batch of set p is in flight
@@ -543,7 +543,7 @@ int fsx_set_pipeline(fsx_ctx *c, int on) {
         use_front(c, 0);
         c->par = 0;
     }
-    c->pipe = on != 0;
+    c->pipe = on < 0 ? 0 : on > 2 ? 1 : on;
     return 0;
 }
 
@@ -704,11 +704,18 @@ static FlowRequest flow_slots(fsx_ctx *c, const FlowRequest *fr, size_t n, int *
 // tail on the walker stream (flows on the aux stream), so the next batch's front overlaps
 // this tail. The batch two back used this batch's front buffers: the host waits for its
 // tail (the device still has the previous batch to run) and checks it.
+// split = false (other limiters, record mode): the whole batch on the context stream, in
+// order after the previous one, still without a host synchronization per call.
 static int run_pipelined(fsx_ctx *c, const PacketIn &in, const uint32_t *d_len, const uint64_t *d_ts, size_t n,
-                         uint8_t *d_verdict, const FlowRequest *fr) {
+                         uint8_t *d_verdict, const FlowRequest *fr, bool split) {
     HIPCHK(c, hipSetDevice(c->device));
     int rc;
     if (c->pending && (rc = fsx_sync(c))) return rc;
+    if (c->rules_dirty) {   // the prefix tables are rebuilt with the device idle
+        if ((rc = fsx_sync(c)) || (rc = upload_rules(c))) return rc;
+    }
+    // an unsplit batch's tail runs on the context stream: a deferred tail goes first
+    if (!split && (rc = sel(c))) return rc;
     const int q = c->par ^ 1;
     if (c->fl_on[q]) {
         HIPCHK(c, hipEventSynchronize(c->tail_done[q]));
@@ -729,19 +736,24 @@ static int run_pipelined(fsx_ctx *c, const PacketIn &in, const uint32_t *d_len, 
         if (c->sc.id_tab) HIPCHK(c, hipMemsetAsync(c->sc.id_tab, 0, c->slots * 32, c->stream));
         c->id_gen = 1;
     }
-    const PipeSplit sp{c->walk_stream, c->front_done, c->fl_on[q ^ 1] ? c->fb[q ^ 1].bs : nullptr,
-                       pipe_on_parse, c, &c->tail_args};
+    const BatchState *prev = c->fl_on[q ^ 1] ? c->fb[q ^ 1].bs : nullptr;
+    const PipeSplit sp = split ? PipeSplit{c->walk_stream, c->front_done, prev, pipe_on_parse, c, &c->tail_args}
+                               : PipeSplit{nullptr, nullptr, prev, nullptr, nullptr, nullptr};
     hipError_t e = launch_verdict_pipeline(in, d_len, d_ts, (uint32_t)n, d_verdict, c->table, c->tstate, c->bs,
                                            c->sc, c->id_gen, table_index(c), c->lim, c->rs, true, fr, c->hist,
                                            c->stream, fork_flows() ? c->aux_stream : nullptr, c->fork_ev,
-                                           c->join_ev, nullptr, c->walk_fork_ev, c->walk_join_ev,
-                                           c->heavy_fork_ev, c->heavy_flow_ev, nullptr, &sp);
+                                           c->join_ev, split ? nullptr : c->walk_stream, c->walk_fork_ev,
+                                           c->walk_join_ev, c->heavy_fork_ev, c->heavy_flow_ev, nullptr, &sp);
     if (e != hipSuccess) return set_err(c, -EIO, "pipeline launch: %s", hipGetErrorString(e));
-    c->tail_pending = true;   // enqueued after the next batch's parse, or by the next sel()
-    c->tail_par = q;
     c->fl_on[q] = true;
     c->fl_born[q] = c->id_gen;
-    c->tail_join = true;
+    if (split) {
+        c->tail_pending = true;   // enqueued after the next batch's parse, or by the next sel()
+        c->tail_par = q;
+        c->tail_join = true;
+    } else {
+        HIPCHK(c, hipEventRecord(c->tail_done[q], c->stream));
+    }
     return 0;
 }
 
@@ -749,10 +761,11 @@ static int run_pipelined(fsx_ctx *c, const PacketIn &in, const uint32_t *d_len, 
 static int run_batch(fsx_ctx *c, const PacketIn &in, const uint32_t *d_len, const uint64_t *d_ts,
                      size_t n, uint8_t *d_verdict, bool do_limit, const FlowRequest *fr) {
     if (n > c->cfg.max_batch) return set_err(c, -E2BIG, "n=%zu exceeds max_batch", n);
-    // pipelined: the fixed window on header records, no per-kernel timing, rules uploaded
-    const bool pipe = c->pipe && do_limit && n && !in.rec && c->cfg.limiter == FSX_LIMIT_FIXED_WINDOW &&
-                      !c->timing && !c->rules_dirty;
-    if (pipe) return run_pipelined(c, in, d_len, d_ts, n, d_verdict, fr);
+    // pipelined (no per-kernel timing): split front / tail for the fixed window on header
+    // records, the whole batch on the context stream otherwise
+    if (c->pipe && do_limit && n && !c->timing)
+        return run_pipelined(c, in, d_len, d_ts, n, d_verdict, fr,
+                             c->pipe == 1 && !in.rec && c->cfg.limiter == FSX_LIMIT_FIXED_WINDOW);
     int rc = sel(c);
     if (rc) return rc;
     if (busy(c)) { rc = fsx_sync(c); if (rc) return rc; }

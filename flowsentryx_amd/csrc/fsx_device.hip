@@ -2101,7 +2101,7 @@ hipError_t launch_tail(const TailArgs &a) {
         }
         return hipSuccess;
     };
-    if (split) {
+    if (split && split->tail) {
         // pipelined: the tail on its own stream (the caller made it and st2 wait for the
         // front); walkers serial on it, the heavy flow sums and the flows on st2
         st = split->tail;
@@ -2229,7 +2229,7 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
     hipError_t e;
     if ((e = hipMemsetAsync(bs, 0, sizeof(BatchState), st)) != hipSuccess) return e;
     if (n == 0) return hipSuccess;
-    if (!split && (e = hipMemsetAsync(sc.marks, 0, n, st)) != hipSuccess) return e;
+    if (!(split && split->tail) && (e = hipMemsetAsync(sc.marks, 0, n, st)) != hipSuccess) return e;
     const uint32_t gridStream = std::min<uint32_t>(2048, std::max<uint32_t>(1, cdiv(n, 256)));
     const uint32_t gridTiles = std::min<uint32_t>(4096, std::max<uint32_t>(1, cdiv(n, kTile)));
 
@@ -2341,7 +2341,7 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
                 return e;
         }
     }
-    if (split) {   // pipelined: the front is done; the tail is handed back (run later)
+    if (split && split->front_done) {   // pipelined: the front is done; the tail is handed back
         if ((e = hipEventRecord(split->front_done, st)) != hipSuccess) return e;
     }
     TailArgs ta{};

@@ -278,10 +278,11 @@ class FsxContext:
     def sync(self):
         self._check(self._lib.fsx_sync(self._h), "fsx_sync")
 
-    def set_pipeline(self, on: bool = True):
+    def set_pipeline(self, on: bool | int = True):
         """Batch pipelining (include/fsx_hip.h fsx_set_pipeline): the next batch's parse and
-        sort overlap this batch's walkers and verdicts; read outputs after sync()."""
-        self._check(self._lib.fsx_set_pipeline(self._h, 1 if on else 0), "fsx_set_pipeline")
+        sort overlap this batch's walkers and verdicts; read outputs after sync(). on = 2:
+        batches whole on the context stream, only without a host synchronization per call."""
+        self._check(self._lib.fsx_set_pipeline(self._h, int(on)), "fsx_set_pipeline")
 
     def set_stream(self, stream_handle: int | None):
         self._check(self._lib.fsx_set_stream(self._h, stream_handle or None), "fsx_set_stream")

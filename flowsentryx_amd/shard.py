@@ -81,24 +81,22 @@ class HipShardEngine:
         # stream: a NULL handle would give the context its own stream back)
         self.stream = torch.cuda.Stream(device)
         ctx.set_stream(self.stream.cuda_stream)
+        # owner batches back to back without a host synchronization per call (errors surface
+        # at the next synchronization; each batch whole on the engine stream)
+        ctx.set_pipeline(2)
         # collectives run from a second stream, so the exchange of sub-batch j + 1 overlaps
         # the owner pipeline of sub-batch j (ShardedDataPlane)
         self.comm = torch.cuda.Stream(device)
         self.max_local = max_local
         self.owner_cap = int(ctx.config.max_batch)
-        # two pipeline slots: sub-batch j uses slot j % 2 of every per-sub-batch buffer
-        self.recs = [torch.empty(max(1, max_local) * REC, dtype=torch.uint8, device=device)
-                     for _ in range(2)]
-        self.send_idxs = [torch.empty(max(1, max_local), dtype=torch.int32, device=device)
-                          for _ in range(2)]
-        self.countss = [torch.empty(lib.MAX_SHARDS + 2, dtype=torch.int64, device=device)
-                        for _ in range(2)]
-        self.rec, self.send_idx, self.counts = self.recs[0], self.send_idxs[0], self.countss[0]
+        # per-sub-batch buffers by pipeline slot (allocated on first use, sized for the piece)
+        self.recs, self.send_idxs, self.countss = {}, {}, {}
+        self.rec = self.send_idx = self.counts = None
         self.clock3 = torch.empty(3, dtype=torch.int64, device=device)
         self.blk = torch.empty(1024 * lib.SHARD_BLOCK_BYTES, dtype=torch.uint8, device=device)
         self.blk_count = torch.empty(1, dtype=torch.int64, device=device)
         self._oh = None  # owner-side header/len/ts buffers, grown on demand
-        self._ov = [None, None]   # owner-side verdicts per slot
+        self._ov = {}             # owner-side verdicts per slot
         self.flows = None
 
     # -- streams of the pipelined plane (the CPU engine has none)
@@ -173,7 +171,7 @@ class HipShardEngine:
         self._run(hdr.data_ptr(), length.data_ptr(), ts.data_ptr(), n, verdict.data_ptr())
 
     def _owner_verdicts(self, m: int, slot: int) -> torch.Tensor:
-        if self._ov[slot] is None or self._ov[slot].numel() < m:
+        if self._ov.get(slot) is None or self._ov[slot].numel() < m:
             self._ov[slot] = torch.empty(max(m, 1), dtype=torch.uint8, device=self.device)
         return self._ov[slot]
 
@@ -222,6 +220,11 @@ class HipShardEngine:
         if n > self.max_local:
             raise ValueError(f"local slice of {n} packets exceeds {self.max_local}")
         flags = lib.SHARD_COMPACT | (lib.SHARD_FILTER_BLOCKLIST if filt else 0)
+        if slot not in self.recs or self.send_idxs[slot].numel() < max(1, n):
+            m = max(1, n)
+            self.recs[slot] = torch.empty(m * REC, dtype=torch.uint8, device=self.device)
+            self.send_idxs[slot] = torch.empty(m, dtype=torch.int32, device=self.device)
+            self.countss[slot] = torch.empty(lib.MAX_SHARDS + 2, dtype=torch.int64, device=self.device)
         rec, idx, cnt = self.recs[slot], self.send_idxs[slot], self.countss[slot]
         self.rec, self.send_idx, self.counts = rec, idx, cnt   # (tests read the last pack)
         self.ctx.shard_pack_device(hdr.data_ptr(), length.data_ptr(), ts.data_ptr(), n, G,
@@ -334,7 +337,21 @@ class ShardedDataPlane:
             if bounds is None:
                 bounds = [n * i // chunks for i in range(chunks + 1)]
             k = len(bounds) - 1
-            filt = self._filter_plan(ts, bounds) if filt_on else [False] * k
+            if not filt_on:
+                # no replica filter: every pack is independent of the owners, so all of them
+                # go first and one exchange of all their counts is the batch's only host
+                # synchronization; the record exchanges then overlap the owner work
+                pend = self._exchange_all(hdr, length, ts, verdict, bounds)
+                sent = recv = 0
+                for j in range(k):
+                    ms, mr = self._stage_owner(verdict, bounds, j, pend[j], slot=j)
+                    pend[j] = None
+                    sent, recv = sent + ms, recv + mr
+                if flows:
+                    self.engine.flows_end()
+                self.last_exchange = {"sent": sent, "received": recv, "filtered": self.filtered}
+                return
+            filt = self._filter_plan(ts, bounds)
             pend = [None] * k
             pend[0] = self._stage_exchange(hdr, length, ts, verdict, bounds, 0, filt[0])
             sent = recv = 0
@@ -392,6 +409,45 @@ class ShardedDataPlane:
             out.append(ok)
         return out
 
+    def _exchange_all(self, hdr, length, ts, verdict, bounds):
+        """Pack every sub-batch j into slot j (engine stream), one all-to-all of all their
+        per-owner counts and ONE host read of them (comm stream), then the record exchange
+        of every sub-batch; per sub-batch what _stage_exchange returns."""
+        G, e = self.world, self.engine
+        k = len(bounds) - 1
+        packs = [e.pack(hdr[bounds[j] * 64:], length[bounds[j]:], ts[bounds[j]:], bounds[j + 1] - bounds[j],
+                        G, verdict[bounds[j]:], False, j) for j in range(k)]
+        pend = []
+        with e.comm_ctx():
+            cnt = torch.stack([c for _, c in packs])                       # [k, G + 2]
+            fmt = (cnt[:, G + 1:G + 2] == lib.SHARD_RECORD16_BYTES).to(cnt.dtype)
+            send = (cnt[:, :G] * 2 + fmt).t().contiguous()                  # [G, k] by destination
+            recv_counts = torch.empty_like(send)                            # [G, k] by source
+            _a2a(recv_counts.view(-1), send.view(-1), [k] * G, [k] * G, self.group)
+            both = torch.cat([cnt.reshape(-1), recv_counts.view(-1).to(cnt.device)]).tolist()
+            base = k * (G + 2)
+            for j in range(k):
+                cj = both[j * (G + 2):(j + 1) * (G + 2)]
+                rw = [int(both[base + r * k + j]) for r in range(G)]
+                self.filtered += int(cj[G])
+                rb = int(cj[G + 1])
+                sc = [int(x) for x in cj[:G]]
+                rc = [x >> 1 for x in rw]
+                rf = [lib.SHARD_RECORD16_BYTES if x & 1 else lib.SHARD_RECORD_BYTES for x in rw]
+                in_b = [x * rb for x in sc]
+                out_b = [c * f for c, f in zip(rc, rf)]
+                recv = e.recv_buffer(sum(out_b))
+                _a2a(recv[:sum(out_b)], packs[j][0][:sum(in_b)], out_b, in_b, self.group)
+                arrived = e.comm_event()
+                segs, off = [], 0
+                for c, f, nb in zip(rc, rf, out_b):
+                    segs.append((off, c, f))
+                    off += nb
+                    if c:
+                        self.formats.add(f)
+                pend.append((recv, segs, sc, rc, arrived))
+        return pend
+
     def _stage_exchange(self, hdr, length, ts, verdict, bounds, j: int, filt: bool):
         """Pack sub-batch j (engine stream) and exchange its counts and records (comm stream)."""
         G, e = self.world, self.engine
@@ -425,13 +481,13 @@ class ShardedDataPlane:
                 self.formats.add(f)
         return recv, segs, sc, rc, arrived
 
-    def _stage_owner(self, verdict, bounds, j: int, pend):
+    def _stage_owner(self, verdict, bounds, j: int, pend, slot=None):
         """Owner pipeline of sub-batch j (engine stream), verdicts back (comm stream) and
         into arrival positions (engine stream)."""
         G, e = self.world, self.engine
         recv, segs, sc, rc, arrived = pend
         a = bounds[j]
-        slot = j % 2
+        slot = j % 2 if slot is None else slot
         ms, mr = sum(sc), sum(rc)
         e.engine_wait(arrived)        # the records of sub-batch j have arrived
         e.keep(recv)                  # allocated on the comm stream, read on the engine's

@@ -181,8 +181,10 @@ int fsx_sync(fsx_ctx *ctx);
  * outputs after fsx_sync (or any other entry point, which orders the context stream after
  * the last tail). A failed batch cancels the batch after it; the error (e.g. -ENOSPC) is
  * returned by fsx_sync or by the call that found it, which enqueues nothing, and neither
- * failed batch changes any map. Other limiters, record mode and timed batches run
- * unpipelined. */
+ * failed batch changes any map. Other limiters and record mode run each batch whole on the
+ * context stream (no overlap, but still no host synchronization per call); so does every
+ * batch with on = 2 (a caller that reuses input buffers in stream order); timed batches
+ * (fsx_enable_timing) run unpipelined. on = 0 turns it off. */
 int fsx_set_pipeline(fsx_ctx *ctx, int on);
 
 /* Replaces fsx() (src/fsx_kern.c:96-347) over a batch of n packets in arrival

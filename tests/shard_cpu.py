@@ -54,7 +54,7 @@ class CpuShardEngine:
         self.oracle = oracle
         self.o = oracle.Oracle(**cfg)
         self.send_idx = np.zeros(0, dtype=np.int64)
-        self.send_idxs = [self.send_idx, self.send_idx]
+        self.send_idxs = {}   # per pipeline slot
         self.replica = {}
 
     def stream_ctx(self):

@@ -202,3 +202,32 @@ def test_pipelined_failure_found_by_the_next_call(native, oracle):
         assert e.value.code == -errno.ENOSPC
         c.sync()   # nothing left in flight
         assert len(c.map_dump(lib.MAP_IPV4_STATS)) == 0
+
+
+@pytest.mark.parametrize("limiter", [1, 2])
+def test_pipelined_other_limiters(native, oracle, limiter):
+    """Sliding window and token bucket with pipelining on: each batch runs whole on the
+    context stream, in order, without a host synchronization per call (device-side
+    cancellation after a failure, as for the split fixed window)."""
+    import torch
+    rng = np.random.default_rng(0x51 + limiter)
+    cfg = dict(pps_threshold=20, window_ns=200_000, block_ns=500_000, limiter=limiter,
+               tb_rate=50_000, tb_burst=8)
+    hdr, ln, ts = rand_stream(rng, 150_000, 800, dt_max=80, v6_frac=0.2, nonip_frac=0.01)
+    cuts = [0, 20_000, 20_001, 90_000, 150_000]
+    o = oracle.Oracle(max_entries=1 << 16, **cfg)
+    maps = (3, 4, 5, 6) if limiter == 2 else MAPS
+    outs = []
+    with native.FsxContext(max_batch=1 << 17, max_entries=1 << 16, **cfg) as c:
+        c.set_pipeline(True)
+        for a, b in zip(cuts[:-1], cuts[1:]):
+            d = [_dev(torch, hdr[a:b]), _dev(torch, ln[a:b]), _dev(torch, ts[a:b]),
+                 torch.empty(b - a, dtype=torch.uint8, device="cuda")]
+            c.verdict_batch_device(d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr(), b - a, d[3].data_ptr())
+            outs.append((d, o.batch(hdr[a:b], ln[a:b], ts[a:b])))
+        c.sync()
+        for j, (d, vo) in enumerate(outs):
+            assert np.array_equal(d[3].cpu().numpy(), vo), j
+        assert c.stats() == o.stats()
+        for m in maps:
+            assert c.map_dump(m) == o.map_dump(m), m

@@ -75,3 +75,14 @@ def test_sharded_mixed_record_formats(tmp_path):
                 cfg=dict(pps_threshold=7, window_ns=200_000, block_ns=1_000_000, max_entries=4096))
     res = run_sharded(tmp_path, 2, spec)
     assert set(res["formats"]) == {16, 32}, res["formats"]
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_without_blocklist_filter_all_packs_first(tmp_path, world):
+    """Filter off (as with flow features): every sub-batch is packed first and one exchange of
+    all their counts precedes the record exchanges (shard.py _exchange_all), mixed record
+    formats and families included."""
+    spec = dict(BASE, chunks=4, filter=False, v6_frac=0.001, seed=31, n_ips=80,
+                cfg=dict(pps_threshold=7, window_ns=200_000, block_ns=1_000_000, max_entries=4096))
+    res = run_sharded(tmp_path, world, spec)
+    assert res["filtered"] == 0
