@@ -59,7 +59,7 @@ def main():
         rows[k] = row
     doc = {"source": f"rocprofv3 --kernel-trace --pmc passes under {d.name} (scripts/gpu_pmc.sh)",
            "workload": {"config": 2, "packets_per_gpu": 67108864, "n_gpus": 1,
-                        "command": "python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-check --legs ''"},
+                        "command": "python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-check --legs ''", "headline": "stream: consecutive batches, maps carried, pipelined (the first batch inserts every source)"},
            "correction": "FETCH_SIZE x2 (gfx950, MI355X_MICROARCH.md HBM section); WRITE_SIZE as read",
            "kernels": rows}
     print(json.dumps(doc, indent=1))
