@@ -130,11 +130,12 @@ struct fsx_ctx {
         BatchState *bs;
     };
     int pipe = 0;                     // fsx_set_pipeline mode (2: never split front / tail)
-    FrontBufs fb[2]{};
+    static constexpr int kSets = 3;   // front buffer sets: batch k waits only for batch k - 3
+    FrontBufs fb[kSets]{};
     int par = 0;                      // set of the last pipelined batch
-    bool fl_on[2]{};                  // a pipelined batch of set p is in flight
-    uint32_t fl_born[2]{};
-    hipEvent_t tail_done[2]{};
+    bool fl_on[kSets]{};              // a pipelined batch of set p is in flight
+    uint32_t fl_born[kSets]{};
+    hipEvent_t tail_done[kSets]{};
     hipEvent_t front_done = nullptr;  // after the last pipelined batch's sort
     hipEvent_t parse_done = nullptr;  // after the current pipelined batch's parse
     TailArgs tail_args{};             // the last pipelined batch's tail, not yet enqueued
@@ -280,7 +281,12 @@ static int sel(fsx_ctx *c) {
     return 0;
 }
 
-static bool busy(const fsx_ctx *c) { return c->pending || c->fl_on[0] || c->fl_on[1]; }
+static bool pipe_busy(const fsx_ctx *c) {
+    for (int p = 0; p < fsx_ctx::kSets; ++p)
+        if (c->fl_on[p]) return true;
+    return false;
+}
+static bool busy(const fsx_ctx *c) { return c->pending || pipe_busy(c); }
 
 // The front buffers of set p become the context's current sort arrays and BatchState.
 static void use_front(fsx_ctx *c, int p) {
@@ -306,11 +312,10 @@ void fsx_close(fsx_ctx *c) {
     if (c->stream) hipStreamSynchronize(c->stream);
     if (c->walk_stream) hipStreamSynchronize(c->walk_stream);
     if (c->aux_stream) hipStreamSynchronize(c->aux_stream);
-    if (c->fb[1].bs) {
-        use_front(c, 0);
-        free_front(c->fb[1]);
-    }
-    for (int p = 0; p < 2; ++p) if (c->tail_done[p]) hipEventDestroy(c->tail_done[p]);
+    if (c->fb[0].bs) use_front(c, 0);   // (set 0 owns what free_scratch frees)
+    for (int p = 1; p < fsx_ctx::kSets; ++p)
+        if (c->fb[p].bs) free_front(c->fb[p]);
+    for (int p = 0; p < fsx_ctx::kSets; ++p) if (c->tail_done[p]) hipEventDestroy(c->tail_done[p]);
     if (c->front_done) hipEventDestroy(c->front_done);
     if (c->parse_done) hipEventDestroy(c->parse_done);
     free_scratch(c);
@@ -479,7 +484,8 @@ static int check_batch(fsx_ctx *c) {
 static int check_pipelined(fsx_ctx *c) {
     int rc = 0;
     bool failed = false;
-    for (int p : {c->par ^ 1, c->par}) {
+    for (int i = 1; i <= fsx_ctx::kSets; ++i) {   // oldest set first
+        const int p = (c->par + i) % fsx_ctx::kSets;
         if (!c->fl_on[p]) continue;
         c->fl_on[p] = false;
         BatchState h;
@@ -519,8 +525,9 @@ int fsx_set_pipeline(fsx_ctx *c, int on) {
     if (!c) return -EINVAL;
     int rc = fsx_sync(c);
     if (rc) return rc;
-    if (on && !c->fb[1].bs) {
-        fsx_ctx::FrontBufs &f = c->fb[1];
+    for (int fs = 1; on && fs < fsx_ctx::kSets; ++fs) {
+        if (c->fb[fs].bs) continue;
+        fsx_ctx::FrontBufs &f = c->fb[fs];
         const uint64_t cap = c->sc.cap;
         for (int b = 0; b < 2; ++b) {
             HIPCHK(c, hipMalloc(&f.packed[b], cap * 8));
@@ -533,13 +540,13 @@ int fsx_set_pipeline(fsx_ctx *c, int on) {
         HIPCHK(c, hipMemset(f.heavy, 0, sizeof(HeavySet)));
         HIPCHK(c, hipMalloc(&f.bs, sizeof(BatchState)));
         HIPCHK(c, hipMemset(f.bs, 0, sizeof(BatchState)));
-        for (int p = 0; p < 2; ++p)
+        for (int p = 0; p < fsx_ctx::kSets; ++p)
             if (!c->tail_done[p]) HIPCHK(c, hipEventCreateWithFlags(&c->tail_done[p], hipEventDisableTiming));
         if (!c->front_done) HIPCHK(c, hipEventCreateWithFlags(&c->front_done, hipEventDisableTiming));
         if (!c->parse_done) HIPCHK(c, hipEventCreateWithFlags(&c->parse_done, hipEventDisableTiming));
     }
-    if (!on && c->par == 1) {   // back to set 0, keeping the last batch's facts
-        HIPCHK(c, hipMemcpy(c->fb[0].bs, c->fb[1].bs, sizeof(BatchState), hipMemcpyDeviceToDevice));
+    if (!on && c->par != 0) {   // back to set 0, keeping the last batch's facts
+        HIPCHK(c, hipMemcpy(c->fb[0].bs, c->fb[c->par].bs, sizeof(BatchState), hipMemcpyDeviceToDevice));
         use_front(c, 0);
         c->par = 0;
     }
@@ -702,7 +709,7 @@ static FlowRequest flow_slots(fsx_ctx *c, const FlowRequest *fr, size_t n, int *
 
 // A pipelined batch (fsx_set_pipeline): its front (parse, sort) on the context stream, its
 // tail on the walker stream (flows on the aux stream), so the next batch's front overlaps
-// this tail. The batch two back used this batch's front buffers: the host waits for its
+// this tail. The batch three back used this batch's front buffers: the host waits for its
 // tail (the device still has the previous batch to run) and checks it.
 // split = false (other limiters, record mode): the whole batch on the context stream, in
 // order after the previous one, still without a host synchronization per call.
@@ -716,7 +723,7 @@ static int run_pipelined(fsx_ctx *c, const PacketIn &in, const uint32_t *d_len, 
     }
     // an unsplit batch's tail runs on the context stream: a deferred tail goes first
     if (!split && (rc = sel(c))) return rc;
-    const int q = c->par ^ 1;
+    const int q = (c->par + 1) % fsx_ctx::kSets;   // the set of the batch three calls back
     if (c->fl_on[q]) {
         HIPCHK(c, hipEventSynchronize(c->tail_done[q]));
         BatchState h;
@@ -730,13 +737,14 @@ static int run_pipelined(fsx_ctx *c, const PacketIn &in, const uint32_t *d_len, 
         if (rc) return rc;
         fr = &frq;
     }
+    // the batch before this one (still in flight: its failure cancels this one)
+    const BatchState *prev = c->fl_on[c->par] ? c->fb[c->par].bs : nullptr;
     use_front(c, q);
     c->par = q;
     if (++c->id_gen == 0x10000u) {
         if (c->sc.id_tab) HIPCHK(c, hipMemsetAsync(c->sc.id_tab, 0, c->slots * 32, c->stream));
         c->id_gen = 1;
     }
-    const BatchState *prev = c->fl_on[q ^ 1] ? c->fb[q ^ 1].bs : nullptr;
     const PipeSplit sp = split ? PipeSplit{c->walk_stream, c->front_done, prev, pipe_on_parse, c, &c->tail_args}
                                : PipeSplit{nullptr, nullptr, prev, nullptr, nullptr, nullptr};
     hipError_t e = launch_verdict_pipeline(in, d_len, d_ts, (uint32_t)n, d_verdict, c->table, c->tstate, c->bs,
@@ -1124,7 +1132,7 @@ int fsx_reset(fsx_ctx *c) {
     if (!c) return -EINVAL;
     int rc = sel(c);
     if (rc) return rc;
-    if ((c->fl_on[0] || c->fl_on[1]) && (rc = fsx_sync(c))) return rc;   // (pipelined batches)
+    if (pipe_busy(c) && (rc = fsx_sync(c))) return rc;   // (pipelined batches)
     c->pending_born = 0;   // the whole table is wiped: no rollback of a pending batch
     HIPCHK(c, hipMemsetAsync(c->table, 0, c->slots * sizeof(Slot), c->stream));
     HIPCHK(c, hipMemsetAsync(c->tstate, 0, sizeof(TableState), c->stream));

@@ -175,8 +175,8 @@ int fsx_sync(fsx_ctx *ctx);
  * fsx_verdict_batch_device / fsx_process_batch_device call enqueues the batch's front
  * (parse, sort) on the context stream and its tail (walkers, verdicts, flows) on the
  * context's own side streams, so the next batch's front overlaps this batch's tail; results
- * and map state are exactly those of the same calls without pipelining. Up to two batches
- * are in flight: a call first waits (on the host) for the batch two calls back. The caller
+ * and map state are exactly those of the same calls without pipelining. Up to three batches
+ * are in flight: a call first waits (on the host) for the batch three calls back. The caller
  * keeps a batch's input and output buffers untouched until that batch completes: read the
  * outputs after fsx_sync (or any other entry point, which orders the context stream after
  * the last tail). A failed batch cancels the batch after it; the error (e.g. -ENOSPC) is

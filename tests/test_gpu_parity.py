@@ -397,6 +397,18 @@ def test_flow_features_heavy_sources(native, oracle):
     _check_flows(native, oracle, hdr, ln, ts)
 
 
+def test_flow_features_long_spans(native, oracle):
+    """Config-1 sources over 4M packets: the top source has ~750K packets (~730 flow tiles),
+    so k_flow_combine's four-partials-per-lane loop (sources spanning >= 194 tiles) runs,
+    not only its remainder loop."""
+    from flowsentryx_amd import synth
+    p, s = synth.config_params(1, n=1 << 22)
+    hdr, ln, ts = oracle.synth(p, s, 0, int(p.n))
+    _, counts = np.unique(hdr[:, 26:30].copy().view(np.uint32), return_counts=True)
+    assert counts.max() >= 194 * 1024
+    _check_flows(native, oracle, hdr, ln, ts, cfg=dict(max_batch=1 << 22))
+
+
 def _process_batch_device(native, oracle, batches, max_entries=1 << 20):
     """Verdicts + per-source features + q8 scores of each batch in one device call on one
     context (maps carried), against the oracle's verdicts and its per-batch flow rows."""

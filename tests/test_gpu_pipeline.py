@@ -183,9 +183,10 @@ def test_pipelined_failed_batch_cancels_next(native, oracle):
         assert_same_state(c, o)
 
 
-def test_pipelined_failure_found_by_the_next_call(native, oracle):
-    """Three calls in a row: the third finds the first one's failure (waiting for the batch
-    two back before reusing its buffers), returns its error and enqueues nothing."""
+def test_pipelined_failure_found_by_a_later_call(native, oracle):
+    """Four calls in a row: the fourth finds the first one's failure (it waits for the batch
+    three back before reusing its buffers), returns its error and enqueues nothing; the two
+    batches in between were cancelled on the device and are rolled back too."""
     from flowsentryx_amd import lib, synth
     import torch
     big = synth.records([synth.frame_ipv4_udp(bytes([10, 78, i // 256, i % 256]), 90) for i in range(400)])
@@ -195,6 +196,7 @@ def test_pipelined_failure_found_by_the_next_call(native, oracle):
     with native.FsxContext(max_batch=4096, max_entries=300) as c:
         c.set_pipeline(True)
         args = (d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr(), 400, d[3].data_ptr())
+        c.verdict_batch_device(*args)
         c.verdict_batch_device(*args)
         c.verdict_batch_device(*args)
         with pytest.raises(lib.FsxError) as e:
