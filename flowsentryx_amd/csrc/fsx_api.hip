@@ -935,6 +935,7 @@ int fsx_verdict_batch(fsx_ctx *c, const uint8_t *hdr, const uint32_t *len, const
     HIPCHK(c, hipMemcpyAsync(c->d_ts, ts, n * 8, hipMemcpyHostToDevice, c->stream));
     rc = fsx_verdict_batch_device(c, c->d_hdr, c->d_len, c->d_ts, n, c->d_verdict);
     if (rc) return rc;
+    if ((rc = sel(c))) return rc;   // (a pipelined batch's tail writes the verdicts)
     HIPCHK(c, hipMemcpyAsync(verdict, c->d_verdict, n, hipMemcpyDeviceToHost, c->stream));
     return fsx_sync(c);
 }

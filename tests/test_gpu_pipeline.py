@@ -233,3 +233,16 @@ def test_pipelined_other_limiters(native, oracle, limiter):
         assert c.stats() == o.stats()
         for m in maps:
             assert c.map_dump(m) == o.map_dump(m), m
+
+
+def test_pipelined_host_pointer_batches(native, oracle):
+    """fsx_verdict_batch (host buffers, staged) on a pipelined context: the copy back waits
+    for the batch's deferred tail."""
+    rng = np.random.default_rng(0x4057)
+    hdr, ln, ts = rand_stream(rng, 120_000, 900, dt_max=100, v6_frac=0.2)
+    o = oracle.Oracle(max_entries=1 << 18)
+    with native.FsxContext(max_batch=1 << 17, max_entries=1 << 18) as c:
+        c.set_pipeline(True)
+        for a, b in ((0, 50_000), (50_000, 50_001), (50_001, 120_000)):
+            assert np.array_equal(c.verdict_batch(hdr[a:b], ln[a:b], ts[a:b]), o.batch(hdr[a:b], ln[a:b], ts[a:b]))
+        assert_same_state(c, o)
