@@ -6,7 +6,7 @@
 //   k_shard_parse     parse (src/parsing_helper.h:49-136 rules) + owner of every IP
 //                     packet from coalesced, LDS-staged header loads; per-tile per-owner
 //                     counts, local verdicts, and the 16-byte records in arrival order
-//   k_shard_scan      exclusive scan over (owner, tile) -> send offsets, per-owner totals
+//   k_shard_scan      per owner (one block each): exclusive scan over its tiles, its total
 //   k_shard_pack16 /  stable partition by owner (16-byte records from k_shard_parse's
 //   k_shard_pack      arrival-order copy / re-parsed into 32-byte records {src key, ts, len,
 //                     L4 dst port, family} (16-byte {IPv4 key, len, dport, ts} when the
@@ -176,6 +176,13 @@ __global__ __launch_bounds__(256) void k_shard_parse(const uint8_t *__restrict__
     if (threadIdx.x < G) cnt[(size_t)threadIdx.x * ntiles + t] = sh[threadIdx.x];
 }
 
+// The first record slot of owner o: the totals of the owners before it.
+__device__ __forceinline__ uint32_t owner_base(const uint64_t *owner_total, uint32_t o) {
+    uint32_t b = 0;
+    for (uint32_t k = 0; k < o; ++k) b += (uint32_t)owner_total[k];
+    return b;
+}
+
 // Compact pack (16-byte records, no header re-read): per tile, the owners and records
 // k_shard_parse left in arrival order are placed stably at their owners' offsets.
 __global__ __launch_bounds__(256) void k_shard_pack16(const uint8_t *__restrict__ own8,
@@ -191,6 +198,7 @@ __global__ __launch_bounds__(256) void k_shard_pack16(const uint8_t *__restrict_
     for (uint32_t o = threadIdx.x; o < 4 * kMaxShards; o += 256) (&s_wc[0][0])[o] = 0;
     __syncthreads();
     uint8_t ob[16];
+    // (loading the records here too, 16 per lane, made the kernel slower: 0.70 -> 0.96 ms)
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
         const uint32_t i = t * kShardTile + w * 1024u + (uint32_t)r * 64u + lane;
@@ -200,7 +208,7 @@ __global__ __launch_bounds__(256) void k_shard_pack16(const uint8_t *__restrict_
     __syncthreads();
     if (threadIdx.x < G) {   // exclusive over the waves, from the tile's owner base
         const uint32_t o = threadIdx.x;
-        uint32_t b = offs[(size_t)o * ntiles + t];
+        uint32_t b = offs[(size_t)o * ntiles + t] + owner_base(owner_total, o);
         for (int k = 0; k < 4; ++k) {
             const uint32_t c = s_wc[k][o];
             s_wc[k][o] = b;
@@ -232,42 +240,40 @@ __global__ __launch_bounds__(256) void k_shard_pack16(const uint8_t *__restrict_
     }
 }
 
-// One block: exclusive scan of cnt in owner-major order (in place) and per-owner totals.
-__global__ __launch_bounds__(1024) void k_shard_scan(uint32_t *__restrict__ cnt, uint64_t total_n,
-                                                     uint64_t *__restrict__ owner_total,
+// One block per owner: exclusive scan of its row of per-tile counts (in place, from 0) and
+// its total; the packs add the owner's base (the totals of the owners before it,
+// owner_base). Rows of 4096 tiles per round (4 per thread).
+__global__ __launch_bounds__(1024) void k_shard_scan(uint32_t *__restrict__ cnt, uint64_t *__restrict__ owner_total,
                                                      uint32_t G, uint32_t ntiles, int compact) {
     __shared__ uint32_t s_w[16];
-    __shared__ uint32_t s_carry;
-    const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
-    if (threadIdx.x == 0) s_carry = 0;
-    __syncthreads();
-    const uint64_t N = (uint64_t)G * ntiles;
-    for (uint64_t c0 = 0; c0 < N; c0 += 1024) {
-        const uint64_t i = c0 + threadIdx.x;
-        const uint32_t x = i < N ? cnt[i] : 0u;
-        const uint32_t incl = wave_incl_sum(x);
+    const uint32_t lane = lane_id(), w = threadIdx.x >> 6, o = blockIdx.x;
+    uint32_t *row = cnt + (size_t)o * ntiles;
+    uint32_t carry = 0;
+    for (uint32_t c0 = 0; c0 < ntiles; c0 += 4096) {
+        const uint32_t i = c0 + threadIdx.x * 4u;
+        uint32_t x[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) x[k] = i + k < ntiles ? row[i + k] : 0u;
+        const uint32_t sum = x[0] + x[1] + x[2] + x[3];
+        const uint32_t incl = wave_incl_sum(sum);
         if (lane == 63) s_w[w] = incl;
         __syncthreads();
-        uint32_t off = s_carry, tot = 0;
+        uint32_t off = carry, tot = 0;
         for (uint32_t k = 0; k < 16; ++k) {
             off += k < w ? s_w[k] : 0u;
             tot += s_w[k];
         }
-        if (i < N) cnt[i] = off + incl - x;
+        off += incl - sum;
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (i + k < ntiles) { row[i + k] = off; off += x[k]; }
+        carry += tot;
         __syncthreads();
-        if (threadIdx.x == 0) s_carry += tot;
-        __syncthreads();
-    }
-    // totals: difference of consecutive owner bases
-    if (threadIdx.x < G) {
-        const uint32_t o = threadIdx.x;
-        const uint32_t b0 = cnt[(size_t)o * ntiles];
-        const uint32_t b1 = o + 1 < G ? cnt[(size_t)(o + 1) * ntiles] : s_carry;
-        owner_total[o] = b1 - b0;
     }
     if (threadIdx.x == 0) {
+        owner_total[o] = carry;
         // compact requests: the wide flag of k_shard_parse becomes the record size
-        if (compact) owner_total[G + 1] = owner_total[G + 1] ? 32u : 16u;
+        if (o == 0 && compact) owner_total[G + 1] = owner_total[G + 1] ? 32u : 16u;
     }
 }
 
@@ -285,7 +291,7 @@ __global__ __launch_bounds__(256) void k_shard_pack(const uint8_t *__restrict__ 
     __shared__ uint32_t s_base[kMaxShards];
     __shared__ uint32_t s_wc[4][kMaxShards];
     const uint32_t t = blockIdx.x, lane = lane_id(), w = threadIdx.x >> 6;
-    if (threadIdx.x < G) s_base[threadIdx.x] = offs[(size_t)threadIdx.x * ntiles + t];
+    if (threadIdx.x < G) s_base[threadIdx.x] = offs[(size_t)threadIdx.x * ntiles + t] + owner_base(owner_total, threadIdx.x);
     // wave w owns packets [t*4096 + w*1024, +1024) in arrival order: count per owner
     // first (so a wave places after the waves before it), then place in order
     uint32_t of[16];   // owner << 4 | class (0 DROP, 1 PASS, 4/6 IP, 15 none)
@@ -433,7 +439,7 @@ hipError_t launch_shard_pack(const uint8_t *hdr, const uint32_t *len, const uint
     ShardRecord16 *cr = compact ? reinterpret_cast<ShardRecord16 *>(crec) : nullptr;
     k_shard_parse<<<ntiles, 256, 0, st>>>(hdr, len, ts, n, G, scratch, ntiles, r, use, wide, verdict, own8, cr,
                                           owner_total);
-    k_shard_scan<<<1, 1024, 0, st>>>(scratch, n, owner_total, G, ntiles, compact);
+    k_shard_scan<<<G, 1024, 0, st>>>(scratch, owner_total, G, ntiles, compact);
     if (compact)
         k_shard_pack16<<<ntiles, 256, 0, st>>>(own8, cr, n, G, scratch, ntiles,
                                                reinterpret_cast<ShardRecord16 *>(rec), send_idx, owner_total);

@@ -8,7 +8,7 @@ import time
 
 import torch
 
-sys.path.insert(0, ".")
+sys.path.insert(0, str(__import__("pathlib").Path(__file__).resolve().parents[1]))
 from flowsentryx_amd import lib, synth  # noqa: E402
 from flowsentryx_amd.shard import HipShardEngine  # noqa: E402
 
