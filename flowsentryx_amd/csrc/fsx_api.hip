@@ -171,7 +171,7 @@ static uint64_t next_pow2(uint64_t x) {
 static void free_scratch(fsx_ctx *c) {
     Scratch &s = c->sc;
     hipFree(s.packed[0]); hipFree(s.packed[1]); hipFree(s.pay[0]); hipFree(s.pay[1]); hipFree(s.marks); hipFree(s.headf);
-    hipFree(s.seg_start); hipFree(s.seg_slot); hipFree(s.hist);
+    hipFree(s.seg_start); hipFree(s.seg_slot); hipFree(s.seg_lo); hipFree(s.seg_len); hipFree(s.hist);
     hipFree(s.tile_aux); hipFree(s.tile_last); hipFree(s.id_tab);
     hipFree(s.seg_order); hipFree(s.sub_cnt); hipFree(s.flow_first); hipFree(s.flow_last);
     hipFree(s.span_list); hipFree(s.sort_ctl); hipFree(s.gbase); hipFree(s.status);
@@ -193,6 +193,8 @@ static int alloc_scratch(fsx_ctx *c, uint64_t cap) {
     HIPCHK(c, hipMalloc(&s.headf, cap + 16));
     HIPCHK(c, hipMalloc(&s.seg_start, (cap + 1) * 4));
     HIPCHK(c, hipMalloc(&s.seg_slot, cap * 4));
+    HIPCHK(c, hipMalloc(&s.seg_lo, (cap + 1) * 4));
+    HIPCHK(c, hipMalloc(&s.seg_len, (cap + 1) * 4));
     HIPCHK(c, hipMalloc(&s.hist, 256ull * std::max<uint64_t>(kSortMaxBlocks, cap / kSortTile + 2) * 4));
     HIPCHK(c, hipMalloc(&s.tile_aux, ntiles * 4));
     HIPCHK(c, hipMalloc(&s.tile_last, ntiles));

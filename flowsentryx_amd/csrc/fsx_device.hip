@@ -1156,7 +1156,7 @@ __global__ __launch_bounds__(256) void k_heads_write(BatchState *bs, const uint8
                                                      uint32_t *__restrict__ seg_start,
                                                      const uint64_t *__restrict__ S,
                                                      uint32_t *__restrict__ seg_slot, uint64_t id_mask,
-                                                     uint32_t light_only) {
+                                                     uint32_t light_only, uint32_t *__restrict__ seg_lo) {
     __shared__ uint32_t s_tmp[4];
     const uint32_t M = light_only ? bs->n_light : bs->n_valid;
     const uint32_t ntiles = (M + kTile - 1) / kTile;
@@ -1177,7 +1177,9 @@ __global__ __launch_bounds__(256) void k_heads_write(BatchState *bs, const uint8
         for (int k = 0; k < 16; ++k) {
             if ((f[k >> 2] >> (8 * (k & 3))) & 1u) {
                 seg_start[off] = p0 + k;
-                if (seg_slot) seg_slot[off] = pk_id(S[p0 + k], id_mask);   // id = table slot
+                const uint64_t v = S[p0 + k];
+                if (seg_slot) seg_slot[off] = pk_id(v, id_mask);   // id = table slot
+                if (seg_lo) seg_lo[off] = (uint32_t)v;
                 ++off;
             }
         }
@@ -1191,7 +1193,8 @@ __global__ __launch_bounds__(256) void k_heads_heavy(BatchState *bs, const uint3
                                                      const uint32_t *__restrict__ base0,
                                                      uint32_t *__restrict__ seg_start,
                                                      uint32_t *__restrict__ seg_slot,
-                                                     const uint64_t *__restrict__ S, uint64_t id_mask) {
+                                                     const uint64_t *__restrict__ S, uint64_t id_mask,
+                                                     uint32_t *__restrict__ seg_lo) {
     __shared__ uint32_t s_tmp[4];
     const uint32_t h = threadIdx.x;
     const uint32_t L = bs->nseg;   // light segments (k_scan_tiles_u32); read before the barrier
@@ -1202,6 +1205,7 @@ __global__ __launch_bounds__(256) void k_heads_heavy(BatchState *bs, const uint3
         const uint32_t a = base0[kHeavyMax + h];
         seg_start[L + r] = a;
         if (seg_slot) seg_slot[L + r] = pk_id(S[a], id_mask);
+        if (seg_lo) seg_lo[L + r] = (uint32_t)S[a];
     }
     if (h == 0) {
         bs->nseg_light = L;
@@ -2122,11 +2126,13 @@ hipError_t launch_tail(const TailArgs &a) {
     k_heads_count<<<gridTiles, 256, 0, st>>>(S, bs, in.hdr, sc.headf, sc.tile_aux, sc.sub_cnt, lo);
     mark("k_heads_count");
     k_scan_tiles_u32<<<1, 256, 0, st>>>(sc.tile_aux, bs, sc.seg_start, lo);
+    // (the first sort word's low half per segment only for the flow rows)
+    uint32_t *seg_lo = flows && !in.rec ? sc.seg_lo : nullptr;
     k_heads_write<<<gridTiles, 256, 0, st>>>(bs, sc.headf, sc.tile_aux, sc.seg_start, S,
-                                             do_limit ? sc.seg_slot : nullptr, lim.table_mask, lo);
+                                             do_limit ? sc.seg_slot : nullptr, lim.table_mask, lo, seg_lo);
     if (tagh)
         k_heads_heavy<<<1, 256, 0, st>>>(bs, sc.sort_ctl, sc.gbase, sc.seg_start, do_limit ? sc.seg_slot : nullptr,
-                                         S, lim.table_mask);
+                                         S, lim.table_mask, seg_lo);
     mark("k_heads_write");
     if (flows) {
         hipStream_t fs = st;
@@ -2140,7 +2146,7 @@ hipError_t launch_tail(const TailArgs &a) {
                               sc.flow_first, sc.flow_last, sc.span_list, flows->acc, flows->keys16,
                               flows->fam, flows->feat, flows->prob, flows->dec, flows->cap, flows->score,
                               lim.salt32, n, do_limit ? flows->sacc : nullptr, flows->epoch, sc.seg_slot,
-                              tagh, fs)) != hipSuccess)
+                              tagh, seg_lo, seg_lo ? sc.seg_len : nullptr, fs)) != hipSuccess)
             return e;
         if (tagh) {   // the heavy sources' rows, from their sums (k_flow_heavy)
             if (hf != fs && (e = hipStreamWaitEvent(fs, heavy_flow_ev, 0)) != hipSuccess) return e;

@@ -80,6 +80,10 @@ struct FlowOut {
     uint32_t epoch;
     const uint32_t *seg_slot;  // table slot of each source (accumulate mode)
     const uint64_t *ts;        // arrival timestamps (first / last packet of a source)
+    // per source (may be null): low word of its first sort word (k_heads_write) and its first
+    // frame length (k_flow_tile), so k_flow_finish gathers only the first header record
+    const uint32_t *seg_lo;
+    uint32_t *seg_len;
 };
 
 // L4 destination port of the source's first packet (oracle fsxo_dst_port).
@@ -116,7 +120,7 @@ __device__ __forceinline__ void flow_finish(uint32_t g, const FlowAcc &a, const 
                             uint32_t salt, const FlowOut &out, const ScoreParams &P) {
     if (g >= out.cap) return;
     const uint32_t p0 = seg_start[g];
-    const uint64_t v = S[p0];
+    const uint64_t v = out.seg_lo ? (uint64_t)out.seg_lo[g] : S[p0];   // (family, arrival index)
     uint32_t k[4];
     const uint32_t idx = pk_idx(v);
     uint32_t tag, dport;
@@ -126,7 +130,7 @@ __device__ __forceinline__ void flow_finish(uint32_t g, const FlowAcc &a, const 
         tag = rec_read(in.rec, in.rec_bytes, idx, k, L, T, dport);
     } else {
         tag = key_of(v, in.hdr, salt, k);
-        dport = dst_port(in.hdr + (size_t)idx * 64, len[idx]);
+        dport = dst_port(in.hdr + (size_t)idx * 64, out.seg_len ? out.seg_len[g] : len[idx]);
     }
     if (out.sacc) {
         SlotAcc &m = out.sacc[out.seg_slot[g]];

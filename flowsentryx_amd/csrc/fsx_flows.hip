@@ -123,6 +123,7 @@ __device__ __forceinline__ void flow_tiles(const uint64_t *__restrict__ S,
                 if (h) {
                     if (seen == 0) F = A;
                     else acc_store(out, g + seen - 1, A);
+                    if (out.seg_len && g + seen < out.cap) out.seg_len[g + seen] = Lk;   // its first frame
                     ++seen;
                     A = acc_zero();
                 }
@@ -258,9 +259,10 @@ hipError_t launch_flows(const uint64_t *S, const uint64_t *pay, BatchState *bs, 
                         uint32_t *span_list, void *acc, uint8_t *keys16, uint8_t *fam, float *feat,
                         float *prob, uint8_t *dec, uint32_t cap, const ScoreParams &P, uint32_t salt,
                         uint32_t n, void *sacc, uint32_t epoch, const uint32_t *seg_slot, bool light_only,
-                        hipStream_t st) {
+                        const uint32_t *seg_lo, uint32_t *seg_len, hipStream_t st) {
     (void)hipGetLastError();   // a stale error of another caller is not ours
-    const FlowOut out{(FlowAcc *)acc, keys16, fam, feat, prob, dec, cap, (SlotAcc *)sacc, epoch, seg_slot, ts};
+    const FlowOut out{(FlowAcc *)acc, keys16, fam, feat, prob, dec, cap, (SlotAcc *)sacc, epoch, seg_slot, ts,
+                      seg_lo, seg_len};
     const uint32_t nsub = (n + kFT - 1) / kFT;
     const uint32_t grid = std::max<uint32_t>(1, std::min<uint32_t>(FSX_FLOW_TILE_BLOCKS, (nsub + 3) / 4));
     k_flow_tile<<<grid, 256, 0, st>>>(S, pay, bs, headf, len, ts, in, tile_off, sub_cnt, seg_start,
@@ -425,7 +427,8 @@ hipError_t launch_flows_heavy_finish(const uint64_t *S, const BatchState *bs, co
                                      const uint32_t *seg_slot, hipStream_t st) {
     (void)hipGetLastError();
     const FlowAcc *hacc = reinterpret_cast<const FlowAcc *>(scratch) + (cap / kHeavyChunk + kHeavyMax + 1);
-    const FlowOut out{nullptr, keys16, fam, feat, prob, dec, rows_cap, (SlotAcc *)sacc, epoch, seg_slot, ts};
+    const FlowOut out{nullptr, keys16, fam, feat, prob, dec, rows_cap, (SlotAcc *)sacc, epoch, seg_slot, ts,
+                      nullptr, nullptr};
     k_flow_heavy_finish<<<1, 256, 0, st>>>(S, bs, cnt0, seg_start, hacc, in, len, out, P, salt);
     return hipGetLastError();
 }

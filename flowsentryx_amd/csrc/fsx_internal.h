@@ -279,6 +279,8 @@ struct Scratch {
     uint8_t *headf;        // per sorted position: segment-head flag
     uint32_t *seg_start;   // nseg + 1
     uint32_t *seg_slot;
+    uint32_t *seg_lo;      // per segment: low word of its first sort word (family, arrival index)
+    uint32_t *seg_len;     // per light segment: frame length of its first packet (flow tiles)
     uint32_t *hist;        // sort: per-tile digit counts [256][cap/kSortTile+2]; walker classes
     uint32_t *tile_aux;    // per kTile tile
     uint8_t *tile_last;
@@ -430,7 +432,7 @@ hipError_t launch_flows(const uint64_t *S, const uint64_t *pay, BatchState *bs, 
                         uint32_t *span_list, void *acc, uint8_t *keys16, uint8_t *fam, float *feat,
                         float *prob, uint8_t *dec, uint32_t cap, const ScoreParams &P, uint32_t salt,
                         uint32_t n, void *sacc, uint32_t epoch, const uint32_t *seg_slot, bool light_only,
-                        hipStream_t st);
+                        const uint32_t *seg_lo, uint32_t *seg_len, hipStream_t st);
 // Heavy verdict lists: the heavy sources' flow sums right after sort pass 0, their rows
 // after the heads (fsx_flows.hip "heavy sources"); scratch of heavy_flow_bytes(cap).
 size_t heavy_flow_bytes(uint64_t cap);
