@@ -77,6 +77,18 @@ __device__ __forceinline__ uint32_t wave_incl_max(uint32_t x) {
     return x;
 }
 
+// XCD-aware tile order (cdna_hip_programming.md §5.5 T1, bijective form): blocks are dealt
+// round-robin over the 8 XCDs, so block b gets tile (b % 8)'s contiguous share — consecutive
+// tiles (whose output runs meet in the same cache lines) land in one XCD's L2. Speed only.
+#ifndef FSX_XCD_SWIZZLE
+#define FSX_XCD_SWIZZLE 1   // (A/B: scripts/build_variant.sh)
+#endif
+__device__ __forceinline__ uint32_t xcd_swizzle(uint32_t b, uint32_t nwg) {
+    if (!FSX_XCD_SWIZZLE || nwg <= 8u) return b;
+    const uint32_t q = nwg >> 3, r = nwg & 7u, x = b & 7u;
+    return (x < r ? x * (q + 1u) : r * (q + 1u) + (x - r) * q) + (b >> 3);
+}
+
 __device__ __forceinline__ uint64_t match_digit(uint32_t d, uint64_t active) {
     uint64_t peers = active;
 #pragma unroll

@@ -992,9 +992,10 @@ __global__ __launch_bounds__(256, kLatePay ? FSX_SCATTER_MINB : 1) void k_tile_s
                                                       const uint64_t *__restrict__ ts,
                                                       const uint32_t *__restrict__ len) {
     const uint32_t L = L_dev ? *L_dev : L_host;
-    if (blockIdx.x * kSortTile >= L) return;
-    sort_tile<kLatePay>(blockIdx.x, in, out, L, shift, dmask, first, bs, pin, pout, ts, len,
-                        TileOffs{offs, tcap, blockIdx.x});
+    const uint32_t nact = (L + kSortTile - 1) / kSortTile;   // tiles of this pass
+    if (blockIdx.x >= nact) return;
+    const uint32_t t = xcd_swizzle(blockIdx.x, nact);
+    sort_tile<kLatePay>(t, in, out, L, shift, dmask, first, bs, pin, pout, ts, len, TileOffs{offs, tcap, t});
 }
 
 // ---- onesweep variant (FSX_FLAG_ONESWEEP_SORT): per-digit decoupled look-back.
