@@ -787,8 +787,10 @@ __global__ __launch_bounds__(256) void k_tile_hist(const uint64_t *__restrict__ 
     __shared__ uint32_t sh[4][256];
     const uint32_t tid = threadIdx.x, w = tid >> 6;
     const uint32_t L = L_dev ? *L_dev : L_host;
-    const uint32_t t = blockIdx.x;
-    if (t * kSortTile >= L) return;
+    const uint32_t nact = (L + kSortTile - 1) / kSortTile;   // tiles of this pass
+    if (blockIdx.x >= nact) return;
+    // (XCD-aware order: neighbouring tiles' counts share the lines of each digit row)
+    const uint32_t t = xcd_swizzle(blockIdx.x, nact);
 #pragma unroll
     for (int k = 0; k < 4; ++k) sh[k][tid] = 0;
     __syncthreads();
@@ -1161,7 +1163,9 @@ __global__ __launch_bounds__(256) void k_heads_write(BatchState *bs, const uint8
     __shared__ uint32_t s_tmp[4];
     const uint32_t M = light_only ? bs->n_light : bs->n_valid;
     const uint32_t ntiles = (M + kTile - 1) / kTile;
-    for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    for (uint32_t b = blockIdx.x; b < ntiles; b += gridDim.x) {
+        // XCD-aware order: the compacted runs of neighbouring tiles share cache lines
+        const uint32_t t = xcd_swizzle(b, ntiles);
         const uint32_t p0 = t * kTile + threadIdx.x * 16u;
         uint32_t f[4] = {0, 0, 0, 0};
         if (p0 + 16 <= M) {
