@@ -2315,10 +2315,17 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
     // like the light flow tiles cover [0, n_light) only (k_heads_heavy appends the heavy
     // segments).
     static const bool no_fork = getenv("FSX_NO_FLOW_FORK") != nullptr;   // A/B: flows serialized
-    // pipelined: the previous batch's tail goes in right after this parse (it overlaps the sort;
-    // A/B: FSX_TAIL_AFTER_PASS0=1 after the first sort pass)
-    static const bool tail_p0 = getenv("FSX_TAIL_AFTER_PASS0") != nullptr;
-    if (split && split->on_parse && !tail_p0 && (e = split->on_parse(split->cb)) != hipSuccess) return e;
+    // pipelined: the previous batch's tail goes in right after this batch's parse, so it
+    // overlaps the sort (A/B, FSX_TAIL_AT: 0 after the parse (default), 1 after the first
+    // pass's offsets scan (same time: 3.46 ms), 2 after the first scatter (3.77 ms))
+    static const int tail_at = getenv("FSX_TAIL_AT") ? atoi(getenv("FSX_TAIL_AT")) : 0;
+    bool hooked = false;   // (exactly once per pipelined batch: a tail left unhooked would be lost)
+    auto tail_hook = [&](int at) -> hipError_t {
+        if (hooked || !split || !split->on_parse || (at != tail_at && at != 3)) return hipSuccess;
+        hooked = true;
+        return split->on_parse(split->cb);
+    };
+    if ((e = tail_hook(0)) != hipSuccess) return e;
     k_hist_prep<<<1, 256, 0, st>>>(sc.sort_ctl, sc.gbase, bs, heavy_sort ? dp.light_b : 256u);
     if (do_limit) k_batch_check<<<1, 1, 0, st>>>(bs, tstate, lim, split ? split->prev : nullptr);
     const uint32_t gen0 = onesweep ? next_generation() : 0u;
@@ -2345,13 +2352,14 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
             }
             k_tile_scan<<<pmask + 1, 256, 0, st>>>(sc.hist, tcap, n, Ld, sc.gbase + 256 * pass);
             mark("k_tile_scan");
+            if (pass == 0 && (e = tail_hook(1)) != hipSuccess) return e;
             k_tile_scatter<kLatePayDefault><<<ntiles, 256, 0, st>>>(in, out, n, Ld, shift, pmask, pass == 0, sc.hist, tcap, bs,
                                                    pin, pout, ts, len);
             mark("k_tile_scatter");
-            if (pass == 0 && tail_p0 && split && split->on_parse && (e = split->on_parse(split->cb)) != hipSuccess)
-                return e;
+            if (pass == 0 && (e = tail_hook(2)) != hipSuccess) return e;
         }
     }
+    if ((e = tail_hook(3)) != hipSuccess) return e;   // (any position not reached: onesweep)
     if (split && split->front_done) {   // pipelined: the front is done; the tail is handed back
         if ((e = hipEventRecord(split->front_done, st)) != hipSuccess) return e;
     }
