@@ -97,8 +97,8 @@ def parse_args():
                     help="config-4 packets per rank (default: 1/8 of the 1B-packet stream)")
     ap.add_argument("--leg-timing", action="store_true",
                     help="per-kernel device times of the config-4 / config-5 legs (extra steps)")
-    ap.add_argument("--config5-oracle", action="store_true",
-                    help="also check the full config-5 leg against the sharded oracle (slow)")
+    ap.add_argument("--no-config5-oracle", action="store_true",
+                    help="skip the full-size config-5 comparison with the sharded oracle")
     return ap.parse_args()
 
 
@@ -835,7 +835,7 @@ def config5_leg(args, torch, np, lib, synth, local, cores):
            "check": check}
     if kern:
         leg["timing"] = kern
-    if args.config5_oracle:
+    if not args.no_config5_oracle and not args.no_check:
         from oracle import pyoracle
         hdr, ln, ts = host_inputs(d, n)
         orc = pyoracle.ShardedOracle(cores, max_entries=max_entries)
