@@ -34,6 +34,7 @@ Prints ONE JSON line on rank 0 with the driver's contract plus:
 from __future__ import annotations
 
 import argparse
+import contextlib
 import json
 import math
 import os
@@ -84,6 +85,9 @@ def parse_args():
                     help="limiter of the timed main loop (diagnostics; the headline is fixed)")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="headline stream without batch pipelining (diagnostics)")
+    ap.add_argument("--ts-ring", type=int, default=0,
+                    help="streaming headline: keep at most this many per-batch timestamp arrays "
+                         "(refilled in the step; >= 6; 0 = all of them up to 30%% of device memory)")
     ap.add_argument("--cold", action="store_true",
                     help="headline: every step the same batch from empty maps (fsx_reset inside "
                          "the step) instead of consecutive batches with the maps carried")
@@ -284,18 +288,35 @@ def main():
                 eng.enable_flows(fcap)
             plane = ShardedDataPlane(eng)
         ntime = max(1, min(steps, args.kernel_timing_steps)) if kernel_timing and args.kernel_timing_steps else 0
+        rs = None
         if stream:
             dur = int(p.duration_ns)
-            tss = [d["ts"] + k * dur for k in range(warmup + steps + ntime)]
+            total = warmup + steps + ntime
+            # one timestamp array per batch; beyond 30 % of the device memory a ring of them,
+            # each refilled (base + k x duration, one elementwise kernel in the step) on the
+            # context's stream once the batch that used it has completed (>= 6 back)
+            budget = int(0.3 * torch.cuda.get_device_properties(local).total_memory)
+            R = total if total * n * 8 <= budget else max(6, budget // (n * 8))
+            if args.ts_ring:
+                R = min(R, max(6, args.ts_ring))
+            tss = [d["ts"] + k * dur for k in range(min(R, total))]
+            held = list(range(len(tss)))   # the batch each array currently holds
             vb = [d["v"], torch.empty_like(d["v"])]
             torch.cuda.synchronize()   # (torch's kernels are not ordered with the library's streams)
+            if R < total and world == 1:
+                rs = torch.cuda.Stream()
+                ctx.set_stream(rs.cuda_stream)
             if world == 1 and pipelined:
                 ctx.set_pipeline(True)
         else:
-            tss, vb = [d["ts"]], [d["v"]]
+            tss, vb, held = [d["ts"]], [d["v"]], [0]
 
         def step(k, feat=False, v=None):
-            ts_k = tss[k if stream else 0]
+            if stream and held[k % len(tss)] != k:   # ring: refill this batch's timestamps in order
+                with torch.cuda.stream(rs) if rs is not None else contextlib.nullcontext():
+                    torch.add(d["ts"], k * dur, out=tss[k % len(tss)])
+                held[k % len(tss)] = k
+            ts_k = tss[k % len(tss) if stream else 0]
             v = vb[k % len(vb)] if v is None else v
             if not stream and not args.no_reset:
                 ctx.reset()
@@ -372,7 +393,7 @@ def main():
             orc = pyoracle.ShardedOracle(cores, max_entries=max_entries)
             ok = True
             for k in range(nb):
-                ts_k = tss[k].cpu().numpy().view(np.uint64)
+                ts_k = tss[k % len(tss)].cpu().numpy().view(np.uint64)
                 c0 = time.perf_counter()
                 vo = orc.batch(hdr, ln, ts_k)
                 if k == 0:   # the CPU baseline: one batch from empty maps
