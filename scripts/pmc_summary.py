@@ -13,6 +13,7 @@ from pathlib import Path
 
 def short_name(k):
     """'void fsx::k_tile_scatter<true>(unsigned long const*, ...)' -> 'k_tile_scatter'."""
+    k = k.replace("(anonymous namespace)::", "")
     k = k.split("(")[0].replace("void ", "").strip()
     k = re.sub(r"<.*>", "", k)
     return k.split("::")[-1]
