@@ -21,7 +21,10 @@ constexpr uint32_t kNoSlot = 0xFFFFFFFFu;
 
 // Radix sort geometry: 8-bit digits, 256-thread blocks, 16 items/thread tiles.
 constexpr int kSortThreads = 256;
-constexpr int kSortItems = 16;
+#ifndef FSX_SORT_ITEMS
+#define FSX_SORT_ITEMS 16   // keys per thread of a sort tile (A/B: scripts/build_variant.sh)
+#endif
+constexpr int kSortItems = FSX_SORT_ITEMS;
 constexpr int kSortTile = kSortThreads * kSortItems;  // 4096
 constexpr int kSortMaxBlocks = 2048;
 constexpr int kTile = 4096;                            // fill / compaction tile
