@@ -529,19 +529,30 @@ int fsx_set_pipeline(fsx_ctx *c, int on) {
     if (rc) return rc;
     for (int fs = 1; on && fs < fsx_ctx::kSets; ++fs) {
         if (c->fb[fs].bs) continue;
-        fsx_ctx::FrontBufs &f = c->fb[fs];
+        // built in a temporary set and committed only when every allocation succeeded (bs,
+        // allocated last, marks a set as present); a partial set is freed
+        fsx_ctx::FrontBufs f{};
         const uint64_t cap = c->sc.cap;
-        for (int b = 0; b < 2; ++b) {
-            HIPCHK(c, hipMalloc(&f.packed[b], cap * 8));
-            HIPCHK(c, hipMalloc(&f.pay[b], cap * 8));
+        auto build = [&]() -> hipError_t {
+            hipError_t e;
+            for (int b = 0; b < 2; ++b) {
+                if ((e = hipMalloc(&f.packed[b], cap * 8)) != hipSuccess) return e;
+                if ((e = hipMalloc(&f.pay[b], cap * 8)) != hipSuccess) return e;
+            }
+            if ((e = hipMalloc(&f.hist, 256ull * std::max<uint64_t>(kSortMaxBlocks, cap / kSortTile + 2) * 4)) != hipSuccess) return e;
+            if ((e = hipMalloc(&f.sort_ctl, kSortCtlWords * 4)) != hipSuccess) return e;
+            if ((e = hipMalloc(&f.gbase, 1024 * 4)) != hipSuccess) return e;
+            if ((e = hipMalloc(&f.heavy, sizeof(HeavySet))) != hipSuccess) return e;
+            if ((e = hipMemset(f.heavy, 0, sizeof(HeavySet))) != hipSuccess) return e;
+            if ((e = hipMalloc(&f.bs, sizeof(BatchState))) != hipSuccess) return e;
+            return hipMemset(f.bs, 0, sizeof(BatchState));
+        };
+        const hipError_t be = build();
+        if (be != hipSuccess) {
+            free_front(f);
+            return set_err(c, -ENOMEM, "pipeline buffers: %s", hipGetErrorString(be));
         }
-        HIPCHK(c, hipMalloc(&f.hist, 256ull * std::max<uint64_t>(kSortMaxBlocks, cap / kSortTile + 2) * 4));
-        HIPCHK(c, hipMalloc(&f.sort_ctl, kSortCtlWords * 4));
-        HIPCHK(c, hipMalloc(&f.gbase, 1024 * 4));
-        HIPCHK(c, hipMalloc(&f.heavy, sizeof(HeavySet)));
-        HIPCHK(c, hipMemset(f.heavy, 0, sizeof(HeavySet)));
-        HIPCHK(c, hipMalloc(&f.bs, sizeof(BatchState)));
-        HIPCHK(c, hipMemset(f.bs, 0, sizeof(BatchState)));
+        c->fb[fs] = f;
         for (int p = 0; p < fsx_ctx::kSets; ++p)
             if (!c->tail_done[p]) HIPCHK(c, hipEventCreateWithFlags(&c->tail_done[p], hipEventDisableTiming));
         if (!c->front_done) HIPCHK(c, hipEventCreateWithFlags(&c->front_done, hipEventDisableTiming));
@@ -741,6 +752,7 @@ static int run_pipelined(fsx_ctx *c, const PacketIn &in, const uint32_t *d_len, 
     }
     // the batch before this one (still in flight: its failure cancels this one)
     const BatchState *prev = c->fl_on[c->par] ? c->fb[c->par].bs : nullptr;
+    const int old_par = c->par;
     use_front(c, q);
     c->par = q;
     if (++c->id_gen == 0x10000u) {
@@ -754,7 +766,13 @@ static int run_pipelined(fsx_ctx *c, const PacketIn &in, const uint32_t *d_len, 
                                            c->stream, fork_flows() ? c->aux_stream : nullptr, c->fork_ev,
                                            c->join_ev, split ? nullptr : c->walk_stream, c->walk_fork_ev,
                                            c->walk_join_ev, c->heavy_fork_ev, c->heavy_flow_ev, nullptr, &sp);
-    if (e != hipSuccess) return set_err(c, -EIO, "pipeline launch: %s", hipGetErrorString(e));
+    if (e != hipSuccess) {
+        // nothing of this batch is in flight: back to the previous set, so the pending tail and
+        // the next sel() still refer to the batch that owns them
+        use_front(c, old_par);
+        c->par = old_par;
+        return set_err(c, -EIO, "pipeline launch: %s", hipGetErrorString(e));
+    }
     c->fl_on[q] = true;
     c->fl_born[q] = c->id_gen;
     if (split) {
@@ -820,7 +838,11 @@ static int run_batch(fsx_ctx *c, const PacketIn &in, const uint32_t *d_len, cons
 static FlowRequest flow_slots(fsx_ctx *c, const FlowRequest *fr, size_t n, int *rc) {
     FlowRequest frq = *fr;
     *rc = 0;
-    const uint64_t need = std::max<uint64_t>(1, std::min<uint64_t>(frq.cap, n));
+    // accumulate mode (fsx_flows_begin .. fsx_flows_end): every source of the call must merge
+    // into its SlotAcc, so the scratch covers all n packets' sources; the row cap applies in
+    // fsx_flows_end only
+    const uint64_t need = frq.sacc ? std::max<uint64_t>(1, n)
+                                   : std::max<uint64_t>(1, std::min<uint64_t>(frq.cap, n));
     if (need > c->flow_acc_cap) {
         if (busy(c) && (*rc = fsx_sync(c))) return frq;   // the old accumulators may be in use
         hipFree(c->d_flow_acc);
@@ -833,7 +855,7 @@ static FlowRequest flow_slots(fsx_ctx *c, const FlowRequest *fr, size_t n, int *
         c->flow_acc_cap = need;
     }
     frq.acc = c->d_flow_acc;
-    frq.cap = (uint32_t)std::min<uint64_t>(frq.cap, c->flow_acc_cap);
+    frq.cap = frq.sacc ? (uint32_t)need : (uint32_t)std::min<uint64_t>(frq.cap, c->flow_acc_cap);
     return frq;
 }
 

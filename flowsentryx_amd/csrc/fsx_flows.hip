@@ -436,8 +436,9 @@ hipError_t launch_flows_heavy_finish(const uint64_t *S, const BatchState *bs, co
 size_t flow_acc_bytes() { return sizeof(FlowAcc); }
 size_t slot_acc_bytes() { return sizeof(SlotAcc); }
 
-// The rows of an accumulation epoch: every slot merged in it, in slot order of arrival at
-// the row counter (rows unordered), features + score from the carried sums.
+// The rows of an accumulation epoch: every live slot merged in it, features + score from the
+// carried sums. Rows are unordered (a row counter): when cap < rows, which rows are kept is
+// unspecified (include/fsx_hip.h fsx_flows_end).
 __global__ __launch_bounds__(256) void k_flows_end(const SlotAcc *__restrict__ sacc, uint32_t epoch,
                                                    const Slot *__restrict__ table, uint64_t slots,
                                                    FlowOut out, ScoreParams P,
@@ -445,6 +446,7 @@ __global__ __launch_bounds__(256) void k_flows_end(const SlotAcc *__restrict__ s
     for (uint64_t s = (uint64_t)blockIdx.x * 256u + threadIdx.x; s < slots; s += (uint64_t)gridDim.x * 256u) {
         const SlotAcc &m = sacc[s];
         if (m.epoch != epoch) continue;
+        if (table[s].tag == 0) continue;   // emptied by a rolled-back sub-batch
         const unsigned long long g = atomicAdd(count, 1ull);
         if (g >= out.cap) continue;
         FlowAcc a = acc_zero();

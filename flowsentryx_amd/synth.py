@@ -46,6 +46,12 @@ def config_params(config: int, n: int | None = None) -> tuple[SynthParams, float
         p.n, p.n_ips, p.duration_ns, p.mode = 1 << 20, 1024, 5_000_000_000, SYNTH_ZIPF_V4
     elif config == 2:
         p.n, p.n_ips, p.duration_ns, p.mode = 64 << 20, 1 << 20, 30_000_000_000, SYNTH_ZIPF_V4
+    elif config == 3:
+        # features + scores of 4M per-IP flows extracted from a packet stream (SURVEY §8 d
+        # config 3): 64M packets from 4M sources drawn uniformly (Zipf exponent 0), so every
+        # source is seen (16 packets per source on average)
+        p.n, p.n_ips, p.duration_ns, p.mode = 64 << 20, 4 << 20, 30_000_000_000, SYNTH_ZIPF_V4
+        zipf_s = 0.0
     elif config == 4:
         p.n, p.n_ips, p.duration_ns, p.mode = 1 << 30, 16 << 20, 120_000_000_000, SYNTH_ZIPF_V4
     elif config == 5:

@@ -241,7 +241,9 @@ int fsx_score_device(fsx_ctx *ctx, const float *d_features, size_t n, float *d_p
  * merges its per-source sums into the source's running sums (table slot) instead of writing
  * rows (its keys/family/feature/score pointers may be NULL); fsx_flows_end writes one row
  * per source merged since fsx_flows_begin — exactly the row one call over the whole batch
- * would give — and the row count to *d_rows (device pointer; NULL: none). Asynchronous. */
+ * would give — and the row count to *d_rows (device pointer; NULL: none). Asynchronous.
+ * Rows are in no particular order; with cap < rows, which rows are written is unspecified
+ * (*d_rows still counts all of them). The calls' own flow_cap does not limit the merge. */
 int fsx_flows_begin(fsx_ctx *ctx);
 int fsx_flows_end(fsx_ctx *ctx, uint8_t *d_keys16, uint8_t *d_family, float *d_features,
                   float *d_prob, uint8_t *d_malicious, size_t cap, uint64_t *d_rows);
