@@ -22,6 +22,8 @@
 #include "fsx_dev_common.h"
 #include "fsx_internal.h"
 #include "fsx_seg.h"
+#include "fsx_walk.h"
+#include "fsx_bins.h"
 #include "fsx_shard.h"
 
 #define XDP_DROP 1
@@ -197,11 +199,17 @@ __device__ __forceinline__ uint32_t packet_src(const PacketIn &in, const uint32_
     return parse_src(len[i], d[3], d[5], d[6], d[7], d[8], d[9], k, v);
 }
 
+// Second sketch hash of a source (independent bits of its 64-bit table hash): two heavy
+// sources that share a bucket of the first sketch rarely share one of the second.
+__device__ __forceinline__ uint32_t sketch2_of(uint32_t tag, const uint32_t k[4], uint64_t seed) {
+    return (uint32_t)(slot_hash(tag, k, seed) >> 40) & (kSketch - 1);
+}
+
 __global__ __launch_bounds__(256) void k_heavy_sample(PacketIn in, const uint32_t *__restrict__ len,
                                                       uint32_t n, uint32_t *__restrict__ sketch,
                                                       uint64_t seed, uint64_t mask, uint32_t test_flags) {
-    __shared__ uint32_t s_cnt[kSketch], s_cand[kSketch];
-    for (uint32_t c = threadIdx.x; c < kSketch; c += 256) s_cnt[c] = 0;
+    __shared__ uint32_t s_cnt[2][kSketch], s_cand[2][kSketch];
+    for (uint32_t c = threadIdx.x; c < kSketch; c += 256) s_cnt[0][c] = s_cnt[1][c] = 0;
     __syncthreads();
     const uint32_t S = n < kHeavySample ? n : kHeavySample;
     const uint32_t per = (S + gridDim.x - 1) / gridDim.x;
@@ -212,21 +220,67 @@ __global__ __launch_bounds__(256) void k_heavy_sample(PacketIn in, const uint32_
         const uint32_t tag = packet_src(in, len, i, k);
         if (!tag) continue;
         const uint32_t h = (uint32_t)probe_start(tag, k, seed, mask, test_flags) & (kSketch - 1);
-        atomicAdd(&s_cnt[h], 1u);
-        s_cand[h] = i;
+        const uint32_t h2 = sketch2_of(tag, k, seed);
+        atomicAdd(&s_cnt[0][h], 1u);
+        s_cand[0][h] = i;
+        atomicAdd(&s_cnt[1][h2], 1u);
+        s_cand[1][h2] = i;
     }
     __syncthreads();
     for (uint32_t c = threadIdx.x; c < kSketch; c += 256) {
-        const uint32_t x = s_cnt[c];
-        if (x >= 2) {
-            atomicAdd(&sketch[c], x);
-            sketch[kSketch + c] = s_cand[c];
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            const uint32_t x = s_cnt[s][c];
+            if (x >= 2) {
+                atomicAdd(&sketch[2 * s * kSketch + c], x);
+                sketch[(2 * s + 1) * kSketch + c] = s_cand[s][c];
+            }
         }
     }
 }
 
-// One block: the (at most nmax) sketch buckets of highest count >= floor become the heavy
-// set: their candidates' keys and an open-addressing map of them. Zeroes the counts.
+// Block-wide selection of at most nmax values (the largest, by log2 bins: every value of
+// the bins above the cut bin, then values of the bin below it while room is left) among
+// the threads' candidates x[0..4) (0: none). sel[k]: candidate k selected.
+template <int kPer>
+__device__ __forceinline__ void select_top(const uint32_t (&x)[kPer], uint32_t nmax, bool (&sel)[kPer],
+                                           uint32_t *s_bin, uint32_t *s_scal) {
+    const uint32_t tid = threadIdx.x;
+    if (tid < 32) s_bin[tid] = 0;
+    if (tid == 0) s_scal[2] = 0;
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kPer; ++k)
+        if (x[k]) atomicAdd(&s_bin[31 - __clz((int)x[k])], 1u);
+    __syncthreads();
+    if (tid == 0) {
+        uint32_t acc = 0, B = 32;
+        for (int b = 31; b >= 0; --b) {
+            if (acc + s_bin[b] > nmax) break;
+            acc += s_bin[b];
+            B = (uint32_t)b;
+        }
+        s_scal[0] = B;
+        s_scal[1] = nmax - acc;
+    }
+    __syncthreads();
+    const uint32_t cut = s_scal[0], room = s_scal[1];
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+        sel[k] = false;
+        if (!x[k]) continue;
+        const uint32_t b = 31u - (uint32_t)__clz((int)x[k]);
+        sel[k] = b >= cut || (b + 1 == cut && atomicAdd(&s_scal[2], 1u) < room);
+    }
+    __syncthreads();
+}
+
+// One block: the heavy set of the batch from the two sketches. Candidates: the sampled
+// source of each of the (at most 2 nmax) buckets of highest count >= floor per sketch; a
+// candidate's estimate is the smaller of its two buckets' counts (a count-min estimate:
+// a source sharing a bucket of one sketch with a heavier one is still found through the
+// other), duplicates dropped; the nmax highest estimates become the heavy set, with an
+// open-addressing map of them. Zeroes the counts.
 // With `resolve`, every heavy source is also found in (or inserted into) the id table
 // here, once, so k_parse takes its slot from LDS instead of probing per packet (not with
 // prefix rules: a rule may drop every packet of the source, which must then never be
@@ -237,56 +291,85 @@ __global__ __launch_bounds__(1024) void k_heavy_pick(PacketIn in, const uint32_t
                                                      uint64_t mask, uint32_t test_flags, IdTable idt,
                                                      uint32_t resolve, BatchState *bs) {
     constexpr uint32_t kMap = 1u << kHeavyMapBits;
-    __shared__ uint32_t s_n;
+    constexpr uint32_t kCand = 2 * 2 * kHeavyMax;   // candidate buckets over both sketches
+    __shared__ uint32_t s_n, s_nc;
+    __shared__ uint32_t s_cb[kCand];                // candidate: sketch << 16 | bucket
+    __shared__ uint32_t s_ctag[kCand], s_ckey[kCand][4], s_cest[kCand];
     __shared__ uint32_t s_sel[kHeavyMax];
     __shared__ uint32_t s_tag[kHeavyMax], s_key[kHeavyMax][4];
     __shared__ uint8_t s_map[kMap];
+    __shared__ uint32_t s_bin[32], s_scal[4];
+    __shared__ uint16_t s_b2c[kSketch];             // first-sketch bucket -> candidate + 1
     const uint32_t tid = threadIdx.x;
     static_assert(kSketch == 4 * 1024, "4 buckets per thread");
-    uint32_t c[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) c[k] = sketch[tid * 4 + k];
-    // the nmax highest counts >= floor, by log2 bins: every bucket of the bins above the
-    // cut bin B, then buckets of bin B - 1 while room is left
-    __shared__ uint32_t s_bin[32], s_cut, s_room, s_extra;
-    if (tid < 32) s_bin[tid] = 0;
-    if (tid == 0) { s_n = 0; s_extra = 0; }
+    for (uint32_t c = tid; c < kSketch; c += 1024) s_b2c[c] = 0;
+    const uint32_t *cnt1 = sketch, *cand1 = sketch + kSketch;
+    const uint32_t *cnt2 = sketch + 2 * kSketch, *cand2 = sketch + 3 * kSketch;
+    if (tid == 0) { s_n = 0; s_nc = 0; }
     s_map[tid] = 0;
-    __syncthreads();
+    // 1. per sketch, the 2 nmax buckets of highest count >= floor
 #pragma unroll
-    for (int k = 0; k < 4; ++k)
-        if (c[k] >= floor_cnt) atomicAdd(&s_bin[31 - __clz((int)c[k])], 1u);
-    __syncthreads();
-    if (tid == 0) {
-        uint32_t acc = 0, B = 32;
-        for (int b = 31; b >= 0; --b) {
-            if (acc + s_bin[b] > nmax) break;
-            acc += s_bin[b];
-            B = (uint32_t)b;
+    for (int s = 0; s < 2; ++s) {
+        const uint32_t *cs = s ? cnt2 : cnt1;
+        uint32_t x[4];
+        bool sel[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t c = cs[tid * 4 + k];
+            x[k] = c >= floor_cnt ? c : 0u;
         }
-        s_cut = B;
-        s_room = nmax - acc;
+        select_top<4>(x, 2 * nmax, sel, s_bin, s_scal);
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (sel[k]) s_cb[atomicAdd(&s_nc, 1u)] = (uint32_t)s << 16 | (tid * 4 + k);
+        __syncthreads();
+    }
+    // 2. the candidates' sources and their count-min estimates
+    const uint32_t nc = s_nc;
+    if (tid < nc) {
+        const uint32_t s = s_cb[tid] >> 16, bk = s_cb[tid] & 0xFFFFu;
+        const uint32_t i = (s ? cand2 : cand1)[bk];
+        uint32_t k[4];
+        const uint32_t tag = packet_src(in, len, i, k);
+        const uint32_t h1 = (uint32_t)probe_start(tag, k, seed, mask, test_flags) & (kSketch - 1);
+        const uint32_t a = cnt1[h1], b = cnt2[sketch2_of(tag, k, seed)];
+        s_ctag[tid] = tag;
+        for (int j = 0; j < 4; ++j) s_ckey[tid][j] = k[j];
+        s_cest[tid] = tag ? (a < b ? a : b) : 0u;
     }
     __syncthreads();
+    // 3. duplicates (a source found through both sketches): a second-sketch candidate whose
+    // first-sketch bucket is a candidate of the same source is dropped
+    if (tid < nc && s_cb[tid] < (1u << 16)) s_b2c[s_cb[tid]] = (uint16_t)(tid + 1);
+    __syncthreads();
+    uint32_t est[1] = {0};
+    if (tid < nc) {
+        est[0] = s_cest[tid] >= floor_cnt ? s_cest[tid] : 0u;
+        if (s_cb[tid] >> 16) {
+            const uint32_t h1 = (uint32_t)probe_start(s_ctag[tid], s_ckey[tid], seed, mask, test_flags) & (kSketch - 1);
+            const uint32_t u = s_b2c[h1];
+            if (u && s_ctag[u - 1] == s_ctag[tid] && s_ckey[u - 1][0] == s_ckey[tid][0] &&
+                s_ckey[u - 1][1] == s_ckey[tid][1] && s_ckey[u - 1][2] == s_ckey[tid][2] &&
+                s_ckey[u - 1][3] == s_ckey[tid][3])
+                est[0] = 0;
+        }
+    }
+    // the counts are read: zero them for the next batch
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-        const uint32_t x = c[k];
-        if (x >= floor_cnt) {
-            const uint32_t b = 31u - (uint32_t)__clz((int)x);
-            if (b >= s_cut || (b + 1 == s_cut && atomicAdd(&s_extra, 1u) < s_room))
-                s_sel[atomicAdd(&s_n, 1u)] = tid * 4 + k;
-        }
         sketch[tid * 4 + k] = 0;
+        sketch[2 * kSketch + tid * 4 + k] = 0;
+    }
+    // 4. the nmax highest estimates
+    bool pick[1];
+    select_top<1>(est, nmax, pick, s_bin, s_scal);
+    if (pick[0]) {
+        const uint32_t e = atomicAdd(&s_n, 1u);
+        s_tag[e] = s_ctag[tid];
+        for (int j = 0; j < 4; ++j) s_key[e][j] = s_ckey[tid][j];
     }
     __syncthreads();
     const uint32_t n = s_n;
-    if (tid < n) {
-        const uint32_t i = sketch[kSketch + s_sel[tid]];
-        uint32_t k[4];
-        s_tag[tid] = packet_src(in, len, i, k);
-        for (int j = 0; j < 4; ++j) s_key[tid][j] = k[j];
-    }
-    __syncthreads();
     if (tid == 0) {
         for (uint32_t e = 0; e < n; ++e) {
             uint32_t h = (uint32_t)probe_start(s_tag[e], s_key[e], seed, mask, test_flags) & (kMap - 1);
@@ -1335,155 +1418,6 @@ constexpr uint32_t kShortSegFixed = FSX_SHORT_SEG_FIXED;
 constexpr uint32_t kShortSegSliding = 512;
 
 
-constexpr uint64_t kBig = 1ull << 62;
-
-struct FwState {
-    bool has_st, has_bl;
-    uint64_t pps, bps, tt, till;
-};
-
-// One packet of src/fsx_kern.c:150-346 (exact, any timestamps, u64 wraparound).
-template <class MW>
-__device__ __forceinline__ void fw_step(FwState &s, uint64_t now, uint32_t L, uint32_t q,
-                                        const Limits &lim, MW &mw) {
-    if (s.has_bl && s.till > 0) {
-        if (now > s.till) s.has_bl = false;                 // :193-204 delete
-        else { mw.emit(q, XDP_DROP); return; }              // :205-215
-    }
-    uint64_t cp, cb;
-    if (s.has_st) {
-        if (now - s.tt > lim.window) { s.pps = 0; s.bps = 0; s.tt = now; cp = 0; cb = 0; }  // :245-250
-        else { s.pps += 1; s.bps += L; cp = s.pps; cb = s.bps; }                            // :258-262
-    } else {
-        s.has_st = true; s.pps = 1; s.bps = L; s.tt = now; cp = 1; cb = L;                  // :265-284
-    }
-    if (cp > lim.pps || cb > lim.bps) {                     // :312
-        s.till = now + lim.block; s.has_bl = true;          // :317-326
-        mw.emit(q, XDP_DROP);
-    } else {
-        mw.emit(q, XDP_PASS);
-    }
-}
-
-// Exact replay for one thread, 16 packets' loads in flight per step.
-template <class SV, class MW>
-__device__ void walk_fixed_exact_thread(const SV &sv, uint32_t a, uint32_t b,
-                                        const Limits &lim, MW &mw, FwState &s) {
-    for (uint32_t q0 = a; q0 < b; q0 += 16) {
-        uint64_t t[16];
-        uint32_t L[16];
-#pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            if (q0 + k < b) sv.tl(q0 + k, t[k], L[k]);
-            else { t[k] = 0; L[k] = 0; }
-        }
-#pragma unroll
-        for (int k = 0; k < 16; ++k)
-            if (q0 + k < b) fw_step(s, t[k], L[k], q0 + k, lim, mw);
-    }
-}
-
-// Exact replay for one wave: 64 packets loaded in parallel, then stepped uniformly
-// (every lane keeps the same state; values broadcast by shuffles).
-template <class SV, class MW>
-__device__ void walk_fixed_exact_wave(const SV &sv, uint32_t a, uint32_t b, const Limits &lim,
-                                      MW &mw, FwState &s) {
-    const uint32_t lane = lane_id();
-    for (uint32_t q0 = a; q0 < b; q0 += 64) {
-        const uint32_t q = q0 + lane;
-        const uint64_t tq = q < b ? sv.t(q) : 0ull;
-        const uint32_t lq = q < b ? sv.l(q) : 0u;
-        const uint32_t cnt = min(64u, b - q0);
-        for (uint32_t k = 0; k < cnt; ++k)
-            fw_step(s, __shfl(tq, (int)k), __shfl(lq, (int)k), q0 + k, lim, mw);
-    }
-}
-
-// Epoch-jump evaluation (non-decreasing timestamps, no u64 overflow). An epoch
-// starts where ip_stats (re)starts a window: the first-ever packet (count 1), a
-// reset packet (count 0, not counted) or the carried window (continuation). With
-// counts consecutive inside an epoch, the count trigger is at a closed-form
-// position; the window end and the blacklist end are searches.
-template <bool kWave, class SV, class MW>
-__device__ void walk_fixed_fast(const SV &sv, uint32_t a, uint32_t b, const Limits &lim,
-                                uint32_t maxL, MW &mw, FwState &s) {
-    const uint64_t P = lim.pps, B = lim.bps, W = lim.window, BLK = lim.block;
-    uint32_t p = a;
-    if (s.has_bl && s.till > 0) {
-        const uint32_t j = search_gt<kWave>(sv, a, b, s.till);
-        if (j > a) mw.emit(a, XDP_DROP);
-        if (j < b) s.has_bl = false;
-        p = j;
-    }
-    bool touched = false;
-    uint32_t ep_lo = 0, ep_hi = 0;
-    uint64_t bps_base = 0;
-    while (p < b) {
-        const uint64_t t = sv.t(p);
-        uint64_t T0, pc, pb;
-        uint32_t cs;
-        if (s.has_st && !(t - s.tt > W)) { T0 = s.tt; pc = s.pps; pb = s.bps; cs = 1; }
-        else if (s.has_st) { T0 = t; pc = 0; pb = 0; cs = 0; }
-        else { T0 = t; pc = 0; pb = 0; cs = 1; }
-        s.has_st = true;
-        touched = true;
-        const uint32_t e = search_gt<kWave>(sv, p + 1, b, T0 + W);
-        const uint64_t c0 = pc + cs;
-        uint64_t k64 = c0 > P ? (uint64_t)p : (uint64_t)p + (P + 1 - c0);
-        if (k64 > e) k64 = e;
-        // bytes: only scanned when bps could exceed B before the count does
-        const bool bytes_possible = pb > B || (maxL && P + 1 > (B - pb) / maxL);
-        if (bytes_possible) k64 = bytes_trigger<kWave>(sv, cs ? p : p + 1, (uint32_t)k64, pb, B);
-        const uint32_t k = (uint32_t)k64;
-        s.tt = T0;
-        bps_base = pb;
-        ep_lo = p + 1 - cs;
-        if (k >= e) {   // window closes without a trigger
-            mw.emit(p, XDP_PASS);
-            s.pps = c0 + (uint64_t)(e - 1 - p);
-            ep_hi = e;
-            p = e;
-            continue;
-        }
-        if (k > p) mw.emit(p, XDP_PASS);
-        mw.emit(k, XDP_DROP);
-        s.pps = c0 + (uint64_t)(k - p);
-        ep_hi = k + 1;
-        s.till = sv.t(k) + BLK;
-        s.has_bl = true;
-        uint32_t q = k + 1;
-        for (;;) {
-            const uint32_t j = search_gt<kWave>(sv, q, b, s.till);
-            if (j >= b) { p = b; break; }
-            s.has_bl = false;                    // expired: deleted at packet j
-            const uint64_t tj = sv.t(j);
-            if (tj - s.tt > W) { p = j; break; } // j resets the window: next epoch
-            s.pps += 1;                          // re-trigger inside the window (block < window)
-            bps_base += sv.l(j);
-            s.till = tj + BLK;
-            s.has_bl = true;
-            q = j + 1;
-        }
-    }
-    if (touched) s.bps = bps_base + sum_len<kWave>(sv, ep_lo, ep_hi);
-}
-
-__device__ __forceinline__ FwState load_state(const Slot &sl) {
-    return FwState{(sl.flags & SLOT_HAS_ST) != 0, (sl.flags & SLOT_HAS_BL) != 0, sl.pps, sl.bps,
-                   sl.tt, sl.till};
-}
-__device__ __forceinline__ void store_state(Slot &sl, const FwState &s) {
-    // (also clears the born stamp: the batch that inserted the slot got this far)
-    sl.flags = (sl.flags & kFlagBits & ~(SLOT_HAS_ST | SLOT_HAS_BL)) | (s.has_st ? SLOT_HAS_ST : 0u) |
-               (s.has_bl ? SLOT_HAS_BL : 0u);
-    sl.pps = s.pps; sl.bps = s.bps; sl.tt = s.tt; sl.till = s.till;
-}
-
-__device__ __forceinline__ bool fast_ok(const BatchState *bs, const Limits &lim) {
-    return !bs->nonmono && lim.block >= 1 && lim.pps < kBig && lim.bps < kBig && lim.window < kBig &&
-           lim.block < kBig && bs->max_ts <= ~0ull - (lim.window > lim.block ? lim.window : lim.block);
-}
-
 // Segments are walked in order of length class (ceil log2 of the packet count), so
 // the lanes of a wave replay segments of similar length; the last class (longer
 // than short_seg) goes to the wave walkers, one wave per segment.
@@ -2114,7 +2048,7 @@ hipError_t launch_tail(const TailArgs &a) {
         // pipelined: the tail on its own stream (the caller made it and st2 wait for the
         // front); walkers serial on it, the heavy flow sums and the flows on st2
         st = split->tail;
-        if ((e = hipMemsetAsync(sc.marks, 0, n, st)) != hipSuccess) return e;
+        if (!a.bins && (e = hipMemsetAsync(sc.marks, 0, n, st)) != hipSuccess) return e;
         st3 = nullptr;
         hs = st;
         hs_id = 0;
@@ -2122,11 +2056,51 @@ hipError_t launch_tail(const TailArgs &a) {
         hf_id = fork ? 1 : 0;
     }
     if (tagh && (e = launch_heavy()) != hipSuccess) return e;
+    // light-bin tail: the light entries are sort pass 1's output (packed[0] / pay[0])
+    const uint64_t *S_light = sc.packed[0], *pay_light = sc.pay[0];
     if (npass & 1) {
         std::swap(sc.packed[0], sc.packed[1]);
         std::swap(sc.pay[0], sc.pay[1]);
     }
     uint64_t *S = sc.packed[0];
+    if (a.bins) {
+        // one wave per slot bin: walkers, flow sums, verdicts of the light sources
+        // (fsx_bins.hip), then the heavy segments numbered after them
+        const BinTail bt{S_light, pay_light, ts, len, in, bs, tstate, sc.bin_start, sc.bin_mask, sc.bin_row,
+                         sc.bin_order, sc.bin_stage, flows ? flows->sacc : nullptr, flows ? flows->epoch : 0u, verdict, table,
+                         lim, a.binbits};
+        if ((e = launch_bins(bt, n, flows, lim.salt32, st, mk)) != hipSuccess) return e;
+        k_heads_heavy<<<1, 256, 0, st>>>(bs, sc.sort_ctl, sc.gbase, sc.seg_start, sc.seg_slot, S, lim.table_mask,
+                                         nullptr);
+        mark("k_heads_heavy");
+        if (flows) {   // the heavy rows after the light ones, on the heavy sums' stream
+            hipStream_t fs = st;
+            if (fork) {
+                if ((e = hipEventRecord(fork_ev, st)) != hipSuccess) return e;
+                if ((e = hipStreamWaitEvent(st2, fork_ev, 0)) != hipSuccess) return e;
+                fs = st2;
+                mark_on(nullptr, 1);
+            }
+            if (hf != fs && (e = hipStreamWaitEvent(fs, heavy_flow_ev, 0)) != hipSuccess) return e;
+            if ((e = launch_flows_heavy_finish(S, bs, sc.sort_ctl, sc.seg_start, in, len, ts, sc.heavy_flow, sc.cap,
+                                               flows->keys16, flows->fam, flows->feat, flows->prob, flows->dec,
+                                               flows->cap, flows->score, lim.salt32, flows->sacc, flows->epoch,
+                                               sc.seg_slot, fs)) != hipSuccess)
+                return e;
+            mark_on("k_flow_heavy_finish", fork ? 1 : 0);
+            if (fork && (e = hipEventRecord(join_ev, st2)) != hipSuccess) return e;
+        }
+        if (hs != st) {   // the heavy walker's verdict lists
+            hipEvent_t je = walk_join_ev ? walk_join_ev : heavy_fork_ev;
+            if ((e = hipEventRecord(je, hs)) != hipSuccess) return e;
+            if ((e = hipStreamWaitEvent(st, je, 0)) != hipSuccess) return e;
+        }
+        k_verdict_apply<<<cdiv(n, kVChunk), 256, 0, st>>>(verdict, n, sc.drop_list, sc.drop_cur, bs, sc.heavy,
+                                                          hlists.list);
+        mark("k_verdict_apply");
+        if (fork && flows && (e = hipStreamWaitEvent(st, join_ev, 0)) != hipSuccess) return e;
+        return hipGetLastError();
+    }
     const uint32_t lo = tagh ? 1u : 0u;   // light-only heads
     k_heads_count<<<gridTiles, 256, 0, st>>>(S, bs, in.hdr, sc.headf, sc.tile_aux, sc.sub_cnt, lo);
     mark("k_heads_count");
@@ -2240,7 +2214,7 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
     hipError_t e;
     if ((e = hipMemsetAsync(bs, 0, sizeof(BatchState), st)) != hipSuccess) return e;
     if (n == 0) return hipSuccess;
-    if (!(split && split->tail) && (e = hipMemsetAsync(sc.marks, 0, n, st)) != hipSuccess) return e;
+
     const uint32_t gridStream = std::min<uint32_t>(2048, std::max<uint32_t>(1, cdiv(n, 256)));
     const uint32_t gridTiles = std::min<uint32_t>(4096, std::max<uint32_t>(1, cdiv(n, kTile)));
 
@@ -2270,10 +2244,20 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
     // entries by a 7-bit id digit and every heavy source into a bucket of its own; passes
     // 1-2 sort the light entries only, by the remaining id bits in two equal digits.
     const bool heavy_sort = !onesweep && !full_digits && !no_heavy && npass == 3 && idbits <= 23;
+    // heavy verdict lists (fixed window with the heavy-source sort; FSX_NO_HEAVY_LISTS=1: A/B)
+    static const bool no_hlists = getenv("FSX_NO_HEAVY_LISTS") != nullptr;
+    const bool tagh = heavy_sort && do_limit && lim.limiter == 0 && verdict && !no_hlists;
+    // light-bin tail (FSX_BINS=0 / 1: A/B): pass 1 leaves bins of 64 slots, no pass 2
+    static const bool no_bins = !getenv("FSX_BINS") || getenv("FSX_BINS")[0] == '0';
+    const bool bins = tagh && !no_bins && idbits >= kBinMinIdBits && idbits <= kBinMaxIdBits && sc.bin_start &&
+                      sc.bin_stage;
+    if (!bins && !(split && split->tail) && (e = hipMemsetAsync(sc.marks, 0, n, st)) != hipSuccess) return e;
     DigitPlan dp{};
     dp.npass = (uint32_t)npass;
+    uint32_t binbits = 0;
     if (heavy_sort) {
-        const uint32_t rest = idbits - 7, w1 = (rest + 1) / 2;
+        const uint32_t rest = idbits - 7, w1 = bins ? rest - kBinSlotBits : (rest + 1) / 2;
+        binbits = 7 + w1;
         dp.light_b = 128;
         dp.shift[0] = 56; dp.mask[0] = 255;
         dp.shift[1] = 39; dp.mask[1] = (1u << w1) - 1u;
@@ -2288,9 +2272,6 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
     } else {
         for (int p = 0; p < 4; ++p) { dp.shift[p] = 32u + dbits * (uint32_t)p; dp.mask[p] = dmask; }
     }
-    // heavy verdict lists (fixed window with the heavy-source sort; FSX_NO_HEAVY_LISTS=1: A/B)
-    static const bool no_hlists = getenv("FSX_NO_HEAVY_LISTS") != nullptr;
-    const bool tagh = heavy_sort && do_limit && lim.limiter == 0 && verdict && !no_hlists;
     {
         const uint32_t g = std::min<uint32_t>(256u * FSX_PARSE_MINB, ntiles);   // one resident block per slot
         const HeavySet *hs = heavy_sort ? sc.heavy : nullptr;
@@ -2329,7 +2310,7 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
     k_hist_prep<<<1, 256, 0, st>>>(sc.sort_ctl, sc.gbase, bs, heavy_sort ? dp.light_b : 256u);
     if (do_limit) k_batch_check<<<1, 1, 0, st>>>(bs, tstate, lim, split ? split->prev : nullptr);
     const uint32_t gen0 = onesweep ? next_generation() : 0u;
-    for (int pass = 0; pass < npass; ++pass) {
+    for (int pass = 0; pass < (bins ? 2 : npass); ++pass) {
         const uint64_t *in = sc.packed[pass & 1];
         uint64_t *out = sc.packed[(pass + 1) & 1];
         const uint64_t *pin = pass == 0 ? nullptr : sc.pay[pass & 1];
@@ -2373,6 +2354,7 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
     ta.heavy_flow_ev = heavy_flow_ev; ta.tm = tm; ta.split = split != nullptr;
     if (split) ta.sp = *split;
     ta.npass = npass; ta.tagh = tagh; ta.gridTiles = gridTiles;
+    ta.bins = bins; ta.binbits = binbits;
     ta.fork = flows && do_limit && st2 && fork_ev && join_ev && !no_fork;
     for (int k = 0; k < 3; ++k) ta.last[k] = last[k];
     if (split && split->tail_out) {

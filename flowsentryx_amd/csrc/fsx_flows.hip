@@ -298,43 +298,6 @@ __device__ __forceinline__ void heavy_chunk_prefix(const uint32_t *cnt0, uint32_
     __syncthreads();
 }
 
-// Flow sums of positions [a, b) of the run that starts at rs <= a, one wave: 1024
-// consecutive positions per round (16 loads in flight per lane), inter-arrival times
-// across lanes by shuffles; the total in every lane.
-template <class SV>
-__device__ FlowAcc flow_wave_acc(const SV &sv, uint32_t rs, uint32_t a, uint32_t b) {
-    const uint32_t lane = lane_id();
-    FlowAcc A = acc_zero();
-    uint64_t carry = a > rs ? sv.t(a - 1) : 0ull;   // timestamp of the position before the round
-    for (uint32_t q0 = a; q0 < b; q0 += 1024) {
-        uint64_t t[16];
-        uint32_t L[16];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const uint32_t q = q0 + 64u * (uint32_t)r + lane;
-            if (q < b) sv.tl(q, t[r], L[r]);
-            else { t[r] = 0; L[r] = 0; }
-        }
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const uint32_t q = q0 + 64u * (uint32_t)r + lane;
-            uint64_t tp = __shfl_up(t[r], 1);
-            if (lane == 0) tp = carry;
-            if (q < b) {
-                FlowAcc c = acc_zero();
-                c.n = 1; c.s1 = L[r]; c.s2 = (u128)L[r] * L[r];
-                if (q != rs) {
-                    const uint64_t d = t[r] - tp;
-                    c.d1 = d; c.d2 = (u128)d * d; c.dmax = d;
-                }
-                acc_add(A, c);
-            }
-            carry = __shfl(t[r], 63);
-        }
-    }
-    return wave_sum_acc(A);
-}
-
 template <class SV>
 __device__ __forceinline__ void flow_heavy_body(const SV &sv, const uint32_t *cnt0, const uint32_t *base0,
                                                 const uint32_t *s_pre, FlowAcc *part) {

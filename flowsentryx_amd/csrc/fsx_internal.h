@@ -303,10 +303,16 @@ struct Scratch {
                            // words [slots][4] (generation-tagged, never cleared)
     uint32_t *drop_list;   // DROP verdicts by arrival chunk: chunk c owns [c, c + 1) * kVChunk
     uint32_t *drop_cur;    // entries per chunk (zeroed by k_verdict_apply after use)
-    uint32_t *sketch;      // heavy-source sample: counts [kSketch], candidate packets [kSketch]
-                           // (counts zeroed by k_heavy_pick after use)
+    uint32_t *sketch;      // heavy-source sample, two sketches: counts [kSketch], candidate
+                           // packets [kSketch] each (counts zeroed by k_heavy_pick after use)
     HeavySet *heavy;
     void *heavy_flow;      // heavy sources' flow chunk sums (heavy_flow_bytes)
+    // light-bin tail (fsx_bins.hip; tables of 2^17..2^21 slots, else null)
+    uint32_t *bin_start;   // bins + 1
+    uint64_t *bin_mask;    // bins
+    uint32_t *bin_row;     // bins
+    uint32_t *bin_order;   // bins
+    void *bin_stage;       // per table slot: FlowAcc (bin_stage_bytes)
     uint64_t cap;          // packets the scratch is sized for
 };
 
@@ -389,6 +395,8 @@ struct TailArgs {
     int npass;
     uint32_t gridTiles;
     int last[3];
+    bool bins;             // light-bin tail (sort passes 0-1 only, fsx_bins.hip)
+    uint32_t binbits;
 };
 hipError_t launch_tail(const TailArgs &a);
 
