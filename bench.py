@@ -364,7 +364,8 @@ def main():
         if plane is not None:
             ex = plane.last_exchange or {"sent": [], "received": []}
             out["exchange"] = {"records_sent": ex["sent"], "records_received": ex["received"],
-                               "dropped_by_replica": ex.get("filtered", 0), "sub_batches": chunks,
+                               "dropped_by_replica": ex.get("filtered", 0),
+                               "flow_partials_sent": getattr(plane, "partials_sent", 0), "sub_batches": chunks,
                                "record_bytes": sorted(plane.formats) or None,
                                "backend": args.dist_backend}
             out["stats"] = plane.stats()

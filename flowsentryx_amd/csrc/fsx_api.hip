@@ -178,7 +178,7 @@ static void free_scratch(fsx_ctx *c) {
     hipFree(s.span_list); hipFree(s.sort_ctl); hipFree(s.gbase); hipFree(s.status);
     hipFree(s.lim_tiles); hipFree(s.sw_seg); hipFree(s.sketch); hipFree(s.heavy);
     hipFree(s.drop_list); hipFree(s.drop_cur); hipFree(s.heavy_flow);
-    hipFree(s.bin_start); hipFree(s.bin_mask); hipFree(s.bin_row); hipFree(s.bin_order); hipFree(s.bin_stage);
+    hipFree(s.bin_start); hipFree(s.bin_order);
     s = Scratch{};
 }
 
@@ -224,16 +224,13 @@ static int alloc_scratch(fsx_ctx *c, uint64_t cap) {
     HIPCHK(c, hipMalloc(&s.heavy, sizeof(HeavySet)));
     HIPCHK(c, hipMemset(s.heavy, 0, sizeof(HeavySet)));
     HIPCHK(c, hipMalloc(&s.heavy_flow, heavy_flow_bytes(cap)));
-    // light-bin tail of the fixed window (fsx_bins.hip): tables of 2^17..2^21 slots
+    // bin sort of the fixed window (fsx_bins.hip): tables of 2^17..2^21 slots
     uint32_t idbits = 0;
     while ((1ull << idbits) < c->slots) ++idbits;
     if (c->cfg.limiter == FSX_LIMIT_FIXED_WINDOW && idbits >= kBinMinIdBits && idbits <= kBinMaxIdBits) {
         const uint64_t nb = c->slots >> kBinSlotBits;
         HIPCHK(c, hipMalloc(&s.bin_start, (nb + 1) * 4));
-        HIPCHK(c, hipMalloc(&s.bin_mask, nb * 8));
-        HIPCHK(c, hipMalloc(&s.bin_row, nb * 4));
         HIPCHK(c, hipMalloc(&s.bin_order, nb * 4));
-        HIPCHK(c, hipMalloc(&s.bin_stage, bin_stage_bytes(c->slots)));
     }
     s.cap = cap;
     return 0;
@@ -907,10 +904,12 @@ int fsx_process_batch_device(fsx_ctx *c, const uint8_t *d_hdr, const uint32_t *d
     return run_batch(c, PacketIn{d_hdr, nullptr, 0, nullptr, nullptr}, d_len, d_ts, n, d_verdict, true, &fr);
 }
 
+static int ensure_stage(fsx_ctx *c, uint64_t n);
+
 // Record mode (the owner side of the sharded path): the pipeline reads the exchange
 // records directly; their len / ts land in context scratch for the later kernels.
 static int run_records(fsx_ctx *c, const void *d_records, size_t n, uint32_t rec_bytes, uint8_t *d_verdict,
-                       const FlowRequest *fr) {
+                       const FlowRequest *fr, bool do_limit = true) {
     if (rec_bytes != FSX_SHARD_RECORD_BYTES && rec_bytes != FSX_SHARD_RECORD16_BYTES)
         return set_err(c, -EINVAL, "record size must be %d or %d", FSX_SHARD_RECORD16_BYTES,
                        FSX_SHARD_RECORD_BYTES);
@@ -927,7 +926,38 @@ static int run_records(fsx_ctx *c, const void *d_records, size_t n, uint32_t rec
         c->rec_cap = n;
     }
     const PacketIn in{nullptr, d_records, rec_bytes, c->d_rec_len, c->d_rec_ts};
-    return run_batch(c, in, c->d_rec_len, c->d_rec_ts, n, d_verdict, true, fr);
+    return run_batch(c, in, c->d_rec_len, c->d_rec_ts, n, d_verdict, do_limit, fr);
+}
+
+int fsx_flow_partials_records_device(fsx_ctx *c, const void *d_records, size_t n, uint32_t rec_bytes, uint32_t G,
+                                     void *d_partials, size_t cap_per_shard, uint64_t *d_counts) {
+    if (!c) return -EINVAL;
+    if (G == 0 || G > FSX_MAX_SHARDS) return set_err(c, -EINVAL, "n_shards must be 1..%d", FSX_MAX_SHARDS);
+    if (!d_counts || (n && cap_per_shard && !d_partials)) return set_err(c, -EINVAL, "null buffer");
+    if (cap_per_shard > 0xFFFFFFFFu) return set_err(c, -EINVAL, "cap_per_shard too large");
+    int rc = sel(c);
+    if (rc) return rc;
+    HIPCHK(c, hipMemsetAsync(d_counts, 0, (size_t)G * 8, c->stream));
+    if (n == 0) return 0;
+    if ((rc = ensure_stage(c, n))) return rc;   // (verdict scratch: no limiter runs)
+    FlowRequest fr{};
+    fr.cap = (uint32_t)std::min<size_t>(n, 0xFFFFFFFFu);
+    fr.score.enabled = 0;
+    fr.part = PartialOut{d_partials, (uint32_t)cap_per_shard, G, reinterpret_cast<unsigned long long *>(d_counts)};
+    return run_records(c, d_records, n, rec_bytes, c->d_verdict, &fr, false);
+}
+
+int fsx_flows_merge_device(fsx_ctx *c, const void *d_partials, size_t m) {
+    if (!c) return -EINVAL;
+    if (!c->flow_accum) return set_err(c, -EINVAL, "fsx_flows_merge_device outside fsx_flows_begin .. end");
+    if (m && !d_partials) return set_err(c, -EINVAL, "null buffer");
+    if (m > 0xFFFFFFFFu) return set_err(c, -E2BIG, "m=%zu too large", m);
+    int rc = sel(c);
+    if (rc) return rc;
+    hipError_t e = launch_flows_merge(d_partials, (uint32_t)m, c->table, c->lim, c->d_slot_acc, c->flow_epoch,
+                                      c->stream);
+    if (e != hipSuccess) return set_err(c, -EIO, "flows merge: %s", hipGetErrorString(e));
+    return 0;
 }
 
 int fsx_verdict_records_device(fsx_ctx *c, const void *d_records, size_t n, uint32_t rec_bytes,
@@ -1337,7 +1367,7 @@ int fsx_shard_pack_device(fsx_ctx *c, const uint8_t *d_hdr, const uint32_t *d_le
         return set_err(c, -EINVAL, "null buffer");
     int rc = sel(c);
     if (rc) return rc;
-    const uint64_t need = (uint64_t)G * (n / 4096 + 1);
+    const uint64_t need = (uint64_t)(G + 1) * (n / 4096 + 1);   // (+ the replica-drop group)
     if (need > c->shard_cnt_cap) {
         hipFree(c->d_shard_cnt);
         c->d_shard_cnt = nullptr;
@@ -1358,9 +1388,10 @@ int fsx_shard_pack_device(fsx_ctx *c, const uint8_t *d_hdr, const uint32_t *d_le
     const Replica rep{c->d_rep, c->rep_slots ? c->rep_slots - 1 : 0};
     const bool filt = (flags & FSX_SHARD_FILTER_BLOCKLIST) && c->rep_valid;
     const bool compact = (flags & FSX_SHARD_COMPACT) != 0;
+    const bool drop_rec = filt && (flags & FSX_SHARD_DROP_RECORDS);
     hipError_t e = launch_shard_pack(d_hdr, d_len, d_ts, (uint32_t)n, G, d_verdict, d_records, d_send_idx,
                                      d_counts, c->d_shard_cnt, c->d_shard_own, c->d_shard_crec,
-                                     filt ? &rep : nullptr, compact, c->stream);
+                                     filt ? &rep : nullptr, compact, drop_rec, c->stream);
     if (e != hipSuccess) return set_err(c, -EIO, "shard pack: %s", hipGetErrorString(e));
     return 0;
 }

@@ -150,6 +150,7 @@ struct DigitPlan {
     uint32_t shift[4], mask[4];
     uint32_t npass;
     uint32_t light_b;   // heavy sort: buckets below light_b are light (id digit 0); 0 = plain
+    uint32_t light_shift;   // the light bucket is id bits [light_shift, +log2 light_b)
 };
 
 // parse_ethhdr / parse_ip6hdr / parse_ip4hdr (src/parsing_helper.h:49-136, dispatch
@@ -574,7 +575,7 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
         uint64_t out = ((uint64_t)(id & idt.mask) << 32) | ((uint64_t)(tag - 1u) << 31) | i;
         if (dp.light_b)   // heavy-source sort: the first pass's bucket in bits 56..63
             out |= (uint64_t)(hidx >= 0 ? dp.light_b + (uint32_t)hidx
-                                        : (uint32_t)(out >> 32) & (dp.light_b - 1u)) << 56;
+                                        : ((uint32_t)(out >> 32) >> dp.light_shift) & (dp.light_b - 1u)) << 56;
         return out;
     };
     // the deferred packets of this wave: full probes (CAS inserts), 64 at a time
@@ -1304,23 +1305,6 @@ __global__ __launch_bounds__(256) void k_heads_heavy(BatchState *bs, const uint3
 
 // ------------------------------------------------------------------ table lookup / insert
 
-__device__ __forceinline__ bool slot_key_eq(const Slot &s, uint32_t tag, const uint32_t k[4]) {
-    return s.tag == tag && s.key[0] == k[0] && s.key[1] == k[1] && s.key[2] == k[2] &&
-           s.key[3] == k[3];
-}
-
-__device__ __forceinline__ uint32_t table_find(const Slot *table, const Limits &lim, uint32_t tag,
-                                               const uint32_t k[4]) {
-    uint64_t i = probe_start(tag, k, lim.seed, lim.table_mask, lim.test_flags);
-    for (uint64_t probes = 0; probes <= lim.table_mask; ++probes) {
-        const uint32_t t = table[i].tag;
-        if (t == 0) return kNoSlot;
-        if (t == tag && slot_key_eq(table[i], tag, k)) return (uint32_t)i;
-        i = (i + 1) & lim.table_mask;
-    }
-    return kNoSlot;
-}
-
 // Publish slot i of (tag, key) in the persistent index (single writer, between batches).
 __device__ __forceinline__ void index_publish(const TableIndex &X, uint64_t i, uint32_t tag,
                                               const uint32_t k[4]) {
@@ -2048,7 +2032,7 @@ hipError_t launch_tail(const TailArgs &a) {
         // pipelined: the tail on its own stream (the caller made it and st2 wait for the
         // front); walkers serial on it, the heavy flow sums and the flows on st2
         st = split->tail;
-        if (!a.bins && (e = hipMemsetAsync(sc.marks, 0, n, st)) != hipSuccess) return e;
+        if ((e = hipMemsetAsync(sc.marks, 0, n, st)) != hipSuccess) return e;
         st3 = nullptr;
         hs = st;
         hs_id = 0;
@@ -2056,54 +2040,31 @@ hipError_t launch_tail(const TailArgs &a) {
         hf_id = fork ? 1 : 0;
     }
     if (tagh && (e = launch_heavy()) != hipSuccess) return e;
-    // light-bin tail: the light entries are sort pass 1's output (packed[0] / pay[0])
-    const uint64_t *S_light = sc.packed[0], *pay_light = sc.pay[0];
+    // sort pass 2 as a per-bin LDS sort (fsx_bins.hip): pass 1's output (packed[0]) ->
+    // packed[1], where the global pass would have written it, with the segment heads
+    // (FSX_BIN_HEADS=0: k_heads_count instead, A/B)
+    static const bool bin_heads = !getenv("FSX_BIN_HEADS") || getenv("FSX_BIN_HEADS")[0] != '0';
+    if (a.bins) {
+        const bool bh = bin_heads && tagh;
+        if (bh) {
+            if ((e = hipMemsetAsync(sc.tile_aux, 0, (size_t)cdiv(n, kTile) * 4, st)) != hipSuccess) return e;
+            if ((e = hipMemsetAsync(sc.sub_cnt, 0, (size_t)(n / 1024 + 8) * 4, st)) != hipSuccess) return e;
+        }
+        const BinSort bsrt{sc.packed[0], sc.pay[0], sc.packed[1], sc.pay[1], bs, sc.bin_start, sc.bin_order,
+                           lim.table_mask, bh ? sc.headf : nullptr, sc.tile_aux, sc.sub_cnt};
+        if ((e = launch_bin_sort(bsrt, n, st)) != hipSuccess) return e;
+        mark("k_bin_sort");
+    }
     if (npass & 1) {
         std::swap(sc.packed[0], sc.packed[1]);
         std::swap(sc.pay[0], sc.pay[1]);
     }
     uint64_t *S = sc.packed[0];
-    if (a.bins) {
-        // one wave per slot bin: walkers, flow sums, verdicts of the light sources
-        // (fsx_bins.hip), then the heavy segments numbered after them
-        const BinTail bt{S_light, pay_light, ts, len, in, bs, tstate, sc.bin_start, sc.bin_mask, sc.bin_row,
-                         sc.bin_order, sc.bin_stage, flows ? flows->sacc : nullptr, flows ? flows->epoch : 0u, verdict, table,
-                         lim, a.binbits};
-        if ((e = launch_bins(bt, n, flows, lim.salt32, st, mk)) != hipSuccess) return e;
-        k_heads_heavy<<<1, 256, 0, st>>>(bs, sc.sort_ctl, sc.gbase, sc.seg_start, sc.seg_slot, S, lim.table_mask,
-                                         nullptr);
-        mark("k_heads_heavy");
-        if (flows) {   // the heavy rows after the light ones, on the heavy sums' stream
-            hipStream_t fs = st;
-            if (fork) {
-                if ((e = hipEventRecord(fork_ev, st)) != hipSuccess) return e;
-                if ((e = hipStreamWaitEvent(st2, fork_ev, 0)) != hipSuccess) return e;
-                fs = st2;
-                mark_on(nullptr, 1);
-            }
-            if (hf != fs && (e = hipStreamWaitEvent(fs, heavy_flow_ev, 0)) != hipSuccess) return e;
-            if ((e = launch_flows_heavy_finish(S, bs, sc.sort_ctl, sc.seg_start, in, len, ts, sc.heavy_flow, sc.cap,
-                                               flows->keys16, flows->fam, flows->feat, flows->prob, flows->dec,
-                                               flows->cap, flows->score, lim.salt32, flows->sacc, flows->epoch,
-                                               sc.seg_slot, fs)) != hipSuccess)
-                return e;
-            mark_on("k_flow_heavy_finish", fork ? 1 : 0);
-            if (fork && (e = hipEventRecord(join_ev, st2)) != hipSuccess) return e;
-        }
-        if (hs != st) {   // the heavy walker's verdict lists
-            hipEvent_t je = walk_join_ev ? walk_join_ev : heavy_fork_ev;
-            if ((e = hipEventRecord(je, hs)) != hipSuccess) return e;
-            if ((e = hipStreamWaitEvent(st, je, 0)) != hipSuccess) return e;
-        }
-        k_verdict_apply<<<cdiv(n, kVChunk), 256, 0, st>>>(verdict, n, sc.drop_list, sc.drop_cur, bs, sc.heavy,
-                                                          hlists.list);
-        mark("k_verdict_apply");
-        if (fork && flows && (e = hipStreamWaitEvent(st, join_ev, 0)) != hipSuccess) return e;
-        return hipGetLastError();
-    }
     const uint32_t lo = tagh ? 1u : 0u;   // light-only heads
-    k_heads_count<<<gridTiles, 256, 0, st>>>(S, bs, in.hdr, sc.headf, sc.tile_aux, sc.sub_cnt, lo);
-    mark("k_heads_count");
+    if (!(a.bins && bin_heads && tagh)) {
+        k_heads_count<<<gridTiles, 256, 0, st>>>(S, bs, in.hdr, sc.headf, sc.tile_aux, sc.sub_cnt, lo);
+        mark("k_heads_count");
+    }
     k_scan_tiles_u32<<<1, 256, 0, st>>>(sc.tile_aux, bs, sc.seg_start, lo);
     // (the first sort word's low half per segment only for the flow rows)
     uint32_t *seg_lo = flows && !in.rec ? sc.seg_lo : nullptr;
@@ -2125,7 +2086,7 @@ hipError_t launch_tail(const TailArgs &a) {
                               sc.flow_first, sc.flow_last, sc.span_list, flows->acc, flows->keys16,
                               flows->fam, flows->feat, flows->prob, flows->dec, flows->cap, flows->score,
                               lim.salt32, n, do_limit ? flows->sacc : nullptr, flows->epoch, sc.seg_slot,
-                              tagh, seg_lo, seg_lo ? sc.seg_len : nullptr, fs)) != hipSuccess)
+                              tagh, seg_lo, seg_lo ? sc.seg_len : nullptr, flows->part, fs)) != hipSuccess)
             return e;
         if (tagh) {   // the heavy sources' rows, from their sums (k_flow_heavy)
             if (hf != fs && (e = hipStreamWaitEvent(fs, heavy_flow_ev, 0)) != hipSuccess) return e;
@@ -2247,21 +2208,29 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
     // heavy verdict lists (fixed window with the heavy-source sort; FSX_NO_HEAVY_LISTS=1: A/B)
     static const bool no_hlists = getenv("FSX_NO_HEAVY_LISTS") != nullptr;
     const bool tagh = heavy_sort && do_limit && lim.limiter == 0 && verdict && !no_hlists;
-    // light-bin tail (FSX_BINS=0 / 1: A/B): pass 1 leaves bins of 64 slots, no pass 2
+    // bin sort (FSX_BINS=0 / 1: A/B): pass 1 leaves bins of 64 slots, each sorted in LDS by
+    // the tail instead of a global third pass
     static const bool no_bins = !getenv("FSX_BINS") || getenv("FSX_BINS")[0] == '0';
-    const bool bins = tagh && !no_bins && idbits >= kBinMinIdBits && idbits <= kBinMaxIdBits && sc.bin_start &&
-                      sc.bin_stage;
-    if (!bins && !(split && split->tail) && (e = hipMemsetAsync(sc.marks, 0, n, st)) != hipSuccess) return e;
+    const bool bins = tagh && !no_bins && idbits >= kBinMinIdBits && idbits <= kBinMaxIdBits && sc.bin_start;
+    if (!(split && split->tail) && (e = hipMemsetAsync(sc.marks, 0, n, st)) != hipSuccess) return e;
     DigitPlan dp{};
-    dp.npass = (uint32_t)npass;
-    uint32_t binbits = 0;
-    if (heavy_sort) {
-        const uint32_t rest = idbits - 7, w1 = bins ? rest - kBinSlotBits : (rest + 1) / 2;
-        binbits = 7 + w1;
+    dp.npass = bins ? 2u : (uint32_t)npass;   // (digits counted by k_parse: no pass 2 with bins)
+    if (heavy_sort && bins) {
+        // light bucket = slot bits [8, 15), pass 1 = slot bits [15, idbits): the pass-1 output
+        // is ordered by slot >> 8, the bin sort orders each bin by slot & 255 (fsx_bins.hip)
+        dp.light_b = 128;
+        dp.light_shift = kBinSlotBits;
+        dp.shift[0] = 56; dp.mask[0] = 255;
+        dp.shift[1] = 32 + kBinSlotBits + 7; dp.mask[1] = (1u << (idbits - kBinSlotBits - 7)) - 1u;
+        dp.shift[2] = 32; dp.mask[2] = (1u << kBinSlotBits) - 1u;
+    } else if (heavy_sort) {
+        const uint32_t rest = idbits - 7, w1 = (rest + 1) / 2;
         dp.light_b = 128;
         dp.shift[0] = 56; dp.mask[0] = 255;
         dp.shift[1] = 39; dp.mask[1] = (1u << w1) - 1u;
         dp.shift[2] = 39 + w1; dp.mask[2] = (1u << (rest - w1)) - 1u;
+    }
+    if (heavy_sort) {
         k_heavy_sample<<<64, 256, 0, st>>>(in, len, n, sc.sketch, lim.seed, lim.table_mask, lim.test_flags);
         // heavy slots resolved once (not under prefix rules; FSX_NO_HEAVY_SLOTS=1: A/B)
         static const bool no_hslots = getenv("FSX_NO_HEAVY_SLOTS") != nullptr;
@@ -2354,7 +2323,7 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
     ta.heavy_flow_ev = heavy_flow_ev; ta.tm = tm; ta.split = split != nullptr;
     if (split) ta.sp = *split;
     ta.npass = npass; ta.tagh = tagh; ta.gridTiles = gridTiles;
-    ta.bins = bins; ta.binbits = binbits;
+    ta.bins = bins;
     ta.fork = flows && do_limit && st2 && fork_ev && join_ev && !no_fork;
     for (int k = 0; k < 3; ++k) ta.last[k] = last[k];
     if (split && split->tail_out) {

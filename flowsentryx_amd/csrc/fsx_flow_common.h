@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstddef>
 
 #include "fsx_dev_common.h"
 #include "fsx_internal.h"
@@ -121,7 +122,34 @@ struct FlowOut {
     // frame length (k_flow_tile), so k_flow_finish gathers only the first header record
     const uint32_t *seg_lo;
     uint32_t *seg_len;
+    PartialOut part;   // partials mode (buf non-null): raw sums per owner run, no row
 };
+
+// include/fsx_hip.h fsx_flow_partial (112 bytes).
+struct FlowPartial {
+    uint32_t key[4];
+    uint32_t tag, dport;
+    uint64_t n, s1, dmax, first_ts, last_ts;
+    u128 s2, d1, d2;
+};
+static_assert(sizeof(FlowPartial) == 112 && offsetof(FlowPartial, s2) == 64, "fsx_flow_partial layout");
+
+// Source (tag, k)'s partial into the run of its owner rank.
+__device__ __forceinline__ void write_partial(const PartialOut &P, uint32_t tag, const uint32_t k[4], uint32_t dport,
+                                              const FlowAcc &a, uint64_t t0, uint64_t t1) {
+    const uint32_t o = shard_owner_of(tag, k, P.G);
+    const unsigned long long j = atomicAdd(&P.cnt[o], 1ull);
+    if (j >= P.cap) return;
+    FlowPartial x;
+    x.key[0] = k[0]; x.key[1] = k[1]; x.key[2] = k[2]; x.key[3] = k[3];
+    x.tag = tag;
+    x.dport = dport;
+    x.n = a.n; x.s1 = a.s1; x.dmax = a.dmax;
+    x.first_ts = t0;
+    x.last_ts = t1;
+    x.s2 = a.s2; x.d1 = a.d1; x.d2 = a.d2;
+    reinterpret_cast<FlowPartial *>(P.buf)[(size_t)o * P.cap + j] = x;
+}
 
 // L4 destination port of the source's first packet (oracle fsxo_dst_port).
 __device__ __forceinline__ uint32_t dst_port(const uint8_t *f, uint32_t len) {
@@ -168,6 +196,10 @@ __device__ __forceinline__ void flow_finish(uint32_t g, const FlowAcc &a, const 
     } else {
         tag = key_of(v, in.hdr, salt, k);
         dport = dst_port(in.hdr + (size_t)idx * 64, out.seg_len ? out.seg_len[g] : len[idx]);
+    }
+    if (out.part.buf) {   // partials mode: the raw sums with the run's first / last timestamp
+        write_partial(out.part, tag, k, dport, a, out.ts[idx], out.ts[pk_idx(S[seg_start[g + 1] - 1])]);
+        return;
     }
     if (out.sacc) {
         SlotAcc &m = out.sacc[out.seg_slot[g]];

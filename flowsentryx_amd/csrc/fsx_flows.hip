@@ -259,10 +259,10 @@ hipError_t launch_flows(const uint64_t *S, const uint64_t *pay, BatchState *bs, 
                         uint32_t *span_list, void *acc, uint8_t *keys16, uint8_t *fam, float *feat,
                         float *prob, uint8_t *dec, uint32_t cap, const ScoreParams &P, uint32_t salt,
                         uint32_t n, void *sacc, uint32_t epoch, const uint32_t *seg_slot, bool light_only,
-                        const uint32_t *seg_lo, uint32_t *seg_len, hipStream_t st) {
+                        const uint32_t *seg_lo, uint32_t *seg_len, const PartialOut &part, hipStream_t st) {
     (void)hipGetLastError();   // a stale error of another caller is not ours
     const FlowOut out{(FlowAcc *)acc, keys16, fam, feat, prob, dec, cap, (SlotAcc *)sacc, epoch, seg_slot, ts,
-                      seg_lo, seg_len};
+                      seg_lo, seg_len, part};
     const uint32_t nsub = (n + kFT - 1) / kFT;
     const uint32_t grid = std::max<uint32_t>(1, std::min<uint32_t>(FSX_FLOW_TILE_BLOCKS, (nsub + 3) / 4));
     k_flow_tile<<<grid, 256, 0, st>>>(S, pay, bs, headf, len, ts, in, tile_off, sub_cnt, seg_start,
@@ -417,6 +417,42 @@ __global__ __launch_bounds__(256) void k_flows_end(const SlotAcc *__restrict__ s
         const Slot &sl = table[s];
         write_row((uint32_t)g, a, sl.tag, sl.key, m.dport, out, P);
     }
+}
+
+// Accumulate mode: partial i of m (distinct sources) merges into its source's SlotAcc of the
+// epoch as the call after everything merged so far (the flow_finish merge, with the partial's
+// own first / last timestamps); a source absent from the table is skipped.
+__global__ __launch_bounds__(256) void k_flows_merge(const FlowPartial *__restrict__ part, uint32_t m,
+                                                     const Slot *__restrict__ table, Limits lim, SlotAcc *sacc,
+                                                     uint32_t epoch) {
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < m; i += gridDim.x * 256u) {
+        const FlowPartial p = part[i];
+        const uint32_t s = table_find(table, lim, p.tag, p.key);
+        if (s == kNoSlot || p.n == 0) continue;
+        SlotAcc &a = sacc[s];
+        if (a.epoch != epoch) {
+            a.n = p.n; a.s1 = p.s1; a.s2 = p.s2; a.d1 = p.d1; a.d2 = p.d2; a.dmax = p.dmax;
+            a.dport = p.dport;
+            a.epoch = epoch;
+        } else {
+            const uint64_t d = p.first_ts - a.last_t;
+            a.n += p.n; a.s1 += p.s1; a.s2 += p.s2;
+            a.d1 += p.d1 + (u128)d;
+            a.d2 += p.d2 + (u128)d * d;
+            const uint64_t mx = p.dmax > d ? p.dmax : d;
+            a.dmax = mx > a.dmax ? mx : a.dmax;
+        }
+        a.last_t = p.last_ts;
+    }
+}
+
+hipError_t launch_flows_merge(const void *partials, uint32_t m, const Slot *table, const Limits &lim, void *sacc,
+                              uint32_t epoch, hipStream_t st) {
+    (void)hipGetLastError();
+    if (m == 0) return hipSuccess;
+    k_flows_merge<<<std::min<uint32_t>(1024, (m + 255) / 256), 256, 0, st>>>(
+        static_cast<const FlowPartial *>(partials), m, table, lim, static_cast<SlotAcc *>(sacc), epoch);
+    return hipGetLastError();
 }
 
 hipError_t launch_flows_end(const void *sacc, uint32_t epoch, const Slot *table, uint64_t slots,

@@ -235,6 +235,24 @@ __host__ __device__ inline uint64_t probe_start(uint32_t tag, const uint32_t k[4
     return slot_hash(tag, k, seed) & mask;
 }
 
+// Slot of (tag, key) in the table (linear probing from its probe start), or kNoSlot.
+__device__ inline bool slot_key_eq(const Slot &s, uint32_t tag, const uint32_t k[4]) {
+    return s.tag == tag && s.key[0] == k[0] && s.key[1] == k[1] && s.key[2] == k[2] &&
+           s.key[3] == k[3];
+}
+
+__device__ inline uint32_t table_find(const Slot *table, const Limits &lim, uint32_t tag,
+                                               const uint32_t k[4]) {
+    uint64_t i = probe_start(tag, k, lim.seed, lim.table_mask, lim.test_flags);
+    for (uint64_t probes = 0; probes <= lim.table_mask; ++probes) {
+        const uint32_t t = table[i].tag;
+        if (t == 0) return kNoSlot;
+        if (t == tag && slot_key_eq(table[i], tag, k)) return (uint32_t)i;
+        i = (i + 1) & lim.table_mask;
+    }
+    return kNoSlot;
+}
+
 // packed sort word: bucket << 56 | source id << 32 | family << 31 | arrival index
 // (n <= 2^31 - 1; ids < 2^32, max_entries <= 2^31); the source id is the source's slot in the id table (k_parse), so equal
 // ids <=> equal (family, address) and the sort needs only log2(slots) key bits. The
@@ -307,13 +325,18 @@ struct Scratch {
                            // packets [kSketch] each (counts zeroed by k_heavy_pick after use)
     HeavySet *heavy;
     void *heavy_flow;      // heavy sources' flow chunk sums (heavy_flow_bytes)
-    // light-bin tail (fsx_bins.hip; tables of 2^17..2^21 slots, else null)
+    // bin sort (fsx_bins.hip; fixed window, tables of 2^17..2^21 slots, else null)
     uint32_t *bin_start;   // bins + 1
-    uint64_t *bin_mask;    // bins
-    uint32_t *bin_row;     // bins
     uint32_t *bin_order;   // bins
-    void *bin_stage;       // per table slot: FlowAcc (bin_stage_bytes)
     uint64_t cap;          // packets the scratch is sized for
+};
+
+// Flow partials (fsx_flow_partials_records_device): every source's raw sums go to the run of
+// its owner rank (G runs of cap partials, cnt[o] per run) instead of a row.
+struct PartialOut {
+    void *buf;
+    uint32_t cap, G;
+    unsigned long long *cnt;
 };
 
 // Optional per-source outputs of a batch (flow features + q8 scores), device pointers.
@@ -330,6 +353,7 @@ struct FlowRequest {
     // its table slot's SlotAcc of this epoch instead of becoming an output row
     void *sacc;
     uint32_t epoch;
+    PartialOut part;  // (buf null: rows / accumulate as above)
 };
 
 // do_limit: run the rate limiter (verdicts + maps); flows: also per-source features.
@@ -395,8 +419,7 @@ struct TailArgs {
     int npass;
     uint32_t gridTiles;
     int last[3];
-    bool bins;             // light-bin tail (sort passes 0-1 only, fsx_bins.hip)
-    uint32_t binbits;
+    bool bins;             // sort pass 2 as the tail's bin sort (fsx_bins.hip)
 };
 hipError_t launch_tail(const TailArgs &a);
 
@@ -443,7 +466,7 @@ hipError_t launch_flows(const uint64_t *S, const uint64_t *pay, BatchState *bs, 
                         uint32_t *span_list, void *acc, uint8_t *keys16, uint8_t *fam, float *feat,
                         float *prob, uint8_t *dec, uint32_t cap, const ScoreParams &P, uint32_t salt,
                         uint32_t n, void *sacc, uint32_t epoch, const uint32_t *seg_slot, bool light_only,
-                        const uint32_t *seg_lo, uint32_t *seg_len, hipStream_t st);
+                        const uint32_t *seg_lo, uint32_t *seg_len, const PartialOut &part, hipStream_t st);
 // Heavy verdict lists: the heavy sources' flow sums right after sort pass 0, their rows
 // after the heads (fsx_flows.hip "heavy sources"); scratch of heavy_flow_bytes(cap).
 size_t heavy_flow_bytes(uint64_t cap);
@@ -459,6 +482,9 @@ hipError_t launch_flows_heavy_finish(const uint64_t *S, const BatchState *bs, co
 
 size_t flow_acc_bytes();
 size_t slot_acc_bytes();
+// Accumulate mode: merge m flow partials (fsx_flow_partial) into the epoch's per-slot sums.
+hipError_t launch_flows_merge(const void *partials, uint32_t m, const Slot *table, const Limits &lim, void *sacc,
+                              uint32_t epoch, hipStream_t st);
 // Rows of every source accumulated in epoch `epoch` (slots of the table), *d_count = rows.
 hipError_t launch_flows_end(const void *sacc, uint32_t epoch, const Slot *table, uint64_t slots,
                             uint8_t *keys16, uint8_t *fam, float *feat, float *prob, uint8_t *dec,

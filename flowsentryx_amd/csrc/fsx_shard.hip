@@ -88,9 +88,12 @@ __device__ __forceinline__ const ShardBlock *replica_find(const Replica &r, uint
 // replica: till > 0 and now <= till, src/fsx_kern.c:189-215 — exact when the clock is
 // monotone over the batches so far, which the host checks before asking for it),
 // 4 / 6 an IP packet for its owner.
+// (fam: the family 4 / 6 of an IP packet, also of a replica-dropped one)
 __device__ __forceinline__ uint32_t shard_classify(const uint8_t *rec, uint32_t L, uint64_t now,
-                                                   const Replica *rep, uint32_t k[4], uint32_t &dport) {
+                                                   const Replica *rep, uint32_t k[4], uint32_t &dport,
+                                                   uint32_t &fam) {
     const uint32_t f = shard_parse(rec, L, k, dport);
+    fam = f;
     if (f >= 4 && rep) {
         const ShardBlock *b = replica_find(*rep, f == 6 ? 2u : 1u, k);
         if (b && b->till > 0 && !(now > b->till)) return 2;
@@ -116,11 +119,11 @@ __global__ __launch_bounds__(256) void k_shard_parse(const uint8_t *__restrict__
                                                      uint8_t *__restrict__ verdict,
                                                      uint8_t *__restrict__ own8,
                                                      ShardRecord16 *__restrict__ crec,
-                                                     uint64_t *__restrict__ owner_total) {
+                                                     uint64_t *__restrict__ owner_total, uint32_t drop_rec) {
     __shared__ uint32_t s_rec[4][64 * 17];
-    __shared__ uint32_t sh[kMaxShards];
+    __shared__ uint32_t sh[kMaxShards + 1];
     const uint32_t t = blockIdx.x, lane = lane_id(), w = threadIdx.x >> 6;
-    if (threadIdx.x < kMaxShards) sh[threadIdx.x] = 0;
+    if (threadIdx.x <= kMaxShards) sh[threadIdx.x] = 0;
     __syncthreads();
     uint32_t *rec = s_rec[w];
     bool need_wide = false;
@@ -143,15 +146,16 @@ __global__ __launch_bounds__(256) void k_shard_parse(const uint8_t *__restrict__
             // L4 port bytes)
             const uint32_t L = len[i];
             const uint64_t now = ts[i];
-            uint32_t k[4], dp;
+            uint32_t k[4], dp, fam;
             const uint32_t f = shard_classify(reinterpret_cast<const uint8_t *>(rec + lane * 17u), L, now,
-                                              use_rep ? &rep : nullptr, k, dp);
+                                              use_rep ? &rep : nullptr, k, dp, fam);
             uint8_t o = 0xFFu;
-            if (f >= 4) {
-                o = (uint8_t)owner_dev(f, k, G);
+            // an IP packet for its owner, or (drop_rec) a replica-dropped one for group G
+            if (f >= 4 || (f == 2 && drop_rec)) {
+                o = (uint8_t)(f >= 4 ? owner_dev(f, k, G) : G);
                 atomicAdd(&sh[o], 1u);
-                need_wide |= f == 6 || L > 0xFFFFu;
-                if (crec && f == 4) {
+                need_wide |= fam == 6 || L > 0xFFFFu;
+                if (crec && fam == 4) {
                     ShardRecord16 x;
                     x.key = k[0];
                     x.len = (uint16_t)L;
@@ -173,7 +177,7 @@ __global__ __launch_bounds__(256) void k_shard_parse(const uint8_t *__restrict__
     if (lane == 0 && filtered)
         atomicAdd(reinterpret_cast<unsigned long long *>(&owner_total[G]), (unsigned long long)filtered);
     __syncthreads();
-    if (threadIdx.x < G) cnt[(size_t)threadIdx.x * ntiles + t] = sh[threadIdx.x];
+    if (threadIdx.x < G + drop_rec) cnt[(size_t)threadIdx.x * ntiles + t] = sh[threadIdx.x];
 }
 
 // The first record slot of owner o: the totals of the owners before it.
@@ -191,11 +195,11 @@ __global__ __launch_bounds__(256) void k_shard_pack16(const uint8_t *__restrict_
                                                       const uint32_t *__restrict__ offs, uint32_t ntiles,
                                                       ShardRecord16 *__restrict__ rec,
                                                       uint32_t *__restrict__ send_idx,
-                                                      const uint64_t *__restrict__ owner_total) {
-    __shared__ uint32_t s_wc[4][kMaxShards];
+                                                      const uint64_t *__restrict__ owner_total, uint32_t Gx) {
+    __shared__ uint32_t s_wc[4][kMaxShards + 1];
     if (owner_total[G + 1] != 16u) return;   // wide slice: k_shard_pack places 32-byte records
     const uint32_t t = blockIdx.x, lane = lane_id(), w = threadIdx.x >> 6;
-    for (uint32_t o = threadIdx.x; o < 4 * kMaxShards; o += 256) (&s_wc[0][0])[o] = 0;
+    for (uint32_t o = threadIdx.x; o < 4 * (kMaxShards + 1); o += 256) (&s_wc[0][0])[o] = 0;
     __syncthreads();
     uint8_t ob[16];
     // (loading the records here too, 16 per lane, made the kernel slower: 0.70 -> 0.96 ms)
@@ -206,7 +210,7 @@ __global__ __launch_bounds__(256) void k_shard_pack16(const uint8_t *__restrict_
         if (ob[r] != 0xFFu) atomicAdd(&s_wc[w][ob[r]], 1u);
     }
     __syncthreads();
-    if (threadIdx.x < G) {   // exclusive over the waves, from the tile's owner base
+    if (threadIdx.x < Gx) {   // exclusive over the waves, from the tile's owner base
         const uint32_t o = threadIdx.x;
         uint32_t b = offs[(size_t)o * ntiles + t] + owner_base(owner_total, o);
         for (int k = 0; k < 4; ++k) {
@@ -223,7 +227,7 @@ __global__ __launch_bounds__(256) void k_shard_pack16(const uint8_t *__restrict_
         const uint32_t own = ob[r];
         const bool ip = own != 0xFFu;
         uint64_t peers = __ballot(ip);
-        for (uint32_t b = 0; (1u << b) < G; ++b) {
+        for (uint32_t b = 0; (1u << b) < Gx; ++b) {
             const bool bit = (own >> b) & 1u;
             const uint64_t bal = __ballot(ip && bit);
             peers &= bit ? bal : ~bal;
@@ -286,28 +290,31 @@ __global__ __launch_bounds__(256) void k_shard_pack(const uint8_t *__restrict__ 
                                                     uint32_t *__restrict__ send_idx,
                                                     uint8_t *__restrict__ verdict, Replica rep,
                                                     int use_rep, uint64_t *__restrict__ owner_total,
-                                                    int compact) {
+                                                    int compact, uint32_t drop_rec) {
     if (compact && owner_total[G + 1] == 16u) return;   // k_shard_pack16 places the records
-    __shared__ uint32_t s_base[kMaxShards];
-    __shared__ uint32_t s_wc[4][kMaxShards];
+    __shared__ uint32_t s_base[kMaxShards + 1];
+    __shared__ uint32_t s_wc[4][kMaxShards + 1];
     const uint32_t t = blockIdx.x, lane = lane_id(), w = threadIdx.x >> 6;
-    if (threadIdx.x < G) s_base[threadIdx.x] = offs[(size_t)threadIdx.x * ntiles + t] + owner_base(owner_total, threadIdx.x);
+    const uint32_t Gx = G + drop_rec;   // (group G: the replica-dropped packets)
+    if (threadIdx.x < Gx) s_base[threadIdx.x] = offs[(size_t)threadIdx.x * ntiles + t] + owner_base(owner_total, threadIdx.x);
     // wave w owns packets [t*4096 + w*1024, +1024) in arrival order: count per owner
     // first (so a wave places after the waves before it), then place in order
-    uint32_t of[16];   // owner << 4 | class (0 DROP, 1 PASS, 4/6 IP, 15 none)
-    for (uint32_t o = threadIdx.x; o < 4 * kMaxShards; o += 256) (&s_wc[0][0])[o] = 0;
+    uint32_t of[16];   // owner << 4 | class (0 DROP, 1 PASS, 4/6 IP, 8 | 4/6 replica-dropped IP, 15 none)
+    for (uint32_t o = threadIdx.x; o < 4 * (kMaxShards + 1); o += 256) (&s_wc[0][0])[o] = 0;
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
         const uint32_t i = t * kShardTile + w * 1024u + (uint32_t)r * 64u + lane;
         of[r] = 15u;
         if (i < n) {
-            uint32_t k[4], dp;
-            const uint32_t f = shard_classify(hdr + (size_t)i * 64, len[i], ts[i], use_rep ? &rep : nullptr, k, dp);
-            if (f >= 4) {
-                const uint32_t o = owner_dev(f, k, G);
-                of[r] = (o << 4) | f;
+            uint32_t k[4], dp, fam;
+            const uint32_t f = shard_classify(hdr + (size_t)i * 64, len[i], ts[i], use_rep ? &rep : nullptr, k, dp,
+                                              fam);
+            if (f >= 4 || (f == 2 && drop_rec)) {
+                const uint32_t o = f >= 4 ? owner_dev(f, k, G) : G;
+                of[r] = (o << 4) | (f >= 4 ? f : 8u | fam);
                 atomicAdd(&s_wc[w][o], 1u);
+                if (f == 2) verdict[i] = 1u;
             } else {
                 of[r] = f;
                 // parse DROP / non-IP PASS are never counted; a replica DROP is counted
@@ -317,7 +324,7 @@ __global__ __launch_bounds__(256) void k_shard_pack(const uint8_t *__restrict__ 
         }
     }
     __syncthreads();
-    if (threadIdx.x < G) {   // exclusive over the waves, from the tile's owner base
+    if (threadIdx.x < Gx) {   // exclusive over the waves, from the tile's owner base
         const uint32_t o = threadIdx.x;
         uint32_t b = s_base[o];
         for (int k = 0; k < 4; ++k) {
@@ -331,11 +338,12 @@ __global__ __launch_bounds__(256) void k_shard_pack(const uint8_t *__restrict__ 
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
         const uint32_t i = t * kShardTile + w * 1024u + (uint32_t)r * 64u + lane;
-        const uint32_t f = of[r] & 15u, own = of[r] >> 4;
-        const bool ip = f == 4u || f == 6u;
+        const uint32_t f = of[r] & 7u, own = of[r] >> 4;
+        const bool ip = (of[r] & 15u) != 15u && (f == 4u || f == 6u);
+        const bool dropped = (of[r] & 8u) != 0 && ip;
         // rank among this step's lanes with the same owner (ballots over the owner bits)
         uint64_t peers = __ballot(ip);
-        for (uint32_t b = 0; (1u << b) < G; ++b) {
+        for (uint32_t b = 0; (1u << b) < Gx; ++b) {
             const bool bit = (own >> b) & 1u;
             const uint64_t bal = __ballot(ip && bit);
             peers &= bit ? bal : ~bal;
@@ -357,7 +365,7 @@ __global__ __launch_bounds__(256) void k_shard_pack(const uint8_t *__restrict__ 
             x.pad = 0;
             reinterpret_cast<ShardRecord *>(rec)[slot] = x;
             send_idx[slot] = i;
-            verdict[i] = 2u;   // placeholder until the owner's verdict returns
+            if (!dropped) verdict[i] = 2u;   // placeholder until the owner's verdict returns
         }
     }
 }
@@ -427,7 +435,7 @@ __global__ void k_shard_empty(uint64_t *owner_total, uint32_t G, int compact) {
 hipError_t launch_shard_pack(const uint8_t *hdr, const uint32_t *len, const uint64_t *ts, uint32_t n,
                              uint32_t G, uint8_t *verdict, void *rec, uint32_t *send_idx,
                              uint64_t *owner_total, uint32_t *scratch, uint8_t *own8, void *crec,
-                             const Replica *rep, bool compact, hipStream_t st) {
+                             const Replica *rep, bool compact, bool drop_rec, hipStream_t st) {
     (void)hipGetLastError();   // a stale error of another caller is not ours
     k_shard_empty<<<1, 1, 0, st>>>(owner_total, G, compact);   // also the wide flag / filtered
     if (n == 0) return hipGetLastError();
@@ -437,14 +445,16 @@ hipError_t launch_shard_pack(const uint8_t *hdr, const uint32_t *len, const uint
     unsigned long long *wide = compact ? reinterpret_cast<unsigned long long *>(owner_total + G + 1) : nullptr;
     if (wide) k_shard_fmt_init<<<1, 1, 0, st>>>(wide);
     ShardRecord16 *cr = compact ? reinterpret_cast<ShardRecord16 *>(crec) : nullptr;
+    const uint32_t dr = drop_rec && use ? 1u : 0u;   // (records of the replica drops: group G)
     k_shard_parse<<<ntiles, 256, 0, st>>>(hdr, len, ts, n, G, scratch, ntiles, r, use, wide, verdict, own8, cr,
-                                          owner_total);
-    k_shard_scan<<<G, 1024, 0, st>>>(scratch, owner_total, G, ntiles, compact);
+                                          owner_total, dr);
+    k_shard_scan<<<G + dr, 1024, 0, st>>>(scratch, owner_total, G, ntiles, compact);
     if (compact)
         k_shard_pack16<<<ntiles, 256, 0, st>>>(own8, cr, n, G, scratch, ntiles,
-                                               reinterpret_cast<ShardRecord16 *>(rec), send_idx, owner_total);
+                                               reinterpret_cast<ShardRecord16 *>(rec), send_idx, owner_total,
+                                               G + dr);
     k_shard_pack<<<ntiles, 256, 0, st>>>(hdr, len, ts, n, G, scratch, ntiles, rec, send_idx, verdict, r,
-                                         use, owner_total, compact);
+                                         use, owner_total, compact, dr);
     return hipGetLastError();
 }
 

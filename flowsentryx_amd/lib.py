@@ -137,6 +137,8 @@ def load_library() -> C.CDLL:
         "fsx_flow_features": (C.c_int, [vp, vp, vp, vp, sz, sz, vp, vp, vp, C.POINTER(sz)]),
         "fsx_flows_begin": (C.c_int, [vp]),
         "fsx_flows_end": (C.c_int, [vp, vp, vp, vp, vp, vp, sz, vp]),
+        "fsx_flow_partials_records_device": (C.c_int, [vp, vp, sz, C.c_uint32, C.c_uint32, vp, sz, vp]),
+        "fsx_flows_merge_device": (C.c_int, [vp, vp, sz]),
         "fsx_last_timings": (C.c_int, [vp, vp, vp, vp, C.c_int, C.c_int, C.POINTER(C.c_int)]),
         "fsx_enable_timing": (C.c_int, [vp, C.c_int]),
         "fsx_last_batch_info": (C.c_int, [vp, vp, C.c_int]),
@@ -166,7 +168,7 @@ ABI_SYMBOLS = [
     "fsx_map_lookup", "fsx_map_update", "fsx_map_update_batch", "fsx_map_delete", "fsx_map_dump",
     "fsx_get_stats",
     "fsx_reset", "fsx_load_q8_model", "fsx_score", "fsx_score_device", "fsx_flow_features",
-    "fsx_flows_begin", "fsx_flows_end",
+    "fsx_flows_begin", "fsx_flows_end", "fsx_flow_partials_records_device", "fsx_flows_merge_device",
     "fsx_last_timings", "fsx_enable_timing", "fsx_last_batch_info",
     "fsx_shard_owner", "fsx_shard_pack_device", "fsx_shard_unpack_device", "fsx_shard_unpack16_device",
     "fsx_shard_scatter_device", "fsx_shard_clock_device", "fsx_blocklist_export_device",
@@ -178,6 +180,8 @@ SHARD_RECORD16_BYTES = 16
 SHARD_BLOCK_BYTES = 32
 SHARD_FILTER_BLOCKLIST = 1
 SHARD_COMPACT = 2
+SHARD_DROP_RECORDS = 4
+FLOW_PARTIAL_BYTES = 112
 MAX_SHARDS = 64
 
 
@@ -475,6 +479,18 @@ class FsxContext:
         """Rows of every source accumulated since flows_begin (device pointers, async)."""
         self._check(self._lib.fsx_flows_end(self._h, d_keys16, d_family, d_features, d_prob,
                                             d_malicious, cap, d_rows), "fsx_flows_end")
+
+    def flow_partials_records_device(self, d_records: int, n: int, rec_bytes: int, n_shards: int,
+                                     d_partials: int, cap_per_shard: int, d_counts: int):
+        """Flow partial (raw sums, first / last ts) of every source of n records, into the run
+        of its owner (n_shards runs of cap_per_shard; d_counts[o] per run). No map state."""
+        self._check(self._lib.fsx_flow_partials_records_device(self._h, d_records, n, rec_bytes, n_shards,
+                                                               d_partials, cap_per_shard, d_counts),
+                    "fsx_flow_partials_records_device")
+
+    def flows_merge_device(self, d_partials: int, m: int):
+        """Between flows_begin and flows_end: merge m partials (distinct sources) in order."""
+        self._check(self._lib.fsx_flows_merge_device(self._h, d_partials, m), "fsx_flows_merge_device")
 
     BATCH_INFO = ("ip_packets", "sources", "new_sources", "any_ipv6", "non_monotone",
                   "max_len", "max_ts", "allowed", "dropped", "prefix_rule_drops", "sorted_payload",

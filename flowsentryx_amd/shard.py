@@ -26,7 +26,15 @@ unchanged batch pipeline on all of that source's packets:
   7. with flow features (HipShardEngine.enable_flows): every owner accumulates its sources'
      sums over the batch's sub-batches (fsx_flows_begin / fsx_flows_end) and writes one row
      per owned source at the end of the batch — the row the 1-GPU run over the whole batch
-     gives; the replica filter (5) is off then, so every packet reaches its owner
+     gives. The packets a replica drops at arrival (5) still count in their source's
+     features: the pack keeps them as records, the arrival rank turns them into one flow
+     partial per source (fsx_flow_partials_records_device: exact sums, first / last
+     timestamp), the partials go to the owners (one small all-to-all) and merge into the
+     owner's sums (fsx_flows_merge_device, sender ranks in order) before the owner's own
+     records of that sub-batch. Exact because a replica drops a source's packets exactly
+     while now <= till, and the filter is only used where the clock is non-decreasing in
+     global order: the dropped packets of a source are the first of its packets in the
+     sub-batch, and in rank order
 
 A global batch is cut into `chunks` sub-batches; in sub-batch i every rank contributes
 the i-th piece of its slice, and the global order of a sub-batch is rank 0's piece,
@@ -98,6 +106,11 @@ class HipShardEngine:
         self._oh = None  # owner-side header/len/ts buffers, grown on demand
         self._ov = {}             # owner-side verdicts per slot
         self.flows = None
+        # arrival side of the replica filter with flows: a flow-only context for the partials
+        # of the replica-dropped packets, its output buffers per pipeline slot
+        self.pctx = None
+        self.pctx_entries = 0
+        self.pbufs, self.pcnts = {}, {}
 
     # -- streams of the pipelined plane (the CPU engine has none)
     @contextlib.contextmanager
@@ -214,12 +227,15 @@ class HipShardEngine:
         self.ctx.blocklist_export_device(buf.data_ptr() + B, cap, buf.data_ptr())
         return buf
 
-    def pack(self, hdr, length, ts, n, G, verdict, filt=False, slot=0):
+    def pack(self, hdr, length, ts, n, G, verdict, filt=False, slot=0, drop_rec=False):
         """-> records, counts[G + 2] (counts[G]: packets dropped by the replica,
-        counts[G + 1]: record bytes, 16 or 32), in pipeline slot `slot`."""
+        counts[G + 1]: record bytes, 16 or 32), in pipeline slot `slot`. drop_rec: the
+        dropped packets' records follow the owners' runs."""
         if n > self.max_local:
             raise ValueError(f"local slice of {n} packets exceeds {self.max_local}")
         flags = lib.SHARD_COMPACT | (lib.SHARD_FILTER_BLOCKLIST if filt else 0)
+        if filt and drop_rec:
+            flags |= lib.SHARD_DROP_RECORDS
         if slot not in self.recs or self.send_idxs[slot].numel() < max(1, n):
             m = max(1, n)
             self.recs[slot] = torch.empty(m * REC, dtype=torch.uint8, device=self.device)
@@ -231,6 +247,33 @@ class HipShardEngine:
                                    verdict.data_ptr(), rec.data_ptr(), idx.data_ptr(), cnt.data_ptr(),
                                    flags)
         return rec, cnt[:G + 2]
+
+    def partials(self, rec, first, m, rb, G, cap, slot=0):
+        """Flow partials of the m replica-dropped records from record index `first` of a pack
+        buffer: G runs of cap partials (source -> run of its owner) and counts[G]; enqueued
+        on the engine stream (no host synchronization)."""
+        if self.pctx is None or self.pctx_entries < cap:
+            if self.pctx is not None:
+                self.pctx.sync()
+                self.pctx.close()
+            ent = max(1024, 2 * cap)
+            self.pctx = lib.FsxContext(max_batch=max(1, self.max_local), max_entries=ent,
+                                       device=self.device.index or 0)
+            self.pctx.set_stream(self.stream.cuda_stream)
+            self.pctx_entries = ent
+        B = lib.FLOW_PARTIAL_BYTES
+        if self.pbufs.get(slot) is None or self.pbufs[slot].numel() < G * cap * B:
+            self.pbufs[slot] = torch.empty(max(1, G * cap * B), dtype=torch.uint8, device=self.device)
+            self.pcnts[slot] = torch.empty(G, dtype=torch.int64, device=self.device)
+        buf, cnt = self.pbufs[slot], self.pcnts[slot]
+        self.pctx.flow_partials_records_device(rec.data_ptr() + first * rb, m, rb, G, buf.data_ptr(), cap,
+                                               cnt.data_ptr())
+        return buf, cnt
+
+    def merge(self, parts: torch.Tensor, m: int):
+        """Merge m received partials (one sender's, distinct sources) into the owner's sums."""
+        if m:
+            self.ctx.flows_merge_device(parts.data_ptr(), m)
 
     def export_blocklist(self) -> tuple[torch.Tensor, int]:
         """This rank's live blacklist entries (32-byte records) and their count."""
@@ -310,6 +353,8 @@ class ShardedDataPlane:
         self.last_exchange = None
         self.formats = set()       # record sizes received (16 / 32)
         self.blk_cap = 1024        # blocklist entries per rank of one all-gather (grows)
+        self.rep_size = 0          # entries of the last replica (bounds the dropped sources)
+        self.partials_sent = 0     # flow partials sent for replica-dropped packets
 
     def verdict_batch(self, hdr, length, ts, n: int, verdict, chunks: int = 1, bounds=None):
         """Verdicts for this rank's slice (arrival order) of one global batch; every rank
@@ -327,9 +372,9 @@ class ShardedDataPlane:
                     f = self.engine.flows
                     f["rows"].fill_(-1)   # (count: ctx.last_batch_info()["sources"])
                 return
-            # with flow features every packet must reach its source's owner (the features
-            # are over all of the source's packets), so the replica filter is off
-            filt_on = self.filter and not flows
+            # with flow features the replica-dropped packets reach their owner as flow
+            # partials (step 7 of the module doc)
+            filt_on = self.filter
             if flows:
                 self.engine.flows_begin()
             if filt_on:
@@ -353,12 +398,12 @@ class ShardedDataPlane:
                 return
             filt = self._filter_plan(ts, bounds)
             pend = [None] * k
-            pend[0] = self._stage_exchange(hdr, length, ts, verdict, bounds, 0, filt[0])
+            pend[0] = self._stage_exchange(hdr, length, ts, verdict, bounds, 0, filt[0], flows)
             sent = recv = 0
             for j in range(k):
                 if j + 1 < k:   # enqueued before the owner work of j: its exchange overlaps it
                     pend[j + 1] = self._stage_exchange(hdr, length, ts, verdict, bounds, j + 1,
-                                                       filt[j + 1])
+                                                       filt[j + 1], flows)
                 ms, mr = self._stage_owner(verdict, bounds, j, pend[j])
                 pend[j] = None
                 sent, recv = sent + ms, recv + mr
@@ -445,15 +490,17 @@ class ShardedDataPlane:
                     off += nb
                     if c:
                         self.formats.add(f)
-                pend.append((recv, segs, sc, rc, arrived))
+                pend.append((recv, segs, sc, rc, arrived, None))
         return pend
 
-    def _stage_exchange(self, hdr, length, ts, verdict, bounds, j: int, filt: bool):
-        """Pack sub-batch j (engine stream) and exchange its counts and records (comm stream)."""
+    def _stage_exchange(self, hdr, length, ts, verdict, bounds, j: int, filt: bool, flows: bool = False):
+        """Pack sub-batch j (engine stream) and exchange its counts and records (comm stream);
+        with flows and the filter, also the flow partials of the replica-dropped packets."""
         G, e = self.world, self.engine
         a, b = bounds[j], bounds[j + 1]
         slot = j % 2
-        recs, counts = e.pack(hdr[a * 64:], length[a:], ts[a:], b - a, G, verdict[a:], filt, slot)
+        drop = flows and filt   # (the same on every rank: the filter plan is global)
+        recs, counts = e.pack(hdr[a * 64:], length[a:], ts[a:], b - a, G, verdict[a:], filt, slot, drop)
         with e.comm_ctx():
             # per-owner counts with the record format in the low bit; the host reads its
             # own and the received counts together (one synchronization, comm stream)
@@ -470,6 +517,8 @@ class ShardedDataPlane:
             rf = [lib.SHARD_RECORD16_BYTES if x & 1 else lib.SHARD_RECORD_BYTES for x in rw]
             in_b = [x * rb for x in sc]
             out_b = [c * f for c, f in zip(rc, rf)]
+        partial = self._exchange_partials(recs, sum(sc), int(cnt[G]), rb, slot) if drop else None
+        with e.comm_ctx():
             recv = e.recv_buffer(sum(out_b))
             _a2a(recv[:sum(out_b)], recs[:sum(in_b)], out_b, in_b, self.group)
         arrived = e.comm_event()      # only these records: the owner work of the previous
@@ -479,18 +528,46 @@ class ShardedDataPlane:
             off += nb
             if c:
                 self.formats.add(f)
-        return recv, segs, sc, rc, arrived
+        return recv, segs, sc, rc, arrived, partial
+
+    def _exchange_partials(self, recs, first: int, m: int, rb: int, slot: int):
+        """The flow partials of this rank's m replica-dropped records (engine stream), their
+        per-owner counts (all-to-all + one host read) and the partials (all-to-all), on the
+        comm stream -> (received partials, per sender)."""
+        G, e = self.world, self.engine
+        B = lib.FLOW_PARTIAL_BYTES
+        cap = max(1, self.rep_size)   # every dropped source is a replica entry
+        buf, pcnt = e.partials(recs, first, m, rb, G, cap, slot)
+        with e.comm_ctx():
+            prc = torch.empty_like(pcnt)
+            _a2a(prc, pcnt, [1] * G, [1] * G, self.group)
+            both = torch.cat([pcnt, prc]).tolist()
+            ps, pr = [int(x) for x in both[:G]], [int(x) for x in both[G:]]
+            if max(ps) > cap:
+                raise RuntimeError(f"flow partials overflow: {max(ps)} sources for {cap} replica entries")
+            send = torch.cat([buf[o * cap * B:(o * cap + ps[o]) * B] for o in range(G)])
+            precv = e.recv_buffer(sum(pr) * B)
+            _a2a(precv[:sum(pr) * B], send, [x * B for x in pr], [x * B for x in ps], self.group)
+        self.partials_sent += sum(ps)
+        return precv, pr
 
     def _stage_owner(self, verdict, bounds, j: int, pend, slot=None):
         """Owner pipeline of sub-batch j (engine stream), verdicts back (comm stream) and
         into arrival positions (engine stream)."""
         G, e = self.world, self.engine
-        recv, segs, sc, rc, arrived = pend
+        recv, segs, sc, rc, arrived, partial = pend
         a = bounds[j]
         slot = j % 2 if slot is None else slot
         ms, mr = sum(sc), sum(rc)
-        e.engine_wait(arrived)        # the records of sub-batch j have arrived
+        e.engine_wait(arrived)        # the records (and partials) of sub-batch j have arrived
         e.keep(recv)                  # allocated on the comm stream, read on the engine's
+        if partial is not None:       # the replica-dropped packets' sums first, senders in order
+            precv, pr = partial
+            e.keep(precv)
+            off = 0
+            for r in range(G):
+                e.merge(precv[off * lib.FLOW_PARTIAL_BYTES:], pr[r])
+                off += pr[r]
         v = e.owner_batch(recv, segs, slot)
         with e.comm_ctx():
             ret = torch.empty(max(ms, 1), dtype=torch.uint8, device=v.device)
@@ -514,6 +591,7 @@ class ShardedDataPlane:
             if max(sizes) <= cap:
                 break
             self.blk_cap = 2 * max(sizes)
+        self.rep_size = sum(sizes)
         parts = [allb[r * per + B: r * per + B + sizes[r] * B] for r in range(G) if sizes[r]]
         if parts:
             e.load_replica(torch.cat(parts), sum(sizes))

@@ -271,6 +271,7 @@ uint32_t fsx_shard_owner(const uint8_t *key16, int family, uint32_t n_shards);
 #define FSX_SHARD_BLOCK_BYTES 32    /* {u32 key[4]; u64 till; u32 tag (1 v4, 2 v6); u32 pad} */
 #define FSX_SHARD_FILTER_BLOCKLIST 1u
 #define FSX_SHARD_COMPACT 2u
+#define FSX_SHARD_DROP_RECORDS 4u
 
 /* Parse a device batch and partition its IP packets by owner, stable in arrival order:
  * d_records (n * 32 bytes capacity) receives the records owner by owner, d_send_idx the
@@ -283,11 +284,40 @@ uint32_t fsx_shard_owner(const uint8_t *key16, int family, uint32_t n_shards);
  * when timestamps are non-decreasing over all batches so far (fsx_shard_clock_device).
  * With FSX_SHARD_COMPACT, d_counts has n_shards + 2 entries and d_counts[n_shards + 1]
  * receives the record size written: FSX_SHARD_RECORD16_BYTES when no IP packet of the
- * slice is IPv6 or 64 KiB or longer, else FSX_SHARD_RECORD_BYTES. */
+ * slice is IPv6 or 64 KiB or longer, else FSX_SHARD_RECORD_BYTES. With
+ * FSX_SHARD_DROP_RECORDS (and the filter), the replica-dropped packets are written as
+ * records too, after every owner's run, in arrival order (d_counts[n_shards] of them; the
+ * first sum(d_counts[0..n_shards)) records are the ones to send), so the arrival rank can
+ * take their flow sums (fsx_flow_partials_records_device). */
 int fsx_shard_pack_device(fsx_ctx *ctx, const uint8_t *d_hdr, const uint32_t *d_len,
                           const uint64_t *d_ts, size_t n, uint32_t n_shards, uint32_t flags,
                           uint8_t *d_verdict, void *d_records, uint32_t *d_send_idx,
                           uint64_t *d_counts);
+/* Flow partial: the exact flow sums of one source over a run of its packets
+ * in arrival order, with the run's first / last timestamp and its first packet's L4
+ * destination port; u128 sums as {low, high} u64 words. */
+#define FSX_FLOW_PARTIAL_BYTES 112
+typedef struct fsx_flow_partial {
+    uint32_t key[4];       /* raw source address words (IPv4: key[0]) */
+    uint32_t tag;          /* 1 IPv4, 2 IPv6 */
+    uint32_t dport;
+    uint64_t n, s1, dmax;  /* packets, sum of frame lengths, largest inter-arrival time */
+    uint64_t first_ts, last_ts;
+    uint64_t s2[2], d1[2], d2[2];   /* sum L^2, sum d, sum d^2 (d: inter-arrival ns) */
+} fsx_flow_partial;
+/* Arrival side of the blocklist filter with flow features: the flow partial of every
+ * source of n exchange records (rec_bytes FSX_SHARD_RECORD_BYTES or
+ * FSX_SHARD_RECORD16_BYTES, in arrival order) into the run of its owner: d_partials holds
+ * n_shards runs of cap_per_shard partials (run o from o * cap_per_shard), d_counts[o] =
+ * sources of owner o (beyond cap_per_shard: counted, not written). Touches no map state. */
+int fsx_flow_partials_records_device(fsx_ctx *ctx, const void *d_records, size_t n, uint32_t rec_bytes,
+                                     uint32_t n_shards, void *d_partials, size_t cap_per_shard,
+                                     uint64_t *d_counts);
+/* Owner side, between fsx_flows_begin and fsx_flows_end: merge m partials of distinct
+ * sources into their running sums, as if the partial's packets were processed right after
+ * everything merged so far (a source absent from the maps is skipped: the protocol sends
+ * partials only for sources of this owner's blocklist). */
+int fsx_flows_merge_device(fsx_ctx *ctx, const void *d_partials, size_t m);
 /* d_out3 = {min ts, max ts, 1 if some ts decreases in arrival order}. */
 int fsx_shard_clock_device(fsx_ctx *ctx, const uint64_t *d_ts, size_t n, uint64_t *d_out3);
 /* Every live blacklist entry (till > 0) of this context's maps as FSX_SHARD_BLOCK_BYTES

@@ -67,6 +67,19 @@ def check(d):
         top = sorted(((float(r["TotalDurationNs"]) / max(1, batches) / 1e6, r["Name"].split("(")[0].split("::")[-1])
                       for r in rows if "fsx::" in r["Name"]), reverse=True)[:8]
         out["pipeline"]["top_kernels_ms_per_batch"] = [(n, round(t, 4)) for t, n in top]
+    # legs measured beside the headline: recompute each pipeline fraction from its own
+    # bytes per step and ms per step (as printed under the profiler)
+    legs = {}
+    for name, leg in (("config3.from_stream", (line.get("config3") or {}).get("from_stream")),
+                      ("config4", line.get("config4")), ("config5", line.get("config5"))):
+        rf_ = (leg or {}).get("roofline") or {}
+        if rf_.get("bytes_per_step") and leg.get("ms_per_step"):
+            ach = rf_["bytes_per_step"] / (leg["ms_per_step"] * 1e-3) / 1e9
+            legs[name] = {"bytes_per_step": rf_["bytes_per_step"], "ms_per_step": leg["ms_per_step"],
+                          "achieved_GBps": round(ach, 1), "frac": round(ach / rf_["peak"], 4),
+                          "frac_bench_line": rf_.get("frac")}
+    if legs:
+        out["legs"] = legs
     return out
 
 

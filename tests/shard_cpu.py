@@ -99,7 +99,8 @@ class CpuShardEngine:
         buf[32:32 + k * 32] = ent[:k * 32]
         return buf
 
-    def pack(self, hdr, length, ts, n, G, verdict, filt=False, slot=0):
+    def pack(self, hdr, length, ts, n, G, verdict, filt=False, slot=0, drop_rec=False):
+        # (drop_rec: the HIP engine's flow partials of replica drops; no flows on the CPU engine)
         h, l, t = self._np(hdr, length, ts, n)
         cls, keys = self.oracle.parse(h, l)
         v = verdict.numpy()

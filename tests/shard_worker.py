@@ -132,7 +132,8 @@ def worker(rank, world, port, spec, out_path, engine_kind):
                     msg.append(f"map {m}: {len(union)} vs {len(o.map_dump(m))} entries differ")
             with open(out_path, "w") as f:
                 json.dump({"ok": ok, "msg": msg, "stats": list(stats),
-                           "filtered": plane.filtered, "formats": sorted(plane.formats)}, f)
+                           "filtered": plane.filtered, "formats": sorted(plane.formats),
+                           "partials": plane.partials_sent}, f)
         dist.barrier()
     finally:
         dist.destroy_process_group()

@@ -80,23 +80,27 @@ def test_sharded_hip_owners(tmp_path, world):
 @pytest.mark.parametrize("world,v6", [(2, 0.0), (3, 0.3)])
 def test_sharded_flow_features_equal_one_gpu(tmp_path, world, v6):
     """Per-source features + q8 scores under sharding: every owner accumulates its sources
-    over the batch's sub-batches (fsx_flows_begin / fsx_flows_end); the union of the rows
-    equals the 1-GPU rows over each whole global batch, bit for bit."""
+    over the batch's sub-batches (fsx_flows_begin / fsx_flows_end); the replica still drops
+    blacklisted packets at their arrival rank, whose flow partials merge into the owners'
+    sums first; the union of the rows equals the 1-GPU rows over each whole global batch,
+    bit for bit."""
     spec = dict(BASE, v6_frac=v6, nonip_frac=0.03, short_frac=0.02, seed=29 + world, flows=True,
                 cfg=dict(pps_threshold=7, window_ns=200_000, block_ns=1_000_000, max_entries=4096),
                 owner_batch=4096)
     res = run_sharded(tmp_path, world, spec, engine="hip")
-    assert res["filtered"] == 0   # (flows: every packet reaches its owner)
+    assert res["filtered"] > 0 and res["partials"] > 0   # dropped at arrival, still in the features
 
 
-def test_sharded_flow_features_heavy_path(tmp_path):
+@pytest.mark.parametrize("filt", [True, False])
+def test_sharded_flow_features_heavy_path(tmp_path, filt):
     """The same with a table of 2^17 slots, so every owner runs the heavy-source sort, the
-    heavy verdict lists and the heavy runs' flow sums (k_flow_heavy) in accumulate mode."""
-    spec = dict(BASE, n_ips=600, v6_frac=0.2, nonip_frac=0.02, seed=41, flows=True,
+    heavy verdict lists and the heavy runs' flow sums (k_flow_heavy) in accumulate mode; with
+    and without the replica filter (without it every packet reaches its owner)."""
+    spec = dict(BASE, n_ips=600, v6_frac=0.2, nonip_frac=0.02, seed=41, flows=True, filter=filt,
                 cfg=dict(pps_threshold=40, window_ns=2_000_000, block_ns=5_000_000, max_entries=1 << 16),
                 owner_batch=1 << 15)
     res = run_sharded(tmp_path, 2, spec, engine="hip")
-    assert res["filtered"] == 0
+    assert (res["filtered"] > 0) == filt
 
 
 def test_sharded_hip_owners_limiters(tmp_path):
