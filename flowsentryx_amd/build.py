@@ -30,12 +30,12 @@ COMMON = [
 
 LIBS = {
     "libfsx_hip.so": ["fsx_device.hip", "fsx_limiters.hip", "fsx_shard.hip", "fsx_pcap.hip",
-                      "fsx_flows.hip", "fsx_bins.hip", "fsx_score.hip",
+                      "fsx_flows.hip", "fsx_score.hip",
                       "fsx_api.hip"],
     "libfsx_synth.so": ["fsx_synth.hip"],
 }
 HEADERS = ["fsx_internal.h", "fsx_synth_common.h", "fsx_dev_common.h", "fsx_q8.h", "fsx_seg.h", "fsx_shard.h", "fsx_walk.h",
-           "fsx_bins.h", "fsx_flow_common.h"]
+           "fsx_flow_common.h"]
 
 
 def _stale(out: Path, srcs: list[Path]) -> bool:

@@ -20,7 +20,6 @@
 
 #include "../../include/fsx_hip.h"
 #include "fsx_internal.h"
-#include "fsx_bins.h"
 #include "fsx_shard.h"
 
 using namespace fsx;
@@ -178,7 +177,6 @@ static void free_scratch(fsx_ctx *c) {
     hipFree(s.span_list); hipFree(s.sort_ctl); hipFree(s.gbase); hipFree(s.status);
     hipFree(s.lim_tiles); hipFree(s.sw_seg); hipFree(s.sketch); hipFree(s.heavy);
     hipFree(s.drop_list); hipFree(s.drop_cur); hipFree(s.heavy_flow);
-    hipFree(s.bin_start); hipFree(s.bin_order);
     s = Scratch{};
 }
 
@@ -224,14 +222,6 @@ static int alloc_scratch(fsx_ctx *c, uint64_t cap) {
     HIPCHK(c, hipMalloc(&s.heavy, sizeof(HeavySet)));
     HIPCHK(c, hipMemset(s.heavy, 0, sizeof(HeavySet)));
     HIPCHK(c, hipMalloc(&s.heavy_flow, heavy_flow_bytes(cap)));
-    // bin sort of the fixed window (fsx_bins.hip): tables of 2^17..2^21 slots
-    uint32_t idbits = 0;
-    while ((1ull << idbits) < c->slots) ++idbits;
-    if (c->cfg.limiter == FSX_LIMIT_FIXED_WINDOW && idbits >= kBinMinIdBits && idbits <= kBinMaxIdBits) {
-        const uint64_t nb = c->slots >> kBinSlotBits;
-        HIPCHK(c, hipMalloc(&s.bin_start, (nb + 1) * 4));
-        HIPCHK(c, hipMalloc(&s.bin_order, nb * 4));
-    }
     s.cap = cap;
     return 0;
 }

@@ -23,7 +23,6 @@
 #include "fsx_internal.h"
 #include "fsx_seg.h"
 #include "fsx_walk.h"
-#include "fsx_bins.h"
 #include "fsx_shard.h"
 
 #define XDP_DROP 1
@@ -150,7 +149,6 @@ struct DigitPlan {
     uint32_t shift[4], mask[4];
     uint32_t npass;
     uint32_t light_b;   // heavy sort: buckets below light_b are light (id digit 0); 0 = plain
-    uint32_t light_shift;   // the light bucket is id bits [light_shift, +log2 light_b)
 };
 
 // parse_ethhdr / parse_ip6hdr / parse_ip4hdr (src/parsing_helper.h:49-136, dispatch
@@ -575,7 +573,7 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
         uint64_t out = ((uint64_t)(id & idt.mask) << 32) | ((uint64_t)(tag - 1u) << 31) | i;
         if (dp.light_b)   // heavy-source sort: the first pass's bucket in bits 56..63
             out |= (uint64_t)(hidx >= 0 ? dp.light_b + (uint32_t)hidx
-                                        : ((uint32_t)(out >> 32) >> dp.light_shift) & (dp.light_b - 1u)) << 56;
+                                        : (uint32_t)(out >> 32) & (dp.light_b - 1u)) << 56;
         return out;
     };
     // the deferred packets of this wave: full probes (CAS inserts), 64 at a time
@@ -2040,31 +2038,14 @@ hipError_t launch_tail(const TailArgs &a) {
         hf_id = fork ? 1 : 0;
     }
     if (tagh && (e = launch_heavy()) != hipSuccess) return e;
-    // sort pass 2 as a per-bin LDS sort (fsx_bins.hip): pass 1's output (packed[0]) ->
-    // packed[1], where the global pass would have written it, with the segment heads
-    // (FSX_BIN_HEADS=0: k_heads_count instead, A/B)
-    static const bool bin_heads = !getenv("FSX_BIN_HEADS") || getenv("FSX_BIN_HEADS")[0] != '0';
-    if (a.bins) {
-        const bool bh = bin_heads && tagh;
-        if (bh) {
-            if ((e = hipMemsetAsync(sc.tile_aux, 0, (size_t)cdiv(n, kTile) * 4, st)) != hipSuccess) return e;
-            if ((e = hipMemsetAsync(sc.sub_cnt, 0, (size_t)(n / 1024 + 8) * 4, st)) != hipSuccess) return e;
-        }
-        const BinSort bsrt{sc.packed[0], sc.pay[0], sc.packed[1], sc.pay[1], bs, sc.bin_start, sc.bin_order,
-                           lim.table_mask, bh ? sc.headf : nullptr, sc.tile_aux, sc.sub_cnt};
-        if ((e = launch_bin_sort(bsrt, n, st)) != hipSuccess) return e;
-        mark("k_bin_sort");
-    }
     if (npass & 1) {
         std::swap(sc.packed[0], sc.packed[1]);
         std::swap(sc.pay[0], sc.pay[1]);
     }
     uint64_t *S = sc.packed[0];
     const uint32_t lo = tagh ? 1u : 0u;   // light-only heads
-    if (!(a.bins && bin_heads && tagh)) {
-        k_heads_count<<<gridTiles, 256, 0, st>>>(S, bs, in.hdr, sc.headf, sc.tile_aux, sc.sub_cnt, lo);
-        mark("k_heads_count");
-    }
+    k_heads_count<<<gridTiles, 256, 0, st>>>(S, bs, in.hdr, sc.headf, sc.tile_aux, sc.sub_cnt, lo);
+    mark("k_heads_count");
     k_scan_tiles_u32<<<1, 256, 0, st>>>(sc.tile_aux, bs, sc.seg_start, lo);
     // (the first sort word's low half per segment only for the flow rows)
     uint32_t *seg_lo = flows && !in.rec ? sc.seg_lo : nullptr;
@@ -2208,22 +2189,10 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
     // heavy verdict lists (fixed window with the heavy-source sort; FSX_NO_HEAVY_LISTS=1: A/B)
     static const bool no_hlists = getenv("FSX_NO_HEAVY_LISTS") != nullptr;
     const bool tagh = heavy_sort && do_limit && lim.limiter == 0 && verdict && !no_hlists;
-    // bin sort (FSX_BINS=0 / 1: A/B): pass 1 leaves bins of 64 slots, each sorted in LDS by
-    // the tail instead of a global third pass
-    static const bool no_bins = !getenv("FSX_BINS") || getenv("FSX_BINS")[0] == '0';
-    const bool bins = tagh && !no_bins && idbits >= kBinMinIdBits && idbits <= kBinMaxIdBits && sc.bin_start;
     if (!(split && split->tail) && (e = hipMemsetAsync(sc.marks, 0, n, st)) != hipSuccess) return e;
     DigitPlan dp{};
-    dp.npass = bins ? 2u : (uint32_t)npass;   // (digits counted by k_parse: no pass 2 with bins)
-    if (heavy_sort && bins) {
-        // light bucket = slot bits [8, 15), pass 1 = slot bits [15, idbits): the pass-1 output
-        // is ordered by slot >> 8, the bin sort orders each bin by slot & 255 (fsx_bins.hip)
-        dp.light_b = 128;
-        dp.light_shift = kBinSlotBits;
-        dp.shift[0] = 56; dp.mask[0] = 255;
-        dp.shift[1] = 32 + kBinSlotBits + 7; dp.mask[1] = (1u << (idbits - kBinSlotBits - 7)) - 1u;
-        dp.shift[2] = 32; dp.mask[2] = (1u << kBinSlotBits) - 1u;
-    } else if (heavy_sort) {
+    dp.npass = (uint32_t)npass;
+    if (heavy_sort) {
         const uint32_t rest = idbits - 7, w1 = (rest + 1) / 2;
         dp.light_b = 128;
         dp.shift[0] = 56; dp.mask[0] = 255;
@@ -2279,7 +2248,7 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
     k_hist_prep<<<1, 256, 0, st>>>(sc.sort_ctl, sc.gbase, bs, heavy_sort ? dp.light_b : 256u);
     if (do_limit) k_batch_check<<<1, 1, 0, st>>>(bs, tstate, lim, split ? split->prev : nullptr);
     const uint32_t gen0 = onesweep ? next_generation() : 0u;
-    for (int pass = 0; pass < (bins ? 2 : npass); ++pass) {
+    for (int pass = 0; pass < npass; ++pass) {
         const uint64_t *in = sc.packed[pass & 1];
         uint64_t *out = sc.packed[(pass + 1) & 1];
         const uint64_t *pin = pass == 0 ? nullptr : sc.pay[pass & 1];
@@ -2323,7 +2292,6 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
     ta.heavy_flow_ev = heavy_flow_ev; ta.tm = tm; ta.split = split != nullptr;
     if (split) ta.sp = *split;
     ta.npass = npass; ta.tagh = tagh; ta.gridTiles = gridTiles;
-    ta.bins = bins;
     ta.fork = flows && do_limit && st2 && fork_ev && join_ev && !no_fork;
     for (int k = 0; k < 3; ++k) ta.last[k] = last[k];
     if (split && split->tail_out) {

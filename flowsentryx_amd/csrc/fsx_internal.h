@@ -325,9 +325,6 @@ struct Scratch {
                            // packets [kSketch] each (counts zeroed by k_heavy_pick after use)
     HeavySet *heavy;
     void *heavy_flow;      // heavy sources' flow chunk sums (heavy_flow_bytes)
-    // bin sort (fsx_bins.hip; fixed window, tables of 2^17..2^21 slots, else null)
-    uint32_t *bin_start;   // bins + 1
-    uint32_t *bin_order;   // bins
     uint64_t cap;          // packets the scratch is sized for
 };
 
@@ -419,7 +416,6 @@ struct TailArgs {
     int npass;
     uint32_t gridTiles;
     int last[3];
-    bool bins;             // sort pass 2 as the tail's bin sort (fsx_bins.hip)
 };
 hipError_t launch_tail(const TailArgs &a);
 
