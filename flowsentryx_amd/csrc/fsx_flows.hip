@@ -64,12 +64,13 @@ __device__ __forceinline__ void flow_tiles(const uint64_t *__restrict__ S,
         for (uint32_t j = 0; j < j4; ++j) hb += sub_cnt[t4 * 4 + j];
         // stage the tile's payload (or sort) words through LDS (coalesced load,
         // 17-word row pitch)
+        // (element r * 64 + lane lands in row 4r + lane / 16: one LDS base, constant offsets)
         const uint64_t *src = kPay ? pay : S;
+        unsigned long long *sdst = sS + (lane >> 4) * 17u + (lane & 15u);
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-            const uint32_t e = (uint32_t)r * 64u + lane;
-            const uint32_t p = base + e;
-            sS[(e >> 4) * 17u + (e & 15u)] = p < M ? src[p] : 0ull;
+            const uint32_t p = base + (uint32_t)r * 64u + lane;
+            sdst[r * 68] = p < M ? src[p] : 0ull;
         }
         wave_lds_order();
         uint32_t hf[4] = {0, 0, 0, 0};

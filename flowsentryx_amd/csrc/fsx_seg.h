@@ -209,8 +209,7 @@ struct MarkWriter {
     __device__ __forceinline__ void emit(uint32_t pos, uint8_t v) {
         if (v != last) {
             if constexpr (kList) {
-                if (last == XDP_DROP) ndrop += pos - last_pos;
-                else if (last) npass += pos - last_pos;
+                count_run(pos);
                 const uint32_t e = pk_idx(S[pos]) << 1 | (v == XDP_DROP ? 1u : 0u);
                 if (!kWave || lane_id() == 0) list[nl] = e;
                 ++nl;
@@ -221,10 +220,16 @@ struct MarkWriter {
             last = v;
         }
     }
+    // list mode: the run [last_pos, pos) of verdict `last` into the counts (selects, not a
+    // branch: a branch between the two counters made the compiler keep them in scratch)
+    __device__ __forceinline__ void count_run(uint32_t pos) {
+        const uint64_t r = pos - last_pos;
+        ndrop += last == XDP_DROP ? r : 0ull;
+        npass += (last && last != XDP_DROP) ? r : 0ull;
+    }
     // list mode: close the counts at the segment end b
     __device__ __forceinline__ void finish(uint32_t b) {
-        if (last == XDP_DROP) ndrop += b - last_pos;
-        else if (last) npass += b - last_pos;
+        count_run(b);
         last_pos = b;
     }
 };

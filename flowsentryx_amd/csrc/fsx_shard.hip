@@ -88,14 +88,16 @@ __device__ __forceinline__ const ShardBlock *replica_find(const Replica &r, uint
 // replica: till > 0 and now <= till, src/fsx_kern.c:189-215 — exact when the clock is
 // monotone over the batches so far, which the host checks before asking for it),
 // 4 / 6 an IP packet for its owner.
-// (fam: the family 4 / 6 of an IP packet, also of a replica-dropped one)
+// (fam: the family 4 / 6 of an IP packet, also of a replica-dropped one; the replica by
+// reference plus a flag: selecting between its address and null put the kernel argument
+// in scratch)
 __device__ __forceinline__ uint32_t shard_classify(const uint8_t *rec, uint32_t L, uint64_t now,
-                                                   const Replica *rep, uint32_t k[4], uint32_t &dport,
-                                                   uint32_t &fam) {
+                                                   const Replica &rep, bool use_rep, uint32_t k[4],
+                                                   uint32_t &dport, uint32_t &fam) {
     const uint32_t f = shard_parse(rec, L, k, dport);
     fam = f;
-    if (f >= 4 && rep) {
-        const ShardBlock *b = replica_find(*rep, f == 6 ? 2u : 1u, k);
+    if (f >= 4 && use_rep) {
+        const ShardBlock *b = replica_find(rep, f == 6 ? 2u : 1u, k);
         if (b && b->till > 0 && !(now > b->till)) return 2;
     }
     return f;
@@ -148,7 +150,7 @@ __global__ __launch_bounds__(256) void k_shard_parse(const uint8_t *__restrict__
             const uint64_t now = ts[i];
             uint32_t k[4], dp, fam;
             const uint32_t f = shard_classify(reinterpret_cast<const uint8_t *>(rec + lane * 17u), L, now,
-                                              use_rep ? &rep : nullptr, k, dp, fam);
+                                              rep, use_rep != 0, k, dp, fam);
             uint8_t o = 0xFFu;
             // an IP packet for its owner, or (drop_rec) a replica-dropped one for group G
             if (f >= 4 || (f == 2 && drop_rec)) {
@@ -308,7 +310,7 @@ __global__ __launch_bounds__(256) void k_shard_pack(const uint8_t *__restrict__ 
         of[r] = 15u;
         if (i < n) {
             uint32_t k[4], dp, fam;
-            const uint32_t f = shard_classify(hdr + (size_t)i * 64, len[i], ts[i], use_rep ? &rep : nullptr, k, dp,
+            const uint32_t f = shard_classify(hdr + (size_t)i * 64, len[i], ts[i], rep, use_rep != 0, k, dp,
                                               fam);
             if (f >= 4 || (f == 2 && drop_rec)) {
                 const uint32_t o = f >= 4 ? owner_dev(f, k, G) : G;
