@@ -59,6 +59,11 @@ struct fsx_ctx {
     uint32_t *idx_k6 = nullptr;
     uint32_t idx_epoch = 1;
     uint32_t pending_born = 0;  // generation of the in-flight limiter batch (rollback)
+    // FSX_FLAG_EVICT_IDLE: survivors' copy (grown on demand), sources evicted before the
+    // last limiter batch
+    Slot *evict_buf = nullptr;
+    uint64_t evict_cap = 0;
+    uint64_t last_evicted = 0;
     // sharding: per (owner, tile) counts of fsx_shard_pack_device, blocklist replica
     uint32_t *d_shard_cnt = nullptr;
     uint64_t shard_cnt_cap = 0;
@@ -331,6 +336,7 @@ void fsx_close(fsx_ctx *c) {
     hipFree(c->d_shard_cnt); hipFree(c->d_rep); hipFree(c->d_shard_own); hipFree(c->d_shard_crec);
     hipFree(c->d_rec_len); hipFree(c->d_rec_ts);
     hipFree(c->idx_heads); hipFree(c->idx_k6);
+    hipFree(c->evict_buf);
     hipFree(c->d_rule_slot); hipFree(c->d_rule_lens); hipFree(c->d_rule_filter);
     for (int r = 0; r < kRing; ++r)
         for (int i = 0; i < kMaxEv; ++i) if (c->ev[r][i]) hipEventDestroy(c->ev[r][i]);
@@ -360,6 +366,8 @@ int fsx_open(fsx_ctx **out, const fsx_config *cfg) {
     if (k.limiter == FSX_LIMIT_TOKEN_BUCKET && k.tb_burst > FSX_TB_MAX_BURST) return -EINVAL;
     // sliding window: a carried log holds <= pps_threshold entries (24-bit count)
     if (k.limiter == FSX_LIMIT_SLIDING_WINDOW && k.pps_threshold > FSX_SW_MAX_PPS) return -EINVAL;
+    // idle eviction is defined for the reference's fixed window only
+    if ((k.flags & FSX_FLAG_EVICT_IDLE) && k.limiter != FSX_LIMIT_FIXED_WINDOW) return -EINVAL;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return -ENODEV;
     if (k.device < 0 || k.device >= ndev) return -EINVAL;
@@ -785,10 +793,54 @@ static int run_pipelined(fsx_ctx *c, const PacketIn &in, const uint32_t *d_len, 
     return 0;
 }
 
+// FSX_FLAG_EVICT_IDLE, before a limiter batch of n packets: when the
+// tracked sources plus n exceed max_entries, every source idle at the batch's smallest
+// timestamp leaves the maps. Synchronous: the previous batches finish first, and the
+// survivors move to new slots (open addressing drops no entry in place).
+static int evict_idle(fsx_ctx *c, const PacketIn &in, const uint64_t *d_ts, size_t n) {
+    int rc;
+    if ((rc = sel(c)) || (rc = fsx_sync(c))) return rc;
+    c->last_evicted = 0;
+    uint64_t count = 0;
+    HIPCHK(c, hipMemcpy(&count, &c->tstate->count, 8, hipMemcpyDeviceToHost));
+    if (count + n <= c->cfg.max_entries) return 0;
+    if (c->flow_accum || c->d_slot_acc)
+        return set_err(c, -EINVAL, "FSX_FLAG_EVICT_IDLE moves sources between slots: not with fsx_flows_begin");
+    if (count > c->evict_cap) {
+        hipFree(c->evict_buf);
+        c->evict_buf = nullptr;
+        c->evict_cap = 0;
+        HIPCHK(c, hipMalloc(&c->evict_buf, count * sizeof(Slot)));
+        c->evict_cap = count;
+    }
+    unsigned long long *scal = reinterpret_cast<unsigned long long *>(c->d_val);
+    HIPCHK(c, hipMemsetAsync(scal, 0xFF, 8, c->stream));
+    HIPCHK(c, hipMemsetAsync(scal + 1, 0, 8, c->stream));
+    hipError_t e = launch_evict_scan(c->table, c->lim, in, d_ts, (uint32_t)n, c->evict_buf, c->evict_cap, scal,
+                                     c->stream);
+    if (e != hipSuccess) return set_err(c, -EIO, "evict scan: %s", hipGetErrorString(e));
+    uint64_t m = 0;
+    HIPCHK(c, hipMemcpyAsync(&m, scal + 1, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (m > count) return set_err(c, -EIO, "evict scan found %llu live sources of %llu",
+                                  (unsigned long long)m, (unsigned long long)count);
+    if (m == count) return 0;   // nothing idle: the batch decides (-ENOSPC if it overflows)
+    if ((rc = next_epoch(c))) return rc;
+    HIPCHK(c, hipMemsetAsync(c->table, 0, c->slots * sizeof(Slot), c->stream));
+    e = launch_evict_reinsert(c->table, c->tstate, c->lim, table_index(c), c->evict_buf, m, c->stream);
+    if (e != hipSuccess) return set_err(c, -EIO, "evict reinsert: %s", hipGetErrorString(e));
+    c->last_evicted = count - m;
+    return 0;
+}
+
 // Enqueue one batch: verdicts + maps when d_verdict is set, per-source flows when fr is.
 static int run_batch(fsx_ctx *c, const PacketIn &in, const uint32_t *d_len, const uint64_t *d_ts,
                      size_t n, uint8_t *d_verdict, bool do_limit, const FlowRequest *fr) {
     if (n > c->cfg.max_batch) return set_err(c, -E2BIG, "n=%zu exceeds max_batch", n);
+    if (do_limit && n && (c->cfg.flags & FSX_FLAG_EVICT_IDLE)) {
+        const int rc = evict_idle(c, in, d_ts, n);
+        if (rc) return rc;
+    }
     // pipelined (no per-kernel timing): split front / tail for the fixed window on header
     // records, the whole batch on the context stream otherwise
     if (c->pipe && do_limit && n && !c->timing)
@@ -1332,10 +1384,11 @@ int fsx_last_batch_info(fsx_ctx *c, uint64_t *info, int cap) {
     HIPCHK(c, hipStreamSynchronize(c->stream));
     BatchState h;
     HIPCHK(c, hipMemcpy(&h, c->bs, sizeof(h), hipMemcpyDeviceToHost));
-    const uint64_t v[12] = {h.n_valid, h.nseg, h.n_new, h.any_v6, h.nonmono, h.max_len,
-                            h.max_ts, h.allowed, h.dropped, h.n_rule, h.pay_ok, h.n_light};
+    const uint64_t v[13] = {h.n_valid, h.nseg, h.n_new, h.any_v6, h.nonmono, h.max_len,
+                            h.max_ts, h.allowed, h.dropped, h.n_rule, h.pay_ok, h.n_light,
+                            c->last_evicted};
     int k = 0;
-    for (; k < cap && k < 12; ++k) info[k] = v[k];
+    for (; k < cap && k < 13; ++k) info[k] = v[k];
     return k;
 }
 

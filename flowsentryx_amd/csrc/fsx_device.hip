@@ -2391,6 +2391,82 @@ hipError_t launch_map_import(Slot *table, TableState *tstate, BatchState *bs, co
     return hipGetLastError();
 }
 
+// ------------------------------------------------------------------ idle eviction
+// FSX_FLAG_EVICT_IDLE (oracle/fsx_oracle.c evict_idle). Open addressing
+// cannot drop an entry in place (a later key's probe chain may run through it), so the
+// survivors are copied out and re-inserted under a new index epoch.
+__device__ __forceinline__ uint64_t batch_ts(const PacketIn &in, const uint64_t *ts, uint32_t i) {
+    if (!in.rec) return ts[i];
+    const uint4 *r = reinterpret_cast<const uint4 *>(in.rec);
+    if (in.rec_bytes == 16) {   // ShardRecord16 {key, len | dport << 16, ts}
+        const uint4 w = r[i];
+        return (uint64_t)w.z | ((uint64_t)w.w << 32);
+    }
+    const uint4 w = r[(size_t)i * 2 + 1];   // ShardRecord: ts after the 16 key bytes
+    return (uint64_t)w.x | ((uint64_t)w.y << 32);
+}
+
+__global__ __launch_bounds__(256) void k_evict_min_ts(PacketIn in, const uint64_t *__restrict__ ts, uint32_t n,
+                                                      unsigned long long *scal) {
+    uint64_t m = ~0ull;
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) {
+        const uint64_t t = batch_ts(in, ts, i);
+        m = t < m ? t : m;
+    }
+    m = ~wave_max(~m);
+    if (lane_id() == 0 && m != ~0ull) atomicMin(&scal[0], (unsigned long long)m);
+}
+
+// Live at now0: a window still open (the reset test of src/fsx_kern.c:245 fails), a live
+// blacklist entry (src/fsx_kern.c:189-204), or token-bucket state.
+__device__ __forceinline__ bool slot_live(const Slot &s, const Limits &lim, uint64_t now0) {
+    return ((s.flags & SLOT_HAS_ST) && !(now0 - s.tt > lim.window)) ||
+           ((s.flags & SLOT_HAS_BL) && s.till > 0 && !(now0 > s.till)) || (s.flags & SLOT_HAS_TB);
+}
+
+__global__ __launch_bounds__(256) void k_evict_compact(const Slot *__restrict__ table, Limits lim, Slot *buf,
+                                                       uint64_t cap, unsigned long long *scal) {
+    const uint64_t now0 = scal[0];
+    for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i <= lim.table_mask;
+         i += (uint64_t)gridDim.x * 256u) {
+        const Slot s = table[i];
+        if (s.tag == 0 || !slot_live(s, lim, now0)) continue;
+        const unsigned long long o = atomicAdd(&scal[1], 1ull);
+        if (o < cap) buf[o] = s;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_evict_reinsert(Slot *table, TableState *tstate, Limits lim, TableIndex X,
+                                                        const Slot *__restrict__ buf, uint64_t m) {
+    const IdTable idt{X.heads, X.k6, lim.table_mask, lim.seed, X.epoch, lim.test_flags, table, 0u, 0u};
+    for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i < m; i += (uint64_t)gridDim.x * 256u) {
+        const Slot s = buf[i];
+        const uint64_t h = id_start(idt, s.tag, s.key);
+        bool fresh = false;
+        const uint32_t id = id_resolve(idt, s.tag, s.key, h, X.heads[h], &fresh);
+        if (id != kNoSlot) table[id] = s;   // (2x the entries in slots: never full)
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) tstate->count = m;
+}
+
+hipError_t launch_evict_scan(const Slot *table, const Limits &lim, const PacketIn &in, const uint64_t *ts,
+                             uint32_t n, Slot *buf, uint64_t cap, unsigned long long *scal, hipStream_t st) {
+    (void)hipGetLastError();   // a stale error of another caller is not ours
+    const uint32_t g0 = std::max<uint32_t>(1, std::min<uint32_t>(2048, (n + 255) / 256));
+    k_evict_min_ts<<<g0, 256, 0, st>>>(in, ts, n, scal);
+    const uint32_t g1 = (uint32_t)std::min<uint64_t>(4096, (lim.table_mask + 256) / 256);
+    k_evict_compact<<<g1, 256, 0, st>>>(table, lim, buf, cap, scal);
+    return hipGetLastError();
+}
+
+hipError_t launch_evict_reinsert(Slot *table, TableState *tstate, const Limits &lim, const TableIndex &X,
+                                 const Slot *buf, uint64_t m, hipStream_t st) {
+    (void)hipGetLastError();
+    const uint32_t g = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(4096, (m + 255) / 256));
+    k_evict_reinsert<<<g, 256, 0, st>>>(table, tstate, lim, X, buf, m);
+    return hipGetLastError();
+}
+
 hipError_t launch_map_op(Slot *table, TableState *tstate, const Limits &lim, const TableIndex &X, int op,
                          int map_id, const uint32_t key[4], const uint64_t val[3], uint64_t flags,
                          int32_t *d_result, uint64_t *d_val, hipStream_t st) {

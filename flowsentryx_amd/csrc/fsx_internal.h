@@ -503,6 +503,16 @@ hipError_t launch_map_import(Slot *table, TableState *tstate, BatchState *bs, co
 hipError_t launch_index_rebuild(Slot *table, const Limits &lim, const TableIndex &X, uint32_t born,
                                 hipStream_t st);
 
+// FSX_FLAG_EVICT_IDLE, with the device idle before a limiter batch:
+// scan: the batch's smallest timestamp into scal[0] (preset ~0), then every source that
+// is not idle at it is copied into buf (scal[1] counts them, preset 0; at most cap);
+// reinsert (after the host started a new index epoch and cleared the table): the m
+// survivors go back into the table under X.epoch with their state, count = m.
+hipError_t launch_evict_scan(const Slot *table, const Limits &lim, const PacketIn &in, const uint64_t *ts,
+                             uint32_t n, Slot *buf, uint64_t cap, unsigned long long *scal, hipStream_t st);
+hipError_t launch_evict_reinsert(Slot *table, TableState *tstate, const Limits &lim, const TableIndex &X,
+                                 const Slot *buf, uint64_t m, hipStream_t st);
+
 hipError_t launch_map_dump(const Slot *table, const Limits &lim, int map_id, uint8_t *d_keys,
                            uint64_t *d_vals, uint64_t cap, unsigned long long *d_count,
                            hipStream_t st);

@@ -50,13 +50,25 @@ extern "C" {
 
 #define FSX_HDR_BYTES 64
 
-/* fsx_config.flags — test hooks only. FSX_FLAG_TEST_V6_COLLIDE makes every IPv6
+/* fsx_config.flags — FSX_FLAG_TEST_V6_COLLIDE and FSX_FLAG_ONESWEEP_SORT are test / A-B
+ * hooks. FSX_FLAG_TEST_V6_COLLIDE makes every IPv6
  * source start its probe of the per-batch source-id table at IPv4 10.0.0.1's slot
  * (one long probe chain shared by all of them; results must not change). */
 #define FSX_FLAG_TEST_V6_COLLIDE 1u
 /* Sort with the single-pass onesweep variant (decoupled look-back) instead of the
  * per-pass tile histograms (A/B measurements only). */
 #define FSX_FLAG_ONESWEEP_SORT 2u
+/* Opt-in overflow policy (fixed window only; DESIGN.md §2.1, parity unpinned like the
+ * reference's LRU_HASH eviction). Default (flag clear): a batch whose new sources would
+ * exceed max_entries fails with -ENOSPC. With the flag: before a limiter batch of n
+ * packets, when the tracked sources plus n exceed max_entries, every source that is idle
+ * at the batch's smallest timestamp now0 leaves the maps first: its window has expired
+ * (no ip_stats, or now0 - track_time > window_ns: the reset test of src/fsx_kern.c:245),
+ * it holds no live blacklist entry (none, till 0 or now0 > till) and no token-bucket
+ * state. The batch then runs as usual (-ENOSPC if it still overflows). The eviction syncs
+ * the context (previous batches finish first) and is not undone if the batch then fails;
+ * the number evicted is fsx_last_batch_info()[12]. Not with fsx_flows_begin. */
+#define FSX_FLAG_EVICT_IDLE 4u
 
 /* Map ids: the five maps of src/fsx_kern.c:56-94, then the token-bucket state maps of
  * the build-defined token bucket (value fsx_tb_state), then the
@@ -134,14 +146,15 @@ typedef struct fsx_config {
     uint64_t block_ns;        /* 10 s       src/fsx_kern.c:308,317 */
     uint64_t max_entries;     /* per map; MAX_TRACK_IPS=100000 src/fsx_struct.h:7.
                                  No LRU eviction: a full table makes a batch fail
-                                 with -ENOSPC. 1 .. 2^31. */
+                                 with -ENOSPC, unless
+                                 FSX_FLAG_EVICT_IDLE. 1 .. 2^31. */
     uint64_t max_batch;       /* largest n per call (device scratch is sized for it) */
     uint64_t tb_rate;         /* token bucket: refill in nano-tokens per ns (1000 = 1000 tok/s) */
     uint64_t tb_burst;        /* token bucket: capacity in tokens (<= FSX_TB_MAX_BURST) */
     uint64_t hash_seed;       /* salt of the table/IPv6 sort hashes */
     int32_t limiter;          /* enum fsx_limiter */
     int32_t device;           /* HIP device ordinal */
-    uint32_t flags;           /* FSX_FLAG_*; 0 in production */
+    uint32_t flags;           /* FSX_FLAG_*: 0 or FSX_FLAG_EVICT_IDLE in production */
     uint32_t reserved[7];
 } fsx_config;
 
@@ -369,7 +382,8 @@ int fsx_pcap_records_device(fsx_ctx *ctx, const uint8_t *d_buf, const uint64_t *
  * dropped by a prefix rule (counted in [8], not in [0]), [10] 1 when (ts, len) travelled with the sort as payload
  * words (timestamps within 2^40 ns of the batch minimum, frame lengths < 2^24), 0 when
  * they were gathered by index, [11] IP packets of non-heavy sources (the entries the
- * later sort passes covered). Returns the number of entries written. */
+ * later sort passes covered), [12] sources evicted before the batch
+ * (FSX_FLAG_EVICT_IDLE). Returns the number of entries written. */
 int fsx_last_batch_info(fsx_ctx *ctx, uint64_t *info, int cap);
 
 /* Per-kernel device timing for the benchmark: while enabled, every batch records a

@@ -176,8 +176,19 @@ typedef struct fsxo_config {
     uint64_t pps_threshold, bps_threshold, window_ns, block_ns, max_entries;
     uint64_t tb_rate, tb_burst;
     int32_t limiter;
-    int32_t pad;
+    int32_t flags;      /* FSXO_EVICT_IDLE (include/fsx_hip.h FSX_FLAG_EVICT_IDLE) */
 } fsxo_config;
+
+/* Opt-in overflow policy, build-defined (parity unpinned like the
+ * reference's LRU): before a fixed-window batch of n packets, when the tracked sources
+ * plus n exceed max_entries, every idle source is evicted. Idle at now0 = the batch's
+ * smallest timestamp: its window has expired (no ip_stats entry, or now0 - track_time >
+ * window, the reset test of src/fsx_kern.c:245), it holds no live blacklist entry (none,
+ * till 0, or now0 > till, src/fsx_kern.c:189-204) and no token-bucket state. A tracked
+ * source is one the GPU table holds a slot for: every source that reached the per-source
+ * maps (after the prefix rules) or was written by a map update; map deletes do not
+ * untrack it. */
+#define FSXO_EVICT_IDLE 4
 
 typedef struct ip_stats { uint64_t pps, bps, track_time; } ip_stats;  /* fsx_struct.h:17-22 */
 typedef struct tb_state { uint64_t tokens, last; } tb_state;
@@ -198,6 +209,9 @@ typedef struct fsxo_ctx {
     int err;
     /* sliding window logs, indexed by a side map key -> slot */
     omap swidx[2];
+    /* FSXO_EVICT_IDLE: tracked sources per family (key -> unused byte) */
+    omap src[2];
+    uint64_t evicted_last;
     sw_log *logs;
     size_t nlogs, caplogs;
 } fsxo_ctx;
@@ -211,7 +225,7 @@ void fsxo_config_default(fsxo_config *c) {
     c->tb_rate = 1000;              /* nano-tokens per ns = 1000 tokens/s */
     c->tb_burst = 1000;             /* tokens */
     c->limiter = 0;
-    c->pad = 0;
+    c->flags = 0;
 }
 
 fsxo_ctx *fsxo_open(const fsxo_config *cfg) {
@@ -231,6 +245,10 @@ fsxo_ctx *fsxo_open(const fsxo_config *cfg) {
     r |= omap_init(&c->swidx[1], me, 16, 8);
     r |= omap_init(&c->pfx[0], PREFIX_MAX_ENTRIES, 8, 8);
     r |= omap_init(&c->pfx[1], PREFIX_MAX_ENTRIES, 20, 8);
+    if (cfg->flags & FSXO_EVICT_IDLE) {
+        r |= omap_init(&c->src[0], me, 4, 1);
+        r |= omap_init(&c->src[1], me, 16, 1);
+    }
     if (r) return NULL;
     return c;
 }
@@ -246,6 +264,7 @@ void fsxo_close(fsxo_ctx *c) {
     for (int i = 0; i < 7; ++i) omap_free(&c->m[i]);
     omap_free(&c->swidx[0]); omap_free(&c->swidx[1]);
     omap_free(&c->pfx[0]); omap_free(&c->pfx[1]);
+    omap_free(&c->src[0]); omap_free(&c->src[1]);
     sw_free_logs(c);
     free(c);
 }
@@ -253,6 +272,8 @@ void fsxo_close(fsxo_ctx *c) {
 void fsxo_reset(fsxo_ctx *c) {
     for (int i = 0; i < 7; ++i) omap_clear(&c->m[i]);
     omap_clear(&c->swidx[0]); omap_clear(&c->swidx[1]);
+    if (c->src[0].used) { omap_clear(&c->src[0]); omap_clear(&c->src[1]); }
+    c->evicted_last = 0;
     sw_free_logs(c);   /* (the prefix blocklists stay: configuration, fsx_hip.h) */
     c->allowed = c->dropped = 0;
     c->err = 0;
@@ -261,6 +282,13 @@ void fsxo_reset(fsxo_ctx *c) {
 int fsxo_error(const fsxo_ctx *c) { return c->err; }
 
 void fsxo_get_stats(const fsxo_ctx *c, uint64_t out[2]) { out[0] = c->allowed; out[1] = c->dropped; }
+
+/* FSXO_EVICT_IDLE: the source (family v6, key) is tracked from now on. */
+static void src_track(fsxo_ctx *c, int v6, const uint8_t *key) {
+    if (!(c->cfg.flags & FSXO_EVICT_IDLE)) return;
+    static const uint8_t one = 1;
+    if (!omap_lookup(&c->src[v6], key) && omap_update(&c->src[v6], key, &one)) c->err = -ENOSPC;
+}
 
 static omap *map_of(fsxo_ctx *c, int map_id) {
     if (map_id < 1 || map_id > 6) return NULL;
@@ -343,7 +371,9 @@ int fsxo_map_update(fsxo_ctx *c, int map_id, const void *key, const void *val) {
     if (map_id == MAP_V4_PREFIX || map_id == MAP_V6_PREFIX) return prefix_op(c, 1, map_id, key, val, NULL);
     omap *m = map_of(c, map_id);
     if (!m) return -EINVAL;
-    return omap_update(m, (const uint8_t *)key, val);
+    int r = omap_update(m, (const uint8_t *)key, val);
+    if (!r) src_track(c, map_id == MAP_V6_STATS || map_id == MAP_V6_BL || map_id == MAP_V6_TB, key);
+    return r;
 }
 
 int fsxo_map_delete(fsxo_ctx *c, int map_id, const void *key) {
@@ -532,6 +562,7 @@ static int one_packet(fsxo_ctx *c, const uint8_t *hdr, uint32_t len, uint64_t ts
         c->dropped++;
         return XDP_DROP;
     }
+    src_track(c, v6, key);
     switch (c->cfg.limiter) {
     case 1: return sliding_window_packet(c, v6, key, len, ts);
     case 2: return token_bucket_packet(c, v6, key, len, ts);
@@ -539,8 +570,47 @@ static int one_packet(fsxo_ctx *c, const uint8_t *hdr, uint32_t len, uint64_t ts
     }
 }
 
+/* FSXO_EVICT_IDLE, before a batch of n packets with smallest timestamp now0. */
+static void evict_idle(fsxo_ctx *c, size_t n, uint64_t now0) {
+    c->evicted_last = 0;
+    if (c->src[0].count + c->src[1].count + n <= c->cfg.max_entries) return;
+    for (int v6 = 0; v6 < 2; ++v6) {
+        omap *src = &c->src[v6];
+        omap *st = &c->m[v6 ? MAP_V6_STATS : MAP_V4_STATS];
+        omap *bl = &c->m[v6 ? MAP_V6_BL : MAP_V4_BL];
+        omap *tb = &c->m[v6 ? MAP_V6_TB : MAP_V4_TB];
+        /* the idle keys first (a delete moves entries of the map it walks) */
+        uint8_t *gone = (uint8_t *)malloc(src->count * src->klen + 1);
+        size_t ng = 0;
+        for (size_t i = 0; i < src->cap; ++i) {
+            if (!src->used[i]) continue;
+            const uint8_t *k = src->keys + i * src->klen;
+            const ip_stats *s = (const ip_stats *)omap_lookup(st, k);
+            const uint64_t *till = (const uint64_t *)omap_lookup(bl, k);
+            int live = (s && !(now0 - s->track_time > c->cfg.window_ns)) ||
+                       (till && *till > 0 && !(now0 > *till)) || omap_lookup(tb, k) != NULL;
+            if (!live) memcpy(gone + ng++ * src->klen, k, src->klen);
+        }
+        for (size_t j = 0; j < ng; ++j) {
+            const uint8_t *k = gone + j * src->klen;
+            omap_delete(src, k);
+            omap_delete(st, k);
+            omap_delete(bl, k);
+        }
+        free(gone);
+        c->evicted_last += ng;
+    }
+}
+
+uint64_t fsxo_evicted_last(const fsxo_ctx *c) { return c->evicted_last; }
+
 int fsxo_batch(fsxo_ctx *c, const uint8_t *hdr, const uint32_t *len, const uint64_t *ts,
                size_t n, uint8_t *verdict) {
+    if ((c->cfg.flags & FSXO_EVICT_IDLE) && c->cfg.limiter == 0 && n) {
+        uint64_t now0 = ts[0];
+        for (size_t i = 1; i < n; ++i) now0 = ts[i] < now0 ? ts[i] : now0;
+        evict_idle(c, n, now0);
+    }
     for (size_t i = 0; i < n; ++i)
         verdict[i] = (uint8_t)one_packet(c, hdr + i * 64, len[i], ts[i]);
     return c->err;

@@ -22,8 +22,11 @@ class OConfig(C.Structure):
         ("pps_threshold", C.c_uint64), ("bps_threshold", C.c_uint64),
         ("window_ns", C.c_uint64), ("block_ns", C.c_uint64), ("max_entries", C.c_uint64),
         ("tb_rate", C.c_uint64), ("tb_burst", C.c_uint64),
-        ("limiter", C.c_int32), ("pad", C.c_int32),
+        ("limiter", C.c_int32), ("flags", C.c_int32),
     ]
+
+
+EVICT_IDLE = 4   # fsxo_config.flags, = include/fsx_hip.h FSX_FLAG_EVICT_IDLE
 
 
 class OQ8Model(C.Structure):
@@ -60,6 +63,7 @@ def lib() -> C.CDLL:
         "fsxo_error": (C.c_int, [vp]),
         "fsxo_get_stats": (None, [vp, vp]),
         "fsxo_batch": (C.c_int, [vp, vp, vp, vp, sz, vp]),
+        "fsxo_evicted_last": (C.c_uint64, [vp]),
         "fsxo_parse_batch": (None, [vp, vp, sz, vp, vp]),
         "fsxo_map_lookup": (C.c_int, [vp, C.c_int, vp, vp]),
         "fsxo_map_update": (C.c_int, [vp, C.c_int, vp, vp]),
@@ -131,6 +135,10 @@ class Oracle:
         s = np.zeros(2, dtype=np.uint64)
         lib().fsxo_get_stats(self._h, _p(s))
         return int(s[0]), int(s[1])
+
+    def evicted_last(self) -> int:
+        """Sources evicted before the last batch (flags=EVICT_IDLE)."""
+        return int(lib().fsxo_evicted_last(self._h))
 
     def map_update(self, map_id: int, key: bytes, value):
         if map_id in (1, 2, 5, 6):
