@@ -477,7 +477,7 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
     __shared__ uint32_t s_htag[kHeavyMax];
     __shared__ uint32_t s_hmap4[(1u << kHeavyMapBits) / 4];   // HeavySet::map
     __shared__ uint32_t s_hslot[kHeavyMax];
-    __shared__ uint32_t s_def[4][256 * 3];  // per wave: deferred probes {i, tag | hidx, key word 0}
+    __shared__ uint32_t s_def[4][128 * 5];  // per wave: deferred probes {i, tag | hidx, key word 0, probe hint}
     const uint8_t *s_hmap = reinterpret_cast<const uint8_t *>(s_hmap4);
     const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
 #pragma unroll
@@ -553,7 +553,8 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
     uint32_t c_tag = 0, c_k0 = 0, c_h = 0;
     int c_hidx = -1;
     uint64_t c_hint0 = 0, c_hint1 = 0;
-    constexpr uint32_t kDefCap = 256;   // deferred packets per wave (LDS)
+    constexpr uint32_t kDefCap = 128;   // deferred packets per wave (LDS)
+    constexpr uint32_t kDefW = 5;       // words per deferred packet
     uint32_t *dq = s_def[w];
     uint32_t ndef = 0;
     const uint64_t lt_mask = (1ull << lane) - 1ull;
@@ -582,13 +583,17 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
             const uint32_t e = e0 + lane;
             bool fresh = false;
             if (e < ndef) {
-                const uint32_t *q = dq + e * 3;
+                const uint32_t *q = dq + e * kDefW;
                 const uint32_t i = q[0], tag = q[1] & 0xFFu;
                 const int hidx = (int)(q[1] >> 8) - 1;
                 uint32_t k[4] = {q[2], 0, 0, 0};
                 if (tag == 2) packet_src(in, len, i, k);   // IPv6: the key again from the record
                 const uint64_t h = id_start(idt, tag, k);
-                const uint64_t hint = __hip_atomic_load(idt.head + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                // IPv4: the first probe slot's head as the probe read it (a stale value only
+                // costs the CAS one retry); IPv6 had no probe read
+                const uint64_t hint = tag == 1 ? ((uint64_t)q[4] << 32 | q[3])
+                                               : __hip_atomic_load(idt.head + h, __ATOMIC_RELAXED,
+                                                                   __HIP_MEMORY_SCOPE_AGENT);
                 const uint32_t id = id_resolve(idt, tag, k, h, hint, &fresh);
                 if (id == kNoSlot) atomicOr(&bs->err, ERR_TABLE_FULL);
                 const uint64_t out = word_of(id, tag, i, hidx);
@@ -726,8 +731,9 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
         if (dm) {
             if (ndef + 64 > kDefCap) flush();
             if (defer) {
-                uint32_t *q = dq + (ndef + (uint32_t)__popcll(dm & lt_mask)) * 3;
+                uint32_t *q = dq + (ndef + (uint32_t)__popcll(dm & lt_mask)) * kDefW;
                 q[0] = i; q[1] = c_tag | (uint32_t)(c_hidx + 1) << 8; q[2] = c_k0;
+                q[3] = (uint32_t)c_hint0; q[4] = (uint32_t)(c_hint0 >> 32);
             }
             ndef += (uint32_t)__popcll(dm);
         }

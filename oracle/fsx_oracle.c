@@ -287,7 +287,10 @@ void fsxo_get_stats(const fsxo_ctx *c, uint64_t out[2]) { out[0] = c->allowed; o
 static void src_track(fsxo_ctx *c, int v6, const uint8_t *key) {
     if (!(c->cfg.flags & FSXO_EVICT_IDLE)) return;
     static const uint8_t one = 1;
-    if (!omap_lookup(&c->src[v6], key) && omap_update(&c->src[v6], key, &one)) c->err = -ENOSPC;
+    if (omap_lookup(&c->src[v6], key)) return;
+    /* one capacity for both families, as the device table's */
+    if (c->src[0].count + c->src[1].count >= c->cfg.max_entries || omap_update(&c->src[v6], key, &one))
+        c->err = -ENOSPC;
 }
 
 static omap *map_of(fsxo_ctx *c, int map_id) {

@@ -93,12 +93,13 @@ def test_config2_stream_at_max_track_ips(native, oracle, pipeline):
 def test_mixed_families_with_gaps(native, oracle):
     rng = np.random.default_rng(31)
     hdr, ln, ts = rand_stream(rng, 60000, 3000, dt_max=40, v6_frac=0.4, nonip_frac=0.05)
-    # six batches 0.4 ms apart in time, window 1 ms: sources of two batches back go idle
+    # six batches 0.4 ms apart in time, window 1 ms: sources of three batches back go idle;
+    # up to 3488 sources tracked (both families share max_entries)
     cuts = np.linspace(0, len(ts), 7).astype(int)
     batches = []
     for j, (a, b) in enumerate(zip(cuts[:-1], cuts[1:])):
         t = ts[a:b] - ts[a] + np.uint64(10**9 + j * 400_000)
         batches.append((hdr[a:b], ln[a:b], t))
-    ev = run_both(native, oracle, batches, max_entries=2500, pps_threshold=20, window_ns=1_000_000,
+    ev = run_both(native, oracle, batches, max_entries=4000, pps_threshold=20, window_ns=1_000_000,
                   block_ns=500_000)
     assert sum(ev) > 0

@@ -86,3 +86,13 @@ def test_flag_rejected_for_other_limiters():
         with pytest.raises(lib.FsxError) as e:
             lib.FsxContext(limiter=lim, flags=lib.FLAG_EVICT_IDLE, max_batch=1024)
         assert e.value.code == -errno.EINVAL
+
+
+def test_families_share_the_capacity(oracle):
+    """Like the device table, IPv4 and IPv6 sources count against one max_entries."""
+    o = oracle.Oracle(max_entries=3, flags=oracle.EVICT_IDLE)
+    v6 = synth.records([synth.frame_ipv6_udp(bytes([0x20, 1] + [0] * 13 + [i]), 100) for i in (1, 2)])
+    o.batch(v6, np.full(2, 100, np.uint32), np.array([0, 1], np.uint64))
+    o.batch(*pkts([(1, 2)]))
+    with pytest.raises(RuntimeError):
+        o.batch(*pkts([(2, 3)]))      # 3 + 1 > 3, nothing idle: the fourth source overflows
