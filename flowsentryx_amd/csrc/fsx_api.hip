@@ -58,6 +58,8 @@ struct fsx_ctx {
     unsigned long long *idx_heads = nullptr;
     uint32_t *idx_k6 = nullptr;
     uint32_t idx_epoch = 1;
+    void *idx_mir = nullptr;     // IPv4 mirror of the heads (fsx_internal.h mir_entry; FSX_NO_MIRROR=1: off)
+    uint32_t idx_shift = 0;      // log2(slots)
     uint32_t pending_born = 0;  // generation of the in-flight limiter batch (rollback)
     // FSX_FLAG_EVICT_IDLE: survivors' copy (grown on demand), sources evicted before the
     // last limiter batch
@@ -335,7 +337,7 @@ void fsx_close(fsx_ctx *c) {
     hipFree(c->hist.tile_cnt); hipFree(c->hist.tile_off); hipFree(c->hist.total);
     hipFree(c->d_shard_cnt); hipFree(c->d_rep); hipFree(c->d_shard_own); hipFree(c->d_shard_crec);
     hipFree(c->d_rec_len); hipFree(c->d_rec_ts);
-    hipFree(c->idx_heads); hipFree(c->idx_k6);
+    hipFree(c->idx_heads); hipFree(c->idx_k6); hipFree(c->idx_mir);
     hipFree(c->evict_buf);
     hipFree(c->d_rule_slot); hipFree(c->d_rule_lens); hipFree(c->d_rule_filter);
     for (int r = 0; r < kRing; ++r)
@@ -402,6 +404,11 @@ int fsx_open(fsx_ctx **out, const fsx_config *cfg) {
     if (hipMalloc(&c->idx_k6, c->slots * 16) != hipSuccess) return fail(-ENOMEM);
     if (hipMemset(c->idx_heads, 0, c->slots * 8) != hipSuccess) return fail(-EIO);
     c->idx_epoch = 1;
+    while ((1ull << c->idx_shift) < c->slots) ++c->idx_shift;
+    if (!getenv("FSX_NO_MIRROR") && mir_bytes(c->idx_shift)) {
+        if (hipMalloc(&c->idx_mir, mir_bytes(c->idx_shift)) != hipSuccess) return fail(-ENOMEM);
+        if (hipMemset(c->idx_mir, 0, mir_bytes(c->idx_shift)) != hipSuccess) return fail(-EIO);
+    }
     if (hipMemset(c->tstate, 0, sizeof(TableState)) != hipSuccess) return fail(-EIO);
     if (hipMemset(c->bs, 0, sizeof(BatchState)) != hipSuccess) return fail(-EIO);
     if (alloc_scratch(c, k.max_batch)) return fail(-ENOMEM);
@@ -448,16 +455,19 @@ int fsx_set_stream(fsx_ctx *c, void *s) {
 }
 
 static TableIndex table_index(const fsx_ctx *c) {
-    return TableIndex{c->idx_heads, c->idx_k6, c->idx_epoch};
+    return TableIndex{c->idx_heads, c->idx_k6, c->idx_epoch, c->idx_mir, c->idx_shift};
 }
 
 // New epoch of the persistent index (every head reads empty); heads are cleared once
-// per 2^16 epochs so a stale cached line can never carry a current epoch.
+// per 2^16 epochs so a stale cached line can never carry a current epoch. The IPv4 mirror
+// carries no epoch: it is cleared at every epoch change (ordered before the next kernel
+// on the context stream; the survivors' entries are re-published by the rebuild).
 static int next_epoch(fsx_ctx *c) {
     if (++c->idx_epoch == 0x10000u) {
         HIPCHK(c, hipMemsetAsync(c->idx_heads, 0, c->slots * 8, c->stream));
         c->idx_epoch = 1;
     }
+    if (c->idx_mir) HIPCHK(c, hipMemsetAsync(c->idx_mir, 0, mir_bytes(c->idx_shift), c->stream));
     return 0;
 }
 

@@ -70,6 +70,8 @@ struct IdTable {
     Slot *slots;                // persistent index: a new source also gets its Slot here
     uint32_t born;              // ... stamped with this batch generation (rollback)
     uint32_t coherent;          // first probe with an agent-scope load (A/B: FSX_ID_COHERENT)
+    void *mir = nullptr;        // persistent index: IPv4 mirror (mir_entry), null when off
+    uint32_t mir_shift = 0;     // log2(slots)
 };
 
 __device__ __forceinline__ uint64_t id_start(const IdTable &T, uint32_t tag, const uint32_t k[4]) {
@@ -79,6 +81,8 @@ __device__ __forceinline__ uint64_t id_start(const IdTable &T, uint32_t tag, con
 // Slot of (tag, key), inserted if absent (*fresh = true); kNoSlot when the table is full
 // or a publication never completes (reported as a full table). h = id_start(...),
 // hint0 = a plain load of T.head[h] issued earlier.
+// kMirPub false: the caller knows the table has no mirror (k_parse's head-probe variant).
+template <bool kMirPub = true>
 __device__ __forceinline__ uint32_t id_resolve(const IdTable &T, uint32_t tag, const uint32_t k[4],
                                                uint64_t h, uint64_t hint0, bool *fresh) {
     const uint64_t ready = id_head(T.gen, kIdReady, tag, k[0]);
@@ -98,6 +102,9 @@ __device__ __forceinline__ uint32_t id_resolve(const IdTable &T, uint32_t tag, c
                         sl.pps = sl.bps = sl.tt = sl.till = sl.aux = 0;
                         sl.tag = tag;
                     }
+                    // (a reader that misses the new entry, 0 in a stale line, defers to this
+                    // full protocol; no other value can be seen in this epoch)
+                    if (kMirPub && tag == 1) mir_publish(T.mir, T.mir_shift, T.mask, T.seed, h, k[0]);
                     if (tag == 2) {
                         // Publication without release / acquire fences: on gfx950 an
                         // agent-scope release is a whole-L2 writeback (buffer_wbl2) and an
@@ -455,7 +462,7 @@ __device__ __forceinline__ bool rule_drop(const RuleSet &R, uint32_t tag, const 
 // pitch: conflict-free 32-bit reads), then each lane parses its own record.
 // Record mode (kRec = 16 / 32): every lane loads its own exchange record (coalesced, no
 // LDS staging), all of them IP packets; their len / ts go out to in.rec_len / rec_ts.
-template <uint32_t kRec, bool kRules>
+template <uint32_t kRec, bool kRules, bool kMir>
 #ifndef FSX_PARSE_MINB
 #define FSX_PARSE_MINB 4   // waves/SIMD bound of k_parse (A/B: scripts/build_variant.sh)
 #endif
@@ -553,6 +560,10 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
     uint32_t c_tag = 0, c_k0 = 0, c_h = 0;
     int c_hidx = -1;
     uint64_t c_hint0 = 0, c_hint1 = 0;
+    // kMir: the two mirror entries as the halves of one register (two 16-bit loads that
+    // stay in flight until the resolve)
+    typedef unsigned short mir2_t __attribute__((ext_vector_type(2)));
+    mir2_t c_m = {0, 0};
     constexpr uint32_t kDefCap = 128;   // deferred packets per wave (LDS)
     constexpr uint32_t kDefW = 5;       // words per deferred packet
     uint32_t *dq = s_def[w];
@@ -590,11 +601,11 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
                 if (tag == 2) packet_src(in, len, i, k);   // IPv6: the key again from the record
                 const uint64_t h = id_start(idt, tag, k);
                 // IPv4: the first probe slot's head as the probe read it (a stale value only
-                // costs the CAS one retry); IPv6 had no probe read
-                const uint64_t hint = tag == 1 ? ((uint64_t)q[4] << 32 | q[3])
+                // costs the CAS one retry); IPv6 (and IPv4 probed on the mirror) had no head read
+                const uint64_t hint = tag == 1 && !kMir ? ((uint64_t)q[4] << 32 | q[3])
                                                : __hip_atomic_load(idt.head + h, __ATOMIC_RELAXED,
                                                                    __HIP_MEMORY_SCOPE_AGENT);
-                const uint32_t id = id_resolve(idt, tag, k, h, hint, &fresh);
+                const uint32_t id = id_resolve<kMir>(idt, tag, k, h, hint, &fresh);
                 if (id == kNoSlot) atomicOr(&bs->err, ERR_TABLE_FULL);
                 const uint64_t out = word_of(id, tag, i, hidx);
                 packed[i] = out;
@@ -673,6 +684,7 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
         // sources are always resolved by the full protocol, which reads their key words
         // only after the head shows READY)
         c_hint0 = c_hint1 = 0;
+        if constexpr (kMir) c_m = mir2_t{0, 0};
 #ifdef FSX_MEASURE_NO_PROBE
         if (false) {
 #else
@@ -681,7 +693,11 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
             // (coherent=1 reads past the XCD's L2, which may hold the head of an older
             // epoch: a stale head can only fail the match, never fake one)
             const uint64_t h1 = (h + 1) & idt.mask;
-            if (idt.coherent) {
+            if constexpr (kMir) {   // the 2-byte mirror entries of the two slots (exact: mir_entry)
+                const unsigned short *mp = static_cast<const unsigned short *>(idt.mir);
+                c_m.x = mp[h];
+                c_m.y = mp[h1];
+            } else if (idt.coherent) {
                 c_hint0 = __hip_atomic_load(idt.head + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 c_hint1 = __hip_atomic_load(idt.head + h1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             } else {
@@ -715,13 +731,19 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
             if (hres && c_hidx >= 0) {
                 id = s_hslot[c_hidx];
             } else if (c_tag == 1) {
+                // the slot's head READY with this key, or its mirror entry (d = 0 / 1)
+                const uint64_t want0 = kMir ? mir_entry(c_k0, idt.seed, idt.mir_shift, 0u)
+                                            : id_head(idt.gen, kIdReady, 1u, c_k0);
+                const uint64_t want1 = kMir ? want0 | 1u << 14 : want0;
 #ifdef FSX_MEASURE_NO_PROBE
                 id = c_h;
-                c_hint0 = id_head(idt.gen, kIdReady, 1u, c_k0);
+                c_hint0 = want0;
+                c_m.x = (unsigned short)want0;
 #endif
-                const uint64_t ready = id_head(idt.gen, kIdReady, 1u, c_k0);
-                if (c_hint0 == ready) id = c_h;
-                else if (c_hint1 == ready) id = (uint32_t)((c_h + 1) & idt.mask);
+                const uint64_t got0 = kMir ? (uint64_t)c_m.x : c_hint0;
+                const uint64_t got1 = kMir ? (uint64_t)c_m.y : c_hint1;
+                if (got0 == want0) id = c_h;
+                else if (got1 == want1) id = (uint32_t)((c_h + 1) & idt.mask);
                 else defer = true;
             } else {
                 defer = true;
@@ -758,7 +780,7 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
     load(step_at(0), h0, L0, T0, P0);
     load(step_at(1), h1, L1, T1, P1);
     load(step_at(2), h2, L2, T2, P2);
-    c_tag = 0; c_hidx = -1; c_hint0 = c_hint1 = 0;
+    c_tag = 0; c_hidx = -1; c_hint0 = c_hint1 = 0; c_m = mir2_t{0, 0};
     if (S) parse_step(step_at(0), h0, L0, T0, P0);
     auto iter = [&](uint32_t q, const uint4 (&hp)[kHv], uint32_t Lp, uint64_t Tp, uint64_t Pp,
                     uint4 (&hl)[kHv], uint32_t &Ll, uint64_t &Tl, uint64_t &Pl) {
@@ -777,7 +799,7 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
             }
         }
         // A: parse step q + 1 (its records were loaded two iterations ago), probes issued
-        c_tag = 0; c_hidx = -1; c_hint0 = c_hint1 = 0;
+        c_tag = 0; c_hidx = -1; c_hint0 = c_hint1 = 0; c_m = mir2_t{0, 0};
         if (q + 1 < S) parse_step(step_at(q + 1), hp, Lp, Tp, Pp);
         // B: the record loads of step q + 3 into the set step q used
         load(step_at(q + 3), hl, Ll, Tl, Pl);
@@ -1310,13 +1332,14 @@ __global__ __launch_bounds__(256) void k_heads_heavy(BatchState *bs, const uint3
 // ------------------------------------------------------------------ table lookup / insert
 
 // Publish slot i of (tag, key) in the persistent index (single writer, between batches).
-__device__ __forceinline__ void index_publish(const TableIndex &X, uint64_t i, uint32_t tag,
-                                              const uint32_t k[4]) {
+__device__ __forceinline__ void index_publish(const TableIndex &X, const Limits &lim, uint64_t i,
+                                              uint32_t tag, const uint32_t k[4]) {
     if (tag == 2) {
         X.k6[i * 4 + 0] = k[1]; X.k6[i * 4 + 1] = k[2]; X.k6[i * 4 + 2] = k[3];
     }
     __threadfence();
     X.heads[i] = id_head(X.epoch, kIdReady, tag, k[0]);
+    if (tag == 1) mir_publish(X.mir, X.mir_shift, lim.table_mask, lim.seed, i, k[0]);
 }
 
 // Claim an empty slot for a key known to be absent (map ops: one thread, no batch in
@@ -1331,7 +1354,7 @@ __device__ __forceinline__ uint32_t table_claim(Slot *table, const Limits &lim, 
             s.flags = 0;
             s.key[0] = k[0]; s.key[1] = k[1]; s.key[2] = k[2]; s.key[3] = k[3];
             s.pps = s.bps = s.tt = s.till = s.aux = 0;
-            index_publish(X, i, tag, k);
+            index_publish(X, lim, i, tag, k);
             return (uint32_t)i;
         }
         i = (i + 1) & lim.table_mask;
@@ -1375,6 +1398,7 @@ __global__ __launch_bounds__(256) void k_index_rebuild(Slot *table, Limits lim, 
             X.k6[i * 4 + 0] = s.key[1]; X.k6[i * 4 + 1] = s.key[2]; X.k6[i * 4 + 2] = s.key[3];
         }
         X.heads[i] = id_head(X.epoch, kIdReady, s.tag, s.key[0]);
+        if (s.tag == 1) mir_publish(X.mir, X.mir_shift, lim.table_mask, lim.seed, i, s.key[0]);
     }
 }
 
@@ -2172,7 +2196,8 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
     // table slot); flow features alone use a per-batch id table and touch no map state
     static const uint32_t coherent = getenv("FSX_ID_COHERENT") ? 1u : 0u;
     const IdTable idt = do_limit
-        ? IdTable{X.heads, X.k6, lim.table_mask, lim.seed, X.epoch, lim.test_flags, table, id_gen, coherent}
+        ? IdTable{X.heads, X.k6, lim.table_mask, lim.seed, X.epoch, lim.test_flags, table, id_gen, coherent,
+                  X.mir, X.mir_shift}
         : IdTable{reinterpret_cast<unsigned long long *>(sc.id_tab), sc.id_tab + 2 * (lim.table_mask + 1),
                   lim.table_mask, lim.seed, id_gen, lim.test_flags, nullptr, 0, coherent};
     if ((e = hipMemsetAsync(sc.sort_ctl, 0, kSortCtlWords * 4, st)) != hipSuccess) return e;
@@ -2223,8 +2248,11 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
         // the prefix rules apply to limiter batches (an instantiation of its own, so the
         // rule-free parse keeps its registers)
         const bool rl = do_limit && rules.slot;
-#define FSX_PARSE(R, Q) k_parse<R, Q><<<g, 256, 0, st>>>(in, len, ts, n, sc.packed[0], verdict, bs, idt, \
-                                                        sc.sort_ctl, th, tcap, dp, hs, rules, tagh ? 1u : 0u)
+        // (kMir: light IPv4 sources probe the persistent index's mirror, not its heads)
+#define FSX_PARSE(R, Q) (idt.mir ? k_parse<R, Q, true><<<g, 256, 0, st>>>(in, len, ts, n, sc.packed[0], verdict, bs, idt, \
+                                                        sc.sort_ctl, th, tcap, dp, hs, rules, tagh ? 1u : 0u) \
+                                 : k_parse<R, Q, false><<<g, 256, 0, st>>>(in, len, ts, n, sc.packed[0], verdict, bs, idt, \
+                                                        sc.sort_ctl, th, tcap, dp, hs, rules, tagh ? 1u : 0u))
         if (!in.rec)
             rl ? FSX_PARSE(0, true) : FSX_PARSE(0, false);
         else if (in.rec_bytes == 16)
@@ -2365,7 +2393,8 @@ __global__ __launch_bounds__(256) void k_map_import(Slot *table, Limits lim, Tab
     const uint32_t tag = map_tag(map_id), bit = map_bit(map_id);
     const uint32_t kw = tag == 2 ? 4u : 1u;
     const uint32_t vw = bit == SLOT_HAS_ST ? 3u : bit == SLOT_HAS_TB ? 2u : 1u;
-    const IdTable idt{X.heads, X.k6, lim.table_mask, lim.seed, X.epoch, lim.test_flags, table, born, 0u};
+    const IdTable idt{X.heads, X.k6, lim.table_mask, lim.seed, X.epoch, lim.test_flags, table, born, 0u,
+                      X.mir, X.mir_shift};
     uint32_t fresh_n = 0;
     for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) {
         uint32_t k[4] = {0, 0, 0, 0};
@@ -2444,7 +2473,8 @@ __global__ __launch_bounds__(256) void k_evict_compact(const Slot *__restrict__ 
 
 __global__ __launch_bounds__(256) void k_evict_reinsert(Slot *table, TableState *tstate, Limits lim, TableIndex X,
                                                         const Slot *__restrict__ buf, uint64_t m) {
-    const IdTable idt{X.heads, X.k6, lim.table_mask, lim.seed, X.epoch, lim.test_flags, table, 0u, 0u};
+    const IdTable idt{X.heads, X.k6, lim.table_mask, lim.seed, X.epoch, lim.test_flags, table, 0u, 0u,
+                      X.mir, X.mir_shift};
     for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i < m; i += (uint64_t)gridDim.x * 256u) {
         const Slot s = buf[i];
         const uint64_t h = id_start(idt, s.tag, s.key);

@@ -56,6 +56,8 @@ struct TableIndex {
     unsigned long long *heads;
     uint32_t *k6;          // [slots][4]: IPv6 key words 1..3
     uint32_t epoch;
+    void *mir = nullptr;   // IPv4 mirror of the heads (mir_entry; null: off), cleared every epoch
+    uint32_t mir_shift = 0;   // log2(slots)
 };
 
 // One source IP (either family). tag: 0 empty, 1 IPv4, 2 IPv6.
@@ -223,16 +225,43 @@ __host__ __device__ inline uint32_t rule_hash(uint32_t tag, const uint32_t a[4])
     return (uint32_t)(h >> 32);
 }
 
+// IPv4 table hash: a bijection of the 32-bit address (salted fmix32), so a source's home
+// slot (the low log2(slots) bits) plus the remaining high bits name its address exactly.
+__host__ __device__ inline uint32_t v4_hash(uint32_t k0, uint64_t seed) {
+    return fmix32(k0 ^ (uint32_t)seed ^ (uint32_t)(seed >> 32));
+}
+
 // First probe slot of a source in the table (shared by k_parse, the map ops and the
 // index rebuild). Test hook FSX_FLAG_TEST_V6_COLLIDE: every IPv6 source starts at IPv4
 // 10.0.0.1's slot.
 __host__ __device__ inline uint64_t probe_start(uint32_t tag, const uint32_t k[4], uint64_t seed,
                                                 uint64_t mask, uint32_t test_flags) {
-    if (tag == 2 && (test_flags & 1u)) {
-        const uint32_t k10[4] = {0x0100000Au, 0, 0, 0};
-        return slot_hash(1u, k10, seed) & mask;
-    }
+    if (tag == 2 && (test_flags & 1u)) return v4_hash(0x0100000Au, seed) & mask;
+    if (tag == 1) return v4_hash(k[0], seed) & mask;
     return slot_hash(tag, k, seed) & mask;
+}
+
+// IPv4 mirror of the source index: one 2-byte entry per table slot, written
+// when an IPv4 source is published at its home slot (d = 0) or the slot after it (d = 1):
+// a valid bit, d and the 32 - log2(slots) hash bits above the home slot. v4_hash is a
+// bijection, so an entry equal to the one computed for an address IS that address: k_parse
+// matches light sources on 2-byte entries instead of the 8-byte heads (a quarter of the
+// bytes to keep in the XCD's L2). Tables of >= 2^18 slots (<= 14 high bits); smaller ones
+// (<= 2 MiB of heads) have none.
+constexpr uint32_t kMirShift = 18;
+__host__ __device__ inline size_t mir_bytes(uint32_t shift) {
+    return shift < kMirShift ? 0 : ((size_t)1 << shift) * 2;
+}
+__host__ __device__ inline uint32_t mir_entry(uint32_t k0, uint64_t seed, uint32_t shift, uint32_t d) {
+    return 0x8000u | d << 14 | (shift >= 32 ? 0u : v4_hash(k0, seed) >> shift);
+}
+// IPv4 source k0 published at slot pos: its mirror entry when pos is its first or second
+// probe slot.
+__device__ __forceinline__ void mir_publish(void *mir, uint32_t shift, uint64_t mask, uint64_t seed,
+                                            uint64_t pos, uint32_t k0) {
+    if (!mir) return;
+    const uint64_t d = (pos - (v4_hash(k0, seed) & mask)) & mask;
+    if (d <= 1) static_cast<uint16_t *>(mir)[pos] = (uint16_t)mir_entry(k0, seed, shift, (uint32_t)d);
 }
 
 // Slot of (tag, key) in the table (linear probing from its probe start), or kNoSlot.

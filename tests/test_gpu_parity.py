@@ -238,6 +238,41 @@ def test_failed_batch_rolls_back(native, oracle, limiter):
             assert c.map_dump(m) == o.map_dump(m), m
 
 
+def test_mirror_cleared_on_rollback_and_reset(native, oracle):
+    """Tables of >= 2^18 slots probe IPv4 sources on the 2-byte mirror of the source index
+    (DESIGN.md §3). A rolled-back batch's sources, and every source after fsx_reset, must not
+    match a stale mirror entry: the next batches re-send rolled-back and surviving sources and
+    equal an oracle that never saw the failed batch; after a reset, one that starts empty."""
+    from flowsentryx_amd import lib, synth
+    rng = np.random.default_rng(77)
+    cfg = dict(CFGS["tight"], max_entries=70_000)
+    h1, l1, t1 = rand_stream(rng, 20000, 3000, dt_max=200)
+    t1 = t1 + np.uint64(10**6)
+    nb = 70_000
+    big = synth.records([synth.frame_ipv4_udp(bytes([10, 77 + (i >> 16), (i >> 8) & 255, i & 255]), 90)
+                         for i in range(nb)])
+    tb = t1[-1] + np.arange(1, nb + 1, dtype=np.uint64)
+    # next batch: the first batch's sources again, plus 1000 of the rolled-back ones
+    pick = rng.integers(0, 1000, 4000)
+    h3 = np.concatenate([h1, big[pick]])
+    l3 = np.concatenate([l1, np.full(pick.size, 90, np.uint32)])
+    t3 = tb[-1] + np.arange(1, h3.shape[0] + 1, dtype=np.uint64) * 7
+    perm = rng.permutation(h3.shape[0])
+    h3, l3 = h3[perm], l3[perm]
+    o = oracle.Oracle(max_entries=1 << 18, **{k: v for k, v in cfg.items() if k != "max_entries"})
+    with gpu_ctx(native, max_batch=1 << 17, **cfg) as c:
+        assert np.array_equal(c.verdict_batch(h1, l1, t1), o.batch(h1, l1, t1))
+        with pytest.raises(lib.FsxError) as e:
+            c.verdict_batch(big, np.full(nb, 90, np.uint32), tb)
+        assert e.value.code == -errno.ENOSPC
+        assert np.array_equal(c.verdict_batch(h3, l3, t3), o.batch(h3, l3, t3))
+        assert_same_state(c, o)
+        c.reset()
+        o2 = oracle.Oracle(max_entries=1 << 18, **{k: v for k, v in cfg.items() if k != "max_entries"})
+        assert np.array_equal(c.verdict_batch(h3, l3, t3), o2.batch(h3, l3, t3))
+        assert_same_state(c, o2)
+
+
 def test_map_syscalls(native):
     from flowsentryx_amd import lib
     with gpu_ctx(native, max_entries=64, max_batch=64) as c:
