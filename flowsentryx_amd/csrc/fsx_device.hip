@@ -583,9 +583,9 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
     };
     auto word_of = [&](uint32_t id, uint32_t tag, uint32_t i, int hidx) -> uint64_t {
         uint64_t out = ((uint64_t)(id & idt.mask) << 32) | ((uint64_t)(tag - 1u) << 31) | i;
-        if (dp.light_b)   // heavy-source sort: the first pass's bucket in bits 56..63
+        if (dp.light_b)   // heavy-source sort: the first pass's bucket in bits [shift[0], 64)
             out |= (uint64_t)(hidx >= 0 ? dp.light_b + (uint32_t)hidx
-                                        : (uint32_t)(out >> 32) & (dp.light_b - 1u)) << 56;
+                                        : (uint32_t)(out >> 32) & (dp.light_b - 1u)) << dp.shift[0];
         return out;
     };
     // the deferred packets of this wave: full probes (CAS inserts), 64 at a time
@@ -881,6 +881,7 @@ __global__ __launch_bounds__(256) void k_hist_prep(const uint32_t *__restrict__ 
         if (dg == 0 && threadIdx.x == 0) bs->n_valid = tot;
         if (dg == 0 && light_b == 256 && threadIdx.x == 0) bs->n_light = tot;
         if (dg == 0 && light_b < 256 && threadIdx.x == light_b) bs->n_light = b;
+        if (dg == 0 && threadIdx.x == 0) bs->light_b = light_b;
     }
     if (threadIdx.x == 0)
         bs->pay_ok = bs->max_len < (1u << kPayLenBits) && bs->max_ts - ~bs->inv_min_ts < kPayTsRange;
@@ -1313,11 +1314,12 @@ __global__ __launch_bounds__(256) void k_heads_heavy(BatchState *bs, const uint3
     __shared__ uint32_t s_tmp[4];
     const uint32_t h = threadIdx.x;
     const uint32_t L = bs->nseg;   // light segments (k_scan_tiles_u32); read before the barrier
-    const bool live = h < kHeavyMax && cnt0[kHeavyMax + h] > 0;
+    const uint32_t lb = bs->light_b;
+    const bool live = h < kHeavyMax && cnt0[lb + h] > 0;
     uint32_t H;
     const uint32_t r = block256_excl(live ? 1u : 0u, s_tmp, &H);
     if (live) {
-        const uint32_t a = base0[kHeavyMax + h];
+        const uint32_t a = base0[lb + h];
         seg_start[L + r] = a;
         if (seg_slot) seg_slot[L + r] = pk_id(S[a], id_mask);
         if (seg_lo) seg_lo[L + r] = (uint32_t)S[a];
@@ -1648,9 +1650,9 @@ __device__ __forceinline__ void walk_heavy(const SV &sv, const BatchState *bs, c
     const uint32_t maxL = bs->max_len;
     const uint32_t h = blockIdx.x * 4u + (threadIdx.x >> 6);
     if (h >= H.hs->n) return;
-    const uint32_t c = cnt0[kHeavyMax + h];
+    const uint32_t c = cnt0[bs->light_b + h];
     if (c == 0) return;
-    const uint32_t a = base0[kHeavyMax + h], b = a + c;
+    const uint32_t a = base0[bs->light_b + h], b = a + c;
     Slot &sl = table[pk_id(sv.S[a], lim.table_mask)];
     FwState st = load_state(sl);
     const bool fast = glob_fast && (!st.has_st || (st.tt <= ~0ull - lim.window &&
@@ -2025,10 +2027,12 @@ hipError_t launch_tail(const TailArgs &a) {
     const bool fork = a.fork;   // flows beside the limiter
     hipStream_t hf = (hs != st && fork) ? st2 : hs;
     int hf_id = hf == st2 && hf != st ? 1 : hs_id;
-    uint64_t *S_fin = sc.packed[npass & 1], *pay_fin = sc.pay[npass & 1];
-    // heavy verdict lists live in the sort's other buffer, over the heavy positions (which the
-    // passes >= 1 never write)
-    const HeavyLists hlists{tagh ? reinterpret_cast<uint32_t *>(sc.packed[(npass + 1) & 1]) : nullptr, sc.heavy,
+    // the heavy runs: pass 0's output (packed[1]), which the light passes never write in
+    // [n_light, n) (with 3 passes also the light entries' final buffer)
+    uint64_t *S_fin = sc.packed[1], *pay_fin = sc.pay[1];
+    // heavy verdict lists live in the parse buffer over the heavy positions (which no pass
+    // writes after pass 0 read it)
+    const HeavyLists hlists{tagh ? reinterpret_cast<uint32_t *>(sc.packed[0]) : nullptr, sc.heavy,
                             tstate, bs};
     // the heavy runs' walker and flow sums, forked right after the sort (A/B, config 2: right
     // after pass 0 they slowed passes 1-2, after the heads they delayed the walkers; a fourth
@@ -2083,7 +2087,7 @@ hipError_t launch_tail(const TailArgs &a) {
                                              do_limit ? sc.seg_slot : nullptr, lim.table_mask, lo, seg_lo);
     if (tagh)
         k_heads_heavy<<<1, 256, 0, st>>>(bs, sc.sort_ctl, sc.gbase, sc.seg_start, do_limit ? sc.seg_slot : nullptr,
-                                         S, lim.table_mask, seg_lo);
+                                         S_fin, lim.table_mask, seg_lo);
     mark("k_heads_write");
     if (flows) {
         hipStream_t fs = st;
@@ -2101,7 +2105,7 @@ hipError_t launch_tail(const TailArgs &a) {
             return e;
         if (tagh) {   // the heavy sources' rows, from their sums (k_flow_heavy)
             if (hf != fs && (e = hipStreamWaitEvent(fs, heavy_flow_ev, 0)) != hipSuccess) return e;
-            if ((e = launch_flows_heavy_finish(S, bs, sc.sort_ctl, sc.seg_start, in, len, ts, sc.heavy_flow, sc.cap,
+            if ((e = launch_flows_heavy_finish(S_fin, bs, sc.sort_ctl, sc.seg_start, in, len, ts, sc.heavy_flow, sc.cap,
                                                flows->keys16, flows->fam, flows->feat, flows->prob, flows->dec,
                                                flows->cap, flows->score, lim.salt32,
                                                do_limit ? flows->sacc : nullptr, flows->epoch, sc.seg_slot, fs)) !=
@@ -2208,34 +2212,53 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
     // most 8 bits (21 bits: 3 x 7 — fewer buckets, longer runs per tile than 8 + 8 + 5)
     uint32_t idbits = 0;
     while ((1ull << idbits) <= lim.table_mask) ++idbits;
-    const int npass = std::max(1, (int)((idbits + 7) / 8));
+    int npass = std::max(1, (int)((idbits + 7) / 8));
     static const bool full_digits = getenv("FSX_SORT_FULL_DIGITS") != nullptr;   // A/B: 8,8,..,rest
     static const bool no_heavy = getenv("FSX_NO_HEAVY_SORT") != nullptr;          // A/B: plain LSD
     const uint32_t dbits = full_digits ? 8u : std::max<uint32_t>(1, (idbits + npass - 1) / npass);
     const uint32_t dmask = (1u << dbits) - 1u;
-    // Heavy-source sort (3-pass tables of <= 2^23 slots): pass 0 buckets the light
-    // entries by a 7-bit id digit and every heavy source into a bucket of its own; passes
-    // 1-2 sort the light entries only, by the remaining id bits in two equal digits.
-    const bool heavy_sort = !onesweep && !full_digits && !no_heavy && npass == 3 && idbits <= 23;
-    // heavy verdict lists (fixed window with the heavy-source sort; FSX_NO_HEAVY_LISTS=1: A/B)
+    // Heavy-source sort (tables of <= 2^25 slots): pass 0 buckets the light entries by a
+    // low id digit and every heavy source into a bucket of its own (the bucket in bits
+    // [bshift, 64) above the id: 8 bits, light digit 7 bits and 128 heavy sources; for
+    // 25-bit ids 7 bits, light digit 6 bits and 64 heavy sources); the later passes sort
+    // the light entries only, by the remaining id bits in equal digits. Pass 0 writes the
+    // other sort buffer, which then holds the heavy runs for good (the later passes cover
+    // [0, n_light)); with an even pass count the light entries end in the parse buffer, so
+    // the heavy runs are read from pass 0's buffer (S_heavy in the tail): only the fixed
+    // window's heavy verdict lists consume them apart from the light entries, so an even
+    // count is taken with those lists only.
     static const bool no_hlists = getenv("FSX_NO_HEAVY_LISTS") != nullptr;
-    const bool tagh = heavy_sort && do_limit && lim.limiter == 0 && verdict && !no_hlists;
+    const bool lists_ok = do_limit && lim.limiter == 0 && verdict && !no_hlists;
+    const uint32_t bshift = std::max<uint32_t>(56, 32 + idbits);
+    const uint32_t lbits = 63 - bshift;                 // light digit bits of the bucket
+    const uint32_t hrest = idbits > lbits ? idbits - lbits : 0;
+    const int hpass = 1 + (int)((hrest + 7) / 8);       // pass 0 + the light passes
+    const bool heavy_sort = !onesweep && !full_digits && !no_heavy && idbits <= 25 && npass >= 3 &&
+                            (hpass == 3 || (hpass == 4 && lists_ok));
+    if (heavy_sort) npass = hpass;   // (24-bit ids: 4 passes instead of 3, 3 of them over the light entries)
+    // heavy verdict lists (fixed window with the heavy-source sort; FSX_NO_HEAVY_LISTS=1: A/B)
+    const bool tagh = heavy_sort && lists_ok;
     if (!(split && split->tail) && (e = hipMemsetAsync(sc.marks, 0, n, st)) != hipSuccess) return e;
     DigitPlan dp{};
     dp.npass = (uint32_t)npass;
+    uint32_t nheavy = kHeavyMax;
     if (heavy_sort) {
-        const uint32_t rest = idbits - 7, w1 = (rest + 1) / 2;
-        dp.light_b = 128;
-        dp.shift[0] = 56; dp.mask[0] = 255;
-        dp.shift[1] = 39; dp.mask[1] = (1u << w1) - 1u;
-        dp.shift[2] = 39 + w1; dp.mask[2] = (1u << (rest - w1)) - 1u;
+        dp.light_b = 1u << lbits;
+        nheavy = std::min<uint32_t>(kHeavyMax, (1u << (64 - bshift)) - dp.light_b);
+        dp.shift[0] = bshift; dp.mask[0] = (1u << (64 - bshift)) - 1u;
+        const uint32_t lp = (uint32_t)hpass - 1, w = (hrest + lp - 1) / lp;
+        for (uint32_t p = 1; p <= lp; ++p) {
+            const uint32_t lo = (p - 1) * w, wb = std::min(w, hrest - lo);
+            dp.shift[p] = 32 + lbits + lo;
+            dp.mask[p] = (1u << wb) - 1u;
+        }
     }
     if (heavy_sort) {
         k_heavy_sample<<<64, 256, 0, st>>>(in, len, n, sc.sketch, lim.seed, lim.table_mask, lim.test_flags);
         // heavy slots resolved once (not under prefix rules; FSX_NO_HEAVY_SLOTS=1: A/B)
         static const bool no_hslots = getenv("FSX_NO_HEAVY_SLOTS") != nullptr;
         const uint32_t resolve = !no_hslots && !(do_limit && rules.slot) ? 1u : 0u;
-        k_heavy_pick<<<1, 1024, 0, st>>>(in, len, sc.sketch, sc.heavy, kHeavyMax, 16, lim.seed,
+        k_heavy_pick<<<1, 1024, 0, st>>>(in, len, sc.sketch, sc.heavy, nheavy, 16, lim.seed,
                                          lim.table_mask, lim.test_flags, idt, resolve, bs);
         mark("k_heavy_pick");
     } else {
@@ -2297,7 +2320,8 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
             mark("k_onesweep");
         } else {
             // passes >= 1 cover [0, n_light): the heavy entries (pass 0's top buckets) are
-            // final in pass 0's output, which is also the last pass's (npass odd)
+            // final in pass 0's output (packed[1]; the light entries end there too when npass
+            // is odd, in packed[0] when it is even)
             const uint32_t *Ld = pass == 0 ? nullptr : &bs->n_light;
             if (pass > 0) {   // pass 0's per-tile counts come from k_parse
                 k_tile_hist<<<ntiles, 256, 0, st>>>(in, n, Ld, shift, pmask, pass == 0, sc.hist, tcap);

@@ -289,9 +289,10 @@ hipError_t launch_flows(const uint64_t *S, const uint64_t *pay, BatchState *bs, 
 #endif
 constexpr uint32_t kHeavyChunk = FSX_HEAVY_CHUNK;
 
-__device__ __forceinline__ void heavy_chunk_prefix(const uint32_t *cnt0, uint32_t *s_pre, uint32_t *s_tmp) {
+__device__ __forceinline__ void heavy_chunk_prefix(const uint32_t *cnt0, uint32_t lb, uint32_t *s_pre,
+                                                   uint32_t *s_tmp) {
     const uint32_t h = threadIdx.x;
-    const uint32_t c = h < kHeavyMax ? (cnt0[kHeavyMax + h] + kHeavyChunk - 1) / kHeavyChunk : 0u;
+    const uint32_t c = h < kHeavyMax ? (cnt0[lb + h] + kHeavyChunk - 1) / kHeavyChunk : 0u;
     uint32_t tot;
     const uint32_t e = block256_excl(c, s_tmp, &tot);
     if (h < kHeavyMax) s_pre[h] = e;
@@ -301,7 +302,7 @@ __device__ __forceinline__ void heavy_chunk_prefix(const uint32_t *cnt0, uint32_
 
 template <class SV>
 __device__ __forceinline__ void flow_heavy_body(const SV &sv, const uint32_t *cnt0, const uint32_t *base0,
-                                                const uint32_t *s_pre, FlowAcc *part) {
+                                                uint32_t lb, const uint32_t *s_pre, FlowAcc *part) {
     const uint32_t items = s_pre[kHeavyMax];
     for (uint32_t it = blockIdx.x * 4u + (threadIdx.x >> 6); it < items; it += gridDim.x * 4u) {
         uint32_t lo = 0, hi = kHeavyMax;   // the bucket h with pre[h] <= it < pre[h + 1]
@@ -309,7 +310,7 @@ __device__ __forceinline__ void flow_heavy_body(const SV &sv, const uint32_t *cn
             const uint32_t m = (lo + hi) >> 1;
             if (s_pre[m] <= it) lo = m; else hi = m;
         }
-        const uint32_t rs = base0[kHeavyMax + lo], e = rs + cnt0[kHeavyMax + lo];
+        const uint32_t rs = base0[lb + lo], e = rs + cnt0[lb + lo];
         const uint32_t a = rs + (it - s_pre[lo]) * kHeavyChunk, b = min(e, a + kHeavyChunk);
         const FlowAcc A = flow_wave_acc(sv, rs, a, b);
         if (lane_id() == 0) part[it] = A;
@@ -324,14 +325,14 @@ __global__ __launch_bounds__(256) void k_flow_heavy(const uint64_t *__restrict__
     __shared__ uint32_t s_pre[kHeavyMax + 1];
     __shared__ uint32_t s_tmp[4];
     if (bs->err) return;
-    heavy_chunk_prefix(cnt0, s_pre, s_tmp);
+    heavy_chunk_prefix(cnt0, bs->light_b, s_pre, s_tmp);
     if (blockIdx.x == 0 && threadIdx.x <= kHeavyMax) pre[threadIdx.x] = s_pre[threadIdx.x];
     if (bs->pay_ok) {
         const SegView<true> sv{S, ts, len, pay, ~bs->inv_min_ts};
-        flow_heavy_body(sv, cnt0, base0, s_pre, part);
+        flow_heavy_body(sv, cnt0, base0, bs->light_b, s_pre, part);
     } else {
         const SegView<false> sv{S, ts, len, pay, 0};
-        flow_heavy_body(sv, cnt0, base0, s_pre, part);
+        flow_heavy_body(sv, cnt0, base0, bs->light_b, s_pre, part);
     }
 }
 
@@ -358,7 +359,7 @@ __global__ __launch_bounds__(256) void k_flow_heavy_finish(const uint64_t *__res
     __shared__ uint32_t s_tmp[4];
     if (bs->err) return;
     const uint32_t h = threadIdx.x;
-    const bool live = h < kHeavyMax && cnt0[kHeavyMax + h] > 0;
+    const bool live = h < kHeavyMax && cnt0[bs->light_b + h] > 0;
     const uint32_t r = block256_excl(live ? 1u : 0u, s_tmp, nullptr);
     if (live) flow_finish(bs->nseg_light + r, hacc[h], S, seg_start, in, len, salt, out, P);
 }

@@ -93,6 +93,8 @@ struct BatchState {
     uint32_t n_light;     // entries of non-heavy sources: sort passes >= 1 cover [0, n_light)
     uint32_t nseg_light;  // heavy verdict lists: segments ids [0, nseg_light) are light, the
                           // heavy sources' segments follow (k_heads_heavy)
+    uint32_t light_b;     // heavy-source sort: heavy source h is pass-0 bucket light_b + h
+                          // (k_hist_prep; 256 without the heavy sort)
 };
 
 // Sorted payload word carried through the onesweep passes next to each sort word:

@@ -246,3 +246,16 @@ def test_pipelined_host_pointer_batches(native, oracle):
         for a, b in ((0, 50_000), (50_000, 50_001), (50_001, 120_000)):
             assert np.array_equal(c.verdict_batch(hdr[a:b], ln[a:b], ts[a:b]), o.batch(hdr[a:b], ln[a:b], ts[a:b]))
         assert_same_state(c, o)
+
+
+def test_pipelined_wide_ids(native, oracle):
+    """Pipelined batches on a 2^25-slot table (the 4-pass heavy-source sort, heavy runs in
+    pass 0's buffer, heavy verdict lists in the parse buffer of each front set): three
+    uneven batches of the config-4 population with features + scores."""
+    from flowsentryx_amd import synth
+    p, s = synth.config_params(4)
+    n = 1 << 20
+    hdr, ln, ts = oracle.synth(p, s, 0, n)
+    cuts = [0, 250_000, 250_001, n]
+    _run(native, oracle, [(hdr[a:b], ln[a:b], ts[a:b]) for a, b in zip(cuts[:-1], cuts[1:])],
+         max_entries=16 << 20)

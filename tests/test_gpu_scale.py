@@ -13,7 +13,7 @@ import numpy as np
 import pytest
 
 from kat import GOLDEN
-from test_gpu_parity import _check_flows
+from test_gpu_parity import _check_flows, _process_batch_device
 
 pytestmark = pytest.mark.gpu
 
@@ -85,8 +85,9 @@ def test_config2_stream_all_limiters(native, oracle, limiter):
 
 def test_config4_share_16m_population(native, oracle):
     """BASELINE config 4's source population (16M Zipf(1.1) sources, 1B packets over 120 s):
-    the first 8M packets of the stream, max_entries = 16M (a 2^25-slot table: source ids
-    wider than 24 bits, the plain 4-pass sort), fixed window with state carried."""
+    the first 8M packets of the stream, max_entries = 16M (a 2^25-slot table: 25-bit source
+    ids, the 4-pass heavy-source sort with a 7-bit first bucket and 64 heavy sources),
+    fixed window with state carried."""
     from flowsentryx_amd import synth
     p, s = synth.config_params(4)
     n = 1 << 23
@@ -154,3 +155,18 @@ def test_flow_features_sources_of_many_tiles(native, oracle):
     counts = np.unique(hdr[:, 26:30].copy().view(np.uint32).reshape(-1), return_counts=True)[1]
     assert counts.max() >= 300_000
     _check_flows(native, oracle, hdr, ln, ts, cfg={"max_batch": 1 << 22})
+
+
+@pytest.mark.parametrize("max_entries", [6 << 20, 16 << 20], ids=["ids24", "ids25"])
+def test_wide_ids_full_path(native, oracle, max_entries):
+    """Tables of 2^24 / 2^25 slots take the 4-pass heavy-source sort (pass 0
+    into the other buffer, three light passes ending in the parse buffer, the heavy runs
+    read from pass 0's buffer): verdicts, features and q8 scores of two carried batches of
+    the config-4 population against the oracle."""
+    from flowsentryx_amd import synth
+    p, s = synth.config_params(4)
+    n = 1 << 21
+    hdr, ln, ts = oracle.synth(p, s, 0, n)
+    cut = 777_777
+    _process_batch_device(native, oracle, [(hdr[:cut], ln[:cut], ts[:cut]), (hdr[cut:], ln[cut:], ts[cut:])],
+                          max_entries=max_entries)
