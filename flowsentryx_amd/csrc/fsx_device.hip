@@ -1272,6 +1272,7 @@ __global__ __launch_bounds__(256) void k_heads_write(BatchState *bs, const uint8
                                                      uint32_t *__restrict__ seg_slot, uint64_t id_mask,
                                                      uint32_t light_only, uint32_t *__restrict__ seg_lo) {
     __shared__ uint32_t s_tmp[4];
+    __shared__ uint32_t s_pos[kTile];   // the tile's head positions, compacted
     const uint32_t M = light_only ? bs->n_light : bs->n_valid;
     const uint32_t ntiles = (M + kTile - 1) / kTile;
     for (uint32_t b = blockIdx.x; b < ntiles; b += gridDim.x) {
@@ -1288,17 +1289,24 @@ __global__ __launch_bounds__(256) void k_heads_write(BatchState *bs, const uint8
         uint32_t cnt = 0;
 #pragma unroll
         for (int k = 0; k < 4; ++k) cnt += __popc(f[k] & 0x01010101u);
-        uint32_t off = tile_off[t] + block256_excl(cnt, s_tmp, nullptr);
+        uint32_t tot;
+        uint32_t off = block256_excl(cnt, s_tmp, &tot);
+        // positions through LDS, then written out by consecutive threads (a tile full of
+        // one-packet sources, config 5's carpet, has 4096 heads: 16 per thread would be
+        // 16 strided 4-byte stores per array)
 #pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            if ((f[k >> 2] >> (8 * (k & 3))) & 1u) {
-                seg_start[off] = p0 + k;
-                const uint64_t v = S[p0 + k];
-                if (seg_slot) seg_slot[off] = pk_id(v, id_mask);   // id = table slot
-                if (seg_lo) seg_lo[off] = (uint32_t)v;
-                ++off;
-            }
+        for (int k = 0; k < 16; ++k)
+            if ((f[k >> 2] >> (8 * (k & 3))) & 1u) s_pos[off++] = p0 + k;
+        __syncthreads();
+        const uint32_t base = tile_off[t];
+        for (uint32_t j = threadIdx.x; j < tot; j += 256u) {
+            const uint32_t p = s_pos[j];
+            seg_start[base + j] = p;
+            const uint64_t v = S[p];
+            if (seg_slot) seg_slot[base + j] = pk_id(v, id_mask);   // id = table slot
+            if (seg_lo) seg_lo[base + j] = (uint32_t)v;
         }
+        __syncthreads();
     }
 }
 
