@@ -184,7 +184,6 @@ static void free_scratch(fsx_ctx *c) {
     hipFree(s.span_list); hipFree(s.sort_ctl); hipFree(s.gbase); hipFree(s.status);
     hipFree(s.lim_tiles); hipFree(s.sw_seg); hipFree(s.sketch); hipFree(s.heavy);
     hipFree(s.drop_list); hipFree(s.drop_cur); hipFree(s.heavy_flow);
-    hipFree(s.bins); hipFree(s.bin_cnt);
     s = Scratch{};
 }
 
@@ -230,19 +229,6 @@ static int alloc_scratch(fsx_ctx *c, uint64_t cap) {
     HIPCHK(c, hipMalloc(&s.heavy, sizeof(HeavySet)));
     HIPCHK(c, hipMemset(s.heavy, 0, sizeof(HeavySet)));
     HIPCHK(c, hipMalloc(&s.heavy_flow, heavy_flow_bytes(cap)));
-    // binned inserts: every context whose limiter batches can run without the heavy-source
-    // sort (ids outside 17..23 bits; launch_verdict_pipeline), bins of 16 home slots or more
-    // (2^15 slots for a 2^29-slot table: 256 KiB of heads, 2 MiB of slots per bin)
-    uint32_t idbits = 0;
-    while ((1ull << idbits) < c->slots) ++idbits;
-    if (idbits < 17 || idbits > 23) {
-        s.bin_bits = std::min<uint32_t>(14, idbits > 4 ? idbits - 4 : 0);
-        s.bin_shift = idbits - s.bin_bits;
-        const uint64_t nb = 1ull << s.bin_bits;
-        s.bin_cap = (uint32_t)std::min<uint64_t>(cap + 1, (cap + cap / 4) / nb + 2048);
-        HIPCHK(c, hipMalloc(&s.bins, nb * s.bin_cap * sizeof(uint4)));
-        HIPCHK(c, hipMalloc(&s.bin_cnt, nb * 4));
-    }
     s.cap = cap;
     return 0;
 }

@@ -158,27 +158,6 @@ struct DigitPlan {
     uint32_t light_b;   // heavy sort: buckets below light_b are light (id digit 0); 0 = plain
 };
 
-// Binned inserts (Scratch::bins; rec null: off). In a flood batch (flood_on) k_parse puts
-// every packet whose source it does not find into the bin of its home slot instead of
-// inserting it in place; k_bin_insert then inserts bin by bin, so the CASes on the heads,
-// the slot initialisations and the mirror entries of one bin touch one small region of the
-// table, and writes those packets' sort words. Which path a packet takes changes nothing
-// but the time: its sort word lands at its arrival index either way.
-struct FloodBins {
-    uint4 *rec;
-    uint32_t *cnt;
-    uint32_t cap, shift;
-};
-// k_parse's sort word for a packet left to the bins: bit 63, its tag and heavy index + 1
-// (q1 = tag | (hidx + 1) << 8) in bits 32..47, key word 0 below. No sort word has bit 63
-// set when ids have at most 31 bits (the condition for bins) except the non-IP sentinel,
-// whose bits 48..62 are set.
-constexpr uint64_t kDeferBit = 1ull << 63;
-__device__ __forceinline__ uint64_t defer_word(uint32_t q1, uint32_t k0) {
-    return kDeferBit | (uint64_t)(q1 & 0xFFFFu) << 32 | k0;
-}
-__device__ __forceinline__ bool is_defer_word(uint64_t v) { return (v >> 48) == (kDeferBit >> 48); }
-
 // parse_ethhdr / parse_ip6hdr / parse_ip4hdr (src/parsing_helper.h:49-136, dispatch
 // src/fsx_kern.c:123-148) on a record's dwords 3 and 5..9: family tag 1 (IPv4) / 2
 // (IPv6) with the raw source address in k, or 0 with the verdict of a packet that
@@ -483,7 +462,7 @@ __device__ __forceinline__ bool rule_drop(const RuleSet &R, uint32_t tag, const 
 // pitch: conflict-free 32-bit reads), then each lane parses its own record.
 // Record mode (kRec = 16 / 32): every lane loads its own exchange record (coalesced, no
 // LDS staging), all of them IP packets; their len / ts go out to in.rec_len / rec_ts.
-template <uint32_t kRec, bool kRules, bool kMir, bool kFlood>
+template <uint32_t kRec, bool kRules, bool kMir>
 #ifndef FSX_PARSE_MINB
 #define FSX_PARSE_MINB 4   // waves/SIMD bound of k_parse (A/B: scripts/build_variant.sh)
 #endif
@@ -495,7 +474,7 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
                                                IdTable idt, uint32_t *__restrict__ ghist,
                                                uint32_t *__restrict__ thist, uint32_t tcap,
                                                DigitPlan dp, const HeavySet *__restrict__ heavy,
-                                               RuleSet rules, uint32_t tagh, FloodBins fbn) {
+                                               RuleSet rules, uint32_t tagh) {
     __shared__ uint32_t s_rec[4][64 * 17];
     __shared__ uint32_t s_red[4][3];
     __shared__ unsigned long long s_ts[4], s_its[4];
@@ -513,7 +492,6 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
     s_t0[threadIdx.x] = 0;
     const uint32_t nh = heavy ? heavy->n : 0u;
     const bool hres = heavy && heavy->resolved;   // heavy slots known: no probe for them
-    const bool flood = kFlood && flood_on(bs);     // binned inserts (k_flood_probe decided)
     if (heavy) {
         s_hmap4[threadIdx.x] = reinterpret_cast<const uint32_t *>(heavy->map)[threadIdx.x];
         if (threadIdx.x < nh) {
@@ -771,11 +749,6 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
                 defer = true;
             }
         }
-        if (flood && defer) {   // a flood batch (no heavy sort): k_bin_scatter bins it by its home slot
-            packed[i] = defer_word(c_tag, c_k0);
-            defer = false;
-            c_tag = 0;   // (no sort word below)
-        }
         const uint64_t dm = __ballot(defer);
         if (dm) {
             if (ndef + 64 > kDefCap) flush();
@@ -877,135 +850,6 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
     }
 }
 
-// ------------------------------------------------------------------ binned inserts
-// k_flood_probe: before k_parse, a strided sample of kFloodSample packets looks its sources
-// up the way k_parse's fast path does (IPv4: the mirror entries or heads of the first two
-// probe slots; IPv6: the heads' tag and key word 0 there); more misses than hits makes the
-// batch a flood (flood_on). A wrong call costs time only.
-constexpr uint32_t kFloodSample = 16384;
-__global__ __launch_bounds__(256) void k_flood_probe(PacketIn in, const uint32_t *__restrict__ len, uint32_t n,
-                                                     IdTable idt, BatchState *bs) {
-    __shared__ uint32_t s_cnt[2];
-    if (threadIdx.x < 2) s_cnt[threadIdx.x] = 0;
-    __syncthreads();
-    const uint32_t g = blockIdx.x * 256u + threadIdx.x;
-    const uint32_t stride = n > kFloodSample ? n / kFloodSample : 1u;
-    const uint32_t i = g * stride;
-    if (g < kFloodSample && i < n) {
-        uint32_t k[4];
-        const uint32_t tag = packet_src(in, len, i, k);
-        if (tag) {
-            const uint64_t h = id_start(idt, tag, k), h1 = (h + 1) & idt.mask;
-            bool hit;
-            if (tag == 1 && idt.mir) {
-                const uint16_t *mp = static_cast<const uint16_t *>(idt.mir);
-                const uint32_t w0 = mir_entry(k[0], idt.seed, idt.mir_shift, 0u);
-                hit = mp[h] == w0 || mp[h1] == (w0 | 1u << 14);
-            } else {
-                const uint64_t want = id_head(idt.gen, kIdReady, tag, k[0]);
-                hit = idt.head[h] == want || idt.head[h1] == want;
-            }
-            atomicAdd(&s_cnt[0], 1u);
-            if (!hit) atomicAdd(&s_cnt[1], 1u);
-        }
-    }
-    __syncthreads();
-    if (threadIdx.x == 0 && s_cnt[0]) {
-        atomicAdd(&bs->flood_ip, s_cnt[0]);
-        atomicAdd(&bs->flood_miss, s_cnt[1]);
-    }
-}
-
-// A source k_parse left to the bins (or whose bin was full): found or inserted, its sort
-// word written at its arrival index, its digits counted into the block's s_hist.
-__device__ __forceinline__ bool bin_resolve(const IdTable &idt, BatchState *bs, uint64_t *packed,
-                                            const DigitPlan &dp, uint32_t (*s_hist)[256], uint32_t i,
-                                            uint32_t tag, const uint32_t k[4]) {
-    const uint64_t h = id_start(idt, tag, k);
-    const uint64_t hint = __hip_atomic_load(idt.head + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    bool fresh = false;
-    const uint32_t id = id_resolve(idt, tag, k, h, hint, &fresh);
-    if (id == kNoSlot) atomicOr(&bs->err, ERR_TABLE_FULL);
-    // (no heavy-source sort in a flood batch: the plain word)
-    const uint64_t out = ((uint64_t)(id & idt.mask) << 32) | ((uint64_t)(tag - 1u) << 31) | i;
-    packed[i] = out;
-    for (uint32_t dg = 0; dg < dp.npass; ++dg)
-        atomicAdd(&s_hist[dg][(uint32_t)(out >> dp.shift[dg]) & dp.mask[dg]], 1u);
-    return fresh;
-}
-
-// The block's digit counts and new sources into the batch totals.
-__device__ __forceinline__ void bin_flush_counts(uint32_t (*s_hist)[256], uint32_t *s_fresh, uint32_t nf,
-                                                 uint32_t *ghist, BatchState *bs) {
-    nf = wave_incl_sum(nf);
-    if (lane_id() == 63 && nf) atomicAdd(s_fresh, nf);
-    __syncthreads();
-#pragma unroll
-    for (int dg = 0; dg < 4; ++dg) {
-        const uint32_t c = s_hist[dg][threadIdx.x];
-        if (c) atomicAdd(&ghist[dg * 256 + threadIdx.x], c);
-    }
-    if (threadIdx.x == 0 && *s_fresh) atomicAdd(&bs->n_new, *s_fresh);
-}
-
-// Flood batches, after k_parse: every packet it left to the bins (defer_word) appended to
-// the bin of its home slot, in one coalesced pass over the parse output; one whose bin is
-// full is resolved here.
-__global__ __launch_bounds__(256) void k_bin_scatter(FloodBins fbn, PacketIn in, const uint32_t *__restrict__ len,
-                                                     uint32_t n, IdTable idt, BatchState *bs,
-                                                     uint64_t *__restrict__ packed, uint32_t *__restrict__ ghist,
-                                                     DigitPlan dp) {
-    __shared__ uint32_t s_hist[4][256];
-    __shared__ uint32_t s_fresh;
-    if (!flood_on(bs)) return;
-#pragma unroll
-    for (int d = 0; d < 4; ++d) s_hist[d][threadIdx.x] = 0;
-    if (threadIdx.x == 0) s_fresh = 0;
-    __syncthreads();
-    uint32_t nf = 0;
-    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) {
-        const uint64_t v = packed[i];
-        if (!is_defer_word(v)) continue;
-        const uint32_t q1 = (uint32_t)(v >> 32) & 0xFFFFu, tag = q1 & 0xFFu;
-        uint32_t k[4] = {(uint32_t)v, 0, 0, 0};
-        if (tag == 2) packet_src(in, len, i, k);
-        const uint32_t b = (uint32_t)(id_start(idt, tag, k) >> fbn.shift);
-        const uint32_t j = atomicAdd(&fbn.cnt[b], 1u);
-        if (j < fbn.cap) fbn.rec[(size_t)b * fbn.cap + j] = make_uint4(i, q1, k[0], 0u);
-        else nf += bin_resolve(idt, bs, packed, dp, s_hist, i, tag, k) ? 1u : 0u;
-    }
-    bin_flush_counts(s_hist, &s_fresh, nf, ghist, bs);
-}
-
-// One block per bin: its packets' sources found or inserted (id_resolve, as k_parse's
-// flush does), their sort words written at their arrival indices, their digits counted
-// into the sort's histograms (k_parse counted only the packets it resolved), the new
-// sources added to n_new. A bin's probe starts lie in 2^bin_shift consecutive slots.
-__global__ __launch_bounds__(256) void k_bin_insert(FloodBins fbn, PacketIn in, const uint32_t *__restrict__ len,
-                                                    IdTable idt, BatchState *bs, uint64_t *__restrict__ packed,
-                                                    uint32_t *__restrict__ ghist, DigitPlan dp) {
-    __shared__ uint32_t s_hist[4][256];
-    __shared__ uint32_t s_fresh;
-    if (!flood_on(bs)) return;
-    const uint32_t b = blockIdx.x;
-    const uint32_t m = min(fbn.cnt[b], fbn.cap);
-    if (m == 0) return;
-#pragma unroll
-    for (int d = 0; d < 4; ++d) s_hist[d][threadIdx.x] = 0;
-    if (threadIdx.x == 0) s_fresh = 0;
-    __syncthreads();
-    const uint4 *rec = fbn.rec + (size_t)b * fbn.cap;
-    uint32_t nf = 0;
-    for (uint32_t e = threadIdx.x; e < m; e += 256u) {
-        const uint4 r = rec[e];
-        const uint32_t i = r.x, tag = r.y & 0xFFu;
-        uint32_t k[4] = {r.z, 0, 0, 0};
-        if (tag == 2) packet_src(in, len, i, k);
-        nf += bin_resolve(idt, bs, packed, dp, s_hist, i, tag, k) ? 1u : 0u;
-    }
-    bin_flush_counts(s_hist, &s_fresh, nf, ghist, bs);
-}
-
 // ------------------------------------------------------------------ radix sort
 // LSD radix sort of the sort words on their 32-bit key: 4 passes of 8 bits, the
 // payload words (kPayLenBits) following the same permutation. Per pass the keys are
@@ -1048,14 +892,10 @@ __device__ __forceinline__ bool sort_item(uint32_t i, uint32_t end, int first, u
 }
 
 // Per-tile digit counts (one block per tile; per-wave LDS counters).
-// gate (pass 0 of a flood batch, whose binned packets k_parse could not count): runs only
-// when flood_on(gate).
 __global__ __launch_bounds__(256) void k_tile_hist(const uint64_t *__restrict__ in, uint32_t L_host,
                                                    const uint32_t *L_dev, uint32_t shift, uint32_t dmask,
-                                                   int first, uint32_t *__restrict__ thist, uint32_t tcap,
-                                                   const BatchState *gate) {
+                                                   int first, uint32_t *__restrict__ thist, uint32_t tcap) {
     __shared__ uint32_t sh[4][256];
-    if (gate && !flood_on(gate)) return;
     const uint32_t tid = threadIdx.x, w = tid >> 6;
     const uint32_t L = L_dev ? *L_dev : L_host;
     const uint32_t nact = (L + kSortTile - 1) / kSortTile;   // tiles of this pass
@@ -2432,17 +2272,6 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
     } else {
         for (int p = 0; p < 4; ++p) { dp.shift[p] = 32u + dbits * (uint32_t)p; dp.mask[p] = dmask; }
     }
-    // binned inserts for flood batches (contexts with bins, limiter batches without the
-    // heavy-source sort; FSX_NO_BINS=1: A/B): the sample decides on the device
-    static const bool no_bins = getenv("FSX_NO_BINS") != nullptr;
-    const bool flood_cap = sc.bins && !heavy_sort && do_limit && !onesweep && !no_bins && idbits <= 31;
-    FloodBins fbn{};
-    if (flood_cap) {
-        fbn = FloodBins{sc.bins, sc.bin_cnt, sc.bin_cap, sc.bin_shift};
-        if ((e = hipMemsetAsync(sc.bin_cnt, 0, (4ull << sc.bin_bits), st)) != hipSuccess) return e;
-        k_flood_probe<<<kFloodSample / 256, 256, 0, st>>>(in, len, n, idt, bs);
-        mark("k_flood_probe");
-    }
     {
         const uint32_t g = std::min<uint32_t>(256u * FSX_PARSE_MINB, ntiles);   // one resident block per slot
         const HeavySet *hs = heavy_sort ? sc.heavy : nullptr;
@@ -2450,33 +2279,20 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
         // the prefix rules apply to limiter batches (an instantiation of its own, so the
         // rule-free parse keeps its registers)
         const bool rl = do_limit && rules.slot;
-        // (kMir: light IPv4 sources probe the persistent index's mirror, not its heads;
-        // kFlood: a context with bins, whose k_parse reads the sample's verdict)
-#define FSX_PARSE4(R, Q, M, F) k_parse<R, Q, M, F><<<g, 256, 0, st>>>(in, len, ts, n, sc.packed[0], verdict, bs, idt, \
-                                                        sc.sort_ctl, th, tcap, dp, hs, rules, tagh ? 1u : 0u, fbn)
-#define FSX_PARSE(R, Q) (idt.mir ? (flood_cap ? FSX_PARSE4(R, Q, true, true) : FSX_PARSE4(R, Q, true, false)) \
-                                 : (flood_cap ? FSX_PARSE4(R, Q, false, true) : FSX_PARSE4(R, Q, false, false)))
+        // (kMir: light IPv4 sources probe the persistent index's mirror, not its heads)
+#define FSX_PARSE(R, Q) (idt.mir ? k_parse<R, Q, true><<<g, 256, 0, st>>>(in, len, ts, n, sc.packed[0], verdict, bs, idt, \
+                                                        sc.sort_ctl, th, tcap, dp, hs, rules, tagh ? 1u : 0u) \
+                                 : k_parse<R, Q, false><<<g, 256, 0, st>>>(in, len, ts, n, sc.packed[0], verdict, bs, idt, \
+                                                        sc.sort_ctl, th, tcap, dp, hs, rules, tagh ? 1u : 0u))
         if (!in.rec)
             rl ? FSX_PARSE(0, true) : FSX_PARSE(0, false);
         else if (in.rec_bytes == 16)
             rl ? FSX_PARSE(16, true) : FSX_PARSE(16, false);
         else
             rl ? FSX_PARSE(32, true) : FSX_PARSE(32, false);
-#undef FSX_PARSE4
 #undef FSX_PARSE
     }
     mark("k_parse");
-    if (flood_cap) {   // (both return at once unless the batch is a flood)
-        k_bin_scatter<<<std::min<uint32_t>(4096, cdiv(n, 256)), 256, 0, st>>>(fbn, in, len, n, idt, bs, sc.packed[0],
-                                                                           sc.sort_ctl, dp);
-        mark("k_bin_scatter");
-        k_bin_insert<<<1u << sc.bin_bits, 256, 0, st>>>(fbn, in, len, idt, bs, sc.packed[0], sc.sort_ctl, dp);
-        mark("k_bin_insert");
-        if (!onesweep)   // pass 0's per-tile counts again, over every packet
-            k_tile_hist<<<ntiles, 256, 0, st>>>(sc.packed[0], n, nullptr, dp.shift[0], dp.mask[0], 1, sc.hist,
-                                                tcap, bs);
-        mark("k_tile_hist");
-    }
     // Heavy verdict lists: every heavy source is one run of pass 0's output (the later passes
     // write [0, n_light) only) whose segment needs no head search, so its walker and its flow
     // sums run on the third stream beside the heads, the classes and the light walkers, which
@@ -2516,7 +2332,7 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
             // is odd, in packed[0] when it is even)
             const uint32_t *Ld = pass == 0 ? nullptr : &bs->n_light;
             if (pass > 0) {   // pass 0's per-tile counts come from k_parse
-                k_tile_hist<<<ntiles, 256, 0, st>>>(in, n, Ld, shift, pmask, pass == 0, sc.hist, tcap, nullptr);
+                k_tile_hist<<<ntiles, 256, 0, st>>>(in, n, Ld, shift, pmask, pass == 0, sc.hist, tcap);
                 mark("k_tile_hist");
             }
             k_tile_scan<<<pmask + 1, 256, 0, st>>>(sc.hist, tcap, n, Ld, sc.gbase + 256 * pass);

@@ -95,15 +95,7 @@ struct BatchState {
                           // heavy sources' segments follow (k_heads_heavy)
     uint32_t light_b;     // heavy-source sort: heavy source h is pass-0 bucket light_b + h
                           // (k_hist_prep; 256 without the heavy sort)
-    uint32_t flood_ip;    // binned inserts: sampled IP packets before k_parse ...
-    uint32_t flood_miss;  // ... and those whose source the index does not hold yet
 };
-
-// A batch whose sampled packets are mostly from sources the index does not hold (a
-// spoofed-source flood) defers its inserts into bins by home slot (k_bin_insert).
-__host__ __device__ inline bool flood_on(const BatchState *bs) {
-    return bs->flood_ip > 0 && 2u * bs->flood_miss > bs->flood_ip;
-}
 
 // Sorted payload word carried through the onesweep passes next to each sort word:
 // (ts - min_ts) << 24 | len. Valid when every ts is within 2^40 ns (~18 min) of the
@@ -364,12 +356,6 @@ struct Scratch {
                            // packets [kSketch] each (counts zeroed by k_heavy_pick after use)
     HeavySet *heavy;
     void *heavy_flow;      // heavy sources' flow chunk sums (heavy_flow_bytes)
-    // binned inserts (contexts whose batches can run without the heavy-source sort): a
-    // flood batch's new-source packets as {arrival index, tag | heavy index + 1 << 8, key
-    // word 0, 0} in 2^bin_bits bins of bin_cap records by home slot (slot >> bin_shift)
-    uint4 *bins;
-    uint32_t *bin_cnt;
-    uint32_t bin_bits, bin_shift, bin_cap;
     uint64_t cap;          // packets the scratch is sized for
 };
 
