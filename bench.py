@@ -91,7 +91,7 @@ def parse_args():
     ap.add_argument("--cold", action="store_true",
                     help="headline: every step the same batch from empty maps (fsx_reset inside "
                          "the step) instead of consecutive batches with the maps carried")
-    ap.add_argument("--legs", default="cold,unpipelined,limiters,rules,config3,config4,config5",
+    ap.add_argument("--legs", default="cold,unpipelined,distinct,limiters,rules,config3,config4,config5",
                     help="comma-separated extra legs ('' for none)")
     ap.add_argument("--leg-steps", type=int, default=5, help="timed steps per leg")
     ap.add_argument("--kernel-timing-steps", type=int, default=5,
@@ -249,7 +249,7 @@ def main():
 
     # ------------------------------------------------------------------ workload runner
     def run_workload(cfg_no, n, steps, warmup, with_flows, kernel_timing=False, check=False,
-                     cpu=False, stream=False, pipelined=True):
+                     cpu=False, stream=False, pipelined=True, distinct=1):
         """Weak-scaled config cfg_no (n packets per rank), full pipeline; returns a dict.
 
         stream=False (cold): every step is the same batch from empty maps (fsx_reset inside
@@ -257,7 +257,10 @@ def main():
         (the reference's maps persist; no reset) — batch k is the config batch shifted by k
         stream durations (one pre-generated ts array per batch in HBM, two verdict buffers
         alternating); on one GPU the batches are pipelined (fsx_set_pipeline: the parse and
-        sort of batch k + 1 overlap the tail of batch k)."""
+        sort of batch k + 1 overlap the tail of batch k). distinct=R (one GPU, stream): R
+        consecutive batches of one R-times longer stream (distinct header bytes: other
+        packets of the same population), batch k = stream batch k mod R shifted by
+        (k div R) x R durations."""
         p, zipf_s = synth.config_params(cfg_no, n=None if cfg_no == 4 else n)
         # ONE stream of world*n packets at the config's packet rate from one population
         # (config 4: the 1B-packet stream itself, rank r's share of n packets); in
@@ -268,7 +271,14 @@ def main():
             p.n = n * world
             p.duration_ns = p.duration_ns * world
         j0s = [world * bounds[i] + rank * (bounds[i + 1] - bounds[i]) for i in range(chunks)]
-        d = gen_stream(torch, synth, p, zipf_s, j0s, n, bounds)
+        nd = distinct if (stream and world == 1) else 1
+        if nd > 1:
+            pg = type(p).from_buffer_copy(p)   # the generator's stream: nd batches long
+            pg.n, pg.duration_ns = p.n * nd, p.duration_ns * nd
+            D = [gen_stream(torch, synth, pg, zipf_s, [k * n], n) for k in range(nd)]
+        else:
+            D = [gen_stream(torch, synth, p, zipf_s, j0s, n, bounds)]
+        d = D[0]
         max_entries = max(1024, int(p.n_ips) if p.n_ips else n * world)
         lim_id = {"fixed": lib.LIMIT_FIXED_WINDOW, "sliding": lib.LIMIT_SLIDING_WINDOW,
                   "token": lib.LIMIT_TOKEN_BUCKET}[args.limiter]
@@ -299,7 +309,9 @@ def main():
             R = total if total * n * 8 <= budget else max(6, budget // (n * 8))
             if args.ts_ring:
                 R = min(R, max(6, args.ts_ring))
-            tss = [d["ts"] + k * dur for k in range(min(R, total))]
+            def ts_of(k):   # batch k's timestamp base and shift
+                return D[k % nd]["ts"], (k // nd) * nd * dur + (k % nd) * 0
+            tss = [ts_of(k)[0] + ts_of(k)[1] for k in range(min(R, total))]
             held = list(range(len(tss)))   # the batch each array currently holds
             # one verdict buffer per pipelined batch in flight (fsx_ctx::kSets = 3): a batch's
             # outputs are not touched until it completes
@@ -316,20 +328,22 @@ def main():
         def step(k, feat=False, v=None):
             if stream and held[k % len(tss)] != k:   # ring: refill this batch's timestamps in order
                 with torch.cuda.stream(rs) if rs is not None else contextlib.nullcontext():
-                    torch.add(d["ts"], k * dur, out=tss[k % len(tss)])
+                    base, shift = ts_of(k)
+                    torch.add(base, shift, out=tss[k % len(tss)])
                 held[k % len(tss)] = k
             ts_k = tss[k % len(tss) if stream else 0]
+            bk = D[k % nd]   # (its header records and lengths)
             v = vb[k % len(vb)] if v is None else v
             if not stream and not args.no_reset:
                 ctx.reset()
             if plane is not None:
                 if not stream:
                     plane.reset()
-                plane.verdict_batch(d["hdr"], d["len"], ts_k, n, v, bounds=bounds, chunks=chunks)
+                plane.verdict_batch(bk["hdr"], bk["len"], ts_k, n, v, bounds=bounds, chunks=chunks)
             elif not with_flows:
-                ctx.verdict_batch_device(d["hdr"].data_ptr(), d["len"].data_ptr(), ts_k.data_ptr(), n, v.data_ptr())
+                ctx.verdict_batch_device(bk["hdr"].data_ptr(), bk["len"].data_ptr(), ts_k.data_ptr(), n, v.data_ptr())
             else:
-                ctx.process_batch_device(d["hdr"].data_ptr(), d["len"].data_ptr(), ts_k.data_ptr(), n, v.data_ptr(),
+                ctx.process_batch_device(bk["hdr"].data_ptr(), bk["len"].data_ptr(), ts_k.data_ptr(), n, v.data_ptr(),
                                          fl["keys"].data_ptr(), fl["fam"].data_ptr(),
                                          fl["feat"].data_ptr() if feat else None,
                                          fl["prob"].data_ptr(), fl["dec"].data_ptr(), fcap)
@@ -391,11 +405,12 @@ def main():
             for k in range(nb):
                 step(k, feat=k == nb - 1, v=vs[k])
             ctx.sync()
-            hdr, ln, _ = host_inputs(d, n)
             from oracle import pyoracle
             orc = pyoracle.ShardedOracle(cores, max_entries=max_entries)
             ok = True
             for k in range(nb):
+                if k < nd:   # batch k's records (the same bytes again once k >= nd)
+                    hdr, ln, _ = host_inputs(D[k % nd], n)
                 ts_k = tss[k % len(tss)].cpu().numpy().view(np.uint64)
                 c0 = time.perf_counter()
                 vo = orc.batch(hdr, ln, ts_k)
@@ -417,6 +432,7 @@ def main():
         ctx.close()
         del tss, vb
         out["d"] = d
+        del D
         return out
 
     # ------------------------------------------------------------------ headline
@@ -567,6 +583,21 @@ def main():
                                  "the headline's stream (maps carried), batches not pipelined"}
             del r_["d"], r_
             torch.cuda.empty_cache()
+    if world == 1 and "distinct" in legs:
+        # the headline with different header bytes in every batch (the
+        # headline replays one batch's records, shifted in time): 4 consecutive batches of one
+        # 4 x 64M-packet stream of the same 1M-source population, cycled (batch k = stream batch
+        # k mod 4, shifted by (k div 4) x 120 s), maps carried, pipelined; the first three
+        # batches checked against the oracle like the headline's
+        r_ = run_workload(args.config, n_head, args.leg_steps * 2, 2, not args.no_mlp,
+                          check=not args.no_check, stream=True, pipelined=True, distinct=4)
+        results["distinct"] = {"value": round(r_["mpps"], 2), "unit": "Mpps",
+                               "ms_per_step": round(r_["ms_step"], 4), "steps": r_["steps"],
+                               "sources_last_batch": r_["sources"], "check": r_.get("check"),
+                               "note": "4 distinct consecutive batches of one stream of the config's "
+                                       "population, cycled with the maps carried, pipelined"}
+        del r_["d"], r_
+        torch.cuda.empty_cache()
     d = None
 
     del d
@@ -768,6 +799,7 @@ def main():
         "check": head.get("check"),
         "limiters": results.get("limiters"), "prefix_rules": results.get("prefix_rules"),
         "cold": results.get("cold"), "unpipelined": results.get("unpipelined"),
+        "distinct": results.get("distinct"),
         "warm": results.get("warm"), "config3": results.get("config3"),
         "config4": results.get("config4"), "config5": results.get("config5"),
         "exchange": head.get("exchange"),
