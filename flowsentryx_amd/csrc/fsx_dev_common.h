@@ -110,15 +110,16 @@ __device__ __forceinline__ void load_key6(const uint8_t *hdr, uint32_t i, uint32
     k[3] = (d8 >> 16) | (d9 << 16);
 }
 
-// Full key (family tag 1/2 + address words) of a packed sort word, from its record.
+// Full key (family tag 1/2 + address words) of a packed sort word, from its record (an IP
+// packet's record: EtherType 0x86DD is IPv6, 0x0800 IPv4, as k_parse decided).
 __device__ __forceinline__ uint32_t key_of(uint64_t v, const uint8_t *hdr, uint32_t salt,
                                            uint32_t k[4]) {
     (void)salt;
-    if (pk_fam(v)) {
+    const uint32_t *d = reinterpret_cast<const uint32_t *>(hdr + (size_t)pk_idx(v) * 64);
+    if ((d[3] & 0xFFFFu) == 0xDD86u) {   // bytes 12..13 = 86 DD
         load_key6(hdr, pk_idx(v), k);
         return 2u;
     }
-    const uint32_t *d = reinterpret_cast<const uint32_t *>(hdr + (size_t)pk_idx(v) * 64);
     k[0] = (d[6] >> 16) | (d[7] << 16);   // bytes 26..29
     k[1] = k[2] = k[3] = 0;
     return 1u;

@@ -582,10 +582,11 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
                 atomicAdd(&s_hist[dg][(uint32_t)(out >> dp.shift[dg]) & dp.mask[dg]], 1u);
     };
     auto word_of = [&](uint32_t id, uint32_t tag, uint32_t i, int hidx) -> uint64_t {
-        uint64_t out = ((uint64_t)(id & idt.mask) << 32) | ((uint64_t)(tag - 1u) << 31) | i;
+        (void)tag;
+        uint64_t out = ((uint64_t)(id & idt.mask) << kIdShift) | i;
         if (dp.light_b)   // heavy-source sort: the first pass's bucket in bits [shift[0], 64)
             out |= (uint64_t)(hidx >= 0 ? dp.light_b + (uint32_t)hidx
-                                        : (uint32_t)(out >> 32) & (dp.light_b - 1u)) << dp.shift[0];
+                                        : (uint32_t)(out >> kIdShift) & (dp.light_b - 1u)) << dp.shift[0];
         return out;
     };
     // the deferred packets of this wave: full probes (CAS inserts), 64 at a time
@@ -1218,7 +1219,7 @@ __global__ __launch_bounds__(256) void k_heads_count(const uint64_t *__restrict_
             uint64_t prev = __shfl_up(cur[k], 1);
             if (lane == 0 && p > 0 && p < M) prev = S[p - 1];
             if (p < M) {
-                const bool h = p == 0 || (prev >> 32) != (cur[k] >> 32);
+                const bool h = p == 0 || (prev >> kIdShift) != (cur[k] >> kIdShift);
                 headf[p] = h ? 1u : 0u;
                 cnt += h;
                 sub[k >> 2] += h;
@@ -2237,7 +2238,7 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
     // count is taken with those lists only.
     static const bool no_hlists = getenv("FSX_NO_HEAVY_LISTS") != nullptr;
     const bool lists_ok = do_limit && lim.limiter == 0 && verdict && !no_hlists;
-    const uint32_t bshift = std::max<uint32_t>(56, 32 + idbits);
+    const uint32_t bshift = std::max<uint32_t>(56, kIdShift + idbits);
     const uint32_t lbits = 63 - bshift;                 // light digit bits of the bucket
     const uint32_t hrest = idbits > lbits ? idbits - lbits : 0;
     const int hpass = 1 + (int)((hrest + 7) / 8);       // pass 0 + the light passes
@@ -2253,11 +2254,13 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
     if (heavy_sort) {
         dp.light_b = 1u << lbits;
         nheavy = std::min<uint32_t>(kHeavyMax, (1u << (64 - bshift)) - dp.light_b);
+        static const uint32_t heavy_n = getenv("FSX_HEAVY_N") ? (uint32_t)atoi(getenv("FSX_HEAVY_N")) : 0u;
+        if (heavy_n) nheavy = std::min(nheavy, heavy_n);   // (A/B: fewer heavy sources)
         dp.shift[0] = bshift; dp.mask[0] = (1u << (64 - bshift)) - 1u;
         const uint32_t lp = (uint32_t)hpass - 1, w = (hrest + lp - 1) / lp;
         for (uint32_t p = 1; p <= lp; ++p) {
             const uint32_t lo = (p - 1) * w, wb = std::min(w, hrest - lo);
-            dp.shift[p] = 32 + lbits + lo;
+            dp.shift[p] = kIdShift + lbits + lo;
             dp.mask[p] = (1u << wb) - 1u;
         }
     }
@@ -2270,7 +2273,7 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
                                          lim.table_mask, lim.test_flags, idt, resolve, bs);
         mark("k_heavy_pick");
     } else {
-        for (int p = 0; p < 4; ++p) { dp.shift[p] = 32u + dbits * (uint32_t)p; dp.mask[p] = dmask; }
+        for (int p = 0; p < 4; ++p) { dp.shift[p] = kIdShift + dbits * (uint32_t)p; dp.mask[p] = dmask; }
     }
     {
         const uint32_t g = std::min<uint32_t>(256u * FSX_PARSE_MINB, ntiles);   // one resident block per slot

@@ -284,16 +284,17 @@ __device__ inline uint32_t table_find(const Slot *table, const Limits &lim, uint
     return kNoSlot;
 }
 
-// packed sort word: bucket << 56 | source id << 32 | family << 31 | arrival index
-// (n <= 2^31 - 1; ids < 2^32, max_entries <= 2^31); the source id is the source's slot in the id table (k_parse), so equal
-// ids <=> equal (family, address) and the sort needs only log2(slots) key bits. The
-// bucket (heavy-source sort only, ids of <= 24 bits) is the first sort pass's digit: the
-// source's heavy index above the light digits, or digit 0 of its id (HeavySet).
-__host__ __device__ inline uint32_t pk_skey(uint64_t v) { return (uint32_t)(v >> 32); }
-// id_mask = table_mask: with the heavy-source sort the top byte holds the first-pass bucket
-// (ids of <= 23 bits); without it the id may use all 32 bits (tables of up to 2^32 slots).
-__host__ __device__ inline uint32_t pk_id(uint64_t v, uint64_t id_mask) { return (uint32_t)((v >> 32) & id_mask); }
-__host__ __device__ inline uint32_t pk_fam(uint64_t v) { return (uint32_t)(v >> 31) & 1u; }
+// packed sort word: bucket << bshift | source id << 31 | arrival index (n <= 2^31 - 1; ids
+// < 2^32, max_entries <= 2^31). The source id is the source's slot in the id table
+// (k_parse), so equal ids <=> equal (family, address) and the sort needs only log2(slots)
+// key bits; the family is read from the packet's own record where it is needed (key_of).
+// The bucket (heavy-source sort only, ids of <= 25 bits: bits 56..63) is the first sort
+// pass's digit: the source's heavy index above the light digits, or a low id digit
+// (HeavySet).
+constexpr uint32_t kIdShift = 31;
+// id_mask = table_mask: with the heavy-source sort the top byte holds the first-pass bucket;
+// without it the id may use bits 31..62 (tables of up to 2^32 slots).
+__host__ __device__ inline uint32_t pk_id(uint64_t v, uint64_t id_mask) { return (uint32_t)((v >> kIdShift) & id_mask); }
 __host__ __device__ inline uint32_t pk_idx(uint64_t v) { return (uint32_t)v & 0x7FFFFFFFu; }
 
 // ------------------------------------------------------------ launchers (fsx_device.hip)
