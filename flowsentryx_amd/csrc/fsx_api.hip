@@ -145,6 +145,11 @@ struct fsx_ctx {
     hipEvent_t tail_done[kSets]{};
     hipEvent_t front_done = nullptr;  // after the last pipelined batch's sort
     hipEvent_t parse_done = nullptr;  // after the current pipelined batch's parse
+    hipEvent_t pro_wait = nullptr, pro_done = nullptr;   // early prologue (PipeSplit)
+    // context-stream work other than a split batch's front was enqueued since pro_wait was
+    // last recorded (every other entry point goes through sel()): the next early prologue
+    // waits for all of it
+    bool pro_fence = true;
     TailArgs tail_args{};             // the last pipelined batch's tail, not yet enqueued
     bool tail_pending = false;
     int tail_par = 0;
@@ -279,6 +284,7 @@ static hipError_t pipe_on_parse(void *p) {
 // the context stream continues after it (the tail runs on its own streams).
 static int sel(fsx_ctx *c) {
     HIPCHK(c, hipSetDevice(c->device));
+    c->pro_fence = true;
     if (c->tail_pending) {
         hipError_t e = flush_tail(c, c->front_done);
         if (e != hipSuccess) return set_err(c, -EIO, "pipelined tail: %s", hipGetErrorString(e));
@@ -327,6 +333,8 @@ void fsx_close(fsx_ctx *c) {
     for (int p = 0; p < fsx_ctx::kSets; ++p) if (c->tail_done[p]) hipEventDestroy(c->tail_done[p]);
     if (c->front_done) hipEventDestroy(c->front_done);
     if (c->parse_done) hipEventDestroy(c->parse_done);
+    if (c->pro_wait) hipEventDestroy(c->pro_wait);
+    if (c->pro_done) hipEventDestroy(c->pro_done);
     free_scratch(c);
     hipFree(c->table); hipFree(c->tstate); hipFree(c->bs);
     hipFree(c->d_hdr); hipFree(c->d_len); hipFree(c->d_ts); hipFree(c->d_verdict);
@@ -575,6 +583,8 @@ int fsx_set_pipeline(fsx_ctx *c, int on) {
             if (!c->tail_done[p]) HIPCHK(c, hipEventCreateWithFlags(&c->tail_done[p], hipEventDisableTiming));
         if (!c->front_done) HIPCHK(c, hipEventCreateWithFlags(&c->front_done, hipEventDisableTiming));
         if (!c->parse_done) HIPCHK(c, hipEventCreateWithFlags(&c->parse_done, hipEventDisableTiming));
+        if (!c->pro_wait) HIPCHK(c, hipEventCreateWithFlags(&c->pro_wait, hipEventDisableTiming));
+        if (!c->pro_done) HIPCHK(c, hipEventCreateWithFlags(&c->pro_done, hipEventDisableTiming));
     }
     if (!on && c->par != 0) {   // back to set 0, keeping the last batch's facts
         HIPCHK(c, hipMemcpy(c->fb[0].bs, c->fb[c->par].bs, sizeof(BatchState), hipMemcpyDeviceToDevice));
@@ -777,7 +787,14 @@ static int run_pipelined(fsx_ctx *c, const PacketIn &in, const uint32_t *d_len, 
         if (c->sc.id_tab) HIPCHK(c, hipMemsetAsync(c->sc.id_tab, 0, c->slots * 32, c->stream));
         c->id_gen = 1;
     }
-    const PipeSplit sp = split ? PipeSplit{c->walk_stream, c->front_done, prev, pipe_on_parse, c, &c->tail_args}
+    // the early prologue on the aux stream (FSX_NO_EARLY_PROLOGUE=1: on the context stream)
+    static const bool no_early = getenv("FSX_NO_EARLY_PROLOGUE") != nullptr;
+    if (split && c->pro_fence) {   // (other work on the context stream since the last front)
+        HIPCHK(c, hipEventRecord(c->pro_wait, c->stream));
+        c->pro_fence = false;
+    }
+    const PipeSplit sp = split ? PipeSplit{c->walk_stream, c->front_done, prev, pipe_on_parse, c, &c->tail_args,
+                                           no_early ? nullptr : c->aux_stream, c->pro_wait, c->pro_done}
                                : PipeSplit{nullptr, nullptr, prev, nullptr, nullptr, nullptr};
     hipError_t e = launch_verdict_pipeline(in, d_len, d_ts, (uint32_t)n, d_verdict, c->table, c->tstate, c->bs,
                                            c->sc, c->id_gen, table_index(c), c->lim, c->rs, true, fr, c->hist,

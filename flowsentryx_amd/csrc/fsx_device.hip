@@ -2197,7 +2197,13 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
     const Marker mk{[](void *p, const char *name) { (*static_cast<decltype(mark) *>(p))(name); }, &mark};
     if (tm) tm->used = 0;
     hipError_t e;
-    if ((e = hipMemsetAsync(bs, 0, sizeof(BatchState), st)) != hipSuccess) return e;
+    // the prologue's stream: a pipelined batch resets its own scratch and picks its heavy
+    // sources on `split->pro` while the previous batch's sort runs on st (it needs only the
+    // previous batch's parse: the index); the parse waits for it below
+    const bool early = split && split->pro && split->pro_wait && split->pro_done && !tm && n > 0;
+    hipStream_t sp0 = early ? split->pro : st;
+    if (early && (e = hipStreamWaitEvent(sp0, split->pro_wait, 0)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(bs, 0, sizeof(BatchState), sp0)) != hipSuccess) return e;
     if (n == 0) return hipSuccess;
 
     const uint32_t gridStream = std::min<uint32_t>(2048, std::max<uint32_t>(1, cdiv(n, 256)));
@@ -2213,7 +2219,7 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
                   X.mir, X.mir_shift}
         : IdTable{reinterpret_cast<unsigned long long *>(sc.id_tab), sc.id_tab + 2 * (lim.table_mask + 1),
                   lim.table_mask, lim.seed, id_gen, lim.test_flags, nullptr, 0, coherent};
-    if ((e = hipMemsetAsync(sc.sort_ctl, 0, kSortCtlWords * 4, st)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(sc.sort_ctl, 0, kSortCtlWords * 4, sp0)) != hipSuccess) return e;
     mark("start");
     const uint32_t ntiles = std::max<uint32_t>(1, cdiv(n, kSortTile));
     const uint32_t tcap = (uint32_t)(sc.cap / kSortTile + 2);
@@ -2265,15 +2271,19 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
         }
     }
     if (heavy_sort) {
-        k_heavy_sample<<<64, 256, 0, st>>>(in, len, n, sc.sketch, lim.seed, lim.table_mask, lim.test_flags);
+        k_heavy_sample<<<64, 256, 0, sp0>>>(in, len, n, sc.sketch, lim.seed, lim.table_mask, lim.test_flags);
         // heavy slots resolved once (not under prefix rules; FSX_NO_HEAVY_SLOTS=1: A/B)
         static const bool no_hslots = getenv("FSX_NO_HEAVY_SLOTS") != nullptr;
         const uint32_t resolve = !no_hslots && !(do_limit && rules.slot) ? 1u : 0u;
-        k_heavy_pick<<<1, 1024, 0, st>>>(in, len, sc.sketch, sc.heavy, nheavy, 16, lim.seed,
-                                         lim.table_mask, lim.test_flags, idt, resolve, bs);
+        k_heavy_pick<<<1, 1024, 0, sp0>>>(in, len, sc.sketch, sc.heavy, nheavy, 16, lim.seed,
+                                          lim.table_mask, lim.test_flags, idt, resolve, bs);
         mark("k_heavy_pick");
     } else {
         for (int p = 0; p < 4; ++p) { dp.shift[p] = kIdShift + dbits * (uint32_t)p; dp.mask[p] = dmask; }
+    }
+    if (early) {   // the parse after the prologue
+        if ((e = hipEventRecord(split->pro_done, sp0)) != hipSuccess) return e;
+        if ((e = hipStreamWaitEvent(st, split->pro_done, 0)) != hipSuccess) return e;
     }
     {
         const uint32_t g = std::min<uint32_t>(256u * FSX_PARSE_MINB, ntiles);   // one resident block per slot
@@ -2296,6 +2306,8 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
 #undef FSX_PARSE
     }
     mark("k_parse");
+    // (the next batch's prologue may start once this parse has updated the index)
+    if (early && (e = hipEventRecord(split->pro_wait, st)) != hipSuccess) return e;
     // Heavy verdict lists: every heavy source is one run of pass 0's output (the later passes
     // write [0, n_light) only) whose segment needs no head search, so its walker and its flow
     // sums run on the third stream beside the heads, the classes and the light walkers, which

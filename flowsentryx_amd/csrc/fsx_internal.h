@@ -423,6 +423,11 @@ struct PipeSplit {
     hipError_t (*on_parse)(void *cb);
     void *cb;
     TailArgs *tail_out;        // this batch's tail is returned here, not enqueued
+    // early prologue (null: on st): this batch's scratch resets and heavy-source pick run on
+    // `pro` after `pro_wait` (the previous batch's parse), beside the previous batch's sort;
+    // st waits for `pro_done` before the parse; `pro_wait` is recorded after this parse
+    hipStream_t pro = nullptr;
+    hipEvent_t pro_wait = nullptr, pro_done = nullptr;
 };
 
 // Everything the tail of a batch needs (launch_tail): by value, so a pipelined batch's tail can
