@@ -389,8 +389,10 @@ int fsx_open(fsx_ctx **out, const fsx_config *cfg) {
     if (rc) { fsx_close(c); return rc; }
     c->slots = next_pow2(std::max<uint64_t>(1024, 2 * k.max_entries));
     auto fail = [&](int r) { fsx_close(c); return r; };
-    // stream priorities (A/B: FSX_STREAM_PRIO="own,aux,walk", lower = more urgent)
-    int prio[3] = {0, 0, 0};
+    // stream priorities (A/B: FSX_STREAM_PRIO="own,aux,walk", lower = more urgent): the
+    // context stream (parse, sort) first, so a pipelined batch's short sort scans find CU
+    // slots among the previous batch's tail (-0.6 % per step, profiles/r03/ab_prio/)
+    int prio[3] = {-1, 0, 0};
     if (const char *ps = getenv("FSX_STREAM_PRIO")) sscanf(ps, "%d,%d,%d", &prio[0], &prio[1], &prio[2]);
     if (hipStreamCreateWithPriority(&c->own_stream, hipStreamNonBlocking, prio[0]) != hipSuccess) return fail(-EIO);
     if (hipStreamCreateWithPriority(&c->aux_stream, hipStreamNonBlocking, prio[1]) != hipSuccess) return fail(-EIO);
