@@ -533,7 +533,9 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
             }
             L_ = stream_load(len + ic);
             T_ = stream_load(ts + ic);
-            P_ = ts[ic > 0 ? ic - 1 : 0];   // (used by lane 0 only: the record before the step)
+            // the record before the step, for lane 0 only (one address instead of 64: the same
+            // s_waitcnt count, a quarter of the cache-line lookups of a full ts load)
+            P_ = lane == 0 ? ts[ic > 0 ? ic - 1 : 0] : 0ull;
         } else {
             const uint4 *r = reinterpret_cast<const uint4 *>(in.rec);
             constexpr uint32_t kW = kRec / 16;   // uint4 words per record
