@@ -2308,8 +2308,9 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
 #undef FSX_PARSE
     }
     mark("k_parse");
-    // (the next batch's prologue may start once this parse has updated the index)
-    if (early && (e = hipEventRecord(split->pro_wait, st)) != hipSuccess) return e;
+    // (the next batch's prologue may start once this parse has updated the index; recorded
+    // after every split batch's parse, also one whose own prologue ran on st)
+    if (split && split->pro_wait && (e = hipEventRecord(split->pro_wait, st)) != hipSuccess) return e;
     // Heavy verdict lists: every heavy source is one run of pass 0's output (the later passes
     // write [0, n_light) only) whose segment needs no head search, so its walker and its flow
     // sums run on the third stream beside the heads, the classes and the light walkers, which
