@@ -273,9 +273,10 @@ static hipError_t flush_tail(fsx_ctx *c, hipEvent_t after) {
 }
 
 // PipeSplit::on_parse: the previous batch's tail goes in right after this batch's parse.
-static hipError_t pipe_on_parse(void *p) {
+static hipError_t pipe_on_parse(void *p, hipEvent_t recorded) {
     fsx_ctx *c = static_cast<fsx_ctx *>(p);
     if (!c->tail_pending) return hipSuccess;
+    if (recorded) return flush_tail(c, recorded);
     hipError_t e = hipEventRecord(c->parse_done, c->stream);
     return e != hipSuccess ? e : flush_tail(c, c->parse_done);
 }

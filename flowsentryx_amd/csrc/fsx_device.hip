@@ -2310,7 +2310,8 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
     mark("k_parse");
     // (the next batch's prologue may start once this parse has updated the index; recorded
     // after every split batch's parse, also one whose own prologue ran on st)
-    if (split && split->pro_wait && (e = hipEventRecord(split->pro_wait, st)) != hipSuccess) return e;
+    const bool pw = split && split->pro_wait;
+    if (pw && (e = hipEventRecord(split->pro_wait, st)) != hipSuccess) return e;
     // Heavy verdict lists: every heavy source is one run of pass 0's output (the later passes
     // write [0, n_light) only) whose segment needs no head search, so its walker and its flow
     // sums run on the third stream beside the heads, the classes and the light walkers, which
@@ -2325,7 +2326,8 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
     auto tail_hook = [&](int at) -> hipError_t {
         if (hooked || !split || !split->on_parse || (at != tail_at && at != 3)) return hipSuccess;
         hooked = true;
-        return split->on_parse(split->cb);
+        // (right after the parse the tail waits on the prologue's event: one marker, not two)
+        return split->on_parse(split->cb, at == 0 && pw ? split->pro_wait : nullptr);
     };
     if ((e = tail_hook(0)) != hipSuccess) return e;
     k_hist_prep<<<1, 256, 0, st>>>(sc.sort_ctl, sc.gbase, bs, heavy_sort ? dp.light_b : 256u);

@@ -420,7 +420,8 @@ struct PipeSplit {
     const BatchState *prev;
     // called right after this batch's parse (enqueues the previous batch's deferred tail, so
     // it overlaps this batch's sort rather than its parse)
-    hipError_t (*on_parse)(void *cb);
+    // (recorded: an event already recorded on st at this point, or null)
+    hipError_t (*on_parse)(void *cb, hipEvent_t recorded);
     void *cb;
     TailArgs *tail_out;        // this batch's tail is returned here, not enqueued
     // early prologue (null: on st): this batch's scratch resets and heavy-source pick run on
