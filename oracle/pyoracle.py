@@ -140,6 +140,10 @@ class Oracle:
         """Sources evicted before the last batch (flags=EVICT_IDLE)."""
         return int(lib().fsxo_evicted_last(self._h))
 
+    def reset(self):
+        """fsx_reset's counterpart: per-source maps and stats cleared, prefix rules kept."""
+        lib().fsxo_reset(self._h)
+
     def map_update(self, map_id: int, key: bytes, value):
         if map_id in (1, 2, 5, 6):
             v = np.array(value, dtype=np.uint64)

@@ -259,3 +259,23 @@ def test_pipelined_wide_ids(native, oracle):
     cuts = [0, 250_000, 250_001, n]
     _run(native, oracle, [(hdr[a:b], ln[a:b], ts[a:b]) for a, b in zip(cuts[:-1], cuts[1:])],
          max_entries=16 << 20)
+
+
+def test_pipelined_reset_and_import_between_batches(native, oracle):
+    """fsx_reset (a new index epoch: the IPv4 mirror is cleared) and a batched map import
+    between pipelined batches: the next batch's early prologue (heavy-source pick, which may
+    insert into the index) must run after them, not beside them."""
+    from flowsentryx_amd import lib
+    batches = _config2_batches(oracle, 1 << 19, [0, 150_000, 300_000, 420_000, 1 << 19])
+    keys = [bytes(batches[2][0][i, 26:30]) for i in range(0, 2000, 7)]   # sources of the stream
+    entries = {k: (3, 77_000, int(batches[2][2][0])) for k in keys}
+
+    def between(j, c, o):
+        if j == 0:
+            c.reset()
+            o.reset()
+        elif j == 1:
+            c.map_update_batch(lib.MAP_IPV4_STATS, entries)
+            for k, v in entries.items():
+                o.map_update(lib.MAP_IPV4_STATS, k, v)
+    _run(native, oracle, batches, between=between)
