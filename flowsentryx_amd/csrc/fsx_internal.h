@@ -248,11 +248,16 @@ __host__ __device__ inline uint64_t probe_start(uint32_t tag, const uint32_t k[4
 // a valid bit, d and the 32 - log2(slots) hash bits above the home slot. v4_hash is a
 // bijection, so an entry equal to the one computed for an address IS that address: k_parse
 // matches light sources on 2-byte entries instead of the 8-byte heads (a quarter of the
-// bytes to keep in the XCD's L2). Tables of >= 2^18 slots (<= 14 high bits); smaller ones
-// (<= 2 MiB of heads) have none.
-constexpr uint32_t kMirShift = 18;
+// bytes to keep in the XCD's L2). Tables of 2^18 .. 2^26 slots (<= 14 high bits); smaller
+// ones (<= 2 MiB of heads) have none, and neither do larger ones: beyond 128 MiB the mirror
+// no longer stays in the caches, and a flood's every insert pays one more random line
+// (config 5's 2^29 slots: 78.9 vs 76.6 ms per step with it, profiles/r03/ab_mirror/).
+#ifndef FSX_MIR_MAX_SHIFT
+#define FSX_MIR_MAX_SHIFT 26   // (A/B: scripts/build_variant.sh)
+#endif
+constexpr uint32_t kMirShift = 18, kMirMaxShift = FSX_MIR_MAX_SHIFT;
 __host__ __device__ inline size_t mir_bytes(uint32_t shift) {
-    return shift < kMirShift ? 0 : ((size_t)1 << shift) * 2;
+    return shift < kMirShift || shift > kMirMaxShift ? 0 : ((size_t)1 << shift) * 2;
 }
 __host__ __device__ inline uint32_t mir_entry(uint32_t k0, uint64_t seed, uint32_t shift, uint32_t d) {
     return 0x8000u | d << 14 | (shift >= 32 ? 0u : v4_hash(k0, seed) >> shift);
