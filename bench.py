@@ -106,6 +106,44 @@ def parse_args():
     return ap.parse_args()
 
 
+def free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def rank_launch_cmd(argv: list[str], n: int, port: int) -> list[str]:
+    """The command that runs this script as n ranks on one node (one process per GPU)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", str(Path(__file__).resolve()), *argv]
+
+
+def launch_ranks(args, argv: list[str]) -> int | None:
+    """--gpus N without a launcher: start the N rank processes as children (before this
+    process touches torch or the GPU: it never initialises a device, never re-execs) and
+    return their exit code. Under a launcher (WORLD_SIZE set): None, or 2 when --gpus
+    disagrees with the world size — a run must never time fewer ranks than it reports."""
+    world_env = os.environ.get("WORLD_SIZE")
+    if args.gpus < 1:
+        print(f"bench.py: --gpus {args.gpus}: need at least one GPU", file=sys.stderr)
+        return 2
+    if world_env is not None:
+        if int(world_env) != args.gpus:
+            print(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world_env} "
+                  "ranks", file=sys.stderr)
+            return 2
+        return None
+    if args.gpus == 1:
+        return None
+    import subprocess
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(rank_launch_cmd(argv, args.gpus, free_port()), env=env)
+
+
 def cpu_cores() -> tuple[int, dict]:
     """Threads the CPU baseline may use on this host: the affinity mask, bounded by the
     cgroup CPU quota and by OMP_NUM_THREADS (the GPU box's CPU share) when set."""
@@ -182,12 +220,16 @@ def compare_state(ctx, orc, maps) -> dict:
 
 def check_flows(d_keys, d_fam, d_feat, d_prob, m, hdr, ln, ts, model) -> dict:
     """Per-source features (bit-exact) and q8 scores of the step against the oracle."""
+    return check_flow_rows(d_keys[: m * 16].cpu().numpy().reshape(m, 16), d_fam[:m].cpu().numpy(),
+                           d_feat[: m * 8].cpu().numpy().reshape(m, 8), d_prob[:m].cpu().numpy(),
+                           hdr, ln, ts, model)
+
+
+def check_flow_rows(kg, fg, xg, pg, hdr, ln, ts, model) -> dict:
+    """Flow rows (host arrays, any row order) against the oracle's rows of (hdr, ln, ts)."""
     import numpy as np
     from oracle import pyoracle
-    kg = d_keys[: m * 16].cpu().numpy().reshape(m, 16)
-    fg = d_fam[:m].cpu().numpy()
-    xg = d_feat[: m * 8].cpu().numpy().reshape(m, 8)
-    pg = d_prob[:m].cpu().numpy()
+    m = kg.shape[0]
     ko, fo, xo = pyoracle.flow_features(hdr, ln, ts, max_sources=max(m, 1))
     if len(fo) != m:
         return {"sources_equal": False}
@@ -204,13 +246,21 @@ def check_flows(d_keys, d_fam, d_feat, d_prob, m, hdr, ln, ts, model) -> dict:
 
 def main():
     args = parse_args()
+    rc = launch_ranks(args, sys.argv[1:])
+    if rc is not None:
+        sys.exit(rc)
     import numpy as np
     import torch
 
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
+    ndev = torch.cuda.device_count()
+    if world > max(1, ndev) and args.dist_backend == "nccl":
+        print(f"bench.py: {world} ranks over RCCL need {world} GPUs, this node has {ndev} "
+              "(rehearse with --dist-backend gloo)", file=sys.stderr)
+        sys.exit(2)
     # one rank per GPU; more ranks than GPUs only in a gloo rehearsal on one device
-    local = int(os.environ.get("LOCAL_RANK", 0)) % max(1, torch.cuda.device_count())
+    local = int(os.environ.get("LOCAL_RANK", 0)) % max(1, ndev)
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
@@ -246,6 +296,84 @@ def main():
         t = torch.tensor([x], dtype=torch.int64, device="cuda" if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(t)
         return int(t.item())
+
+    # ------------------------------------------------------------------ N > 1 parity check
+    def sharded_check(ctx, plane, eng, step, v, p, zipf_s, n, bounds, chunks, max_entries, with_flows):
+        """One global batch of the stream from empty maps through the sharded plane (every
+        rank), outside the timed region: rank 0 gathers every rank's verdicts, the owners'
+        map dumps and flow rows, regenerates the global stream piece by piece (the global
+        order of a sub-batch is rank 0's piece, then rank 1's, ...: packets [0, world x n)
+        of the generator's stream) and runs the sequential oracle over it carrying its maps:
+        verdicts, stats_map, every map entry and (global batches <= 2^28 packets) the flow
+        rows, bit-exact."""
+        from flowsentryx_amd.shard import _all_gather
+        ctx.sync()
+        ctx.reset()
+        plane.reset()
+        step(0, v=v)
+        ctx.sync()
+        torch.cuda.synchronize()
+        allv = _all_gather(v[:n], world).cpu().numpy()          # rank r's slice at [r n, (r + 1) n)
+        stats = plane.stats()
+        maps = (1, 2, 3, 4)
+        mine = {m: ctx.map_arrays(m) for m in maps}
+        rows = None
+        if with_flows:
+            f, m_ = eng.flows, int(eng.flows["rows"].item())
+            rows = (f["keys"][: m_ * 16].cpu().numpy().reshape(m_, 16), f["fam"][:m_].cpu().numpy(),
+                    f["feat"][: m_ * 8].cpu().numpy().reshape(m_, 8), f["prob"][:m_].cpu().numpy())
+        got = [None] * world
+        dist.all_gather_object(got, {"maps": mine, "rows": rows})
+        res = None
+        if rank == 0:
+            from oracle import pyoracle
+            total = world * n
+            keep = with_flows and total <= (1 << 28)
+            orc = pyoracle.ShardedOracle(cores, max_entries=max_entries)
+            ok, t_orc, pieces = True, 0.0, []
+            cap = max(bounds[i + 1] - bounds[i] for i in range(chunks))
+            buf = dict(hdr=torch.empty(cap * 64, dtype=torch.uint8, device="cuda"),
+                       len=torch.empty(cap, dtype=torch.int32, device="cuda"),
+                       ts=torch.empty(cap, dtype=torch.int64, device="cuda"))
+            for i in range(chunks):
+                a, b = bounds[i], bounds[i + 1]
+                for r in range(world):
+                    g0 = world * a + r * (b - a)
+                    synth.generate_device(p, zipf_s, g0, b - a, buf["hdr"].data_ptr(), buf["len"].data_ptr(),
+                                          buf["ts"].data_ptr())
+                    torch.cuda.synchronize()
+                    hdr, ln, ts = host_inputs(buf, b - a)
+                    c0 = time.perf_counter()
+                    vo = orc.batch(hdr, ln, ts)
+                    t_orc += time.perf_counter() - c0
+                    ok = ok and bool(np.array_equal(allv[r * n + a: r * n + b], vo))
+                    if keep:
+                        pieces.append((hdr, ln, ts))
+            res = {"batches": 1, "packets": total, "ranks": world, "verdicts_equal": ok,
+                   "stats_equal": stats == orc.stats(), "oracle_seconds": round(t_orc, 3),
+                   "oracle_threads": cores}
+            same = True
+            for m in maps:
+                gk = np.concatenate([g["maps"][m][0] for g in got])
+                gv = np.concatenate([g["maps"][m][1] for g in got])
+                ro = orc.map_arrays(m)
+                res[f"map{m}_entries"] = int(gk.shape[0])
+                same = same and gk.shape[0] == ro[0].shape[0] and pyoracle.same_map((gk, gv), ro)
+            res["maps_equal"] = same
+            orc.close()
+            if keep:
+                hdr = np.concatenate([x[0] for x in pieces])
+                ln = np.concatenate([x[1] for x in pieces])
+                ts = np.concatenate([x[2] for x in pieces])
+                del pieces
+                cat = [np.concatenate([g["rows"][j] for g in got]) for j in range(4)]
+                res["flows"] = check_flow_rows(*cat, hdr, ln, ts, model_fields)
+                del hdr, ln, ts
+            elif with_flows:
+                res["flows"] = f"not checked: {total} packets in the global batch (> 2^28)"
+            del buf
+        barrier()
+        return res
 
     # ------------------------------------------------------------------ workload runner
     def run_workload(cfg_no, n, steps, warmup, with_flows, kernel_timing=False, check=False,
@@ -369,12 +497,17 @@ def main():
             # above carry no event records
             ctx.enable_timing(True)
             ctx.last_timings()
+            calls0 = eng.owner_calls if eng is not None else 0
             for k in range(warmup + steps, warmup + steps + ntime):
                 step(k)
             ctx.sync()
             torch.cuda.synchronize()
             out["timings"] = ctx.last_timings()
             ctx.enable_timing(False)
+            if eng is not None:   # per owner call -> per step (several owner calls per step)
+                per = (eng.owner_calls - calls0) / ntime
+                out["owner_calls_per_step"] = per
+                out["timings"] = [(a, b * per, c * per) for a, b, c in out["timings"]]
         if plane is not None:
             ex = plane.last_exchange or {"sent": [], "received": []}
             out["exchange"] = {"records_sent": ex["sent"], "records_received": ex["received"],
@@ -394,6 +527,24 @@ def main():
             out["info"] = info
             if with_flows:
                 out["malicious_sources"] = int(fl["dec"][:info["sources"]].sum().item())
+        if plane is not None:
+            # per GPU: its owned sources and its pipeline fraction (77 B per local packet +
+            # 64 B per owned source over the step), gathered on every rank
+            own = int(eng.flows["rows"].item()) if with_flows else None
+            per_rank = {"rank": rank, "owned_sources": own, "ms_step": out["ms_step"],
+                        "owner_calls_per_step": out.get("owner_calls_per_step"),
+                        "records_received": out["exchange"]["records_received"],
+                        "kernels": [{"name": a, "ms_per_step": round(b, 4), "launches": round(c, 2)}
+                                    for a, b, c in out.get("timings", [])]}
+            if own is not None:
+                algo = PKT_ALGO_BYTES * n + SRC_ALGO_BYTES * own
+                per_rank["pipeline_frac"] = round(algo / (out["ms_step"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+            allr = [None] * world
+            dist.all_gather_object(allr, per_rank)
+            out["per_rank"] = allr
+        if check and world > 1:
+            out["check"] = sharded_check(ctx, plane, eng, step, vb[0], p, zipf_s, n, bounds, chunks,
+                                         max_entries, with_flows)
         if (check or cpu) and world == 1:
             # from empty maps: one batch (cold) or three consecutive pipelined batches
             # (stream), the features written, then the CPU oracle on the same input bytes
@@ -438,7 +589,7 @@ def main():
     # ------------------------------------------------------------------ headline
     n_head = args.packets or int(synth.config_params(args.config)[0].n)
     head = run_workload(args.config, n_head, args.steps, args.warmup, not args.no_mlp,
-                        kernel_timing=True, check=not args.no_check and world == 1,
+                        kernel_timing=True, check=not args.no_check,
                         cpu=not args.no_cpu_baseline and world == 1, stream=not args.cold,
                         pipelined=not args.no_pipeline)
     n = head["n"]
@@ -730,10 +881,21 @@ def main():
     # launches of pure implementation traffic)
     dom = max(timings, key=lambda r: r[1] / max(r[2], 1e-9)) if timings else None
     roofline = None
-    if world > 1:   # the per-kernel split is of one owner sub-batch: the roofline is the N = 1 line's
-        roofline = {"bound": "hbm", "kernel": "k_parse", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": None, "traffic": None,
-                    "note": "N > 1: kernels run on owner sub-batches of received records; see the N = 1 line"}
+    if world > 1 and dom:
+        # the owners' k_parse reads received 16-byte records, not the 76-byte arrival records:
+        # the N > 1 roofline is that kernel's record bytes (16 B in + the 8-byte sort word out
+        # per received packet, over rank 0's launches)
+        name, ms_per_step, launches = dom
+        recv = head["exchange"]["records_received"] if head.get("exchange") else 0
+        per_launch_ms = ms_per_step / max(launches, 1e-9)
+        bpl = 16 * recv / max(launches, 1e-9)
+        achieved = bpl / (per_launch_ms * 1e-3) / 1e9 if name == "k_parse" and recv else None
+        roofline = {"bound": "hbm", "kernel": name, "achieved": round(achieved, 1) if achieved else None,
+                    "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None, "traffic": None,
+                    "bytes_per_unit": 16, "unit_of_work": "received 16-byte record",
+                    "launch_ms": round(per_launch_ms, 4), "launches_per_step": round(launches, 2),
+                    "note": "N > 1, rank 0: owner pipeline over received records (per-rank split in per_rank)"}
         dom = None
     if dom:
         name, ms_per_batch, launches = dom
@@ -761,10 +923,12 @@ def main():
         }
     pipeline = None
     if sources:
-        algo = PKT_ALGO_BYTES * n + SRC_ALGO_BYTES * sources
+        # per GPU: the whole job's algorithmic bytes / N (at N > 1 per_rank holds each rank's own)
+        algo = (PKT_ALGO_BYTES * n * world + SRC_ALGO_BYTES * sources) / world
         pipe_gbs = algo / (ms_step * 1e-3) / 1e9
         pipeline = {"bound": "hbm", "algorithmic_bytes_per_step": algo, "achieved": round(pipe_gbs, 1),
-                    "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(pipe_gbs / HBM_PEAK_GBS, 4)}
+                    "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(pipe_gbs / HBM_PEAK_GBS, 4),
+                    "per": "GPU"}
 
     cpu = None
     if "cpu" in head:
@@ -802,7 +966,7 @@ def main():
         "distinct": results.get("distinct"),
         "warm": results.get("warm"), "config3": results.get("config3"),
         "config4": results.get("config4"), "config5": results.get("config5"),
-        "exchange": head.get("exchange"),
+        "exchange": head.get("exchange"), "per_rank": head.get("per_rank"),
         "kernels": [{"name": a, "ms_per_step": round(b, 4), "launches": c} for a, b, c in timings],
         "stats": {"allowed": head["stats"][0], "dropped": head["stats"][1], "sources": sources,
                   "light_packets": info.get("light_packets"),

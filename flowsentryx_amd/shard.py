@@ -111,6 +111,7 @@ class HipShardEngine:
         self.pctx = None
         self.pctx_entries = 0
         self.pbufs, self.pcnts = {}, {}
+        self.owner_calls = 0      # batch-pipeline calls of this rank (per-kernel timings are per call)
 
     # -- streams of the pipelined plane (the CPU engine has none)
     @contextlib.contextmanager
@@ -189,6 +190,7 @@ class HipShardEngine:
         return self._ov[slot]
 
     def _run_records(self, rec, n, rb, v):
+        self.owner_calls += 1
         if self.flows is None:
             self.ctx.verdict_records_device(rec, n, rb, v)
         else:
@@ -198,6 +200,7 @@ class HipShardEngine:
                                             f["cap"])
 
     def _run(self, h, l, t, n, v):
+        self.owner_calls += 1
         if self.flows is None:
             self.ctx.verdict_batch_device(h, l, t, n, v)
         else:
