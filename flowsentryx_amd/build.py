@@ -30,7 +30,7 @@ COMMON = [
 
 LIBS = {
     "libfsx_hip.so": ["fsx_device.hip", "fsx_limiters.hip", "fsx_shard.hip", "fsx_pcap.hip",
-                      "fsx_flows.hip", "fsx_score.hip",
+                      "fsx_flows.hip", "fsx_score.hip", "fsx_heavy.hip",
                       "fsx_api.hip"],
     "libfsx_synth.so": ["fsx_synth.hip"],
 }

@@ -134,6 +134,8 @@ struct fsx_ctx {
         uint64_t *packed[2], *pay[2];
         uint32_t *hist, *sort_ctl, *gbase;
         HeavySet *heavy;
+        uint32_t *chunk_cnt;
+        void *hrec;
         BatchState *bs;
     };
     int pipe = 0;                     // fsx_set_pipeline mode (2: never split front / tail)
@@ -189,6 +191,7 @@ static void free_scratch(fsx_ctx *c) {
     hipFree(s.span_list); hipFree(s.sort_ctl); hipFree(s.gbase); hipFree(s.status);
     hipFree(s.lim_tiles); hipFree(s.sw_seg); hipFree(s.sketch); hipFree(s.heavy);
     hipFree(s.drop_list); hipFree(s.drop_cur); hipFree(s.heavy_flow);
+    hipFree(s.chunk_cnt); hipFree(s.hrec); hipFree(s.hflow);
     s = Scratch{};
 }
 
@@ -234,6 +237,9 @@ static int alloc_scratch(fsx_ctx *c, uint64_t cap) {
     HIPCHK(c, hipMalloc(&s.heavy, sizeof(HeavySet)));
     HIPCHK(c, hipMemset(s.heavy, 0, sizeof(HeavySet)));
     HIPCHK(c, hipMalloc(&s.heavy_flow, heavy_flow_bytes(cap)));
+    HIPCHK(c, hipMalloc(&s.chunk_cnt, chunk_cnt_bytes(cap)));
+    HIPCHK(c, hipMalloc(&s.hrec, heavy_rec_bytes(cap)));
+    HIPCHK(c, hipMalloc(&s.hflow, hflow_bytes(cap)));
     s.cap = cap;
     return 0;
 }
@@ -312,12 +318,15 @@ static void use_front(fsx_ctx *c, int p) {
     c->sc.sort_ctl = f.sort_ctl;
     c->sc.gbase = f.gbase;
     c->sc.heavy = f.heavy;
+    c->sc.chunk_cnt = f.chunk_cnt;
+    c->sc.hrec = f.hrec;
     c->bs = f.bs;
 }
 
 static void free_front(fsx_ctx::FrontBufs &f) {
     for (int b = 0; b < 2; ++b) { hipFree(f.packed[b]); hipFree(f.pay[b]); }
     hipFree(f.hist); hipFree(f.sort_ctl); hipFree(f.gbase); hipFree(f.heavy); hipFree(f.bs);
+    hipFree(f.chunk_cnt); hipFree(f.hrec);
     f = fsx_ctx::FrontBufs{};
 }
 
@@ -427,6 +436,7 @@ int fsx_open(fsx_ctx **out, const fsx_config *cfg) {
         fsx_ctx::FrontBufs &f = c->fb[0];
         for (int b = 0; b < 2; ++b) { f.packed[b] = c->sc.packed[b]; f.pay[b] = c->sc.pay[b]; }
         f.hist = c->sc.hist; f.sort_ctl = c->sc.sort_ctl; f.gbase = c->sc.gbase; f.heavy = c->sc.heavy;
+        f.chunk_cnt = c->sc.chunk_cnt; f.hrec = c->sc.hrec;
         f.bs = c->bs;
     }
     if (k.limiter == FSX_LIMIT_SLIDING_WINDOW) {
@@ -573,6 +583,8 @@ int fsx_set_pipeline(fsx_ctx *c, int on) {
             if ((e = hipMalloc(&f.gbase, 1024 * 4)) != hipSuccess) return e;
             if ((e = hipMalloc(&f.heavy, sizeof(HeavySet))) != hipSuccess) return e;
             if ((e = hipMemset(f.heavy, 0, sizeof(HeavySet))) != hipSuccess) return e;
+            if ((e = hipMalloc(&f.chunk_cnt, chunk_cnt_bytes(cap))) != hipSuccess) return e;
+            if ((e = hipMalloc(&f.hrec, heavy_rec_bytes(cap))) != hipSuccess) return e;
             if ((e = hipMalloc(&f.bs, sizeof(BatchState))) != hipSuccess) return e;
             return hipMemset(f.bs, 0, sizeof(BatchState));
         };
@@ -1414,11 +1426,11 @@ int fsx_last_batch_info(fsx_ctx *c, uint64_t *info, int cap) {
     HIPCHK(c, hipStreamSynchronize(c->stream));
     BatchState h;
     HIPCHK(c, hipMemcpy(&h, c->bs, sizeof(h), hipMemcpyDeviceToHost));
-    const uint64_t v[13] = {h.n_valid, h.nseg, h.n_new, h.any_v6, h.nonmono, h.max_len,
+    const uint64_t v[14] = {h.n_valid, h.nseg, h.n_new, h.any_v6, h.nonmono, h.max_len,
                             h.max_ts, h.allowed, h.dropped, h.n_rule, h.pay_ok, h.n_light,
-                            c->last_evicted};
+                            c->last_evicted, h.hfast};
     int k = 0;
-    for (; k < cap && k < 13; ++k) info[k] = v[k];
+    for (; k < cap && k < 14; ++k) info[k] = v[k];
     return k;
 }
 

@@ -462,7 +462,7 @@ __device__ __forceinline__ bool rule_drop(const RuleSet &R, uint32_t tag, const 
 // pitch: conflict-free 32-bit reads), then each lane parses its own record.
 // Record mode (kRec = 16 / 32): every lane loads its own exchange record (coalesced, no
 // LDS staging), all of them IP packets; their len / ts go out to in.rec_len / rec_ts.
-template <uint32_t kRec, bool kRules, bool kMir>
+template <uint32_t kRec, bool kRules, bool kMir, bool kHf>
 #ifndef FSX_PARSE_MINB
 #define FSX_PARSE_MINB 4   // waves/SIMD bound of k_parse (A/B: scripts/build_variant.sh)
 #endif
@@ -474,7 +474,12 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
                                                IdTable idt, uint32_t *__restrict__ ghist,
                                                uint32_t *__restrict__ thist, uint32_t tcap,
                                                DigitPlan dp, const HeavySet *__restrict__ heavy,
-                                               RuleSet rules, uint32_t tagh) {
+                                               RuleSet rules, uint32_t tagh,
+                                               uint32_t *__restrict__ chunk_cnt) {
+    // kHf (unsorted heavy sources): no timestamp loads (k_pass0h reads them),
+    // no sort word for a heavy source's packet (its verdict byte carries 0x80 | h), the light
+    // sort words compacted per 1024-packet chunk (wave) with their count in chunk_cnt
+    static_assert(!kHf || (kRec == 0 && !kRules), "unsorted heavy sources: header records, no rules");
     __shared__ uint32_t s_rec[4][64 * 17];
     __shared__ uint32_t s_red[4][3];
     __shared__ unsigned long long s_ts[4], s_its[4];
@@ -484,7 +489,7 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
     __shared__ uint32_t s_htag[kHeavyMax];
     __shared__ uint32_t s_hmap4[(1u << kHeavyMapBits) / 4];   // HeavySet::map
     __shared__ uint32_t s_hslot[kHeavyMax];
-    __shared__ uint32_t s_def[4][128 * 5];  // per wave: deferred probes {i, tag | hidx, key word 0, probe hint}
+    __shared__ uint32_t s_def[4][128 * (kHf ? 6 : 5)];  // per wave: deferred probes {i, tag | hidx, key word 0, probe hint[, light position]}
     const uint8_t *s_hmap = reinterpret_cast<const uint8_t *>(s_hmap4);
     const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
 #pragma unroll
@@ -532,10 +537,15 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
                 h[k] = stream_load16(in.hdr + (size_t)rr * 64u + c * 16u);
             }
             L_ = stream_load(len + ic);
-            T_ = stream_load(ts + ic);
-            // the record before the step, for lane 0 only (one address instead of 64: the same
-            // s_waitcnt count, a quarter of the cache-line lookups of a full ts load)
-            P_ = lane == 0 ? ts[ic > 0 ? ic - 1 : 0] : 0ull;
+            if constexpr (kHf) {
+                T_ = 0ull;
+                P_ = 0ull;
+            } else {
+                T_ = stream_load(ts + ic);
+                // the record before the step, for lane 0 only (one address instead of 64: the
+                // same s_waitcnt count, a quarter of the cache-line lookups of a full ts load)
+                P_ = lane == 0 ? ts[ic > 0 ? ic - 1 : 0] : 0ull;
+            }
         } else {
             const uint4 *r = reinterpret_cast<const uint4 *>(in.rec);
             constexpr uint32_t kW = kRec / 16;   // uint4 words per record
@@ -567,7 +577,8 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
     typedef unsigned short mir2_t __attribute__((ext_vector_type(2)));
     mir2_t c_m = {0, 0};
     constexpr uint32_t kDefCap = 128;   // deferred packets per wave (LDS)
-    constexpr uint32_t kDefW = 5;       // words per deferred packet
+    constexpr uint32_t kDefW = kHf ? 6 : 5;   // words per deferred packet
+    uint32_t crun = 0;                  // kHf: light words of the wave's current chunk so far
     uint32_t *dq = s_def[w];
     uint32_t ndef = 0;
     const uint64_t lt_mask = (1ull << lane) - 1ull;
@@ -611,7 +622,11 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
                 const uint32_t id = id_resolve<kMir>(idt, tag, k, h, hint, &fresh);
                 if (id == kNoSlot) atomicOr(&bs->err, ERR_TABLE_FULL);
                 const uint64_t out = word_of(id, tag, i, hidx);
-                packed[i] = out;
+                if constexpr (kHf) {
+                    if (hidx < 0) packed[q[5]] = out;
+                } else {
+                    packed[i] = out;
+                }
                 count_digits(out, hidx);
             }
             nfresh += (uint32_t)__popcll(__ballot(fresh));   // new sources (persistent index)
@@ -718,11 +733,13 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
             // (tagh: a heavy source's packet carries 0x80 | its index until k_verdict_apply)
             if (verdict) verdict[i] = !ip ? v : (tagh && hidx >= 0) ? (uint8_t)(0x80u | (uint32_t)hidx)
                                                                   : (uint8_t)XDP_PASS;
-            if (!ip) packed[i] = kSentinel;
-            nonmono |= T < prev ? 1u : 0u;
             maxlen = L > maxlen ? L : maxlen;
-            maxts = T > maxts ? T : maxts;
-            inv_mints = ~T > inv_mints ? ~T : inv_mints;
+            if constexpr (!kHf) {   // (kHf: k_pass0h has the clock facts)
+                if (!ip) packed[i] = kSentinel;
+                nonmono |= T < prev ? 1u : 0u;
+                maxts = T > maxts ? T : maxts;
+                inv_mints = ~T > inv_mints ? ~T : inv_mints;
+            }
         }
     };
     // resolve step t ("cur"): heavy slot from LDS, the fast-path probe match, or defer
@@ -752,6 +769,13 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
                 defer = true;
             }
         }
+        // kHf: the light packets' positions in the chunk, in arrival order (deferred or not)
+        uint32_t lpos = 0;
+        if constexpr (kHf) {
+            const uint64_t lm = __ballot(c_tag != 0 && c_hidx < 0);
+            lpos = ((t >> 4) << 10) + crun + (uint32_t)__popcll(lm & lt_mask);
+            crun += (uint32_t)__popcll(lm);
+        }
         const uint64_t dm = __ballot(defer);
         if (dm) {
             if (ndef + 64 > kDefCap) flush();
@@ -759,12 +783,17 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
                 uint32_t *q = dq + (ndef + (uint32_t)__popcll(dm & lt_mask)) * kDefW;
                 q[0] = i; q[1] = c_tag | (uint32_t)(c_hidx + 1) << 8; q[2] = c_k0;
                 q[3] = (uint32_t)c_hint0; q[4] = (uint32_t)(c_hint0 >> 32);
+                if constexpr (kHf) q[5] = lpos;
             }
             ndef += (uint32_t)__popcll(dm);
         }
         if (c_tag && !defer) {
             const uint64_t out = word_of(id, c_tag, i, c_hidx);
-            packed[i] = out;
+            if constexpr (kHf) {
+                if (c_hidx < 0) packed[lpos] = out;
+            } else {
+                packed[i] = out;
+            }
             count_digits(out, c_hidx);
         }
     };
@@ -792,6 +821,10 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
         wave_lds_order();
         if (q % kSteps == kSteps - 1) {   // sort tile done: its deferred packets, then its digit-0 counts
             flush();
+            if constexpr (kHf) {   // the wave's chunk: its light word count
+                if (lane == 0) chunk_cnt[step_at(q) >> 4] = crun;
+                crun = 0;
+            }
             if (ghist) {
                 __syncthreads();
                 const uint32_t c0 = s_t0[threadIdx.x];
@@ -1114,6 +1147,237 @@ __global__ __launch_bounds__(256, kLatePay ? FSX_SCATTER_MINB : 1) void k_tile_s
     sort_tile<kLatePay>(t, in, out, L, shift, dmask, first, bs, pin, pout, ts, len, TileOffs{offs, tcap, t});
 }
 
+// ---- pass 0 with the heavy sources outside the sort (k_parse<..., kHf>; fsx_heavy.hip).
+// One block per sort tile t, wave w = the tile's parse chunk w (1024 arrival positions):
+//   1. every packet's timestamp, length and verdict byte (coalesced): the batch's clock facts
+//      (non-decreasing?, min / max, tile span), and for every heavy source h (byte 0x80 | h)
+//      its sums over the tile (HeavyTileRec): lengths, squared lengths, first / last
+//      timestamp and the gaps between its consecutive packets — a packet's predecessor is
+//      the last lane below it with the same h (eight ballots), else the wave's last packet
+//      of h in an earlier row; the waves' chunks are joined at the tile end;
+//   2. pass 0 of the light sort words, which k_parse compacted per chunk (chunk_cnt): the
+//      stable in-tile ranking of sort_tile, payload words gathered by arrival index (their
+//      lines were just read in step 1).
+__global__ __launch_bounds__(256, FSX_SCATTER_MINB) void k_pass0h(const uint64_t *__restrict__ in,
+                                                                  uint64_t *__restrict__ out, uint32_t n,
+                                                                  uint32_t shift, uint32_t dmask,
+                                                                  const uint32_t *__restrict__ offs, uint32_t tcap,
+                                                                  BatchState *bs, uint64_t *__restrict__ pout,
+                                                                  const uint64_t *__restrict__ ts,
+                                                                  const uint32_t *__restrict__ len,
+                                                                  const uint8_t *__restrict__ tags,
+                                                                  const uint32_t *__restrict__ chunk_cnt,
+                                                                  HeavyTileRec *__restrict__ rec,
+                                                                  const HeavySet *__restrict__ hs) {
+    __shared__ unsigned long long s_el[kSortTile];
+    __shared__ uint32_t s_wc[4][256];
+    __shared__ uint32_t s_dst[256], s_tbase[256], s_tcnt[256];
+    __shared__ uint32_t s_tmp[4];
+    __shared__ unsigned long long s_red[4][3];
+    __shared__ uint32_t s_flag[4];
+    const uint32_t tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
+    const uint32_t ntiles = (n + kSortTile - 1) / kSortTile;
+    if (blockIdx.x >= ntiles) return;
+    const uint32_t t = xcd_swizzle(blockIdx.x, ntiles);
+    const uint32_t t0 = t * kSortTile;
+    const uint64_t lt_mask = (1ull << lane) - 1ull;
+    const uint32_t nh = hs->n;
+    const uint64_t tb = ts[0];
+    // ---- 1. heavy sums and clock facts (LDS: the scratch region of s_el)
+    uint32_t *h_s1 = reinterpret_cast<uint32_t *>(s_el);            // [128]
+    uint32_t *h_dmax = h_s1 + kHeavyMax;                            // [128]
+    uint32_t *h_fo = h_dmax + kHeavyMax;                            // [128]
+    unsigned long long *h_s2 = s_el + 256;                          // [128] (bytes 2048..)
+    unsigned long long *h_d2 = h_s2 + kHeavyMax;                    // [128]
+    unsigned long long *h_first = h_d2 + kHeavyMax;                 // [4][128]
+    unsigned long long *h_last = h_first + 4 * kHeavyMax;           // [4][128]
+    constexpr unsigned long long kNone = ~0ull;
+    if (tid < kHeavyMax) {
+        h_s1[tid] = 0; h_dmax[tid] = 0; h_fo[tid] = 0xFFFFFFFFu;
+        h_s2[tid] = 0; h_d2[tid] = 0;
+    }
+    for (uint32_t j = tid; j < 4 * kHeavyMax; j += 256) { h_first[j] = kNone; h_last[j] = kNone; }
+    __syncthreads();
+    const uint32_t c0 = t0 + w * 1024u;
+    uint64_t prev_t = lane == 0 && c0 > 0 && c0 < n ? ts[c0 - 1] : 0ull;   // (lane 0: before the chunk)
+    uint32_t nonmono = 0;
+    uint64_t mx = 0, imn = 0;   // max, ~min
+    for (uint32_t r = 0; r < 16; ++r) {
+        const uint32_t i = c0 + r * 64u + lane;
+        const bool live = i < n;
+        const uint64_t T = live ? ts[i] : 0ull;
+        const uint32_t L = live ? len[i] : 0u;
+        const uint32_t g = live ? tags[i] : 0u;
+        uint64_t pv = __shfl_up(T, 1);
+        if (lane == 0) pv = (c0 + r * 64u > 0) ? prev_t : T;
+        if (live) {
+            nonmono |= T < pv ? 1u : 0u;
+            mx = T > mx ? T : mx;
+            imn = ~T > imn ? ~T : imn;
+        }
+        prev_t = __shfl(T, 63);
+        const bool hv = g >= 0x80u && (g & 0x7Fu) < nh;
+        const uint64_t act = __ballot(hv);
+        if (act) {
+            const uint32_t h = g & 0x7Fu;
+            const uint64_t peers = match_digit(h, act);   // (every lane: ballots)
+            const uint64_t below = peers & lt_mask;
+            const uint32_t pl = below ? 63u - (uint32_t)__clzll((long long)below) : lane;
+            const uint64_t tpl = __shfl(T, (int)pl);
+            if (hv) {
+                uint64_t tp = tpl;
+                bool gap = below != 0;
+                if (!gap) {   // first of h in this row: the wave's last packet of h so far
+                    tp = h_last[w * kHeavyMax + h];
+                    gap = tp != kNone;
+                    if (!gap) {
+                        h_first[w * kHeavyMax + h] = T;
+                        atomicMin(&h_fo[h], i - t0);
+                    }
+                }
+                atomicAdd(&h_s1[h], L);
+                atomicAdd(&h_s2[h], (unsigned long long)L * L);
+                if (gap) {
+                    const uint64_t d = T - tp;
+                    atomicAdd(&h_d2[h], (unsigned long long)(d * d));
+                    atomicMax(&h_dmax[h], d > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)d);
+                }
+                if ((peers >> lane) == 1ull) h_last[w * kHeavyMax + h] = T;   // the row's last of h
+            }
+            wave_lds_order();
+        }
+    }
+    nonmono = __ballot(nonmono != 0) ? 1u : 0u;
+    mx = wave_max(mx);
+    imn = wave_max(imn);
+    if (lane == 0) { s_red[w][0] = mx; s_red[w][1] = imn; s_flag[w] = nonmono; }
+    __syncthreads();
+    if (tid < kHeavyMax) {   // join the waves' chunks: the gaps across chunk boundaries
+        const uint32_t h = tid;
+        uint64_t d2 = h_d2[h], first = kNone, last = kNone;
+        uint32_t dm = h_dmax[h];
+        for (uint32_t ww = 0; ww < 4; ++ww) {
+            const uint64_t f = h_first[ww * kHeavyMax + h];
+            if (f == kNone) continue;
+            if (last != kNone) {
+                const uint64_t d = f - last;
+                d2 += d * d;
+                const uint32_t d32 = d > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)d;
+                dm = d32 > dm ? d32 : dm;
+            } else {
+                first = f;
+            }
+            last = h_last[ww * kHeavyMax + h];
+        }
+        HeavyTileRec &R = rec[t];
+        R.s1[h] = h_s1[h]; R.dmax[h] = dm; R.fo[h] = h_fo[h];
+        R.s2[h] = h_s2[h]; R.t0[h] = first; R.t1[h] = last; R.d2[h] = d2;
+    }
+    if (tid == 0) {
+        uint64_t m = 0, im = 0;
+        uint32_t nm = 0;
+        for (int k = 0; k < 4; ++k) {
+            m = s_red[k][0] > m ? s_red[k][0] : m;
+            im = s_red[k][1] > im ? s_red[k][1] : im;
+            nm |= s_flag[k];
+        }
+        if (nm) atomicOr(&bs->nonmono, 1u);
+        if (m - ~im >= (1ull << 32) && m >= ~im) atomicOr(&bs->span_big, 1u);
+        atomicMax(reinterpret_cast<unsigned long long *>(&bs->max_ts), (unsigned long long)m);
+        atomicMax(reinterpret_cast<unsigned long long *>(&bs->inv_min_ts), (unsigned long long)im);
+    }
+    __syncthreads();
+    // ---- 2. pass 0 of the tile's light words (sort_tile, keys from the chunk runs)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) s_wc[w][lane * 4 + k] = 0;
+    __syncthreads();
+    const uint32_t ccnt = chunk_cnt[t * 4u + w];
+    uint64_t v[kSortItems];
+    uint32_t lr[kSortItems];
+#pragma unroll
+    for (int r = 0; r < kSortItems; ++r) {
+        const uint32_t j = (uint32_t)r * 64u + lane;
+        v[r] = j < ccnt ? in[c0 + j] : kSentinel;
+    }
+#pragma unroll
+    for (int r = 0; r < kSortItems; ++r) {
+        const bool valid = v[r] != kSentinel;
+        const uint64_t act = __ballot(valid);
+        const uint32_t d = (uint32_t)(v[r] >> shift) & dmask;
+        const int lead0 = act ? __ffsll((unsigned long long)act) - 1 : 0;
+        const uint32_t dl = __shfl(d, lead0);
+        const uint64_t peers = __ballot(valid && d == dl) == act ? act : match_digit(d, act);
+        const uint32_t below = (uint32_t)__popcll(peers & lt_mask);
+        uint32_t base = 0;
+        if (valid && below == 0) base = atomicAdd(&s_wc[w][d], (uint32_t)__popcll(peers));
+        base = __shfl(base, __ffsll((unsigned long long)peers) - 1);
+        lr[r] = valid ? base + below : 0xFFFFFFFFu;
+    }
+    __syncthreads();
+    const uint32_t d = tid;
+    const uint32_t q0 = s_wc[0][d], q1 = s_wc[1][d], q2 = s_wc[2][d], q3 = s_wc[3][d];
+    const uint32_t tc = q0 + q1 + q2 + q3;
+    s_dst[d] = d <= dmask && tc ? offs[(size_t)d * tcap + t] : 0u;
+    __syncthreads();
+    s_wc[0][d] = 0; s_wc[1][d] = q0; s_wc[2][d] = q0 + q1; s_wc[3][d] = q0 + q1 + q2;
+    s_tcnt[d] = tc;
+    s_tbase[d] = block256_excl(tc, s_tmp, nullptr);
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < kSortItems; ++r) {
+        if (lr[r] != 0xFFFFFFFFu) {
+            const uint32_t dd = (uint32_t)(v[r] >> shift) & dmask;
+            lr[r] += s_tbase[dd] + s_wc[w][dd];
+            s_el[lr[r]] = v[r];
+        }
+    }
+    __syncthreads();
+    const uint32_t T = s_tbase[255] + s_tcnt[255];
+    uint32_t dst[kSortItems];
+#pragma unroll
+    for (int m = 0; m < kSortItems; ++m) {
+        const uint32_t j = tid + 256u * (uint32_t)m;
+        if (j < T) {
+            const uint64_t x = s_el[j];
+            const uint32_t dd = (uint32_t)(x >> shift) & dmask;
+            dst[m] = s_dst[dd] + (j - s_tbase[dd]);
+            out[dst[m]] = x;
+        }
+    }
+    // payload words (ts - ts[0]) << kPayLenBits | len, gathered by arrival index (k_hmode
+    // decides whether they are exact: pay_ok)
+    uint64_t pv[kSortItems];
+#pragma unroll
+    for (int r = 0; r < kSortItems; ++r) {
+        if (lr[r] != 0xFFFFFFFFu) {
+            const uint32_t i = pk_idx(v[r]);
+            pv[r] = ((ts[i] - tb) << kPayLenBits) | len[i];
+        } else {
+            pv[r] = 0;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < kSortItems; ++r)
+        if (lr[r] != 0xFFFFFFFFu) s_el[lr[r]] = pv[r];
+    __syncthreads();
+#pragma unroll
+    for (int m = 0; m < kSortItems; ++m) {
+        const uint32_t j = tid + 256u * (uint32_t)m;
+        if (j < T) pout[dst[m]] = s_el[j];
+    }
+}
+
+hipError_t launch_pass0h(const uint64_t *in, uint64_t *out, uint32_t n, uint32_t shift, uint32_t dmask,
+                         const uint32_t *offs, uint32_t tcap, BatchState *bs, uint64_t *pout, const uint64_t *ts,
+                         const uint32_t *len, const uint8_t *tags, const uint32_t *chunk_cnt, void *rec,
+                         const HeavySet *hs, hipStream_t st) {
+    const uint32_t ntiles = std::max<uint32_t>(1, (n + kSortTile - 1) / kSortTile);
+    k_pass0h<<<ntiles, 256, 0, st>>>(in, out, n, shift, dmask, offs, tcap, bs, pout, ts, len, tags, chunk_cnt,
+                                     static_cast<HeavyTileRec *>(rec), hs);
+    return hipGetLastError();
+}
+
 // ---- onesweep variant (FSX_FLAG_ONESWEEP_SORT): per-digit decoupled look-back.
 // Status words are 8-byte {generation, inclusive?, count} granules written with one
 // agent-scope store and polled with agent-scope loads; tiles take ids from an atomic
@@ -1321,7 +1585,7 @@ __global__ __launch_bounds__(256) void k_heads_heavy(BatchState *bs, const uint3
                                                      uint32_t *__restrict__ seg_start,
                                                      uint32_t *__restrict__ seg_slot,
                                                      const uint64_t *__restrict__ S, uint64_t id_mask,
-                                                     uint32_t *__restrict__ seg_lo) {
+                                                     uint32_t *__restrict__ seg_lo, const HeavySet *hs) {
     __shared__ uint32_t s_tmp[4];
     const uint32_t h = threadIdx.x;
     const uint32_t L = bs->nseg;   // light segments (k_scan_tiles_u32); read before the barrier
@@ -1332,8 +1596,10 @@ __global__ __launch_bounds__(256) void k_heads_heavy(BatchState *bs, const uint3
     if (live) {
         const uint32_t a = base0[lb + h];
         seg_start[L + r] = a;
-        if (seg_slot) seg_slot[L + r] = pk_id(S[a], id_mask);
-        if (seg_lo) seg_lo[L + r] = (uint32_t)S[a];
+        // (hfast: no runs in S; the heavy sources' slots are resolved in k_heavy_pick)
+        const bool runs = !bs->hfast;
+        if (seg_slot) seg_slot[L + r] = runs ? pk_id(S[a], id_mask) : hs->slot[h];
+        if (seg_lo) seg_lo[L + r] = runs ? (uint32_t)S[a] : 0u;
     }
     if (h == 0) {
         bs->nseg_light = L;
@@ -1683,7 +1949,7 @@ __global__ __launch_bounds__(256) void k_walk_heavy(const uint64_t *__restrict__
                                                     const uint32_t *__restrict__ len,
                                                     const uint64_t *__restrict__ pay, Slot *table,
                                                     Limits lim, HeavyLists H) {
-    if (bs->err) return;
+    if (bs->err || bs->hfast) return;   // (hfast: k_walk_heavy_sel)
     if (bs->pay_ok) {
         const SegView<true> sv{S, ts, len, pay, ~bs->inv_min_ts};
         walk_heavy(sv, bs, cnt0, base0, table, lim, H);
@@ -2017,6 +2283,7 @@ hipError_t launch_tail(const TailArgs &a) {
     PipeTiming *tm = a.tm;
     const PipeSplit *split = a.split ? &a.sp : nullptr;
     const int npass = a.npass;
+    const uint32_t tcap = (uint32_t)(a.sc.cap / kSortTile + 2);
     const bool tagh = a.tagh;
     const uint32_t gridTiles = a.gridTiles;
     int last[3] = {a.last[0], a.last[1], a.last[2]};
@@ -2062,9 +2329,18 @@ hipError_t launch_tail(const TailArgs &a) {
         k_walk_heavy<<<kHeavyMax / 4, 256, 0, hs>>>(S_fin, bs, sc.sort_ctl, sc.gbase, ts, len, pay_fin,
                                                       table, lim, hlists);
         mark_on("k_walk_heavy", hs_id);
+        if (a.hfm) {   // (the path k_hmode picked runs; the other kernel returns at once)
+            if ((e = launch_walk_heavy_sel(bs, sc.sort_ctl, sc.gbase, sc.hist, tcap, verdict, ts, len, n, sc.hrec,
+                                           table, lim, sc.heavy, hlists.list, tstate, hs)) != hipSuccess)
+                return e;
+            mark_on("k_walk_heavy_sel", hs_id);
+        }
         if (flows) {
             if ((e = launch_flows_heavy(S_fin, pay_fin, ts, len, bs, sc.sort_ctl, sc.gbase, sc.heavy_flow,
                                         sc.cap, hf)) != hipSuccess)
+                return e;
+            if (a.hfm && (e = launch_hflow_combine(bs, sc.sort_ctl, sc.gbase, sc.hist, tcap, n, sc.hrec, sc.hflow,
+                                                   hf)) != hipSuccess)
                 return e;
             mark_on("k_flow_heavy", hf_id);
             if (hf != st && (e = hipEventRecord(heavy_flow_ev, hf)) != hipSuccess) return e;
@@ -2082,6 +2358,11 @@ hipError_t launch_tail(const TailArgs &a) {
         hf = fork ? st2 : st;
         hf_id = fork ? 1 : 0;
     }
+    // unsorted heavy sources that k_hmode sent back to the run path: their runs first
+    if (a.hfm && (e = launch_heavy_gather(bs, verdict, ts, len, n, sc.hist, tcap, sc.heavy, a.shift0, lim.table_mask,
+                                          S_fin, pay_fin, st)) != hipSuccess)
+        return e;
+    if (a.hfm) mark("k_heavy_gather");
     if (tagh && (e = launch_heavy()) != hipSuccess) return e;
     if (npass & 1) {
         std::swap(sc.packed[0], sc.packed[1]);
@@ -2098,7 +2379,7 @@ hipError_t launch_tail(const TailArgs &a) {
                                              do_limit ? sc.seg_slot : nullptr, lim.table_mask, lo, seg_lo);
     if (tagh)
         k_heads_heavy<<<1, 256, 0, st>>>(bs, sc.sort_ctl, sc.gbase, sc.seg_start, do_limit ? sc.seg_slot : nullptr,
-                                         S_fin, lim.table_mask, seg_lo);
+                                         S_fin, lim.table_mask, seg_lo, sc.heavy);
     mark("k_heads_write");
     if (flows) {
         hipStream_t fs = st;
@@ -2121,6 +2402,11 @@ hipError_t launch_tail(const TailArgs &a) {
                                                flows->cap, flows->score, lim.salt32,
                                                do_limit ? flows->sacc : nullptr, flows->epoch, sc.seg_slot, fs)) !=
                 hipSuccess)
+                return e;
+            if (a.hfm && (e = launch_hflow_finish(bs, sc.sort_ctl, sc.heavy, sc.hflow, n, in, len, ts, flows->keys16,
+                                                  flows->fam, flows->feat, flows->prob, flows->dec, flows->cap,
+                                                  flows->score, do_limit ? flows->sacc : nullptr, flows->epoch,
+                                                  PartialOut{}, fs)) != hipSuccess)
                 return e;
         }
         mark_on("k_flow_features", fork ? 1 : 0);
@@ -2255,6 +2541,13 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
     if (heavy_sort) npass = hpass;   // (24-bit ids: 4 passes instead of 3, 3 of them over the light entries)
     // heavy verdict lists (fixed window with the heavy-source sort; FSX_NO_HEAVY_LISTS=1: A/B)
     const bool tagh = heavy_sort && lists_ok;
+    // heavy slots resolved once in k_heavy_pick (not under prefix rules; FSX_NO_HEAVY_SLOTS=1: A/B)
+    static const bool no_hslots = getenv("FSX_NO_HEAVY_SLOTS") != nullptr;
+    const uint32_t resolve = !no_hslots && !(do_limit && rules.slot) ? 1u : 0u;
+    // heavy sources outside the sort (fsx_heavy.hip): header records with resolved heavy
+    // slots; k_hmode picks the batch's path on the device (FSX_NO_HFAST=1: the runs, A/B)
+    static const bool no_hfast = getenv("FSX_NO_HFAST") != nullptr;
+    const bool hfm = tagh && resolve && !in.rec && !no_hfast;
     if (!(split && split->tail) && (e = hipMemsetAsync(sc.marks, 0, n, st)) != hipSuccess) return e;
     DigitPlan dp{};
     dp.npass = (uint32_t)npass;
@@ -2274,9 +2567,6 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
     }
     if (heavy_sort) {
         k_heavy_sample<<<64, 256, 0, sp0>>>(in, len, n, sc.sketch, lim.seed, lim.table_mask, lim.test_flags);
-        // heavy slots resolved once (not under prefix rules; FSX_NO_HEAVY_SLOTS=1: A/B)
-        static const bool no_hslots = getenv("FSX_NO_HEAVY_SLOTS") != nullptr;
-        const uint32_t resolve = !no_hslots && !(do_limit && rules.slot) ? 1u : 0u;
         k_heavy_pick<<<1, 1024, 0, sp0>>>(in, len, sc.sketch, sc.heavy, nheavy, 16, lim.seed,
                                           lim.table_mask, lim.test_flags, idt, resolve, bs);
         mark("k_heavy_pick");
@@ -2295,16 +2585,18 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
         // rule-free parse keeps its registers)
         const bool rl = do_limit && rules.slot;
         // (kMir: light IPv4 sources probe the persistent index's mirror, not its heads)
-#define FSX_PARSE(R, Q) (idt.mir ? k_parse<R, Q, true><<<g, 256, 0, st>>>(in, len, ts, n, sc.packed[0], verdict, bs, idt, \
-                                                        sc.sort_ctl, th, tcap, dp, hs, rules, tagh ? 1u : 0u) \
-                                 : k_parse<R, Q, false><<<g, 256, 0, st>>>(in, len, ts, n, sc.packed[0], verdict, bs, idt, \
-                                                        sc.sort_ctl, th, tcap, dp, hs, rules, tagh ? 1u : 0u))
-        if (!in.rec)
-            rl ? FSX_PARSE(0, true) : FSX_PARSE(0, false);
+#define FSX_PARSE(R, Q, H) (idt.mir ? k_parse<R, Q, true, H><<<g, 256, 0, st>>>(in, len, ts, n, sc.packed[0], verdict, bs, idt, \
+                                                        sc.sort_ctl, th, tcap, dp, hs, rules, tagh ? 1u : 0u, sc.chunk_cnt) \
+                                 : k_parse<R, Q, false, H><<<g, 256, 0, st>>>(in, len, ts, n, sc.packed[0], verdict, bs, idt, \
+                                                        sc.sort_ctl, th, tcap, dp, hs, rules, tagh ? 1u : 0u, sc.chunk_cnt))
+        if (hfm)
+            FSX_PARSE(0, false, true);
+        else if (!in.rec)
+            rl ? FSX_PARSE(0, true, false) : FSX_PARSE(0, false, false);
         else if (in.rec_bytes == 16)
-            rl ? FSX_PARSE(16, true) : FSX_PARSE(16, false);
+            rl ? FSX_PARSE(16, true, false) : FSX_PARSE(16, false, false);
         else
-            rl ? FSX_PARSE(32, true) : FSX_PARSE(32, false);
+            rl ? FSX_PARSE(32, true, false) : FSX_PARSE(32, false, false);
 #undef FSX_PARSE
     }
     mark("k_parse");
@@ -2358,9 +2650,18 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
             k_tile_scan<<<pmask + 1, 256, 0, st>>>(sc.hist, tcap, n, Ld, sc.gbase + 256 * pass);
             mark("k_tile_scan");
             if (pass == 0 && (e = tail_hook(1)) != hipSuccess) return e;
-            k_tile_scatter<kLatePayDefault><<<ntiles, 256, 0, st>>>(in, out, n, Ld, shift, pmask, pass == 0, sc.hist, tcap, bs,
-                                                   pin, pout, ts, len);
-            mark("k_tile_scatter");
+            if (pass == 0 && hfm) {   // light words from the parse chunks; heavy tile sums; the path
+                if ((e = launch_pass0h(in, out, n, shift, pmask, sc.hist, tcap, bs, pout, ts, len, verdict,
+                                       sc.chunk_cnt, sc.hrec, sc.heavy, st)) != hipSuccess)
+                    return e;
+                mark("k_pass0h");
+                if ((e = launch_hmode(bs, ts, n, sc.heavy, table, lim, st)) != hipSuccess) return e;
+                mark("k_hmode");
+            } else {
+                k_tile_scatter<kLatePayDefault><<<ntiles, 256, 0, st>>>(in, out, n, Ld, shift, pmask, pass == 0, sc.hist, tcap, bs,
+                                                       pin, pout, ts, len);
+                mark("k_tile_scatter");
+            }
             if (pass == 0 && (e = tail_hook(2)) != hipSuccess) return e;
         }
     }
@@ -2378,6 +2679,7 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
     ta.heavy_flow_ev = heavy_flow_ev; ta.tm = tm; ta.split = split != nullptr;
     if (split) ta.sp = *split;
     ta.npass = npass; ta.tagh = tagh; ta.gridTiles = gridTiles;
+    ta.hfm = hfm; ta.shift0 = dp.shift[0];
     ta.fork = flows && do_limit && st2 && fork_ev && join_ev && !no_fork;
     for (int k = 0; k < 3; ++k) ta.last[k] = last[k];
     if (split && split->tail_out) {

@@ -177,6 +177,9 @@ __device__ __forceinline__ void acc_store(const FlowOut &out, uint32_t g, const 
 
 __device__ __forceinline__ void write_row(uint32_t g, const FlowAcc &a, uint32_t tag, const uint32_t k[4],
                                  uint32_t dport, const FlowOut &out, const ScoreParams &P);
+__device__ __forceinline__ void flow_emit(uint32_t g, const FlowAcc &a, uint32_t tag, const uint32_t k[4],
+                                          uint32_t dport, uint64_t t0, uint64_t t1, uint32_t slot,
+                                          const FlowOut &out, const ScoreParams &P);
 
 // Features of source g from its exact sums, then the q8 score (accumulate mode: the sums
 // merge into the source's SlotAcc instead).
@@ -197,13 +200,23 @@ __device__ __forceinline__ void flow_finish(uint32_t g, const FlowAcc &a, const 
         tag = key_of(v, in.hdr, salt, k);
         dport = dst_port(in.hdr + (size_t)idx * 64, out.seg_len ? out.seg_len[g] : len[idx]);
     }
+    const bool need_t = out.part.buf || out.sacc;
+    flow_emit(g, a, tag, k, dport, need_t ? out.ts[idx] : 0ull,
+              need_t ? out.ts[pk_idx(S[seg_start[g + 1] - 1])] : 0ull, out.sacc ? out.seg_slot[g] : 0u, out, P);
+}
+
+// Source g's finished sums (first / last timestamp t0 / t1, table slot for the accumulate
+// mode): its flow partial, its merge into the carried per-slot sums, or its output row.
+__device__ __forceinline__ void flow_emit(uint32_t g, const FlowAcc &a, uint32_t tag, const uint32_t k[4],
+                                          uint32_t dport, uint64_t t0, uint64_t t1, uint32_t slot,
+                                          const FlowOut &out, const ScoreParams &P) {
+    if (g >= out.cap) return;
     if (out.part.buf) {   // partials mode: the raw sums with the run's first / last timestamp
-        write_partial(out.part, tag, k, dport, a, out.ts[idx], out.ts[pk_idx(S[seg_start[g + 1] - 1])]);
+        write_partial(out.part, tag, k, dport, a, t0, t1);
         return;
     }
     if (out.sacc) {
-        SlotAcc &m = out.sacc[out.seg_slot[g]];
-        const uint64_t t0 = out.ts[idx], t1 = out.ts[pk_idx(S[seg_start[g + 1] - 1])];
+        SlotAcc &m = out.sacc[slot];
         if (m.epoch != out.epoch) {   // the source's first call of this epoch
             m.n = a.n; m.s1 = a.s1; m.s2 = a.s2; m.d1 = a.d1; m.d2 = a.d2; m.dmax = a.dmax;
             m.dport = dport;

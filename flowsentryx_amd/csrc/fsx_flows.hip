@@ -324,7 +324,7 @@ __global__ __launch_bounds__(256) void k_flow_heavy(const uint64_t *__restrict__
                                                     FlowAcc *__restrict__ part) {
     __shared__ uint32_t s_pre[kHeavyMax + 1];
     __shared__ uint32_t s_tmp[4];
-    if (bs->err) return;
+    if (bs->err || bs->hfast) return;   // (hfast: k_hflow_combine)
     heavy_chunk_prefix(cnt0, bs->light_b, s_pre, s_tmp);
     if (blockIdx.x == 0 && threadIdx.x <= kHeavyMax) pre[threadIdx.x] = s_pre[threadIdx.x];
     if (bs->pay_ok) {
@@ -339,7 +339,7 @@ __global__ __launch_bounds__(256) void k_flow_heavy(const uint64_t *__restrict__
 // One wave per heavy bucket: the sum of its chunks.
 __global__ __launch_bounds__(256) void k_flow_heavy_sum(const BatchState *bs, const uint32_t *__restrict__ pre,
                                                         const FlowAcc *__restrict__ part, FlowAcc *__restrict__ hacc) {
-    if (bs->err) return;
+    if (bs->err || bs->hfast) return;
     const uint32_t h = blockIdx.x * 4u + (threadIdx.x >> 6), lane = lane_id();
     if (h >= kHeavyMax) return;
     FlowAcc A = acc_zero();
@@ -357,7 +357,7 @@ __global__ __launch_bounds__(256) void k_flow_heavy_finish(const uint64_t *__res
                                                            const uint32_t *__restrict__ len, FlowOut out,
                                                            ScoreParams P, uint32_t salt) {
     __shared__ uint32_t s_tmp[4];
-    if (bs->err) return;
+    if (bs->err || bs->hfast) return;   // (hfast: k_hflow_finish)
     const uint32_t h = threadIdx.x;
     const bool live = h < kHeavyMax && cnt0[bs->light_b + h] > 0;
     const uint32_t r = block256_excl(live ? 1u : 0u, s_tmp, nullptr);

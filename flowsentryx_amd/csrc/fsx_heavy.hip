@@ -1,0 +1,501 @@
+// fsx_heavy.hip — heavy sources outside the sort (fixed window with heavy verdict lists,
+// DESIGN.md §3 "Heavy sources outside the sort").
+//
+// A Zipf flood puts half of a batch's packets in its 128 heaviest sources. k_parse tags
+// their verdict bytes 0x80 | h and counts them per sort tile (pass 0's digit counts, whose
+// scan gives "h's packets before tile t"); it writes no sort word for them, and k_pass0h
+// reduces each tile's packets of every heavy source to a HeavyTileRec (flow sums). The
+// heavy source's packets are then addressed by rank in arrival order:
+//   select(h, r)  the arrival index of h's r-th packet: a 64-wide search of the tile
+//                 prefix row, then a scan of that tile's 4096 verdict bytes;
+//   rank(h, i)    h's packets before arrival index i: prefix row + one tile scan;
+// and, with the batch clock non-decreasing, "h's first packet later than X" is rank(h, the
+// first arrival index later than X) — one search over the timestamps. The epoch-jump
+// walker of src/fsx_kern.c:150-346 (fsx_walk.h walk_fixed_fast) runs unchanged on that view.
+//
+// k_hmode decides per batch (on the device) whether this holds: clock non-decreasing,
+// payloads exact, frames < 2^16 B, tiles < 2^32 ns, every heavy source's carried state on
+// the epoch-jump path. Otherwise k_heavy_gather builds the runs pass 0 used to build and
+// the run-based kernels (k_walk_heavy, k_flow_heavy) take over; every kernel of the other
+// path returns at once.
+#include <hip/hip_runtime.h>
+
+#include "fsx_dev_common.h"
+#include "fsx_flow_common.h"
+#include "fsx_internal.h"
+#include "fsx_seg.h"
+#include "fsx_walk.h"
+
+namespace fsx {
+
+// The 0x80-byte of every byte of x that equals b (exact: no borrow across bytes).
+__device__ __forceinline__ uint32_t byte_eq_mask(uint32_t x, uint32_t pat) {
+    const uint32_t y = x ^ pat;
+    return ~(((y & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | y | 0x7F7F7F7Fu);
+}
+
+// Heavy source h's packets by rank (fsx_walk.h SegView interface; wave-cooperative: every
+// lane calls with the same arguments).
+struct HeavyView {
+    const uint8_t *tags;          // verdict bytes: 0x80 | h for h's packets
+    const uint64_t *ts;
+    const uint32_t *len;
+    const uint32_t *row;          // pass-0 tile offsets of bucket light_b + h (incl. base)
+    const HeavyTileRec *rec;
+    uint32_t base, cnt, ntiles, n, h;
+    uint32_t pat;                 // (0x80 | h) in every byte
+
+    __device__ __forceinline__ uint32_t pre(uint32_t t) const { return row[t] - base; }
+
+    // lane's 64 verdict bytes of tile t as 16 words (0 beyond n)
+    __device__ __forceinline__ void tile_words(uint32_t t, uint32_t (&w)[16]) const {
+        const uint32_t lane = lane_id();
+        const uint32_t p0 = t * (uint32_t)kSortTile + lane * 64u;
+        if (p0 + 64u <= n) {
+            const uint4 *q = reinterpret_cast<const uint4 *>(tags + p0);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint4 v = q[k];
+                w[4 * k] = v.x; w[4 * k + 1] = v.y; w[4 * k + 2] = v.z; w[4 * k + 3] = v.w;
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                uint32_t x = 0;
+                for (uint32_t b = 0; b < 4; ++b) {
+                    const uint32_t p = p0 + (uint32_t)k * 4u + b;
+                    if (p < n) x |= (uint32_t)tags[p] << (8 * b);
+                }
+                w[k] = x;
+            }
+        }
+    }
+
+    // arrival index of h's r-th packet (r < cnt)
+    __device__ __forceinline__ uint32_t select(uint32_t r) const {
+        const uint32_t lane = lane_id();
+        uint32_t lo = 0, hi = ntiles;   // the largest tile t with pre(t) <= r lies in [lo, hi)
+        while (hi - lo > 1) {
+            const uint32_t step = (hi - lo + 63u) / 64u;
+            const uint32_t q = lo + lane * step;
+            const uint64_t m = __ballot(q < hi && pre(q) <= r);   // lane 0 (q = lo) always
+            const uint32_t f = 63u - (uint32_t)__clzll((long long)m);
+            lo = lo + f * step;
+            hi = min(hi, lo + step);
+        }
+        const uint32_t t = lo;
+        uint32_t k = r - pre(t);
+        uint32_t w[16];
+        tile_words(t, w);
+        uint32_t c = 0;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) c += (uint32_t)__popc(byte_eq_mask(w[j], pat));
+        const uint32_t incl = wave_incl_sum(c);
+        const uint32_t excl = incl - c;
+        const bool mine = excl <= k && k < incl;
+        uint32_t idx = 0;
+        if (mine) {
+            uint32_t kk = k - excl;
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                uint32_t m = byte_eq_mask(w[j], pat);
+                const uint32_t pc = (uint32_t)__popc(m);
+                if (kk < pc && idx == 0) {
+                    for (uint32_t s = 0; s < kk; ++s) m &= m - 1u;
+                    idx = 1u + t * (uint32_t)kSortTile + lane * 64u + (uint32_t)j * 4u +
+                          (uint32_t)(__ffs((int)m) - 1) / 8u;
+                }
+                kk = kk >= pc ? kk - pc : 0xFFFFFFFFu;
+            }
+        }
+        const uint64_t bm = __ballot(mine);
+        return __shfl(idx, __ffsll((unsigned long long)bm) - 1) - 1u;
+    }
+
+    // h's packets at arrival indices < i (i <= n)
+    __device__ __forceinline__ uint32_t rank(uint32_t i) const {
+        if (i >= n) return cnt;
+        const uint32_t lane = lane_id();
+        const uint32_t t = i / (uint32_t)kSortTile;
+        uint32_t w[16];
+        tile_words(t, w);
+        const uint32_t p0 = t * (uint32_t)kSortTile + lane * 64u;
+        uint32_t c = 0;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            uint32_t m = byte_eq_mask(w[j], pat);
+            const uint32_t pj = p0 + (uint32_t)j * 4u;   // byte b of word j: position pj + b
+            if (pj + 4u <= i) c += (uint32_t)__popc(m);
+            else if (pj < i) c += (uint32_t)__popc(m & ((1u << (8u * (i - pj))) - 1u));
+        }
+        return pre(t) + wave_sum(c);
+    }
+
+    // first arrival index with ts > X (the batch clock non-decreasing), n if none
+    __device__ __forceinline__ uint32_t first_after(uint64_t X) const {
+        const uint32_t lane = lane_id();
+        uint32_t lo = 0, hi = n;   // ts <= X before lo, ts > X from hi on
+        while (hi - lo > 64u) {
+            const uint32_t step = (hi - lo + 63u) / 64u;
+            const uint32_t q = lo + lane * step;
+            const bool valid = q < hi;
+            const uint64_t m = __ballot(valid && ts[q] > X);
+            if (m) {
+                const uint32_t f = (uint32_t)__ffsll((unsigned long long)m) - 1u;
+                hi = lo + f * step;
+                if (f) lo = lo + (f - 1u) * step + 1u;
+            } else {
+                const uint64_t vm = __ballot(valid);
+                lo = lo + (63u - (uint32_t)__clzll((long long)vm)) * step + 1u;
+            }
+        }
+        const uint32_t q = lo + lane;
+        const uint64_t m = __ballot(q < hi && ts[q] > X);
+        return m ? lo + (uint32_t)__ffsll((unsigned long long)m) - 1u : hi;
+    }
+
+    __device__ __forceinline__ uint64_t t(uint32_t r) const { return ts[select(r)]; }
+    __device__ __forceinline__ uint32_t l(uint32_t r) const { return len[select(r)]; }
+
+    // sum of h's frame lengths at arrival positions [a, b] of tile t
+    __device__ __forceinline__ uint64_t tile_len_sum(uint32_t t, uint32_t a, uint32_t b) const {
+        const uint32_t lane = lane_id();
+        uint64_t s = 0;
+        const uint32_t p0 = t * (uint32_t)kSortTile;
+#pragma unroll 4
+        for (uint32_t j = 0; j < (uint32_t)kSortTile; j += 64u) {
+            const uint32_t p = p0 + j + lane;
+            if (p >= a && p <= b && p < n && tags[p] == (pat & 0xFFu)) s += len[p];
+        }
+        return wave_sum(s);
+    }
+};
+
+// fsx_walk.h's accessors on the heavy view (found by argument-dependent lookup from
+// walk_fixed_fast): ranks instead of sorted positions.
+template <bool kWave>
+__device__ __forceinline__ uint32_t search_gt(const HeavyView &sv, uint32_t lo, uint32_t hi, uint64_t X) {
+    if (lo >= hi) return hi;
+    const uint32_t r = sv.rank(sv.first_after(X));
+    return r < lo ? lo : r > hi ? hi : r;
+}
+
+template <bool kWave>
+__device__ __forceinline__ uint64_t sum_len(const HeavyView &sv, uint32_t lo, uint32_t hi) {
+    if (lo >= hi) return 0;
+    const uint32_t ia = sv.select(lo), ib = sv.select(hi - 1);
+    const uint32_t ta = ia / (uint32_t)kSortTile, tb = ib / (uint32_t)kSortTile;
+    if (ta == tb) return sv.tile_len_sum(ta, ia, ib);
+    uint64_t s = sv.tile_len_sum(ta, ia, ~0u) + sv.tile_len_sum(tb, 0, ib);
+    uint64_t mid = 0;
+    for (uint32_t t = ta + 1 + lane_id(); t < tb; t += 64u) mid += sv.rec[t].s1[sv.h];
+    return s + wave_sum(mid);
+}
+
+// First rank q in [from, lim) where acc0 + the lengths of ranks from..q exceed B (else lim):
+// a scan of h's packets in arrival order from select(from). k_hmode keeps the byte trigger
+// out of reach (the batch takes the run path otherwise); this is its exact definition.
+template <bool kWave>
+__device__ __forceinline__ uint32_t bytes_trigger(const HeavyView &sv, uint32_t from, uint32_t lim, uint64_t acc0, uint64_t B) {
+    if (from >= lim) return lim;
+    const uint32_t lane = lane_id();
+    uint64_t acc = acc0;
+    uint32_t q = from;
+    for (uint32_t p0 = sv.select(from); p0 < sv.n && q < lim; p0 += 64u) {
+        const uint32_t p = p0 + lane;
+        const bool mine = p < sv.n && sv.tags[p] == (sv.pat & 0xFFu);
+        const uint64_t L = mine ? sv.len[p] : 0ull;
+        const uint64_t bm = __ballot(mine);
+        const uint64_t incl = wave_incl_sum(L);
+        const uint32_t rk = q + (uint32_t)__popcll(bm & ((1ull << lane) - 1ull));
+        const uint64_t hit = __ballot(mine && rk < lim && acc + incl > B);
+        if (hit) return q + (uint32_t)__popcll(bm & ((1ull << (__ffsll((unsigned long long)hit) - 1)) - 1ull));
+        acc += __shfl(incl, 63);
+        q += (uint32_t)__popcll(bm);
+    }
+    return lim;
+}
+
+// Verdict changes of heavy source h as its list {arrival index << 1 | DROP} (the
+// MarkWriter<true, true> of the run path, positions = ranks).
+struct HeavyMarkWriter {
+    HeavyView hv;   // (by value: a pointer to it would put the view in scratch)
+    uint32_t *list;
+    uint8_t last = 0;
+    uint32_t nl = 0, last_pos = 0;
+    uint64_t npass = 0, ndrop = 0;
+    __device__ __forceinline__ void count_run(uint32_t pos) {
+        const uint64_t r = pos - last_pos;
+        ndrop += last == XDP_DROP ? r : 0ull;
+        npass += (last && last != XDP_DROP) ? r : 0ull;
+    }
+    __device__ __forceinline__ void emit(uint32_t pos, uint8_t v) {
+        if (v != last) {
+            count_run(pos);
+            const uint32_t e = hv.select(pos) << 1 | (v == XDP_DROP ? 1u : 0u);
+            if (lane_id() == 0) list[nl] = e;
+            ++nl;
+            last_pos = pos;
+            last = v;
+        }
+    }
+    __device__ __forceinline__ void finish(uint32_t b) {
+        count_run(b);
+        last_pos = b;
+    }
+};
+
+// ------------------------------------------------------------------ k_hmode
+// After k_pass0h (one block of 128 threads): the payload words' validity and the batch's
+// path for its heavy sources.
+__global__ __launch_bounds__(128) void k_hmode(BatchState *bs, const uint64_t *__restrict__ ts, uint32_t n,
+                                               const HeavySet *__restrict__ hs, const Slot *__restrict__ table,
+                                               Limits lim) {
+    __shared__ uint32_t s_bad;
+    const uint32_t h = threadIdx.x;
+    if (h == 0) s_bad = 0;
+    __syncthreads();
+    const uint64_t t0 = n ? ts[0] : 0ull;
+    const uint32_t maxL = bs->max_len;
+    const uint64_t P = lim.pps, B = lim.bps, W = lim.window;
+    if (h < hs->n && hs->resolved && hs->slot[h] != kNoSlot) {
+        const FwState st = load_state(table[hs->slot[h]]);
+        bool ok = !st.has_st || (st.tt <= ~0ull - W && st.pps < kBig && st.bps < kBig);
+        if (st.has_st && (st.bps > B || (maxL && P + 1 > (B - st.bps) / maxL))) ok = false;
+        if (!ok) atomicOr(&s_bad, 1u);
+    } else if (h < hs->n) {
+        atomicOr(&s_bad, 1u);
+    }
+    __syncthreads();
+    if (h != 0) return;
+    const uint64_t mn = ~bs->inv_min_ts;
+    const bool pay = maxL < (1u << kPayLenBits) && mn == t0 && bs->max_ts - t0 < kPayTsRange;
+    bs->pay_ok = pay ? 1u : 0u;
+    const bool fast = !bs->err && pay && !bs->nonmono && !bs->span_big && maxL < (1u << 16) &&
+                      fast_ok(bs, lim) && !(maxL && P + 1 > B / maxL) && !s_bad;
+    bs->hfast = fast ? 1u : 0u;
+}
+
+// ------------------------------------------------------------------ k_heavy_gather
+// The run path's input when k_hmode refused the batch: every heavy packet's sort word and
+// payload word at its place in its source's run (pass 0's layout: bucket light_b + h from
+// its base), stable in arrival order. One wave per sort tile.
+__global__ __launch_bounds__(256) void k_heavy_gather(const BatchState *bs, const uint8_t *__restrict__ tags,
+                                                      const uint64_t *__restrict__ ts, const uint32_t *__restrict__ len,
+                                                      uint32_t n, const uint32_t *__restrict__ offs, uint32_t tcap,
+                                                      const HeavySet *__restrict__ hs, uint32_t shift0,
+                                                      uint64_t id_mask, uint64_t *__restrict__ out,
+                                                      uint64_t *__restrict__ pout) {
+    __shared__ uint32_t s_cnt[4][kHeavyMax];
+    if (bs->err || bs->hfast) return;
+    const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
+    const uint32_t lb = bs->light_b, nh = hs->n;
+    const uint64_t tb = n ? ts[0] : 0ull;
+    const uint32_t ntiles = (n + kSortTile - 1) / kSortTile;
+    const uint64_t lt = (1ull << lane) - 1ull;
+    for (uint32_t t = blockIdx.x * 4u + w; t < ntiles; t += gridDim.x * 4u) {
+        for (uint32_t h = lane; h < kHeavyMax; h += 64) s_cnt[w][h] = 0;
+        wave_lds_order();
+        for (uint32_t r = 0; r < (uint32_t)kSortTile / 64u; ++r) {
+            const uint32_t i = t * (uint32_t)kSortTile + r * 64u + lane;
+            const uint32_t g = i < n ? tags[i] : 0u;
+            const bool hv = g >= 0x80u && (g & 0x7Fu) < nh;
+            const uint64_t act = __ballot(hv);
+            if (!act) continue;
+            const uint32_t h = g & 0x7Fu;
+            const uint64_t peers = match_digit(h, act);
+            const uint32_t lead = (uint32_t)__ffsll((unsigned long long)peers) - 1u;
+            uint32_t base = 0;
+            if (hv && lane == lead) base = s_cnt[w][h];
+            base = __shfl(base, (int)lead);
+            wave_lds_order();
+            if (hv) {
+                const uint32_t pos = offs[(size_t)(lb + h) * tcap + t] + base + (uint32_t)__popcll(peers & lt);
+                out[pos] = ((uint64_t)(lb + h) << shift0) | ((uint64_t)(hs->slot[h] & id_mask) << kIdShift) | i;
+                pout[pos] = ((ts[i] - tb) << kPayLenBits) | len[i];
+                if ((peers >> lane) == 1ull) s_cnt[w][h] = base + (uint32_t)__popcll(peers);
+            }
+            wave_lds_order();
+        }
+    }
+}
+
+// ------------------------------------------------------------------ k_walk_heavy_sel
+// One wave per heavy source: the epoch-jump walker (fsx_walk.h) over its packets by rank.
+__global__ __launch_bounds__(256) void k_walk_heavy_sel(BatchState *bs, const uint32_t *__restrict__ cnt0,
+                                                        const uint32_t *__restrict__ base0,
+                                                        const uint32_t *__restrict__ offs, uint32_t tcap,
+                                                        const uint8_t *__restrict__ tags,
+                                                        const uint64_t *__restrict__ ts,
+                                                        const uint32_t *__restrict__ len, uint32_t n,
+                                                        const HeavyTileRec *__restrict__ rec, Slot *table,
+                                                        Limits lim, HeavySet *hs, uint32_t *list,
+                                                        TableState *tstate) {
+    if (bs->err || !bs->hfast) return;
+    const uint32_t h = blockIdx.x * 4u + (threadIdx.x >> 6);
+    if (h >= hs->n) return;
+    const uint32_t lb = bs->light_b;
+    const uint32_t c = cnt0[lb + h];
+    if (c == 0) return;
+    const uint32_t a = base0[lb + h];
+    HeavyView hv{tags, ts, len, offs + (size_t)(lb + h) * tcap, rec, a, c, (n + kSortTile - 1) / kSortTile, n, h,
+                 (0x80u | h) * 0x01010101u};
+    Slot &sl = table[hs->slot[h]];
+    FwState st = load_state(sl);
+    HeavyMarkWriter mw{hv, list + 2u * a};
+    walk_fixed_fast<true>(hv, 0, c, lim, bs->max_len, mw, st);
+    mw.finish(c);
+    if (lane_id() != 0) return;
+    store_state(sl, st);
+    hs->lbase[h] = 2u * a;
+    hs->lcnt[h] = mw.nl;
+    unsigned long long *sp = reinterpret_cast<unsigned long long *>(tstate->stats);
+    if (mw.npass) {
+        atomicAdd(sp, (unsigned long long)mw.npass);
+        atomicAdd(reinterpret_cast<unsigned long long *>(&bs->allowed), (unsigned long long)mw.npass);
+    }
+    if (mw.ndrop) {
+        atomicAdd(sp + 1, (unsigned long long)mw.ndrop);
+        atomicAdd(reinterpret_cast<unsigned long long *>(&bs->dropped), (unsigned long long)mw.ndrop);
+    }
+}
+
+// ------------------------------------------------------------------ heavy flow rows
+// Per (group of kHGroupTiles tiles, heavy source): the group's sums over h's packets.
+struct HFlowPart {
+    FlowAcc a;
+    uint64_t t0, t1;    // first / last timestamp
+    uint32_t fi, has;   // arrival index of the first packet; any packet
+    uint32_t pad_[2];
+};
+
+__device__ __forceinline__ void hpart_merge(HFlowPart &x, const HFlowPart &y) {
+    if (!y.has) return;
+    if (!x.has) { x = y; return; }
+    const uint64_t d = y.t0 - x.t1;
+    acc_add(x.a, y.a);
+    x.a.d1 += (u128)d;
+    x.a.d2 += (u128)d * d;
+    x.a.dmax = d > x.a.dmax ? d : x.a.dmax;
+    x.t1 = y.t1;
+}
+
+// group g = blockIdx.x, thread h: the group's tiles in order
+__global__ __launch_bounds__(128) void k_hflow_combine(const BatchState *bs, const uint32_t *__restrict__ cnt0,
+                                                       const uint32_t *__restrict__ base0,
+                                                       const uint32_t *__restrict__ offs, uint32_t tcap, uint32_t n,
+                                                       const HeavyTileRec *__restrict__ rec, HFlowPart *part) {
+    if (bs->err || !bs->hfast) return;
+    const uint32_t h = threadIdx.x;
+    const uint32_t ntiles = (n + kSortTile - 1) / kSortTile;
+    const uint32_t g = blockIdx.x;
+    const uint32_t lb = bs->light_b;
+    const uint32_t *row = offs + (size_t)(lb + h) * tcap;
+    const uint32_t end = base0[lb + h] + cnt0[lb + h];
+    HFlowPart x;
+    x.a = acc_zero();
+    x.t0 = x.t1 = 0;
+    x.fi = 0;
+    x.has = 0;
+    x.pad_[0] = x.pad_[1] = 0;
+    const uint32_t t1 = min(ntiles, (g + 1) * kHGroupTiles);
+    for (uint32_t t = g * kHGroupTiles; t < t1; ++t) {
+        const uint32_t c = (t + 1 < ntiles ? row[t + 1] : end) - row[t];
+        if (c == 0) continue;
+        const HeavyTileRec &R = rec[t];
+        HFlowPart y;
+        y.a = acc_zero();
+        y.a.n = c;
+        y.a.s1 = R.s1[h];
+        y.a.s2 = R.s2[h];
+        y.a.d1 = R.t1[h] - R.t0[h];   // (consecutive gaps of a non-decreasing clock)
+        y.a.d2 = R.d2[h];
+        y.a.dmax = R.dmax[h];
+        y.t0 = R.t0[h];
+        y.t1 = R.t1[h];
+        y.fi = t * (uint32_t)kSortTile + R.fo[h];
+        y.has = 1;
+        y.pad_[0] = y.pad_[1] = 0;
+        hpart_merge(x, y);
+    }
+    part[(size_t)g * kHeavyMax + h] = x;
+}
+
+// After the heads (k_heads_heavy numbered the heavy segments): heavy source h's row is
+// segment nseg_light + (its rank among the non-empty ones), as on the run path.
+__global__ __launch_bounds__(128) void k_hflow_finish(const BatchState *bs, const uint32_t *__restrict__ cnt0,
+                                                      const HeavySet *__restrict__ hs,
+                                                      const HFlowPart *__restrict__ part, uint32_t ngroups,
+                                                      PacketIn in, const uint32_t *__restrict__ len, FlowOut out,
+                                                      ScoreParams P) {
+    __shared__ uint32_t s_live[kHeavyMax];
+    if (bs->err || !bs->hfast) return;
+    const uint32_t h = threadIdx.x;
+    const bool live = h < hs->n && cnt0[bs->light_b + h] > 0;
+    s_live[h] = live ? 1u : 0u;
+    __syncthreads();
+    if (!live) return;
+    uint32_t r = 0;
+    for (uint32_t j = 0; j < h; ++j) r += s_live[j];
+    HFlowPart x = part[h];
+    for (uint32_t g = 1; g < ngroups; ++g) hpart_merge(x, part[(size_t)g * kHeavyMax + h]);
+    const uint32_t row = bs->nseg_light + r;
+    uint32_t k[4] = {hs->key[h][0], hs->key[h][1], hs->key[h][2], hs->key[h][3]};
+    const uint32_t dport = dst_port(in.hdr + (size_t)x.fi * 64, len[x.fi]);
+    flow_emit(row, x.a, hs->tag[h], k, dport, x.t0, x.t1, hs->slot[h], out, P);
+}
+
+size_t hflow_bytes(uint64_t cap) {
+    return ((cap / kSortTile + 2) / kHGroupTiles + 1) * kHeavyMax * sizeof(HFlowPart);
+}
+
+// ------------------------------------------------------------------ launchers
+hipError_t launch_hmode(BatchState *bs, const uint64_t *ts, uint32_t n, const HeavySet *hs, const Slot *table,
+                        const Limits &lim, hipStream_t st) {
+    k_hmode<<<1, 128, 0, st>>>(bs, ts, n, hs, table, lim);
+    return hipGetLastError();
+}
+
+hipError_t launch_heavy_gather(const BatchState *bs, const uint8_t *tags, const uint64_t *ts, const uint32_t *len,
+                               uint32_t n, const uint32_t *offs, uint32_t tcap, const HeavySet *hs, uint32_t shift0,
+                               uint64_t id_mask, uint64_t *out, uint64_t *pout, hipStream_t st) {
+    const uint32_t ntiles = (n + kSortTile - 1) / kSortTile;
+    const uint32_t grid = std::max<uint32_t>(1, std::min<uint32_t>(1024, (ntiles + 3) / 4));
+    k_heavy_gather<<<grid, 256, 0, st>>>(bs, tags, ts, len, n, offs, tcap, hs, shift0, id_mask, out, pout);
+    return hipGetLastError();
+}
+
+hipError_t launch_walk_heavy_sel(BatchState *bs, const uint32_t *cnt0, const uint32_t *base0, const uint32_t *offs,
+                                 uint32_t tcap, const uint8_t *tags, const uint64_t *ts, const uint32_t *len,
+                                 uint32_t n, const void *rec, Slot *table, const Limits &lim, HeavySet *hs,
+                                 uint32_t *list, TableState *tstate, hipStream_t st) {
+    k_walk_heavy_sel<<<kHeavyMax / 4, 256, 0, st>>>(bs, cnt0, base0, offs, tcap, tags, ts, len, n,
+                                                     static_cast<const HeavyTileRec *>(rec), table, lim, hs, list,
+                                                     tstate);
+    return hipGetLastError();
+}
+
+hipError_t launch_hflow_combine(const BatchState *bs, const uint32_t *cnt0, const uint32_t *base0,
+                                const uint32_t *offs, uint32_t tcap, uint32_t n, const void *rec, void *part,
+                                hipStream_t st) {
+    const uint32_t ntiles = (n + kSortTile - 1) / kSortTile;
+    const uint32_t ng = std::max<uint32_t>(1, (ntiles + kHGroupTiles - 1) / kHGroupTiles);
+    k_hflow_combine<<<ng, 128, 0, st>>>(bs, cnt0, base0, offs, tcap, n, static_cast<const HeavyTileRec *>(rec),
+                                         static_cast<HFlowPart *>(part));
+    return hipGetLastError();
+}
+
+hipError_t launch_hflow_finish(const BatchState *bs, const uint32_t *cnt0, const HeavySet *hs, const void *part,
+                               uint32_t n, const PacketIn &in, const uint32_t *len, const uint64_t *ts,
+                               uint8_t *keys16, uint8_t *fam, float *feat, float *prob, uint8_t *dec,
+                               uint32_t rows_cap, const ScoreParams &P, void *sacc, uint32_t epoch,
+                               const PartialOut &partial, hipStream_t st) {
+    const uint32_t ntiles = (n + kSortTile - 1) / kSortTile;
+    const uint32_t ng = std::max<uint32_t>(1, (ntiles + kHGroupTiles - 1) / kHGroupTiles);
+    FlowOut out{nullptr, keys16, fam, feat, prob, dec, rows_cap, (SlotAcc *)sacc, epoch, nullptr, ts,
+                nullptr, nullptr, partial};
+    k_hflow_finish<<<1, 128, 0, st>>>(bs, cnt0, hs, static_cast<const HFlowPart *>(part), ng, in, len, out, P);
+    return hipGetLastError();
+}
+
+}  // namespace fsx

@@ -95,6 +95,13 @@ struct BatchState {
                           // heavy sources' segments follow (k_heads_heavy)
     uint32_t light_b;     // heavy-source sort: heavy source h is pass-0 bucket light_b + h
                           // (k_hist_prep; 256 without the heavy sort)
+    // unsorted heavy sources (DESIGN.md §3 "Heavy sources outside the sort"): k_pass0h's
+    // clock facts and k_hmode's verdict — 1: the heavy walker and flow rows work on the
+    // arrival order (select / rank over the tagged verdict bytes); 0: k_heavy_gather
+    // builds the heavy runs and the run-based kernels take over
+    uint32_t hfast;
+    uint32_t span_big;    // some sort tile spans >= 2^32 ns (u64 gap-square sums could wrap)
+    uint64_t ts0;         // timestamp of packet 0 (payload base of the parse-side payloads)
 };
 
 // Sorted payload word carried through the onesweep passes next to each sort word:
@@ -362,8 +369,33 @@ struct Scratch {
                            // packets [kSketch] each (counts zeroed by k_heavy_pick after use)
     HeavySet *heavy;
     void *heavy_flow;      // heavy sources' flow chunk sums (heavy_flow_bytes)
+    // unsorted heavy sources (front buffers, one per pipelined set): light sort-word count
+    // of every 1024-packet parse chunk (k_parse writes the light words compacted per chunk)
+    // and one HeavyTileRec per sort tile (k_pass0h)
+    uint32_t *chunk_cnt;
+    void *hrec;
+    void *hflow;           // tail: per (group of kHGroupTiles tiles, heavy source) flow sums
     uint64_t cap;          // packets the scratch is sized for
 };
+
+// Unsorted heavy sources: per sort tile (4096 arrival positions) and heavy source h, the
+// sums the flow features need over h's packets of the tile (SoA, so a block writes one
+// contiguous record per tile and a thread per h reads it coalesced). Exact while the batch
+// clock is non-decreasing, every frame < 2^16 B and every tile spans < 2^32 ns (k_hmode
+// checks; otherwise the runs are built and the records ignored).
+struct HeavyTileRec {
+    uint32_t s1[kHeavyMax];     // sum of frame lengths
+    uint32_t dmax[kHeavyMax];   // largest gap between consecutive packets of h inside the tile
+    uint32_t fo[kHeavyMax];     // arrival offset (in the tile) of h's first packet
+    uint32_t pad_[kHeavyMax];
+    uint64_t s2[kHeavyMax];     // sum of squared lengths
+    uint64_t t0[kHeavyMax];     // first and last timestamp
+    uint64_t t1[kHeavyMax];
+    uint64_t d2[kHeavyMax];     // sum of squared gaps inside the tile
+};
+constexpr uint32_t kHGroupTiles = 256;   // tiles per k_hflow_combine group
+inline size_t heavy_rec_bytes(uint64_t cap) { return (cap / kSortTile + 2) * sizeof(HeavyTileRec); }
+inline size_t chunk_cnt_bytes(uint64_t cap) { return (cap / 1024 + 8) * 4; }
 
 // Flow partials (fsx_flow_partials_records_device): every source's raw sums go to the run of
 // its owner rank (G runs of cap partials, cnt[o] per run) instead of a row.
@@ -450,6 +482,8 @@ struct TailArgs {
     Scratch sc;
     Limits lim;
     bool do_limit, has_flows, split, tagh, fork;
+    bool hfm;             // heavy sources outside the sort (k_pass0h ran; k_hmode picks the path)
+    uint32_t shift0;      // pass 0's bucket shift (k_heavy_gather's sort words)
     FlowRequest fq;
     HistBufs hist;
     hipStream_t st, st2, st3;
@@ -518,6 +552,30 @@ hipError_t launch_flows_heavy_finish(const uint64_t *S, const BatchState *bs, co
                                      float *feat, float *prob, uint8_t *dec, uint32_t rows_cap,
                                      const ScoreParams &P, uint32_t salt, void *sacc, uint32_t epoch,
                                      const uint32_t *seg_slot, hipStream_t st);
+
+// Heavy sources outside the sort (fsx_heavy.hip; k_pass0h in fsx_device.hip), DESIGN.md §3.
+hipError_t launch_pass0h(const uint64_t *in, uint64_t *out, uint32_t n, uint32_t shift, uint32_t dmask,
+                         const uint32_t *offs, uint32_t tcap, BatchState *bs, uint64_t *pout, const uint64_t *ts,
+                         const uint32_t *len, const uint8_t *tags, const uint32_t *chunk_cnt, void *rec,
+                         const HeavySet *hs, hipStream_t st);
+hipError_t launch_hmode(BatchState *bs, const uint64_t *ts, uint32_t n, const HeavySet *hs, const Slot *table,
+                        const Limits &lim, hipStream_t st);
+hipError_t launch_heavy_gather(const BatchState *bs, const uint8_t *tags, const uint64_t *ts, const uint32_t *len,
+                               uint32_t n, const uint32_t *offs, uint32_t tcap, const HeavySet *hs, uint32_t shift0,
+                               uint64_t id_mask, uint64_t *out, uint64_t *pout, hipStream_t st);
+hipError_t launch_walk_heavy_sel(BatchState *bs, const uint32_t *cnt0, const uint32_t *base0, const uint32_t *offs,
+                                 uint32_t tcap, const uint8_t *tags, const uint64_t *ts, const uint32_t *len,
+                                 uint32_t n, const void *rec, Slot *table, const Limits &lim, HeavySet *hs,
+                                 uint32_t *list, TableState *tstate, hipStream_t st);
+size_t hflow_bytes(uint64_t cap);
+hipError_t launch_hflow_combine(const BatchState *bs, const uint32_t *cnt0, const uint32_t *base0,
+                                const uint32_t *offs, uint32_t tcap, uint32_t n, const void *rec, void *part,
+                                hipStream_t st);
+hipError_t launch_hflow_finish(const BatchState *bs, const uint32_t *cnt0, const HeavySet *hs, const void *part,
+                               uint32_t n, const PacketIn &in, const uint32_t *len, const uint64_t *ts,
+                               uint8_t *keys16, uint8_t *fam, float *feat, float *prob, uint8_t *dec,
+                               uint32_t rows_cap, const ScoreParams &P, void *sacc, uint32_t epoch,
+                               const PartialOut &partial, hipStream_t st);
 
 size_t flow_acc_bytes();
 size_t slot_acc_bytes();

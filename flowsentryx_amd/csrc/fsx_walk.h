@@ -77,7 +77,7 @@ __device__ void walk_fixed_exact_wave(const SV &sv, uint32_t a, uint32_t b, cons
 // counts consecutive inside an epoch, the count trigger is at a closed-form
 // position; the window end and the blacklist end are searches.
 template <bool kWave, class SV, class MW>
-__device__ void walk_fixed_fast(const SV &sv, uint32_t a, uint32_t b, const Limits &lim,
+__device__ __forceinline__ void walk_fixed_fast(const SV &sv, uint32_t a, uint32_t b, const Limits &lim,
                                 uint32_t maxL, MW &mw, FwState &s) {
     const uint64_t P = lim.pps, B = lim.bps, W = lim.window, BLK = lim.block;
     uint32_t p = a;

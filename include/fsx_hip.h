@@ -383,7 +383,9 @@ int fsx_pcap_records_device(fsx_ctx *ctx, const uint8_t *d_buf, const uint64_t *
  * words (timestamps within 2^40 ns of the batch minimum, frame lengths < 2^24), 0 when
  * they were gathered by index, [11] IP packets of non-heavy sources (the entries the
  * later sort passes covered), [12] sources evicted before the batch
- * (FSX_FLAG_EVICT_IDLE). Returns the number of entries written. */
+ * (FSX_FLAG_EVICT_IDLE), [13] 1 when the heavy sources' verdicts and flow rows were
+ * computed outside the sort, 0 on the run path. Returns the number of
+ * entries written. */
 int fsx_last_batch_info(fsx_ctx *ctx, uint64_t *info, int cap);
 
 /* Per-kernel device timing for the benchmark: while enabled, every batch records a
