@@ -38,6 +38,8 @@ struct fsx_ctx {
     hipStream_t stream = nullptr;
     Slot *table = nullptr;
     uint64_t slots = 0;
+    uint64_t id_slots = 0;       // per-batch id table (flow-only batches; FSX_FLAG_OVERFLOW_ADMIT)
+    uint64_t tr_slots = 0;       // FSX_FLAG_OVERFLOW_ADMIT: transient slots after the table
     TableState *tstate = nullptr;
     BatchState *bs = nullptr;
     Scratch sc{};
@@ -192,6 +194,7 @@ static void free_scratch(fsx_ctx *c) {
     hipFree(s.lim_tiles); hipFree(s.sw_seg); hipFree(s.sketch); hipFree(s.heavy);
     hipFree(s.drop_list); hipFree(s.drop_cur); hipFree(s.heavy_flow);
     hipFree(s.chunk_cnt); hipFree(s.hrec); hipFree(s.hflow);
+    hipFree(s.admit_rank); hipFree(s.admit_cnt);
     s = Scratch{};
 }
 
@@ -388,6 +391,9 @@ int fsx_open(fsx_ctx **out, const fsx_config *cfg) {
     if (k.limiter == FSX_LIMIT_SLIDING_WINDOW && k.pps_threshold > FSX_SW_MAX_PPS) return -EINVAL;
     // idle eviction is defined for the reference's fixed window only
     if ((k.flags & FSX_FLAG_EVICT_IDLE) && k.limiter != FSX_LIMIT_FIXED_WINDOW) return -EINVAL;
+    // admission: transient slots (slots + segment id) must stay below 2^32 (u32 seg_slot)
+    const bool admit = (k.flags & FSX_FLAG_OVERFLOW_ADMIT) != 0;
+    if (admit && next_pow2(std::max<uint64_t>(1024, 2 * k.max_entries)) + k.max_batch >= (1ull << 32)) return -EINVAL;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return -ENODEV;
     if (k.device < 0 || k.device >= ndev) return -EINVAL;
@@ -398,6 +404,8 @@ int fsx_open(fsx_ctx **out, const fsx_config *cfg) {
     int rc = sel(c);
     if (rc) { fsx_close(c); return rc; }
     c->slots = next_pow2(std::max<uint64_t>(1024, 2 * k.max_entries));
+    c->tr_slots = admit ? k.max_batch : 0;
+    c->id_slots = admit ? std::max<uint64_t>(c->slots, next_pow2(std::max<uint64_t>(1024, 2 * k.max_batch))) : c->slots;
     auto fail = [&](int r) { fsx_close(c); return r; };
     // stream priorities (A/B: FSX_STREAM_PRIO="own,aux,walk", lower = more urgent): the
     // context stream (parse, sort) first, so a pipelined batch's short sort scans find CU
@@ -414,7 +422,7 @@ int fsx_open(fsx_ctx **out, const fsx_config *cfg) {
     if (hipEventCreateWithFlags(&c->heavy_fork_ev, hipEventDisableTiming) != hipSuccess) return fail(-EIO);
     if (hipEventCreateWithFlags(&c->heavy_flow_ev, hipEventDisableTiming) != hipSuccess) return fail(-EIO);
     c->stream = c->own_stream;
-    if (hipMalloc(&c->table, c->slots * sizeof(Slot)) != hipSuccess) return fail(-ENOMEM);
+    if (hipMalloc(&c->table, (c->slots + c->tr_slots) * sizeof(Slot)) != hipSuccess) return fail(-ENOMEM);
     if (hipMalloc(&c->tstate, sizeof(TableState)) != hipSuccess) return fail(-ENOMEM);
     if (hipMalloc(&c->bs, sizeof(BatchState)) != hipSuccess) return fail(-ENOMEM);
     if (hipMalloc(&c->d_res, 64) != hipSuccess) return fail(-ENOMEM);
@@ -462,6 +470,13 @@ int fsx_open(fsx_ctx **out, const fsx_config *cfg) {
     L.salt32 = (uint32_t)(mix64(k.hash_seed ^ 0xABCDEFull) >> 32);
     L.limiter = k.limiter;
     L.test_flags = k.flags;
+    L.admit_mask = admit ? c->id_slots - 1 : 0;
+    if (admit) {   // the per-batch id table and the rank scratch, up front
+        if (hipMalloc(&c->sc.id_tab, c->id_slots * 32) != hipSuccess) return fail(-ENOMEM);
+        if (hipMemset(c->sc.id_tab, 0, c->id_slots * 32) != hipSuccess) return fail(-EIO);
+        if (hipMalloc(&c->sc.admit_rank, std::max<uint64_t>(1, k.max_batch) * 4) != hipSuccess) return fail(-ENOMEM);
+        if (hipMalloc(&c->sc.admit_cnt, (k.max_batch / kTile + 2) * 4) != hipSuccess) return fail(-ENOMEM);
+    }
     if (hipDeviceSynchronize() != hipSuccess) return fail(-EIO);
     *out = c;
     return 0;
@@ -799,7 +814,7 @@ static int run_pipelined(fsx_ctx *c, const PacketIn &in, const uint32_t *d_len, 
     use_front(c, q);
     c->par = q;
     if (++c->id_gen == 0x10000u) {
-        if (c->sc.id_tab) HIPCHK(c, hipMemsetAsync(c->sc.id_tab, 0, c->slots * 32, c->stream));
+        if (c->sc.id_tab) HIPCHK(c, hipMemsetAsync(c->sc.id_tab, 0, c->id_slots * 32, c->stream));
         c->id_gen = 1;
     }
     // the early prologue on the aux stream (FSX_NO_EARLY_PROLOGUE=1: on the context stream)
@@ -887,7 +902,8 @@ static int run_batch(fsx_ctx *c, const PacketIn &in, const uint32_t *d_len, cons
     // records, the whole batch on the context stream otherwise
     if (c->pipe && do_limit && n && !c->timing)
         return run_pipelined(c, in, d_len, d_ts, n, d_verdict, fr,
-                             c->pipe == 1 && !in.rec && c->cfg.limiter == FSX_LIMIT_FIXED_WINDOW);
+                             c->pipe == 1 && !in.rec && c->cfg.limiter == FSX_LIMIT_FIXED_WINDOW &&
+                                 !(c->cfg.flags & FSX_FLAG_OVERFLOW_ADMIT));
     int rc = sel(c);
     if (rc) return rc;
     if (busy(c)) { rc = fsx_sync(c); if (rc) return rc; }
@@ -906,11 +922,11 @@ static int run_batch(fsx_ctx *c, const PacketIn &in, const uint32_t *d_len, cons
         tm = &tmv;
     }
     if (!do_limit && !c->sc.id_tab) {   // flow-only batch: its per-batch id table
-        HIPCHK(c, hipMalloc(&c->sc.id_tab, c->slots * 32));
-        HIPCHK(c, hipMemsetAsync(c->sc.id_tab, 0, c->slots * 32, c->stream));   // every slot empty
+        HIPCHK(c, hipMalloc(&c->sc.id_tab, c->id_slots * 32));
+        HIPCHK(c, hipMemsetAsync(c->sc.id_tab, 0, c->id_slots * 32, c->stream));   // every slot empty
     }
     if (++c->id_gen == 0x10000u) {   // 16-bit generations: clear the id table on wrap
-        if (c->sc.id_tab) HIPCHK(c, hipMemsetAsync(c->sc.id_tab, 0, c->slots * 32, c->stream));
+        if (c->sc.id_tab) HIPCHK(c, hipMemsetAsync(c->sc.id_tab, 0, c->id_slots * 32, c->stream));
         c->id_gen = 1;
     }
     hipError_t e = launch_verdict_pipeline(in, d_len, d_ts, (uint32_t)n, d_verdict, c->table,
@@ -1196,7 +1212,7 @@ int fsx_map_update_batch(fsx_ctx *c, int map_id, const void *keys, const void *v
     hipError_t e = hipMemcpyAsync(dk, keys, n * klen, hipMemcpyHostToDevice, c->stream);
     if (e == hipSuccess) e = hipMemcpyAsync(dv, values, n * vlen, hipMemcpyHostToDevice, c->stream);
     if (e == hipSuccess && ++c->id_gen == 0x10000u) {   // 16-bit generations (as run_batch)
-        if (c->sc.id_tab) e = hipMemsetAsync(c->sc.id_tab, 0, c->slots * 32, c->stream);
+        if (c->sc.id_tab) e = hipMemsetAsync(c->sc.id_tab, 0, c->id_slots * 32, c->stream);
         c->id_gen = 1;
     }
     const uint32_t born = c->id_gen;
@@ -1387,6 +1403,8 @@ int fsx_flow_features(fsx_ctx *c, const uint8_t *hdr, const uint32_t *len, const
 
 int fsx_flows_begin(fsx_ctx *c) {
     if (!c) return -EINVAL;
+    if (c->cfg.flags & FSX_FLAG_OVERFLOW_ADMIT)   // (transient sources have no slot to carry sums in)
+        return set_err(c, -EINVAL, "FSX_FLAG_OVERFLOW_ADMIT: not with fsx_flows_begin");
     int rc = sel(c);
     if (rc) return rc;
     if (!c->d_slot_acc) {
@@ -1426,11 +1444,11 @@ int fsx_last_batch_info(fsx_ctx *c, uint64_t *info, int cap) {
     HIPCHK(c, hipStreamSynchronize(c->stream));
     BatchState h;
     HIPCHK(c, hipMemcpy(&h, c->bs, sizeof(h), hipMemcpyDeviceToHost));
-    const uint64_t v[14] = {h.n_valid, h.nseg, h.n_new, h.any_v6, h.nonmono, h.max_len,
+    const uint64_t v[16] = {h.n_valid, h.nseg, h.n_new, h.any_v6, h.nonmono, h.max_len,
                             h.max_ts, h.allowed, h.dropped, h.n_rule, h.pay_ok, h.n_light,
-                            c->last_evicted, h.hfast};
+                            c->last_evicted, h.hfast, h.n_admit, h.n_trans};
     int k = 0;
-    for (; k < cap && k < 14; ++k) info[k] = v[k];
+    for (; k < cap && k < 16; ++k) info[k] = v[k];
     return k;
 }
 

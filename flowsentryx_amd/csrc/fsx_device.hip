@@ -1202,12 +1202,25 @@ __global__ __launch_bounds__(256, FSX_SCATTER_MINB) void k_pass0h(const uint64_t
     uint64_t prev_t = lane == 0 && c0 > 0 && c0 < n ? ts[c0 - 1] : 0ull;   // (lane 0: before the chunk)
     uint32_t nonmono = 0;
     uint64_t mx = 0, imn = 0;   // max, ~min
+    // the chunk's 16 rows loaded up front (the LDS ordering below is a compiler barrier: loads
+    // issued inside the row loop would each wait a full memory latency)
+    uint64_t Tr[16];
+    uint32_t Lr[16], Gr[16];
+#pragma unroll
     for (uint32_t r = 0; r < 16; ++r) {
         const uint32_t i = c0 + r * 64u + lane;
         const bool live = i < n;
-        const uint64_t T = live ? ts[i] : 0ull;
-        const uint32_t L = live ? len[i] : 0u;
-        const uint32_t g = live ? tags[i] : 0u;
+        Tr[r] = ts[live ? i : 0u];
+        Lr[r] = len[live ? i : 0u];
+        Gr[r] = live ? tags[i] : 0u;
+    }
+#pragma unroll
+    for (uint32_t r = 0; r < 16; ++r) {
+        const uint32_t i = c0 + r * 64u + lane;
+        const bool live = i < n;
+        const uint64_t T = live ? Tr[r] : 0ull;
+        const uint32_t L = live ? Lr[r] : 0u;
+        const uint32_t g = Gr[r];
         uint64_t pv = __shfl_up(T, 1);
         if (lane == 0) pv = (c0 + r * 64u > 0) ? prev_t : T;
         if (live) {
@@ -1659,6 +1672,178 @@ __global__ void k_batch_check(BatchState *bs, TableState *tstate, Limits lim, co
         atomicAdd(reinterpret_cast<unsigned long long *>(&tstate->stats[1]), (unsigned long long)bs->n_rule);
         bs->dropped += bs->n_rule;
     }
+}
+
+// ------------------------------------------------------------------ overflow admission
+// FSX_FLAG_OVERFLOW_ADMIT (include/fsx_hip.h): the batch's sources carry
+// per-batch ids; after the segment heads, every source is found in the persistent index
+// (read only) or flagged at its first packet's arrival index; the flags' exclusive scan in
+// arrival order is each new source's admission rank; ranks below the free room are inserted
+// into the index (their fresh table slot), the others get a slot of the transient region
+// after the table (slots + segment id), fresh for this batch and never dumped or looked up.
+
+// Slot of (tag, key) in the persistent index, kNoSlot when absent (no inserts race it).
+__device__ __forceinline__ uint32_t index_find(const TableIndex &X, const Limits &lim, uint32_t tag,
+                                               const uint32_t k[4]) {
+    // (the probe start computed from scalars: through the array, the compiler kept two of
+    // the key words in scratch)
+    const uint32_t k0 = k[0], k1 = k[1], k2 = k[2], k3 = k[3];
+    const uint64_t hv6 = mix64(mix64(lim.seed ^ (2ull << 56) ^ ((uint64_t)k0 | ((uint64_t)k1 << 32))) ^
+                               ((uint64_t)k2 | ((uint64_t)k3 << 32)));
+    uint64_t h = tag == 1 ? (uint64_t)v4_hash(k0, lim.seed)
+                          : (lim.test_flags & 1u) ? (uint64_t)v4_hash(0x0100000Au, lim.seed) : hv6;
+    h &= lim.table_mask;
+    for (uint64_t probes = 0; probes <= lim.table_mask; ++probes, h = (h + 1) & lim.table_mask) {
+        const uint64_t cur = __hip_atomic_load(X.heads + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((uint32_t)(cur >> 48) != X.epoch) return kNoSlot;   // empty in this epoch
+        if (((cur >> 32) & 0xFFu) != tag || (uint32_t)cur != k0) continue;
+        if (tag == 1) return (uint32_t)h;
+        const uint32_t *kw = X.k6 + h * 4;
+        if (__hip_atomic_load(kw + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == k1 &&
+            __hip_atomic_load(kw + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == k2 &&
+            __hip_atomic_load(kw + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == k3)
+            return (uint32_t)h;
+    }
+    return kNoSlot;
+}
+
+// The source of segment g (its first packet's record), and that packet's arrival index.
+__device__ __forceinline__ uint32_t seg_source(const uint64_t *S, const uint32_t *seg_start, uint32_t g,
+                                               const PacketIn &in, uint32_t salt, uint32_t k[4], uint32_t &idx) {
+    (void)salt;
+    const uint64_t v = S[seg_start[g]];
+    idx = pk_idx(v);
+    // (the key words as scalars, written once: branches that filled the array differently
+    // made the compiler select them through scratch)
+    uint32_t k0, k1 = 0, k2 = 0, k3 = 0, tag;
+    if (in.rec) {   // ShardRecord16 {key, len | dport << 16, ts} / ShardRecord {key[4], ts, len, ...}
+        if (in.rec_bytes == 16) {
+            k0 = reinterpret_cast<const uint4 *>(in.rec)[idx].x;
+            tag = 1;
+        } else {
+            const uint4 *p = reinterpret_cast<const uint4 *>(in.rec) + 2 * (size_t)idx;
+            const uint4 a = p[0], b = p[1];
+            k0 = a.x; k1 = a.y; k2 = a.z; k3 = a.w;
+            tag = ((b.w >> 16) & 0xFFu) == 6 ? 2u : 1u;
+        }
+    } else {        // key_of, both families' words computed and selected
+        const uint32_t *d = reinterpret_cast<const uint32_t *>(in.hdr + (size_t)idx * 64);
+        const uint32_t d3 = d[3], d5 = d[5], d6 = d[6], d7 = d[7], d8 = d[8], d9 = d[9];
+        const bool v6 = (d3 & 0xFFFFu) == 0xDD86u;
+        k0 = v6 ? (d5 >> 16) | (d6 << 16) : (d6 >> 16) | (d7 << 16);
+        k1 = v6 ? (d6 >> 16) | (d7 << 16) : 0u;
+        k2 = v6 ? (d7 >> 16) | (d8 << 16) : 0u;
+        k3 = v6 ? (d8 >> 16) | (d9 << 16) : 0u;
+        tag = v6 ? 2u : 1u;
+    }
+    k[0] = k0; k[1] = k1; k[2] = k2; k[3] = k3;
+    return tag;
+}
+
+__global__ __launch_bounds__(256) void k_admit_find(const BatchState *bs, const uint64_t *__restrict__ S,
+                                                    const uint32_t *__restrict__ seg_start,
+                                                    uint32_t *__restrict__ seg_slot, PacketIn in, TableIndex X,
+                                                    Limits lim, uint32_t *__restrict__ flag) {
+    if (bs->err) return;
+    const uint32_t nseg = bs->nseg;
+    for (uint32_t g = blockIdx.x * 256u + threadIdx.x; g < nseg; g += gridDim.x * 256u) {
+        uint32_t k[4], idx;
+        const uint32_t tag = seg_source(S, seg_start, g, in, lim.salt32, k, idx);
+        const uint32_t s = index_find(X, lim, tag, k);
+        seg_slot[g] = s;
+        if (s == kNoSlot) flag[idx] = 1u;
+    }
+}
+
+// per 4096 arrival positions: the flagged ones (tile_cnt), then (mode 1, after the scan of
+// tile_cnt) each flagged position's rank in place
+template <int kMode>
+__global__ __launch_bounds__(256) void k_admit_rank(const BatchState *bs, uint32_t *__restrict__ flag, uint32_t n,
+                                                    uint32_t *__restrict__ tile_cnt) {
+    __shared__ uint32_t s_tmp[4];
+    if (bs->err) return;
+    const uint32_t ntiles = (n + kTile - 1) / kTile;
+    for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const uint32_t p0 = t * kTile + threadIdx.x * 16u;
+        uint32_t f[16], c = 0;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            f[j] = p0 + j < n ? flag[p0 + j] : 0u;
+            c += f[j];
+        }
+        uint32_t tot;
+        uint32_t off = block256_excl(c, s_tmp, &tot);
+        if constexpr (kMode == 0) {
+            if (threadIdx.x == 0) tile_cnt[t] = tot;
+        } else {
+            off += tile_cnt[t];
+#pragma unroll
+            for (int j = 0; j < 16; ++j)
+                if (f[j]) flag[p0 + j] = off++;
+        }
+    }
+}
+
+// one block: exclusive scan of the per-tile counts in place
+__global__ __launch_bounds__(256) void k_admit_scan(const BatchState *bs, uint32_t *__restrict__ cnt, uint32_t n) {
+    __shared__ uint32_t s_tmp[4];
+    if (bs->err) return;
+    const uint32_t ntiles = (n + kTile - 1) / kTile;
+    uint32_t carry = 0;
+    for (uint32_t c0 = 0; c0 < ntiles; c0 += 256) {
+        const uint32_t i = c0 + threadIdx.x;
+        const uint32_t x = i < ntiles ? cnt[i] : 0u;
+        uint32_t tot;
+        const uint32_t e = block256_excl(x, s_tmp, &tot);
+        if (i < ntiles) cnt[i] = carry + e;
+        carry += tot;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_admit_insert(BatchState *bs, const TableState *tstate,
+                                                      const uint64_t *__restrict__ S,
+                                                      const uint32_t *__restrict__ seg_start,
+                                                      uint32_t *__restrict__ seg_slot, PacketIn in, IdTable idt,
+                                                      Limits lim, const uint32_t *__restrict__ rank, Slot *table,
+                                                      uint64_t tbase) {
+    if (bs->err) return;
+    const uint64_t cnt = tstate->count;
+    const uint64_t room = cnt < lim.max_entries ? lim.max_entries - cnt : 0ull;
+    const uint32_t nseg = bs->nseg;
+    uint32_t na = 0, nt = 0;
+    for (uint32_t g = blockIdx.x * 256u + threadIdx.x; g < nseg; g += gridDim.x * 256u) {
+        if (seg_slot[g] != kNoSlot) continue;
+        uint32_t k[4], idx;
+        const uint32_t tag = seg_source(S, seg_start, g, in, lim.salt32, k, idx);
+        if (rank[idx] < room) {   // admitted: its slot in the persistent index
+            const uint64_t h = id_start(idt, tag, k);
+            const uint64_t hint = __hip_atomic_load(idt.head + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            bool fresh = false;
+            const uint32_t s = id_resolve(idt, tag, k, h, hint, &fresh);
+            if (s == kNoSlot) atomicOr(&bs->err, ERR_TABLE_FULL);
+            seg_slot[g] = s;
+            ++na;
+        } else {                  // transient: a fresh slot of its own for this batch
+            Slot &sl = table[tbase + g];
+            sl.tag = tag;
+            sl.flags = 0;
+            sl.key[0] = k[0]; sl.key[1] = k[1]; sl.key[2] = k[2]; sl.key[3] = k[3];
+            sl.pps = sl.bps = sl.tt = sl.till = sl.aux = 0;
+            seg_slot[g] = (uint32_t)(tbase + g);
+            ++nt;
+        }
+    }
+    na = wave_sum(na);
+    nt = wave_sum(nt);
+    if (lane_id() == 0) {
+        if (na) atomicAdd(&bs->n_admit, na);
+        if (nt) atomicAdd(&bs->n_trans, nt);
+    }
+}
+
+__global__ void k_admit_commit(BatchState *bs, TableState *tstate) {
+    if (bs->err) return;
+    tstate->count += bs->n_admit;
 }
 
 // Rollback / epoch change: re-publish every live slot under the new epoch; slots born in
@@ -2376,11 +2561,27 @@ hipError_t launch_tail(const TailArgs &a) {
     // (the first sort word's low half per segment only for the flow rows)
     uint32_t *seg_lo = flows && !in.rec ? sc.seg_lo : nullptr;
     k_heads_write<<<gridTiles, 256, 0, st>>>(bs, sc.headf, sc.tile_aux, sc.seg_start, S,
-                                             do_limit ? sc.seg_slot : nullptr, lim.table_mask, lo, seg_lo);
+                                             do_limit ? sc.seg_slot : nullptr,
+                                             a.admit ? lim.admit_mask : lim.table_mask, lo, seg_lo);
     if (tagh)
         k_heads_heavy<<<1, 256, 0, st>>>(bs, sc.sort_ctl, sc.gbase, sc.seg_start, do_limit ? sc.seg_slot : nullptr,
                                          S_fin, lim.table_mask, seg_lo, sc.heavy);
     mark("k_heads_write");
+    if (a.admit) {   // FSX_FLAG_OVERFLOW_ADMIT: every segment's table slot (admitted / transient)
+        const uint32_t ga = std::min<uint32_t>(2048, std::max<uint32_t>(1, cdiv(n, 256)));
+        const uint32_t gt = std::min<uint32_t>(4096, std::max<uint32_t>(1, cdiv(n, kTile)));
+        k_admit_find<<<ga, 256, 0, st>>>(bs, S, sc.seg_start, sc.seg_slot, in, a.X, lim, sc.admit_rank);
+        k_admit_rank<0><<<gt, 256, 0, st>>>(bs, sc.admit_rank, n, sc.admit_cnt);
+        k_admit_scan<<<1, 256, 0, st>>>(bs, sc.admit_cnt, n);
+        k_admit_rank<1><<<gt, 256, 0, st>>>(bs, sc.admit_rank, n, sc.admit_cnt);
+        static const uint32_t coherent = getenv("FSX_ID_COHERENT") ? 1u : 0u;
+        const IdTable pidt{a.X.heads, a.X.k6, lim.table_mask, lim.seed, a.X.epoch, lim.test_flags, table, a.id_gen,
+                           coherent, a.X.mir, a.X.mir_shift};
+        k_admit_insert<<<ga, 256, 0, st>>>(bs, tstate, S, sc.seg_start, sc.seg_slot, in, pidt, lim, sc.admit_rank,
+                                           table, lim.table_mask + 1);
+        k_admit_commit<<<1, 1, 0, st>>>(bs, tstate);
+        mark("k_admit");
+    }
     if (flows) {
         hipStream_t fs = st;
         if (fork) {   // the features run beside the limiter
@@ -2502,19 +2703,24 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
     // with the limiter, sources are found / inserted in the persistent index (sort id =
     // table slot); flow features alone use a per-batch id table and touch no map state
     static const uint32_t coherent = getenv("FSX_ID_COHERENT") ? 1u : 0u;
-    const IdTable idt = do_limit
+    // FSX_FLAG_OVERFLOW_ADMIT: per-batch ids for every source; table slots from the admission
+    // kernels after the heads (launch_tail)
+    const bool admit = do_limit && (lim.test_flags & kFlagAdmit) != 0;
+    const uint64_t bmask = admit ? lim.admit_mask : lim.table_mask;   // the per-batch id table's
+    const IdTable idt = do_limit && !admit
         ? IdTable{X.heads, X.k6, lim.table_mask, lim.seed, X.epoch, lim.test_flags, table, id_gen, coherent,
                   X.mir, X.mir_shift}
-        : IdTable{reinterpret_cast<unsigned long long *>(sc.id_tab), sc.id_tab + 2 * (lim.table_mask + 1),
-                  lim.table_mask, lim.seed, id_gen, lim.test_flags, nullptr, 0, coherent};
+        : IdTable{reinterpret_cast<unsigned long long *>(sc.id_tab), sc.id_tab + 2 * (bmask + 1),
+                  bmask, lim.seed, id_gen, lim.test_flags, nullptr, 0, coherent};
     if ((e = hipMemsetAsync(sc.sort_ctl, 0, kSortCtlWords * 4, sp0)) != hipSuccess) return e;
+    if (admit && (e = hipMemsetAsync(sc.admit_rank, 0, (size_t)n * 4, sp0)) != hipSuccess) return e;
     mark("start");
     const uint32_t ntiles = std::max<uint32_t>(1, cdiv(n, kSortTile));
     const uint32_t tcap = (uint32_t)(sc.cap / kSortTile + 2);
     // source ids have log2(slots) bits: ceil(bits / 8) LSD passes of equal digits of at
     // most 8 bits (21 bits: 3 x 7 — fewer buckets, longer runs per tile than 8 + 8 + 5)
     uint32_t idbits = 0;
-    while ((1ull << idbits) <= lim.table_mask) ++idbits;
+    while ((1ull << idbits) <= idt.mask) ++idbits;
     int npass = std::max(1, (int)((idbits + 7) / 8));
     static const bool full_digits = getenv("FSX_SORT_FULL_DIGITS") != nullptr;   // A/B: 8,8,..,rest
     static const bool no_heavy = getenv("FSX_NO_HEAVY_SORT") != nullptr;          // A/B: plain LSD
@@ -2531,12 +2737,12 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
     // window's heavy verdict lists consume them apart from the light entries, so an even
     // count is taken with those lists only.
     static const bool no_hlists = getenv("FSX_NO_HEAVY_LISTS") != nullptr;
-    const bool lists_ok = do_limit && lim.limiter == 0 && verdict && !no_hlists;
+    const bool lists_ok = do_limit && lim.limiter == 0 && verdict && !no_hlists && !admit;
     const uint32_t bshift = std::max<uint32_t>(56, kIdShift + idbits);
     const uint32_t lbits = 63 - bshift;                 // light digit bits of the bucket
     const uint32_t hrest = idbits > lbits ? idbits - lbits : 0;
     const int hpass = 1 + (int)((hrest + 7) / 8);       // pass 0 + the light passes
-    const bool heavy_sort = !onesweep && !full_digits && !no_heavy && idbits <= 25 && npass >= 3 &&
+    const bool heavy_sort = !admit && !onesweep && !full_digits && !no_heavy && idbits <= 25 && npass >= 3 &&
                             (hpass == 3 || (hpass == 4 && lists_ok));
     if (heavy_sort) npass = hpass;   // (24-bit ids: 4 passes instead of 3, 3 of them over the light entries)
     // heavy verdict lists (fixed window with the heavy-source sort; FSX_NO_HEAVY_LISTS=1: A/B)
@@ -2680,6 +2886,7 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
     if (split) ta.sp = *split;
     ta.npass = npass; ta.tagh = tagh; ta.gridTiles = gridTiles;
     ta.hfm = hfm; ta.shift0 = dp.shift[0];
+    ta.admit = admit; ta.X = X; ta.id_gen = id_gen;
     ta.fork = flows && do_limit && st2 && fork_ev && join_ev && !no_fork;
     for (int k = 0; k < 3; ++k) ta.last[k] = last[k];
     if (split && split->tail_out) {

@@ -399,24 +399,38 @@ __global__ __launch_bounds__(128) void k_hflow_combine(const BatchState *bs, con
     x.has = 0;
     x.pad_[0] = x.pad_[1] = 0;
     const uint32_t t1 = min(ntiles, (g + 1) * kHGroupTiles);
-    for (uint32_t t = g * kHGroupTiles; t < t1; ++t) {
-        const uint32_t c = (t + 1 < ntiles ? row[t + 1] : end) - row[t];
-        if (c == 0) continue;
-        const HeavyTileRec &R = rec[t];
-        HFlowPart y;
-        y.a = acc_zero();
-        y.a.n = c;
-        y.a.s1 = R.s1[h];
-        y.a.s2 = R.s2[h];
-        y.a.d1 = R.t1[h] - R.t0[h];   // (consecutive gaps of a non-decreasing clock)
-        y.a.d2 = R.d2[h];
-        y.a.dmax = R.dmax[h];
-        y.t0 = R.t0[h];
-        y.t1 = R.t1[h];
-        y.fi = t * (uint32_t)kSortTile + R.fo[h];
-        y.has = 1;
-        y.pad_[0] = y.pad_[1] = 0;
-        hpart_merge(x, y);
+    // eight tiles' loads in flight at a time, merged in order
+    constexpr int kU = 8;
+    for (uint32_t tb = g * kHGroupTiles; tb < t1; tb += kU) {
+        uint32_t c[kU], s1[kU], dm[kU], fo[kU];
+        uint64_t s2[kU], a0[kU], a1[kU], d2[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const uint32_t t = tb + (uint32_t)u;
+            const uint32_t tc = t < t1 ? t : tb;
+            const HeavyTileRec &R = rec[tc];
+            c[u] = t < t1 ? (t + 1 < ntiles ? row[t + 1] : end) - row[t] : 0u;
+            s1[u] = R.s1[h]; dm[u] = R.dmax[h]; fo[u] = R.fo[h];
+            s2[u] = R.s2[h]; a0[u] = R.t0[h]; a1[u] = R.t1[h]; d2[u] = R.d2[h];
+        }
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            if (c[u] == 0) continue;
+            HFlowPart y;
+            y.a = acc_zero();
+            y.a.n = c[u];
+            y.a.s1 = s1[u];
+            y.a.s2 = s2[u];
+            y.a.d1 = a1[u] - a0[u];   // (consecutive gaps of a non-decreasing clock)
+            y.a.d2 = d2[u];
+            y.a.dmax = dm[u];
+            y.t0 = a0[u];
+            y.t1 = a1[u];
+            y.fi = (tb + (uint32_t)u) * (uint32_t)kSortTile + fo[u];
+            y.has = 1;
+            y.pad_[0] = y.pad_[1] = 0;
+            hpart_merge(x, y);
+        }
     }
     part[(size_t)g * kHeavyMax + h] = x;
 }
@@ -438,7 +452,17 @@ __global__ __launch_bounds__(128) void k_hflow_finish(const BatchState *bs, cons
     uint32_t r = 0;
     for (uint32_t j = 0; j < h; ++j) r += s_live[j];
     HFlowPart x = part[h];
-    for (uint32_t g = 1; g < ngroups; ++g) hpart_merge(x, part[(size_t)g * kHeavyMax + h]);
+    for (uint32_t g0 = 1; g0 < ngroups; g0 += 8) {   // eight groups' loads in flight
+        HFlowPart y[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const uint32_t g = g0 + (uint32_t)u;
+            y[u] = part[(size_t)(g < ngroups ? g : 0u) * kHeavyMax + h];
+            if (g >= ngroups) y[u].has = 0;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) hpart_merge(x, y[u]);
+    }
     const uint32_t row = bs->nseg_light + r;
     uint32_t k[4] = {hs->key[h][0], hs->key[h][1], hs->key[h][2], hs->key[h][3]};
     const uint32_t dport = dst_port(in.hdr + (size_t)x.fi * 64, len[x.fi]);

@@ -101,7 +101,8 @@ struct BatchState {
     // builds the heavy runs and the run-based kernels take over
     uint32_t hfast;
     uint32_t span_big;    // some sort tile spans >= 2^32 ns (u64 gap-square sums could wrap)
-    uint64_t ts0;         // timestamp of packet 0 (payload base of the parse-side payloads)
+    uint32_t n_admit;     // FSX_FLAG_OVERFLOW_ADMIT: sources admitted / transient this batch
+    uint32_t n_trans;
 };
 
 // Sorted payload word carried through the onesweep passes next to each sort word:
@@ -157,8 +158,12 @@ struct Limits {           // the rate-limiter constants, src/fsx_kern.c:245,308-
     uint64_t seed;
     uint32_t salt32;
     int32_t limiter;
-    uint32_t test_flags;  // FSX_FLAG_TEST_*: test hooks (include/fsx_hip.h)
+    uint32_t test_flags;  // fsx_config.flags (FSX_FLAG_TEST_* test hooks, policies)
+    // FSX_FLAG_OVERFLOW_ADMIT: the batch's sources get ids in the per-batch id table (this
+    // mask), their table slots come from the admission kernels
+    uint64_t admit_mask;
 };
+constexpr uint32_t kFlagAdmit = 8u;   // include/fsx_hip.h FSX_FLAG_OVERFLOW_ADMIT
 
 // ------------------------------------------------------------ hashing
 __host__ __device__ inline uint64_t mix64(uint64_t x) {
@@ -375,6 +380,10 @@ struct Scratch {
     uint32_t *chunk_cnt;
     void *hrec;
     void *hflow;           // tail: per (group of kHGroupTiles tiles, heavy source) flow sums
+    // FSX_FLAG_OVERFLOW_ADMIT: per arrival index, 1 at a new source's first packet, then its
+    // admission rank; per 4096 positions, their count / exclusive scan
+    uint32_t *admit_rank;
+    uint32_t *admit_cnt;
     uint64_t cap;          // packets the scratch is sized for
 };
 
@@ -393,7 +402,7 @@ struct HeavyTileRec {
     uint64_t t1[kHeavyMax];
     uint64_t d2[kHeavyMax];     // sum of squared gaps inside the tile
 };
-constexpr uint32_t kHGroupTiles = 256;   // tiles per k_hflow_combine group
+constexpr uint32_t kHGroupTiles = 64;    // tiles per k_hflow_combine group
 inline size_t heavy_rec_bytes(uint64_t cap) { return (cap / kSortTile + 2) * sizeof(HeavyTileRec); }
 inline size_t chunk_cnt_bytes(uint64_t cap) { return (cap / 1024 + 8) * 4; }
 
@@ -483,6 +492,9 @@ struct TailArgs {
     Limits lim;
     bool do_limit, has_flows, split, tagh, fork;
     bool hfm;             // heavy sources outside the sort (k_pass0h ran; k_hmode picks the path)
+    bool admit;           // FSX_FLAG_OVERFLOW_ADMIT (admission kernels after the heads)
+    TableIndex X;         // (admission: the persistent index)
+    uint32_t id_gen;      // (admission: the batch generation stamped on admitted slots)
     uint32_t shift0;      // pass 0's bucket shift (k_heavy_gather's sort words)
     FlowRequest fq;
     HistBufs hist;

@@ -48,6 +48,7 @@ BPF_ANY, BPF_NOEXIST, BPF_EXIST = 0, 1, 2
 FLAG_TEST_V6_COLLIDE = 1
 FLAG_ONESWEEP_SORT = 2
 FLAG_EVICT_IDLE = 4   # opt-in idle eviction on overflow
+FLAG_OVERFLOW_ADMIT = 8   # opt-in admission of a flood's new sources
 
 LIMIT_FIXED_WINDOW = 0
 LIMIT_SLIDING_WINDOW = 1
@@ -499,7 +500,7 @@ class FsxContext:
 
     BATCH_INFO = ("ip_packets", "sources", "new_sources", "any_ipv6", "non_monotone",
                   "max_len", "max_ts", "allowed", "dropped", "prefix_rule_drops", "sorted_payload",
-                  "light_packets", "evicted", "heavy_unsorted")
+                  "light_packets", "evicted", "heavy_unsorted", "admitted", "transient")
 
     def last_batch_info(self) -> dict:
         buf = (C.c_uint64 * len(self.BATCH_INFO))()

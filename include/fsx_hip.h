@@ -69,6 +69,21 @@ extern "C" {
  * the context (previous batches finish first) and is not undone if the batch then fails;
  * the number evicted is fsx_last_batch_info()[12]. Not with fsx_flows_begin. */
 #define FSX_FLAG_EVICT_IDLE 4u
+/* Opt-in overflow policy for floods beyond max_entries (any limiter; DESIGN.md §2.2,
+ * build-defined, parity unpinned like the reference's LRU_HASH maps of
+ * MAX_TRACK_IPS = 100000 entries, src/fsx_struct.h:7, src/fsx_kern.c:64-94). A source is
+ * tracked once it has map state (as for FSX_FLAG_EVICT_IDLE). Within a limiter batch, in
+ * arrival order, a source that is not tracked when its first packet reaches the per-source
+ * maps (after the prefix rules) is ADMITTED — tracked from then on, with the maps as usual —
+ * while fewer than max_entries sources are tracked; otherwise it is TRANSIENT for this
+ * batch: its packets are evaluated exactly like a new source's (fixed window: ip_stats
+ * {1, len, now} on its first packet, then src/fsx_kern.c:150-346; sliding window / token
+ * bucket: their specs), with state that lives for this batch only and is never visible in
+ * the maps. So every packet gets a verdict (stats_map counts them all) and a batch never
+ * fails with -ENOSPC for lack of table room. With FSX_FLAG_EVICT_IDLE the idle eviction
+ * runs first. Batches run unpipelined (mode 2) and the heavy-source sort is off; not with
+ * fsx_flows_begin. fsx_last_batch_info()[14] / [15]: sources admitted / transient. */
+#define FSX_FLAG_OVERFLOW_ADMIT 8u
 
 /* Map ids: the five maps of src/fsx_kern.c:56-94, then the token-bucket state maps of
  * the build-defined token bucket (value fsx_tb_state), then the
@@ -384,8 +399,8 @@ int fsx_pcap_records_device(fsx_ctx *ctx, const uint8_t *d_buf, const uint64_t *
  * they were gathered by index, [11] IP packets of non-heavy sources (the entries the
  * later sort passes covered), [12] sources evicted before the batch
  * (FSX_FLAG_EVICT_IDLE), [13] 1 when the heavy sources' verdicts and flow rows were
- * computed outside the sort, 0 on the run path. Returns the number of
- * entries written. */
+ * computed outside the sort, 0 on the run path, [14] / [15] sources admitted
+ * / transient (FSX_FLAG_OVERFLOW_ADMIT). Returns the number of entries written. */
 int fsx_last_batch_info(fsx_ctx *ctx, uint64_t *info, int cap);
 
 /* Per-kernel device timing for the benchmark: while enabled, every batch records a

@@ -189,6 +189,13 @@ typedef struct fsxo_config {
  * maps (after the prefix rules) or was written by a map update; map deletes do not
  * untrack it. */
 #define FSXO_EVICT_IDLE 4
+/* Opt-in overflow policy FSX_FLAG_OVERFLOW_ADMIT (include/fsx_hip.h, DESIGN.md §2.2;
+ * build-defined, parity unpinned): in arrival order, a source that is not tracked when its
+ * first packet of the batch reaches the per-source maps is admitted (tracked, the maps as
+ * usual) while fewer than max_entries sources are tracked, else it is transient for the
+ * batch: its packets run against maps of their own (c->tr) that start empty with the batch
+ * and are never visible; stats_map counts every verdict. */
+#define FSXO_OVERFLOW_ADMIT 8
 
 typedef struct ip_stats { uint64_t pps, bps, track_time; } ip_stats;  /* fsx_struct.h:17-22 */
 typedef struct tb_state { uint64_t tokens, last; } tb_state;
@@ -212,6 +219,9 @@ typedef struct fsxo_ctx {
     /* FSXO_EVICT_IDLE: tracked sources per family (key -> unused byte) */
     omap src[2];
     uint64_t evicted_last;
+    /* FSXO_OVERFLOW_ADMIT: the batch's transient sources' maps, and the batch's counts */
+    struct fsxo_ctx *tr;
+    uint64_t admitted_last, transient_last;
     sw_log *logs;
     size_t nlogs, caplogs;
 } fsxo_ctx;
@@ -245,7 +255,7 @@ fsxo_ctx *fsxo_open(const fsxo_config *cfg) {
     r |= omap_init(&c->swidx[1], me, 16, 8);
     r |= omap_init(&c->pfx[0], PREFIX_MAX_ENTRIES, 8, 8);
     r |= omap_init(&c->pfx[1], PREFIX_MAX_ENTRIES, 20, 8);
-    if (cfg->flags & FSXO_EVICT_IDLE) {
+    if (cfg->flags & (FSXO_EVICT_IDLE | FSXO_OVERFLOW_ADMIT)) {
         r |= omap_init(&c->src[0], me, 4, 1);
         r |= omap_init(&c->src[1], me, 16, 1);
     }
@@ -266,6 +276,7 @@ void fsxo_close(fsxo_ctx *c) {
     omap_free(&c->pfx[0]); omap_free(&c->pfx[1]);
     omap_free(&c->src[0]); omap_free(&c->src[1]);
     sw_free_logs(c);
+    if (c->tr) fsxo_close(c->tr);
     free(c);
 }
 
@@ -274,6 +285,7 @@ void fsxo_reset(fsxo_ctx *c) {
     omap_clear(&c->swidx[0]); omap_clear(&c->swidx[1]);
     if (c->src[0].used) { omap_clear(&c->src[0]); omap_clear(&c->src[1]); }
     c->evicted_last = 0;
+    c->admitted_last = c->transient_last = 0;
     sw_free_logs(c);   /* (the prefix blocklists stay: configuration, fsx_hip.h) */
     c->allowed = c->dropped = 0;
     c->err = 0;
@@ -283,9 +295,9 @@ int fsxo_error(const fsxo_ctx *c) { return c->err; }
 
 void fsxo_get_stats(const fsxo_ctx *c, uint64_t out[2]) { out[0] = c->allowed; out[1] = c->dropped; }
 
-/* FSXO_EVICT_IDLE: the source (family v6, key) is tracked from now on. */
+/* FSXO_EVICT_IDLE / FSXO_OVERFLOW_ADMIT: the source (family v6, key) is tracked from now on. */
 static void src_track(fsxo_ctx *c, int v6, const uint8_t *key) {
-    if (!(c->cfg.flags & FSXO_EVICT_IDLE)) return;
+    if (!(c->cfg.flags & (FSXO_EVICT_IDLE | FSXO_OVERFLOW_ADMIT))) return;
     static const uint8_t one = 1;
     if (omap_lookup(&c->src[v6], key)) return;
     /* one capacity for both families, as the device table's */
@@ -565,12 +577,32 @@ static int one_packet(fsxo_ctx *c, const uint8_t *hdr, uint32_t len, uint64_t ts
         c->dropped++;
         return XDP_DROP;
     }
-    src_track(c, v6, key);
-    switch (c->cfg.limiter) {
-    case 1: return sliding_window_packet(c, v6, key, len, ts);
-    case 2: return token_bucket_packet(c, v6, key, len, ts);
-    default: return fixed_window_packet(c, v6, key, len, ts);
+    fsxo_ctx *m = c;   /* the maps this packet runs against */
+    if ((c->cfg.flags & FSXO_OVERFLOW_ADMIT) && !omap_lookup(&c->src[v6], key)) {
+        if (c->src[0].count + c->src[1].count < c->cfg.max_entries) {
+            c->admitted_last++;                        /* admitted: tracked from now on */
+        } else {                                       /* transient for this batch */
+            m = c->tr;
+            if (!omap_lookup(&m->src[v6], key)) {
+                static const uint8_t one = 1;
+                if (omap_update(&m->src[v6], key, &one)) c->err = -ENOSPC;
+                c->transient_last++;
+            }
+        }
     }
+    if (m == c) src_track(c, v6, key);
+    int v;
+    switch (c->cfg.limiter) {
+    case 1: v = sliding_window_packet(m, v6, key, len, ts); break;
+    case 2: v = token_bucket_packet(m, v6, key, len, ts); break;
+    default: v = fixed_window_packet(m, v6, key, len, ts); break;
+    }
+    if (m != c) {   /* the transient maps' verdict counts go to stats_map */
+        c->allowed += m->allowed; c->dropped += m->dropped;
+        m->allowed = m->dropped = 0;
+        if (m->err) c->err = m->err;
+    }
+    return v;
 }
 
 /* FSXO_EVICT_IDLE, before a batch of n packets with smallest timestamp now0. */
@@ -606,6 +638,7 @@ static void evict_idle(fsxo_ctx *c, size_t n, uint64_t now0) {
 }
 
 uint64_t fsxo_evicted_last(const fsxo_ctx *c) { return c->evicted_last; }
+void fsxo_admit_last(const fsxo_ctx *c, uint64_t out[2]) { out[0] = c->admitted_last; out[1] = c->transient_last; }
 
 int fsxo_batch(fsxo_ctx *c, const uint8_t *hdr, const uint32_t *len, const uint64_t *ts,
                size_t n, uint8_t *verdict) {
@@ -613,6 +646,19 @@ int fsxo_batch(fsxo_ctx *c, const uint8_t *hdr, const uint32_t *len, const uint6
         uint64_t now0 = ts[0];
         for (size_t i = 1; i < n; ++i) now0 = ts[i] < now0 ? ts[i] : now0;
         evict_idle(c, n, now0);
+    }
+    if (c->cfg.flags & FSXO_OVERFLOW_ADMIT) {   /* fresh transient maps for this batch */
+        c->admitted_last = c->transient_last = 0;
+        if (c->tr && c->tr->cfg.max_entries < n) { fsxo_close(c->tr); c->tr = NULL; }
+        if (!c->tr) {
+            fsxo_config tc = c->cfg;
+            tc.flags = FSXO_OVERFLOW_ADMIT;   /* (its src maps: the batch's transient sources) */
+            tc.max_entries = n > 1024 ? n : 1024;
+            c->tr = fsxo_open(&tc);
+            if (!c->tr) return -ENOMEM;
+        } else {
+            fsxo_reset(c->tr);
+        }
     }
     for (size_t i = 0; i < n; ++i)
         verdict[i] = (uint8_t)one_packet(c, hdr + i * 64, len[i], ts[i]);
@@ -702,6 +748,7 @@ void fsxo_shards_close(fsxo_shards *h) {
 fsxo_shards *fsxo_shards_open(const fsxo_config *cfg, int nthreads) {
     if (nthreads < 1) nthreads = 1;
     if (nthreads > 256) nthreads = 256;
+    if (cfg->flags & FSXO_OVERFLOW_ADMIT) nthreads = 1;   /* admission follows the global arrival order */
     fsxo_shards *h = (fsxo_shards *)calloc(1, sizeof(*h));
     if (!h) return NULL;
     fsxo_config k = *cfg;

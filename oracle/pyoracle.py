@@ -27,6 +27,7 @@ class OConfig(C.Structure):
 
 
 EVICT_IDLE = 4   # fsxo_config.flags, = include/fsx_hip.h FSX_FLAG_EVICT_IDLE
+OVERFLOW_ADMIT = 8   # = include/fsx_hip.h FSX_FLAG_OVERFLOW_ADMIT
 
 
 class OQ8Model(C.Structure):
@@ -64,6 +65,7 @@ def lib() -> C.CDLL:
         "fsxo_get_stats": (None, [vp, vp]),
         "fsxo_batch": (C.c_int, [vp, vp, vp, vp, sz, vp]),
         "fsxo_evicted_last": (C.c_uint64, [vp]),
+        "fsxo_admit_last": (None, [vp, vp]),
         "fsxo_parse_batch": (None, [vp, vp, sz, vp, vp]),
         "fsxo_map_lookup": (C.c_int, [vp, C.c_int, vp, vp]),
         "fsxo_map_update": (C.c_int, [vp, C.c_int, vp, vp]),
@@ -139,6 +141,12 @@ class Oracle:
     def evicted_last(self) -> int:
         """Sources evicted before the last batch (flags=EVICT_IDLE)."""
         return int(lib().fsxo_evicted_last(self._h))
+
+    def admit_last(self) -> tuple[int, int]:
+        """Sources admitted / transient in the last batch (flags=OVERFLOW_ADMIT)."""
+        s = np.zeros(2, dtype=np.uint64)
+        lib().fsxo_admit_last(self._h, _p(s))
+        return int(s[0]), int(s[1])
 
     def reset(self):
         """fsx_reset's counterpart: per-source maps and stats cleared, prefix rules kept."""
