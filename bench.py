@@ -52,6 +52,9 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.
 KERNEL_BYTES = {
     # 64-B header record + len + ts in, verdict byte out (the sort word is implementation)
     "k_parse": {"unit": "packet", "algo": 77, "impl": 64 + 4 + 8 + 8 + 1},
+    # with the heavy sources outside the sort (k_pass0h in the split) k_parse reads no
+    # timestamps: 64-B record + len in, verdict byte out; k_pass0h reads ts + len + verdict
+    "k_parse/hfm": {"unit": "packet", "algo": 69, "impl": 64 + 4 + 1 + 8 * 0.47},
     "k_tile_scatter": {"unit": "ip_packet", "algo": 0, "impl": 33},
     "k_flow_features": {"unit": "ip_packet", "algo": 0, "impl": 8 + 4 + 8},
     "k_score": {"unit": "flow", "algo": 37, "impl": 37},
@@ -899,7 +902,9 @@ def main():
         dom = None
     if dom:
         name, ms_per_batch, launches = dom
-        kb = KERNEL_BYTES.get(name, {"unit": "packet", "algo": 0, "impl": 0})
+        hfm = any(r[0] == "k_pass0h" for r in timings)
+        kb = KERNEL_BYTES.get(name + ("/hfm" if hfm and name == "k_parse" else ""),
+                              {"unit": "packet", "algo": 0, "impl": 0})
         units = n if kb["unit"] == "packet" else info.get("ip_packets", n)
         per_launch_ms = ms_per_batch / max(launches, 1e-9)
         bytes_per_launch = kb["algo"] * units

@@ -2500,6 +2500,7 @@ hipError_t launch_tail(const TailArgs &a) {
     // the heavy runs' walker and flow sums, forked right after the sort (A/B, config 2: right
     // after pass 0 they slowed passes 1-2, after the heads they delayed the walkers; a fourth
     // stream shared a hardware queue with the limiter chain)
+    bool heavy_join = false;
     auto launch_heavy = [&]() -> hipError_t {
         hipError_t e;
         if (hs != st) {
@@ -2520,6 +2521,8 @@ hipError_t launch_tail(const TailArgs &a) {
                 return e;
             mark_on("k_walk_heavy_sel", hs_id);
         }
+        // (pipelined: the heavy walker beside the tail's chain; k_verdict_apply joins it)
+        if (heavy_join && (e = hipEventRecord(walk_join_ev, hs)) != hipSuccess) return e;
         if (flows) {
             if ((e = launch_flows_heavy(S_fin, pay_fin, ts, len, bs, sc.sort_ctl, sc.gbase, sc.heavy_flow,
                                         sc.cap, hf)) != hipSuccess)
@@ -2542,6 +2545,13 @@ hipError_t launch_tail(const TailArgs &a) {
         hs_id = 0;
         hf = fork ? st2 : st;
         hf_id = fork ? 1 : 0;
+        // unsorted heavy sources: their walker (select / rank searches, latency-bound on 32
+        // blocks) on the flow stream ahead of the heavy flow rows, not ahead of the heads
+        if (a.hfm && st2 && walk_join_ev) {
+            hs = st2;
+            hs_id = 1;
+            heavy_join = true;
+        }
     }
     // unsorted heavy sources that k_hmode sent back to the run path: their runs first
     if (a.hfm && (e = launch_heavy_gather(bs, verdict, ts, len, n, sc.hist, tcap, sc.heavy, a.shift0, lim.table_mask,
@@ -2653,6 +2663,7 @@ hipError_t launch_tail(const TailArgs &a) {
     k_fill_scatter<<<gridTiles, 256, 0, st>>>(sc.marks, S, bs, sc.tile_last, sc.drop_list, sc.drop_cur,
                                               tstate, cdiv(n, kVChunk), tagh ? 1u : 0u);
     mark("k_fill_scatter");
+    if (heavy_join && (e = hipStreamWaitEvent(st, walk_join_ev, 0)) != hipSuccess) return e;
     k_verdict_apply<<<cdiv(n, kVChunk), 256, 0, st>>>(verdict, n, sc.drop_list, sc.drop_cur, bs, sc.heavy,
                                                       hlists.list);
     mark("k_verdict_apply");

@@ -186,6 +186,15 @@ class Oracle:
         return {keys[i].tobytes(): (tuple(int(x) for x in vals[i]) if vw > 1 else int(vals[i, 0]))
                 for i in range(n)}
 
+    def map_arrays(self, map_id: int):
+        """(keys [n, klen] u8, values [n, words] u64) of one map, unordered."""
+        n = lib().fsxo_map_dump(self._h, map_id, None, None, 0)
+        keys = np.zeros((n, _klen(map_id)), dtype=np.uint8)
+        vals = np.zeros((n, _vw(map_id)), dtype=np.uint64)
+        if n:
+            lib().fsxo_map_dump(self._h, map_id, _p(keys), _p(vals), n)
+        return keys, vals
+
 
 def _klen(map_id: int) -> int:
     return 16 if map_id in (2, 4, 6) else 8 if map_id == 7 else 20 if map_id == 8 else 4
