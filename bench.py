@@ -380,7 +380,7 @@ def main():
 
     # ------------------------------------------------------------------ workload runner
     def run_workload(cfg_no, n, steps, warmup, with_flows, kernel_timing=False, check=False,
-                     cpu=False, stream=False, pipelined=True, distinct=1):
+                     cpu=False, stream=False, pipelined=True, distinct=1, limiter=None):
         """Weak-scaled config cfg_no (n packets per rank), full pipeline; returns a dict.
 
         stream=False (cold): every step is the same batch from empty maps (fsx_reset inside
@@ -412,7 +412,8 @@ def main():
         d = D[0]
         max_entries = max(1024, int(p.n_ips) if p.n_ips else n * world)
         lim_id = {"fixed": lib.LIMIT_FIXED_WINDOW, "sliding": lib.LIMIT_SLIDING_WINDOW,
-                  "token": lib.LIMIT_TOKEN_BUCKET}[args.limiter]
+                  "token": lib.LIMIT_TOKEN_BUCKET}[limiter or args.limiter]
+        state_maps = (3, 4, 5, 6) if lim_id == lib.LIMIT_TOKEN_BUCKET else (1, 2, 3, 4)
         ctx = lib.FsxContext(max_batch=n, max_entries=max_entries, device=local, limiter=lim_id)
         ctx.load_q8_model(model)
         fcap = max_entries
@@ -441,7 +442,9 @@ def main():
             if args.ts_ring:
                 R = min(R, max(6, args.ts_ring))
             def ts_of(k):   # batch k's timestamp base and shift
-                return D[k % nd]["ts"], (k // nd) * nd * dur + (k % nd) * 0
+                # (D[k % nd] was generated at j0 = (k % nd) * n of the nd-times-longer stream,
+                # so its timestamps already carry the (k % nd) x duration offset)
+                return D[k % nd]["ts"], (k // nd) * nd * dur
             tss = [ts_of(k)[0] + ts_of(k)[1] for k in range(min(R, total))]
             held = list(range(len(tss)))   # the batch each array currently holds
             # one verdict buffer per pipelined batch in flight (fsx_ctx::kSets = 3): a batch's
@@ -560,7 +563,7 @@ def main():
                 step(k, feat=k == nb - 1, v=vs[k])
             ctx.sync()
             from oracle import pyoracle
-            orc = pyoracle.ShardedOracle(cores, max_entries=max_entries)
+            orc = pyoracle.ShardedOracle(cores, max_entries=max_entries, limiter=lim_id)
             ok = True
             for k in range(nb):
                 if k < nd:   # batch k's records (the same bytes again once k >= nd)
@@ -574,7 +577,7 @@ def main():
             out["cpu"] = {"value": round(n / cdt / 1e6, 3), "unit": "Mpps", "seconds": round(cdt, 3)}
             if check:
                 chk = {"batches": nb, "packets": nb * n, "verdicts_equal": ok}
-                chk.update(compare_state(ctx, orc, (1, 2, 3, 4)))
+                chk.update(compare_state(ctx, orc, state_maps))
                 if with_flows:
                     chk["flows" if nb == 1 else "flows_last_batch"] = check_flows(
                         fl["keys"], fl["fam"], fl["feat"], fl["prob"], ctx.last_batch_info()["sources"],
@@ -603,38 +606,31 @@ def main():
     # ------------------------------------------------------------------ legs (N=1)
     d = head.pop("d")
     if world == 1 and "limiters" in legs:
+        # the build-defined limiters as the headline runs: the config's stream
+        # with the maps carried, batches pipelined (whole on the context stream: their
+        # walkers have no split tail), per-source features + q8 scores, checked against the
+        # oracle over three consecutive batches; roofline on SURVEY §8 d's bytes
         res = {}
-        for lname, lid, extra in (("sliding_window", lib.LIMIT_SLIDING_WINDOW, {}),
-                                  ("token_bucket", lib.LIMIT_TOKEN_BUCKET, {})):
-            with lib.FsxContext(max_batch=n, max_entries=head["max_entries"], device=local,
-                                limiter=lid, **extra) as lc:
-                def lstep():
-                    lc.reset()
-                    lc.verdict_batch_device(d["hdr"].data_ptr(), d["len"].data_ptr(), d["ts"].data_ptr(),
-                                            n, d["v"].data_ptr())
-                lstep()
-                lc.sync()
-                torch.cuda.synchronize()
-                l0 = time.perf_counter()
-                for _ in range(args.leg_steps):
-                    lstep()
-                lc.sync()
-                torch.cuda.synchronize()
-                lt = time.perf_counter() - l0
-                la, ld = lc.stats()
-                r = {"value": round(n * args.leg_steps / lt / 1e6, 2), "unit": "Mpps",
-                     "ms_per_step": round(lt / args.leg_steps * 1e3, 4), "steps": args.leg_steps,
-                     "allowed": la, "dropped": ld}
-                if not args.no_check:
-                    from oracle import pyoracle
-                    hdr, ln, ts = host_inputs(d, n)
-                    orc = pyoracle.ShardedOracle(cores, max_entries=head["max_entries"], limiter=lid)
-                    vo = orc.batch(hdr, ln, ts)
-                    r["check"] = {"packets": n, "verdicts_equal": bool(np.array_equal(d["v"].cpu().numpy(), vo))}
-                    r["check"].update(compare_state(lc, orc, (3, 4, 5, 6) if lid == 2 else (1, 2, 3, 4)))
-                    orc.close()
-                    del hdr, ln, ts
-                res[lname] = r
+        for lname, lkey in (("sliding_window", "sliding"), ("token_bucket", "token")):
+            r_ = run_workload(args.config, n, args.leg_steps * 2, 2, not args.no_mlp,
+                              check=not args.no_check, stream=True, pipelined=True, limiter=lkey,
+                              kernel_timing=args.leg_timing)
+            algo = PKT_ALGO_BYTES * n + SRC_ALGO_BYTES * (r_["sources"] or 0)
+            res[lname] = {"value": round(r_["mpps"], 2), "unit": "Mpps",
+                          "ms_per_step": round(r_["ms_step"], 4), "steps": r_["steps"],
+                          "allowed": r_["stats"][0], "dropped": r_["stats"][1], "sources": r_["sources"],
+                          "roofline": {"bound": "hbm", "bytes_per_step": algo,
+                                       "bytes_rule": "77 B per packet + 64 B per source (SURVEY §8 d)",
+                                       "achieved": round(algo / (r_["ms_step"] * 1e-3) / 1e9, 1),
+                                       "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                       "frac": round(algo / (r_["ms_step"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
+                          "check": r_.get("check"),
+                          "stream": "the headline's stream (maps carried), pipelined, features + q8 scores"}
+            if r_.get("timings"):
+                res[lname]["kernels"] = [{"name": a, "ms_per_step": round(b, 4), "launches": c}
+                                         for a, b, c in r_["timings"]]
+            del r_["d"], r_
+            torch.cuda.empty_cache()
         results["limiters"] = res
 
     if world == 1 and "rules" in legs:

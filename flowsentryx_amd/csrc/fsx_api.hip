@@ -68,6 +68,9 @@ struct fsx_ctx {
     Slot *evict_buf = nullptr;
     uint64_t evict_cap = 0;
     uint64_t last_evicted = 0;
+    // FSX_FLAG_EVICT_IDLE: an upper bound on the tracked sources (the last count read plus
+    // the packets of every batch since); ~0 = unknown (map imports, reset)
+    uint64_t count_bound = ~0ull;
     // sharding: per (owner, tile) counts of fsx_shard_pack_device, blocklist replica
     uint32_t *d_shard_cnt = nullptr;
     uint64_t shard_cnt_cap = 0;
@@ -189,7 +192,7 @@ static void free_scratch(fsx_ctx *c) {
     hipFree(s.packed[0]); hipFree(s.packed[1]); hipFree(s.pay[0]); hipFree(s.pay[1]); hipFree(s.marks); hipFree(s.headf);
     hipFree(s.seg_start); hipFree(s.seg_slot); hipFree(s.seg_lo); hipFree(s.seg_len); hipFree(s.hist);
     hipFree(s.tile_aux); hipFree(s.tile_last); hipFree(s.id_tab);
-    hipFree(s.seg_order); hipFree(s.sub_cnt); hipFree(s.flow_first); hipFree(s.flow_last);
+    hipFree(s.seg_order); hipFree(s.seg_cls); hipFree(s.sub_cnt); hipFree(s.flow_first); hipFree(s.flow_last);
     hipFree(s.span_list); hipFree(s.sort_ctl); hipFree(s.gbase); hipFree(s.status);
     hipFree(s.lim_tiles); hipFree(s.sw_seg); hipFree(s.sketch); hipFree(s.heavy);
     hipFree(s.drop_list); hipFree(s.drop_cur); hipFree(s.heavy_flow);
@@ -220,6 +223,7 @@ static int alloc_scratch(fsx_ctx *c, uint64_t cap) {
     // slots * 32 bytes, 16 GiB for a 2^28-source context that never needs it)
     c->id_gen = 0;
     HIPCHK(c, hipMalloc(&s.seg_order, (cap + 1) * 4));
+    HIPCHK(c, hipMalloc(&s.seg_cls, kSegClassWords * 4));
     HIPCHK(c, hipMalloc(&s.sub_cnt, (cap / 1024 + 8) * 4));
     HIPCHK(c, hipMalloc(&s.flow_first, (cap / 1024 + 8) * flow_acc_bytes()));
     HIPCHK(c, hipMalloc(&s.flow_last, (cap / 1024 + 8) * flow_acc_bytes()));
@@ -855,11 +859,18 @@ static int run_pipelined(fsx_ctx *c, const PacketIn &in, const uint32_t *d_len, 
 // timestamp leaves the maps. Synchronous: the previous batches finish first, and the
 // survivors move to new slots (open addressing drops no entry in place).
 static int evict_idle(fsx_ctx *c, const PacketIn &in, const uint64_t *d_ts, size_t n) {
+    c->last_evicted = 0;
+    // no synchronization while the bound says the batch fits: a batch adds at
+    // most n sources
+    if (c->count_bound <= c->cfg.max_entries && n <= c->cfg.max_entries - c->count_bound) {
+        c->count_bound += n;
+        return 0;
+    }
     int rc;
     if ((rc = sel(c)) || (rc = fsx_sync(c))) return rc;
-    c->last_evicted = 0;
     uint64_t count = 0;
     HIPCHK(c, hipMemcpy(&count, &c->tstate->count, 8, hipMemcpyDeviceToHost));
+    c->count_bound = count + n;
     if (count + n <= c->cfg.max_entries) return 0;
     if (c->flow_accum || c->d_slot_acc)
         return set_err(c, -EINVAL, "FSX_FLAG_EVICT_IDLE moves sources between slots: not with fsx_flows_begin");
@@ -887,6 +898,7 @@ static int evict_idle(fsx_ctx *c, const PacketIn &in, const uint64_t *d_ts, size
     e = launch_evict_reinsert(c->table, c->tstate, c->lim, table_index(c), c->evict_buf, m, c->stream);
     if (e != hipSuccess) return set_err(c, -EIO, "evict reinsert: %s", hipGetErrorString(e));
     c->last_evicted = count - m;
+    c->count_bound = m + n;
     return 0;
 }
 
@@ -1142,6 +1154,7 @@ static int map_op(fsx_ctx *c, int op, int map_id, const void *key, const void *v
         return 0;
     }
     if (prefix_map(map_id)) return prefix_op(c, op, map_id, key, value, out, flags);
+    if (op == 1) c->count_bound = ~0ull;
     uint32_t k[4];
     if ((rc = key_words(map_id, key, k))) return set_err(c, rc, "bad map id %d", map_id);
     if (flags > FSX_BPF_EXIST) return -EINVAL;
@@ -1205,6 +1218,7 @@ int fsx_map_update_batch(fsx_ctx *c, int map_id, const void *keys, const void *v
         return 0;
     }
     const size_t klen = map_v6(map_id) ? 16 : 4, vlen = map_vlen(map_id);
+    c->count_bound = ~0ull;
     uint32_t *dk = nullptr;
     uint64_t *dv = nullptr;
     HIPCHK(c, hipMalloc(&dk, n * klen));

@@ -1906,6 +1906,7 @@ __device__ __forceinline__ uint32_t seg_class(uint32_t L, uint32_t short_seg) {
 // chunks, one scan, then per-block LDS cursors (no contended global atomics; order
 // inside a class is irrelevant to the result).
 constexpr uint32_t kSegBlocks = 1024;
+static_assert(kSegClasses * kSegBlocks == kSegClassWords, "Scratch::seg_cls size");
 
 __device__ __forceinline__ void seg_chunk(uint32_t nseg, uint32_t b, uint32_t &lo, uint32_t &hi) {
     const uint32_t chunk = (nseg + kSegBlocks - 1) / kSegBlocks;
@@ -1978,43 +1979,6 @@ __global__ __launch_bounds__(256) void k_seg_order(const BatchState *bs,
     uint32_t lo, hi;
     seg_chunk(bs->nseg, blockIdx.x, lo, hi);
     seg_classes_pass<true>(seg_start, lo, hi, short_seg, cur, order);
-}
-
-// Heavy verdict lists: a heavy source's segment (the sorted positions from
-// n_light on, one run per heavy source) writes its verdict changes as an arrival-index list
-// over its own positions in hl instead of marks, and counts its PASS / DROP packets into
-// stats_map here (k_fill_* cover the light positions only).
-struct HeavyLists {
-    uint32_t *list;   // nullptr: every segment writes marks
-    HeavySet *hs;
-    TableState *tstate;
-    BatchState *bs;
-};
-
-template <bool kWave>
-__device__ __forceinline__ int heavy_list_open(const HeavyLists &H, const uint64_t *S, uint32_t a,
-                                               MarkWriter<kWave, true> &mw) {
-    mw.list = H.list + 2u * a;   // bytes [8a, 8a + 4 * entries): inside the run's own 8-byte positions
-    mw.S = S;
-    return (int)(S[a] >> 56) - (int)kHeavyMax;   // bucket = 128 + heavy index
-}
-
-template <bool kWave>
-__device__ __forceinline__ void heavy_list_close(const HeavyLists &H, int h, uint32_t a, uint32_t b,
-                                                 MarkWriter<kWave, true> &mw) {
-    mw.finish(b);
-    if (kWave && lane_id() != 0) return;
-    H.hs->lbase[h] = 2u * a;
-    H.hs->lcnt[h] = mw.nl;
-    unsigned long long *st = reinterpret_cast<unsigned long long *>(H.tstate->stats);
-    if (mw.npass) {
-        atomicAdd(st, (unsigned long long)mw.npass);
-        atomicAdd(reinterpret_cast<unsigned long long *>(&H.bs->allowed), (unsigned long long)mw.npass);
-    }
-    if (mw.ndrop) {
-        atomicAdd(st + 1, (unsigned long long)mw.ndrop);
-        atomicAdd(reinterpret_cast<unsigned long long *>(&H.bs->dropped), (unsigned long long)mw.ndrop);
-    }
 }
 
 template <class SV>
@@ -2120,7 +2084,7 @@ __device__ __forceinline__ void walk_heavy(const SV &sv, const BatchState *bs, c
     const bool fast = glob_fast && (!st.has_st || (st.tt <= ~0ull - lim.window &&
                                                    st.pps < kBig && st.bps < kBig));
     MarkWriter<true, true> mw{nullptr, 0};
-    heavy_list_open(H, sv.S, a, mw);
+    heavy_list_open(H, sv.S, a, mw);   // (h: this wave's heavy bucket)
     if (fast) walk_fixed_fast<true>(sv, a, b, lim, maxL, mw, st);
     else walk_fixed_exact_wave(sv, a, b, lim, mw, st);
     heavy_list_close(H, (int)h, a, b, mw);
@@ -2512,9 +2476,11 @@ hipError_t launch_tail(const TailArgs &a) {
                 mark_on(nullptr, hf_id);
             }
         }
-        k_walk_heavy<<<kHeavyMax / 4, 256, 0, hs>>>(S_fin, bs, sc.sort_ctl, sc.gbase, ts, len, pay_fin,
-                                                      table, lim, hlists);
-        mark_on("k_walk_heavy", hs_id);
+        if (lim.limiter == 0) {   // (the sliding window's heavy walker: launch_sliding_window)
+            k_walk_heavy<<<kHeavyMax / 4, 256, 0, hs>>>(S_fin, bs, sc.sort_ctl, sc.gbase, ts, len, pay_fin,
+                                                          table, lim, hlists);
+            mark_on("k_walk_heavy", hs_id);
+        }
         if (a.hfm) {   // (the path k_hmode picked runs; the other kernel returns at once)
             if ((e = launch_walk_heavy_sel(bs, sc.sort_ctl, sc.gbase, sc.hist, tcap, verdict, ts, len, n, sc.hrec,
                                            table, lim, sc.heavy, hlists.list, tstate, hs)) != hipSuccess)
@@ -2629,13 +2595,13 @@ hipError_t launch_tail(const TailArgs &a) {
     } else {
         uint32_t *cls = sc.sort_ctl + 1028;
         const uint32_t short_seg = lim.limiter == 1 ? kShortSegSliding : kShortSegFixed;
-        k_seg_count<<<kSegBlocks, 256, 0, st>>>(bs, sc.seg_start, sc.hist, short_seg);
-        k_seg_scan<<<1, 256, 0, st>>>(sc.hist, cls);
-        k_seg_order<<<kSegBlocks, 256, 0, st>>>(bs, sc.seg_start, sc.hist, sc.seg_order, short_seg);
+        k_seg_count<<<kSegBlocks, 256, 0, st>>>(bs, sc.seg_start, sc.seg_cls, short_seg);
+        k_seg_scan<<<1, 256, 0, st>>>(sc.seg_cls, cls);
+        k_seg_order<<<kSegBlocks, 256, 0, st>>>(bs, sc.seg_start, sc.seg_cls, sc.seg_order, short_seg);
         mark("k_seg_order");
         if (lim.limiter == 1) {   // FSX_LIMIT_SLIDING_WINDOW
             if ((e = launch_sliding_window(S, ts, len, bs, sc, table, tstate, hist, lim, n, st, mk, st3,
-                                           walk_fork_ev, walk_join_ev)) != hipSuccess)
+                                           walk_fork_ev, walk_join_ev, &hlists)) != hipSuccess)
                 return e;
         } else {
             // short and long segments are disjoint: the wave walker runs on its own
@@ -2746,9 +2712,11 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
     // [0, n_light)); with an even pass count the light entries end in the parse buffer, so
     // the heavy runs are read from pass 0's buffer (S_heavy in the tail): only the fixed
     // window's heavy verdict lists consume them apart from the light entries, so an even
-    // count is taken with those lists only.
+    // count is taken with those lists only. The sliding window's heavy lists (its history
+    // rebuild reads every segment from the final buffer) need an odd count.
     static const bool no_hlists = getenv("FSX_NO_HEAVY_LISTS") != nullptr;
-    const bool lists_ok = do_limit && lim.limiter == 0 && verdict && !no_hlists && !admit;
+    const bool lists_any = do_limit && verdict && !no_hlists && !admit;
+    const bool lists_ok = lists_any && lim.limiter == 0;
     const uint32_t bshift = std::max<uint32_t>(56, kIdShift + idbits);
     const uint32_t lbits = 63 - bshift;                 // light digit bits of the bucket
     const uint32_t hrest = idbits > lbits ? idbits - lbits : 0;
@@ -2756,15 +2724,16 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
     const bool heavy_sort = !admit && !onesweep && !full_digits && !no_heavy && idbits <= 25 && npass >= 3 &&
                             (hpass == 3 || (hpass == 4 && lists_ok));
     if (heavy_sort) npass = hpass;   // (24-bit ids: 4 passes instead of 3, 3 of them over the light entries)
-    // heavy verdict lists (fixed window with the heavy-source sort; FSX_NO_HEAVY_LISTS=1: A/B)
-    const bool tagh = heavy_sort && lists_ok;
+    // heavy verdict lists (fixed / sliding window with the heavy-source sort; FSX_NO_HEAVY_LISTS=1: A/B)
+    const bool lists_sw = lists_any && lim.limiter == 1 && (npass & 1);
+    const bool tagh = heavy_sort && (lists_ok || lists_sw);
     // heavy slots resolved once in k_heavy_pick (not under prefix rules; FSX_NO_HEAVY_SLOTS=1: A/B)
     static const bool no_hslots = getenv("FSX_NO_HEAVY_SLOTS") != nullptr;
     const uint32_t resolve = !no_hslots && !(do_limit && rules.slot) ? 1u : 0u;
     // heavy sources outside the sort (fsx_heavy.hip): header records with resolved heavy
     // slots; k_hmode picks the batch's path on the device (FSX_NO_HFAST=1: the runs, A/B)
     static const bool no_hfast = getenv("FSX_NO_HFAST") != nullptr;
-    const bool hfm = tagh && resolve && !in.rec && !no_hfast;
+    const bool hfm = tagh && lim.limiter == 0 && resolve && !in.rec && !no_hfast;
     if (!(split && split->tail) && (e = hipMemsetAsync(sc.marks, 0, n, st)) != hipSuccess) return e;
     DigitPlan dp{};
     dp.npass = (uint32_t)npass;

@@ -111,6 +111,7 @@ struct BatchState {
 constexpr uint32_t kPayLenBits = 24;
 constexpr uint32_t kSegClasses = 16;  // walker length classes (last: wave-walked segments)
 constexpr uint32_t kSortCtlWords = 1028 + 2 * kSegClasses;
+constexpr uint32_t kSegClassWords = kSegClasses * 1024;   // Scratch::seg_cls (kSegBlocks per class)
 constexpr uint64_t kPayTsRange = 1ull << (64 - kPayLenBits);
 
 // Persistent device scalars.
@@ -355,6 +356,9 @@ struct Scratch {
     uint32_t *tile_aux;    // per kTile tile
     uint8_t *tile_last;
     uint32_t *seg_order;   // segment ids grouped by length class (walker load balance)
+    // per-block length-class counts of k_seg_count / scan / order (their own buffer: the
+    // tail's heavy kernels read pass 0's scanned rows in hist beside them on another stream)
+    uint32_t *seg_cls;
     uint32_t *sub_cnt;     // heads per 1024-position flow tile
     void *flow_first;      // FlowAcc per flow tile (fsx_flows.hip)
     void *flow_last;
@@ -532,6 +536,7 @@ struct Marker {
     void operator()(const char *name) const { if (fn) fn(ctx, name); }
 };
 
+struct HeavyLists;
 hipError_t launch_token_bucket(const uint64_t *S, const uint64_t *ts, const uint32_t *len, BatchState *bs,
                                const Scratch &sc, Slot *table, const Limits &lim, uint32_t n,
                                hipStream_t st, const Marker &mark);
@@ -540,7 +545,8 @@ hipError_t launch_token_bucket(const uint64_t *S, const uint64_t *ts, const uint
 hipError_t launch_sliding_window(const uint64_t *S, const uint64_t *ts, const uint32_t *len, BatchState *bs,
                                  const Scratch &sc, Slot *table, TableState *tstate, const HistBufs &hb,
                                  const Limits &lim, uint32_t n, hipStream_t st, const Marker &mark,
-                                 hipStream_t st3, hipEvent_t fork_ev, hipEvent_t join_ev);
+                                 hipStream_t st3, hipEvent_t fork_ev, hipEvent_t join_ev,
+                                 const HeavyLists *H);   // (H->list: heavy verdict lists)
 
 hipError_t launch_pcap_records(const uint8_t *buf, const uint64_t *off, const uint32_t *caplen, uint32_t n,
                                uint8_t *hdr, hipStream_t st);

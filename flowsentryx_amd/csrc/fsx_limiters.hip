@@ -399,10 +399,10 @@ __device__ __forceinline__ void sw_hist_of(uint64_t aux, uint64_t &hoff, uint32_
 }
 
 // Exact sequential replay (any clock, u64 wraparound as the oracle).
-template <class SV>
+template <class SV, class MW>
 __device__ void sw_walk_exact(const SV &sv, uint32_t a, uint32_t b, const Limits &lim,
                               const uint64_t *ht, const uint32_t *hl, uint64_t hoff, uint32_t m,
-                              MarkWriter<false> &mw, SwState &s, SwSeg &rec) {
+                              MW &mw, SwState &s, SwSeg &rec) {
     uint32_t q = a;
     if (s.has_bl && s.till > 0) {                           // src/fsx_kern.c:189-215 semantics
         while (q < b && !(sv.t(q) > s.till)) { mw.emit(q, XDP_DROP); ++q; }
@@ -457,10 +457,10 @@ __device__ __forceinline__ uint32_t sw_log_start(const VV &vv, uint32_t f, uint3
 }
 
 // Monotone clocks, no byte trigger possible before the count trigger, no u64 overflow.
-template <class SV>
+template <class SV, class MW>
 __device__ void sw_walk_fast_wave(const SV &sv, uint32_t a, uint32_t b, const Limits &lim,
                                   const uint64_t *ht, const uint32_t *hl, uint64_t hoff, uint32_t m,
-                                  MarkWriter<true> &mw, SwState &s, SwSeg &rec) {
+                                  MW &mw, SwState &s, SwSeg &rec) {
     const uint32_t lane = lane_id();
     const uint64_t P = lim.pps, W = lim.window;
     uint32_t p = a;
@@ -602,12 +602,13 @@ __device__ __forceinline__ void sw_short_body(const SV &sv, const BatchState *bs
                                               const uint32_t *seg_slot, const uint32_t *order,
                                               const uint32_t *cls, uint8_t *marks, Slot *table,
                                               const Limits &lim, const uint64_t *ht, const uint32_t *hl,
-                                              SwSeg *segs) {
+                                              SwSeg *segs, bool lists) {
     const uint32_t nshort = bs->nseg - cls[kSegClasses - 1];
     const bool fast = sw_fast(bs, tst, lim);
     for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < nshort; i += gridDim.x * 256u) {
         const uint32_t g = order[i];
         const uint32_t a = seg_start[g], b = seg_start[g + 1];
+        if (lists && a >= bs->n_light) continue;   // a heavy source: k_walk_sw_heavy
         Slot &sl = table[seg_slot[g]];
         SwState st = sw_load(sl);
         uint64_t hoff;
@@ -627,13 +628,14 @@ __device__ __forceinline__ void sw_long_body(const SV &sv, const BatchState *bs,
                                              const uint32_t *seg_start, const uint32_t *seg_slot,
                                              const uint32_t *order, const uint32_t *cls, uint8_t *marks,
                                              Slot *table, const Limits &lim, const uint64_t *ht,
-                                             const uint32_t *hl, SwSeg *segs) {
+                                             const uint32_t *hl, SwSeg *segs, bool lists) {
     const uint32_t nl = cls[kSegClasses - 1], first = bs->nseg - nl;
     const bool fast = sw_fast(bs, tst, lim);
     const uint32_t lane = lane_id();
     for (uint32_t i = blockIdx.x * 4u + (threadIdx.x >> 6); i < nl; i += gridDim.x * 4u) {
         const uint32_t g = order[first + i];
         const uint32_t a = seg_start[g], b = seg_start[g + 1];
+        if (lists && a >= bs->n_light) continue;   // a heavy source: k_walk_sw_heavy
         Slot &sl = table[seg_slot[g]];
         SwState st = sw_load(sl);
         uint64_t hoff;
@@ -665,19 +667,74 @@ __global__ __launch_bounds__(256) void k_walk_sw(const uint64_t *__restrict__ S,
                                                  const uint32_t *__restrict__ order,
                                                  const uint32_t *__restrict__ cls,
                                                  uint8_t *__restrict__ marks, Slot *table, Limits lim,
-                                                 HistBufs hb, SwSeg *__restrict__ segs) {
+                                                 HistBufs hb, SwSeg *__restrict__ segs, uint32_t lists) {
     if (bs->err) return;
     const uint32_t cur = tst->hist_cur;
     const uint64_t *ht = hb.t[cur];
     const uint32_t *hl = hb.l[cur];
     if (bs->pay_ok) {
         const SegView<true> sv{S, ts, len, pay, ~bs->inv_min_ts};
-        if constexpr (kLong) sw_long_body(sv, bs, tst, seg_start, seg_slot, order, cls, marks, table, lim, ht, hl, segs);
-        else sw_short_body(sv, bs, tst, seg_start, seg_slot, order, cls, marks, table, lim, ht, hl, segs);
+        if constexpr (kLong) sw_long_body(sv, bs, tst, seg_start, seg_slot, order, cls, marks, table, lim, ht, hl, segs, lists != 0);
+        else sw_short_body(sv, bs, tst, seg_start, seg_slot, order, cls, marks, table, lim, ht, hl, segs, lists != 0);
     } else {
         const SegView<false> sv{S, ts, len, pay, 0};
-        if constexpr (kLong) sw_long_body(sv, bs, tst, seg_start, seg_slot, order, cls, marks, table, lim, ht, hl, segs);
-        else sw_short_body(sv, bs, tst, seg_start, seg_slot, order, cls, marks, table, lim, ht, hl, segs);
+        if constexpr (kLong) sw_long_body(sv, bs, tst, seg_start, seg_slot, order, cls, marks, table, lim, ht, hl, segs, lists != 0);
+        else sw_short_body(sv, bs, tst, seg_start, seg_slot, order, cls, marks, table, lim, ht, hl, segs, lists != 0);
+    }
+}
+
+// Heavy verdict lists (fixed window's scheme): one wave per heavy source, its
+// pass-0 run [base0, + cnt0) walked like a long segment, its verdict changes as the list
+// k_verdict_apply reads; its segment id (nseg_light + rank among the non-empty buckets, as
+// k_heads_heavy numbered them) keys its log record for the history rebuild.
+__global__ __launch_bounds__(256) void k_walk_sw_heavy(const uint64_t *__restrict__ S, BatchState *bs,
+                                                       const TableState *tst, const uint32_t *__restrict__ cnt0,
+                                                       const uint32_t *__restrict__ base0,
+                                                       const uint32_t *__restrict__ seg_slot,
+                                                       const uint64_t *__restrict__ ts,
+                                                       const uint32_t *__restrict__ len,
+                                                       const uint64_t *__restrict__ pay, Slot *table, Limits lim,
+                                                       HistBufs hb, SwSeg *__restrict__ segs, HeavyLists H) {
+    if (bs->err) return;
+    const uint32_t h = blockIdx.x * 4u + (threadIdx.x >> 6), lane = lane_id();
+    const uint32_t lb = bs->light_b;
+    const bool live0 = lane < kHeavyMax && cnt0[lb + lane] > 0;
+    const bool live1 = lane + 64u < kHeavyMax && cnt0[lb + 64u + lane] > 0;
+    const uint64_t m0 = __ballot(live0), m1 = __ballot(live1);
+    if (h >= H.hs->n) return;
+    const uint32_t c = cnt0[lb + h];
+    if (c == 0) return;
+    const uint32_t rk = h < 64 ? (uint32_t)__popcll(m0 & ((1ull << h) - 1ull))
+                               : (uint32_t)__popcll(m0) + (uint32_t)__popcll(m1 & ((1ull << (h - 64)) - 1ull));
+    const uint32_t g = bs->nseg_light + rk;
+    const uint32_t a = base0[lb + h], b = a + c;
+    const uint32_t cur = tst->hist_cur;
+    const uint64_t *ht = hb.t[cur];
+    const uint32_t *hl = hb.l[cur];
+    Slot &sl = table[seg_slot[g]];
+    SwState st = sw_load(sl);
+    uint64_t hoff;
+    uint32_t m;
+    sw_hist_of(sl.aux, hoff, m);
+    SwSeg rec{};
+    auto walk = [&](const auto &sv) {
+        if (sw_fast(bs, tst, lim)) {
+            MarkWriter<true, true> mw{nullptr, 0};
+            heavy_list_open(H, S, a, mw);
+            sw_walk_fast_wave(sv, a, b, lim, ht, hl, hoff, m, mw, st, rec);
+            heavy_list_close(H, (int)h, a, b, mw);
+        } else if (lane == 0) {
+            MarkWriter<false, true> mw{nullptr, 0};
+            heavy_list_open(H, S, a, mw);
+            sw_walk_exact(sv, a, b, lim, ht, hl, hoff, m, mw, st, rec);
+            heavy_list_close(H, (int)h, a, b, mw);
+        }
+    };
+    if (bs->pay_ok) walk(SegView<true>{S, ts, len, pay, ~bs->inv_min_ts});
+    else walk(SegView<false>{S, ts, len, pay, 0});
+    if (lane == 0) {
+        segs[g] = rec;
+        sw_store(sl, st, g);
     }
 }
 
@@ -847,8 +904,9 @@ __global__ void k_sw_finish(const BatchState *bs, TableState *tst, const uint64_
 hipError_t launch_sliding_window(const uint64_t *S, const uint64_t *ts, const uint32_t *len, BatchState *bs,
                                  const Scratch &sc, Slot *table, TableState *tstate, const HistBufs &hb,
                                  const Limits &lim, uint32_t n, hipStream_t st, const Marker &mark,
-                                 hipStream_t st3, hipEvent_t fork_ev, hipEvent_t join_ev) {
+                                 hipStream_t st3, hipEvent_t fork_ev, hipEvent_t join_ev, const HeavyLists *H) {
     (void)hipGetLastError();   // a stale error of another caller is not ours
+    const uint32_t lists = H && H->list ? 1u : 0u;
     const uint32_t gridSeg = std::min<uint32_t>(2048, std::max<uint32_t>(1, (n + 255) / 256));
     const uint32_t *cls = sc.sort_ctl + 1028;
     // short and long segments are disjoint (marks, slots, log records): the wave walker
@@ -859,12 +917,19 @@ hipError_t launch_sliding_window(const uint64_t *S, const uint64_t *ts, const ui
         if ((e = hipEventRecord(fork_ev, st)) != hipSuccess) return e;
         if ((e = hipStreamWaitEvent(st3, fork_ev, 0)) != hipSuccess) return e;
     }
-    k_walk_sw<true><<<1024, 256, 0, fork ? st3 : st>>>(S, bs, tstate, sc.seg_start, sc.seg_slot, ts, len,
-                                                       sc.pay[0], sc.seg_order, cls, sc.marks, table, lim, hb,
-                                                       sc.sw_seg);
+    // heavy verdict lists: the heavy sources' runs (pass 0's buffer, which with 3 passes is
+    // also the light entries' final one: S, pay[0]) first on the side stream, latency-bound
+    if (lists) {
+        k_walk_sw_heavy<<<kHeavyMax / 4, 256, 0, fork ? st3 : st>>>(S, bs, tstate, sc.sort_ctl, sc.gbase, sc.seg_slot,
+                                                                    ts, len, sc.pay[0], table, lim, hb, sc.sw_seg, *H);
+        mark("k_walk_sw_heavy");
+    }
+    k_walk_sw<true><<<1024, 256, 0, fork && !lists ? st3 : st>>>(S, bs, tstate, sc.seg_start, sc.seg_slot, ts, len,
+                                                                 sc.pay[0], sc.seg_order, cls, sc.marks, table, lim,
+                                                                 hb, sc.sw_seg, lists);
     if (fork && (e = hipEventRecord(join_ev, st3)) != hipSuccess) return e;
     k_walk_sw<false><<<gridSeg, 256, 0, st>>>(S, bs, tstate, sc.seg_start, sc.seg_slot, ts, len, sc.pay[0],
-                                              sc.seg_order, cls, sc.marks, table, lim, hb, sc.sw_seg);
+                                              sc.seg_order, cls, sc.marks, table, lim, hb, sc.sw_seg, lists);
     mark("k_walk_sw_short");
     if (fork && (e = hipStreamWaitEvent(st, join_ev, 0)) != hipSuccess) return e;
     mark("k_walk_sw_long_join");

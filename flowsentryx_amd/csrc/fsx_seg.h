@@ -234,4 +234,41 @@ struct MarkWriter {
     }
 };
 
+// Heavy verdict lists: a heavy source's segment (one run of sort pass 0, from
+// n_light on) writes its verdict changes as an arrival-index list over its own positions in
+// `list` instead of marks, and counts its PASS / DROP packets into stats_map here (k_fill_*
+// cover the light positions only). Shared by the fixed-window and sliding-window walkers.
+struct HeavyLists {
+    uint32_t *list;   // nullptr: every segment writes marks
+    HeavySet *hs;
+    TableState *tstate;
+    BatchState *bs;
+};
+
+template <bool kWave>
+__device__ __forceinline__ void heavy_list_open(const HeavyLists &H, const uint64_t *S, uint32_t a,
+                                                MarkWriter<kWave, true> &mw) {
+    mw.list = H.list + 2u * a;   // bytes [8a, 8a + 4 * entries): inside the run's own 8-byte positions
+    mw.S = S;
+}
+
+// heavy source h's list: its place and length for k_verdict_apply, its verdict counts
+template <bool kWave>
+__device__ __forceinline__ void heavy_list_close(const HeavyLists &H, int h, uint32_t a, uint32_t b,
+                                                 MarkWriter<kWave, true> &mw) {
+    mw.finish(b);
+    if (kWave && lane_id() != 0) return;
+    H.hs->lbase[h] = 2u * a;
+    H.hs->lcnt[h] = mw.nl;
+    unsigned long long *st = reinterpret_cast<unsigned long long *>(H.tstate->stats);
+    if (mw.npass) {
+        atomicAdd(st, (unsigned long long)mw.npass);
+        atomicAdd(reinterpret_cast<unsigned long long *>(&H.bs->allowed), (unsigned long long)mw.npass);
+    }
+    if (mw.ndrop) {
+        atomicAdd(st + 1, (unsigned long long)mw.ndrop);
+        atomicAdd(reinterpret_cast<unsigned long long *>(&H.bs->dropped), (unsigned long long)mw.ndrop);
+    }
+}
+
 }  // namespace fsx

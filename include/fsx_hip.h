@@ -65,8 +65,11 @@ extern "C" {
  * at the batch's smallest timestamp now0 leaves the maps first: its window has expired
  * (no ip_stats, or now0 - track_time > window_ns: the reset test of src/fsx_kern.c:245),
  * it holds no live blacklist entry (none, till 0 or now0 > till) and no token-bucket
- * state. The batch then runs as usual (-ENOSPC if it still overflows). The eviction syncs
- * the context (previous batches finish first) and is not undone if the batch then fails;
+ * state. The batch then runs as usual (-ENOSPC if it still overflows). The check reads the
+ * tracked count (a context sync: previous batches finish first) only when a host-side bound
+ * (the last count read plus the packets of every batch since) plus n could exceed
+ * max_entries, so pipelined batches far below capacity do not wait; an eviction is not
+ * undone if the batch then fails;
  * the number evicted is fsx_last_batch_info()[12]. Not with fsx_flows_begin. */
 #define FSX_FLAG_EVICT_IDLE 4u
 /* Opt-in overflow policy for floods beyond max_entries (any limiter; DESIGN.md §2.2,

@@ -153,3 +153,36 @@ def test_blacklisted_heavy_source_carried(native, oracle):
             c.map_update(3, k, v)
             o.map_update(3, k, v)
     _run(native, oracle, [(hdr, ln, ts)], CFG, prepare=prepare, want_path=[1])
+
+
+SW = dict(CFG, limiter=1)   # the sliding window's heavy verdict lists (3-pass sort: 21-bit ids)
+
+
+@pytest.mark.parametrize("case", ["slices", "non_monotone", "byte_trigger", "blacklisted", "pipelined"])
+def test_sliding_window_heavy_lists(native, oracle, case):
+    """The sliding window with heavy verdict lists: k_walk_sw_heavy walks each
+    heavy source's pass-0 run (epoch walker when clocks are monotone and the byte trigger
+    unreachable, the exact replay otherwise) and writes its log record for the history
+    rebuild; carried over the cut, verdicts / flows / stats / maps bit-exact."""
+    n = 1 << 21 if case in ("slices", "pipelined") else 1 << 20
+    hdr, ln, ts = _config2(oracle, n)
+    cfg, prepare = dict(SW), None
+    if case == "non_monotone":
+        ts = ts.copy()
+        ts[500_000], ts[500_001] = ts[500_001], ts[500_000] - 7
+    elif case == "byte_trigger":
+        cfg.update(bps_threshold=300_000)
+    elif case == "blacklisted":
+        src, cnt = np.unique(hdr[:, 26:30].copy().view(np.uint32).reshape(-1), return_counts=True)
+        order = np.argsort(-cnt)
+        a, b = (int(src[order[i]]).to_bytes(4, "little") for i in (0, 3))
+        mid = int(ts[len(ts) // 2])
+
+        def prepare(c, o):
+            for k, v in ((a, mid), (b, 2**64 - 1)):
+                c.map_update(3, k, v)
+                o.map_update(3, k, v)
+    k = 3 if case == "pipelined" else 2
+    cuts = [i * n // k for i in range(k + 1)]
+    _run(native, oracle, [(hdr[x:y], ln[x:y], ts[x:y]) for x, y in zip(cuts[:-1], cuts[1:])], cfg,
+         prepare=prepare, want_path=[0] * k, pipeline=case == "pipelined")
