@@ -72,6 +72,9 @@ struct IdTable {
     uint32_t coherent;          // first probe with an agent-scope load (A/B: FSX_ID_COHERENT)
     void *mir = nullptr;        // persistent index: IPv4 mirror (mir_entry), null when off
     uint32_t mir_shift = 0;     // log2(slots)
+    // 0: a new source's Slot is left to its walker (the fixed window's k_parse: one random
+    // line per insert, the head's; SlotKeys)
+    uint32_t init = 1;
 };
 
 __device__ __forceinline__ uint64_t id_start(const IdTable &T, uint32_t tag, const uint32_t k[4]) {
@@ -95,7 +98,7 @@ __device__ __forceinline__ uint32_t id_resolve(const IdTable &T, uint32_t tag, c
                 const uint64_t prev = atomicCAS(hp, (unsigned long long)cur, (unsigned long long)want);
                 if (prev == cur) {
                     *fresh = true;
-                    if (T.slots) {   // a new source of the persistent index: its map state
+                    if (T.slots && T.init) {   // a new source of the persistent index: its map state
                         Slot &sl = T.slots[h];
                         sl.flags = T.born << kBornShift;
                         sl.key[0] = k[0]; sl.key[1] = k[1]; sl.key[2] = k[2]; sl.key[3] = k[3];
@@ -479,7 +482,7 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
     // kHf (unsorted heavy sources): no timestamp loads (k_pass0h reads them),
     // no sort word for a heavy source's packet (its verdict byte carries 0x80 | h), the light
     // sort words compacted per 1024-packet chunk (wave) with their count in chunk_cnt
-    static_assert(!kHf || (kRec == 0 && !kRules), "unsorted heavy sources: header records, no rules");
+    static_assert(!kHf || !kRules, "unsorted heavy sources: no prefix rules");
     __shared__ uint32_t s_rec[4][64 * 17];
     __shared__ uint32_t s_red[4][3];
     __shared__ unsigned long long s_ts[4], s_its[4];
@@ -1986,17 +1989,20 @@ __device__ __forceinline__ void walk_short(const SV &sv, const BatchState *bs,
                                            const uint32_t *seg_start, const uint32_t *seg_slot,
                                            const uint32_t *order, const uint32_t *cls,
                                            uint8_t *marks, Slot *table, const Limits &lim,
-                                           const HeavyLists &H) {
+                                           const HeavyLists &H, const SlotKeys &K) {
     const uint32_t nshort = bs->nseg - cls[kSegClasses - 1];
     for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < nshort; i += gridDim.x * 256u) {
         const uint32_t g = order[i];
         const uint32_t a = seg_start[g], b = seg_start[g + 1];
         if (H.list && a >= bs->n_light) continue;   // a heavy source: k_walk_heavy
-        Slot &sl = table[seg_slot[g]];
+        const uint32_t si = seg_slot[g];
+        Slot &sl = table[si];
         FwState st = load_state(sl);
+        const bool fresh = K.heads && sl.tag == 0;
         MarkWriter<false> mw{marks, 0};
         walk_fixed_exact_thread(sv, a, b, lim, mw, st);
         store_state(sl, st);
+        if (fresh) slot_adopt(sl, K, si);
     }
 }
 
@@ -2009,14 +2015,14 @@ __global__ __launch_bounds__(256) void k_walk_fixed(const uint64_t *__restrict__
                                                     const uint32_t *__restrict__ order,
                                                     const uint32_t *__restrict__ cls,
                                                     uint8_t *__restrict__ marks, Slot *table,
-                                                    Limits lim, HeavyLists H) {
+                                                    Limits lim, HeavyLists H, SlotKeys K) {
     if (bs->err) return;
     if (bs->pay_ok) {
         const SegView<true> sv{S, ts, len, pay, ~bs->inv_min_ts};
-        walk_short(sv, bs, seg_start, seg_slot, order, cls, marks, table, lim, H);
+        walk_short(sv, bs, seg_start, seg_slot, order, cls, marks, table, lim, H, K);
     } else {
         const SegView<false> sv{S, ts, len, pay, 0};
-        walk_short(sv, bs, seg_start, seg_slot, order, cls, marks, table, lim, H);
+        walk_short(sv, bs, seg_start, seg_slot, order, cls, marks, table, lim, H, K);
     }
 }
 
@@ -2025,7 +2031,7 @@ __device__ __forceinline__ void walk_long(const SV &sv, const BatchState *bs,
                                           const uint32_t *seg_start, const uint32_t *seg_slot,
                                           const uint32_t *order, const uint32_t *cls,
                                           uint8_t *marks, Slot *table, const Limits &lim,
-                                          const HeavyLists &H) {
+                                          const HeavyLists &H, const SlotKeys &K) {
     const uint32_t nl = cls[kSegClasses - 1], first = bs->nseg - nl;
     const bool glob_fast = fast_ok(bs, lim);
     const uint32_t maxL = bs->max_len;
@@ -2034,14 +2040,19 @@ __device__ __forceinline__ void walk_long(const SV &sv, const BatchState *bs,
         const uint32_t g = order[first + i];
         const uint32_t a = seg_start[g], b = seg_start[g + 1];
         if (H.list && a >= bs->n_light) continue;   // a heavy source: k_walk_heavy
-        Slot &sl = table[seg_slot[g]];
+        const uint32_t si = seg_slot[g];
+        Slot &sl = table[si];
         FwState st = load_state(sl);
+        const bool fresh = K.heads && sl.tag == 0;
         const bool fast = glob_fast && (!st.has_st || (st.tt <= ~0ull - lim.window &&
                                                        st.pps < kBig && st.bps < kBig));
         MarkWriter<true> mw{marks, 0};
         if (fast) walk_fixed_fast<true>(sv, a, b, lim, maxL, mw, st);
         else walk_fixed_exact_wave(sv, a, b, lim, mw, st);
-        if (lane_id() == 0) store_state(sl, st);
+        if (lane_id() == 0) {
+            store_state(sl, st);
+            if (fresh) slot_adopt(sl, K, si);
+        }
     }
 }
 
@@ -2055,14 +2066,14 @@ __global__ __launch_bounds__(256) void k_walk_fixed_long(const uint64_t *__restr
                                                          const uint32_t *__restrict__ order,
                                                          const uint32_t *__restrict__ cls,
                                                          uint8_t *__restrict__ marks, Slot *table,
-                                                         Limits lim, HeavyLists H) {
+                                                         Limits lim, HeavyLists H, SlotKeys K) {
     if (bs->err) return;
     if (bs->pay_ok) {
         const SegView<true> sv{S, ts, len, pay, ~bs->inv_min_ts};
-        walk_long(sv, bs, seg_start, seg_slot, order, cls, marks, table, lim, H);
+        walk_long(sv, bs, seg_start, seg_slot, order, cls, marks, table, lim, H, K);
     } else {
         const SegView<false> sv{S, ts, len, pay, 0};
-        walk_long(sv, bs, seg_start, seg_slot, order, cls, marks, table, lim, H);
+        walk_long(sv, bs, seg_start, seg_slot, order, cls, marks, table, lim, H, K);
     }
 }
 
@@ -2071,7 +2082,7 @@ __global__ __launch_bounds__(256) void k_walk_fixed_long(const uint64_t *__restr
 template <class SV>
 __device__ __forceinline__ void walk_heavy(const SV &sv, const BatchState *bs, const uint32_t *cnt0,
                                            const uint32_t *base0, Slot *table, const Limits &lim,
-                                           const HeavyLists &H) {
+                                           const HeavyLists &H, const SlotKeys &K) {
     const bool glob_fast = fast_ok(bs, lim);
     const uint32_t maxL = bs->max_len;
     const uint32_t h = blockIdx.x * 4u + (threadIdx.x >> 6);
@@ -2079,8 +2090,11 @@ __device__ __forceinline__ void walk_heavy(const SV &sv, const BatchState *bs, c
     const uint32_t c = cnt0[bs->light_b + h];
     if (c == 0) return;
     const uint32_t a = base0[bs->light_b + h], b = a + c;
-    Slot &sl = table[pk_id(sv.S[a], lim.table_mask)];
+    const uint32_t si = pk_id(sv.S[a], lim.table_mask);
+    Slot &sl = table[si];
     FwState st = load_state(sl);
+    // (unresolved heavy sources, under prefix rules, are inserted by k_parse: lazily)
+    const bool fresh = K.heads && sl.tag == 0;
     const bool fast = glob_fast && (!st.has_st || (st.tt <= ~0ull - lim.window &&
                                                    st.pps < kBig && st.bps < kBig));
     MarkWriter<true, true> mw{nullptr, 0};
@@ -2088,7 +2102,10 @@ __device__ __forceinline__ void walk_heavy(const SV &sv, const BatchState *bs, c
     if (fast) walk_fixed_fast<true>(sv, a, b, lim, maxL, mw, st);
     else walk_fixed_exact_wave(sv, a, b, lim, mw, st);
     heavy_list_close(H, (int)h, a, b, mw);
-    if (lane_id() == 0) store_state(sl, st);
+    if (lane_id() == 0) {
+        store_state(sl, st);
+        if (fresh) slot_adopt(sl, K, si);
+    }
 }
 
 __global__ __launch_bounds__(256) void k_walk_heavy(const uint64_t *__restrict__ S, BatchState *bs,
@@ -2097,14 +2114,14 @@ __global__ __launch_bounds__(256) void k_walk_heavy(const uint64_t *__restrict__
                                                     const uint64_t *__restrict__ ts,
                                                     const uint32_t *__restrict__ len,
                                                     const uint64_t *__restrict__ pay, Slot *table,
-                                                    Limits lim, HeavyLists H) {
+                                                    Limits lim, HeavyLists H, SlotKeys K) {
     if (bs->err || bs->hfast) return;   // (hfast: k_walk_heavy_sel)
     if (bs->pay_ok) {
         const SegView<true> sv{S, ts, len, pay, ~bs->inv_min_ts};
-        walk_heavy(sv, bs, cnt0, base0, table, lim, H);
+        walk_heavy(sv, bs, cnt0, base0, table, lim, H, K);
     } else {
         const SegView<false> sv{S, ts, len, pay, 0};
-        walk_heavy(sv, bs, cnt0, base0, table, lim, H);
+        walk_heavy(sv, bs, cnt0, base0, table, lim, H, K);
     }
 }
 
@@ -2461,6 +2478,8 @@ hipError_t launch_tail(const TailArgs &a) {
     // writes after pass 0 read it)
     const HeavyLists hlists{tagh ? reinterpret_cast<uint32_t *>(sc.packed[0]) : nullptr, sc.heavy,
                             tstate, bs};
+    // (lazy slots: the fixed window's walkers write a new source's family and key)
+    const SlotKeys skeys{a.lazy ? a.X.heads : nullptr, a.X.k6};
     // the heavy runs' walker and flow sums, forked right after the sort (A/B, config 2: right
     // after pass 0 they slowed passes 1-2, after the heads they delayed the walkers; a fourth
     // stream shared a hardware queue with the limiter chain)
@@ -2478,7 +2497,7 @@ hipError_t launch_tail(const TailArgs &a) {
         }
         if (lim.limiter == 0) {   // (the sliding window's heavy walker: launch_sliding_window)
             k_walk_heavy<<<kHeavyMax / 4, 256, 0, hs>>>(S_fin, bs, sc.sort_ctl, sc.gbase, ts, len, pay_fin,
-                                                          table, lim, hlists);
+                                                          table, lim, hlists, skeys);
             mark_on("k_walk_heavy", hs_id);
         }
         if (a.hfm) {   // (the path k_hmode picked runs; the other kernel returns at once)
@@ -2614,11 +2633,11 @@ hipError_t launch_tail(const TailArgs &a) {
             }
             k_walk_fixed_long<<<FSX_WALK_LONG_BLOCKS, 256, 0, fork3 ? st3 : st>>>(S, bs, sc.seg_start, sc.seg_slot, ts, len,
                                                                   sc.pay[0], sc.seg_order, cls, sc.marks,
-                                                                  table, lim, hlists);
+                                                                  table, lim, hlists, skeys);
             mark_on("k_walk_fixed_long", fork3 ? 2 : 0);
             if (fork3 && (e = hipEventRecord(walk_join_ev, st3)) != hipSuccess) return e;
             k_walk_fixed<<<std::min<uint32_t>(FSX_WALK_SHORT_BLOCKS, cdiv(n, 256)), 256, 0, st>>>(S, bs, sc.seg_start, sc.seg_slot, ts, len, sc.pay[0],
-                                                     sc.seg_order, cls, sc.marks, table, lim, hlists);
+                                                     sc.seg_order, cls, sc.marks, table, lim, hlists, skeys);
             mark("k_walk_fixed");
             if (fork3 && (e = hipStreamWaitEvent(st, walk_join_ev, 0)) != hipSuccess) return e;
         }
@@ -2733,7 +2752,8 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
     // heavy sources outside the sort (fsx_heavy.hip): header records with resolved heavy
     // slots; k_hmode picks the batch's path on the device (FSX_NO_HFAST=1: the runs, A/B)
     static const bool no_hfast = getenv("FSX_NO_HFAST") != nullptr;
-    const bool hfm = tagh && lim.limiter == 0 && resolve && !in.rec && !no_hfast;
+    // (record mode too: the records' len / ts go to in.rec_len / rec_ts, which k_pass0h reads)
+    const bool hfm = tagh && lim.limiter == 0 && resolve && !no_hfast;
     if (!(split && split->tail) && (e = hipMemsetAsync(sc.marks, 0, n, st)) != hipSuccess) return e;
     DigitPlan dp{};
     dp.npass = (uint32_t)npass;
@@ -2763,6 +2783,14 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
         if ((e = hipEventRecord(split->pro_done, sp0)) != hipSuccess) return e;
         if ((e = hipStreamWaitEvent(st, split->pro_done, 0)) != hipSuccess) return e;
     }
+    // Lazy slots (fixed window): k_parse claims a new source's index head only; the walker
+    // that first stores its state writes the rest (one random line per insert instead of
+    // two: the head's and the slot's; FSX_EAGER_SLOTS=1: A/B). The heavy pick, the other
+    // limiters and the admission path initialise slots as they insert.
+    static const bool eager = getenv("FSX_EAGER_SLOTS") != nullptr;
+    const bool lazy = do_limit && !admit && lim.limiter == 0 && !eager;
+    IdTable pidt = idt;
+    if (lazy) pidt.init = 0;
     {
         const uint32_t g = std::min<uint32_t>(256u * FSX_PARSE_MINB, ntiles);   // one resident block per slot
         const HeavySet *hs = heavy_sort ? sc.heavy : nullptr;
@@ -2771,12 +2799,12 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
         // rule-free parse keeps its registers)
         const bool rl = do_limit && rules.slot;
         // (kMir: light IPv4 sources probe the persistent index's mirror, not its heads)
-#define FSX_PARSE(R, Q, H) (idt.mir ? k_parse<R, Q, true, H><<<g, 256, 0, st>>>(in, len, ts, n, sc.packed[0], verdict, bs, idt, \
+#define FSX_PARSE(R, Q, H) (idt.mir ? k_parse<R, Q, true, H><<<g, 256, 0, st>>>(in, len, ts, n, sc.packed[0], verdict, bs, pidt, \
                                                         sc.sort_ctl, th, tcap, dp, hs, rules, tagh ? 1u : 0u, sc.chunk_cnt) \
-                                 : k_parse<R, Q, false, H><<<g, 256, 0, st>>>(in, len, ts, n, sc.packed[0], verdict, bs, idt, \
+                                 : k_parse<R, Q, false, H><<<g, 256, 0, st>>>(in, len, ts, n, sc.packed[0], verdict, bs, pidt, \
                                                         sc.sort_ctl, th, tcap, dp, hs, rules, tagh ? 1u : 0u, sc.chunk_cnt))
         if (hfm)
-            FSX_PARSE(0, false, true);
+            !in.rec ? FSX_PARSE(0, false, true) : in.rec_bytes == 16 ? FSX_PARSE(16, false, true) : FSX_PARSE(32, false, true);
         else if (!in.rec)
             rl ? FSX_PARSE(0, true, false) : FSX_PARSE(0, false, false);
         else if (in.rec_bytes == 16)
@@ -2866,7 +2894,7 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
     if (split) ta.sp = *split;
     ta.npass = npass; ta.tagh = tagh; ta.gridTiles = gridTiles;
     ta.hfm = hfm; ta.shift0 = dp.shift[0];
-    ta.admit = admit; ta.X = X; ta.id_gen = id_gen;
+    ta.admit = admit; ta.X = X; ta.id_gen = id_gen; ta.lazy = lazy;
     ta.fork = flows && do_limit && st2 && fork_ev && join_ev && !no_fork;
     for (int k = 0; k < 3; ++k) ta.last[k] = last[k];
     if (split && split->tail_out) {

@@ -465,7 +465,14 @@ __global__ __launch_bounds__(128) void k_hflow_finish(const BatchState *bs, cons
     }
     const uint32_t row = bs->nseg_light + r;
     uint32_t k[4] = {hs->key[h][0], hs->key[h][1], hs->key[h][2], hs->key[h][3]};
-    const uint32_t dport = dst_port(in.hdr + (size_t)x.fi * 64, len[x.fi]);
+    uint32_t dport;
+    if (in.rec) {   // record mode: the port travels in the exchange record
+        uint32_t kr[4], L;
+        uint64_t T;
+        rec_read(in.rec, in.rec_bytes, x.fi, kr, L, T, dport);
+    } else {
+        dport = dst_port(in.hdr + (size_t)x.fi * 64, len[x.fi]);
+    }
     flow_emit(row, x.a, hs->tag[h], k, dport, x.t0, x.t1, hs->slot[h], out, P);
 }
 

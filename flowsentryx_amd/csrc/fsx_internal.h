@@ -499,6 +499,7 @@ struct TailArgs {
     bool admit;           // FSX_FLAG_OVERFLOW_ADMIT (admission kernels after the heads)
     TableIndex X;         // (admission: the persistent index)
     uint32_t id_gen;      // (admission: the batch generation stamped on admitted slots)
+    bool lazy;            // k_parse left new sources' slots to the fixed window's walkers
     uint32_t shift0;      // pass 0's bucket shift (k_heavy_gather's sort words)
     FlowRequest fq;
     HistBufs hist;

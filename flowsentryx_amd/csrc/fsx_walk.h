@@ -144,6 +144,27 @@ __device__ __forceinline__ FwState load_state(const Slot &sl) {
     return FwState{(sl.flags & SLOT_HAS_ST) != 0, (sl.flags & SLOT_HAS_BL) != 0, sl.pps, sl.bps,
                    sl.tt, sl.till};
 }
+// A new source's Slot under lazy initialisation (IdTable::init = 0, the fixed window): k_parse
+// claimed only its index head, so the walker that first stores its state also writes its
+// family and key, from the head (IPv4 key word) and the IPv6 key words (agent-scope loads:
+// the index lines may sit in another XCD's L2). heads null: k_parse initialised every slot.
+struct SlotKeys {
+    const unsigned long long *heads;
+    const uint32_t *k6;
+};
+
+__device__ __forceinline__ void slot_adopt(Slot &sl, const SlotKeys &K, uint32_t i) {
+    const unsigned long long h = __hip_atomic_load(K.heads + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t tag = (uint32_t)(h >> 32) & 0xFFu;
+    sl.key[0] = (uint32_t)h;
+    if (tag == 2) {
+        sl.key[1] = __hip_atomic_load(K.k6 + (size_t)i * 4 + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        sl.key[2] = __hip_atomic_load(K.k6 + (size_t)i * 4 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        sl.key[3] = __hip_atomic_load(K.k6 + (size_t)i * 4 + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    sl.tag = tag;
+}
+
 __device__ __forceinline__ void store_state(Slot &sl, const FwState &s) {
     // (also clears the born stamp: the batch that inserted the slot got this far)
     sl.flags = (sl.flags & kFlagBits & ~(SLOT_HAS_ST | SLOT_HAS_BL)) | (s.has_st ? SLOT_HAS_ST : 0u) |

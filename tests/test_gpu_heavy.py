@@ -186,3 +186,63 @@ def test_sliding_window_heavy_lists(native, oracle, case):
     cuts = [i * n // k for i in range(k + 1)]
     _run(native, oracle, [(hdr[x:y], ln[x:y], ts[x:y]) for x, y in zip(cuts[:-1], cuts[1:])], cfg,
          prepare=prepare, want_path=[0] * k, pipeline=case == "pipelined")
+
+
+def test_unsorted_heavy_path_record_mode(native, oracle):
+    """The owner side of the sharded path (record mode: 16-byte exchange records read
+    directly, their len / ts in context scratch) on the unsorted heavy path: two carried
+    config-2 slices through fsx_process_records_device, verdicts / flow rows / stats / maps
+    equal to the oracle on the original header records."""
+    import torch
+    from flowsentryx_amd import fsx_load
+    from flowsentryx_amd.shard import HipShardEngine
+    from oracle import pyoracle
+    ref = json.loads((GOLDEN / "model_weights.json").read_text())
+    n = 1 << 21
+    hdr, ln, ts = _config2(oracle, n)
+    dev = torch.device("cuda", 0)
+    th = torch.from_numpy(hdr.reshape(-1).copy()).to(dev)
+    tl = torch.from_numpy(ln.view(np.int32).copy()).to(dev)
+    tt = torch.from_numpy(ts.view(np.int64).copy()).to(dev)
+    tv = torch.zeros(n, dtype=torch.uint8, device=dev)
+    o = oracle.Oracle(**CFG)
+    cut = n // 2
+    with native.FsxContext(max_batch=n, **CFG) as c:
+        c.load_q8_model(fsx_load.model_from_dict(ref))
+        e = HipShardEngine(c, n, dev)
+        rec, counts = e.pack(th, tl, tt, n, 1, tv)
+        c.sync()
+        m, rb = int(counts[0].item()), int(counts[2].item())
+        assert m == n and rb == 16   # config 2: every packet an IPv4 packet, in arrival order
+        v = torch.zeros(n, dtype=torch.uint8, device=dev)
+        out = dict(k=torch.empty(n * 16, dtype=torch.uint8, device=dev),
+                   f=torch.empty(n, dtype=torch.uint8, device=dev),
+                   x=torch.empty(n * 8, dtype=torch.float32, device=dev),
+                   p=torch.empty(n, dtype=torch.float32, device=dev),
+                   d=torch.empty(n, dtype=torch.uint8, device=dev))
+        for a, b in ((0, cut), (cut, n)):
+            c.process_records_device(rec.data_ptr() + a * rb, b - a, rb, v.data_ptr() + a, out["k"].data_ptr(),
+                                     out["f"].data_ptr(), out["x"].data_ptr(), out["p"].data_ptr(),
+                                     out["d"].data_ptr(), n)
+            c.sync()
+            info = c.last_batch_info()
+            assert info["heavy_unsorted"] == 1
+            vo = o.batch(hdr[a:b], ln[a:b], ts[a:b])
+            bad = np.nonzero(v[a:b].cpu().numpy() != vo)[0]
+            assert bad.size == 0, f"{bad.size} verdicts differ, first at {bad[:8]}"
+            rows = info["sources"]
+            kg = out["k"].cpu().numpy().reshape(n, 16)[:rows]
+            fg = out["f"].cpu().numpy()[:rows]
+            xg = out["x"].cpu().numpy().reshape(n, 8)[:rows]
+            pg = out["p"].cpu().numpy()[:rows]
+            ko, fo, xo = oracle.flow_features(hdr[a:b], ln[a:b], ts[a:b])
+            assert rows == len(fo)
+            og = sorted(range(rows), key=lambda i: (int(fg[i]), kg[i].tobytes()))
+            oo = sorted(range(rows), key=lambda i: (int(fo[i]), ko[i].tobytes()))
+            assert np.array_equal(kg[og], ko[oo])
+            assert np.array_equal(xg[og].view(np.uint32), xo[oo].view(np.uint32))
+            po, _, _ = oracle.score(ref, xo[oo])
+            assert np.array_equal(pg[og].view(np.uint32), po.view(np.uint32))
+        assert c.stats() == o.stats()
+        for mid in (1, 2, 3, 4):
+            assert pyoracle.same_map(c.map_arrays(mid), o.map_arrays(mid)), mid
