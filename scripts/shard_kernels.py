@@ -71,6 +71,42 @@ def main():
                                                  ov.data_ptr())
                 ctx.sync()
                 out[f"owner_{mode}_ms"] = (time.perf_counter() - t0) / 3 * 1e3
+    # the owner as the sharded stream runs it: maps carried (no reset), every call the next
+    # batch of the stream (the records' timestamps shifted by one duration), calls enqueued
+    # back to back (pipeline mode 2, HipShardEngine's), verdicts only and with features +
+    # q8 scores (per-source rows)
+    from flowsentryx_amd import fsx_load   # noqa: E402
+    from pathlib import Path
+    model = fsx_load.load_weights(Path(__file__).resolve().parents[1] / "tests" / "golden" / "model_weights.json")
+    dur = int(p.duration_ns)
+    tsw = rec[:m * rb].view(torch.int64)[1::2]   # ShardRecord16.ts (bytes 8..15)
+    assert rb == 16
+    for flows in (False, True):
+        with lib.FsxContext(max_batch=n, max_entries=int(p.n_ips), device=0) as ctx:
+            ctx.load_q8_model(model)
+            ctx.set_pipeline(2)
+            ov = torch.empty(m, dtype=torch.uint8, device=dev)
+            cap = int(p.n_ips)
+            fo = [torch.empty(cap * 16, dtype=torch.uint8, device=dev), torch.empty(cap, dtype=torch.uint8, device=dev),
+                  torch.empty(cap * 8, dtype=torch.float32, device=dev), torch.empty(cap, dtype=torch.float32, device=dev),
+                  torch.empty(cap, dtype=torch.uint8, device=dev)]
+            K = 6
+            for it in range(K + 2):
+                if it == 2:
+                    ctx.sync()
+                    t0 = time.perf_counter()
+                tsw.add_(dur)
+                torch.cuda.synchronize()   # (the shift on torch's stream, before the call)
+                if flows:
+                    ctx.process_records_device(rec.data_ptr(), m, rb, ov.data_ptr(), *[x.data_ptr() for x in fo], cap)
+                else:
+                    ctx.verdict_records_device(rec.data_ptr(), m, rb, ov.data_ptr())
+            ctx.sync()
+            el = (time.perf_counter() - t0) / K * 1e3
+            out["owner_records_warm_flows_ms" if flows else "owner_records_warm_ms"] = el
+            out["owner_heavy_unsorted"] = ctx.last_batch_info().get("heavy_unsorted")
+    out["note"] = ("owner_records_warm*: maps carried, one 64M-record batch per call incl. a torch shift "
+                   "of the record timestamps and a device sync per call")
     print(json.dumps(out))
 
 
