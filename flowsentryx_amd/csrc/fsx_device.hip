@@ -1151,28 +1151,31 @@ __global__ __launch_bounds__(256, kLatePay ? FSX_SCATTER_MINB : 1) void k_tile_s
 }
 
 // ---- pass 0 with the heavy sources outside the sort (k_parse<..., kHf>; fsx_heavy.hip).
-// Two kernels, one block per sort tile t, wave w = the tile's parse chunk w (1024 arrival
-// positions):
-//   k_heavy_tiles  every packet's timestamp, length and verdict byte (coalesced): the batch's
-//                  clock facts (non-decreasing?, min / max, tile span), and for every heavy
-//                  source h (byte 0x80 | h) its sums over the tile (HeavyTileRec): lengths,
-//                  squared lengths, first / last timestamp and the gaps between its
-//                  consecutive packets — a packet's predecessor is the last lane below it
-//                  with the same h (eight ballots), else the wave's last packet of h in an
-//                  earlier row; the waves' chunks are joined at the tile end. It runs on the
-//                  aux stream beside the light sort passes (only k_hmode and the tail read it);
-//   k_pass0h       pass 0 of the light sort words, which k_parse compacted per chunk
-//                  (chunk_cnt): the stable in-tile ranking of sort_tile, payload words
-//                  gathered by arrival index.
-__global__ __launch_bounds__(256) void k_heavy_tiles(uint32_t n, BatchState *bs,
-                                                     const uint64_t *__restrict__ ts,
-                                                     const uint32_t *__restrict__ len,
-                                                     const uint8_t *__restrict__ tags,
-                                                     HeavyTileRec *__restrict__ rec,
-                                                     const HeavySet *__restrict__ hs) {
-    __shared__ uint32_t h_s1[kHeavyMax], h_dmax[kHeavyMax], h_fo[kHeavyMax];
-    __shared__ unsigned long long h_s2[kHeavyMax], h_d2[kHeavyMax];
-    __shared__ unsigned long long h_first[4 * kHeavyMax], h_last[4 * kHeavyMax];
+// One block per sort tile t, wave w = the tile's parse chunk w (1024 arrival positions):
+//   1. every packet's timestamp, length and verdict byte (coalesced): the batch's clock facts
+//      (non-decreasing?, min / max, tile span), and for every heavy source h (byte 0x80 | h)
+//      its sums over the tile (HeavyTileRec): lengths, squared lengths, first / last
+//      timestamp and the gaps between its consecutive packets — a packet's predecessor is
+//      the last lane below it with the same h (eight ballots), else the wave's last packet
+//      of h in an earlier row; the waves' chunks are joined at the tile end;
+//   2. pass 0 of the light sort words, which k_parse compacted per chunk (chunk_cnt): the
+//      stable in-tile ranking of sort_tile, payload words gathered by arrival index (their
+//      lines were just read in step 1).
+__global__ __launch_bounds__(256, FSX_SCATTER_MINB) void k_pass0h(const uint64_t *__restrict__ in,
+                                                                  uint64_t *__restrict__ out, uint32_t n,
+                                                                  uint32_t shift, uint32_t dmask,
+                                                                  const uint32_t *__restrict__ offs, uint32_t tcap,
+                                                                  BatchState *bs, uint64_t *__restrict__ pout,
+                                                                  const uint64_t *__restrict__ ts,
+                                                                  const uint32_t *__restrict__ len,
+                                                                  const uint8_t *__restrict__ tags,
+                                                                  const uint32_t *__restrict__ chunk_cnt,
+                                                                  HeavyTileRec *__restrict__ rec,
+                                                                  const HeavySet *__restrict__ hs) {
+    __shared__ unsigned long long s_el[kSortTile];
+    __shared__ uint32_t s_wc[4][256];
+    __shared__ uint32_t s_dst[256], s_tbase[256], s_tcnt[256];
+    __shared__ uint32_t s_tmp[4];
     __shared__ unsigned long long s_red[4][3];
     __shared__ uint32_t s_flag[4];
     const uint32_t tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
@@ -1182,6 +1185,15 @@ __global__ __launch_bounds__(256) void k_heavy_tiles(uint32_t n, BatchState *bs,
     const uint32_t t0 = t * kSortTile;
     const uint64_t lt_mask = (1ull << lane) - 1ull;
     const uint32_t nh = hs->n;
+    const uint64_t tb = ts[0];
+    // ---- 1. heavy sums and clock facts (LDS: the scratch region of s_el)
+    uint32_t *h_s1 = reinterpret_cast<uint32_t *>(s_el);            // [128]
+    uint32_t *h_dmax = h_s1 + kHeavyMax;                            // [128]
+    uint32_t *h_fo = h_dmax + kHeavyMax;                            // [128]
+    unsigned long long *h_s2 = s_el + 256;                          // [128] (bytes 2048..)
+    unsigned long long *h_d2 = h_s2 + kHeavyMax;                    // [128]
+    unsigned long long *h_first = h_d2 + kHeavyMax;                 // [4][128]
+    unsigned long long *h_last = h_first + 4 * kHeavyMax;           // [4][128]
     constexpr unsigned long long kNone = ~0ull;
     if (tid < kHeavyMax) {
         h_s1[tid] = 0; h_dmax[tid] = 0; h_fo[tid] = 0xFFFFFFFFu;
@@ -1290,29 +1302,8 @@ __global__ __launch_bounds__(256) void k_heavy_tiles(uint32_t n, BatchState *bs,
         atomicMax(reinterpret_cast<unsigned long long *>(&bs->max_ts), (unsigned long long)m);
         atomicMax(reinterpret_cast<unsigned long long *>(&bs->inv_min_ts), (unsigned long long)im);
     }
-}
-
-__global__ __launch_bounds__(256, FSX_SCATTER_MINB) void k_pass0h(const uint64_t *__restrict__ in,
-                                                                  uint64_t *__restrict__ out, uint32_t n,
-                                                                  uint32_t shift, uint32_t dmask,
-                                                                  const uint32_t *__restrict__ offs, uint32_t tcap,
-                                                                  BatchState *bs, uint64_t *__restrict__ pout,
-                                                                  const uint64_t *__restrict__ ts,
-                                                                  const uint32_t *__restrict__ len,
-                                                                  const uint32_t *__restrict__ chunk_cnt) {
-    __shared__ unsigned long long s_el[kSortTile];
-    __shared__ uint32_t s_wc[4][256];
-    __shared__ uint32_t s_dst[256], s_tbase[256], s_tcnt[256];
-    __shared__ uint32_t s_tmp[4];
-    const uint32_t tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
-    const uint32_t ntiles = (n + kSortTile - 1) / kSortTile;
-    if (blockIdx.x >= ntiles) return;
-    const uint32_t t = xcd_swizzle(blockIdx.x, ntiles);
-    const uint32_t t0 = t * kSortTile;
-    const uint64_t lt_mask = (1ull << lane) - 1ull;
-    const uint64_t tb = ts[0];
-    // light words of the tile's chunks (sort_tile ranking, keys from the chunk runs)
-    const uint32_t c0 = t0 + w * 1024u;
+    __syncthreads();
+    // ---- 2. pass 0 of the tile's light words (sort_tile, keys from the chunk runs)
 #pragma unroll
     for (int k = 0; k < 4; ++k) s_wc[w][lane * 4 + k] = 0;
     __syncthreads();
@@ -1395,16 +1386,11 @@ __global__ __launch_bounds__(256, FSX_SCATTER_MINB) void k_pass0h(const uint64_t
 
 hipError_t launch_pass0h(const uint64_t *in, uint64_t *out, uint32_t n, uint32_t shift, uint32_t dmask,
                          const uint32_t *offs, uint32_t tcap, BatchState *bs, uint64_t *pout, const uint64_t *ts,
-                         const uint32_t *len, const uint32_t *chunk_cnt, hipStream_t st) {
+                         const uint32_t *len, const uint8_t *tags, const uint32_t *chunk_cnt, void *rec,
+                         const HeavySet *hs, hipStream_t st) {
     const uint32_t ntiles = std::max<uint32_t>(1, (n + kSortTile - 1) / kSortTile);
-    k_pass0h<<<ntiles, 256, 0, st>>>(in, out, n, shift, dmask, offs, tcap, bs, pout, ts, len, chunk_cnt);
-    return hipGetLastError();
-}
-
-hipError_t launch_heavy_tiles(uint32_t n, BatchState *bs, const uint64_t *ts, const uint32_t *len,
-                              const uint8_t *tags, void *rec, const HeavySet *hs, hipStream_t st) {
-    const uint32_t ntiles = std::max<uint32_t>(1, (n + kSortTile - 1) / kSortTile);
-    k_heavy_tiles<<<ntiles, 256, 0, st>>>(n, bs, ts, len, tags, static_cast<HeavyTileRec *>(rec), hs);
+    k_pass0h<<<ntiles, 256, 0, st>>>(in, out, n, shift, dmask, offs, tcap, bs, pout, ts, len, tags, chunk_cnt,
+                                     static_cast<HeavyTileRec *>(rec), hs);
     return hipGetLastError();
 }
 
@@ -2563,9 +2549,6 @@ hipError_t launch_tail(const TailArgs &a) {
             heavy_join = true;
         }
     }
-    // the heavy tile sums and k_hmode ran beside the light passes (st2): everything below
-    // reads them (recorded before the next batch's front can record join_ev again)
-    if (a.p0_join && (e = hipStreamWaitEvent(st, join_ev, 0)) != hipSuccess) return e;
     // unsorted heavy sources that k_hmode sent back to the run path: their runs first
     if (a.hfm && (e = launch_heavy_gather(bs, verdict, ts, len, n, sc.hist, tcap, sc.heavy, a.shift0, lim.table_mask,
                                           S_fin, pay_fin, st)) != hipSuccess)
@@ -2871,7 +2854,6 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
     k_hist_prep<<<1, 256, 0, st>>>(sc.sort_ctl, sc.gbase, bs, heavy_sort ? dp.light_b : 256u);
     if (do_limit) k_batch_check<<<1, 1, 0, st>>>(bs, tstate, lim, split ? split->prev : nullptr);
     const uint32_t gen0 = onesweep ? next_generation() : 0u;
-    bool p0fork = false;   // the heavy tile sums on st2 (the tail joins them)
     for (int pass = 0; pass < npass; ++pass) {
         const uint64_t *in = sc.packed[pass & 1];
         uint64_t *out = sc.packed[(pass + 1) & 1];
@@ -2898,24 +2880,12 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
             mark("k_tile_scan");
             if (pass == 0 && (e = tail_hook(1)) != hipSuccess) return e;
             if (pass == 0 && hfm) {   // light words from the parse chunks; heavy tile sums; the path
-                // (the heavy tile sums and k_hmode on the aux stream beside the light passes when
-                // it is given: only the tail reads them, after waiting for join_ev; FSX_P0H_SERIAL=1: A/B)
-                static const bool p0_serial = getenv("FSX_P0H_SERIAL") != nullptr;
-                p0fork = st2 && fork_ev && join_ev && !p0_serial && !tm;
-                hipStream_t sh = p0fork ? st2 : st;
-                if (p0fork) {
-                    if ((e = hipEventRecord(fork_ev, st)) != hipSuccess) return e;
-                    if ((e = hipStreamWaitEvent(st2, fork_ev, 0)) != hipSuccess) return e;
-                }
-                if ((e = launch_heavy_tiles(n, bs, ts, len, verdict, sc.hrec, sc.heavy, sh)) != hipSuccess) return e;
-                mark_on("k_heavy_tiles", p0fork ? 1 : 0);
-                if ((e = launch_hmode(bs, ts, n, sc.heavy, table, lim, sh)) != hipSuccess) return e;
-                mark_on("k_hmode", p0fork ? 1 : 0);
-                if (p0fork && (e = hipEventRecord(join_ev, st2)) != hipSuccess) return e;
-                if ((e = launch_pass0h(in, out, n, shift, pmask, sc.hist, tcap, bs, pout, ts, len, sc.chunk_cnt,
-                                       st)) != hipSuccess)
+                if ((e = launch_pass0h(in, out, n, shift, pmask, sc.hist, tcap, bs, pout, ts, len, verdict,
+                                       sc.chunk_cnt, sc.hrec, sc.heavy, st)) != hipSuccess)
                     return e;
                 mark("k_pass0h");
+                if ((e = launch_hmode(bs, ts, n, sc.heavy, table, lim, st)) != hipSuccess) return e;
+                mark("k_hmode");
             } else {
                 k_tile_scatter<kLatePayDefault><<<ntiles, 256, 0, st>>>(in, out, n, Ld, shift, pmask, pass == 0, sc.hist, tcap, bs,
                                                        pin, pout, ts, len);
@@ -2939,7 +2909,7 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
     if (split) ta.sp = *split;
     ta.npass = npass; ta.tagh = tagh; ta.gridTiles = gridTiles;
     ta.hfm = hfm; ta.shift0 = dp.shift[0];
-    ta.admit = admit; ta.X = X; ta.id_gen = id_gen; ta.lazy = lazy; ta.p0_join = p0fork;
+    ta.admit = admit; ta.X = X; ta.id_gen = id_gen; ta.lazy = lazy;
     ta.fork = flows && do_limit && st2 && fork_ev && join_ev && !no_fork;
     for (int k = 0; k < 3; ++k) ta.last[k] = last[k];
     if (split && split->tail_out) {

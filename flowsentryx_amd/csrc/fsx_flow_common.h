@@ -171,6 +171,44 @@ __device__ __forceinline__ uint32_t dst_port(const uint8_t *f, uint32_t len) {
     return ((uint32_t)f[off + 2] << 8) | f[off + 3];
 }
 
+// Family, key and L4 destination port of one 64-byte header record from four 16-byte loads
+// (key_of + dst_port read the same bytes with up to eight scattered loads of a random
+// record); identical results: the IPv4 port at byte off + 2 = 16 + 4 IHL is the low half
+// of dword 4 + IHL, the IPv6 one at byte 56 that of dword 14.
+__device__ __forceinline__ uint32_t record_src_port(const uint8_t *rec, uint32_t len, uint32_t k[4],
+                                                   uint32_t &dport) {
+    const uint4 *q = reinterpret_cast<const uint4 *>(rec);
+    const uint4 a = q[0], b = q[1], c = q[2], d = q[3];
+    const uint32_t w[16] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y, c.z, c.w, d.x, d.y, d.z, d.w};
+    const uint32_t proto = ((w[3] & 0xFFu) << 8) | ((w[3] >> 8) & 0xFFu);
+    uint32_t tag, off, l4;
+    if (proto == 0x86DDu) {
+        tag = 2;
+        k[0] = (w[5] >> 16) | (w[6] << 16); k[1] = (w[6] >> 16) | (w[7] << 16);
+        k[2] = (w[7] >> 16) | (w[8] << 16); k[3] = (w[8] >> 16) | (w[9] << 16);
+        off = 54;
+        l4 = w[5] & 0xFFu;   // byte 20: next header
+        if (len < 54) { dport = 0; return tag; }
+    } else {
+        tag = 1;
+        k[0] = (w[6] >> 16) | (w[7] << 16);   // bytes 26..29
+        k[1] = k[2] = k[3] = 0;
+        off = 14u + 4u * ((w[3] >> 16) & 0x0Fu);   // byte 14: IHL
+        l4 = w[5] >> 24;                           // byte 23: protocol
+        if (len < 34) { dport = 0; return tag; }
+    }
+    dport = 0;
+    if ((l4 == 6 || l4 == 17) && off + 4 <= len && off + 4 <= 64) {
+        // (IHL 0 .. 12: dword 4 .. 15, the port's first byte at the dword's start)
+        const uint32_t wi = (off + 2) >> 2;
+        uint32_t x = 0;
+#pragma unroll
+        for (uint32_t j = 4; j < 16; ++j) x = wi == j ? w[j] : x;
+        dport = ((x & 0xFFu) << 8) | ((x >> 8) & 0xFFu);
+    }
+    return tag;
+}
+
 __device__ __forceinline__ void acc_store(const FlowOut &out, uint32_t g, const FlowAcc &a) {
     if (g < out.cap) out.acc[g] = a;
 }
@@ -197,8 +235,8 @@ __device__ __forceinline__ void flow_finish(uint32_t g, const FlowAcc &a, const 
         uint64_t T;
         tag = rec_read(in.rec, in.rec_bytes, idx, k, L, T, dport);
     } else {
-        tag = key_of(v, in.hdr, salt, k);
-        dport = dst_port(in.hdr + (size_t)idx * 64, out.seg_len ? out.seg_len[g] : len[idx]);
+        (void)salt;
+        tag = record_src_port(in.hdr + (size_t)idx * 64, out.seg_len ? out.seg_len[g] : len[idx], k, dport);
     }
     const bool need_t = out.part.buf || out.sacc;
     flow_emit(g, a, tag, k, dport, need_t ? out.ts[idx] : 0ull,

@@ -500,7 +500,6 @@ struct TailArgs {
     TableIndex X;         // (admission: the persistent index)
     uint32_t id_gen;      // (admission: the batch generation stamped on admitted slots)
     bool lazy;            // k_parse left new sources' slots to the fixed window's walkers
-    bool p0_join;         // the heavy tile sums / k_hmode ran on st2: the tail waits for join_ev
     uint32_t shift0;      // pass 0's bucket shift (k_heavy_gather's sort words)
     FlowRequest fq;
     HistBufs hist;
@@ -576,9 +575,8 @@ hipError_t launch_flows_heavy_finish(const uint64_t *S, const BatchState *bs, co
 // Heavy sources outside the sort (fsx_heavy.hip; k_pass0h in fsx_device.hip), DESIGN.md §3.
 hipError_t launch_pass0h(const uint64_t *in, uint64_t *out, uint32_t n, uint32_t shift, uint32_t dmask,
                          const uint32_t *offs, uint32_t tcap, BatchState *bs, uint64_t *pout, const uint64_t *ts,
-                         const uint32_t *len, const uint32_t *chunk_cnt, hipStream_t st);
-hipError_t launch_heavy_tiles(uint32_t n, BatchState *bs, const uint64_t *ts, const uint32_t *len,
-                              const uint8_t *tags, void *rec, const HeavySet *hs, hipStream_t st);
+                         const uint32_t *len, const uint8_t *tags, const uint32_t *chunk_cnt, void *rec,
+                         const HeavySet *hs, hipStream_t st);
 hipError_t launch_hmode(BatchState *bs, const uint64_t *ts, uint32_t n, const HeavySet *hs, const Slot *table,
                         const Limits &lim, hipStream_t st);
 hipError_t launch_heavy_gather(const BatchState *bs, const uint8_t *tags, const uint64_t *ts, const uint32_t *len,

@@ -423,6 +423,39 @@ def test_flow_features_random(native, oracle):
     _check_flows(native, oracle, hdr, ln, ts)
 
 
+def test_flow_features_header_variants(native, oracle):
+    """The per-source port column on unusual headers: every IPv4 IHL 0..15 (the port's
+    offset 14 + 4 IHL, past the 64-byte record for IHL > 12), TCP / UDP / other protocols,
+    frames too short for the port, IPv6 with and without room for it; each source's first
+    packet decides its port."""
+    import struct
+    from flowsentryx_amd import synth
+    rng = np.random.default_rng(77)
+    frames, lens = [], []
+    for i in range(3000):
+        src = bytes([10, 20, (i // 7) % 256, (i // 7) // 256 + 1])
+        if i % 5 == 4:
+            L = int(rng.choice([40, 54, 57, 58, 60, 100, 1500]))
+            f = bytearray(synth.frame_ipv6_udp(bytes([0x20, 1]) + src + bytes(10), L,
+                                              dport=int(rng.integers(0, 65536))))
+            f[20] = int(rng.choice([6, 17, 58]))
+        else:
+            L = int(rng.choice([20, 33, 34, 37, 38, 41, 64, 80, 1500]))
+            ihl = int(rng.integers(0, 16))
+            f = bytearray(synth.frame_ipv4_udp(src, L, dport=int(rng.integers(0, 65536)), ihl_byte=0x40 | ihl))
+            # a port word at every candidate offset, so a wrong offset reads different bytes
+            for w in range(16, 62, 2):
+                if w not in (26, 28):
+                    f[w:w + 2] = struct.pack("!H", int(rng.integers(0, 65536)))
+            f[23] = int(rng.choice([6, 17, 1]))
+        frames.append(bytes(f[:64]))
+        lens.append(L)
+    hdr = synth.records(frames)
+    ln = np.array(lens, dtype=np.uint32)
+    ts = np.cumsum(rng.integers(1, 1000, len(ln))).astype(np.uint64)
+    _check_flows(native, oracle, hdr, ln, ts)
+
+
 def test_flow_features_heavy_sources(native, oracle):
     """Config-1 stream: 1024 Zipf sources over 1M packets, so the heavy sources span
     hundreds of flow tiles (exercises the cross-tile combine)."""
