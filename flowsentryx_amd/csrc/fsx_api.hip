@@ -160,6 +160,7 @@ struct fsx_ctx {
     TailArgs tail_args{};             // the last pipelined batch's tail, not yet enqueued
     bool tail_pending = false;
     int tail_par = 0;
+    int tail_prev = -1;               // set of the last tail enqueued (its completion: tail_done)
     bool tail_join = false;           // the last pipelined batch's tail is not joined into stream
     char err[512]{};
 };
@@ -275,14 +276,22 @@ const char *fsx_last_error(const fsx_ctx *ctx) { return ctx ? ctx->err : "null c
 
 // The deferred tail of the last pipelined batch onto the walker stream (and the flows on the
 // aux stream), after event `after` on the context stream.
+// A tail whose flows run on the aux stream ends there (the aux stream waits for the
+// walker stream's verdict apply): the walker stream is free for the next batch's early
+// prologue at once, and the next tail starts after this one's flows (tail_done), which
+// share the segment arrays with it.
 static hipError_t flush_tail(fsx_ctx *c, hipEvent_t after) {
     if (!c->tail_pending) return hipSuccess;
     c->tail_pending = false;
     hipError_t e;
     if ((e = hipStreamWaitEvent(c->walk_stream, after, 0)) != hipSuccess) return e;
     if ((e = hipStreamWaitEvent(c->aux_stream, after, 0)) != hipSuccess) return e;
+    if (c->tail_prev >= 0 && (e = hipStreamWaitEvent(c->walk_stream, c->tail_done[c->tail_prev], 0)) != hipSuccess)
+        return e;
     if ((e = launch_tail(c->tail_args)) != hipSuccess) return e;
-    return hipEventRecord(c->tail_done[c->tail_par], c->walk_stream);
+    c->tail_prev = c->tail_par;
+    static const bool old_join = getenv("FSX_TAIL_JOIN_WALK") != nullptr;
+    return hipEventRecord(c->tail_done[c->tail_par], c->tail_args.fork && !old_join ? c->aux_stream : c->walk_stream);
 }
 
 // PipeSplit::on_parse: the previous batch's tail goes in right after this batch's parse.
@@ -827,8 +836,12 @@ static int run_pipelined(fsx_ctx *c, const PacketIn &in, const uint32_t *d_len, 
         HIPCHK(c, hipEventRecord(c->pro_wait, c->stream));
         c->pro_fence = false;
     }
+    // (the early prologue on the walker stream: the aux stream carries the previous tail's
+    // flows, which the next parse should not wait for)
+    static const bool old_join = getenv("FSX_TAIL_JOIN_WALK") != nullptr;   // A/B: round-3 placement
     const PipeSplit sp = split ? PipeSplit{c->walk_stream, c->front_done, prev, pipe_on_parse, c, &c->tail_args,
-                                           no_early ? nullptr : c->aux_stream, c->pro_wait, c->pro_done}
+                                           no_early ? nullptr : old_join ? c->aux_stream : c->walk_stream,
+                                           c->pro_wait, c->pro_done}
                                : PipeSplit{nullptr, nullptr, prev, nullptr, nullptr, nullptr};
     hipError_t e = launch_verdict_pipeline(in, d_len, d_ts, (uint32_t)n, d_verdict, c->table, c->tstate, c->bs,
                                            c->sc, c->id_gen, table_index(c), c->lim, c->rs, true, fr, c->hist,

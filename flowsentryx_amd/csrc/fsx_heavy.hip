@@ -435,34 +435,65 @@ __global__ __launch_bounds__(128) void k_hflow_combine(const BatchState *bs, con
     part[(size_t)g * kHeavyMax + h] = x;
 }
 
+__device__ __forceinline__ HFlowPart shfl_down_part(const HFlowPart &x, uint32_t o) {
+    HFlowPart y;
+    y.a.n = __shfl_down(x.a.n, o); y.a.s1 = __shfl_down(x.a.s1, o); y.a.dmax = __shfl_down(x.a.dmax, o);
+    y.a.pad = 0;
+    const uint64_t s2l = __shfl_down((uint64_t)x.a.s2, o), s2h = __shfl_down((uint64_t)(x.a.s2 >> 64), o);
+    const uint64_t d1l = __shfl_down((uint64_t)x.a.d1, o), d1h = __shfl_down((uint64_t)(x.a.d1 >> 64), o);
+    const uint64_t d2l = __shfl_down((uint64_t)x.a.d2, o), d2h = __shfl_down((uint64_t)(x.a.d2 >> 64), o);
+    y.a.s2 = ((u128)s2h << 64) | s2l;
+    y.a.d1 = ((u128)d1h << 64) | d1l;
+    y.a.d2 = ((u128)d2h << 64) | d2l;
+    y.t0 = __shfl_down(x.t0, o); y.t1 = __shfl_down(x.t1, o);
+    y.fi = __shfl_down(x.fi, o); y.has = __shfl_down(x.has, o);
+    y.pad_[0] = y.pad_[1] = 0;
+    return y;
+}
+
 // After the heads (k_heads_heavy numbered the heavy segments): heavy source h's row is
-// segment nseg_light + (its rank among the non-empty ones), as on the run path.
-__global__ __launch_bounds__(128) void k_hflow_finish(const BatchState *bs, const uint32_t *__restrict__ cnt0,
+// segment nseg_light + (its rank among the non-empty ones), as on the run path. One wave
+// per heavy source: lane j merges a contiguous run of the groups' partials in order, then
+// an ordered tree over the lanes (the merge is associative, not commutative).
+__global__ __launch_bounds__(256) void k_hflow_finish(const BatchState *bs, const uint32_t *__restrict__ cnt0,
                                                       const HeavySet *__restrict__ hs,
                                                       const HFlowPart *__restrict__ part, uint32_t ngroups,
                                                       PacketIn in, const uint32_t *__restrict__ len, FlowOut out,
                                                       ScoreParams P) {
-    __shared__ uint32_t s_live[kHeavyMax];
     if (bs->err || !bs->hfast) return;
-    const uint32_t h = threadIdx.x;
-    const bool live = h < hs->n && cnt0[bs->light_b + h] > 0;
-    s_live[h] = live ? 1u : 0u;
-    __syncthreads();
-    if (!live) return;
-    uint32_t r = 0;
-    for (uint32_t j = 0; j < h; ++j) r += s_live[j];
-    HFlowPart x = part[h];
-    for (uint32_t g0 = 1; g0 < ngroups; g0 += 8) {   // eight groups' loads in flight
-        HFlowPart y[8];
+    const uint32_t h = blockIdx.x * 4u + (threadIdx.x >> 6), lane = lane_id();
+    const uint32_t lb = bs->light_b;
+    const bool live0 = lane < kHeavyMax && lane < hs->n && cnt0[lb + lane] > 0;
+    const bool live1 = lane + 64u < kHeavyMax && lane + 64u < hs->n && cnt0[lb + 64u + lane] > 0;
+    const uint64_t m0 = __ballot(live0), m1 = __ballot(live1);
+    if (h >= hs->n || cnt0[lb + h] == 0) return;
+    const uint32_t r = h < 64 ? (uint32_t)__popcll(m0 & ((1ull << h) - 1ull))
+                              : (uint32_t)__popcll(m0) + (uint32_t)__popcll(m1 & ((1ull << (h - 64)) - 1ull));
+    const uint32_t per = (ngroups + 63u) / 64u;
+    const uint32_t g0 = min(ngroups, lane * per), g1 = min(ngroups, g0 + per);
+    HFlowPart x;
+    x.a = acc_zero();
+    x.t0 = x.t1 = 0;
+    x.fi = 0;
+    x.has = 0;
+    x.pad_[0] = x.pad_[1] = 0;
+    for (uint32_t g = g0; g < g1; g += 4) {   // four groups' loads in flight
+        HFlowPart y[4];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            const uint32_t g = g0 + (uint32_t)u;
-            y[u] = part[(size_t)(g < ngroups ? g : 0u) * kHeavyMax + h];
-            if (g >= ngroups) y[u].has = 0;
+        for (int u = 0; u < 4; ++u) {
+            const uint32_t gg = g + (uint32_t)u;
+            y[u] = part[(size_t)(gg < g1 ? gg : g0) * kHeavyMax + h];
+            if (gg >= g1) y[u].has = 0;
         }
 #pragma unroll
-        for (int u = 0; u < 8; ++u) hpart_merge(x, y[u]);
+        for (int u = 0; u < 4; ++u) hpart_merge(x, y[u]);
     }
+#pragma unroll
+    for (uint32_t o = 1; o < 64; o <<= 1) {   // lane k (multiple of 2o) merges lane k + o's run
+        const HFlowPart y = shfl_down_part(x, o);
+        if ((lane & (2u * o - 1u)) == 0) hpart_merge(x, y);
+    }
+    if (lane != 0) return;
     const uint32_t row = bs->nseg_light + r;
     uint32_t k[4] = {hs->key[h][0], hs->key[h][1], hs->key[h][2], hs->key[h][3]};
     uint32_t dport;
@@ -525,7 +556,8 @@ hipError_t launch_hflow_finish(const BatchState *bs, const uint32_t *cnt0, const
     const uint32_t ng = std::max<uint32_t>(1, (ntiles + kHGroupTiles - 1) / kHGroupTiles);
     FlowOut out{nullptr, keys16, fam, feat, prob, dec, rows_cap, (SlotAcc *)sacc, epoch, nullptr, ts,
                 nullptr, nullptr, partial};
-    k_hflow_finish<<<1, 128, 0, st>>>(bs, cnt0, hs, static_cast<const HFlowPart *>(part), ng, in, len, out, P);
+    k_hflow_finish<<<kHeavyMax / 4, 256, 0, st>>>(bs, cnt0, hs, static_cast<const HFlowPart *>(part), ng, in, len,
+                                                  out, P);
     return hipGetLastError();
 }
 

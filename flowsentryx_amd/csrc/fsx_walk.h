@@ -146,21 +146,23 @@ __device__ __forceinline__ FwState load_state(const Slot &sl) {
 }
 // A new source's Slot under lazy initialisation (IdTable::init = 0, the fixed window): k_parse
 // claimed only its index head, so the walker that first stores its state also writes its
-// family and key, from the head (IPv4 key word) and the IPv6 key words (agent-scope loads:
-// the index lines may sit in another XCD's L2). heads null: k_parse initialised every slot.
+// family and key, from the head (IPv4 key word) and the IPv6 key words. Plain loads: the head
+// was published by an earlier kernel (the parse, ordered before the tail by the stream or
+// its front_done event), and no later writer changes it. heads null: k_parse initialised
+// every slot. (Called after store_state, which leaves the tag alone: a tag still 0 is new.)
 struct SlotKeys {
     const unsigned long long *heads;
     const uint32_t *k6;
 };
 
 __device__ __forceinline__ void slot_adopt(Slot &sl, const SlotKeys &K, uint32_t i) {
-    const unsigned long long h = __hip_atomic_load(K.heads + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long h = K.heads[i];
     const uint32_t tag = (uint32_t)(h >> 32) & 0xFFu;
     sl.key[0] = (uint32_t)h;
     if (tag == 2) {
-        sl.key[1] = __hip_atomic_load(K.k6 + (size_t)i * 4 + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        sl.key[2] = __hip_atomic_load(K.k6 + (size_t)i * 4 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        sl.key[3] = __hip_atomic_load(K.k6 + (size_t)i * 4 + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        sl.key[1] = K.k6[(size_t)i * 4 + 0];
+        sl.key[2] = K.k6[(size_t)i * 4 + 1];
+        sl.key[3] = K.k6[(size_t)i * 4 + 2];
     }
     sl.tag = tag;
 }
