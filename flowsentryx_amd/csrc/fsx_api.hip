@@ -290,8 +290,8 @@ static hipError_t flush_tail(fsx_ctx *c, hipEvent_t after) {
         return e;
     if ((e = launch_tail(c->tail_args)) != hipSuccess) return e;
     c->tail_prev = c->tail_par;
-    static const bool old_join = getenv("FSX_TAIL_JOIN_WALK") != nullptr;
-    return hipEventRecord(c->tail_done[c->tail_par], c->tail_args.fork && !old_join ? c->aux_stream : c->walk_stream);
+    static const bool end_aux = getenv("FSX_TAIL_END_AUX") != nullptr;
+    return hipEventRecord(c->tail_done[c->tail_par], c->tail_args.fork && end_aux ? c->aux_stream : c->walk_stream);
 }
 
 // PipeSplit::on_parse: the previous batch's tail goes in right after this batch's parse.
@@ -838,9 +838,11 @@ static int run_pipelined(fsx_ctx *c, const PacketIn &in, const uint32_t *d_len, 
     }
     // (the early prologue on the walker stream: the aux stream carries the previous tail's
     // flows, which the next parse should not wait for)
-    static const bool old_join = getenv("FSX_TAIL_JOIN_WALK") != nullptr;   // A/B: round-3 placement
+    // (FSX_TAIL_END_AUX=1: tails end on the aux stream and the early prologue runs on the walker
+    // stream; measured 2.99 vs 2.96 ms per step, profiles/r04/ab_r04n.txt)
+    static const bool end_aux = getenv("FSX_TAIL_END_AUX") != nullptr;
     const PipeSplit sp = split ? PipeSplit{c->walk_stream, c->front_done, prev, pipe_on_parse, c, &c->tail_args,
-                                           no_early ? nullptr : old_join ? c->aux_stream : c->walk_stream,
+                                           no_early ? nullptr : end_aux ? c->walk_stream : c->aux_stream,
                                            c->pro_wait, c->pro_done}
                                : PipeSplit{nullptr, nullptr, prev, nullptr, nullptr, nullptr};
     hipError_t e = launch_verdict_pipeline(in, d_len, d_ts, (uint32_t)n, d_verdict, c->table, c->tstate, c->bs,

@@ -1995,12 +1995,14 @@ __device__ __forceinline__ void walk_short(const SV &sv, const BatchState *bs,
         const uint32_t g = order[i];
         const uint32_t a = seg_start[g], b = seg_start[g + 1];
         if (H.list && a >= bs->n_light) continue;   // a heavy source: k_walk_heavy
-        Slot &sl = table[seg_slot[g]];
+        const uint32_t si = seg_slot[g];
+        Slot &sl = table[si];
         FwState st = load_state(sl);
+        const unsigned long long hd = K.heads ? K.heads[si] : 0ull;
         MarkWriter<false> mw{marks, 0};
         walk_fixed_exact_thread(sv, a, b, lim, mw, st);
         store_state(sl, st);
-        if (K.heads && sl.tag == 0) slot_adopt(sl, K, (uint32_t)(&sl - table));
+        if (K.heads && sl.tag == 0) slot_adopt(sl, K, si, hd);
     }
 }
 
@@ -2038,8 +2040,10 @@ __device__ __forceinline__ void walk_long(const SV &sv, const BatchState *bs,
         const uint32_t g = order[first + i];
         const uint32_t a = seg_start[g], b = seg_start[g + 1];
         if (H.list && a >= bs->n_light) continue;   // a heavy source: k_walk_heavy
-        Slot &sl = table[seg_slot[g]];
+        const uint32_t si = seg_slot[g];
+        Slot &sl = table[si];
         FwState st = load_state(sl);
+        const unsigned long long hd = K.heads ? K.heads[si] : 0ull;
         const bool fast = glob_fast && (!st.has_st || (st.tt <= ~0ull - lim.window &&
                                                        st.pps < kBig && st.bps < kBig));
         MarkWriter<true> mw{marks, 0};
@@ -2047,7 +2051,7 @@ __device__ __forceinline__ void walk_long(const SV &sv, const BatchState *bs,
         else walk_fixed_exact_wave(sv, a, b, lim, mw, st);
         if (lane_id() == 0) {
             store_state(sl, st);
-            if (K.heads && sl.tag == 0) slot_adopt(sl, K, (uint32_t)(&sl - table));
+            if (K.heads && sl.tag == 0) slot_adopt(sl, K, si, hd);
         }
     }
 }
@@ -2086,9 +2090,11 @@ __device__ __forceinline__ void walk_heavy(const SV &sv, const BatchState *bs, c
     const uint32_t c = cnt0[bs->light_b + h];
     if (c == 0) return;
     const uint32_t a = base0[bs->light_b + h], b = a + c;
-    Slot &sl = table[pk_id(sv.S[a], lim.table_mask)];
+    const uint32_t si = pk_id(sv.S[a], lim.table_mask);
+    Slot &sl = table[si];
     FwState st = load_state(sl);
     // (unresolved heavy sources, under prefix rules, are inserted by k_parse: lazily)
+    const unsigned long long hd = K.heads ? K.heads[si] : 0ull;
     const bool fast = glob_fast && (!st.has_st || (st.tt <= ~0ull - lim.window &&
                                                    st.pps < kBig && st.bps < kBig));
     MarkWriter<true, true> mw{nullptr, 0};
@@ -2098,7 +2104,7 @@ __device__ __forceinline__ void walk_heavy(const SV &sv, const BatchState *bs, c
     heavy_list_close(H, (int)h, a, b, mw);
     if (lane_id() == 0) {
         store_state(sl, st);
-        if (K.heads && sl.tag == 0) slot_adopt(sl, K, (uint32_t)(&sl - table));
+        if (K.heads && sl.tag == 0) slot_adopt(sl, K, si, hd);
     }
 }
 
@@ -2662,8 +2668,8 @@ hipError_t launch_tail(const TailArgs &a) {
                                                       hlists.list);
     mark("k_verdict_apply");
     if (fork) {
-        static const bool old_join = getenv("FSX_TAIL_JOIN_WALK") != nullptr;   // A/B
-        if (split && split->tail && !old_join) {   // pipelined: the tail ends on the flow stream (flush_tail)
+        static const bool end_aux = getenv("FSX_TAIL_END_AUX") != nullptr;   // A/B (slower: 2.99 vs 2.96 ms)
+        if (split && split->tail && end_aux) {   // pipelined: the tail ends on the flow stream (flush_tail)
             if ((e = hipEventRecord(walk_join_ev, st)) != hipSuccess) return e;
             if ((e = hipStreamWaitEvent(st2, walk_join_ev, 0)) != hipSuccess) return e;
         } else if ((e = hipStreamWaitEvent(st, join_ev, 0)) != hipSuccess) {
