@@ -917,6 +917,13 @@ static int evict_idle(fsx_ctx *c, const PacketIn &in, const uint64_t *d_ts, size
     return 0;
 }
 
+// Split pipelining for every limiter (round 4; FSX_SPLIT_FIXED_ONLY=1: the fixed window only,
+// the others whole on the context stream, A/B)
+static bool no_split_limiters(const fsx_ctx *c) {
+    static const bool fixed_only = getenv("FSX_SPLIT_FIXED_ONLY") != nullptr;
+    return fixed_only && c->cfg.limiter != FSX_LIMIT_FIXED_WINDOW;
+}
+
 // Enqueue one batch: verdicts + maps when d_verdict is set, per-source flows when fr is.
 static int run_batch(fsx_ctx *c, const PacketIn &in, const uint32_t *d_len, const uint64_t *d_ts,
                      size_t n, uint8_t *d_verdict, bool do_limit, const FlowRequest *fr) {
@@ -929,7 +936,7 @@ static int run_batch(fsx_ctx *c, const PacketIn &in, const uint32_t *d_len, cons
     // records, the whole batch on the context stream otherwise
     if (c->pipe && do_limit && n && !c->timing)
         return run_pipelined(c, in, d_len, d_ts, n, d_verdict, fr,
-                             c->pipe == 1 && !in.rec && c->cfg.limiter == FSX_LIMIT_FIXED_WINDOW &&
+                             c->pipe == 1 && !in.rec && !no_split_limiters(c) &&
                                  !(c->cfg.flags & FSX_FLAG_OVERFLOW_ADMIT));
     int rc = sel(c);
     if (rc) return rc;

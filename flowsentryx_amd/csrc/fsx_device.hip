@@ -1661,11 +1661,14 @@ __device__ __forceinline__ uint32_t table_claim(Slot *table, const Limits &lim, 
 // sliding window its carried logs plus packets the history buffer — checked before any
 // limiter state changes; a failing batch is rolled back by the host (fsx_api.hip).
 // Pipelined batches: a batch whose predecessor failed is cancelled (the host rolls both back).
-__global__ void k_batch_check(BatchState *bs, TableState *tstate, Limits lim, const BatchState *prev) {
+// (hist_in_tail: a split sliding-window batch checks its history room in its tail, after the
+// previous tail has set hist_total: k_sw_tail_check)
+__global__ void k_batch_check(BatchState *bs, TableState *tstate, Limits lim, const BatchState *prev,
+                              uint32_t hist_in_tail = 0) {
     if (bs->err) return;
     if (prev && prev->err) { bs->err |= ERR_CANCELED; return; }
     if (tstate->count + bs->n_new > lim.max_entries) { bs->err |= ERR_TABLE_FULL; return; }
-    if (lim.limiter == 1 && tstate->hist_total + bs->n_valid > lim.hist_cap) {
+    if (lim.limiter == 1 && !hist_in_tail && tstate->hist_total + bs->n_valid > lim.hist_cap) {
         bs->err |= ERR_HIST_FULL;
         return;
     }
@@ -1674,6 +1677,21 @@ __global__ void k_batch_check(BatchState *bs, TableState *tstate, Limits lim, co
         // (atomic: a pipelined batch's tail may be adding its counters meanwhile)
         atomicAdd(reinterpret_cast<unsigned long long *>(&tstate->stats[1]), (unsigned long long)bs->n_rule);
         bs->dropped += bs->n_rule;
+    }
+}
+
+// A split sliding-window batch's history room, at the start of its tail (the previous tail
+// has set hist_total): a batch that does not fit fails with ERR_HIST_FULL before any state
+// changes, undoing what k_batch_check counted (the rollback rebuilds the index).
+__global__ void k_sw_tail_check(BatchState *bs, TableState *tstate, Limits lim) {
+    if (bs->err) return;
+    if (tstate->hist_total + bs->n_valid > lim.hist_cap) {
+        bs->err |= ERR_HIST_FULL;
+        tstate->count -= bs->n_new;
+        if (bs->n_rule) {
+            atomicAdd(reinterpret_cast<unsigned long long *>(&tstate->stats[1]), (unsigned long long)(0ull - bs->n_rule));
+            bs->dropped -= bs->n_rule;
+        }
     }
 }
 
@@ -2549,6 +2567,7 @@ hipError_t launch_tail(const TailArgs &a) {
             heavy_join = true;
         }
     }
+    if (split && split->tail && do_limit && lim.limiter == 1) k_sw_tail_check<<<1, 1, 0, st>>>(bs, tstate, lim);
     // unsorted heavy sources that k_hmode sent back to the run path: their runs first
     if (a.hfm && (e = launch_heavy_gather(bs, verdict, ts, len, n, sc.hist, tcap, sc.heavy, a.shift0, lim.table_mask,
                                           S_fin, pay_fin, st)) != hipSuccess)
@@ -2860,7 +2879,9 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
     };
     if ((e = tail_hook(0)) != hipSuccess) return e;
     k_hist_prep<<<1, 256, 0, st>>>(sc.sort_ctl, sc.gbase, bs, heavy_sort ? dp.light_b : 256u);
-    if (do_limit) k_batch_check<<<1, 1, 0, st>>>(bs, tstate, lim, split ? split->prev : nullptr);
+    if (do_limit)
+        k_batch_check<<<1, 1, 0, st>>>(bs, tstate, lim, split ? split->prev : nullptr,
+                                       split && split->tail && lim.limiter == 1 ? 1u : 0u);
     const uint32_t gen0 = onesweep ? next_generation() : 0u;
     for (int pass = 0; pass < npass; ++pass) {
         const uint64_t *in = sc.packed[pass & 1];

@@ -279,3 +279,52 @@ def test_pipelined_reset_and_import_between_batches(native, oracle):
             for k, v in entries.items():
                 o.map_update(lib.MAP_IPV4_STATS, k, v)
     _run(native, oracle, batches, between=between)
+
+
+def test_pipelined_sliding_window_history_full(native, oracle):
+    """Split sliding-window batches check their history room in their tail (after the
+    previous tail set it): logs that keep every packet (huge thresholds, 10 s window) fill
+    the history buffer; the batch that does not fit fails with -ENOSPC, it and the batches
+    after it are rolled back, and the state equals an unpipelined context's that stopped at
+    the same batch and the oracle's over the batches before it."""
+    import torch
+    from flowsentryx_amd import lib
+    rng = np.random.default_rng(0x415)
+    B = 1 << 15
+    cfg = dict(limiter=1, pps_threshold=10**6, bps_threshold=10**12, window_ns=10**10, block_ns=10**9,
+               max_entries=1 << 16, max_batch=B)
+    hdr, ln, ts = rand_stream(rng, 12 * B, 3000, dt_max=100)
+    batches = [(hdr[k * B:(k + 1) * B], ln[k * B:(k + 1) * B], ts[k * B:(k + 1) * B]) for k in range(12)]
+    failed = None
+    with native.FsxContext(**cfg) as cu:
+        for j, b in enumerate(batches):
+            try:
+                cu.verdict_batch(*b)
+            except lib.FsxError as e:
+                assert e.code == -errno.ENOSPC
+                failed = j
+                break
+        assert failed is not None and failed >= 2, failed
+        o = oracle.Oracle(**{k: v for k, v in cfg.items() if k != "max_batch"})
+        for b in batches[:failed]:
+            o.batch(*b)
+        with native.FsxContext(**cfg) as cp:
+            cp.set_pipeline(True)
+            d = [(_dev(torch, h), _dev(torch, l), _dev(torch, t), torch.empty(B, dtype=torch.uint8, device="cuda"))
+                 for h, l, t in batches]
+            raised = False
+            for x in d:
+                try:
+                    cp.verdict_batch_device(x[0].data_ptr(), x[1].data_ptr(), x[2].data_ptr(), B, x[3].data_ptr())
+                except lib.FsxError as e:
+                    assert e.code == -errno.ENOSPC
+                    raised = True
+                    break
+            if not raised:
+                with pytest.raises(lib.FsxError) as e:
+                    cp.sync()
+                assert e.value.code == -errno.ENOSPC
+            cp.sync()
+            assert cp.stats() == cu.stats() == o.stats()
+            for m in MAPS:
+                assert cp.map_dump(m) == cu.map_dump(m) == o.map_dump(m), m
