@@ -2009,18 +2009,23 @@ __device__ __forceinline__ void walk_short(const SV &sv, const BatchState *bs,
                                            uint8_t *marks, Slot *table, const Limits &lim,
                                            const HeavyLists &H, const SlotKeys &K) {
     const uint32_t nshort = bs->nseg - cls[kSegClasses - 1];
+    // (a batch without new sources loads no heads: warm streams keep their walker as it was)
+    const bool knew = K.heads && bs->n_new != 0;
     for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < nshort; i += gridDim.x * 256u) {
         const uint32_t g = order[i];
         const uint32_t a = seg_start[g], b = seg_start[g + 1];
         if (H.list && a >= bs->n_light) continue;   // a heavy source: k_walk_heavy
         const uint32_t si = seg_slot[g];
         Slot &sl = table[si];
-        FwState st = load_state(sl);
-        const unsigned long long hd = K.heads ? K.heads[si] : 0ull;
+        const SlotLine L0 = load_line(sl);
+        FwState st = state_of(L0);
+        const uint32_t flags0 = L0.q[0].y;
+        const bool fresh = knew && tag_of(L0) == 0;
+        const unsigned long long hd = knew ? K.heads[si] : 0ull;
         MarkWriter<false> mw{marks, 0};
         walk_fixed_exact_thread(sv, a, b, lim, mw, st);
-        store_state(sl, st);
-        if (K.heads && sl.tag == 0) slot_adopt(sl, K, si, hd);
+        if (fresh) store_new_line(sl, st, K, si, hd);
+        else store_state_f(sl, st, flags0);
     }
 }
 
@@ -2054,22 +2059,26 @@ __device__ __forceinline__ void walk_long(const SV &sv, const BatchState *bs,
     const bool glob_fast = fast_ok(bs, lim);
     const uint32_t maxL = bs->max_len;
     const uint32_t wave = blockIdx.x * 4u + (threadIdx.x >> 6);
+    const bool knew = K.heads && bs->n_new != 0;
     for (uint32_t i = wave; i < nl; i += gridDim.x * 4u) {
         const uint32_t g = order[first + i];
         const uint32_t a = seg_start[g], b = seg_start[g + 1];
         if (H.list && a >= bs->n_light) continue;   // a heavy source: k_walk_heavy
         const uint32_t si = seg_slot[g];
         Slot &sl = table[si];
-        FwState st = load_state(sl);
-        const unsigned long long hd = K.heads ? K.heads[si] : 0ull;
+        const SlotLine L0 = load_line(sl);
+        FwState st = state_of(L0);
+        const uint32_t flags0 = L0.q[0].y;
+        const bool fresh = knew && tag_of(L0) == 0;
+        const unsigned long long hd = knew ? K.heads[si] : 0ull;
         const bool fast = glob_fast && (!st.has_st || (st.tt <= ~0ull - lim.window &&
                                                        st.pps < kBig && st.bps < kBig));
         MarkWriter<true> mw{marks, 0};
         if (fast) walk_fixed_fast<true>(sv, a, b, lim, maxL, mw, st);
         else walk_fixed_exact_wave(sv, a, b, lim, mw, st);
         if (lane_id() == 0) {
-            store_state(sl, st);
-            if (K.heads && sl.tag == 0) slot_adopt(sl, K, si, hd);
+            if (fresh) store_new_line(sl, st, K, si, hd);
+            else store_state_f(sl, st, flags0);
         }
     }
 }

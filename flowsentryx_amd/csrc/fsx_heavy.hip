@@ -187,8 +187,18 @@ __device__ __forceinline__ uint64_t sum_len(const HeavyView &sv, uint32_t lo, ui
     const uint32_t ta = ia / (uint32_t)kSortTile, tb = ib / (uint32_t)kSortTile;
     if (ta == tb) return sv.tile_len_sum(ta, ia, ib);
     uint64_t s = sv.tile_len_sum(ta, ia, ~0u) + sv.tile_len_sum(tb, 0, ib);
+    // the tiles in between from their sums, eight loads in flight per lane (a heavy source
+    // spans up to every tile: one dependent load per 64 tiles made this the walker's long pole)
     uint64_t mid = 0;
-    for (uint32_t t = ta + 1 + lane_id(); t < tb; t += 64u) mid += sv.rec[t].s1[sv.h];
+    uint32_t t = ta + 1 + lane_id();
+    for (; t + 7u * 64u < tb; t += 8u * 64u) {
+        uint32_t x[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) x[u] = sv.rec[t + (uint32_t)u * 64u].s1[sv.h];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) mid += x[u];
+    }
+    for (; t < tb; t += 64u) mid += sv.rec[t].s1[sv.h];
     return s + wave_sum(mid);
 }
 

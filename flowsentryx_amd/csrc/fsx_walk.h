@@ -140,6 +140,25 @@ __device__ __forceinline__ void walk_fixed_fast(const SV &sv, uint32_t a, uint32
     if (touched) s.bps = bps_base + sum_len<kWave>(sv, ep_lo, ep_hi);
 }
 
+// The whole slot line in four 16-byte loads: the walkers' state and the tag (0: a new
+// source under lazy initialisation), one memory instruction per quarter instead of one per
+// field (a flood's walker is bound by the per-segment memory operations).
+struct SlotLine {
+    uint4 q[4];
+};
+__device__ __forceinline__ SlotLine load_line(const Slot &sl) {
+    const uint4 *p = reinterpret_cast<const uint4 *>(&sl);
+    return SlotLine{{p[0], p[1], p[2], p[3]}};
+}
+__device__ __forceinline__ uint64_t u64_of(uint32_t lo, uint32_t hi) { return (uint64_t)hi << 32 | lo; }
+// field offsets: tag 0, flags 4, key 8..23, pps 24, bps 32, tt 40, till 48, aux 56
+__device__ __forceinline__ FwState state_of(const SlotLine &L) {
+    const uint32_t flags = L.q[0].y;
+    return FwState{(flags & SLOT_HAS_ST) != 0, (flags & SLOT_HAS_BL) != 0, u64_of(L.q[1].z, L.q[1].w),
+                   u64_of(L.q[2].x, L.q[2].y), u64_of(L.q[2].z, L.q[2].w), u64_of(L.q[3].x, L.q[3].y)};
+}
+__device__ __forceinline__ uint32_t tag_of(const SlotLine &L) { return L.q[0].x; }
+
 __device__ __forceinline__ FwState load_state(const Slot &sl) {
     return FwState{(sl.flags & SLOT_HAS_ST) != 0, (sl.flags & SLOT_HAS_BL) != 0, sl.pps, sl.bps,
                    sl.tt, sl.till};
@@ -166,6 +185,28 @@ __device__ __forceinline__ void slot_adopt(Slot &sl, const SlotKeys &K, uint32_t
         sl.key[3] = K.k6[(size_t)i * 4 + 2];
     }
     sl.tag = tag;
+}
+
+// A new source's first state (lazy slots): the whole line in four 16-byte stores — family
+// and key from its head h (and the IPv6 key words), the state, aux 0, no born stamp.
+__device__ __forceinline__ void store_new_line(Slot &sl, const FwState &s, const SlotKeys &K, uint32_t i,
+                                               unsigned long long h) {
+    const uint32_t tag = (uint32_t)(h >> 32) & 0xFFu;
+    uint32_t k1 = 0, k2 = 0, k3 = 0;
+    if (tag == 2) { k1 = K.k6[(size_t)i * 4 + 0]; k2 = K.k6[(size_t)i * 4 + 1]; k3 = K.k6[(size_t)i * 4 + 2]; }
+    const uint32_t flags = (s.has_st ? SLOT_HAS_ST : 0u) | (s.has_bl ? SLOT_HAS_BL : 0u);
+    uint4 *p = reinterpret_cast<uint4 *>(&sl);
+    p[0] = make_uint4(tag, flags, (uint32_t)h, k1);
+    p[1] = make_uint4(k2, k3, (uint32_t)s.pps, (uint32_t)(s.pps >> 32));
+    p[2] = make_uint4((uint32_t)s.bps, (uint32_t)(s.bps >> 32), (uint32_t)s.tt, (uint32_t)(s.tt >> 32));
+    p[3] = make_uint4((uint32_t)s.till, (uint32_t)(s.till >> 32), 0u, 0u);
+}
+
+// store_state with the slot's flags as loaded (no re-read)
+__device__ __forceinline__ void store_state_f(Slot &sl, const FwState &s, uint32_t flags0) {
+    sl.flags = (flags0 & kFlagBits & ~(SLOT_HAS_ST | SLOT_HAS_BL)) | (s.has_st ? SLOT_HAS_ST : 0u) |
+               (s.has_bl ? SLOT_HAS_BL : 0u);
+    sl.pps = s.pps; sl.bps = s.bps; sl.tt = s.tt; sl.till = s.till;
 }
 
 __device__ __forceinline__ void store_state(Slot &sl, const FwState &s) {

@@ -202,7 +202,7 @@ const char *fsx_last_error(const fsx_ctx *ctx);
 int fsx_set_stream(fsx_ctx *ctx, void *hip_stream);
 /* Wait for enqueued device work and report deferred device-side errors. */
 int fsx_sync(fsx_ctx *ctx);
-/* Batch pipelining (default off; DESIGN.md §3 "Pipelined batches"). When on, a fixed-window
+/* Batch pipelining (default off; DESIGN.md §3 "Pipelined batches"). When on, a limiter
  * fsx_verdict_batch_device / fsx_process_batch_device call enqueues the batch's front
  * (parse, sort) on the context stream and its tail (walkers, verdicts, flows) on the
  * context's own side streams, so the next batch's front overlaps this batch's tail; results
@@ -212,8 +212,10 @@ int fsx_sync(fsx_ctx *ctx);
  * outputs after fsx_sync (or any other entry point, which orders the context stream after
  * the last tail). A failed batch cancels the batch after it; the error (e.g. -ENOSPC) is
  * returned by fsx_sync or by the call that found it, which enqueues nothing, and neither
- * failed batch changes any map. Other limiters and record mode run each batch whole on the
- * context stream (no overlap, but still no host synchronization per call); so does every
+ * failed batch changes any map (all three limiters; a sliding-window batch whose history
+ * does not fit fails with -ENOSPC when its tail starts). Record mode and the overflow
+ * admission flag run each batch whole on the context stream (no overlap, but still no host
+ * synchronization per call); so does every
  * batch with on = 2 (a caller that reuses input buffers in stream order); timed batches
  * (fsx_enable_timing) run unpipelined. on = 0 turns it off. */
 int fsx_set_pipeline(fsx_ctx *ctx, int on);
