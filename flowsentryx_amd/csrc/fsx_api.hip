@@ -917,10 +917,14 @@ static int evict_idle(fsx_ctx *c, const PacketIn &in, const uint64_t *d_ts, size
     return 0;
 }
 
-// Split pipelining for every limiter (round 4; FSX_SPLIT_FIXED_ONLY=1: the fixed window only,
-// the others whole on the context stream, A/B)
+// Split pipelining for the fixed and the sliding window (round 4; FSX_SPLIT_FIXED_ONLY=1: the
+// fixed window only). The token bucket runs each batch whole on the context stream: split, its
+// tail (two tile scans and the flows over every position) beside the next front measured
+// 4.73 vs 4.39 ms per step (profiles/r04/ab_r04t_token.txt; FSX_SPLIT_TOKEN=1: split, A/B).
 static bool no_split_limiters(const fsx_ctx *c) {
     static const bool fixed_only = getenv("FSX_SPLIT_FIXED_ONLY") != nullptr;
+    static const bool split_token = getenv("FSX_SPLIT_TOKEN") != nullptr;
+    if (c->cfg.limiter == FSX_LIMIT_TOKEN_BUCKET) return !split_token;
     return fixed_only && c->cfg.limiter != FSX_LIMIT_FIXED_WINDOW;
 }
 

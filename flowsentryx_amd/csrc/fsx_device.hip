@@ -2684,12 +2684,14 @@ hipError_t launch_tail(const TailArgs &a) {
     k_fill_last<<<gridTiles, 256, 0, st>>>(sc.marks, bs, sc.tile_last, tagh ? 1u : 0u);
     k_fill_carry<<<1, 1024, 0, st>>>(sc.tile_last, bs, tagh ? 1u : 0u);
     mark("k_fill_last");
-    // (DROPs stored straight into the verdicts; FSX_DROP_LISTS=1: per-chunk lists that
-    // k_verdict_apply merges, A/B)
+    // Light DROPs (heavy verdict lists on: the rest are lists) stored straight into the
+    // verdicts: config 4's 12.8M light DROPs 1.11 -> 0.32 ms. Without heavy lists (the token
+    // bucket: about every other packet a DROP) per-chunk lists that k_verdict_apply merges:
+    // 33M scattered byte stores took 0.44 ms and 1.15 GB. (FSX_DROP_LISTS=1: lists always.)
     static const bool drop_lists = getenv("FSX_DROP_LISTS") != nullptr;
     k_fill_scatter<<<gridTiles, 256, 0, st>>>(sc.marks, S, bs, sc.tile_last, sc.drop_list, sc.drop_cur,
                                               tstate, cdiv(n, kVChunk), tagh ? 1u : 0u,
-                                              drop_lists ? nullptr : verdict);
+                                              drop_lists || !tagh ? nullptr : verdict);
     mark("k_fill_scatter");
     if (heavy_join && (e = hipStreamWaitEvent(st, walk_join_ev, 0)) != hipSuccess) return e;
     k_verdict_apply<<<cdiv(n, kVChunk), 256, 0, st>>>(verdict, n, sc.drop_list, sc.drop_cur, bs, sc.heavy,

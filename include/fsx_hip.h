@@ -202,8 +202,8 @@ const char *fsx_last_error(const fsx_ctx *ctx);
 int fsx_set_stream(fsx_ctx *ctx, void *hip_stream);
 /* Wait for enqueued device work and report deferred device-side errors. */
 int fsx_sync(fsx_ctx *ctx);
-/* Batch pipelining (default off; DESIGN.md §3 "Pipelined batches"). When on, a limiter
- * fsx_verdict_batch_device / fsx_process_batch_device call enqueues the batch's front
+/* Batch pipelining (default off; DESIGN.md §3 "Pipelined batches"). When on, a fixed- or
+ * sliding-window fsx_verdict_batch_device / fsx_process_batch_device call enqueues the batch's front
  * (parse, sort) on the context stream and its tail (walkers, verdicts, flows) on the
  * context's own side streams, so the next batch's front overlaps this batch's tail; results
  * and map state are exactly those of the same calls without pipelining. Up to three batches
@@ -212,8 +212,8 @@ int fsx_sync(fsx_ctx *ctx);
  * outputs after fsx_sync (or any other entry point, which orders the context stream after
  * the last tail). A failed batch cancels the batch after it; the error (e.g. -ENOSPC) is
  * returned by fsx_sync or by the call that found it, which enqueues nothing, and neither
- * failed batch changes any map (all three limiters; a sliding-window batch whose history
- * does not fit fails with -ENOSPC when its tail starts). Record mode and the overflow
+ * failed batch changes any map (a sliding-window batch whose history does not fit fails
+ * with -ENOSPC when its tail starts). The token bucket, record mode and the overflow
  * admission flag run each batch whole on the context stream (no overlap, but still no host
  * synchronization per call); so does every
  * batch with on = 2 (a caller that reuses input buffers in stream order); timed batches
