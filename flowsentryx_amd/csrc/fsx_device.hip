@@ -478,10 +478,12 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
                                                uint32_t *__restrict__ thist, uint32_t tcap,
                                                DigitPlan dp, const HeavySet *__restrict__ heavy,
                                                RuleSet rules, uint32_t tagh,
-                                               uint32_t *__restrict__ chunk_cnt) {
+                                               uint32_t *__restrict__ chunk_cnt,
+                                               uint64_t *__restrict__ lmask) {
     // kHf (unsorted heavy sources): no timestamp loads (k_pass0h reads them),
     // no sort word for a heavy source's packet (its verdict byte carries 0x80 | h), the light
-    // sort words compacted per 1024-packet chunk (wave) with their count in chunk_cnt
+    // sort words compacted per 1024-packet chunk (wave) with their count in chunk_cnt and
+    // the light-packet mask of every 64-packet step in lmask
     static_assert(!kHf || !kRules, "unsorted heavy sources: no prefix rules");
     __shared__ uint32_t s_rec[4][64 * 17];
     __shared__ uint32_t s_red[4][3];
@@ -776,6 +778,7 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
         uint32_t lpos = 0;
         if constexpr (kHf) {
             const uint64_t lm = __ballot(c_tag != 0 && c_hidx < 0);
+            if (lane == 0 && t < ntiles) lmask[t] = lm;
             lpos = ((t >> 4) << 10) + crun + (uint32_t)__popcll(lm & lt_mask);
             crun += (uint32_t)__popcll(lm);
         }
@@ -1159,9 +1162,18 @@ __global__ __launch_bounds__(256, kLatePay ? FSX_SCATTER_MINB : 1) void k_tile_s
 //      the last lane below it with the same h (eight ballots), else the wave's last packet
 //      of h in an earlier row; the waves' chunks are joined at the tile end;
 //   2. pass 0 of the light sort words, which k_parse compacted per chunk (chunk_cnt): the
-//      stable in-tile ranking of sort_tile, payload words gathered by arrival index (their
-//      lines were just read in step 1).
-__global__ __launch_bounds__(256, FSX_SCATTER_MINB) void k_pass0h(const uint64_t *__restrict__ in,
+//      stable in-tile ranking of sort_tile. The payload words come from step 1's registers:
+//      the chunk's light words mark their packets in an LDS bitmap, every lane compacts the
+//      payload words of its light packets into the wave's LDS row, and light word j of the
+//      chunk takes entry j (k_parse compacted them in arrival order). (Gathering them from
+//      ts / len by arrival index missed L2 beside the tail kernels: 0.8 GB per batch.)
+#ifndef FSX_PASS0H_GATHER
+#define FSX_PASS0H_GATHER 0   // 1: the payload words gathered from ts / len (A/B)
+#endif
+#ifndef FSX_PASS0H_MINB
+#define FSX_PASS0H_MINB FSX_SCATTER_MINB
+#endif
+__global__ __launch_bounds__(256, FSX_PASS0H_MINB) void k_pass0h(const uint64_t *__restrict__ in,
                                                                   uint64_t *__restrict__ out, uint32_t n,
                                                                   uint32_t shift, uint32_t dmask,
                                                                   const uint32_t *__restrict__ offs, uint32_t tcap,
@@ -1170,6 +1182,7 @@ __global__ __launch_bounds__(256, FSX_SCATTER_MINB) void k_pass0h(const uint64_t
                                                                   const uint32_t *__restrict__ len,
                                                                   const uint8_t *__restrict__ tags,
                                                                   const uint32_t *__restrict__ chunk_cnt,
+                                                                  const uint64_t *__restrict__ lmask,
                                                                   HeavyTileRec *__restrict__ rec,
                                                                   const HeavySet *__restrict__ hs) {
     __shared__ unsigned long long s_el[kSortTile];
@@ -1217,6 +1230,7 @@ __global__ __launch_bounds__(256, FSX_SCATTER_MINB) void k_pass0h(const uint64_t
         Lr[r] = len[live ? i : 0u];
         Gr[r] = live ? tags[i] : 0u;
     }
+    uint64_t Pr[16];   // the payload words of the lane's packets (step 2)
 #pragma unroll
     for (uint32_t r = 0; r < 16; ++r) {
         const uint32_t i = c0 + r * 64u + lane;
@@ -1263,6 +1277,13 @@ __global__ __launch_bounds__(256, FSX_SCATTER_MINB) void k_pass0h(const uint64_t
             wave_lds_order();
         }
     }
+#pragma unroll
+    for (uint32_t r = 0; r < 16; ++r) Pr[r] = ((Tr[r] - tb) << kPayLenBits) | Lr[r];
+    // the chunk's light-packet masks (k_parse; wave-uniform: scalar loads)
+    const uint32_t s0 = __builtin_amdgcn_readfirstlane(c0 >> 6);
+    uint64_t Mr[16];
+#pragma unroll
+    for (uint32_t r = 0; r < 16; ++r) Mr[r] = !FSX_PASS0H_GATHER && (s0 + r) * 64u < n ? lmask[s0 + r] : 0ull;
     nonmono = __ballot(nonmono != 0) ? 1u : 0u;
     mx = wave_max(mx);
     imn = wave_max(imn);
@@ -1303,6 +1324,18 @@ __global__ __launch_bounds__(256, FSX_SCATTER_MINB) void k_pass0h(const uint64_t
         atomicMax(reinterpret_cast<unsigned long long *>(&bs->inv_min_ts), (unsigned long long)im);
     }
     __syncthreads();
+    // the payload words of the chunk's light packets in arrival order: row w * 1024 + j of s_el
+    // (light word j of the chunk is its j-th light packet)
+    unsigned long long *row = s_el + w * 1024u;
+    if constexpr (!FSX_PASS0H_GATHER) {
+        uint32_t run = 0;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const uint64_t m = Mr[r];
+            if ((m >> lane) & 1ull) row[run + (uint32_t)__popcll(m & lt_mask)] = Pr[r];
+            run += (uint32_t)__popcll(m);
+        }
+    }
     // ---- 2. pass 0 of the tile's light words (sort_tile, keys from the chunk runs)
 #pragma unroll
     for (int k = 0; k < 4; ++k) s_wc[w][lane * 4 + k] = 0;
@@ -1328,6 +1361,12 @@ __global__ __launch_bounds__(256, FSX_SCATTER_MINB) void k_pass0h(const uint64_t
         if (valid && below == 0) base = atomicAdd(&s_wc[w][d], (uint32_t)__popcll(peers));
         base = __shfl(base, __ffsll((unsigned long long)peers) - 1);
         lr[r] = valid ? base + below : 0xFFFFFFFFu;
+    }
+    uint64_t pv[kSortItems];   // payload words (ts - ts[0]) << kPayLenBits | len (k_hmode: pay_ok)
+    if constexpr (!FSX_PASS0H_GATHER) {
+#pragma unroll
+        for (int r = 0; r < kSortItems; ++r)
+            pv[r] = lr[r] != 0xFFFFFFFFu ? row[(uint32_t)r * 64u + lane] : 0ull;
     }
     __syncthreads();
     const uint32_t d = tid;
@@ -1360,16 +1399,15 @@ __global__ __launch_bounds__(256, FSX_SCATTER_MINB) void k_pass0h(const uint64_t
             out[dst[m]] = x;
         }
     }
-    // payload words (ts - ts[0]) << kPayLenBits | len, gathered by arrival index (k_hmode
-    // decides whether they are exact: pay_ok)
-    uint64_t pv[kSortItems];
+    if constexpr (FSX_PASS0H_GATHER) {   // (A/B: gathered by arrival index)
 #pragma unroll
-    for (int r = 0; r < kSortItems; ++r) {
-        if (lr[r] != 0xFFFFFFFFu) {
-            const uint32_t i = pk_idx(v[r]);
-            pv[r] = ((ts[i] - tb) << kPayLenBits) | len[i];
-        } else {
-            pv[r] = 0;
+        for (int r = 0; r < kSortItems; ++r) {
+            if (lr[r] != 0xFFFFFFFFu) {
+                const uint32_t i = pk_idx(v[r]);
+                pv[r] = ((ts[i] - tb) << kPayLenBits) | len[i];
+            } else {
+                pv[r] = 0;
+            }
         }
     }
     __syncthreads();
@@ -1386,10 +1424,10 @@ __global__ __launch_bounds__(256, FSX_SCATTER_MINB) void k_pass0h(const uint64_t
 
 hipError_t launch_pass0h(const uint64_t *in, uint64_t *out, uint32_t n, uint32_t shift, uint32_t dmask,
                          const uint32_t *offs, uint32_t tcap, BatchState *bs, uint64_t *pout, const uint64_t *ts,
-                         const uint32_t *len, const uint8_t *tags, const uint32_t *chunk_cnt, void *rec,
-                         const HeavySet *hs, hipStream_t st) {
+                         const uint32_t *len, const uint8_t *tags, const uint32_t *chunk_cnt,
+                         const uint64_t *lmask, void *rec, const HeavySet *hs, hipStream_t st) {
     const uint32_t ntiles = std::max<uint32_t>(1, (n + kSortTile - 1) / kSortTile);
-    k_pass0h<<<ntiles, 256, 0, st>>>(in, out, n, shift, dmask, offs, tcap, bs, pout, ts, len, tags, chunk_cnt,
+    k_pass0h<<<ntiles, 256, 0, st>>>(in, out, n, shift, dmask, offs, tcap, bs, pout, ts, len, tags, chunk_cnt, lmask,
                                      static_cast<HeavyTileRec *>(rec), hs);
     return hipGetLastError();
 }
@@ -2848,14 +2886,15 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
         const uint32_t g = std::min<uint32_t>(256u * FSX_PARSE_MINB, ntiles);   // one resident block per slot
         const HeavySet *hs = heavy_sort ? sc.heavy : nullptr;
         uint32_t *th = onesweep ? nullptr : sc.hist;
+        uint64_t *lmask = light_masks(sc.chunk_cnt, sc.cap);
         // the prefix rules apply to limiter batches (an instantiation of its own, so the
         // rule-free parse keeps its registers)
         const bool rl = do_limit && rules.slot;
         // (kMir: light IPv4 sources probe the persistent index's mirror, not its heads)
 #define FSX_PARSE(R, Q, H) (idt.mir ? k_parse<R, Q, true, H><<<g, 256, 0, st>>>(in, len, ts, n, sc.packed[0], verdict, bs, pidt, \
-                                                        sc.sort_ctl, th, tcap, dp, hs, rules, tagh ? 1u : 0u, sc.chunk_cnt) \
+                                                        sc.sort_ctl, th, tcap, dp, hs, rules, tagh ? 1u : 0u, sc.chunk_cnt, lmask) \
                                  : k_parse<R, Q, false, H><<<g, 256, 0, st>>>(in, len, ts, n, sc.packed[0], verdict, bs, pidt, \
-                                                        sc.sort_ctl, th, tcap, dp, hs, rules, tagh ? 1u : 0u, sc.chunk_cnt))
+                                                        sc.sort_ctl, th, tcap, dp, hs, rules, tagh ? 1u : 0u, sc.chunk_cnt, lmask))
         if (hfm)
             !in.rec ? FSX_PARSE(0, false, true) : in.rec_bytes == 16 ? FSX_PARSE(16, false, true) : FSX_PARSE(32, false, true);
         else if (!in.rec)
@@ -2921,7 +2960,8 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
             if (pass == 0 && (e = tail_hook(1)) != hipSuccess) return e;
             if (pass == 0 && hfm) {   // light words from the parse chunks; heavy tile sums; the path
                 if ((e = launch_pass0h(in, out, n, shift, pmask, sc.hist, tcap, bs, pout, ts, len, verdict,
-                                       sc.chunk_cnt, sc.hrec, sc.heavy, st)) != hipSuccess)
+                                       sc.chunk_cnt, light_masks(sc.chunk_cnt, sc.cap), sc.hrec, sc.heavy,
+                                       st)) != hipSuccess)
                     return e;
                 mark("k_pass0h");
                 if ((e = launch_hmode(bs, ts, n, sc.heavy, table, lim, st)) != hipSuccess) return e;

@@ -408,7 +408,13 @@ struct HeavyTileRec {
 };
 constexpr uint32_t kHGroupTiles = 64;    // tiles per k_hflow_combine group
 inline size_t heavy_rec_bytes(uint64_t cap) { return (cap / kSortTile + 2) * sizeof(HeavyTileRec); }
-inline size_t chunk_cnt_bytes(uint64_t cap) { return (cap / 1024 + 8) * 4; }
+// ... followed (16-byte aligned) by the light-packet mask of every 64-packet parse step
+// (k_parse's ballot; k_pass0h compacts the light packets' payload words by it)
+inline size_t chunk_cnt_head(uint64_t cap) { return ((cap / 1024 + 8) * 4 + 15) / 16 * 16; }
+inline size_t chunk_cnt_bytes(uint64_t cap) { return chunk_cnt_head(cap) + (cap / 64 + 8) * 8; }
+inline uint64_t *light_masks(uint32_t *chunk_cnt, uint64_t cap) {
+    return reinterpret_cast<uint64_t *>(reinterpret_cast<char *>(chunk_cnt) + chunk_cnt_head(cap));
+}
 
 // Flow partials (fsx_flow_partials_records_device): every source's raw sums go to the run of
 // its owner rank (G runs of cap partials, cnt[o] per run) instead of a row.
@@ -575,7 +581,8 @@ hipError_t launch_flows_heavy_finish(const uint64_t *S, const BatchState *bs, co
 // Heavy sources outside the sort (fsx_heavy.hip; k_pass0h in fsx_device.hip), DESIGN.md §3.
 hipError_t launch_pass0h(const uint64_t *in, uint64_t *out, uint32_t n, uint32_t shift, uint32_t dmask,
                          const uint32_t *offs, uint32_t tcap, BatchState *bs, uint64_t *pout, const uint64_t *ts,
-                         const uint32_t *len, const uint8_t *tags, const uint32_t *chunk_cnt, void *rec,
+                         const uint32_t *len, const uint8_t *tags, const uint32_t *chunk_cnt,
+                         const uint64_t *lmask, void *rec,
                          const HeavySet *hs, hipStream_t st);
 hipError_t launch_hmode(BatchState *bs, const uint64_t *ts, uint32_t n, const HeavySet *hs, const Slot *table,
                         const Limits &lim, hipStream_t st);
