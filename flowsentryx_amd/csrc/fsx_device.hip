@@ -513,6 +513,8 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
     __syncthreads();
     uint32_t *rec = s_rec[w];
     uint32_t any6 = 0, nonmono = 0, maxlen = 0, nfresh = 0, nrule = 0;
+    // the high word's kFreshBit for an inserting packet (lazy slots, no heavy-source sort)
+    const uint32_t fresh_hi = __builtin_amdgcn_readfirstlane(!idt.init && !dp.light_b ? 0x80000000u : 0u);
     uint64_t maxts = 0, inv_mints = 0;  // ~min ts, max-reduced
     // a block owns whole 4096-record sort tiles (so it can emit pass 0's per-tile digit
     // counts: no k_tile_hist for pass 0); wave w parses records [w*1024, +1024) of the
@@ -626,7 +628,7 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
                                                                    __HIP_MEMORY_SCOPE_AGENT);
                 const uint32_t id = id_resolve<kMir>(idt, tag, k, h, hint, &fresh);
                 if (id == kNoSlot) atomicOr(&bs->err, ERR_TABLE_FULL);
-                const uint64_t out = word_of(id, tag, i, hidx);
+                const uint64_t out = word_of(id, tag, i, hidx) | (uint64_t)(fresh ? fresh_hi : 0u) << 32;
                 if constexpr (kHf) {
                     if (hidx < 0) packed[q[5]] = out;
                 } else {
@@ -1539,7 +1541,7 @@ __global__ __launch_bounds__(256) void k_heads_count(const uint64_t *__restrict_
             uint64_t prev = __shfl_up(cur[k], 1);
             if (lane == 0 && p > 0 && p < M) prev = S[p - 1];
             if (p < M) {
-                const bool h = p == 0 || (prev >> kIdShift) != (cur[k] >> kIdShift);
+                const bool h = p == 0 || ((prev ^ cur[k]) & ~kFreshBit) >> kIdShift != 0;
                 headf[p] = h ? 1u : 0u;
                 cnt += h;
                 sub[k >> 2] += h;
@@ -1996,14 +1998,24 @@ __device__ __forceinline__ void seg_classes_pass(const uint32_t *seg_start, uint
     }
 }
 
+// Every segment one packet (a carpet of new sources, config 5): class 0 throughout, the
+// order the identity (no seg_start reads).
+__device__ __forceinline__ bool seg_all_single(const BatchState *bs) {
+    return bs->nseg == bs->n_valid && bs->n_light == bs->n_valid;
+}
+
 __global__ __launch_bounds__(256) void k_seg_count(const BatchState *bs,
                                                    const uint32_t *__restrict__ seg_start,
                                                    uint32_t *__restrict__ blk, uint32_t short_seg) {
     __shared__ uint32_t sh[kSegClasses];
-    if (threadIdx.x < kSegClasses) sh[threadIdx.x] = 0;
-    __syncthreads();
     uint32_t lo, hi;
     seg_chunk(bs->nseg, blockIdx.x, lo, hi);
+    if (seg_all_single(bs)) {
+        if (threadIdx.x < kSegClasses) blk[threadIdx.x * kSegBlocks + blockIdx.x] = threadIdx.x == 0 ? hi - lo : 0u;
+        return;
+    }
+    if (threadIdx.x < kSegClasses) sh[threadIdx.x] = 0;
+    __syncthreads();
     seg_classes_pass<false>(seg_start, lo, hi, short_seg, sh, nullptr);
     __syncthreads();
     if (threadIdx.x < kSegClasses) blk[threadIdx.x * kSegBlocks + blockIdx.x] = sh[threadIdx.x];
@@ -2033,10 +2045,14 @@ __global__ __launch_bounds__(256) void k_seg_order(const BatchState *bs,
                                                    const uint32_t *__restrict__ blk,
                                                    uint32_t *__restrict__ order, uint32_t short_seg) {
     __shared__ uint32_t cur[kSegClasses];
-    if (threadIdx.x < kSegClasses) cur[threadIdx.x] = blk[threadIdx.x * kSegBlocks + blockIdx.x];
-    __syncthreads();
     uint32_t lo, hi;
     seg_chunk(bs->nseg, blockIdx.x, lo, hi);
+    if (seg_all_single(bs)) {   // (block b's class-0 cursor is lo)
+        for (uint32_t g = lo + threadIdx.x; g < hi; g += 256u) order[g] = g;
+        return;
+    }
+    if (threadIdx.x < kSegClasses) cur[threadIdx.x] = blk[threadIdx.x * kSegBlocks + blockIdx.x];
+    __syncthreads();
     seg_classes_pass<true>(seg_start, lo, hi, short_seg, cur, order);
 }
 
@@ -2049,12 +2065,23 @@ __device__ __forceinline__ void walk_short(const SV &sv, const BatchState *bs,
     const uint32_t nshort = bs->nseg - cls[kSegClasses - 1];
     // (a batch without new sources loads no heads: warm streams keep their walker as it was)
     const bool knew = K.heads && bs->n_new != 0;
+    // mostly new sources (a flood, config 5): a segment whose first word carries kFreshBit
+    // has a slot this batch claimed, written whole without reading it
+    const bool flood = knew && K.fresh_bit && 2ull * bs->n_new > bs->nseg;
     for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < nshort; i += gridDim.x * 256u) {
         const uint32_t g = order[i];
         const uint32_t a = seg_start[g], b = seg_start[g + 1];
         if (H.list && a >= bs->n_light) continue;   // a heavy source: k_walk_heavy
         const uint32_t si = seg_slot[g];
         Slot &sl = table[si];
+        if (flood && (sv.S[a] & kFreshBit)) {
+            const unsigned long long hd = K.heads[si];
+            FwState st{false, false, 0, 0, 0, 0};
+            MarkWriter<false> mw{marks, 0};
+            walk_fixed_exact_thread(sv, a, b, lim, mw, st);
+            store_new_line(sl, st, K, si, hd);
+            continue;
+        }
         const SlotLine L0 = load_line(sl);
         FwState st = state_of(L0);
         const uint32_t flags0 = L0.q[0].y;
@@ -2555,7 +2582,7 @@ hipError_t launch_tail(const TailArgs &a) {
     const HeavyLists hlists{tagh ? reinterpret_cast<uint32_t *>(sc.packed[0]) : nullptr, sc.heavy,
                             tstate, bs};
     // (lazy slots: the fixed window's walkers write a new source's family and key)
-    const SlotKeys skeys{a.lazy ? a.X.heads : nullptr, a.X.k6};
+    const SlotKeys skeys{a.lazy ? a.X.heads : nullptr, a.X.k6, a.lazy && a.fresh_bit ? 1u : 0u};
     // the heavy runs' walker and flow sums, forked right after the sort (A/B, config 2: right
     // after pass 0 they slowed passes 1-2, after the heads they delayed the walkers; a fourth
     // stream shared a hardware queue with the limiter chain)
@@ -2989,7 +3016,7 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
     if (split) ta.sp = *split;
     ta.npass = npass; ta.tagh = tagh; ta.gridTiles = gridTiles;
     ta.hfm = hfm; ta.shift0 = dp.shift[0];
-    ta.admit = admit; ta.X = X; ta.id_gen = id_gen; ta.lazy = lazy;
+    ta.admit = admit; ta.X = X; ta.id_gen = id_gen; ta.lazy = lazy; ta.fresh_bit = lazy && !heavy_sort;
     ta.fork = flows && do_limit && st2 && fork_ev && join_ev && !no_fork;
     for (int k = 0; k < 3; ++k) ta.last[k] = last[k];
     if (split && split->tail_out) {

@@ -314,6 +314,10 @@ constexpr uint32_t kIdShift = 31;
 // without it the id may use bits 31..62 (tables of up to 2^32 slots).
 __host__ __device__ inline uint32_t pk_id(uint64_t v, uint64_t id_mask) { return (uint32_t)((v >> kIdShift) & id_mask); }
 __host__ __device__ inline uint32_t pk_idx(uint64_t v) { return (uint32_t)v & 0x7FFFFFFFu; }
+// Without the heavy-source sort no digit reaches bit 63: there it marks the packet that
+// inserted its source in this batch (lazy slots; the walker writes that slot's line without
+// reading it). Segment heads compare the words without it.
+constexpr uint64_t kFreshBit = 1ull << 63;
 
 // ------------------------------------------------------------ launchers (fsx_device.hip)
 // Heavy sources of a batch: up to kHeavyMax source keys picked from a
@@ -506,6 +510,7 @@ struct TailArgs {
     TableIndex X;         // (admission: the persistent index)
     uint32_t id_gen;      // (admission: the batch generation stamped on admitted slots)
     bool lazy;            // k_parse left new sources' slots to the fixed window's walkers
+    bool fresh_bit;       // ... and marked the inserting packets' sort words (kFreshBit)
     uint32_t shift0;      // pass 0's bucket shift (k_heavy_gather's sort words)
     FlowRequest fq;
     HistBufs hist;

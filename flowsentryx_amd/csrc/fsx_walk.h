@@ -172,6 +172,7 @@ __device__ __forceinline__ FwState load_state(const Slot &sl) {
 struct SlotKeys {
     const unsigned long long *heads;
     const uint32_t *k6;
+    uint32_t fresh_bit = 0;   // sort words carry kFreshBit (fsx_internal.h)
 };
 
 // h: the slot's head, loaded beside the slot's state (a load issued after the walk would
