@@ -1126,7 +1126,7 @@ __device__ __forceinline__ void sort_tile(uint32_t t, const uint64_t *__restrict
 
 constexpr bool kLatePayDefault = true;
 #ifndef FSX_SCATTER_MINB
-#define FSX_SCATTER_MINB 4   // waves/SIMD bound of k_tile_scatter (A/B: scripts/build_variant.sh)
+#define FSX_SCATTER_MINB 3   // waves/SIMD bound of k_tile_scatter (A/B: scripts/build_variant.sh; 4: profiles/r04/ab_r04z.txt)
 #endif
 
 struct TileOffs {

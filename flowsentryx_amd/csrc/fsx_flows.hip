@@ -179,7 +179,7 @@ __device__ __forceinline__ void flow_tiles(const uint64_t *__restrict__ S,
 }
 
 #ifndef FSX_FLOW_TILE_BLOCKS
-#define FSX_FLOW_TILE_BLOCKS 2048   // k_flow_tile grid cap: leaves CU slots to the walkers beside it (4.08 -> 4.05 ms)
+#define FSX_FLOW_TILE_BLOCKS 1024   // k_flow_tile grid cap: leaves CU slots to the walkers and classes beside it (2048: profiles/r04/ab_r04z.txt)
 #endif
 #ifndef FSX_FLOW_MINB
 #define FSX_FLOW_MINB 4   // waves/SIMD bound of k_flow_tile (A/B: scripts/build_variant.sh)
