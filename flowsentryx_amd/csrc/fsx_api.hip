@@ -294,7 +294,7 @@ static hipError_t flush_tail(fsx_ctx *c, hipEvent_t after) {
     return hipEventRecord(c->tail_done[c->tail_par], c->tail_args.fork && end_aux ? c->aux_stream : c->walk_stream);
 }
 
-// PipeSplit::on_parse: the previous batch's tail goes in right after this batch's parse.
+// PipeSplit::on_parse: the previous batch's tail goes in beside this batch's parse (before it by default).
 static hipError_t pipe_on_parse(void *p, hipEvent_t recorded) {
     fsx_ctx *c = static_cast<fsx_ctx *>(p);
     if (!c->tail_pending) return hipSuccess;

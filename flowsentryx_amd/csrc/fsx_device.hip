@@ -2642,7 +2642,9 @@ hipError_t launch_tail(const TailArgs &a) {
         }
     }
     if (split && split->tail && do_limit && lim.limiter == 1) k_sw_tail_check<<<1, 1, 0, st>>>(bs, tstate, lim);
-    // unsorted heavy sources that k_hmode sent back to the run path: their runs first
+    // unsorted heavy sources: their carried state decides the path now that the previous
+    // batch's walkers have stored it; those sent back to the run path get their runs first
+    if (a.hfm && (e = launch_hmode_state(bs, sc.heavy, table, lim, st)) != hipSuccess) return e;
     if (a.hfm && (e = launch_heavy_gather(bs, verdict, ts, len, n, sc.hist, tcap, sc.heavy, a.shift0, lim.table_mask,
                                           S_fin, pay_fin, st)) != hipSuccess)
         return e;
@@ -2842,8 +2844,8 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
     const uint32_t dmask = (1u << dbits) - 1u;
     // Heavy-source sort (tables of <= 2^25 slots): pass 0 buckets the light entries by a
     // low id digit and every heavy source into a bucket of its own (the bucket in bits
-    // [bshift, 64) above the id: 8 bits, light digit 7 bits and 128 heavy sources; for
-    // 25-bit ids 7 bits, light digit 6 bits and 64 heavy sources); the later passes sort
+    // [bshift, 64) above the id: 8 bits, light digit 7 bits and 128 heavy sources for every
+    // id width it takes, up to 25 bits: bshift = 56); the later passes sort
     // the light entries only, by the remaining id bits in equal digits. Pass 0 writes the
     // other sort buffer, which then holds the heavy runs for good (the later passes cover
     // [0, n_light)); with an even pass count the light entries end in the parse buffer, so
@@ -2907,6 +2909,23 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
     // limiters and the admission path initialise slots as they insert.
     static const bool eager = getenv("FSX_EAGER_SLOTS") != nullptr;
     const bool lazy = do_limit && !admit && lim.limiter == 0 && !eager;
+    // pipelined: the previous batch's tail goes in right before this batch's parse, so it
+    // overlaps the parse and the sort (the parse touches the index heads and new sources'
+    // slots only, the previous batch's walkers its own sources' slots; the heavy sources'
+    // carried state is read at the tail's start, k_hmode_state). A/B, FSX_TAIL_AT: -1 before
+    // the parse (default; 2.914 / 2.918 vs 2.937 / 2.939 ms, profiles/r04/ab_r04ab.txt), 0
+    // after it (round 3's default), 1 after the first pass's offsets scan, 2 after the first
+    // scatter (3.46 / 3.77 vs 3.46 ms in round 3).
+    const bool pw = split && split->pro_wait;
+    static const int tail_at = getenv("FSX_TAIL_AT") ? atoi(getenv("FSX_TAIL_AT")) : -1;
+    bool hooked = false;   // (exactly once per pipelined batch: a tail left unhooked would be lost)
+    auto tail_hook = [&](int at) -> hipError_t {
+        if (hooked || !split || !split->on_parse || (at != tail_at && at != 3)) return hipSuccess;
+        hooked = true;
+        // (right after the parse the tail waits on the prologue's event: one marker, not two)
+        return split->on_parse(split->cb, at == 0 && pw ? split->pro_wait : nullptr);
+    };
+    if ((e = tail_hook(-1)) != hipSuccess) return e;
     IdTable pidt = idt;
     if (lazy) pidt.init = 0;
     {
@@ -2935,7 +2954,6 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
     mark("k_parse");
     // (the next batch's prologue may start once this parse has updated the index; recorded
     // after every split batch's parse, also one whose own prologue ran on st)
-    const bool pw = split && split->pro_wait;
     if (pw && (e = hipEventRecord(split->pro_wait, st)) != hipSuccess) return e;
     // Heavy verdict lists: every heavy source is one run of pass 0's output (the later passes
     // write [0, n_light) only) whose segment needs no head search, so its walker and its flow
@@ -2943,17 +2961,6 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
     // like the light flow tiles cover [0, n_light) only (k_heads_heavy appends the heavy
     // segments).
     static const bool no_fork = getenv("FSX_NO_FLOW_FORK") != nullptr;   // A/B: flows serialized
-    // pipelined: the previous batch's tail goes in right after this batch's parse, so it
-    // overlaps the sort (A/B, FSX_TAIL_AT: 0 after the parse (default), 1 after the first
-    // pass's offsets scan (same time: 3.46 ms), 2 after the first scatter (3.77 ms))
-    static const int tail_at = getenv("FSX_TAIL_AT") ? atoi(getenv("FSX_TAIL_AT")) : 0;
-    bool hooked = false;   // (exactly once per pipelined batch: a tail left unhooked would be lost)
-    auto tail_hook = [&](int at) -> hipError_t {
-        if (hooked || !split || !split->on_parse || (at != tail_at && at != 3)) return hipSuccess;
-        hooked = true;
-        // (right after the parse the tail waits on the prologue's event: one marker, not two)
-        return split->on_parse(split->cb, at == 0 && pw ? split->pro_wait : nullptr);
-    };
     if ((e = tail_hook(0)) != hipSuccess) return e;
     k_hist_prep<<<1, 256, 0, st>>>(sc.sort_ctl, sc.gbase, bs, heavy_sort ? dp.light_b : 256u);
     if (do_limit)
@@ -2991,7 +2998,7 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
                                        st)) != hipSuccess)
                     return e;
                 mark("k_pass0h");
-                if ((e = launch_hmode(bs, ts, n, sc.heavy, table, lim, st)) != hipSuccess) return e;
+                if ((e = launch_hmode(bs, ts, n, lim, st)) != hipSuccess) return e;
                 mark("k_hmode");
             } else {
                 k_tile_scatter<kLatePayDefault><<<ntiles, 256, 0, st>>>(in, out, n, Ld, shift, pmask, pass == 0, sc.hist, tcap, bs,

@@ -256,34 +256,39 @@ struct HeavyMarkWriter {
 };
 
 // ------------------------------------------------------------------ k_hmode
-// After k_pass0h (one block of 128 threads): the payload words' validity and the batch's
-// path for its heavy sources.
-__global__ __launch_bounds__(128) void k_hmode(BatchState *bs, const uint64_t *__restrict__ ts, uint32_t n,
-                                               const HeavySet *__restrict__ hs, const Slot *__restrict__ table,
-                                               Limits lim) {
-    __shared__ uint32_t s_bad;
-    const uint32_t h = threadIdx.x;
-    if (h == 0) s_bad = 0;
-    __syncthreads();
+// After k_pass0h (one thread): the payload words' validity and the batch's path for its
+// heavy sources from the batch's own facts. The heavy sources' carried state is checked at
+// the start of the batch's tail (k_hmode_state), after the previous batch's walkers stored
+// it: a pipelined front runs beside the previous tail.
+__global__ void k_hmode(BatchState *bs, const uint64_t *__restrict__ ts, uint32_t n, Limits lim) {
     const uint64_t t0 = n ? ts[0] : 0ull;
     const uint32_t maxL = bs->max_len;
-    const uint64_t P = lim.pps, B = lim.bps, W = lim.window;
-    if (h < hs->n && hs->resolved && hs->slot[h] != kNoSlot) {
-        const FwState st = load_state(table[hs->slot[h]]);
-        bool ok = !st.has_st || (st.tt <= ~0ull - W && st.pps < kBig && st.bps < kBig);
-        if (st.has_st && (st.bps > B || (maxL && P + 1 > (B - st.bps) / maxL))) ok = false;
-        if (!ok) atomicOr(&s_bad, 1u);
-    } else if (h < hs->n) {
-        atomicOr(&s_bad, 1u);
-    }
-    __syncthreads();
-    if (h != 0) return;
+    const uint64_t P = lim.pps, B = lim.bps;
     const uint64_t mn = ~bs->inv_min_ts;
     const bool pay = maxL < (1u << kPayLenBits) && mn == t0 && bs->max_ts - t0 < kPayTsRange;
     bs->pay_ok = pay ? 1u : 0u;
     const bool fast = !bs->err && pay && !bs->nonmono && !bs->span_big && maxL < (1u << 16) &&
-                      fast_ok(bs, lim) && !(maxL && P + 1 > B / maxL) && !s_bad;
+                      fast_ok(bs, lim) && !(maxL && P + 1 > B / maxL);
     bs->hfast = fast ? 1u : 0u;
+}
+
+// First kernel of the tail (one block of 128 threads, a thread per heavy source): every
+// heavy source's carried state on the epoch-jump path, or the batch takes the run path.
+__global__ __launch_bounds__(128) void k_hmode_state(BatchState *bs, const HeavySet *__restrict__ hs,
+                                                     const Slot *__restrict__ table, Limits lim) {
+    if (!bs->hfast) return;
+    const uint32_t h = threadIdx.x;
+    const uint32_t maxL = bs->max_len;
+    const uint64_t P = lim.pps, B = lim.bps, W = lim.window;
+    bool ok = true;
+    if (h < hs->n && hs->resolved && hs->slot[h] != kNoSlot) {
+        const FwState st = load_state(table[hs->slot[h]]);
+        ok = !st.has_st || (st.tt <= ~0ull - W && st.pps < kBig && st.bps < kBig);
+        if (st.has_st && (st.bps > B || (maxL && P + 1 > (B - st.bps) / maxL))) ok = false;
+    } else if (h < hs->n) {
+        ok = false;
+    }
+    if (!ok) bs->hfast = 0;
 }
 
 // ------------------------------------------------------------------ k_heavy_gather
@@ -522,9 +527,14 @@ size_t hflow_bytes(uint64_t cap) {
 }
 
 // ------------------------------------------------------------------ launchers
-hipError_t launch_hmode(BatchState *bs, const uint64_t *ts, uint32_t n, const HeavySet *hs, const Slot *table,
-                        const Limits &lim, hipStream_t st) {
-    k_hmode<<<1, 128, 0, st>>>(bs, ts, n, hs, table, lim);
+hipError_t launch_hmode(BatchState *bs, const uint64_t *ts, uint32_t n, const Limits &lim, hipStream_t st) {
+    k_hmode<<<1, 1, 0, st>>>(bs, ts, n, lim);
+    return hipGetLastError();
+}
+
+hipError_t launch_hmode_state(BatchState *bs, const HeavySet *hs, const Slot *table, const Limits &lim,
+                              hipStream_t st) {
+    k_hmode_state<<<1, 128, 0, st>>>(bs, hs, table, lim);
     return hipGetLastError();
 }
 

@@ -589,8 +589,10 @@ hipError_t launch_pass0h(const uint64_t *in, uint64_t *out, uint32_t n, uint32_t
                          const uint32_t *len, const uint8_t *tags, const uint32_t *chunk_cnt,
                          const uint64_t *lmask, void *rec,
                          const HeavySet *hs, hipStream_t st);
-hipError_t launch_hmode(BatchState *bs, const uint64_t *ts, uint32_t n, const HeavySet *hs, const Slot *table,
-                        const Limits &lim, hipStream_t st);
+hipError_t launch_hmode(BatchState *bs, const uint64_t *ts, uint32_t n, const Limits &lim, hipStream_t st);
+// (the tail's first kernel: the heavy sources' carried state, after the previous tail stored it)
+hipError_t launch_hmode_state(BatchState *bs, const HeavySet *hs, const Slot *table, const Limits &lim,
+                              hipStream_t st);
 hipError_t launch_heavy_gather(const BatchState *bs, const uint8_t *tags, const uint64_t *ts, const uint32_t *len,
                                uint32_t n, const uint32_t *offs, uint32_t tcap, const HeavySet *hs, uint32_t shift0,
                                uint64_t id_mask, uint64_t *out, uint64_t *pout, hipStream_t st);

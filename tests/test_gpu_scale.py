@@ -86,7 +86,7 @@ def test_config2_stream_all_limiters(native, oracle, limiter):
 def test_config4_share_16m_population(native, oracle):
     """BASELINE config 4's source population (16M Zipf(1.1) sources, 1B packets over 120 s):
     the first 8M packets of the stream, max_entries = 16M (a 2^25-slot table: 25-bit source
-    ids, the 4-pass heavy-source sort with a 7-bit first bucket and 64 heavy sources),
+    ids, the 4-pass heavy-source sort with an 8-bit first bucket and 128 heavy sources),
     fixed window with state carried."""
     from flowsentryx_amd import synth
     p, s = synth.config_params(4)
