@@ -469,6 +469,9 @@ template <uint32_t kRec, bool kRules, bool kMir, bool kHf>
 #ifndef FSX_PARSE_MINB
 #define FSX_PARSE_MINB 4   // waves/SIMD bound of k_parse (A/B: scripts/build_variant.sh)
 #endif
+#ifndef FSX_PARSE_GRID   // persistent blocks of k_parse (256 CUs x its blocks per CU)
+#define FSX_PARSE_GRID (256u * FSX_PARSE_MINB)
+#endif
 __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
                                                const uint32_t *__restrict__ len,
                                                const uint64_t *__restrict__ ts, uint32_t n,
@@ -2929,7 +2932,7 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
     IdTable pidt = idt;
     if (lazy) pidt.init = 0;
     {
-        const uint32_t g = std::min<uint32_t>(256u * FSX_PARSE_MINB, ntiles);   // one resident block per slot
+        const uint32_t g = std::min<uint32_t>(FSX_PARSE_GRID, ntiles);   // one resident block per slot
         const HeavySet *hs = heavy_sort ? sc.heavy : nullptr;
         uint32_t *th = onesweep ? nullptr : sc.hist;
         uint64_t *lmask = light_masks(sc.chunk_cnt, sc.cap);
