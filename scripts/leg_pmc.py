@@ -5,8 +5,10 @@
 
 <dir>/FETCH_SIZE/run_counter_collection.csv and <dir>/WRITE_SIZE/... (KiB per dispatch);
 FETCH_SIZE doubled per the gfx950 correction of MI355X_MICROARCH.md (HBM section). The leg
-is every dispatch after the last synthetic-stream kernel (k_synth); bytes are summed per
-kernel and divided by the leg's k_parse launches (one per batch)."""
+is every dispatch after the last synthetic-stream kernel (k_synth), product kernels only
+(the library's k_* kernels and its memsets / copies; not the bench's torch-side checks or
+map dumps); bytes are summed per kernel and divided by the leg's k_parse launches (one per
+batch)."""
 import csv
 import re
 import sys
@@ -28,7 +30,8 @@ def leg_rows(path, counter):
         rows.append((int(r["Start_Timestamp"]), short(r["Kernel_Name"]), float(r["Counter_Value"]) * 1024))
     rows.sort()
     last = max((i for i, r in enumerate(rows) if r[1] == "k_synth"), default=-1)
-    return rows[last + 1:]
+    keep = lambda k: (k.startswith("k_") and k != "k_map_dump") or k.startswith("__amd_rocclr")
+    return [r for r in rows[last + 1:] if keep(r[1])]
 
 
 def main(d):
