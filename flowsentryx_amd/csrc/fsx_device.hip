@@ -469,6 +469,9 @@ template <uint32_t kRec, bool kRules, bool kMir, bool kHf>
 #ifndef FSX_PARSE_MINB
 #define FSX_PARSE_MINB 4   // waves/SIMD bound of k_parse (A/B: scripts/build_variant.sh)
 #endif
+#ifndef FSX_PARSE_DEFCAP   // deferred probes per wave before k_parse resolves them (CAS inserts)
+#define FSX_PARSE_DEFCAP 128u
+#endif
 #ifndef FSX_PARSE_GRID   // persistent blocks of k_parse (256 CUs x its blocks per CU)
 #define FSX_PARSE_GRID (256u * FSX_PARSE_MINB)
 #endif
@@ -497,7 +500,7 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
     __shared__ uint32_t s_htag[kHeavyMax];
     __shared__ uint32_t s_hmap4[(1u << kHeavyMapBits) / 4];   // HeavySet::map
     __shared__ uint32_t s_hslot[kHeavyMax];
-    __shared__ uint32_t s_def[4][128 * (kHf ? 6 : 5)];  // per wave: deferred probes {i, tag | hidx, key word 0, probe hint[, light position]}
+    __shared__ uint32_t s_def[4][FSX_PARSE_DEFCAP * (kHf ? 6 : 5)];  // per wave: deferred probes {i, tag | hidx, key word 0, probe hint[, light position]}
     const uint8_t *s_hmap = reinterpret_cast<const uint8_t *>(s_hmap4);
     const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
 #pragma unroll
@@ -586,7 +589,7 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
     // stay in flight until the resolve)
     typedef unsigned short mir2_t __attribute__((ext_vector_type(2)));
     mir2_t c_m = {0, 0};
-    constexpr uint32_t kDefCap = 128;   // deferred packets per wave (LDS)
+    constexpr uint32_t kDefCap = FSX_PARSE_DEFCAP;   // deferred packets per wave (LDS)
     constexpr uint32_t kDefW = kHf ? 6 : 5;   // words per deferred packet
     uint32_t crun = 0;                  // kHf: light words of the wave's current chunk so far
     uint32_t *dq = s_def[w];
