@@ -519,8 +519,9 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
     __syncthreads();
     uint32_t *rec = s_rec[w];
     uint32_t any6 = 0, nonmono = 0, maxlen = 0, nfresh = 0, nrule = 0;
-    // the high word's kFreshBit for an inserting packet (lazy slots, no heavy-source sort)
-    const uint32_t fresh_hi = __builtin_amdgcn_readfirstlane(!idt.init && !dp.light_b ? 0x80000000u : 0u);
+    // the high word's kFreshBit for an inserting packet (lazy slots; without the heavy-source
+    // sort, or kHf: a light word's bucket is below 128 and k_pass0h ranks it without the bit)
+    const uint32_t fresh_hi = __builtin_amdgcn_readfirstlane(!idt.init && (!dp.light_b || kHf) ? 0x80000000u : 0u);
     uint64_t maxts = 0, inv_mints = 0;  // ~min ts, max-reduced
     // a block owns whole 4096-record sort tiles (so it can emit pass 0's per-tile digit
     // counts: no k_tile_hist for pass 0); wave w parses records [w*1024, +1024) of the
@@ -634,11 +635,12 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
                                                                    __HIP_MEMORY_SCOPE_AGENT);
                 const uint32_t id = id_resolve<kMir>(idt, tag, k, h, hint, &fresh);
                 if (id == kNoSlot) atomicOr(&bs->err, ERR_TABLE_FULL);
-                const uint64_t out = word_of(id, tag, i, hidx) | (uint64_t)(fresh ? fresh_hi : 0u) << 32;
+                const uint64_t out = word_of(id, tag, i, hidx);
+                const uint64_t outf = out | (uint64_t)(fresh ? fresh_hi : 0u) << 32;
                 if constexpr (kHf) {
-                    if (hidx < 0) packed[q[5]] = out;
+                    if (hidx < 0) packed[q[5]] = outf;
                 } else {
-                    packed[i] = out;
+                    packed[i] = outf;
                 }
                 count_digits(out, hidx);
             }
@@ -1360,7 +1362,7 @@ __global__ __launch_bounds__(256, FSX_PASS0H_MINB) void k_pass0h(const uint64_t 
     for (int r = 0; r < kSortItems; ++r) {
         const bool valid = v[r] != kSentinel;
         const uint64_t act = __ballot(valid);
-        const uint32_t d = (uint32_t)(v[r] >> shift) & dmask;
+        const uint32_t d = (uint32_t)((v[r] & ~kFreshBit) >> shift) & dmask;
         const int lead0 = act ? __ffsll((unsigned long long)act) - 1 : 0;
         const uint32_t dl = __shfl(d, lead0);
         const uint64_t peers = __ballot(valid && d == dl) == act ? act : match_digit(d, act);
@@ -1389,7 +1391,7 @@ __global__ __launch_bounds__(256, FSX_PASS0H_MINB) void k_pass0h(const uint64_t 
 #pragma unroll
     for (int r = 0; r < kSortItems; ++r) {
         if (lr[r] != 0xFFFFFFFFu) {
-            const uint32_t dd = (uint32_t)(v[r] >> shift) & dmask;
+            const uint32_t dd = (uint32_t)((v[r] & ~kFreshBit) >> shift) & dmask;
             lr[r] += s_tbase[dd] + s_wc[w][dd];
             s_el[lr[r]] = v[r];
         }
@@ -1402,7 +1404,7 @@ __global__ __launch_bounds__(256, FSX_PASS0H_MINB) void k_pass0h(const uint64_t 
         const uint32_t j = tid + 256u * (uint32_t)m;
         if (j < T) {
             const uint64_t x = s_el[j];
-            const uint32_t dd = (uint32_t)(x >> shift) & dmask;
+            const uint32_t dd = (uint32_t)((x & ~kFreshBit) >> shift) & dmask;
             dst[m] = s_dst[dd] + (j - s_tbase[dd]);
             out[dst[m]] = x;
         }
@@ -3029,7 +3031,7 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
     if (split) ta.sp = *split;
     ta.npass = npass; ta.tagh = tagh; ta.gridTiles = gridTiles;
     ta.hfm = hfm; ta.shift0 = dp.shift[0];
-    ta.admit = admit; ta.X = X; ta.id_gen = id_gen; ta.lazy = lazy; ta.fresh_bit = lazy && !heavy_sort;
+    ta.admit = admit; ta.X = X; ta.id_gen = id_gen; ta.lazy = lazy; ta.fresh_bit = lazy && (!heavy_sort || hfm);
     ta.fork = flows && do_limit && st2 && fork_ev && join_ev && !no_fork;
     for (int k = 0; k < 3; ++k) ta.last[k] = last[k];
     if (split && split->tail_out) {

@@ -314,9 +314,11 @@ constexpr uint32_t kIdShift = 31;
 // without it the id may use bits 31..62 (tables of up to 2^32 slots).
 __host__ __device__ inline uint32_t pk_id(uint64_t v, uint64_t id_mask) { return (uint32_t)((v >> kIdShift) & id_mask); }
 __host__ __device__ inline uint32_t pk_idx(uint64_t v) { return (uint32_t)v & 0x7FFFFFFFu; }
-// Without the heavy-source sort no digit reaches bit 63: there it marks the packet that
-// inserted its source in this batch (lazy slots; the walker writes that slot's line without
-// reading it). Segment heads compare the words without it.
+// Without the heavy-source sort no digit reaches bit 63, and with the heavy sources outside
+// the sort a light word's pass-0 bucket is below 128 (k_pass0h ranks it without the bit):
+// there bit 63 marks the packet that inserted its source in this batch (lazy slots; the
+// walker writes that slot's line without reading it). Segment heads compare the words
+// without it.
 constexpr uint64_t kFreshBit = 1ull << 63;
 
 // ------------------------------------------------------------ launchers (fsx_device.hip)
