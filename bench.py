@@ -487,6 +487,7 @@ def main():
         ctx.sync()
         torch.cuda.synchronize()
         barrier()
+        i0 = ctx.last_batch_info()   # (the device is idle: no wait inside the timed region)
         t0 = time.perf_counter()
         for k in range(warmup, warmup + steps):
             step(k)
@@ -497,6 +498,11 @@ def main():
         out = {"n": n, "p": p, "steps": steps, "elapsed": elapsed, "max_entries": max_entries,
                "mpps": n * world * steps / elapsed / 1e6, "ms_step": elapsed / steps * 1e3}
         info = ctx.last_batch_info()
+        # which path the heavy sources of each timed batch took (unsorted = by
+        # rank over the arrival order, run = k_heavy_gather + the run walkers); per owner call
+        # at N > 1
+        out["heavy_path"] = {"unsorted": info["hfast_batches"] - i0["hfast_batches"],
+                             "run": info["hrun_batches"] - i0["hrun_batches"]}
         if ntime:
             # per-kernel device times (a HIP event after every kernel) from separate steps
             # (the stream continued; timed batches run unpipelined), so the timed steps
@@ -727,7 +733,7 @@ def main():
                               stream=leg_name != "cold", pipelined=False)
             results[leg_name] = {"value": round(r_["mpps"], 2), "unit": "Mpps",
                                  "ms_per_step": round(r_["ms_step"], 4), "steps": r_["steps"],
-                                 "check": r_.get("check"),
+                                 "check": r_.get("check"), "heavy_path": r_.get("heavy_path"),
                                  "note": "every step the same batch from empty maps (fsx_reset in the step)"
                                  if leg_name == "cold" else
                                  "the headline's stream (maps carried), batches not pipelined"}
@@ -744,6 +750,7 @@ def main():
         results["distinct"] = {"value": round(r_["mpps"], 2), "unit": "Mpps",
                                "ms_per_step": round(r_["ms_step"], 4), "steps": r_["steps"],
                                "sources_last_batch": r_["sources"], "check": r_.get("check"),
+                               "heavy_path": r_.get("heavy_path"),
                                "note": "4 distinct consecutive batches of one stream of the config's "
                                        "population, cycled with the maps carried, pipelined"}
         del r_["d"], r_
@@ -846,6 +853,7 @@ def main():
                "steps": r4["steps"], "packets_per_gpu": n4, "n_gpus": world,
                "packets_total": n4 * world, "source_population": int(p4.n_ips),
                "sources": r4["sources"], "allowed": r4["stats"][0], "dropped": r4["stats"][1],
+               "heavy_path": r4.get("heavy_path"),
                "stream": f"packets [r*{n4}, (r+1)*{n4}) of the config-4 stream per rank r"
                          if world == 1 else f"{world} x {n4} packets of the config-4 stream"}
         if r4["sources"]:
@@ -961,7 +969,7 @@ def main():
                    "packets_per_gpu": n, "sources": sources,
                    "parallelism": f"dp{world}" + ("" if world == 1 else " (sources hash-sharded, all-to-all)")},
         "roofline": roofline, "pipeline": pipeline, "cpu_baseline": cpu,
-        "check": head.get("check"),
+        "check": head.get("check"), "heavy_path": head.get("heavy_path"),
         "limiters": results.get("limiters"), "prefix_rules": results.get("prefix_rules"),
         "cold": results.get("cold"), "unpipelined": results.get("unpipelined"),
         "distinct": results.get("distinct"),

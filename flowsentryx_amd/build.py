@@ -46,21 +46,37 @@ def _stale(out: Path, srcs: list[Path]) -> bool:
     return any(d.exists() and d.stat().st_mtime > t for d in deps)
 
 
+def _compile(src: Path, obj: Path, extra: list[str]) -> None:
+    cmd = [HIPCC, *[f for f in COMMON if f != "-shared"], *extra, "-c", "-o", str(obj), str(src)]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc failed for {src.name}:\n{r.stdout}\n{r.stderr}")
+
+
 def build_lib(name: str, force: bool = False, verbose: bool = False,
-              only_missing: bool = False) -> Path:
-    out = PKG / name
+              only_missing: bool = False, extra: list[str] | None = None, out: Path | None = None) -> Path:
+    """One translation unit per source, compiled in parallel (objects under build/), then
+    linked into the shared library. `extra` / `out`: A/B variants (scripts/build_variant.sh)."""
+    from concurrent.futures import ThreadPoolExecutor
+    out = out or PKG / name
     srcs = [CSRC / s for s in LIBS[name]]
     if only_missing and out.exists() and not force:
         return out
-    if not force and not _stale(out, srcs):
+    if not force and not extra and not _stale(out, srcs):
         return out
-    tmp = out.with_suffix(".so.tmp")
-    cmd = [HIPCC, *COMMON, "-o", str(tmp), *map(str, srcs)]
+    objdir = ROOT / "build" / (out.name + ".obj")
+    objdir.mkdir(parents=True, exist_ok=True)
+    objs = [objdir / (s.stem + ".o") for s in srcs]
     if verbose:
-        print(" ".join(cmd), file=sys.stderr)
+        print(f"hipcc {len(srcs)} sources -> {out.name}", file=sys.stderr)
+    jobs = max(1, min(len(srcs), int(os.environ.get("MAX_JOBS", os.cpu_count() or 4))))
+    with ThreadPoolExecutor(jobs) as ex:
+        list(ex.map(lambda so: _compile(so[0], so[1], list(extra or [])), zip(srcs, objs)))
+    tmp = out.with_suffix(".so.tmp")
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(tmp), *map(str, objs)]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
-        raise RuntimeError(f"hipcc failed for {name}:\n{r.stdout}\n{r.stderr}")
+        raise RuntimeError(f"hipcc link failed for {name}:\n{r.stdout}\n{r.stderr}")
     os.replace(tmp, out)
     return out
 

@@ -567,6 +567,9 @@ static int check_pipelined(fsx_ctx *c) {
         if (!failed) rc = batch_error(c, h.err);
         failed = true;
     }
+    // (the tail-side cancel flag of split sliding-window batches: everything it cancelled
+    // is rolled back now)
+    if (failed) HIPCHK(c, hipMemsetAsync(&c->tstate->tail_fail, 0, sizeof(uint32_t), c->stream));
     return rc;
 }
 
@@ -1342,8 +1345,9 @@ int fsx_reset(fsx_ctx *c) {
     if (rc) return rc;
     if (pipe_busy(c) && (rc = fsx_sync(c))) return rc;   // (pipelined batches)
     c->pending_born = 0;   // the whole table is wiped: no rollback of a pending batch
+    c->count_bound = 0;    // (no source is tracked after the reset: ADVICE r04)
     HIPCHK(c, hipMemsetAsync(c->table, 0, c->slots * sizeof(Slot), c->stream));
-    HIPCHK(c, hipMemsetAsync(c->tstate, 0, sizeof(TableState), c->stream));
+    HIPCHK(c, hipMemsetAsync(c->tstate, 0, kTableStateResetBytes, c->stream));   // (path counters kept)
     return next_epoch(c);   // (the prefix blocklists stay: configuration)   // every index head reads empty
 }
 
@@ -1484,11 +1488,13 @@ int fsx_last_batch_info(fsx_ctx *c, uint64_t *info, int cap) {
     HIPCHK(c, hipStreamSynchronize(c->stream));
     BatchState h;
     HIPCHK(c, hipMemcpy(&h, c->bs, sizeof(h), hipMemcpyDeviceToHost));
-    const uint64_t v[16] = {h.n_valid, h.nseg, h.n_new, h.any_v6, h.nonmono, h.max_len,
+    TableState t;
+    HIPCHK(c, hipMemcpy(&t, c->tstate, sizeof(t), hipMemcpyDeviceToHost));
+    const uint64_t v[18] = {h.n_valid, h.nseg, h.n_new, h.any_v6, h.nonmono, h.max_len,
                             h.max_ts, h.allowed, h.dropped, h.n_rule, h.pay_ok, h.n_light,
-                            c->last_evicted, h.hfast, h.n_admit, h.n_trans};
+                            c->last_evicted, h.hfast, h.n_admit, h.n_trans, t.n_hfast, t.n_hrun};
     int k = 0;
-    for (; k < cap && k < 16; ++k) info[k] = v[k];
+    for (; k < cap && k < 18; ++k) info[k] = v[k];
     return k;
 }
 

@@ -89,6 +89,13 @@ __device__ __forceinline__ uint32_t xcd_swizzle(uint32_t b, uint32_t nwg) {
     return (x < r ? x * (q + 1u) : r * (q + 1u) + (x - r) * q) + (b >> 3);
 }
 
+// A wave-uniform 64-bit value into scalar registers.
+__device__ __forceinline__ uint64_t uni64(uint64_t x) {
+    // (readfirstlane returns int: through uint32_t, or the low half sign-extends)
+    return (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)x) |
+           (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(x >> 32)) << 32;
+}
+
 __device__ __forceinline__ uint64_t match_digit(uint32_t d, uint64_t active) {
     uint64_t peers = active;
 #pragma unroll

@@ -461,10 +461,22 @@ __device__ __forceinline__ bool rule_drop(const RuleSet &R, uint32_t tag, const 
 }
 
 // One wave handles 64 consecutive records per step: the 4 KiB tile is loaded with
-// four fully coalesced 1 KiB wave loads and staged through LDS (17-dword record
+// four fully coalesced 1 KiB wave loads and staged through LDS (13-dword record
 // pitch: conflict-free 32-bit reads), then each lane parses its own record.
 // Record mode (kRec = 16 / 32): every lane loads its own exchange record (coalesced, no
 // LDS staging), all of them IP packets; their len / ts go out to in.rec_len / rec_ts.
+// FSX_PARSE_PAY (A/B, default 0; DESIGN.md §3 "Pass 0 in the parse, measured"): with the heavy
+// sources outside the sort, k_parse also reads the timestamps, computes the clock facts (and
+// each sort tile's span) and writes every light packet's payload word beside its sort word,
+// so pass 0 (k_pass0h<false>) only ranks and scatters the light words; the heavy tile records
+// come from k_heavy_recs at the start of the tail. Bit-exact, slower: 3.09-3.19 vs 2.95-2.96
+// ms per step (profiles/r05/ab_r05d_parse_pay.txt). 0 (the product): k_parse reads no
+// timestamps and k_pass0h<true> reads ts / len / verdicts once for the records, the clock facts
+// and the payload words.
+#ifndef FSX_PARSE_PAY
+#define FSX_PARSE_PAY 0
+#endif
+constexpr uint32_t kRecPitch = 13;   // LDS staging pitch of a record (12 dwords used; odd: conflict-free reads)
 template <uint32_t kRec, bool kRules, bool kMir, bool kHf>
 #ifndef FSX_PARSE_MINB
 #define FSX_PARSE_MINB 4   // waves/SIMD bound of k_parse (A/B: scripts/build_variant.sh)
@@ -486,12 +498,16 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
                                                RuleSet rules, uint32_t tagh,
                                                uint32_t *__restrict__ chunk_cnt,
                                                uint64_t *__restrict__ lmask) {
-    // kHf (unsorted heavy sources): no timestamp loads (k_pass0h reads them),
-    // no sort word for a heavy source's packet (its verdict byte carries 0x80 | h), the light
-    // sort words compacted per 1024-packet chunk (wave) with their count in chunk_cnt and
-    // the light-packet mask of every 64-packet step in lmask
+    // kHf (unsorted heavy sources): no sort word for a heavy source's packet (its
+    // verdict byte carries 0x80 | h), the light sort words compacted per 1024-packet chunk
+    // (wave) with their count in chunk_cnt, and
+    //   FSX_PARSE_PAY: each light packet's payload word at the same compacted position of
+    //   lmask (the payload array), the clock facts and the sort tiles' span;
+    //   else: no timestamp loads, the light-packet mask of every 64-packet step in lmask
+    //   (k_pass0h<true> reads ts / len / verdicts for the records and the payloads)
     static_assert(!kHf || !kRules, "unsorted heavy sources: no prefix rules");
-    __shared__ uint32_t s_rec[4][64 * 17];
+    constexpr bool kHr = kHf && FSX_PARSE_PAY;   // (the payload words from the parse)
+    __shared__ uint32_t s_rec[4][64 * kRecPitch];
     __shared__ uint32_t s_red[4][3];
     __shared__ unsigned long long s_ts[4], s_its[4];
     __shared__ uint32_t s_hist[4][256];     // the radix digits of every sort key (per pass)
@@ -500,7 +516,12 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
     __shared__ uint32_t s_htag[kHeavyMax];
     __shared__ uint32_t s_hmap4[(1u << kHeavyMapBits) / 4];   // HeavySet::map
     __shared__ uint32_t s_hslot[kHeavyMax];
-    __shared__ uint32_t s_def[4][FSX_PARSE_DEFCAP * (kHf ? 6 : 5)];  // per wave: deferred probes {i, tag | hidx, key word 0, probe hint[, light position]}
+    // per wave: deferred probes {i, tag | hidx, key word 0, probe hint (not with kMir + kHf),
+    // light position (kHf)}
+    constexpr uint32_t kDefW = kHf ? (kMir ? 4 : 6) : 5;   // words per deferred packet
+    constexpr uint32_t kDefPos = kDefW - 1;                 // (kHf) its light position
+    __shared__ uint32_t s_def[4][FSX_PARSE_DEFCAP * kDefW];
+    __shared__ unsigned long long s_cb[4], s_cz[4];   // kHr: each chunk's first / last timestamp
     const uint8_t *s_hmap = reinterpret_cast<const uint8_t *>(s_hmap4);
     const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
 #pragma unroll
@@ -551,8 +572,11 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
                 h[k] = stream_load16(in.hdr + (size_t)rr * 64u + c * 16u);
             }
             L_ = stream_load(len + ic);
-            if constexpr (kHf) {
+            if constexpr (kHf && !kHr) {
                 T_ = 0ull;
+                P_ = 0ull;
+            } else if constexpr (kHr) {   // (the record before a step: c_prev, see parse_step)
+                T_ = stream_load(ts + ic);
                 P_ = 0ull;
             } else {
                 T_ = stream_load(ts + ic);
@@ -585,13 +609,28 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
     // two probe reads
     uint32_t c_tag = 0, c_k0 = 0, c_h = 0;
     int c_hidx = -1;
+    // kHr: the wave's chunk's first timestamp and the last one so far (wave-uniform): the clock
+    // check of a step's first record against the step before it, the tile's span and the
+    // check across its chunks at the tile's end (across tiles: k_pass0h<false>)
+    uint64_t c_base = 0, c_prev = 0;
+    uint64_t tb = 0;   // kHr: the batch's first timestamp (payload words: ts - tb)
+    if constexpr (kHr) {
+        if (n) {
+            if constexpr (kRec == 0) {
+                tb = ts[0];
+            } else {
+                const uint4 *r0 = reinterpret_cast<const uint4 *>(in.rec);
+                tb = kRec == 16 ? ((uint64_t)r0[0].z | ((uint64_t)r0[0].w << 32))
+                                : ((uint64_t)r0[1].x | ((uint64_t)r0[1].y << 32));
+            }
+        }
+    }
     uint64_t c_hint0 = 0, c_hint1 = 0;
     // kMir: the two mirror entries as the halves of one register (two 16-bit loads that
     // stay in flight until the resolve)
     typedef unsigned short mir2_t __attribute__((ext_vector_type(2)));
     mir2_t c_m = {0, 0};
     constexpr uint32_t kDefCap = FSX_PARSE_DEFCAP;   // deferred packets per wave (LDS)
-    constexpr uint32_t kDefW = kHf ? 6 : 5;   // words per deferred packet
     uint32_t crun = 0;                  // kHf: light words of the wave's current chunk so far
     uint32_t *dq = s_def[w];
     uint32_t ndef = 0;
@@ -630,7 +669,7 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
                 const uint64_t h = id_start(idt, tag, k);
                 // IPv4: the first probe slot's head as the probe read it (a stale value only
                 // costs the CAS one retry); IPv6 (and IPv4 probed on the mirror) had no head read
-                const uint64_t hint = tag == 1 && !kMir ? ((uint64_t)q[4] << 32 | q[3])
+                const uint64_t hint = tag == 1 && kDefW >= 5 && !kMir ? ((uint64_t)q[kDefW >= 5 ? 4 : 0] << 32 | q[3])
                                                : __hip_atomic_load(idt.head + h, __ATOMIC_RELAXED,
                                                                    __HIP_MEMORY_SCOPE_AGENT);
                 const uint32_t id = id_resolve<kMir>(idt, tag, k, h, hint, &fresh);
@@ -638,7 +677,7 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
                 const uint64_t out = word_of(id, tag, i, hidx);
                 const uint64_t outf = out | (uint64_t)(fresh ? fresh_hi : 0u) << 32;
                 if constexpr (kHf) {
-                    if (hidx < 0) packed[q[5]] = outf;
+                    if (hidx < 0) packed[q[kDefPos]] = outf;
                 } else {
                     packed[i] = outf;
                 }
@@ -664,11 +703,11 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
 #pragma unroll
             for (int q = 0; q < 3; ++q) {
                 const uint32_t f = (uint32_t)q * 64u + lane, r = f / 3u, c = f - 3u * r;
-                uint32_t *d = rec + r * 17u + c * 4u;
+                uint32_t *d = rec + r * kRecPitch + c * 4u;
                 d[0] = hv[q].x; d[1] = hv[q].y; d[2] = hv[q].z; d[3] = hv[q].w;
             }
             wave_lds_order();
-            const uint32_t *my = rec + lane * 17u;
+            const uint32_t *my = rec + lane * kRecPitch;
             const uint32_t d3 = my[3], d5 = my[5], d6 = my[6], d7 = my[7], d8 = my[8], d9 = my[9];
             tag = live ? parse_src(L, d3, d5, d6, d7, d8, d9, k, v) : 0u;
         } else if (live) {   // ShardRecord16 {key, len | dport << 16, ts} / ShardRecord
@@ -694,7 +733,12 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
             }
         }
         uint64_t prev = __shfl_up(T, 1);
-        if (lane == 0) prev = (live && i > 0) ? Pc : T;
+        if constexpr (kHr) {
+            (void)Pc;
+            if (lane == 0) prev = (t & 15u) ? c_prev : T;
+        } else {
+            if (lane == 0) prev = (live && i > 0) ? Pc : T;
+        }
         const bool ip = tag != 0;
         if (tag == 2) any6 = 1;
         uint64_t h = 0;
@@ -742,6 +786,20 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
         c_k0 = k[0];
         c_h = (uint32_t)h;
         c_hidx = hidx;
+        if constexpr (kHr) {
+            {   // the light packets' positions in the chunk (arrival order) and payload words
+                const bool lt = live && tag != 0 && hidx < 0;
+                const uint64_t lm = __ballot(lt);
+                // (ts - tb) << kPayLenBits | len (k_hmode: pay_ok), at the light word's compacted
+                // position (lmask is the payload array); resolve_step recomputes the position
+                if (lt) lmask[((t >> 4) << 10) + crun + (uint32_t)__popcll(lm & lt_mask)] = ((T - tb) << kPayLenBits) | L;
+                crun += (uint32_t)__popcll(lm);
+            }
+            // the chunk's first and last timestamp (a step past n: its lane 63 is no packet, but
+            // then no later chunk of the tile holds one either)
+            if ((t & 15u) == 0) c_base = uni64(__shfl(T, 0));
+            c_prev = uni64(__shfl(T, 63));
+        }
         if (live) {
             // IP packets default to PASS here (coalesced); the fill pass writes only
             // the DROP verdicts, which cluster in the heavy sources' segments
@@ -749,8 +807,8 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
             if (verdict) verdict[i] = !ip ? v : (tagh && hidx >= 0) ? (uint8_t)(0x80u | (uint32_t)hidx)
                                                                   : (uint8_t)XDP_PASS;
             maxlen = L > maxlen ? L : maxlen;
-            if constexpr (!kHf) {   // (kHf: k_pass0h has the clock facts)
-                if (!ip) packed[i] = kSentinel;
+            if constexpr (!kHf || kHr) {   // (kHf && !kHr: k_pass0h<true> has the clock facts)
+                if (!kHf && !ip) packed[i] = kSentinel;
                 nonmono |= T < prev ? 1u : 0u;
                 maxts = T > maxts ? T : maxts;
                 inv_mints = ~T > inv_mints ? ~T : inv_mints;
@@ -786,7 +844,10 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
         }
         // kHf: the light packets' positions in the chunk, in arrival order (deferred or not)
         uint32_t lpos = 0;
-        if constexpr (kHf) {
+        if constexpr (kHr) {   // (parse_step counted this step's light packets into crun)
+            const uint64_t lm = __ballot(c_tag != 0 && c_hidx < 0);
+            lpos = ((t >> 4) << 10) + crun - (uint32_t)__popcll(lm) + (uint32_t)__popcll(lm & lt_mask);
+        } else if constexpr (kHf) {
             const uint64_t lm = __ballot(c_tag != 0 && c_hidx < 0);
             if (lane == 0 && t < ntiles) lmask[t] = lm;
             lpos = ((t >> 4) << 10) + crun + (uint32_t)__popcll(lm & lt_mask);
@@ -798,8 +859,8 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
             if (defer) {
                 uint32_t *q = dq + (ndef + (uint32_t)__popcll(dm & lt_mask)) * kDefW;
                 q[0] = i; q[1] = c_tag | (uint32_t)(c_hidx + 1) << 8; q[2] = c_k0;
-                q[3] = (uint32_t)c_hint0; q[4] = (uint32_t)(c_hint0 >> 32);
-                if constexpr (kHf) q[5] = lpos;
+                if constexpr (kDefW >= 5) { q[3] = (uint32_t)c_hint0; q[4] = (uint32_t)(c_hint0 >> 32); }
+                if constexpr (kHf) q[kDefPos] = lpos;
             }
             ndef += (uint32_t)__popcll(dm);
         }
@@ -841,12 +902,31 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
                 if (lane == 0) chunk_cnt[step_at(q) >> 4] = crun;
                 crun = 0;
             }
+            if constexpr (kHr) {   // the chunk's first / last timestamp
+                if (lane == 0) { s_cb[w] = c_base; s_cz[w] = c_prev; }
+            }
             if (ghist) {
                 __syncthreads();
                 const uint32_t c0 = s_t0[threadIdx.x];
                 s_hist[0][threadIdx.x] += c0;
                 if (thist && threadIdx.x <= dp.mask[0]) thist[(size_t)threadIdx.x * tcap + tile_of(q)] = c0;
                 s_t0[threadIdx.x] = 0;
+                if constexpr (kHr) {
+                    // a tile spanning 2^32 ns or more: no unsorted path (k_hmode; with a clock
+                    // that goes back it is refused anyway, so first / last bound the span)
+                    const uint32_t tt = tile_of(q);
+                    if (threadIdx.x == 0) {
+                        uint64_t last = s_cz[0];
+                        bool back = false;   // (a chunk starting before the one before it ended)
+                        for (uint32_t k = 1; k < 4; ++k)
+                            if (tt * kSortTile + k * 1024u < n) {
+                                back |= s_cb[k] < s_cz[k - 1];
+                                last = s_cz[k];
+                            }
+                        if (last >= s_cb[0] && last - s_cb[0] >= (1ull << 32)) atomicOr(&bs->span_big, 1u);
+                        if (back) atomicOr(&bs->nonmono, 1u);
+                    }
+                }
                 __syncthreads();
             }
         }
@@ -1164,7 +1244,12 @@ __global__ __launch_bounds__(256, kLatePay ? FSX_SCATTER_MINB : 1) void k_tile_s
 }
 
 // ---- pass 0 with the heavy sources outside the sort (k_parse<..., kHf>; fsx_heavy.hip).
-// One block per sort tile t, wave w = the tile's parse chunk w (1024 arrival positions):
+// One block per sort tile t, wave w = the tile's parse chunk w (1024 arrival positions).
+// kRecs = false (FSX_PARSE_PAY, the default): k_parse computed the clock facts and wrote each
+// light word's payload word beside it, and k_heavy_recs builds the tile records in the tail,
+// so this is step 2 alone — the chunk's light words and payload words read from their
+// compacted runs, ranked and scattered (16 B read + 16 B written per light entry).
+// kRecs = true (round 4):
 //   1. every packet's timestamp, length and verdict byte (coalesced): the batch's clock facts
 //      (non-decreasing?, min / max, tile span), and for every heavy source h (byte 0x80 | h)
 //      its sums over the tile (HeavyTileRec): lengths, squared lengths, first / last
@@ -1180,9 +1265,12 @@ __global__ __launch_bounds__(256, kLatePay ? FSX_SCATTER_MINB : 1) void k_tile_s
 #ifndef FSX_PASS0H_GATHER
 #define FSX_PASS0H_GATHER 0   // 1: the payload words gathered from ts / len (A/B)
 #endif
+// (k_pass0h and k_parse<..., kHf> cut a sort tile into four 1024-packet chunks of 16 rows)
+static_assert(kSortTile == 4096 && kSortItems == 16, "k_pass0h / kHf parse: 4 x 1024-packet chunks per tile");
 #ifndef FSX_PASS0H_MINB
 #define FSX_PASS0H_MINB FSX_SCATTER_MINB
 #endif
+template <bool kRecs>
 __global__ __launch_bounds__(256, FSX_PASS0H_MINB) void k_pass0h(const uint64_t *__restrict__ in,
                                                                   uint64_t *__restrict__ out, uint32_t n,
                                                                   uint32_t shift, uint32_t dmask,
@@ -1194,7 +1282,8 @@ __global__ __launch_bounds__(256, FSX_PASS0H_MINB) void k_pass0h(const uint64_t 
                                                                   const uint32_t *__restrict__ chunk_cnt,
                                                                   const uint64_t *__restrict__ lmask,
                                                                   HeavyTileRec *__restrict__ rec,
-                                                                  const HeavySet *__restrict__ hs) {
+                                                                  const HeavySet *__restrict__ hs,
+                                                                  const uint64_t *__restrict__ pin) {
     __shared__ unsigned long long s_el[kSortTile];
     __shared__ uint32_t s_wc[4][256];
     __shared__ uint32_t s_dst[256], s_tbase[256], s_tcnt[256];
@@ -1207,6 +1296,12 @@ __global__ __launch_bounds__(256, FSX_PASS0H_MINB) void k_pass0h(const uint64_t 
     const uint32_t t = xcd_swizzle(blockIdx.x, ntiles);
     const uint32_t t0 = t * kSortTile;
     const uint64_t lt_mask = (1ull << lane) - 1ull;
+    const uint32_t c0 = t0 + w * 1024u;
+    unsigned long long *row = s_el + w * 1024u;
+    if constexpr (!kRecs) {   // (k_parse checked the clock inside each tile; here across tiles)
+        if (tid == 0 && t > 0 && t0 < n && ts[t0] < ts[t0 - 1]) atomicOr(&bs->nonmono, 1u);
+    }
+    if constexpr (kRecs) {
     const uint32_t nh = hs->n;
     const uint64_t tb = ts[0];
     // ---- 1. heavy sums and clock facts (LDS: the scratch region of s_el)
@@ -1224,7 +1319,6 @@ __global__ __launch_bounds__(256, FSX_PASS0H_MINB) void k_pass0h(const uint64_t 
     }
     for (uint32_t j = tid; j < 4 * kHeavyMax; j += 256) { h_first[j] = kNone; h_last[j] = kNone; }
     __syncthreads();
-    const uint32_t c0 = t0 + w * 1024u;
     uint64_t prev_t = lane == 0 && c0 > 0 && c0 < n ? ts[c0 - 1] : 0ull;   // (lane 0: before the chunk)
     uint32_t nonmono = 0;
     uint64_t mx = 0, imn = 0;   // max, ~min
@@ -1336,7 +1430,6 @@ __global__ __launch_bounds__(256, FSX_PASS0H_MINB) void k_pass0h(const uint64_t 
     __syncthreads();
     // the payload words of the chunk's light packets in arrival order: row w * 1024 + j of s_el
     // (light word j of the chunk is its j-th light packet)
-    unsigned long long *row = s_el + w * 1024u;
     if constexpr (!FSX_PASS0H_GATHER) {
         uint32_t run = 0;
 #pragma unroll
@@ -1346,6 +1439,7 @@ __global__ __launch_bounds__(256, FSX_PASS0H_MINB) void k_pass0h(const uint64_t 
             run += (uint32_t)__popcll(m);
         }
     }
+    }   // kRecs
     // ---- 2. pass 0 of the tile's light words (sort_tile, keys from the chunk runs)
 #pragma unroll
     for (int k = 0; k < 4; ++k) s_wc[w][lane * 4 + k] = 0;
@@ -1353,10 +1447,12 @@ __global__ __launch_bounds__(256, FSX_PASS0H_MINB) void k_pass0h(const uint64_t 
     const uint32_t ccnt = chunk_cnt[t * 4u + w];
     uint64_t v[kSortItems];
     uint32_t lr[kSortItems];
+    uint64_t pv[kSortItems];   // payload words (ts - ts[0]) << kPayLenBits | len (k_hmode: pay_ok)
 #pragma unroll
     for (int r = 0; r < kSortItems; ++r) {
         const uint32_t j = (uint32_t)r * 64u + lane;
         v[r] = j < ccnt ? in[c0 + j] : kSentinel;
+        if constexpr (!kRecs) pv[r] = j < ccnt ? pin[c0 + j] : 0ull;   // (k_parse's, compacted like the words)
     }
 #pragma unroll
     for (int r = 0; r < kSortItems; ++r) {
@@ -1372,8 +1468,7 @@ __global__ __launch_bounds__(256, FSX_PASS0H_MINB) void k_pass0h(const uint64_t 
         base = __shfl(base, __ffsll((unsigned long long)peers) - 1);
         lr[r] = valid ? base + below : 0xFFFFFFFFu;
     }
-    uint64_t pv[kSortItems];   // payload words (ts - ts[0]) << kPayLenBits | len (k_hmode: pay_ok)
-    if constexpr (!FSX_PASS0H_GATHER) {
+    if constexpr (kRecs && !FSX_PASS0H_GATHER) {
 #pragma unroll
         for (int r = 0; r < kSortItems; ++r)
             pv[r] = lr[r] != 0xFFFFFFFFu ? row[(uint32_t)r * 64u + lane] : 0ull;
@@ -1409,7 +1504,8 @@ __global__ __launch_bounds__(256, FSX_PASS0H_MINB) void k_pass0h(const uint64_t 
             out[dst[m]] = x;
         }
     }
-    if constexpr (FSX_PASS0H_GATHER) {   // (A/B: gathered by arrival index)
+    if constexpr (kRecs && FSX_PASS0H_GATHER) {   // (A/B: gathered by arrival index)
+        const uint64_t tb = ts[0];
 #pragma unroll
         for (int r = 0; r < kSortItems; ++r) {
             if (lr[r] != 0xFFFFFFFFu) {
@@ -1435,10 +1531,14 @@ __global__ __launch_bounds__(256, FSX_PASS0H_MINB) void k_pass0h(const uint64_t 
 hipError_t launch_pass0h(const uint64_t *in, uint64_t *out, uint32_t n, uint32_t shift, uint32_t dmask,
                          const uint32_t *offs, uint32_t tcap, BatchState *bs, uint64_t *pout, const uint64_t *ts,
                          const uint32_t *len, const uint8_t *tags, const uint32_t *chunk_cnt,
-                         const uint64_t *lmask, void *rec, const HeavySet *hs, hipStream_t st) {
+                         const uint64_t *lmask, void *rec, const HeavySet *hs, const uint64_t *pin, hipStream_t st) {
     const uint32_t ntiles = std::max<uint32_t>(1, (n + kSortTile - 1) / kSortTile);
-    k_pass0h<<<ntiles, 256, 0, st>>>(in, out, n, shift, dmask, offs, tcap, bs, pout, ts, len, tags, chunk_cnt, lmask,
-                                     static_cast<HeavyTileRec *>(rec), hs);
+    if (pin)   // (FSX_PARSE_PAY: the clock facts and payload words came from k_parse)
+        k_pass0h<false><<<ntiles, 256, 0, st>>>(in, out, n, shift, dmask, offs, tcap, bs, pout, ts, len, tags,
+                                                chunk_cnt, lmask, static_cast<HeavyTileRec *>(rec), hs, pin);
+    else
+        k_pass0h<true><<<ntiles, 256, 0, st>>>(in, out, n, shift, dmask, offs, tcap, bs, pout, ts, len, tags,
+                                               chunk_cnt, lmask, static_cast<HeavyTileRec *>(rec), hs, nullptr);
     return hipGetLastError();
 }
 
@@ -1711,16 +1811,20 @@ __device__ __forceinline__ uint32_t table_claim(Slot *table, const Limits &lim, 
 // Pipelined batches: a batch whose predecessor failed is cancelled (the host rolls both back).
 // (hist_in_tail: a split sliding-window batch checks its history room in its tail, after the
 // previous tail has set hist_total: k_sw_tail_check)
+// The source count moves atomically: a split tail (k_sw_tail_check) may undo its batch's
+// count on another stream meanwhile.
 __global__ void k_batch_check(BatchState *bs, TableState *tstate, Limits lim, const BatchState *prev,
                               uint32_t hist_in_tail = 0) {
     if (bs->err) return;
     if (prev && prev->err) { bs->err |= ERR_CANCELED; return; }
-    if (tstate->count + bs->n_new > lim.max_entries) { bs->err |= ERR_TABLE_FULL; return; }
+    unsigned long long *cnt = reinterpret_cast<unsigned long long *>(&tstate->count);
+    const uint64_t count = __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (count + bs->n_new > lim.max_entries) { bs->err |= ERR_TABLE_FULL; return; }
     if (lim.limiter == 1 && !hist_in_tail && tstate->hist_total + bs->n_valid > lim.hist_cap) {
         bs->err |= ERR_HIST_FULL;
         return;
     }
-    tstate->count += bs->n_new;
+    if (bs->n_new) atomicAdd(cnt, (unsigned long long)bs->n_new);
     if (bs->n_rule) {   // prefix-rule drops count in stats_map like blacklist drops
         // (atomic: a pipelined batch's tail may be adding its counters meanwhile)
         atomicAdd(reinterpret_cast<unsigned long long *>(&tstate->stats[1]), (unsigned long long)bs->n_rule);
@@ -1728,18 +1832,26 @@ __global__ void k_batch_check(BatchState *bs, TableState *tstate, Limits lim, co
     }
 }
 
-// A split sliding-window batch's history room, at the start of its tail (the previous tail
-// has set hist_total): a batch that does not fit fails with ERR_HIST_FULL before any state
-// changes, undoing what k_batch_check counted (the rollback rebuilds the index).
+// The first kernel of a split sliding-window batch's tail (the previous tail has finished
+// and set hist_total): the batch fails with ERR_HIST_FULL when its packets do not fit the
+// history buffer, and is cancelled when an earlier split batch failed in its own tail
+// (TableState::tail_fail; its k_batch_check may have run before that failure was known,
+// and its predecessor's BatchState may already belong to a later front) — in both cases
+// before any state changes, undoing what k_batch_check counted (the rollback rebuilds the
+// index).
 __global__ void k_sw_tail_check(BatchState *bs, TableState *tstate, Limits lim) {
     if (bs->err) return;
-    if (tstate->hist_total + bs->n_valid > lim.hist_cap) {
-        bs->err |= ERR_HIST_FULL;
-        tstate->count -= bs->n_new;
-        if (bs->n_rule) {
-            atomicAdd(reinterpret_cast<unsigned long long *>(&tstate->stats[1]), (unsigned long long)(0ull - bs->n_rule));
-            bs->dropped -= bs->n_rule;
-        }
+    uint32_t err = 0;
+    if (tstate->tail_fail) err = ERR_CANCELED;
+    else if (tstate->hist_total + bs->n_valid > lim.hist_cap) err = ERR_HIST_FULL;
+    if (!err) return;
+    bs->err |= err;
+    tstate->tail_fail = 1;
+    if (bs->n_new)
+        atomicAdd(reinterpret_cast<unsigned long long *>(&tstate->count), (unsigned long long)(0ull - bs->n_new));
+    if (bs->n_rule) {
+        atomicAdd(reinterpret_cast<unsigned long long *>(&tstate->stats[1]), (unsigned long long)(0ull - bs->n_rule));
+        bs->dropped -= bs->n_rule;
     }
 }
 
@@ -2595,8 +2707,18 @@ hipError_t launch_tail(const TailArgs &a) {
     // after pass 0 they slowed passes 1-2, after the heads they delayed the walkers; a fourth
     // stream shared a hardware queue with the limiter chain)
     bool heavy_join = false;
+    // FSX_PARSE_PAY: the heavy tile records (k_heavy_recs) before the heavy walker and the
+    // heavy flow sums read them — on their stream when both run there, else before the fork
+    const bool recs = a.hfm && FSX_PARSE_PAY;
+    const bool recs_on_hs = recs && hs != st && (!flows || hf == hs);
+    auto launch_recs = [&](hipStream_t rs, int rs_id) -> hipError_t {
+        hipError_t e = launch_heavy_recs(bs, ts, len, verdict, n, sc.heavy, sc.hrec, rs);
+        mark_on("k_heavy_recs", rs_id);
+        return e;
+    };
     auto launch_heavy = [&]() -> hipError_t {
         hipError_t e;
+        if (recs && !recs_on_hs && (e = launch_recs(st, 0)) != hipSuccess) return e;
         if (hs != st) {
             if ((e = hipEventRecord(heavy_fork_ev, st)) != hipSuccess) return e;
             if ((e = hipStreamWaitEvent(hs, heavy_fork_ev, 0)) != hipSuccess) return e;
@@ -2606,6 +2728,7 @@ hipError_t launch_tail(const TailArgs &a) {
                 mark_on(nullptr, hf_id);
             }
         }
+        if (recs_on_hs && (e = launch_recs(hs, hs_id)) != hipSuccess) return e;
         if (lim.limiter == 0) {   // (the sliding window's heavy walker: launch_sliding_window)
             k_walk_heavy<<<kHeavyMax / 4, 256, 0, hs>>>(S_fin, bs, sc.sort_ctl, sc.gbase, ts, len, pay_fin,
                                                           table, lim, hlists, skeys);
@@ -2652,7 +2775,7 @@ hipError_t launch_tail(const TailArgs &a) {
     if (split && split->tail && do_limit && lim.limiter == 1) k_sw_tail_check<<<1, 1, 0, st>>>(bs, tstate, lim);
     // unsorted heavy sources: their carried state decides the path now that the previous
     // batch's walkers have stored it; those sent back to the run path get their runs first
-    if (a.hfm && (e = launch_hmode_state(bs, sc.heavy, table, lim, st)) != hipSuccess) return e;
+    if (a.hfm && (e = launch_hmode_state(bs, sc.heavy, table, lim, tstate, st)) != hipSuccess) return e;
     if (a.hfm && (e = launch_heavy_gather(bs, verdict, ts, len, n, sc.hist, tcap, sc.heavy, a.shift0, lim.table_mask,
                                           S_fin, pay_fin, st)) != hipSuccess)
         return e;
@@ -2940,7 +3063,9 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
         const uint32_t g = std::min<uint32_t>(FSX_PARSE_GRID, ntiles);   // one resident block per slot
         const HeavySet *hs = heavy_sort ? sc.heavy : nullptr;
         uint32_t *th = onesweep ? nullptr : sc.hist;
-        uint64_t *lmask = light_masks(sc.chunk_cnt, sc.cap);
+        // (FSX_PARSE_PAY: the light payload words, compacted like the words, into pay[0], which
+        // pass 0 reads before pass 1 writes it; else the light-packet masks)
+        uint64_t *lmask = hfm && FSX_PARSE_PAY ? sc.pay[0] : light_masks(sc.chunk_cnt, sc.cap);
         // the prefix rules apply to limiter batches (an instantiation of its own, so the
         // rule-free parse keeps its registers)
         const bool rl = do_limit && rules.slot;
@@ -3003,7 +3128,7 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
             if (pass == 0 && hfm) {   // light words from the parse chunks; heavy tile sums; the path
                 if ((e = launch_pass0h(in, out, n, shift, pmask, sc.hist, tcap, bs, pout, ts, len, verdict,
                                        sc.chunk_cnt, light_masks(sc.chunk_cnt, sc.cap), sc.hrec, sc.heavy,
-                                       st)) != hipSuccess)
+                                       FSX_PARSE_PAY ? sc.pay[0] : nullptr, st)) != hipSuccess)
                     return e;
                 mark("k_pass0h");
                 if ((e = launch_hmode(bs, ts, n, lim, st)) != hipSuccess) return e;

@@ -274,21 +274,137 @@ __global__ void k_hmode(BatchState *bs, const uint64_t *__restrict__ ts, uint32_
 
 // First kernel of the tail (one block of 128 threads, a thread per heavy source): every
 // heavy source's carried state on the epoch-jump path, or the batch takes the run path.
+// Counts the path taken (TableState::n_hfast / n_hrun, fsx_last_batch_info [16] / [17]).
 __global__ __launch_bounds__(128) void k_hmode_state(BatchState *bs, const HeavySet *__restrict__ hs,
-                                                     const Slot *__restrict__ table, Limits lim) {
-    if (!bs->hfast) return;
-    const uint32_t h = threadIdx.x;
-    const uint32_t maxL = bs->max_len;
-    const uint64_t P = lim.pps, B = lim.bps, W = lim.window;
-    bool ok = true;
-    if (h < hs->n && hs->resolved && hs->slot[h] != kNoSlot) {
-        const FwState st = load_state(table[hs->slot[h]]);
-        ok = !st.has_st || (st.tt <= ~0ull - W && st.pps < kBig && st.bps < kBig);
-        if (st.has_st && (st.bps > B || (maxL && P + 1 > (B - st.bps) / maxL))) ok = false;
-    } else if (h < hs->n) {
-        ok = false;
+                                                     const Slot *__restrict__ table, Limits lim,
+                                                     TableState *tstate) {
+    __shared__ uint32_t s_bad;
+    if (threadIdx.x == 0) s_bad = 0;
+    __syncthreads();
+    const bool fast0 = bs->hfast != 0;
+    if (fast0) {
+        const uint32_t h = threadIdx.x;
+        const uint32_t maxL = bs->max_len;
+        const uint64_t P = lim.pps, B = lim.bps, W = lim.window;
+        bool ok = true;
+        if (h < hs->n && hs->resolved && hs->slot[h] != kNoSlot) {
+            const FwState st = load_state(table[hs->slot[h]]);
+            ok = !st.has_st || (st.tt <= ~0ull - W && st.pps < kBig && st.bps < kBig);
+            if (st.has_st && (st.bps > B || (maxL && P + 1 > (B - st.bps) / maxL))) ok = false;
+        } else if (h < hs->n) {
+            ok = false;
+        }
+        if (!ok) s_bad = 1;
     }
-    if (!ok) bs->hfast = 0;
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    const bool fast = fast0 && !s_bad;
+    if (fast0 && !fast) bs->hfast = 0;
+    if (!bs->err) atomicAdd(fast ? &tstate->n_hfast : &tstate->n_hrun, 1u);
+}
+
+// ------------------------------------------------------------------ k_heavy_recs
+// (FSX_PARSE_PAY) Every sort tile's sums of every heavy source (HeavyTileRec), at the start of
+// the tail beside the next batch's light passes: one block per tile, wave w = the tile's
+// 1024-packet chunk w. Lengths, squared lengths, first / last timestamp, first arrival offset,
+// and the squared gaps and the largest gap between consecutive packets of a source — a
+// packet's predecessor is the last lane below it with the same source (eight ballots), else
+// the wave's last packet of it in an earlier row; the waves' chunks are joined at the end.
+// Only on the unsorted path (k_hmode / k_hmode_state decided it before the fork).
+__global__ __launch_bounds__(256) void k_heavy_recs(const BatchState *bs, const uint64_t *__restrict__ ts,
+                                                    const uint32_t *__restrict__ len,
+                                                    const uint8_t *__restrict__ tags, uint32_t n,
+                                                    const HeavySet *__restrict__ hs,
+                                                    HeavyTileRec *__restrict__ rec) {
+    __shared__ uint32_t h_s1[kHeavyMax], h_dmax[kHeavyMax], h_fo[kHeavyMax];
+    __shared__ unsigned long long h_s2[kHeavyMax], h_d2[kHeavyMax];
+    __shared__ unsigned long long h_first[4][kHeavyMax], h_last[4][kHeavyMax];
+    if (bs->err || !bs->hfast) return;
+    const uint32_t tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
+    const uint32_t ntiles = (n + kSortTile - 1) / kSortTile;
+    if (blockIdx.x >= ntiles) return;
+    const uint32_t t = xcd_swizzle(blockIdx.x, ntiles);
+    const uint32_t t0 = t * kSortTile, c0 = t0 + w * 1024u;
+    const uint64_t lt_mask = (1ull << lane) - 1ull;
+    const uint32_t nh = hs->n;
+    constexpr unsigned long long kNone = ~0ull;
+    if (tid < kHeavyMax) {
+        h_s1[tid] = 0; h_dmax[tid] = 0; h_fo[tid] = 0xFFFFFFFFu;
+        h_s2[tid] = 0; h_d2[tid] = 0;
+    }
+    for (uint32_t j = tid; j < 4 * kHeavyMax; j += 256) {
+        (&h_first[0][0])[j] = kNone;
+        (&h_last[0][0])[j] = kNone;
+    }
+    __syncthreads();
+    // the chunk's 16 rows loaded up front (the LDS ordering below is a compiler barrier)
+    uint64_t Tr[16];
+    uint32_t Lr[16], Gr[16];
+#pragma unroll
+    for (uint32_t r = 0; r < 16; ++r) {
+        const uint32_t i = c0 + r * 64u + lane;
+        const bool live = i < n;
+        Gr[r] = live ? tags[i] : 0u;
+        Tr[r] = ts[live ? i : 0u];
+        Lr[r] = len[live ? i : 0u];
+    }
+#pragma unroll
+    for (uint32_t r = 0; r < 16; ++r) {
+        const uint32_t i = c0 + r * 64u + lane;
+        const uint64_t T = Tr[r];
+        const uint32_t L = Lr[r], g = Gr[r];
+        const bool hv = g >= 0x80u && (g & 0x7Fu) < nh;
+        const uint64_t act = __ballot(hv);
+        if (!act) continue;
+        const uint32_t h = g & 0x7Fu;
+        const uint64_t peers = match_digit(h, act);
+        const uint64_t below = peers & lt_mask;
+        const uint32_t pl = below ? 63u - (uint32_t)__clzll((long long)below) : lane;
+        const uint64_t tpl = __shfl(T, (int)pl);
+        if (hv) {
+            uint64_t tp = tpl;
+            bool gap = below != 0;
+            if (!gap) {   // first of h in this row: the wave's last packet of h so far
+                tp = h_last[w][h];
+                gap = tp != kNone;
+                if (!gap) {
+                    h_first[w][h] = T;
+                    atomicMin(&h_fo[h], i - t0);
+                }
+            }
+            atomicAdd(&h_s1[h], L);
+            atomicAdd(&h_s2[h], (unsigned long long)L * L);
+            if (gap) {
+                const uint64_t d = T - tp;
+                atomicAdd(&h_d2[h], (unsigned long long)(d * d));
+                atomicMax(&h_dmax[h], d > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)d);
+            }
+            if ((peers >> lane) == 1ull) h_last[w][h] = T;   // the row's last of h
+        }
+        wave_lds_order();
+    }
+    __syncthreads();
+    if (tid >= kHeavyMax) return;
+    const uint32_t h = tid;   // join the waves' chunks: the gaps across chunk boundaries
+    uint64_t d2 = h_d2[h], first = kNone, last = kNone;
+    uint32_t dm = h_dmax[h];
+#pragma unroll
+    for (uint32_t ww = 0; ww < 4; ++ww) {
+        const uint64_t f = h_first[ww][h];
+        if (f == kNone) continue;
+        if (last != kNone) {
+            const uint64_t d = f - last;
+            d2 += d * d;
+            const uint32_t d32 = d > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)d;
+            dm = d32 > dm ? d32 : dm;
+        } else {
+            first = f;
+        }
+        last = h_last[ww][h];
+    }
+    HeavyTileRec &R = rec[t];
+    R.s1[h] = h_s1[h]; R.dmax[h] = dm; R.fo[h] = h_fo[h];
+    R.s2[h] = h_s2[h]; R.t0[h] = first; R.t1[h] = last; R.d2[h] = d2;
 }
 
 // ------------------------------------------------------------------ k_heavy_gather
@@ -532,9 +648,16 @@ hipError_t launch_hmode(BatchState *bs, const uint64_t *ts, uint32_t n, const Li
     return hipGetLastError();
 }
 
+hipError_t launch_heavy_recs(const BatchState *bs, const uint64_t *ts, const uint32_t *len, const uint8_t *tags,
+                             uint32_t n, const HeavySet *hs, void *rec, hipStream_t st) {
+    const uint32_t ntiles = std::max<uint32_t>(1, (n + kSortTile - 1) / kSortTile);
+    k_heavy_recs<<<ntiles, 256, 0, st>>>(bs, ts, len, tags, n, hs, static_cast<HeavyTileRec *>(rec));
+    return hipGetLastError();
+}
+
 hipError_t launch_hmode_state(BatchState *bs, const HeavySet *hs, const Slot *table, const Limits &lim,
-                              hipStream_t st) {
-    k_hmode_state<<<1, 128, 0, st>>>(bs, hs, table, lim);
+                              TableState *tstate, hipStream_t st) {
+    k_hmode_state<<<1, 128, 0, st>>>(bs, hs, table, lim, tstate);
     return hipGetLastError();
 }
 

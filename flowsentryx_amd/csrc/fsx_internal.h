@@ -124,8 +124,14 @@ struct TableState {
     uint32_t ever_nonmono;  // some batch (or batch boundary) went back in time
     uint32_t hist_cur;    // which of the two history buffers is current
     uint32_t max_len_seen;  // largest frame length of all batches so far
-    uint32_t pad_;
+    // a split sliding-window batch failed in its tail (k_sw_tail_check): every later split
+    // batch cancels itself there too, until the host has rolled them back and cleared it
+    uint32_t tail_fail;
+    // (kept by fsx_reset: diagnostics since fsx_open) fixed-window batches whose heavy
+    // sources took the unsorted path / the run path (k_hmode_state)
+    uint32_t n_hfast, n_hrun;
 };
+constexpr size_t kTableStateResetBytes = offsetof(TableState, n_hfast);
 
 // Sliding-window logs carried between batches: per source, the log of counted packets
 // still inside the window (<= pps_threshold entries, oldest first), packed by source in
@@ -590,11 +596,14 @@ hipError_t launch_pass0h(const uint64_t *in, uint64_t *out, uint32_t n, uint32_t
                          const uint32_t *offs, uint32_t tcap, BatchState *bs, uint64_t *pout, const uint64_t *ts,
                          const uint32_t *len, const uint8_t *tags, const uint32_t *chunk_cnt,
                          const uint64_t *lmask, void *rec,
-                         const HeavySet *hs, hipStream_t st);
+                         const HeavySet *hs, const uint64_t *pin, hipStream_t st);
 hipError_t launch_hmode(BatchState *bs, const uint64_t *ts, uint32_t n, const Limits &lim, hipStream_t st);
+// (FSX_PARSE_PAY: every sort tile's HeavyTileRec, at the start of the tail)
+hipError_t launch_heavy_recs(const BatchState *bs, const uint64_t *ts, const uint32_t *len, const uint8_t *tags,
+                             uint32_t n, const HeavySet *hs, void *rec, hipStream_t st);
 // (the tail's first kernel: the heavy sources' carried state, after the previous tail stored it)
 hipError_t launch_hmode_state(BatchState *bs, const HeavySet *hs, const Slot *table, const Limits &lim,
-                              hipStream_t st);
+                              TableState *tstate, hipStream_t st);
 hipError_t launch_heavy_gather(const BatchState *bs, const uint8_t *tags, const uint64_t *ts, const uint32_t *len,
                                uint32_t n, const uint32_t *offs, uint32_t tcap, const HeavySet *hs, uint32_t shift0,
                                uint64_t id_mask, uint64_t *out, uint64_t *pout, hipStream_t st);

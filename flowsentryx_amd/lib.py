@@ -500,7 +500,8 @@ class FsxContext:
 
     BATCH_INFO = ("ip_packets", "sources", "new_sources", "any_ipv6", "non_monotone",
                   "max_len", "max_ts", "allowed", "dropped", "prefix_rule_drops", "sorted_payload",
-                  "light_packets", "evicted", "heavy_unsorted", "admitted", "transient")
+                  "light_packets", "evicted", "heavy_unsorted", "admitted", "transient",
+                  "hfast_batches", "hrun_batches")
 
     def last_batch_info(self) -> dict:
         buf = (C.c_uint64 * len(self.BATCH_INFO))()

@@ -405,7 +405,9 @@ int fsx_pcap_records_device(fsx_ctx *ctx, const uint8_t *d_buf, const uint64_t *
  * later sort passes covered), [12] sources evicted before the batch
  * (FSX_FLAG_EVICT_IDLE), [13] 1 when the heavy sources' verdicts and flow rows were
  * computed outside the sort, 0 on the run path, [14] / [15] sources admitted
- * / transient (FSX_FLAG_OVERFLOW_ADMIT). Returns the number of entries written. */
+ * / transient (FSX_FLAG_OVERFLOW_ADMIT), [16] / [17] fixed-window batches since fsx_open
+ * (not cleared by fsx_reset) whose heavy sources took the unsorted path / the run path.
+ * Returns the number of entries written. */
 int fsx_last_batch_info(fsx_ctx *ctx, uint64_t *info, int cap);
 
 /* Per-kernel device timing for the benchmark: while enabled, every batch records a

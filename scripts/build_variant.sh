@@ -6,13 +6,8 @@ set -euo pipefail
 cd "$(dirname "$0")/.."
 name=$1; shift
 python3 - "$name" "$@" <<'PY'
-import subprocess, sys
+import sys
 from flowsentryx_amd import build as b
 name, defs = sys.argv[1], sys.argv[2:]
-out = b.PKG / f"libfsx_hip.{name}.so"
-cmd = [b.HIPCC, *b.COMMON, *defs, "-o", str(out), *[str(b.CSRC / s) for s in b.LIBS["libfsx_hip.so"]]]
-r = subprocess.run(cmd, capture_output=True, text=True)
-if r.returncode:
-    sys.exit(r.stderr)
-print(out)
+print(b.build_lib("libfsx_hip.so", extra=defs, out=b.PKG / f"libfsx_hip.{name}.so"))
 PY

@@ -328,3 +328,60 @@ def test_pipelined_sliding_window_history_full(native, oracle):
             assert cp.stats() == cu.stats() == o.stats()
             for m in MAPS:
                 assert cp.map_dump(m) == cu.map_dump(m) == o.map_dump(m), m
+
+
+def test_pipelined_sliding_window_history_full_then_fits(native, oracle):
+    """the batch after a split sliding-window batch that fails its history check
+    in its tail must not run, even when it would fit by itself (here: a small batch after a
+    large one that overflows). Its k_batch_check may run before the failure is known, so
+    the tail of every later split batch cancels itself (TableState::tail_fail): the state
+    equals an unpipelined context's that stopped at the failed batch, and the oracle's over
+    the batches before it."""
+    import torch
+    from flowsentryx_amd import lib
+    rng = np.random.default_rng(0x416)
+    B = 1 << 15   # history buffer: max(2 B, 64K) = 65536 entries
+    cfg = dict(limiter=1, pps_threshold=10**6, bps_threshold=10**12, window_ns=10**10, block_ns=10**9,
+               max_entries=1 << 16, max_batch=B)
+    sizes = [B, 20000, B, 4096, 2048]   # 32768 + 20000 fit; + 32768 overflows; + 4096 would fit
+    hdr, ln, ts = rand_stream(rng, sum(sizes), 3000, dt_max=100)
+    cuts = np.cumsum([0] + sizes)
+    batches = [(hdr[a:b], ln[a:b], ts[a:b]) for a, b in zip(cuts[:-1], cuts[1:])]
+    with native.FsxContext(**cfg) as cu:
+        failed = None
+        for j, b in enumerate(batches):
+            try:
+                cu.verdict_batch(*b)
+            except lib.FsxError as e:
+                assert e.code == -errno.ENOSPC
+                failed = j
+                break
+        assert failed == 2, failed
+        o = oracle.Oracle(**{k: v for k, v in cfg.items() if k != "max_batch"})
+        for b in batches[:failed]:
+            o.batch(*b)
+        for rep in range(3):   # (the race depends on timing: a few tries, each from empty maps)
+            with native.FsxContext(**cfg) as cp:
+                cp.set_pipeline(True)
+                d = [(_dev(torch, h), _dev(torch, l), _dev(torch, t), torch.empty(len(l), dtype=torch.uint8, device="cuda"))
+                     for h, l, t in batches]
+                raised = False
+                for x, b in zip(d, batches):
+                    try:
+                        cp.verdict_batch_device(x[0].data_ptr(), x[1].data_ptr(), x[2].data_ptr(), len(b[1]),
+                                                x[3].data_ptr())
+                    except lib.FsxError as e:
+                        assert e.code == -errno.ENOSPC
+                        raised = True
+                        break
+                if not raised:
+                    with pytest.raises(lib.FsxError) as e:
+                        cp.sync()
+                    assert e.value.code == -errno.ENOSPC
+                cp.sync()
+                assert cp.stats() == cu.stats() == o.stats(), rep
+                for m in MAPS:
+                    assert cp.map_dump(m) == cu.map_dump(m) == o.map_dump(m), (rep, m)
+                # after the rollback the context works on: the small batch now runs and fits
+                cp.verdict_batch(*batches[3])
+                cp.sync()
