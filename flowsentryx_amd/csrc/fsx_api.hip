@@ -912,7 +912,7 @@ static int evict_idle(fsx_ctx *c, const PacketIn &in, const uint64_t *d_ts, size
                                   (unsigned long long)m, (unsigned long long)count);
     if (m == count) return 0;   // nothing idle: the batch decides (-ENOSPC if it overflows)
     if ((rc = next_epoch(c))) return rc;
-    HIPCHK(c, hipMemsetAsync(c->table, 0, c->slots * sizeof(Slot), c->stream));
+    HIPCHK(c, launch_clear(c->table, c->slots * sizeof(Slot), c->stream));
     e = launch_evict_reinsert(c->table, c->tstate, c->lim, table_index(c), c->evict_buf, m, c->stream);
     if (e != hipSuccess) return set_err(c, -EIO, "evict reinsert: %s", hipGetErrorString(e));
     c->last_evicted = count - m;
@@ -1346,7 +1346,7 @@ int fsx_reset(fsx_ctx *c) {
     if (pipe_busy(c) && (rc = fsx_sync(c))) return rc;   // (pipelined batches)
     c->pending_born = 0;   // the whole table is wiped: no rollback of a pending batch
     c->count_bound = 0;    // (no source is tracked after the reset: ADVICE r04)
-    HIPCHK(c, hipMemsetAsync(c->table, 0, c->slots * sizeof(Slot), c->stream));
+    HIPCHK(c, launch_clear(c->table, c->slots * sizeof(Slot), c->stream));
     HIPCHK(c, hipMemsetAsync(c->tstate, 0, kTableStateResetBytes, c->stream));   // (path counters kept)
     return next_epoch(c);   // (the prefix blocklists stay: configuration)   // every index head reads empty
 }

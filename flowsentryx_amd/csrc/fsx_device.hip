@@ -3166,6 +3166,37 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
     return launch_tail(ta);
 }
 
+// ------------------------------------------------------------------ table clear
+// fsx_reset / the eviction rebuild: the slot table zeroed with 16-byte stores, each wave
+// writing 1 KiB runs (whole lines), four stores in flight per lane, XCD-contiguous chunks
+// (FSX_CLEAR_MEMSET=1: hipMemsetAsync, A/B; config 5's 32 GiB table).
+__global__ __launch_bounds__(256) void k_clear16(uint4 *__restrict__ p, uint64_t n16) {
+    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+    v4u *q = reinterpret_cast<v4u *>(p);
+    const uint64_t nb = gridDim.x;
+    const uint64_t b = xcd_swizzle(blockIdx.x, gridDim.x);
+    // block b owns the contiguous share [lo, hi) of the 16-byte words
+    const uint64_t lo = n16 * b / nb, hi = n16 * (b + 1) / nb;
+    const v4u z = {0u, 0u, 0u, 0u};
+    uint64_t i = lo + threadIdx.x;
+    for (; i + 768 < hi; i += 1024) {
+        __builtin_nontemporal_store(z, q + i);
+        __builtin_nontemporal_store(z, q + i + 256);
+        __builtin_nontemporal_store(z, q + i + 512);
+        __builtin_nontemporal_store(z, q + i + 768);
+    }
+    for (; i < hi; i += 256) __builtin_nontemporal_store(z, q + i);
+}
+
+hipError_t launch_clear(void *p, uint64_t bytes, hipStream_t st) {
+    static const bool memset = getenv("FSX_CLEAR_MEMSET") != nullptr;
+    if (memset || (bytes & 15) || (reinterpret_cast<uintptr_t>(p) & 15)) return hipMemsetAsync(p, 0, bytes, st);
+    const uint64_t n16 = bytes / 16;
+    const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(8192, n16 / 4096));
+    k_clear16<<<grid, 256, 0, st>>>(static_cast<uint4 *>(p), n16);
+    return hipGetLastError();
+}
+
 // ------------------------------------------------------------------ map syscalls
 // op: 0 lookup, 1 update, 2 delete. Result: 0 / -ENOENT(-2) / -EEXIST(-17) / -ENOSPC(-28).
 // Map id -> table tag (1 IPv4, 2 IPv6) and slot flag bit (include/fsx_hip.h map ids).

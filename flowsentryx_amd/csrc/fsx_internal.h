@@ -662,6 +662,9 @@ hipError_t launch_map_dump(const Slot *table, const Limits &lim, int map_id, uin
                            uint64_t *d_vals, uint64_t cap, unsigned long long *d_count,
                            hipStream_t st);
 
+// Zero `bytes` of device memory on st (the slot table: fsx_reset, eviction).
+hipError_t launch_clear(void *p, uint64_t bytes, hipStream_t st);
+
 hipError_t launch_score(const float *feat, size_t n, float *prob, uint8_t *dec,
                         const int8_t w[8], float inv_in, int32_t zp_in, float bias_over_ats,
                         float mult, int32_t zp_out, const uint8_t lut[256], hipStream_t st);

@@ -10,6 +10,7 @@
 #   timeline       kernel timeline of 3 steps                         -> timeline_TAG.txt
 #   pmc            PMC passes (FETCH_SIZE, WRITE_SIZE, SQ) + summary  -> pmc_TAG/
 #   ab=V1,V2,..    A/B of library variants (scripts/ab.sh)           -> TAG_ab.txt
+#   leg=LEG        A/B of one bench leg under env settings $LEG_ENVS (";"-separated, scripts/ab_leg.sh)
 # Env: BENCH_ARGS (bench / prof / pmc / timeline / ab), PROF_LEGS, LEG (prof: a bench leg
 # run as the headline: config4 / config5 / config3).
 set -u
@@ -53,6 +54,11 @@ for s in "$@"; do
       IFS=, read -r -a vs <<< "${s#ab=}"
       AB_ARGS="${BENCH_ARGS:-}" run ab 900 bash scripts/ab.sh "${vs[@]}" > "gpurun_out/${TAG}_ab.txt" 2>&1 || exit $?
       cat "gpurun_out/${TAG}_ab.txt" ;;
+    leg=*)
+      IFS=';' read -r -a es <<< "${LEG_ENVS:-}"
+      [ ${#es[@]} -eq 0 ] && es=("")
+      run leg 1000 bash scripts/ab_leg.sh "${s#leg=}" "${es[@]}" > "gpurun_out/${TAG}_leg.txt" 2>&1 || exit $?
+      cat "gpurun_out/${TAG}_leg.txt" ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
