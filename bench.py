@@ -18,9 +18,12 @@ of 16/32-byte records to the owners, the pipeline there, verdicts back
 (flowsentryx_amd/shard.py).
 
 Prints ONE JSON line on rank 0 with the driver's contract plus:
-  roofline      the dominant kernel (largest device time per step): SURVEY §8 d
-                algorithmic bytes per launch (77 B per packet for k_parse) over its mean
-                launch time, HIP events on the library's stream (separate steps);
+  roofline      the dominant kernel (longest mean launch), k_parse: the bytes it must move
+                per launch over its mean launch time (HIP events on the library's stream,
+                separate steps). With the heavy sources outside the sort (the headline)
+                k_parse reads no timestamps — k_pass0h does — so its algorithmic bytes are
+                the 64-byte record + 4-byte length in and the verdict byte out, 69 B per
+                packet ("k_parse/hfm" below); otherwise SURVEY §8 d's 77 B per packet;
   pipeline      the whole step against SURVEY §8 d: 77 B/packet + 64 B per source;
   check         full-size parity of the benchmarked step (outside the timed region):
                 verdicts, stats_map and every map entry against the sharded CPU oracle,
@@ -488,6 +491,7 @@ def main():
         torch.cuda.synchronize()
         barrier()
         i0 = ctx.last_batch_info()   # (the device is idle: no wait inside the timed region)
+        hr0 = plane.host_reads if plane is not None else 0
         t0 = time.perf_counter()
         for k in range(warmup, warmup + steps):
             step(k)
@@ -503,6 +507,8 @@ def main():
         # at N > 1
         out["heavy_path"] = {"unsorted": info["hfast_batches"] - i0["hfast_batches"],
                              "run": info["hrun_batches"] - i0["hrun_batches"]}
+        if plane is not None:   # the sharded plane's host synchronizations per timed step
+            out["host_reads_per_step"] = (plane.host_reads - hr0) / steps
         if ntime:
             # per-kernel device times (a HIP event after every kernel) from separate steps
             # (the stream continued; timed batches run unpipelined), so the timed steps
@@ -526,6 +532,7 @@ def main():
                                "dropped_by_replica": ex.get("filtered", 0),
                                "flow_partials_sent": getattr(plane, "partials_sent", 0), "sub_batches": chunks,
                                "record_bytes": sorted(plane.formats) or None,
+                               "host_reads_per_step": out.get("host_reads_per_step"),
                                "backend": args.dist_backend}
             out["stats"] = plane.stats()
             out["sources"] = None

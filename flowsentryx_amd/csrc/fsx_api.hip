@@ -1088,6 +1088,19 @@ int fsx_flow_partials_records_device(fsx_ctx *c, const void *d_records, size_t n
     return run_records(c, d_records, n, rec_bytes, c->d_verdict, &fr, false);
 }
 
+int fsx_flows_merge_counted_device(fsx_ctx *c, const void *d_partials, size_t cap, const uint64_t *d_count) {
+    if (!c || !d_count) return -EINVAL;
+    if (!c->flow_accum) return set_err(c, -EINVAL, "fsx_flows_merge_counted_device outside fsx_flows_begin .. end");
+    if (cap && !d_partials) return set_err(c, -EINVAL, "null buffer");
+    if (cap > 0xFFFFFFFFu) return set_err(c, -E2BIG, "cap=%zu too large", cap);
+    int rc = sel(c);
+    if (rc) return rc;
+    hipError_t e = launch_flows_merge(d_partials, (uint32_t)cap, c->table, c->lim, c->d_slot_acc, c->flow_epoch,
+                                      c->stream, d_count);
+    if (e != hipSuccess) return set_err(c, -EIO, "flows merge: %s", hipGetErrorString(e));
+    return 0;
+}
+
 int fsx_flows_merge_device(fsx_ctx *c, const void *d_partials, size_t m) {
     if (!c) return -EINVAL;
     if (!c->flow_accum) return set_err(c, -EINVAL, "fsx_flows_merge_device outside fsx_flows_begin .. end");
@@ -1506,9 +1519,9 @@ uint32_t fsx_shard_owner(const uint8_t *key16, int family, uint32_t n_shards) {
     return shard_owner_of(family == 6 ? 2u : 1u, k, n_shards);
 }
 
-int fsx_shard_pack_device(fsx_ctx *c, const uint8_t *d_hdr, const uint32_t *d_len, const uint64_t *d_ts,
-                          size_t n, uint32_t G, uint32_t flags, uint8_t *d_verdict, void *d_records,
-                          uint32_t *d_send_idx, uint64_t *d_counts) {
+static int shard_pack(fsx_ctx *c, const uint8_t *d_hdr, const uint32_t *d_len, const uint64_t *d_ts, size_t n,
+                      uint32_t G, uint32_t flags, const uint32_t *d_filter, uint8_t *d_verdict, void *d_records,
+                      uint32_t *d_send_idx, uint64_t *d_counts) {
     if (!c) return -EINVAL;
     if (G == 0 || G > FSX_MAX_SHARDS) return set_err(c, -EINVAL, "n_shards must be 1..%d", FSX_MAX_SHARDS);
     if (n > kMaxBatchLimit) return set_err(c, -E2BIG, "n=%zu too large", n);
@@ -1540,8 +1553,31 @@ int fsx_shard_pack_device(fsx_ctx *c, const uint8_t *d_hdr, const uint32_t *d_le
     const bool drop_rec = filt && (flags & FSX_SHARD_DROP_RECORDS);
     hipError_t e = launch_shard_pack(d_hdr, d_len, d_ts, (uint32_t)n, G, d_verdict, d_records, d_send_idx,
                                      d_counts, c->d_shard_cnt, c->d_shard_own, c->d_shard_crec,
-                                     filt ? &rep : nullptr, compact, drop_rec, c->stream);
+                                     filt ? &rep : nullptr, compact, drop_rec, filt ? d_filter : nullptr, c->stream);
     if (e != hipSuccess) return set_err(c, -EIO, "shard pack: %s", hipGetErrorString(e));
+    return 0;
+}
+
+int fsx_shard_pack_device(fsx_ctx *c, const uint8_t *d_hdr, const uint32_t *d_len, const uint64_t *d_ts,
+                          size_t n, uint32_t G, uint32_t flags, uint8_t *d_verdict, void *d_records,
+                          uint32_t *d_send_idx, uint64_t *d_counts) {
+    return shard_pack(c, d_hdr, d_len, d_ts, n, G, flags, nullptr, d_verdict, d_records, d_send_idx, d_counts);
+}
+
+int fsx_shard_pack_filtered_device(fsx_ctx *c, const uint8_t *d_hdr, const uint32_t *d_len, const uint64_t *d_ts,
+                                   size_t n, uint32_t G, uint32_t flags, const uint32_t *d_filter,
+                                   uint8_t *d_verdict, void *d_records, uint32_t *d_send_idx, uint64_t *d_counts) {
+    if (!d_filter) return c ? set_err(c, -EINVAL, "null filter flag") : -EINVAL;
+    return shard_pack(c, d_hdr, d_len, d_ts, n, G, flags | FSX_SHARD_FILTER_BLOCKLIST, d_filter, d_verdict,
+                      d_records, d_send_idx, d_counts);
+}
+
+int fsx_shard_filter_plan_device(fsx_ctx *c, const uint64_t *d_clocks, uint32_t G, uint32_t k, uint32_t *d_filter) {
+    if (!c || !d_clocks || !d_filter || G == 0 || G > FSX_MAX_SHARDS || k == 0) return -EINVAL;
+    int rc = sel(c);
+    if (rc) return rc;
+    hipError_t e = launch_filter_plan(d_clocks, G, k, d_filter, c->stream);
+    if (e != hipSuccess) return set_err(c, -EIO, "filter plan: %s", hipGetErrorString(e));
     return 0;
 }
 
@@ -1563,6 +1599,26 @@ int fsx_blocklist_export_device(fsx_ctx *c, void *d_entries, size_t cap, uint64_
     hipError_t e = launch_blocklist_export(c->table, c->lim.table_mask, reinterpret_cast<ShardBlock *>(d_entries),
                                            cap, reinterpret_cast<unsigned long long *>(d_count), c->stream);
     if (e != hipSuccess) return set_err(c, -EIO, "blocklist export: %s", hipGetErrorString(e));
+    return 0;
+}
+
+int fsx_blocklist_replica_blocks_device(fsx_ctx *c, const void *d_blocks, uint32_t n_blocks, size_t cap) {
+    if (!c || (n_blocks && cap && !d_blocks)) return -EINVAL;
+    int rc = sel(c);
+    if (rc) return rc;
+    const uint64_t need = next_pow2(std::max<uint64_t>(64, 2 * (uint64_t)n_blocks * cap));
+    if (need > c->rep_slots) {
+        HIPCHK(c, hipStreamSynchronize(c->stream));   // (grows once: capacities are fixed per plane)
+        hipFree(c->d_rep);
+        c->d_rep = nullptr;
+        c->rep_slots = 0;
+        c->rep_valid = false;
+        HIPCHK(c, hipMalloc(&c->d_rep, need * sizeof(ShardBlock)));
+        c->rep_slots = need;
+    }
+    hipError_t e = launch_replica_build_blocks(d_blocks, n_blocks, cap, c->d_rep, c->rep_slots - 1, c->stream);
+    if (e != hipSuccess) return set_err(c, -EIO, "replica build: %s", hipGetErrorString(e));
+    c->rep_valid = true;
     return 0;
 }
 

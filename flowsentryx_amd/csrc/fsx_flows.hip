@@ -424,9 +424,12 @@ __global__ __launch_bounds__(256) void k_flows_end(const SlotAcc *__restrict__ s
 // Accumulate mode: partial i of m (distinct sources) merges into its source's SlotAcc of the
 // epoch as the call after everything merged so far (the flow_finish merge, with the partial's
 // own first / last timestamps); a source absent from the table is skipped.
-__global__ __launch_bounds__(256) void k_flows_merge(const FlowPartial *__restrict__ part, uint32_t m,
+__global__ __launch_bounds__(256) void k_flows_merge(const FlowPartial *__restrict__ part, uint32_t m0,
+                                                     const unsigned long long *__restrict__ d_m,
                                                      const Slot *__restrict__ table, Limits lim, SlotAcc *sacc,
                                                      uint32_t epoch) {
+    // (d_m: the count on the device, at most m0: a fixed-capacity exchange block)
+    const uint32_t m = d_m ? (uint32_t)(*d_m < m0 ? *d_m : m0) : m0;
     for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < m; i += gridDim.x * 256u) {
         const FlowPartial p = part[i];
         const uint32_t s = table_find(table, lim, p.tag, p.key);
@@ -449,11 +452,12 @@ __global__ __launch_bounds__(256) void k_flows_merge(const FlowPartial *__restri
 }
 
 hipError_t launch_flows_merge(const void *partials, uint32_t m, const Slot *table, const Limits &lim, void *sacc,
-                              uint32_t epoch, hipStream_t st) {
+                              uint32_t epoch, hipStream_t st, const uint64_t *d_m) {
     (void)hipGetLastError();
     if (m == 0) return hipSuccess;
     k_flows_merge<<<std::min<uint32_t>(1024, (m + 255) / 256), 256, 0, st>>>(
-        static_cast<const FlowPartial *>(partials), m, table, lim, static_cast<SlotAcc *>(sacc), epoch);
+        static_cast<const FlowPartial *>(partials), m, reinterpret_cast<const unsigned long long *>(d_m), table, lim,
+        static_cast<SlotAcc *>(sacc), epoch);
     return hipGetLastError();
 }
 

@@ -624,8 +624,9 @@ hipError_t launch_hflow_finish(const BatchState *bs, const uint32_t *cnt0, const
 size_t flow_acc_bytes();
 size_t slot_acc_bytes();
 // Accumulate mode: merge m flow partials (fsx_flow_partial) into the epoch's per-slot sums.
+// (d_m non-null: the count is min(*d_m, m), read on the device)
 hipError_t launch_flows_merge(const void *partials, uint32_t m, const Slot *table, const Limits &lim, void *sacc,
-                              uint32_t epoch, hipStream_t st);
+                              uint32_t epoch, hipStream_t st, const uint64_t *d_m = nullptr);
 // Rows of every source accumulated in epoch `epoch` (slots of the table), *d_count = rows.
 hipError_t launch_flows_end(const void *sacc, uint32_t epoch, const Slot *table, uint64_t slots,
                             uint8_t *keys16, uint8_t *fam, float *feat, float *prob, uint8_t *dec,

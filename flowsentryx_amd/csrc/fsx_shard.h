@@ -82,12 +82,16 @@ __host__ __device__ inline uint32_t shard_owner_of(uint32_t tag, const uint32_t 
 hipError_t launch_shard_pack(const uint8_t *hdr, const uint32_t *len, const uint64_t *ts, uint32_t n,
                              uint32_t G, uint8_t *verdict, void *rec, uint32_t *send_idx,
                              uint64_t *owner_total, uint32_t *scratch, uint8_t *own8, void *crec,
-                             const Replica *rep, bool compact, bool drop_rec, hipStream_t st);
+                             const Replica *rep, bool compact, bool drop_rec, const uint32_t *use_dev,
+                             hipStream_t st);
 hipError_t launch_shard_clock(const uint64_t *ts, uint32_t n, uint64_t *out3, hipStream_t st);
 hipError_t launch_blocklist_export(const Slot *table, uint64_t table_mask, ShardBlock *out, uint64_t cap,
                                    unsigned long long *count, hipStream_t st);
 hipError_t launch_replica_build(const ShardBlock *in, uint64_t m, ShardBlock *slots, uint64_t mask,
                                 hipStream_t st);
+hipError_t launch_replica_build_blocks(const void *blocks, uint32_t nb, uint64_t cap, ShardBlock *slots,
+                                       uint64_t mask, hipStream_t st);
+hipError_t launch_filter_plan(const uint64_t *clk, uint32_t G, uint32_t k, uint32_t *out, hipStream_t st);
 hipError_t launch_shard_unpack(const void *rec, uint32_t rec_bytes, uint32_t m, uint8_t *hdr, uint32_t *len,
                                uint64_t *ts, hipStream_t st);
 hipError_t launch_shard_scatter(const uint8_t *ret, const uint32_t *send_idx, uint32_t m, uint8_t *verdict,

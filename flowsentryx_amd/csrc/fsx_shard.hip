@@ -116,7 +116,8 @@ __global__ __launch_bounds__(256) void k_shard_parse(const uint8_t *__restrict__
                                                      const uint32_t *__restrict__ len,
                                                      const uint64_t *__restrict__ ts, uint32_t n,
                                                      uint32_t G, uint32_t *__restrict__ cnt,
-                                                     uint32_t ntiles, Replica rep, int use_rep,
+                                                     uint32_t ntiles, Replica rep, int use_rep0,
+                                                     const uint32_t *__restrict__ use_dev,
                                                      unsigned long long *wide,
                                                      uint8_t *__restrict__ verdict,
                                                      uint8_t *__restrict__ own8,
@@ -124,6 +125,8 @@ __global__ __launch_bounds__(256) void k_shard_parse(const uint8_t *__restrict__
                                                      uint64_t *__restrict__ owner_total, uint32_t drop_rec) {
     __shared__ uint32_t s_rec[4][64 * 17];
     __shared__ uint32_t sh[kMaxShards + 1];
+    // (use_dev: the sub-batch's filter decision, made on the device: fsx_shard_filter_plan_device)
+    const int use_rep = use_rep0 && (!use_dev || *use_dev);
     const uint32_t t = blockIdx.x, lane = lane_id(), w = threadIdx.x >> 6;
     if (threadIdx.x <= kMaxShards) sh[threadIdx.x] = 0;
     __syncthreads();
@@ -291,8 +294,10 @@ __global__ __launch_bounds__(256) void k_shard_pack(const uint8_t *__restrict__ 
                                                     uint32_t ntiles, void *__restrict__ rec,
                                                     uint32_t *__restrict__ send_idx,
                                                     uint8_t *__restrict__ verdict, Replica rep,
-                                                    int use_rep, uint64_t *__restrict__ owner_total,
+                                                    int use_rep0, const uint32_t *__restrict__ use_dev,
+                                                    uint64_t *__restrict__ owner_total,
                                                     int compact, uint32_t drop_rec) {
+    const int use_rep = use_rep0 && (!use_dev || *use_dev);
     if (compact && owner_total[G + 1] == 16u) return;   // k_shard_pack16 places the records
     __shared__ uint32_t s_base[kMaxShards + 1];
     __shared__ uint32_t s_wc[4][kMaxShards + 1];
@@ -437,7 +442,8 @@ __global__ void k_shard_empty(uint64_t *owner_total, uint32_t G, int compact) {
 hipError_t launch_shard_pack(const uint8_t *hdr, const uint32_t *len, const uint64_t *ts, uint32_t n,
                              uint32_t G, uint8_t *verdict, void *rec, uint32_t *send_idx,
                              uint64_t *owner_total, uint32_t *scratch, uint8_t *own8, void *crec,
-                             const Replica *rep, bool compact, bool drop_rec, hipStream_t st) {
+                             const Replica *rep, bool compact, bool drop_rec, const uint32_t *use_dev,
+                             hipStream_t st) {
     (void)hipGetLastError();   // a stale error of another caller is not ours
     k_shard_empty<<<1, 1, 0, st>>>(owner_total, G, compact);   // also the wide flag / filtered
     if (n == 0) return hipGetLastError();
@@ -448,15 +454,15 @@ hipError_t launch_shard_pack(const uint8_t *hdr, const uint32_t *len, const uint
     if (wide) k_shard_fmt_init<<<1, 1, 0, st>>>(wide);
     ShardRecord16 *cr = compact ? reinterpret_cast<ShardRecord16 *>(crec) : nullptr;
     const uint32_t dr = drop_rec && use ? 1u : 0u;   // (records of the replica drops: group G)
-    k_shard_parse<<<ntiles, 256, 0, st>>>(hdr, len, ts, n, G, scratch, ntiles, r, use, wide, verdict, own8, cr,
-                                          owner_total, dr);
+    k_shard_parse<<<ntiles, 256, 0, st>>>(hdr, len, ts, n, G, scratch, ntiles, r, use, use_dev, wide, verdict,
+                                          own8, cr, owner_total, dr);
     k_shard_scan<<<G + dr, 1024, 0, st>>>(scratch, owner_total, G, ntiles, compact);
     if (compact)
         k_shard_pack16<<<ntiles, 256, 0, st>>>(own8, cr, n, G, scratch, ntiles,
                                                reinterpret_cast<ShardRecord16 *>(rec), send_idx, owner_total,
                                                G + dr);
     k_shard_pack<<<ntiles, 256, 0, st>>>(hdr, len, ts, n, G, scratch, ntiles, rec, send_idx, verdict, r,
-                                         use, owner_total, compact, dr);
+                                         use, use_dev, owner_total, compact, dr);
     return hipGetLastError();
 }
 
@@ -549,6 +555,83 @@ hipError_t launch_replica_build(const ShardBlock *in, uint64_t m, ShardBlock *sl
     if (m == 0) return hipGetLastError();
     const uint32_t grid = (uint32_t)std::min<uint64_t>(1024, (m + 255) / 256);
     k_replica_build<<<grid, 256, 0, st>>>(in, m, slots, mask);
+    return hipGetLastError();
+}
+
+// The replica from n_blocks all-gathered fixed-capacity blocks (fsx_blocklist_replica_blocks_device):
+// block b = a 32-byte header (its entry count, int64) then cap entries; min(count, cap) used.
+__global__ __launch_bounds__(256) void k_replica_build_blocks(const uint8_t *__restrict__ blocks, uint32_t nb,
+                                                              uint64_t cap, ShardBlock *slots, uint64_t mask) {
+    const uint64_t per = (cap + 1) * sizeof(ShardBlock);
+    for (uint32_t b = 0; b < nb; ++b) {
+        const uint8_t *blk = blocks + (size_t)b * per;
+        const uint64_t cnt = *reinterpret_cast<const unsigned long long *>(blk);
+        const uint64_t m = cnt < cap ? cnt : cap;
+        const ShardBlock *in = reinterpret_cast<const ShardBlock *>(blk + sizeof(ShardBlock));
+        for (uint64_t j = (uint64_t)blockIdx.x * 256u + threadIdx.x; j < m; j += (uint64_t)gridDim.x * 256u) {
+            const ShardBlock e = in[j];
+            uint64_t i = slot_hash(e.tag, e.key, kReplicaSeed) & mask;
+            for (uint64_t probes = 0; probes <= mask; ++probes) {
+                if (atomicCAS(&slots[i].tag, 0u, e.tag) == 0u) {
+                    slots[i].key[0] = e.key[0]; slots[i].key[1] = e.key[1];
+                    slots[i].key[2] = e.key[2]; slots[i].key[3] = e.key[3];
+                    slots[i].till = e.till;
+                    break;
+                }
+                i = (i + 1) & mask;
+            }
+        }
+    }
+}
+
+hipError_t launch_replica_build_blocks(const void *blocks, uint32_t nb, uint64_t cap, ShardBlock *slots,
+                                       uint64_t mask, hipStream_t st) {
+    (void)hipGetLastError();   // a stale error of another caller is not ours
+    const uint32_t cgrid = (uint32_t)std::min<uint64_t>(1024, (mask + 256) / 256);
+    k_replica_clear<<<cgrid, 256, 0, st>>>(slots, mask);
+    if (nb == 0 || cap == 0) return hipGetLastError();
+    const uint32_t grid = (uint32_t)std::min<uint64_t>(1024, (cap + 255) / 256);
+    k_replica_build_blocks<<<grid, 256, 0, st>>>(static_cast<const uint8_t *>(blocks), nb, cap, slots, mask);
+    return hipGetLastError();
+}
+
+// The replica filter's per-sub-batch decision from every rank's piece clocks
+// {min, max, decreases} ([G][k][3], all-gathered; an empty piece is {~0, 0, 0}): sub-batch j
+// filters iff no piece of it goes back, its pieces follow each other in rank order, and no
+// earlier sub-batch holds a packet later than its first — the global clock does not go back
+// up to it, so no earlier packet can have deleted a replica entry at a later time.
+__global__ void k_filter_plan(const unsigned long long *__restrict__ clk, uint32_t G, uint32_t k,
+                              uint32_t *__restrict__ out) {
+    if (threadIdx.x || blockIdx.x) return;
+    bool any_prev = false;
+    uint64_t prev_hi = 0;
+    for (uint32_t j = 0; j < k; ++j) {
+        bool ok = true, seen = false, have = false;
+        uint64_t last = 0, lo = 0, hi = 0;
+        for (uint32_t r = 0; r < G; ++r) {
+            const unsigned long long *c = clk + 3ull * ((uint64_t)r * k + j);
+            const uint64_t mn = c[0], mx = c[1];
+            if (c[2]) ok = false;
+            if (mx == 0 && mn == ~0ull) continue;   // empty piece
+            if (seen && mn < last) ok = false;
+            seen = true;
+            last = mx;
+            lo = have ? (mn < lo ? mn : lo) : mn;
+            hi = have ? (mx > hi ? mx : hi) : mx;
+            have = true;
+        }
+        if (ok && any_prev && have && lo < prev_hi) ok = false;
+        out[j] = ok ? 1u : 0u;
+        if (have) {
+            prev_hi = any_prev ? (hi > prev_hi ? hi : prev_hi) : hi;
+            any_prev = true;
+        }
+    }
+}
+
+hipError_t launch_filter_plan(const uint64_t *clk, uint32_t G, uint32_t k, uint32_t *out, hipStream_t st) {
+    (void)hipGetLastError();
+    k_filter_plan<<<1, 1, 0, st>>>(reinterpret_cast<const unsigned long long *>(clk), G, k, out);
     return hipGetLastError();
 }
 

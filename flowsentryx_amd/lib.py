@@ -145,6 +145,11 @@ def load_library() -> C.CDLL:
         "fsx_flows_end": (C.c_int, [vp, vp, vp, vp, vp, vp, sz, vp]),
         "fsx_flow_partials_records_device": (C.c_int, [vp, vp, sz, C.c_uint32, C.c_uint32, vp, sz, vp]),
         "fsx_flows_merge_device": (C.c_int, [vp, vp, sz]),
+        "fsx_flows_merge_counted_device": (C.c_int, [vp, vp, sz, vp]),
+        "fsx_shard_pack_filtered_device": (C.c_int, [vp, vp, vp, vp, sz, C.c_uint32, C.c_uint32, vp, vp, vp,
+                                                     vp, vp]),
+        "fsx_shard_filter_plan_device": (C.c_int, [vp, vp, C.c_uint32, C.c_uint32, vp]),
+        "fsx_blocklist_replica_blocks_device": (C.c_int, [vp, vp, C.c_uint32, sz]),
         "fsx_last_timings": (C.c_int, [vp, vp, vp, vp, C.c_int, C.c_int, C.POINTER(C.c_int)]),
         "fsx_enable_timing": (C.c_int, [vp, C.c_int]),
         "fsx_last_batch_info": (C.c_int, [vp, vp, C.c_int]),
@@ -175,6 +180,8 @@ ABI_SYMBOLS = [
     "fsx_get_stats",
     "fsx_reset", "fsx_load_q8_model", "fsx_score", "fsx_score_device", "fsx_flow_features",
     "fsx_flows_begin", "fsx_flows_end", "fsx_flow_partials_records_device", "fsx_flows_merge_device",
+    "fsx_flows_merge_counted_device", "fsx_shard_pack_filtered_device", "fsx_shard_filter_plan_device",
+    "fsx_blocklist_replica_blocks_device",
     "fsx_last_timings", "fsx_enable_timing", "fsx_last_batch_info",
     "fsx_shard_owner", "fsx_shard_pack_device", "fsx_shard_unpack_device", "fsx_shard_unpack16_device",
     "fsx_shard_scatter_device", "fsx_shard_clock_device", "fsx_blocklist_export_device",
@@ -517,6 +524,27 @@ class FsxContext:
         self._check(self._lib.fsx_shard_pack_device(self._h, d_hdr, d_len, d_ts, n, n_shards,
                                                     flags, d_verdict, d_records, d_send_idx,
                                                     d_counts), "fsx_shard_pack_device")
+
+    def shard_pack_filtered_device(self, d_hdr: int, d_len: int, d_ts: int, n: int, n_shards: int,
+                                   d_filter: int, d_verdict: int, d_records: int, d_send_idx: int,
+                                   d_counts: int, flags: int = 0):
+        """shard_pack_device with the replica filter iff the device word *d_filter != 0."""
+        self._check(self._lib.fsx_shard_pack_filtered_device(self._h, d_hdr, d_len, d_ts, n, n_shards, flags,
+                                                             d_filter, d_verdict, d_records, d_send_idx,
+                                                             d_counts), "fsx_shard_pack_filtered_device")
+
+    def shard_filter_plan_device(self, d_clocks: int, n_shards: int, k: int, d_filter: int):
+        self._check(self._lib.fsx_shard_filter_plan_device(self._h, d_clocks, n_shards, k, d_filter),
+                    "fsx_shard_filter_plan_device")
+
+    def blocklist_replica_blocks_device(self, d_blocks: int, n_blocks: int, cap: int):
+        self._check(self._lib.fsx_blocklist_replica_blocks_device(self._h, d_blocks, n_blocks, cap),
+                    "fsx_blocklist_replica_blocks_device")
+
+    def flows_merge_counted_device(self, d_partials: int, cap: int, d_count: int):
+        """Between flows_begin and flows_end: merge min(*d_count, cap) partials (device count)."""
+        self._check(self._lib.fsx_flows_merge_counted_device(self._h, d_partials, cap, d_count),
+                    "fsx_flows_merge_counted_device")
 
     def shard_clock_device(self, d_ts: int, n: int, d_out3: int):
         self._check(self._lib.fsx_shard_clock_device(self._h, d_ts, n, d_out3),

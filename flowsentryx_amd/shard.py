@@ -16,12 +16,13 @@ unchanged batch pipeline on all of that source's packets:
                senders used both record sizes: records -> header records first) — maps,
                verdicts, optionally flow features + MLP scores of the owned sources
   4. all-to-all of the verdicts back (1 byte per packet), scatter to arrival positions
-  5. all-gather of every owner's live blacklist entries (the replicated blocklist);
-     the next sub-batch's pack drops packets of replica-blacklisted sources locally
-     (now <= till: the owner would drop them without touching any state,
-     src/fsx_kern.c:189-215) — taken only when that sub-batch's clock is non-decreasing
-     in global order (one all-gather of {min, max, decreases} per rank), which is exactly
-     the condition under which no earlier packet can have deleted the entry
+  5. all-gather of every owner's live blacklist entries (the replicated blocklist, once per
+     global batch, fixed-capacity blocks whose counts stay on the device); the packs drop
+     packets of replica-blacklisted sources locally (now <= till: the owner would drop them
+     without touching any state, src/fsx_kern.c:189-215) — for the sub-batches whose
+     global clock does not go back up to their end (one all-gather of {min, max,
+     decreases} per piece, the decision made on the device), which is exactly the
+     condition under which no earlier packet can have deleted the entry
   6. stats_map = all-reduce(sum) of the owners' counters + the locally dropped packets
   7. with flow features (HipShardEngine.enable_flows): every owner accumulates its sources'
      sums over the batch's sub-batches (fsx_flows_begin / fsx_flows_end) and writes one row
@@ -34,7 +35,15 @@ unchanged batch pipeline on all of that source's packets:
      records of that sub-batch. Exact because a replica drops a source's packets exactly
      while now <= till, and the filter is only used where the clock is non-decreasing in
      global order: the dropped packets of a source are the first of its packets in the
-     sub-batch, and in rank order
+     sub-batch, and in rank order. The partials travel in fixed-capacity blocks (the
+     replica's per-owner capacity bounds the sources an owner can have dropped) whose
+     counts stay on the device
+
+Host synchronization: ONE host read per global batch — every sub-batch is packed first,
+then one all-to-all carries all their per-owner record counts (plus the replica-drop
+counts and the replica blocks' sizes) and the host reads them together;
+torch.distributed.all_to_all_single needs its split sizes on the host. Everything else (the
+replica, the filter decision, the flow partials and their merge) stays on the device.
 
 A global batch is cut into `chunks` sub-batches; in sub-batch i every rank contributes
 the i-th piece of its slice, and the global order of a sub-batch is rank 0's piece,
@@ -230,14 +239,15 @@ class HipShardEngine:
         self.ctx.blocklist_export_device(buf.data_ptr() + B, cap, buf.data_ptr())
         return buf
 
-    def pack(self, hdr, length, ts, n, G, verdict, filt=False, slot=0, drop_rec=False):
+    def pack(self, hdr, length, ts, n, G, verdict, filt=None, slot=0, drop_rec=False):
         """-> records, counts[G + 2] (counts[G]: packets dropped by the replica,
-        counts[G + 1]: record bytes, 16 or 32), in pipeline slot `slot`. drop_rec: the
-        dropped packets' records follow the owners' runs."""
+        counts[G + 1]: record bytes, 16 or 32), in pipeline slot `slot`. filt: a device word
+        (filter_plan), the replica filter applies iff it is nonzero; drop_rec: the dropped
+        packets' records follow the owners' runs."""
         if n > self.max_local:
             raise ValueError(f"local slice of {n} packets exceeds {self.max_local}")
-        flags = lib.SHARD_COMPACT | (lib.SHARD_FILTER_BLOCKLIST if filt else 0)
-        if filt and drop_rec:
+        flags = lib.SHARD_COMPACT
+        if filt is not None and drop_rec:
             flags |= lib.SHARD_DROP_RECORDS
         if slot not in self.recs or self.send_idxs[slot].numel() < max(1, n):
             m = max(1, n)
@@ -246,15 +256,31 @@ class HipShardEngine:
             self.countss[slot] = torch.empty(lib.MAX_SHARDS + 2, dtype=torch.int64, device=self.device)
         rec, idx, cnt = self.recs[slot], self.send_idxs[slot], self.countss[slot]
         self.rec, self.send_idx, self.counts = rec, idx, cnt   # (tests read the last pack)
-        self.ctx.shard_pack_device(hdr.data_ptr(), length.data_ptr(), ts.data_ptr(), n, G,
-                                   verdict.data_ptr(), rec.data_ptr(), idx.data_ptr(), cnt.data_ptr(),
-                                   flags)
+        if filt is None:
+            self.ctx.shard_pack_device(hdr.data_ptr(), length.data_ptr(), ts.data_ptr(), n, G,
+                                       verdict.data_ptr(), rec.data_ptr(), idx.data_ptr(), cnt.data_ptr(),
+                                       flags)
+        else:
+            self.ctx.shard_pack_filtered_device(hdr.data_ptr(), length.data_ptr(), ts.data_ptr(), n, G,
+                                                filt.data_ptr(), verdict.data_ptr(), rec.data_ptr(),
+                                                idx.data_ptr(), cnt.data_ptr(), flags)
         return rec, cnt[:G + 2]
+
+    def filter_plan(self, clocks: torch.Tensor, G: int, k: int) -> torch.Tensor:
+        """The replica filter's decision per sub-batch from the all-gathered piece clocks
+        ([G][k][3]), on the device: int32 [k]."""
+        out = torch.empty(k, dtype=torch.int32, device=self.device)
+        self.ctx.shard_filter_plan_device(clocks.data_ptr(), G, k, out.data_ptr())
+        return out
+
+    def load_replica_blocks(self, blocks: torch.Tensor, G: int, cap: int):
+        """The replica from G all-gathered blocklist_buffer(cap) blocks (counts on the device)."""
+        self.ctx.blocklist_replica_blocks_device(blocks.data_ptr(), G, cap)
 
     def partials(self, rec, first, m, rb, G, cap, slot=0):
         """Flow partials of the m replica-dropped records from record index `first` of a pack
         buffer: G runs of cap partials (source -> run of its owner) and counts[G]; enqueued
-        on the engine stream (no host synchronization)."""
+        on the engine stream (no host synchronization). m = 0: zero counts."""
         if self.pctx is None or self.pctx_entries < cap:
             if self.pctx is not None:
                 self.pctx.sync()
@@ -269,14 +295,21 @@ class HipShardEngine:
             self.pbufs[slot] = torch.empty(max(1, G * cap * B), dtype=torch.uint8, device=self.device)
             self.pcnts[slot] = torch.empty(G, dtype=torch.int64, device=self.device)
         buf, cnt = self.pbufs[slot], self.pcnts[slot]
-        self.pctx.flow_partials_records_device(rec.data_ptr() + first * rb, m, rb, G, buf.data_ptr(), cap,
-                                               cnt.data_ptr())
-        return buf, cnt
+        if m == 0:
+            cnt.zero_()
+        else:
+            self.pctx.flow_partials_records_device(rec.data_ptr() + first * rb, m, rb, G, buf.data_ptr(), cap,
+                                                   cnt.data_ptr())
+        return buf[:G * cap * B], cnt
 
     def merge(self, parts: torch.Tensor, m: int):
         """Merge m received partials (one sender's, distinct sources) into the owner's sums."""
         if m:
             self.ctx.flows_merge_device(parts.data_ptr(), m)
+
+    def merge_counted(self, parts: torch.Tensor, cap: int, count: torch.Tensor):
+        """Merge one sender's fixed-capacity block: min(count[0], cap) partials (device count)."""
+        self.ctx.flows_merge_counted_device(parts.data_ptr(), cap, count.data_ptr())
 
     def export_blocklist(self) -> tuple[torch.Tensor, int]:
         """This rank's live blacklist entries (32-byte records) and their count."""
@@ -356,17 +389,18 @@ class ShardedDataPlane:
         self.last_exchange = None
         self.formats = set()       # record sizes received (16 / 32)
         self.blk_cap = 1024        # blocklist entries per rank of one all-gather (grows)
-        self.rep_size = 0          # entries of the last replica (bounds the dropped sources)
         self.partials_sent = 0     # flow partials sent for replica-dropped packets
+        self.host_reads = 0        # host synchronizations of the data plane (one per global batch)
 
     def verdict_batch(self, hdr, length, ts, n: int, verdict, chunks: int = 1, bounds=None):
         """Verdicts for this rank's slice (arrival order) of one global batch; every rank
         calls it once per batch with its own slice, cut into `chunks` equal sub-batch
         pieces (or at the explicit local cut points `bounds`, chunks + 1 of them).
 
-        Sub-batches run as a two-stage software pipeline: the pack and record exchange of
-        sub-batch j + 1 (collectives on the engine's comm stream) overlap the owner
-        pipeline of sub-batch j; buffers alternate between two slots."""
+        Every sub-batch is packed first (the replica refreshed at the batch start, the
+        filter decided on the device), one all-to-all of all their counts is the batch's
+        only host read, then the record exchanges (comm stream) overlap the owner pipelines
+        of the sub-batches before them."""
         with self.engine.stream_ctx():
             flows = getattr(self.engine, "flows", None) is not None
             if self.world == 1:
@@ -375,96 +409,63 @@ class ShardedDataPlane:
                     f = self.engine.flows
                     f["rows"].fill_(-1)   # (count: ctx.last_batch_info()["sources"])
                 return
-            # with flow features the replica-dropped packets reach their owner as flow
-            # partials (step 7 of the module doc)
-            filt_on = self.filter
             if flows:
                 self.engine.flows_begin()
-            if filt_on:
-                self._sync_blocklist()   # maps may have changed since the last batch
             if bounds is None:
                 bounds = [n * i // chunks for i in range(chunks + 1)]
             k = len(bounds) - 1
-            if not filt_on:
-                # no replica filter: every pack is independent of the owners, so all of them
-                # go first and one exchange of all their counts is the batch's only host
-                # synchronization; the record exchanges then overlap the owner work
-                pend = self._exchange_all(hdr, length, ts, verdict, bounds)
-                sent = recv = 0
-                for j in range(k):
-                    ms, mr = self._stage_owner(verdict, bounds, j, pend[j], slot=j)
-                    pend[j] = None
-                    sent, recv = sent + ms, recv + mr
-                if flows:
-                    self.engine.flows_end()
-                self.last_exchange = {"sent": sent, "received": recv, "filtered": self.filtered}
-                return
-            filt = self._filter_plan(ts, bounds)
-            pend = [None] * k
-            pend[0] = self._stage_exchange(hdr, length, ts, verdict, bounds, 0, filt[0], flows)
+            filt = blk = None
+            if self.filter:
+                blk = self._refresh_replica()   # maps may have changed since the last batch
+                filt = self._filter_plan(ts, bounds)
+            pend = self._exchange_all(hdr, length, ts, verdict, bounds, filt, blk, flows)
             sent = recv = 0
             for j in range(k):
-                if j + 1 < k:   # enqueued before the owner work of j: its exchange overlaps it
-                    pend[j + 1] = self._stage_exchange(hdr, length, ts, verdict, bounds, j + 1,
-                                                       filt[j + 1], flows)
-                ms, mr = self._stage_owner(verdict, bounds, j, pend[j])
+                ms, mr = self._stage_owner(verdict, bounds, j, pend[j], slot=j)
                 pend[j] = None
                 sent, recv = sent + ms, recv + mr
-                # the replica packs j + 2 onward filter with (one sub-batch stale: exact for
-                # clocks that do not go back between consecutive sub-batches, _filter_plan)
-                if filt_on and j + 2 < k:
-                    self._sync_blocklist()
             if flows:
                 self.engine.flows_end()
             self.last_exchange = {"sent": sent, "received": recv, "filtered": self.filtered}
 
-    def _filter_plan(self, ts, bounds) -> list:
-        """Per sub-batch: may its pack drop replica-blacklisted packets? Pack j filters
-        with the replica refreshed at the batch start (j = 0, 1) or after the owners of
-        sub-batch j - 2 (j >= 2), so it can miss what the owners did in sub-batch j - 1.
-        A stale entry only drops packets the owner drops too unless some earlier packet
-        deleted it at a later time, so the filter is exact when the clock is
-        non-decreasing in global order (rank 0's piece, then rank 1's, ...) inside the
-        sub-batch and no packet of an earlier sub-batch of the batch is later than its
-        first. One all-gather of {min, max, decreases} of every piece."""
-        k = len(bounds) - 1
-        c = _all_gather(self.engine.clocks(ts, bounds), self.world, self.group).tolist()
-        within, lo, hi = [], [], []
-        for j in range(k):
-            ok, last, mn_j, mx_j = True, None, None, None
-            for r in range(self.world):
-                mn, mx, dec = c[3 * (r * k + j): 3 * (r * k + j) + 3]
-                if dec:
-                    ok = False
-                if mx == 0 and mn == -1:      # empty piece ({~0, 0} as int64)
-                    continue
-                mn, mx = mn & (2**64 - 1), mx & (2**64 - 1)
-                if last is not None and mn < last:
-                    ok = False
-                last = mx
-                mn_j = mn if mn_j is None else min(mn_j, mn)
-                mx_j = mx if mx_j is None else max(mx_j, mx)
-            within.append(ok)
-            lo.append(mn_j)
-            hi.append(mx_j)
-        out = []
-        for j in range(k):
-            ok = within[j]
-            if ok and j >= 1:
-                prev = max((h for h in hi[:j] if h is not None), default=None)
-                if prev is not None and lo[j] is not None and lo[j] < prev:
-                    ok = False
-            out.append(ok)
-        return out
+    def _refresh_replica(self):
+        """All-gather every owner's live blacklist entries into every rank's replica: one
+        all-gather of fixed-capacity blocks whose entry counts stay on the device (an owner
+        with more than blk_cap entries contributes blk_cap of them: its other sources' packets
+        go to it and are decided there). -> (the blocks' counts [G] on the device, cap)."""
+        G, e = self.world, self.engine
+        B = lib.SHARD_BLOCK_BYTES
+        cap = self.blk_cap
+        allb = _all_gather(e.blocklist_buffer(cap), G, self.group)
+        e.load_replica_blocks(allb, G, cap)
+        per = B + cap * B
+        sizes = allb.view(-1)[:G * per].view(G, per)[:, :8].contiguous().view(torch.int64).view(-1)
+        return sizes, cap
 
-    def _exchange_all(self, hdr, length, ts, verdict, bounds):
+    def _filter_plan(self, ts, bounds) -> torch.Tensor:
+        """Per sub-batch: may its pack drop replica-blacklisted packets? The replica holds the
+        owners' entries as of the batch start. A stale entry only drops packets the owner
+        drops too unless some earlier packet deleted it at a later time, so the filter is
+        exact when the clock is non-decreasing in global order (rank 0's piece, then rank
+        1's, ...) inside the sub-batch and no packet of an earlier sub-batch of the batch is
+        later than its first. One all-gather of {min, max, decreases} of every piece; the
+        decision on the device (fsx_shard_filter_plan_device) -> int32 [k]."""
+        k = len(bounds) - 1
+        c = _all_gather(self.engine.clocks(ts, bounds), self.world, self.group)
+        return self.engine.filter_plan(c, self.world, k)
+
+    def _exchange_all(self, hdr, length, ts, verdict, bounds, filt=None, blk=None, flows=False):
         """Pack every sub-batch j into slot j (engine stream), one all-to-all of all their
         per-owner counts and ONE host read of them (comm stream), then the record exchange
-        of every sub-batch; per sub-batch what _stage_exchange returns."""
+        of every sub-batch and, with flows and the filter, the flow partials of its
+        replica-dropped packets (fixed-capacity blocks); per sub-batch (received records,
+        segments, sent / received counts, arrival event, partials)."""
         G, e = self.world, self.engine
         k = len(bounds) - 1
+        drop = flows and filt is not None
         packs = [e.pack(hdr[bounds[j] * 64:], length[bounds[j]:], ts[bounds[j]:], bounds[j + 1] - bounds[j],
-                        G, verdict[bounds[j]:], False, j) for j in range(k)]
+                        G, verdict[bounds[j]:], None if filt is None else filt[j:j + 1], j, drop)
+                 for j in range(k)]
         pend = []
         with e.comm_ctx():
             cnt = torch.stack([c for _, c in packs])                       # [k, G + 2]
@@ -472,87 +473,58 @@ class ShardedDataPlane:
             send = (cnt[:, :G] * 2 + fmt).t().contiguous()                  # [G, k] by destination
             recv_counts = torch.empty_like(send)                            # [G, k] by source
             _a2a(recv_counts.view(-1), send.view(-1), [k] * G, [k] * G, self.group)
-            both = torch.cat([cnt.reshape(-1), recv_counts.view(-1).to(cnt.device)]).tolist()
-            base = k * (G + 2)
-            for j in range(k):
-                cj = both[j * (G + 2):(j + 1) * (G + 2)]
-                rw = [int(both[base + r * k + j]) for r in range(G)]
-                self.filtered += int(cj[G])
-                rb = int(cj[G + 1])
-                sc = [int(x) for x in cj[:G]]
-                rc = [x >> 1 for x in rw]
-                rf = [lib.SHARD_RECORD16_BYTES if x & 1 else lib.SHARD_RECORD_BYTES for x in rw]
-                in_b = [x * rb for x in sc]
-                out_b = [c * f for c, f in zip(rc, rf)]
-                recv = e.recv_buffer(sum(out_b))
-                _a2a(recv[:sum(out_b)], packs[j][0][:sum(in_b)], out_b, in_b, self.group)
-                arrived = e.comm_event()
-                segs, off = [], 0
-                for c, f, nb in zip(rc, rf, out_b):
-                    segs.append((off, c, f))
-                    off += nb
-                    if c:
-                        self.formats.add(f)
-                pend.append((recv, segs, sc, rc, arrived, None))
-        return pend
-
-    def _stage_exchange(self, hdr, length, ts, verdict, bounds, j: int, filt: bool, flows: bool = False):
-        """Pack sub-batch j (engine stream) and exchange its counts and records (comm stream);
-        with flows and the filter, also the flow partials of the replica-dropped packets."""
-        G, e = self.world, self.engine
-        a, b = bounds[j], bounds[j + 1]
-        slot = j % 2
-        drop = flows and filt   # (the same on every rank: the filter plan is global)
-        recs, counts = e.pack(hdr[a * 64:], length[a:], ts[a:], b - a, G, verdict[a:], filt, slot, drop)
-        with e.comm_ctx():
-            # per-owner counts with the record format in the low bit; the host reads its
-            # own and the received counts together (one synchronization, comm stream)
-            send = (counts[:G] * 2 + (counts[G + 1] == lib.SHARD_RECORD16_BYTES).to(counts.dtype)).contiguous()
-            recv_counts = torch.empty_like(send)
-            ones = [1] * G
-            _a2a(recv_counts, send, ones, ones, self.group)
-            both = torch.cat([counts.to(recv_counts.device), recv_counts]).tolist()
-            cnt, rw = both[:G + 2], [int(x) for x in both[G + 2:]]
-            self.filtered += int(cnt[G])
-            rb = int(cnt[G + 1])   # this sender's record size (16: compact IPv4 records)
-            sc = [int(x) for x in cnt[:G]]
+            parts = [cnt.reshape(-1), recv_counts.view(-1).to(cnt.device)]
+            if blk is not None:
+                parts.append(blk[0].to(cnt.device))
+            both = torch.cat(parts).tolist()   # the batch's one host read
+        self.host_reads += 1
+        base = k * (G + 2)
+        if blk is not None:   # an owner overflowed the replica's capacity: larger next batch
+            big = max(both[base + G * k: base + G * k + G])
+            if big > blk[1]:
+                self.blk_cap = max(self.blk_cap, 2 * int(big))
+        for j in range(k):
+            cj = both[j * (G + 2):(j + 1) * (G + 2)]
+            rw = [int(both[base + r * k + j]) for r in range(G)]
+            self.filtered += int(cj[G])
+            rb = int(cj[G + 1])
+            sc = [int(x) for x in cj[:G]]
             rc = [x >> 1 for x in rw]
             rf = [lib.SHARD_RECORD16_BYTES if x & 1 else lib.SHARD_RECORD_BYTES for x in rw]
             in_b = [x * rb for x in sc]
             out_b = [c * f for c, f in zip(rc, rf)]
-        partial = self._exchange_partials(recs, sum(sc), int(cnt[G]), rb, slot) if drop else None
-        with e.comm_ctx():
-            recv = e.recv_buffer(sum(out_b))
-            _a2a(recv[:sum(out_b)], recs[:sum(in_b)], out_b, in_b, self.group)
-        arrived = e.comm_event()      # only these records: the owner work of the previous
-        segs, off = [], 0             # sub-batch must not wait for later exchanges
-        for c, f, nb in zip(rc, rf, out_b):
-            segs.append((off, c, f))
-            off += nb
-            if c:
-                self.formats.add(f)
-        return recv, segs, sc, rc, arrived, partial
+            with e.comm_ctx():
+                recv = e.recv_buffer(sum(out_b))
+                _a2a(recv[:sum(out_b)], packs[j][0][:sum(in_b)], out_b, in_b, self.group)
+            # with flows and the filter: the flow partials of the replica-dropped packets
+            partial = (self._exchange_partials(packs[j][0], sum(sc), int(cj[G]), rb, blk[1], j)
+                       if drop else None)
+            segs, off = [], 0
+            for c, f, nb in zip(rc, rf, out_b):
+                segs.append((off, c, f))
+                off += nb
+                if c:
+                    self.formats.add(f)
+            # (only this sub-batch's exchanges: the owner work of the one before must not
+            # wait for later ones)
+            pend.append((recv, segs, sc, rc, e.comm_event(), partial))
+        return pend
 
-    def _exchange_partials(self, recs, first: int, m: int, rb: int, slot: int):
-        """The flow partials of this rank's m replica-dropped records (engine stream), their
-        per-owner counts (all-to-all + one host read) and the partials (all-to-all), on the
-        comm stream -> (received partials, per sender)."""
+    def _exchange_partials(self, recs, first: int, m: int, rb: int, cap: int, slot: int):
+        """The flow partials of this rank's m replica-dropped records (engine stream) in G
+        runs of cap (a source's owner contributed it to the replica, which holds at most cap
+        entries per owner), exchanged as fixed-capacity blocks with their counts (comm
+        stream; no host read) -> (received partials [G x cap], received counts [G])."""
         G, e = self.world, self.engine
         B = lib.FLOW_PARTIAL_BYTES
-        cap = max(1, self.rep_size)   # every dropped source is a replica entry
         buf, pcnt = e.partials(recs, first, m, rb, G, cap, slot)
         with e.comm_ctx():
             prc = torch.empty_like(pcnt)
             _a2a(prc, pcnt, [1] * G, [1] * G, self.group)
-            both = torch.cat([pcnt, prc]).tolist()
-            ps, pr = [int(x) for x in both[:G]], [int(x) for x in both[G:]]
-            if max(ps) > cap:
-                raise RuntimeError(f"flow partials overflow: {max(ps)} sources for {cap} replica entries")
-            send = torch.cat([buf[o * cap * B:(o * cap + ps[o]) * B] for o in range(G)])
-            precv = e.recv_buffer(sum(pr) * B)
-            _a2a(precv[:sum(pr) * B], send, [x * B for x in pr], [x * B for x in ps], self.group)
-        self.partials_sent += sum(ps)
-        return precv, pr
+            precv = e.recv_buffer(G * cap * B)
+            _a2a(precv[:G * cap * B], buf, [cap * B] * G, [cap * B] * G, self.group)
+        self.partials_sent += m
+        return precv, prc, cap
 
     def _stage_owner(self, verdict, bounds, j: int, pend, slot=None):
         """Owner pipeline of sub-batch j (engine stream), verdicts back (comm stream) and
@@ -565,12 +537,12 @@ class ShardedDataPlane:
         e.engine_wait(arrived)        # the records (and partials) of sub-batch j have arrived
         e.keep(recv)                  # allocated on the comm stream, read on the engine's
         if partial is not None:       # the replica-dropped packets' sums first, senders in order
-            precv, pr = partial
+            precv, prc, cap = partial
             e.keep(precv)
-            off = 0
+            e.keep(prc)
+            B = lib.FLOW_PARTIAL_BYTES
             for r in range(G):
-                e.merge(precv[off * lib.FLOW_PARTIAL_BYTES:], pr[r])
-                off += pr[r]
+                e.merge_counted(precv[r * cap * B:], cap, prc[r:r + 1])
         v = e.owner_batch(recv, segs, slot)
         with e.comm_ctx():
             ret = torch.empty(max(ms, 1), dtype=torch.uint8, device=v.device)
@@ -579,27 +551,6 @@ class ShardedDataPlane:
         e.keep(ret)
         e.scatter(ret, ms, verdict[a:], slot)
         return ms, mr
-
-    def _sync_blocklist(self):
-        """All-gather every owner's live blacklist entries into every rank's replica: one
-        all-gather of fixed-capacity buffers (entry count in the header), repeated with a
-        larger capacity only when some rank overflowed it."""
-        G, e = self.world, self.engine
-        B = lib.SHARD_BLOCK_BYTES
-        while True:
-            cap = self.blk_cap
-            allb = _all_gather(e.blocklist_buffer(cap), G, self.group)
-            per = B + cap * B
-            sizes = allb.view(-1)[:G * per].view(G, per)[:, :8].contiguous().view(torch.int64).view(-1).tolist()
-            if max(sizes) <= cap:
-                break
-            self.blk_cap = 2 * max(sizes)
-        self.rep_size = sum(sizes)
-        parts = [allb[r * per + B: r * per + B + sizes[r] * B] for r in range(G) if sizes[r]]
-        if parts:
-            e.load_replica(torch.cat(parts), sum(sizes))
-        else:
-            e.load_replica(allb, 0)
 
     def stats(self) -> tuple[int, int]:
         """stats_map of the whole sharded data plane: sum over the owners, plus the

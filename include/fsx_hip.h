@@ -326,6 +326,19 @@ int fsx_shard_pack_device(fsx_ctx *ctx, const uint8_t *d_hdr, const uint32_t *d_
                           const uint64_t *d_ts, size_t n, uint32_t n_shards, uint32_t flags,
                           uint8_t *d_verdict, void *d_records, uint32_t *d_send_idx,
                           uint64_t *d_counts);
+/* The same with the replica filter decided on the device: the blocklist filter applies iff
+ * *d_filter != 0 (fsx_shard_filter_plan_device), so no host read is needed to decide it. */
+int fsx_shard_pack_filtered_device(fsx_ctx *ctx, const uint8_t *d_hdr, const uint32_t *d_len,
+                                   const uint64_t *d_ts, size_t n, uint32_t n_shards, uint32_t flags,
+                                   const uint32_t *d_filter, uint8_t *d_verdict, void *d_records,
+                                   uint32_t *d_send_idx, uint64_t *d_counts);
+/* The replica filter's decision for each of k sub-batches, on the device: d_clocks holds the
+ * all-gathered {min, max, decreases} (fsx_shard_clock_device) of every rank's piece of every
+ * sub-batch ([n_shards][k][3] u64; an empty piece is {~0, 0, 0}); d_filter[j] = 1 when the
+ * global clock (rank 0's piece, then rank 1's, ...) does not go back up to the end of
+ * sub-batch j, which makes the filter exact. */
+int fsx_shard_filter_plan_device(fsx_ctx *ctx, const uint64_t *d_clocks, uint32_t n_shards, uint32_t k,
+                                 uint32_t *d_filter);
 /* Flow partial: the exact flow sums of one source over a run of its packets
  * in arrival order, with the run's first / last timestamp and its first packet's L4
  * destination port; u128 sums as {low, high} u64 words. */
@@ -351,6 +364,9 @@ int fsx_flow_partials_records_device(fsx_ctx *ctx, const void *d_records, size_t
  * everything merged so far (a source absent from the maps is skipped: the protocol sends
  * partials only for sources of this owner's blocklist). */
 int fsx_flows_merge_device(fsx_ctx *ctx, const void *d_partials, size_t m);
+/* The same for min(*d_count, cap) partials: a fixed-capacity exchange block whose count is
+ * on the device (no host read). */
+int fsx_flows_merge_counted_device(fsx_ctx *ctx, const void *d_partials, size_t cap, const uint64_t *d_count);
 /* d_out3 = {min ts, max ts, 1 if some ts decreases in arrival order}. */
 int fsx_shard_clock_device(fsx_ctx *ctx, const uint64_t *d_ts, size_t n, uint64_t *d_out3);
 /* Every live blacklist entry (till > 0) of this context's maps as FSX_SHARD_BLOCK_BYTES
@@ -358,6 +374,11 @@ int fsx_shard_clock_device(fsx_ctx *ctx, const uint64_t *d_ts, size_t n, uint64_
 int fsx_blocklist_export_device(fsx_ctx *ctx, void *d_entries, size_t cap, uint64_t *d_count);
 /* Replace the context's blocklist replica with m all-gathered entries (distinct keys). */
 int fsx_blocklist_replica_device(fsx_ctx *ctx, const void *d_entries, size_t m);
+/* The same from n_blocks all-gathered fixed-capacity blocks, each FSX_SHARD_BLOCK_BYTES of
+ * header (int64 entry count first) then cap entries, as fsx_blocklist_export_device fills
+ * them (entries beyond cap are left out: a missing entry only sends its packets to their
+ * owner, which decides them exactly). No host read. */
+int fsx_blocklist_replica_blocks_device(fsx_ctx *ctx, const void *d_blocks, uint32_t n_blocks, size_t cap);
 /* Owner side: m received records -> header records + len + ts for the batch entry points
  * (same source key, family, frame length, timestamp and L4 destination port). */
 int fsx_shard_unpack_device(fsx_ctx *ctx, const void *d_records, size_t m, uint8_t *d_hdr,

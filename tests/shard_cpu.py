@@ -99,8 +99,44 @@ class CpuShardEngine:
         buf[32:32 + k * 32] = ent[:k * 32]
         return buf
 
-    def pack(self, hdr, length, ts, n, G, verdict, filt=False, slot=0, drop_rec=False):
-        # (drop_rec: the HIP engine's flow partials of replica drops; no flows on the CPU engine)
+    @staticmethod
+    def filter_plan(clocks, G, k):
+        """The replica filter's decision per sub-batch (fsx_shard_filter_plan_device restated)."""
+        c = clocks.numpy().view(np.uint64).reshape(G, k, 3)
+        out, prev_hi = [], None
+        for j in range(k):
+            ok, last, lo, hi = True, None, None, None
+            for r in range(G):
+                mn, mx, dec = (int(x) for x in c[r, j])
+                if dec:
+                    ok = False
+                if mx == 0 and mn == 2**64 - 1:   # empty piece
+                    continue
+                if last is not None and mn < last:
+                    ok = False
+                last = mx
+                lo = mn if lo is None else min(lo, mn)
+                hi = mx if hi is None else max(hi, mx)
+            if ok and prev_hi is not None and lo is not None and lo < prev_hi:
+                ok = False
+            out.append(1 if ok else 0)
+            if hi is not None:
+                prev_hi = hi if prev_hi is None else max(prev_hi, hi)
+        return torch.tensor(out, dtype=torch.int32)
+
+    def load_replica_blocks(self, blocks, G, cap):
+        b = blocks.numpy().reshape(G, 32 + cap * 32)
+        self.replica = {}
+        for r in range(G):
+            m = min(int(b[r, :8].view(np.int64)[0]), cap)
+            for e in b[r, 32:32 + m * 32].view(self.BLK_DTYPE):
+                fam = 6 if e["tag"] == 2 else 4
+                self.replica[(fam, e["key"].tobytes()[:16 if fam == 6 else 4])] = int(e["till"])
+
+    def pack(self, hdr, length, ts, n, G, verdict, filt=None, slot=0, drop_rec=False):
+        # (filt: the plan's word for this sub-batch; drop_rec: the HIP engine's flow partials of
+        # replica drops; no flows on the CPU engine)
+        filt = filt is not None and int(filt[0]) != 0
         h, l, t = self._np(hdr, length, ts, n)
         cls, keys = self.oracle.parse(h, l)
         v = verdict.numpy()

@@ -53,6 +53,8 @@ def worker(rank, world, port, spec, out_path, engine_kind):
                 ctx.load_q8_model(fsx_load.load_weights(Path(__file__).parent / "golden" / "model_weights.json"))
                 eng.enable_flows(cfg["max_entries"])
         plane = ShardedDataPlane(eng, blocklist_filter=spec.get("filter", True))
+        if spec.get("blk_cap"):   # a tiny replica capacity: owners overflow it (entries left out)
+            plane.blk_cap = spec["blk_cap"]
         k = spec.get("chunks", 1)
         mine = []
         for a, b in zip(cuts[:-1], cuts[1:]):
@@ -133,7 +135,8 @@ def worker(rank, world, port, spec, out_path, engine_kind):
             with open(out_path, "w") as f:
                 json.dump({"ok": ok, "msg": msg, "stats": list(stats),
                            "filtered": plane.filtered, "formats": sorted(plane.formats),
-                           "partials": plane.partials_sent}, f)
+                           "partials": plane.partials_sent, "host_reads": plane.host_reads,
+                           "blk_cap": plane.blk_cap}, f)
         dist.barrier()
     finally:
         dist.destroy_process_group()

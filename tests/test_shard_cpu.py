@@ -38,6 +38,18 @@ def test_sharded_fixed_window(tmp_path, world):
                                max_entries=4096))
     res = run_sharded(tmp_path, world, spec)
     assert res["filtered"] > 0      # the replicated blocklist dropped packets at arrival
+    # one host read per global batch with the filter on
+    assert res["host_reads"] == len(BASE["cuts"]) - 1, res["host_reads"]
+
+
+def test_sharded_replica_capacity_overflow(tmp_path):
+    """A replica capacity of 2 entries per owner: the owners' other blacklisted sources are
+    left out of the replica (their packets go to the owner, which decides them), the result
+    stays exact, and the capacity grows for the next batch from the one host read."""
+    spec = dict(BASE, blk_cap=2, cfg=dict(pps_threshold=7, window_ns=200_000, block_ns=1_000_000,
+                                          max_entries=4096))
+    res = run_sharded(tmp_path, 2, spec)
+    assert res["blk_cap"] > 2 and res["host_reads"] == len(BASE["cuts"]) - 1
 
 
 def test_sharded_without_blocklist_filter_one_chunk(tmp_path):

@@ -89,6 +89,20 @@ def test_sharded_flow_features_equal_one_gpu(tmp_path, world, v6):
                 owner_batch=4096)
     res = run_sharded(tmp_path, world, spec, engine="hip")
     assert res["filtered"] > 0 and res["partials"] > 0   # dropped at arrival, still in the features
+    # one host read per global batch with the filter and the flows on:
+    # replica, filter decision and flow partials stay on the device
+    assert res["host_reads"] == len(BASE["cuts"]) - 1, res["host_reads"]
+
+
+def test_sharded_flow_features_small_replica(tmp_path):
+    """The flow partials travel in fixed blocks of the replica's per-owner capacity: with a
+    capacity of 2 the owners' other blacklisted sources stay out of the replica, their
+    packets reach the owner, and the rows still equal the 1-GPU rows."""
+    spec = dict(BASE, v6_frac=0.1, seed=37, flows=True, blk_cap=2,
+                cfg=dict(pps_threshold=7, window_ns=200_000, block_ns=1_000_000, max_entries=4096),
+                owner_batch=4096)
+    res = run_sharded(tmp_path, 2, spec, engine="hip")
+    assert res["filtered"] > 0 and res["blk_cap"] > 2
 
 
 @pytest.mark.parametrize("filt", [True, False])
