@@ -11,6 +11,7 @@
 #   pmc            PMC passes (FETCH_SIZE, WRITE_SIZE, SQ) + summary  -> pmc_TAG/
 #   ab=V1,V2,..    A/B of library variants (scripts/ab.sh)           -> TAG_ab.txt
 #   leg=LEG        A/B of one bench leg under env settings $LEG_ENVS (";"-separated, scripts/ab_leg.sh)
+#   abenv          A/B of the headline under env settings $AB_ENVS (";"-separated, scripts/ab_env.sh)
 # Env: BENCH_ARGS (bench / prof / pmc / timeline / ab), PROF_LEGS, LEG (prof: a bench leg
 # run as the headline: config4 / config5 / config3).
 set -u
@@ -59,6 +60,11 @@ for s in "$@"; do
       [ ${#es[@]} -eq 0 ] && es=("")
       run leg 1000 bash scripts/ab_leg.sh "${s#leg=}" "${es[@]}" > "gpurun_out/${TAG}_leg.txt" 2>&1 || exit $?
       cat "gpurun_out/${TAG}_leg.txt" ;;
+    abenv)
+      IFS=';' read -r -a es <<< "${AB_ENVS:-}"
+      [ ${#es[@]} -eq 0 ] && es=("")
+      run abenv 1000 bash scripts/ab_env.sh "${es[@]}" > "gpurun_out/${TAG}_abenv.txt" 2>&1 || exit $?
+      cut -c1-400 "gpurun_out/${TAG}_abenv.txt" ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
