@@ -464,9 +464,11 @@ int fsx_open(fsx_ctx **out, const fsx_config *cfg) {
         HistBufs &h = c->hist;
         h.cap = std::max<uint64_t>(2 * k.max_batch, 1u << 16);
         const uint64_t stiles = c->slots / 4096 + 1;
+        // (past cap: the heavy sources' staged final logs, k_walk_sw_heavy_sel)
+        const uint64_t ent = h.cap + (uint64_t)kHeavyMax * kSwHeavyMaxP;
         for (int b = 0; b < 2; ++b) {
-            if (hipMalloc(&h.t[b], h.cap * 8) != hipSuccess) return fail(-ENOMEM);
-            if (hipMalloc(&h.l[b], h.cap * 4) != hipSuccess) return fail(-ENOMEM);
+            if (hipMalloc(&h.t[b], ent * 8) != hipSuccess) return fail(-ENOMEM);
+            if (hipMalloc(&h.l[b], ent * 4) != hipSuccess) return fail(-ENOMEM);
         }
         if (hipMalloc(&h.tile_cnt, stiles * 4) != hipSuccess) return fail(-ENOMEM);
         if (hipMalloc(&h.tile_off, stiles * 8) != hipSuccess) return fail(-ENOMEM);

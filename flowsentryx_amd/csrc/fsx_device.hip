@@ -2734,7 +2734,7 @@ hipError_t launch_tail(const TailArgs &a) {
                                                           table, lim, hlists, skeys);
             mark_on("k_walk_heavy", hs_id);
         }
-        if (a.hfm) {   // (the path k_hmode picked runs; the other kernel returns at once)
+        if (a.hfm && lim.limiter == 0) {   // (the path k_hmode picked runs; the other returns at once)
             if ((e = launch_walk_heavy_sel(bs, sc.sort_ctl, sc.gbase, sc.hist, tcap, verdict, ts, len, n, sc.hrec,
                                            table, lim, sc.heavy, hlists.list, tstate, hs)) != hipSuccess)
                 return e;
@@ -2766,7 +2766,7 @@ hipError_t launch_tail(const TailArgs &a) {
         hf_id = fork ? 1 : 0;
         // unsorted heavy sources: their walker (select / rank searches, latency-bound on 32
         // blocks) on the flow stream ahead of the heavy flow rows, not ahead of the heads
-        if (a.hfm && st2 && walk_join_ev) {
+        if (a.hfm && lim.limiter == 0 && st2 && walk_join_ev) {
             hs = st2;
             hs_id = 1;
             heavy_join = true;
@@ -2775,7 +2775,8 @@ hipError_t launch_tail(const TailArgs &a) {
     if (split && split->tail && do_limit && lim.limiter == 1) k_sw_tail_check<<<1, 1, 0, st>>>(bs, tstate, lim);
     // unsorted heavy sources: their carried state decides the path now that the previous
     // batch's walkers have stored it; those sent back to the run path get their runs first
-    if (a.hfm && (e = launch_hmode_state(bs, sc.heavy, table, lim, tstate, st)) != hipSuccess) return e;
+    if (a.hfm && (e = launch_hmode_state(sc.sort_ctl, n, bs, sc.heavy, table, lim, tstate, st)) != hipSuccess)
+        return e;
     if (a.hfm && (e = launch_heavy_gather(bs, verdict, ts, len, n, sc.hist, tcap, sc.heavy, a.shift0, lim.table_mask,
                                           S_fin, pay_fin, st)) != hipSuccess)
         return e;
@@ -2813,6 +2814,20 @@ hipError_t launch_tail(const TailArgs &a) {
                                            table, lim.table_mask + 1);
         k_admit_commit<<<1, 1, 0, st>>>(bs, tstate);
         mark("k_admit");
+    }
+    // pipelined sliding window with heavy lists: the heavy walkers (latency-bound, 32 blocks)
+    // on the flow stream ahead of the flows, beside the light walkers; k_sw_hist joins them
+    hipEvent_t sw_heavy_done = nullptr;
+    if (do_limit && lim.limiter == 1 && tagh && split && split->tail && st2 && walk_fork_ev && walk_join_ev) {
+        if ((e = hipEventRecord(walk_fork_ev, st)) != hipSuccess) return e;
+        if ((e = hipStreamWaitEvent(st2, walk_fork_ev, 0)) != hipSuccess) return e;
+        mark_on(nullptr, 1);
+        if ((e = launch_sw_heavy(S, ts, len, bs, sc, table, tstate, hist, lim, n, hlists,
+                                 a.hfm ? verdict : nullptr, st2)) != hipSuccess)
+            return e;
+        mark_on("k_walk_sw_heavy", 1);
+        if ((e = hipEventRecord(walk_join_ev, st2)) != hipSuccess) return e;
+        sw_heavy_done = walk_join_ev;
     }
     if (flows) {
         hipStream_t fs = st;
@@ -2857,7 +2872,8 @@ hipError_t launch_tail(const TailArgs &a) {
         mark("k_seg_order");
         if (lim.limiter == 1) {   // FSX_LIMIT_SLIDING_WINDOW
             if ((e = launch_sliding_window(S, ts, len, bs, sc, table, tstate, hist, lim, n, st, mk, st3,
-                                           walk_fork_ev, walk_join_ev, &hlists)) != hipSuccess)
+                                           walk_fork_ev, walk_join_ev, &hlists, a.hfm ? verdict : nullptr,
+                                           sw_heavy_done)) != hipSuccess)
                 return e;
         } else {
             // short and long segments are disjoint: the wave walker runs on its own
@@ -3004,7 +3020,7 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
     // slots; k_hmode picks the batch's path on the device (FSX_NO_HFAST=1: the runs, A/B)
     static const bool no_hfast = getenv("FSX_NO_HFAST") != nullptr;
     // (record mode too: the records' len / ts go to in.rec_len / rec_ts, which k_pass0h reads)
-    const bool hfm = tagh && lim.limiter == 0 && resolve && !no_hfast;
+    const bool hfm = tagh && lim.limiter <= 1 && resolve && !no_hfast;
     if (!(split && split->tail) && (e = hipMemsetAsync(sc.marks, 0, n, st)) != hipSuccess) return e;
     DigitPlan dp{};
     dp.npass = (uint32_t)npass;
@@ -3024,7 +3040,13 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
     }
     if (heavy_sort) {
         k_heavy_sample<<<64, 256, 0, sp0>>>(in, len, n, sc.sketch, lim.seed, lim.table_mask, lim.test_flags);
-        k_heavy_pick<<<1, 1024, 0, sp0>>>(in, len, sc.sketch, sc.heavy, nheavy, 16, lim.seed,
+        // (sliding window on the unsorted path: only sources with >= 1/96 of the sample — the
+        // rank walker's dense ones, k_hmode_state sends any under 1/128 of the batch to the
+        // run path — the rest sort with the light sources)
+        const uint32_t S = std::min<uint32_t>(n, kHeavySample);
+        const bool sw_dense = hfm && lim.limiter == 1 && !(lim.test_flags & kFlagSwSparse);
+        const uint32_t floor_cnt = sw_dense ? std::max<uint32_t>(16, S / 96) : 16u;
+        k_heavy_pick<<<1, 1024, 0, sp0>>>(in, len, sc.sketch, sc.heavy, nheavy, floor_cnt, lim.seed,
                                           lim.table_mask, lim.test_flags, idt, resolve, bs);
         mark("k_heavy_pick");
     } else {

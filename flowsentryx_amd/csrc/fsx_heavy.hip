@@ -25,235 +25,9 @@
 #include "fsx_internal.h"
 #include "fsx_seg.h"
 #include "fsx_walk.h"
+#include "fsx_heavy_view.h"
 
 namespace fsx {
-
-// The 0x80-byte of every byte of x that equals b (exact: no borrow across bytes).
-__device__ __forceinline__ uint32_t byte_eq_mask(uint32_t x, uint32_t pat) {
-    const uint32_t y = x ^ pat;
-    return ~(((y & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | y | 0x7F7F7F7Fu);
-}
-
-// Heavy source h's packets by rank (fsx_walk.h SegView interface; wave-cooperative: every
-// lane calls with the same arguments).
-struct HeavyView {
-    const uint8_t *tags;          // verdict bytes: 0x80 | h for h's packets
-    const uint64_t *ts;
-    const uint32_t *len;
-    const uint32_t *row;          // pass-0 tile offsets of bucket light_b + h (incl. base)
-    const HeavyTileRec *rec;
-    uint32_t base, cnt, ntiles, n, h;
-    uint32_t pat;                 // (0x80 | h) in every byte
-
-    __device__ __forceinline__ uint32_t pre(uint32_t t) const { return row[t] - base; }
-
-    // lane's 64 verdict bytes of tile t as 16 words (0 beyond n)
-    __device__ __forceinline__ void tile_words(uint32_t t, uint32_t (&w)[16]) const {
-        const uint32_t lane = lane_id();
-        const uint32_t p0 = t * (uint32_t)kSortTile + lane * 64u;
-        if (p0 + 64u <= n) {
-            const uint4 *q = reinterpret_cast<const uint4 *>(tags + p0);
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const uint4 v = q[k];
-                w[4 * k] = v.x; w[4 * k + 1] = v.y; w[4 * k + 2] = v.z; w[4 * k + 3] = v.w;
-            }
-        } else {
-#pragma unroll
-            for (int k = 0; k < 16; ++k) {
-                uint32_t x = 0;
-                for (uint32_t b = 0; b < 4; ++b) {
-                    const uint32_t p = p0 + (uint32_t)k * 4u + b;
-                    if (p < n) x |= (uint32_t)tags[p] << (8 * b);
-                }
-                w[k] = x;
-            }
-        }
-    }
-
-    // arrival index of h's r-th packet (r < cnt)
-    __device__ __forceinline__ uint32_t select(uint32_t r) const {
-        const uint32_t lane = lane_id();
-        uint32_t lo = 0, hi = ntiles;   // the largest tile t with pre(t) <= r lies in [lo, hi)
-        while (hi - lo > 1) {
-            const uint32_t step = (hi - lo + 63u) / 64u;
-            const uint32_t q = lo + lane * step;
-            const uint64_t m = __ballot(q < hi && pre(q) <= r);   // lane 0 (q = lo) always
-            const uint32_t f = 63u - (uint32_t)__clzll((long long)m);
-            lo = lo + f * step;
-            hi = min(hi, lo + step);
-        }
-        const uint32_t t = lo;
-        uint32_t k = r - pre(t);
-        uint32_t w[16];
-        tile_words(t, w);
-        uint32_t c = 0;
-#pragma unroll
-        for (int j = 0; j < 16; ++j) c += (uint32_t)__popc(byte_eq_mask(w[j], pat));
-        const uint32_t incl = wave_incl_sum(c);
-        const uint32_t excl = incl - c;
-        const bool mine = excl <= k && k < incl;
-        uint32_t idx = 0;
-        if (mine) {
-            uint32_t kk = k - excl;
-#pragma unroll
-            for (int j = 0; j < 16; ++j) {
-                uint32_t m = byte_eq_mask(w[j], pat);
-                const uint32_t pc = (uint32_t)__popc(m);
-                if (kk < pc && idx == 0) {
-                    for (uint32_t s = 0; s < kk; ++s) m &= m - 1u;
-                    idx = 1u + t * (uint32_t)kSortTile + lane * 64u + (uint32_t)j * 4u +
-                          (uint32_t)(__ffs((int)m) - 1) / 8u;
-                }
-                kk = kk >= pc ? kk - pc : 0xFFFFFFFFu;
-            }
-        }
-        const uint64_t bm = __ballot(mine);
-        return __shfl(idx, __ffsll((unsigned long long)bm) - 1) - 1u;
-    }
-
-    // h's packets at arrival indices < i (i <= n)
-    __device__ __forceinline__ uint32_t rank(uint32_t i) const {
-        if (i >= n) return cnt;
-        const uint32_t lane = lane_id();
-        const uint32_t t = i / (uint32_t)kSortTile;
-        uint32_t w[16];
-        tile_words(t, w);
-        const uint32_t p0 = t * (uint32_t)kSortTile + lane * 64u;
-        uint32_t c = 0;
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            uint32_t m = byte_eq_mask(w[j], pat);
-            const uint32_t pj = p0 + (uint32_t)j * 4u;   // byte b of word j: position pj + b
-            if (pj + 4u <= i) c += (uint32_t)__popc(m);
-            else if (pj < i) c += (uint32_t)__popc(m & ((1u << (8u * (i - pj))) - 1u));
-        }
-        return pre(t) + wave_sum(c);
-    }
-
-    // first arrival index with ts > X (the batch clock non-decreasing), n if none
-    __device__ __forceinline__ uint32_t first_after(uint64_t X) const {
-        const uint32_t lane = lane_id();
-        uint32_t lo = 0, hi = n;   // ts <= X before lo, ts > X from hi on
-        while (hi - lo > 64u) {
-            const uint32_t step = (hi - lo + 63u) / 64u;
-            const uint32_t q = lo + lane * step;
-            const bool valid = q < hi;
-            const uint64_t m = __ballot(valid && ts[q] > X);
-            if (m) {
-                const uint32_t f = (uint32_t)__ffsll((unsigned long long)m) - 1u;
-                hi = lo + f * step;
-                if (f) lo = lo + (f - 1u) * step + 1u;
-            } else {
-                const uint64_t vm = __ballot(valid);
-                lo = lo + (63u - (uint32_t)__clzll((long long)vm)) * step + 1u;
-            }
-        }
-        const uint32_t q = lo + lane;
-        const uint64_t m = __ballot(q < hi && ts[q] > X);
-        return m ? lo + (uint32_t)__ffsll((unsigned long long)m) - 1u : hi;
-    }
-
-    __device__ __forceinline__ uint64_t t(uint32_t r) const { return ts[select(r)]; }
-    __device__ __forceinline__ uint32_t l(uint32_t r) const { return len[select(r)]; }
-
-    // sum of h's frame lengths at arrival positions [a, b] of tile t
-    __device__ __forceinline__ uint64_t tile_len_sum(uint32_t t, uint32_t a, uint32_t b) const {
-        const uint32_t lane = lane_id();
-        uint64_t s = 0;
-        const uint32_t p0 = t * (uint32_t)kSortTile;
-#pragma unroll 4
-        for (uint32_t j = 0; j < (uint32_t)kSortTile; j += 64u) {
-            const uint32_t p = p0 + j + lane;
-            if (p >= a && p <= b && p < n && tags[p] == (pat & 0xFFu)) s += len[p];
-        }
-        return wave_sum(s);
-    }
-};
-
-// fsx_walk.h's accessors on the heavy view (found by argument-dependent lookup from
-// walk_fixed_fast): ranks instead of sorted positions.
-template <bool kWave>
-__device__ __forceinline__ uint32_t search_gt(const HeavyView &sv, uint32_t lo, uint32_t hi, uint64_t X) {
-    if (lo >= hi) return hi;
-    const uint32_t r = sv.rank(sv.first_after(X));
-    return r < lo ? lo : r > hi ? hi : r;
-}
-
-template <bool kWave>
-__device__ __forceinline__ uint64_t sum_len(const HeavyView &sv, uint32_t lo, uint32_t hi) {
-    if (lo >= hi) return 0;
-    const uint32_t ia = sv.select(lo), ib = sv.select(hi - 1);
-    const uint32_t ta = ia / (uint32_t)kSortTile, tb = ib / (uint32_t)kSortTile;
-    if (ta == tb) return sv.tile_len_sum(ta, ia, ib);
-    uint64_t s = sv.tile_len_sum(ta, ia, ~0u) + sv.tile_len_sum(tb, 0, ib);
-    // the tiles in between from their sums, eight loads in flight per lane (a heavy source
-    // spans up to every tile: one dependent load per 64 tiles made this the walker's long pole)
-    uint64_t mid = 0;
-    uint32_t t = ta + 1 + lane_id();
-    for (; t + 7u * 64u < tb; t += 8u * 64u) {
-        uint32_t x[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) x[u] = sv.rec[t + (uint32_t)u * 64u].s1[sv.h];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) mid += x[u];
-    }
-    for (; t < tb; t += 64u) mid += sv.rec[t].s1[sv.h];
-    return s + wave_sum(mid);
-}
-
-// First rank q in [from, lim) where acc0 + the lengths of ranks from..q exceed B (else lim):
-// a scan of h's packets in arrival order from select(from). k_hmode keeps the byte trigger
-// out of reach (the batch takes the run path otherwise); this is its exact definition.
-template <bool kWave>
-__device__ __forceinline__ uint32_t bytes_trigger(const HeavyView &sv, uint32_t from, uint32_t lim, uint64_t acc0, uint64_t B) {
-    if (from >= lim) return lim;
-    const uint32_t lane = lane_id();
-    uint64_t acc = acc0;
-    uint32_t q = from;
-    for (uint32_t p0 = sv.select(from); p0 < sv.n && q < lim; p0 += 64u) {
-        const uint32_t p = p0 + lane;
-        const bool mine = p < sv.n && sv.tags[p] == (sv.pat & 0xFFu);
-        const uint64_t L = mine ? sv.len[p] : 0ull;
-        const uint64_t bm = __ballot(mine);
-        const uint64_t incl = wave_incl_sum(L);
-        const uint32_t rk = q + (uint32_t)__popcll(bm & ((1ull << lane) - 1ull));
-        const uint64_t hit = __ballot(mine && rk < lim && acc + incl > B);
-        if (hit) return q + (uint32_t)__popcll(bm & ((1ull << (__ffsll((unsigned long long)hit) - 1)) - 1ull));
-        acc += __shfl(incl, 63);
-        q += (uint32_t)__popcll(bm);
-    }
-    return lim;
-}
-
-// Verdict changes of heavy source h as its list {arrival index << 1 | DROP} (the
-// MarkWriter<true, true> of the run path, positions = ranks).
-struct HeavyMarkWriter {
-    HeavyView hv;   // (by value: a pointer to it would put the view in scratch)
-    uint32_t *list;
-    uint8_t last = 0;
-    uint32_t nl = 0, last_pos = 0;
-    uint64_t npass = 0, ndrop = 0;
-    __device__ __forceinline__ void count_run(uint32_t pos) {
-        const uint64_t r = pos - last_pos;
-        ndrop += last == XDP_DROP ? r : 0ull;
-        npass += (last && last != XDP_DROP) ? r : 0ull;
-    }
-    __device__ __forceinline__ void emit(uint32_t pos, uint8_t v) {
-        if (v != last) {
-            count_run(pos);
-            const uint32_t e = hv.select(pos) << 1 | (v == XDP_DROP ? 1u : 0u);
-            if (lane_id() == 0) list[nl] = e;
-            ++nl;
-            last_pos = pos;
-            last = v;
-        }
-    }
-    __device__ __forceinline__ void finish(uint32_t b) {
-        count_run(b);
-        last_pos = b;
-    }
-};
 
 // ------------------------------------------------------------------ k_hmode
 // After k_pass0h (one thread): the payload words' validity and the batch's path for its
@@ -267,27 +41,53 @@ __global__ void k_hmode(BatchState *bs, const uint64_t *__restrict__ ts, uint32_
     const uint64_t mn = ~bs->inv_min_ts;
     const bool pay = maxL < (1u << kPayLenBits) && mn == t0 && bs->max_ts - t0 < kPayTsRange;
     bs->pay_ok = pay ? 1u : 0u;
-    const bool fast = !bs->err && pay && !bs->nonmono && !bs->span_big && maxL < (1u << 16) &&
-                      fast_ok(bs, lim) && !(maxL && P + 1 > B / maxL);
+    // (fixed window: walk_fixed_fast's preconditions; sliding window: its final logs fit their
+    // staging, the clock facts across batches in k_hmode_state)
+    const bool lim_ok = lim.limiter == 1 ? P <= kSwHeavyMaxP : fast_ok(bs, lim) && !(maxL && P + 1 > B / maxL);
+    const bool fast = !bs->err && pay && !bs->nonmono && !bs->span_big && maxL < (1u << 16) && lim_ok;
     bs->hfast = fast ? 1u : 0u;
 }
 
 // First kernel of the tail (one block of 128 threads, a thread per heavy source): every
 // heavy source's carried state on the epoch-jump path, or the batch takes the run path.
-// Counts the path taken (TableState::n_hfast / n_hrun, fsx_last_batch_info [16] / [17]).
-__global__ __launch_bounds__(128) void k_hmode_state(BatchState *bs, const HeavySet *__restrict__ hs,
+// Sliding window: a heavy source with fewer than 1/kSwDenseDiv of the batch's packets (on
+// average < 32 per sort tile, where a block of 64 ranks costs a tile scan per packet or two)
+// takes the run path alone (HeavySet::srun). Counts the path taken (TableState::n_hfast /
+// n_hrun, fsx_last_batch_info [16] / [17]).
+constexpr uint32_t kSwDenseDiv = 128;
+__global__ __launch_bounds__(128) void k_hmode_state(const uint32_t *__restrict__ cnt0, uint32_t n, BatchState *bs,
+                                                     HeavySet *__restrict__ hs,
                                                      const Slot *__restrict__ table, Limits lim,
                                                      TableState *tstate) {
-    __shared__ uint32_t s_bad;
+    __shared__ uint32_t s_bad, s_nrun[2];
     if (threadIdx.x == 0) s_bad = 0;
-    __syncthreads();
     const bool fast0 = bs->hfast != 0;
+    {   // (every batch: the fixed window and the run path leave the mask empty)
+        const uint32_t h = threadIdx.x;
+        const bool sparse = fast0 && lim.limiter == 1 && h < hs->n &&
+                            (uint64_t)cnt0[bs->light_b + h] * kSwDenseDiv < n;
+        const uint64_t b = __ballot(sparse);
+        if (lane_id() == 0) {
+            hs->srun[h >> 6] = b;
+            s_nrun[h >> 6] = (uint32_t)__popcll(b);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) hs->nrun = s_nrun[0] + s_nrun[1];
     if (fast0) {
         const uint32_t h = threadIdx.x;
         const uint32_t maxL = bs->max_len;
         const uint64_t P = lim.pps, B = lim.bps, W = lim.window;
         bool ok = true;
-        if (h < hs->n && hs->resolved && hs->slot[h] != kNoSlot) {
+        if (lim.limiter == 1) {   // sliding window: sw_walk_fast_wave's facts; carried logs fit
+            ok = sw_fast(bs, tstate, lim);
+            if (h < hs->n && hs->resolved && hs->slot[h] != kNoSlot) {
+                const uint64_t aux = table[hs->slot[h]].aux;
+                ok = ok && (aux & ((1ull << kHistCntBits) - 1)) <= kSwHeavyMaxP;
+            } else if (h < hs->n) {
+                ok = false;
+            }
+        } else if (h < hs->n && hs->resolved && hs->slot[h] != kNoSlot) {
             const FwState st = load_state(table[hs->slot[h]]);
             ok = !st.has_st || (st.tt <= ~0ull - W && st.pps < kBig && st.bps < kBig);
             if (st.has_st && (st.bps > B || (maxL && P + 1 > (B - st.bps) / maxL))) ok = false;
@@ -410,7 +210,8 @@ __global__ __launch_bounds__(256) void k_heavy_recs(const BatchState *bs, const 
 // ------------------------------------------------------------------ k_heavy_gather
 // The run path's input when k_hmode refused the batch: every heavy packet's sort word and
 // payload word at its place in its source's run (pass 0's layout: bucket light_b + h from
-// its base), stable in arrival order. One wave per sort tile.
+// its base), stable in arrival order — on the unsorted path, of the sliding window's sparse
+// heavy sources only (HeavySet::srun). One wave per sort tile.
 __global__ __launch_bounds__(256) void k_heavy_gather(const BatchState *bs, const uint8_t *__restrict__ tags,
                                                       const uint64_t *__restrict__ ts, const uint32_t *__restrict__ len,
                                                       uint32_t n, const uint32_t *__restrict__ offs, uint32_t tcap,
@@ -418,35 +219,55 @@ __global__ __launch_bounds__(256) void k_heavy_gather(const BatchState *bs, cons
                                                       uint64_t id_mask, uint64_t *__restrict__ out,
                                                       uint64_t *__restrict__ pout) {
     __shared__ uint32_t s_cnt[4][kHeavyMax];
-    if (bs->err || bs->hfast) return;
+    if (bs->err || (bs->hfast && !hs->nrun)) return;
     const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
     const uint32_t lb = bs->light_b, nh = hs->n;
+    const uint64_t r0m = bs->hfast ? hs->srun[0] : ~0ull, r1m = bs->hfast ? hs->srun[1] : ~0ull;
     const uint64_t tb = n ? ts[0] : 0ull;
     const uint32_t ntiles = (n + kSortTile - 1) / kSortTile;
     const uint64_t lt = (1ull << lane) - 1ull;
     for (uint32_t t = blockIdx.x * 4u + w; t < ntiles; t += gridDim.x * 4u) {
         for (uint32_t h = lane; h < kHeavyMax; h += 64) s_cnt[w][h] = 0;
         wave_lds_order();
-        for (uint32_t r = 0; r < (uint32_t)kSortTile / 64u; ++r) {
-            const uint32_t i = t * (uint32_t)kSortTile + r * 64u + lane;
-            const uint32_t g = i < n ? tags[i] : 0u;
-            const bool hv = g >= 0x80u && (g & 0x7Fu) < nh;
-            const uint64_t act = __ballot(hv);
-            if (!act) continue;
-            const uint32_t h = g & 0x7Fu;
-            const uint64_t peers = match_digit(h, act);
-            const uint32_t lead = (uint32_t)__ffsll((unsigned long long)peers) - 1u;
-            uint32_t base = 0;
-            if (hv && lane == lead) base = s_cnt[w][h];
-            base = __shfl(base, (int)lead);
-            wave_lds_order();
-            if (hv) {
-                const uint32_t pos = offs[(size_t)(lb + h) * tcap + t] + base + (uint32_t)__popcll(peers & lt);
-                out[pos] = ((uint64_t)(lb + h) << shift0) | ((uint64_t)(hs->slot[h] & id_mask) << kIdShift) | i;
-                pout[pos] = ((ts[i] - tb) << kPayLenBits) | len[i];
-                if ((peers >> lane) == 1ull) s_cnt[w][h] = base + (uint32_t)__popcll(peers);
+        // 16 rows' tags, then their heavy packets' timestamps and lengths, in flight at once
+        for (uint32_t r0 = 0; r0 < (uint32_t)kSortTile / 64u; r0 += 16) {
+            uint32_t G[16], L[16];
+            uint64_t T[16];
+#pragma unroll
+            for (uint32_t r = 0; r < 16; ++r) {
+                const uint32_t i = t * (uint32_t)kSortTile + (r0 + r) * 64u + lane;
+                G[r] = i < n ? tags[i] : 0u;
             }
-            wave_lds_order();
+#pragma unroll
+            for (uint32_t r = 0; r < 16; ++r) {
+                const uint32_t i = t * (uint32_t)kSortTile + (r0 + r) * 64u + lane;
+                const uint32_t hg = G[r] & 0x7Fu;
+                const bool hv = G[r] >= 0x80u && hg < nh && (((hg < 64 ? r0m : r1m) >> (hg & 63u)) & 1u);
+                G[r] = hv ? hg : 0xFFu;
+                T[r] = hv ? ts[i] : 0ull;
+                L[r] = hv ? len[i] : 0u;
+            }
+#pragma unroll
+            for (uint32_t r = 0; r < 16; ++r) {
+                const uint32_t i = t * (uint32_t)kSortTile + (r0 + r) * 64u + lane;
+                const bool hv = G[r] != 0xFFu;
+                const uint64_t act = __ballot(hv);
+                if (!act) continue;
+                const uint32_t h = G[r] & 0x7Fu;
+                const uint64_t peers = match_digit(h, act);
+                const uint32_t lead = (uint32_t)__ffsll((unsigned long long)peers) - 1u;
+                uint32_t base = 0;
+                if (hv && lane == lead) base = s_cnt[w][h];
+                base = __shfl(base, (int)lead);
+                wave_lds_order();
+                if (hv) {
+                    const uint32_t pos = offs[(size_t)(lb + h) * tcap + t] + base + (uint32_t)__popcll(peers & lt);
+                    out[pos] = ((uint64_t)(lb + h) << shift0) | ((uint64_t)(hs->slot[h] & id_mask) << kIdShift) | i;
+                    pout[pos] = ((T[r] - tb) << kPayLenBits) | L[r];
+                    if ((peers >> lane) == 1ull) s_cnt[w][h] = base + (uint32_t)__popcll(peers);
+                }
+                wave_lds_order();
+            }
         }
     }
 }
@@ -655,9 +476,9 @@ hipError_t launch_heavy_recs(const BatchState *bs, const uint64_t *ts, const uin
     return hipGetLastError();
 }
 
-hipError_t launch_hmode_state(BatchState *bs, const HeavySet *hs, const Slot *table, const Limits &lim,
-                              TableState *tstate, hipStream_t st) {
-    k_hmode_state<<<1, 128, 0, st>>>(bs, hs, table, lim, tstate);
+hipError_t launch_hmode_state(const uint32_t *cnt0, uint32_t n, BatchState *bs, HeavySet *hs, const Slot *table,
+                              const Limits &lim, TableState *tstate, hipStream_t st) {
+    k_hmode_state<<<1, 128, 0, st>>>(cnt0, n, bs, hs, table, lim, tstate);
     return hipGetLastError();
 }
 

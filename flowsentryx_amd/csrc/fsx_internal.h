@@ -137,6 +137,10 @@ constexpr size_t kTableStateResetBytes = offsetof(TableState, n_hfast);
 // still inside the window (<= pps_threshold entries, oldest first), packed by source in
 // one of two ping-pong buffers. Slot.aux = offset << kHistCntBits | count.
 constexpr uint32_t kHistCntBits = 24;
+// The sliding window's heavy sources by rank (k_walk_sw_heavy_sel) stage every heavy source's
+// final log (<= pps_threshold entries) past the history's capacity: pps_threshold <= this,
+// else the run path.
+constexpr uint32_t kSwHeavyMaxP = 4096;
 constexpr uint64_t kAuxWalked = 1ull << 63;   // Slot.aux during a batch: walked segment id
 
 struct HistBufs {
@@ -171,6 +175,7 @@ struct Limits {           // the rate-limiter constants, src/fsx_kern.c:245,308-
     uint64_t admit_mask;
 };
 constexpr uint32_t kFlagAdmit = 8u;   // include/fsx_hip.h FSX_FLAG_OVERFLOW_ADMIT
+constexpr uint32_t kFlagSwSparse = 16u;   // include/fsx_hip.h FSX_FLAG_TEST_SW_SPARSE
 
 // ------------------------------------------------------------ hashing
 __host__ __device__ inline uint64_t mix64(uint64_t x) {
@@ -350,6 +355,11 @@ struct HeavySet {
     // walker of its segment; read by k_verdict_apply for the packets k_parse tagged 0x80 | h)
     uint32_t lbase[kHeavyMax];
     uint32_t lcnt[kHeavyMax];
+    // sliding window on the unsorted path (k_hmode_state): bit h set = heavy source h is too
+    // sparse for the rank walker (select / rank cost a verdict-tile scan each) and takes the
+    // run path (k_heavy_gather, k_walk_sw_heavy); nrun = their count
+    uint64_t srun[2];
+    uint32_t nrun, pad_;
     // open addressing on the source's probe start (its table hash) modulo the map size:
     // heavy index + 1, 0 empty
     alignas(16) uint8_t map[1u << kHeavyMapBits];
@@ -566,7 +576,13 @@ hipError_t launch_sliding_window(const uint64_t *S, const uint64_t *ts, const ui
                                  const Scratch &sc, Slot *table, TableState *tstate, const HistBufs &hb,
                                  const Limits &lim, uint32_t n, hipStream_t st, const Marker &mark,
                                  hipStream_t st3, hipEvent_t fork_ev, hipEvent_t join_ev,
-                                 const HeavyLists *H);   // (H->list: heavy verdict lists)
+                                 const HeavyLists *H,    // (H->list: heavy verdict lists)
+                                 const uint8_t *tags,    // (heavy sources outside the sort: verdict tags)
+                                 hipEvent_t heavy_done); // (launch_sw_heavy ran on another stream)
+hipError_t launch_sw_heavy(const uint64_t *S, const uint64_t *ts, const uint32_t *len, BatchState *bs,
+                           const Scratch &sc, Slot *table, TableState *tstate, const HistBufs &hb,
+                           const Limits &lim, uint32_t n, const HeavyLists &H, const uint8_t *tags,
+                           hipStream_t st);
 
 hipError_t launch_pcap_records(const uint8_t *buf, const uint64_t *off, const uint32_t *caplen, uint32_t n,
                                uint8_t *hdr, hipStream_t st);
@@ -602,8 +618,8 @@ hipError_t launch_hmode(BatchState *bs, const uint64_t *ts, uint32_t n, const Li
 hipError_t launch_heavy_recs(const BatchState *bs, const uint64_t *ts, const uint32_t *len, const uint8_t *tags,
                              uint32_t n, const HeavySet *hs, void *rec, hipStream_t st);
 // (the tail's first kernel: the heavy sources' carried state, after the previous tail stored it)
-hipError_t launch_hmode_state(BatchState *bs, const HeavySet *hs, const Slot *table, const Limits &lim,
-                              TableState *tstate, hipStream_t st);
+hipError_t launch_hmode_state(const uint32_t *cnt0, uint32_t n, BatchState *bs, HeavySet *hs, const Slot *table,
+                              const Limits &lim, TableState *tstate, hipStream_t st);
 hipError_t launch_heavy_gather(const BatchState *bs, const uint8_t *tags, const uint64_t *ts, const uint32_t *len,
                                uint32_t n, const uint32_t *offs, uint32_t tcap, const HeavySet *hs, uint32_t shift0,
                                uint64_t id_mask, uint64_t *out, uint64_t *pout, hipStream_t st);

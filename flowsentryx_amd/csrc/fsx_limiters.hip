@@ -41,6 +41,7 @@
 #include "fsx_dev_common.h"
 #include "fsx_internal.h"
 #include "fsx_seg.h"
+#include "fsx_heavy_view.h"
 
 namespace fsx {
 
@@ -584,18 +585,6 @@ __device__ void sw_walk_fast_thread(const SV &sv, uint32_t a, uint32_t b, const 
     }
 }
 
-__device__ __forceinline__ bool sw_mono(const BatchState *bs, const TableState *ts) {
-    return !bs->nonmono && !ts->ever_nonmono && ~bs->inv_min_ts >= ts->last_max_ts;
-}
-
-// The epoch-style walkers hold when clocks are monotone, no byte trigger can come before
-// the count trigger and till / window ends do not overflow u64.
-__device__ __forceinline__ bool sw_fast(const BatchState *bs, const TableState *tst, const Limits &lim) {
-    const uint32_t maxL = bs->max_len > tst->max_len_seen ? bs->max_len : tst->max_len_seen;
-    const uint64_t lim_ts = lim.window > lim.block ? lim.window : lim.block;
-    return sw_mono(bs, tst) && lim.pps * (uint64_t)maxL <= lim.bps && bs->max_ts <= ~0ull - lim_ts;
-}
-
 template <class SV>
 __device__ __forceinline__ void sw_short_body(const SV &sv, const BatchState *bs, const TableState *tst,
                                               const uint32_t *seg_start,
@@ -695,13 +684,14 @@ __global__ __launch_bounds__(256) void k_walk_sw_heavy(const uint64_t *__restric
                                                        const uint32_t *__restrict__ len,
                                                        const uint64_t *__restrict__ pay, Slot *table, Limits lim,
                                                        HistBufs hb, SwSeg *__restrict__ segs, HeavyLists H) {
-    if (bs->err) return;
+    if (bs->err || (bs->hfast && !H.hs->nrun)) return;   // (hfast: k_walk_sw_heavy_sel, but sparse ones)
     const uint32_t h = blockIdx.x * 4u + (threadIdx.x >> 6), lane = lane_id();
     const uint32_t lb = bs->light_b;
     const bool live0 = lane < kHeavyMax && cnt0[lb + lane] > 0;
     const bool live1 = lane + 64u < kHeavyMax && cnt0[lb + 64u + lane] > 0;
     const uint64_t m0 = __ballot(live0), m1 = __ballot(live1);
     if (h >= H.hs->n) return;
+    if (bs->hfast && !((H.hs->srun[h >> 6] >> (h & 63u)) & 1u)) return;
     const uint32_t c = cnt0[lb + h];
     if (c == 0) return;
     const uint32_t rk = h < 64 ? (uint32_t)__popcll(m0 & ((1ull << h) - 1ull))
@@ -735,6 +725,188 @@ __global__ __launch_bounds__(256) void k_walk_sw_heavy(const uint64_t *__restric
     if (lane == 0) {
         segs[g] = rec;
         sw_store(sl, st, g);
+    }
+}
+
+// A carried log as a plain timestamp array (wave_gallop_gt over its entries).
+struct LogView {
+    const uint64_t *t_;
+    __device__ __forceinline__ uint64_t t(uint32_t v) const { return t_[v]; }
+};
+
+// Heavy sources outside the sort: one wave per heavy source, sw_walk_fast_wave's
+// phases over its carried log (hoff, m) followed by its packets by rank (HeavyView: select /
+// rank over the verdict tags, block() for 64 consecutive ranks). Monotone clocks only
+// (k_hmode_state: sw_fast); the final log — at most pps_threshold <= kSwHeavyMaxP entries —
+// is staged past the history's capacity (hist_cap + h * kSwHeavyMaxP of the current buffer)
+// so that k_sw_hist copies it like any carried log.
+__global__ __launch_bounds__(256) void k_walk_sw_heavy_sel(BatchState *bs, const TableState *tst,
+                                                           const uint32_t *__restrict__ cnt0,
+                                                           const uint32_t *__restrict__ base0,
+                                                           const uint32_t *__restrict__ offs, uint32_t tcap,
+                                                           const uint8_t *__restrict__ tags,
+                                                           const uint64_t *__restrict__ ts,
+                                                           const uint32_t *__restrict__ len, uint32_t n,
+                                                           const HeavyTileRec *__restrict__ hrec, Slot *table,
+                                                           Limits lim, HistBufs hb, SwSeg *__restrict__ segs,
+                                                           HeavySet *hs, uint32_t *list, TableState *tstate) {
+    __shared__ uint32_t s_idx[4][64];
+    if (bs->err || !bs->hfast) return;
+    const uint32_t wv = threadIdx.x >> 6, h = blockIdx.x * 4u + wv, lane = lane_id();
+    const uint32_t lb = bs->light_b;
+    const bool live0 = lane < kHeavyMax && cnt0[lb + lane] > 0;
+    const bool live1 = lane + 64u < kHeavyMax && cnt0[lb + 64u + lane] > 0;
+    const uint64_t m0 = __ballot(live0), m1 = __ballot(live1);
+    if (h >= hs->n || ((hs->srun[h >> 6] >> (h & 63u)) & 1u)) return;   // (sparse: k_walk_sw_heavy)
+    const uint32_t c = cnt0[lb + h];
+    if (c == 0) return;
+    const uint32_t rk = h < 64 ? (uint32_t)__popcll(m0 & ((1ull << h) - 1ull))
+                               : (uint32_t)__popcll(m0) + (uint32_t)__popcll(m1 & ((1ull << (h - 64)) - 1ull));
+    const uint32_t g = bs->nseg_light + rk;   // (k_heads_heavy's numbering)
+    const uint32_t a = base0[lb + h];
+    uint32_t *sx = s_idx[wv];
+    const HeavyView hv{tags, ts, len, offs + (size_t)(lb + h) * tcap, hrec, a, c, (n + kSortTile - 1) / kSortTile,
+                       n, h, (0x80u | h) * 0x01010101u};
+    const uint32_t cur = tst->hist_cur;
+    uint64_t *ht = hb.t[cur];
+    uint32_t *hl = hb.l[cur];
+    Slot &sl = table[hs->slot[h]];
+    SwState s = sw_load(sl);
+    uint64_t hoff;
+    uint32_t m;
+    sw_hist_of(sl.aux, hoff, m);
+    HeavyMarkWriter mw{hv, list + 2u * a};
+    const uint64_t P = lim.pps, W = lim.window;
+    uint32_t p = 0;   // ranks
+    if (s.has_bl && s.till > 0) {
+        p = search_gt<true>(hv, 0, c, s.till);
+        if (p > 0) mw.emit(0, XDP_DROP);
+        if (p < c) s.has_bl = false;
+    }
+    const uint32_t j0 = p;   // virtual index v: the log's entry v < m, else rank j0 + v - m
+    const LogView lv{ht + hoff};
+    auto vt = [&](uint32_t v) __attribute__((always_inline)) -> uint64_t { return v < m ? ht[hoff + v] : hv.t(j0 + v - m); };
+    auto vgt = [&](uint32_t lo, uint32_t hi, uint64_t X) __attribute__((always_inline)) -> uint32_t {   // first v in [lo, hi): t(v) > X
+        if (lo >= hi) return hi;
+        if (lo < m) {
+            const uint32_t e = min(hi, m);
+            const uint32_t r = wave_gallop_gt(lv, lo, e, X);
+            if (r < e || e == hi) return r;
+            lo = m;
+        }
+        return m + search_gt<true>(hv, j0 + lo - m, j0 + hi - m, X) - j0;
+    };
+    auto vsum = [&](uint32_t lo, uint32_t hi) __attribute__((always_inline)) -> uint64_t {
+        uint64_t x = 0;
+        for (uint32_t v = lo + lane; v < min(hi, m); v += 64) x += hl[hoff + v];
+        x = wave_sum(x);
+        const uint32_t l2 = max(lo, m);
+        if (hi > l2) x += sum_len<true>(hv, j0 + l2 - m, j0 + hi - m);
+        return x;
+    };
+    auto log_start = [&](uint32_t f, uint32_t vq, uint64_t tq) __attribute__((always_inline)) -> uint32_t {
+        if (tq < W) return f;
+        const uint32_t lo = vgt(f, vq + 1, tq - W);
+        return lo < vq ? lo : vq;
+    };
+    auto stats = [&](uint32_t lo, uint32_t v) __attribute__((always_inline)) {
+        s.has_st = true;
+        s.pps = (uint64_t)(v - lo) + 1;
+        s.bps = vsum(lo, v + 1);
+        s.tt = vt(lo);
+    };
+    SwSeg rec{};
+    rec.hoff = hoff; rec.m = m; rec.j0 = j0;
+    rec.lo = 0; rec.hi = m;   // no counted packet: the log is unchanged
+    uint32_t f = 0;
+    while (p < c) {
+        uint32_t k = c;   // first count trigger at or after p (not before v = f + P)
+        uint32_t qs = p;
+        if (P > 0) {
+            const uint64_t need = (uint64_t)f + P, vp = (uint64_t)m + (p - j0);
+            if (need > vp) qs = (uint32_t)min((uint64_t)c, (uint64_t)j0 + (need - m));
+        }
+        for (uint32_t q0 = qs; q0 < c; q0 += 64) {
+            const uint32_t q = q0 + lane;
+            const uint32_t iq = hv.block(q0, sx);
+            const uint64_t tq = iq < n ? ts[iq] : 0ull;
+            bool pr;
+            if (P == 0) {
+                pr = q < c;
+            } else {
+                // the entry P before each lane's packet: u = v - P >= f (q0 >= qs), from the log
+                // below m, else rank j0 + u - m — one block from the first such rank, shifted
+                const uint32_t u0 = m + (q0 - j0) - (uint32_t)P;
+                const uint32_t u = u0 + lane;
+                uint64_t tu = 0;
+                if (u0 + 63u >= m) {
+                    const uint32_t b0 = max(u0, m), sft = b0 - u0;
+                    const uint32_t iu = hv.block(j0 + b0 - m, sx);
+                    const uint64_t tb = iu < n ? ts[iu] : 0ull;
+                    tu = __shfl(tb, (int)(lane >= sft ? lane - sft : 0u));
+                }
+                if (u < m) tu = ht[hoff + u];
+                pr = q < c && tq - tu < W;
+            }
+            const uint64_t bal = __ballot(pr);
+            if (bal) { k = q0 + (uint32_t)__ffsll((unsigned long long)bal) - 1u; break; }
+        }
+        if (k >= c) {   // the phase runs to the end of the batch
+            mw.emit(p, XDP_PASS);
+            const uint32_t vl = m + (c - 1 - j0);
+            const uint32_t lo = log_start(f, vl, hv.t(c - 1));
+            stats(lo, vl);
+            rec.lo = lo; rec.hi = vl + 1;
+            break;
+        }
+        if (k > p) mw.emit(p, XDP_PASS);
+        mw.emit(k, XDP_DROP);
+        const uint32_t vk = m + (k - j0);
+        const uint64_t tk = hv.t(k);
+        stats(log_start(f, vk, tk), vk);
+        s.till = tk + lim.block;
+        s.has_bl = true;
+        rec.lo = 0; rec.hi = 0;   // log cleared
+        const uint32_t j = search_gt<true>(hv, k + 1, c, s.till);
+        if (j >= c) break;        // blacklisted to the end of the batch
+        s.has_bl = false;
+        f = m + (j - j0);
+        p = j;
+    }
+    mw.finish(c);
+    if (rec.hi > m) {   // the log holds packets of this batch: stage it (<= P entries)
+        const uint64_t so = hb.cap + (uint64_t)h * kSwHeavyMaxP;
+        const uint32_t lo = rec.lo, hi = rec.hi;
+        for (uint32_t v = lo + lane; v < min(hi, m); v += 64) {
+            ht[so + (v - lo)] = ht[hoff + v];
+            hl[so + (v - lo)] = hl[hoff + v];
+        }
+        const uint32_t l2 = max(lo, m);
+        const uint32_t r1 = j0 + hi - m;
+        for (uint32_t r0 = j0 + l2 - m; r0 < r1; r0 += 64) {
+            const uint32_t i = hv.block(r0, sx);
+            const uint32_t r = r0 + lane;
+            if (r < r1) {
+                const uint64_t o = so + (m + r - j0 - lo);
+                ht[o] = ts[i];
+                hl[o] = len[i];
+            }
+        }
+        rec.hoff = so; rec.m = hi - lo; rec.j0 = 0; rec.lo = 0; rec.hi = hi - lo;
+    }
+    if (lane != 0) return;
+    segs[g] = rec;
+    sw_store(sl, s, g);
+    hs->lbase[h] = 2u * a;
+    hs->lcnt[h] = mw.nl;
+    unsigned long long *sp = reinterpret_cast<unsigned long long *>(tstate->stats);
+    if (mw.npass) {
+        atomicAdd(sp, (unsigned long long)mw.npass);
+        atomicAdd(reinterpret_cast<unsigned long long *>(&bs->allowed), (unsigned long long)mw.npass);
+    }
+    if (mw.ndrop) {
+        atomicAdd(sp + 1, (unsigned long long)mw.ndrop);
+        atomicAdd(reinterpret_cast<unsigned long long *>(&bs->dropped), (unsigned long long)mw.ndrop);
     }
 }
 
@@ -901,10 +1073,28 @@ __global__ void k_sw_finish(const BatchState *bs, TableState *tst, const uint64_
     if (bs->max_len > tst->max_len_seen) tst->max_len_seen = bs->max_len;
 }
 
+// The heavy sources' walkers (heavy verdict lists): by rank on the unsorted path (tags), the
+// pass-0 runs otherwise and for the sparse ones; each returns at once on the other path.
+hipError_t launch_sw_heavy(const uint64_t *S, const uint64_t *ts, const uint32_t *len, BatchState *bs,
+                           const Scratch &sc, Slot *table, TableState *tstate, const HistBufs &hb,
+                           const Limits &lim, uint32_t n, const HeavyLists &H, const uint8_t *tags,
+                           hipStream_t st) {
+    if (tags) {
+        const uint32_t tcap = (uint32_t)(sc.cap / kSortTile + 2);
+        k_walk_sw_heavy_sel<<<kHeavyMax / 4, 256, 0, st>>>(
+            bs, tstate, sc.sort_ctl, sc.gbase, sc.hist, tcap, tags, ts, len, n,
+            static_cast<const HeavyTileRec *>(sc.hrec), table, lim, hb, sc.sw_seg, sc.heavy, H.list, tstate);
+    }
+    k_walk_sw_heavy<<<kHeavyMax / 4, 256, 0, st>>>(S, bs, tstate, sc.sort_ctl, sc.gbase, sc.seg_slot, ts, len,
+                                                   sc.pay[0], table, lim, hb, sc.sw_seg, H);
+    return hipGetLastError();
+}
+
 hipError_t launch_sliding_window(const uint64_t *S, const uint64_t *ts, const uint32_t *len, BatchState *bs,
                                  const Scratch &sc, Slot *table, TableState *tstate, const HistBufs &hb,
                                  const Limits &lim, uint32_t n, hipStream_t st, const Marker &mark,
-                                 hipStream_t st3, hipEvent_t fork_ev, hipEvent_t join_ev, const HeavyLists *H) {
+                                 hipStream_t st3, hipEvent_t fork_ev, hipEvent_t join_ev, const HeavyLists *H,
+                                 const uint8_t *tags, hipEvent_t heavy_done) {
     (void)hipGetLastError();   // a stale error of another caller is not ours
     const uint32_t lists = H && H->list ? 1u : 0u;
     const uint32_t gridSeg = std::min<uint32_t>(2048, std::max<uint32_t>(1, (n + 255) / 256));
@@ -919,9 +1109,11 @@ hipError_t launch_sliding_window(const uint64_t *S, const uint64_t *ts, const ui
     }
     // heavy verdict lists: the heavy sources' runs (pass 0's buffer, which with 3 passes is
     // also the light entries' final one: S, pay[0]) first on the side stream, latency-bound
-    if (lists) {
-        k_walk_sw_heavy<<<kHeavyMax / 4, 256, 0, fork ? st3 : st>>>(S, bs, tstate, sc.sort_ctl, sc.gbase, sc.seg_slot,
-                                                                    ts, len, sc.pay[0], table, lim, hb, sc.sw_seg, *H);
+    // (heavy_done: the caller launched them on another stream)
+    if (lists && !heavy_done) {
+        if ((e = launch_sw_heavy(S, ts, len, bs, sc, table, tstate, hb, lim, n, *H, tags, fork ? st3 : st)) !=
+            hipSuccess)
+            return e;
         mark("k_walk_sw_heavy");
     }
     k_walk_sw<true><<<1024, 256, 0, fork && !lists ? st3 : st>>>(S, bs, tstate, sc.seg_start, sc.seg_slot, ts, len,
@@ -933,6 +1125,7 @@ hipError_t launch_sliding_window(const uint64_t *S, const uint64_t *ts, const ui
     mark("k_walk_sw_short");
     if (fork && (e = hipStreamWaitEvent(st, join_ev, 0)) != hipSuccess) return e;
     mark("k_walk_sw_long_join");
+    if (lists && heavy_done && (e = hipStreamWaitEvent(st, heavy_done, 0)) != hipSuccess) return e;
     const uint64_t nslots = lim.table_mask + 1;
     const uint64_t ntiles = (nslots + kSlotTile - 1) / kSlotTile;
     const uint32_t grid = (uint32_t)std::min<uint64_t>(4096, ntiles);

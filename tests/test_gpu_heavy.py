@@ -1,8 +1,8 @@
 """GPU: heavy sources outside the sort (DESIGN.md §3 "Heavy sources outside the sort").
 
-The fixed window's heavy sources are walked by rank over the arrival order (select / rank
-over the tagged verdict bytes) and their flow rows come from per-tile sums, when k_hmode
-finds the batch eligible; otherwise k_heavy_gather builds their runs and the run path
+The fixed and sliding windows' heavy sources are walked by rank over the arrival order
+(select / rank over the tagged verdict bytes) and their flow rows come from per-tile sums,
+when k_hmode finds the batch eligible; otherwise k_heavy_gather builds their runs and the run path
 takes over. Both paths, bit-exact against the oracle: verdicts, stats_map, every map entry,
 and the per-source features + q8 scores (src/fsx_kern.c:150-346, model/model.py:132-137)."""
 import json
@@ -15,7 +15,7 @@ from kat import GOLDEN
 pytestmark = pytest.mark.gpu
 
 
-def _run(native, oracle, batches, cfg, prepare=None, want_path=None, pipeline=False):
+def _run(native, oracle, batches, cfg, prepare=None, want_path=None, pipeline=False, cap=None):
     """Each batch through fsx_process_batch_device on one context (maps carried); after each
     one: verdicts, flow rows and (at the end) stats + maps against the oracle. Returns the
     heavy_unsorted flag of every batch."""
@@ -24,7 +24,7 @@ def _run(native, oracle, batches, cfg, prepare=None, want_path=None, pipeline=Fa
     from oracle import pyoracle
     ref = json.loads((GOLDEN / "model_weights.json").read_text())
     o = oracle.Oracle(**cfg)
-    cap = max(len(b[1]) for b in batches)
+    cap = cap or max(len(b[1]) for b in batches)   # (also sizes the sliding-window history: 2 x cap)
     dev = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).reshape(-1)).cuda()
     out = dict(v=torch.empty(cap, dtype=torch.uint8, device="cuda"),
                k=torch.empty(cap * 16, dtype=torch.uint8, device="cuda"),
@@ -158,20 +158,34 @@ def test_blacklisted_heavy_source_carried(native, oracle):
 SW = dict(CFG, limiter=1)   # the sliding window's heavy verdict lists (3-pass sort: 21-bit ids)
 
 
-@pytest.mark.parametrize("case", ["slices", "non_monotone", "byte_trigger", "blacklisted", "pipelined"])
+@pytest.mark.parametrize("case", ["slices", "slices4", "sparse", "sparse_pipelined", "non_monotone", "byte_trigger",
+                                  "blacklisted", "pipelined", "pps_over_staging"])
 def test_sliding_window_heavy_lists(native, oracle, case):
-    """The sliding window with heavy verdict lists: k_walk_sw_heavy walks each
-    heavy source's pass-0 run (epoch walker when clocks are monotone and the byte trigger
-    unreachable, the exact replay otherwise) and writes its log record for the history
-    rebuild; carried over the cut, verdicts / flows / stats / maps bit-exact."""
-    n = 1 << 21 if case in ("slices", "pipelined") else 1 << 20
+    """The sliding window with heavy verdict lists. Monotone clocks with the
+    byte trigger out of reach: k_walk_sw_heavy_sel walks each heavy source by rank over the
+    arrival order and stages its final log for the history rebuild (heavy_unsorted = 1 every
+    batch, the first one from an empty map included); heavy sources under 1/128 of a batch
+    take the run path alone ("sparse": the test flag keeps them in the heavy set). Otherwise (a clock step back — then
+    for good —, a reachable byte trigger, pps_threshold above the 4096-entry staging)
+    k_heavy_gather builds the runs and k_walk_sw_heavy walks them. Carried over the cuts,
+    verdicts / flows / stats / maps bit-exact."""
+    n = 1 << 21 if case in ("slices", "slices4", "pipelined", "sparse_pipelined") else 1 << 20
     hdr, ln, ts = _config2(oracle, n)
     cfg, prepare = dict(SW), None
+    fast = 1
     if case == "non_monotone":
         ts = ts.copy()
         ts[500_000], ts[500_001] = ts[500_001], ts[500_000] - 7
+        fast = 0
     elif case == "byte_trigger":
         cfg.update(bps_threshold=300_000)
+        fast = 0
+    elif case.startswith("sparse"):
+        from flowsentryx_amd import lib
+        cfg.update(flags=lib.FLAG_TEST_SW_SPARSE)
+    elif case == "pps_over_staging":
+        cfg.update(pps_threshold=4097)
+        fast = 0
     elif case == "blacklisted":
         src, cnt = np.unique(hdr[:, 26:30].copy().view(np.uint32).reshape(-1), return_counts=True)
         order = np.argsort(-cnt)
@@ -182,10 +196,11 @@ def test_sliding_window_heavy_lists(native, oracle, case):
             for k, v in ((a, mid), (b, 2**64 - 1)):
                 c.map_update(3, k, v)
                 o.map_update(3, k, v)
-    k = 3 if case == "pipelined" else 2
+    k = {"pipelined": 3, "sparse_pipelined": 3, "slices4": 4}.get(case, 2)
     cuts = [i * n // k for i in range(k + 1)]
     _run(native, oracle, [(hdr[x:y], ln[x:y], ts[x:y]) for x, y in zip(cuts[:-1], cuts[1:])], cfg,
-         prepare=prepare, want_path=[0] * k, pipeline=case == "pipelined")
+         prepare=prepare, want_path=[fast] * k, pipeline=case.endswith("pipelined"),
+         cap=n if case == "slices4" else None)
 
 
 def test_unsorted_heavy_path_record_mode(native, oracle):
