@@ -3020,7 +3020,9 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
     // slots; k_hmode picks the batch's path on the device (FSX_NO_HFAST=1: the runs, A/B)
     static const bool no_hfast = getenv("FSX_NO_HFAST") != nullptr;
     // (record mode too: the records' len / ts go to in.rec_len / rec_ts, which k_pass0h reads)
-    const bool hfm = tagh && lim.limiter <= 1 && resolve && !no_hfast;
+    // (sliding window: FSX_FLAG_SW_UNSORTED only — measured slower than the sort)
+    const bool hfm = tagh && (lim.limiter == 0 || (lim.limiter == 1 && (lim.test_flags & kFlagSwUnsorted))) &&
+                     resolve && !no_hfast;
     if (!(split && split->tail) && (e = hipMemsetAsync(sc.marks, 0, n, st)) != hipSuccess) return e;
     DigitPlan dp{};
     dp.npass = (uint32_t)npass;
@@ -3044,8 +3046,10 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
         // rank walker's dense ones, k_hmode_state sends any under 1/128 of the batch to the
         // run path — the rest sort with the light sources)
         const uint32_t S = std::min<uint32_t>(n, kHeavySample);
-        const bool sw_dense = hfm && lim.limiter == 1 && !(lim.test_flags & kFlagSwSparse);
-        const uint32_t floor_cnt = sw_dense ? std::max<uint32_t>(16, S / 96) : 16u;
+        // (FSX_SW_FLOOR=D: 1/D of the sample instead, 0 the fixed window's floor — A/B)
+        static const uint32_t sw_div = getenv("FSX_SW_FLOOR") ? (uint32_t)atoi(getenv("FSX_SW_FLOOR")) : 96u;
+        const bool sw_dense = hfm && lim.limiter == 1 && !(lim.test_flags & kFlagSwSparse) && sw_div;
+        const uint32_t floor_cnt = sw_dense ? std::max<uint32_t>(16, S / sw_div) : 16u;
         k_heavy_pick<<<1, 1024, 0, sp0>>>(in, len, sc.sketch, sc.heavy, nheavy, floor_cnt, lim.seed,
                                           lim.table_mask, lim.test_flags, idt, resolve, bs);
         mark("k_heavy_pick");

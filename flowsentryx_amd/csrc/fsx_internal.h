@@ -175,7 +175,8 @@ struct Limits {           // the rate-limiter constants, src/fsx_kern.c:245,308-
     uint64_t admit_mask;
 };
 constexpr uint32_t kFlagAdmit = 8u;   // include/fsx_hip.h FSX_FLAG_OVERFLOW_ADMIT
-constexpr uint32_t kFlagSwSparse = 16u;   // include/fsx_hip.h FSX_FLAG_TEST_SW_SPARSE
+constexpr uint32_t kFlagSwUnsorted = 16u;   // include/fsx_hip.h FSX_FLAG_SW_UNSORTED
+constexpr uint32_t kFlagSwSparse = 32u;     // include/fsx_hip.h FSX_FLAG_TEST_SW_SPARSE
 
 // ------------------------------------------------------------ hashing
 __host__ __device__ inline uint64_t mix64(uint64_t x) {

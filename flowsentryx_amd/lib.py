@@ -49,7 +49,8 @@ FLAG_TEST_V6_COLLIDE = 1
 FLAG_ONESWEEP_SORT = 2
 FLAG_EVICT_IDLE = 4   # opt-in idle eviction on overflow
 FLAG_OVERFLOW_ADMIT = 8   # opt-in admission of a flood's new sources
-FLAG_TEST_SW_SPARSE = 16  # test hook: sparse heavy sources on the sliding window's run path
+FLAG_SW_UNSORTED = 16     # A/B hook: the sliding window's heavy sources outside the sort
+FLAG_TEST_SW_SPARSE = 32  # test hook: sparse heavy sources on the sliding window's run path
 
 LIMIT_FIXED_WINDOW = 0
 LIMIT_SLIDING_WINDOW = 1

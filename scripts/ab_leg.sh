@@ -12,6 +12,10 @@ for e in "$@"; do
 import json, sys
 leg, e = sys.argv[1], sys.argv[2]
 d = json.loads(open("gpurun_out/abl.json").read().strip().splitlines()[-1])
-print(e or "default", leg, d[leg]["ms_per_step"])
+r = d[leg]
+if "ms_per_step" in r:
+    print(e or "default", leg, r["ms_per_step"])
+else:   # (a leg of several runs: limiters)
+    print(e or "default", leg, {k: v["ms_per_step"] for k, v in r.items() if isinstance(v, dict)})
 PY
 done

@@ -158,11 +158,12 @@ def test_blacklisted_heavy_source_carried(native, oracle):
 SW = dict(CFG, limiter=1)   # the sliding window's heavy verdict lists (3-pass sort: 21-bit ids)
 
 
-@pytest.mark.parametrize("case", ["slices", "slices4", "sparse", "sparse_pipelined", "non_monotone", "byte_trigger",
-                                  "blacklisted", "pipelined", "pps_over_staging"])
+@pytest.mark.parametrize("case", ["default", "slices", "slices4", "sparse", "sparse_pipelined", "non_monotone",
+                                  "byte_trigger", "blacklisted", "pipelined", "pps_over_staging"])
 def test_sliding_window_heavy_lists(native, oracle, case):
-    """The sliding window with heavy verdict lists. Monotone clocks with the
-    byte trigger out of reach: k_walk_sw_heavy_sel walks each heavy source by rank over the
+    """The sliding window with heavy verdict lists: by default on the heavy-source
+    sort (k_walk_sw_heavy over the pass-0 runs). With FSX_FLAG_SW_UNSORTED (A/B), monotone
+    clocks and the byte trigger out of reach: k_walk_sw_heavy_sel walks each heavy source by rank over the
     arrival order and stages its final log for the history rebuild (heavy_unsorted = 1 every
     batch, the first one from an empty map included); heavy sources under 1/128 of a batch
     take the run path alone ("sparse": the test flag keeps them in the heavy set). Otherwise (a clock step back — then
@@ -171,8 +172,11 @@ def test_sliding_window_heavy_lists(native, oracle, case):
     verdicts / flows / stats / maps bit-exact."""
     n = 1 << 21 if case in ("slices", "slices4", "pipelined", "sparse_pipelined") else 1 << 20
     hdr, ln, ts = _config2(oracle, n)
-    cfg, prepare = dict(SW), None
+    from flowsentryx_amd import lib
+    cfg, prepare = dict(SW, flags=lib.FLAG_SW_UNSORTED), None
     fast = 1
+    if case == "default":
+        cfg, fast = dict(SW), 0
     if case == "non_monotone":
         ts = ts.copy()
         ts[500_000], ts[500_001] = ts[500_001], ts[500_000] - 7
@@ -181,8 +185,7 @@ def test_sliding_window_heavy_lists(native, oracle, case):
         cfg.update(bps_threshold=300_000)
         fast = 0
     elif case.startswith("sparse"):
-        from flowsentryx_amd import lib
-        cfg.update(flags=lib.FLAG_TEST_SW_SPARSE)
+        cfg.update(flags=lib.FLAG_SW_UNSORTED | lib.FLAG_TEST_SW_SPARSE)
     elif case == "pps_over_staging":
         cfg.update(pps_threshold=4097)
         fast = 0
