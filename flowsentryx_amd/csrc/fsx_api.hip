@@ -71,6 +71,9 @@ struct fsx_ctx {
     // FSX_FLAG_EVICT_IDLE: an upper bound on the tracked sources (the last count read plus
     // the packets of every batch since); ~0 = unknown (map imports, reset)
     uint64_t count_bound = ~0ull;
+    // the last checked limiter batch inserted more new sources than half its IP packets: the
+    // next batches take the home-ordered inserts (FSX_FLAG_ORDERED_INSERTS: always)
+    bool flood_hint = false;
     // sharding: per (owner, tile) counts of fsx_shard_pack_device, blocklist replica
     uint32_t *d_shard_cnt = nullptr;
     uint64_t shard_cnt_cap = 0;
@@ -536,6 +539,11 @@ static int rollback_batch(fsx_ctx *c, uint32_t born) {
 
 static int batch_error(fsx_ctx *c, uint32_t err);
 
+// A finished batch's facts the host keeps: a flood of new sources (home-ordered inserts next).
+static void note_batch(fsx_ctx *c, const BatchState &h) {
+    if (!h.err && h.n_valid) c->flood_hint = 2ull * h.n_new > h.n_valid;
+}
+
 static int check_batch(fsx_ctx *c) {
     if (!c->pending) return 0;
     c->pending = false;
@@ -543,6 +551,7 @@ static int check_batch(fsx_ctx *c) {
     c->pending_born = 0;
     BatchState h;
     HIPCHK(c, hipMemcpy(&h, c->bs, sizeof(h), hipMemcpyDeviceToHost));
+    note_batch(c, h);
     if (h.err && born) {
         const int rc = rollback_batch(c, born);
         if (rc) return rc;
@@ -561,6 +570,7 @@ static int check_pipelined(fsx_ctx *c) {
         c->fl_on[p] = false;
         BatchState h;
         HIPCHK(c, hipMemcpy(&h, c->fb[p].bs, sizeof(h), hipMemcpyDeviceToHost));
+        note_batch(c, h);
         if (!h.err && !failed) continue;
         if (c->fl_born[p]) {
             const int r = rollback_batch(c, c->fl_born[p]);
@@ -579,6 +589,9 @@ static int batch_error(fsx_ctx *c, uint32_t err) {
     if (err & ERR_TABLE_FULL)
         return set_err(c, -ENOSPC, "map full: more than max_entries=%llu source IPs",
                        (unsigned long long)c->cfg.max_entries);
+    if (err & ERR_FIXUP)
+        return set_err(c, -EIO, "home-ordered inserts: more than %u packets share one key hash with two sources",
+                       512u);
     if (err & ERR_HIST_FULL)
         return set_err(c, -ENOSPC, "sliding-window history full: carried logs + batch > %llu entries",
                        (unsigned long long)c->hist.cap);
@@ -817,6 +830,7 @@ static int run_pipelined(fsx_ctx *c, const PacketIn &in, const uint32_t *d_len, 
         HIPCHK(c, hipEventSynchronize(c->tail_done[q]));
         BatchState h;
         HIPCHK(c, hipMemcpy(&h, c->fb[q].bs, sizeof(h), hipMemcpyDeviceToHost));
+        note_batch(c, h);
         if (h.err) return fsx_sync(c);   // rolls it back, and the batch after it
         c->fl_on[q] = false;
     }
@@ -941,12 +955,19 @@ static int run_batch(fsx_ctx *c, const PacketIn &in, const uint32_t *d_len, cons
         const int rc = evict_idle(c, in, d_ts, n);
         if (rc) return rc;
     }
+    // home-ordered inserts for this batch: a flood of new sources (the last
+    // checked batch's n_new > half its IP packets) or FSX_FLAG_ORDERED_INSERTS; FSX_ORDERED=0 /
+    // 1: never / always (A/B). The fixed window on header records without flows, whole batches.
+    static const int ord_env = getenv("FSX_ORDERED") ? atoi(getenv("FSX_ORDERED")) : -1;
+    const bool ord_want = ord_env >= 0 ? ord_env > 0 : (c->flood_hint || (c->cfg.flags & FSX_FLAG_ORDERED_INSERTS));
+    c->lim.ord = do_limit && !fr && !in.rec && d_verdict && c->cfg.limiter == FSX_LIMIT_FIXED_WINDOW &&
+                 !(c->cfg.flags & FSX_FLAG_OVERFLOW_ADMIT) && ord_want ? 1u : 0u;
     // pipelined (no per-kernel timing): split front / tail for the fixed window on header
     // records, the whole batch on the context stream otherwise
     if (c->pipe && do_limit && n && !c->timing)
         return run_pipelined(c, in, d_len, d_ts, n, d_verdict, fr,
                              c->pipe == 1 && !in.rec && !no_split_limiters(c) &&
-                                 !(c->cfg.flags & FSX_FLAG_OVERFLOW_ADMIT));
+                                 !(c->cfg.flags & FSX_FLAG_OVERFLOW_ADMIT) && !c->lim.ord);
     int rc = sel(c);
     if (rc) return rc;
     if (busy(c)) { rc = fsx_sync(c); if (rc) return rc; }
@@ -1505,11 +1526,11 @@ int fsx_last_batch_info(fsx_ctx *c, uint64_t *info, int cap) {
     HIPCHK(c, hipMemcpy(&h, c->bs, sizeof(h), hipMemcpyDeviceToHost));
     TableState t;
     HIPCHK(c, hipMemcpy(&t, c->tstate, sizeof(t), hipMemcpyDeviceToHost));
-    const uint64_t v[18] = {h.n_valid, h.nseg, h.n_new, h.any_v6, h.nonmono, h.max_len,
+    const uint64_t v[19] = {h.n_valid, h.nseg, h.n_new, h.any_v6, h.nonmono, h.max_len,
                             h.max_ts, h.allowed, h.dropped, h.n_rule, h.pay_ok, h.n_light,
-                            c->last_evicted, h.hfast, h.n_admit, h.n_trans, t.n_hfast, t.n_hrun};
+                            c->last_evicted, h.hfast, h.n_admit, h.n_trans, t.n_hfast, t.n_hrun, h.ord};
     int k = 0;
-    for (; k < cap && k < 18; ++k) info[k] = v[k];
+    for (; k < cap && k < 19; ++k) info[k] = v[k];
     return k;
 }
 

@@ -477,7 +477,10 @@ __device__ __forceinline__ bool rule_drop(const RuleSet &R, uint32_t tag, const 
 #define FSX_PARSE_PAY 0
 #endif
 constexpr uint32_t kRecPitch = 13;   // LDS staging pitch of a record (12 dwords used; odd: conflict-free reads)
-template <uint32_t kRec, bool kRules, bool kMir, bool kHf>
+// kOrd (home-ordered inserts): no index probe at all — an IP packet's sort word
+// is its home-ordered key hash (ord_hkey) << kIdShift | arrival index, bit 63 set for IPv6; the
+// segment heads find / insert their slots after the sort (k_ord_resolve).
+template <uint32_t kRec, bool kRules, bool kMir, bool kHf, bool kOrd = false>
 #ifndef FSX_PARSE_MINB
 #define FSX_PARSE_MINB 4   // waves/SIMD bound of k_parse (A/B: scripts/build_variant.sh)
 #endif
@@ -506,6 +509,8 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
     //   else: no timestamp loads, the light-packet mask of every 64-packet step in lmask
     //   (k_pass0h<true> reads ts / len / verdicts for the records and the payloads)
     static_assert(!kHf || !kRules, "unsorted heavy sources: no prefix rules");
+    static_assert(!kOrd || (!kHf && !kMir && kRec == 0), "home-ordered inserts: header records, no heavy sources");
+    const uint32_t ord_s = kOrd ? (uint32_t)__popcll(idt.mask) : 0u;   // log2(slots)
     constexpr bool kHr = kHf && FSX_PARSE_PAY;   // (the payload words from the parse)
     __shared__ uint32_t s_rec[4][64 * kRecPitch];
     __shared__ uint32_t s_red[4][3];
@@ -762,10 +767,15 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
         // only after the head shows READY)
         c_hint0 = c_hint1 = 0;
         if constexpr (kMir) c_m = mir2_t{0, 0};
+        if constexpr (kOrd) {   // (no probe: the key hash, resolve_step writes the word)
+            c_tag = live ? tag : 0u;
+            c_h = ip ? ord_hkey(tag, k, h, idt.seed, ord_s) : 0u;
+            c_hidx = -1;
+        }
 #ifdef FSX_MEASURE_NO_PROBE
         if (false) {
 #else
-        if (tag == 1 && !(hres && hidx >= 0)) {
+        if (!kOrd && tag == 1 && !(hres && hidx >= 0)) {
 #endif
             // (coherent=1 reads past the XCD's L2, which may hold the head of an older
             // epoch: a stale head can only fail the match, never fake one)
@@ -782,10 +792,12 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
                 c_hint1 = idt.head[h1];
             }
         }
-        c_tag = live ? tag : 0u;
-        c_k0 = k[0];
-        c_h = (uint32_t)h;
-        c_hidx = hidx;
+        if constexpr (!kOrd) {
+            c_tag = live ? tag : 0u;
+            c_k0 = k[0];
+            c_h = (uint32_t)h;
+            c_hidx = hidx;
+        }
         if constexpr (kHr) {
             {   // the light packets' positions in the chunk (arrival order) and payload words
                 const bool lt = live && tag != 0 && hidx < 0;
@@ -818,6 +830,14 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
     // resolve step t ("cur"): heavy slot from LDS, the fast-path probe match, or defer
     auto resolve_step = [&](uint32_t t) {
         const uint32_t i = (t << 6) + lane;
+        if constexpr (kOrd) {
+            if (c_tag) {
+                const uint64_t out = ((uint64_t)c_h << kIdShift) | i | (c_tag == 2 ? kFreshBit : 0ull);
+                packed[i] = out;
+                count_digits(out, -1);
+            }
+            return;
+        }
         uint32_t id = kNoSlot;
         bool defer = false;
         if (c_tag) {
@@ -1628,11 +1648,14 @@ __global__ __launch_bounds__(256) void k_heads_count(const uint64_t *__restrict_
                                                      const uint8_t *__restrict__ hdr,
                                                      uint8_t *__restrict__ headf,
                                                      uint32_t *__restrict__ tile_cnt,
-                                                     uint32_t *__restrict__ sub_cnt, uint32_t light_only) {
+                                                     uint32_t *__restrict__ sub_cnt, uint32_t light_only,
+                                                     uint32_t ord = 0) {
     __shared__ uint32_t s_tmp[4];
     const uint32_t M = light_only ? bs->n_light : bs->n_valid;
     const uint32_t ntiles = (M + kTile - 1) / kTile;
     const uint32_t lane = lane_id();
+    // (ord: k_ord_fix marked the starts of the sources it separated inside a key-hash run)
+    const bool ofix = ord != 0;
     for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
         // coalesced: round k covers positions [t*kTile + 256k, +256), one per thread
         uint64_t cur[16];
@@ -1649,7 +1672,7 @@ __global__ __launch_bounds__(256) void k_heads_count(const uint64_t *__restrict_
             uint64_t prev = __shfl_up(cur[k], 1);
             if (lane == 0 && p > 0 && p < M) prev = S[p - 1];
             if (p < M) {
-                const bool h = p == 0 || ((prev ^ cur[k]) & ~kFreshBit) >> kIdShift != 0;
+                const bool h = p == 0 || ((prev ^ cur[k]) & ~kFreshBit) >> kIdShift != 0 || (ofix && headf[p]);
                 headf[p] = h ? 1u : 0u;
                 cnt += h;
                 sub[k >> 2] += h;
@@ -1770,6 +1793,209 @@ __global__ __launch_bounds__(256) void k_heads_heavy(BatchState *bs, const uint3
         bs->nseg = L + H;
         seg_start[L + H] = bs->n_valid;
     }
+}
+
+// ------------------------------------------------------------------ home-ordered inserts
+// (DESIGN.md §3 "Home-ordered inserts") A flood of new sources inserted as k_parse meets them
+// claims index heads at random: one 128-byte line read and written back per 8-byte head
+// (config 5: 25.8 of 52.6 ms per step). Instead k_parse writes the home-ordered key hash
+// (ord_hkey: the first probe slot in the top bits), the sort brings each source's packets
+// together in home order, and k_ord_resolve finds / inserts one slot per segment in that order:
+// consecutive heads claim neighbouring slots (the lines stay in L2). IPv4 keys are exact (a
+// bijection of the address); sources sharing an IPv6 (or mixed-family) key hash are separated
+// here: a run of equal hashes holding an IPv6 packet is regrouped stably by (family, address)
+// and every source after the first gets a head mark (k_heads_count ORs them in).
+constexpr uint32_t kOrdSmall = 8;     // runs up to this length: one thread
+constexpr uint32_t kOrdLong = 512;    // longer mixed runs: one wave with the keys in LDS
+
+__device__ __forceinline__ uint32_t ord_key_of(uint64_t w) { return (uint32_t)(w >> kIdShift); }
+
+// One thread per run start; runs of 2 .. kOrdSmall regrouped in registers, longer ones listed
+// (bs->n_ofix, positions in `list`) for k_ord_long.
+__global__ __launch_bounds__(256) void k_ord_fix(uint64_t *__restrict__ S, uint64_t *__restrict__ pay,
+                                                 BatchState *bs, PacketIn in, const uint32_t *__restrict__ len,
+                                                 uint8_t *__restrict__ headf, uint32_t *__restrict__ list) {
+    if (bs->err) return;
+    const uint32_t M = bs->n_valid;
+    for (uint32_t p = blockIdx.x * 256u + threadIdx.x; p < M; p += gridDim.x * 256u) {
+        const uint64_t w0 = S[p];
+        const uint32_t hk = ord_key_of(w0);
+        if (p > 0 && ord_key_of(S[p - 1]) == hk) continue;        // not a run start
+        if (p + 1 >= M || ord_key_of(S[p + 1]) != hk) continue;    // a run of one
+        uint64_t W[kOrdSmall], Pw[kOrdSmall];
+        uint32_t L = 0;
+        bool any6 = false, more = false;
+#pragma unroll
+        for (uint32_t j = 0; j < kOrdSmall; ++j) {
+            const uint64_t x = p + j < M ? S[p + j] : 0ull;
+            const bool in_run = p + j < M && ord_key_of(x) == hk && L == j;
+            W[j] = x;
+            L += in_run ? 1u : 0u;
+            any6 |= in_run && (x >> 63);
+        }
+        if (L == kOrdSmall && p + kOrdSmall < M && ord_key_of(S[p + kOrdSmall]) == hk) more = true;
+        if (more) {   // a long run: k_ord_long
+            list[atomicAdd(&bs->n_ofix, 1u)] = p;
+            continue;
+        }
+        if (!any6) continue;   // IPv4 only: equal hashes are equal addresses
+        uint32_t T[kOrdSmall], K[kOrdSmall][4];
+#pragma unroll
+        for (uint32_t j = 0; j < kOrdSmall; ++j) {
+            K[j][0] = K[j][1] = K[j][2] = K[j][3] = 0;
+            T[j] = j < L ? packet_src(in, len, pk_idx(W[j]), K[j]) : 0u;
+            Pw[j] = j < L ? pay[p + j] : 0ull;
+        }
+        // group leader of j: the first entry of its source; rank: stable order by leader
+        uint32_t G[kOrdSmall];
+#pragma unroll
+        for (uint32_t j = 0; j < kOrdSmall; ++j) {
+            G[j] = j;
+#pragma unroll
+            for (uint32_t m = 0; m < kOrdSmall; ++m)
+                if (m < j && G[j] == j && T[m] == T[j] && K[m][0] == K[j][0] && K[m][1] == K[j][1] &&
+                    K[m][2] == K[j][2] && K[m][3] == K[j][3])
+                    G[j] = m;
+        }
+        bool moved = false;
+        uint32_t R[kOrdSmall];
+#pragma unroll
+        for (uint32_t j = 0; j < kOrdSmall; ++j) {
+            uint32_t r = 0;
+#pragma unroll
+            for (uint32_t m = 0; m < kOrdSmall; ++m)
+                r += (m < L && (G[m] < G[j] || (G[m] == G[j] && m < j))) ? 1u : 0u;
+            R[j] = r;
+            moved |= j < L && r != j;
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < kOrdSmall; ++j) {
+            if (j >= L) continue;
+            if (moved) {
+                S[p + R[j]] = W[j];
+                pay[p + R[j]] = Pw[j];
+            }
+            if (G[j] == j && j > 0) headf[p + R[j]] = 1;   // a further source of the run
+        }
+    }
+}
+
+// One wave per listed run (longer than kOrdSmall): its length, then — if it holds an IPv6
+// packet — every packet's (family, address) in LDS, leaders, stable ranks; the words move through
+// the idle sort buffer (tmp / ptmp) at the same positions. More than kOrdLong packets with two
+// different sources: ERR_FIXUP (with the table's salted hash, a run that long holding two
+// sources does not occur by chance).
+__global__ __launch_bounds__(64) void k_ord_long(uint64_t *__restrict__ S, uint64_t *__restrict__ pay,
+                                                 BatchState *bs, PacketIn in, const uint32_t *__restrict__ len,
+                                                 uint8_t *__restrict__ headf, const uint32_t *__restrict__ list,
+                                                 uint64_t *__restrict__ tmp, uint64_t *__restrict__ ptmp) {
+    __shared__ uint32_t s_t[kOrdLong], s_k[kOrdLong][4], s_g[kOrdLong];
+    if (bs->err) return;
+    const uint32_t M = bs->n_valid, nl = bs->n_ofix, lane = lane_id();
+    for (uint32_t r = blockIdx.x; r < nl; r += gridDim.x) {
+        const uint32_t p = list[r];
+        const uint32_t hk = ord_key_of(S[p]);
+        uint32_t e = p;
+        bool any6 = false;
+        for (;;) {   // the run's end and whether it holds an IPv6 packet
+            const uint32_t q = e + lane;
+            const uint64_t x = q < M ? S[q] : 0ull;
+            const bool in_run = q < M && ord_key_of(x) == hk;
+            const uint64_t m = __ballot(in_run);
+            any6 |= __ballot(in_run && (x >> 63)) != 0;
+            if (~m) { e += (uint32_t)__ffsll((unsigned long long)~m) - 1u; break; }
+            e += 64;
+        }
+        if (!any6) continue;
+        const uint32_t L = e - p;
+        // the run's first source against every packet (a repeated source: nothing to move)
+        uint32_t k0[4];
+        const uint32_t t0 = packet_src(in, len, pk_idx(S[p]), k0);
+        bool same = true;
+        for (uint32_t j = lane; j < L; j += 64) {
+            uint32_t k[4];
+            const uint32_t t = packet_src(in, len, pk_idx(S[p + j]), k);
+            same &= t == t0 && k[0] == k0[0] && k[1] == k0[1] && k[2] == k0[2] && k[3] == k0[3];
+        }
+        if (__ballot(!same) == 0) continue;
+        if (L > kOrdLong) {
+            if (lane == 0) atomicOr(&bs->err, ERR_FIXUP);
+            return;
+        }
+        for (uint32_t j = lane; j < L; j += 64) s_t[j] = packet_src(in, len, pk_idx(S[p + j]), s_k[j]);
+        __syncthreads();
+        for (uint32_t j = lane; j < L; j += 64) {
+            uint32_t g = j;
+            for (uint32_t m = 0; m < j; ++m)
+                if (s_t[m] == s_t[j] && s_k[m][0] == s_k[j][0] && s_k[m][1] == s_k[j][1] &&
+                    s_k[m][2] == s_k[j][2] && s_k[m][3] == s_k[j][3]) { g = m; break; }
+            s_g[j] = g;
+        }
+        __syncthreads();
+        for (uint32_t j = lane; j < L; j += 64) {
+            const uint32_t gj = s_g[j];
+            uint32_t rk = 0;
+            for (uint32_t m = 0; m < L; ++m) rk += (s_g[m] < gj || (s_g[m] == gj && m < j)) ? 1u : 0u;
+            tmp[p + rk] = S[p + j];
+            ptmp[p + rk] = pay[p + j];
+            if (gj == j && j > 0) headf[p + rk] = 1;
+        }
+        __syncthreads();   // (global writes of this wave: ordered for its own later reads)
+        __threadfence_block();
+        for (uint32_t j = lane; j < L; j += 64) {
+            S[p + j] = tmp[p + j];
+            pay[p + j] = ptmp[p + j];
+        }
+        __syncthreads();
+    }
+}
+
+// One thread per segment, in home order: the source from its first word (IPv4: the inverse of
+// the key hash; IPv6: its record), its slot found or inserted from its home (id_resolve, lazy:
+// the head only), the slot into seg_slot and "inserted here" into the first word's bit 63
+// (kFreshBit, the walkers' flood path; bit 63 marked IPv6 until now). New sources counted.
+__global__ __launch_bounds__(256) void k_ord_resolve(BatchState *bs, const uint32_t *__restrict__ seg_start,
+                                                     uint64_t *__restrict__ S, PacketIn in,
+                                                     const uint32_t *__restrict__ len, IdTable idt,
+                                                     uint32_t *__restrict__ seg_slot) {
+    if (bs->err) return;
+    const uint32_t nseg = bs->nseg, lane = lane_id();
+    const uint32_t s = (uint32_t)__popcll(idt.mask);
+    if (blockIdx.x == 0 && threadIdx.x == 0) bs->ord = 1;
+    uint32_t nfresh = 0;
+    const uint32_t stride = gridDim.x * 256u;
+    for (uint32_t g0 = blockIdx.x * 256u; g0 < nseg; g0 += stride) {   // (wave-uniform trips)
+        const uint32_t g = g0 + threadIdx.x;
+        bool fresh = false;
+        if (g < nseg) {
+            const uint32_t a = seg_start[g];
+            const uint64_t w = S[a];
+            const uint32_t hk = ord_key_of(w);
+            uint32_t k[4] = {0, 0, 0, 0};
+            uint32_t tag = 1;
+            if (w >> 63) tag = packet_src(in, len, pk_idx(w), k);
+            else k[0] = ord_v4_key(hk, idt.seed, s);
+            const uint64_t home = hk >> (32 - s);
+            const uint64_t hint = idt.head[home];
+            const uint32_t id = id_resolve<true>(idt, tag, k, home, hint, &fresh);
+            if (id == kNoSlot) atomicOr(&bs->err, ERR_TABLE_FULL);
+            seg_slot[g] = id;
+            S[a] = (w & ~kFreshBit) | (fresh ? kFreshBit : 0ull);
+        }
+        nfresh += (uint32_t)__popcll(__ballot(fresh));
+    }
+    if (lane == 0 && nfresh) atomicAdd(&bs->n_new, nfresh);
+}
+
+hipError_t launch_ord_heads(uint64_t *S, uint64_t *pay, BatchState *bs, const PacketIn &in, const uint32_t *len,
+                            uint8_t *headf, uint32_t *list, uint64_t *tmp, uint64_t *ptmp, uint32_t n,
+                            hipStream_t st) {
+    hipError_t e;
+    if ((e = hipMemsetAsync(headf, 0, n, st)) != hipSuccess) return e;
+    const uint32_t grid = std::min<uint32_t>(4096, std::max<uint32_t>(1, (n + 255) / 256));
+    k_ord_fix<<<grid, 256, 0, st>>>(S, pay, bs, in, len, headf, list);
+    k_ord_long<<<1024, 64, 0, st>>>(S, pay, bs, in, len, headf, list, tmp, ptmp);
+    return hipGetLastError();
 }
 
 // ------------------------------------------------------------------ table lookup / insert
@@ -2788,7 +3014,13 @@ hipError_t launch_tail(const TailArgs &a) {
     }
     uint64_t *S = sc.packed[0];
     const uint32_t lo = tagh ? 1u : 0u;   // light-only heads
-    k_heads_count<<<gridTiles, 256, 0, st>>>(S, bs, in.hdr, sc.headf, sc.tile_aux, sc.sub_cnt, lo);
+    if (a.ord) {   // home-ordered inserts: sources sharing a key hash separated (the idle sort buffer as scratch)
+        if ((e = launch_ord_heads(S, sc.pay[0], bs, in, len, sc.headf, sc.seg_order, sc.packed[1], sc.pay[1], n,
+                                  st)) != hipSuccess)
+            return e;
+        mark("k_ord_fix");
+    }
+    k_heads_count<<<gridTiles, 256, 0, st>>>(S, bs, in.hdr, sc.headf, sc.tile_aux, sc.sub_cnt, lo, a.ord ? 1u : 0u);
     mark("k_heads_count");
     k_scan_tiles_u32<<<1, 256, 0, st>>>(sc.tile_aux, bs, sc.seg_start, lo);
     // (the first sort word's low half per segment only for the flow rows)
@@ -2800,6 +3032,16 @@ hipError_t launch_tail(const TailArgs &a) {
         k_heads_heavy<<<1, 256, 0, st>>>(bs, sc.sort_ctl, sc.gbase, sc.seg_start, do_limit ? sc.seg_slot : nullptr,
                                          S_fin, lim.table_mask, seg_lo, sc.heavy);
     mark("k_heads_write");
+    if (a.ord) {   // every segment's slot found / inserted in home order, then the table check
+        static const uint32_t coh = getenv("FSX_ID_COHERENT") ? 1u : 0u;
+        IdTable idt{a.X.heads, a.X.k6, lim.table_mask, lim.seed, a.X.epoch, lim.test_flags, table, a.id_gen, coh,
+                    a.X.mir, a.X.mir_shift};
+        idt.init = 0;   // (lazy slots: the walkers write a new source's line)
+        const uint32_t gr = std::min<uint32_t>(4096, std::max<uint32_t>(1, cdiv(n, 256)));
+        k_ord_resolve<<<gr, 256, 0, st>>>(bs, sc.seg_start, S, in, len, idt, sc.seg_slot);
+        k_batch_check<<<1, 1, 0, st>>>(bs, tstate, lim, nullptr, 0u);
+        mark("k_ord_resolve");
+    }
     if (a.admit) {   // FSX_FLAG_OVERFLOW_ADMIT: every segment's table slot (admitted / transient)
         const uint32_t ga = std::min<uint32_t>(2048, std::max<uint32_t>(1, cdiv(n, 256)));
         const uint32_t gt = std::min<uint32_t>(4096, std::max<uint32_t>(1, cdiv(n, kTile)));
@@ -2984,6 +3226,12 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
     // most 8 bits (21 bits: 3 x 7 — fewer buckets, longer runs per tile than 8 + 8 + 5)
     uint32_t idbits = 0;
     while ((1ull << idbits) <= idt.mask) ++idbits;
+    // home-ordered inserts (the host asks per batch: a flood of new sources; fixed window with
+    // lazy slots, header records, no flows): 32-bit key hashes sort in four 8-bit passes
+    static const bool eager_slots = getenv("FSX_EAGER_SLOTS") != nullptr;
+    const bool ord = lim.ord && do_limit && lim.limiter == 0 && !(lim.test_flags & kFlagAdmit) && !eager_slots &&
+                     !flows && !in.rec && idbits >= 1 && idbits <= 31;
+    if (ord) idbits = 32;
     int npass = std::max(1, (int)((idbits + 7) / 8));
     static const bool full_digits = getenv("FSX_SORT_FULL_DIGITS") != nullptr;   // A/B: 8,8,..,rest
     static const bool no_heavy = getenv("FSX_NO_HEAVY_SORT") != nullptr;          // A/B: plain LSD
@@ -3100,7 +3348,14 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
                                                         sc.sort_ctl, th, tcap, dp, hs, rules, tagh ? 1u : 0u, sc.chunk_cnt, lmask) \
                                  : k_parse<R, Q, false, H><<<g, 256, 0, st>>>(in, len, ts, n, sc.packed[0], verdict, bs, pidt, \
                                                         sc.sort_ctl, th, tcap, dp, hs, rules, tagh ? 1u : 0u, sc.chunk_cnt, lmask))
-        if (hfm)
+        if (ord)
+            rl ? k_parse<0, true, false, false, true><<<g, 256, 0, st>>>(in, len, ts, n, sc.packed[0], verdict, bs, pidt,
+                                                                        sc.sort_ctl, th, tcap, dp, hs, rules, 0u,
+                                                                        sc.chunk_cnt, lmask)
+               : k_parse<0, false, false, false, true><<<g, 256, 0, st>>>(in, len, ts, n, sc.packed[0], verdict, bs,
+                                                                         pidt, sc.sort_ctl, th, tcap, dp, hs, rules,
+                                                                         0u, sc.chunk_cnt, lmask);
+        else if (hfm)
             !in.rec ? FSX_PARSE(0, false, true) : in.rec_bytes == 16 ? FSX_PARSE(16, false, true) : FSX_PARSE(32, false, true);
         else if (!in.rec)
             rl ? FSX_PARSE(0, true, false) : FSX_PARSE(0, false, false);
@@ -3122,7 +3377,7 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
     static const bool no_fork = getenv("FSX_NO_FLOW_FORK") != nullptr;   // A/B: flows serialized
     if ((e = tail_hook(0)) != hipSuccess) return e;
     k_hist_prep<<<1, 256, 0, st>>>(sc.sort_ctl, sc.gbase, bs, heavy_sort ? dp.light_b : 256u);
-    if (do_limit)
+    if (do_limit && !ord)   // (home-ordered: after the slots are found, launch_tail)
         k_batch_check<<<1, 1, 0, st>>>(bs, tstate, lim, split ? split->prev : nullptr,
                                        split && split->tail && lim.limiter == 1 ? 1u : 0u);
     const uint32_t gen0 = onesweep ? next_generation() : 0u;
@@ -3183,6 +3438,7 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
     ta.npass = npass; ta.tagh = tagh; ta.gridTiles = gridTiles;
     ta.hfm = hfm; ta.shift0 = dp.shift[0];
     ta.admit = admit; ta.X = X; ta.id_gen = id_gen; ta.lazy = lazy; ta.fresh_bit = lazy && (!heavy_sort || hfm);
+    ta.ord = ord;
     ta.fork = flows && do_limit && st2 && fork_ev && join_ev && !no_fork;
     for (int k = 0; k < 3; ++k) ta.last[k] = last[k];
     if (split && split->tail_out) {

@@ -103,6 +103,8 @@ struct BatchState {
     uint32_t span_big;    // some sort tile spans >= 2^32 ns (u64 gap-square sums could wrap)
     uint32_t n_admit;     // FSX_FLAG_OVERFLOW_ADMIT: sources admitted / transient this batch
     uint32_t n_trans;
+    uint32_t n_ofix;      // home-ordered batches: key-hash runs longer than 8 (k_ord_long)
+    uint32_t ord;         // home-ordered inserts (Limits::ord) ran for this batch
 };
 
 // Sorted payload word carried through the onesweep passes next to each sort word:
@@ -173,10 +175,15 @@ struct Limits {           // the rate-limiter constants, src/fsx_kern.c:245,308-
     // FSX_FLAG_OVERFLOW_ADMIT: the batch's sources get ids in the per-batch id table (this
     // mask), their table slots come from the admission kernels
     uint64_t admit_mask;
+    // home-ordered inserts for this batch (DESIGN.md §3 "Home-ordered inserts"; set by the
+    // host per batch: a flood of new sources): k_parse writes a key-hash sort word, the
+    // segment heads find / insert their slots in home-slot order after the sort
+    uint32_t ord;
 };
 constexpr uint32_t kFlagAdmit = 8u;   // include/fsx_hip.h FSX_FLAG_OVERFLOW_ADMIT
 constexpr uint32_t kFlagSwUnsorted = 16u;   // include/fsx_hip.h FSX_FLAG_SW_UNSORTED
 constexpr uint32_t kFlagSwSparse = 32u;     // include/fsx_hip.h FSX_FLAG_TEST_SW_SPARSE
+constexpr uint32_t kFlagOrdered = 64u;      // include/fsx_hip.h FSX_FLAG_ORDERED_INSERTS
 
 // ------------------------------------------------------------ hashing
 __host__ __device__ inline uint64_t mix64(uint64_t x) {
@@ -266,6 +273,20 @@ __host__ __device__ inline uint64_t probe_start(uint32_t tag, const uint32_t k[4
     if (tag == 2 && (test_flags & 1u)) return v4_hash(0x0100000Au, seed) & mask;
     if (tag == 1) return v4_hash(k[0], seed) & mask;
     return slot_hash(tag, k, seed) & mask;
+}
+
+// Home-ordered sort key (DESIGN.md §3 "Home-ordered inserts"): the source's first probe slot
+// `home` (probe_start, s = log2(slots) bits, 1 <= s <= 31) in the top s bits, hash bits below.
+// IPv4: rotr(v4_hash, s) — a bijection of the address (ord_v4_key inverts it); IPv6: 32 bits
+// of its table hash (equal keys of different sources are separated by k_ord_fix).
+__host__ __device__ inline uint32_t ord_hkey(uint32_t tag, const uint32_t k[4], uint64_t home, uint64_t seed,
+                                             uint32_t s) {
+    const uint32_t h = tag == 1 ? v4_hash(k[0], seed) : (uint32_t)slot_hash(tag, k, seed);
+    return (uint32_t)(home << (32 - s)) | (h >> s);
+}
+__host__ __device__ inline uint32_t ord_v4_key(uint32_t hk, uint64_t seed, uint32_t s) {
+    const uint32_t h = (hk << s) | (hk >> (32 - s));   // v4_hash
+    return fmix32_inv(h) ^ (uint32_t)seed ^ (uint32_t)(seed >> 32);
 }
 
 // IPv4 mirror of the source index: one 2-byte entry per table slot, written
@@ -530,6 +551,7 @@ struct TailArgs {
     uint32_t id_gen;      // (admission: the batch generation stamped on admitted slots)
     bool lazy;            // k_parse left new sources' slots to the fixed window's walkers
     bool fresh_bit;       // ... and marked the inserting packets' sort words (kFreshBit)
+    bool ord;             // home-ordered inserts: key-hash words, slots found after the heads
     uint32_t shift0;      // pass 0's bucket shift (k_heavy_gather's sort words)
     FlowRequest fq;
     HistBufs hist;

@@ -51,6 +51,7 @@ FLAG_EVICT_IDLE = 4   # opt-in idle eviction on overflow
 FLAG_OVERFLOW_ADMIT = 8   # opt-in admission of a flood's new sources
 FLAG_SW_UNSORTED = 16     # A/B hook: the sliding window's heavy sources outside the sort
 FLAG_TEST_SW_SPARSE = 32  # test hook: sparse heavy sources on the sliding window's run path
+FLAG_ORDERED_INSERTS = 64  # home-ordered inserts on every fixed-window batch
 
 LIMIT_FIXED_WINDOW = 0
 LIMIT_SLIDING_WINDOW = 1
@@ -510,7 +511,7 @@ class FsxContext:
     BATCH_INFO = ("ip_packets", "sources", "new_sources", "any_ipv6", "non_monotone",
                   "max_len", "max_ts", "allowed", "dropped", "prefix_rule_drops", "sorted_payload",
                   "light_packets", "evicted", "heavy_unsorted", "admitted", "transient",
-                  "hfast_batches", "hrun_batches")
+                  "hfast_batches", "hrun_batches", "ordered_inserts")
 
     def last_batch_info(self) -> dict:
         buf = (C.c_uint64 * len(self.BATCH_INFO))()

@@ -94,6 +94,12 @@ extern "C" {
 /* Test hook (with FSX_FLAG_SW_UNSORTED): the heavy-source pick keeps the fixed window's
  * floor, so heavy sources too sparse for the rank walker reach its per-source run path. */
 #define FSX_FLAG_TEST_SW_SPARSE 32u
+/* Home-ordered inserts on every fixed-window batch (header records, no flows):
+ * k_parse writes each IP packet's home-ordered source hash instead of probing the index, and
+ * the segment heads find / insert their slots in home-slot order after the sort. Without the
+ * flag a batch takes them when the previous checked batch was a flood (new sources > half of
+ * its IP packets). Results are the same either way. */
+#define FSX_FLAG_ORDERED_INSERTS 64u
 
 /* Map ids: the five maps of src/fsx_kern.c:56-94, then the token-bucket state maps of
  * the build-defined token bucket (value fsx_tb_state), then the
@@ -434,7 +440,8 @@ int fsx_pcap_records_device(fsx_ctx *ctx, const uint8_t *d_buf, const uint64_t *
  * (FSX_FLAG_EVICT_IDLE), [13] 1 when the heavy sources' verdicts and flow rows were
  * computed outside the sort, 0 on the run path, [14] / [15] sources admitted
  * / transient (FSX_FLAG_OVERFLOW_ADMIT), [16] / [17] fixed-window batches since fsx_open
- * (not cleared by fsx_reset) whose heavy sources took the unsorted path / the run path.
+ * (not cleared by fsx_reset) whose heavy sources took the unsorted path / the run path,
+ * [18] 1 when the batch took the home-ordered inserts (FSX_FLAG_ORDERED_INSERTS).
  * Returns the number of entries written. */
 int fsx_last_batch_info(fsx_ctx *ctx, uint64_t *info, int cap);
 
