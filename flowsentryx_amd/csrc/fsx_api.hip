@@ -220,7 +220,8 @@ static int alloc_scratch(fsx_ctx *c, uint64_t cap) {
     HIPCHK(c, hipMalloc(&s.seg_slot, cap * 4));
     HIPCHK(c, hipMalloc(&s.seg_lo, (cap + 1) * 4));
     HIPCHK(c, hipMalloc(&s.seg_len, (cap + 1) * 4));
-    HIPCHK(c, hipMalloc(&s.hist, 256ull * std::max<uint64_t>(kSortMaxBlocks, cap / kSortTile + 2) * 4));
+    // (two regions of 256 rows: pass 0's and the light passes', launch_verdict_pipeline)
+    HIPCHK(c, hipMalloc(&s.hist, 256ull * std::max<uint64_t>(kSortMaxBlocks, 2 * (cap / kSortTile + 2)) * 4));
     HIPCHK(c, hipMalloc(&s.tile_aux, ntiles * 4));
     HIPCHK(c, hipMalloc(&s.tile_last, ntiles));
     // (s.id_tab, the per-batch id table of flow-only batches, is allocated on first use:
@@ -624,7 +625,7 @@ int fsx_set_pipeline(fsx_ctx *c, int on) {
                 if ((e = hipMalloc(&f.packed[b], cap * 8)) != hipSuccess) return e;
                 if ((e = hipMalloc(&f.pay[b], cap * 8)) != hipSuccess) return e;
             }
-            if ((e = hipMalloc(&f.hist, 256ull * std::max<uint64_t>(kSortMaxBlocks, cap / kSortTile + 2) * 4)) != hipSuccess) return e;
+            if ((e = hipMalloc(&f.hist, 256ull * std::max<uint64_t>(kSortMaxBlocks, 2 * (cap / kSortTile + 2)) * 4)) != hipSuccess) return e;
             if ((e = hipMalloc(&f.sort_ctl, kSortCtlWords * 4)) != hipSuccess) return e;
             if ((e = hipMalloc(&f.gbase, 1024 * 4)) != hipSuccess) return e;
             if ((e = hipMalloc(&f.heavy, sizeof(HeavySet))) != hipSuccess) return e;

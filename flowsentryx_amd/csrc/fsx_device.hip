@@ -3387,6 +3387,10 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
         const uint64_t *pin = pass == 0 ? nullptr : sc.pay[pass & 1];
         uint64_t *pout = sc.pay[(pass + 1) & 1];
         const uint32_t shift = dp.shift[pass], pmask = dp.mask[pass];
+        // the light passes' tile rows in a region of their own: pass 0's rows of the heavy
+        // buckets (light_b + h) are read in the tail (k_walk_heavy_sel, k_hflow_combine,
+        // k_heavy_gather) — an 8-bit light digit (tables of 2^22 / 2^23 slots) would overwrite them
+        uint32_t *hst = pass > 0 && heavy_sort ? sc.hist + 256ull * tcap : sc.hist;
         if (onesweep) {
             const uint32_t *Ld = pass == 0 ? nullptr : &bs->n_valid;
             k_onesweep<kLookW><<<ntiles, 256, 0, st>>>(in, out, n, Ld, shift, pmask, sc.gbase + 256 * pass,
@@ -3400,10 +3404,10 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
             // is odd, in packed[0] when it is even)
             const uint32_t *Ld = pass == 0 ? nullptr : &bs->n_light;
             if (pass > 0) {   // pass 0's per-tile counts come from k_parse
-                k_tile_hist<<<ntiles, 256, 0, st>>>(in, n, Ld, shift, pmask, pass == 0, sc.hist, tcap);
+                k_tile_hist<<<ntiles, 256, 0, st>>>(in, n, Ld, shift, pmask, pass == 0, hst, tcap);
                 mark("k_tile_hist");
             }
-            k_tile_scan<<<pmask + 1, 256, 0, st>>>(sc.hist, tcap, n, Ld, sc.gbase + 256 * pass);
+            k_tile_scan<<<pmask + 1, 256, 0, st>>>(hst, tcap, n, Ld, sc.gbase + 256 * pass);
             mark("k_tile_scan");
             if (pass == 0 && (e = tail_hook(1)) != hipSuccess) return e;
             if (pass == 0 && hfm) {   // light words from the parse chunks; heavy tile sums; the path
@@ -3415,7 +3419,7 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
                 if ((e = launch_hmode(bs, ts, n, lim, st)) != hipSuccess) return e;
                 mark("k_hmode");
             } else {
-                k_tile_scatter<kLatePayDefault><<<ntiles, 256, 0, st>>>(in, out, n, Ld, shift, pmask, pass == 0, sc.hist, tcap, bs,
+                k_tile_scatter<kLatePayDefault><<<ntiles, 256, 0, st>>>(in, out, n, Ld, shift, pmask, pass == 0, hst, tcap, bs,
                                                        pin, pout, ts, len);
                 mark("k_tile_scatter");
             }

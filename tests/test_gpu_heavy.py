@@ -84,13 +84,16 @@ def _config2(oracle, n, j0=0):
 CFG = dict(max_entries=1 << 20)   # a 2^21-slot table: the heavy-source sort with verdict lists
 
 
-def test_unsorted_heavy_path_config2_slices(native, oracle):
+@pytest.mark.parametrize("max_entries", [1 << 20, 1 << 21, 1 << 22])
+def test_unsorted_heavy_path_config2_slices(native, oracle, max_entries):
     """Two carried 1M-packet slices of the config-2 stream (heads blacklisted across the
-    cut): both batches on the unsorted path, everything equal to the oracle."""
+    cut): both batches on the unsorted path, everything equal to the oracle. Tables of 2^21,
+    2^22 and 2^23 slots: 7- and 8-bit light digits (an 8-bit light pass once overwrote the
+    heavy buckets' pass-0 tile rows the walker reads)."""
     hdr, ln, ts = _config2(oracle, 1 << 21)
     cut = 1 << 20
-    _run(native, oracle, [(hdr[:cut], ln[:cut], ts[:cut]), (hdr[cut:], ln[cut:], ts[cut:])], CFG,
-         want_path=[1, 1])
+    _run(native, oracle, [(hdr[:cut], ln[:cut], ts[:cut]), (hdr[cut:], ln[cut:], ts[cut:])],
+         dict(CFG, max_entries=max_entries), want_path=[1, 1])
 
 
 def test_unsorted_heavy_path_pipelined(native, oracle):

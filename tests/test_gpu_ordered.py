@@ -137,11 +137,11 @@ def test_ordered_table_full_rolls_back(native, oracle):
     from flowsentryx_amd import lib, synth
     rng = np.random.default_rng(61)
     cfg = dict(pps_threshold=5, window_ns=100_000, block_ns=300_000, max_entries=300)
-    h1, l1, t1 = rand_stream(rng, 3000, 120, dt_max=200, v6_frac=0.3)
+    h1, l1, t1 = rand_stream(rng, 3000, 60, dt_max=200, v6_frac=0.3)   # (<= 120 sources)
     t1 = t1 + np.uint64(10**6)
     big = synth.records([synth.frame_ipv4_udp(bytes([10, 77, i // 256, i % 256]), 90) for i in range(400)])
     tb = t1[-1] + np.arange(1, 401, dtype=np.uint64)
-    h3, l3, t3 = rand_stream(rng, 3000, 120, dt_max=200, v6_frac=0.3)
+    h3, l3, t3 = rand_stream(rng, 3000, 60, dt_max=200, v6_frac=0.3)
     t3 = t3 + tb[-1]
     okw = {k: v for k, v in cfg.items() if k != "max_entries"}
     o = oracle.Oracle(max_entries=1 << 12, **okw)
