@@ -1810,18 +1810,40 @@ constexpr uint32_t kOrdLong = 512;    // longer mixed runs: one wave with the ke
 
 __device__ __forceinline__ uint32_t ord_key_of(uint64_t w) { return (uint32_t)(w >> kIdShift); }
 
-// One thread per run start; runs of 2 .. kOrdSmall regrouped in registers, longer ones listed
+// The starts of the runs of two or more equal key hashes, listed (bs->n_orun; streaming, one
+// wave-aggregated append per wave and step).
+__global__ __launch_bounds__(256) void k_ord_scan(const uint64_t *__restrict__ S, BatchState *bs,
+                                                  uint32_t *__restrict__ runs) {
+    if (bs->err) return;
+    const uint32_t M = bs->n_valid, lane = lane_id();
+    for (uint32_t p0 = blockIdx.x * 256u; p0 < M; p0 += gridDim.x * 256u) {   // (wave-uniform trips)
+        const uint32_t p = p0 + threadIdx.x;
+        bool st = false;
+        if (p < M) {
+            const uint32_t hk = ord_key_of(S[p]);
+            st = (p == 0 || ord_key_of(S[p - 1]) != hk) && p + 1 < M && ord_key_of(S[p + 1]) == hk;
+        }
+        const uint64_t b = __ballot(st);
+        if (!b) continue;
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(&bs->n_orun, (uint32_t)__popcll(b));
+        base = __shfl(base, 0);
+        if (st) runs[base + (uint32_t)__popcll(b & ((1ull << lane) - 1ull))] = p;
+    }
+}
+
+// One thread per listed run; runs of 2 .. kOrdSmall regrouped in registers, longer ones listed
 // (bs->n_ofix, positions in `list`) for k_ord_long.
 __global__ __launch_bounds__(256) void k_ord_fix(uint64_t *__restrict__ S, uint64_t *__restrict__ pay,
                                                  BatchState *bs, PacketIn in, const uint32_t *__restrict__ len,
-                                                 uint8_t *__restrict__ headf, uint32_t *__restrict__ list) {
+                                                 uint8_t *__restrict__ headf, const uint32_t *__restrict__ runs,
+                                                 uint32_t *__restrict__ list) {
     if (bs->err) return;
-    const uint32_t M = bs->n_valid;
-    for (uint32_t p = blockIdx.x * 256u + threadIdx.x; p < M; p += gridDim.x * 256u) {
+    const uint32_t M = bs->n_valid, nr = bs->n_orun;
+    for (uint32_t r = blockIdx.x * 256u + threadIdx.x; r < nr; r += gridDim.x * 256u) {
+        const uint32_t p = runs[r];
         const uint64_t w0 = S[p];
         const uint32_t hk = ord_key_of(w0);
-        if (p > 0 && ord_key_of(S[p - 1]) == hk) continue;        // not a run start
-        if (p + 1 >= M || ord_key_of(S[p + 1]) != hk) continue;    // a run of one
         uint64_t W[kOrdSmall], Pw[kOrdSmall];
         uint32_t L = 0;
         bool any6 = false, more = false;
@@ -1963,9 +1985,15 @@ __global__ __launch_bounds__(256) void k_ord_resolve(BatchState *bs, const uint3
     const uint32_t s = (uint32_t)__popcll(idt.mask);
     if (blockIdx.x == 0 && threadIdx.x == 0) bs->ord = 1;
     uint32_t nfresh = 0;
-    const uint32_t stride = gridDim.x * 256u;
-    for (uint32_t g0 = blockIdx.x * 256u; g0 < nseg; g0 += stride) {   // (wave-uniform trips)
-        const uint32_t g = g0 + threadIdx.x;
+    // wave w takes 64 * kK consecutive segments, lane j its kK segments j * kK .. (in order):
+    // one instruction's 64 claims land in 64 different head lines (claims to one line are
+    // serialized at the L2), while each lane walks its own lines in order
+    constexpr uint32_t kK = 32;
+    const uint32_t wv = (blockIdx.x * 256u + threadIdx.x) >> 6, nwv = gridDim.x * 4u;
+    for (uint64_t g0 = (uint64_t)wv * 64u * kK; g0 < nseg; g0 += (uint64_t)nwv * 64u * kK)
+    for (uint32_t it = 0; it < kK; ++it) {   // (wave-uniform trips)
+        const uint64_t g64 = g0 + (uint64_t)lane * kK + it;
+        const uint32_t g = g64 < nseg ? (uint32_t)g64 : nseg;
         bool fresh = false;
         if (g < nseg) {
             const uint32_t a = seg_start[g];
@@ -1993,8 +2021,11 @@ hipError_t launch_ord_heads(uint64_t *S, uint64_t *pay, BatchState *bs, const Pa
     hipError_t e;
     if ((e = hipMemsetAsync(headf, 0, n, st)) != hipSuccess) return e;
     const uint32_t grid = std::min<uint32_t>(4096, std::max<uint32_t>(1, (n + 255) / 256));
-    k_ord_fix<<<grid, 256, 0, st>>>(S, pay, bs, in, len, headf, list);
-    k_ord_long<<<1024, 64, 0, st>>>(S, pay, bs, in, len, headf, list, tmp, ptmp);
+    // (list: the run starts in [0, n / 2) — a run holds two packets or more —, the long ones after)
+    uint32_t *runs = list, *longs = list + n / 2;
+    k_ord_scan<<<grid, 256, 0, st>>>(S, bs, runs);
+    k_ord_fix<<<grid, 256, 0, st>>>(S, pay, bs, in, len, headf, runs, longs);
+    k_ord_long<<<1024, 64, 0, st>>>(S, pay, bs, in, len, headf, longs, tmp, ptmp);
     return hipGetLastError();
 }
 

@@ -104,6 +104,7 @@ struct BatchState {
     uint32_t n_admit;     // FSX_FLAG_OVERFLOW_ADMIT: sources admitted / transient this batch
     uint32_t n_trans;
     uint32_t n_ofix;      // home-ordered batches: key-hash runs longer than 8 (k_ord_long)
+    uint32_t n_orun;      // ... key-hash runs of two or more packets (k_ord_scan)
     uint32_t ord;         // home-ordered inserts (Limits::ord) ran for this batch
 };
 
