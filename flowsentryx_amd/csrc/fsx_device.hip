@@ -1810,6 +1810,19 @@ constexpr uint32_t kOrdLong = 512;    // longer mixed runs: one wave with the ke
 
 __device__ __forceinline__ uint32_t ord_key_of(uint64_t w) { return (uint32_t)(w >> kIdShift); }
 
+// The source of a home-ordered sort word (bit 63: IPv6): IPv4 from the key hash itself (no
+// memory access), IPv6 from its record's address bytes.
+__device__ __forceinline__ uint32_t ord_src(uint64_t w, const uint8_t *hdr, uint64_t seed, uint32_t s,
+                                            uint32_t k[4]) {
+    if (w >> 63) {
+        load_key6(hdr, pk_idx(w), k);
+        return 2u;
+    }
+    k[0] = ord_v4_key(ord_key_of(w), seed, s);
+    k[1] = k[2] = k[3] = 0;
+    return 1u;
+}
+
 // The starts of the runs of two or more equal key hashes, listed (bs->n_orun; streaming, one
 // wave-aggregated append per wave and step).
 __global__ __launch_bounds__(256) void k_ord_scan(const uint64_t *__restrict__ S, BatchState *bs,
@@ -1837,7 +1850,7 @@ __global__ __launch_bounds__(256) void k_ord_scan(const uint64_t *__restrict__ S
 __global__ __launch_bounds__(256) void k_ord_fix(uint64_t *__restrict__ S, uint64_t *__restrict__ pay,
                                                  BatchState *bs, PacketIn in, const uint32_t *__restrict__ len,
                                                  uint8_t *__restrict__ headf, const uint32_t *__restrict__ runs,
-                                                 uint32_t *__restrict__ list) {
+                                                 uint32_t *__restrict__ list, uint64_t seed, uint32_t s) {
     if (bs->err) return;
     const uint32_t M = bs->n_valid, nr = bs->n_orun;
     for (uint32_t r = blockIdx.x * 256u + threadIdx.x; r < nr; r += gridDim.x * 256u) {
@@ -1865,7 +1878,7 @@ __global__ __launch_bounds__(256) void k_ord_fix(uint64_t *__restrict__ S, uint6
 #pragma unroll
         for (uint32_t j = 0; j < kOrdSmall; ++j) {
             K[j][0] = K[j][1] = K[j][2] = K[j][3] = 0;
-            T[j] = j < L ? packet_src(in, len, pk_idx(W[j]), K[j]) : 0u;
+            T[j] = j < L ? ord_src(W[j], in.hdr, seed, s, K[j]) : 0u;
             Pw[j] = j < L ? pay[p + j] : 0ull;
         }
         // group leader of j: the first entry of its source; rank: stable order by leader
@@ -1910,7 +1923,8 @@ __global__ __launch_bounds__(256) void k_ord_fix(uint64_t *__restrict__ S, uint6
 __global__ __launch_bounds__(64) void k_ord_long(uint64_t *__restrict__ S, uint64_t *__restrict__ pay,
                                                  BatchState *bs, PacketIn in, const uint32_t *__restrict__ len,
                                                  uint8_t *__restrict__ headf, const uint32_t *__restrict__ list,
-                                                 uint64_t *__restrict__ tmp, uint64_t *__restrict__ ptmp) {
+                                                 uint64_t *__restrict__ tmp, uint64_t *__restrict__ ptmp, uint64_t seed,
+                                                 uint32_t s) {
     __shared__ uint32_t s_t[kOrdLong], s_k[kOrdLong][4], s_g[kOrdLong];
     if (bs->err) return;
     const uint32_t M = bs->n_valid, nl = bs->n_ofix, lane = lane_id();
@@ -1932,11 +1946,11 @@ __global__ __launch_bounds__(64) void k_ord_long(uint64_t *__restrict__ S, uint6
         const uint32_t L = e - p;
         // the run's first source against every packet (a repeated source: nothing to move)
         uint32_t k0[4];
-        const uint32_t t0 = packet_src(in, len, pk_idx(S[p]), k0);
+        const uint32_t t0 = ord_src(S[p], in.hdr, seed, s, k0);
         bool same = true;
         for (uint32_t j = lane; j < L; j += 64) {
             uint32_t k[4];
-            const uint32_t t = packet_src(in, len, pk_idx(S[p + j]), k);
+            const uint32_t t = ord_src(S[p + j], in.hdr, seed, s, k);
             same &= t == t0 && k[0] == k0[0] && k[1] == k0[1] && k[2] == k0[2] && k[3] == k0[3];
         }
         if (__ballot(!same) == 0) continue;
@@ -1944,7 +1958,7 @@ __global__ __launch_bounds__(64) void k_ord_long(uint64_t *__restrict__ S, uint6
             if (lane == 0) atomicOr(&bs->err, ERR_FIXUP);
             return;
         }
-        for (uint32_t j = lane; j < L; j += 64) s_t[j] = packet_src(in, len, pk_idx(S[p + j]), s_k[j]);
+        for (uint32_t j = lane; j < L; j += 64) s_t[j] = ord_src(S[p + j], in.hdr, seed, s, s_k[j]);
         __syncthreads();
         for (uint32_t j = lane; j < L; j += 64) {
             uint32_t g = j;
@@ -1999,10 +2013,8 @@ __global__ __launch_bounds__(256) void k_ord_resolve(BatchState *bs, const uint3
             const uint32_t a = seg_start[g];
             const uint64_t w = S[a];
             const uint32_t hk = ord_key_of(w);
-            uint32_t k[4] = {0, 0, 0, 0};
-            uint32_t tag = 1;
-            if (w >> 63) tag = packet_src(in, len, pk_idx(w), k);
-            else k[0] = ord_v4_key(hk, idt.seed, s);
+            uint32_t k[4];
+            const uint32_t tag = ord_src(w, in.hdr, idt.seed, s, k);
             const uint64_t home = hk >> (32 - s);
             const uint64_t hint = idt.head[home];
             const uint32_t id = id_resolve<true>(idt, tag, k, home, hint, &fresh);
@@ -2017,15 +2029,16 @@ __global__ __launch_bounds__(256) void k_ord_resolve(BatchState *bs, const uint3
 
 hipError_t launch_ord_heads(uint64_t *S, uint64_t *pay, BatchState *bs, const PacketIn &in, const uint32_t *len,
                             uint8_t *headf, uint32_t *list, uint64_t *tmp, uint64_t *ptmp, uint32_t n,
-                            hipStream_t st) {
+                            uint64_t seed, uint64_t mask, hipStream_t st) {
+    const uint32_t s = (uint32_t)__builtin_popcountll(mask);
     hipError_t e;
     if ((e = hipMemsetAsync(headf, 0, n, st)) != hipSuccess) return e;
     const uint32_t grid = std::min<uint32_t>(4096, std::max<uint32_t>(1, (n + 255) / 256));
     // (list: the run starts in [0, n / 2) — a run holds two packets or more —, the long ones after)
     uint32_t *runs = list, *longs = list + n / 2;
     k_ord_scan<<<grid, 256, 0, st>>>(S, bs, runs);
-    k_ord_fix<<<grid, 256, 0, st>>>(S, pay, bs, in, len, headf, runs, longs);
-    k_ord_long<<<1024, 64, 0, st>>>(S, pay, bs, in, len, headf, longs, tmp, ptmp);
+    k_ord_fix<<<grid, 256, 0, st>>>(S, pay, bs, in, len, headf, runs, longs, seed, s);
+    k_ord_long<<<1024, 64, 0, st>>>(S, pay, bs, in, len, headf, longs, tmp, ptmp, seed, s);
     return hipGetLastError();
 }
 
@@ -3047,7 +3060,7 @@ hipError_t launch_tail(const TailArgs &a) {
     const uint32_t lo = tagh ? 1u : 0u;   // light-only heads
     if (a.ord) {   // home-ordered inserts: sources sharing a key hash separated (the idle sort buffer as scratch)
         if ((e = launch_ord_heads(S, sc.pay[0], bs, in, len, sc.headf, sc.seg_order, sc.packed[1], sc.pay[1], n,
-                                  st)) != hipSuccess)
+                                  lim.seed, lim.table_mask, st)) != hipSuccess)
             return e;
         mark("k_ord_fix");
     }
