@@ -1823,26 +1823,43 @@ __device__ __forceinline__ uint32_t ord_src(uint64_t w, const uint8_t *hdr, uint
     return 1u;
 }
 
-// The starts of the runs of two or more equal key hashes, listed (bs->n_orun; streaming, one
-// wave-aggregated append per wave and step).
+// Block-chunked list append: block b owns positions [b * chunk, (b + 1) * chunk); it counts
+// its flags, takes its range of the list with ONE atomic (a single counter hit once per wave
+// serialized at the L2: 26 ms for config 5), then writes the flagged positions in order.
+template <class F>
+__device__ __forceinline__ void chunk_append(uint32_t M, uint32_t *counter, uint32_t *out, uint32_t *s_tmp,
+                                             const F &flag) {
+    const uint32_t chunk = ((M + gridDim.x - 1) / gridDim.x + 255u) & ~255u;
+    const uint32_t c0 = blockIdx.x * chunk, c1 = min(M, c0 + chunk);
+    if (c0 >= c1) return;
+    uint32_t cnt = 0;
+    for (uint32_t p = c0 + threadIdx.x; p < c1; p += 256u) cnt += flag(p) ? 1u : 0u;
+    uint32_t tot;
+    block256_excl(cnt, s_tmp, &tot);
+    __shared__ uint32_t s_base;
+    if (threadIdx.x == 0) s_base = tot ? atomicAdd(counter, tot) : 0u;
+    __syncthreads();
+    uint32_t base = s_base;
+    for (uint32_t p0 = c0; p0 < c1; p0 += 256u) {
+        const uint32_t p = p0 + threadIdx.x;
+        const bool f = p < c1 && flag(p);
+        uint32_t stot;
+        const uint32_t off = block256_excl(f ? 1u : 0u, s_tmp, &stot);
+        if (f) out[base + off] = p;
+        base += stot;
+    }
+}
+
+// The starts of the runs of two or more equal key hashes, listed (bs->n_orun).
 __global__ __launch_bounds__(256) void k_ord_scan(const uint64_t *__restrict__ S, BatchState *bs,
                                                   uint32_t *__restrict__ runs) {
+    __shared__ uint32_t s_tmp[4];
     if (bs->err) return;
-    const uint32_t M = bs->n_valid, lane = lane_id();
-    for (uint32_t p0 = blockIdx.x * 256u; p0 < M; p0 += gridDim.x * 256u) {   // (wave-uniform trips)
-        const uint32_t p = p0 + threadIdx.x;
-        bool st = false;
-        if (p < M) {
-            const uint32_t hk = ord_key_of(S[p]);
-            st = (p == 0 || ord_key_of(S[p - 1]) != hk) && p + 1 < M && ord_key_of(S[p + 1]) == hk;
-        }
-        const uint64_t b = __ballot(st);
-        if (!b) continue;
-        uint32_t base = 0;
-        if (lane == 0) base = atomicAdd(&bs->n_orun, (uint32_t)__popcll(b));
-        base = __shfl(base, 0);
-        if (st) runs[base + (uint32_t)__popcll(b & ((1ull << lane) - 1ull))] = p;
-    }
+    const uint32_t M = bs->n_valid;
+    chunk_append(M, &bs->n_orun, runs, s_tmp, [&](uint32_t p) {
+        const uint32_t hk = ord_key_of(S[p]);
+        return (p == 0 || ord_key_of(S[p - 1]) != hk) && p + 1 < M && ord_key_of(S[p + 1]) == hk;
+    });
 }
 
 // One thread per listed run; runs of 2 .. kOrdSmall regrouped in registers, longer ones listed
@@ -1986,42 +2003,79 @@ __global__ __launch_bounds__(64) void k_ord_long(uint64_t *__restrict__ S, uint6
     }
 }
 
-// One thread per segment, in home order: the source from its first word (IPv4: the inverse of
-// the key hash; IPv6: its record), its slot found or inserted from its home (id_resolve, lazy:
-// the head only), the slot into seg_slot and "inserted here" into the first word's bit 63
-// (kFreshBit, the walkers' flood path; bit 63 marked IPv6 until now). New sources counted.
-__global__ __launch_bounds__(256) void k_ord_resolve(BatchState *bs, const uint32_t *__restrict__ seg_start,
-                                                     uint64_t *__restrict__ S, PacketIn in,
-                                                     const uint32_t *__restrict__ len, IdTable idt,
-                                                     uint32_t *__restrict__ seg_slot) {
+// One thread per segment, in home order: the source from its first word, its slot found or
+// inserted from its home (id_resolve, lazy: the head only), the slot into seg_slot and
+// "inserted here" into the first word's bit 63 (kFreshBit, the walkers' flood path; bit 63
+// marked IPv6 until now). New sources counted. Block b owns a contiguous chunk of segments;
+// k_ord_resolve4 takes the IPv4 ones (the key from the hash: no memory access before the
+// claim) and leaves the chunk's IPv6 ones in order at the chunk's own positions of `list6`
+// (their count in cnt6[b]), so that k_ord_resolve6 — the same blocks — runs them densely,
+// without IPv4 lanes waiting on their record reads and key publication.
+__device__ __forceinline__ void ord_chunk(uint32_t nseg, uint32_t &c0, uint32_t &c1) {
+    const uint32_t chunk = ((nseg + gridDim.x - 1) / gridDim.x + 255u) & ~255u;
+    c0 = min(nseg, blockIdx.x * chunk);
+    c1 = min(nseg, c0 + chunk);
+}
+
+__device__ __forceinline__ bool ord_claim(const IdTable &idt, uint32_t s, uint32_t g, uint64_t *S,
+                                          const uint32_t *seg_start, uint32_t *seg_slot, const uint8_t *hdr,
+                                          BatchState *bs) {
+    const uint32_t a = seg_start[g];
+    const uint64_t w = S[a];
+    uint32_t k[4];
+    const uint32_t tag = ord_src(w, hdr, idt.seed, s, k);
+    const uint64_t home = ord_key_of(w) >> (32 - s);
+    bool fresh = false;
+    const uint32_t id = id_resolve<true>(idt, tag, k, home, idt.head[home], &fresh);
+    if (id == kNoSlot) atomicOr(&bs->err, ERR_TABLE_FULL);
+    seg_slot[g] = id;
+    S[a] = (w & ~kFreshBit) | (fresh ? kFreshBit : 0ull);
+    return fresh;
+}
+
+__global__ __launch_bounds__(256) void k_ord_resolve4(BatchState *bs, const uint32_t *__restrict__ seg_start,
+                                                      uint64_t *__restrict__ S, PacketIn in, IdTable idt,
+                                                      uint32_t *__restrict__ seg_slot, uint32_t *__restrict__ list6,
+                                                      uint32_t *__restrict__ cnt6) {
+    __shared__ uint32_t s_tmp[4];
     if (bs->err) return;
-    const uint32_t nseg = bs->nseg, lane = lane_id();
-    const uint32_t s = (uint32_t)__popcll(idt.mask);
+    const uint32_t s = (uint32_t)__popcll(idt.mask), lane = lane_id();
     if (blockIdx.x == 0 && threadIdx.x == 0) bs->ord = 1;
-    uint32_t nfresh = 0;
-    // wave w takes 64 * kK consecutive segments, lane j its kK segments j * kK .. (in order):
-    // one instruction's 64 claims land in 64 different head lines (claims to one line are
-    // serialized at the L2), while each lane walks its own lines in order
-    constexpr uint32_t kK = 32;
-    const uint32_t wv = (blockIdx.x * 256u + threadIdx.x) >> 6, nwv = gridDim.x * 4u;
-    for (uint64_t g0 = (uint64_t)wv * 64u * kK; g0 < nseg; g0 += (uint64_t)nwv * 64u * kK)
-    for (uint32_t it = 0; it < kK; ++it) {   // (wave-uniform trips)
-        const uint64_t g64 = g0 + (uint64_t)lane * kK + it;
-        const uint32_t g = g64 < nseg ? (uint32_t)g64 : nseg;
-        bool fresh = false;
-        if (g < nseg) {
-            const uint32_t a = seg_start[g];
-            const uint64_t w = S[a];
-            const uint32_t hk = ord_key_of(w);
-            uint32_t k[4];
-            const uint32_t tag = ord_src(w, in.hdr, idt.seed, s, k);
-            const uint64_t home = hk >> (32 - s);
-            const uint64_t hint = idt.head[home];
-            const uint32_t id = id_resolve<true>(idt, tag, k, home, hint, &fresh);
-            if (id == kNoSlot) atomicOr(&bs->err, ERR_TABLE_FULL);
-            seg_slot[g] = id;
-            S[a] = (w & ~kFreshBit) | (fresh ? kFreshBit : 0ull);
+    uint32_t c0, c1;
+    ord_chunk(bs->nseg, c0, c1);
+    uint32_t nfresh = 0, n6 = 0;
+    for (uint32_t g0 = c0; g0 < c1; g0 += 256u) {   // (block-uniform trips)
+        const uint32_t g = g0 + threadIdx.x;
+        bool fresh = false, six = false;
+        if (g < c1) {
+            six = (S[seg_start[g]] >> 63) != 0;
+            if (!six) fresh = ord_claim(idt, s, g, S, seg_start, seg_slot, in.hdr, bs);
         }
+        nfresh += (uint32_t)__popcll(__ballot(fresh));
+        uint32_t t6;
+        const uint32_t off = block256_excl(six ? 1u : 0u, s_tmp, &t6);
+        if (six) list6[c0 + n6 + off] = g;
+        n6 += t6;
+    }
+    if (threadIdx.x == 0) cnt6[blockIdx.x] = n6;
+    if (lane == 0 && nfresh) atomicAdd(&bs->n_new, nfresh);
+}
+
+__global__ __launch_bounds__(256) void k_ord_resolve6(BatchState *bs, const uint32_t *__restrict__ seg_start,
+                                                      uint64_t *__restrict__ S, PacketIn in, IdTable idt,
+                                                      uint32_t *__restrict__ seg_slot,
+                                                      const uint32_t *__restrict__ list6,
+                                                      const uint32_t *__restrict__ cnt6) {
+    if (bs->err) return;
+    const uint32_t s = (uint32_t)__popcll(idt.mask), lane = lane_id();
+    uint32_t c0, c1;
+    ord_chunk(bs->nseg, c0, c1);
+    const uint32_t m = c0 < c1 ? cnt6[blockIdx.x] : 0u;
+    uint32_t nfresh = 0;
+    for (uint32_t j0 = 0; j0 < m; j0 += 256u) {   // (block-uniform trips)
+        const uint32_t j = j0 + threadIdx.x;
+        bool fresh = false;
+        if (j < m) fresh = ord_claim(idt, s, list6[c0 + j], S, seg_start, seg_slot, in.hdr, bs);
         nfresh += (uint32_t)__popcll(__ballot(fresh));
     }
     if (lane == 0 && nfresh) atomicAdd(&bs->n_new, nfresh);
@@ -3081,8 +3135,11 @@ hipError_t launch_tail(const TailArgs &a) {
         IdTable idt{a.X.heads, a.X.k6, lim.table_mask, lim.seed, a.X.epoch, lim.test_flags, table, a.id_gen, coh,
                     a.X.mir, a.X.mir_shift};
         idt.init = 0;   // (lazy slots: the walkers write a new source's line)
+        // (the segment-order buffer holds the IPv6 lists, pass 0's tile rows — unused without
+        // the heavy sort — their per-block counts)
         const uint32_t gr = std::min<uint32_t>(4096, std::max<uint32_t>(1, cdiv(n, 256)));
-        k_ord_resolve<<<gr, 256, 0, st>>>(bs, sc.seg_start, S, in, len, idt, sc.seg_slot);
+        k_ord_resolve4<<<gr, 256, 0, st>>>(bs, sc.seg_start, S, in, idt, sc.seg_slot, sc.seg_order, sc.hist);
+        k_ord_resolve6<<<gr, 256, 0, st>>>(bs, sc.seg_start, S, in, idt, sc.seg_slot, sc.seg_order, sc.hist);
         k_batch_check<<<1, 1, 0, st>>>(bs, tstate, lim, nullptr, 0u);
         mark("k_ord_resolve");
     }
