@@ -2033,6 +2033,19 @@ __device__ __forceinline__ bool ord_claim(const IdTable &idt, uint32_t s, uint32
     return fresh;
 }
 
+// kOrdU segments per thread and step, their loads and first-probe claims in flight together:
+// a head whose first probe slot is empty in this epoch is claimed by one CAS issued beside the
+// others; a READY head with the source's key is found; anything else (a lost race, a longer
+// probe chain, an IPv6 key to compare) takes id_resolve's full protocol from there.
+constexpr uint32_t kOrdU = 4;
+
+__device__ __forceinline__ void ord_finish(const IdTable &idt, uint32_t g, uint32_t a, uint64_t w, uint32_t id,
+                                           bool fresh, uint64_t *S, uint32_t *seg_slot, BatchState *bs) {
+    if (id == kNoSlot) atomicOr(&bs->err, ERR_TABLE_FULL);
+    seg_slot[g] = id;
+    S[a] = (w & ~kFreshBit) | (fresh ? kFreshBit : 0ull);
+}
+
 __global__ __launch_bounds__(256) void k_ord_resolve4(BatchState *bs, const uint32_t *__restrict__ seg_start,
                                                       uint64_t *__restrict__ S, PacketIn in, IdTable idt,
                                                       uint32_t *__restrict__ seg_slot, uint32_t *__restrict__ list6,
@@ -2044,23 +2057,71 @@ __global__ __launch_bounds__(256) void k_ord_resolve4(BatchState *bs, const uint
     uint32_t c0, c1;
     ord_chunk(bs->nseg, c0, c1);
     uint32_t nfresh = 0, n6 = 0;
-    for (uint32_t g0 = c0; g0 < c1; g0 += 256u) {   // (block-uniform trips)
-        const uint32_t g = g0 + threadIdx.x;
-        bool fresh = false, six = false;
-        if (g < c1) {
-            six = (S[seg_start[g]] >> 63) != 0;
-            if (!six) fresh = ord_claim(idt, s, g, S, seg_start, seg_slot, in.hdr, bs);
+    for (uint32_t g0 = c0; g0 < c1; g0 += 256u * kOrdU) {   // (block-uniform trips)
+        uint32_t a[kOrdU], k0[kOrdU];
+        uint64_t w[kOrdU], home[kOrdU], hint[kOrdU], prev[kOrdU];
+        bool v4[kOrdU], six[kOrdU];
+#pragma unroll
+        for (uint32_t u = 0; u < kOrdU; ++u) {
+            const uint32_t g = g0 + u * 256u + threadIdx.x;
+            a[u] = g < c1 ? seg_start[g] : 0u;
         }
-        nfresh += (uint32_t)__popcll(__ballot(fresh));
-        uint32_t t6;
-        const uint32_t off = block256_excl(six ? 1u : 0u, s_tmp, &t6);
-        if (six) list6[c0 + n6 + off] = g;
-        n6 += t6;
+#pragma unroll
+        for (uint32_t u = 0; u < kOrdU; ++u) {
+            const uint32_t g = g0 + u * 256u + threadIdx.x;
+            w[u] = g < c1 ? S[a[u]] : 0ull;
+            six[u] = g < c1 && (w[u] >> 63);
+            v4[u] = g < c1 && !six[u];
+            k0[u] = ord_v4_key(ord_key_of(w[u]), idt.seed, s);
+            home[u] = ord_key_of(w[u]) >> (32 - s);
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < kOrdU; ++u) hint[u] = v4[u] ? idt.head[home[u]] : 0ull;
+        const uint64_t want_hi = id_head(idt.gen, kIdReady, 1u, 0u);
+#pragma unroll
+        for (uint32_t u = 0; u < kOrdU; ++u) {   // first-slot claims, all in flight
+            const bool empty = v4[u] && (uint32_t)(hint[u] >> 48) != idt.gen;
+            prev[u] = empty ? atomicCAS(idt.head + home[u], (unsigned long long)hint[u],
+                                        (unsigned long long)(want_hi | k0[u]))
+                            : hint[u];
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < kOrdU; ++u) {
+            bool fresh = false;
+            if (v4[u]) {
+                const uint32_t g = g0 + u * 256u + threadIdx.x;
+                const uint64_t want = want_hi | k0[u];
+                const bool empty = (uint32_t)(hint[u] >> 48) != idt.gen;
+                uint32_t id;
+                if (empty && prev[u] == hint[u]) {   // claimed here
+                    fresh = true;
+                    id = (uint32_t)home[u];
+                    mir_publish(idt.mir, idt.mir_shift, idt.mask, idt.seed, home[u], k0[u]);
+                } else if (prev[u] == want) {          // found (or another lane claimed it for us: never —
+                    id = (uint32_t)home[u];            // one segment per source)
+                } else {
+                    const uint32_t kk[4] = {k0[u], 0u, 0u, 0u};
+                    id = id_resolve<true>(idt, 1u, kk, home[u], prev[u], &fresh);
+                }
+                ord_finish(idt, g, a[u], w[u], id, fresh, S, seg_slot, bs);
+            }
+            nfresh += (uint32_t)__popcll(__ballot(fresh));
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < kOrdU; ++u) {   // the IPv6 segments, listed in order
+            uint32_t t6;
+            const uint32_t off = block256_excl(six[u] ? 1u : 0u, s_tmp, &t6);
+            if (six[u]) list6[c0 + n6 + off] = g0 + u * 256u + threadIdx.x;
+            n6 += t6;
+        }
     }
     if (threadIdx.x == 0) cnt6[blockIdx.x] = n6;
     if (lane == 0 && nfresh) atomicAdd(&bs->n_new, nfresh);
 }
 
+// The chunk's IPv6 segments, kOrdU per thread: records and first-slot heads loaded together,
+// an empty first slot claimed BUSY (CAS), the three key words published by returning
+// exchanges for all claims at once, then READY (id_resolve's protocol); the rest by id_resolve.
 __global__ __launch_bounds__(256) void k_ord_resolve6(BatchState *bs, const uint32_t *__restrict__ seg_start,
                                                       uint64_t *__restrict__ S, PacketIn in, IdTable idt,
                                                       uint32_t *__restrict__ seg_slot,
@@ -2072,11 +2133,71 @@ __global__ __launch_bounds__(256) void k_ord_resolve6(BatchState *bs, const uint
     ord_chunk(bs->nseg, c0, c1);
     const uint32_t m = c0 < c1 ? cnt6[blockIdx.x] : 0u;
     uint32_t nfresh = 0;
-    for (uint32_t j0 = 0; j0 < m; j0 += 256u) {   // (block-uniform trips)
-        const uint32_t j = j0 + threadIdx.x;
-        bool fresh = false;
-        if (j < m) fresh = ord_claim(idt, s, list6[c0 + j], S, seg_start, seg_slot, in.hdr, bs);
-        nfresh += (uint32_t)__popcll(__ballot(fresh));
+    const uint64_t busy_hi = id_head(idt.gen, kIdBusy, 2u, 0u), ready_hi = id_head(idt.gen, kIdReady, 2u, 0u);
+    for (uint32_t j0 = 0; j0 < m; j0 += 256u * kOrdU) {   // (block-uniform trips)
+        uint32_t g[kOrdU], a[kOrdU], k[kOrdU][4];
+        uint64_t w[kOrdU], home[kOrdU], hint[kOrdU], prev[kOrdU];
+        bool live[kOrdU], claimed[kOrdU];
+#pragma unroll
+        for (uint32_t u = 0; u < kOrdU; ++u) {
+            const uint32_t j = j0 + u * 256u + threadIdx.x;
+            live[u] = j < m;
+            g[u] = live[u] ? list6[c0 + j] : c0;
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < kOrdU; ++u) a[u] = live[u] ? seg_start[g[u]] : 0u;
+#pragma unroll
+        for (uint32_t u = 0; u < kOrdU; ++u) {
+            w[u] = live[u] ? S[a[u]] : 0ull;
+            home[u] = ord_key_of(w[u]) >> (32 - s);
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < kOrdU; ++u) {
+            if (live[u]) load_key6(in.hdr, pk_idx(w[u]), k[u]);
+            else k[u][0] = k[u][1] = k[u][2] = k[u][3] = 0;
+            hint[u] = live[u] ? idt.head[home[u]] : 0ull;
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < kOrdU; ++u) {
+            const bool empty = live[u] && (uint32_t)(hint[u] >> 48) != idt.gen;
+            prev[u] = empty ? atomicCAS(idt.head + home[u], (unsigned long long)hint[u],
+                                        (unsigned long long)(busy_hi | k[u][0]))
+                            : hint[u];
+            claimed[u] = empty && prev[u] == hint[u];
+        }
+        uint32_t r[kOrdU][3];
+#pragma unroll
+        for (uint32_t u = 0; u < kOrdU; ++u) {   // the claimed heads' key words, all in flight
+            if (claimed[u]) {
+                uint32_t *kw = idt.k6 + home[u] * 4;
+                r[u][0] = __hip_atomic_exchange(kw + 0, k[u][1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                r[u][1] = __hip_atomic_exchange(kw + 1, k[u][2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                r[u][2] = __hip_atomic_exchange(kw + 2, k[u][3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else {
+                r[u][0] = r[u][1] = r[u][2] = 0;
+            }
+        }
+        // every claim of this wave READY (after its key words returned) before any lane of it
+        // may wait on a BUSY head in id_resolve
+#pragma unroll
+        for (uint32_t u = 0; u < kOrdU; ++u) {
+            if (claimed[u]) {
+                asm volatile("" ::"v"(r[u][0]), "v"(r[u][1]), "v"(r[u][2]) : "memory");
+                __hip_atomic_store(idt.head + home[u], (unsigned long long)(ready_hi | k[u][0]), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+                ord_finish(idt, g[u], a[u], w[u], (uint32_t)home[u], true, S, seg_slot, bs);
+            }
+            nfresh += (uint32_t)__popcll(__ballot(claimed[u]));
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < kOrdU; ++u) {
+            bool fresh = false;
+            if (live[u] && !claimed[u]) {
+                const uint32_t id = id_resolve<true>(idt, 2u, k[u], home[u], prev[u], &fresh);
+                ord_finish(idt, g[u], a[u], w[u], id, fresh, S, seg_slot, bs);
+            }
+            nfresh += (uint32_t)__popcll(__ballot(fresh));
+        }
     }
     if (lane == 0 && nfresh) atomicAdd(&bs->n_new, nfresh);
 }
