@@ -2202,6 +2202,130 @@ __global__ __launch_bounds__(256) void k_ord_resolve6(BatchState *bs, const uint
     if (lane == 0 && nfresh) atomicAdd(&bs->n_new, nfresh);
 }
 
+// Region claims (the ordered path's default): block b takes kRegSeg consecutive segments
+// and, exclusively, the heads from its first segment's home to the next block's first home
+// (at most kRegMax of them): they are loaded into LDS, every segment probes / claims there
+// (LDS CAS; a slot claimed in this block is another source — one segment per source — so no
+// key comparison against it), and the block's claims go back to HBM as plain stores (heads,
+// IPv6 key words, IPv4 mirror entries): no global atomic for a flood's inserts, which the
+// device processes at ~30 G/s (k_ord_resolve4 / 6: 18 ms for config 5's 2^28). A probe that
+// leaves the region is spilled to k_ord_spill (the global protocol, after this kernel).
+constexpr uint32_t kRegSeg = 1024, kRegMax = 4096;
+constexpr uint64_t kIdLocal = 3;   // head state in LDS: claimed by this block
+
+__global__ __launch_bounds__(256) void k_ord_claim(BatchState *bs, const uint32_t *__restrict__ seg_start,
+                                                   uint64_t *__restrict__ S, PacketIn in, IdTable idt,
+                                                   uint32_t *__restrict__ seg_slot, uint32_t *__restrict__ spill,
+                                                   uint32_t *__restrict__ nspill, uint32_t *__restrict__ nfresh_b) {
+    __shared__ unsigned long long H[kRegMax];
+    __shared__ uint32_t s_nsp, s_fresh;
+    __shared__ uint64_t s_r[2];
+    if (bs->err) return;
+    const uint32_t nseg = bs->nseg, b = blockIdx.x, tid = threadIdx.x;
+    const uint32_t c0 = b * kRegSeg;
+    if (c0 >= nseg) {
+        if (tid == 0) { nspill[b] = 0; nfresh_b[b] = 0; }
+        return;
+    }
+    const uint32_t c1 = min(nseg, c0 + kRegSeg);
+    const uint32_t s = (uint32_t)__popcll(idt.mask), gen = idt.gen;
+    if (tid == 0) {
+        s_r[0] = ord_key_of(S[seg_start[c0]]) >> (32 - s);
+        s_r[1] = c1 < nseg ? ord_key_of(S[seg_start[c1]]) >> (32 - s) : idt.mask + 1;
+        s_nsp = 0;
+        s_fresh = 0;
+    }
+    __syncthreads();
+    const uint64_t R0 = s_r[0];
+    const uint32_t Rn = (uint32_t)min<uint64_t>(s_r[1] - R0, kRegMax);
+    for (uint32_t r = tid; r < Rn; r += 256u) H[r] = idt.head[R0 + r];
+    __syncthreads();
+    uint32_t nfr = 0;
+    for (uint32_t j = tid; j < c1 - c0; j += 256u) {
+        const uint32_t g = c0 + j, a = seg_start[g];
+        const uint64_t w = S[a];
+        uint32_t k[4];
+        const uint32_t tag = ord_src(w, in.hdr, idt.seed, s, k);
+        uint32_t r = (uint32_t)((ord_key_of(w) >> (32 - s)) - R0);
+        const uint64_t mine = id_head(gen, kIdLocal, tag, tag == 1 ? k[0] : j);
+        int res = 0;   // 1 claimed, 2 found, 3 spilled
+        while (!res) {
+            if (r >= Rn) { res = 3; break; }
+            const unsigned long long cur = H[r];
+            if ((uint32_t)(cur >> 48) != gen) {   // empty in this epoch: claim it in LDS
+                if (atomicCAS(&H[r], cur, (unsigned long long)mine) == cur) res = 1;
+                continue;
+            }
+            const uint32_t st = (uint32_t)(cur >> 40) & 0xFFu, ct = (uint32_t)(cur >> 32) & 0xFFu;
+            if (st == kIdReady && ct == tag && (uint32_t)cur == k[0]) {   // a source of the index
+                if (tag == 1) { res = 2; break; }
+                const uint32_t *kw = idt.k6 + (R0 + r) * 4;
+                if (kw[0] == k[1] && kw[1] == k[2] && kw[2] == k[3]) { res = 2; break; }
+            } else if (st != kIdReady && st != kIdLocal) {   // (no BUSY head outside a claim)
+                res = 3;
+                break;
+            }
+            ++r;
+        }
+        if (res == 3) {
+            spill[c0 + atomicAdd(&s_nsp, 1u)] = g;
+        } else {
+            seg_slot[g] = (uint32_t)(R0 + r);
+            S[a] = (w & ~kFreshBit) | (res == 1 ? kFreshBit : 0ull);
+            nfr += res == 1 ? 1u : 0u;
+        }
+    }
+    if (nfr) atomicAdd(&s_fresh, nfr);
+    __syncthreads();
+    // the block's claims to HBM: heads READY, IPv6 key words, IPv4 mirror entries
+    for (uint32_t r = tid; r < Rn; r += 256u) {
+        const unsigned long long cur = H[r];
+        if ((uint32_t)(cur >> 48) != gen || ((cur >> 40) & 0xFFu) != kIdLocal) continue;
+        const uint32_t ct = (uint32_t)(cur >> 32) & 0xFFu;
+        const uint64_t pos = R0 + r;
+        uint32_t k0 = (uint32_t)cur;
+        if (ct == 2) {
+            uint32_t k[4];
+            load_key6(in.hdr, pk_idx(S[seg_start[c0 + (uint32_t)cur]]), k);
+            k0 = k[0];
+            uint32_t *kw = idt.k6 + pos * 4;
+            kw[0] = k[1]; kw[1] = k[2]; kw[2] = k[3];
+        } else {
+            mir_publish(idt.mir, idt.mir_shift, idt.mask, idt.seed, pos, k0);
+        }
+        idt.head[pos] = id_head(gen, kIdReady, ct, k0);
+    }
+    if (tid == 0) { nspill[b] = s_nsp; nfresh_b[b] = s_fresh; }
+}
+
+// The segments k_ord_claim spilled (their probe left the block's region): the global protocol.
+__global__ __launch_bounds__(256) void k_ord_spill(BatchState *bs, const uint32_t *__restrict__ seg_start,
+                                                   uint64_t *__restrict__ S, PacketIn in, IdTable idt,
+                                                   uint32_t *__restrict__ seg_slot, const uint32_t *__restrict__ spill,
+                                                   const uint32_t *__restrict__ nspill, uint32_t *__restrict__ nfresh_b) {
+    if (bs->err) return;
+    const uint32_t b = blockIdx.x, c0 = b * kRegSeg;
+    if (c0 >= bs->nseg) return;
+    const uint32_t m = nspill[b], s = (uint32_t)__popcll(idt.mask);
+    uint32_t nfr = 0;
+    for (uint32_t j = threadIdx.x; j < m; j += 256u)
+        nfr += ord_claim(idt, s, spill[c0 + j], S, seg_start, seg_slot, in.hdr, bs) ? 1u : 0u;
+    if (nfr) atomicAdd(nfresh_b + b, nfr);
+}
+
+__global__ void k_bs_flag(BatchState *bs) { bs->ord = 1; }
+
+// n_new += the blocks' fresh counts (one block).
+__global__ __launch_bounds__(256) void k_ord_count(BatchState *bs, const uint32_t *__restrict__ nfresh_b, uint32_t nb) {
+    __shared__ uint32_t s_tmp[4];
+    if (bs->err) return;
+    uint64_t t = 0;
+    for (uint32_t i = threadIdx.x; i < nb; i += 256u) t += nfresh_b[i];
+    uint32_t tot;
+    block256_excl((uint32_t)t, s_tmp, &tot);
+    if (threadIdx.x == 0) bs->n_new += tot;
+}
+
 hipError_t launch_ord_heads(uint64_t *S, uint64_t *pay, BatchState *bs, const PacketIn &in, const uint32_t *len,
                             uint8_t *headf, uint32_t *list, uint64_t *tmp, uint64_t *ptmp, uint32_t n,
                             uint64_t seed, uint64_t mask, hipStream_t st) {
@@ -3258,9 +3382,21 @@ hipError_t launch_tail(const TailArgs &a) {
         idt.init = 0;   // (lazy slots: the walkers write a new source's line)
         // (the segment-order buffer holds the IPv6 lists, pass 0's tile rows — unused without
         // the heavy sort — their per-block counts)
-        const uint32_t gr = std::min<uint32_t>(4096, std::max<uint32_t>(1, cdiv(n, 256)));
-        k_ord_resolve4<<<gr, 256, 0, st>>>(bs, sc.seg_start, S, in, idt, sc.seg_slot, sc.seg_order, sc.hist);
-        k_ord_resolve6<<<gr, 256, 0, st>>>(bs, sc.seg_start, S, in, idt, sc.seg_slot, sc.seg_order, sc.hist);
+        static const bool no_region = getenv("FSX_ORD_NO_REGION") != nullptr;   // A/B: global claims only
+        if (!no_region) {
+            // (pass 0's tile rows, unused without the heavy sort, hold the per-block counts)
+            const uint32_t nb = std::max<uint32_t>(1, cdiv(n, kRegSeg));
+            k_bs_flag<<<1, 1, 0, st>>>(bs);
+            k_ord_claim<<<nb, 256, 0, st>>>(bs, sc.seg_start, S, in, idt, sc.seg_slot, sc.seg_order, sc.hist,
+                                            sc.hist + nb);
+            k_ord_spill<<<nb, 256, 0, st>>>(bs, sc.seg_start, S, in, idt, sc.seg_slot, sc.seg_order, sc.hist,
+                                            sc.hist + nb);
+            k_ord_count<<<1, 256, 0, st>>>(bs, sc.hist + nb, nb);
+        } else {
+            const uint32_t gr = std::min<uint32_t>(4096, std::max<uint32_t>(1, cdiv(n, 256)));
+            k_ord_resolve4<<<gr, 256, 0, st>>>(bs, sc.seg_start, S, in, idt, sc.seg_slot, sc.seg_order, sc.hist);
+            k_ord_resolve6<<<gr, 256, 0, st>>>(bs, sc.seg_start, S, in, idt, sc.seg_slot, sc.seg_order, sc.hist);
+        }
         k_batch_check<<<1, 1, 0, st>>>(bs, tstate, lim, nullptr, 0u);
         mark("k_ord_resolve");
     }
