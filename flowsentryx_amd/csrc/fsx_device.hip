@@ -2269,32 +2269,24 @@ __global__ __launch_bounds__(256) void k_ord_claim(BatchState *bs, const uint32_
         }
         if (res == 3) {
             spill[c0 + atomicAdd(&s_nsp, 1u)] = g;
-        } else {
-            seg_slot[g] = (uint32_t)(R0 + r);
-            S[a] = (w & ~kFreshBit) | (res == 1 ? kFreshBit : 0ull);
-            nfr += res == 1 ? 1u : 0u;
+            continue;
+        }
+        const uint64_t pos = R0 + r;
+        seg_slot[g] = (uint32_t)pos;
+        S[a] = (w & ~kFreshBit) | (res == 1 ? kFreshBit : 0ull);
+        if (res == 1) {   // the claim to HBM right away (no other block reads this region):
+            ++nfr;        // head READY, IPv6 key words, IPv4 mirror entry
+            if (tag == 2) {
+                uint32_t *kw = idt.k6 + pos * 4;
+                kw[0] = k[1]; kw[1] = k[2]; kw[2] = k[3];
+            } else {
+                mir_publish(idt.mir, idt.mir_shift, idt.mask, idt.seed, pos, k[0]);
+            }
+            idt.head[pos] = id_head(gen, kIdReady, tag, k[0]);
         }
     }
     if (nfr) atomicAdd(&s_fresh, nfr);
     __syncthreads();
-    // the block's claims to HBM: heads READY, IPv6 key words, IPv4 mirror entries
-    for (uint32_t r = tid; r < Rn; r += 256u) {
-        const unsigned long long cur = H[r];
-        if ((uint32_t)(cur >> 48) != gen || ((cur >> 40) & 0xFFu) != kIdLocal) continue;
-        const uint32_t ct = (uint32_t)(cur >> 32) & 0xFFu;
-        const uint64_t pos = R0 + r;
-        uint32_t k0 = (uint32_t)cur;
-        if (ct == 2) {
-            uint32_t k[4];
-            load_key6(in.hdr, pk_idx(S[seg_start[c0 + (uint32_t)cur]]), k);
-            k0 = k[0];
-            uint32_t *kw = idt.k6 + pos * 4;
-            kw[0] = k[1]; kw[1] = k[2]; kw[2] = k[3];
-        } else {
-            mir_publish(idt.mir, idt.mir_shift, idt.mask, idt.seed, pos, k0);
-        }
-        idt.head[pos] = id_head(gen, kIdReady, ct, k0);
-    }
     if (tid == 0) { nspill[b] = s_nsp; nfresh_b[b] = s_fresh; }
 }
 
