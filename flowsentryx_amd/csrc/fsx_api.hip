@@ -848,6 +848,7 @@ static int run_pipelined(fsx_ctx *c, const PacketIn &in, const uint32_t *d_len, 
     c->par = q;
     if (++c->id_gen == 0x10000u) {
         if (c->sc.id_tab) HIPCHK(c, hipMemsetAsync(c->sc.id_tab, 0, c->id_slots * 32, c->stream));
+        HIPCHK(c, launch_born_clear(c->table, c->slots, c->stream));   // (stamps left by k_ord_claim)
         c->id_gen = 1;
     }
     // the early prologue on the aux stream (FSX_NO_EARLY_PROLOGUE=1: on the context stream)
@@ -992,6 +993,7 @@ static int run_batch(fsx_ctx *c, const PacketIn &in, const uint32_t *d_len, cons
     }
     if (++c->id_gen == 0x10000u) {   // 16-bit generations: clear the id table on wrap
         if (c->sc.id_tab) HIPCHK(c, hipMemsetAsync(c->sc.id_tab, 0, c->id_slots * 32, c->stream));
+        HIPCHK(c, launch_born_clear(c->table, c->slots, c->stream));   // (stamps left by k_ord_claim)
         c->id_gen = 1;
     }
     hipError_t e = launch_verdict_pipeline(in, d_len, d_ts, (uint32_t)n, d_verdict, c->table,
@@ -1293,6 +1295,7 @@ int fsx_map_update_batch(fsx_ctx *c, int map_id, const void *keys, const void *v
     if (e == hipSuccess) e = hipMemcpyAsync(dv, values, n * vlen, hipMemcpyHostToDevice, c->stream);
     if (e == hipSuccess && ++c->id_gen == 0x10000u) {   // 16-bit generations (as run_batch)
         if (c->sc.id_tab) e = hipMemsetAsync(c->sc.id_tab, 0, c->id_slots * 32, c->stream);
+        if (e == hipSuccess) e = launch_born_clear(c->table, c->slots, c->stream);
         c->id_gen = 1;
     }
     const uint32_t born = c->id_gen;

@@ -2216,7 +2216,10 @@ constexpr uint64_t kIdLocal = 3;   // head state in LDS: claimed by this block
 __global__ __launch_bounds__(256) void k_ord_claim(BatchState *bs, const uint32_t *__restrict__ seg_start,
                                                    uint64_t *__restrict__ S, PacketIn in, IdTable idt,
                                                    uint32_t *__restrict__ seg_slot, uint32_t *__restrict__ spill,
-                                                   uint32_t *__restrict__ nspill, uint32_t *__restrict__ nfresh_b) {
+                                                   uint32_t *__restrict__ nspill, uint32_t *__restrict__ nfresh_b,
+                                                   const uint64_t *__restrict__ pay, const uint64_t *__restrict__ ts,
+                                                   const uint32_t *__restrict__ len, uint8_t *__restrict__ marks,
+                                                   Slot *table, Limits lim) {
     __shared__ unsigned long long H[kRegMax];
     __shared__ uint32_t s_nsp, s_fresh;
     __shared__ uint64_t s_r[2];
@@ -2238,6 +2241,8 @@ __global__ __launch_bounds__(256) void k_ord_claim(BatchState *bs, const uint32_
     __syncthreads();
     const uint64_t R0 = s_r[0];
     const uint32_t Rn = (uint32_t)min<uint64_t>(s_r[1] - R0, kRegMax);
+    const bool pay_ok = bs->pay_ok != 0;
+    const uint64_t tbase = ~bs->inv_min_ts;
     for (uint32_t r = tid; r < Rn; r += 256u) H[r] = idt.head[R0 + r];
     __syncthreads();
     uint32_t nfr = 0;
@@ -2272,8 +2277,6 @@ __global__ __launch_bounds__(256) void k_ord_claim(BatchState *bs, const uint32_
             continue;
         }
         const uint64_t pos = R0 + r;
-        seg_slot[g] = (uint32_t)pos;
-        S[a] = (w & ~kFreshBit) | (res == 1 ? kFreshBit : 0ull);
         if (res == 1) {   // the claim to HBM right away (no other block reads this region):
             ++nfr;        // head READY, IPv6 key words, IPv4 mirror entry
             if (tag == 2) {
@@ -2283,7 +2286,39 @@ __global__ __launch_bounds__(256) void k_ord_claim(BatchState *bs, const uint32_
                 mir_publish(idt.mir, idt.mir_shift, idt.mask, idt.seed, pos, k[0]);
             }
             idt.head[pos] = id_head(gen, kIdReady, tag, k[0]);
+            if (seg_start[g + 1] - a == 1) {
+                // a new source's only packet (a flood): its walk here — fw_step from no state
+                // (src/fsx_kern.c:265-284, :312-326), the mark at its position, its whole line
+                // stamped with the batch generation (a failed batch's lines are rolled back; the
+                // stamps of a passed one are cleared at the generation wrap) — and no walker
+                // visit (seg_slot = kNoSlot)
+                uint64_t T;
+                uint32_t L;
+                if (pay_ok) {
+                    const uint64_t pw = pay[a];
+                    T = tbase + (pw >> kPayLenBits);
+                    L = (uint32_t)pw & ((1u << kPayLenBits) - 1u);
+                } else {
+                    T = ts[pk_idx(w)];
+                    L = len[pk_idx(w)];
+                }
+                FwState st{false, false, 0, 0, 0, 0};
+                MarkWriter<false> mw{marks, 0};
+                fw_step(st, T, L, a, lim, mw);
+                const uint32_t fl = (st.has_st ? SLOT_HAS_ST : 0u) | (st.has_bl ? SLOT_HAS_BL : 0u) |
+                                    (idt.born << kBornShift);
+                uint4 *p = reinterpret_cast<uint4 *>(table + pos);
+                p[0] = make_uint4(tag, fl, k[0], tag == 2 ? k[1] : 0u);
+                p[1] = make_uint4(tag == 2 ? k[2] : 0u, tag == 2 ? k[3] : 0u, (uint32_t)st.pps, (uint32_t)(st.pps >> 32));
+                p[2] = make_uint4((uint32_t)st.bps, (uint32_t)(st.bps >> 32), (uint32_t)st.tt, (uint32_t)(st.tt >> 32));
+                p[3] = make_uint4((uint32_t)st.till, (uint32_t)(st.till >> 32), 0u, 0u);
+                seg_slot[g] = kNoSlot;
+                S[a] = w & ~kFreshBit;
+                continue;
+            }
         }
+        seg_slot[g] = (uint32_t)pos;
+        S[a] = (w & ~kFreshBit) | (res == 1 ? kFreshBit : 0ull);
     }
     if (nfr) atomicAdd(&s_fresh, nfr);
     __syncthreads();
@@ -2306,6 +2341,18 @@ __global__ __launch_bounds__(256) void k_ord_spill(BatchState *bs, const uint32_
 }
 
 __global__ void k_bs_flag(BatchState *bs) { bs->ord = 1; }
+
+// Every slot's generation stamp cleared (at the 16-bit batch-generation wrap: k_ord_claim leaves
+// the stamps of the lines it writes, which a failed batch of the same generation 65536 batches
+// later would otherwise roll back).
+__global__ __launch_bounds__(256) void k_born_clear(Slot *table, uint64_t nslots) {
+    for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i < nslots; i += (uint64_t)gridDim.x * 256u)
+        if (table[i].flags >> kBornShift) table[i].flags &= kFlagBits;
+}
+hipError_t launch_born_clear(Slot *table, uint64_t nslots, hipStream_t st) {
+    k_born_clear<<<4096, 256, 0, st>>>(table, nslots);
+    return hipGetLastError();
+}
 
 // n_new += the blocks' fresh counts (one block).
 __global__ __launch_bounds__(256) void k_ord_count(BatchState *bs, const uint32_t *__restrict__ nfresh_b, uint32_t nb) {
@@ -2754,6 +2801,7 @@ __device__ __forceinline__ void walk_short(const SV &sv, const BatchState *bs,
         const uint32_t a = seg_start[g], b = seg_start[g + 1];
         if (H.list && a >= bs->n_light) continue;   // a heavy source: k_walk_heavy
         const uint32_t si = seg_slot[g];
+        if (si == kNoSlot) continue;   // (home-ordered inserts walked it: k_ord_claim)
         Slot &sl = table[si];
         if (flood && (sv.S[a] & kFreshBit)) {
             const unsigned long long hd = K.heads[si];
@@ -2811,6 +2859,7 @@ __device__ __forceinline__ void walk_long(const SV &sv, const BatchState *bs,
         const uint32_t a = seg_start[g], b = seg_start[g + 1];
         if (H.list && a >= bs->n_light) continue;   // a heavy source: k_walk_heavy
         const uint32_t si = seg_slot[g];
+        if (si == kNoSlot) continue;   // (k_ord_claim walked it)
         Slot &sl = table[si];
         const SlotLine L0 = load_line(sl);
         FwState st = state_of(L0);
@@ -3380,7 +3429,7 @@ hipError_t launch_tail(const TailArgs &a) {
             const uint32_t nb = std::max<uint32_t>(1, cdiv(n, kRegSeg));
             k_bs_flag<<<1, 1, 0, st>>>(bs);
             k_ord_claim<<<nb, 256, 0, st>>>(bs, sc.seg_start, S, in, idt, sc.seg_slot, sc.seg_order, sc.hist,
-                                            sc.hist + nb);
+                                            sc.hist + nb, sc.pay[0], ts, len, sc.marks, table, lim);
             k_ord_spill<<<nb, 256, 0, st>>>(bs, sc.seg_start, S, in, idt, sc.seg_slot, sc.seg_order, sc.hist,
                                             sc.hist + nb);
             k_ord_count<<<1, 256, 0, st>>>(bs, sc.hist + nb, nb);

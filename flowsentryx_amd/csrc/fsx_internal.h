@@ -565,6 +565,7 @@ struct TailArgs {
     int last[3];
 };
 hipError_t launch_tail(const TailArgs &a);
+hipError_t launch_born_clear(Slot *table, uint64_t nslots, hipStream_t st);
 
 // st: the batch stream. st2 (optional, with fork/join events): the flow features run
 // on it concurrently with the rate limiter (they share only read-only inputs). st3
