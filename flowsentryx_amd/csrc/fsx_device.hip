@@ -2210,7 +2210,7 @@ __global__ __launch_bounds__(256) void k_ord_resolve6(BatchState *bs, const uint
 // IPv6 key words, IPv4 mirror entries): no global atomic for a flood's inserts, which the
 // device processes at ~30 G/s (k_ord_resolve4 / 6: 18 ms for config 5's 2^28). A probe that
 // leaves the region is spilled to k_ord_spill (the global protocol, after this kernel).
-constexpr uint32_t kRegSeg = 1024, kRegMax = 4096;
+constexpr uint32_t kRegSeg = 256, kRegMax = 1024;
 constexpr uint64_t kIdLocal = 3;   // head state in LDS: claimed by this block
 
 __global__ __launch_bounds__(256) void k_ord_claim(BatchState *bs, const uint32_t *__restrict__ seg_start,
@@ -2221,13 +2221,13 @@ __global__ __launch_bounds__(256) void k_ord_claim(BatchState *bs, const uint32_
                                                    const uint32_t *__restrict__ len, uint8_t *__restrict__ marks,
                                                    Slot *table, Limits lim) {
     __shared__ unsigned long long H[kRegMax];
-    __shared__ uint32_t s_nsp, s_fresh;
+    __shared__ uint32_t s_nsp, s_fresh, s_fused;
     __shared__ uint64_t s_r[2];
     if (bs->err) return;
     const uint32_t nseg = bs->nseg, b = blockIdx.x, tid = threadIdx.x;
     const uint32_t c0 = b * kRegSeg;
     if (c0 >= nseg) {
-        if (tid == 0) { nspill[b] = 0; nfresh_b[b] = 0; }
+        if (tid == 0) { nspill[b] = 0; nfresh_b[b] = 0; nfresh_b[gridDim.x + b] = 0; }
         return;
     }
     const uint32_t c1 = min(nseg, c0 + kRegSeg);
@@ -2237,6 +2237,7 @@ __global__ __launch_bounds__(256) void k_ord_claim(BatchState *bs, const uint32_
         s_r[1] = c1 < nseg ? ord_key_of(S[seg_start[c1]]) >> (32 - s) : idt.mask + 1;
         s_nsp = 0;
         s_fresh = 0;
+        s_fused = 0;
     }
     __syncthreads();
     const uint64_t R0 = s_r[0];
@@ -2245,7 +2246,7 @@ __global__ __launch_bounds__(256) void k_ord_claim(BatchState *bs, const uint32_
     const uint64_t tbase = ~bs->inv_min_ts;
     for (uint32_t r = tid; r < Rn; r += 256u) H[r] = idt.head[R0 + r];
     __syncthreads();
-    uint32_t nfr = 0;
+    uint32_t nfr = 0, nfu = 0;
     for (uint32_t j = tid; j < c1 - c0; j += 256u) {
         const uint32_t g = c0 + j, a = seg_start[g];
         const uint64_t w = S[a];
@@ -2314,6 +2315,7 @@ __global__ __launch_bounds__(256) void k_ord_claim(BatchState *bs, const uint32_
                 p[3] = make_uint4((uint32_t)st.till, (uint32_t)(st.till >> 32), 0u, 0u);
                 seg_slot[g] = kNoSlot;
                 S[a] = w & ~kFreshBit;
+                ++nfu;
                 continue;
             }
         }
@@ -2321,8 +2323,9 @@ __global__ __launch_bounds__(256) void k_ord_claim(BatchState *bs, const uint32_
         S[a] = (w & ~kFreshBit) | (res == 1 ? kFreshBit : 0ull);
     }
     if (nfr) atomicAdd(&s_fresh, nfr);
+    if (nfu) atomicAdd(&s_fused, nfu);
     __syncthreads();
-    if (tid == 0) { nspill[b] = s_nsp; nfresh_b[b] = s_fresh; }
+    if (tid == 0) { nspill[b] = s_nsp; nfresh_b[b] = s_fresh; nfresh_b[gridDim.x + b] = s_fused; }
 }
 
 // The segments k_ord_claim spilled (their probe left the block's region): the global protocol.
@@ -2354,15 +2357,20 @@ hipError_t launch_born_clear(Slot *table, uint64_t nslots, hipStream_t st) {
     return hipGetLastError();
 }
 
-// n_new += the blocks' fresh counts (one block).
+// n_new += the blocks' fresh counts (one block); every segment walked by k_ord_claim: the
+// walkers have nothing to do.
 __global__ __launch_bounds__(256) void k_ord_count(BatchState *bs, const uint32_t *__restrict__ nfresh_b, uint32_t nb) {
     __shared__ uint32_t s_tmp[4];
     if (bs->err) return;
-    uint64_t t = 0;
-    for (uint32_t i = threadIdx.x; i < nb; i += 256u) t += nfresh_b[i];
-    uint32_t tot;
+    uint64_t t = 0, f = 0;
+    for (uint32_t i = threadIdx.x; i < nb; i += 256u) { t += nfresh_b[i]; f += nfresh_b[nb + i]; }
+    uint32_t tot, fu;
     block256_excl((uint32_t)t, s_tmp, &tot);
-    if (threadIdx.x == 0) bs->n_new += tot;
+    block256_excl((uint32_t)f, s_tmp, &fu);
+    if (threadIdx.x == 0) {
+        bs->n_new += tot;
+        bs->ord_walked = fu == bs->nseg ? 1u : 0u;
+    }
 }
 
 hipError_t launch_ord_heads(uint64_t *S, uint64_t *pay, BatchState *bs, const PacketIn &in, const uint32_t *len,
@@ -2833,7 +2841,7 @@ __global__ __launch_bounds__(256) void k_walk_fixed(const uint64_t *__restrict__
                                                     const uint32_t *__restrict__ cls,
                                                     uint8_t *__restrict__ marks, Slot *table,
                                                     Limits lim, HeavyLists H, SlotKeys K) {
-    if (bs->err) return;
+    if (bs->err || bs->ord_walked) return;
     if (bs->pay_ok) {
         const SegView<true> sv{S, ts, len, pay, ~bs->inv_min_ts};
         walk_short(sv, bs, seg_start, seg_slot, order, cls, marks, table, lim, H, K);
@@ -2889,7 +2897,7 @@ __global__ __launch_bounds__(256) void k_walk_fixed_long(const uint64_t *__restr
                                                          const uint32_t *__restrict__ cls,
                                                          uint8_t *__restrict__ marks, Slot *table,
                                                          Limits lim, HeavyLists H, SlotKeys K) {
-    if (bs->err) return;
+    if (bs->err || bs->ord_walked) return;
     if (bs->pay_ok) {
         const SegView<true> sv{S, ts, len, pay, ~bs->inv_min_ts};
         walk_long(sv, bs, seg_start, seg_slot, order, cls, marks, table, lim, H, K);

@@ -106,6 +106,7 @@ struct BatchState {
     uint32_t n_ofix;      // home-ordered batches: key-hash runs longer than 8 (k_ord_long)
     uint32_t n_orun;      // ... key-hash runs of two or more packets (k_ord_scan)
     uint32_t ord;         // home-ordered inserts (Limits::ord) ran for this batch
+    uint32_t ord_walked;  // ... and walked every segment (k_ord_claim): the walkers return at once
 };
 
 // Sorted payload word carried through the onesweep passes next to each sort word:
