@@ -2210,7 +2210,7 @@ __global__ __launch_bounds__(256) void k_ord_resolve6(BatchState *bs, const uint
 // IPv6 key words, IPv4 mirror entries): no global atomic for a flood's inserts, which the
 // device processes at ~30 G/s (k_ord_resolve4 / 6: 18 ms for config 5's 2^28). A probe that
 // leaves the region is spilled to k_ord_spill (the global protocol, after this kernel).
-constexpr uint32_t kRegSeg = 256, kRegMax = 1024;
+constexpr uint32_t kRegSeg = 512, kRegMax = 2048;
 constexpr uint64_t kIdLocal = 3;   // head state in LDS: claimed by this block
 
 __global__ __launch_bounds__(256) void k_ord_claim(BatchState *bs, const uint32_t *__restrict__ seg_start,
