@@ -80,6 +80,8 @@ struct fsx_ctx {
     uint32_t *d_rec_len = nullptr;       // record mode: len / ts written by k_parse
     uint64_t *d_rec_ts = nullptr;
     uint64_t rec_cap = 0;
+    unsigned long long *d_shard_stat = nullptr;   // per (tile, owner) look-back words (k_shard_place16)
+    uint32_t *d_shard_ticket = nullptr;
     uint8_t *d_shard_own = nullptr;      // per packet owner (k_shard_parse)
     void *d_shard_crec = nullptr;        // per packet 16-byte record in arrival order
     uint64_t shard_scr_cap = 0;
@@ -126,6 +128,7 @@ struct fsx_ctx {
     // second stream: flow features beside the limiter (fork / join events)
     hipStream_t aux_stream = nullptr;
     hipEvent_t fork_ev = nullptr, join_ev = nullptr;
+    hipEvent_t wait_ev = nullptr;     // fsx_stream_wait_batches
     hipStream_t walk_stream = nullptr;   // third stream: long-segment walker
     hipEvent_t walk_fork_ev = nullptr, walk_join_ev = nullptr;
     hipEvent_t heavy_fork_ev = nullptr, heavy_flow_ev = nullptr;   // heavy work after the sort
@@ -165,6 +168,10 @@ struct fsx_ctx {
     int tail_par = 0;
     int tail_prev = -1;               // set of the last tail enqueued (its completion: tail_done)
     bool tail_join = false;           // the last pipelined batch's tail is not joined into stream
+    // record mode, pipelined: the records' len / ts per front set (a split tail reads its
+    // batch's while the next front writes its own); max_batch each, allocated on first use
+    uint32_t *rec_len_set[kSets]{};
+    uint64_t *rec_ts_set[kSets]{};
     char err[512]{};
 };
 
@@ -374,7 +381,9 @@ void fsx_close(fsx_ctx *c) {
     for (int b = 0; b < 2; ++b) { hipFree(c->hist.t[b]); hipFree(c->hist.l[b]); }
     hipFree(c->hist.tile_cnt); hipFree(c->hist.tile_off); hipFree(c->hist.total);
     hipFree(c->d_shard_cnt); hipFree(c->d_rep); hipFree(c->d_shard_own); hipFree(c->d_shard_crec);
+    hipFree(c->d_shard_stat); hipFree(c->d_shard_ticket);
     hipFree(c->d_rec_len); hipFree(c->d_rec_ts);
+    for (int p = 0; p < fsx_ctx::kSets; ++p) { hipFree(c->rec_len_set[p]); hipFree(c->rec_ts_set[p]); }
     hipFree(c->idx_heads); hipFree(c->idx_k6); hipFree(c->idx_mir);
     hipFree(c->evict_buf);
     hipFree(c->d_rule_slot); hipFree(c->d_rule_lens); hipFree(c->d_rule_filter);
@@ -389,6 +398,7 @@ void fsx_close(fsx_ctx *c) {
     if (c->heavy_flow_ev) hipEventDestroy(c->heavy_flow_ev);
     if (c->fork_ev) hipEventDestroy(c->fork_ev);
     if (c->join_ev) hipEventDestroy(c->join_ev);
+    if (c->wait_ev) hipEventDestroy(c->wait_ev);
     delete c;
 }
 
@@ -609,6 +619,25 @@ int fsx_sync(fsx_ctx *c) {
     return check_batch(c);
 }
 
+int fsx_stream_wait_batches(fsx_ctx *c, void *hip_stream, int all) {
+    if (!c) return -EINVAL;
+    HIPCHK(c, hipSetDevice(c->device));
+    if (all) {   // the last batch's deferred tail goes in first; the context stream joins it
+        const int rc = sel(c);
+        if (rc) return rc;
+    }
+    hipStream_t s = static_cast<hipStream_t>(hip_stream);
+    // the enqueued split tails end in order (each starts after the one before: flush_tail)
+    if (c->tail_prev >= 0 && c->tail_done[c->tail_prev])
+        HIPCHK(c, hipStreamWaitEvent(s, c->tail_done[c->tail_prev], 0));
+    if (s != c->stream) {   // and everything on the context stream so far
+        if (!c->wait_ev) HIPCHK(c, hipEventCreateWithFlags(&c->wait_ev, hipEventDisableTiming));
+        HIPCHK(c, hipEventRecord(c->wait_ev, c->stream));
+        HIPCHK(c, hipStreamWaitEvent(s, c->wait_ev, 0));
+    }
+    return 0;
+}
+
 int fsx_set_pipeline(fsx_ctx *c, int on) {
     if (!c) return -EINVAL;
     int rc = fsx_sync(c);
@@ -816,10 +845,18 @@ static FlowRequest flow_slots(fsx_ctx *c, const FlowRequest *fr, size_t n, int *
 // tail (the device still has the previous batch to run) and checks it.
 // split = false (other limiters, record mode): the whole batch on the context stream, in
 // order after the previous one, still without a host synchronization per call.
-static int run_pipelined(fsx_ctx *c, const PacketIn &in, const uint32_t *d_len, const uint64_t *d_ts, size_t n,
+static int run_pipelined(fsx_ctx *c, const PacketIn &in0, const uint32_t *d_len, const uint64_t *d_ts, size_t n,
                          uint8_t *d_verdict, const FlowRequest *fr, bool split) {
     HIPCHK(c, hipSetDevice(c->device));
     int rc;
+    // record mode (run_records): the set's len / ts buffers (fresh allocations: in use by nobody)
+    PacketIn in = in0;
+    if (in.rec && !in.rec_len && !c->rec_len_set[0]) {
+        for (int p = 0; p < fsx_ctx::kSets; ++p) {
+            HIPCHK(c, hipMalloc(&c->rec_len_set[p], (size_t)c->cfg.max_batch * 4));
+            HIPCHK(c, hipMalloc(&c->rec_ts_set[p], (size_t)c->cfg.max_batch * 8));
+        }
+    }
     if (c->pending && (rc = fsx_sync(c))) return rc;
     if (c->rules_dirty) {   // the prefix tables are rebuilt with the device idle
         if ((rc = fsx_sync(c)) || (rc = upload_rules(c))) return rc;
@@ -846,6 +883,12 @@ static int run_pipelined(fsx_ctx *c, const PacketIn &in, const uint32_t *d_len, 
     const int old_par = c->par;
     use_front(c, q);
     c->par = q;
+    if (in.rec && !in.rec_len) {   // (set q's batch three back has finished: above)
+        in.rec_len = c->rec_len_set[q];
+        in.rec_ts = c->rec_ts_set[q];
+        d_len = in.rec_len;
+        d_ts = in.rec_ts;
+    }
     if (++c->id_gen == 0x10000u) {
         if (c->sc.id_tab) HIPCHK(c, hipMemsetAsync(c->sc.id_tab, 0, c->id_slots * 32, c->stream));
         HIPCHK(c, launch_born_clear(c->table, c->slots, c->stream));   // (stamps left by k_ord_claim)
@@ -968,11 +1011,12 @@ static int run_batch(fsx_ctx *c, const PacketIn &in, const uint32_t *d_len, cons
     // records, the whole batch on the context stream otherwise
     if (c->pipe && do_limit && n && !c->timing)
         return run_pipelined(c, in, d_len, d_ts, n, d_verdict, fr,
-                             c->pipe == 1 && !in.rec && !no_split_limiters(c) &&
+                             c->pipe == 1 && !no_split_limiters(c) &&
                                  !(c->cfg.flags & FSX_FLAG_OVERFLOW_ADMIT) && !c->lim.ord);
     int rc = sel(c);
     if (rc) return rc;
     if (busy(c)) { rc = fsx_sync(c); if (rc) return rc; }
+    if (in.rec && !in.rec_len) return set_err(c, -EINVAL, "record batch without its len / ts buffers");
     if (do_limit && c->rules_dirty && (rc = upload_rules(c))) return rc;
     FlowRequest frq;
     if (fr) {
@@ -1082,6 +1126,11 @@ static int run_records(fsx_ctx *c, const void *d_records, size_t n, uint32_t rec
                        FSX_SHARD_RECORD_BYTES);
     if (n > c->cfg.max_batch) return set_err(c, -E2BIG, "n=%zu exceeds max_batch", n);
     if (n && (!d_records || !d_verdict)) return set_err(c, -EINVAL, "null buffer");
+    // pipelined (run_batch takes run_pipelined): the front set's own len / ts buffers, so a
+    // split tail reading this batch's overlaps the next front writing its own
+    if (c->pipe && do_limit && n && !c->timing)
+        return run_batch(c, PacketIn{nullptr, d_records, rec_bytes, nullptr, nullptr}, nullptr, nullptr, n,
+                         d_verdict, do_limit, fr);
     int rc = sel(c);
     if (rc) return rc;
     if (n > c->rec_cap) {
@@ -1558,12 +1607,17 @@ static int shard_pack(fsx_ctx *c, const uint8_t *d_hdr, const uint32_t *d_len, c
     if (rc) return rc;
     const uint64_t need = (uint64_t)(G + 1) * (n / 4096 + 1);   // (+ the replica-drop group)
     if (need > c->shard_cnt_cap) {
+        if (busy(c) && (rc = fsx_sync(c))) return rc;   // (an earlier pack may still use them)
         hipFree(c->d_shard_cnt);
+        hipFree(c->d_shard_stat);
         c->d_shard_cnt = nullptr;
+        c->d_shard_stat = nullptr;
         c->shard_cnt_cap = 0;
         HIPCHK(c, hipMalloc(&c->d_shard_cnt, need * 4));
+        HIPCHK(c, hipMalloc(&c->d_shard_stat, need * 8));
         c->shard_cnt_cap = need;
     }
+    if (!c->d_shard_ticket) HIPCHK(c, hipMalloc(&c->d_shard_ticket, 4));
     if (n > c->shard_scr_cap) {
         hipFree(c->d_shard_own);
         hipFree(c->d_shard_crec);
@@ -1578,9 +1632,11 @@ static int shard_pack(fsx_ctx *c, const uint8_t *d_hdr, const uint32_t *d_len, c
     const bool filt = (flags & FSX_SHARD_FILTER_BLOCKLIST) && c->rep_valid;
     const bool compact = (flags & FSX_SHARD_COMPACT) != 0;
     const bool drop_rec = filt && (flags & FSX_SHARD_DROP_RECORDS);
+    const bool regions = (flags & FSX_SHARD_REGIONS) != 0;
     hipError_t e = launch_shard_pack(d_hdr, d_len, d_ts, (uint32_t)n, G, d_verdict, d_records, d_send_idx,
                                      d_counts, c->d_shard_cnt, c->d_shard_own, c->d_shard_crec,
-                                     filt ? &rep : nullptr, compact, drop_rec, filt ? d_filter : nullptr, c->stream);
+                                     filt ? &rep : nullptr, compact, drop_rec, filt ? d_filter : nullptr, regions,
+                                     c->d_shard_stat, c->d_shard_ticket, c->stream);
     if (e != hipSuccess) return set_err(c, -EIO, "shard pack: %s", hipGetErrorString(e));
     return 0;
 }
@@ -1703,6 +1759,21 @@ int fsx_shard_scatter_device(fsx_ctx *c, const uint8_t *d_ret, const uint32_t *d
     int rc = sel(c);
     if (rc) return rc;
     hipError_t e = launch_shard_scatter(d_ret, d_send_idx, (uint32_t)m, d_verdict, c->stream);
+    if (e != hipSuccess) return set_err(c, -EIO, "shard scatter: %s", hipGetErrorString(e));
+    return 0;
+}
+
+int fsx_shard_scatter_regions_device(fsx_ctx *c, const uint8_t *d_ret, const uint32_t *d_send_idx, size_t m,
+                                     size_t region, const uint64_t *d_counts, uint32_t n_shards,
+                                     uint8_t *d_verdict) {
+    if (!c) return -EINVAL;
+    if (m > kMaxBatchLimit) return set_err(c, -E2BIG, "m=%zu too large", m);
+    if (n_shards == 0 || n_shards > FSX_MAX_SHARDS) return set_err(c, -EINVAL, "n_shards must be 1..%d", FSX_MAX_SHARDS);
+    if (m && (!d_ret || !d_send_idx || !d_verdict || !d_counts)) return set_err(c, -EINVAL, "null buffer");
+    int rc = sel(c);
+    if (rc) return rc;
+    hipError_t e = launch_shard_scatter_regions(d_ret, d_send_idx, (uint32_t)m, region, d_counts, n_shards, d_verdict,
+                                                c->stream);
     if (e != hipSuccess) return set_err(c, -EIO, "shard scatter: %s", hipGetErrorString(e));
     return 0;
 }

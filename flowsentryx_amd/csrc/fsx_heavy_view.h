@@ -90,7 +90,9 @@ struct HeavyView {
             }
         }
         const uint64_t bm = __ballot(mine);
-        return __shfl(idx, __ffsll((unsigned long long)bm) - 1) - 1u;
+        // (no lane: the tags do not hold r — a caller that rewrote the verdict buffer while the
+        // batch was in flight; an index inside the batch rather than a fault)
+        return bm ? __shfl(idx, __ffsll((unsigned long long)bm) - 1) - 1u : n - 1u;
     }
 
     // h's packets at arrival indices < i (i <= n)

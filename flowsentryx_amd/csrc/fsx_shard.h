@@ -70,6 +70,7 @@ struct Replica {
 constexpr uint32_t kShardFilter = 1u;   // fsx_shard_pack_device flag (FSX_SHARD_FILTER_BLOCKLIST)
 constexpr uint32_t kShardCompact = 2u;  // fsx_shard_pack_device flag (FSX_SHARD_COMPACT)
 constexpr uint32_t kShardDropRecords = 4u;   // fsx_shard_pack_device flag (FSX_SHARD_DROP_RECORDS)
+constexpr uint32_t kShardRegions = 8u;       // fsx_shard_pack_device flag (FSX_SHARD_REGIONS)
 
 // owner = floor(h * G / 2^32) of a 32-bit mix of (family tag, address).
 __host__ __device__ inline uint32_t shard_owner_of(uint32_t tag, const uint32_t k[4], uint32_t G) {
@@ -83,7 +84,7 @@ hipError_t launch_shard_pack(const uint8_t *hdr, const uint32_t *len, const uint
                              uint32_t G, uint8_t *verdict, void *rec, uint32_t *send_idx,
                              uint64_t *owner_total, uint32_t *scratch, uint8_t *own8, void *crec,
                              const Replica *rep, bool compact, bool drop_rec, const uint32_t *use_dev,
-                             hipStream_t st);
+                             bool regions, unsigned long long *status, uint32_t *ticket, hipStream_t st);
 hipError_t launch_shard_clock(const uint64_t *ts, uint32_t n, uint64_t *out3, hipStream_t st);
 hipError_t launch_blocklist_export(const Slot *table, uint64_t table_mask, ShardBlock *out, uint64_t cap,
                                    unsigned long long *count, hipStream_t st);
@@ -96,5 +97,7 @@ hipError_t launch_shard_unpack(const void *rec, uint32_t rec_bytes, uint32_t m, 
                                uint64_t *ts, hipStream_t st);
 hipError_t launch_shard_scatter(const uint8_t *ret, const uint32_t *send_idx, uint32_t m, uint8_t *verdict,
                                 hipStream_t st);
+hipError_t launch_shard_scatter_regions(const uint8_t *ret, const uint32_t *send_idx, uint32_t m, uint64_t region,
+                                        const uint64_t *counts, uint32_t G, uint8_t *verdict, hipStream_t st);
 
 }  // namespace fsx

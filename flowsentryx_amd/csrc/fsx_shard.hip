@@ -185,6 +185,144 @@ __global__ __launch_bounds__(256) void k_shard_parse(const uint8_t *__restrict__
     if (threadIdx.x < G + drop_rec) cnt[(size_t)threadIdx.x * ntiles + t] = sh[threadIdx.x];
 }
 
+// Regions (FSX_SHARD_REGIONS) with compact requests: k_shard_parse's work, and every record
+// placed at once — owner o's run starts at record o * n (group G, the replica drops, at G * n),
+// in arrival order — so no arrival-order copy is written and read back (k_shard_pack16).
+// A tile's offsets inside each region come from a decoupled look-back over the tiles before
+// it: tiles are taken in ticket order, each publishes its per-owner count (flag 1) and then
+// its inclusive prefix (flag 2) in one 64-bit word per (tile, owner) — the data is the flag.
+// Each lane keeps its 16 packets' records in registers between the parse and the placement.
+// The per-tile counts still go to `cnt`, for k_shard_scan and the 32-byte fallback
+// (k_shard_pack re-places a wide slice).
+constexpr uint32_t kPlaceSpin = 1u << 22;
+
+__device__ __forceinline__ uint32_t place_lookback(unsigned long long *status, uint32_t t, uint32_t o,
+                                                   uint32_t Gx, uint32_t tot) {
+    unsigned long long *my = status + (size_t)t * Gx + o;
+    if (t == 0) {
+        __hip_atomic_store(my, (2ull << 62) | tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return 0;
+    }
+    __hip_atomic_store(my, (1ull << 62) | tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t excl = 0, spins = 0;
+    for (int64_t tt = (int64_t)t - 1; tt >= 0;) {
+        const unsigned long long w = __hip_atomic_load(status + (size_t)tt * Gx + o, __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t flag = (uint32_t)(w >> 62);
+        if (flag == 0) {   // not published yet (its block holds a lower ticket: it is running)
+            if (++spins > kPlaceSpin) break;   // (never expected; a bounded wait, not a hang)
+            __builtin_amdgcn_s_sleep(1);
+            continue;
+        }
+        excl += (uint32_t)w;
+        if (flag == 2) break;
+        --tt;
+    }
+    __hip_atomic_store(my, (2ull << 62) | (excl + tot), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return excl;
+}
+
+__global__ __launch_bounds__(256) void k_shard_place16(const uint8_t *__restrict__ hdr,
+                                                       const uint32_t *__restrict__ len,
+                                                       const uint64_t *__restrict__ ts, uint32_t n,
+                                                       uint32_t G, uint32_t *__restrict__ cnt,
+                                                       uint32_t ntiles, Replica rep, int use_rep0,
+                                                       const uint32_t *__restrict__ use_dev,
+                                                       unsigned long long *wide,
+                                                       uint8_t *__restrict__ verdict,
+                                                       uint4 *__restrict__ out, uint32_t *__restrict__ send_idx,
+                                                       uint64_t *__restrict__ owner_total, uint32_t drop_rec,
+                                                       unsigned long long *status, uint32_t *ticket) {
+    __shared__ uint32_t s_rec[4][64 * 17];
+    __shared__ uint32_t s_wc[4][kMaxShards + 1];
+    __shared__ uint32_t s_tile;
+    const int use_rep = use_rep0 && (!use_dev || *use_dev);
+    const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
+    const uint32_t Gx = G + drop_rec;
+    if (threadIdx.x == 0) s_tile = atomicAdd(ticket, 1u);
+    for (uint32_t o = threadIdx.x; o < 4 * (kMaxShards + 1); o += 256) (&s_wc[0][0])[o] = 0;
+    __syncthreads();
+    const uint32_t t = s_tile;
+    uint32_t *rec = s_rec[w];
+    bool need_wide = false;
+    uint32_t filtered = 0;
+    uint4 r[16];
+    uint32_t ob[4] = {~0u, ~0u, ~0u, ~0u};   // owners, a byte per packet (0xFF: not sent)
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        const uint32_t base = t * kShardTile + w * 1024u + (uint32_t)j * 64u;
+        const uint8_t *src = hdr + (size_t)base * 64;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t g = (uint32_t)k * 1024u + lane * 16u;
+            uint4 x = make_uint4(0, 0, 0, 0);
+            if (base + (g >> 6) < n) x = *reinterpret_cast<const uint4 *>(src + g);
+            uint32_t *d = rec + (g >> 6) * 17u + ((g & 63u) >> 2);
+            d[0] = x.x; d[1] = x.y; d[2] = x.z; d[3] = x.w;
+        }
+        wave_lds_order();
+        const uint32_t i = base + lane;
+        r[j] = make_uint4(0, 0, 0, 0);
+        if (i < n) {
+            const uint32_t L = len[i];
+            const uint64_t now = ts[i];
+            uint32_t k[4], dp, fam;
+            const uint32_t f = shard_classify(reinterpret_cast<const uint8_t *>(rec + lane * 17u), L, now,
+                                              rep, use_rep != 0, k, dp, fam);
+            if (f >= 4 || (f == 2 && drop_rec)) {
+                const uint32_t o = f >= 4 ? owner_dev(f, k, G) : G;
+                atomicAdd(&s_wc[w][o], 1u);
+                need_wide |= fam == 6 || L > 0xFFFFu;
+                ob[j >> 2] = (ob[j >> 2] & ~(0xFFu << (8 * (j & 3)))) | (o << (8 * (j & 3)));
+                // (ShardRecord16 {key, len | dport << 16, ts}; a wide slice is re-placed)
+                r[j] = make_uint4(k[0], (L & 0xFFFFu) | (dp << 16), (uint32_t)now, (uint32_t)(now >> 32));
+            }
+            verdict[i] = f == 1 || f >= 4 ? 2u : 1u;
+            filtered += f == 2;
+        }
+        wave_lds_order();
+    }
+    if (wide && __ballot(need_wide) && lane == 0) atomicOr(wide, 1ull);
+    filtered = wave_sum(filtered);
+    if (lane == 0 && filtered)
+        atomicAdd(reinterpret_cast<unsigned long long *>(&owner_total[G]), (unsigned long long)filtered);
+    __syncthreads();
+    if (threadIdx.x < Gx) {   // per owner: the tile's count, its offset in the region, per wave
+        const uint32_t o = threadIdx.x;
+        const uint32_t c0 = s_wc[0][o], c1 = s_wc[1][o], c2 = s_wc[2][o], c3 = s_wc[3][o];
+        const uint32_t tot = c0 + c1 + c2 + c3;
+        cnt[(size_t)o * ntiles + t] = tot;
+        const uint32_t b = place_lookback(status, t, o, Gx, tot);
+        s_wc[0][o] = b;
+        s_wc[1][o] = b + c0;
+        s_wc[2][o] = b + c0 + c1;
+        s_wc[3][o] = b + c0 + c1 + c2;
+    }
+    __syncthreads();
+    const uint64_t lt = (1ull << lane) - 1ull;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        const uint32_t i = t * kShardTile + w * 1024u + (uint32_t)j * 64u + lane;
+        const uint32_t own = (ob[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+        const bool ip = own != 0xFFu;
+        uint64_t peers = __ballot(ip);
+        for (uint32_t b = 0; (1u << b) < Gx; ++b) {
+            const bool bit = (own >> b) & 1u;
+            const uint64_t bal = __ballot(ip && bit);
+            peers &= bit ? bal : ~bal;
+        }
+        const uint32_t below = (uint32_t)__popcll(peers & lt);
+        uint32_t base = 0;
+        if (ip && below == 0) base = atomicAdd(&s_wc[w][own], (uint32_t)__popcll(peers));
+        base = __shfl(base, ip ? __ffsll((unsigned long long)peers) - 1 : 0);
+        if (ip) {
+            const size_t slot = (size_t)own * n + base + below;
+            out[slot] = r[j];
+            send_idx[slot] = i;
+        }
+    }
+}
+
 // The first record slot of owner o: the totals of the owners before it.
 __device__ __forceinline__ uint32_t owner_base(const uint64_t *owner_total, uint32_t o) {
     uint32_t b = 0;
@@ -296,14 +434,16 @@ __global__ __launch_bounds__(256) void k_shard_pack(const uint8_t *__restrict__ 
                                                     uint8_t *__restrict__ verdict, Replica rep,
                                                     int use_rep0, const uint32_t *__restrict__ use_dev,
                                                     uint64_t *__restrict__ owner_total,
-                                                    int compact, uint32_t drop_rec) {
+                                                    int compact, uint32_t drop_rec, int regions) {
     const int use_rep = use_rep0 && (!use_dev || *use_dev);
-    if (compact && owner_total[G + 1] == 16u) return;   // k_shard_pack16 places the records
+    if (compact && owner_total[G + 1] == 16u) return;   // k_shard_pack16 / k_shard_place16 placed them
     __shared__ uint32_t s_base[kMaxShards + 1];
     __shared__ uint32_t s_wc[4][kMaxShards + 1];
     const uint32_t t = blockIdx.x, lane = lane_id(), w = threadIdx.x >> 6;
     const uint32_t Gx = G + drop_rec;   // (group G: the replica-dropped packets)
-    if (threadIdx.x < Gx) s_base[threadIdx.x] = offs[(size_t)threadIdx.x * ntiles + t] + owner_base(owner_total, threadIdx.x);
+    // (regions: owner o's run starts at record o * n; else after the owners before it)
+    if (threadIdx.x < Gx)
+        s_base[threadIdx.x] = offs[(size_t)threadIdx.x * ntiles + t] + (regions ? 0u : owner_base(owner_total, threadIdx.x));
     // wave w owns packets [t*4096 + w*1024, +1024) in arrival order: count per owner
     // first (so a wave places after the waves before it), then place in order
     uint32_t of[16];   // owner << 4 | class (0 DROP, 1 PASS, 4/6 IP, 8 | 4/6 replica-dropped IP, 15 none)
@@ -362,7 +502,7 @@ __global__ __launch_bounds__(256) void k_shard_pack(const uint8_t *__restrict__ 
         if (ip) {
             uint32_t k[4], dp;
             shard_parse(hdr + (size_t)i * 64, len[i], k, dp);
-            const uint32_t slot = base + below;
+            const size_t slot = (regions ? (size_t)own * n : 0) + base + below;
             ShardRecord x;
             x.key[0] = k[0]; x.key[1] = k[1]; x.key[2] = k[2]; x.key[3] = k[3];
             x.ts = ts[i];
@@ -434,6 +574,28 @@ __global__ __launch_bounds__(256) void k_shard_scatter(const uint8_t *__restrict
         verdict[send_idx[i]] = ret[i];
 }
 
+// Regions: returned verdict i (owner by owner, counts[o] each) -> its owner's region entry.
+__global__ __launch_bounds__(256) void k_shard_scatter_regions(const uint8_t *__restrict__ ret,
+                                                               const uint32_t *__restrict__ send_idx, uint32_t m,
+                                                               uint64_t region, const uint64_t *__restrict__ counts,
+                                                               uint32_t G, uint8_t *__restrict__ verdict) {
+    __shared__ uint32_t s_pre[kMaxShards + 1];
+    if (threadIdx.x == 0) {
+        uint32_t a = 0;
+        for (uint32_t o = 0; o < G; ++o) { s_pre[o] = a; a += (uint32_t)counts[o]; }
+        s_pre[G] = a;
+    }
+    __syncthreads();
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < m && i < s_pre[G]; i += gridDim.x * 256u) {
+        uint32_t lo = 0, hi = G;   // the owner o with s_pre[o] <= i < s_pre[o + 1]
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (s_pre[mid] <= i) lo = mid; else hi = mid;
+        }
+        verdict[send_idx[(size_t)lo * region + (i - s_pre[lo])]] = ret[i];
+    }
+}
+
 __global__ void k_shard_empty(uint64_t *owner_total, uint32_t G, int compact) {
     for (uint32_t o = 0; o <= G; ++o) owner_total[o] = 0;
     if (compact) owner_total[G + 1] = 16u;
@@ -443,7 +605,7 @@ hipError_t launch_shard_pack(const uint8_t *hdr, const uint32_t *len, const uint
                              uint32_t G, uint8_t *verdict, void *rec, uint32_t *send_idx,
                              uint64_t *owner_total, uint32_t *scratch, uint8_t *own8, void *crec,
                              const Replica *rep, bool compact, bool drop_rec, const uint32_t *use_dev,
-                             hipStream_t st) {
+                             bool regions, unsigned long long *status, uint32_t *ticket, hipStream_t st) {
     (void)hipGetLastError();   // a stale error of another caller is not ours
     k_shard_empty<<<1, 1, 0, st>>>(owner_total, G, compact);   // also the wide flag / filtered
     if (n == 0) return hipGetLastError();
@@ -454,15 +616,25 @@ hipError_t launch_shard_pack(const uint8_t *hdr, const uint32_t *len, const uint
     if (wide) k_shard_fmt_init<<<1, 1, 0, st>>>(wide);
     ShardRecord16 *cr = compact ? reinterpret_cast<ShardRecord16 *>(crec) : nullptr;
     const uint32_t dr = drop_rec && use ? 1u : 0u;   // (records of the replica drops: group G)
-    k_shard_parse<<<ntiles, 256, 0, st>>>(hdr, len, ts, n, G, scratch, ntiles, r, use, use_dev, wide, verdict,
-                                          own8, cr, owner_total, dr);
+    const bool place = compact && regions;   // (k_shard_place16: no arrival-order copy)
+    if (place) {
+        hipError_t e = hipMemsetAsync(status, 0, (size_t)ntiles * (G + dr) * 8, st);
+        if (e == hipSuccess) e = hipMemsetAsync(ticket, 0, 4, st);
+        if (e != hipSuccess) return e;
+        k_shard_place16<<<ntiles, 256, 0, st>>>(hdr, len, ts, n, G, scratch, ntiles, r, use, use_dev, wide, verdict,
+                                                reinterpret_cast<uint4 *>(rec), send_idx, owner_total, dr, status,
+                                                ticket);
+    } else {
+        k_shard_parse<<<ntiles, 256, 0, st>>>(hdr, len, ts, n, G, scratch, ntiles, r, use, use_dev, wide, verdict,
+                                              own8, cr, owner_total, dr);
+    }
     k_shard_scan<<<G + dr, 1024, 0, st>>>(scratch, owner_total, G, ntiles, compact);
-    if (compact)
+    if (compact && !place)
         k_shard_pack16<<<ntiles, 256, 0, st>>>(own8, cr, n, G, scratch, ntiles,
                                                reinterpret_cast<ShardRecord16 *>(rec), send_idx, owner_total,
                                                G + dr);
     k_shard_pack<<<ntiles, 256, 0, st>>>(hdr, len, ts, n, G, scratch, ntiles, rec, send_idx, verdict, r,
-                                         use, use_dev, owner_total, compact, dr);
+                                         use, use_dev, owner_total, compact, dr, regions ? 1 : 0);
     return hipGetLastError();
 }
 
@@ -644,6 +816,15 @@ hipError_t launch_shard_unpack(const void *rec, uint32_t rec_bytes, uint32_t m, 
         k_shard_unpack<<<grid, 256, 0, st>>>(reinterpret_cast<const ShardRecord16 *>(rec), m, hdr, len, ts);
     else
         k_shard_unpack<<<grid, 256, 0, st>>>(reinterpret_cast<const ShardRecord *>(rec), m, hdr, len, ts);
+    return hipGetLastError();
+}
+
+hipError_t launch_shard_scatter_regions(const uint8_t *ret, const uint32_t *send_idx, uint32_t m, uint64_t region,
+                                        const uint64_t *counts, uint32_t G, uint8_t *verdict, hipStream_t st) {
+    (void)hipGetLastError();   // a stale error of another caller is not ours
+    if (m == 0) return hipSuccess;
+    const uint32_t grid = std::min<uint32_t>(4096, (m + 255) / 256);
+    k_shard_scatter_regions<<<grid, 256, 0, st>>>(ret, send_idx, m, region, counts, G, verdict);
     return hipGetLastError();
 }
 

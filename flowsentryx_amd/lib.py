@@ -128,6 +128,7 @@ def load_library() -> C.CDLL:
         "fsx_set_stream": (C.c_int, [vp, vp]),
         "fsx_sync": (C.c_int, [vp]),
         "fsx_set_pipeline": (C.c_int, [vp, C.c_int]),
+        "fsx_stream_wait_batches": (C.c_int, [vp, vp, C.c_int]),
         "fsx_verdict_batch": (C.c_int, [vp, u8p, u8p, u8p, sz, u8p]),
         "fsx_verdict_batch_device": (C.c_int, [vp, vp, vp, vp, sz, vp]),
         "fsx_process_batch_device": (C.c_int, [vp, vp, vp, vp, sz, vp, vp, vp, vp, vp, vp, sz]),
@@ -165,6 +166,7 @@ def load_library() -> C.CDLL:
         "fsx_shard_unpack_device": (C.c_int, [vp, vp, sz, vp, vp, vp]),
         "fsx_shard_unpack16_device": (C.c_int, [vp, vp, sz, vp, vp, vp]),
         "fsx_shard_scatter_device": (C.c_int, [vp, vp, vp, sz, vp]),
+        "fsx_shard_scatter_regions_device": (C.c_int, [vp, vp, vp, sz, sz, vp, C.c_uint32, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -177,7 +179,7 @@ def load_library() -> C.CDLL:
 # Every symbol include/fsx_hip.h declares (checked by tests/test_abi.py).
 ABI_SYMBOLS = [
     "fsx_abi_version", "fsx_config_default", "fsx_open", "fsx_close", "fsx_last_error",
-    "fsx_set_stream", "fsx_sync", "fsx_set_pipeline", "fsx_verdict_batch", "fsx_verdict_batch_device",
+    "fsx_set_stream", "fsx_sync", "fsx_set_pipeline", "fsx_stream_wait_batches", "fsx_verdict_batch", "fsx_verdict_batch_device",
     "fsx_process_batch_device", "fsx_verdict_records_device", "fsx_process_records_device",
     "fsx_map_lookup", "fsx_map_update", "fsx_map_update_batch", "fsx_map_delete", "fsx_map_dump",
     "fsx_get_stats",
@@ -187,7 +189,7 @@ ABI_SYMBOLS = [
     "fsx_blocklist_replica_blocks_device",
     "fsx_last_timings", "fsx_enable_timing", "fsx_last_batch_info",
     "fsx_shard_owner", "fsx_shard_pack_device", "fsx_shard_unpack_device", "fsx_shard_unpack16_device",
-    "fsx_shard_scatter_device", "fsx_shard_clock_device", "fsx_blocklist_export_device",
+    "fsx_shard_scatter_device", "fsx_shard_scatter_regions_device", "fsx_shard_clock_device", "fsx_blocklist_export_device",
     "fsx_blocklist_replica_device", "fsx_pcap_index", "fsx_pcap_records_device",
 ]
 
@@ -197,6 +199,7 @@ SHARD_BLOCK_BYTES = 32
 SHARD_FILTER_BLOCKLIST = 1
 SHARD_COMPACT = 2
 SHARD_DROP_RECORDS = 4
+SHARD_REGIONS = 8
 FLOW_PARTIAL_BYTES = 112
 MAX_SHARDS = 64
 
@@ -303,6 +306,13 @@ class FsxContext:
         sort overlap this batch's walkers and verdicts; read outputs after sync(). on = 2:
         batches whole on the context stream, only without a host synchronization per call."""
         self._check(self._lib.fsx_set_pipeline(self._h, int(on)), "fsx_set_pipeline")
+
+    def stream_wait_batches(self, stream_handle: int, all_batches: bool = True):
+        """hip_stream waits for the batches enqueued so far (include/fsx_hip.h
+        fsx_stream_wait_batches): all_batches=False leaves out the last split batch, whose
+        tail the next batch call enqueues."""
+        self._check(self._lib.fsx_stream_wait_batches(self._h, stream_handle, int(bool(all_batches))),
+                    "fsx_stream_wait_batches")
 
     def set_stream(self, stream_handle: int | None):
         self._check(self._lib.fsx_set_stream(self._h, stream_handle or None), "fsx_set_stream")
@@ -569,6 +579,14 @@ class FsxContext:
     def shard_scatter_device(self, d_ret: int, d_send_idx: int, m: int, d_verdict: int):
         self._check(self._lib.fsx_shard_scatter_device(self._h, d_ret, d_send_idx, m, d_verdict),
                     "fsx_shard_scatter_device")
+
+    def shard_scatter_regions_device(self, d_ret: int, d_send_idx: int, m: int, region: int, d_counts: int,
+                                     n_shards: int, d_verdict: int):
+        """fsx_shard_scatter_regions_device: m verdicts owner by owner back through a
+        FSX_SHARD_REGIONS pack's send indices (regions of `region` entries, its counts)."""
+        self._check(self._lib.fsx_shard_scatter_regions_device(self._h, d_ret, d_send_idx, m, region, d_counts,
+                                                               n_shards, d_verdict),
+                    "fsx_shard_scatter_regions_device")
 
     # -- timing
     def enable_timing(self, on: bool = True):

@@ -78,6 +78,17 @@ def _a2a(out: torch.Tensor, inp: torch.Tensor, out_splits, in_splits, group=None
         dist.all_to_all_single(out, inp, out_splits, in_splits, group=group)
 
 
+def _a2a_views(out: torch.Tensor, out_splits, ins, group=None):
+    """all-to-all of one view per destination (not one contiguous tensor: a regions pack,
+    HipShardEngine.send_views) into `out` split by out_splits. RCCL takes the views as they
+    are (grouped send / receive); gloo gets them concatenated."""
+    if dist.get_backend(group) == "gloo":
+        inp = torch.cat(ins) if ins else out[:0]
+        _a2a(out, inp, out_splits, [int(x.numel()) for x in ins], group)
+    else:
+        dist.all_to_all(list(out.split(list(out_splits))), list(ins), group=group)
+
+
 def _all_reduce_sum(t: torch.Tensor, group=None) -> torch.Tensor:
     if t.is_cuda and dist.get_backend(group) == "gloo":
         h = t.cpu()
@@ -99,8 +110,10 @@ class HipShardEngine:
         self.stream = torch.cuda.Stream(device)
         ctx.set_stream(self.stream.cuda_stream)
         # owner batches back to back without a host synchronization per call (errors surface
-        # at the next synchronization; each batch whole on the engine stream)
-        ctx.set_pipeline(2)
+        # at the next synchronization), split: a record batch's tail (walkers, verdicts, flows)
+        # runs on the context's side streams beside the next sub-batch's front, and its
+        # verdicts go back after that next call (ShardedDataPlane, fsx_stream_wait_batches)
+        ctx.set_pipeline(1)
         # collectives run from a second stream, so the exchange of sub-batch j + 1 overlaps
         # the owner pipeline of sub-batch j (ShardedDataPlane)
         self.comm = torch.cuda.Stream(device)
@@ -108,6 +121,10 @@ class HipShardEngine:
         self.owner_cap = int(ctx.config.max_batch)
         # per-sub-batch buffers by pipeline slot (allocated on first use, sized for the piece)
         self.recs, self.send_idxs, self.countss = {}, {}, {}
+        # FSX_SHARD_REGIONS packs (one pass over the headers: owner o's records at o * n); the
+        # pieces' n and G per slot for the views and the scatter
+        self.regions = True
+        self.pack_ng = {}
         self.rec = self.send_idx = self.counts = None
         self.clock3 = torch.empty(3, dtype=torch.int64, device=device)
         self.blk = torch.empty(1024 * lib.SHARD_BLOCK_BYTES, dtype=torch.uint8, device=device)
@@ -136,6 +153,14 @@ class HipShardEngine:
         ev.record(self.comm)
         return ev
 
+    def return_ctx(self, all_batches: bool):
+        """Collectives on the comm stream after the owner batches enqueued so far: the engine
+        stream's work and their split tails (all_batches=False: except the last batch's, still
+        deferred beside the next call)."""
+        self.comm.wait_stream(self.stream)
+        self.ctx.stream_wait_batches(self.comm.cuda_stream, all_batches)
+        return torch.cuda.stream(self.comm)
+
     def engine_wait(self, ev):
         """The engine stream continues after `ev` (a comm_event)."""
         self.stream.wait_event(ev)
@@ -154,7 +179,8 @@ class HipShardEngine:
         self.stream.wait_stream(cur)
         with torch.cuda.stream(self.stream):
             yield
-        cur.wait_stream(self.stream)
+        # (the engine stream and every split tail, the last one enqueued first)
+        self.ctx.stream_wait_batches(cur.cuda_stream, True)
 
     def _owner_buffers(self, m: int):
         if self._oh is None or self._oh[0].numel() < m * 64:
@@ -249,11 +275,14 @@ class HipShardEngine:
         flags = lib.SHARD_COMPACT
         if filt is not None and drop_rec:
             flags |= lib.SHARD_DROP_RECORDS
-        if slot not in self.recs or self.send_idxs[slot].numel() < max(1, n):
-            m = max(1, n)
+        if self.regions:
+            flags |= lib.SHARD_REGIONS
+        m = max(1, n) * ((G + 1) if self.regions else 1)
+        if slot not in self.recs or self.send_idxs[slot].numel() < m:
             self.recs[slot] = torch.empty(m * REC, dtype=torch.uint8, device=self.device)
             self.send_idxs[slot] = torch.empty(m, dtype=torch.int32, device=self.device)
             self.countss[slot] = torch.empty(lib.MAX_SHARDS + 2, dtype=torch.int64, device=self.device)
+        self.pack_ng[slot] = (n, G)
         rec, idx, cnt = self.recs[slot], self.send_idxs[slot], self.countss[slot]
         self.rec, self.send_idx, self.counts = rec, idx, cnt   # (tests read the last pack)
         if filt is None:
@@ -265,6 +294,18 @@ class HipShardEngine:
                                                 filt.data_ptr(), verdict.data_ptr(), rec.data_ptr(),
                                                 idx.data_ptr(), cnt.data_ptr(), flags)
         return rec, cnt[:G + 2]
+
+    def send_views(self, rec: torch.Tensor, sc, rb: int, slot: int):
+        """The records for each owner (sc[o] of rb bytes): views into its region."""
+        if not self.regions:
+            return list(rec[:sum(sc) * rb].split([c * rb for c in sc]))
+        n = self.pack_ng[slot][0]
+        return [rec[o * n * rb:(o * n + c) * rb] for o, c in enumerate(sc)]
+
+    def drop_first(self, slot: int, sent: int) -> int:
+        """Record index of the first replica-dropped record (FSX_SHARD_DROP_RECORDS)."""
+        n, G = self.pack_ng[slot]
+        return G * n if self.regions else sent
 
     def filter_plan(self, clocks: torch.Tensor, G: int, k: int) -> torch.Tensor:
         """The replica filter's decision per sub-batch from the all-gathered piece clocks
@@ -357,7 +398,14 @@ class HipShardEngine:
         return v[:max(m, 1)]
 
     def scatter(self, ret: torch.Tensor, m: int, verdict, slot: int = 0):
-        if m:
+        """ret: the m returned verdicts, owner by owner, into their arrival positions."""
+        if not m:
+            return
+        if self.regions:
+            n, G = self.pack_ng[slot]
+            self.ctx.shard_scatter_regions_device(ret.data_ptr(), self.send_idxs[slot].data_ptr(), m, n,
+                                                  self.countss[slot].data_ptr(), G, verdict.data_ptr())
+        else:
             self.ctx.shard_scatter_device(ret.data_ptr(), self.send_idxs[slot].data_ptr(), m,
                                           verdict.data_ptr())
 
@@ -391,6 +439,7 @@ class ShardedDataPlane:
         self.blk_cap = 1024        # blocklist entries per rank of one all-gather (grows)
         self.partials_sent = 0     # flow partials sent for replica-dropped packets
         self.host_reads = 0        # host synchronizations of the data plane (one per global batch)
+        self._sc, self._rc = {}, {}  # per sub-batch: records sent to / received from each rank
 
     def verdict_batch(self, hdr, length, ts, n: int, verdict, chunks: int = 1, bounds=None):
         """Verdicts for this rank's slice (arrival order) of one global batch; every rank
@@ -420,10 +469,27 @@ class ShardedDataPlane:
                 filt = self._filter_plan(ts, bounds)
             pend = self._exchange_all(hdr, length, ts, verdict, bounds, filt, blk, flows)
             sent = recv = 0
+            # owner j's verdicts go back after owner j + 1 is enqueued (its split tail runs
+            # beside that call's front), the last after its tail is enqueued; the scatters into
+            # arrival positions after all of them (every other library call joins the tail)
+            back, live = [], []
             for j in range(k):
-                ms, mr = self._stage_owner(verdict, bounds, j, pend[j], slot=j)
+                calls = getattr(self.engine, "owner_calls", 0)
+                ms, mr, v = self._stage_owner(verdict, bounds, j, pend[j], slot=j)
+                live.append(pend[j][0])   # (the records: read by the tail on the side streams)
                 pend[j] = None
+                if back:
+                    # (no owner call for sub-batch j: the tail of j - 1 is still deferred)
+                    back[-1] = self._return(*back[-1], all_batches=getattr(self.engine, "owner_calls", 0) == calls)
+                back.append((j, ms, mr, v))
                 sent, recv = sent + ms, recv + mr
+            if back:
+                back[-1] = self._return(*back[-1], all_batches=True)
+            self.engine.engine_wait(self.engine.comm_event())
+            for j, ms, ret in back:
+                self.engine.keep(ret)
+                self.engine.scatter(ret, ms, verdict[bounds[j]:], j)
+            del live
             if flows:
                 self.engine.flows_end()
             self.last_exchange = {"sent": sent, "received": recv, "filtered": self.filtered}
@@ -495,9 +561,9 @@ class ShardedDataPlane:
             out_b = [c * f for c, f in zip(rc, rf)]
             with e.comm_ctx():
                 recv = e.recv_buffer(sum(out_b))
-                _a2a(recv[:sum(out_b)], packs[j][0][:sum(in_b)], out_b, in_b, self.group)
+                _a2a_views(recv[:sum(out_b)], out_b, e.send_views(packs[j][0], sc, rb, j), self.group)
             # with flows and the filter: the flow partials of the replica-dropped packets
-            partial = (self._exchange_partials(packs[j][0], sum(sc), int(cj[G]), rb, blk[1], j)
+            partial = (self._exchange_partials(packs[j][0], e.drop_first(j, sum(sc)), int(cj[G]), rb, blk[1], j)
                        if drop else None)
             segs, off = [], 0
             for c, f, nb in zip(rc, rf, out_b):
@@ -526,12 +592,19 @@ class ShardedDataPlane:
         self.partials_sent += m
         return precv, prc, cap
 
+    def _return(self, j: int, ms: int, mr: int, v, all_batches: bool):
+        """Sub-batch j's verdicts back to their arrival ranks (comm stream, after its owner
+        batches' tails) -> (j, ms, received verdicts)."""
+        with self.engine.return_ctx(all_batches):
+            ret = torch.empty(max(ms, 1), dtype=torch.uint8, device=v.device)
+            _a2a(ret[:ms], v[:mr], self._sc[j], self._rc[j], self.group)
+        return j, ms, ret
+
     def _stage_owner(self, verdict, bounds, j: int, pend, slot=None):
-        """Owner pipeline of sub-batch j (engine stream), verdicts back (comm stream) and
-        into arrival positions (engine stream)."""
+        """Owner pipeline of sub-batch j (engine stream) -> (sent, received, its verdicts in
+        received order); _return sends them back."""
         G, e = self.world, self.engine
         recv, segs, sc, rc, arrived, partial = pend
-        a = bounds[j]
         slot = j % 2 if slot is None else slot
         ms, mr = sum(sc), sum(rc)
         e.engine_wait(arrived)        # the records (and partials) of sub-batch j have arrived
@@ -544,13 +617,8 @@ class ShardedDataPlane:
             for r in range(G):
                 e.merge_counted(precv[r * cap * B:], cap, prc[r:r + 1])
         v = e.owner_batch(recv, segs, slot)
-        with e.comm_ctx():
-            ret = torch.empty(max(ms, 1), dtype=torch.uint8, device=v.device)
-            _a2a(ret[:ms], v[:mr], sc, rc, self.group)
-        e.engine_wait(e.comm_event())
-        e.keep(ret)
-        e.scatter(ret, ms, verdict[a:], slot)
-        return ms, mr
+        self._sc[j], self._rc[j] = sc, rc
+        return ms, mr, v
 
     def stats(self) -> tuple[int, int]:
         """stats_map of the whole sharded data plane: sum over the owners, plus the

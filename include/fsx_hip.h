@@ -219,19 +219,28 @@ int fsx_sync(fsx_ctx *ctx);
  * sliding-window fsx_verdict_batch_device / fsx_process_batch_device call enqueues the batch's front
  * (parse, sort) on the context stream and its tail (walkers, verdicts, flows) on the
  * context's own side streams, so the next batch's front overlaps this batch's tail; results
- * and map state are exactly those of the same calls without pipelining. Up to three batches
+ * and map state are exactly those of the same calls without pipelining. Record batches
+ * (fsx_verdict_records_device / fsx_process_records_device) split the same way. Up to three batches
  * are in flight: a call first waits (on the host) for the batch three calls back. The caller
  * keeps a batch's input and output buffers untouched until that batch completes: read the
  * outputs after fsx_sync (or any other entry point, which orders the context stream after
  * the last tail). A failed batch cancels the batch after it; the error (e.g. -ENOSPC) is
  * returned by fsx_sync or by the call that found it, which enqueues nothing, and neither
  * failed batch changes any map (a sliding-window batch whose history does not fit fails
- * with -ENOSPC when its tail starts). The token bucket, record mode and the overflow
+ * with -ENOSPC when its tail starts). The token bucket and the overflow
  * admission flag run each batch whole on the context stream (no overlap, but still no host
  * synchronization per call); so does every
  * batch with on = 2 (a caller that reuses input buffers in stream order); timed batches
  * (fsx_enable_timing) run unpipelined. on = 0 turns it off. */
 int fsx_set_pipeline(fsx_ctx *ctx, int on);
+/* Order a caller's hipStream_t after the batches enqueued so far, without a host
+ * synchronization: `hip_stream` waits for the context stream's work and for every split
+ * tail already enqueued. A pipelined batch's tail is enqueued by the next batch call (beside
+ * its parse) or by any other entry point, so with all = 0 the last split batch is NOT
+ * covered — the caller keeps overlapping it with the next batch and waits for batch j after
+ * enqueueing batch j + 1 (the sharded plane's owners, flowsentryx_amd/shard.py); all = 1
+ * enqueues that tail first and covers every batch. */
+int fsx_stream_wait_batches(fsx_ctx *ctx, void *hip_stream, int all);
 
 /* Replaces fsx() (src/fsx_kern.c:96-347) over a batch of n packets in arrival
  * order. Host pointers; hdr is n*64 bytes; verdict receives n bytes (1/2).
@@ -318,6 +327,7 @@ uint32_t fsx_shard_owner(const uint8_t *key16, int family, uint32_t n_shards);
 #define FSX_SHARD_FILTER_BLOCKLIST 1u
 #define FSX_SHARD_COMPACT 2u
 #define FSX_SHARD_DROP_RECORDS 4u
+#define FSX_SHARD_REGIONS 8u
 
 /* Parse a device batch and partition its IP packets by owner, stable in arrival order:
  * d_records (n * 32 bytes capacity) receives the records owner by owner, d_send_idx the
@@ -334,7 +344,11 @@ uint32_t fsx_shard_owner(const uint8_t *key16, int family, uint32_t n_shards);
  * FSX_SHARD_DROP_RECORDS (and the filter), the replica-dropped packets are written as
  * records too, after every owner's run, in arrival order (d_counts[n_shards] of them; the
  * first sum(d_counts[0..n_shards)) records are the ones to send), so the arrival rank can
- * take their flow sums (fsx_flow_partials_records_device). */
+ * take their flow sums (fsx_flow_partials_records_device). With FSX_SHARD_REGIONS every
+ * owner has a region of n records instead: owner o's records (and d_send_idx entries) start at
+ * record o * n, the replica-dropped ones at n_shards * n — d_records holds (n_shards + 1) * n
+ * records of 32 bytes, d_send_idx as many entries; with FSX_SHARD_COMPACT too, the records
+ * are placed as the headers are parsed (one pass: DESIGN.md §7). */
 int fsx_shard_pack_device(fsx_ctx *ctx, const uint8_t *d_hdr, const uint32_t *d_len,
                           const uint64_t *d_ts, size_t n, uint32_t n_shards, uint32_t flags,
                           uint8_t *d_verdict, void *d_records, uint32_t *d_send_idx,
@@ -413,6 +427,12 @@ int fsx_process_records_device(fsx_ctx *ctx, const void *d_records, size_t n, ui
 /* Origin side: d_verdict[d_send_idx[i]] = d_ret[i] for the m returned verdicts. */
 int fsx_shard_scatter_device(fsx_ctx *ctx, const uint8_t *d_ret, const uint32_t *d_send_idx,
                              size_t m, uint8_t *d_verdict);
+/* The same for a FSX_SHARD_REGIONS pack: d_ret holds the m returned verdicts owner by owner
+ * (d_counts[o] of owner o, the pack's counts), d_send_idx the pack's regions of `region`
+ * entries (its n). */
+int fsx_shard_scatter_regions_device(fsx_ctx *ctx, const uint8_t *d_ret, const uint32_t *d_send_idx,
+                                     size_t m, size_t region, const uint64_t *d_counts, uint32_t n_shards,
+                                     uint8_t *d_verdict);
 
 /* ---- pcap ingest (SURVEY.md §8 f). Classic pcap records (the 24-byte file header is
  * the caller's): FSX_PCAP_NANOSECONDS for magic 0xA1B23C4D, FSX_PCAP_SWAPPED when the

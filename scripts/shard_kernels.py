@@ -28,14 +28,21 @@ def main():
     with lib.FsxContext(max_batch=n, max_entries=int(p.n_ips), device=0) as ctx:
         e = HipShardEngine(ctx, n, dev)
         with e.stream_ctx():
-            for _ in range(2):
-                rec, counts = e.pack(hdr, ln, ts, n, G, v)
+            # (pack_contiguous_ms: the owners' runs back to back — parse, then k_shard_pack16
+            # from the arrival-order copy; pack_ms: FSX_SHARD_REGIONS, HipShardEngine's, one pass)
+            for regions in (False, True):
+                e.regions = regions
+                for _ in range(2):
+                    rec, counts = e.pack(hdr, ln, ts, n, G, v)
+                ctx.sync()
+                t0 = time.perf_counter()
+                for _ in range(5):
+                    rec, counts = e.pack(hdr, ln, ts, n, G, v)
+                ctx.sync()
+                out["pack_ms" if regions else "pack_contiguous_ms"] = (time.perf_counter() - t0) / 5 * 1e3
+            e.regions = False   # (the unpack below reads the first m records)
+            rec, counts = e.pack(hdr, ln, ts, n, G, v)
             ctx.sync()
-            t0 = time.perf_counter()
-            for _ in range(5):
-                rec, counts = e.pack(hdr, ln, ts, n, G, v)
-            ctx.sync()
-            out["pack_ms"] = (time.perf_counter() - t0) / 5 * 1e3
             c = counts.tolist()
             rb = int(c[G + 1])
             m = int(sum(c[:G]))
@@ -106,8 +113,43 @@ def main():
             el = sorted(per[2:])[len(per[2:]) // 2]   # median of the warm calls
             out["owner_records_warm_flows_ms" if flows else "owner_records_warm_ms"] = el
             out["owner_heavy_unsorted"] = ctx.last_batch_info().get("heavy_unsorted")
+    # the owner as HipShardEngine runs it (pipeline mode 1: each record batch's tail beside the
+    # next call's front): W + K calls back to back, each on its own copy of the records
+    # shifted by one more stream duration, timed over the K calls after the W
+    W, K = 3, 8
+    base = rec.clone()
+    bufs = []
+    for i in range(W + K):
+        b = base.clone()
+        b.view(torch.int64)[1::2].add_((i + 1) * dur)
+        bufs.append(b)
+    torch.cuda.synchronize()
+    for flows in (False, True):
+        with lib.FsxContext(max_batch=n, max_entries=int(p.n_ips), device=0) as ctx:
+            ctx.load_q8_model(model)
+            ctx.set_pipeline(1)
+            # (a batch's verdict buffer holds its heavy tags until its tail is done: one each)
+            ovs = [torch.empty(m, dtype=torch.uint8, device=dev) for _ in bufs]
+            cap = int(p.n_ips)
+            fo = [torch.empty(cap * 16, dtype=torch.uint8, device=dev), torch.empty(cap, dtype=torch.uint8, device=dev),
+                  torch.empty(cap * 8, dtype=torch.float32, device=dev), torch.empty(cap, dtype=torch.float32, device=dev),
+                  torch.empty(cap, dtype=torch.uint8, device=dev)]
+            for i, (b, ov) in enumerate(zip(bufs, ovs)):
+                if i == W:
+                    ctx.sync()
+                    t0 = time.perf_counter()
+                if flows:
+                    ctx.process_records_device(b.data_ptr(), m, rb, ov.data_ptr(), *[x.data_ptr() for x in fo], cap)
+                else:
+                    ctx.verdict_records_device(b.data_ptr(), m, rb, ov.data_ptr())
+            ctx.sync()
+            el = (time.perf_counter() - t0) / K * 1e3
+            out["owner_records_split_flows_ms" if flows else "owner_records_split_ms"] = el
+    del bufs
     out["note"] = ("owner_records_warm*: maps carried, one 64M-record batch per call (records shifted by one "
-                   "stream duration per call), median host time of a call through its sync")
+                   "stream duration per call), median host time of a call through its sync; "
+                   "owner_records_split*: the same stream, pipeline mode 1 (HipShardEngine's), "
+                   f"{K} calls back to back after {W}, per call")
     print(json.dumps(out))
 
 

@@ -66,6 +66,17 @@ class CpuShardEngine:
     def comm_event(self):
         return None
 
+    def return_ctx(self, all_batches):
+        return contextlib.nullcontext()
+
+    @staticmethod
+    def send_views(rec, sc, rb, slot):
+        return list(rec[:sum(sc) * rb].split([c * rb for c in sc]))
+
+    @staticmethod
+    def drop_first(slot, sent):
+        return sent
+
     def engine_wait(self, ev):
         pass
 

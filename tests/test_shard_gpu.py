@@ -18,8 +18,12 @@ from test_shard_cpu import BASE, run_sharded
 pytestmark = pytest.mark.gpu
 
 
+@pytest.mark.parametrize("regions", [False, True])
 @pytest.mark.parametrize("v6_frac,rec_bytes", [(0.4, 32), (0.0, 16)])
-def test_pack_unpack_scatter_match_restatement(native, oracle, v6_frac, rec_bytes):
+def test_pack_unpack_scatter_match_restatement(native, oracle, v6_frac, rec_bytes, regions):
+    """regions: FSX_SHARD_REGIONS (owner o's records at o * n; compact records placed by
+    k_shard_place16 in one pass with a look-back over the tiles) — the same records per
+    owner, in the same order, as the contiguous layout and the restatement."""
     rng = np.random.default_rng(41)
     hdr, ln, ts = rand_stream(rng, 20000, 500, dt_max=300, v6_frac=v6_frac, nonip_frac=0.05,
                               short_frac=0.05)
@@ -32,6 +36,7 @@ def test_pack_unpack_scatter_match_restatement(native, oracle, v6_frac, rec_byte
     from flowsentryx_amd.shard import HipShardEngine
     with native.FsxContext(max_batch=1 << 15, max_entries=4096) as c:
         e = HipShardEngine(c, n, dev)
+        e.regions = regions
         rec, counts = e.pack(th, tl, tt, n, G, tv)
         c.sync()
         cpu = CpuShardEngine(oracle, max_entries=4096)
@@ -42,8 +47,11 @@ def test_pack_unpack_scatter_match_restatement(native, oracle, v6_frac, rec_byte
         m = int(ccounts[:G].sum())
         assert counts.cpu().tolist() == ccounts.tolist()
         assert int(ccounts[G + 1]) == rec_bytes
-        assert np.array_equal(rec[:m * rec_bytes].cpu().numpy(), crec.numpy())
-        assert np.array_equal(e.send_idx[:m].cpu().numpy().astype(np.int64), cpu.send_idx)
+        sc = [int(x) for x in ccounts[:G]]
+        rec = torch.cat(e.send_views(rec, sc, rec_bytes, 0))
+        sidx = torch.cat(e.send_views(e.send_idx.view(torch.uint8), sc, 4, 0)).view(torch.int32)
+        assert np.array_equal(rec.cpu().numpy(), crec.numpy())
+        assert np.array_equal(sidx.cpu().numpy().astype(np.int64), cpu.send_idx)
         ipmask = np.zeros(n, dtype=bool)
         ipmask[cpu.send_idx] = True
         assert np.array_equal(tv.cpu().numpy()[~ipmask], cv.numpy()[~ipmask])
@@ -192,3 +200,67 @@ def test_record_mode_equals_header_mode(native, oracle, v6_frac):
         idx = e.send_idx[:m].cpu().numpy().astype(np.int64)
         vo = o.batch(hdr[idx], ln[idx], ts[idx])
         assert np.array_equal(outs["rec"][0], vo)
+
+
+@pytest.mark.parametrize("flows", [False, True])
+def test_record_batches_split_pipelined(native, oracle, flows):
+    """Record batches split like header batches (fsx_set_pipeline 1: each tail beside the
+    next batch's front, the len / ts of every front set in its own buffers): five record
+    batches enqueued back to back without a synchronization, each batch's verdicts copied
+    on another stream after fsx_stream_wait_batches(all=0) following the NEXT call (the last
+    after all=1) — every copy, the maps and stats equal the oracle over the whole stream."""
+    from flowsentryx_amd.shard import HipShardEngine
+    from test_gpu_parity import MAPS, assert_same_state
+    rng = np.random.default_rng(47)
+    hdr, ln, ts = rand_stream(rng, 150000, 900, dt_max=150, v6_frac=0.0, nonip_frac=0.02, short_frac=0.01)
+    n = hdr.shape[0]
+    dev = torch.device("cuda", 0)
+    th = torch.from_numpy(hdr.reshape(-1).copy()).to(dev)
+    tl = torch.from_numpy(ln.view(np.int32).copy()).to(dev)
+    tt = torch.from_numpy(ts.view(np.int64).copy()).to(dev)
+    tv = torch.zeros(n, dtype=torch.uint8, device=dev)
+    cfg = dict(pps_threshold=7, window_ns=200_000, block_ns=1_000_000)
+    with native.FsxContext(max_batch=1 << 18, max_entries=1 << 15, **cfg) as c:
+        e = HipShardEngine(c, n, dev)      # (pipeline mode 1)
+        rec, counts = e.pack(th, tl, tt, n, 1, tv)
+        c.sync()
+        m, rb = int(counts[0].item()), int(counts[2].item())
+        assert rb == 16
+        cuts = [0, m // 7, 2 * m // 7, m // 2, 4 * m // 5, m]
+        v = torch.zeros(m, dtype=torch.uint8, device=dev)
+        side = torch.cuda.Stream(dev)
+        got = torch.zeros(m, dtype=torch.uint8, device=dev)
+        fo = None
+        if flows:
+            fo = [torch.zeros(m * 16, dtype=torch.uint8, device=dev), torch.zeros(m, dtype=torch.uint8, device=dev),
+                  torch.zeros(m * 8, dtype=torch.float32, device=dev), torch.zeros(m, dtype=torch.float32, device=dev),
+                  torch.zeros(m, dtype=torch.uint8, device=dev)]
+            from flowsentryx_amd import fsx_load
+            from pathlib import Path
+            c.load_q8_model(fsx_load.load_weights(Path(__file__).parent / "golden" / "model_weights.json"))
+
+        def copy_back(j, all_batches):
+            a, b = cuts[j], cuts[j + 1]
+            c.stream_wait_batches(side.cuda_stream, all_batches)
+            with torch.cuda.stream(side):
+                got[a:b].copy_(v[a:b])
+
+        for j in range(len(cuts) - 1):
+            a, b = cuts[j], cuts[j + 1]
+            if flows:
+                c.process_records_device(rec.data_ptr() + a * rb, b - a, rb, v.data_ptr() + a,
+                                         *[x.data_ptr() for x in fo], m)
+            else:
+                c.verdict_records_device(rec.data_ptr() + a * rb, b - a, rb, v.data_ptr() + a)
+            if j:
+                copy_back(j - 1, False)
+        copy_back(len(cuts) - 2, True)
+        side.synchronize()
+        c.sync()
+        idx = e.send_idx[:m].cpu().numpy().astype(np.int64)
+        o = oracle.Oracle(max_entries=1 << 15, **cfg)
+        vo = np.concatenate([o.batch(hdr[idx[a:b]], ln[idx[a:b]], ts[idx[a:b]])
+                             for a, b in zip(cuts[:-1], cuts[1:])])
+        assert np.array_equal(got.cpu().numpy(), vo)
+        assert np.array_equal(v.cpu().numpy(), vo)
+        assert_same_state(c, o)
