@@ -981,14 +981,14 @@ static int evict_idle(fsx_ctx *c, const PacketIn &in, const uint64_t *d_ts, size
     return 0;
 }
 
-// Split pipelining for the fixed and the sliding window (round 4; FSX_SPLIT_FIXED_ONLY=1: the
-// fixed window only). The token bucket runs each batch whole on the context stream: split, its
-// tail (two tile scans and the flows over every position) beside the next front measured
-// 4.73 vs 4.39 ms per step (profiles/r04/ab_r04t_token.txt; FSX_SPLIT_TOKEN=1: split, A/B).
+// Split pipelining for every limiter (FSX_SPLIT_FIXED_ONLY=1: the fixed window only). The
+// token bucket's tail was two tile scans over every position and measured slower split (4.73
+// vs 4.39 ms, profiles/r04/ab_r04t_token.txt); with the one-pass scan (k_tb_scan) split wins,
+// 4.06 vs 4.22 ms (profiles/r05/ab_r05tb5_token_split.txt; FSX_NO_SPLIT_TOKEN=1: whole batches, A/B).
 static bool no_split_limiters(const fsx_ctx *c) {
     static const bool fixed_only = getenv("FSX_SPLIT_FIXED_ONLY") != nullptr;
-    static const bool split_token = getenv("FSX_SPLIT_TOKEN") != nullptr;
-    if (c->cfg.limiter == FSX_LIMIT_TOKEN_BUCKET) return !split_token;
+    static const bool no_split_token = getenv("FSX_NO_SPLIT_TOKEN") != nullptr;
+    if (c->cfg.limiter == FSX_LIMIT_TOKEN_BUCKET && no_split_token) return true;
     return fixed_only && c->cfg.limiter != FSX_LIMIT_FIXED_WINDOW;
 }
 

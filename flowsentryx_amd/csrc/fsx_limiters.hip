@@ -17,10 +17,12 @@
 // from the table), which cuts the scan into independent segments by itself.
 //   k_tb_seg      one thread per source: blacklist prefix (static rules still apply,
 //                 src/fsx_kern.c:159-216 semantics), state after the first counted packet
-//   k_tb_tiles<0> per 4096-position tile: composed map of the tile
-//   k_tb_carry    one block: state entering every tile
-//   k_tb_tiles<1> per tile: replay the tile from its entering state, verdict marks, the
-//                 final {tokens, last} of every source ending in the tile
+//   k_tb_scan     per 4096-position tile, one pass: the tile's composed map, the state
+//                 entering it by a decoupled look-back over the tiles before it (tiles in
+//                 ticket order), then the replay from that state — verdict marks, the final
+//                 {tokens, last} of every source ending in the tile
+//   (FSX_TB_TWO_PASS=1, A/B: k_tb_tiles<0> maps per tile, k_tb_carry one block for the
+//   entering states, k_tb_tiles<1> the replay — the timestamps read twice)
 //
 // Sliding window. Per counted packet: expire the source's log from the
 // oldest entry while now - t_oldest >= W, append, count = |log|, bytes = sum of lengths;
@@ -138,10 +140,87 @@ __global__ __launch_bounds__(256) void k_tb_seg(const uint64_t *__restrict__ S, 
 // Position kinds inside a tile.
 enum : uint32_t { TB_BLOCKED = 0, TB_FIRST = 1, TB_NEXT = 2, TB_NONE = 3 };
 
-// One 4096-position tile, 16 consecutive positions per thread. kApply = false: the
-// tile's composed map to tile_map[t]; true: replay from tile_x[t], marks and final
-// source states.
-template <bool kApply, class SV>
+// One-pass look-back state (k_tb_scan): three 64-bit words per tile, each its own flag (the
+// words are memset to 0 per batch; relaxed agent-scope atomics, no fence: a word is valid
+// alone, so no ordering between them is needed) —
+//   A: 1 << 62 | lo of the tile's composed map, or 2 << 62 | x the state leaving the tile
+//   B: 1 << 63 | hi,   C: 1 << 63 | (d + 2^61)      (lo, hi, x in [0, 2^61], |d| <= 2^61)
+// Wave 0 of the tile looks back 64 tiles at a time: lane k reads tile j - k; the nearest
+// inclusive state ends the walk, and the maps of the tiles after it are composed by an
+// ordered tree over the lanes.
+__device__ __forceinline__ CMap cm_shfl_down(const CMap &m, int o) {
+    return CMap{__shfl_down(m.lo, o), __shfl_down(m.hi, o), __shfl_down(m.d, o)};
+}
+
+__device__ __forceinline__ void tb_put(unsigned long long *p, unsigned long long v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned long long tb_get(const unsigned long long *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ int64_t tb_lookback(unsigned long long *status, uint32_t t, const CMap &agg,
+                                               int64_t hi) {
+    const uint32_t lane = lane_id();
+    constexpr unsigned long long kM62 = (1ull << 62) - 1ull, kM63 = (1ull << 63) - 1ull;
+    unsigned long long *my = status + 3ull * t;
+    if (t == 0) {   // (tile 0 starts with a source head: the state entering it is irrelevant, 0)
+        if (lane == 0) tb_put(my, (2ull << 62) | (unsigned long long)cm_apply(agg, 0));
+        return 0;
+    }
+    if (lane == 0) {
+        tb_put(my + 1, (1ull << 63) | (unsigned long long)agg.hi);
+        tb_put(my + 2, (1ull << 63) | (unsigned long long)(agg.d + kTbSat));
+        tb_put(my, (1ull << 62) | (unsigned long long)agg.lo);
+    }
+    const CMap id{0, hi, 0};
+    CMap m = id;   // the maps of the tiles walked so far, composed (later tiles outer)
+    int64_t x = 0;
+    uint32_t spins = 0;
+    for (int64_t j = (int64_t)t - 1;;) {
+        const int64_t idx = j - (int64_t)lane;
+        unsigned long long wa = 2ull << 62, wb = 0, wc = 0;   // (before tile 0: state 0)
+        if (idx >= 0) {
+            const unsigned long long *q = status + 3ull * (uint64_t)idx;
+            wa = tb_get(q);
+            if ((wa >> 62) == 1) {
+                wb = tb_get(q + 1);
+                wc = tb_get(q + 2);
+                if (!(wb >> 63) || !(wc >> 63)) wa = 0;   // (its other words not seen yet)
+            }
+        }
+        const uint32_t f = (uint32_t)(wa >> 62);
+        const uint64_t b2 = __ballot(f == 2), b0 = __ballot(f == 0);
+        const uint32_t l2 = b2 ? (uint32_t)__ffsll((unsigned long long)b2) - 1u : 64u;
+        const uint32_t l0 = b0 ? (uint32_t)__ffsll((unsigned long long)b0) - 1u : 64u;
+        if (l0 < l2) {   // a tile before the nearest state has published nothing yet: wait
+            if (++spins > (1u << 22)) break;   // (never expected: lower tickets are running)
+            __builtin_amdgcn_s_sleep(1);
+            continue;
+        }
+        CMap a = id;   // lanes before the nearest state: their maps
+        if (lane < l2) a = CMap{(int64_t)(wa & kM62), (int64_t)(wb & kM63), (int64_t)(wc & kM63) - kTbSat};
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {   // lane 0: A_j o A_(j-1) o ... (ordered tree)
+            const CMap y = cm_shfl_down(a, o);
+            if ((lane & (2u * (uint32_t)o - 1u)) == 0 && lane + (uint32_t)o < 64u) a = cm_compose(a, y);
+        }
+        m = cm_compose(m, CMap{__shfl(a.lo, 0), __shfl(a.hi, 0), __shfl(a.d, 0)});
+        if (l2 < 64u) {
+            x = (int64_t)__shfl((long long)(wa & kM62), (int)l2);
+            break;
+        }
+        j -= 64;
+    }
+    const int64_t xin = cm_apply(m, x);
+    if (lane == 0) tb_put(my, (2ull << 62) | (unsigned long long)cm_apply(agg, xin));
+    return xin;
+}
+
+// One 4096-position tile, 16 consecutive positions per thread. kMode 0: the tile's composed
+// map to tile_map[t]; 1: replay from tile_x[t], marks and final source states; 2 (k_tb_scan):
+// the map, the entering state by look-back (status), then the replay.
+template <int kMode, class SV>
 __device__ __forceinline__ void tb_tile(const SV &sv, uint32_t t, uint32_t M,
                                         const uint8_t *__restrict__ headf,
                                         const uint32_t *__restrict__ tile_off,
@@ -149,7 +228,9 @@ __device__ __forceinline__ void tb_tile(const SV &sv, uint32_t t, uint32_t M,
                                         const uint64_t *__restrict__ seg_x,
                                         const uint32_t *__restrict__ seg_slot, Slot *table,
                                         const Limits &lim, CMap *tile_map, const int64_t *tile_x,
-                                        uint8_t *__restrict__ marks, CMap *s_w, uint32_t *s_tmp) {
+                                        uint8_t *__restrict__ marks, CMap *s_w, uint32_t *s_tmp,
+                                        unsigned long long *status = nullptr, int64_t *s_x = nullptr) {
+    constexpr bool kApply = kMode != 0;
     const uint32_t tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
     const uint32_t p0 = t * kTile + tid * 16u;
     const int64_t hi = lim.tb_cap >= kTbCost ? (int64_t)(lim.tb_cap - kTbCost) : 0;
@@ -235,8 +316,21 @@ __device__ __forceinline__ void tb_tile(const SV &sv, uint32_t t, uint32_t M,
             tile_map[t] = a;
         }
     } else {
+        int64_t xt;
+        if constexpr (kMode == 2) {
+            if (w == 0) {   // (wave 0 looks back)
+                CMap a = s_w[0];
+                for (int k = 1; k < 4; ++k) a = cm_compose(s_w[k], a);
+                const int64_t xin = tb_lookback(status, t, a, hi);
+                if (lane == 0) *s_x = xin;
+            }
+            __syncthreads();
+            xt = *s_x;
+        } else {
+            xt = tile_x[t];
+        }
         excl = cm_compose(excl, pre);
-        int64_t x = cm_apply(excl, tile_x[t]);
+        int64_t x = cm_apply(excl, xt);
         uint32_t out[4] = {0, 0, 0, 0};
         int32_t g = (int32_t)hb - 1;
         uint64_t tprev = tprev0;
@@ -279,7 +373,7 @@ __device__ __forceinline__ void tb_tile(const SV &sv, uint32_t t, uint32_t M,
     }
 }
 
-template <bool kApply>
+template <int kMode>
 __global__ __launch_bounds__(256) void k_tb_tiles(const uint64_t *__restrict__ S, BatchState *bs,
                                                   const uint64_t *__restrict__ ts,
                                                   const uint32_t *__restrict__ len,
@@ -299,13 +393,44 @@ __global__ __launch_bounds__(256) void k_tb_tiles(const uint64_t *__restrict__ S
     const bool pay_ok = bs->pay_ok != 0;
     for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
         if (pay_ok)
-            tb_tile<kApply>(SegView<true>{S, ts, len, pay, ~bs->inv_min_ts}, t, M, headf, tile_off, seg_j,
-                            seg_x, seg_slot, table, lim, tile_map, tile_x, marks, s_w, s_tmp);
+            tb_tile<kMode>(SegView<true>{S, ts, len, pay, ~bs->inv_min_ts}, t, M, headf, tile_off, seg_j,
+                           seg_x, seg_slot, table, lim, tile_map, tile_x, marks, s_w, s_tmp);
         else
-            tb_tile<kApply>(SegView<false>{S, ts, len, pay, 0}, t, M, headf, tile_off, seg_j, seg_x,
-                            seg_slot, table, lim, tile_map, tile_x, marks, s_w, s_tmp);
+            tb_tile<kMode>(SegView<false>{S, ts, len, pay, 0}, t, M, headf, tile_off, seg_j, seg_x,
+                           seg_slot, table, lim, tile_map, tile_x, marks, s_w, s_tmp);
         __syncthreads();
     }
+}
+
+// One pass (see the file header): a block per tile, tiles in ticket order.
+__global__ __launch_bounds__(256) void k_tb_scan(const uint64_t *__restrict__ S, BatchState *bs,
+                                                 const uint64_t *__restrict__ ts,
+                                                 const uint32_t *__restrict__ len,
+                                                 const uint64_t *__restrict__ pay,
+                                                 const uint8_t *__restrict__ headf,
+                                                 const uint32_t *__restrict__ tile_off,
+                                                 const uint32_t *__restrict__ seg_j,
+                                                 const uint64_t *__restrict__ seg_x,
+                                                 const uint32_t *__restrict__ seg_slot, Slot *table,
+                                                 Limits lim, CMap *tile_map, unsigned long long *status,
+                                                 uint32_t *ticket, uint8_t *__restrict__ marks) {
+    __shared__ CMap s_w[4];
+    __shared__ uint32_t s_tmp[4];
+    __shared__ uint32_t s_t;
+    __shared__ int64_t s_x;
+    if (bs->err) return;
+    const uint32_t M = bs->n_valid;
+    const uint32_t ntiles = (M + kTile - 1) / kTile;
+    if (threadIdx.x == 0) s_t = atomicAdd(ticket, 1u);
+    __syncthreads();
+    const uint32_t t = s_t;
+    if (t >= ntiles) return;
+    if (bs->pay_ok)
+        tb_tile<2>(SegView<true>{S, ts, len, pay, ~bs->inv_min_ts}, t, M, headf, tile_off, seg_j, seg_x, seg_slot,
+                   table, lim, tile_map, nullptr, marks, s_w, s_tmp, status, &s_x);
+    else
+        tb_tile<2>(SegView<false>{S, ts, len, pay, 0}, t, M, headf, tile_off, seg_j, seg_x, seg_slot, table, lim,
+                   tile_map, nullptr, marks, s_w, s_tmp, status, &s_x);
 }
 
 // One block: the state entering every tile (tile 0 starts with a source head, so its
@@ -354,14 +479,28 @@ hipError_t launch_token_bucket(const uint64_t *S, const uint64_t *ts, const uint
     k_tb_seg<<<gridSeg, 256, 0, st>>>(S, bs, sc.seg_start, sc.seg_slot, ts, len, sc.pay[0], table, lim,
                                       seg_j, seg_x);
     mark("k_tb_seg");
-    k_tb_tiles<false><<<gridTiles, 256, 0, st>>>(S, bs, ts, len, sc.pay[0], sc.headf, sc.tile_aux, seg_j,
-                                                 seg_x, sc.seg_slot, table, lim, tile_map, tile_x,
-                                                 sc.marks);
+    static const bool two_pass = getenv("FSX_TB_TWO_PASS") != nullptr;
+    if (!two_pass) {
+        // (three status words per tile over the map and carry region; the ticket in its last
+        // word, past every tile: 3 * tiles < 4 * lim_tiles_n - 1)
+        unsigned long long *status = reinterpret_cast<unsigned long long *>(sc.lim_tiles);
+        uint32_t *ticket = reinterpret_cast<uint32_t *>(sc.lim_tiles + 4 * sc.lim_tiles_n - 1);
+        hipError_t e = hipMemsetAsync(sc.lim_tiles, 0, sc.lim_tiles_n * 4 * 8, st);
+        if (e != hipSuccess) return e;
+        const uint32_t grid = std::max<uint32_t>(1, (n + kTile - 1) / kTile);   // (>= the valid tiles)
+        k_tb_scan<<<grid, 256, 0, st>>>(S, bs, ts, len, sc.pay[0], sc.headf, sc.tile_aux, seg_j, seg_x,
+                                        sc.seg_slot, table, lim, tile_map, status, ticket, sc.marks);
+        mark("k_tb_scan");
+        return hipGetLastError();
+    }
+    k_tb_tiles<0><<<gridTiles, 256, 0, st>>>(S, bs, ts, len, sc.pay[0], sc.headf, sc.tile_aux, seg_j,
+                                             seg_x, sc.seg_slot, table, lim, tile_map, tile_x,
+                                             sc.marks);
     mark("k_tb_tiles_reduce");
     k_tb_carry<<<1, 1024, 0, st>>>(bs, tile_map, tile_x, lim);
-    k_tb_tiles<true><<<gridTiles, 256, 0, st>>>(S, bs, ts, len, sc.pay[0], sc.headf, sc.tile_aux, seg_j,
-                                                seg_x, sc.seg_slot, table, lim, tile_map, tile_x,
-                                                sc.marks);
+    k_tb_tiles<1><<<gridTiles, 256, 0, st>>>(S, bs, ts, len, sc.pay[0], sc.headf, sc.tile_aux, seg_j,
+                                             seg_x, sc.seg_slot, table, lim, tile_map, tile_x,
+                                             sc.marks);
     mark("k_tb_tiles_apply");
     return hipGetLastError();
 }

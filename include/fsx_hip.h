@@ -227,8 +227,8 @@ int fsx_sync(fsx_ctx *ctx);
  * the last tail). A failed batch cancels the batch after it; the error (e.g. -ENOSPC) is
  * returned by fsx_sync or by the call that found it, which enqueues nothing, and neither
  * failed batch changes any map (a sliding-window batch whose history does not fit fails
- * with -ENOSPC when its tail starts). The token bucket and the overflow
- * admission flag run each batch whole on the context stream (no overlap, but still no host
+ * with -ENOSPC when its tail starts). The overflow
+ * admission flag runs each batch whole on the context stream (no overlap, but still no host
  * synchronization per call); so does every
  * batch with on = 2 (a caller that reuses input buffers in stream order); timed batches
  * (fsx_enable_timing) run unpipelined. on = 0 turns it off. */
