@@ -168,6 +168,24 @@ struct fsx_ctx {
     int tail_par = 0;
     int tail_prev = -1;               // set of the last tail enqueued (its completion: tail_done)
     bool tail_join = false;           // the last pipelined batch's tail is not joined into stream
+    // fsx_reset between pipelined batches (fixed window / token bucket): a second table set
+    // (slots, scalars, index) is swapped in and cleared on the device after the last tail
+    // that used it, so the reset neither waits on the host nor orders the next front after
+    // the last tail (DESIGN.md §3 "Pipelined resets"); FSX_RESET_SYNC=1: the synchronous reset
+    struct TableSet {
+        Slot *table = nullptr;
+        TableState *tstate = nullptr;
+        unsigned long long *heads = nullptr;
+        uint32_t *k6 = nullptr;
+        void *mir = nullptr;
+        uint32_t epoch = 1;
+    };
+    TableSet spare{};
+    hipEvent_t spare_free[2]{};       // walk / aux stream after the last tails on the spare set
+    bool spare_tail = false;          // ... and the deferred tail too, when it is enqueued
+    uint32_t tgen = 0;                // table generation: one per pipelined reset
+    uint32_t fl_tgen[kSets]{};
+    bool fresh_tables = false;        // the next pipelined batch starts a table generation
     // record mode, pipelined: the records' len / ts per front set (a split tail reads its
     // batch's while the next front writes its own); max_batch each, allocated on first use
     uint32_t *rec_len_set[kSets]{};
@@ -301,6 +319,11 @@ static hipError_t flush_tail(fsx_ctx *c, hipEvent_t after) {
         return e;
     if ((e = launch_tail(c->tail_args)) != hipSuccess) return e;
     c->tail_prev = c->tail_par;
+    if (c->spare_tail) {   // (the tail of the last batch before a pipelined reset: the spare's last user)
+        c->spare_tail = false;
+        if ((e = hipEventRecord(c->spare_free[0], c->walk_stream)) != hipSuccess) return e;
+        if ((e = hipEventRecord(c->spare_free[1], c->aux_stream)) != hipSuccess) return e;
+    }
     static const bool end_aux = getenv("FSX_TAIL_END_AUX") != nullptr;
     return hipEventRecord(c->tail_done[c->tail_par], c->tail_args.fork && end_aux ? c->aux_stream : c->walk_stream);
 }
@@ -384,6 +407,9 @@ void fsx_close(fsx_ctx *c) {
     hipFree(c->d_shard_stat); hipFree(c->d_shard_ticket);
     hipFree(c->d_rec_len); hipFree(c->d_rec_ts);
     for (int p = 0; p < fsx_ctx::kSets; ++p) { hipFree(c->rec_len_set[p]); hipFree(c->rec_ts_set[p]); }
+    hipFree(c->spare.table); hipFree(c->spare.tstate); hipFree(c->spare.heads); hipFree(c->spare.k6);
+    hipFree(c->spare.mir);
+    for (int k = 0; k < 2; ++k) if (c->spare_free[k]) hipEventDestroy(c->spare_free[k]);
     hipFree(c->idx_heads); hipFree(c->idx_k6); hipFree(c->idx_mir);
     hipFree(c->evict_buf);
     hipFree(c->d_rule_slot); hipFree(c->d_rule_lens); hipFree(c->d_rule_filter);
@@ -575,6 +601,7 @@ static int check_batch(fsx_ctx *c) {
 static int check_pipelined(fsx_ctx *c) {
     int rc = 0;
     bool failed = false;
+    uint32_t fgen = 0;   // (a failure cancels the later batches of its table generation only)
     for (int i = 1; i <= fsx_ctx::kSets; ++i) {   // oldest set first
         const int p = (c->par + i) % fsx_ctx::kSets;
         if (!c->fl_on[p]) continue;
@@ -582,12 +609,16 @@ static int check_pipelined(fsx_ctx *c) {
         BatchState h;
         HIPCHK(c, hipMemcpy(&h, c->fb[p].bs, sizeof(h), hipMemcpyDeviceToHost));
         note_batch(c, h);
-        if (!h.err && !failed) continue;
-        if (c->fl_born[p]) {
+        const bool cancelled = failed && c->fl_tgen[p] == fgen;
+        if (!h.err && !cancelled) continue;
+        // (a batch on tables a pipelined reset has since replaced changed nothing that is
+        // still visible: no rollback)
+        if (c->fl_born[p] && c->fl_tgen[p] == c->tgen) {
             const int r = rollback_batch(c, c->fl_born[p]);
             if (r) return r;
         }
         if (!failed) rc = batch_error(c, h.err);
+        if (!failed || c->fl_tgen[p] != fgen) fgen = c->fl_tgen[p];
         failed = true;
     }
     // (the tail-side cancel flag of split sliding-window batches: everything it cancelled
@@ -878,8 +909,10 @@ static int run_pipelined(fsx_ctx *c, const PacketIn &in0, const uint32_t *d_len,
         if (rc) return rc;
         fr = &frq;
     }
-    // the batch before this one (still in flight: its failure cancels this one)
-    const BatchState *prev = c->fl_on[c->par] ? c->fb[c->par].bs : nullptr;
+    // the batch before this one (still in flight: its failure cancels this one — not across
+    // a pipelined reset: this batch runs on other tables)
+    const BatchState *prev = c->fl_on[c->par] && !c->fresh_tables ? c->fb[c->par].bs : nullptr;
+    c->fresh_tables = false;
     const int old_par = c->par;
     use_front(c, q);
     c->par = q;
@@ -923,6 +956,7 @@ static int run_pipelined(fsx_ctx *c, const PacketIn &in0, const uint32_t *d_len,
     }
     c->fl_on[q] = true;
     c->fl_born[q] = c->id_gen;
+    c->fl_tgen[q] = c->tgen;
     if (split) {
         c->tail_pending = true;   // enqueued after the next batch's parse, or by the next sel()
         c->tail_par = q;
@@ -1428,8 +1462,60 @@ int fsx_get_stats(fsx_ctx *c, fsx_stats *out) {
     return 0;
 }
 
+// fsx_reset with pipelined batches in flight (DESIGN.md §3 "Pipelined resets"): the spare
+// table set becomes current and is cleared on the context stream once the tails that last
+// used it are done; the old set stays with the batches in flight (their tails captured it)
+// and becomes the spare. No host synchronization, and the next front does not wait for the
+// last tail. An in-flight batch's error still surfaces at the next synchronization; it
+// changed nothing visible (its tables are gone), so nothing is rolled back, and the first
+// batch after the reset does not cancel itself for it.
+static bool reset_swap_ok(const fsx_ctx *c) {
+    static const bool sync_reset = getenv("FSX_RESET_SYNC") != nullptr;
+    return !sync_reset && c->pipe == 1 && pipe_busy(c) && !c->pending && !c->flow_accum && !c->timing &&
+           c->cfg.limiter != FSX_LIMIT_SLIDING_WINDOW && c->tr_slots == 0 &&
+           !(c->cfg.flags & FSX_FLAG_EVICT_IDLE) && c->slots <= (1ull << 25);
+}
+
+static int reset_swap(fsx_ctx *c) {
+    HIPCHK(c, hipSetDevice(c->device));
+    fsx_ctx::TableSet &sp = c->spare;
+    if (!sp.table) {   // first use: allocate (fresh memory: cleared below like a reused set)
+        HIPCHK(c, hipMalloc(&sp.table, c->slots * sizeof(Slot)));
+        HIPCHK(c, hipMalloc(&sp.tstate, sizeof(TableState)));
+        HIPCHK(c, hipMemsetAsync(sp.tstate, 0, sizeof(TableState), c->stream));
+        HIPCHK(c, hipMalloc(&sp.heads, c->slots * 8));
+        HIPCHK(c, hipMemsetAsync(sp.heads, 0, c->slots * 8, c->stream));
+        HIPCHK(c, hipMalloc(&sp.k6, c->slots * 16));
+        if (c->idx_mir) HIPCHK(c, hipMalloc(&sp.mir, mir_bytes(c->idx_shift)));
+        for (int k = 0; k < 2; ++k)
+            if (!c->spare_free[k]) HIPCHK(c, hipEventCreateWithFlags(&c->spare_free[k], hipEventDisableTiming));
+    } else {   // the tails that last used the spare have finished before it is cleared
+        HIPCHK(c, hipStreamWaitEvent(c->stream, c->spare_free[0], 0));
+        HIPCHK(c, hipStreamWaitEvent(c->stream, c->spare_free[1], 0));
+    }
+    // the current set's last users: every tail enqueued so far, and a deferred one when it goes in
+    HIPCHK(c, hipEventRecord(c->spare_free[0], c->walk_stream));
+    HIPCHK(c, hipEventRecord(c->spare_free[1], c->aux_stream));
+    c->spare_tail = c->tail_pending;
+    std::swap(c->table, sp.table);
+    std::swap(c->tstate, sp.tstate);
+    std::swap(c->idx_heads, sp.heads);
+    std::swap(c->idx_k6, sp.k6);
+    std::swap(c->idx_mir, sp.mir);
+    std::swap(c->idx_epoch, sp.epoch);
+    c->pending_born = 0;
+    c->count_bound = 0;
+    HIPCHK(c, launch_clear(c->table, c->slots * sizeof(Slot), c->stream));
+    HIPCHK(c, hipMemsetAsync(c->tstate, 0, kTableStateResetBytes, c->stream));   // (path counters kept)
+    ++c->tgen;
+    c->fresh_tables = true;
+    c->pro_fence = true;   // (the next early prologue waits for the clear)
+    return next_epoch(c);
+}
+
 int fsx_reset(fsx_ctx *c) {
     if (!c) return -EINVAL;
+    if (reset_swap_ok(c)) return reset_swap(c);
     int rc = sel(c);
     if (rc) return rc;
     if (pipe_busy(c) && (rc = fsx_sync(c))) return rc;   // (pipelined batches)
@@ -1579,6 +1665,12 @@ int fsx_last_batch_info(fsx_ctx *c, uint64_t *info, int cap) {
     HIPCHK(c, hipMemcpy(&h, c->bs, sizeof(h), hipMemcpyDeviceToHost));
     TableState t;
     HIPCHK(c, hipMemcpy(&t, c->tstate, sizeof(t), hipMemcpyDeviceToHost));
+    if (c->spare.tstate) {   // (the path counters are since fsx_open: both table sets')
+        TableState t2;
+        HIPCHK(c, hipMemcpy(&t2, c->spare.tstate, sizeof(t2), hipMemcpyDeviceToHost));
+        t.n_hfast += t2.n_hfast;
+        t.n_hrun += t2.n_hrun;
+    }
     const uint64_t v[19] = {h.n_valid, h.nseg, h.n_new, h.any_v6, h.nonmono, h.max_len,
                             h.max_ts, h.allowed, h.dropped, h.n_rule, h.pay_ok, h.n_light,
                             c->last_evicted, h.hfast, h.n_admit, h.n_trans, t.n_hfast, t.n_hrun, h.ord};

@@ -280,7 +280,11 @@ int fsx_map_dump(fsx_ctx *ctx, int map_id, void *keys, void *values, size_t cap,
                  size_t *n_out);
 int fsx_get_stats(fsx_ctx *ctx, fsx_stats *out);
 /* Empty every per-source map and zero the stats (a fresh program load). The prefix
- * blocklists are operator configuration, like the loaded model, and stay. */
+ * blocklists are operator configuration, like the loaded model, and stay. With pipelined
+ * batches in flight (fsx_set_pipeline 1; fixed window / token bucket) it does not wait for
+ * them: a second set of tables is swapped in and cleared on the device, and the next batch
+ * overlaps their tails; an in-flight batch's error is then returned by the next fsx_sync
+ * (it changed nothing the reset keeps) and does not cancel the batches after the reset. */
 int fsx_reset(fsx_ctx *ctx);
 
 /* Scoring (model/model.py:132-137, decision model/model.py:206). */

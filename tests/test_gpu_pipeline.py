@@ -385,3 +385,61 @@ def test_pipelined_sliding_window_history_full_then_fits(native, oracle):
                 # after the rollback the context works on: the small batch now runs and fits
                 cp.verdict_batch(*batches[3])
                 cp.sync()
+
+
+@pytest.mark.parametrize("same_batch", [False, True])
+def test_pipelined_reset_every_batch(native, oracle, same_batch):
+    """fsx_reset after every pipelined batch (the bench's cold leg): each reset swaps in the
+    spare table set (slots, scalars, index) and clears it on the device after the tails that
+    last used it, without a host synchronization and without ordering the next front after
+    the last tail (DESIGN.md §3 "Pipelined resets"). Every batch equals the oracle from empty
+    maps; the final maps are the last batch's; features + scores of every batch."""
+    batches = _config2_batches(oracle, 1 << 19, [0, 150_000, 300_000, 420_000, 1 << 19])
+    if same_batch:
+        batches = [batches[1]] * 5
+
+    def between(j, c, o):
+        if j < len(batches) - 1:
+            c.reset()
+            o.reset()
+    _run(native, oracle, batches, between=between)
+
+
+def test_pipelined_failed_batch_then_reset(native, oracle):
+    """A batch fails (max_entries) and the caller resets before its error is seen: the batch
+    after the reset runs on fresh tables and is not cancelled; the error surfaces at sync;
+    the maps are those of the batch after the reset alone."""
+    from flowsentryx_amd import lib, synth
+    import torch
+    rng = np.random.default_rng(79)
+    cfg = dict(pps_threshold=5, window_ns=100_000, block_ns=300_000)
+    h1, l1, t1 = rand_stream(rng, 3000, 120, dt_max=200)
+    big = synth.records([synth.frame_ipv4_udp(bytes([10, 77, i // 256, i % 256]), 90) for i in range(400)])
+    lb = np.full(400, 90, np.uint32)
+    tb = t1[-1] + np.arange(1, 401, dtype=np.uint64)
+    h3, l3, t3 = rand_stream(rng, 3000, 120, dt_max=200, v6_frac=0.3)
+    t3 = t3 + tb[-1]
+    keep = []
+
+    def launch(c, h, l, t):
+        d = [_dev(torch, h), _dev(torch, l), _dev(torch, t), torch.empty(len(l), dtype=torch.uint8, device="cuda")]
+        keep.append(d)
+        c.verdict_batch_device(d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr(), len(l), d[3].data_ptr())
+        return d[3]
+
+    with native.FsxContext(max_batch=4096, max_entries=300, **cfg) as c:
+        c.set_pipeline(True)
+        launch(c, h1, l1, t1)
+        launch(c, big, lb, tb)          # fails: 400 new sources > 300 - 120
+        c.reset()                       # (pipelined: no wait, the spare tables swapped in)
+        v3 = launch(c, h3, l3, t3)
+        with pytest.raises(lib.FsxError) as e:
+            c.sync()
+        assert e.value.code == -errno.ENOSPC
+        o = oracle.Oracle(max_entries=1 << 12, **cfg)
+        assert np.array_equal(v3.cpu().numpy(), o.batch(h3, l3, t3))
+        assert_same_state(c, o)
+        v4 = launch(c, h3, l3, t3 + t3[-1])   # (the same 225 sources: no new ones)
+        c.sync()
+        assert np.array_equal(v4.cpu().numpy(), o.batch(h3, l3, t3 + t3[-1]))
+        assert_same_state(c, o)
