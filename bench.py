@@ -860,8 +860,11 @@ def main():
         # r-th 1/8 share of the stream (weak scaling: at N = 8 the whole of config 4)
         p4, _ = synth.config_params(4)
         n4 = args.config4_packets or int(p4.n) // 8
+        # (every step the same share from empty maps; unpipelined: pipelined across the resets
+        # measured no faster here, the GPU already saturated — FSX_C4_PIPELINED=1 for the A/B)
         r4 = run_workload(4, n4, max(1, args.leg_steps // 2), 1, not args.no_mlp,
-                          kernel_timing=args.leg_timing, check=not args.no_check and world == 1)
+                          kernel_timing=args.leg_timing, check=not args.no_check and world == 1,
+                          pipelined=os.environ.get("FSX_C4_PIPELINED") == "1")
         r4.pop("d")
         torch.cuda.empty_cache()
         leg = {"value": round(r4["mpps"], 2), "unit": "Mpps", "ms_per_step": round(r4["ms_step"], 4),

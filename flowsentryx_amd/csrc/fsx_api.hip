@@ -181,8 +181,12 @@ struct fsx_ctx {
         uint32_t epoch = 1;
     };
     TableSet spare{};
-    hipEvent_t spare_free[2]{};       // walk / aux stream after the last tails on the spare set
-    bool spare_tail = false;          // ... and the deferred tail too, when it is enqueued
+    // the spare's last users: the walk / aux streams after its tails (and after the deferred
+    // tail too, when it is enqueued), the context stream after its fronts
+    hipEvent_t spare_free[3]{};
+    bool spare_tail = false;
+    hipStream_t clr_stream = nullptr; // the swapped-in set is cleared here, beside the last front
+    hipEvent_t clr_done = nullptr;
     uint32_t tgen = 0;                // table generation: one per pipelined reset
     uint32_t fl_tgen[kSets]{};
     bool fresh_tables = false;        // the next pipelined batch starts a table generation
@@ -409,7 +413,9 @@ void fsx_close(fsx_ctx *c) {
     for (int p = 0; p < fsx_ctx::kSets; ++p) { hipFree(c->rec_len_set[p]); hipFree(c->rec_ts_set[p]); }
     hipFree(c->spare.table); hipFree(c->spare.tstate); hipFree(c->spare.heads); hipFree(c->spare.k6);
     hipFree(c->spare.mir);
-    for (int k = 0; k < 2; ++k) if (c->spare_free[k]) hipEventDestroy(c->spare_free[k]);
+    for (int k = 0; k < 3; ++k) if (c->spare_free[k]) hipEventDestroy(c->spare_free[k]);
+    if (c->clr_done) hipEventDestroy(c->clr_done);
+    if (c->clr_stream) hipStreamDestroy(c->clr_stream);
     hipFree(c->idx_heads); hipFree(c->idx_k6); hipFree(c->idx_mir);
     hipFree(c->evict_buf);
     hipFree(c->d_rule_slot); hipFree(c->d_rule_lens); hipFree(c->d_rule_filter);
@@ -669,6 +675,8 @@ int fsx_stream_wait_batches(fsx_ctx *c, void *hip_stream, int all) {
     return 0;
 }
 
+static int alloc_spare(fsx_ctx *c);
+
 int fsx_set_pipeline(fsx_ctx *c, int on) {
     if (!c) return -EINVAL;
     int rc = fsx_sync(c);
@@ -714,6 +722,10 @@ int fsx_set_pipeline(fsx_ctx *c, int on) {
         c->par = 0;
     }
     c->pipe = on < 0 ? 0 : on > 2 ? 1 : on;
+    if (c->pipe == 1) {   // (resets between pipelined batches: DESIGN.md §3 "Pipelined resets")
+        const int r = alloc_spare(c);
+        if (r) return r;
+    }
     return 0;
 }
 
@@ -1471,31 +1483,63 @@ int fsx_get_stats(fsx_ctx *c, fsx_stats *out) {
 // batch after the reset does not cancel itself for it.
 static bool reset_swap_ok(const fsx_ctx *c) {
     static const bool sync_reset = getenv("FSX_RESET_SYNC") != nullptr;
-    return !sync_reset && c->pipe == 1 && pipe_busy(c) && !c->pending && !c->flow_accum && !c->timing &&
-           c->cfg.limiter != FSX_LIMIT_SLIDING_WINDOW && c->tr_slots == 0 &&
-           !(c->cfg.flags & FSX_FLAG_EVICT_IDLE) && c->slots <= (1ull << 25);
+    return !sync_reset && c->pipe == 1 && c->spare.table && pipe_busy(c) && !c->pending && !c->flow_accum &&
+           !c->timing && !(c->cfg.flags & FSX_FLAG_EVICT_IDLE);
+}
+
+// The spare table set, allocated with pipelining (fsx_set_pipeline 1) for the limiters and table
+// sizes a pipelined reset serves: the table and index memory once more.
+static int alloc_spare(fsx_ctx *c) {
+    if (c->spare.table || c->cfg.limiter == FSX_LIMIT_SLIDING_WINDOW || c->tr_slots != 0 ||
+        c->slots > (1ull << 25) || getenv("FSX_RESET_SYNC"))
+        return 0;
+    fsx_ctx::TableSet sp{};
+    auto build = [&]() -> hipError_t {
+        hipError_t e;
+        if ((e = hipMalloc(&sp.table, c->slots * sizeof(Slot))) != hipSuccess) return e;
+        if ((e = hipMalloc(&sp.tstate, sizeof(TableState))) != hipSuccess) return e;
+        if ((e = hipMemset(sp.tstate, 0, sizeof(TableState))) != hipSuccess) return e;
+        if ((e = hipMalloc(&sp.heads, c->slots * 8)) != hipSuccess) return e;
+        if ((e = hipMemset(sp.heads, 0, c->slots * 8)) != hipSuccess) return e;
+        if ((e = hipMalloc(&sp.k6, c->slots * 16)) != hipSuccess) return e;
+        if (c->idx_mir && (e = hipMalloc(&sp.mir, mir_bytes(c->idx_shift))) != hipSuccess) return e;
+        for (int k = 0; k < 3; ++k)
+            if (!c->spare_free[k] && (e = hipEventCreateWithFlags(&c->spare_free[k], hipEventDisableTiming)) != hipSuccess)
+                return e;
+        if (!c->clr_done && (e = hipEventCreateWithFlags(&c->clr_done, hipEventDisableTiming)) != hipSuccess) return e;
+        if (!c->clr_stream && (e = hipStreamCreateWithFlags(&c->clr_stream, hipStreamNonBlocking)) != hipSuccess)
+            return e;
+        // (nothing uses the new set yet: its "last users" are already done)
+        for (int k = 0; k < 3; ++k)
+            if ((e = hipEventRecord(c->spare_free[k], c->stream)) != hipSuccess) return e;
+        return hipSuccess;
+    };
+    const hipError_t e = build();
+    if (e != hipSuccess) {   // (no spare: resets stay synchronous)
+        hipFree(sp.table); hipFree(sp.tstate); hipFree(sp.heads); hipFree(sp.k6); hipFree(sp.mir);
+        return set_err(c, -ENOMEM, "spare table set: %s", hipGetErrorString(e));
+    }
+    c->spare = sp;
+    return 0;
 }
 
 static int reset_swap(fsx_ctx *c) {
     HIPCHK(c, hipSetDevice(c->device));
     fsx_ctx::TableSet &sp = c->spare;
-    if (!sp.table) {   // first use: allocate (fresh memory: cleared below like a reused set)
-        HIPCHK(c, hipMalloc(&sp.table, c->slots * sizeof(Slot)));
-        HIPCHK(c, hipMalloc(&sp.tstate, sizeof(TableState)));
-        HIPCHK(c, hipMemsetAsync(sp.tstate, 0, sizeof(TableState), c->stream));
-        HIPCHK(c, hipMalloc(&sp.heads, c->slots * 8));
-        HIPCHK(c, hipMemsetAsync(sp.heads, 0, c->slots * 8, c->stream));
-        HIPCHK(c, hipMalloc(&sp.k6, c->slots * 16));
-        if (c->idx_mir) HIPCHK(c, hipMalloc(&sp.mir, mir_bytes(c->idx_shift)));
-        for (int k = 0; k < 2; ++k)
-            if (!c->spare_free[k]) HIPCHK(c, hipEventCreateWithFlags(&c->spare_free[k], hipEventDisableTiming));
-    } else {   // the tails that last used the spare have finished before it is cleared
-        HIPCHK(c, hipStreamWaitEvent(c->stream, c->spare_free[0], 0));
-        HIPCHK(c, hipStreamWaitEvent(c->stream, c->spare_free[1], 0));
+    // (two resets with no batch between: the tail deferred before the first one uses the
+    // spare — it goes in now, so the events below cover it)
+    if (c->spare_tail && c->tail_pending) {
+        const hipError_t e = flush_tail(c, c->front_done);
+        if (e != hipSuccess) return set_err(c, -EIO, "pipelined tail: %s", hipGetErrorString(e));
     }
-    // the current set's last users: every tail enqueued so far, and a deferred one when it goes in
+    // the spare is cleared on its own stream once its last users are done — beside the front
+    // just enqueued, which uses the current set; the next front waits for the clear
+    for (int k = 0; k < 3; ++k) HIPCHK(c, hipStreamWaitEvent(c->clr_stream, c->spare_free[k], 0));
+    // the current set's last users: every tail enqueued so far, the fronts on the context
+    // stream, and the deferred tail when it goes in (flush_tail)
     HIPCHK(c, hipEventRecord(c->spare_free[0], c->walk_stream));
     HIPCHK(c, hipEventRecord(c->spare_free[1], c->aux_stream));
+    HIPCHK(c, hipEventRecord(c->spare_free[2], c->stream));
     c->spare_tail = c->tail_pending;
     std::swap(c->table, sp.table);
     std::swap(c->tstate, sp.tstate);
@@ -1505,12 +1549,19 @@ static int reset_swap(fsx_ctx *c) {
     std::swap(c->idx_epoch, sp.epoch);
     c->pending_born = 0;
     c->count_bound = 0;
-    HIPCHK(c, launch_clear(c->table, c->slots * sizeof(Slot), c->stream));
-    HIPCHK(c, hipMemsetAsync(c->tstate, 0, kTableStateResetBytes, c->stream));   // (path counters kept)
+    HIPCHK(c, launch_clear(c->table, c->slots * sizeof(Slot), c->clr_stream));
+    HIPCHK(c, hipMemsetAsync(c->tstate, 0, kTableStateResetBytes, c->clr_stream));   // (path counters kept)
+    if (++c->idx_epoch == 0x10000u) {   // (next_epoch, on the clear stream)
+        HIPCHK(c, hipMemsetAsync(c->idx_heads, 0, c->slots * 8, c->clr_stream));
+        c->idx_epoch = 1;
+    }
+    if (c->idx_mir) HIPCHK(c, hipMemsetAsync(c->idx_mir, 0, mir_bytes(c->idx_shift), c->clr_stream));
+    HIPCHK(c, hipEventRecord(c->clr_done, c->clr_stream));
+    HIPCHK(c, hipStreamWaitEvent(c->stream, c->clr_done, 0));
     ++c->tgen;
     c->fresh_tables = true;
-    c->pro_fence = true;   // (the next early prologue waits for the clear)
-    return next_epoch(c);
+    c->pro_fence = true;   // (the next early prologue waits for the clear, via the context stream)
+    return 0;
 }
 
 int fsx_reset(fsx_ctx *c) {

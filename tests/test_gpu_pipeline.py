@@ -387,8 +387,8 @@ def test_pipelined_sliding_window_history_full_then_fits(native, oracle):
                 cp.sync()
 
 
-@pytest.mark.parametrize("same_batch", [False, True])
-def test_pipelined_reset_every_batch(native, oracle, same_batch):
+@pytest.mark.parametrize("same_batch,resets", [(False, 1), (True, 1), (False, 2)])
+def test_pipelined_reset_every_batch(native, oracle, same_batch, resets):
     """fsx_reset after every pipelined batch (the bench's cold leg): each reset swaps in the
     spare table set (slots, scalars, index) and clears it on the device after the tails that
     last used it, without a host synchronization and without ordering the next front after
@@ -400,7 +400,8 @@ def test_pipelined_reset_every_batch(native, oracle, same_batch):
 
     def between(j, c, o):
         if j < len(batches) - 1:
-            c.reset()
+            for _ in range(resets):   # (two in a row: the second swaps the sets back)
+                c.reset()
             o.reset()
     _run(native, oracle, batches, between=between)
 
