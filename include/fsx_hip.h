@@ -231,7 +231,9 @@ int fsx_sync(fsx_ctx *ctx);
  * admission flag runs each batch whole on the context stream (no overlap, but still no host
  * synchronization per call); so does every
  * batch with on = 2 (a caller that reuses input buffers in stream order); timed batches
- * (fsx_enable_timing) run unpipelined. on = 0 turns it off. */
+ * (fsx_enable_timing) run unpipelined. on = 0 turns it off. on = 1 also allocates a second
+ * table set (fixed window / token bucket, tables of <= 2^25 slots) so that fsx_reset between
+ * pipelined batches does not wait for them. */
 int fsx_set_pipeline(fsx_ctx *ctx, int on);
 /* Order a caller's hipStream_t after the batches enqueued so far, without a host
  * synchronization: `hip_stream` waits for the context stream's work and for every split
