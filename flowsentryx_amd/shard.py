@@ -78,15 +78,22 @@ def _a2a(out: torch.Tensor, inp: torch.Tensor, out_splits, in_splits, group=None
         dist.all_to_all_single(out, inp, out_splits, in_splits, group=group)
 
 
+_A2A_LISTS = True   # the backend takes list all-to-alls (cleared at the first refusal)
+
+
 def _a2a_views(out: torch.Tensor, out_splits, ins, group=None):
     """all-to-all of one view per destination (not one contiguous tensor: a regions pack,
     HipShardEngine.send_views) into `out` split by out_splits. RCCL takes the views as they
     are (grouped send / receive); gloo gets them concatenated."""
-    if dist.get_backend(group) == "gloo":
-        inp = torch.cat(ins) if ins else out[:0]
-        _a2a(out, inp, out_splits, [int(x.numel()) for x in ins], group)
-    else:
-        dist.all_to_all(list(out.split(list(out_splits))), list(ins), group=group)
+    global _A2A_LISTS
+    if dist.get_backend(group) != "gloo" and _A2A_LISTS:
+        try:
+            dist.all_to_all(list(out.split(list(out_splits))), list(ins), group=group)
+            return
+        except (RuntimeError, ValueError):   # (a backend without list all-to-all: one copy)
+            _A2A_LISTS = False
+    inp = torch.cat(ins) if ins else out[:0]
+    _a2a(out, inp, out_splits, [int(x.numel()) for x in ins], group)
 
 
 def _all_reduce_sum(t: torch.Tensor, group=None) -> torch.Tensor:
