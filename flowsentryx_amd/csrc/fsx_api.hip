@@ -187,6 +187,7 @@ struct fsx_ctx {
     bool spare_tail = false;
     hipStream_t clr_stream = nullptr; // the swapped-in set is cleared here, beside the last front
     hipEvent_t clr_done = nullptr;
+    bool spare_dirty = false;         // the spare holds lines of table generations that come round again
     uint32_t tgen = 0;                // table generation: one per pipelined reset
     uint32_t fl_tgen[kSets]{};
     bool fresh_tables = false;        // the next pipelined batch starts a table generation
@@ -1481,6 +1482,22 @@ int fsx_get_stats(fsx_ctx *c, fsx_stats *out) {
 // last tail. An in-flight batch's error still surfaces at the next synchronization; it
 // changed nothing visible (its tables are gone), so nothing is rolled back, and the first
 // batch after the reset does not cancel itself for it.
+// Clear-free reset (DESIGN.md §3 "Clear-free reset"): a slot's tag word carries the table
+// generation (Limits::tgen), and a line of another generation reads as empty — to the walkers
+// (a fresh source's stale line holds no state), the map dumps, the index rebuild, the
+// blocklist export and the history rebuild — so fsx_reset moves to the next generation
+// instead of clearing the table (config 5: 32 GB of stores per reset). At the 16-bit wrap
+// the table is cleared. FSX_RESET_CLEAR=1: clear at every reset (A/B). Returns the wrap.
+static bool next_table_gen(fsx_ctx *c) {
+    if (++c->lim.tgen < 0x10000u) return false;
+    c->lim.tgen = 0;
+    return true;
+}
+static bool reset_clears() {
+    static const bool clear = getenv("FSX_RESET_CLEAR") != nullptr;
+    return clear;
+}
+
 static bool reset_swap_ok(const fsx_ctx *c) {
     static const bool sync_reset = getenv("FSX_RESET_SYNC") != nullptr;
     return !sync_reset && c->pipe == 1 && c->spare.table && pipe_busy(c) && !c->pending && !c->flow_accum &&
@@ -1549,7 +1566,12 @@ static int reset_swap(fsx_ctx *c) {
     std::swap(c->idx_epoch, sp.epoch);
     c->pending_born = 0;
     c->count_bound = 0;
-    HIPCHK(c, launch_clear(c->table, c->slots * sizeof(Slot), c->clr_stream));
+    // clear-free (the next table generation): only a set that holds lines of generations that
+    // come round again — at the 16-bit wrap — is cleared
+    const bool wrap = next_table_gen(c);
+    if (c->spare_dirty || wrap || reset_clears())
+        HIPCHK(c, launch_clear(c->table, c->slots * sizeof(Slot), c->clr_stream));
+    c->spare_dirty = wrap;   // (the set just swapped out: its lines' generations come round again)
     HIPCHK(c, hipMemsetAsync(c->tstate, 0, kTableStateResetBytes, c->clr_stream));   // (path counters kept)
     if (++c->idx_epoch == 0x10000u) {   // (next_epoch, on the clear stream)
         HIPCHK(c, hipMemsetAsync(c->idx_heads, 0, c->slots * 8, c->clr_stream));
@@ -1572,7 +1594,10 @@ int fsx_reset(fsx_ctx *c) {
     if (pipe_busy(c) && (rc = fsx_sync(c))) return rc;   // (pipelined batches)
     c->pending_born = 0;   // the whole table is wiped: no rollback of a pending batch
     c->count_bound = 0;    // (no source is tracked after the reset: ADVICE r04)
-    HIPCHK(c, launch_clear(c->table, c->slots * sizeof(Slot), c->stream));
+    // clear-free: the next table generation (every line of this one reads as empty)
+    const bool wrap = next_table_gen(c);
+    if (wrap || reset_clears()) HIPCHK(c, launch_clear(c->table, c->slots * sizeof(Slot), c->stream));
+    if (wrap && c->spare.table) c->spare_dirty = true;
     HIPCHK(c, hipMemsetAsync(c->tstate, 0, kTableStateResetBytes, c->stream));   // (path counters kept)
     return next_epoch(c);   // (the prefix blocklists stay: configuration)   // every index head reads empty
 }
@@ -1701,7 +1726,8 @@ int fsx_flows_end(fsx_ctx *c, uint8_t *d_keys16, uint8_t *d_family, float *d_fea
     c->flow_accum = false;
     const FlowRequest fr = flow_request(c, d_keys16, d_family, d_features, d_prob, d_malicious, cap);
     unsigned long long *cnt = d_rows ? reinterpret_cast<unsigned long long *>(d_rows) : c->d_flow_rows;
-    hipError_t e = launch_flows_end(c->d_slot_acc, c->flow_epoch, c->table, c->slots, fr.keys16, fr.fam, fr.feat,
+    hipError_t e = launch_flows_end(c->d_slot_acc, c->flow_epoch, c->table, c->slots, c->lim.tgen, fr.keys16, fr.fam,
+                                    fr.feat,
                                     fr.prob, fr.dec, fr.cap, fr.score, cnt, c->stream);
     if (e != hipSuccess) return set_err(c, -EIO, "flows end: %s", hipGetErrorString(e));
     return 0;
@@ -1822,7 +1848,7 @@ int fsx_blocklist_export_device(fsx_ctx *c, void *d_entries, size_t cap, uint64_
     int rc = sel(c);
     if (rc) return rc;
     // (stream-ordered after a pending batch; its errors surface at the next fsx_sync)
-    hipError_t e = launch_blocklist_export(c->table, c->lim.table_mask, reinterpret_cast<ShardBlock *>(d_entries),
+    hipError_t e = launch_blocklist_export(c->table, c->lim.table_mask, c->lim.tgen, reinterpret_cast<ShardBlock *>(d_entries),
                                            cap, reinterpret_cast<unsigned long long *>(d_count), c->stream);
     if (e != hipSuccess) return set_err(c, -EIO, "blocklist export: %s", hipGetErrorString(e));
     return 0;

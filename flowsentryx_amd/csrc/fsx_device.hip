@@ -75,6 +75,7 @@ struct IdTable {
     // 0: a new source's Slot is left to its walker (the fixed window's k_parse: one random
     // line per insert, the head's; SlotKeys)
     uint32_t init = 1;
+    uint32_t tgen = 0;          // the table generation its new slots are tagged with (Limits::tgen)
 };
 
 __device__ __forceinline__ uint64_t id_start(const IdTable &T, uint32_t tag, const uint32_t k[4]) {
@@ -103,7 +104,7 @@ __device__ __forceinline__ uint32_t id_resolve(const IdTable &T, uint32_t tag, c
                         sl.flags = T.born << kBornShift;
                         sl.key[0] = k[0]; sl.key[1] = k[1]; sl.key[2] = k[2]; sl.key[3] = k[3];
                         sl.pps = sl.bps = sl.tt = sl.till = sl.aux = 0;
-                        sl.tag = tag;
+                        sl.tag = slot_tag(tag, T.tgen);
                     }
                     // (a reader that misses the new entry, 0 in a stale line, defers to this
                     // full protocol; no other value can be seen in this epoch)
@@ -2309,7 +2310,7 @@ __global__ __launch_bounds__(256) void k_ord_claim(BatchState *bs, const uint32_
                 const uint32_t fl = (st.has_st ? SLOT_HAS_ST : 0u) | (st.has_bl ? SLOT_HAS_BL : 0u) |
                                     (idt.born << kBornShift);
                 uint4 *p = reinterpret_cast<uint4 *>(table + pos);
-                p[0] = make_uint4(tag, fl, k[0], tag == 2 ? k[1] : 0u);
+                p[0] = make_uint4(slot_tag(tag, lim.tgen), fl, k[0], tag == 2 ? k[1] : 0u);
                 p[1] = make_uint4(tag == 2 ? k[2] : 0u, tag == 2 ? k[3] : 0u, (uint32_t)st.pps, (uint32_t)(st.pps >> 32));
                 p[2] = make_uint4((uint32_t)st.bps, (uint32_t)(st.bps >> 32), (uint32_t)st.tt, (uint32_t)(st.tt >> 32));
                 p[3] = make_uint4((uint32_t)st.till, (uint32_t)(st.till >> 32), 0u, 0u);
@@ -2407,9 +2408,9 @@ __device__ __forceinline__ uint32_t table_claim(Slot *table, const Limits &lim, 
                                                 uint32_t tag, const uint32_t k[4]) {
     uint64_t i = probe_start(tag, k, lim.seed, lim.table_mask, lim.test_flags);
     for (uint64_t probes = 0; probes <= lim.table_mask; ++probes) {
-        if (table[i].tag == 0) {
+        if (slot_fam(table[i].tag, lim.tgen) == 0) {
             Slot &s = table[i];
-            s.tag = tag;
+            s.tag = slot_tag(tag, lim.tgen);
             s.flags = 0;
             s.key[0] = k[0]; s.key[1] = k[1]; s.key[2] = k[2]; s.key[3] = k[3];
             s.pps = s.bps = s.tt = s.till = s.aux = 0;
@@ -2622,7 +2623,7 @@ __global__ __launch_bounds__(256) void k_admit_insert(BatchState *bs, const Tabl
             ++na;
         } else {                  // transient: a fresh slot of its own for this batch
             Slot &sl = table[tbase + g];
-            sl.tag = tag;
+            sl.tag = slot_tag(tag, lim.tgen);
             sl.flags = 0;
             sl.key[0] = k[0]; sl.key[1] = k[1]; sl.key[2] = k[2]; sl.key[3] = k[3];
             sl.pps = sl.bps = sl.tt = sl.till = sl.aux = 0;
@@ -2649,17 +2650,18 @@ __global__ __launch_bounds__(256) void k_index_rebuild(Slot *table, Limits lim, 
     for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i <= lim.table_mask;
          i += (uint64_t)gridDim.x * 256u) {
         Slot &s = table[i];
-        if (s.tag == 0) continue;
+        const uint32_t fam = slot_fam(s.tag, lim.tgen);
+        if (fam == 0) continue;
         if (born && (s.flags >> kBornShift) == born) {
             s.tag = 0;
             s.flags = 0;
             continue;
         }
-        if (s.tag == 2) {
+        if (fam == 2) {
             X.k6[i * 4 + 0] = s.key[1]; X.k6[i * 4 + 1] = s.key[2]; X.k6[i * 4 + 2] = s.key[3];
         }
-        X.heads[i] = id_head(X.epoch, kIdReady, s.tag, s.key[0]);
-        if (s.tag == 1) mir_publish(X.mir, X.mir_shift, lim.table_mask, lim.seed, i, s.key[0]);
+        X.heads[i] = id_head(X.epoch, kIdReady, fam, s.key[0]);
+        if (fam == 1) mir_publish(X.mir, X.mir_shift, lim.table_mask, lim.seed, i, s.key[0]);
     }
 }
 
@@ -2820,9 +2822,10 @@ __device__ __forceinline__ void walk_short(const SV &sv, const BatchState *bs,
             continue;
         }
         const SlotLine L0 = load_line(sl);
-        FwState st = state_of(L0);
         const uint32_t flags0 = L0.q[0].y;
-        const bool fresh = knew && tag_of(L0) == 0;
+        const bool fresh = knew && slot_fam(tag_of(L0), lim.tgen) == 0;
+        // (a fresh slot's line may hold an older table generation's source: no state)
+        FwState st = fresh ? FwState{false, false, 0, 0, 0, 0} : state_of(L0);
         const unsigned long long hd = knew ? K.heads[si] : 0ull;
         MarkWriter<false> mw{marks, 0};
         walk_fixed_exact_thread(sv, a, b, lim, mw, st);
@@ -2870,9 +2873,9 @@ __device__ __forceinline__ void walk_long(const SV &sv, const BatchState *bs,
         if (si == kNoSlot) continue;   // (k_ord_claim walked it)
         Slot &sl = table[si];
         const SlotLine L0 = load_line(sl);
-        FwState st = state_of(L0);
         const uint32_t flags0 = L0.q[0].y;
-        const bool fresh = knew && tag_of(L0) == 0;
+        const bool fresh = knew && slot_fam(tag_of(L0), lim.tgen) == 0;
+        FwState st = fresh ? FwState{false, false, 0, 0, 0, 0} : state_of(L0);
         const unsigned long long hd = knew ? K.heads[si] : 0ull;
         const bool fast = glob_fast && (!st.has_st || (st.tt <= ~0ull - lim.window &&
                                                        st.pps < kBig && st.bps < kBig));
@@ -2922,8 +2925,10 @@ __device__ __forceinline__ void walk_heavy(const SV &sv, const BatchState *bs, c
     const uint32_t a = base0[bs->light_b + h], b = a + c;
     const uint32_t si = pk_id(sv.S[a], lim.table_mask);
     Slot &sl = table[si];
-    FwState st = load_state(sl);
-    // (unresolved heavy sources, under prefix rules, are inserted by k_parse: lazily)
+    // (unresolved heavy sources, under prefix rules, are inserted by k_parse: lazily — a line
+    // of another table generation is a new source's, with no state)
+    const bool adopt = K.heads && slot_fam(sl.tag, lim.tgen) == 0;
+    FwState st = adopt ? FwState{false, false, 0, 0, 0, 0} : load_state(sl);
     const unsigned long long hd = K.heads ? K.heads[si] : 0ull;
     const bool fast = glob_fast && (!st.has_st || (st.tt <= ~0ull - lim.window &&
                                                    st.pps < kBig && st.bps < kBig));
@@ -2934,7 +2939,7 @@ __device__ __forceinline__ void walk_heavy(const SV &sv, const BatchState *bs, c
     heavy_list_close(H, (int)h, a, b, mw);
     if (lane_id() == 0) {
         store_state(sl, st);
-        if (K.heads && sl.tag == 0) slot_adopt(sl, K, si, hd);
+        if (adopt) slot_adopt(sl, K, si, hd, lim.tgen);
     }
 }
 
@@ -3320,7 +3325,7 @@ hipError_t launch_tail(const TailArgs &a) {
     const HeavyLists hlists{tagh ? reinterpret_cast<uint32_t *>(sc.packed[0]) : nullptr, sc.heavy,
                             tstate, bs};
     // (lazy slots: the fixed window's walkers write a new source's family and key)
-    const SlotKeys skeys{a.lazy ? a.X.heads : nullptr, a.X.k6, a.lazy && a.fresh_bit ? 1u : 0u};
+    const SlotKeys skeys{a.lazy ? a.X.heads : nullptr, a.X.k6, a.lazy && a.fresh_bit ? 1u : 0u, lim.tgen};
     // the heavy runs' walker and flow sums, forked right after the sort (A/B, config 2: right
     // after pass 0 they slowed passes 1-2, after the heads they delayed the walkers; a fourth
     // stream shared a hardware queue with the limiter chain)
@@ -3429,6 +3434,7 @@ hipError_t launch_tail(const TailArgs &a) {
         IdTable idt{a.X.heads, a.X.k6, lim.table_mask, lim.seed, a.X.epoch, lim.test_flags, table, a.id_gen, coh,
                     a.X.mir, a.X.mir_shift};
         idt.init = 0;   // (lazy slots: the walkers write a new source's line)
+        idt.tgen = lim.tgen;
         // (the segment-order buffer holds the IPv6 lists, pass 0's tile rows — unused without
         // the heavy sort — their per-block counts)
         static const bool no_region = getenv("FSX_ORD_NO_REGION") != nullptr;   // A/B: global claims only
@@ -3457,8 +3463,9 @@ hipError_t launch_tail(const TailArgs &a) {
         k_admit_scan<<<1, 256, 0, st>>>(bs, sc.admit_cnt, n);
         k_admit_rank<1><<<gt, 256, 0, st>>>(bs, sc.admit_rank, n, sc.admit_cnt);
         static const uint32_t coherent = getenv("FSX_ID_COHERENT") ? 1u : 0u;
-        const IdTable pidt{a.X.heads, a.X.k6, lim.table_mask, lim.seed, a.X.epoch, lim.test_flags, table, a.id_gen,
-                           coherent, a.X.mir, a.X.mir_shift};
+        IdTable pidt{a.X.heads, a.X.k6, lim.table_mask, lim.seed, a.X.epoch, lim.test_flags, table, a.id_gen,
+                     coherent, a.X.mir, a.X.mir_shift};
+        pidt.tgen = lim.tgen;
         k_admit_insert<<<ga, 256, 0, st>>>(bs, tstate, S, sc.seg_start, sc.seg_slot, in, pidt, lim, sc.admit_rank,
                                            table, lim.table_mask + 1);
         k_admit_commit<<<1, 1, 0, st>>>(bs, tstate);
@@ -3619,11 +3626,12 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
     // kernels after the heads (launch_tail)
     const bool admit = do_limit && (lim.test_flags & kFlagAdmit) != 0;
     const uint64_t bmask = admit ? lim.admit_mask : lim.table_mask;   // the per-batch id table's
-    const IdTable idt = do_limit && !admit
+    IdTable idt = do_limit && !admit
         ? IdTable{X.heads, X.k6, lim.table_mask, lim.seed, X.epoch, lim.test_flags, table, id_gen, coherent,
                   X.mir, X.mir_shift}
         : IdTable{reinterpret_cast<unsigned long long *>(sc.id_tab), sc.id_tab + 2 * (bmask + 1),
                   bmask, lim.seed, id_gen, lim.test_flags, nullptr, 0, coherent};
+    idt.tgen = lim.tgen;
     if ((e = hipMemsetAsync(sc.sort_ctl, 0, kSortCtlWords * 4, sp0)) != hipSuccess) return e;
     if (admit && (e = hipMemsetAsync(sc.admit_rank, 0, (size_t)n * 4, sp0)) != hipSuccess) return e;
     mark("start");
@@ -3948,8 +3956,9 @@ __global__ __launch_bounds__(256) void k_map_import(Slot *table, Limits lim, Tab
     const uint32_t tag = map_tag(map_id), bit = map_bit(map_id);
     const uint32_t kw = tag == 2 ? 4u : 1u;
     const uint32_t vw = bit == SLOT_HAS_ST ? 3u : bit == SLOT_HAS_TB ? 2u : 1u;
-    const IdTable idt{X.heads, X.k6, lim.table_mask, lim.seed, X.epoch, lim.test_flags, table, born, 0u,
-                      X.mir, X.mir_shift};
+    IdTable idt{X.heads, X.k6, lim.table_mask, lim.seed, X.epoch, lim.test_flags, table, born, 0u,
+                X.mir, X.mir_shift};
+    idt.tgen = lim.tgen;
     uint32_t fresh_n = 0;
     for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) {
         uint32_t k[4] = {0, 0, 0, 0};
@@ -4020,7 +4029,7 @@ __global__ __launch_bounds__(256) void k_evict_compact(const Slot *__restrict__ 
     for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i <= lim.table_mask;
          i += (uint64_t)gridDim.x * 256u) {
         const Slot s = table[i];
-        if (s.tag == 0 || !slot_live(s, lim, now0)) continue;
+        if (slot_fam(s.tag, lim.tgen) == 0 || !slot_live(s, lim, now0)) continue;
         const unsigned long long o = atomicAdd(&scal[1], 1ull);
         if (o < cap) buf[o] = s;
     }
@@ -4028,13 +4037,15 @@ __global__ __launch_bounds__(256) void k_evict_compact(const Slot *__restrict__ 
 
 __global__ __launch_bounds__(256) void k_evict_reinsert(Slot *table, TableState *tstate, Limits lim, TableIndex X,
                                                         const Slot *__restrict__ buf, uint64_t m) {
-    const IdTable idt{X.heads, X.k6, lim.table_mask, lim.seed, X.epoch, lim.test_flags, table, 0u, 0u,
-                      X.mir, X.mir_shift};
+    IdTable idt{X.heads, X.k6, lim.table_mask, lim.seed, X.epoch, lim.test_flags, table, 0u, 0u,
+                X.mir, X.mir_shift};
+    idt.tgen = lim.tgen;
     for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i < m; i += (uint64_t)gridDim.x * 256u) {
-        const Slot s = buf[i];
-        const uint64_t h = id_start(idt, s.tag, s.key);
+        Slot s = buf[i];
+        const uint32_t fam = slot_fam(s.tag, lim.tgen);
+        const uint64_t h = id_start(idt, fam, s.key);
         bool fresh = false;
-        const uint32_t id = id_resolve(idt, s.tag, s.key, h, X.heads[h], &fresh);
+        const uint32_t id = id_resolve(idt, fam, s.key, h, X.heads[h], &fresh);
         if (id != kNoSlot) table[id] = s;   // (2x the entries in slots: never full)
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) tstate->count = m;
@@ -4077,7 +4088,7 @@ __global__ __launch_bounds__(256) void k_map_dump(const Slot *table, Limits lim,
     for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i <= lim.table_mask;
          i += (uint64_t)gridDim.x * 256u) {
         const Slot &s = table[i];
-        if (s.tag != tag || !(s.flags & bit)) continue;
+        if (slot_fam(s.tag, lim.tgen) != tag || !(s.flags & bit)) continue;
         const unsigned long long o = atomicAdd(count, 1ull);
         if (o >= cap) continue;
         const uint8_t *kb = reinterpret_cast<const uint8_t *>(s.key);

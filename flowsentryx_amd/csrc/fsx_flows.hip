@@ -405,19 +405,20 @@ size_t slot_acc_bytes() { return sizeof(SlotAcc); }
 // carried sums. Rows are unordered (a row counter): when cap < rows, which rows are kept is
 // unspecified (include/fsx_hip.h fsx_flows_end).
 __global__ __launch_bounds__(256) void k_flows_end(const SlotAcc *__restrict__ sacc, uint32_t epoch,
-                                                   const Slot *__restrict__ table, uint64_t slots,
+                                                   const Slot *__restrict__ table, uint64_t slots, uint32_t tgen,
                                                    FlowOut out, ScoreParams P,
                                                    unsigned long long *count) {
     for (uint64_t s = (uint64_t)blockIdx.x * 256u + threadIdx.x; s < slots; s += (uint64_t)gridDim.x * 256u) {
         const SlotAcc &m = sacc[s];
         if (m.epoch != epoch) continue;
-        if (table[s].tag == 0) continue;   // emptied by a rolled-back sub-batch
+        const uint32_t fam = slot_fam(table[s].tag, tgen);
+        if (fam == 0) continue;   // emptied by a rolled-back sub-batch
         const unsigned long long g = atomicAdd(count, 1ull);
         if (g >= out.cap) continue;
         FlowAcc a = acc_zero();
         a.n = m.n; a.s1 = m.s1; a.s2 = m.s2; a.d1 = m.d1; a.d2 = m.d2; a.dmax = m.dmax;
         const Slot &sl = table[s];
-        write_row((uint32_t)g, a, sl.tag, sl.key, m.dport, out, P);
+        write_row((uint32_t)g, a, fam, sl.key, m.dport, out, P);
     }
 }
 
@@ -461,7 +462,7 @@ hipError_t launch_flows_merge(const void *partials, uint32_t m, const Slot *tabl
     return hipGetLastError();
 }
 
-hipError_t launch_flows_end(const void *sacc, uint32_t epoch, const Slot *table, uint64_t slots,
+hipError_t launch_flows_end(const void *sacc, uint32_t epoch, const Slot *table, uint64_t slots, uint32_t tgen,
                             uint8_t *keys16, uint8_t *fam, float *feat, float *prob, uint8_t *dec,
                             uint32_t cap, const ScoreParams &P, unsigned long long *d_count,
                             hipStream_t st) {
@@ -470,7 +471,7 @@ hipError_t launch_flows_end(const void *sacc, uint32_t epoch, const Slot *table,
     hipError_t e = hipMemsetAsync(d_count, 0, 8, st);
     if (e != hipSuccess) return e;
     const uint32_t grid = (uint32_t)std::min<uint64_t>(4096, (slots + 255) / 256);
-    k_flows_end<<<grid, 256, 0, st>>>((const SlotAcc *)sacc, epoch, table, slots, out, P, d_count);
+    k_flows_end<<<grid, 256, 0, st>>>((const SlotAcc *)sacc, epoch, table, slots, tgen, out, P, d_count);
     return hipGetLastError();
 }
 

@@ -181,6 +181,10 @@ struct Limits {           // the rate-limiter constants, src/fsx_kern.c:245,308-
     // host per batch: a flood of new sources): k_parse writes a key-hash sort word, the
     // segment heads find / insert their slots in home-slot order after the sort
     uint32_t ord;
+    // table generation (16 bits): a slot's tag word is its family | tgen << 16, and a line of
+    // another generation reads as empty — fsx_reset moves to the next generation instead of
+    // clearing the table (DESIGN.md §3 "Clear-free reset")
+    uint32_t tgen;
 };
 constexpr uint32_t kFlagAdmit = 8u;   // include/fsx_hip.h FSX_FLAG_OVERFLOW_ADMIT
 constexpr uint32_t kFlagSwUnsorted = 16u;   // include/fsx_hip.h FSX_FLAG_SW_UNSORTED
@@ -319,17 +323,23 @@ __device__ __forceinline__ void mir_publish(void *mir, uint32_t shift, uint64_t 
     if (d <= 1) static_cast<uint16_t *>(mir)[pos] = (uint16_t)mir_entry(k0, seed, shift, (uint32_t)d);
 }
 
+// Slot tag words: family (1 IPv4, 2 IPv6) | table generation << 16 (Limits::tgen); the
+// family of a line, 0 when it is empty or of another generation.
+__host__ __device__ inline uint32_t slot_tag(uint32_t fam, uint32_t tgen) { return fam | tgen << 16; }
+__host__ __device__ inline uint32_t slot_fam(uint32_t tagw, uint32_t tgen) {
+    return (tagw >> 16) == tgen ? (tagw & 0xFFFFu) : 0u;
+}
+
 // Slot of (tag, key) in the table (linear probing from its probe start), or kNoSlot.
 __device__ inline bool slot_key_eq(const Slot &s, uint32_t tag, const uint32_t k[4]) {
-    return s.tag == tag && s.key[0] == k[0] && s.key[1] == k[1] && s.key[2] == k[2] &&
-           s.key[3] == k[3];
+    return s.key[0] == k[0] && s.key[1] == k[1] && s.key[2] == k[2] && s.key[3] == k[3];
 }
 
 __device__ inline uint32_t table_find(const Slot *table, const Limits &lim, uint32_t tag,
                                                const uint32_t k[4]) {
     uint64_t i = probe_start(tag, k, lim.seed, lim.table_mask, lim.test_flags);
     for (uint64_t probes = 0; probes <= lim.table_mask; ++probes) {
-        const uint32_t t = table[i].tag;
+        const uint32_t t = slot_fam(table[i].tag, lim.tgen);
         if (t == 0) return kNoSlot;
         if (t == tag && slot_key_eq(table[i], tag, k)) return (uint32_t)i;
         i = (i + 1) & lim.table_mask;
@@ -670,7 +680,7 @@ size_t slot_acc_bytes();
 hipError_t launch_flows_merge(const void *partials, uint32_t m, const Slot *table, const Limits &lim, void *sacc,
                               uint32_t epoch, hipStream_t st, const uint64_t *d_m = nullptr);
 // Rows of every source accumulated in epoch `epoch` (slots of the table), *d_count = rows.
-hipError_t launch_flows_end(const void *sacc, uint32_t epoch, const Slot *table, uint64_t slots,
+hipError_t launch_flows_end(const void *sacc, uint32_t epoch, const Slot *table, uint64_t slots, uint32_t tgen,
                             uint8_t *keys16, uint8_t *fam, float *feat, float *prob, uint8_t *dec,
                             uint32_t cap, const ScoreParams &P, unsigned long long *d_count,
                             hipStream_t st);

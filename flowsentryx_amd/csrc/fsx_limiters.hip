@@ -1054,8 +1054,8 @@ __global__ __launch_bounds__(256) void k_walk_sw_heavy_sel(BatchState *bs, const
 template <class SV>
 __device__ __forceinline__ uint32_t sw_slot_log(const SV &sv, const Slot &sl, const SwSeg *segs,
                                                 const uint64_t *ht, const uint32_t *hl, bool prune,
-                                                uint64_t cutoff, SwSeg &r) {
-    if (sl.tag == 0 || sl.aux == 0) return 0;
+                                                uint64_t cutoff, SwSeg &r, uint32_t tgen) {
+    if (slot_fam(sl.tag, tgen) == 0 || sl.aux == 0) return 0;
     if (sl.aux & kAuxWalked) {
         r = segs[(uint32_t)(sl.aux & 0xFFFFFFFFull)];
     } else {
@@ -1109,8 +1109,8 @@ __global__ __launch_bounds__(256) void k_sw_hist(const uint64_t *__restrict__ S,
         const uint64_t i0 = t * kSlotTile + threadIdx.x;
         auto slot_log = [&](uint64_t i, SwSeg &r) -> uint32_t {
             if (i >= nslots) return 0;
-            return pay_ok ? sw_slot_log(svp, table[i], segs, ht, hl, ck.prune, ck.cutoff, r)
-                          : sw_slot_log(svg, table[i], segs, ht, hl, ck.prune, ck.cutoff, r);
+            return pay_ok ? sw_slot_log(svp, table[i], segs, ht, hl, ck.prune, ck.cutoff, r, lim.tgen)
+                          : sw_slot_log(svg, table[i], segs, ht, hl, ck.prune, ck.cutoff, r, lim.tgen);
         };
         uint32_t cnt = 0;
         for (int k = 0; k < 16; ++k) {
@@ -1144,7 +1144,7 @@ __global__ __launch_bounds__(256) void k_sw_hist(const uint64_t *__restrict__ S,
                 const uint32_t c = slot_log(i, r);
                 if (i < nslots) {
                     Slot &sl = table[i];
-                    if (sl.tag != 0) {
+                    if (slot_fam(sl.tag, lim.tgen) != 0) {
                         if (c == 0) sl.aux = 0;
                         else {
                             if (c <= kCoopLog) copy(r, off, 0, 1);

@@ -86,8 +86,8 @@ hipError_t launch_shard_pack(const uint8_t *hdr, const uint32_t *len, const uint
                              const Replica *rep, bool compact, bool drop_rec, const uint32_t *use_dev,
                              bool regions, unsigned long long *status, uint32_t *ticket, hipStream_t st);
 hipError_t launch_shard_clock(const uint64_t *ts, uint32_t n, uint64_t *out3, hipStream_t st);
-hipError_t launch_blocklist_export(const Slot *table, uint64_t table_mask, ShardBlock *out, uint64_t cap,
-                                   unsigned long long *count, hipStream_t st);
+hipError_t launch_blocklist_export(const Slot *table, uint64_t table_mask, uint32_t tgen, ShardBlock *out,
+                                   uint64_t cap, unsigned long long *count, hipStream_t st);
 hipError_t launch_replica_build(const ShardBlock *in, uint64_t m, ShardBlock *slots, uint64_t mask,
                                 hipStream_t st);
 hipError_t launch_replica_build_blocks(const void *blocks, uint32_t nb, uint64_t cap, ShardBlock *slots,

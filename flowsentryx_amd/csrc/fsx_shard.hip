@@ -670,29 +670,30 @@ hipError_t launch_shard_clock(const uint64_t *ts, uint32_t n, uint64_t *out3, hi
 }
 
 // Every live blacklist entry (till > 0) of this rank's table.
-__global__ __launch_bounds__(256) void k_blocklist_export(const Slot *table, uint64_t mask, ShardBlock *out,
-                                                          uint64_t cap, unsigned long long *count) {
+__global__ __launch_bounds__(256) void k_blocklist_export(const Slot *table, uint64_t mask, uint32_t tgen,
+                                                          ShardBlock *out, uint64_t cap, unsigned long long *count) {
     for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i <= mask; i += (uint64_t)gridDim.x * 256u) {
         const Slot &s = table[i];
-        if (s.tag == 0 || !(s.flags & SLOT_HAS_BL) || s.till == 0) continue;
+        const uint32_t fam = slot_fam(s.tag, tgen);
+        if (fam == 0 || !(s.flags & SLOT_HAS_BL) || s.till == 0) continue;
         const unsigned long long o = atomicAdd(count, 1ull);
         if (o >= cap) continue;
         ShardBlock b;
         b.key[0] = s.key[0]; b.key[1] = s.key[1]; b.key[2] = s.key[2]; b.key[3] = s.key[3];
         b.till = s.till;
-        b.tag = s.tag;
+        b.tag = fam;
         b.pad = 0;
         out[o] = b;
     }
 }
 
-hipError_t launch_blocklist_export(const Slot *table, uint64_t table_mask, ShardBlock *out, uint64_t cap,
-                                   unsigned long long *count, hipStream_t st) {
+hipError_t launch_blocklist_export(const Slot *table, uint64_t table_mask, uint32_t tgen, ShardBlock *out,
+                                   uint64_t cap, unsigned long long *count, hipStream_t st) {
     (void)hipGetLastError();   // a stale error of another caller is not ours
     hipError_t e = hipMemsetAsync(count, 0, 8, st);
     if (e != hipSuccess) return e;
     const uint32_t grid = (uint32_t)std::min<uint64_t>(4096, (table_mask + 256) / 256);
-    k_blocklist_export<<<grid, 256, 0, st>>>(table, table_mask, out, cap, count);
+    k_blocklist_export<<<grid, 256, 0, st>>>(table, table_mask, tgen, out, cap, count);
     return hipGetLastError();
 }
 

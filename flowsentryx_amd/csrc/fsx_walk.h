@@ -173,19 +173,20 @@ struct SlotKeys {
     const unsigned long long *heads;
     const uint32_t *k6;
     uint32_t fresh_bit = 0;   // sort words carry kFreshBit (fsx_internal.h)
+    uint32_t tgen = 0;        // the table generation new lines are tagged with (Limits::tgen)
 };
 
 // h: the slot's head, loaded beside the slot's state (a load issued after the walk would
 // add a memory round trip to every segment of a flood: config 5's walkers 11 -> 19.5 ms)
-__device__ __forceinline__ void slot_adopt(Slot &sl, const SlotKeys &K, uint32_t i, unsigned long long h) {
+__device__ __forceinline__ void slot_adopt(Slot &sl, const SlotKeys &K, uint32_t i, unsigned long long h,
+                                           uint32_t tgen) {
     const uint32_t tag = (uint32_t)(h >> 32) & 0xFFu;
     sl.key[0] = (uint32_t)h;
-    if (tag == 2) {
-        sl.key[1] = K.k6[(size_t)i * 4 + 0];
-        sl.key[2] = K.k6[(size_t)i * 4 + 1];
-        sl.key[3] = K.k6[(size_t)i * 4 + 2];
-    }
-    sl.tag = tag;
+    sl.key[1] = tag == 2 ? K.k6[(size_t)i * 4 + 0] : 0u;
+    sl.key[2] = tag == 2 ? K.k6[(size_t)i * 4 + 1] : 0u;
+    sl.key[3] = tag == 2 ? K.k6[(size_t)i * 4 + 2] : 0u;
+    sl.aux = 0;   // (a line of another table generation may hold its source's)
+    sl.tag = slot_tag(tag, tgen);
 }
 
 // A new source's first state (lazy slots): the whole line in four 16-byte stores — family
@@ -197,7 +198,7 @@ __device__ __forceinline__ void store_new_line(Slot &sl, const FwState &s, const
     if (tag == 2) { k1 = K.k6[(size_t)i * 4 + 0]; k2 = K.k6[(size_t)i * 4 + 1]; k3 = K.k6[(size_t)i * 4 + 2]; }
     const uint32_t flags = (s.has_st ? SLOT_HAS_ST : 0u) | (s.has_bl ? SLOT_HAS_BL : 0u);
     uint4 *p = reinterpret_cast<uint4 *>(&sl);
-    p[0] = make_uint4(tag, flags, (uint32_t)h, k1);
+    p[0] = make_uint4(slot_tag(tag, K.tgen), flags, (uint32_t)h, k1);
     p[1] = make_uint4(k2, k3, (uint32_t)s.pps, (uint32_t)(s.pps >> 32));
     p[2] = make_uint4((uint32_t)s.bps, (uint32_t)(s.bps >> 32), (uint32_t)s.tt, (uint32_t)(s.tt >> 32));
     p[3] = make_uint4((uint32_t)s.till, (uint32_t)(s.till >> 32), 0u, 0u);
