@@ -1083,13 +1083,52 @@ __device__ __forceinline__ SwClock sw_clock(const BatchState *bs, const TableSta
     return SwClock{sw_mono(bs, tst) && T >= lim.window, T - lim.window};
 }
 
-template <bool kWrite>
+// The history rebuild's tile offsets in one pass (kMode 2, k_sw_hist_scan not needed): tiles in
+// ticket order, per tile one status word — 1 << 62 | its entries, or 2 << 62 | the entries of
+// every tile up to it (the word is the data) — and wave 0 looks back 64 tiles at a time.
+__device__ __forceinline__ uint64_t hist_lookback(unsigned long long *status, uint32_t t, uint64_t cnt) {
+    const uint32_t lane = lane_id();
+    constexpr unsigned long long kM = (1ull << 62) - 1ull;
+    if (t == 0) {
+        if (lane == 0) __hip_atomic_store(status, (2ull << 62) | cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return 0;
+    }
+    if (lane == 0) __hip_atomic_store(status + t, (1ull << 62) | cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint64_t excl = 0;
+    uint32_t spins = 0;
+    for (int64_t j = (int64_t)t - 1;;) {
+        const int64_t idx = j - (int64_t)lane;
+        const unsigned long long w = idx >= 0 ? __hip_atomic_load(status + idx, __ATOMIC_RELAXED,
+                                                                  __HIP_MEMORY_SCOPE_AGENT)
+                                              : (2ull << 62);
+        const uint32_t f = (uint32_t)(w >> 62);
+        const uint64_t b2 = __ballot(f == 2), b0 = __ballot(f == 0);
+        const uint32_t l2 = b2 ? (uint32_t)__ffsll((unsigned long long)b2) - 1u : 64u;
+        const uint32_t l0 = b0 ? (uint32_t)__ffsll((unsigned long long)b0) - 1u : 64u;
+        if (l0 < l2) {   // a tile before the nearest prefix has published nothing yet
+            if (++spins > (1u << 22)) break;   // (never expected: lower tickets are running)
+            __builtin_amdgcn_s_sleep(1);
+            continue;
+        }
+        // (lanes before the nearest prefix: their tiles' counts; lane l2: that prefix)
+        excl += wave_sum(lane <= l2 ? (uint64_t)(w & kM) : 0ull);
+        if (l2 < 64u) break;
+        j -= 64;
+    }
+    if (lane == 0) __hip_atomic_store(status + t, (2ull << 62) | (excl + cnt), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return excl;
+}
+
+template <int kMode>
 __global__ __launch_bounds__(256) void k_sw_hist(const uint64_t *__restrict__ S, const BatchState *bs,
                                                  const TableState *tst, const uint64_t *__restrict__ ts,
                                                  const uint32_t *__restrict__ len,
                                                  const uint64_t *__restrict__ pay, Slot *table,
                                                  Limits lim, HistBufs hb, const SwSeg *__restrict__ segs) {
+    constexpr bool kWrite = kMode != 0;
     __shared__ uint32_t s_tmp[4];
+    __shared__ uint64_t s_base;
+    __shared__ uint32_t s_t;
     if (bs->err) return;
     const uint64_t nslots = lim.table_mask + 1;
     const uint64_t ntiles = (nslots + kSlotTile - 1) / kSlotTile;
@@ -1103,7 +1142,13 @@ __global__ __launch_bounds__(256) void k_sw_hist(const uint64_t *__restrict__ S,
     const SegView<true> svp{S, ts, len, pay, ~bs->inv_min_ts};
     const SegView<false> svg{S, ts, len, pay, 0};
     uint32_t *tile_cnt = hb.tile_cnt;
-    for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    uint64_t t0 = blockIdx.x;
+    if constexpr (kMode == 2) {   // (one tile per block, in ticket order: the ticket in tile_cnt[0])
+        if (threadIdx.x == 0) s_t = atomicAdd(tile_cnt, 1u);
+        __syncthreads();
+        t0 = s_t;
+    }
+    for (uint64_t t = t0; t < ntiles; t += kMode == 2 ? ntiles : gridDim.x) {
         // thread x owns slots i0 + 256 k (coalesced slot reads); its logs are stored
         // contiguously in k order (any order works: the slot's aux holds the offset)
         const uint64_t i0 = t * kSlotTile + threadIdx.x;
@@ -1122,7 +1167,23 @@ __global__ __launch_bounds__(256) void k_sw_hist(const uint64_t *__restrict__ S,
             block256_excl(cnt, s_tmp, &tot);
             if (threadIdx.x == 0) tile_cnt[t] = tot;
         } else {
-            uint64_t off = hb.tile_off[t] + block256_excl(cnt, s_tmp, nullptr);
+            uint64_t off;
+            if constexpr (kMode == 2) {
+                uint32_t tot;
+                const uint32_t ex = block256_excl(cnt, s_tmp, &tot);
+                if (threadIdx.x < 64) {   // (wave 0)
+                    const uint64_t b = hist_lookback(reinterpret_cast<unsigned long long *>(hb.tile_off),
+                                                     (uint32_t)t, tot);
+                    if (threadIdx.x == 0) {
+                        s_base = b;
+                        if (t == ntiles - 1) *hb.total = b + tot;
+                    }
+                }
+                __syncthreads();
+                off = s_base + ex;
+            } else {
+                off = hb.tile_off[t] + block256_excl(cnt, s_tmp, nullptr);
+            }
             // copy log entries [lo + first, hi) step `step` of r to off + (v - lo)
             auto copy = [&](const SwSeg &r, uint64_t o0, uint32_t first, uint32_t step) {
                 if (pay_ok) {
@@ -1268,10 +1329,19 @@ hipError_t launch_sliding_window(const uint64_t *S, const uint64_t *ts, const ui
     const uint64_t nslots = lim.table_mask + 1;
     const uint64_t ntiles = (nslots + kSlotTile - 1) / kSlotTile;
     const uint32_t grid = (uint32_t)std::min<uint64_t>(4096, ntiles);
-    k_sw_hist<false><<<grid, 256, 0, st>>>(S, bs, tstate, ts, len, sc.pay[0], table, lim, hb, sc.sw_seg);
-    k_sw_hist_scan<<<1, 1024, 0, st>>>(bs, hb.tile_cnt, hb.tile_off, ntiles, hb.total);
-    mark("k_sw_hist_count");
-    k_sw_hist<true><<<grid, 256, 0, st>>>(S, bs, tstate, ts, len, sc.pay[0], table, lim, hb, sc.sw_seg);
+    static const bool two_pass = getenv("FSX_SW_HIST_TWO_PASS") != nullptr;   // A/B: count, scan, write
+    if (!two_pass && ntiles < (1ull << 31)) {
+        // one pass: each tile's offset by a look-back (status words in tile_off, the ticket in
+        // tile_cnt[0]); the last tile writes the total
+        if ((e = hipMemsetAsync(hb.tile_off, 0, ntiles * 8, st)) != hipSuccess) return e;
+        if ((e = hipMemsetAsync(hb.tile_cnt, 0, 4, st)) != hipSuccess) return e;
+        k_sw_hist<2><<<(uint32_t)ntiles, 256, 0, st>>>(S, bs, tstate, ts, len, sc.pay[0], table, lim, hb, sc.sw_seg);
+    } else {
+        k_sw_hist<0><<<grid, 256, 0, st>>>(S, bs, tstate, ts, len, sc.pay[0], table, lim, hb, sc.sw_seg);
+        k_sw_hist_scan<<<1, 1024, 0, st>>>(bs, hb.tile_cnt, hb.tile_off, ntiles, hb.total);
+        mark("k_sw_hist_count");
+        k_sw_hist<1><<<grid, 256, 0, st>>>(S, bs, tstate, ts, len, sc.pay[0], table, lim, hb, sc.sw_seg);
+    }
     k_sw_finish<<<1, 1, 0, st>>>(bs, tstate, hb.total);
     mark("k_sw_hist_write");
     return hipGetLastError();
