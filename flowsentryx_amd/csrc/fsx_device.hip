@@ -285,6 +285,14 @@ __device__ __forceinline__ void select_top(const uint32_t (&x)[kPer], uint32_t n
     __syncthreads();
 }
 
+// A rule may cover the address: its /24 filter bit is set (rules of any length set the bits
+// of every /24 they touch); false without rules.
+__device__ __forceinline__ bool rule_maybe(const RuleSet &R, uint32_t tag, const uint32_t k[4]) {
+    if (!R.slot) return false;
+    const uint32_t p24 = (k[0] & 0xFFu) << 16 | (k[0] & 0xFF00u) | ((k[0] >> 16) & 0xFFu);
+    return (R.filter[(tag - 1u) << (kRuleFilterBits - 5) | p24 >> 5] >> (p24 & 31u)) & 1u;
+}
+
 // One block: the heavy set of the batch from the two sketches. Candidates: the sampled
 // source of each of the (at most 2 nmax) buckets of highest count >= floor per sketch; a
 // candidate's estimate is the smaller of its two buckets' counts (a count-min estimate:
@@ -299,7 +307,7 @@ __global__ __launch_bounds__(1024) void k_heavy_pick(PacketIn in, const uint32_t
                                                      uint32_t *__restrict__ sketch, HeavySet *hs,
                                                      uint32_t nmax, uint32_t floor_cnt, uint64_t seed,
                                                      uint64_t mask, uint32_t test_flags, IdTable idt,
-                                                     uint32_t resolve, BatchState *bs) {
+                                                     uint32_t resolve, BatchState *bs, RuleSet rules) {
     constexpr uint32_t kMap = 1u << kHeavyMapBits;
     constexpr uint32_t kCand = 2 * 2 * kHeavyMax;   // candidate buckets over both sketches
     __shared__ uint32_t s_n, s_nc;
@@ -345,7 +353,9 @@ __global__ __launch_bounds__(1024) void k_heavy_pick(PacketIn in, const uint32_t
         const uint32_t a = cnt1[h1], b = cnt2[sketch2_of(tag, k, seed)];
         s_ctag[tid] = tag;
         for (int j = 0; j < 4; ++j) s_ckey[tid][j] = k[j];
-        s_cest[tid] = tag ? (a < b ? a : b) : 0u;
+        // (prefix rules: a source whose /24 some rule touches stays light — the parse decides
+        // its packets one by one — so a heavy source is never rule-dropped and is inserted here)
+        s_cest[tid] = tag && !rule_maybe(rules, tag, k) ? (a < b ? a : b) : 0u;
     }
     __syncthreads();
     // 3. duplicates (a source found through both sketches): a second-sketch candidate whose
@@ -509,7 +519,6 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
     //   lmask (the payload array), the clock facts and the sort tiles' span;
     //   else: no timestamp loads, the light-packet mask of every 64-packet step in lmask
     //   (k_pass0h<true> reads ts / len / verdicts for the records and the payloads)
-    static_assert(!kHf || !kRules, "unsorted heavy sources: no prefix rules");
     static_assert(!kOrd || (!kHf && !kMir && kRec == 0), "home-ordered inserts: header records, no heavy sources");
     const uint32_t ord_s = kOrd ? (uint32_t)__popcll(idt.mask) : 0u;   // log2(slots)
     constexpr bool kHr = kHf && FSX_PARSE_PAY;   // (the payload words from the parse)
@@ -578,8 +587,8 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
                 h[k] = stream_load16(in.hdr + (size_t)rr * 64u + c * 16u);
             }
             L_ = stream_load(len + ic);
-            if constexpr (kHf && !kHr) {
-                T_ = 0ull;
+            if constexpr (kHf && !kHr) {   // (prefix rules: a rule's till is checked against ts)
+                T_ = kRules ? stream_load(ts + ic) : 0ull;
                 P_ = 0ull;
             } else if constexpr (kHr) {   // (the record before a step: c_prev, see parse_step)
                 T_ = stream_load(ts + ic);
@@ -3676,9 +3685,14 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
     // heavy verdict lists (fixed / sliding window with the heavy-source sort; FSX_NO_HEAVY_LISTS=1: A/B)
     const bool lists_sw = lists_any && lim.limiter == 1 && (npass & 1);
     const bool tagh = heavy_sort && (lists_ok || lists_sw);
-    // heavy slots resolved once in k_heavy_pick (not under prefix rules; FSX_NO_HEAVY_SLOTS=1: A/B)
+    // heavy slots resolved once in k_heavy_pick (FSX_NO_HEAVY_SLOTS=1: A/B). Under prefix rules
+    // the pick leaves every source whose /24 a rule touches light (rule_maybe), so a heavy
+    // source is never rule-dropped and may be inserted there (round 5; FSX_RULES_LAZY_HEAVY=1:
+    // round 4's unresolved heavy sources under rules, inserted by the parse, on the run path)
     static const bool no_hslots = getenv("FSX_NO_HEAVY_SLOTS") != nullptr;
-    const uint32_t resolve = !no_hslots && !(do_limit && rules.slot) ? 1u : 0u;
+    static const bool rules_lazy = getenv("FSX_RULES_LAZY_HEAVY") != nullptr;
+    const bool rl_batch = do_limit && rules.slot;
+    const uint32_t resolve = !no_hslots && !(rl_batch && (rules_lazy || in.rec)) ? 1u : 0u;
     // heavy sources outside the sort (fsx_heavy.hip): header records with resolved heavy
     // slots; k_hmode picks the batch's path on the device (FSX_NO_HFAST=1: the runs, A/B)
     static const bool no_hfast = getenv("FSX_NO_HFAST") != nullptr;
@@ -3714,7 +3728,8 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
         const bool sw_dense = hfm && lim.limiter == 1 && !(lim.test_flags & kFlagSwSparse) && sw_div;
         const uint32_t floor_cnt = sw_dense ? std::max<uint32_t>(16, S / sw_div) : 16u;
         k_heavy_pick<<<1, 1024, 0, sp0>>>(in, len, sc.sketch, sc.heavy, nheavy, floor_cnt, lim.seed,
-                                          lim.table_mask, lim.test_flags, idt, resolve, bs);
+                                          lim.table_mask, lim.test_flags, idt, resolve, bs,
+                                          rl_batch ? rules : RuleSet{});
         mark("k_heavy_pick");
     } else {
         for (int p = 0; p < 4; ++p) { dp.shift[p] = kIdShift + dbits * (uint32_t)p; dp.mask[p] = dmask; }
@@ -3770,8 +3785,9 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
                : k_parse<0, false, false, false, true><<<g, 256, 0, st>>>(in, len, ts, n, sc.packed[0], verdict, bs,
                                                                          pidt, sc.sort_ctl, th, tcap, dp, hs, rules,
                                                                          0u, sc.chunk_cnt, lmask);
-        else if (hfm)
-            !in.rec ? FSX_PARSE(0, false, true) : in.rec_bytes == 16 ? FSX_PARSE(16, false, true) : FSX_PARSE(32, false, true);
+        else if (hfm)   // (with prefix rules: header records only, resolve above)
+            !in.rec ? (rl ? FSX_PARSE(0, true, true) : FSX_PARSE(0, false, true))
+                    : in.rec_bytes == 16 ? FSX_PARSE(16, false, true) : FSX_PARSE(32, false, true);
         else if (!in.rec)
             rl ? FSX_PARSE(0, true, false) : FSX_PARSE(0, false, false);
         else if (in.rec_bytes == 16)
