@@ -1104,8 +1104,14 @@ __global__ __launch_bounds__(256) void k_tile_hist(const uint64_t *__restrict__ 
     if (tid <= dmask) thist[(size_t)tid * tcap + t] = sh[0][tid] + sh[1][tid] + sh[2][tid] + sh[3][tid];
 }
 
-// Block d: offs[d][t] = base[d] + sum of thist[d][t'] over t' < t (in place), in
-// coalesced chunks of 1024 tiles (4 per thread) with a running carry.
+// Block d: offs[d][t] = base[d] + sum of thist[d][t'] over t' < t (in place), in chunks of
+// 4096 tiles with a running carry: a chunk's counts are loaded and stored coalesced (16 per
+// thread, strided by 256) and staged through LDS (padded: conflict-free), where thread x
+// scans the 16 consecutive tiles 16x..16x+15. A light pass of a 64M-packet batch (~8K tiles)
+// is two chunks: the scan is a chain of block scans on the front's critical path.
+#ifndef FSX_TILE_SCAN_WIDE
+#define FSX_TILE_SCAN_WIDE 1   // 0: round 4's chunks of 1024 tiles, 4 per thread (A/B)
+#endif
 __global__ __launch_bounds__(256) void k_tile_scan(uint32_t *__restrict__ thist, uint32_t tcap,
                                                    uint32_t L_host, const uint32_t *L_dev,
                                                    const uint32_t *__restrict__ gbase) {
@@ -1114,8 +1120,41 @@ __global__ __launch_bounds__(256) void k_tile_scan(uint32_t *__restrict__ thist,
     const uint32_t ntiles = (L + kSortTile - 1) / kSortTile;
     uint32_t *row = thist + (size_t)blockIdx.x * tcap;
     uint32_t carry = gbase[blockIdx.x];
+    const uint32_t tid = threadIdx.x;
+#if FSX_TILE_SCAN_WIDE
+    __shared__ uint32_t s_x[4096 + 256];   // tile e of the chunk at e + e / 16
+    for (uint32_t c0 = 0; c0 < ntiles; c0 += 4096u) {
+        uint32_t x[16];
+#pragma unroll
+        for (uint32_t k = 0; k < 16; ++k) {
+            const uint32_t e = k * 256u + tid;
+            x[k] = c0 + e < ntiles ? row[c0 + e] : 0u;
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < 16; ++k) {
+            const uint32_t e = k * 256u + tid;
+            s_x[e + (e >> 4)] = x[k];
+        }
+        __syncthreads();
+        uint32_t sum = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < 16; ++j) { x[j] = s_x[tid * 17u + j]; sum += x[j]; }
+        uint32_t tot;
+        uint32_t off = carry + block256_excl(sum, s_tmp, &tot);
+#pragma unroll
+        for (uint32_t j = 0; j < 16; ++j) { s_x[tid * 17u + j] = off; off += x[j]; }
+        __syncthreads();
+#pragma unroll
+        for (uint32_t k = 0; k < 16; ++k) {
+            const uint32_t e = k * 256u + tid;
+            if (c0 + e < ntiles) row[c0 + e] = s_x[e + (e >> 4)];
+        }
+        carry += tot;
+        __syncthreads();
+    }
+#else
     for (uint32_t c0 = 0; c0 < ntiles; c0 += 1024) {
-        const uint32_t i = c0 + threadIdx.x * 4u;
+        const uint32_t i = c0 + tid * 4u;
         uint32_t x[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) x[k] = i + k < ntiles ? row[i + k] : 0u;
@@ -1126,6 +1165,7 @@ __global__ __launch_bounds__(256) void k_tile_scan(uint32_t *__restrict__ thist,
             if (i + k < ntiles) { row[i + k] = off; off += x[k]; }
         carry += tot;
     }
+#endif
 }
 
 // One tile: stable rank, global bases from offs(d, tile count of d), LDS-sorted
