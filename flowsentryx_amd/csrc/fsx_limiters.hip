@@ -403,7 +403,10 @@ __global__ __launch_bounds__(256) void k_tb_tiles(const uint64_t *__restrict__ S
 }
 
 // One pass (see the file header): a block per tile, tiles in ticket order.
-__global__ __launch_bounds__(256) void k_tb_scan(const uint64_t *__restrict__ S, BatchState *bs,
+#ifndef FSX_TB_SCAN_MINB
+#define FSX_TB_SCAN_MINB 1   // waves/SIMD bound (A/B: scripts/build_variant.sh)
+#endif
+__global__ __launch_bounds__(256, FSX_TB_SCAN_MINB) void k_tb_scan(const uint64_t *__restrict__ S, BatchState *bs,
                                                  const uint64_t *__restrict__ ts,
                                                  const uint32_t *__restrict__ len,
                                                  const uint64_t *__restrict__ pay,
