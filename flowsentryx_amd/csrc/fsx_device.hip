@@ -422,9 +422,15 @@ __global__ __launch_bounds__(1024) void k_heavy_pick(PacketIn in, const uint32_t
 // (the first slots of four lengths at a time loaded together); the first rule found is
 // the longest match and drops the packet when 0 < now <= till (till 0 or expired: the
 // packet goes on, an exception inside a shorter blocked prefix).
-__device__ __forceinline__ bool rule_drop(const RuleSet &R, uint32_t tag, const uint32_t k[4], uint64_t now) {
+// (the filter word is loaded by the caller, rule_filter_word, ahead of the work that does
+// not depend on it)
+__device__ __forceinline__ uint32_t rule_filter_word(const RuleSet &R, uint32_t tag, const uint32_t k[4]) {
     const uint32_t p24 = (k[0] & 0xFFu) << 16 | (k[0] & 0xFF00u) | ((k[0] >> 16) & 0xFFu);
-    const uint32_t fw = R.filter[(tag - 1u) << (kRuleFilterBits - 5) | p24 >> 5];
+    return R.filter[(tag - 1u) << (kRuleFilterBits - 5) | p24 >> 5];
+}
+__device__ __forceinline__ bool rule_drop(const RuleSet &R, uint32_t tag, const uint32_t k[4], uint64_t now,
+                                          uint32_t fw) {
+    const uint32_t p24 = (k[0] & 0xFFu) << 16 | (k[0] & 0xFF00u) | ((k[0] >> 16) & 0xFFu);
     if (!((fw >> (p24 & 31u)) & 1u)) return false;
     const uint32_t nl = tag == 1 ? R.nlen4 : R.nlen6;
     const uint8_t *lens = R.lens + (tag == 1 ? 0u : kRuleLens6);
@@ -740,12 +746,12 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
             in.rec_len[i] = L;
             in.rec_ts[i] = T;
         }
-        if constexpr (kRules) {   // prefix blocklist: the longest matching rule decides
-            if (tag && rule_drop(rules, tag, k, T)) {
-                tag = 0;              // never reaches the per-source path
-                v = XDP_DROP;
-                ++nrule;
-            }
+        // prefix blocklist: the /24 filter word loaded first, its latency under the source's
+        // hash and heavy-map lookup; a heavy source needs no rule check (the pick leaves every
+        // source whose filter bit is set light, rule_maybe)
+        uint32_t rfw = 0;
+        if constexpr (kRules) {
+            if (tag) rfw = rule_filter_word(rules, tag, k);
         }
         uint64_t prev = __shfl_up(T, 1);
         if constexpr (kHr) {
@@ -754,13 +760,11 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
         } else {
             if (lane == 0) prev = (live && i > 0) ? Pc : T;
         }
-        const bool ip = tag != 0;
-        if (tag == 2) any6 = 1;
         uint64_t h = 0;
-        if (ip) h = id_start(idt, tag, k);
+        if (tag) h = id_start(idt, tag, k);
         // heavy source? (LDS map of the batch's heavy set)
         int hidx = -1;
-        if (ip && nh) {
+        if (tag && nh) {
             constexpr uint32_t kMapMask = (1u << kHeavyMapBits) - 1u;
             uint32_t hh = (uint32_t)h & kMapMask;
             for (uint32_t e; (e = s_hmap[hh]) != 0; hh = (hh + 1) & kMapMask) {
@@ -772,6 +776,16 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
                 }
             }
         }
+        if constexpr (kRules) {   // the longest matching rule decides
+            if (tag && hidx < 0 && rule_drop(rules, tag, k, T, rfw)) {
+                tag = 0;              // never reaches the per-source path
+                v = XDP_DROP;
+                ++nrule;
+                h = 0;
+            }
+        }
+        const bool ip = tag != 0;
+        if (tag == 2) any6 = 1;
         // the fast path reads the first two slots of an IPv4 source's probe chain (IPv6
         // sources are always resolved by the full protocol, which reads their key words
         // only after the head shows READY)

@@ -12,7 +12,7 @@ for e in "$@"; do
 import json, sys
 leg, e = sys.argv[1], sys.argv[2]
 d = json.loads(open("gpurun_out/abl.json").read().strip().splitlines()[-1])
-r = d[leg]
+r = d[{"rules": "prefix_rules"}.get(leg, leg)]
 if "ms_per_step" in r:
     print(e or "default", leg, r["ms_per_step"])
 else:   # (a leg of several runs: limiters)
