@@ -746,12 +746,20 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
             in.rec_len[i] = L;
             in.rec_ts[i] = T;
         }
-        // prefix blocklist: the /24 filter word loaded first, its latency under the source's
-        // hash and heavy-map lookup; a heavy source needs no rule check (the pick leaves every
-        // source whose filter bit is set light, rule_maybe)
+        // prefix blocklist, kHf: the /24 filter word loaded first, its latency under the
+        // source's hash and heavy-map lookup; a heavy source needs no rule check (the pick
+        // leaves every source whose filter bit is set light, rule_maybe). (Without kHf the rule
+        // decides first: the early word spills in those instantiations.)
         uint32_t rfw = 0;
-        if constexpr (kRules) {
+        if constexpr (kRules && kHf) {
             if (tag) rfw = rule_filter_word(rules, tag, k);
+        }
+        if constexpr (kRules && !kHf) {
+            if (tag && rule_drop(rules, tag, k, T, rule_filter_word(rules, tag, k))) {
+                tag = 0;              // never reaches the per-source path
+                v = XDP_DROP;
+                ++nrule;
+            }
         }
         uint64_t prev = __shfl_up(T, 1);
         if constexpr (kHr) {
@@ -776,7 +784,7 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
                 }
             }
         }
-        if constexpr (kRules) {   // the longest matching rule decides
+        if constexpr (kRules && kHf) {   // the longest matching rule decides
             if (tag && hidx < 0 && rule_drop(rules, tag, k, T, rfw)) {
                 tag = 0;              // never reaches the per-source path
                 v = XDP_DROP;
