@@ -261,3 +261,41 @@ def test_prefix_rules_and_flow_features(native, oracle):
     ko, fo, xo = _sorted_flows(ko, fo, xo)
     assert np.array_equal(fg, fo) and np.array_equal(kg, ko)
     assert np.array_equal(xg.view(np.uint32), xo.view(np.uint32))
+
+
+@pytest.mark.parametrize("cover", ["some", "top"])
+def test_prefix_rules_unsorted_heavy_path(native, oracle, cover):
+    """Prefix rules on the unsorted-heavy path: the pick leaves every source
+    whose /24 a rule touches light, so the heavy sources are resolved in the pick and every
+    batch still takes the unsorted path (heavy_unsorted). Rules on the most popular sources —
+    permanent, expiring inside the batch and exceptions — across three carried batches, against
+    the oracle. "top": every one of the 16 most popular sources is under a rule (the heavy set
+    is the next ones down)."""
+    from collections import Counter
+    from flowsentryx_amd.lib import prefix_key
+    rng = np.random.default_rng(91)
+    hdr, ln, ts = rand_stream(rng, 90000, 600, dt_max=300, v6_frac=0.2)
+    ips = _ips(hdr, ln)
+    t0, t1 = int(ts[0]), int(ts[-1])
+    top = [s for s, _ in Counter(x for x in ips if x is not None).most_common(16)]
+    rules = {}
+    for j, (fam, a) in enumerate(top if cover == "top" else top[::3]):
+        bits = 32 if fam == 4 else 128
+        plen = (bits, bits - 4, 24 if fam == 4 else 64)[j % 3]
+        till = (2**64 - 1, (t0 + t1) // 2, 0)[j % 3] if cover == "top" else (2**64 - 1, (t0 + t1) // 2)[j % 2]
+        rules[(7 if fam == 4 else 8, prefix_key(a, plen))] = till
+    cfg = dict(CFGS["tight"], max_entries=1 << 18)   # (>= 2^17 slots: the heavy-source sort)
+    o = oracle.Oracle(**cfg)
+    for (m, k), v in rules.items():
+        o.map_update(m, k, v)
+    with gpu_ctx(native, **cfg) as c:
+        _install(c, rules, batched=True)
+        for b, (a, z) in enumerate(((0, 30000), (30000, 60000), (60000, 90000))):
+            vg = c.verdict_batch(hdr[a:z], ln[a:z], ts[a:z])
+            vo = o.batch(hdr[a:z], ln[a:z], ts[a:z])
+            bad = np.nonzero(vg != vo)[0]
+            assert bad.size == 0, f"batch {b}: {bad.size} verdicts differ, first at {bad[:8]}"
+            info = c.last_batch_info()
+            assert info["heavy_unsorted"] == 1, (b, info)
+            assert info["prefix_rule_drops"] > 0
+            _assert_same(c, o)
