@@ -644,6 +644,10 @@ static int batch_error(fsx_ctx *c, uint32_t err) {
     if (err & ERR_HIST_FULL)
         return set_err(c, -ENOSPC, "sliding-window history full: carried logs + batch > %llu entries",
                        (unsigned long long)c->hist.cap);
+    if (err & ERR_HEAVY_VIEW)
+        return set_err(c, -EIO, "heavy-source rank view: inconsistent tile-count row or tags (flags 0x%x)", err);
+    if (err & ERR_SORT_HANG)
+        return set_err(c, -EIO, "a decoupled look-back timed out (flags 0x%x)", err);
     if (err) return set_err(c, -EIO, "device error flags 0x%x", err);
     return 0;
 }
@@ -907,6 +911,10 @@ static int run_pipelined(fsx_ctx *c, const PacketIn &in0, const uint32_t *d_len,
     }
     // an unsplit batch's tail runs on the context stream: a deferred tail goes first
     if (!split && (rc = sel(c))) return rc;
+    //  the batch generation wraps in this call: k_born_clear rewrites the flags word
+    // of every stamped slot, which a tail still in flight may be storing — the deferred tail goes
+    // in first and the context stream waits for the last tail (tails run in order)
+    if (split && c->id_gen + 1 == 0x10000u && (rc = sel(c))) return rc;
     const int q = (c->par + 1) % fsx_ctx::kSets;   // the set of the batch three calls back
     if (c->fl_on[q]) {
         HIPCHK(c, hipEventSynchronize(c->tail_done[q]));
@@ -1504,6 +1512,25 @@ static bool reset_swap_ok(const fsx_ctx *c) {
            !c->timing && !(c->cfg.flags & FSX_FLAG_EVICT_IDLE);
 }
 
+// Test hook (FSX_TEST_SPARE_POISON): fill a freshly allocated spare table with what a recycled
+// allocation could hold — live-looking IPv4 lines of the next table generation (state and a
+// blacklist entry each) — so a test can check that nothing of it survives the swap-in.
+static hipError_t poison_table(Slot *t, uint64_t slots, uint32_t tgen) {
+    std::vector<Slot> h(slots);
+    for (uint64_t i = 0; i < slots; ++i) {
+        Slot &s = h[i];
+        memset(&s, 0, sizeof(s));
+        s.tag = slot_tag(1u, (tgen + 1u) & 0xFFFFu);
+        s.flags = SLOT_HAS_ST | SLOT_HAS_BL;
+        s.key[0] = 0x0A000000u | (uint32_t)i;
+        s.pps = 7;
+        s.bps = 700;
+        s.tt = 1;
+        s.till = ~0ull;
+    }
+    return hipMemcpy(t, h.data(), slots * sizeof(Slot), hipMemcpyHostToDevice);
+}
+
 // The spare table set, allocated with pipelining (fsx_set_pipeline 1) for the limiters and table
 // sizes a pipelined reset serves: the table and index memory once more.
 static int alloc_spare(fsx_ctx *c) {
@@ -1514,6 +1541,13 @@ static int alloc_spare(fsx_ctx *c) {
     auto build = [&]() -> hipError_t {
         hipError_t e;
         if ((e = hipMalloc(&sp.table, c->slots * sizeof(Slot))) != hipSuccess) return e;
+        // (hipMalloc may hand back recycled memory — e.g. an earlier context's table, whose
+        // lines carry table generations this context reaches: the first swap-in must find
+        // nothing but empty lines, as fsx_open's table does)
+        if (getenv("FSX_TEST_SPARE_POISON")) {
+            if ((e = poison_table(sp.table, c->slots, c->lim.tgen)) != hipSuccess) return e;
+        }
+        if ((e = hipMemset(sp.table, 0, c->slots * sizeof(Slot))) != hipSuccess) return e;
         if ((e = hipMalloc(&sp.tstate, sizeof(TableState))) != hipSuccess) return e;
         if ((e = hipMemset(sp.tstate, 0, sizeof(TableState))) != hipSuccess) return e;
         if ((e = hipMalloc(&sp.heads, c->slots * 8)) != hipSuccess) return e;
@@ -1529,7 +1563,8 @@ static int alloc_spare(fsx_ctx *c) {
         // (nothing uses the new set yet: its "last users" are already done)
         for (int k = 0; k < 3; ++k)
             if ((e = hipEventRecord(c->spare_free[k], c->stream)) != hipSuccess) return e;
-        return hipSuccess;
+        // (the memsets above ran on the null stream: done before any context stream uses the set)
+        return hipStreamSynchronize(nullptr);
     };
     const hipError_t e = build();
     if (e != hipSuccess) {   // (no spare: resets stay synchronous)

@@ -2004,11 +2004,66 @@ __global__ __launch_bounds__(256) void k_ord_fix(uint64_t *__restrict__ S, uint6
     }
 }
 
+// A mixed run longer than kOrdLong (a heavy IPv6 source whose 32-bit key hash a flood source
+// shares: rare, but not impossible under a flood of ~10^6 IPv6 sources): its sources are taken
+// out one at a time, stably — the run's first remaining packet names the next source, one pass
+// moves that source's packets to tmp / ptmp (after the sources taken before) and compacts the
+// others in place (a write never passes the chunk being read) — then the run is copied back.
+// O(L · sources); more than kOrdMaxSrc sources in one run (not reachable by chance): false.
+constexpr uint32_t kOrdMaxSrc = 1024;
+
+__device__ bool ord_extract(uint64_t *S, uint64_t *pay, uint8_t *headf, uint64_t *tmp, uint64_t *ptmp,
+                            uint32_t p, uint32_t L, const uint8_t *hdr, uint64_t seed, uint32_t s) {
+    const uint32_t lane = lane_id();
+    const uint64_t below = (1ull << lane) - 1ull;
+    uint32_t rem = L, out = 0;
+    for (uint32_t round = 0; rem; ++round) {
+        if (round == kOrdMaxSrc) return false;
+        uint32_t kl[4];
+        const uint32_t tl = ord_src(S[p], hdr, seed, s, kl);
+        const uint32_t out0 = out;
+        uint32_t nm = 0;
+        for (uint32_t j0 = 0; j0 < rem; j0 += 64) {
+            const uint32_t j = j0 + lane;
+            const bool in = j < rem;
+            uint64_t x = 0, pw = 0;
+            bool match = false;
+            if (in) {
+                x = S[p + j];
+                pw = pay[p + j];
+                uint32_t k[4];
+                const uint32_t t = ord_src(x, hdr, seed, s, k);
+                match = t == tl && k[0] == kl[0] && k[1] == kl[1] && k[2] == kl[2] && k[3] == kl[3];
+            }
+            const uint64_t mm = __ballot(in && match), mn = __ballot(in && !match);
+            if (in && match) {
+                const uint32_t o = out + (uint32_t)__popcll(mm & below);
+                tmp[p + o] = x;
+                ptmp[p + o] = pw;
+            } else if (in) {   // (o <= j: only positions this wave has read already)
+                const uint32_t o = nm + (uint32_t)__popcll(mn & below);
+                S[p + o] = x;
+                pay[p + o] = pw;
+            }
+            out += (uint32_t)__popcll(mm);
+            nm += (uint32_t)__popcll(mn);
+        }
+        if (out0 && lane == 0) headf[p + out0] = 1;   // a further source of the run
+        rem = nm;
+        __threadfence_block();   // (this wave's compacted words: read back next round)
+    }
+    __threadfence_block();
+    for (uint32_t j = lane; j < L; j += 64) {
+        S[p + j] = tmp[p + j];
+        pay[p + j] = ptmp[p + j];
+    }
+    __threadfence_block();
+    return true;
+}
+
 // One wave per listed run (longer than kOrdSmall): its length, then — if it holds an IPv6
 // packet — every packet's (family, address) in LDS, leaders, stable ranks; the words move through
-// the idle sort buffer (tmp / ptmp) at the same positions. More than kOrdLong packets with two
-// different sources: ERR_FIXUP (with the table's salted hash, a run that long holding two
-// sources does not occur by chance).
+// the idle sort buffer (tmp / ptmp) at the same positions. Longer mixed runs: ord_extract.
 __global__ __launch_bounds__(64) void k_ord_long(uint64_t *__restrict__ S, uint64_t *__restrict__ pay,
                                                  BatchState *bs, PacketIn in, const uint32_t *__restrict__ len,
                                                  uint8_t *__restrict__ headf, const uint32_t *__restrict__ list,
@@ -2043,9 +2098,12 @@ __global__ __launch_bounds__(64) void k_ord_long(uint64_t *__restrict__ S, uint6
             same &= t == t0 && k[0] == k0[0] && k[1] == k0[1] && k[2] == k0[2] && k[3] == k0[3];
         }
         if (__ballot(!same) == 0) continue;
-        if (L > kOrdLong) {
-            if (lane == 0) atomicOr(&bs->err, ERR_FIXUP);
-            return;
+        if (L > kOrdLong) {   // (an IPv6 flood source sharing a heavy source's hash)
+            if (!ord_extract(S, pay, headf, tmp, ptmp, p, L, in.hdr, seed, s)) {
+                if (lane == 0) atomicOr(&bs->err, ERR_FIXUP);
+                return;
+            }
+            continue;
         }
         for (uint32_t j = lane; j < L; j += 64) s_t[j] = ord_src(S[p + j], in.hdr, seed, s, s_k[j]);
         __syncthreads();

@@ -291,7 +291,7 @@ __global__ __launch_bounds__(256) void k_walk_heavy_sel(BatchState *bs, const ui
     if (c == 0) return;
     const uint32_t a = base0[lb + h];
     HeavyView hv{tags, ts, len, offs + (size_t)(lb + h) * tcap, rec, a, c, (n + kSortTile - 1) / kSortTile, n, h,
-                 (0x80u | h) * 0x01010101u};
+                 (0x80u | h) * 0x01010101u, &bs->err};
     Slot &sl = table[hs->slot[h]];
     FwState st = load_state(sl);
     HeavyMarkWriter mw{hv, list + 2u * a};
@@ -491,10 +491,27 @@ hipError_t launch_heavy_gather(const BatchState *bs, const uint8_t *tags, const 
     return hipGetLastError();
 }
 
+// Test hook (FSX_TEST_HEAVY_ROW_CORRUPT, tests/test_gpu_heavy.py): every heavy source's prefix
+// row is overwritten past its count — what round 5's aliasing did (ff010e0) — so the walker's
+// searches meet an inconsistent row; the batch must fail with -EIO instead of hanging.
+__global__ void k_test_corrupt_rows(const BatchState *bs, const uint32_t *cnt0, const uint32_t *base0,
+                                    uint32_t *offs, uint32_t tcap, uint32_t n, const HeavySet *hs) {
+    if (bs->err || !bs->hfast) return;
+    const uint32_t lb = bs->light_b, ntiles = (n + kSortTile - 1) / kSortTile;
+    for (uint32_t h = blockIdx.x; h < hs->n; h += gridDim.x) {
+        uint32_t *row = offs + (size_t)(lb + h) * tcap;
+        const uint32_t bad = base0[lb + h] + cnt0[lb + h] + 7u;
+        for (uint32_t t = threadIdx.x; t < ntiles; t += blockDim.x) row[t] = bad;
+    }
+}
+
 hipError_t launch_walk_heavy_sel(BatchState *bs, const uint32_t *cnt0, const uint32_t *base0, const uint32_t *offs,
                                  uint32_t tcap, const uint8_t *tags, const uint64_t *ts, const uint32_t *len,
                                  uint32_t n, const void *rec, Slot *table, const Limits &lim, HeavySet *hs,
                                  uint32_t *list, TableState *tstate, hipStream_t st) {
+    const bool corrupt = getenv("FSX_TEST_HEAVY_ROW_CORRUPT") != nullptr;   // (per call: tests set it)
+    if (corrupt) k_test_corrupt_rows<<<kHeavyMax, 256, 0, st>>>(bs, cnt0, base0, const_cast<uint32_t *>(offs), tcap,
+                                                                n, hs);
     k_walk_heavy_sel<<<kHeavyMax / 4, 256, 0, st>>>(bs, cnt0, base0, offs, tcap, tags, ts, len, n,
                                                      static_cast<const HeavyTileRec *>(rec), table, lim, hs, list,
                                                      tstate);

@@ -5,6 +5,7 @@
 #pragma once
 #include "fsx_dev_common.h"
 #include "fsx_internal.h"
+#include "fsx_search.h"
 #include "fsx_seg.h"
 
 namespace fsx {
@@ -25,8 +26,27 @@ struct HeavyView {
     const HeavyTileRec *rec;
     uint32_t base, cnt, ntiles, n, h;
     uint32_t pat;                 // (0x80 | h) in every byte
+    uint32_t *err = nullptr;      // BatchState::err: ERR_HEAVY_VIEW on an inconsistent row / tags
 
     __device__ __forceinline__ uint32_t pre(uint32_t t) const { return row[t] - base; }
+
+    // (a corrupted row or tag array fails the batch instead of hanging it)
+    __device__ __forceinline__ void fail() const {
+        if (err && lane_id() == 0) atomicOr(err, ERR_HEAVY_VIEW);
+    }
+
+    // the largest tile t with pre(t) <= r (bounded: ary64_step, fsx_search.h)
+    __device__ __forceinline__ uint32_t tile_of(uint32_t r) const {
+        const uint32_t lane = lane_id();
+        uint32_t lo = 0, hi = ntiles;
+        while (hi - lo > 1) {
+            const uint32_t step = ary64_width(lo, hi);
+            const uint32_t q = lo + lane * step;
+            const uint64_t m = __ballot(q < hi && pre(q) <= r);   // lane 0 (q = lo) on a valid row
+            if (!ary64_step(lo, hi, step, m)) fail();
+        }
+        return lo;
+    }
 
     // lane's 64 verdict bytes of tile t as 16 words (0 beyond n)
     __device__ __forceinline__ void tile_words(uint32_t t, uint32_t (&w)[16]) const {
@@ -55,16 +75,7 @@ struct HeavyView {
     // arrival index of h's r-th packet (r < cnt)
     __device__ __forceinline__ uint32_t select(uint32_t r) const {
         const uint32_t lane = lane_id();
-        uint32_t lo = 0, hi = ntiles;   // the largest tile t with pre(t) <= r lies in [lo, hi)
-        while (hi - lo > 1) {
-            const uint32_t step = (hi - lo + 63u) / 64u;
-            const uint32_t q = lo + lane * step;
-            const uint64_t m = __ballot(q < hi && pre(q) <= r);   // lane 0 (q = lo) always
-            const uint32_t f = 63u - (uint32_t)__clzll((long long)m);
-            lo = lo + f * step;
-            hi = min(hi, lo + step);
-        }
-        const uint32_t t = lo;
+        const uint32_t t = tile_of(r);
         uint32_t k = r - pre(t);
         uint32_t w[16];
         tile_words(t, w);
@@ -91,7 +102,9 @@ struct HeavyView {
         }
         const uint64_t bm = __ballot(mine);
         // (no lane: the tags do not hold r — a caller that rewrote the verdict buffer while the
-        // batch was in flight; an index inside the batch rather than a fault)
+        // batch was in flight, or a corrupted row; an index inside the batch rather than a
+        // fault, and the batch fails)
+        if (!bm) fail();
         return bm ? __shfl(idx, __ffsll((unsigned long long)bm) - 1) - 1u : n - 1u;
     }
 
@@ -146,16 +159,7 @@ struct HeavyView {
         s_idx[lane] = n;
         wave_lds_order();
         if (R0 < cnt) {
-            uint32_t lo = 0, hi = ntiles;   // (as select)
-            while (hi - lo > 1) {
-                const uint32_t step = (hi - lo + 63u) / 64u;
-                const uint32_t q = lo + lane * step;
-                const uint64_t mk = __ballot(q < hi && pre(q) <= R0);
-                const uint32_t f = 63u - (uint32_t)__clzll((long long)mk);
-                lo = lo + f * step;
-                hi = min(hi, lo + step);
-            }
-            uint32_t t = lo, k0 = R0 - pre(t), filled = 0;
+            uint32_t t = tile_of(R0), k0 = R0 - pre(t), filled = 0;
             const uint32_t want = min(64u, cnt - R0);
             while (filled < want && t < ntiles) {
                 uint32_t w[16];
@@ -185,6 +189,7 @@ struct HeavyView {
                 ++t;
                 wave_lds_order();
             }
+            if (filled < want) fail();   // (the tiles ran out before the ranks did)
         }
         wave_lds_order();
         return s_idx[lane];

@@ -39,6 +39,7 @@ enum : uint32_t {
     ERR_SORT_HANG = 8u,
     ERR_HIST_FULL = 16u,
     ERR_CANCELED = 32u,   // pipelined batches: the batch before this one failed
+    ERR_HEAVY_VIEW = 64u, // a heavy source's tile-count row / tags inconsistent (fsx_heavy_view.h)
 };
 
 enum : uint32_t { SLOT_HAS_ST = 1u, SLOT_HAS_BL = 2u, SLOT_HAS_TB = 4u };

@@ -160,7 +160,7 @@ __device__ __forceinline__ unsigned long long tb_get(const unsigned long long *p
 }
 
 __device__ __forceinline__ int64_t tb_lookback(unsigned long long *status, uint32_t t, const CMap &agg,
-                                               int64_t hi) {
+                                               int64_t hi, uint32_t *err) {
     const uint32_t lane = lane_id();
     constexpr unsigned long long kM62 = (1ull << 62) - 1ull, kM63 = (1ull << 63) - 1ull;
     unsigned long long *my = status + 3ull * t;
@@ -194,7 +194,10 @@ __device__ __forceinline__ int64_t tb_lookback(unsigned long long *status, uint3
         const uint32_t l2 = b2 ? (uint32_t)__ffsll((unsigned long long)b2) - 1u : 64u;
         const uint32_t l0 = b0 ? (uint32_t)__ffsll((unsigned long long)b0) - 1u : 64u;
         if (l0 < l2) {   // a tile before the nearest state has published nothing yet: wait
-            if (++spins > (1u << 22)) break;   // (never expected: lower tickets are running)
+            if (++spins > (1u << 22)) {   // (never expected: lower tickets are running)
+                if (lane == 0 && err) atomicOr(err, ERR_SORT_HANG);   // the batch fails (-EIO)
+                break;
+            }
             __builtin_amdgcn_s_sleep(1);
             continue;
         }
@@ -229,7 +232,8 @@ __device__ __forceinline__ void tb_tile(const SV &sv, uint32_t t, uint32_t M,
                                         const uint32_t *__restrict__ seg_slot, Slot *table,
                                         const Limits &lim, CMap *tile_map, const int64_t *tile_x,
                                         uint8_t *__restrict__ marks, CMap *s_w, uint32_t *s_tmp,
-                                        unsigned long long *status = nullptr, int64_t *s_x = nullptr) {
+                                        unsigned long long *status = nullptr, int64_t *s_x = nullptr,
+                                        uint32_t *err = nullptr) {
     constexpr bool kApply = kMode != 0;
     const uint32_t tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
     const uint32_t p0 = t * kTile + tid * 16u;
@@ -321,7 +325,7 @@ __device__ __forceinline__ void tb_tile(const SV &sv, uint32_t t, uint32_t M,
             if (w == 0) {   // (wave 0 looks back)
                 CMap a = s_w[0];
                 for (int k = 1; k < 4; ++k) a = cm_compose(s_w[k], a);
-                const int64_t xin = tb_lookback(status, t, a, hi);
+                const int64_t xin = tb_lookback(status, t, a, hi, err);
                 if (lane == 0) *s_x = xin;
             }
             __syncthreads();
@@ -430,10 +434,10 @@ __global__ __launch_bounds__(256, FSX_TB_SCAN_MINB) void k_tb_scan(const uint64_
     if (t >= ntiles) return;
     if (bs->pay_ok)
         tb_tile<2>(SegView<true>{S, ts, len, pay, ~bs->inv_min_ts}, t, M, headf, tile_off, seg_j, seg_x, seg_slot,
-                   table, lim, tile_map, nullptr, marks, s_w, s_tmp, status, &s_x);
+                   table, lim, tile_map, nullptr, marks, s_w, s_tmp, status, &s_x, &bs->err);
     else
         tb_tile<2>(SegView<false>{S, ts, len, pay, 0}, t, M, headf, tile_off, seg_j, seg_x, seg_slot, table, lim,
-                   tile_map, nullptr, marks, s_w, s_tmp, status, &s_x);
+                   tile_map, nullptr, marks, s_w, s_tmp, status, &s_x, &bs->err);
 }
 
 // One block: the state entering every tile (tile 0 starts with a source head, so its
@@ -908,7 +912,7 @@ __global__ __launch_bounds__(256) void k_walk_sw_heavy_sel(BatchState *bs, const
     const uint32_t a = base0[lb + h];
     uint32_t *sx = s_idx[wv];
     const HeavyView hv{tags, ts, len, offs + (size_t)(lb + h) * tcap, hrec, a, c, (n + kSortTile - 1) / kSortTile,
-                       n, h, (0x80u | h) * 0x01010101u};
+                       n, h, (0x80u | h) * 0x01010101u, &bs->err};
     const uint32_t cur = tst->hist_cur;
     uint64_t *ht = hb.t[cur];
     uint32_t *hl = hb.l[cur];
@@ -1089,7 +1093,8 @@ __device__ __forceinline__ SwClock sw_clock(const BatchState *bs, const TableSta
 // The history rebuild's tile offsets in one pass (kMode 2, k_sw_hist_scan not needed): tiles in
 // ticket order, per tile one status word — 1 << 62 | its entries, or 2 << 62 | the entries of
 // every tile up to it (the word is the data) — and wave 0 looks back 64 tiles at a time.
-__device__ __forceinline__ uint64_t hist_lookback(unsigned long long *status, uint32_t t, uint64_t cnt) {
+__device__ __forceinline__ uint64_t hist_lookback(unsigned long long *status, uint32_t t, uint64_t cnt,
+                                                  uint32_t *err) {
     const uint32_t lane = lane_id();
     constexpr unsigned long long kM = (1ull << 62) - 1ull;
     if (t == 0) {
@@ -1109,7 +1114,10 @@ __device__ __forceinline__ uint64_t hist_lookback(unsigned long long *status, ui
         const uint32_t l2 = b2 ? (uint32_t)__ffsll((unsigned long long)b2) - 1u : 64u;
         const uint32_t l0 = b0 ? (uint32_t)__ffsll((unsigned long long)b0) - 1u : 64u;
         if (l0 < l2) {   // a tile before the nearest prefix has published nothing yet
-            if (++spins > (1u << 22)) break;   // (never expected: lower tickets are running)
+            if (++spins > (1u << 22)) {   // (never expected: lower tickets are running)
+                if (lane == 0) atomicOr(err, ERR_SORT_HANG);   // the batch fails (-EIO)
+                break;
+            }
             __builtin_amdgcn_s_sleep(1);
             continue;
         }
@@ -1176,7 +1184,7 @@ __global__ __launch_bounds__(256) void k_sw_hist(const uint64_t *__restrict__ S,
                 const uint32_t ex = block256_excl(cnt, s_tmp, &tot);
                 if (threadIdx.x < 64) {   // (wave 0)
                     const uint64_t b = hist_lookback(reinterpret_cast<unsigned long long *>(hb.tile_off),
-                                                     (uint32_t)t, tot);
+                                                     (uint32_t)t, tot, const_cast<uint32_t *>(&bs->err));
                     if (threadIdx.x == 0) {
                         s_base = b;
                         if (t == ntiles - 1) *hb.total = b + tot;

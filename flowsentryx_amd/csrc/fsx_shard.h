@@ -71,6 +71,8 @@ constexpr uint32_t kShardFilter = 1u;   // fsx_shard_pack_device flag (FSX_SHARD
 constexpr uint32_t kShardCompact = 2u;  // fsx_shard_pack_device flag (FSX_SHARD_COMPACT)
 constexpr uint32_t kShardDropRecords = 4u;   // fsx_shard_pack_device flag (FSX_SHARD_DROP_RECORDS)
 constexpr uint32_t kShardRegions = 8u;       // fsx_shard_pack_device flag (FSX_SHARD_REGIONS)
+// counts[G + 1] of a pack whose placement look-back timed out (never expected): the host raises
+constexpr uint32_t kShardPackErr = 1u;
 
 // owner = floor(h * G / 2^32) of a 32-bit mix of (family tag, address).
 __host__ __device__ inline uint32_t shard_owner_of(uint32_t tag, const uint32_t k[4], uint32_t G) {

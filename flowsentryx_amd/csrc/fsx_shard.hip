@@ -197,7 +197,7 @@ __global__ __launch_bounds__(256) void k_shard_parse(const uint8_t *__restrict__
 constexpr uint32_t kPlaceSpin = 1u << 22;
 
 __device__ __forceinline__ uint32_t place_lookback(unsigned long long *status, uint32_t t, uint32_t o,
-                                                   uint32_t Gx, uint32_t tot) {
+                                                   uint32_t Gx, uint32_t tot, unsigned long long *wide) {
     unsigned long long *my = status + (size_t)t * Gx + o;
     if (t == 0) {
         __hip_atomic_store(my, (2ull << 62) | tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -210,7 +210,10 @@ __device__ __forceinline__ uint32_t place_lookback(unsigned long long *status, u
                                                        __HIP_MEMORY_SCOPE_AGENT);
         const uint32_t flag = (uint32_t)(w >> 62);
         if (flag == 0) {   // not published yet (its block holds a lower ticket: it is running)
-            if (++spins > kPlaceSpin) break;   // (never expected; a bounded wait, not a hang)
+            if (++spins > kPlaceSpin) {   // (never expected; a bounded wait, not a hang)
+                atomicOr(wide, 2ull);   // -> the pack's record size reads kShardPackErr
+                break;
+            }
             __builtin_amdgcn_s_sleep(1);
             continue;
         }
@@ -292,7 +295,7 @@ __global__ __launch_bounds__(256) void k_shard_place16(const uint8_t *__restrict
         const uint32_t c0 = s_wc[0][o], c1 = s_wc[1][o], c2 = s_wc[2][o], c3 = s_wc[3][o];
         const uint32_t tot = c0 + c1 + c2 + c3;
         cnt[(size_t)o * ntiles + t] = tot;
-        const uint32_t b = place_lookback(status, t, o, Gx, tot);
+        const uint32_t b = place_lookback(status, t, o, Gx, tot, wide);
         s_wc[0][o] = b;
         s_wc[1][o] = b + c0;
         s_wc[2][o] = b + c0 + c1;
@@ -420,7 +423,11 @@ __global__ __launch_bounds__(1024) void k_shard_scan(uint32_t *__restrict__ cnt,
     if (threadIdx.x == 0) {
         owner_total[o] = carry;
         // compact requests: the wide flag of k_shard_parse becomes the record size
-        if (o == 0 && compact) owner_total[G + 1] = owner_total[G + 1] ? 32u : 16u;
+        // (bit 1: a look-back of k_shard_place16 timed out — the host raises on kShardPackErr)
+        if (o == 0 && compact) {
+            const uint64_t wf = owner_total[G + 1];
+            owner_total[G + 1] = (wf & 2u) ? kShardPackErr : wf ? 32u : 16u;
+        }
     }
 }
 
@@ -436,7 +443,8 @@ __global__ __launch_bounds__(256) void k_shard_pack(const uint8_t *__restrict__ 
                                                     uint64_t *__restrict__ owner_total,
                                                     int compact, uint32_t drop_rec, int regions) {
     const int use_rep = use_rep0 && (!use_dev || *use_dev);
-    if (compact && owner_total[G + 1] == 16u) return;   // k_shard_pack16 / k_shard_place16 placed them
+    // (k_shard_pack16 / k_shard_place16 placed them; or a failed placement: nothing more)
+    if (compact && (owner_total[G + 1] == 16u || owner_total[G + 1] == kShardPackErr)) return;
     __shared__ uint32_t s_base[kMaxShards + 1];
     __shared__ uint32_t s_wc[4][kMaxShards + 1];
     const uint32_t t = blockIdx.x, lane = lane_id(), w = threadIdx.x >> 6;

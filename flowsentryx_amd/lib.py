@@ -195,6 +195,7 @@ ABI_SYMBOLS = [
 
 SHARD_RECORD_BYTES = 32
 SHARD_RECORD16_BYTES = 16
+SHARD_PACK_ERR = 1   # counts[G + 1] of a pack whose device placement failed (FSX_SHARD_PACK_ERR)
 SHARD_BLOCK_BYTES = 32
 SHARD_FILTER_BLOCKLIST = 1
 SHARD_COMPACT = 2

@@ -561,6 +561,8 @@ class ShardedDataPlane:
             rw = [int(both[base + r * k + j]) for r in range(G)]
             self.filtered += int(cj[G])
             rb = int(cj[G + 1])
+            if rb not in (lib.SHARD_RECORD16_BYTES, lib.SHARD_RECORD_BYTES):   # (FSX_SHARD_PACK_ERR)
+                raise RuntimeError(f"sharded pack of sub-batch {j} failed on the device (record size {rb})")
             sc = [int(x) for x in cj[:G]]
             rc = [x >> 1 for x in rw]
             rf = [lib.SHARD_RECORD16_BYTES if x & 1 else lib.SHARD_RECORD_BYTES for x in rw]

@@ -329,6 +329,7 @@ int fsx_flow_features(fsx_ctx *ctx, const uint8_t *hdr, const uint32_t *len,
  * Host-only (no device work). */
 uint32_t fsx_shard_owner(const uint8_t *key16, int family, uint32_t n_shards);
 #define FSX_SHARD_RECORD16_BYTES 16 /* {u32 ipv4 key; u16 len; u16 dport; u64 ts} */
+#define FSX_SHARD_PACK_ERR 1        /* d_counts[n_shards + 1] of a failed placement */
 #define FSX_SHARD_BLOCK_BYTES 32    /* {u32 key[4]; u64 till; u32 tag (1 v4, 2 v6); u32 pad} */
 #define FSX_SHARD_FILTER_BLOCKLIST 1u
 #define FSX_SHARD_COMPACT 2u
@@ -346,7 +347,9 @@ uint32_t fsx_shard_owner(const uint8_t *key16, int family, uint32_t n_shards);
  * when timestamps are non-decreasing over all batches so far (fsx_shard_clock_device).
  * With FSX_SHARD_COMPACT, d_counts has n_shards + 2 entries and d_counts[n_shards + 1]
  * receives the record size written: FSX_SHARD_RECORD16_BYTES when no IP packet of the
- * slice is IPv6 or 64 KiB or longer, else FSX_SHARD_RECORD_BYTES. With
+ * slice is IPv6 or 64 KiB or longer, else FSX_SHARD_RECORD_BYTES — or FSX_SHARD_PACK_ERR
+ * when the placement failed on the device (a bounded look-back timed out; the caller must
+ * treat the pack as failed). With
  * FSX_SHARD_DROP_RECORDS (and the filter), the replica-dropped packets are written as
  * records too, after every owner's run, in arrival order (d_counts[n_shards] of them; the
  * first sum(d_counts[0..n_shards)) records are the ones to send), so the arrival rank can

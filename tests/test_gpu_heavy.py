@@ -96,6 +96,24 @@ def test_unsorted_heavy_path_config2_slices(native, oracle, max_entries):
          dict(CFG, max_entries=max_entries), want_path=[1, 1])
 
 
+def test_corrupted_heavy_row_fails_not_hangs(native, oracle, monkeypatch):
+    """round 5's aliasing bug (ff010e0) corrupted the heavy sources'
+    pass-0 tile-count rows and the rank view's search never ended. With the rows overwritten
+    through a test hook (FSX_TEST_HEAVY_ROW_CORRUPT), the bounded searches (fsx_search.h)
+    flag ERR_HEAVY_VIEW and the batch fails with -EIO; a fresh context afterwards is exact."""
+    import errno
+    from flowsentryx_amd import lib
+    hdr, ln, ts = _config2(oracle, 1 << 20)
+    monkeypatch.setenv("FSX_TEST_HEAVY_ROW_CORRUPT", "1")
+    with native.FsxContext(max_batch=1 << 20, **CFG) as c:
+        with pytest.raises(lib.FsxError) as e:
+            c.verdict_batch(hdr, ln, ts)
+        assert e.value.code == -errno.EIO
+        assert "rank view" in str(e.value)
+    monkeypatch.delenv("FSX_TEST_HEAVY_ROW_CORRUPT")
+    _run(native, oracle, [(hdr, ln, ts)], CFG, want_path=[1])
+
+
 def test_unsorted_heavy_path_pipelined(native, oracle):
     """The same slices pipelined (the tail of one batch beside the next batch's front:
     per-set tile sums and chunk counts)."""

@@ -106,6 +106,33 @@ def test_ordered_repeated_ipv6_source(native, oracle):
         assert o.stats()[1] > 0   # (the repeated source was blacklisted)
 
 
+def test_ordered_long_mixed_ipv6_run(native, oracle):
+    """A key-hash run far longer than k_ord_long's LDS regroup (kOrdLong = 512) that holds many
+    sources (a heavy IPv6 source sharing its 32-bit key hash with flood sources):
+    under FSX_FLAG_TEST_V6_COLLIDE ~77 IPv6 carpet sources share each key hash, and one of them
+    is repeated 3000 times. The run is separated source by source (ord_extract) instead of
+    failing the batch; verdicts, stats and maps equal the oracle, the source is blacklisted."""
+    from flowsentryx_amd import synth
+    p, s = synth.config_params(5, n=1 << 19)
+    n = int(p.n)
+    hdr, ln, ts = oracle.synth(p, s, 0, n)
+    hdr = hdr.copy()
+    ln = ln.copy()
+    v6 = np.nonzero((hdr[:, 12] == 0x86) & (hdr[:, 13] == 0xDD))[0]
+    rng = np.random.default_rng(19)
+    src = v6[3]
+    dst = np.sort(rng.choice(np.arange(v6[3] + 1, n), 3000, replace=False))
+    hdr[dst] = hdr[src]
+    ln[dst] = ln[src]
+    cfg = dict(max_entries=1 << 20)
+    o = oracle.Oracle(flags=1, **cfg)
+    with native.FsxContext(max_batch=n, flags=_flags("FLAG_ORDERED_INSERTS", "FLAG_TEST_V6_COLLIDE"), **cfg) as c:
+        _verdicts_equal(c.verdict_batch(hdr, ln, ts), o.batch(hdr, ln, ts))
+        assert c.last_batch_info()["ordered_inserts"] == 1
+        _same_state(c, o, (1, 2, 3, 4))
+        assert o.stats()[1] > 0   # (the repeated source was blacklisted)
+
+
 def test_ordered_inserts_follow_a_flood(native, oracle):
     """Without the flag the host chooses: a batch after a flood (new sources > half of its IP
     packets) takes the home-ordered path, a batch after a stream of known sources does not."""

@@ -406,6 +406,22 @@ def test_pipelined_reset_every_batch(native, oracle, same_batch, resets):
     _run(native, oracle, batches, between=between)
 
 
+def test_pipelined_reset_into_recycled_spare(native, oracle, monkeypatch):
+    """The spare table set may come from recycled device memory: with
+    FSX_TEST_SPARE_POISON its slots are filled at allocation with live-looking lines of the
+    very table generation the first pipelined reset moves to (state + blacklist entries). The
+    allocation zeroes it, so after the swap-in verdicts, stats_map and every map dump equal
+    the oracle's from empty maps — no phantom source."""
+    monkeypatch.setenv("FSX_TEST_SPARE_POISON", "1")
+    batches = _config2_batches(oracle, 1 << 18, [0, 100_000, 200_000, 1 << 18])
+
+    def between(j, c, o):
+        if j < len(batches) - 1:
+            c.reset()
+            o.reset()
+    _run(native, oracle, batches, between=between)
+
+
 def test_pipelined_failed_batch_then_reset(native, oracle):
     """A batch fails (max_entries) and the caller resets before its error is seen: the batch
     after the reset runs on fresh tables and is not cancelled; the error surfaces at sync;
