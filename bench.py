@@ -932,12 +932,14 @@ def main():
         bytes_per_launch = kb["algo"] * units
         achieved = bytes_per_launch / (per_launch_ms * 1e-3) / 1e9 if kb["algo"] else None
         traffic = None
+        traffic_src = None
         pmc = ROOT / "profiles" / "pmc_traffic.json"
         if pmc.exists():
             doc = json.loads(pmc.read_text())
             wl = doc.get("workload", {})
             if wl.get("packets_per_gpu") == n and wl.get("config") == args.config and world == 1:
                 traffic = doc.get("kernels", {}).get(name, {}).get("hbm_bytes_per_launch")
+                traffic_src = doc.get("source")
         roofline = {
             "bound": "hbm", "kernel": name, "achieved": round(achieved, 1) if achieved else None,
             "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -945,7 +947,7 @@ def main():
             "traffic": traffic, "bytes_per_unit": kb["algo"], "unit_of_work": kb["unit"],
             "impl_bytes_per_unit": kb["impl"], "bytes_per_launch": bytes_per_launch,
             "launch_ms": round(per_launch_ms, 4), "launches_per_step": launches,
-            "traffic_source": "profiles/pmc_traffic.json (rocprofv3 PMC passes, FETCH_SIZE x2 + WRITE_SIZE)"
+            "traffic_source": f"profiles/pmc_traffic.json ({traffic_src}; FETCH_SIZE x2 + WRITE_SIZE)"
             if traffic else None,
         }
     pipeline = None

@@ -230,7 +230,7 @@ static void free_scratch(fsx_ctx *c) {
     hipFree(s.span_list); hipFree(s.sort_ctl); hipFree(s.gbase); hipFree(s.status);
     hipFree(s.lim_tiles); hipFree(s.sw_seg); hipFree(s.sketch); hipFree(s.heavy);
     hipFree(s.drop_list); hipFree(s.drop_cur); hipFree(s.heavy_flow);
-    hipFree(s.chunk_cnt); hipFree(s.hrec); hipFree(s.hflow);
+    hipFree(s.chunk_cnt); hipFree(s.hrec); hipFree(s.hflow); hipFree(s.tbh);
     hipFree(s.admit_rank); hipFree(s.admit_cnt);
     s = Scratch{};
 }
@@ -282,6 +282,7 @@ static int alloc_scratch(fsx_ctx *c, uint64_t cap) {
     HIPCHK(c, hipMalloc(&s.chunk_cnt, chunk_cnt_bytes(cap)));
     HIPCHK(c, hipMalloc(&s.hrec, heavy_rec_bytes(cap)));
     HIPCHK(c, hipMalloc(&s.hflow, hflow_bytes(cap)));
+    if (c->cfg.limiter == FSX_LIMIT_TOKEN_BUCKET) HIPCHK(c, hipMalloc(&s.tbh, tb_heavy_bytes(cap)));
     s.cap = cap;
     return 0;
 }

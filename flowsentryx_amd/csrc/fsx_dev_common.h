@@ -10,6 +10,14 @@ namespace fsx {
 // ------------------------------------------------------------------ helpers
 __device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
 
+// Sorted positions a kernel covers: every IP packet, or (light_only 1) the light ones only
+// — the heavy sources' verdicts come from their lists — or (2, the token bucket's heavy
+// sources) the light ones only when the batch took the unsorted path (k_hmode), where the
+// heavy sources never entered the sort.
+__device__ __forceinline__ uint32_t cover_n(const BatchState *bs, uint32_t light_only) {
+    return light_only == 1 || (light_only == 2 && bs->hfast) ? bs->n_light : bs->n_valid;
+}
+
 // Orders this wave's LDS accesses for the compiler (the hardware executes one wave's LDS
 // operations in order). A wavefront-scope fence would also wait for every outstanding
 // global load (s_waitcnt vmcnt(0)), draining software-pipelined prefetches each step.

@@ -1723,7 +1723,7 @@ __global__ __launch_bounds__(256) void k_heads_count(const uint64_t *__restrict_
                                                      uint32_t *__restrict__ sub_cnt, uint32_t light_only,
                                                      uint32_t ord = 0) {
     __shared__ uint32_t s_tmp[4];
-    const uint32_t M = light_only ? bs->n_light : bs->n_valid;
+    const uint32_t M = cover_n(bs, light_only);
     const uint32_t ntiles = (M + kTile - 1) / kTile;
     const uint32_t lane = lane_id();
     // (ord: k_ord_fix marked the starts of the sources it separated inside a key-hash run)
@@ -1770,7 +1770,7 @@ __global__ __launch_bounds__(256) void k_heads_count(const uint64_t *__restrict_
 __global__ __launch_bounds__(256) void k_scan_tiles_u32(uint32_t *__restrict__ cnt, BatchState *bs,
                                                         uint32_t *seg_start, uint32_t light_only) {
     __shared__ uint32_t s_tmp[4];
-    const uint32_t M = light_only ? bs->n_light : bs->n_valid;
+    const uint32_t M = cover_n(bs, light_only);
     const uint32_t ntiles = (M + kTile - 1) / kTile;
     uint32_t carry = 0;
     for (uint32_t c0 = 0; c0 < ntiles; c0 += 1024) {
@@ -1799,7 +1799,7 @@ __global__ __launch_bounds__(256) void k_heads_write(BatchState *bs, const uint8
                                                      uint32_t light_only, uint32_t *__restrict__ seg_lo) {
     __shared__ uint32_t s_tmp[4];
     __shared__ uint32_t s_pos[kTile];   // the tile's head positions, compacted
-    const uint32_t M = light_only ? bs->n_light : bs->n_valid;
+    const uint32_t M = cover_n(bs, light_only);
     const uint32_t ntiles = (M + kTile - 1) / kTile;
     for (uint32_t b = blockIdx.x; b < ntiles; b += gridDim.x) {
         // XCD-aware order: the compacted runs of neighbouring tiles share cache lines
@@ -3101,11 +3101,12 @@ __device__ __forceinline__ void load_marks16(const uint8_t *marks, uint32_t p0, 
     }
 }
 
-// (light_only: the heavy sources' positions [n_light, n_valid) have verdict lists instead)
+// (light_only: the heavy sources' positions [n_light, n_valid) have verdict lists instead;
+// 2: the token bucket's heavy sources, decided outside the sort only on the unsorted path)
 __global__ __launch_bounds__(256) void k_fill_last(const uint8_t *__restrict__ marks, BatchState *bs,
                                                    uint8_t *__restrict__ tile_last, uint32_t light_only) {
     __shared__ uint32_t s_w[4];
-    const uint32_t M = light_only ? bs->n_light : bs->n_valid;
+    const uint32_t M = cover_n(bs, light_only);
     const uint32_t ntiles = (M + kTile - 1) / kTile;
     for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
         const uint32_t p0 = t * kTile + threadIdx.x * 16u;
@@ -3134,7 +3135,7 @@ __global__ __launch_bounds__(1024) void k_fill_carry(uint8_t *__restrict__ tile_
                                                      uint32_t light_only) {
     __shared__ uint32_t s_w[16];
     __shared__ uint32_t s_carry;
-    const uint32_t M = light_only ? bs->n_light : bs->n_valid;
+    const uint32_t M = cover_n(bs, light_only);
     const uint32_t ntiles = (M + kTile - 1) / kTile;
     const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
     if (threadIdx.x == 0) s_carry = 0;
@@ -3180,7 +3181,7 @@ __global__ __launch_bounds__(256) void k_fill_scatter(const uint8_t *__restrict_
     __shared__ uint32_t s_cc[kMaxTileChunks];   // per arrival chunk: tile count, then base
     __shared__ uint16_t s_rk[kTile];            // per DROP position: rank in its chunk
     if (bs->err) return;
-    const uint32_t M = light_only ? bs->n_light : bs->n_valid;
+    const uint32_t M = cover_n(bs, light_only);
     const uint32_t ntiles = (M + kTile - 1) / kTile;
     const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
     // batches of <= kMaxTileChunks chunks: a tile reserves its DROPs' list slots with one
@@ -3451,7 +3452,10 @@ hipError_t launch_tail(const TailArgs &a) {
     uint64_t *S_fin = sc.packed[1], *pay_fin = sc.pay[1];
     // heavy verdict lists live in the parse buffer over the heavy positions (which no pass
     // writes after pass 0 read it)
-    const HeavyLists hlists{tagh ? reinterpret_cast<uint32_t *>(sc.packed[0]) : nullptr, sc.heavy,
+    // (the token bucket's heavy packets get their verdict bytes directly: launch_tb_heavy, or on
+    // the run path the fill's DROP stores and k_tb_untag)
+    const bool tb_tag = tagh && do_limit && lim.limiter == 2;
+    const HeavyLists hlists{tagh && !tb_tag ? reinterpret_cast<uint32_t *>(sc.packed[0]) : nullptr, sc.heavy,
                             tstate, bs};
     // (lazy slots: the fixed window's walkers write a new source's family and key)
     const SlotKeys skeys{a.lazy ? a.X.heads : nullptr, a.X.k6, a.lazy && a.fresh_bit ? 1u : 0u, lim.tgen};
@@ -3492,6 +3496,12 @@ hipError_t launch_tail(const TailArgs &a) {
                 return e;
             mark_on("k_walk_heavy_sel", hs_id);
         }
+        if (a.hfm && tb_tag) {   // token bucket: the heavy packets' verdicts in arrival order (unsorted path)
+            if ((e = launch_tb_heavy(bs, sc.sort_ctl, sc.gbase, sc.hist, tcap, verdict, ts, n, sc.hrec, sc.tbh, table,
+                                     lim, sc.heavy, tstate, hs)) != hipSuccess)
+                return e;
+            mark_on("k_tb_heavy", hs_id);
+        }
         // (pipelined: the heavy walker beside the tail's chain; k_verdict_apply joins it)
         if (heavy_join && (e = hipEventRecord(walk_join_ev, hs)) != hipSuccess) return e;
         if (flows) {
@@ -3518,12 +3528,15 @@ hipError_t launch_tail(const TailArgs &a) {
         hf_id = fork ? 1 : 0;
         // unsorted heavy sources: their walker (select / rank searches, latency-bound on 32
         // blocks) on the flow stream ahead of the heavy flow rows, not ahead of the heads
-        if (a.hfm && lim.limiter == 0 && st2 && walk_join_ev) {
+        if (a.hfm && (lim.limiter == 0 || tb_tag) && st2 && walk_join_ev) {
             hs = st2;
             hs_id = 1;
             heavy_join = true;
         }
     }
+    // (unsplit: the token bucket's heavy kernels on the walker stream are joined before the
+    // verdicts are final — no fork of walkers follows them there)
+    if (!(split && split->tail) && a.hfm && tb_tag && hs != st && walk_join_ev) heavy_join = true;
     if (split && split->tail && do_limit && lim.limiter == 1) k_sw_tail_check<<<1, 1, 0, st>>>(bs, tstate, lim);
     // unsorted heavy sources: their carried state decides the path now that the previous
     // batch's walkers have stored it; those sent back to the run path get their runs first
@@ -3647,7 +3660,11 @@ hipError_t launch_tail(const TailArgs &a) {
     }
     if (!do_limit) return hipGetLastError();
     if (lim.limiter == 2) {   // FSX_LIMIT_TOKEN_BUCKET
-        if ((e = launch_token_bucket(S, ts, len, bs, sc, table, lim, n, st, mk)) != hipSuccess) return e;
+        // (tagged heavy packets on the run path: their runs' heads and the tiles' segment offsets)
+        if (tb_tag && (e = launch_tb_run_heads(bs, sc.seg_start, sc.headf, sc.tile_aux, n, st)) != hipSuccess)
+            return e;
+        if ((e = launch_token_bucket(S, ts, len, bs, sc, table, lim, n, st, mk, tb_tag ? 2u : 0u)) != hipSuccess)
+            return e;
     } else {
         uint32_t *cls = sc.sort_ctl + 1028;
         const uint32_t short_seg = lim.limiter == 1 ? kShortSegSliding : kShortSegFixed;
@@ -3680,8 +3697,9 @@ hipError_t launch_tail(const TailArgs &a) {
             if (fork3 && (e = hipStreamWaitEvent(st, walk_join_ev, 0)) != hipSuccess) return e;
         }
     }
-    k_fill_last<<<gridTiles, 256, 0, st>>>(sc.marks, bs, sc.tile_last, tagh ? 1u : 0u);
-    k_fill_carry<<<1, 1024, 0, st>>>(sc.tile_last, bs, tagh ? 1u : 0u);
+    const uint32_t fill_lo = tb_tag ? 2u : tagh ? 1u : 0u;   // (cover_n)
+    k_fill_last<<<gridTiles, 256, 0, st>>>(sc.marks, bs, sc.tile_last, fill_lo);
+    k_fill_carry<<<1, 1024, 0, st>>>(sc.tile_last, bs, fill_lo);
     mark("k_fill_last");
     // Light DROPs (heavy verdict lists on: the rest are lists) stored straight into the
     // verdicts: config 4's 12.8M light DROPs 1.11 -> 0.32 ms. Without heavy lists (the token
@@ -3689,9 +3707,10 @@ hipError_t launch_tail(const TailArgs &a) {
     // 33M scattered byte stores took 0.44 ms and 1.15 GB. (FSX_DROP_LISTS=1: lists always.)
     static const bool drop_lists = getenv("FSX_DROP_LISTS") != nullptr;
     k_fill_scatter<<<gridTiles, 256, 0, st>>>(sc.marks, S, bs, sc.tile_last, sc.drop_list, sc.drop_cur,
-                                              tstate, cdiv(n, kVChunk), tagh ? 1u : 0u,
+                                              tstate, cdiv(n, kVChunk), fill_lo,
                                               drop_lists || !tagh ? nullptr : verdict);
     mark("k_fill_scatter");
+    if (tb_tag && (e = launch_tb_untag(bs, verdict, n, st)) != hipSuccess) return e;   // (run path only)
     if (heavy_join && (e = hipStreamWaitEvent(st, walk_join_ev, 0)) != hipSuccess) return e;
     k_verdict_apply<<<cdiv(n, kVChunk), 256, 0, st>>>(verdict, n, sc.drop_list, sc.drop_cur, bs, sc.heavy,
                                                       hlists.list);
@@ -3795,6 +3814,8 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
     static const bool no_hlists = getenv("FSX_NO_HEAVY_LISTS") != nullptr;
     const bool lists_any = do_limit && verdict && !no_hlists && !admit;
     const bool lists_ok = lists_any && lim.limiter == 0;
+    // heavy verdict lists (fixed / sliding window with the heavy-source sort; FSX_NO_HEAVY_LISTS=1: A/B)
+    const bool lists_sw0 = lists_any && lim.limiter == 1;
     const uint32_t bshift = std::max<uint32_t>(56, kIdShift + idbits);
     const uint32_t lbits = 63 - bshift;                 // light digit bits of the bucket
     const uint32_t hrest = idbits > lbits ? idbits - lbits : 0;
@@ -3802,9 +3823,7 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
     const bool heavy_sort = !admit && !onesweep && !full_digits && !no_heavy && idbits <= 25 && npass >= 3 &&
                             (hpass == 3 || (hpass == 4 && lists_ok));
     if (heavy_sort) npass = hpass;   // (24-bit ids: 4 passes instead of 3, 3 of them over the light entries)
-    // heavy verdict lists (fixed / sliding window with the heavy-source sort; FSX_NO_HEAVY_LISTS=1: A/B)
-    const bool lists_sw = lists_any && lim.limiter == 1 && (npass & 1);
-    const bool tagh = heavy_sort && (lists_ok || lists_sw);
+    const bool lists_sw = lists_sw0 && (npass & 1);
     // heavy slots resolved once in k_heavy_pick (FSX_NO_HEAVY_SLOTS=1: A/B). Under prefix rules
     // the pick leaves every source whose /24 a rule touches light (rule_maybe), so a heavy
     // source is never rule-dropped and may be inserted there (round 5; FSX_RULES_LAZY_HEAVY=1:
@@ -3813,12 +3832,21 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
     static const bool rules_lazy = getenv("FSX_RULES_LAZY_HEAVY") != nullptr;
     const bool rl_batch = do_limit && rules.slot;
     const uint32_t resolve = !no_hslots && !(rl_batch && (rules_lazy || in.rec)) ? 1u : 0u;
+    // token bucket: the heavy sources outside the sort (launch_tb_heavy; round 6, VERDICT r05
+    // item 4) — tagged heavy packets with resolved slots, the heavy runs in the light entries'
+    // final buffer (an odd pass count) for the run path. Bit-exact and measured slower than the
+    // heavy-source sort (4.70 / 4.74 vs 3.96 / 3.94 ms per 64M packets), so
+    // opt-in: FSX_TB_UNSORTED=1 (read per batch: tests switch it)
+    const bool tb_unsorted = getenv("FSX_TB_UNSORTED") != nullptr;
+    const bool lists_tb = lists_any && lim.limiter == 2 && (npass & 1) && resolve && tb_unsorted;
+    const bool tagh = heavy_sort && (lists_ok || lists_sw || lists_tb);
     // heavy sources outside the sort (fsx_heavy.hip): header records with resolved heavy
     // slots; k_hmode picks the batch's path on the device (FSX_NO_HFAST=1: the runs, A/B)
     static const bool no_hfast = getenv("FSX_NO_HFAST") != nullptr;
     // (record mode too: the records' len / ts go to in.rec_len / rec_ts, which k_pass0h reads)
     // (sliding window: FSX_FLAG_SW_UNSORTED only — measured slower than the sort)
-    const bool hfm = tagh && (lim.limiter == 0 || (lim.limiter == 1 && (lim.test_flags & kFlagSwUnsorted))) &&
+    const bool hfm = tagh && (lim.limiter == 0 || lim.limiter == 2 ||
+                              (lim.limiter == 1 && (lim.test_flags & kFlagSwUnsorted))) &&
                      resolve && !no_hfast;
     if (!(split && split->tail) && (e = hipMemsetAsync(sc.marks, 0, n, st)) != hipSuccess) return e;
     DigitPlan dp{};

@@ -43,7 +43,10 @@ __global__ void k_hmode(BatchState *bs, const uint64_t *__restrict__ ts, uint32_
     bs->pay_ok = pay ? 1u : 0u;
     // (fixed window: walk_fixed_fast's preconditions; sliding window: its final logs fit their
     // staging, the clock facts across batches in k_hmode_state)
-    const bool lim_ok = lim.limiter == 1 ? P <= kSwHeavyMaxP : fast_ok(bs, lim) && !(maxL && P + 1 > B / maxL);
+    // (token bucket: its heavy maps assume a capacity of at least one token, C >= cost)
+    const bool lim_ok = lim.limiter == 2   ? lim.tb_cap >= 1000000000ull
+                        : lim.limiter == 1 ? P <= kSwHeavyMaxP
+                                           : fast_ok(bs, lim) && !(maxL && P + 1 > B / maxL);
     const bool fast = !bs->err && pay && !bs->nonmono && !bs->span_big && maxL < (1u << 16) && lim_ok;
     bs->hfast = fast ? 1u : 0u;
 }
@@ -79,7 +82,14 @@ __global__ __launch_bounds__(128) void k_hmode_state(const uint32_t *__restrict_
         const uint32_t maxL = bs->max_len;
         const uint64_t P = lim.pps, B = lim.bps, W = lim.window;
         bool ok = true;
-        if (lim.limiter == 1) {   // sliding window: sw_walk_fast_wave's facts; carried logs fit
+        if (lim.limiter == 2) {   // token bucket: no live blacklist entry (a user rule) on a heavy source
+            if (h < hs->n && hs->resolved && hs->slot[h] != kNoSlot) {
+                const Slot &sl = table[hs->slot[h]];
+                ok = !((sl.flags & SLOT_HAS_BL) && sl.till > 0);
+            } else if (h < hs->n) {
+                ok = false;
+            }
+        } else if (lim.limiter == 1) {   // sliding window: sw_walk_fast_wave's facts; carried logs fit
             ok = sw_fast(bs, tstate, lim);
             if (h < hs->n && hs->resolved && hs->slot[h] != kNoSlot) {
                 const uint64_t aux = table[hs->slot[h]].aux;

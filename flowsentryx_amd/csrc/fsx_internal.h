@@ -441,6 +441,8 @@ struct Scratch {
     uint32_t *chunk_cnt;
     void *hrec;
     void *hflow;           // tail: per (group of kHGroupTiles tiles, heavy source) flow sums
+    void *tbh;             // token bucket, heavy sources unsorted: per (sort tile, heavy source)
+                           // map + state (tb_heavy_bytes; null for the other limiters)
     // FSX_FLAG_OVERFLOW_ADMIT: per arrival index, 1 at a new source's first packet, then its
     // admission rank; per 4096 positions, their count / exclusive scan
     uint32_t *admit_rank;
@@ -604,9 +606,22 @@ struct Marker {
 };
 
 struct HeavyLists;
+// light_only 2: the heavy sources' packets are decided outside the sort when the batch takes
+// the unsorted path (launch_tb_heavy), so the scan covers the light entries only then
 hipError_t launch_token_bucket(const uint64_t *S, const uint64_t *ts, const uint32_t *len, BatchState *bs,
                                const Scratch &sc, Slot *table, const Limits &lim, uint32_t n,
-                               hipStream_t st, const Marker &mark);
+                               hipStream_t st, const Marker &mark, uint32_t light_only = 0);
+// token bucket, heavy sources outside the sort (fsx_limiters.hip): per-tile maps, a scan per
+// heavy source over its tiles, the replay writing its verdict bytes; the run path's heavy heads
+// and the untagging of its passed heavy packets
+size_t tb_heavy_bytes(uint64_t cap);
+hipError_t launch_tb_heavy(BatchState *bs, const uint32_t *cnt0, const uint32_t *base0, const uint32_t *offs,
+                           uint32_t tcap, uint8_t *verdict, const uint64_t *ts, uint32_t n, const void *rec,
+                           void *tbh, Slot *table, const Limits &lim, const HeavySet *hs, TableState *tstate,
+                           hipStream_t st);
+hipError_t launch_tb_run_heads(const BatchState *bs, const uint32_t *seg_start, uint8_t *headf, uint32_t *tile_off,
+                               uint32_t n, hipStream_t st);
+hipError_t launch_tb_untag(const BatchState *bs, uint8_t *verdict, uint32_t n, hipStream_t st);
 
 // st3 (optional, with fork/join events): the long-segment walker beside the short one.
 hipError_t launch_sliding_window(const uint64_t *S, const uint64_t *ts, const uint32_t *len, BatchState *bs,

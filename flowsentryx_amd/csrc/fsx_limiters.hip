@@ -88,8 +88,10 @@ __device__ __forceinline__ int64_t tb_refill(uint64_t dt, uint64_t rate, uint64_
 template <class SV>
 __device__ __forceinline__ void tb_seg_body(const SV &sv, BatchState *bs, const uint32_t *seg_start,
                                             const uint32_t *seg_slot, Slot *table, const Limits &lim,
-                                            uint32_t *seg_j, uint64_t *seg_x) {
-    const uint32_t nseg = bs->nseg;
+                                            uint32_t *seg_j, uint64_t *seg_x, uint32_t light_only) {
+    // (light_only 2 on the unsorted path: the heavy segments k_heads_heavy appended hold no
+    // sorted packets — launch_tb_heavy decides them)
+    const uint32_t nseg = light_only == 2 && bs->hfast ? bs->nseg_light : bs->nseg;
     const bool mono = !bs->nonmono;
     for (uint32_t g = blockIdx.x * 256u + threadIdx.x; g < nseg; g += gridDim.x * 256u) {
         const uint32_t a = seg_start[g], b = seg_start[g + 1];
@@ -131,10 +133,10 @@ __global__ __launch_bounds__(256) void k_tb_seg(const uint64_t *__restrict__ S, 
                                                 const uint32_t *__restrict__ len,
                                                 const uint64_t *__restrict__ pay, Slot *table,
                                                 Limits lim, uint32_t *__restrict__ seg_j,
-                                                uint64_t *__restrict__ seg_x) {
+                                                uint64_t *__restrict__ seg_x, uint32_t light_only) {
     if (bs->err) return;
-    if (bs->pay_ok) tb_seg_body(SegView<true>{S, ts, len, pay, ~bs->inv_min_ts}, bs, seg_start, seg_slot, table, lim, seg_j, seg_x);
-    else tb_seg_body(SegView<false>{S, ts, len, pay, 0}, bs, seg_start, seg_slot, table, lim, seg_j, seg_x);
+    if (bs->pay_ok) tb_seg_body(SegView<true>{S, ts, len, pay, ~bs->inv_min_ts}, bs, seg_start, seg_slot, table, lim, seg_j, seg_x, light_only);
+    else tb_seg_body(SegView<false>{S, ts, len, pay, 0}, bs, seg_start, seg_slot, table, lim, seg_j, seg_x, light_only);
 }
 
 // Position kinds inside a tile.
@@ -388,11 +390,11 @@ __global__ __launch_bounds__(256) void k_tb_tiles(const uint64_t *__restrict__ S
                                                   const uint64_t *__restrict__ seg_x,
                                                   const uint32_t *__restrict__ seg_slot, Slot *table,
                                                   Limits lim, CMap *tile_map, const int64_t *tile_x,
-                                                  uint8_t *__restrict__ marks) {
+                                                  uint8_t *__restrict__ marks, uint32_t light_only) {
     __shared__ CMap s_w[4];
     __shared__ uint32_t s_tmp[4];
     if (bs->err) return;
-    const uint32_t M = bs->n_valid;
+    const uint32_t M = cover_n(bs, light_only);
     const uint32_t ntiles = (M + kTile - 1) / kTile;
     const bool pay_ok = bs->pay_ok != 0;
     for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
@@ -420,13 +422,13 @@ __global__ __launch_bounds__(256, FSX_TB_SCAN_MINB) void k_tb_scan(const uint64_
                                                  const uint64_t *__restrict__ seg_x,
                                                  const uint32_t *__restrict__ seg_slot, Slot *table,
                                                  Limits lim, CMap *tile_map, unsigned long long *status,
-                                                 uint32_t *ticket, uint8_t *__restrict__ marks) {
+                                                 uint32_t *ticket, uint8_t *__restrict__ marks, uint32_t light_only) {
     __shared__ CMap s_w[4];
     __shared__ uint32_t s_tmp[4];
     __shared__ uint32_t s_t;
     __shared__ int64_t s_x;
     if (bs->err) return;
-    const uint32_t M = bs->n_valid;
+    const uint32_t M = cover_n(bs, light_only);
     const uint32_t ntiles = (M + kTile - 1) / kTile;
     if (threadIdx.x == 0) s_t = atomicAdd(ticket, 1u);
     __syncthreads();
@@ -443,10 +445,10 @@ __global__ __launch_bounds__(256, FSX_TB_SCAN_MINB) void k_tb_scan(const uint64_
 // One block: the state entering every tile (tile 0 starts with a source head, so its
 // entering state is irrelevant and taken as 0).
 __global__ __launch_bounds__(1024) void k_tb_carry(BatchState *bs, const CMap *__restrict__ tile_map,
-                                                   int64_t *__restrict__ tile_x, Limits lim) {
+                                                   int64_t *__restrict__ tile_x, Limits lim, uint32_t light_only) {
     __shared__ CMap s_w[16];
     if (bs->err) return;
-    const uint32_t M = bs->n_valid;
+    const uint32_t M = cover_n(bs, light_only);
     const uint32_t ntiles = (M + kTile - 1) / kTile;
     const int64_t hi = lim.tb_cap >= kTbCost ? (int64_t)(lim.tb_cap - kTbCost) : 0;
     const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
@@ -475,7 +477,7 @@ __global__ __launch_bounds__(1024) void k_tb_carry(BatchState *bs, const CMap *_
 
 hipError_t launch_token_bucket(const uint64_t *S, const uint64_t *ts, const uint32_t *len, BatchState *bs,
                                const Scratch &sc, Slot *table, const Limits &lim, uint32_t n,
-                               hipStream_t st, const Marker &mark) {
+                               hipStream_t st, const Marker &mark, uint32_t light_only) {
     (void)hipGetLastError();   // a stale error of another caller is not ours
     const uint32_t gridSeg = std::min<uint32_t>(2048, std::max<uint32_t>(1, (n + 255) / 256));
     const uint32_t gridTiles = std::min<uint32_t>(4096, std::max<uint32_t>(1, (n + kTile - 1) / kTile));
@@ -484,7 +486,7 @@ hipError_t launch_token_bucket(const uint64_t *S, const uint64_t *ts, const uint
     CMap *tile_map = reinterpret_cast<CMap *>(sc.lim_tiles);
     int64_t *tile_x = reinterpret_cast<int64_t *>(sc.lim_tiles + 3 * sc.lim_tiles_n);
     k_tb_seg<<<gridSeg, 256, 0, st>>>(S, bs, sc.seg_start, sc.seg_slot, ts, len, sc.pay[0], table, lim,
-                                      seg_j, seg_x);
+                                      seg_j, seg_x, light_only);
     mark("k_tb_seg");
     static const bool two_pass = getenv("FSX_TB_TWO_PASS") != nullptr;
     if (!two_pass) {
@@ -496,19 +498,525 @@ hipError_t launch_token_bucket(const uint64_t *S, const uint64_t *ts, const uint
         if (e != hipSuccess) return e;
         const uint32_t grid = std::max<uint32_t>(1, (n + kTile - 1) / kTile);   // (>= the valid tiles)
         k_tb_scan<<<grid, 256, 0, st>>>(S, bs, ts, len, sc.pay[0], sc.headf, sc.tile_aux, seg_j, seg_x,
-                                        sc.seg_slot, table, lim, tile_map, status, ticket, sc.marks);
+                                        sc.seg_slot, table, lim, tile_map, status, ticket, sc.marks, light_only);
         mark("k_tb_scan");
         return hipGetLastError();
     }
     k_tb_tiles<0><<<gridTiles, 256, 0, st>>>(S, bs, ts, len, sc.pay[0], sc.headf, sc.tile_aux, seg_j,
                                              seg_x, sc.seg_slot, table, lim, tile_map, tile_x,
-                                             sc.marks);
+                                             sc.marks, light_only);
     mark("k_tb_tiles_reduce");
-    k_tb_carry<<<1, 1024, 0, st>>>(bs, tile_map, tile_x, lim);
+    k_tb_carry<<<1, 1024, 0, st>>>(bs, tile_map, tile_x, lim, light_only);
     k_tb_tiles<1><<<gridTiles, 256, 0, st>>>(S, bs, ts, len, sc.pay[0], sc.headf, sc.tile_aux, seg_j,
                                              seg_x, sc.seg_slot, table, lim, tile_map, tile_x,
-                                             sc.marks);
+                                             sc.marks, light_only);
     mark("k_tb_tiles_apply");
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------ token bucket, heavy sources unsorted
+// (DESIGN.md §4.2 "Heavy sources outside the sort") As for the fixed
+// window, k_parse tags a heavy source's packets 0x80 | h and writes no sort word for them, so
+// the sort carries the light entries only. A heavy source's packets are decided in arrival
+// order by clamp-add maps (its refill between consecutive packets is a map, and maps compose):
+//   k_tb_heavy_tiles<0>  per sort tile: for every heavy source, the map of its packets of the
+//                        tile after the first one, composed in arrival order (lanes of one
+//                        64-packet row by pointer jumping over "the last lane below with the
+//                        same source", rows and the block's four 1024-packet chunks in order)
+//   k_tb_heavy_scan      one wave per heavy source: the tiles in order, 64 at a time — the
+//                        map of a tile's first packet from the previous tile's last timestamp
+//                        (HeavyTileRec t1), an ordered scan of the tile maps from the carried
+//                        {tokens, last} (a new source starts full) — the state after each
+//                        tile's first packet with its verdict, and the source's final state
+//   k_tb_heavy_tiles<1>  per sort tile again: the replay from those states, every heavy
+//                        packet's verdict byte written over its tag, PASS / DROP counted
+// A heavy source with a live blacklist entry (a user rule: the token bucket inserts none)
+// sends the batch to the run path (k_hmode_state), as do the clock facts k_hmode checks.
+constexpr unsigned long long kTbNone = ~0ull;
+
+__device__ __forceinline__ CMap cm_shfl(const CMap &m, uint32_t src) {
+    return CMap{__shfl(m.lo, (int)src), __shfl(m.hi, (int)src), __shfl(m.d, (int)src)};
+}
+
+// The inclusive composition, in lane order, of the maps of the lanes of one source up to this
+// lane (ptr: the last lane below with the same source, 64 for none): pointer jumping, one
+// round per doubling of the longest same-source chain in the row (at most six for 64 lanes;
+// every lane takes part in the shuffles). mc: the row's largest same-source lane count.
+__device__ __forceinline__ CMap tb_row_incl(CMap acc, uint32_t ptr, uint32_t mc) {
+    const uint32_t lane = lane_id();
+    const uint32_t rounds = mc > 1 ? 32u - (uint32_t)__clz((int)(mc - 1u)) : 0u;   // ceil(log2 mc)
+    for (uint32_t r = 0; r < rounds; ++r) {
+        const uint32_t src = ptr < 64u ? ptr : lane;
+        const CMap y = cm_shfl(acc, src);
+        const uint32_t yp = (uint32_t)__shfl((int)ptr, (int)src);
+        if (ptr < 64u) {
+            acc = cm_compose(acc, y);
+            ptr = yp;
+        }
+    }
+    return acc;
+}
+
+struct TbHeavyOut {
+    CMap *map;      // [tile][kHeavyMax]: h's packets of the tile after its first, composed
+    uint64_t *x1;   // [tile][kHeavyMax]: the state after the tile's first packet of h | PASS << 63
+};
+
+template <bool kApply>
+__global__ __launch_bounds__(256) void k_tb_heavy_tiles(BatchState *bs, uint8_t *__restrict__ verdict,
+                                                        const uint64_t *__restrict__ ts, uint32_t n,
+                                                        const HeavySet *__restrict__ hs, Limits lim, TbHeavyOut o,
+                                                        TableState *tstate) {
+    __shared__ CMap s_m[4][kHeavyMax];
+    __shared__ unsigned long long s_f[4][kHeavyMax], s_l[4][kHeavyMax];
+    __shared__ long long s_xa[4][kHeavyMax], s_xb[4][kHeavyMax];
+    __shared__ unsigned long long s_pv[4][kHeavyMax];
+    __shared__ uint32_t s_p1[kHeavyMax];
+    __shared__ unsigned long long s_cnt[2];
+    if (bs->err || !bs->hfast) return;
+    const uint32_t tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
+    const uint32_t ntiles = (n + kSortTile - 1) / kSortTile;
+    if (blockIdx.x >= ntiles) return;
+    const uint32_t t = xcd_swizzle(blockIdx.x, ntiles);
+    const uint32_t c0 = t * kSortTile + w * 1024u;
+    const uint64_t lt_mask = (1ull << lane) - 1ull;
+    const uint32_t nh = hs->n;
+    const int64_t H = (int64_t)(lim.tb_cap - kTbCost);   // (k_hmode: C >= cost on this path)
+    const uint64_t dt_sat = tb_dt_sat(lim.tb_rate);
+    auto delta = [&](uint64_t tp, uint64_t tprev) -> int64_t {
+        return tb_refill(tp - tprev, lim.tb_rate, dt_sat) - (int64_t)kTbCost;
+    };
+    const CMap id{0, H, 0};
+    for (uint32_t j = tid; j < 4 * kHeavyMax; j += 256) {
+        (&s_m[0][0])[j] = id;
+        (&s_f[0][0])[j] = kTbNone;
+        (&s_l[0][0])[j] = kTbNone;
+    }
+    if (tid < 2) s_cnt[tid] = 0;
+    __syncthreads();
+    uint64_t Tr[16];
+    uint32_t Gr[16];
+#pragma unroll
+    for (uint32_t r = 0; r < 16; ++r) {
+        const uint32_t i = c0 + r * 64u + lane;
+        const bool live = i < n;
+        const uint32_t g = live ? verdict[i] : 0u;
+        Gr[r] = g >= 0x80u && (g & 0x7Fu) < nh ? (g & 0x7Fu) : 0xFFu;
+        Tr[r] = ts[live ? i : 0u];
+    }
+    // 1. per wave and heavy source: the chunk's first / last timestamp and the maps of its
+    //    packets after the first, composed
+#pragma unroll
+    for (uint32_t r = 0; r < 16; ++r) {
+        const uint32_t g = Gr[r];
+        const bool hv = g != 0xFFu;
+        const uint64_t act = __ballot(hv);
+        if (!act) continue;
+        const uint64_t T = Tr[r];
+        const uint64_t peers = match_digit(g, act);
+        const uint64_t below = peers & lt_mask;
+        const uint32_t pl = below ? 63u - (uint32_t)__clzll((long long)below) : lane;
+        const uint64_t tpl = __shfl(T, (int)pl);
+        CMap m = id;
+        if (hv) {
+            uint64_t tp = tpl;
+            bool pred = below != 0;
+            if (!pred) {
+                tp = s_l[w][g];
+                pred = tp != kTbNone;
+                if (!pred) s_f[w][g] = T;
+            }
+            if (pred) m = CMap{0, H, delta(T, tp)};
+        }
+        const uint32_t mc = wave_max(hv ? (uint32_t)__popcll(peers) : 0u);
+        const CMap acc = tb_row_incl(m, hv && below ? pl : 64u, mc);
+        if (hv && (peers >> lane) == 1ull) {   // the row's last packet of h
+            s_m[w][g] = cm_compose(acc, s_m[w][g]);
+            s_l[w][g] = T;
+        }
+        wave_lds_order();
+    }
+    __syncthreads();
+    if constexpr (!kApply) {   // the tile's map after h's first packet (the chunks joined in order)
+        if (tid < nh) {
+            const uint32_t h = tid;
+            CMap M = id;
+            uint64_t last = kTbNone;
+#pragma unroll
+            for (uint32_t ww = 0; ww < 4; ++ww) {
+                const uint64_t f = s_f[ww][h];
+                if (f == kTbNone) continue;
+                M = last != kTbNone ? cm_compose(s_m[ww][h], cm_compose(CMap{0, H, delta(f, last)}, M)) : s_m[ww][h];
+                last = s_l[ww][h];
+            }
+            if (last != kTbNone) o.map[(size_t)t * kHeavyMax + h] = M;
+        }
+        return;
+    } else {
+        // 2. per heavy source: the state around each chunk's first packet, from the state
+        //    after the tile's first packet (k_tb_heavy_scan)
+        if (tid < nh) {
+            const uint32_t h = tid;
+            int64_t x = 0;
+            uint64_t last = kTbNone;
+#pragma unroll
+            for (uint32_t ww = 0; ww < 4; ++ww) {
+                const uint64_t f = s_f[ww][h];
+                if (f == kTbNone) continue;
+                if (last == kTbNone) {   // the tile's first packet of h
+                    const uint64_t x1 = o.x1[(size_t)t * kHeavyMax + h];
+                    s_p1[h] = (uint32_t)(x1 >> 63);
+                    x = (int64_t)(x1 & ~(1ull << 63));
+                    s_xa[ww][h] = x;
+                    s_pv[ww][h] = kTbNone;
+                } else {
+                    s_xb[ww][h] = x;
+                    s_pv[ww][h] = last;
+                    x = cm_apply(CMap{0, H, delta(f, last)}, x);
+                    s_xa[ww][h] = x;
+                }
+                x = cm_apply(s_m[ww][h], x);
+                last = s_l[ww][h];
+            }
+        }
+        __syncthreads();
+        for (uint32_t j = tid; j < 4 * kHeavyMax; j += 256) (&s_l[0][0])[j] = kTbNone;
+        __syncthreads();
+        // 3. the replay, row by row: s_xa[w][h] becomes the state after h's latest packet. The
+        //    rows are read again (L2-resident since step 1): kept in registers across steps 1-3
+        //    the fully unrolled replay took 357 VGPRs + 101 AGPRs (3.0 ms per 64M packets)
+        uint32_t np = 0, nd = 0;
+        // (the next row's tag and timestamp loaded one row ahead)
+        uint32_t gn = c0 + lane < n ? verdict[c0 + lane] : 0u;
+        uint64_t Tn = ts[c0 + lane < n ? c0 + lane : 0u];
+#pragma unroll 1
+        for (uint32_t r = 0; r < 16; ++r) {
+            const uint32_t i = c0 + r * 64u + lane;
+            const uint32_t g0 = gn;
+            const uint64_t T = Tn;
+            if (r + 1 < 16) {
+                const uint32_t i1 = i + 64u;
+                gn = i1 < n ? verdict[i1] : 0u;
+                Tn = ts[i1 < n ? i1 : 0u];
+            }
+            const uint32_t g = g0 >= 0x80u && (g0 & 0x7Fu) < nh ? (g0 & 0x7Fu) : 0xFFu;
+            const bool hv = g != 0xFFu;
+            const uint64_t act = __ballot(hv);
+            if (!act) continue;
+            const uint64_t peers = match_digit(g, act);
+            const uint64_t below = peers & lt_mask;
+            const uint32_t pl = below ? 63u - (uint32_t)__clzll((long long)below) : lane;
+            const uint64_t tpl = __shfl(T, (int)pl);
+            CMap m = id;
+            uint64_t tp = tpl;
+            bool seen = false;
+            if (hv) {
+                seen = s_l[w][g] != kTbNone;   // h had a packet in an earlier row of the chunk
+                if (!below) tp = s_l[w][g];
+                if (below || seen) m = CMap{0, H, delta(T, tp)};
+            }
+            const uint32_t mc = wave_max(hv ? (uint32_t)__popcll(peers) : 0u);
+            const CMap acc = tb_row_incl(m, hv && below ? pl : 64u, mc);
+            const CMap accp = cm_shfl(acc, pl);   // (the predecessor's inclusive map)
+            if (hv) {
+                const int64_t xin = s_xa[w][g];   // the state entering the row's first packet of h
+                uint8_t v;
+                if (below || seen) {
+                    const int64_t xb = below ? cm_apply(accp, xin) : xin;
+                    v = xb + m.d >= 0 ? XDP_PASS : XDP_DROP;
+                } else if (s_pv[w][g] == kTbNone) {   // the tile's first packet of h
+                    v = s_p1[g] ? XDP_PASS : XDP_DROP;
+                } else {                               // the chunk's first, after an earlier chunk's
+                    v = s_xb[w][g] + delta(T, s_pv[w][g]) >= 0 ? XDP_PASS : XDP_DROP;
+                }
+                verdict[i] = v;
+                np += v == XDP_PASS;
+                nd += v == XDP_DROP;
+            }
+            wave_lds_order();
+            if (hv && (peers >> lane) == 1ull) {
+                s_xa[w][g] = cm_apply(acc, s_xa[w][g]);
+                s_l[w][g] = T;
+            }
+            wave_lds_order();
+        }
+        np = wave_sum(np);
+        nd = wave_sum(nd);
+        if (lane == 0) {
+            if (np) atomicAdd(&s_cnt[0], (unsigned long long)np);
+            if (nd) atomicAdd(&s_cnt[1], (unsigned long long)nd);
+        }
+        __syncthreads();
+        if (tid == 0) {
+            unsigned long long *sp = reinterpret_cast<unsigned long long *>(tstate->stats);
+            if (s_cnt[0]) {
+                atomicAdd(sp, s_cnt[0]);
+                atomicAdd(reinterpret_cast<unsigned long long *>(&bs->allowed), s_cnt[0]);
+            }
+            if (s_cnt[1]) {
+                atomicAdd(sp + 1, s_cnt[1]);
+                atomicAdd(reinterpret_cast<unsigned long long *>(&bs->dropped), s_cnt[1]);
+            }
+        }
+    }
+}
+
+// The scan over a heavy source's tiles, in groups of kTbGroup tiles so that 128 sources fill
+// the device (one wave per source took 0.8-1.1 ms per 64M packets: 256 dependent steps of 64
+// tiles): k_tb_heavy_gmap composes each group's tiles into one map, k_tb_heavy_scan applies
+// the groups before its own to the carried state and replays the group's tiles. A tile's count
+// comes from pass 0's prefix row, its first / last timestamp from the tile records, its map
+// after the first packet from k_tb_heavy_tiles<0>; a group's first tile takes its previous
+// timestamp from the tile of the source's packet before the group (a search of the prefix row).
+constexpr uint32_t kTbGroup = 1024;   // tiles per group: 16 steps of 64
+
+struct TbHeavyCtx {
+    const uint32_t *row;    // pass-0 prefix row of bucket light_b + h (h's packets before tile t, + base)
+    uint32_t base, end, ntiles, h;
+    const HeavyTileRec *rec;
+    TbHeavyOut o;
+    int64_t H;
+    uint64_t rate, dt_sat;
+};
+
+// h's last timestamp before tile t0 (its carried one when it has no packet before t0)
+__device__ __forceinline__ uint64_t tb_prev_ts(const TbHeavyCtx &C, uint32_t t0, uint64_t carried_last) {
+    const uint32_t before = C.row[t0] - C.base;
+    if (before == 0) return carried_last;
+    const uint32_t r = before - 1, lane = lane_id();
+    uint32_t lo = 0, hi = t0;   // the largest tile t < t0 with pre(t) <= r (fsx_search.h)
+    while (hi - lo > 1) {
+        const uint32_t step = ary64_width(lo, hi);
+        const uint32_t q = lo + lane * step;
+        const uint64_t m = __ballot(q < hi && C.row[q] - C.base <= r);
+        ary64_step(lo, hi, step, m);
+    }
+    return C.rec[lo].t1[C.h];
+}
+
+// Tiles [t0, t1) of h from the state x (previous timestamp `last`): kWrite stores every present
+// tile's state after its first packet with that packet's verdict; returns the composed map of
+// the range (and leaves `last` at the range's last timestamp).
+template <bool kWrite>
+__device__ CMap tb_heavy_range(const TbHeavyCtx &C, uint32_t t0, uint32_t t1, int64_t x, uint64_t &last) {
+    const uint32_t lane = lane_id();
+    const CMap id{0, C.H, 0};
+    CMap acc = id;
+    const uint64_t lt = (1ull << lane) - 1ull;
+    for (uint32_t tb = t0; tb < t1; tb += 64) {
+        const uint32_t t = tb + lane;
+        uint32_t cnt = 0;
+        if (t < t1) cnt = (t + 1 < C.ntiles ? C.row[t + 1] : C.end) - C.row[t];
+        const bool present = cnt != 0;
+        const uint64_t pm = __ballot(present);
+        if (!pm) continue;
+        uint64_t f = 0, l = 0;
+        CMap M = id;
+        if (present) {
+            f = C.rec[t].t0[C.h];
+            l = C.rec[t].t1[C.h];
+            M = C.o.map[(size_t)t * kHeavyMax + C.h];
+        }
+        const uint64_t below = pm & lt;
+        const uint32_t pl = below ? 63u - (uint32_t)__clzll((long long)below) : lane;
+        const uint64_t lpl = __shfl(l, (int)pl);
+        const uint64_t prev = below ? lpl : last;
+        // the tile's first packet: a refill from the source's previous packet, or (a new
+        // source) a full bucket
+        const CMap F = prev != kTbNone ? CMap{0, C.H, tb_refill(f - prev, C.rate, C.dt_sat) - (int64_t)kTbCost}
+                                       : CMap{C.H, C.H, 0};
+        const CMap T = present ? cm_compose(M, F) : id;
+        CMap incl = T;
+#pragma unroll
+        for (int k = 1; k < 64; k <<= 1) {
+            const CMap y = cm_shfl_up(incl, k);
+            if (lane >= (uint32_t)k) incl = cm_compose(incl, y);
+        }
+        if constexpr (kWrite) {
+            CMap excl = cm_shfl_up(incl, 1);
+            if (lane == 0) excl = id;
+            const int64_t xin = cm_apply(cm_compose(excl, acc), x);
+            if (present) {
+                const bool pass = prev == kTbNone || xin + F.d >= 0;
+                const int64_t x1 = cm_apply(F, xin);
+                C.o.x1[(size_t)t * kHeavyMax + C.h] = (uint64_t)x1 | (pass ? (1ull << 63) : 0ull);
+            }
+        }
+        acc = cm_compose(cm_shfl(incl, 63), acc);
+        last = __shfl(l, 63 - __clzll((long long)pm));
+    }
+    return acc;
+}
+
+__device__ __forceinline__ bool tb_heavy_ctx(const BatchState *bs, const uint32_t *cnt0, const uint32_t *base0,
+                                             const uint32_t *offs, uint32_t tcap, uint32_t n,
+                                             const HeavyTileRec *rec, const TbHeavyOut &o, const Limits &lim,
+                                             const HeavySet *hs, uint32_t h, TbHeavyCtx &C) {
+    if (h >= hs->n) return false;
+    const uint32_t lb = bs->light_b;
+    const uint32_t c = cnt0[lb + h];
+    if (c == 0) return false;
+    C.row = offs + (size_t)(lb + h) * tcap;
+    C.base = base0[lb + h];
+    C.end = C.base + c;
+    C.ntiles = (n + kSortTile - 1) / kSortTile;
+    C.h = h;
+    C.rec = rec;
+    C.o = o;
+    C.H = (int64_t)(lim.tb_cap - kTbCost);
+    C.rate = lim.tb_rate;
+    C.dt_sat = tb_dt_sat(lim.tb_rate);
+    return true;
+}
+
+// the carried {tokens, last} of h's slot (a stored token count above the capacity — a map
+// update may write one — clamps as the first packet's min(C, ...) does: 2^62 is past every
+// state the maps reach)
+__device__ __forceinline__ void tb_carried(const Slot &sl, int64_t &x, uint64_t &last) {
+    const bool carried = ((sl.flags & kFlagBits) & SLOT_HAS_TB) != 0;
+    x = carried ? (int64_t)(sl.aux < (1ull << 62) ? sl.aux : (1ull << 62)) : 0;
+    last = carried ? sl.tt : kTbNone;
+}
+
+struct TbCarried {
+    int64_t x;        // tokens after the previous batch (clamped, tb_carried)
+    uint64_t last;    // its last packet's timestamp (kTbNone: a new source)
+    uint32_t flags, pad_[3];
+};
+
+// one wave per (heavy source, group): the group's composed map -> gmap[h][g]; group 0's wave
+// also copies the carried state (k_tb_heavy_scan's last group rewrites the slot)
+__global__ __launch_bounds__(256) void k_tb_heavy_gmap(const BatchState *bs, const uint32_t *__restrict__ cnt0,
+                                                       const uint32_t *__restrict__ base0,
+                                                       const uint32_t *__restrict__ offs, uint32_t tcap, uint32_t n,
+                                                       const HeavyTileRec *__restrict__ rec, TbHeavyOut o,
+                                                       const Slot *table, Limits lim, const HeavySet *__restrict__ hs,
+                                                       CMap *gmap, TbCarried *carried, uint32_t ngroups) {
+    if (bs->err || !bs->hfast) return;
+    const uint32_t wv = blockIdx.x * 4u + (threadIdx.x >> 6);
+    const uint32_t h = wv / ngroups, g = wv % ngroups;
+    TbHeavyCtx C;
+    if (!tb_heavy_ctx(bs, cnt0, base0, offs, tcap, n, rec, o, lim, hs, h, C)) return;
+    const uint32_t t0 = g * kTbGroup, t1 = min(C.ntiles, t0 + kTbGroup);
+    if (t0 >= t1) return;
+    const Slot &sl = table[hs->slot[h]];
+    int64_t x;
+    uint64_t last;
+    tb_carried(sl, x, last);
+    if (g == 0 && lane_id() == 0) carried[h] = TbCarried{x, last, sl.flags & kFlagBits, {0, 0, 0}};
+    last = tb_prev_ts(C, t0, last);
+    const CMap M = tb_heavy_range<false>(C, t0, t1, 0, last);
+    if (lane_id() == 0) gmap[(size_t)h * ngroups + g] = M;
+}
+
+// one wave per (heavy source, group): the state entering the group (the groups before it
+// applied to the carried state), the replay of its tiles; the last group stores the source's
+// state after the batch
+__global__ __launch_bounds__(256) void k_tb_heavy_scan(const BatchState *bs, const uint32_t *__restrict__ cnt0,
+                                                       const uint32_t *__restrict__ base0,
+                                                       const uint32_t *__restrict__ offs, uint32_t tcap, uint32_t n,
+                                                       const HeavyTileRec *__restrict__ rec, TbHeavyOut o,
+                                                       Slot *table, Limits lim, const HeavySet *__restrict__ hs,
+                                                       const CMap *gmap, const TbCarried *carried, uint32_t ngroups) {
+    if (bs->err || !bs->hfast) return;
+    const uint32_t wv = blockIdx.x * 4u + (threadIdx.x >> 6);
+    const uint32_t h = wv / ngroups, g = wv % ngroups;
+    TbHeavyCtx C;
+    if (!tb_heavy_ctx(bs, cnt0, base0, offs, tcap, n, rec, o, lim, hs, h, C)) return;
+    const uint32_t t0 = g * kTbGroup, t1 = min(C.ntiles, t0 + kTbGroup);
+    if (t0 >= t1) return;
+    const TbCarried cs = carried[h];
+    int64_t x = cs.x;
+    for (uint32_t k = 0; k < g; ++k) x = cm_apply(gmap[(size_t)h * ngroups + k], x);
+    uint64_t last = tb_prev_ts(C, t0, cs.last);
+    const CMap M = tb_heavy_range<true>(C, t0, t1, x, last);
+    if (t1 == C.ntiles && lane_id() == 0) {
+        Slot &sl = table[hs->slot[h]];
+        sl.aux = (uint64_t)cm_apply(M, x);
+        sl.tt = last;
+        sl.flags = cs.flags | SLOT_HAS_TB;   // (drops the born stamp, as k_tb_seg)
+    }
+}
+
+static uint32_t tb_groups(uint64_t tiles) { return (uint32_t)std::max<uint64_t>(1, (tiles + kTbGroup - 1) / kTbGroup); }
+
+hipError_t launch_tb_heavy(BatchState *bs, const uint32_t *cnt0, const uint32_t *base0, const uint32_t *offs,
+                           uint32_t tcap, uint8_t *verdict, const uint64_t *ts, uint32_t n, const void *rec,
+                           void *tbh, Slot *table, const Limits &lim, const HeavySet *hs, TableState *tstate,
+                           hipStream_t st) {
+    const uint32_t ntiles = std::max<uint32_t>(1, (n + kSortTile - 1) / kSortTile);
+    const uint64_t tiles_cap = tcap;   // (tcap >= ntiles: the rows' pitch)
+    CMap *maps = static_cast<CMap *>(tbh);
+    uint64_t *x1 = reinterpret_cast<uint64_t *>(maps + tiles_cap * kHeavyMax);
+    CMap *gmap = reinterpret_cast<CMap *>(x1 + tiles_cap * kHeavyMax);
+    TbCarried *carried = reinterpret_cast<TbCarried *>(gmap + (size_t)kHeavyMax * tb_groups(tiles_cap));
+    const TbHeavyOut o{maps, x1};
+    const uint32_t ng = tb_groups(ntiles);
+    const HeavyTileRec *R = static_cast<const HeavyTileRec *>(rec);
+    const uint32_t gw = (kHeavyMax * ng + 3) / 4;   // (4 waves per block)
+    k_tb_heavy_tiles<false><<<ntiles, 256, 0, st>>>(bs, verdict, ts, n, hs, lim, o, tstate);
+    k_tb_heavy_gmap<<<gw, 256, 0, st>>>(bs, cnt0, base0, offs, tcap, n, R, o, table, lim, hs, gmap, carried, ng);
+    k_tb_heavy_scan<<<gw, 256, 0, st>>>(bs, cnt0, base0, offs, tcap, n, R, o, table, lim, hs, gmap, carried, ng);
+    k_tb_heavy_tiles<true><<<ntiles, 256, 0, st>>>(bs, verdict, ts, n, hs, lim, o, tstate);
+    return hipGetLastError();
+}
+
+size_t tb_heavy_bytes(uint64_t cap) {
+    const uint64_t tiles = cap / kSortTile + 2;
+    return (size_t)tiles * kHeavyMax * (sizeof(CMap) + 8) + (size_t)kHeavyMax * tb_groups(tiles) * sizeof(CMap) +
+           kHeavyMax * sizeof(TbCarried);
+}
+
+// The run path of a token-bucket batch with tagged heavy packets (k_hmode_state refused the
+// unsorted path): k_heavy_gather built the heavy runs at [n_light, n_valid), whose heads
+// (k_heads_heavy's segments) the light heads kernels did not flag; after the fill stored the
+// DROPs, a heavy packet still tagged passed.
+__global__ __launch_bounds__(256) void k_tb_run_heads(const BatchState *bs, const uint32_t *__restrict__ seg_start,
+                                                      uint8_t *__restrict__ headf, uint32_t *__restrict__ tile_off) {
+    __shared__ uint32_t s_st[kHeavyMax];
+    if (bs->err || bs->hfast) return;
+    const uint32_t L = bs->nseg_light, nhs = bs->nseg - L;
+    for (uint32_t k = threadIdx.x; k < nhs && k < kHeavyMax; k += 256) s_st[k] = seg_start[L + k];
+    __syncthreads();
+    const uint32_t a = bs->n_light, b = bs->n_valid;
+    for (uint32_t p = a + blockIdx.x * 256u + threadIdx.x; p < b; p += gridDim.x * 256u) {
+        uint32_t lo = 0, hi = nhs;   // (the run starts are increasing)
+        while (lo < hi) {
+            const uint32_t md = (lo + hi) >> 1;
+            if (s_st[md] < p) lo = md + 1; else hi = md;
+        }
+        headf[p] = lo < nhs && s_st[lo] == p ? 1u : 0u;
+    }
+    // the scan's per-tile segment offsets past the light tiles (heads before the tile's first
+    // position: every light segment and the heavy runs that start before it)
+    const uint32_t t0 = (a + kTile - 1) / kTile, t1 = (b + kTile - 1) / kTile;
+    for (uint32_t t = t0 + blockIdx.x * 256u + threadIdx.x; t < t1; t += gridDim.x * 256u) {
+        const uint32_t p = t * kTile;
+        uint32_t lo = 0, hi = nhs;   // heavy runs starting before p
+        while (lo < hi) {
+            const uint32_t md = (lo + hi) >> 1;
+            if (s_st[md] < p) lo = md + 1; else hi = md;
+        }
+        tile_off[t] = L + lo;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_tb_untag(const BatchState *bs, uint8_t *__restrict__ verdict, uint32_t n) {
+    if (bs->err || bs->hfast) return;
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u)
+        if (verdict[i] >= 0x80u) verdict[i] = XDP_PASS;
+}
+
+hipError_t launch_tb_run_heads(const BatchState *bs, const uint32_t *seg_start, uint8_t *headf, uint32_t *tile_off,
+                               uint32_t n, hipStream_t st) {
+    const uint32_t grid = std::min<uint32_t>(2048, std::max<uint32_t>(1, (n + 255) / 256));
+    k_tb_run_heads<<<grid, 256, 0, st>>>(bs, seg_start, headf, tile_off);
+    return hipGetLastError();
+}
+
+hipError_t launch_tb_untag(const BatchState *bs, uint8_t *verdict, uint32_t n, hipStream_t st) {
+    const uint32_t grid = std::min<uint32_t>(2048, std::max<uint32_t>(1, (n + 255) / 256));
+    k_tb_untag<<<grid, 256, 0, st>>>(bs, verdict, n);
     return hipGetLastError();
 }
 

@@ -15,7 +15,8 @@ from kat import GOLDEN
 pytestmark = pytest.mark.gpu
 
 
-def _run(native, oracle, batches, cfg, prepare=None, want_path=None, pipeline=False, cap=None):
+def _run(native, oracle, batches, cfg, prepare=None, want_path=None, pipeline=False, cap=None,
+         maps=(1, 2, 3, 4)):
     """Each batch through fsx_process_batch_device on one context (maps carried); after each
     one: verdicts, flow rows and (at the end) stats + maps against the oracle. Returns the
     heavy_unsorted flag of every batch."""
@@ -66,7 +67,7 @@ def _run(native, oracle, batches, cfg, prepare=None, want_path=None, pipeline=Fa
             po, _, _ = oracle.score(ref, xo[oo])
             assert np.array_equal(pg[og].view(np.uint32), po.view(np.uint32))
         assert c.stats() == o.stats()
-        for mid in (1, 2, 3, 4):
+        for mid in maps:
             g, r = c.map_arrays(mid), o.map_arrays(mid)
             assert g[0].shape[0] == r[0].shape[0], mid
             assert pyoracle.same_map(g, r), mid
@@ -285,3 +286,52 @@ def test_unsorted_heavy_path_record_mode(native, oracle):
         assert c.stats() == o.stats()
         for mid in (1, 2, 3, 4):
             assert pyoracle.same_map(c.map_arrays(mid), o.map_arrays(mid)), mid
+
+
+TB = dict(CFG, limiter=2)   # token bucket, default rate / burst (1000 tokens/s, burst 1000)
+
+
+@pytest.mark.parametrize("case", ["slices", "pipelined", "mixed_rate", "blacklisted", "non_monotone", "sorted"])
+def test_token_bucket_unsorted_heavy(native, oracle, case, monkeypatch):
+    """Token bucket with the heavy sources outside the sort (round 6, opt-in
+    FSX_TB_UNSORTED=1: measured slower than the heavy-source sort): their packets' verdicts
+    come from per-tile clamp-add maps, a scan over the tiles per source and a replay in arrival
+    order (launch_tb_heavy); the sort carries the light entries only. Config-2 slices carried
+    over the cuts — the heavy sources rate-limited — verdicts, flow rows, stats and the
+    blacklist + token maps bit-exact against the oracle, heavy_unsorted every batch (the first
+    from empty maps: every heavy source new, starting full). A heavy source with a live
+    blacklist entry, or a clock step back, sends the batch to the run path (heavy runs gathered
+    into the sort's buffer, DROPs stored, the passed ones untagged); "sorted": the default."""
+    n = 1 << 21 if case in ("slices", "pipelined") else 1 << 20
+    hdr, ln, ts = _config2(oracle, n)
+    cfg, prepare, fast = dict(TB), None, 1
+    if case == "mixed_rate":
+        cfg.update(tb_rate=300_000, tb_burst=4)
+    elif case == "non_monotone":
+        ts = ts.copy()
+        ts[500_000], ts[500_001] = ts[500_001], ts[500_000] - 7
+        fast = 0
+    elif case == "blacklisted":
+        src, cnt = np.unique(hdr[:, 26:30].copy().view(np.uint32).reshape(-1), return_counts=True)
+        order = np.argsort(-cnt)
+        a, b = (int(src[order[i]]).to_bytes(4, "little") for i in (0, 3))
+        mid = int(ts[len(ts) // 4])
+
+        def prepare(c, o):
+            for k, v in ((a, mid), (b, 2**64 - 1)):
+                c.map_update(3, k, v)
+                o.map_update(3, k, v)
+        fast = 0
+    k = 3 if case == "pipelined" else 2
+    cuts = [i * n // k for i in range(k + 1)]
+    want = [fast] * k
+    if case == "non_monotone":
+        want = [0, 1]   # (the step back is in the first slice; the token bucket's maps need no
+                        # monotone clock across batches — the flow sums refuse only that batch)
+    if case == "sorted":
+        monkeypatch.delenv("FSX_TB_UNSORTED", raising=False)
+        want = None
+    else:
+        monkeypatch.setenv("FSX_TB_UNSORTED", "1")
+    _run(native, oracle, [(hdr[x:y], ln[x:y], ts[x:y]) for x, y in zip(cuts[:-1], cuts[1:])], cfg,
+         prepare=prepare, want_path=want, pipeline=case == "pipelined", maps=(3, 4, 5, 6))

@@ -54,8 +54,21 @@ TB_CFGS = {
 }
 
 
+@pytest.fixture(params=["sorted", "unsorted_heavy"])
+def tb_path(request, monkeypatch):
+    """Both token-bucket paths: every packet through the heavy-source sort (the default), and
+    the heavy sources outside the sort (FSX_TB_UNSORTED=1; small batches pick up
+    to 128 heavy sources too, and the run-path refusals — capacity below one token, a clock step
+    back, blacklisted heavy sources — take the run path with tagged heavy packets)."""
+    if request.param == "unsorted_heavy":
+        monkeypatch.setenv("FSX_TB_UNSORTED", "1")
+    else:
+        monkeypatch.delenv("FSX_TB_UNSORTED", raising=False)
+    return request.param
+
+
 @pytest.mark.parametrize("name", list(TB_CFGS))
-def test_token_bucket_random(native, oracle, name):
+def test_token_bucket_random(native, oracle, name, tb_path):
     rng = np.random.default_rng(zlib.crc32(b"tb" + name.encode()))
     hdr, ln, ts = rand_stream(rng, 60000, 300, dt_max=400)
     st = run_limiter(native, oracle, [(hdr, ln, ts)], dict(limiter=TB, **TB_CFGS[name]), TB_MAPS)
@@ -65,14 +78,14 @@ def test_token_bucket_random(native, oracle, name):
         assert st[0] > 1000 and st[1] > 1000
 
 
-def test_token_bucket_mixed_families(native, oracle):
+def test_token_bucket_mixed_families(native, oracle, tb_path):
     rng = np.random.default_rng(21)
     hdr, ln, ts = rand_stream(rng, 40000, 600, dt_max=300, v6_frac=0.4, nonip_frac=0.05,
                               short_frac=0.03)
     run_limiter(native, oracle, [(hdr, ln, ts)], dict(limiter=TB, **TB_CFGS["mixed"]), TB_MAPS)
 
 
-def test_token_bucket_state_carry(native, oracle):
+def test_token_bucket_state_carry(native, oracle, tb_path):
     rng = np.random.default_rng(22)
     hdr, ln, ts = rand_stream(rng, 30000, 200, dt_max=300, v6_frac=0.2)
     cuts = [0, 1, 2, 777, 4096, 4097, 17000, 29999, 30000]
@@ -80,7 +93,7 @@ def test_token_bucket_state_carry(native, oracle):
     run_limiter(native, oracle, batches, dict(limiter=TB, **TB_CFGS["mixed"]), TB_MAPS)
 
 
-def test_token_bucket_heavy_source(native, oracle):
+def test_token_bucket_heavy_source(native, oracle, tb_path):
     """One source with most packets of a 300k-packet batch: a segment spanning ~60 scan
     tiles, alternating verdicts inside one tile."""
     rng = np.random.default_rng(23)
@@ -89,7 +102,7 @@ def test_token_bucket_heavy_source(native, oracle):
                 TB_MAPS)
 
 
-def test_token_bucket_non_monotone_clock(native, oracle):
+def test_token_bucket_non_monotone_clock(native, oracle, tb_path):
     rng = np.random.default_rng(24)
     hdr, ln, ts = rand_stream(rng, 20000, 100, dt_max=200)
     sw = rng.choice(len(ts), 3000, replace=False)
@@ -98,7 +111,7 @@ def test_token_bucket_non_monotone_clock(native, oracle):
     run_limiter(native, oracle, [(hdr, ln, ts)], dict(limiter=TB, **TB_CFGS["mixed"]), TB_MAPS)
 
 
-def test_token_bucket_with_rules_and_state_updates(native, oracle):
+def test_token_bucket_with_rules_and_state_updates(native, oracle, tb_path):
     """Static and expiring blacklist rules apply before the bucket (src/fsx_kern.c:159-216
     semantics); user-written bucket states are honoured."""
     rng = np.random.default_rng(25)
