@@ -628,8 +628,7 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
     // of the sort tile, or earlier when the LDS list fills.
     // the parsed step awaiting resolution: tag, key word 0, probe start, heavy index, the
     // two probe reads
-    uint32_t c_tag = 0, c_k0 = 0, c_h = 0;
-    int c_hidx = -1;
+    // (one step's worth of these awaits its resolution: ProbeSet)
     // kHr: the wave's chunk's first timestamp and the last one so far (wave-uniform): the clock
     // check of a step's first record against the step before it, the tile's span and the
     // check across its chunks at the tile's end (across tiles: k_pass0h<false>)
@@ -646,11 +645,15 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
             }
         }
     }
-    uint64_t c_hint0 = 0, c_hint1 = 0;
     // kMir: the two mirror entries as the halves of one register (two 16-bit loads that
     // stay in flight until the resolve)
     typedef unsigned short mir2_t __attribute__((ext_vector_type(2)));
-    mir2_t c_m = {0, 0};
+    struct ProbeSet {
+        uint32_t tag = 0, k0 = 0, h = 0;
+        int hidx = -1;
+        uint64_t hint0 = 0, hint1 = 0;
+        mir2_t m = {0, 0};
+    };
     constexpr uint32_t kDefCap = FSX_PARSE_DEFCAP;   // deferred packets per wave (LDS)
     uint32_t crun = 0;                  // kHf: light words of the wave's current chunk so far
     uint32_t *dq = s_def[w];
@@ -711,7 +714,7 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
     };
     // parse one step (its records in hv / Lc / Tc / Pc): verdict bytes, clock facts, and
     // the probes of its IP packets into the c_* registers
-    auto parse_step = [&](uint32_t t, const uint4 (&hv)[kHv], uint32_t Lc, uint64_t Tc, uint64_t Pc) {
+    auto parse_step = [&](ProbeSet &c, uint32_t t, const uint4 (&hv)[kHv], uint32_t Lc, uint64_t Tc, uint64_t Pc) {
         const uint32_t base = t << 6;
         const uint32_t i = base + lane;
         const bool live = t < ntiles && i < n;
@@ -797,12 +800,12 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
         // the fast path reads the first two slots of an IPv4 source's probe chain (IPv6
         // sources are always resolved by the full protocol, which reads their key words
         // only after the head shows READY)
-        c_hint0 = c_hint1 = 0;
-        if constexpr (kMir) c_m = mir2_t{0, 0};
+        c.hint0 = c.hint1 = 0;
+        if constexpr (kMir) c.m = mir2_t{0, 0};
         if constexpr (kOrd) {   // (no probe: the key hash, resolve_step writes the word)
-            c_tag = live ? tag : 0u;
-            c_h = ip ? ord_hkey(tag, k, h, idt.seed, ord_s) : 0u;
-            c_hidx = -1;
+            c.tag = live ? tag : 0u;
+            c.h = ip ? ord_hkey(tag, k, h, idt.seed, ord_s) : 0u;
+            c.hidx = -1;
         }
 #ifdef FSX_MEASURE_NO_PROBE
         if (false) {
@@ -814,21 +817,21 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
             const uint64_t h1 = (h + 1) & idt.mask;
             if constexpr (kMir) {   // the 2-byte mirror entries of the two slots (exact: mir_entry)
                 const unsigned short *mp = static_cast<const unsigned short *>(idt.mir);
-                c_m.x = mp[h];
-                c_m.y = mp[h1];
+                c.m.x = mp[h];
+                c.m.y = mp[h1];
             } else if (idt.coherent) {
-                c_hint0 = __hip_atomic_load(idt.head + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                c_hint1 = __hip_atomic_load(idt.head + h1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                c.hint0 = __hip_atomic_load(idt.head + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                c.hint1 = __hip_atomic_load(idt.head + h1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             } else {
-                c_hint0 = idt.head[h];
-                c_hint1 = idt.head[h1];
+                c.hint0 = idt.head[h];
+                c.hint1 = idt.head[h1];
             }
         }
         if constexpr (!kOrd) {
-            c_tag = live ? tag : 0u;
-            c_k0 = k[0];
-            c_h = (uint32_t)h;
-            c_hidx = hidx;
+            c.tag = live ? tag : 0u;
+            c.k0 = k[0];
+            c.h = (uint32_t)h;
+            c.hidx = hidx;
         }
         if constexpr (kHr) {
             {   // the light packets' positions in the chunk (arrival order) and payload words
@@ -860,11 +863,11 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
         }
     };
     // resolve step t ("cur"): heavy slot from LDS, the fast-path probe match, or defer
-    auto resolve_step = [&](uint32_t t) {
+    auto resolve_step = [&](ProbeSet &c, uint32_t t) {
         const uint32_t i = (t << 6) + lane;
         if constexpr (kOrd) {
-            if (c_tag) {
-                const uint64_t out = ((uint64_t)c_h << kIdShift) | i | (c_tag == 2 ? kFreshBit : 0ull);
+            if (c.tag) {
+                const uint64_t out = ((uint64_t)c.h << kIdShift) | i | (c.tag == 2 ? kFreshBit : 0ull);
                 packed[i] = out;
                 count_digits(out, -1);
             }
@@ -872,23 +875,23 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
         }
         uint32_t id = kNoSlot;
         bool defer = false;
-        if (c_tag) {
-            if (hres && c_hidx >= 0) {
-                id = s_hslot[c_hidx];
-            } else if (c_tag == 1) {
+        if (c.tag) {
+            if (hres && c.hidx >= 0) {
+                id = s_hslot[c.hidx];
+            } else if (c.tag == 1) {
                 // the slot's head READY with this key, or its mirror entry (d = 0 / 1)
-                const uint64_t want0 = kMir ? mir_entry(c_k0, idt.seed, idt.mir_shift, 0u)
-                                            : id_head(idt.gen, kIdReady, 1u, c_k0);
+                const uint64_t want0 = kMir ? mir_entry(c.k0, idt.seed, idt.mir_shift, 0u)
+                                            : id_head(idt.gen, kIdReady, 1u, c.k0);
                 const uint64_t want1 = kMir ? want0 | 1u << 14 : want0;
 #ifdef FSX_MEASURE_NO_PROBE
-                id = c_h;
-                c_hint0 = want0;
-                c_m.x = (unsigned short)want0;
+                id = c.h;
+                c.hint0 = want0;
+                c.m.x = (unsigned short)want0;
 #endif
-                const uint64_t got0 = kMir ? (uint64_t)c_m.x : c_hint0;
-                const uint64_t got1 = kMir ? (uint64_t)c_m.y : c_hint1;
-                if (got0 == want0) id = c_h;
-                else if (got1 == want1) id = (uint32_t)((c_h + 1) & idt.mask);
+                const uint64_t got0 = kMir ? (uint64_t)c.m.x : c.hint0;
+                const uint64_t got1 = kMir ? (uint64_t)c.m.y : c.hint1;
+                if (got0 == want0) id = c.h;
+                else if (got1 == want1) id = (uint32_t)((c.h + 1) & idt.mask);
                 else defer = true;
             } else {
                 defer = true;
@@ -897,10 +900,10 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
         // kHf: the light packets' positions in the chunk, in arrival order (deferred or not)
         uint32_t lpos = 0;
         if constexpr (kHr) {   // (parse_step counted this step's light packets into crun)
-            const uint64_t lm = __ballot(c_tag != 0 && c_hidx < 0);
+            const uint64_t lm = __ballot(c.tag != 0 && c.hidx < 0);
             lpos = ((t >> 4) << 10) + crun - (uint32_t)__popcll(lm) + (uint32_t)__popcll(lm & lt_mask);
         } else if constexpr (kHf) {
-            const uint64_t lm = __ballot(c_tag != 0 && c_hidx < 0);
+            const uint64_t lm = __ballot(c.tag != 0 && c.hidx < 0);
             if (lane == 0 && t < ntiles) lmask[t] = lm;
             lpos = ((t >> 4) << 10) + crun + (uint32_t)__popcll(lm & lt_mask);
             crun += (uint32_t)__popcll(lm);
@@ -910,20 +913,20 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
             if (ndef + 64 > kDefCap) flush();
             if (defer) {
                 uint32_t *q = dq + (ndef + (uint32_t)__popcll(dm & lt_mask)) * kDefW;
-                q[0] = i; q[1] = c_tag | (uint32_t)(c_hidx + 1) << 8; q[2] = c_k0;
-                if constexpr (kDefW >= 5) { q[3] = (uint32_t)c_hint0; q[4] = (uint32_t)(c_hint0 >> 32); }
+                q[0] = i; q[1] = c.tag | (uint32_t)(c.hidx + 1) << 8; q[2] = c.k0;
+                if constexpr (kDefW >= 5) { q[3] = (uint32_t)c.hint0; q[4] = (uint32_t)(c.hint0 >> 32); }
                 if constexpr (kHf) q[kDefPos] = lpos;
             }
             ndef += (uint32_t)__popcll(dm);
         }
-        if (c_tag && !defer) {
-            const uint64_t out = word_of(id, c_tag, i, c_hidx);
+        if (c.tag && !defer) {
+            const uint64_t out = word_of(id, c.tag, i, c.hidx);
             if constexpr (kHf) {
-                if (c_hidx < 0) packed[lpos] = out;
+                if (c.hidx < 0) packed[lpos] = out;
             } else {
                 packed[i] = out;
             }
-            count_digits(out, c_hidx);
+            count_digits(out, c.hidx);
         }
     };
     // The wave's steps in order: s -> (tile blockIdx.x + (s / kSteps) * gridDim.x, step
@@ -941,13 +944,9 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
     load(step_at(0), h0, L0, T0, P0);
     load(step_at(1), h1, L1, T1, P1);
     load(step_at(2), h2, L2, T2, P2);
-    c_tag = 0; c_hidx = -1; c_hint0 = c_hint1 = 0; c_m = mir2_t{0, 0};
-    if (S) parse_step(step_at(0), h0, L0, T0, P0);
-    auto iter = [&](uint32_t q, const uint4 (&hp)[kHv], uint32_t Lp, uint64_t Tp, uint64_t Pp,
-                    uint4 (&hl)[kHv], uint32_t &Ll, uint64_t &Tl, uint64_t &Pl) {
-        // C: resolve step q with the probes issued one iteration ago
-        resolve_step(step_at(q));
-        wave_lds_order();
+    ProbeSet c;
+    if (S) parse_step(c, step_at(0), h0, L0, T0, P0);
+    auto tile_end = [&](uint32_t q) {
         if (q % kSteps == kSteps - 1) {   // sort tile done: its deferred packets, then its digit-0 counts
             flush();
             if constexpr (kHf) {   // the wave's chunk: its light word count
@@ -982,9 +981,16 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
                 __syncthreads();
             }
         }
+    };
+    auto iter = [&](uint32_t q, const uint4 (&hp)[kHv], uint32_t Lp, uint64_t Tp, uint64_t Pp,
+                    uint4 (&hl)[kHv], uint32_t &Ll, uint64_t &Tl, uint64_t &Pl) {
+        // C: resolve step q with the probes issued one iteration ago
+        resolve_step(c, step_at(q));
+        wave_lds_order();
+        tile_end(q);
         // A: parse step q + 1 (its records were loaded two iterations ago), probes issued
-        c_tag = 0; c_hidx = -1; c_hint0 = c_hint1 = 0; c_m = mir2_t{0, 0};
-        if (q + 1 < S) parse_step(step_at(q + 1), hp, Lp, Tp, Pp);
+        c = ProbeSet{};
+        if (q + 1 < S) parse_step(c, step_at(q + 1), hp, Lp, Tp, Pp);
         // B: the record loads of step q + 3 into the set step q used
         load(step_at(q + 3), hl, Ll, Tl, Pl);
     };
