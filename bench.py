@@ -667,11 +667,23 @@ def main():
             r4[lib.prefix_key(int(a).to_bytes(4, "little"), 32 if i & 1 else 28)] = 2**64 - 1
         with lib.FsxContext(max_batch=n, max_entries=head["max_entries"], device=local) as rc_:
             rc_.map_update_batch(lib.MAP_IPV4_PREFIX, r4)
+            # pipelined like the headline and the cold leg (round 6; each step resets: the spare
+            # table set swaps in, the rules stay — configuration); FSX_RULES_LEG_SYNC=1: the
+            # round-5 unpipelined leg
+            if os.environ.get("FSX_RULES_LEG_SYNC") != "1":
+                rc_.set_pipeline(True)
+
+            # (two verdict buffers alternating: a pipelined batch's buffer holds its heavy tags
+            # until its tail ends, so consecutive batches in flight never share one)
+            vbufs = [d["v"], torch.empty_like(d["v"])]
+            rk = [0]
 
             def rstep():
                 rc_.reset()
+                vb = vbufs[rk[0] & 1]
+                rk[0] += 1
                 rc_.verdict_batch_device(d["hdr"].data_ptr(), d["len"].data_ptr(), d["ts"].data_ptr(), n,
-                                         d["v"].data_ptr())
+                                         vb.data_ptr())
             rstep()
             rc_.sync()
             torch.cuda.synchronize()
@@ -686,7 +698,9 @@ def main():
             leg = {"value": round(n * args.leg_steps / rt / 1e6, 2), "unit": "Mpps",
                    "ms_per_step": round(rt / args.leg_steps * 1e3, 4), "steps": args.leg_steps,
                    "rules": len(r4), "prefix_lengths": [24, 28, 32],
-                   "rule_drops": ri["prefix_rule_drops"], "allowed": ra, "dropped": rd}
+                   "rule_drops": ri["prefix_rule_drops"], "allowed": ra, "dropped": rd,
+                   "step": "fsx_reset + verdict batch (maps from empty, rules kept), pipelined"
+                   if os.environ.get("FSX_RULES_LEG_SYNC") != "1" else "fsx_reset + verdict batch, unpipelined"}
             if not args.no_check:
                 from oracle import pyoracle
                 hdr, ln, ts = host_inputs(d, n)
@@ -694,7 +708,8 @@ def main():
                 for k, v in r4.items():
                     orc.map_update(lib.MAP_IPV4_PREFIX, k, v)
                 vo = orc.batch(hdr, ln, ts)
-                leg["check"] = {"packets": n, "verdicts_equal": bool(np.array_equal(d["v"].cpu().numpy(), vo))}
+                vlast = vbufs[(rk[0] - 1) & 1]   # (every step: the same batch from empty maps)
+                leg["check"] = {"packets": n, "verdicts_equal": bool(np.array_equal(vlast.cpu().numpy(), vo))}
                 leg["check"].update(compare_state(rc_, orc, (1, 3)))
                 orc.close()
                 del hdr, ln, ts
