@@ -35,7 +35,7 @@ LIBS = {
     "libfsx_synth.so": ["fsx_synth.hip"],
 }
 HEADERS = ["fsx_internal.h", "fsx_synth_common.h", "fsx_dev_common.h", "fsx_q8.h", "fsx_seg.h", "fsx_shard.h", "fsx_walk.h",
-           "fsx_flow_common.h", "fsx_heavy_view.h"]
+           "fsx_flow_common.h", "fsx_heavy_view.h", "fsx_search.h"]
 
 
 def _stale(out: Path, srcs: list[Path]) -> bool:

@@ -520,9 +520,8 @@ hipError_t launch_token_bucket(const uint64_t *S, const uint64_t *ts, const uint
 // the sort carries the light entries only. A heavy source's packets are decided in arrival
 // order by clamp-add maps (its refill between consecutive packets is a map, and maps compose):
 //   k_tb_heavy_tiles<0>  per sort tile: for every heavy source, the map of its packets of the
-//                        tile after the first one, composed in arrival order (lanes of one
-//                        64-packet row by pointer jumping over "the last lane below with the
-//                        same source", rows and the block's four 1024-packet chunks in order)
+//                        tile after the first one, composed in arrival order (the tile's heavy
+//                        packets listed by source in LDS, a segmented scan over the lists)
 //   k_tb_heavy_scan      one wave per heavy source: the tiles in order, 64 at a time — the
 //                        map of a tile's first packet from the previous tile's last timestamp
 //                        (HeavyTileRec t1), an ordered scan of the tile maps from the carried
@@ -538,208 +537,196 @@ __device__ __forceinline__ CMap cm_shfl(const CMap &m, uint32_t src) {
     return CMap{__shfl(m.lo, (int)src), __shfl(m.hi, (int)src), __shfl(m.d, (int)src)};
 }
 
-// The inclusive composition, in lane order, of the maps of the lanes of one source up to this
-// lane (ptr: the last lane below with the same source, 64 for none): pointer jumping, one
-// round per doubling of the longest same-source chain in the row (at most six for 64 lanes;
-// every lane takes part in the shuffles). mc: the row's largest same-source lane count.
-__device__ __forceinline__ CMap tb_row_incl(CMap acc, uint32_t ptr, uint32_t mc) {
-    const uint32_t lane = lane_id();
-    const uint32_t rounds = mc > 1 ? 32u - (uint32_t)__clz((int)(mc - 1u)) : 0u;   // ceil(log2 mc)
-    for (uint32_t r = 0; r < rounds; ++r) {
-        const uint32_t src = ptr < 64u ? ptr : lane;
-        const CMap y = cm_shfl(acc, src);
-        const uint32_t yp = (uint32_t)__shfl((int)ptr, (int)src);
-        if (ptr < 64u) {
-            acc = cm_compose(acc, y);
-            ptr = yp;
-        }
-    }
-    return acc;
-}
-
 struct TbHeavyOut {
     CMap *map;      // [tile][kHeavyMax]: h's packets of the tile after its first, composed
     uint64_t *x1;   // [tile][kHeavyMax]: the state after the tile's first packet of h | PASS << 63
 };
 
+// Per sort tile (one block): the tile's heavy packets listed by source in arrival order (a
+// stable counting sort in LDS: per-wave counts, their offsets, then each 64-packet row's
+// same-source lanes placed in order), the timestamps staged in LDS, and a segmented scan of
+// the packets' maps over the lists (a segment per source, 16 entries per thread) — kApply
+// false: the maps of a source's packets after its first composed (-> o.map); true: the replay
+// from the state after the tile's first packet (o.x1), every packet's verdict byte written over
+// its tag, PASS / DROP counted.
+// (Measured, maps + replay per 64M packets, DESIGN.md §4.2: per-row pointer jumping over
+// same-source lanes 0.6-0.75 + 1.25-1.43 ms; one thread walking each list 2.6-3.6 + 1.9 ms;
+// one wave per source scanning its list 1.75-3.0 + 1.6-1.9 ms — 2M (tile, source) pairs each a
+// dependent scan; this segmented scan 1.0 (beside the light scan) + 0.57 ms.)
 template <bool kApply>
 __global__ __launch_bounds__(256) void k_tb_heavy_tiles(BatchState *bs, uint8_t *__restrict__ verdict,
                                                         const uint64_t *__restrict__ ts, uint32_t n,
                                                         const HeavySet *__restrict__ hs, Limits lim, TbHeavyOut o,
                                                         TableState *tstate) {
-    __shared__ CMap s_m[4][kHeavyMax];
-    __shared__ unsigned long long s_f[4][kHeavyMax], s_l[4][kHeavyMax];
-    __shared__ long long s_xa[4][kHeavyMax], s_xb[4][kHeavyMax];
-    __shared__ unsigned long long s_pv[4][kHeavyMax];
-    __shared__ uint32_t s_p1[kHeavyMax];
+    __shared__ unsigned long long s_ts[kSortTile];
+    __shared__ __attribute__((aligned(16))) uint16_t s_list[kSortTile];
+    __shared__ uint32_t s_wc[4][kHeavyMax];   // per wave: its count of h, then its next place
+    __shared__ uint32_t s_off[kHeavyMax + 1];
+    __shared__ __attribute__((aligned(16))) uint8_t s_hsrc[kSortTile];   // the source of each entry
+    __shared__ unsigned long long s_x1[kHeavyMax];
+    __shared__ CMap s_wagg[4];
+    __shared__ uint32_t s_wflag[4];
     __shared__ unsigned long long s_cnt[2];
     if (bs->err || !bs->hfast) return;
     const uint32_t tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
     const uint32_t ntiles = (n + kSortTile - 1) / kSortTile;
     if (blockIdx.x >= ntiles) return;
     const uint32_t t = xcd_swizzle(blockIdx.x, ntiles);
-    const uint32_t c0 = t * kSortTile + w * 1024u;
+    const uint32_t t0 = t * kSortTile;
     const uint64_t lt_mask = (1ull << lane) - 1ull;
     const uint32_t nh = hs->n;
     const int64_t H = (int64_t)(lim.tb_cap - kTbCost);   // (k_hmode: C >= cost on this path)
     const uint64_t dt_sat = tb_dt_sat(lim.tb_rate);
-    auto delta = [&](uint64_t tp, uint64_t tprev) -> int64_t {
-        return tb_refill(tp - tprev, lim.tb_rate, dt_sat) - (int64_t)kTbCost;
-    };
-    const CMap id{0, H, 0};
-    for (uint32_t j = tid; j < 4 * kHeavyMax; j += 256) {
-        (&s_m[0][0])[j] = id;
-        (&s_f[0][0])[j] = kTbNone;
-        (&s_l[0][0])[j] = kTbNone;
-    }
+    for (uint32_t j = tid; j < 4 * kHeavyMax; j += 256) (&s_wc[0][0])[j] = 0;
     if (tid < 2) s_cnt[tid] = 0;
     __syncthreads();
-    uint64_t Tr[16];
+    // 1. the chunk's rows: tags, timestamps to LDS, per-wave counts of every heavy source
     uint32_t Gr[16];
 #pragma unroll
     for (uint32_t r = 0; r < 16; ++r) {
-        const uint32_t i = c0 + r * 64u + lane;
+        const uint32_t p = w * 1024u + r * 64u + lane, i = t0 + p;
         const bool live = i < n;
         const uint32_t g = live ? verdict[i] : 0u;
         Gr[r] = g >= 0x80u && (g & 0x7Fu) < nh ? (g & 0x7Fu) : 0xFFu;
-        Tr[r] = ts[live ? i : 0u];
+        s_ts[p] = ts[live ? i : 0u];
     }
-    // 1. per wave and heavy source: the chunk's first / last timestamp and the maps of its
-    //    packets after the first, composed
+    // (LDS atomics: a ballot match here would be kept alive by the compiler for step 3's —
+    // 320 VGPRs)
+#pragma unroll
+    for (uint32_t r = 0; r < 16; ++r)
+        if (Gr[r] != 0xFFu) atomicAdd(&s_wc[w][Gr[r]], 1u);
+    __syncthreads();
+    // 2. the lists' offsets: sources in order, waves in order within a source (a scan over the
+    //    128 sources by two waves; one thread's serial pass over them cost ~50 us per tile)
+    static_assert(kHeavyMax == 128, "two waves scan the sources");
+    __shared__ uint32_t s_w0;
+    uint32_t c4[4] = {0, 0, 0, 0}, tot = 0;
+    if (tid < kHeavyMax) {
+#pragma unroll
+        for (uint32_t ww = 0; ww < 4; ++ww) { c4[ww] = s_wc[ww][tid]; tot += c4[ww]; }
+    }
+    const uint32_t incl = tid < kHeavyMax ? wave_incl_sum(tot) : 0u;
+    if (tid == 63) s_w0 = incl;
+    __syncthreads();
+    if (tid < kHeavyMax) {
+        uint32_t a = incl - tot + (tid >= 64 ? s_w0 : 0u);
+        s_off[tid] = a;
+#pragma unroll
+        for (uint32_t ww = 0; ww < 4; ++ww) { s_wc[ww][tid] = a; a += c4[ww]; }
+        if (tid == kHeavyMax - 1) s_off[kHeavyMax] = a;
+        if constexpr (kApply) {   // the tile's first packet of h: from k_tb_heavy_scan
+            if (tid < nh && tot) s_x1[tid] = o.x1[(size_t)t * kHeavyMax + tid];
+        }
+    }
+    __syncthreads();
+    // 3. every heavy packet's place in its source's list (rows in order: stable)
 #pragma unroll
     for (uint32_t r = 0; r < 16; ++r) {
         const uint32_t g = Gr[r];
-        const bool hv = g != 0xFFu;
-        const uint64_t act = __ballot(hv);
+        const uint64_t act = __ballot(g != 0xFFu);
         if (!act) continue;
-        const uint64_t T = Tr[r];
         const uint64_t peers = match_digit(g, act);
-        const uint64_t below = peers & lt_mask;
-        const uint32_t pl = below ? 63u - (uint32_t)__clzll((long long)below) : lane;
-        const uint64_t tpl = __shfl(T, (int)pl);
-        CMap m = id;
-        if (hv) {
-            uint64_t tp = tpl;
-            bool pred = below != 0;
-            if (!pred) {
-                tp = s_l[w][g];
-                pred = tp != kTbNone;
-                if (!pred) s_f[w][g] = T;
-            }
-            if (pred) m = CMap{0, H, delta(T, tp)};
+        if (g != 0xFFu) {
+            const uint32_t base = s_wc[w][g];
+            const uint32_t e = base + (uint32_t)__popcll(peers & lt_mask);
+            s_list[e] = (uint16_t)(w * 1024u + r * 64u + lane);
+            s_hsrc[e] = (uint8_t)g;
         }
-        const uint32_t mc = wave_max(hv ? (uint32_t)__popcll(peers) : 0u);
-        const CMap acc = tb_row_incl(m, hv && below ? pl : 64u, mc);
-        if (hv && (peers >> lane) == 1ull) {   // the row's last packet of h
-            s_m[w][g] = cm_compose(acc, s_m[w][g]);
-            s_l[w][g] = T;
-        }
+        wave_lds_order();
+        if (g != 0xFFu && (peers >> lane) == 1ull) s_wc[w][g] += (uint32_t)__popcll(peers);   // (the last lane)
         wave_lds_order();
     }
     __syncthreads();
-    if constexpr (!kApply) {   // the tile's map after h's first packet (the chunks joined in order)
-        if (tid < nh) {
-            const uint32_t h = tid;
-            CMap M = id;
-            uint64_t last = kTbNone;
+    // 4. a segmented scan over the lists (one segment per source, its first entry the identity):
+    //    each thread composes 16 consecutive entries, the 256 thread aggregates are scanned
+    //    across the block, then each thread replays its entries from its exclusive prefix
+    //    (kApply false: a source's last entry writes its map; true: every entry's verdict from
+    //    the state after the source's first packet, o.x1, staged in LDS)
+    const uint32_t total = s_off[kHeavyMax];
+    const uint32_t j0 = tid * 16u;
+    const CMap id{0, H, 0};
+    uint32_t hp = 0xFFu;   // the source and timestamp of the entry before j0
+    uint64_t Tp = 0;
+    if (j0 > 0 && j0 - 1u < total) {
+        hp = s_hsrc[j0 - 1u];
+        Tp = s_ts[s_list[j0 - 1u]];
+    }
+    // the thread's 16 entries in registers (vector LDS reads; the timestamps gathered at once)
+    uint32_t hw[4], pw[8];
+    *reinterpret_cast<uint4 *>(hw) = *reinterpret_cast<const uint4 *>(&s_hsrc[j0]);
+    *reinterpret_cast<uint4 *>(pw) = *reinterpret_cast<const uint4 *>(&s_list[j0]);
+    *reinterpret_cast<uint4 *>(pw + 4) = *reinterpret_cast<const uint4 *>(&s_list[j0 + 8u]);
+    const uint32_t hnext = j0 + 16u < total ? s_hsrc[j0 + 16u] : 0xFFu;
+    const uint32_t nv = total > j0 ? min(total - j0, 16u) : 0u;
+    uint64_t Tv[16];
 #pragma unroll
-            for (uint32_t ww = 0; ww < 4; ++ww) {
-                const uint64_t f = s_f[ww][h];
-                if (f == kTbNone) continue;
-                M = last != kTbNone ? cm_compose(s_m[ww][h], cm_compose(CMap{0, H, delta(f, last)}, M)) : s_m[ww][h];
-                last = s_l[ww][h];
-            }
-            if (last != kTbNone) o.map[(size_t)t * kHeavyMax + h] = M;
-        }
-        return;
-    } else {
-        // 2. per heavy source: the state around each chunk's first packet, from the state
-        //    after the tile's first packet (k_tb_heavy_scan)
-        if (tid < nh) {
-            const uint32_t h = tid;
-            int64_t x = 0;
-            uint64_t last = kTbNone;
+    for (uint32_t k = 0; k < 16; ++k) {
+        const uint32_t P = (pw[k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
+        Tv[k] = s_ts[k < nv ? P : 0u];
+    }
+    int64_t dv[16];
+    uint32_t firstm = 0;
+    CMap agg = id;
+    bool fl = false;
 #pragma unroll
-            for (uint32_t ww = 0; ww < 4; ++ww) {
-                const uint64_t f = s_f[ww][h];
-                if (f == kTbNone) continue;
-                if (last == kTbNone) {   // the tile's first packet of h
-                    const uint64_t x1 = o.x1[(size_t)t * kHeavyMax + h];
-                    s_p1[h] = (uint32_t)(x1 >> 63);
-                    x = (int64_t)(x1 & ~(1ull << 63));
-                    s_xa[ww][h] = x;
-                    s_pv[ww][h] = kTbNone;
-                } else {
-                    s_xb[ww][h] = x;
-                    s_pv[ww][h] = last;
-                    x = cm_apply(CMap{0, H, delta(f, last)}, x);
-                    s_xa[ww][h] = x;
-                }
-                x = cm_apply(s_m[ww][h], x);
-                last = s_l[ww][h];
+    for (uint32_t k = 0; k < 16; ++k) {
+        const uint32_t h = (hw[k >> 2] >> (8 * (k & 3))) & 0xFFu;
+        const uint32_t hq = k == 0 ? hp : (hw[(k - 1) >> 2] >> (8 * ((k - 1) & 3))) & 0xFFu;
+        const uint64_t Tq = k == 0 ? Tp : Tv[k - 1];
+        const bool first = h != hq;
+        dv[k] = first ? 0 : tb_refill(Tv[k] - Tq, lim.tb_rate, dt_sat) - (int64_t)kTbCost;
+        if (k < nv) {
+            firstm |= (uint32_t)first << k;
+            agg = first ? id : cm_compose(CMap{0, H, dv[k]}, agg);
+            fl = fl || first;
+        }
+    }
+    CMap inc = agg;
+    bool ifl = fl;
+#pragma unroll
+    for (int k = 1; k < 64; k <<= 1) {
+        const CMap y = cm_shfl_up(inc, k);
+        const bool yf = __shfl_up((int)ifl, k) != 0;
+        if (lane >= (uint32_t)k) {
+            if (!ifl) inc = cm_compose(inc, y);
+            ifl = ifl || yf;
+        }
+    }
+    if (lane == 63) {
+        s_wagg[w] = inc;
+        s_wflag[w] = ifl;
+    }
+    __syncthreads();
+    CMap run = id;   // the block's entries before the wave
+    for (uint32_t ww = 0; ww < w; ++ww) run = s_wflag[ww] ? s_wagg[ww] : cm_compose(s_wagg[ww], run);
+    {
+        const CMap y = cm_shfl_up(inc, 1);
+        const bool yf = __shfl_up((int)ifl, 1) != 0;
+        if (lane > 0) run = yf ? y : cm_compose(y, run);
+    }
+    uint32_t np = 0, nd = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 16; ++k) {
+        if (k < nv) {
+            const uint32_t h = (hw[k >> 2] >> (8 * (k & 3))) & 0xFFu;
+            const bool first = (firstm >> k) & 1u;
+            if constexpr (kApply) {
+                const uint32_t P = (pw[k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
+                const uint64_t x1 = s_x1[h];
+                const bool pass = first ? (x1 >> 63) != 0
+                                        : cm_apply(run, (int64_t)(x1 & ~(1ull << 63))) + dv[k] >= 0;
+                verdict[t0 + P] = pass ? XDP_PASS : XDP_DROP;
+                np += pass;
+                nd += !pass;
+            }
+            run = first ? id : cm_compose(CMap{0, H, dv[k]}, run);
+            if constexpr (!kApply) {
+                const uint32_t hn = k == 15 ? hnext : (k + 1 < nv ? (hw[(k + 1) >> 2] >> (8 * ((k + 1) & 3))) & 0xFFu : 0xFFu);
+                if (hn != h) o.map[(size_t)t * kHeavyMax + h] = run;
             }
         }
-        __syncthreads();
-        for (uint32_t j = tid; j < 4 * kHeavyMax; j += 256) (&s_l[0][0])[j] = kTbNone;
-        __syncthreads();
-        // 3. the replay, row by row: s_xa[w][h] becomes the state after h's latest packet. The
-        //    rows are read again (L2-resident since step 1): kept in registers across steps 1-3
-        //    the fully unrolled replay took 357 VGPRs + 101 AGPRs (3.0 ms per 64M packets)
-        uint32_t np = 0, nd = 0;
-        // (the next row's tag and timestamp loaded one row ahead)
-        uint32_t gn = c0 + lane < n ? verdict[c0 + lane] : 0u;
-        uint64_t Tn = ts[c0 + lane < n ? c0 + lane : 0u];
-#pragma unroll 1
-        for (uint32_t r = 0; r < 16; ++r) {
-            const uint32_t i = c0 + r * 64u + lane;
-            const uint32_t g0 = gn;
-            const uint64_t T = Tn;
-            if (r + 1 < 16) {
-                const uint32_t i1 = i + 64u;
-                gn = i1 < n ? verdict[i1] : 0u;
-                Tn = ts[i1 < n ? i1 : 0u];
-            }
-            const uint32_t g = g0 >= 0x80u && (g0 & 0x7Fu) < nh ? (g0 & 0x7Fu) : 0xFFu;
-            const bool hv = g != 0xFFu;
-            const uint64_t act = __ballot(hv);
-            if (!act) continue;
-            const uint64_t peers = match_digit(g, act);
-            const uint64_t below = peers & lt_mask;
-            const uint32_t pl = below ? 63u - (uint32_t)__clzll((long long)below) : lane;
-            const uint64_t tpl = __shfl(T, (int)pl);
-            CMap m = id;
-            uint64_t tp = tpl;
-            bool seen = false;
-            if (hv) {
-                seen = s_l[w][g] != kTbNone;   // h had a packet in an earlier row of the chunk
-                if (!below) tp = s_l[w][g];
-                if (below || seen) m = CMap{0, H, delta(T, tp)};
-            }
-            const uint32_t mc = wave_max(hv ? (uint32_t)__popcll(peers) : 0u);
-            const CMap acc = tb_row_incl(m, hv && below ? pl : 64u, mc);
-            const CMap accp = cm_shfl(acc, pl);   // (the predecessor's inclusive map)
-            if (hv) {
-                const int64_t xin = s_xa[w][g];   // the state entering the row's first packet of h
-                uint8_t v;
-                if (below || seen) {
-                    const int64_t xb = below ? cm_apply(accp, xin) : xin;
-                    v = xb + m.d >= 0 ? XDP_PASS : XDP_DROP;
-                } else if (s_pv[w][g] == kTbNone) {   // the tile's first packet of h
-                    v = s_p1[g] ? XDP_PASS : XDP_DROP;
-                } else {                               // the chunk's first, after an earlier chunk's
-                    v = s_xb[w][g] + delta(T, s_pv[w][g]) >= 0 ? XDP_PASS : XDP_DROP;
-                }
-                verdict[i] = v;
-                np += v == XDP_PASS;
-                nd += v == XDP_DROP;
-            }
-            wave_lds_order();
-            if (hv && (peers >> lane) == 1ull) {
-                s_xa[w][g] = cm_apply(acc, s_xa[w][g]);
-                s_l[w][g] = T;
-            }
-            wave_lds_order();
-        }
+    }
+    if constexpr (kApply) {
         np = wave_sum(np);
         nd = wave_sum(nd);
         if (lane == 0) {
