@@ -475,6 +475,14 @@ size_t hflow_bytes(uint64_t cap) {
 
 // ------------------------------------------------------------------ launchers
 hipError_t launch_hmode(BatchState *bs, const uint64_t *ts, uint32_t n, const Limits &lim, hipStream_t st) {
+    // (A/B: FSX_TB_RUNS=1 sends every token-bucket batch of the unsorted path to its run path —
+    // the heavy runs gathered in the tail and scanned with the light entries; read per batch)
+    if (lim.limiter == 2 && getenv("FSX_TB_RUNS")) {
+        Limits l = lim;
+        l.tb_cap = 0;   // (k_hmode's decision only)
+        k_hmode<<<1, 1, 0, st>>>(bs, ts, n, l);
+        return hipGetLastError();
+    }
     k_hmode<<<1, 1, 0, st>>>(bs, ts, n, lim);
     return hipGetLastError();
 }
