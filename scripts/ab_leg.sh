@@ -16,6 +16,6 @@ r = d[{"rules": "prefix_rules"}.get(leg, leg)]
 if "ms_per_step" in r:
     print(e or "default", leg, r["ms_per_step"])
 else:   # (a leg of several runs: limiters)
-    print(e or "default", leg, {k: v["ms_per_step"] for k, v in r.items() if isinstance(v, dict)})
+    print(e or "default", leg, {k: v["ms_per_step"] for k, v in r.items() if isinstance(v, dict) and "ms_per_step" in v})
 PY
 done
