@@ -85,12 +85,13 @@ def _config2(oracle, n, j0=0):
 CFG = dict(max_entries=1 << 20)   # a 2^21-slot table: the heavy-source sort with verdict lists
 
 
-@pytest.mark.parametrize("max_entries", [1 << 20, 1 << 21, 1 << 22])
+@pytest.mark.parametrize("max_entries", [1 << 19, 1 << 20, 1 << 21, 1 << 22, 1 << 23, 1 << 24])
 def test_unsorted_heavy_path_config2_slices(native, oracle, max_entries):
     """Two carried 1M-packet slices of the config-2 stream (heads blacklisted across the
-    cut): both batches on the unsorted path, everything equal to the oracle. Tables of 2^21,
-    2^22 and 2^23 slots: 7- and 8-bit light digits (an 8-bit light pass once overwrote the
-    heavy buckets' pass-0 tile rows the walker reads)."""
+    cut): both batches on the unsorted path, everything equal to the oracle. Tables of 2^20
+    to 2^25 slots: 6-, 7- and 8-bit light digits, two light passes up to 23-bit ids and three
+    for 24 / 25 (an 8-bit light pass once overwrote the heavy buckets' pass-0 tile rows the
+    walker reads)."""
     hdr, ln, ts = _config2(oracle, 1 << 21)
     cut = 1 << 20
     _run(native, oracle, [(hdr[:cut], ln[:cut], ts[:cut]), (hdr[cut:], ln[cut:], ts[cut:])],
