@@ -230,7 +230,7 @@ static void free_scratch(fsx_ctx *c) {
     hipFree(s.span_list); hipFree(s.sort_ctl); hipFree(s.gbase); hipFree(s.status);
     hipFree(s.lim_tiles); hipFree(s.sw_seg); hipFree(s.sketch); hipFree(s.heavy);
     hipFree(s.drop_list); hipFree(s.drop_cur); hipFree(s.heavy_flow);
-    hipFree(s.chunk_cnt); hipFree(s.hrec); hipFree(s.hflow); hipFree(s.tbh);
+    hipFree(s.chunk_cnt); hipFree(s.hrec); hipFree(s.hflow); hipFree(s.tbh); hipFree(s.dig);
     hipFree(s.admit_rank); hipFree(s.admit_cnt);
     s = Scratch{};
 }
@@ -245,6 +245,7 @@ static int alloc_scratch(fsx_ctx *c, uint64_t cap) {
     HIPCHK(c, hipMalloc(&s.pay[0], cap * 8));
     HIPCHK(c, hipMalloc(&s.pay[1], cap * 8));
     HIPCHK(c, hipMalloc(&s.marks, cap + 16));
+    HIPCHK(c, hipMalloc(&s.dig, cap + 16));
     HIPCHK(c, hipMalloc(&s.headf, cap + 16));
     HIPCHK(c, hipMalloc(&s.seg_start, (cap + 1) * 4));
     HIPCHK(c, hipMalloc(&s.seg_slot, cap * 4));

@@ -1082,9 +1082,12 @@ __device__ __forceinline__ bool sort_item(uint32_t i, uint32_t end, int first, u
 }
 
 // Per-tile digit counts (one block per tile; per-wave LDS counters).
+// din (passes >= 1): the digits the previous pass's scatter wrote, one byte per position —
+// 4 KiB per tile read instead of 32 KiB of keys.
 __global__ __launch_bounds__(256) void k_tile_hist(const uint64_t *__restrict__ in, uint32_t L_host,
                                                    const uint32_t *L_dev, uint32_t shift, uint32_t dmask,
-                                                   int first, uint32_t *__restrict__ thist, uint32_t tcap) {
+                                                   int first, uint32_t *__restrict__ thist, uint32_t tcap,
+                                                   const uint8_t *__restrict__ din) {
     __shared__ uint32_t sh[4][256];
     const uint32_t tid = threadIdx.x, w = tid >> 6;
     const uint32_t L = L_dev ? *L_dev : L_host;
@@ -1096,6 +1099,36 @@ __global__ __launch_bounds__(256) void k_tile_hist(const uint64_t *__restrict__ 
     for (int k = 0; k < 4; ++k) sh[k][tid] = 0;
     __syncthreads();
     const uint32_t t0 = t * kSortTile, end = min(L, t0 + kSortTile);
+    const uint32_t lane = lane_id();
+    if (din) {   // thread x: positions t0 + 16x .. t0 + 16x + 15
+        static_assert(kSortTile == 16 * 256, "16 digit bytes per thread");
+        const uint32_t p0 = t0 + 16u * tid;
+        uint32_t wd[4] = {0, 0, 0, 0};
+        if (p0 + 16u <= end) {
+            const uint4 x = *reinterpret_cast<const uint4 *>(din + p0);
+            wd[0] = x.x; wd[1] = x.y; wd[2] = x.z; wd[3] = x.w;
+        } else {
+            for (uint32_t k = 0; k < 16; ++k)
+                if (p0 + k < end) wd[k >> 2] |= (uint32_t)din[p0 + k] << (8 * (k & 3));
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < 16; ++k) {
+            const bool ok = p0 + k < end;
+            const uint32_t d = (wd[k >> 2] >> (8 * (k & 3))) & dmask;
+            const uint64_t act = __ballot(ok);
+            if (!act) continue;
+            const int lead = __ffsll((unsigned long long)act) - 1;
+            const uint32_t dl = __shfl(d, lead);
+            if (__ballot(ok && d == dl) == act) {
+                if ((int)lane == lead) atomicAdd(&sh[w][dl], (uint32_t)__popcll(act));
+            } else if (ok) {
+                atomicAdd(&sh[w][d], 1u);
+            }
+        }
+        __syncthreads();
+        if (tid <= dmask) thist[(size_t)tid * tcap + t] = sh[0][tid] + sh[1][tid] + sh[2][tid] + sh[3][tid];
+        return;
+    }
     // 16-byte loads: thread x holds keys 2(256 r + x) and 2(256 r + x) + 1 (the order of
     // a histogram's inputs is irrelevant)
     uint64_t v[kSortItems];
@@ -1110,7 +1143,6 @@ __global__ __launch_bounds__(256) void k_tile_hist(const uint64_t *__restrict__ 
 #pragma unroll
         for (int r = 0; r < kSortItems; ++r) v[r] = item(r) < end ? in[item(r)] : kSentinel;
     }
-    const uint32_t lane = lane_id();
 #pragma unroll
     for (int r = 0; r < kSortItems; ++r) {
         const uint32_t i = item(r);
@@ -1204,7 +1236,9 @@ __device__ __forceinline__ void sort_tile(uint32_t t, const uint64_t *__restrict
                                           uint32_t dmask, int first, const BatchState *bs,
                                           const uint64_t *__restrict__ pin, uint64_t *__restrict__ pout,
                                           const uint64_t *__restrict__ ts,
-                                          const uint32_t *__restrict__ len, Offs offs) {
+                                          const uint32_t *__restrict__ len, Offs offs,
+                                          uint8_t *__restrict__ dout = nullptr, uint32_t nshift = 0,
+                                          uint32_t nmask = 0) {
     __shared__ unsigned long long s_el[kSortTile];
     __shared__ uint32_t s_wc[4][256];
     __shared__ uint32_t s_dst[256], s_tbase[256], s_tcnt[256];
@@ -1292,6 +1326,7 @@ __device__ __forceinline__ void sort_tile(uint32_t t, const uint64_t *__restrict
             const uint32_t dd = (uint32_t)(x >> shift) & dmask;
             dst[m] = s_dst[dd] + (j - s_tbase[dd]);
             out[dst[m]] = x;
+            if (dout) dout[dst[m]] = (uint8_t)((x >> nshift) & nmask);   // (the next pass's digit)
         }
     }
     FSX_STAMP(t, 4);
@@ -1333,12 +1368,15 @@ __global__ __launch_bounds__(256, kLatePay ? FSX_SCATTER_MINB : 1) void k_tile_s
                                                       const uint64_t *__restrict__ pin,
                                                       uint64_t *__restrict__ pout,
                                                       const uint64_t *__restrict__ ts,
-                                                      const uint32_t *__restrict__ len) {
+                                                      const uint32_t *__restrict__ len,
+                                                      uint8_t *__restrict__ dout, uint32_t nshift,
+                                                      uint32_t nmask) {
     const uint32_t L = L_dev ? *L_dev : L_host;
     const uint32_t nact = (L + kSortTile - 1) / kSortTile;   // tiles of this pass
     if (blockIdx.x >= nact) return;
     const uint32_t t = xcd_swizzle(blockIdx.x, nact);
-    sort_tile<kLatePay>(t, in, out, L, shift, dmask, first, bs, pin, pout, ts, len, TileOffs{offs, tcap, t});
+    sort_tile<kLatePay>(t, in, out, L, shift, dmask, first, bs, pin, pout, ts, len, TileOffs{offs, tcap, t},
+                        dout, nshift, nmask);
 }
 
 // ---- pass 0 with the heavy sources outside the sort (k_parse<..., kHf>; fsx_heavy.hip).
@@ -1381,7 +1419,9 @@ __global__ __launch_bounds__(256, FSX_PASS0H_MINB) void k_pass0h(const uint64_t 
                                                                   const uint64_t *__restrict__ lmask,
                                                                   HeavyTileRec *__restrict__ rec,
                                                                   const HeavySet *__restrict__ hs,
-                                                                  const uint64_t *__restrict__ pin) {
+                                                                  const uint64_t *__restrict__ pin,
+                                                                  uint8_t *__restrict__ dout, uint32_t nshift,
+                                                                  uint32_t nmask) {
     __shared__ unsigned long long s_el[kSortTile];
     __shared__ uint32_t s_wc[4][256];
     __shared__ uint32_t s_dst[256], s_tbase[256], s_tcnt[256];
@@ -1600,6 +1640,7 @@ __global__ __launch_bounds__(256, FSX_PASS0H_MINB) void k_pass0h(const uint64_t 
             const uint32_t dd = (uint32_t)((x & ~kFreshBit) >> shift) & dmask;
             dst[m] = s_dst[dd] + (j - s_tbase[dd]);
             out[dst[m]] = x;
+            if (dout) dout[dst[m]] = (uint8_t)(((x & ~kFreshBit) >> nshift) & nmask);   // (pass 1's digit)
         }
     }
     if constexpr (kRecs && FSX_PASS0H_GATHER) {   // (A/B: gathered by arrival index)
@@ -1629,14 +1670,17 @@ __global__ __launch_bounds__(256, FSX_PASS0H_MINB) void k_pass0h(const uint64_t 
 hipError_t launch_pass0h(const uint64_t *in, uint64_t *out, uint32_t n, uint32_t shift, uint32_t dmask,
                          const uint32_t *offs, uint32_t tcap, BatchState *bs, uint64_t *pout, const uint64_t *ts,
                          const uint32_t *len, const uint8_t *tags, const uint32_t *chunk_cnt,
-                         const uint64_t *lmask, void *rec, const HeavySet *hs, const uint64_t *pin, hipStream_t st) {
+                         const uint64_t *lmask, void *rec, const HeavySet *hs, const uint64_t *pin, hipStream_t st,
+                         uint8_t *dout, uint32_t nshift, uint32_t nmask) {
     const uint32_t ntiles = std::max<uint32_t>(1, (n + kSortTile - 1) / kSortTile);
     if (pin)   // (FSX_PARSE_PAY: the clock facts and payload words came from k_parse)
         k_pass0h<false><<<ntiles, 256, 0, st>>>(in, out, n, shift, dmask, offs, tcap, bs, pout, ts, len, tags,
-                                                chunk_cnt, lmask, static_cast<HeavyTileRec *>(rec), hs, pin);
+                                                chunk_cnt, lmask, static_cast<HeavyTileRec *>(rec), hs, pin,
+                                                dout, nshift, nmask);
     else
         k_pass0h<true><<<ntiles, 256, 0, st>>>(in, out, n, shift, dmask, offs, tcap, bs, pout, ts, len, tags,
-                                               chunk_cnt, lmask, static_cast<HeavyTileRec *>(rec), hs, nullptr);
+                                               chunk_cnt, lmask, static_cast<HeavyTileRec *>(rec), hs, nullptr,
+                                               dout, nshift, nmask);
     return hipGetLastError();
 }
 
@@ -3976,6 +4020,13 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
         // buckets (light_b + h) are read in the tail (k_walk_heavy_sel, k_hflow_combine,
         // k_heavy_gather) — an 8-bit light digit (tables of 2^22 / 2^23 slots) would overwrite them
         uint32_t *hst = pass > 0 && heavy_sort ? sc.hist + 256ull * tcap : sc.hist;
+        // the next pass's digit byte per output position (its tile histogram reads those
+        // instead of the keys; FSX_SORT_KEY_HIST=1: the keys, A/B)
+        static const bool key_hist = getenv("FSX_SORT_KEY_HIST") != nullptr;
+        const bool dig_on = !key_hist && sc.dig;
+        uint8_t *dout = dig_on && pass + 1 < npass ? sc.dig : nullptr;
+        const uint32_t nshift = pass + 1 < npass ? dp.shift[pass + 1] : 0u;
+        const uint32_t nmask = pass + 1 < npass ? dp.mask[pass + 1] : 0u;
         if (onesweep) {
             const uint32_t *Ld = pass == 0 ? nullptr : &bs->n_valid;
             k_onesweep<kLookW><<<ntiles, 256, 0, st>>>(in, out, n, Ld, shift, pmask, sc.gbase + 256 * pass,
@@ -3989,7 +4040,8 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
             // is odd, in packed[0] when it is even)
             const uint32_t *Ld = pass == 0 ? nullptr : &bs->n_light;
             if (pass > 0) {   // pass 0's per-tile counts come from k_parse
-                k_tile_hist<<<ntiles, 256, 0, st>>>(in, n, Ld, shift, pmask, pass == 0, hst, tcap);
+                k_tile_hist<<<ntiles, 256, 0, st>>>(in, n, Ld, shift, pmask, pass == 0, hst, tcap,
+                                                    dig_on ? sc.dig : nullptr);
                 mark("k_tile_hist");
             }
             k_tile_scan<<<pmask + 1, 256, 0, st>>>(hst, tcap, n, Ld, sc.gbase + 256 * pass);
@@ -3998,14 +4050,14 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
             if (pass == 0 && hfm) {   // light words from the parse chunks; heavy tile sums; the path
                 if ((e = launch_pass0h(in, out, n, shift, pmask, sc.hist, tcap, bs, pout, ts, len, verdict,
                                        sc.chunk_cnt, light_masks(sc.chunk_cnt, sc.cap), sc.hrec, sc.heavy,
-                                       FSX_PARSE_PAY ? sc.pay[0] : nullptr, st)) != hipSuccess)
+                                       FSX_PARSE_PAY ? sc.pay[0] : nullptr, st, dout, nshift, nmask)) != hipSuccess)
                     return e;
                 mark("k_pass0h");
                 if ((e = launch_hmode(bs, ts, n, lim, st)) != hipSuccess) return e;
                 mark("k_hmode");
             } else {
                 k_tile_scatter<kLatePayDefault><<<ntiles, 256, 0, st>>>(in, out, n, Ld, shift, pmask, pass == 0, hst, tcap, bs,
-                                                       pin, pout, ts, len);
+                                                       pin, pout, ts, len, dout, nshift, nmask);
                 mark("k_tile_scatter");
             }
             if (pass == 0 && (e = tail_hook(2)) != hipSuccess) return e;

@@ -441,6 +441,8 @@ struct Scratch {
     uint32_t *chunk_cnt;
     void *hrec;
     void *hflow;           // tail: per (group of kHGroupTiles tiles, heavy source) flow sums
+    uint8_t *dig;          // the next sort pass's digit of every output position (cap bytes):
+                           // written by pass p's scatter, read by pass p + 1's tile histogram
     void *tbh;             // token bucket, heavy sources unsorted: per (sort tile, heavy source)
                            // map + state (tb_heavy_bytes; null for the other limiters)
     // FSX_FLAG_OVERFLOW_ADMIT: per arrival index, 1 at a new source's first packet, then its
@@ -664,7 +666,8 @@ hipError_t launch_pass0h(const uint64_t *in, uint64_t *out, uint32_t n, uint32_t
                          const uint32_t *offs, uint32_t tcap, BatchState *bs, uint64_t *pout, const uint64_t *ts,
                          const uint32_t *len, const uint8_t *tags, const uint32_t *chunk_cnt,
                          const uint64_t *lmask, void *rec,
-                         const HeavySet *hs, const uint64_t *pin, hipStream_t st);
+                         const HeavySet *hs, const uint64_t *pin, hipStream_t st,
+                         uint8_t *dout = nullptr, uint32_t nshift = 0, uint32_t nmask = 0);
 hipError_t launch_hmode(BatchState *bs, const uint64_t *ts, uint32_t n, const Limits &lim, hipStream_t st);
 // (FSX_PARSE_PAY: every sort tile's HeavyTileRec, at the start of the tail)
 hipError_t launch_heavy_recs(const BatchState *bs, const uint64_t *ts, const uint32_t *len, const uint8_t *tags,
