@@ -237,7 +237,10 @@ __global__ __launch_bounds__(256) void k_heavy_gather(const BatchState *bs, cons
     const uint32_t ntiles = (n + kSortTile - 1) / kSortTile;
     const uint64_t lt = (1ull << lane) - 1ull;
     for (uint32_t t = blockIdx.x * 4u + w; t < ntiles; t += gridDim.x * 4u) {
-        for (uint32_t h = lane; h < kHeavyMax; h += 64) s_cnt[w][h] = 0;
+        // each heavy source's next place in its run: its pass-0 tile offset, then advanced by
+        // the rows (a global load of the offset per row and lane, waited on inside the row
+        // loop, made this kernel take ~1 ms per 64M packets)
+        for (uint32_t h = lane; h < kHeavyMax; h += 64) s_cnt[w][h] = h < nh ? offs[(size_t)(lb + h) * tcap + t] : 0u;
         wave_lds_order();
         // 16 rows' tags, then their heavy packets' timestamps and lengths, in flight at once
         for (uint32_t r0 = 0; r0 < (uint32_t)kSortTile / 64u; r0 += 16) {
@@ -254,8 +257,11 @@ __global__ __launch_bounds__(256) void k_heavy_gather(const BatchState *bs, cons
                 const uint32_t hg = G[r] & 0x7Fu;
                 const bool hv = G[r] >= 0x80u && hg < nh && (((hg < 64 ? r0m : r1m) >> (hg & 63u)) & 1u);
                 G[r] = hv ? hg : 0xFFu;
-                T[r] = hv ? ts[i] : 0ull;
-                L[r] = hv ? len[i] : 0u;
+                // (unconditional loads, all in flight — a load under hv waited for the one
+                // before it; a lane not gathering reads element 0, so only the gathered packets'
+                // lines are fetched: the sliding window gathers its sparse heavy sources alone)
+                T[r] = ts[hv ? i : 0u];
+                L[r] = len[hv ? i : 0u];
             }
 #pragma unroll
             for (uint32_t r = 0; r < 16; ++r) {
@@ -271,7 +277,7 @@ __global__ __launch_bounds__(256) void k_heavy_gather(const BatchState *bs, cons
                 base = __shfl(base, (int)lead);
                 wave_lds_order();
                 if (hv) {
-                    const uint32_t pos = offs[(size_t)(lb + h) * tcap + t] + base + (uint32_t)__popcll(peers & lt);
+                    const uint32_t pos = base + (uint32_t)__popcll(peers & lt);
                     out[pos] = ((uint64_t)(lb + h) << shift0) | ((uint64_t)(hs->slot[h] & id_mask) << kIdShift) | i;
                     pout[pos] = ((T[r] - tb) << kPayLenBits) | L[r];
                     if ((peers >> lane) == 1ull) s_cnt[w][h] = base + (uint32_t)__popcll(peers);
