@@ -170,3 +170,25 @@ def test_wide_ids_full_path(native, oracle, max_entries):
     cut = 777_777
     _process_batch_device(native, oracle, [(hdr[:cut], ln[:cut], ts[:cut]), (hdr[cut:], ln[cut:], ts[cut:])],
                           max_entries=max_entries)
+
+
+@pytest.mark.parametrize("limiter", [1, 2], ids=["sliding", "token"])
+@pytest.mark.parametrize("max_entries", [6 << 20, 16 << 20], ids=["ids24", "ids25"])
+def test_wide_ids_limiters(native, oracle, limiter, max_entries):
+    """The sliding window and the token bucket on tables of 2^24 / 2^25 slots (24- / 25-bit
+    source ids: the plain four-pass sort, each pass's digit bytes read by the next pass's tile
+    histogram; DESIGN.md §3 "Wider ids", §8): the config-4 population over two carried
+    batches, verdicts and every map against the oracle."""
+    from flowsentryx_amd import synth
+    p, s = synth.config_params(4)
+    n = 1 << 21
+    hdr, ln, ts = oracle.synth(p, s, 0, n)
+    cfg = dict(limiter=limiter, max_entries=max_entries)
+    if limiter == 2:
+        cfg.update(tb_rate=2000, tb_burst=50)
+    o = oracle.ShardedOracle(THREADS, **cfg)
+    cut = 777_777
+    with native.FsxContext(max_batch=n, **cfg) as c:
+        for a, b in ((0, cut), (cut, n)):
+            _verdicts_equal(c.verdict_batch(hdr[a:b], ln[a:b], ts[a:b]), o.batch(hdr[a:b], ln[a:b], ts[a:b]))
+        _same_state(c, o, (3, 4, 5, 6) if limiter == 2 else (1, 2, 3, 4))
