@@ -497,7 +497,12 @@ hipError_t launch_token_bucket(const uint64_t *S, const uint64_t *ts, const uint
         hipError_t e = hipMemsetAsync(sc.lim_tiles, 0, sc.lim_tiles_n * 4 * 8, st);
         if (e != hipSuccess) return e;
         const uint32_t grid = std::max<uint32_t>(1, (n + kTile - 1) / kTile);   // (>= the valid tiles)
-        k_tb_scan<<<grid, 256, 0, st>>>(S, bs, ts, len, sc.pay[0], sc.headf, sc.tile_aux, seg_j, seg_x,
+        // Unused dynamic LDS caps the blocks in flight at three per CU (four fit the VGPRs): a
+        // tile's look-back walks back over the tiles still in flight, and fewer of them beside
+        // the front measured 3.85-3.96 vs 3.92-3.93 ms per step (two per CU 4.02-4.05, one
+        // 4.52; profiles/r06/ab_r06ts*). FSX_TB_SCAN_LDS=<bytes> overrides (0: uncapped).
+        static const uint32_t scan_lds = getenv("FSX_TB_SCAN_LDS") ? (uint32_t)atoi(getenv("FSX_TB_SCAN_LDS")) : 42000u;
+        k_tb_scan<<<grid, 256, scan_lds, st>>>(S, bs, ts, len, sc.pay[0], sc.headf, sc.tile_aux, seg_j, seg_x,
                                         sc.seg_slot, table, lim, tile_map, status, ticket, sc.marks, light_only);
         mark("k_tb_scan");
         return hipGetLastError();
