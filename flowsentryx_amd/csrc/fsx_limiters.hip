@@ -1846,7 +1846,10 @@ hipError_t launch_sliding_window(const uint64_t *S, const uint64_t *ts, const ui
         // tile_cnt[0]); the last tile writes the total
         if ((e = hipMemsetAsync(hb.tile_off, 0, ntiles * 8, st)) != hipSuccess) return e;
         if ((e = hipMemsetAsync(hb.tile_cnt, 0, 4, st)) != hipSuccess) return e;
-        k_sw_hist<2><<<(uint32_t)ntiles, 256, 0, st>>>(S, bs, tstate, ts, len, sc.pay[0], table, lim, hb, sc.sw_seg);
+        // (A/B: FSX_SW_HIST_LDS bytes of unused dynamic LDS per block cap the blocks in flight,
+        // hence the look-back's depth, as for k_tb_scan)
+        static const uint32_t hist_lds = getenv("FSX_SW_HIST_LDS") ? (uint32_t)atoi(getenv("FSX_SW_HIST_LDS")) : 0u;
+        k_sw_hist<2><<<(uint32_t)ntiles, 256, hist_lds, st>>>(S, bs, tstate, ts, len, sc.pay[0], table, lim, hb, sc.sw_seg);
     } else {
         k_sw_hist<0><<<grid, 256, 0, st>>>(S, bs, tstate, ts, len, sc.pay[0], table, lim, hb, sc.sw_seg);
         k_sw_hist_scan<<<1, 1024, 0, st>>>(bs, hb.tile_cnt, hb.tile_off, ntiles, hb.total);
