@@ -3741,7 +3741,10 @@ hipError_t launch_tail(const TailArgs &a) {
                                                                   table, lim, hlists, skeys);
             mark_on("k_walk_fixed_long", fork3 ? 2 : 0);
             if (fork3 && (e = hipEventRecord(walk_join_ev, st3)) != hipSuccess) return e;
-            k_walk_fixed<<<std::min<uint32_t>(FSX_WALK_SHORT_BLOCKS, cdiv(n, 256)), 256, 0, st>>>(S, bs, sc.seg_start, sc.seg_slot, ts, len, sc.pay[0],
+            // (A/B: FSX_WALK_LDS bytes of unused dynamic LDS per block cap the thread walker's
+            // blocks per CU beside the next batch's front)
+            static const uint32_t walk_lds = getenv("FSX_WALK_LDS") ? (uint32_t)atoi(getenv("FSX_WALK_LDS")) : 0u;
+            k_walk_fixed<<<std::min<uint32_t>(FSX_WALK_SHORT_BLOCKS, cdiv(n, 256)), 256, walk_lds, st>>>(S, bs, sc.seg_start, sc.seg_slot, ts, len, sc.pay[0],
                                                      sc.seg_order, cls, sc.marks, table, lim, hlists, skeys);
             mark("k_walk_fixed");
             if (fork3 && (e = hipStreamWaitEvent(st, walk_join_ev, 0)) != hipSuccess) return e;
