@@ -245,14 +245,15 @@ static int alloc_scratch(fsx_ctx *c, uint64_t cap) {
     HIPCHK(c, hipMalloc(&s.pay[0], cap * 8));
     HIPCHK(c, hipMalloc(&s.pay[1], cap * 8));
     HIPCHK(c, hipMalloc(&s.marks, cap + 16));
-    HIPCHK(c, hipMalloc(&s.dig, cap + 16));
+    HIPCHK(c, hipMalloc(&s.dig, 2 * cap + 32));   // (16-bit words for 9-bit digits)
     HIPCHK(c, hipMalloc(&s.headf, cap + 16));
     HIPCHK(c, hipMalloc(&s.seg_start, (cap + 1) * 4));
     HIPCHK(c, hipMalloc(&s.seg_slot, cap * 4));
     HIPCHK(c, hipMalloc(&s.seg_lo, (cap + 1) * 4));
     HIPCHK(c, hipMalloc(&s.seg_len, (cap + 1) * 4));
-    // (two regions of 256 rows: pass 0's and the light passes', launch_verdict_pipeline)
-    HIPCHK(c, hipMalloc(&s.hist, 256ull * std::max<uint64_t>(kSortMaxBlocks, 2 * (cap / kSortTile + 2)) * 4));
+    // (two regions: pass 0's 256 rows and the light passes' 512 — 9-bit digits —,
+    // launch_verdict_pipeline)
+    HIPCHK(c, hipMalloc(&s.hist, 256ull * std::max<uint64_t>(kSortMaxBlocks, 3 * (cap / kSortTile + 2)) * 4));
     HIPCHK(c, hipMalloc(&s.tile_aux, ntiles * 4));
     HIPCHK(c, hipMalloc(&s.tile_last, ntiles));
     // (s.id_tab, the per-batch id table of flow-only batches, is allocated on first use:
@@ -265,7 +266,7 @@ static int alloc_scratch(fsx_ctx *c, uint64_t cap) {
     HIPCHK(c, hipMalloc(&s.flow_last, (cap / 1024 + 8) * flow_acc_bytes()));
     HIPCHK(c, hipMalloc(&s.span_list, (cap / 1024 + 8) * 4));
     HIPCHK(c, hipMalloc(&s.sort_ctl, kSortCtlWords * 4));
-    HIPCHK(c, hipMalloc(&s.gbase, 1024 * 4));
+    HIPCHK(c, hipMalloc(&s.gbase, 1536 * 4));   // (+ the 9-bit passes' 512 bases)
     HIPCHK(c, hipMalloc(&s.status, (cap / kSortTile + 2) * 256 * 8));
     HIPCHK(c, hipMemset(s.status, 0, (cap / kSortTile + 2) * 256 * 8));
     s.lim_tiles_n = cap / kTile + 2;
@@ -700,9 +701,9 @@ int fsx_set_pipeline(fsx_ctx *c, int on) {
                 if ((e = hipMalloc(&f.packed[b], cap * 8)) != hipSuccess) return e;
                 if ((e = hipMalloc(&f.pay[b], cap * 8)) != hipSuccess) return e;
             }
-            if ((e = hipMalloc(&f.hist, 256ull * std::max<uint64_t>(kSortMaxBlocks, 2 * (cap / kSortTile + 2)) * 4)) != hipSuccess) return e;
+            if ((e = hipMalloc(&f.hist, 256ull * std::max<uint64_t>(kSortMaxBlocks, 3 * (cap / kSortTile + 2)) * 4)) != hipSuccess) return e;
             if ((e = hipMalloc(&f.sort_ctl, kSortCtlWords * 4)) != hipSuccess) return e;
-            if ((e = hipMalloc(&f.gbase, 1024 * 4)) != hipSuccess) return e;
+            if ((e = hipMalloc(&f.gbase, 1536 * 4)) != hipSuccess) return e;
             if ((e = hipMalloc(&f.heavy, sizeof(HeavySet))) != hipSuccess) return e;
             if ((e = hipMemset(f.heavy, 0, sizeof(HeavySet))) != hipSuccess) return e;
             if ((e = hipMalloc(&f.chunk_cnt, chunk_cnt_bytes(cap))) != hipSuccess) return e;

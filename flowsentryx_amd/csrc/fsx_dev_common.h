@@ -104,10 +104,11 @@ __device__ __forceinline__ uint64_t uni64(uint64_t x) {
            (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(x >> 32)) << 32;
 }
 
+template <int kBits = 8>
 __device__ __forceinline__ uint64_t match_digit(uint32_t d, uint64_t active) {
     uint64_t peers = active;
 #pragma unroll
-    for (int b = 0; b < 8; ++b) {
+    for (int b = 0; b < kBits; ++b) {
         const bool bit = (d >> b) & 1u;
         const uint64_t bal = __ballot(bit);
         peers &= bit ? bal : ~bal;

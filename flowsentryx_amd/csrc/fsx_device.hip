@@ -160,6 +160,8 @@ struct DigitPlan {
     uint32_t shift[4], mask[4];
     uint32_t npass;
     uint32_t light_b;   // heavy sort: buckets below light_b are light (id digit 0); 0 = plain
+    uint32_t nhist;     // digits k_parse counts (the 9-bit light passes take their bases from
+                        // the tile scan: k_digit_base)
 };
 
 // parse_ethhdr / parse_ip6hdr / parse_ip4hdr (src/parsing_helper.h:49-136, dispatch
@@ -668,7 +670,7 @@ __global__ __launch_bounds__(256, FSX_PARSE_MINB) void k_parse(PacketIn in,
         const uint32_t d0 = (uint32_t)(out >> dp.shift[0]) & dp.mask[0];
         atomicAdd(&s_t0[d0], 1u);   // (the block's digit-0 totals from s_t0 per sort tile)
         if (hidx < 0)   // heavy entries are final after pass 0
-            for (uint32_t dg = 1; dg < dp.npass; ++dg)
+            for (uint32_t dg = 1; dg < dp.nhist; ++dg)
                 atomicAdd(&s_hist[dg][(uint32_t)(out >> dp.shift[dg]) & dp.mask[dg]], 1u);
     };
     auto word_of = [&](uint32_t id, uint32_t tag, uint32_t i, int hidx) -> uint64_t {
@@ -1083,12 +1085,16 @@ __device__ __forceinline__ bool sort_item(uint32_t i, uint32_t end, int first, u
 
 // Per-tile digit counts (one block per tile; per-wave LDS counters).
 // din (passes >= 1): the digits the previous pass's scatter wrote, one byte per position —
-// 4 KiB per tile read instead of 32 KiB of keys.
+// 4 KiB per tile read instead of 32 KiB of keys (kDig = 512, the 9-bit light passes: one
+// 16-bit word per position, 8 KiB per tile).
+template <int kDig>
 __global__ __launch_bounds__(256) void k_tile_hist(const uint64_t *__restrict__ in, uint32_t L_host,
                                                    const uint32_t *L_dev, uint32_t shift, uint32_t dmask,
                                                    int first, uint32_t *__restrict__ thist, uint32_t tcap,
-                                                   const uint8_t *__restrict__ din) {
-    __shared__ uint32_t sh[4][256];
+                                                   const void *__restrict__ din) {
+    static_assert(kDig == 256 || kDig == 512, "8- or 9-bit digits");
+    constexpr int kPer = kDig / 256;   // digits per thread
+    __shared__ uint32_t sh[4][kDig];
     const uint32_t tid = threadIdx.x, w = tid >> 6;
     const uint32_t L = L_dev ? *L_dev : L_host;
     const uint32_t nact = (L + kSortTile - 1) / kSortTile;   // tiles of this pass
@@ -1096,25 +1102,46 @@ __global__ __launch_bounds__(256) void k_tile_hist(const uint64_t *__restrict__ 
     // (XCD-aware order: neighbouring tiles' counts share the lines of each digit row)
     const uint32_t t = xcd_swizzle(blockIdx.x, nact);
 #pragma unroll
-    for (int k = 0; k < 4; ++k) sh[k][tid] = 0;
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int q = 0; q < kPer; ++q) sh[k][tid + 256 * q] = 0;
     __syncthreads();
     const uint32_t t0 = t * kSortTile, end = min(L, t0 + kSortTile);
     const uint32_t lane = lane_id();
+    auto store_rows = [&]() {   // digit-major rows (only the dmask + 1 live digits)
+#pragma unroll
+        for (int q = 0; q < kPer; ++q) {
+            const uint32_t d = tid + 256u * (uint32_t)q;
+            if (d <= dmask) thist[(size_t)d * tcap + t] = sh[0][d] + sh[1][d] + sh[2][d] + sh[3][d];
+        }
+    };
     if (din) {   // thread x: positions t0 + 16x .. t0 + 16x + 15
-        static_assert(kSortTile == 16 * 256, "16 digit bytes per thread");
+        static_assert(kSortTile == 16 * 256, "16 digits per thread");
         const uint32_t p0 = t0 + 16u * tid;
-        uint32_t wd[4] = {0, 0, 0, 0};
+        constexpr uint32_t kW = kDig == 256 ? 4 : 8;   // 32-bit words of the thread's 16 digits
+        constexpr uint32_t kB = kDig == 256 ? 8 : 16;  // bits per digit slot
+        uint32_t wd[kW];
+#pragma unroll
+        for (uint32_t k = 0; k < kW; ++k) wd[k] = 0;
         if (p0 + 16u <= end) {
-            const uint4 x = *reinterpret_cast<const uint4 *>(din + p0);
-            wd[0] = x.x; wd[1] = x.y; wd[2] = x.z; wd[3] = x.w;
+            const uint4 *src = reinterpret_cast<const uint4 *>(static_cast<const uint8_t *>(din) + (size_t)p0 * (kB / 8));
+#pragma unroll
+            for (uint32_t k = 0; k < kW / 4; ++k) {
+                const uint4 x = src[k];
+                wd[4 * k] = x.x; wd[4 * k + 1] = x.y; wd[4 * k + 2] = x.z; wd[4 * k + 3] = x.w;
+            }
         } else {
             for (uint32_t k = 0; k < 16; ++k)
-                if (p0 + k < end) wd[k >> 2] |= (uint32_t)din[p0 + k] << (8 * (k & 3));
+                if (p0 + k < end) {
+                    const uint32_t x = kDig == 256 ? (uint32_t)static_cast<const uint8_t *>(din)[p0 + k]
+                                                   : (uint32_t)static_cast<const uint16_t *>(din)[p0 + k];
+                    wd[k * kB / 32] |= x << ((k * kB) & 31);
+                }
         }
 #pragma unroll
         for (uint32_t k = 0; k < 16; ++k) {
             const bool ok = p0 + k < end;
-            const uint32_t d = (wd[k >> 2] >> (8 * (k & 3))) & dmask;
+            const uint32_t d = (wd[k * kB / 32] >> ((k * kB) & 31)) & dmask;
             const uint64_t act = __ballot(ok);
             if (!act) continue;
             const int lead = __ffsll((unsigned long long)act) - 1;
@@ -1126,7 +1153,7 @@ __global__ __launch_bounds__(256) void k_tile_hist(const uint64_t *__restrict__ 
             }
         }
         __syncthreads();
-        if (tid <= dmask) thist[(size_t)tid * tcap + t] = sh[0][tid] + sh[1][tid] + sh[2][tid] + sh[3][tid];
+        store_rows();
         return;
     }
     // 16-byte loads: thread x holds keys 2(256 r + x) and 2(256 r + x) + 1 (the order of
@@ -1160,8 +1187,7 @@ __global__ __launch_bounds__(256) void k_tile_hist(const uint64_t *__restrict__ 
         }
     }
     __syncthreads();
-    // digit-major rows (one partial line per count: only the dmask + 1 live digits)
-    if (tid <= dmask) thist[(size_t)tid * tcap + t] = sh[0][tid] + sh[1][tid] + sh[2][tid] + sh[3][tid];
+    store_rows();   // (one partial line per count)
 }
 
 // Block d: offs[d][t] = base[d] + sum of thist[d][t'] over t' < t (in place), in chunks of
@@ -1172,14 +1198,18 @@ __global__ __launch_bounds__(256) void k_tile_hist(const uint64_t *__restrict__ 
 #ifndef FSX_TILE_SCAN_WIDE
 #define FSX_TILE_SCAN_WIDE 1   // 0: round 4's chunks of 1024 tiles, 4 per thread (A/B)
 #endif
+// gbase == nullptr (the 9-bit light passes, whose digit totals k_parse does not count): the
+// rows are scanned from 0 and each digit's total goes to tot[d] (k_digit_base turns those
+// into the bases the scatter adds).
 __global__ __launch_bounds__(256) void k_tile_scan(uint32_t *__restrict__ thist, uint32_t tcap,
                                                    uint32_t L_host, const uint32_t *L_dev,
-                                                   const uint32_t *__restrict__ gbase) {
+                                                   const uint32_t *__restrict__ gbase,
+                                                   uint32_t *__restrict__ tot_out = nullptr) {
     __shared__ uint32_t s_tmp[4];
     const uint32_t L = L_dev ? *L_dev : L_host;
     const uint32_t ntiles = (L + kSortTile - 1) / kSortTile;
     uint32_t *row = thist + (size_t)blockIdx.x * tcap;
-    uint32_t carry = gbase[blockIdx.x];
+    uint32_t carry = gbase ? gbase[blockIdx.x] : 0u;
     const uint32_t tid = threadIdx.x;
 #if FSX_TILE_SCAN_WIDE
     __shared__ uint32_t s_x[4096 + 256];   // tile e of the chunk at e + e / 16
@@ -1226,26 +1256,41 @@ __global__ __launch_bounds__(256) void k_tile_scan(uint32_t *__restrict__ thist,
         carry += tot;
     }
 #endif
+    if (tot_out && tid == 0) tot_out[blockIdx.x] = carry;
+}
+
+// The 9-bit light passes' digit bases: exclusive scan of the 512 digit totals k_tile_scan
+// left in tot (in place; thread x: digits 2x, 2x + 1).
+__global__ __launch_bounds__(256) void k_digit_base(uint32_t *__restrict__ tot) {
+    __shared__ uint32_t s_tmp[4];
+    const uint32_t a = tot[2 * threadIdx.x], b = tot[2 * threadIdx.x + 1];
+    const uint32_t x = block256_excl(a + b, s_tmp, nullptr);
+    tot[2 * threadIdx.x] = x;
+    tot[2 * threadIdx.x + 1] = x + a;
 }
 
 // One tile: stable rank, global bases from offs(d, tile count of d), LDS-sorted
-// tile, runs to the buckets; payload words through the same LDS slots.
-template <bool kLatePay, class Offs>
+// tile, runs to the buckets; payload words through the same LDS slots. kDig: 256 (8-bit
+// digits) or 512 (the 9-bit light passes of 24- / 25-bit ids); dwide: the next pass's
+// digit goes to dout as a 16-bit word (a 9-bit next digit), else a byte.
+template <bool kLatePay, class Offs, int kDig = 256>
 __device__ __forceinline__ void sort_tile(uint32_t t, const uint64_t *__restrict__ in,
                                           uint64_t *__restrict__ out, uint32_t L, uint32_t shift,
                                           uint32_t dmask, int first, const BatchState *bs,
                                           const uint64_t *__restrict__ pin, uint64_t *__restrict__ pout,
                                           const uint64_t *__restrict__ ts,
                                           const uint32_t *__restrict__ len, Offs offs,
-                                          uint8_t *__restrict__ dout = nullptr, uint32_t nshift = 0,
-                                          uint32_t nmask = 0) {
+                                          void *__restrict__ dout = nullptr, uint32_t nshift = 0,
+                                          uint32_t nmask = 0, bool dwide = false) {
+    static_assert(kDig == 256 || kDig == 512, "8- or 9-bit digits");
+    constexpr int kPer = kDig / 256;   // digits per thread
     __shared__ unsigned long long s_el[kSortTile];
-    __shared__ uint32_t s_wc[4][256];
-    __shared__ uint32_t s_dst[256], s_tbase[256], s_tcnt[256];
+    __shared__ uint32_t s_wc[4][kDig];
+    __shared__ uint32_t s_dst[kDig], s_tbase[kDig], s_tcnt[kDig];
     __shared__ uint32_t s_tmp[4];
     const uint32_t tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) s_wc[w][lane * 4 + k] = 0;
+    for (int k = 0; k < 4 * kPer; ++k) s_wc[w][lane * 4 * kPer + k] = 0;
     __syncthreads();
     FSX_STAMP(t, 0);
     const uint32_t t0 = t * kSortTile;
@@ -1287,7 +1332,7 @@ __device__ __forceinline__ void sort_tile(uint32_t t, const uint64_t *__restrict
         const uint32_t d = (uint32_t)(v[r] >> shift) & dmask;
         const int lead0 = act ? __ffsll((unsigned long long)act) - 1 : 0;
         const uint32_t dl = __shfl(d, lead0);
-        const uint64_t peers = __ballot(valid && d == dl) == act ? act : match_digit(d, act);
+        const uint64_t peers = __ballot(valid && d == dl) == act ? act : match_digit<kDig == 256 ? 8 : 9>(d, act);
         const uint32_t below = (uint32_t)__popcll(peers & lt_mask);
         uint32_t base = 0;
         if (valid && below == 0) base = atomicAdd(&s_wc[w][d], (uint32_t)__popcll(peers));
@@ -1296,15 +1341,29 @@ __device__ __forceinline__ void sort_tile(uint32_t t, const uint64_t *__restrict
     }
     __syncthreads();
     FSX_STAMP(t, 1);
-    const uint32_t d = tid;
-    const uint32_t c0 = s_wc[0][d], c1 = s_wc[1][d], c2 = s_wc[2][d], c3 = s_wc[3][d];
-    const uint32_t tc = c0 + c1 + c2 + c3;
-    s_dst[d] = d <= dmask ? offs(d, tc) : 0u;   // rows of dead digits are never written
+    // thread x owns digits kPer * x .. kPer * x + kPer - 1 (consecutive: one block scan)
+    uint32_t c[kPer][4], tc[kPer];
+#pragma unroll
+    for (int q = 0; q < kPer; ++q) {
+        const uint32_t d = kPer * tid + q;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) c[q][k] = s_wc[k][d];
+        tc[q] = c[q][0] + c[q][1] + c[q][2] + c[q][3];
+        s_dst[d] = d <= dmask ? offs(d, tc[q]) : 0u;   // rows of dead digits are never written
+    }
     __syncthreads();
     FSX_STAMP(t, 2);
-    s_wc[0][d] = 0; s_wc[1][d] = c0; s_wc[2][d] = c0 + c1; s_wc[3][d] = c0 + c1 + c2;
-    s_tcnt[d] = tc;
-    s_tbase[d] = block256_excl(tc, s_tmp, nullptr);
+    uint32_t tsum = 0;
+#pragma unroll
+    for (int q = 0; q < kPer; ++q) {
+        const uint32_t d = kPer * tid + q;
+        s_wc[0][d] = 0; s_wc[1][d] = c[q][0]; s_wc[2][d] = c[q][0] + c[q][1]; s_wc[3][d] = c[q][0] + c[q][1] + c[q][2];
+        s_tcnt[d] = tc[q];
+        tsum += tc[q];
+    }
+    uint32_t tb = block256_excl(tsum, s_tmp, nullptr);
+#pragma unroll
+    for (int q = 0; q < kPer; ++q) { s_tbase[kPer * tid + q] = tb; tb += tc[q]; }
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < kSortItems; ++r) {
@@ -1316,7 +1375,7 @@ __device__ __forceinline__ void sort_tile(uint32_t t, const uint64_t *__restrict
     }
     __syncthreads();
     FSX_STAMP(t, 3);
-    const uint32_t T = s_tbase[255] + s_tcnt[255];
+    const uint32_t T = s_tbase[kDig - 1] + s_tcnt[kDig - 1];
     uint32_t dst[kSortItems];
 #pragma unroll
     for (int m = 0; m < kSortItems; ++m) {
@@ -1326,7 +1385,11 @@ __device__ __forceinline__ void sort_tile(uint32_t t, const uint64_t *__restrict
             const uint32_t dd = (uint32_t)(x >> shift) & dmask;
             dst[m] = s_dst[dd] + (j - s_tbase[dd]);
             out[dst[m]] = x;
-            if (dout) dout[dst[m]] = (uint8_t)((x >> nshift) & nmask);   // (the next pass's digit)
+            if (dout) {   // (the next pass's digit)
+                const uint32_t nd = (uint32_t)(x >> nshift) & nmask;
+                if (dwide) static_cast<uint16_t *>(dout)[dst[m]] = (uint16_t)nd;
+                else static_cast<uint8_t *>(dout)[dst[m]] = (uint8_t)nd;
+            }
         }
     }
     FSX_STAMP(t, 4);
@@ -1357,8 +1420,16 @@ struct TileOffs {
         return offs[(size_t)d * tcap + t];
     }
 };
+// (the 9-bit plan's light passes: rows scanned from 0, the digit bases from k_digit_base)
+struct TileOffsB {
+    const uint32_t *offs, *base;
+    uint32_t tcap, t;
+    __device__ __forceinline__ uint32_t operator()(uint32_t d, uint32_t) const {
+        return base[d] + offs[(size_t)d * tcap + t];
+    }
+};
 
-template <bool kLatePay>
+template <bool kLatePay, int kDig = 256, bool kBase = false>
 __global__ __launch_bounds__(256, kLatePay ? FSX_SCATTER_MINB : 1) void k_tile_scatter(const uint64_t *__restrict__ in,
                                                       uint64_t *__restrict__ out, uint32_t L_host,
                                                       const uint32_t *L_dev, uint32_t shift, uint32_t dmask,
@@ -1369,14 +1440,19 @@ __global__ __launch_bounds__(256, kLatePay ? FSX_SCATTER_MINB : 1) void k_tile_s
                                                       uint64_t *__restrict__ pout,
                                                       const uint64_t *__restrict__ ts,
                                                       const uint32_t *__restrict__ len,
-                                                      uint8_t *__restrict__ dout, uint32_t nshift,
-                                                      uint32_t nmask) {
+                                                      void *__restrict__ dout, uint32_t nshift,
+                                                      uint32_t nmask, const uint32_t *__restrict__ dbase,
+                                                      int dwide) {
     const uint32_t L = L_dev ? *L_dev : L_host;
     const uint32_t nact = (L + kSortTile - 1) / kSortTile;   // tiles of this pass
     if (blockIdx.x >= nact) return;
     const uint32_t t = xcd_swizzle(blockIdx.x, nact);
-    sort_tile<kLatePay>(t, in, out, L, shift, dmask, first, bs, pin, pout, ts, len, TileOffs{offs, tcap, t},
-                        dout, nshift, nmask);
+    if constexpr (kBase)
+        sort_tile<kLatePay, TileOffsB, kDig>(t, in, out, L, shift, dmask, first, bs, pin, pout, ts, len,
+                                             TileOffsB{offs, dbase, tcap, t}, dout, nshift, nmask, dwide != 0);
+    else
+        sort_tile<kLatePay, TileOffs, kDig>(t, in, out, L, shift, dmask, first, bs, pin, pout, ts, len,
+                                            TileOffs{offs, tcap, t}, dout, nshift, nmask, dwide != 0);
 }
 
 // ---- pass 0 with the heavy sources outside the sort (k_parse<..., kHf>; fsx_heavy.hip).
@@ -1420,8 +1496,8 @@ __global__ __launch_bounds__(256, FSX_PASS0H_MINB) void k_pass0h(const uint64_t 
                                                                   HeavyTileRec *__restrict__ rec,
                                                                   const HeavySet *__restrict__ hs,
                                                                   const uint64_t *__restrict__ pin,
-                                                                  uint8_t *__restrict__ dout, uint32_t nshift,
-                                                                  uint32_t nmask) {
+                                                                  void *__restrict__ dout, uint32_t nshift,
+                                                                  uint32_t nmask, int dwide) {
     __shared__ unsigned long long s_el[kSortTile];
     __shared__ uint32_t s_wc[4][256];
     __shared__ uint32_t s_dst[256], s_tbase[256], s_tcnt[256];
@@ -1640,7 +1716,11 @@ __global__ __launch_bounds__(256, FSX_PASS0H_MINB) void k_pass0h(const uint64_t 
             const uint32_t dd = (uint32_t)((x & ~kFreshBit) >> shift) & dmask;
             dst[m] = s_dst[dd] + (j - s_tbase[dd]);
             out[dst[m]] = x;
-            if (dout) dout[dst[m]] = (uint8_t)(((x & ~kFreshBit) >> nshift) & nmask);   // (pass 1's digit)
+            if (dout) {   // (pass 1's digit: a byte, or a 16-bit word for a 9-bit digit)
+                const uint32_t nd = (uint32_t)((x & ~kFreshBit) >> nshift) & nmask;
+                if (dwide) static_cast<uint16_t *>(dout)[dst[m]] = (uint16_t)nd;
+                else static_cast<uint8_t *>(dout)[dst[m]] = (uint8_t)nd;
+            }
         }
     }
     if constexpr (kRecs && FSX_PASS0H_GATHER) {   // (A/B: gathered by arrival index)
@@ -1671,16 +1751,16 @@ hipError_t launch_pass0h(const uint64_t *in, uint64_t *out, uint32_t n, uint32_t
                          const uint32_t *offs, uint32_t tcap, BatchState *bs, uint64_t *pout, const uint64_t *ts,
                          const uint32_t *len, const uint8_t *tags, const uint32_t *chunk_cnt,
                          const uint64_t *lmask, void *rec, const HeavySet *hs, const uint64_t *pin, hipStream_t st,
-                         uint8_t *dout, uint32_t nshift, uint32_t nmask) {
+                         void *dout, uint32_t nshift, uint32_t nmask, int dwide) {
     const uint32_t ntiles = std::max<uint32_t>(1, (n + kSortTile - 1) / kSortTile);
     if (pin)   // (FSX_PARSE_PAY: the clock facts and payload words came from k_parse)
         k_pass0h<false><<<ntiles, 256, 0, st>>>(in, out, n, shift, dmask, offs, tcap, bs, pout, ts, len, tags,
                                                 chunk_cnt, lmask, static_cast<HeavyTileRec *>(rec), hs, pin,
-                                                dout, nshift, nmask);
+                                                dout, nshift, nmask, dwide);
     else
         k_pass0h<true><<<ntiles, 256, 0, st>>>(in, out, n, shift, dmask, offs, tcap, bs, pout, ts, len, tags,
                                                chunk_cnt, lmask, static_cast<HeavyTileRec *>(rec), hs, nullptr,
-                                               dout, nshift, nmask);
+                                               dout, nshift, nmask, dwide);
     return hipGetLastError();
 }
 
@@ -3872,7 +3952,13 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
     const uint32_t bshift = std::max<uint32_t>(56, kIdShift + idbits);
     const uint32_t lbits = 63 - bshift;                 // light digit bits of the bucket
     const uint32_t hrest = idbits > lbits ? idbits - lbits : 0;
-    const int hpass = 1 + (int)((hrest + 7) / 8);       // pass 0 + the light passes
+    // 24- / 25-bit ids (17 / 18 light bits after pass 0's 7): two light passes of 9-bit digits
+    // (512-digit tiles, bases from the tile scan: k_digit_base) instead of three of 6 bits —
+    // with the fixed window's heavy lists (the other limiters keep the plain 4-pass sort).
+    // FSX_SORT_LIGHT6=1: the three 6-bit passes (A/B)
+    static const bool light6 = getenv("FSX_SORT_LIGHT6") != nullptr;
+    const bool wide9 = lists_ok && !light6 && hrest > 16 && hrest <= 18;
+    const int hpass = 1 + (wide9 ? 2 : (int)((hrest + 7) / 8));   // pass 0 + the light passes
     const bool heavy_sort = !admit && !onesweep && !full_digits && !no_heavy && idbits <= 25 && npass >= 3 &&
                             (hpass == 3 || (hpass == 4 && lists_ok));
     if (heavy_sort) npass = hpass;   // (24-bit ids: 4 passes instead of 3, 3 of them over the light entries)
@@ -3904,6 +3990,8 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
     if (!(split && split->tail) && (e = hipMemsetAsync(sc.marks, 0, n, st)) != hipSuccess) return e;
     DigitPlan dp{};
     dp.npass = (uint32_t)npass;
+    const bool wide_plan = heavy_sort && wide9;   // (light passes: bases from the tile scan)
+    dp.nhist = wide_plan ? 1u : (uint32_t)npass;
     uint32_t nheavy = kHeavyMax;
     if (heavy_sort) {
         dp.light_b = 1u << lbits;
@@ -4030,6 +4118,11 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
         uint8_t *dout = dig_on && pass + 1 < npass ? sc.dig : nullptr;
         const uint32_t nshift = pass + 1 < npass ? dp.shift[pass + 1] : 0u;
         const uint32_t nmask = pass + 1 < npass ? dp.mask[pass + 1] : 0u;
+        // the 9-bit plan's light passes: 512-digit tiles, 16-bit digit words, bases from the
+        // tile scan's row totals (k_parse counted pass 0's digits only)
+        const bool kwide = pmask > 255u, nwide = nmask > 255u;
+        const bool tbase = wide_plan && pass > 0;
+        uint32_t *dbase = sc.gbase + 1024;
         if (onesweep) {
             const uint32_t *Ld = pass == 0 ? nullptr : &bs->n_valid;
             k_onesweep<kLookW><<<ntiles, 256, 0, st>>>(in, out, n, Ld, shift, pmask, sc.gbase + 256 * pass,
@@ -4043,24 +4136,39 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
             // is odd, in packed[0] when it is even)
             const uint32_t *Ld = pass == 0 ? nullptr : &bs->n_light;
             if (pass > 0) {   // pass 0's per-tile counts come from k_parse
-                k_tile_hist<<<ntiles, 256, 0, st>>>(in, n, Ld, shift, pmask, pass == 0, hst, tcap,
-                                                    dig_on ? sc.dig : nullptr);
+                if (kwide)
+                    k_tile_hist<512><<<ntiles, 256, 0, st>>>(in, n, Ld, shift, pmask, pass == 0, hst, tcap,
+                                                             dig_on ? sc.dig : nullptr);
+                else
+                    k_tile_hist<256><<<ntiles, 256, 0, st>>>(in, n, Ld, shift, pmask, pass == 0, hst, tcap,
+                                                             dig_on ? sc.dig : nullptr);
                 mark("k_tile_hist");
             }
-            k_tile_scan<<<pmask + 1, 256, 0, st>>>(hst, tcap, n, Ld, sc.gbase + 256 * pass);
+            if (tbase) {
+                k_tile_scan<<<pmask + 1, 256, 0, st>>>(hst, tcap, n, Ld, nullptr, dbase);
+                k_digit_base<<<1, 256, 0, st>>>(dbase);
+            } else {
+                k_tile_scan<<<pmask + 1, 256, 0, st>>>(hst, tcap, n, Ld, sc.gbase + 256 * pass);
+            }
             mark("k_tile_scan");
             if (pass == 0 && (e = tail_hook(1)) != hipSuccess) return e;
             if (pass == 0 && hfm) {   // light words from the parse chunks; heavy tile sums; the path
                 if ((e = launch_pass0h(in, out, n, shift, pmask, sc.hist, tcap, bs, pout, ts, len, verdict,
                                        sc.chunk_cnt, light_masks(sc.chunk_cnt, sc.cap), sc.hrec, sc.heavy,
-                                       FSX_PARSE_PAY ? sc.pay[0] : nullptr, st, dout, nshift, nmask)) != hipSuccess)
+                                       FSX_PARSE_PAY ? sc.pay[0] : nullptr, st, dout, nshift, nmask,
+                                       nwide ? 1 : 0)) != hipSuccess)
                     return e;
                 mark("k_pass0h");
                 if ((e = launch_hmode(bs, ts, n, lim, st)) != hipSuccess) return e;
                 mark("k_hmode");
             } else {
-                k_tile_scatter<kLatePayDefault><<<ntiles, 256, 0, st>>>(in, out, n, Ld, shift, pmask, pass == 0, hst, tcap, bs,
-                                                       pin, pout, ts, len, dout, nshift, nmask);
+#define FSX_SCATTER(D, B) k_tile_scatter<kLatePayDefault, D, B><<<ntiles, 256, 0, st>>>( \
+                    in, out, n, Ld, shift, pmask, pass == 0, hst, tcap, bs, pin, pout, ts, len, dout, nshift, nmask, \
+                    dbase, nwide ? 1 : 0)
+                if (!tbase) FSX_SCATTER(256, false);
+                else if (!kwide) FSX_SCATTER(256, true);
+                else FSX_SCATTER(512, true);
+#undef FSX_SCATTER
                 mark("k_tile_scatter");
             }
             if (pass == 0 && (e = tail_hook(2)) != hipSuccess) return e;

@@ -667,7 +667,7 @@ hipError_t launch_pass0h(const uint64_t *in, uint64_t *out, uint32_t n, uint32_t
                          const uint32_t *len, const uint8_t *tags, const uint32_t *chunk_cnt,
                          const uint64_t *lmask, void *rec,
                          const HeavySet *hs, const uint64_t *pin, hipStream_t st,
-                         uint8_t *dout = nullptr, uint32_t nshift = 0, uint32_t nmask = 0);
+                         void *dout = nullptr, uint32_t nshift = 0, uint32_t nmask = 0, int dwide = 0);
 hipError_t launch_hmode(BatchState *bs, const uint64_t *ts, uint32_t n, const Limits &lim, hipStream_t st);
 // (FSX_PARSE_PAY: every sort tile's HeavyTileRec, at the start of the tail)
 hipError_t launch_heavy_recs(const BatchState *bs, const uint64_t *ts, const uint32_t *len, const uint8_t *tags,
