@@ -86,7 +86,8 @@ def test_config2_stream_all_limiters(native, oracle, limiter):
 def test_config4_share_16m_population(native, oracle):
     """BASELINE config 4's source population (16M Zipf(1.1) sources, 1B packets over 120 s):
     the first 8M packets of the stream, max_entries = 16M (a 2^25-slot table: 25-bit source
-    ids, the 4-pass heavy-source sort with an 8-bit first bucket and 128 heavy sources),
+    ids, the heavy-source sort with an 8-bit first bucket, 128 heavy sources and two 9-bit light
+    passes),
     fixed window with state carried."""
     from flowsentryx_amd import synth
     p, s = synth.config_params(4)
@@ -159,10 +160,11 @@ def test_flow_features_sources_of_many_tiles(native, oracle):
 
 @pytest.mark.parametrize("max_entries", [6 << 20, 16 << 20], ids=["ids24", "ids25"])
 def test_wide_ids_full_path(native, oracle, max_entries):
-    """Tables of 2^24 / 2^25 slots take the 4-pass heavy-source sort (pass 0
-    into the other buffer, three light passes ending in the parse buffer, the heavy runs
-    read from pass 0's buffer): verdicts, features and q8 scores of two carried batches of
-    the config-4 population against the oracle."""
+    """Tables of 2^24 / 2^25 slots take the 3-pass heavy-source sort (DESIGN.md §3 "Two 9-bit
+    light passes": pass 0's 8-bit bucket, then two light passes of 9 + 8 / 9 + 9 bits with
+    512-digit tiles, 16-bit digit words and the digit bases from the tile scan): verdicts,
+    features and q8 scores of two carried batches of the config-4 population against the
+    oracle."""
     from flowsentryx_amd import synth
     p, s = synth.config_params(4)
     n = 1 << 21
