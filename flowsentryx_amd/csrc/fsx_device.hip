@@ -3988,9 +3988,18 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
                               (lim.limiter == 1 && (lim.test_flags & kFlagSwUnsorted))) &&
                      resolve && !no_hfast;
     if (!(split && split->tail) && (e = hipMemsetAsync(sc.marks, 0, n, st)) != hipSuccess) return e;
+    // plain sorts of 25- / 26-bit ids (the sliding window and the token bucket on 2^25-slot
+    // tables, flow-only batches): three passes of 8 + 8 + 9 / 8 + 9 + 9 bits instead of four of
+    // 7 — pass 0's digits counted by k_parse, the later ones with bases from the tile scan
+    // (FSX_SORT_PLAIN4=1: the four passes, A/B)
+    static const bool plain4 = getenv("FSX_SORT_PLAIN4") != nullptr;
+    const bool plain9 = !heavy_sort && !ord && !onesweep && !full_digits && !admit && !plain4 && npass == 4 &&
+                        idbits >= 25 && idbits <= 26;
+    if (plain9) npass = 3;
     DigitPlan dp{};
     dp.npass = (uint32_t)npass;
-    const bool wide_plan = heavy_sort && wide9;   // (light passes: bases from the tile scan)
+    // (passes >= 1: bases from the tile scan)
+    const bool wide_plan = (heavy_sort && wide9) || plain9;
     dp.nhist = wide_plan ? 1u : (uint32_t)npass;
     uint32_t nheavy = kHeavyMax;
     if (heavy_sort) {
@@ -4020,6 +4029,12 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
                                           lim.table_mask, lim.test_flags, idt, resolve, bs,
                                           rl_batch ? rules : RuleSet{});
         mark("k_heavy_pick");
+    } else if (plain9) {
+        const uint32_t w1 = idbits - 17;   // 8 (25-bit ids) or 9 (26-bit ids)
+        dp.shift[0] = kIdShift;          dp.mask[0] = 255u;
+        dp.shift[1] = kIdShift + 8;      dp.mask[1] = (1u << w1) - 1u;
+        dp.shift[2] = kIdShift + 8 + w1; dp.mask[2] = 511u;
+        dp.shift[3] = kIdShift + 8 + w1 + 9; dp.mask[3] = 0u;   // (no fourth pass)
     } else {
         for (int p = 0; p < 4; ++p) { dp.shift[p] = kIdShift + dbits * (uint32_t)p; dp.mask[p] = dmask; }
     }

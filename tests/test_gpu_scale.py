@@ -178,9 +178,10 @@ def test_wide_ids_full_path(native, oracle, max_entries):
 @pytest.mark.parametrize("max_entries", [6 << 20, 16 << 20], ids=["ids24", "ids25"])
 def test_wide_ids_limiters(native, oracle, limiter, max_entries):
     """The sliding window and the token bucket on tables of 2^24 / 2^25 slots (24- / 25-bit
-    source ids: the plain four-pass sort, each pass's digit bytes read by the next pass's tile
-    histogram; DESIGN.md §3 "Wider ids", §8): the config-4 population over two carried
-    batches, verdicts and every map against the oracle."""
+    source ids: the plain sort, three 8-bit passes for 24 bits, 8 + 8 + 9 bits for 25 — the
+    last with 512-digit tiles, 16-bit digit words and bases from the tile scan; each pass's
+    digits read by the next pass's tile histogram; DESIGN.md §3 "Wider ids", §8): the config-4
+    population over two carried batches, verdicts and every map against the oracle."""
     from flowsentryx_amd import synth
     p, s = synth.config_params(4)
     n = 1 << 21
@@ -194,3 +195,13 @@ def test_wide_ids_limiters(native, oracle, limiter, max_entries):
         for a, b in ((0, cut), (cut, n)):
             _verdicts_equal(c.verdict_batch(hdr[a:b], ln[a:b], ts[a:b]), o.batch(hdr[a:b], ln[a:b], ts[a:b]))
         _same_state(c, o, (3, 4, 5, 6) if limiter == 2 else (1, 2, 3, 4))
+
+
+def test_wide_ids_flow_features(native, oracle):
+    """Flow-only batches on a 2^25-slot table (the per-batch id table has the table's 25-bit
+    ids): the plain sort in three passes of 8 + 8 + 9 bits, features of the
+    config-4 population against the oracle."""
+    from flowsentryx_amd import synth
+    p, s = synth.config_params(4)
+    hdr, ln, ts = oracle.synth(p, s, 0, 1 << 21)
+    _check_flows(native, oracle, hdr, ln, ts, cfg={"max_batch": 1 << 21, "max_entries": 16 << 20})
