@@ -3953,11 +3953,13 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
     const uint32_t lbits = 63 - bshift;                 // light digit bits of the bucket
     const uint32_t hrest = idbits > lbits ? idbits - lbits : 0;
     // 24- / 25-bit ids (17 / 18 light bits after pass 0's 7): two light passes of 9-bit digits
-    // (512-digit tiles, bases from the tile scan: k_digit_base) instead of three of 6 bits —
-    // with the fixed window's heavy lists (the other limiters keep the plain 4-pass sort).
-    // FSX_SORT_LIGHT6=1: the three 6-bit passes (A/B)
+    // (512-digit tiles, bases from the tile scan: k_digit_base) instead of three of 6 bits, for
+    // every limiter batch with verdicts: the fixed window (heavy lists), the sliding window
+    // (heavy lists: the odd count they need) and the token bucket (sorted heavy runs).
+    // FSX_SORT_LIGHT6=1: the three 6-bit passes (A/B; the sliding window and the token bucket
+    // then take the plain sort)
     static const bool light6 = getenv("FSX_SORT_LIGHT6") != nullptr;
-    const bool wide9 = lists_ok && !light6 && hrest > 16 && hrest <= 18;
+    const bool wide9 = lists_any && !light6 && hrest > 16 && hrest <= 18;
     const int hpass = 1 + (wide9 ? 2 : (int)((hrest + 7) / 8));   // pass 0 + the light passes
     const bool heavy_sort = !admit && !onesweep && !full_digits && !no_heavy && idbits <= 25 && npass >= 3 &&
                             (hpass == 3 || (hpass == 4 && lists_ok));
