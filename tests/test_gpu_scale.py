@@ -205,3 +205,66 @@ def test_wide_ids_flow_features(native, oracle):
     p, s = synth.config_params(4)
     hdr, ln, ts = oracle.synth(p, s, 0, 1 << 21)
     _check_flows(native, oracle, hdr, ln, ts, cfg={"max_batch": 1 << 21, "max_entries": 16 << 20})
+
+
+def _wide_cfg(limiter):
+    cfg = dict(limiter=limiter, max_entries=16 << 20)
+    if limiter == 2:
+        cfg.update(tb_rate=2000, tb_burst=50)
+    return cfg
+
+
+@pytest.mark.parametrize("limiter", [0, 1, 2], ids=["fixed", "sliding", "token"])
+def test_wide_ids_edge_batches(native, oracle, limiter):
+    """The 9-bit plans at their edges (DESIGN.md §3 "Two 9-bit light passes"): on a 2^25-slot
+    table, carried batches of 1, 100, 4095, 4097 and 70000 packets (one to 18 sort tiles), a
+    batch of three sources (light passes over next to nothing), IPv6, non-IP and short frames
+    mixed in, and a batch whose clock steps back (the run path) — verdicts and every map
+    against the oracle."""
+    from test_gpu_parity import rand_stream
+    rng = np.random.default_rng(77)
+    cfg = _wide_cfg(limiter)
+    o = oracle.ShardedOracle(THREADS, **cfg)
+    batches, t = [], 10**9
+    for n, ips in ((1, 1), (100, 30), (4095, 500), (4097, 3000), (70000, 20000), (50000, 3)):
+        hdr, ln, ts = rand_stream(rng, n, ips, v6_frac=0.2, nonip_frac=0.02, short_frac=0.01, t0=t)
+        t = int(ts[-1]) + 1
+        batches.append((hdr, ln, ts))
+    hdr, ln, ts = rand_stream(rng, 30000, 2000, t0=t + 10**6)
+    ts[15000:] -= np.uint64(10**6)   # (the clock steps back mid-batch)
+    batches.append((hdr, ln, ts))
+    with native.FsxContext(max_batch=70000, **cfg) as c:
+        for hdr, ln, ts in batches:
+            _verdicts_equal(c.verdict_batch(hdr, ln, ts), o.batch(hdr, ln, ts))
+        _same_state(c, o, (3, 4, 5, 6) if limiter == 2 else (1, 2, 3, 4))
+
+
+@pytest.mark.parametrize("limiter", [1, 2], ids=["sliding", "token"])
+def test_wide_ids_limiters_pipelined(native, oracle, limiter):
+    """The sliding window and the token bucket on a 2^25-slot table with pipelined batches
+    (the heavy-source sort with two 9-bit light passes in each front set): three
+    uneven carried batches of the config-4 population, one sync at the end, verdicts and every
+    map against the oracle."""
+    import torch
+    from flowsentryx_amd import synth
+    p, s = synth.config_params(4)
+    n = 1 << 20
+    hdr, ln, ts = oracle.synth(p, s, 0, n)
+    cuts = [0, 250_000, 250_001, n]
+    cfg = _wide_cfg(limiter)
+    o = oracle.ShardedOracle(THREADS, **cfg)
+    dev = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).reshape(-1)).cuda()
+    with native.FsxContext(max_batch=n, **cfg) as c:
+        c.set_pipeline(True)
+        outs = []
+        for a, b in zip(cuts[:-1], cuts[1:]):
+            d = dict(h=dev(hdr[a:b]), l=dev(ln[a:b]), t=dev(ts[a:b]),
+                     v=torch.empty(b - a, dtype=torch.uint8, device="cuda"))
+            c.verdict_batch_device(d["h"].data_ptr(), d["l"].data_ptr(), d["t"].data_ptr(), b - a,
+                                   d["v"].data_ptr())
+            d["vo"] = o.batch(hdr[a:b], ln[a:b], ts[a:b])
+            outs.append(d)
+        c.sync()
+        for d in outs:
+            _verdicts_equal(d["v"].cpu().numpy(), d["vo"])
+        _same_state(c, o, (3, 4, 5, 6) if limiter == 2 else (1, 2, 3, 4))
