@@ -20,6 +20,7 @@
 #include <cstdlib>
 
 #include "fsx_dev_common.h"
+#include "fsx_plan.h"
 #include "fsx_internal.h"
 #include "fsx_seg.h"
 #include "fsx_walk.h"
@@ -3928,11 +3929,8 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
     const bool ord = lim.ord && do_limit && lim.limiter == 0 && !(lim.test_flags & kFlagAdmit) && !eager_slots &&
                      !flows && !in.rec && idbits >= 1 && idbits <= 31;
     if (ord) idbits = 32;
-    int npass = std::max(1, (int)((idbits + 7) / 8));
     static const bool full_digits = getenv("FSX_SORT_FULL_DIGITS") != nullptr;   // A/B: 8,8,..,rest
     static const bool no_heavy = getenv("FSX_NO_HEAVY_SORT") != nullptr;          // A/B: plain LSD
-    const uint32_t dbits = full_digits ? 8u : std::max<uint32_t>(1, (idbits + npass - 1) / npass);
-    const uint32_t dmask = (1u << dbits) - 1u;
     // Heavy-source sort (tables of <= 2^25 slots): pass 0 buckets the light entries by a
     // low id digit and every heavy source into a bucket of its own (the bucket in bits
     // [bshift, 64) above the id: 8 bits, light digit 7 bits and 128 heavy sources for every
@@ -3949,21 +3947,24 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
     const bool lists_ok = lists_any && lim.limiter == 0;
     // heavy verdict lists (fixed / sliding window with the heavy-source sort; FSX_NO_HEAVY_LISTS=1: A/B)
     const bool lists_sw0 = lists_any && lim.limiter == 1;
-    const uint32_t bshift = std::max<uint32_t>(56, kIdShift + idbits);
-    const uint32_t lbits = 63 - bshift;                 // light digit bits of the bucket
-    const uint32_t hrest = idbits > lbits ? idbits - lbits : 0;
-    // 24- / 25-bit ids (17 / 18 light bits after pass 0's 7): two light passes of 9-bit digits
-    // (512-digit tiles, bases from the tile scan: k_digit_base) instead of three of 6 bits, for
-    // every limiter batch with verdicts: the fixed window (heavy lists), the sliding window
-    // (heavy lists: the odd count they need) and the token bucket (sorted heavy runs).
-    // FSX_SORT_LIGHT6=1: the three 6-bit passes (A/B; the sliding window and the token bucket
-    // then take the plain sort)
+    // The digit plan (fsx_plan.h). 24- / 25-bit ids (17 / 18 light bits after pass 0's 7): two
+    // light passes of 9-bit digits (512-digit tiles, bases from the tile scan: k_digit_base)
+    // instead of three of 6 bits, for every limiter batch with verdicts — the fixed window (heavy
+    // lists), the sliding window (heavy lists: the odd count they need) and the token bucket
+    // (sorted heavy runs); FSX_SORT_LIGHT6=1: the three 6-bit passes (A/B; the sliding window
+    // and the token bucket then take the plain sort). Plain sorts of 25- / 26-bit ids (flow-only
+    // batches, admission off): three passes of 8 + 8 + 9 / 8 + 9 + 9 bits instead of four of 7
+    // (FSX_SORT_PLAIN4=1: the four passes, A/B).
     static const bool light6 = getenv("FSX_SORT_LIGHT6") != nullptr;
-    const bool wide9 = lists_any && !light6 && hrest > 16 && hrest <= 18;
-    const int hpass = 1 + (wide9 ? 2 : (int)((hrest + 7) / 8));   // pass 0 + the light passes
-    const bool heavy_sort = !admit && !onesweep && !full_digits && !no_heavy && idbits <= 25 && npass >= 3 &&
-                            (hpass == 3 || (hpass == 4 && lists_ok));
-    if (heavy_sort) npass = hpass;   // (24-bit ids: 4 passes instead of 3, 3 of them over the light entries)
+    static const bool plain4 = getenv("FSX_SORT_PLAIN4") != nullptr;
+    static_assert(kPlanIdShift == kIdShift, "fsx_plan.h's id position");
+    SortPlanIn pq;
+    pq.idbits = idbits; pq.onesweep = onesweep; pq.full_digits = full_digits; pq.no_heavy = no_heavy;
+    pq.admit = admit; pq.lists_any = lists_any; pq.lists_ok = lists_ok; pq.light6 = light6; pq.plain4 = plain4;
+    const SortPlan plan = make_sort_plan(pq);
+    const int npass = plan.npass;
+    const bool heavy_sort = plan.heavy_sort;
+    const uint32_t bshift = plan.bshift;
     const bool lists_sw = lists_sw0 && (npass & 1);
     // heavy slots resolved once in k_heavy_pick (FSX_NO_HEAVY_SLOTS=1: A/B). Under prefix rules
     // the pick leaves every source whose /24 a rule touches light (rule_maybe), so a heavy
@@ -3990,32 +3991,17 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
                               (lim.limiter == 1 && (lim.test_flags & kFlagSwUnsorted))) &&
                      resolve && !no_hfast;
     if (!(split && split->tail) && (e = hipMemsetAsync(sc.marks, 0, n, st)) != hipSuccess) return e;
-    // plain sorts of 25- / 26-bit ids (the sliding window and the token bucket on 2^25-slot
-    // tables, flow-only batches): three passes of 8 + 8 + 9 / 8 + 9 + 9 bits instead of four of
-    // 7 — pass 0's digits counted by k_parse, the later ones with bases from the tile scan
-    // (FSX_SORT_PLAIN4=1: the four passes, A/B)
-    static const bool plain4 = getenv("FSX_SORT_PLAIN4") != nullptr;
-    const bool plain9 = !heavy_sort && !ord && !onesweep && !full_digits && !admit && !plain4 && npass == 4 &&
-                        idbits >= 25 && idbits <= 26;
-    if (plain9) npass = 3;
     DigitPlan dp{};
     dp.npass = (uint32_t)npass;
-    // (passes >= 1: bases from the tile scan)
-    const bool wide_plan = (heavy_sort && wide9) || plain9;
-    dp.nhist = wide_plan ? 1u : (uint32_t)npass;
+    dp.nhist = plan.nhist;
+    dp.light_b = plan.light_b;
+    for (int p = 0; p < 4; ++p) { dp.shift[p] = plan.shift[p]; dp.mask[p] = plan.mask[p]; }
+    const bool wide_plan = plan.tile_bases;   // (passes >= 1: bases from the tile scan)
     uint32_t nheavy = kHeavyMax;
     if (heavy_sort) {
-        dp.light_b = 1u << lbits;
         nheavy = std::min<uint32_t>(kHeavyMax, (1u << (64 - bshift)) - dp.light_b);
         static const uint32_t heavy_n = getenv("FSX_HEAVY_N") ? (uint32_t)atoi(getenv("FSX_HEAVY_N")) : 0u;
         if (heavy_n) nheavy = std::min(nheavy, heavy_n);   // (A/B: fewer heavy sources)
-        dp.shift[0] = bshift; dp.mask[0] = (1u << (64 - bshift)) - 1u;
-        const uint32_t lp = (uint32_t)hpass - 1, w = (hrest + lp - 1) / lp;
-        for (uint32_t p = 1; p <= lp; ++p) {
-            const uint32_t lo = (p - 1) * w, wb = std::min(w, hrest - lo);
-            dp.shift[p] = kIdShift + lbits + lo;
-            dp.mask[p] = (1u << wb) - 1u;
-        }
     }
     if (heavy_sort) {
         k_heavy_sample<<<64, 256, 0, sp0>>>(in, len, n, sc.sketch, lim.seed, lim.table_mask, lim.test_flags);
@@ -4031,14 +4017,6 @@ hipError_t launch_verdict_pipeline(const PacketIn &in, const uint32_t *len, cons
                                           lim.table_mask, lim.test_flags, idt, resolve, bs,
                                           rl_batch ? rules : RuleSet{});
         mark("k_heavy_pick");
-    } else if (plain9) {
-        const uint32_t w1 = idbits - 17;   // 8 (25-bit ids) or 9 (26-bit ids)
-        dp.shift[0] = kIdShift;          dp.mask[0] = 255u;
-        dp.shift[1] = kIdShift + 8;      dp.mask[1] = (1u << w1) - 1u;
-        dp.shift[2] = kIdShift + 8 + w1; dp.mask[2] = 511u;
-        dp.shift[3] = kIdShift + 8 + w1 + 9; dp.mask[3] = 0u;   // (no fourth pass)
-    } else {
-        for (int p = 0; p < 4; ++p) { dp.shift[p] = kIdShift + dbits * (uint32_t)p; dp.mask[p] = dmask; }
     }
     if (early) {   // the parse after the prologue
         if ((e = hipEventRecord(split->pro_done, sp0)) != hipSuccess) return e;
