@@ -249,9 +249,10 @@ def test_pipelined_host_pointer_batches(native, oracle):
 
 
 def test_pipelined_wide_ids(native, oracle):
-    """Pipelined batches on a 2^25-slot table (the 4-pass heavy-source sort, heavy runs in
-    pass 0's buffer, heavy verdict lists in the parse buffer of each front set): three
-    uneven batches of the config-4 population with features + scores."""
+    """Pipelined batches on a 2^25-slot table (the heavy-source sort with two 9-bit light
+    passes, DESIGN.md §3: heavy runs and light entries in pass 0's buffer, 512-digit tiles and
+    tile-scan bases in each front set): three uneven batches of the config-4 population with
+    features + scores."""
     from flowsentryx_amd import synth
     p, s = synth.config_params(4)
     n = 1 << 20
