@@ -74,6 +74,7 @@ struct fsx_ctx {
     // the last checked limiter batch inserted more new sources than half its IP packets: the
     // next batches take the home-ordered inserts (FSX_FLAG_ORDERED_INSERTS: always)
     bool flood_hint = false;
+    bool light_dom = false;   // the last checked batch: >= 90 % of its IP packets light (Limits::light_dom)
     // sharding: per (owner, tile) counts of fsx_shard_pack_device, blocklist replica
     uint32_t *d_shard_cnt = nullptr;
     uint64_t shard_cnt_cap = 0;
@@ -588,7 +589,10 @@ static int batch_error(fsx_ctx *c, uint32_t err);
 
 // A finished batch's facts the host keeps: a flood of new sources (home-ordered inserts next).
 static void note_batch(fsx_ctx *c, const BatchState &h) {
-    if (!h.err && h.n_valid) c->flood_hint = 2ull * h.n_new > h.n_valid;
+    if (!h.err && h.n_valid) {
+        c->flood_hint = 2ull * h.n_new > h.n_valid;
+        c->light_dom = 10ull * h.n_light >= 9ull * h.n_valid;
+    }
 }
 
 static int check_batch(fsx_ctx *c) {
@@ -1065,6 +1069,7 @@ static int run_batch(fsx_ctx *c, const PacketIn &in, const uint32_t *d_len, cons
     const bool ord_want = ord_env >= 0 ? ord_env > 0 : (c->flood_hint || (c->cfg.flags & FSX_FLAG_ORDERED_INSERTS));
     c->lim.ord = do_limit && !fr && !in.rec && d_verdict && c->cfg.limiter == FSX_LIMIT_FIXED_WINDOW &&
                  !(c->cfg.flags & FSX_FLAG_OVERFLOW_ADMIT) && ord_want ? 1u : 0u;
+    c->lim.light_dom = c->light_dom ? 1u : 0u;
     // pipelined (no per-kernel timing): split front / tail for the fixed window on header
     // records, the whole batch on the context stream otherwise
     if (c->pipe && do_limit && n && !c->timing)

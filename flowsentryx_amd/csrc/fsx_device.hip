@@ -3822,9 +3822,12 @@ hipError_t launch_tail(const TailArgs &a) {
                                                                   table, lim, hlists, skeys);
             mark_on("k_walk_fixed_long", fork3 ? 2 : 0);
             if (fork3 && (e = hipEventRecord(walk_join_ev, st3)) != hipSuccess) return e;
-            // (A/B: FSX_WALK_LDS bytes of unused dynamic LDS per block cap the thread walker's
-            // blocks per CU beside the next batch's front)
-            static const uint32_t walk_lds = getenv("FSX_WALK_LDS") ? (uint32_t)atoi(getenv("FSX_WALK_LDS")) : 0u;
+            // Unused dynamic LDS caps the thread walker's blocks per CU (53000 B: three) beside the
+            // next batch's front when the host saw an all-light stream (Limits::light_dom): config 3
+            // from a stream 5.96 / 6.04 -> 5.75 / 5.76 ms, while the headline (+5 %) and config 4
+            // (+1.5 %) want it uncapped (profiles/r06/ab_r06wk*). FSX_WALK_LDS=B: B bytes always (A/B)
+            static const int walk_env = getenv("FSX_WALK_LDS") ? atoi(getenv("FSX_WALK_LDS")) : -1;
+            const uint32_t walk_lds = walk_env >= 0 ? (uint32_t)walk_env : lim.light_dom ? 53000u : 0u;
             k_walk_fixed<<<std::min<uint32_t>(FSX_WALK_SHORT_BLOCKS, cdiv(n, 256)), 256, walk_lds, st>>>(S, bs, sc.seg_start, sc.seg_slot, ts, len, sc.pay[0],
                                                      sc.seg_order, cls, sc.marks, table, lim, hlists, skeys);
             mark("k_walk_fixed");

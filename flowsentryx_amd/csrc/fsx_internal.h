@@ -186,6 +186,10 @@ struct Limits {           // the rate-limiter constants, src/fsx_kern.c:245,308-
     // another generation reads as empty — fsx_reset moves to the next generation instead of
     // clearing the table (DESIGN.md §3 "Clear-free reset")
     uint32_t tgen;
+    // host hint (set per batch): the last batch the host checked had >= 90 % of its IP packets
+    // in light sources (an all-light stream, config 3's shape) — the thread walker then runs
+    // with its blocks per CU capped beside the next batch's front
+    uint32_t light_dom;
 };
 constexpr uint32_t kFlagAdmit = 8u;   // include/fsx_hip.h FSX_FLAG_OVERFLOW_ADMIT
 constexpr uint32_t kFlagSwUnsorted = 16u;   // include/fsx_hip.h FSX_FLAG_SW_UNSORTED
